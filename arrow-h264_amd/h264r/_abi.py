@@ -1,0 +1,102 @@
+"""ctypes / numpy mirror of include/h264r.h and include/h264r_synth.h.
+
+Pure data-layout definitions shared by the host API (h264r/__init__.py), the
+benchmark and the tests.  No behaviour lives here.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+# ---- constants (include/h264r.h) -------------------------------------------------
+OK, EINVAL, ENOMEM, EDEVICE, ESTATE, EUNSUPPORTED, ENODEVICE = 0, -1, -2, -3, -4, -5, -6
+MAX_REFS, MAX_SLOTS, MAX_SLICES = 16, 32, 256
+
+P_SKIP, P_16x16, P_16x8, P_8x16, P_8x8, P_8x4, P_4x8, P_4x4 = range(8)
+I_4x4, I_8x8, I_16x16, SI, I_PCM = 8, 9, 10, 11, 12
+SLICE_P, SLICE_B, SLICE_I, SLICE_SP, SLICE_SI = range(5)
+MBF_INTRA, MBF_T8x8, MBF_BYPASS = 1, 2, 4
+
+SYNTH_INTRA, SYNTH_P, SYNTH_B = 0, 1, 2
+SYNTH_MAX_LEVELS_PER_MB = 416
+
+# ---- numpy dtypes of the canonical device formats ----------------------------------
+MB_DTYPE = np.dtype([
+    ("mb_type", "u1"), ("flags", "u1"), ("cbp", "u1"), ("qp_y", "i1"),
+    ("qp_c", "i1", (2,)), ("i16_mode", "u1"), ("chroma_mode", "u1"),
+    ("cbp_blks", "<u2"), ("slice", "<u2"), ("qp_scaled", "u1", (3,)), ("pad0", "u1"),
+    ("coef_off", "<u4"), ("ipred", "u1", (8,)), ("pad1", "u1", (4,)),
+])
+assert MB_DTYPE.itemsize == 32
+
+SLICE_DTYPE = np.dtype([
+    ("slice_type", "u1"), ("deblock_idc", "u1"), ("filter_offset_a", "i1"),
+    ("filter_offset_b", "i1"), ("wp_mode", "u1"), ("luma_log2_wd", "u1"),
+    ("chroma_log2_wd", "u1"), ("num_ref", "u1", (2,)), ("pad", "u1", (7,)),
+    ("ref_slot", "i1", (2, MAX_REFS)), ("wp_weight", "i1", (2, MAX_REFS, 3)),
+    ("wp_offset", "i1", (2, MAX_REFS, 3)), ("implicit_w1", "<i2", (MAX_REFS, MAX_REFS)),
+])
+assert SLICE_DTYPE.itemsize == 752
+
+QUANT_DTYPE = np.dtype([("scale4x4", "<i2", (2, 3, 6, 16)), ("scale8x8", "<i2", (2, 3, 6, 64))])
+assert QUANT_DTYPE.itemsize == 5760
+
+PIC_DTYPE = np.dtype([("constrained_intra_pred", "<i4"), ("num_slices", "<i4"),
+                      ("poc", "<i4"), ("pad", "<i4")])
+
+
+class SynthCfg(C.Structure):
+    _fields_ = [
+        ("width_mbs", C.c_int32), ("height_mbs", C.c_int32), ("kind", C.c_int32),
+        ("num_slices", C.c_int32), ("deblock_idc", C.c_int32),
+        ("filter_offset_a", C.c_int32), ("filter_offset_b", C.c_int32),
+        ("transform8x8", C.c_int32), ("wp_mode", C.c_int32),
+        ("constrained_intra", C.c_int32), ("num_refs", C.c_int32),
+        ("qp_min", C.c_int32), ("qp_max", C.c_int32), ("pcm_permille", C.c_int32),
+        ("intra_permille", C.c_int32), ("mv_range_x", C.c_int32),
+        ("mv_range_y", C.c_int32), ("seed", C.c_uint64),
+    ]
+
+    def as_dict(self) -> dict:
+        return {name: int(getattr(self, name)) for name, _ in self._fields_}
+
+    @classmethod
+    def from_dict(cls, d: dict) -> "SynthCfg":
+        c = cls()
+        for k, v in d.items():
+            setattr(c, k, int(v))
+        return c
+
+
+class Batch(C.Structure):
+    """h264r_batch: device pointers of a resident batch."""
+    _fields_ = [
+        ("num_pics", C.c_int32), ("width_mbs", C.c_int32), ("height_mbs", C.c_int32),
+        ("slice_stride", C.c_int32), ("mbs", C.c_void_p), ("levels", C.c_void_p),
+        ("mv", C.c_void_p), ("ref_idx", C.c_void_p), ("slices", C.c_void_p),
+        ("pics", C.c_void_p), ("quant", C.c_void_p), ("ref_planes", C.c_void_p),
+        ("out_y", C.c_void_p), ("out_u", C.c_void_p), ("out_v", C.c_void_p),
+    ]
+
+
+def ptr(a: np.ndarray) -> C.c_void_p:
+    """Host pointer of a C-contiguous numpy array."""
+    assert a.flags["C_CONTIGUOUS"]
+    return C.c_void_p(a.ctypes.data)
+
+
+def bind_synth(lib: C.CDLL) -> None:
+    """Declare the h264r_synth_* prototypes on a library that exports them."""
+    P = C.c_void_p
+    lib.h264r_synth_default.argtypes = [C.POINTER(SynthCfg), C.c_int, C.c_int, C.c_int]
+    lib.h264r_synth_picture.argtypes = [C.POINTER(SynthCfg), C.c_int, P, P,
+                                        C.POINTER(C.c_int64), P, P, P, P]
+    lib.h264r_synth_refpic.argtypes = [C.c_uint64, C.c_int, C.c_int, C.c_int, P, P, P]
+    lib.h264r_synth_slot_poc.argtypes = [C.c_int]
+    lib.h264r_synth_cur_poc.argtypes = [C.POINTER(SynthCfg)]
+    lib.h264r_synth_algo_bytes.argtypes = [P, P, C.c_int, C.c_int,
+                                           C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
+    for f in ("h264r_synth_default", "h264r_synth_picture", "h264r_synth_refpic",
+              "h264r_synth_slot_poc", "h264r_synth_cur_poc", "h264r_synth_algo_bytes"):
+        getattr(lib, f).restype = C.c_int

@@ -1,0 +1,232 @@
+/*
+ * h264r.h -- C ABI of the MI355X-native H.264 macroblock-reconstruction path.
+ *
+ * This header is the drop-in boundary for the post-entropy hot path of
+ * luuvish/arrow-h264 (`R/` = reference root, `H/` = R/src/codec/h264/):
+ *
+ *   reference interface                          replaced by (this header)
+ *   -------------------------------------------  ------------------------------------------
+ *   Decoder::assign_quant_params  decoder.cc:59   h264r_quant_init_flat / h264r_quant_init_lists
+ *     (-> Transform::init/set_quant transform.cc:173-302)
+ *   Decoder::coeff_luma_dc/ac,    decoder.cc:81-96 levels are written RAW (not dequantised) into
+ *   Decoder::coeff_chroma_dc/ac                    the per-MB compacted level block described
+ *   Decoder::transform_luma_dc,   decoder.cc:98-105 below (dequant + DC Hadamard move to the GPU)
+ *   Decoder::transform_chroma_dc
+ *   Decoder::decode(mb_t&)        decoder.cc:65-79 h264r_mb_submit   (one MB, host buffers) or
+ *                                                   h264r_decode_batch (device-resident arrays)
+ *   Decoder::deblock_filter       decoder.cc:107   h264r_picture_end  (recon + deblock + readback)
+ *   storable_picture planes       picture.cc:17-83 h264r_set_ref / output planes (8-bit, unpadded)
+ *
+ * All entry points are extern "C", take plain pointers and sizes, and return
+ * an int status (H264R_OK == 0, negative on error).  No exceptions cross the
+ * boundary; the reference's void/assert/exit() error convention
+ * (decoder.h:301-338, ldecod.cc:33-48) becomes status codes.
+ *
+ * Data formats (all little-endian, 4:2:0, 8-bit, frame pictures):
+ *   - h264r_mb       32-byte MB record (subset of mb_t, macroblock.h:78-135).
+ *   - levels         int16 pool; each MB owns a compacted block at mb.coef_off
+ *                    (in int16 units, multiple of 8):
+ *                      for b8 in 0..3 with (cbp & 1<<b8): 64 levels
+ *                          4x4 transform: 4 sub-blocks (raster inside the 8x8) x 16
+ *                                         raster levels; 8x8 transform: 64 raster levels
+ *                      if cbp_chroma == 2: 128 levels = Cb 4x16 then Cr 4x16
+ *                                         (raster per 4x4 block, index 0 unused)
+ *                      if I_16x16:        16 luma DC levels (raster of the 4x4 DC matrix)
+ *                      if cbp_chroma != 0: 8 chroma DC levels (Cb c00 c01 c10 c11, Cr ...)
+ *                      I_PCM:             384 raw samples as bytes (Y 256, Cb 64, Cr 64)
+ *                    Levels are the entropy decoder's levels placed at their raster
+ *                    position (inverse zig-zag done by the producer, transform.cc:307-386).
+ *   - motion         per 4x4 block, per list: uint32 mv (int16 x in low half, int16 y
+ *                    in high half, quarter-pel) and int8 ref_idx (-1 = list unused),
+ *                    arrays [list][H4][W4] (pic_motion_params, picture.h:66-71).
+ *   - planes         uint8 Y [H][W], Cb/Cr [H/2][W/2], pitch == width, no padding
+ *                    (the reference pads by edge replication, picture.cc:182-205;
+ *                     the GPU clamps coordinates instead -- equivalent).
+ */
+#ifndef H264R_H_
+#define H264R_H_
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define H264R_ABI_VERSION 1
+
+/* ---- status codes ---------------------------------------------------------- */
+#define H264R_OK               0
+#define H264R_EINVAL          -1   /* bad argument / unsupported configuration   */
+#define H264R_ENOMEM          -2   /* device or host allocation failed           */
+#define H264R_EDEVICE         -3   /* HIP runtime error                          */
+#define H264R_ESTATE          -4   /* call out of order (e.g. mb before begin)   */
+#define H264R_EUNSUPPORTED    -5   /* valid H.264 but not on this path (MBAFF..) */
+#define H264R_ENODEVICE       -6   /* no usable GPU / kernels not loaded         */
+
+/* ---- limits ---------------------------------------------------------------- */
+#define H264R_MAX_REFS        16   /* per list, frame pictures                   */
+#define H264R_MAX_SLOTS       32   /* DPB slots addressable by ref tables        */
+#define H264R_MAX_SLICES      256  /* per picture                                */
+
+/* ---- mb_type values: identical to mb_t::mb_type (macroblock.h:48-76) -------- */
+#define H264R_P_SKIP     0   /* also B_Skip / B_Direct_16x16 */
+#define H264R_P_16x16    1
+#define H264R_P_16x8     2
+#define H264R_P_8x16     3
+#define H264R_P_8x8      4
+#define H264R_P_8x4      5
+#define H264R_P_4x8      6
+#define H264R_P_4x4      7
+#define H264R_I_4x4      8
+#define H264R_I_8x8      9
+#define H264R_I_16x16   10
+#define H264R_SI        11
+#define H264R_I_PCM     12
+
+/* ---- slice types (slice.h:29-35) ------------------------------------------- */
+#define H264R_SLICE_P   0
+#define H264R_SLICE_B   1
+#define H264R_SLICE_I   2
+#define H264R_SLICE_SP  3
+#define H264R_SLICE_SI  4
+
+/* ---- h264r_mb.flags ---------------------------------------------------------- */
+#define H264R_MBF_INTRA   0x01   /* mb_t::is_intra_block            */
+#define H264R_MBF_T8x8    0x02   /* mb_t::transform_size_8x8_flag   */
+#define H264R_MBF_BYPASS  0x04   /* mb_t::TransformBypassModeFlag (unsupported -> EUNSUPPORTED) */
+
+/* 32-byte macroblock record (fields named after mb_t, macroblock.h:78-135). */
+typedef struct h264r_mb {
+    uint8_t  mb_type;        /* mb_t::mb_type                                        */
+    uint8_t  flags;          /* H264R_MBF_*                                          */
+    uint8_t  cbp;            /* CodedBlockPatternLuma | CodedBlockPatternChroma << 4 */
+    int8_t   qp_y;           /* QpY   (deblock, deblock.cc:469-470)                  */
+    int8_t   qp_c[2];        /* QpC[] (deblock)                                      */
+    uint8_t  i16_mode;       /* Intra16x16PredMode                                   */
+    uint8_t  chroma_mode;    /* intra_chroma_pred_mode                               */
+    uint16_t cbp_blks;       /* cbp_blks[0] (non-zero 4x4 mask, deblock bS=2)        */
+    uint16_t slice;          /* index into the picture's slice table (slice_nr)      */
+    uint8_t  qp_scaled[3];   /* qp_scaled[] (dequant, transform.cc:400-401)          */
+    uint8_t  pad0;
+    uint32_t coef_off;       /* offset of the compacted level block, int16 units     */
+    uint8_t  ipred[8];       /* Intra4x4PredMode[16] as nibbles (blkIdx order, low
+                                nibble first) or Intra8x8PredMode[4] in nibbles 0..3 */
+    uint8_t  pad1[4];
+} h264r_mb;
+
+/* Per-slice parameters (subset of slice_header_t + ref lists, slice.h:37-131). */
+typedef struct h264r_slice {
+    uint8_t  slice_type;           /* H264R_SLICE_*                                      */
+    uint8_t  deblock_idc;          /* disable_deblocking_filter_idc                      */
+    int8_t   filter_offset_a;      /* FilterOffsetA                                      */
+    int8_t   filter_offset_b;      /* FilterOffsetB                                      */
+    uint8_t  wp_mode;              /* 0 default, 1 explicit, 2 implicit (inter_prediction.cc:62-63,99-139) */
+    uint8_t  luma_log2_wd;         /* luma_log2_weight_denom (5 when not explicit, interpret_rbsp.cc:722) */
+    uint8_t  chroma_log2_wd;       /* chroma_log2_weight_denom                           */
+    uint8_t  num_ref[2];
+    uint8_t  pad[7];
+    int8_t   ref_slot[2][H264R_MAX_REFS];       /* RefPicList[l][i] -> DPB slot       */
+    int8_t   wp_weight[2][H264R_MAX_REFS][3];   /* pred_weight_l[l][pl][i].weight     */
+    int8_t   wp_offset[2][H264R_MAX_REFS][3];   /* pred_weight_l[l][pl][i].offset     */
+    int16_t  implicit_w1[H264R_MAX_REFS][H264R_MAX_REFS]; /* weight1 for (ref0,ref1), w0 = 64-w1 */
+} h264r_slice;
+
+/* Dequantisation tables (Transform::InvLevelScale*, transform.cc:264-301). */
+typedef struct h264r_quant {
+    int16_t scale4x4[2][3][6][16];   /* [0 intra / 1 inter][plane][qp%6][raster] */
+    int16_t scale8x8[2][3][6][64];
+} h264r_quant;
+
+/* Per-picture parameters. */
+typedef struct h264r_pic {
+    int32_t  constrained_intra_pred;  /* pps.constrained_intra_pred_flag */
+    int32_t  num_slices;
+    int32_t  poc;                     /* informational (implicit weights are precomputed) */
+    int32_t  pad;
+} h264r_pic;
+
+/* A batch of same-sized pictures whose arrays are already resident on the device.
+ * Per-picture strides: MBs W*H records; motion 2*(4H)*(4W) entries; slices
+ * `slice_stride` entries; planes (16W)*(16H) bytes (Y) and (8W)*(8H) (Cb, Cr).
+ * `ref_planes` is a device array of 3*H264R_MAX_SLOTS device pointers
+ * (Y,Cb,Cr per DPB slot) to full-size planes. */
+typedef struct h264r_batch {
+    int32_t             num_pics;
+    int32_t             width_mbs;
+    int32_t             height_mbs;
+    int32_t             slice_stride;
+    const h264r_mb*     mbs;
+    const int16_t*      levels;
+    const uint32_t*     mv;
+    const int8_t*       ref_idx;
+    const h264r_slice*  slices;
+    const h264r_pic*    pics;
+    const h264r_quant*  quant;       /* one table per picture */
+    const uint8_t* const* ref_planes;
+    uint8_t*            out_y;
+    uint8_t*            out_u;
+    uint8_t*            out_v;
+} h264r_batch;
+
+typedef struct h264r_ctx h264r_ctx;
+
+/* ---- library / device ---------------------------------------------------------- */
+int  h264r_abi_version(void);
+/* Human-readable text for a status code. */
+const char* h264r_strerror(int status);
+/* Number of usable gfx950 devices (0 when no GPU; never falls back to the CPU). */
+int  h264r_device_count(void);
+
+/* ---- quantisation tables (Transform::init + set_quant, transform.cc:173-302) -- */
+/* Flat_4x4_16 / Flat_8x8_16 matrices (no scaling lists). */
+int  h264r_quant_init_flat(h264r_quant* q);
+/* qmatrix[12] already resolved by the caller (fall-back rules A/B, transform.cc:178-254):
+ * lists 0..5 are 16-entry 4x4 lists (Intra Y,Cb,Cr, Inter Y,Cb,Cr), 6..11 64-entry
+ * 8x8 lists (Intra Y, Inter Y, Intra Cb, Inter Cb, Intra Cr, Inter Cr), raster order. */
+int  h264r_quant_init_lists(h264r_quant* q, const int32_t* const qmatrix[12]);
+
+/* ---- context ------------------------------------------------------------------- */
+/* chroma_format_idc must be 1 and bit_depth 8 (other formats: H264R_EUNSUPPORTED). */
+int  h264r_create(h264r_ctx** out, int device, int max_width_mbs, int max_height_mbs,
+                  int chroma_format_idc, int bit_depth);
+int  h264r_destroy(h264r_ctx* ctx);
+
+/* Load (host -> device) a decoded reference picture into DPB slot `slot`
+ * (storable_picture planes after deblock, exit_picture picture.cc:239-269). */
+int  h264r_set_ref(h264r_ctx* ctx, int slot, const uint8_t* y, const uint8_t* u,
+                   const uint8_t* v, int width_mbs, int height_mbs);
+
+/* ---- per-picture streaming API (the Decoder shim drives this) ---------------------- */
+int  h264r_picture_begin(h264r_ctx* ctx, int width_mbs, int height_mbs,
+                         const h264r_pic* pic, const h264r_slice* slices,
+                         const h264r_quant* quant);
+/* Decoder::decode(mb) for MB address mb_addr.  `levels` is this MB's compacted
+ * level block (n_levels int16), mv/ref_idx are its 16 4x4 entries per list in
+ * raster order ([list][16]). */
+int  h264r_mb_submit(h264r_ctx* ctx, int mb_addr, const h264r_mb* mb,
+                     const int16_t* levels, int n_levels,
+                     const uint32_t* mv /*[2][16]*/, const int8_t* ref_idx /*[2][16]*/);
+/* Decoder::deblock_filter: reconstruct + deblock on the GPU, copy planes back.
+ * If keep_as_ref_slot >= 0 the result also stays on the device as that DPB slot. */
+int  h264r_picture_end(h264r_ctx* ctx, uint8_t* y, uint8_t* u, uint8_t* v,
+                       int keep_as_ref_slot);
+
+/* ---- batch API (bench / throughput mode): arrays already on the device ---------- */
+/* Launches recon + deblock for every picture of the batch on `stream`
+ * (a hipStream_t, NULL = the context's stream).  Asynchronous. */
+int  h264r_decode_batch(h264r_ctx* ctx, const h264r_batch* batch, void* stream);
+/* Device pointer of DPB slot planes (for building h264r_batch.ref_planes). */
+int  h264r_ref_planes(h264r_ctx* ctx, int slot, uint8_t** y, uint8_t** u, uint8_t** v);
+
+/* ---- instrumentation ------------------------------------------------------------- */
+/* Average device time (ms) of the last h264r_decode_batch phases, measured with
+ * HIP events on the launch stream: out[0] inter, out[1] intra, out[2] deblock,
+ * out[3] total.  Returns H264R_OK or an error. */
+int  h264r_last_timing(h264r_ctx* ctx, float out_ms[4]);
+int  h264r_set_timing(h264r_ctx* ctx, int enable);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* H264R_H_ */

@@ -1,0 +1,73 @@
+/*
+ * h264r_synth.h -- seeded synthetic post-entropy workload generator.
+ *
+ * Produces canonical h264r inputs (include/h264r.h) with the distributions of
+ * MB-type mixes per picture kind, QP, CBP, level
+ * statistics, quarter-pel motion over all 16 phases, intra modes drawn only
+ * from the modes valid for the actual neighbour availability (the reference
+ * asserts otherwise, intra_prediction.cc:191-873).  Deterministic: the same
+ * (cfg, picture index) always yields the same bytes on every host.  Used by the
+ * benchmark (GPU inputs + CPU baseline), the parity tests and the reference
+ * fixture driver -- identical inputs everywhere.
+ */
+#ifndef H264R_SYNTH_H_
+#define H264R_SYNTH_H_
+
+#include "h264r.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define H264R_SYNTH_INTRA 0   /* config 2: all-intra                     */
+#define H264R_SYNTH_P     1   /* config 3: P pictures (IPPP Main)         */
+#define H264R_SYNTH_B     2   /* config 4/5: B pictures (IBBP High)       */
+
+/* Upper bound of int16 level-pool entries one MB can use (4*64+128+16+8, rounded to 8). */
+#define H264R_SYNTH_MAX_LEVELS_PER_MB 416
+
+typedef struct h264r_synth_cfg {
+    int32_t  width_mbs, height_mbs;
+    int32_t  kind;               /* H264R_SYNTH_*                                         */
+    int32_t  num_slices;         /* contiguous MB-row bands                               */
+    int32_t  deblock_idc;        /* disable_deblocking_filter_idc for every slice         */
+    int32_t  filter_offset_a;    /* FilterOffsetA (even, -12..12)                         */
+    int32_t  filter_offset_b;
+    int32_t  transform8x8;       /* allow 8x8 transform / I_8x8 (High profile)            */
+    int32_t  wp_mode;            /* P: 0/1, B: 0/1/2                                       */
+    int32_t  constrained_intra;  /* pps.constrained_intra_pred_flag                       */
+    int32_t  num_refs;           /* reference pictures (DPB slots 0..num_refs-1), <= 16   */
+    int32_t  qp_min, qp_max;
+    int32_t  pcm_permille;       /* I_PCM MBs per 1000 MBs (0 for the bench configs)      */
+    int32_t  intra_permille;     /* intra MBs in P/B pictures (default 100)               */
+    int32_t  mv_range_x, mv_range_y;   /* integer-pel MV range (default 64 / 32)          */
+    uint64_t seed;
+} h264r_synth_cfg;
+
+/* Fill cfg with the defaults of a SURVEY config (2 intra, 3 P, 4/5 B) at the given size. */
+int  h264r_synth_default(h264r_synth_cfg* cfg, int config_idx, int width_mbs, int height_mbs);
+
+/* Generate picture `index` of the stream.  Caller-owned outputs:
+ *   mbs[W*H], levels[W*H*H264R_SYNTH_MAX_LEVELS_PER_MB] (int16), mv[2*16*W*H],
+ *   ref_idx[2*16*W*H], slices[cfg->num_slices], pic[1].
+ * *n_levels receives the number of pool entries used. */
+int  h264r_synth_picture(const h264r_synth_cfg* cfg, int index, h264r_mb* mbs, int16_t* levels,
+                         int64_t* n_levels, uint32_t* mv, int8_t* ref_idx, h264r_slice* slices,
+                         h264r_pic* pic);
+
+/* Deterministic reference-picture content for DPB slot `slot` (smooth texture + noise). */
+int  h264r_synth_refpic(uint64_t seed, int slot, int width_mbs, int height_mbs,
+                        uint8_t* y, uint8_t* u, uint8_t* v);
+
+/* POC assigned to DPB slot `slot` / to the current picture by the generator. */
+int  h264r_synth_slot_poc(int slot);
+int  h264r_synth_cur_poc(const h264r_synth_cfg* cfg);
+
+/* Algorithmic bytes of a batch: R and W summed over the MBs. */
+int  h264r_synth_algo_bytes(const h264r_mb* mbs, const int8_t* ref_idx, int width_mbs,
+                            int height_mbs, int64_t* read_bytes, int64_t* write_bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,1041 @@
+/*
+ * h264r_oracle.c -- TEST INFRASTRUCTURE ONLY (see h264r_oracle.h).
+ *
+ * Plain-C restatement of the reference's post-entropy reconstruction path on
+ * the canonical formats of include/h264r.h.  Every function names the
+ * reference lines it follows (H/ = R/src/codec/h264/).  Two documented
+ * restatement choices:
+ *   (1) motion compensation walks 4x4 blocks with their own mv_info entry
+ *       instead of the partition walk of decoder.cc:217-254; with the per-4x4
+ *       motion field filled per partition (interpret_mb.cc ref_idx_l/mvd_l)
+ *       both give identical samples (per-sample filter, translation-invariant).
+ *   (2) get_block_luma's padded-plane reads (inter_prediction.cc:185-339) are
+ *       written as per-coordinate clamping; within the 32/12 pads of
+ *       picture.cc:27-37 / pad_buf picture.cc:182-205 the two are identical.
+ * Both choices are pinned by tests/golden (outputs of the compiled reference).
+ */
+#include "h264r_oracle.h"
+
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ---------------------------------------------------------------- helpers */
+static inline int clip3(int lo, int hi, int x) { return x < lo ? lo : (x > hi ? hi : x); } /* defines.h:48-52 */
+static inline int clip1(int hi, int x) { return clip3(0, hi, x); }                         /* defines.h:54-58 */
+static inline int iabs(int x) { return x < 0 ? -x : x; }
+
+/* ------------------------------------------------ quant tables (transform.cc:93-170) */
+static const int dequant_coef[6][4][4] = {
+    {{10, 13, 10, 13}, {13, 16, 13, 16}, {10, 13, 10, 13}, {13, 16, 13, 16}},
+    {{11, 14, 11, 14}, {14, 18, 14, 18}, {11, 14, 11, 14}, {14, 18, 14, 18}},
+    {{13, 16, 13, 16}, {16, 20, 16, 20}, {13, 16, 13, 16}, {16, 20, 16, 20}},
+    {{14, 18, 14, 18}, {18, 23, 18, 23}, {14, 18, 14, 18}, {18, 23, 18, 23}},
+    {{16, 20, 16, 20}, {20, 25, 20, 25}, {16, 20, 16, 20}, {20, 25, 20, 25}},
+    {{18, 23, 18, 23}, {23, 29, 23, 29}, {18, 23, 18, 23}, {23, 29, 23, 29}}};
+
+/* 8x8 normative scale: v[qp%6][class] (spec Table 8-16 form of transform.cc:121-170). */
+static const int dq8_v[6][6] = {
+    {20, 18, 32, 19, 25, 24}, {22, 19, 35, 21, 28, 26}, {26, 23, 42, 24, 33, 31},
+    {28, 25, 45, 26, 35, 33}, {32, 28, 51, 30, 40, 38}, {36, 32, 58, 34, 46, 43}};
+
+static int dq8(int m, int i, int j)
+{
+    /* class of position (i row, j col) */
+    if (i % 4 == 0 && j % 4 == 0) return dq8_v[m][0];
+    if (i % 2 == 1 && j % 2 == 1) return dq8_v[m][1];
+    if (i % 4 == 2 && j % 4 == 2) return dq8_v[m][2];
+    if ((i % 4 == 0 && j % 2 == 1) || (i % 2 == 1 && j % 4 == 0)) return dq8_v[m][3];
+    if ((i % 4 == 0 && j % 4 == 2) || (i % 4 == 2 && j % 4 == 0)) return dq8_v[m][4];
+    return dq8_v[m][5];
+}
+
+void oracle_quant_init_flat(h264r_quant* q)
+{
+    /* Flat_4x4_16 / Flat_8x8_16 (transform.cc:34-50) x dequant_coef (set_quant :264-301) */
+    for (int t = 0; t < 2; ++t)
+        for (int pl = 0; pl < 3; ++pl)
+            for (int m = 0; m < 6; ++m) {
+                for (int k = 0; k < 16; ++k)
+                    q->scale4x4[t][pl][m][k] = (int16_t)(dequant_coef[m][k / 4][k % 4] * 16);
+                for (int k = 0; k < 64; ++k)
+                    q->scale8x8[t][pl][m][k] = (int16_t)(dq8(m, k / 8, k % 8) * 16);
+            }
+}
+
+/* --------------------------------------------- level block layout (include/h264r.h) */
+typedef struct {
+    const int16_t* b8[4];   /* NULL when the 8x8 is not coded */
+    const int16_t* cac;     /* chroma AC, 128 levels, or NULL */
+    const int16_t* ldc;     /* I16x16 luma DC, 16 levels, or NULL */
+    const int16_t* cdc;     /* chroma DC, 8 levels, or NULL */
+} levels_view;
+
+static levels_view view_levels(const h264r_mb* mb, const int16_t* pool)
+{
+    levels_view v;
+    memset(&v, 0, sizeof(v));
+    const int16_t* p = pool + mb->coef_off;
+    int cbpl = mb->cbp & 15, cbpc = mb->cbp >> 4;
+    for (int k = 0; k < 4; ++k)
+        if (cbpl & (1 << k)) { v.b8[k] = p; p += 64; }
+    if (cbpc == 2) { v.cac = p; p += 128; }
+    if (mb->mb_type == H264R_I_16x16) { v.ldc = p; p += 16; }
+    if (cbpc != 0) { v.cdc = p; p += 8; }
+    return v;
+}
+
+/* ----------------------------------------------------- transforms (transform.cc) */
+static void ihadamard_2x2(int c[2][2], int f[2][2])            /* transform.cc:460-481 */
+{
+    int e[2][2];
+    for (int i = 0; i < 2; ++i) { e[i][0] = c[i][0] + c[i][1]; e[i][1] = c[i][0] - c[i][1]; }
+    for (int j = 0; j < 2; ++j) { f[0][j] = e[0][j] + e[1][j]; f[1][j] = e[0][j] - e[1][j]; }
+}
+
+static void ihadamard_4x4(int c[4][4], int f[4][4])            /* transform.cc:515-554 */
+{
+    int e[4][4];
+    for (int i = 0; i < 4; ++i) {
+        int d0 = c[i][0] + c[i][2], d1 = c[i][0] - c[i][2];
+        int d2 = c[i][1] - c[i][3], d3 = c[i][1] + c[i][3];
+        e[i][0] = d0 + d3; e[i][1] = d1 + d2; e[i][2] = d1 - d2; e[i][3] = d0 - d3;
+    }
+    for (int j = 0; j < 4; ++j) {
+        int h0 = e[0][j] + e[2][j], h1 = e[0][j] - e[2][j];
+        int h2 = e[1][j] - e[3][j], h3 = e[1][j] + e[3][j];
+        f[0][j] = h0 + h3; f[1][j] = h1 + h2; f[2][j] = h1 - h2; f[3][j] = h0 - h3;
+    }
+}
+
+static void inverse_4x4(int d[16][16], int r[16][16], int py, int px)   /* transform.cc:597-641 */
+{
+    int f[4][4];
+    for (int i = 0; i < 4; ++i) {
+        int d0 = d[py + i][px + 0], d1 = d[py + i][px + 1];
+        int d2 = d[py + i][px + 2], d3 = d[py + i][px + 3];
+        int e0 = d0 + d2, e1 = d0 - d2, e2 = (d1 >> 1) - d3, e3 = d1 + (d3 >> 1);
+        f[i][0] = e0 + e3; f[i][1] = e1 + e2; f[i][2] = e1 - e2; f[i][3] = e0 - e3;
+    }
+    for (int j = 0; j < 4; ++j) {
+        int g0 = f[0][j] + f[2][j], g1 = f[0][j] - f[2][j];
+        int g2 = (f[1][j] >> 1) - f[3][j], g3 = f[1][j] + (f[3][j] >> 1);
+        r[py + 0][px + j] = (g0 + g3 + 32) >> 6;
+        r[py + 1][px + j] = (g1 + g2 + 32) >> 6;
+        r[py + 2][px + j] = (g1 - g2 + 32) >> 6;
+        r[py + 3][px + j] = (g0 - g3 + 32) >> 6;
+    }
+}
+
+static void idct8_1d(const int in[8], int out[8])                 /* transform.cc:658-683 */
+{
+    int e0 = in[0] + in[4];
+    int e1 = -in[3] + in[5] - in[7] - (in[7] >> 1);
+    int e2 = in[0] - in[4];
+    int e3 = in[1] + in[7] - in[3] - (in[3] >> 1);
+    int e4 = (in[2] >> 1) - in[6];
+    int e5 = -in[1] + in[7] + in[5] + (in[5] >> 1);
+    int e6 = in[2] + (in[6] >> 1);
+    int e7 = in[3] + in[5] + in[1] + (in[1] >> 1);
+    int f0 = e0 + e6, f1 = e1 + (e7 >> 2), f2 = e2 + e4, f3 = e3 + (e5 >> 2);
+    int f4 = e2 - e4, f5 = (e3 >> 2) - e5, f6 = e0 - e6, f7 = e7 - (e1 >> 2);
+    out[0] = f0 + f7; out[1] = f2 + f5; out[2] = f4 + f3; out[3] = f6 + f1;
+    out[4] = f6 - f1; out[5] = f4 - f3; out[6] = f2 - f5; out[7] = f0 - f7;
+}
+
+static void inverse_8x8(int d[16][16], int r[16][16], int py, int px)   /* transform.cc:643-733 */
+{
+    int g[8][8], in[8], out[8];
+    for (int i = 0; i < 8; ++i) {
+        for (int k = 0; k < 8; ++k) in[k] = d[py + i][px + k];
+        idct8_1d(in, g[i]);
+    }
+    for (int j = 0; j < 8; ++j) {
+        for (int k = 0; k < 8; ++k) in[k] = g[k][j];
+        idct8_1d(in, out);
+        for (int k = 0; k < 8; ++k) r[py + k][px + j] = (out[k] + 32) >> 6;
+    }
+}
+
+/* Coefficient push: coeff_luma_ac/coeff_chroma_ac + inverse_quantize (transform.cc:394-456),
+ * transform_luma_dc (:825-856), transform_chroma_dc (:858-910). */
+static void load_cof(const h264r_mb* mb, const int16_t* pool, const h264r_quant* q, int cof[3][16][16])
+{
+    memset(cof, 0, sizeof(int) * 3 * 16 * 16);
+    levels_view v = view_levels(mb, pool);
+    int inter = (mb->flags & H264R_MBF_INTRA) ? 0 : 1;
+    int t8 = (mb->flags & H264R_MBF_T8x8) != 0;
+    int i16 = mb->mb_type == H264R_I_16x16;
+
+    if (i16) {
+        int c[4][4], f[4][4];
+        int qP = mb->qp_scaled[0];
+        int scale = q->scale4x4[0][0][qP % 6][0];
+        for (int i = 0; i < 4; ++i)
+            for (int j = 0; j < 4; ++j) c[i][j] = v.ldc[i * 4 + j];
+        ihadamard_4x4(c, f);
+        for (int i = 0; i < 4; ++i)
+            for (int j = 0; j < 4; ++j) {
+                if (qP >= 36)
+                    cof[0][i * 4][j * 4] = (f[i][j] * scale) * (1 << (qP / 6 - 6));
+                else
+                    cof[0][i * 4][j * 4] = (f[i][j] * scale + (1 << (5 - qP / 6))) >> (6 - qP / 6);
+            }
+    }
+    {
+        int qp = mb->qp_scaled[0], per = qp / 6, rem = qp % 6;
+        for (int b8 = 0; b8 < 4; ++b8) {
+            const int16_t* blk = v.b8[b8];
+            if (!blk) continue;
+            if (!t8) {
+                for (int b4 = 0; b4 < 4; ++b4) {
+                    int bx = (b8 & 1) * 2 + (b4 & 1), by = (b8 >> 1) * 2 + (b4 >> 1);
+                    for (int pos = i16 ? 1 : 0; pos < 16; ++pos) {
+                        int lev = blk[b4 * 16 + pos];
+                        if (!lev) continue;
+                        int s = q->scale4x4[inter][0][rem][pos];
+                        cof[0][by * 4 + pos / 4][bx * 4 + pos % 4] = ((lev * s) * (1 << per) + 8) >> 4;
+                    }
+                }
+            } else {
+                int x0 = (b8 & 1) * 8, y0 = (b8 >> 1) * 8;
+                for (int pos = 0; pos < 64; ++pos) {
+                    int lev = blk[pos];
+                    if (!lev) continue;
+                    int s = q->scale8x8[inter][0][rem][pos];
+                    cof[0][y0 + pos / 8][x0 + pos % 8] = ((lev * s) * (1 << per) + 32) >> 6;
+                }
+            }
+        }
+    }
+    for (int pl = 1; pl <= 2; ++pl) {
+        int qP = mb->qp_scaled[pl];
+        if (v.cdc) {
+            int c[2][2], f[2][2];
+            int scale = q->scale4x4[inter][pl][qP % 6][0];
+            for (int k = 0; k < 4; ++k) c[k / 2][k % 2] = v.cdc[(pl - 1) * 4 + k];
+            ihadamard_2x2(c, f);
+            for (int i = 0; i < 2; ++i)
+                for (int j = 0; j < 2; ++j)
+                    cof[pl][i * 4][j * 4] = ((f[i][j] * scale) * (1 << (qP / 6))) >> 5;
+        }
+        if (v.cac) {
+            const int16_t* blk = v.cac + (pl - 1) * 64;
+            for (int b = 0; b < 4; ++b)
+                for (int pos = 1; pos < 16; ++pos) {
+                    int lev = blk[b * 16 + pos];
+                    if (!lev) continue;
+                    int s = q->scale4x4[inter][pl][qP % 6][pos];
+                    cof[pl][(b / 2) * 4 + pos / 4][(b % 2) * 4 + pos % 4] =
+                        ((lev * s) * (1 << (qP / 6)) + 8) >> 4;
+                }
+        }
+    }
+}
+
+
+/* --------------------------------------------------------------- picture state */
+typedef struct {
+    const oracle_picture* p;
+    int wmb, hmb, W, H, Wc, Hc, W4, H4;
+    int16_t* slice_nr;     /* slice_nr per MB, -1 until decoded (reset_mbs slice_data.cc:55, mb.init :465) */
+    uint8_t  (*strength_ver)[4][16];   /* mb_t::strength_ver, deblock.cc:80 */
+    uint8_t  (*strength_hor)[4][16];   /* mb_t::strength_hor, deblock.cc:159 */
+    uint8_t  (*fver)[2][4];            /* filterVerEdgeFlag[chroma][edge], deblock.cc:255-278 */
+    uint8_t  (*fhor)[2][4];            /* filterHorEdgeFlag */
+} pstate;
+
+static inline const h264r_mb* mb_at(const pstate* s, int addr) { return &s->p->mbs[addr]; }
+static inline const h264r_slice* slice_of(const pstate* s, const h264r_mb* mb) { return &s->p->slices[mb->slice]; }
+
+/* Neighbour::get_neighbour for non-MBAFF frames (neighbour.cc:123-173) followed by the
+ * callers' slice check (e.g. intra_prediction.cc:145-152).  Returns the MB address or -1;
+ * (*ax,*ay) receive the absolute sample location. */
+static int get_neighbour(const pstate* s, int chroma, int addr, int ox, int oy, int* ax, int* ay)
+{
+    int maxW = chroma ? 8 : 16, maxH = chroma ? 8 : 16;
+    int x = (addr % s->wmb) * maxW + ox, y = (addr / s->wmb) * maxH + oy;
+    if (x < 0 || x >= s->wmb * maxW || y < 0 || y >= s->hmb * maxH) return -1;
+    int n = (y / maxH) * s->wmb + (x / maxW);
+    if (s->slice_nr[n] != s->slice_nr[addr]) return -1;
+    *ax = x; *ay = y;
+    return n;
+}
+
+static inline int is_intra(const pstate* s, int addr) { return (mb_at(s, addr)->flags & H264R_MBF_INTRA) != 0; }
+
+/* --------------------------------------------------------- intra prediction */
+typedef struct { int avail[4]; int smp[18 * 18]; int stride; } nbr_t;   /* samples p(x,y), x,y >= -1 */
+#define P(n, x, y) ((n)->smp[((y) + 1) * (n)->stride + ((x) + 1)])
+
+/* Intra4x4 ctor (intra_prediction.cc:137-187) and Intra8x8 ctor (:359-411), size 4 or 8. */
+static void gather_nxn(const pstate* s, int addr, int size, int xO, int yO, const uint8_t* img, int pitch, nbr_t* n)
+{
+    int cip = s->p->pic->constrained_intra_pred;
+    int ax, ay, a0x = 0, a0y = 0, bx = 0, by = 0, cx = 0, cy = 0, dx = 0, dy = 0;
+    int nA[8];
+    for (int i = 0; i < size; ++i) {
+        int tx = 0, ty = 0;
+        nA[i] = get_neighbour(s, 0, addr, xO - 1, yO + i, &tx, &ty);
+        if (i == 0) { a0x = tx; a0y = ty; }
+    }
+    int nB = get_neighbour(s, 0, addr, xO, yO - 1, &bx, &by);
+    int nC = get_neighbour(s, 0, addr, xO + size, yO - 1, &cx, &cy);
+    int nD = get_neighbour(s, 0, addr, xO - 1, yO - 1, &dx, &dy);
+    if (size == 4 && xO == 4 && (yO == 4 || yO == 12)) nC = -1;   /* :154 */
+    if (size == 8 && xO == 8 && yO == 8) nC = -1;                  /* :376 */
+    (void)ax; (void)ay;
+    n->stride = 18;
+    if (cip) {
+        n->avail[0] = 1;
+        for (int i = 0; i < size; ++i) n->avail[0] &= nA[i] >= 0 && is_intra(s, nA[i]);
+        n->avail[1] = nB >= 0 && is_intra(s, nB);
+        n->avail[2] = nC >= 0 && is_intra(s, nC);
+        n->avail[3] = nD >= 0 && is_intra(s, nD);
+    } else {
+        n->avail[0] = nA[0] >= 0; n->avail[1] = nB >= 0;
+        n->avail[2] = nC >= 0;    n->avail[3] = nD >= 0;
+    }
+    if (n->avail[3]) P(n, -1, -1) = img[dy * pitch + dx];
+    if (n->avail[0])
+        for (int y = 0; y < size; ++y) P(n, -1, y) = img[(a0y + y) * pitch + a0x];
+    if (n->avail[1]) {
+        for (int x = 0; x < size; ++x) P(n, x, -1) = img[by * pitch + bx + x];
+        for (int x = size; x < 2 * size; ++x)
+            P(n, x, -1) = n->avail[2] ? img[cy * pitch + cx + (x - size)] : P(n, size - 1, -1);
+        n->avail[2] = n->avail[1];
+    }
+}
+
+static void pred_4x4(nbr_t* n, int mode, int pred[16][16], int xO, int yO)   /* :189-346 */
+{
+#define PR(x, y) pred[yO + (y)][xO + (x)]
+    for (int y = 0; y < 4; ++y)
+        for (int x = 0; x < 4; ++x) {
+            int v;
+            switch (mode) {
+            case 0: v = P(n, x, -1); break;
+            case 1: v = P(n, -1, y); break;
+            case 2: {
+                int aA = n->avail[0], aB = n->avail[1], sum = 0;
+                if (aA || aB) {
+                    if (aA) for (int k = 0; k < 4; ++k) sum += P(n, -1, k);
+                    if (aB) for (int k = 0; k < 4; ++k) sum += P(n, k, -1);
+                    v = (sum + (aA ? 2 : 0) + (aB ? 2 : 0)) >> (1 + aA + aB);
+                } else v = 128;
+                break; }
+            case 3:
+                if (x == 3 && y == 3) v = (P(n, 6, -1) + 3 * P(n, 7, -1) + 2) >> 2;
+                else v = (P(n, x + y, -1) + 2 * P(n, x + y + 1, -1) + P(n, x + y + 2, -1) + 2) >> 2;
+                break;
+            case 4:
+                if (x > y) v = (P(n, x - y - 2, -1) + 2 * P(n, x - y - 1, -1) + P(n, x - y, -1) + 2) >> 2;
+                else if (x < y) v = (P(n, -1, y - x - 2) + 2 * P(n, -1, y - x - 1) + P(n, -1, y - x) + 2) >> 2;
+                else v = (P(n, 0, -1) + 2 * P(n, -1, -1) + P(n, -1, 0) + 2) >> 2;
+                break;
+            case 5: {
+                int z = 2 * x - y;
+                if (z >= 0 && (z & 1) == 0) v = (P(n, x - (y >> 1) - 1, -1) + P(n, x - (y >> 1), -1) + 1) >> 1;
+                else if (z >= 0) v = (P(n, x - (y >> 1) - 2, -1) + 2 * P(n, x - (y >> 1) - 1, -1) + P(n, x - (y >> 1), -1) + 2) >> 2;
+                else if (z == -1) v = (P(n, -1, 0) + 2 * P(n, -1, -1) + P(n, 0, -1) + 2) >> 2;
+                else v = (P(n, -1, y - 2 * x - 1) + 2 * P(n, -1, y - 2 * x - 2) + P(n, -1, y - 2 * x - 3) + 2) >> 2;
+                break; }
+            case 6: {
+                int z = 2 * y - x;
+                if (z >= 0 && (z & 1) == 0) v = (P(n, -1, y - (x >> 1) - 1) + P(n, -1, y - (x >> 1)) + 1) >> 1;
+                else if (z >= 0) v = (P(n, -1, y - (x >> 1) - 2) + 2 * P(n, -1, y - (x >> 1) - 1) + P(n, -1, y - (x >> 1)) + 2) >> 2;
+                else if (z == -1) v = (P(n, -1, 0) + 2 * P(n, -1, -1) + P(n, 0, -1) + 2) >> 2;
+                else v = (P(n, x - 2 * y - 1, -1) + 2 * P(n, x - 2 * y - 2, -1) + P(n, x - 2 * y - 3, -1) + 2) >> 2;
+                break; }
+            case 7:
+                if ((y & 1) == 0) v = (P(n, x + (y >> 1), -1) + P(n, x + (y >> 1) + 1, -1) + 1) >> 1;
+                else v = (P(n, x + (y >> 1), -1) + 2 * P(n, x + (y >> 1) + 1, -1) + P(n, x + (y >> 1) + 2, -1) + 2) >> 2;
+                break;
+            default: {   /* 8: horizontal up */
+                int z = x + 2 * y;
+                if (z < 5 && (z & 1) == 0) v = (P(n, -1, y + (x >> 1)) + P(n, -1, y + (x >> 1) + 1) + 1) >> 1;
+                else if (z < 5) v = (P(n, -1, y + (x >> 1)) + 2 * P(n, -1, y + (x >> 1) + 1) + P(n, -1, y + (x >> 1) + 2) + 2) >> 2;
+                else if (z == 5) v = (P(n, -1, 2) + 3 * P(n, -1, 3) + 2) >> 2;
+                else v = P(n, -1, 3);
+                break; }
+            }
+            PR(x, y) = v;
+        }
+#undef PR
+}
+
+/* Intra8x8::filtering (intra_prediction.cc:413-447): n holds po(), returns p() in f. */
+static void filter_8x8(const nbr_t* n, nbr_t* f)
+{
+    int aA = n->avail[0], aB = n->avail[1], aD = n->avail[3];
+    *f = *n;
+    if (aB) {
+        P(f, 0, -1) = aD ? (P(n, -1, -1) + 2 * P(n, 0, -1) + P(n, 1, -1) + 2) >> 2
+                         : (3 * P(n, 0, -1) + P(n, 1, -1) + 2) >> 2;
+        for (int x = 1; x < 15; ++x) P(f, x, -1) = (P(n, x - 1, -1) + 2 * P(n, x, -1) + P(n, x + 1, -1) + 2) >> 2;
+        P(f, 15, -1) = (P(n, 14, -1) + 3 * P(n, 15, -1) + 2) >> 2;
+    }
+    if (aD) {
+        if (aA && aB) P(f, -1, -1) = (P(n, 0, -1) + 2 * P(n, -1, -1) + P(n, -1, 0) + 2) >> 2;
+        else if (aB) P(f, -1, -1) = (3 * P(n, -1, -1) + P(n, 0, -1) + 2) >> 2;
+        else if (aA) P(f, -1, -1) = (3 * P(n, -1, -1) + P(n, -1, 0) + 2) >> 2;
+        else P(f, -1, -1) = P(n, -1, -1);
+    }
+    if (aA) {
+        P(f, -1, 0) = aD ? (P(n, -1, -1) + 2 * P(n, -1, 0) + P(n, -1, 1) + 2) >> 2
+                         : (3 * P(n, -1, 0) + P(n, -1, 1) + 2) >> 2;
+        for (int y = 1; y < 7; ++y) P(f, -1, y) = (P(n, -1, y - 1) + 2 * P(n, -1, y) + P(n, -1, y + 1) + 2) >> 2;
+        P(f, -1, 7) = (P(n, -1, 6) + 3 * P(n, -1, 7) + 2) >> 2;
+    }
+}
+
+static void pred_8x8(nbr_t* n, int mode, int pred[16][16], int xO, int yO)   /* :449-606 */
+{
+    for (int y = 0; y < 8; ++y)
+        for (int x = 0; x < 8; ++x) {
+            int v;
+            switch (mode) {
+            case 0: v = P(n, x, -1); break;
+            case 1: v = P(n, -1, y); break;
+            case 2: {
+                int aA = n->avail[0], aB = n->avail[1], sum = 0;
+                if (aA || aB) {
+                    if (aA) for (int k = 0; k < 8; ++k) sum += P(n, -1, k);
+                    if (aB) for (int k = 0; k < 8; ++k) sum += P(n, k, -1);
+                    v = (sum + (aA ? 4 : 0) + (aB ? 4 : 0)) >> (2 + aA + aB);
+                } else v = 128;
+                break; }
+            case 3:
+                if (x == 7 && y == 7) v = (P(n, 14, -1) + 3 * P(n, 15, -1) + 2) >> 2;
+                else v = (P(n, x + y, -1) + 2 * P(n, x + y + 1, -1) + P(n, x + y + 2, -1) + 2) >> 2;
+                break;
+            case 4:
+                if (x > y) v = (P(n, x - y - 2, -1) + 2 * P(n, x - y - 1, -1) + P(n, x - y, -1) + 2) >> 2;
+                else if (x < y) v = (P(n, -1, y - x - 2) + 2 * P(n, -1, y - x - 1) + P(n, -1, y - x) + 2) >> 2;
+                else v = (P(n, 0, -1) + 2 * P(n, -1, -1) + P(n, -1, 0) + 2) >> 2;
+                break;
+            case 5: {
+                int z = 2 * x - y;
+                if (z >= 0 && (z & 1) == 0) v = (P(n, x - (y >> 1) - 1, -1) + P(n, x - (y >> 1), -1) + 1) >> 1;
+                else if (z >= 0) v = (P(n, x - (y >> 1) - 2, -1) + 2 * P(n, x - (y >> 1) - 1, -1) + P(n, x - (y >> 1), -1) + 2) >> 2;
+                else if (z == -1) v = (P(n, -1, 0) + 2 * P(n, -1, -1) + P(n, 0, -1) + 2) >> 2;
+                else v = (P(n, -1, y - 2 * x - 1) + 2 * P(n, -1, y - 2 * x - 2) + P(n, -1, y - 2 * x - 3) + 2) >> 2;
+                break; }
+            case 6: {
+                int z = 2 * y - x;
+                if (z >= 0 && (z & 1) == 0) v = (P(n, -1, y - (x >> 1) - 1) + P(n, -1, y - (x >> 1)) + 1) >> 1;
+                else if (z >= 0) v = (P(n, -1, y - (x >> 1) - 2) + 2 * P(n, -1, y - (x >> 1) - 1) + P(n, -1, y - (x >> 1)) + 2) >> 2;
+                else if (z == -1) v = (P(n, -1, 0) + 2 * P(n, -1, -1) + P(n, 0, -1) + 2) >> 2;
+                else v = (P(n, x - 2 * y - 1, -1) + 2 * P(n, x - 2 * y - 2, -1) + P(n, x - 2 * y - 3, -1) + 2) >> 2;
+                break; }
+            case 7:
+                if ((y & 1) == 0) v = (P(n, x + (y >> 1), -1) + P(n, x + (y >> 1) + 1, -1) + 1) >> 1;
+                else v = (P(n, x + (y >> 1), -1) + 2 * P(n, x + (y >> 1) + 1, -1) + P(n, x + (y >> 1) + 2, -1) + 2) >> 2;
+                break;
+            default: {
+                int z = x + 2 * y;
+                if (z < 13 && (z & 1) == 0) v = (P(n, -1, y + (x >> 1)) + P(n, -1, y + (x >> 1) + 1) + 1) >> 1;
+                else if (z < 13) v = (P(n, -1, y + (x >> 1)) + 2 * P(n, -1, y + (x >> 1) + 1) + P(n, -1, y + (x >> 1) + 2) + 2) >> 2;
+                else if (z == 13) v = (P(n, -1, 6) + 3 * P(n, -1, 7) + 2) >> 2;
+                else v = P(n, -1, 7);
+                break; }
+            }
+            pred[yO + y][xO + x] = v;
+        }
+}
+
+/* Intra16x16 ctor + modes (intra_prediction.cc:624-735); chroma=1: Chroma (:748-894), 4:2:0. */
+static void pred_mb(const pstate* s, int addr, int chroma, int mode, const uint8_t* img, int pitch, int pred[16][16])
+{
+    int N = chroma ? 8 : 16;
+    int cip = s->p->pic->constrained_intra_pred;
+    nbr_t nb, *n = &nb;
+    n->stride = 18;
+    int nA[16], ax[16], ay[16], bx = 0, by = 0, dx = 0, dy = 0;
+    for (int i = 0; i < N; ++i) nA[i] = get_neighbour(s, chroma, addr, -1, i, &ax[i], &ay[i]);
+    int nB = get_neighbour(s, chroma, addr, 0, -1, &bx, &by);
+    int nD = get_neighbour(s, chroma, addr, -1, -1, &dx, &dy);
+    int av[4];
+    if (cip) {
+        if (!chroma) {
+            av[0] = 1;
+            for (int i = 0; i < 16; ++i) av[0] &= nA[i] >= 0 && is_intra(s, nA[i]);
+            av[2] = 0;
+        } else {
+            av[0] = 1; av[2] = 1;
+            for (int i = 0; i < N / 2; ++i) av[0] &= nA[i] >= 0 && is_intra(s, nA[i]);
+            for (int i = N / 2; i < N; ++i) av[2] &= nA[i] >= 0 && is_intra(s, nA[i]);
+        }
+        av[1] = nB >= 0 && is_intra(s, nB);
+        av[3] = nD >= 0 && is_intra(s, nD);
+    } else {
+        av[0] = nA[0] >= 0; av[1] = nB >= 0;
+        av[2] = chroma ? nA[0] >= 0 : 0;
+        av[3] = nD >= 0;
+    }
+    if (av[3]) P(n, -1, -1) = img[dy * pitch + dx];
+    if (!chroma) {
+        if (av[0]) for (int y = 0; y < 16; ++y) P(n, -1, y) = img[ay[y] * pitch + ax[y]];
+    } else {
+        if (av[0]) for (int y = 0; y < N / 2; ++y) P(n, -1, y) = img[ay[y] * pitch + ax[y]];
+        if (av[2]) for (int y = N / 2; y < N; ++y) P(n, -1, y) = img[ay[y] * pitch + ax[y]];
+    }
+    if (av[1]) for (int x = 0; x < N; ++x) P(n, x, -1) = img[by * pitch + bx + x];
+
+    if (!chroma) {
+        switch (mode) {
+        case 0: for (int y = 0; y < 16; ++y) for (int x = 0; x < 16; ++x) pred[y][x] = P(n, x, -1); break;
+        case 1: for (int y = 0; y < 16; ++y) for (int x = 0; x < 16; ++x) pred[y][x] = P(n, -1, y); break;
+        case 2: {
+            int sum = 0, v;
+            if (av[0] || av[1]) {
+                if (av[0]) for (int k = 0; k < 16; ++k) sum += P(n, -1, k);
+                if (av[1]) for (int k = 0; k < 16; ++k) sum += P(n, k, -1);
+                v = (sum + (av[0] ? 8 : 0) + (av[1] ? 8 : 0)) >> (3 + av[0] + av[1]);
+            } else v = 128;
+            for (int y = 0; y < 16; ++y) for (int x = 0; x < 16; ++x) pred[y][x] = v;
+            break; }
+        default: {
+            int H = 0, V = 0;
+            for (int x = 0; x < 8; ++x) H += (x + 1) * (P(n, 8 + x, -1) - P(n, 6 - x, -1));
+            for (int y = 0; y < 8; ++y) V += (y + 1) * (P(n, -1, 8 + y) - P(n, -1, 6 - y));
+            int a = 16 * (P(n, -1, 15) + P(n, 15, -1));
+            int b = (5 * H + 32) >> 6, c = (5 * V + 32) >> 6;
+            for (int y = 0; y < 16; ++y)
+                for (int x = 0; x < 16; ++x) pred[y][x] = clip3(0, 255, (a + b * (x - 7) + c * (y - 7) + 16) >> 5);
+            break; }
+        }
+    } else {
+        switch (mode) {
+        case 0: /* DC per 4x4 (intra_prediction.cc:825-849) */
+            for (int blk = 0; blk < 4; ++blk) {
+                int xO = (blk & 1) * 4, yO = (blk >> 1) * 4;
+                int aA, aB;
+                if ((xO == 0 && yO == 0) || (xO > 0 && yO > 0)) { aA = yO > 0 ? av[2] : av[0]; aB = av[1]; }
+                else if (xO > 0 && yO == 0) { aA = av[1] ? 0 : av[0]; aB = av[1]; }
+                else { aA = av[2]; aB = av[2] ? 0 : av[1]; }
+                int sum = 0, v;
+                if (aA || aB) {
+                    if (aA) for (int k = 0; k < 4; ++k) sum += P(n, -1, k + yO);
+                    if (aB) for (int k = 0; k < 4; ++k) sum += P(n, k + xO, -1);
+                    v = (sum + (aA ? 2 : 0) + (aB ? 2 : 0)) >> (1 + aA + aB);
+                } else v = 128;
+                for (int y = 0; y < 4; ++y) for (int x = 0; x < 4; ++x) pred[yO + y][xO + x] = v;
+            }
+            break;
+        case 1: for (int y = 0; y < 8; ++y) for (int x = 0; x < 8; ++x) pred[y][x] = P(n, -1, y); break;
+        case 2: for (int y = 0; y < 8; ++y) for (int x = 0; x < 8; ++x) pred[y][x] = P(n, x, -1); break;
+        default: {
+            int H = 0, V = 0;
+            for (int x = 0; x < 4; ++x) H += (x + 1) * (P(n, 4 + x, -1) - P(n, 2 - x, -1));
+            for (int y = 0; y < 4; ++y) V += (y + 1) * (P(n, -1, 4 + y) - P(n, -1, 2 - y));
+            int a = 16 * (P(n, -1, 7) + P(n, 7, -1));
+            int b = (34 * H + 32) >> 6, c = (34 * V + 32) >> 6;
+            for (int y = 0; y < 8; ++y)
+                for (int x = 0; x < 8; ++x) pred[y][x] = clip3(0, 255, (a + b * (x - 3) + c * (y - 3) + 16) >> 5);
+            break; }
+        }
+    }
+}
+
+/* --------------------------------------------------------- inter prediction */
+static inline int px(const uint8_t* img, int W, int H, int x, int y)
+{
+    return img[clip3(0, H - 1, y) * W + clip3(0, W - 1, x)];
+}
+static inline int tap6(int a, int b, int c, int d, int e, int f) { return a - 5 * b + 20 * c + 20 * d - 5 * e + f; }
+
+/* One luma sample of get_block_luma (inter_prediction.cc:158-340), spec 8.4.2.2.1 form. */
+static int luma_sample(const uint8_t* img, int W, int H, int x, int y, int xf, int yf)
+{
+#define S(dx, dy) px(img, W, H, x + (dx), y + (dy))
+#define B1(dy) tap6(S(-2, dy), S(-1, dy), S(0, dy), S(1, dy), S(2, dy), S(3, dy))
+#define H1(dx) tap6(S(dx, -2), S(dx, -1), S(dx, 0), S(dx, 1), S(dx, 2), S(dx, 3))
+    if (xf == 0 && yf == 0) return S(0, 0);
+    int b = clip1(255, (B1(0) + 16) >> 5);
+    int h = clip1(255, (H1(0) + 16) >> 5);
+    if (yf == 0) return xf == 2 ? b : (S(xf == 1 ? 0 : 1, 0) + b + 1) >> 1;
+    if (xf == 0) return yf == 2 ? h : (S(0, yf == 1 ? 0 : 1) + h + 1) >> 1;
+    if ((xf & 1) && (yf & 1)) {
+        int bb = yf == 3 ? clip1(255, (B1(1) + 16) >> 5) : b;
+        int hh = xf == 3 ? clip1(255, (H1(1) + 16) >> 5) : h;
+        return (bb + hh + 1) >> 1;
+    }
+    int j1 = tap6(B1(-2), B1(-1), B1(0), B1(1), B1(2), B1(3));
+    int j = clip1(255, (j1 + 512) >> 10);
+    if (xf == 2 && yf == 2) return j;
+    if (xf == 2) { int q0 = yf == 3 ? clip1(255, (B1(1) + 16) >> 5) : b; return (j + q0 + 1) >> 1; }
+    { int q0 = xf == 3 ? clip1(255, (H1(1) + 16) >> 5) : h; return (j + q0 + 1) >> 1; }
+#undef S
+#undef B1
+#undef H1
+}
+
+/* get_block_chroma sample (inter_prediction.cc:380-404), 4:2:0 frame. */
+static int chroma_sample(const uint8_t* img, int W, int H, int xi, int yi, int xf, int yf)
+{
+    int A = px(img, W, H, xi, yi), B = px(img, W, H, xi + 1, yi);
+    int C = px(img, W, H, xi, yi + 1), D = px(img, W, H, xi + 1, yi + 1);
+    return ((8 - xf) * (8 - yf) * A + xf * (8 - yf) * B + (8 - xf) * yf * C + xf * yf * D + 32) >> 6;
+}
+
+static inline int rshift_rnd(int x, int a) { return a > 0 ? (x + (1 << (a - 1))) >> a : x * (1 << -a); } /* inter_prediction.cc:35-38 */
+
+/* mb_pred_inter + inter_pred + mc_prediction/bi_prediction (decoder.cc:217-262,
+ * inter_prediction.cc:53-156, 448-536) into mb_pred[3][16][16]. */
+static int inter_pred_mb(const pstate* s, int addr, int mbp[3][16][16])
+{
+    const oracle_picture* p = s->p;
+    const h264r_mb* mb = mb_at(s, addr);
+    const h264r_slice* sl = slice_of(s, mb);
+    int mbx = addr % s->wmb, mby = addr / s->wmb;
+    int plane_n = s->W4 * s->H4;
+    for (int j = 0; j < 4; ++j)
+        for (int i = 0; i < 4; ++i) {
+            int idx = (mby * 4 + j) * s->W4 + mbx * 4 + i;
+            int r[2], vx[2], vy[2], slot[2];
+            for (int l = 0; l < 2; ++l) {
+                r[l] = p->ref_idx[l * plane_n + idx];
+                uint32_t m = p->mv[l * plane_n + idx];
+                vx[l] = (mbx * 4 + i) * 16 + (int16_t)(m & 0xFFFF);
+                vy[l] = (mby * 4 + j) * 16 + (int16_t)(m >> 16);
+                slot[l] = r[l] >= 0 ? sl->ref_slot[l][r[l]] : -1;
+            }
+            int dir = (r[0] >= 0 && r[1] >= 0) ? 2 : (r[0] >= 0 ? 0 : (r[1] >= 0 ? 1 : -1));
+            if (dir < 0) return H264R_EINVAL;
+            for (int l = 0; l < 2; ++l)
+                if ((dir == 2 || dir == l) && (slot[l] < 0 || !p->ref_planes[slot[l]][0])) return H264R_EINVAL;
+            for (int pl = 0; pl < 3; ++pl) {
+                int n = pl ? 2 : 4, ox = pl ? i * 2 : i * 4, oy = pl ? j * 2 : j * 4;
+                int Wp = pl ? s->Wc : s->W, Hp = pl ? s->Hc : s->H;
+                for (int y = 0; y < n; ++y)
+                    for (int x = 0; x < n; ++x) {
+                        int v[2] = {0, 0};
+                        for (int l = 0; l < 2; ++l) {
+                            if (!(dir == 2 || dir == l)) continue;
+                            const uint8_t* img = p->ref_planes[slot[l]][pl];
+                            if (!pl) v[l] = luma_sample(img, Wp, Hp, (vx[l] >> 2) + x, (vy[l] >> 2) + y, vx[l] & 3, vy[l] & 3);
+                            else v[l] = chroma_sample(img, Wp, Hp, (vx[l] >> 3) + x, (vy[l] >> 3) + y, vx[l] & 7, vy[l] & 7);
+                        }
+                        int out;
+                        if (dir != 2) {
+                            int wpf = sl->wp_mode == 1;      /* mc_prediction :62-85 */
+                            if (wpf) {
+                                int w = sl->wp_weight[dir][r[dir]][pl], o = sl->wp_offset[dir][r[dir]][pl];
+                                int d = pl ? sl->chroma_log2_wd : sl->luma_log2_wd;
+                                out = clip1(255, rshift_rnd(w * v[dir], d) + o);
+                            } else out = v[dir];
+                        } else if (sl->wp_mode) {               /* bi_prediction :99-153 */
+                            int w0, w1, o0, o1;
+                            if (sl->wp_mode == 1) {
+                                w0 = sl->wp_weight[0][r[0]][pl]; w1 = sl->wp_weight[1][r[1]][pl];
+                                o0 = sl->wp_offset[0][r[0]][pl]; o1 = sl->wp_offset[1][r[1]][pl];
+                            } else {
+                                w1 = sl->implicit_w1[r[0]][r[1]]; w0 = 64 - w1; o0 = o1 = 0;
+                            }
+                            int d = (pl ? sl->chroma_log2_wd : sl->luma_log2_wd) + 1;
+                            out = clip1(255, rshift_rnd(w0 * v[0] + w1 * v[1], d) + ((o0 + o1 + 1) >> 1));
+                        } else out = (v[0] + v[1] + 1) >> 1;
+                        mbp[pl][oy + y][ox + x] = out;
+                    }
+            }
+        }
+    return 0;
+}
+
+/* ------------------------------------------------------------ construction */
+static uint8_t* plane_ptr(const pstate* s, int pl) { return s->p->out[pl]; }
+
+/* construction / construction_16x16 / construction_chroma (transform.cc:913-984) */
+static void construct(const pstate* s, int addr, int pl, int x0, int y0, int w, int h,
+                      int use_res, int rres[16][16], int mbp[16][16])
+{
+    int mbx = addr % s->wmb, mby = addr / s->wmb;
+    int N = pl ? 8 : 16, pitch = pl ? s->Wc : s->W;
+    uint8_t* img = plane_ptr(s, pl) + (mby * N) * pitch + mbx * N;
+    for (int y = y0; y < y0 + h; ++y)
+        for (int x = x0; x < x0 + w; ++x)
+            img[y * pitch + x] = (uint8_t)(use_res ? clip1(255, rres[y][x] + mbp[y][x]) : mbp[y][x]);
+}
+
+static int intra4_mode(const h264r_mb* mb, int blk) { return (mb->ipred[blk >> 1] >> ((blk & 1) * 4)) & 15; }
+
+/* Decoder::decode (decoder.cc:65-262) for one MB. */
+static int decode_mb(pstate* s, int addr)
+{
+    const oracle_picture* p = s->p;
+    const h264r_mb* mb = mb_at(s, addr);
+    int mbx = addr % s->wmb, mby = addr / s->wmb;
+    static __thread int cof[3][16][16], rres[3][16][16], mbp[3][16][16];
+    s->slice_nr[addr] = (int16_t)mb->slice;               /* mb.init, slice_data.cc:465 */
+    if (mb->flags & H264R_MBF_BYPASS) return H264R_EUNSUPPORTED;
+
+    if (mb->mb_type == H264R_I_PCM) {                      /* mb_pred_ipcm decoder.cc:149-168 */
+        const uint8_t* raw = (const uint8_t*)(p->levels + mb->coef_off);
+        for (int y = 0; y < 16; ++y) for (int x = 0; x < 16; ++x)
+            p->out[0][(mby * 16 + y) * s->W + mbx * 16 + x] = raw[y * 16 + x];
+        for (int k = 0; k < 2; ++k)
+            for (int y = 0; y < 8; ++y) for (int x = 0; x < 8; ++x)
+                p->out[1 + k][(mby * 8 + y) * s->Wc + mbx * 8 + x] = raw[256 + k * 64 + y * 8 + x];
+        return 0;
+    }
+    load_cof(mb, p->levels, p->quant, cof);
+    int cbpl = mb->cbp & 15, cbpc = mb->cbp >> 4;
+
+    if (mb->mb_type == H264R_I_4x4 || mb->mb_type == H264R_I_8x8 || mb->mb_type == H264R_I_16x16) {
+        /* mb_pred_intra decoder.cc:170-208 */
+        const uint8_t* img = p->out[0];
+        int step = mb->mb_type == H264R_I_4x4 ? 1 : mb->mb_type == H264R_I_8x8 ? 4 : 16;
+        for (int b = 0; b < 16; b += step) {
+            int ioff = ((b / 4) % 2) * 8 + ((b % 4) % 2) * 4;
+            int joff = ((b / 4) / 2) * 8 + ((b % 4) / 2) * 4;
+            if (mb->mb_type == H264R_I_4x4) {
+                nbr_t n;
+                gather_nxn(s, addr, 4, ioff, joff, img, s->W, &n);
+                pred_4x4(&n, intra4_mode(mb, b), mbp[0], ioff, joff);
+                int coded = cbpl & (1 << ((joff / 8) * 2 + ioff / 8));
+                if (coded) inverse_4x4(cof[0], rres[0], joff, ioff);
+                construct(s, addr, 0, ioff, joff, 4, 4, coded, rres[0], mbp[0]);
+            } else if (mb->mb_type == H264R_I_8x8) {
+                nbr_t n, f;
+                gather_nxn(s, addr, 8, ioff, joff, img, s->W, &n);
+                filter_8x8(&n, &f);
+                pred_8x8(&f, intra4_mode(mb, b / 4), mbp[0], ioff, joff);
+                int coded = cbpl & (1 << ((joff / 8) * 2 + ioff / 8));
+                if (coded) inverse_8x8(cof[0], rres[0], joff, ioff);
+                construct(s, addr, 0, ioff, joff, 8, 8, coded, rres[0], mbp[0]);
+            } else {
+                pred_mb(s, addr, 0, mb->i16_mode, img, s->W, mbp[0]);
+                for (int y = 0; y < 16; y += 4) for (int x = 0; x < 16; x += 4) inverse_4x4(cof[0], rres[0], y, x);
+                construct(s, addr, 0, 0, 0, 16, 16, 1, rres[0], mbp[0]);
+            }
+        }
+        for (int pl = 1; pl <= 2; ++pl) {
+            pred_mb(s, addr, 1, mb->chroma_mode, p->out[pl], s->Wc, mbp[pl]);
+        }
+        for (int pl = 1; pl <= 2; ++pl) {                  /* inverse_transform_chroma :1033-1049 */
+            for (int y = 0; y < 8; y += 4) for (int x = 0; x < 8; x += 4) inverse_4x4(cof[pl], rres[pl], y, x);
+            construct(s, addr, pl, 0, 0, 8, 8, 1, rres[pl], mbp[pl]);
+        }
+        return 0;
+    }
+
+    int st = inter_pred_mb(s, addr, mbp);
+    if (st) return st;
+    /* inverse_transform_inter transform.cc:1051-1095 */
+    if (cbpl) {
+        if (!(mb->flags & H264R_MBF_T8x8)) {
+            for (int y = 0; y < 16; y += 4)
+                for (int x = 0; x < 16; x += 4) {
+                    int coded = cbpl & (1 << ((y / 8) * 2 + x / 8));
+                    if (coded) inverse_4x4(cof[0], rres[0], y, x);
+                    construct(s, addr, 0, x, y, 4, 4, coded, rres[0], mbp[0]);
+                }
+        } else {
+            for (int y = 0; y < 16; y += 8)
+                for (int x = 0; x < 16; x += 8) {
+                    int coded = cbpl & (1 << ((y / 8) * 2 + x / 8));
+                    if (coded) inverse_8x8(cof[0], rres[0], y, x);
+                    construct(s, addr, 0, x, y, 8, 8, coded, rres[0], mbp[0]);
+                }
+        }
+    } else construct(s, addr, 0, 0, 0, 16, 16, 0, rres[0], mbp[0]);
+    for (int pl = 1; pl <= 2; ++pl) {
+        if (cbpc) {
+            for (int y = 0; y < 8; y += 4) for (int x = 0; x < 8; x += 4) inverse_4x4(cof[pl], rres[pl], y, x);
+            construct(s, addr, pl, 0, 0, 8, 8, 1, rres[pl], mbp[pl]);
+        } else construct(s, addr, pl, 0, 0, 8, 8, 0, rres[pl], mbp[pl]);
+    }
+    return 0;
+}
+
+/* ---------------------------------------------------------------- deblocking */
+static const uint8_t TABLE_ALPHA[52] = {                               /* deblock.cc:294-299 */
+    0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 4, 4, 5, 6, 7, 8, 9, 10, 12, 13,
+    15, 17, 20, 22, 25, 28, 32, 36, 40, 45, 50, 56, 63, 71, 80, 90, 101, 113, 127, 144, 162, 182, 203, 226, 255, 255};
+static const uint8_t TABLE_BETA[52] = {                                /* deblock.cc:301-306 */
+    0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4,
+    6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13, 14, 14, 15, 15, 16, 16, 17, 17, 18, 18};
+static const uint8_t TABLE_TC0[52][3] = {                              /* deblock.cc:310-324 */
+    {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0},
+    {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, {0, 0, 0},
+    {0, 0, 0}, {0, 0, 1}, {0, 0, 1}, {0, 0, 1}, {0, 0, 1}, {0, 1, 1}, {0, 1, 1}, {1, 1, 1},
+    {1, 1, 1}, {1, 1, 1}, {1, 1, 1}, {1, 1, 2}, {1, 1, 2}, {1, 1, 2}, {1, 1, 2}, {1, 2, 3},
+    {1, 2, 3}, {2, 2, 3}, {2, 2, 4}, {2, 3, 4}, {2, 3, 4}, {3, 3, 5}, {3, 4, 6}, {3, 4, 6},
+    {4, 5, 7}, {4, 5, 8}, {4, 6, 9}, {5, 7, 10}, {6, 8, 11}, {6, 8, 13}, {7, 10, 14}, {8, 11, 16},
+    {9, 12, 18}, {10, 13, 20}, {11, 15, 23}, {13, 17, 25}};
+
+typedef struct { int ref[2]; int mvx[2], mvy[2]; } mvinfo_t;
+
+/* pic_motion_params of one 4x4 block; ref = DPB slot identity (ref_pic pointer) or -1. */
+static mvinfo_t mvinfo(const pstate* s, int bx4, int by4)
+{
+    const oracle_picture* p = s->p;
+    int plane_n = s->W4 * s->H4, idx = by4 * s->W4 + bx4;
+    const h264r_mb* mb = mb_at(s, (by4 / 4) * s->wmb + bx4 / 4);
+    const h264r_slice* sl = slice_of(s, mb);
+    mvinfo_t m;
+    for (int l = 0; l < 2; ++l) {
+        int r = p->ref_idx[l * plane_n + idx];
+        uint32_t v = p->mv[l * plane_n + idx];
+        m.ref[l] = r >= 0 ? sl->ref_slot[l][r] : -1;
+        m.mvx[l] = (int16_t)(v & 0xFFFF);
+        m.mvy[l] = (int16_t)(v >> 16);
+    }
+    return m;
+}
+
+static inline int compare_mvs(const mvinfo_t* a, int la, const mvinfo_t* b, int lb)   /* deblock.cc:35-38 */
+{
+    return (iabs(a->mvx[la] - b->mvx[lb]) >= 4) | (iabs(a->mvy[la] - b->mvy[lb]) >= 4);
+}
+
+static int bs_compare_mvs(const mvinfo_t* p, const mvinfo_t* q)     /* deblock.cc:40-75 */
+{
+    int p0 = p->ref[0], q0 = q->ref[0], p1 = p->ref[1], q1 = q->ref[1];
+    if ((p0 == q0 && p1 == q1) || (p0 == q1 && p1 == q0)) {
+        if (p0 != p1) {
+            if (p0 == q0) return compare_mvs(p, 0, q, 0) | compare_mvs(p, 1, q, 1);
+            return compare_mvs(p, 0, q, 1) | compare_mvs(p, 1, q, 0);
+        }
+        return (compare_mvs(p, 0, q, 0) | compare_mvs(p, 1, q, 1)) &
+               (compare_mvs(p, 0, q, 1) | compare_mvs(p, 1, q, 0));
+    }
+    return 1;
+}
+
+static int is_special(const pstate* s, const h264r_mb* m)
+{
+    int t = slice_of(s, m)->slice_type;
+    return t == H264R_SLICE_SP || t == H264R_SLICE_SI;
+}
+
+/* Deblock::strength + strength_vertical/horizontal (deblock.cc:78-289), frame pictures. */
+static void strength(pstate* s, int addr)
+{
+    const h264r_mb* q = mb_at(s, addr);
+    const h264r_slice* sl = slice_of(s, q);
+    int mbx = addr % s->wmb, mby = addr / s->wmb;
+    memset(s->fver[addr], 0, sizeof(s->fver[addr]));
+    memset(s->fhor[addr], 0, sizeof(s->fhor[addr]));
+    if (sl->deblock_idc == 1) return;
+    int L = mbx > 0 ? addr - 1 : -1, U = mby > 0 ? addr - s->wmb : -1;
+    int fl = 0, ft = 0;
+    if (sl->deblock_idc == 0) { fl = L >= 0; ft = U >= 0; }
+    else if (sl->deblock_idc == 2) {
+        fl = L >= 0 && mb_at(s, L)->slice == q->slice;
+        ft = U >= 0 && mb_at(s, U)->slice == q->slice;
+    }
+    for (int c = 0; c < 2; ++c) {
+        s->fver[addr][c][0] = fl; s->fhor[addr][c][0] = ft;
+        for (int e = 1; e < 4; ++e) s->fver[addr][c][e] = s->fhor[addr][c][e] = 1;
+    }
+    if (q->flags & H264R_MBF_T8x8) s->fver[addr][0][1] = s->fver[addr][0][3] = s->fhor[addr][0][1] = s->fhor[addr][0][3] = 0;
+    s->fver[addr][1][2] = s->fver[addr][1][3] = s->fhor[addr][1][2] = s->fhor[addr][1][3] = 0;
+
+    int qintra = (q->flags & H264R_MBF_INTRA) != 0;
+    int pskip = sl->slice_type == H264R_SLICE_P && q->mb_type == H264R_P_SKIP;
+    for (int e = 0; e < 4; ++e) {
+        if (s->fver[addr][0][e]) {                                  /* strength_vertical */
+            uint8_t* St = s->strength_ver[addr][e];
+            const h264r_mb* pm = e == 0 ? mb_at(s, L) : q;
+            int special = is_special(s, pm) || is_special(s, q);
+            if (e == 0 && special) memset(St, 4, 16);
+            else if (special) memset(St, 3, 16);
+            else if (e > 0 && pskip) memset(St, 0, 16);
+            else {
+                int intra = qintra || (pm->flags & H264R_MBF_INTRA);
+                for (int y = 0; y < 16; ++y) {
+                    int v;
+                    int blkQ = (y & 12) + e, blkP = (y & 12) + (e == 0 ? 3 : e - 1);
+                    if (e == 0 && intra) v = 4;
+                    else if (intra) v = 3;
+                    else if (((q->cbp_blks >> blkQ) & 1) || ((pm->cbp_blks >> blkP) & 1)) v = 2;
+                    else if (e > 0 && (q->mb_type == H264R_P_16x16 || q->mb_type == H264R_P_16x8)) v = 0;
+                    else {
+                        mvinfo_t mq = mvinfo(s, mbx * 4 + e, mby * 4 + y / 4);
+                        mvinfo_t mp = mvinfo(s, mbx * 4 + e - 1, mby * 4 + y / 4);
+                        v = bs_compare_mvs(&mq, &mp);
+                    }
+                    St[y] = (uint8_t)v;
+                }
+            }
+        }
+        if (s->fhor[addr][0][e]) {                                  /* strength_horizontal */
+            uint8_t* St = s->strength_hor[addr][e];
+            const h264r_mb* pm = e == 0 ? mb_at(s, U) : q;
+            int special = is_special(s, pm) || is_special(s, q);
+            int intra = qintra || (pm->flags & H264R_MBF_INTRA);
+            if (e == 0 && (special || intra)) memset(St, 4, 16);
+            else if (special || intra) memset(St, 3, 16);
+            else if (e > 0 && pskip) memset(St, 0, 16);
+            else {
+                for (int x4 = 0; x4 < 4; ++x4) {
+                    int v;
+                    int blkQ = 4 * e + x4, blkP = (e == 0 ? 12 : 4 * (e - 1)) + x4;
+                    if (((q->cbp_blks >> blkQ) & 1) || ((pm->cbp_blks >> blkP) & 1)) v = 2;
+                    else if (e > 0 && (q->mb_type == H264R_P_16x16 || q->mb_type == H264R_P_8x16)) v = 0;
+                    else {
+                        mvinfo_t mq = mvinfo(s, mbx * 4 + x4, mby * 4 + e);
+                        mvinfo_t mp = mvinfo(s, mbx * 4 + x4, mby * 4 + e - 1);
+                        v = bs_compare_mvs(&mq, &mp);
+                    }
+                    memset(St + 4 * x4, v, 4);
+                }
+            }
+        }
+    }
+}
+
+/* filter_strong / filter_normal (deblock.cc:327-415) on one line across the edge. */
+static void filter_line(uint8_t* q, int inc, int alpha, int beta, int bS, int chroma, int tc0)
+{
+#define Pp(i) q[-((i) + 1) * inc]
+#define Qq(i) q[(i) * inc]
+    int p0 = Pp(0), p1 = Pp(1), p2 = Pp(2), q0 = Qq(0), q1 = Qq(1), q2 = Qq(2);
+    if (!(iabs(p0 - q0) < alpha && iabs(p1 - p0) < beta && iabs(q1 - q0) < beta)) return;
+    int ap = iabs(p2 - p0), aq = iabs(q2 - q0);
+    if (bS == 4) {
+        int np0, np1, np2, nq0, nq1, nq2;
+        if (!chroma && ap < beta && iabs(p0 - q0) < (alpha >> 2) + 2) {
+            int p3 = Pp(3);
+            np0 = (p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3;
+            np1 = (p2 + p1 + p0 + q0 + 2) >> 2;
+            np2 = (2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3;
+        } else { np0 = (2 * p1 + p0 + q1 + 2) >> 2; np1 = p1; np2 = p2; }
+        if (!chroma && aq < beta && iabs(p0 - q0) < (alpha >> 2) + 2) {
+            int q3 = Qq(3);
+            nq0 = (p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3;
+            nq1 = (p0 + q0 + q1 + q2 + 2) >> 2;
+            nq2 = (2 * q3 + 3 * q2 + q1 + q0 + p0 + 4) >> 3;
+        } else { nq0 = (2 * q1 + q0 + p1 + 2) >> 2; nq1 = q1; nq2 = q2; }
+        Pp(0) = (uint8_t)np0; Pp(1) = (uint8_t)np1; Pp(2) = (uint8_t)np2;
+        Qq(0) = (uint8_t)nq0; Qq(1) = (uint8_t)nq1; Qq(2) = (uint8_t)nq2;
+    } else {
+        int tc = chroma ? tc0 + 1 : tc0 + (ap < beta) + (aq < beta);
+        int delta = clip3(-tc, tc, (((q0 - p0) * 4) + (p1 - q1) + 4) >> 3);
+        int np1 = p1, nq1 = q1;
+        if (!chroma && ap < beta) np1 = p1 + clip3(-tc0, tc0, (p2 + ((p0 + q0 + 1) >> 1) - (p1 * 2)) >> 1);
+        if (!chroma && aq < beta) nq1 = q1 + clip3(-tc0, tc0, (q2 + ((p0 + q0 + 1) >> 1) - (q1 * 2)) >> 1);
+        Pp(0) = (uint8_t)clip1(255, p0 + delta);
+        Qq(0) = (uint8_t)clip1(255, q0 - delta);
+        Pp(1) = (uint8_t)np1; Qq(1) = (uint8_t)nq1;
+    }
+#undef Pp
+#undef Qq
+}
+
+/* filter_edge (deblock.cc:418-486), frame pictures, 4:2:0.  `edge` is the sample offset. */
+static void filter_edge(pstate* s, int addr, int chroma, int pl, int vertical, int edge)
+{
+    const h264r_mb* q = mb_at(s, addr);
+    const h264r_slice* sl = slice_of(s, q);
+    int mbx = addr % s->wmb, mby = addr / s->wmb;
+    const uint8_t* St = vertical ? s->strength_ver[addr][chroma ? edge * 4 / 8 : edge / 4]
+                                 : s->strength_hor[addr][chroma ? edge * 4 / 8 : edge / 4];
+    int nE = chroma ? 8 : 16;
+    int pitch = chroma ? s->Wc : s->W;
+    int x0 = mbx * nE, y0 = mby * nE;
+    uint8_t* img = s->p->out[pl];
+    int paddr = edge == 0 ? (vertical ? addr - 1 : addr - s->wmb) : addr;
+    const h264r_mb* pm = mb_at(s, paddr);
+    int qPp = chroma ? pm->qp_c[pl - 1] : pm->qp_y, qPq = chroma ? q->qp_c[pl - 1] : q->qp_y;
+    int qPav = (qPp + qPq + 1) >> 1;
+    int indexA = clip3(0, 51, qPav + sl->filter_offset_a);
+    int indexB = clip3(0, 51, qPav + sl->filter_offset_b);
+    int alpha = TABLE_ALPHA[indexA], beta = TABLE_BETA[indexB];
+    for (int pel = 0; pel < nE; ++pel) {
+        int bS = St[chroma ? pel << 1 : pel];
+        if (!bS) continue;
+        uint8_t* qp = vertical ? &img[(y0 + pel) * pitch + x0 + edge] : &img[(y0 + edge) * pitch + x0 + pel];
+        int inc = vertical ? 1 : pitch;
+        filter_line(qp, inc, alpha, beta, bS, chroma, bS < 4 ? TABLE_TC0[indexA][bS - 1] : 0);
+    }
+}
+
+/* deblock_pic (deblock.cc:537-552) + the Deblock::deblock gate (:631-640). */
+int oracle_deblock_picture(const oracle_picture* p)
+{
+    int n = p->width_mbs * p->height_mbs;
+    pstate s;
+    s.p = p; s.wmb = p->width_mbs; s.hmb = p->height_mbs;
+    s.W = s.wmb * 16; s.H = s.hmb * 16; s.Wc = s.wmb * 8; s.Hc = s.hmb * 8; s.W4 = s.wmb * 4; s.H4 = s.hmb * 4;
+    int any = 0;
+    for (int i = 0; i < p->pic->num_slices; ++i) any |= p->slices[i].deblock_idc != 1;
+    if (!any) return 0;
+    s.slice_nr = NULL;
+    s.strength_ver = calloc((size_t)n, sizeof(*s.strength_ver));
+    s.strength_hor = calloc((size_t)n, sizeof(*s.strength_hor));
+    s.fver = calloc((size_t)n, sizeof(*s.fver));
+    s.fhor = calloc((size_t)n, sizeof(*s.fhor));
+    if (!s.strength_ver || !s.strength_hor || !s.fver || !s.fhor) {
+        free(s.strength_ver); free(s.strength_hor); free(s.fver); free(s.fhor);
+        return H264R_ENOMEM;
+    }
+    for (int a = 0; a < n; ++a) strength(&s, a);
+    for (int a = 0; a < n; ++a) {
+        /* filter_vertical (:488-504) then filter_horizontal (:506-535) */
+        for (int e = 0; e < 4; ++e) {
+            if (s.fver[a][0][e]) filter_edge(&s, a, 0, 0, 1, e * 4);
+            if (s.fver[a][1][e]) { filter_edge(&s, a, 1, 1, 1, e * 4); filter_edge(&s, a, 1, 2, 1, e * 4); }
+        }
+        for (int e = 0; e < 4; ++e) {
+            if (s.fhor[a][0][e]) filter_edge(&s, a, 0, 0, 0, e * 4);
+            if (s.fhor[a][1][e]) { filter_edge(&s, a, 1, 1, 0, e * 4); filter_edge(&s, a, 1, 2, 0, e * 4); }
+        }
+    }
+    free(s.strength_ver); free(s.strength_hor); free(s.fver); free(s.fhor);
+    return 0;
+}
+
+int oracle_reconstruct_picture(const oracle_picture* p)
+{
+    int n = p->width_mbs * p->height_mbs;
+    pstate s;
+    memset(&s, 0, sizeof(s));
+    s.p = p; s.wmb = p->width_mbs; s.hmb = p->height_mbs;
+    s.W = s.wmb * 16; s.H = s.hmb * 16; s.Wc = s.wmb * 8; s.Hc = s.hmb * 8; s.W4 = s.wmb * 4; s.H4 = s.hmb * 4;
+    s.slice_nr = malloc(sizeof(int16_t) * (size_t)n);
+    if (!s.slice_nr) return H264R_ENOMEM;
+    for (int a = 0; a < n; ++a) s.slice_nr[a] = -1;
+    int st = 0;
+    for (int a = 0; a < n && !st; ++a) st = decode_mb(&s, a);
+    free(s.slice_nr);
+    return st;
+}
+
+int oracle_decode_picture(const oracle_picture* p)
+{
+    int st = oracle_reconstruct_picture(p);
+    if (st) return st;
+    return oracle_deblock_picture(p);
+}
+
+typedef struct { const oracle_picture* pics; int n, tid, threads, status; } job_t;
+static void* worker(void* arg)
+{
+    job_t* j = (job_t*)arg;
+    for (int i = j->tid; i < j->n; i += j->threads) {
+        int st = oracle_decode_picture(&j->pics[i]);
+        if (st) j->status = st;
+    }
+    return NULL;
+}
+
+int oracle_decode_pictures(const oracle_picture* pics, int n, int threads)
+{
+    if (threads <= 1) {
+        for (int i = 0; i < n; ++i) { int st = oracle_decode_picture(&pics[i]); if (st) return st; }
+        return 0;
+    }
+    pthread_t th[256];
+    job_t jobs[256];
+    if (threads > 256) threads = 256;
+    for (int t = 0; t < threads; ++t) {
+        jobs[t].pics = pics; jobs[t].n = n; jobs[t].tid = t; jobs[t].threads = threads; jobs[t].status = 0;
+        pthread_create(&th[t], NULL, worker, &jobs[t]);
+    }
+    int st = 0;
+    for (int t = 0; t < threads; ++t) { pthread_join(th[t], NULL); if (jobs[t].status) st = jobs[t].status; }
+    return st;
+}

@@ -1,0 +1,334 @@
+/*
+ * ref_driver.cc -- TEST INFRASTRUCTURE ONLY.  Drives the *unmodified* reference
+ * decoder (luuvish/arrow-h264, compiled from /root/reference by oracle/Makefile)
+ * on one synthetic picture and writes its output planes, so that the oracle
+ * restatement and the GPU path can be pinned to the reference's own bytes.
+ *
+ * It contains no reference code: it includes the reference headers and calls
+ * the reference's per-MB boundary exactly as the parser would:
+ *   Decoder::assign_quant_params  (slice_header.cc:185)
+ *   Decoder::init                 (slice_data.cc:618)
+ *   Decoder::coeff_luma_dc/ac, coeff_chroma_dc/ac, transform_luma_dc/chroma_dc
+ *                                  (interpret_residual.cc:159-170, 405-415, 430, 475)
+ *   Decoder::decode(mb)            (slice_data.cc:646), MBs in raster order
+ *   Decoder::deblock_filter        (picture.cc:253)
+ * Reference pictures are padded with the reference's own pad_buf (picture.cc:182).
+ *
+ * usage: ref_driver W H kind nslices idc offA offB t8 wp cip nrefs qpmin qpmax
+ *                   pcm_permille intra_permille mvx mvy seed index out.yuv [recon_only]
+ * Output: Y plane then Cb then Cr, 8-bit, unpadded.
+ */
+#include "global.h"
+#include "slice.h"
+#include "dpb.h"
+#include "macroblock.h"
+#include "decoder.h"
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+extern "C" {
+#include "h264r.h"
+#include "h264r_synth.h"
+}
+
+extern void pad_buf(px_t* pImgBuf, int iWidth, int iHeight, int iStride, int iPadX, int iPadY);
+
+using namespace vio::h264;
+
+static void zigzag(int n, int* inv /* raster -> scan index */)
+{
+    /* frame zig-zag (spec Tables 8-12/8-13): anti-diagonals, odd ones top-right to bottom-left */
+    int idx = 0;
+    for (int s = 0; s <= 2 * (n - 1); ++s) {
+        if (s & 1) {
+            for (int x = (s < n ? s : n - 1); x >= 0 && s - x < n; --x) inv[(s - x) * n + x] = idx++;
+        } else {
+            for (int x = (s < n ? 0 : s - n + 1); x <= s && x < n; ++x) inv[(s - x) * n + x] = idx++;
+        }
+    }
+}
+
+int main(int argc, char** argv)
+{
+    if (argc < 21) {
+        fprintf(stderr, "usage: %s W H kind nslices idc offA offB t8 wp cip nrefs qpmin qpmax pcm intra mvx mvy seed index out [recon_only]\n", argv[0]);
+        return 2;
+    }
+    h264r_synth_cfg cfg;
+    memset(&cfg, 0, sizeof(cfg));
+    int k = 1;
+    cfg.width_mbs = atoi(argv[k++]); cfg.height_mbs = atoi(argv[k++]);
+    cfg.kind = atoi(argv[k++]); cfg.num_slices = atoi(argv[k++]);
+    cfg.deblock_idc = atoi(argv[k++]); cfg.filter_offset_a = atoi(argv[k++]); cfg.filter_offset_b = atoi(argv[k++]);
+    cfg.transform8x8 = atoi(argv[k++]); cfg.wp_mode = atoi(argv[k++]); cfg.constrained_intra = atoi(argv[k++]);
+    cfg.num_refs = atoi(argv[k++]); cfg.qp_min = atoi(argv[k++]); cfg.qp_max = atoi(argv[k++]);
+    cfg.pcm_permille = atoi(argv[k++]); cfg.intra_permille = atoi(argv[k++]);
+    cfg.mv_range_x = atoi(argv[k++]); cfg.mv_range_y = atoi(argv[k++]);
+    cfg.seed = strtoull(argv[k++], nullptr, 0);
+    int index = atoi(argv[k++]);
+    const char* out_path = argv[k++];
+    bool recon_only = argc > k && atoi(argv[k]) != 0;
+
+    const int W = cfg.width_mbs, H = cfg.height_mbs, NMB = W * H, W4 = W * 4, PL = W4 * H * 4;
+    std::vector<h264r_mb> mbs(NMB);
+    std::vector<int16_t> levels((size_t)NMB * H264R_SYNTH_MAX_LEVELS_PER_MB);
+    std::vector<uint32_t> mv(2 * (size_t)PL);
+    std::vector<int8_t> ref_idx(2 * (size_t)PL);
+    std::vector<h264r_slice> slices(cfg.num_slices);
+    h264r_pic pic;
+    int64_t nlev = 0;
+    if (h264r_synth_picture(&cfg, index, mbs.data(), levels.data(), &nlev, mv.data(), ref_idx.data(),
+                            slices.data(), &pic) != H264R_OK) {
+        fprintf(stderr, "synth failed\n");
+        return 3;
+    }
+
+    VideoParameters* vid = new VideoParameters();
+    sps_t* sps = new sps_t();
+    pps_t* pps = new pps_t();
+    sps->profile_idc = 100; sps->level_idc = 51;
+    sps->chroma_format_idc = 1; sps->ChromaArrayType = 1;
+    sps->SubWidthC = 2; sps->SubHeightC = 2; sps->MbWidthC = 8; sps->MbHeightC = 8;
+    sps->BitDepthY = 8; sps->BitDepthC = 8;
+    sps->frame_mbs_only_flag = 1; sps->direct_8x8_inference_flag = 1;
+    sps->PicWidthInMbs = W; sps->FrameHeightInMbs = H;
+    sps->PicWidthInSamplesL = W * 16; sps->PicWidthInSamplesC = W * 8;
+    sps->PicHeightInMapUnits = H; sps->PicSizeInMapUnits = W * H;
+    pps->entropy_coding_mode_flag = 0;
+    pps->weighted_pred_flag = cfg.kind == H264R_SYNTH_P && cfg.wp_mode == 1;
+    pps->weighted_bipred_idc = cfg.kind == H264R_SYNTH_B ? cfg.wp_mode : 0;
+    pps->constrained_intra_pred_flag = cfg.constrained_intra;
+    pps->transform_8x8_mode_flag = cfg.transform8x8;
+    pps->deblocking_filter_control_present_flag = 1;
+    vid->active_sps = sps; vid->active_pps = pps;
+    vid->no_reference_picture = nullptr;
+
+    /* DPB: reference pictures, padded like exit_picture (picture.cc:258-259) */
+    std::vector<storable_picture*> refs(cfg.num_refs);
+    std::vector<uint8_t> ty(W * 16 * H * 16), tu(W * 8 * H * 8), tv(W * 8 * H * 8);
+    for (int s = 0; s < cfg.num_refs; ++s) {
+        storable_picture* r = new storable_picture(vid, FRAME, W * 16, H * 16, W * 8, H * 8, 1);
+        h264r_synth_refpic(cfg.seed, s, W, H, ty.data(), tu.data(), tv.data());
+        for (int y = 0; y < H * 16; ++y) for (int x = 0; x < W * 16; ++x) r->imgY[y][x] = ty[y * W * 16 + x];
+        for (int y = 0; y < H * 8; ++y) for (int x = 0; x < W * 8; ++x) {
+            r->imgUV[0][y][x] = tu[y * W * 8 + x];
+            r->imgUV[1][y][x] = tv[y * W * 8 + x];
+        }
+        pad_buf(*r->imgY, W * 16, H * 16, r->iLumaStride, MCBUF_LUMA_PAD_X, MCBUF_LUMA_PAD_Y);
+        pad_buf(*r->imgUV[0], W * 8, H * 8, r->iChromaStride, MCBUF_CHROMA_PAD_X, MCBUF_CHROMA_PAD_Y);
+        pad_buf(*r->imgUV[1], W * 8, H * 8, r->iChromaStride, MCBUF_CHROMA_PAD_X, MCBUF_CHROMA_PAD_Y);
+        r->poc = r->frame_poc = r->top_poc = r->bottom_poc = h264r_synth_slot_poc(s);
+        r->is_long_term = 0; r->used_for_reference = 1;
+        refs[s] = r;
+    }
+
+    storable_picture* dec = new storable_picture(vid, FRAME, W * 16, H * 16, W * 8, H * 8, 1);
+    dec->sps = sps; dec->pps = pps;
+    dec->used_for_reference = 1;
+    dec->poc = dec->frame_poc = pic.poc;
+    vid->dec_picture = dec;
+    mb_t* mb_data = new mb_t[NMB];
+    memset((void*)mb_data, 0, sizeof(mb_t) * NMB);
+    for (int a = 0; a < NMB; ++a) mb_data[a].slice_nr = -1;   /* reset_mbs, slice_data.cc:53-58 */
+    vid->mb_data = mb_data;
+
+    std::vector<slice_t*> sl(cfg.num_slices);
+    for (int s = 0; s < cfg.num_slices; ++s) {
+        const h264r_slice& c = slices[s];
+        slice_t* x = new slice_t();
+        x->p_Vid = vid; x->active_sps = sps; x->active_pps = pps;
+        shr_t& h = x->header;
+        h.slice_type = c.slice_type;
+        h.structure = FRAME; h.MbaffFrameFlag = 0; h.field_pic_flag = 0;
+        h.PicHeightInMbs = H; h.PicHeightInSamplesL = H * 16; h.PicHeightInSamplesC = H * 8;
+        h.PicSizeInMbs = W * H;
+        h.disable_deblocking_filter_idc = c.deblock_idc;
+        h.FilterOffsetA = c.filter_offset_a; h.FilterOffsetB = c.filter_offset_b;
+        h.luma_log2_weight_denom = c.luma_log2_wd; h.chroma_log2_weight_denom = c.chroma_log2_wd;
+        h.PicOrderCnt = h.TopFieldOrderCnt = h.BottomFieldOrderCnt = pic.poc;
+        h.direct_spatial_mv_pred_flag = 0;
+        for (int l = 0; l < 2; ++l)
+            for (int pl = 0; pl < 3; ++pl) {
+                h.pred_weight_l[l][pl].resize(H264R_MAX_REFS);
+                for (int i = 0; i < H264R_MAX_REFS; ++i) {
+                    h.pred_weight_l[l][pl][i].weight_flag = 1;
+                    h.pred_weight_l[l][pl][i].weight = c.wp_weight[l][i][pl];
+                    h.pred_weight_l[l][pl][i].offset = c.wp_offset[l][i][pl];
+                }
+            }
+        for (int l = 0; l < 2; ++l) {
+            x->RefPicSize[l] = (char)c.num_ref[l];
+            for (int i = 0; i < c.num_ref[l]; ++i) x->RefPicList[l][i] = refs[c.ref_slot[l][i]];
+        }
+        x->current_slice_nr = (short)s;
+        x->dec_picture = dec;
+        x->neighbour.mb_data = mb_data;
+        x->decoder.init(*x);
+        x->decoder.assign_quant_params(*x);
+        dec->slice_headers.push_back(x);
+        sl[s] = x;
+    }
+
+    /* motion field (written by the parser, interpret_mb.cc:583-623) */
+    for (int y4 = 0; y4 < H * 4; ++y4)
+        for (int x4 = 0; x4 < W4; ++x4) {
+            int idx = y4 * W4 + x4;
+            const h264r_mb& m = mbs[(y4 / 4) * W + x4 / 4];
+            pic_motion_params& p = dec->mv_info[y4][x4];
+            p.slice_no = (uint8_t)m.slice;
+            for (int l = 0; l < 2; ++l) {
+                int r = ref_idx[(size_t)l * PL + idx];
+                uint32_t v = mv[(size_t)l * PL + idx];
+                p.ref_idx[l] = (char)r;
+                p.mv[l].mv_x = (int16_t)(v & 0xFFFF);
+                p.mv[l].mv_y = (int16_t)(v >> 16);
+                p.ref_pic[l] = r >= 0 ? sl[m.slice]->RefPicList[l][r] : nullptr;
+            }
+        }
+
+    int inv4[16], inv8[64];
+    zigzag(4, inv4);
+    zigzag(8, inv8);
+
+    for (int a = 0; a < NMB; ++a) {
+        const h264r_mb& c = mbs[a];
+        slice_t& s = *sl[c.slice];
+        mb_t& mb = mb_data[a];
+        mb.p_Slice = &s; mb.mbAddrX = a; mb.mb.x = a % W; mb.mb.y = a / W;
+        mb.slice_nr = (short)c.slice;
+        mb.is_intra_block = (c.flags & H264R_MBF_INTRA) != 0;
+        mb.mb_type = c.mb_type;
+        mb.transform_size_8x8_flag = (c.flags & H264R_MBF_T8x8) != 0;
+        mb.mb_field_decoding_flag = 0;
+        for (int b = 0; b < 16; ++b) mb.Intra4x4PredMode[b] = (c.ipred[b >> 1] >> ((b & 1) * 4)) & 15;
+        for (int b = 0; b < 4; ++b) mb.Intra8x8PredMode[b] = (c.ipred[b >> 1] >> ((b & 1) * 4)) & 15;
+        mb.Intra16x16PredMode = c.i16_mode;
+        mb.intra_chroma_pred_mode = c.chroma_mode;
+        mb.CodedBlockPatternLuma = c.cbp & 15;
+        mb.CodedBlockPatternChroma = c.cbp >> 4;
+        mb.QpY = c.qp_y; mb.QpC[0] = c.qp_c[0]; mb.QpC[1] = c.qp_c[1];
+        mb.qp_scaled[0] = c.qp_scaled[0]; mb.qp_scaled[1] = c.qp_scaled[1]; mb.qp_scaled[2] = c.qp_scaled[2];
+        mb.TransformBypassModeFlag = 0;
+        memset(mb.cbp_blks, 0, sizeof(mb.cbp_blks));
+        /* partition shape for the reference's own partition walk (decoder.cc:217-254) */
+        if (!mb.is_intra_block) {
+            for (int b8 = 0; b8 < 4; ++b8) {
+                int bx = (b8 & 1) * 2 + mb.mb.x * 4, by = (b8 >> 1) * 2 + mb.mb.y * 4;
+                const pic_motion_params& t = dec->mv_info[by][bx];
+                mb.SubMbPredMode[b8] = (t.ref_idx[0] >= 0 && t.ref_idx[1] >= 0) ? 2 : (t.ref_idx[0] >= 0 ? 0 : 1);
+                if (c.mb_type >= 1 && c.mb_type <= 3) mb.SubMbType[b8] = c.mb_type;
+                else if (c.mb_type == 4) {
+                    auto same = [&](int dx0, int dy0, int dx1, int dy1) {
+                        const pic_motion_params& u = dec->mv_info[by + dy0][bx + dx0];
+                        const pic_motion_params& v = dec->mv_info[by + dy1][bx + dx1];
+                        return u.ref_idx[0] == v.ref_idx[0] && u.ref_idx[1] == v.ref_idx[1] &&
+                               u.mv[0] == v.mv[0] && u.mv[1] == v.mv[1];
+                    };
+                    bool rows = same(0, 0, 1, 0) && same(0, 1, 1, 1);   /* each row uniform -> 8x4 */
+                    bool cols = same(0, 0, 0, 1) && same(1, 0, 1, 1);   /* each col uniform -> 4x8 */
+                    mb.SubMbType[b8] = (rows && cols) ? 4 : rows ? 5 : cols ? 6 : 7;
+                } else mb.SubMbType[b8] = 0;
+            }
+        }
+
+        /* coefficient push, slice_data.cc:496-503 reset protocol then the parser's calls */
+        Transform* tr = s.decoder.transform;
+        memset(tr->cof, 0, sizeof(tr->cof));
+        const int16_t* lv = levels.data() + c.coef_off;
+        if (c.mb_type == H264R_I_PCM) {
+            const uint8_t* raw = (const uint8_t*)lv;
+            for (int y = 0; y < 16; ++y) for (int x = 0; x < 16; ++x) tr->cof[0][y][x] = raw[y * 16 + x];
+            for (int q = 0; q < 2; ++q)
+                for (int y = 0; y < 8; ++y) for (int x = 0; x < 8; ++x) tr->cof[1 + q][y][x] = raw[256 + q * 64 + y * 8 + x];
+            mb.cbp_blks[0] = 0xFFFF;
+        } else {
+            int cbpl = c.cbp & 15, cbpc = c.cbp >> 4;
+            const int16_t* p = lv;
+            const int16_t* b8p[4] = {nullptr, nullptr, nullptr, nullptr};
+            for (int q = 0; q < 4; ++q) if (cbpl & (1 << q)) { b8p[q] = p; p += 64; }
+            const int16_t* cac = nullptr; if (cbpc == 2) { cac = p; p += 128; }
+            const int16_t* ldc = nullptr; if (c.mb_type == H264R_I_16x16) { ldc = p; p += 16; }
+            const int16_t* cdc = nullptr; if (cbpc) { cdc = p; p += 8; }
+            if (ldc) {
+                for (int pos = 0; pos < 16; ++pos)
+                    if (ldc[pos]) s.decoder.coeff_luma_dc(&mb, PLANE_Y, 0, 0, inv4[pos], ldc[pos]);
+                s.decoder.transform_luma_dc(&mb, PLANE_Y);
+            }
+            for (int q = 0; q < 4; ++q) {
+                if (!b8p[q]) continue;
+                if (!mb.transform_size_8x8_flag) {
+                    for (int b4 = 0; b4 < 4; ++b4) {
+                        int x0 = (q & 1) * 2 + (b4 & 1), y0 = (q >> 1) * 2 + (b4 >> 1);
+                        for (int pos = 0; pos < 16; ++pos) {
+                            int v = b8p[q][b4 * 16 + pos];
+                            if (v) s.decoder.coeff_luma_ac(&mb, PLANE_Y, x0, y0, inv4[pos], v);
+                        }
+                    }
+                } else {
+                    int x0 = (q & 1) * 2, y0 = (q >> 1) * 2;
+                    for (int pos = 0; pos < 64; ++pos) {
+                        int v = b8p[q][pos];
+                        if (v) s.decoder.coeff_luma_ac(&mb, PLANE_Y, x0, y0, inv8[pos], v);
+                    }
+                }
+            }
+            if (cbpc) {
+                for (int pl = 1; pl <= 2; ++pl) {
+                    for (int q = 0; q < 4; ++q)
+                        if (cdc[(pl - 1) * 4 + q]) s.decoder.coeff_chroma_dc(&mb, (ColorPlane)pl, 0, 0, q, cdc[(pl - 1) * 4 + q]);
+                    s.decoder.transform_chroma_dc(&mb, (ColorPlane)pl);
+                }
+            }
+            if (cac) {
+                for (int pl = 1; pl <= 2; ++pl)
+                    for (int b = 0; b < 4; ++b)
+                        for (int pos = 1; pos < 16; ++pos) {
+                            int v = cac[(pl - 1) * 64 + b * 16 + pos];
+                            if (v) s.decoder.coeff_chroma_ac(&mb, (ColorPlane)pl, b % 2, b / 2, inv4[pos], v);
+                        }
+            }
+        }
+        if ((uint16_t)mb.cbp_blks[0] != c.cbp_blks) {
+            fprintf(stderr, "cbp_blks mismatch at MB %d: reference %04x synth %04x\n", a, (unsigned)mb.cbp_blks[0], c.cbp_blks);
+            return 4;
+        }
+        static const char* dump = getenv("H264R_DUMP_MB");
+        if (dump && atoi(dump) == a) {
+            int x0 = mb.mb.x * 16 - 1, y0 = mb.mb.y * 16;
+            fprintf(stderr, "left column x=%d:", x0);
+            for (int y = 0; y < 16 && x0 >= 0; ++y) fprintf(stderr, " %d", dec->imgY[y0 + y][x0]);
+            fprintf(stderr, "\ncof (dequantised) plane 0:\n");
+            for (int y = 0; y < 16; ++y) { for (int x = 0; x < 16; ++x) fprintf(stderr, "%6d", tr->cof[0][y][x]); fprintf(stderr, "\n"); }
+        }
+        s.decoder.decode(mb);
+        if (dump && atoi(dump) == a) {
+            fprintf(stderr, "mb_pred plane 0:\n");
+            for (int y = 0; y < 16; ++y) { for (int x = 0; x < 16; ++x) fprintf(stderr, "%4d", s.mb_pred[0][y][x]); fprintf(stderr, "\n"); }
+        }
+    }
+    if (!recon_only) sl[0]->decoder.deblock_filter(*sl[0]);
+
+    FILE* f = fopen(out_path, "wb");
+    if (!f) return 5;
+    std::vector<uint8_t> row(W * 16);
+    for (int y = 0; y < H * 16; ++y) {
+        for (int x = 0; x < W * 16; ++x) {
+            if (dec->imgY[y][x] > 255) { fprintf(stderr, "sample > 255 at Y(%d,%d)\n", x, y); return 6; }
+            row[x] = (uint8_t)dec->imgY[y][x];
+        }
+        fwrite(row.data(), 1, W * 16, f);
+    }
+    for (int q = 0; q < 2; ++q)
+        for (int y = 0; y < H * 8; ++y) {
+            for (int x = 0; x < W * 8; ++x) {
+                if (dec->imgUV[q][y][x] > 255) { fprintf(stderr, "sample > 255 at C%d(%d,%d)\n", q, x, y); return 6; }
+                row[x] = (uint8_t)dec->imgUV[q][y][x];
+            }
+            fwrite(row.data(), 1, W * 8, f);
+        }
+    fclose(f);
+    return 0;
+}

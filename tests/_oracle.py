@@ -1,0 +1,129 @@
+"""Test-side access to the CPU oracle (oracle/liboracle.so) and, in this
+container only, to the compiled reference driver (oracle/_ref/ref_driver).
+
+TEST INFRASTRUCTURE: only tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg import this module.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "arrow-h264_amd")
+if PKG not in sys.path:
+    sys.path.insert(0, PKG)
+
+from h264r import _abi as A  # noqa: E402
+from h264r import synth  # noqa: E402
+
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+ORACLE_LIB = os.path.join(ORACLE_DIR, "liboracle.so")
+REF_DRIVER = os.path.join(ORACLE_DIR, "_ref", "ref_driver")
+REFERENCE = "/root/reference"
+
+_lib = None
+
+
+def build_oracle() -> None:
+    subprocess.run(["make", "-s", "-C", ORACLE_DIR, "all"], check=True)
+
+
+def reference_available() -> bool:
+    return os.path.isdir(os.path.join(REFERENCE, "src", "codec", "h264"))
+
+
+def build_ref() -> str:
+    subprocess.run(["make", "-s", "-j8", "-C", ORACLE_DIR, "ref"], check=True)
+    return REF_DRIVER
+
+
+class OraclePicture(C.Structure):
+    _fields_ = [
+        ("width_mbs", C.c_int), ("height_mbs", C.c_int),
+        ("mbs", C.c_void_p), ("levels", C.c_void_p), ("mv", C.c_void_p),
+        ("ref_idx", C.c_void_p), ("slices", C.c_void_p), ("pic", C.c_void_p),
+        ("quant", C.c_void_p), ("ref_planes", (C.c_void_p * 3) * A.MAX_SLOTS),
+        ("out", C.c_void_p * 3),
+    ]
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        build_oracle()
+        L = C.CDLL(ORACLE_LIB)
+        A.bind_synth(L)
+        L.oracle_quant_init_flat.argtypes = [C.c_void_p]
+        L.oracle_quant_init_flat.restype = None
+        for f in ("oracle_decode_picture", "oracle_reconstruct_picture", "oracle_deblock_picture"):
+            getattr(L, f).argtypes = [C.POINTER(OraclePicture)]
+            getattr(L, f).restype = C.c_int
+        L.oracle_decode_pictures.argtypes = [C.POINTER(OraclePicture), C.c_int, C.c_int]
+        L.oracle_decode_pictures.restype = C.c_int
+        _lib = L
+    return _lib
+
+
+def quant_flat() -> np.ndarray:
+    q = np.zeros(1, A.QUANT_DTYPE)
+    lib().oracle_quant_init_flat(A.ptr(q))
+    return q
+
+
+def make_oracle_picture(p: synth.Picture, refs, quant: np.ndarray, out) -> OraclePicture:
+    o = OraclePicture()
+    o.width_mbs, o.height_mbs = p.cfg.width_mbs, p.cfg.height_mbs
+    o.mbs, o.levels, o.mv = A.ptr(p.mbs).value, A.ptr(p.levels).value, A.ptr(p.mv).value
+    o.ref_idx, o.slices, o.pic = A.ptr(p.ref_idx).value, A.ptr(p.slices).value, A.ptr(p.pic).value
+    o.quant = A.ptr(quant).value
+    for s, planes in enumerate(refs):
+        for k in range(3):
+            o.ref_planes[s][k] = A.ptr(planes[k]).value
+    for k in range(3):
+        o.out[k] = A.ptr(out[k]).value
+    return o
+
+
+def new_planes(W: int, H: int):
+    return (np.zeros((16 * H, 16 * W), np.uint8), np.zeros((8 * H, 8 * W), np.uint8),
+            np.zeros((8 * H, 8 * W), np.uint8))
+
+
+def decode(p: synth.Picture, refs=None, stage: str = "full"):
+    """Oracle output planes (Y, Cb, Cr) for one synthetic picture."""
+    L = lib()
+    if refs is None:
+        refs = synth.refpics(L, p.cfg)
+    q = quant_flat()
+    out = new_planes(p.cfg.width_mbs, p.cfg.height_mbs)
+    o = make_oracle_picture(p, refs, q, out)
+    fn = {"full": L.oracle_decode_picture, "recon": L.oracle_reconstruct_picture}[stage]
+    st = fn(C.byref(o))
+    if st != 0:
+        raise RuntimeError(f"oracle -> {st}")
+    return out
+
+
+def run_reference(cfg: A.SynthCfg, index: int, recon_only: bool = False):
+    """Planes produced by the compiled reference decoder (this container only)."""
+    drv = build_ref()
+    W, H = cfg.width_mbs, cfg.height_mbs
+    with tempfile.TemporaryDirectory() as td:
+        out = os.path.join(td, "o.yuv")
+        args = [drv, W, H, cfg.kind, cfg.num_slices, cfg.deblock_idc, cfg.filter_offset_a,
+                cfg.filter_offset_b, cfg.transform8x8, cfg.wp_mode, cfg.constrained_intra,
+                cfg.num_refs, cfg.qp_min, cfg.qp_max, cfg.pcm_permille, cfg.intra_permille,
+                cfg.mv_range_x, cfg.mv_range_y, hex(cfg.seed), index, out, int(recon_only)]
+        r = subprocess.run([str(a) for a in args], capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"ref_driver failed ({r.returncode}): {r.stderr[-2000:]}")
+        raw = np.fromfile(out, np.uint8)
+    ny, nc = 256 * W * H, 64 * W * H
+    return (raw[:ny].reshape(16 * H, 16 * W), raw[ny:ny + nc].reshape(8 * H, 8 * W),
+            raw[ny + nc:].reshape(8 * H, 8 * W))

@@ -1,0 +1,106 @@
+#!/usr/bin/env python3
+"""Generate tests/golden/golden.json from the compiled REFERENCE decoder.
+
+Run in the container that holds /root/reference (the GPU box never does):
+
+    python tests/golden/make_golden.py
+
+For every case below, the seeded synthetic picture (arrow-h264_amd/csrc/synth.c)
+is decoded by the unmodified reference (oracle/_ref/ref_driver, built from
+/root/reference by oracle/Makefile: Decoder::coeff_* pushes, Decoder::decode per
+MB in raster order, Decoder::deblock_filter).  The fixture keeps:
+  - the synth configuration and picture index (inputs are regenerated),
+  - an MD5 of every generated input array (detects generator drift),
+  - per-plane MD5 of the reconstruction before deblocking and of the final output
+    (the reference's own compare protocol is per-frame MD5 of the YUV,
+     R/script/test/model/__init__.py:119-183).
+The script also checks the oracle restatement against the reference bytes and
+refuses to write fixtures if they differ.
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+
+import numpy as np  # noqa: E402
+
+import _oracle as O  # noqa: E402
+from h264r import synth  # noqa: E402
+
+# name, SURVEY config index, W, H, overrides, picture indices
+CASES = [
+    ("intra_qcif", 2, 11, 9, dict(pcm_permille=20), [0, 1, 2]),
+    ("intra_qcif_4x4only", 2, 11, 9, dict(transform8x8=0), [0]),
+    ("intra_cif_3slices_idc2", 2, 22, 18, dict(num_slices=3, deblock_idc=2, pcm_permille=10), [0]),
+    ("intra_cif_3slices_idc0", 2, 22, 18, dict(num_slices=3, deblock_idc=0), [0]),
+    ("intra_qcif_offsets", 2, 11, 9, dict(filter_offset_a=12, filter_offset_b=-12), [0]),
+    ("intra_qcif_lowqp", 2, 11, 9, dict(qp_min=0, qp_max=15), [0]),
+    ("intra_qcif_highqp", 2, 11, 9, dict(qp_min=40, qp_max=51), [0]),
+    ("p_qcif", 3, 11, 9, {}, [0, 1, 2]),
+    ("p_qcif_wp", 3, 11, 9, dict(wp_mode=1), [0, 1]),
+    ("p_qcif_cip", 3, 11, 9, dict(constrained_intra=1, intra_permille=400), [0, 1]),
+    ("p_qcif_idc1", 3, 11, 9, dict(deblock_idc=1), [0]),
+    ("p_qcif_3slices_idc2", 3, 11, 9, dict(num_slices=3, deblock_idc=2), [0]),
+    ("p_qcif_3slices_idc0", 3, 11, 9, dict(num_slices=3, deblock_idc=0), [0]),
+    ("p_qcif_bigmv", 3, 11, 9, dict(mv_range_x=300, mv_range_y=200), [0, 1]),
+    ("p_qcif_4refs_t8", 3, 11, 9, dict(num_refs=4, transform8x8=1), [0]),
+    ("p_qcif_offsets", 3, 11, 9, dict(filter_offset_a=-6, filter_offset_b=8), [0]),
+    ("p_qcif_pcm_highqp", 3, 11, 9, dict(pcm_permille=100, intra_permille=300, qp_min=36, qp_max=51), [0]),
+    ("b_qcif_implicit", 4, 11, 9, dict(num_slices=1, deblock_idc=0), [0, 1]),
+    ("b_qcif_default", 4, 11, 9, dict(wp_mode=0), [0]),
+    ("b_qcif_explicit", 4, 11, 9, dict(wp_mode=1), [0, 1]),
+    ("b_qcif_4refs", 4, 11, 9, dict(num_refs=4), [0]),
+    ("b_qcif_bigmv_cip", 4, 11, 9, dict(mv_range_x=250, mv_range_y=150, constrained_intra=1), [0]),
+    ("b_cif_4slices", 4, 22, 18, {}, [0]),
+    ("p_1080p_strip", 3, 120, 4, {}, [0]),
+    ("intra_1080p", 2, 120, 68, {}, [0]),
+    ("p_1080p", 3, 120, 68, {}, [0]),
+    ("b_1080p_4slices", 4, 120, 68, {}, [0]),
+]
+
+
+def md5(a: np.ndarray) -> str:
+    return hashlib.md5(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def main() -> int:
+    if not O.reference_available():
+        print("reference not available: fixtures cannot be regenerated here", file=sys.stderr)
+        return 2
+    L = O.lib()
+    fixtures = []
+    for name, cidx, W, H, over, indices in CASES:
+        cfg = synth.default_cfg(L, cidx, W, H, **over)
+        for idx in indices:
+            t0 = time.time()
+            p = synth.picture(L, cfg, idx)
+            entry = {"name": name, "config": cidx, "cfg": cfg.as_dict(), "index": idx,
+                     "input_md5": synth.input_digest(p)}
+            for stage, recon_only in (("recon", True), ("out", False)):
+                ref = O.run_reference(cfg, idx, recon_only=recon_only)
+                ora = O.decode(p, stage="recon" if recon_only else "full")
+                for k, pl in enumerate("YUV"):
+                    if not np.array_equal(ref[k], ora[k]):
+                        bad = np.argwhere(ref[k] != ora[k])
+                        print(f"MISMATCH {name}[{idx}] {stage} plane {pl}: {len(bad)} samples, "
+                              f"first at (y,x)={tuple(bad[0])}", file=sys.stderr)
+                        return 1
+                entry[f"{stage}_md5"] = {pl: md5(ref[k]) for k, pl in enumerate("YUV")}
+            fixtures.append(entry)
+            print(f"{name}[{idx}] {W}x{H} ok ({time.time() - t0:.2f}s)")
+    with open(os.path.join(HERE, "golden.json"), "w") as f:
+        json.dump({"generator": "tests/golden/make_golden.py",
+                   "reference": "luuvish/arrow-h264 decoder/*.cc compiled by oracle/Makefile",
+                   "fixtures": fixtures}, f, indent=1)
+    print(f"wrote {len(fixtures)} fixtures")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
