@@ -1,0 +1,398 @@
+// h264r_host.hip -- the C ABI of include/h264r.h on top of the gfx950 kernels.
+//
+// Host-side replacement of vio::h264::Decoder (decoder.h:301-338):
+//   picture_begin / mb_submit / picture_end   ~ Decoder::init, decode(mb), deblock_filter
+//   decode_batch                              ~ decode + deblock_filter of many pictures at once
+// The reconstruction itself never runs on the CPU: every entry point that
+// produces samples launches k_inter / k_intra / k_deblock and fails with
+// H264R_ENODEVICE when no gfx950 device is present.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "h264r.h"
+
+extern "C" __global__ void k_inter(h264r_batch b);
+extern "C" __global__ void k_intra(h264r_batch b, int step);
+extern "C" __global__ void k_deblock(h264r_batch b, int step);
+
+namespace {
+
+#define HIP_OK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
+        fprintf(stderr, "h264r: %s failed: %s\n", #x, hipGetErrorString(e_)); return H264R_EDEVICE; } } while (0)
+
+const int dequant_coef[6][3] = {{10, 13, 16}, {11, 14, 18}, {13, 16, 20}, {14, 18, 23}, {16, 20, 25}, {18, 23, 29}};
+const int dq8_v[6][6] = {{20, 18, 32, 19, 25, 24}, {22, 19, 35, 21, 28, 26}, {26, 23, 42, 24, 33, 31},
+                         {28, 25, 45, 26, 35, 33}, {32, 28, 51, 30, 40, 38}, {36, 32, 58, 34, 46, 43}};
+
+// normative LevelScale(m, i, j) (transform.cc:93-170 tables dequant_coef / dequant_coef8)
+int norm4(int m, int i, int j)
+{
+    if ((i & 1) == 0 && (j & 1) == 0) return dequant_coef[m][0];
+    if ((i & 1) && (j & 1)) return dequant_coef[m][2];
+    return dequant_coef[m][1];
+}
+int norm8(int m, int i, int j)
+{
+    if (i % 4 == 0 && j % 4 == 0) return dq8_v[m][0];
+    if (i % 2 == 1 && j % 2 == 1) return dq8_v[m][1];
+    if (i % 4 == 2 && j % 4 == 2) return dq8_v[m][2];
+    if ((i % 4 == 0 && j % 2 == 1) || (i % 2 == 1 && j % 4 == 0)) return dq8_v[m][3];
+    if ((i % 4 == 0 && j % 4 == 2) || (i % 4 == 2 && j % 4 == 0)) return dq8_v[m][4];
+    return dq8_v[m][5];
+}
+
+int grid_diag(int step, int W, int H)
+{
+    int ymin = step - (W - 1) > 0 ? (step - (W - 1) + 1) / 2 : 0;
+    int ymax = std::min(step / 2, H - 1);
+    return ymax >= ymin ? ymax - ymin + 1 : 0;
+}
+
+template <typename T>
+int dev_resize(T** p, size_t* cap, size_t n)
+{
+    if (n <= *cap && *p) return H264R_OK;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr; *cap = 0;
+    if (hipMalloc(reinterpret_cast<void**>(p), std::max<size_t>(n, 1) * sizeof(T)) != hipSuccess) return H264R_ENOMEM;
+    *cap = n;
+    return H264R_OK;
+}
+
+}  // namespace
+
+struct h264r_ctx {
+    int device = 0;
+    int max_w = 0, max_h = 0;
+    hipStream_t stream = nullptr;
+    // DPB slots
+    uint8_t* slot[H264R_MAX_SLOTS][3] = {};
+    int slot_w[H264R_MAX_SLOTS] = {}, slot_h[H264R_MAX_SLOTS] = {};
+    const uint8_t** d_ref_planes = nullptr;
+    // streaming-API staging
+    bool in_pic = false;
+    int pw = 0, ph = 0;
+    std::vector<h264r_mb> h_mbs;
+    std::vector<int16_t> h_levels;
+    std::vector<uint32_t> h_mv;
+    std::vector<int8_t> h_ref;
+    std::vector<h264r_slice> h_slices;
+    h264r_pic h_pic{};
+    h264r_quant h_quant{};
+    std::vector<uint8_t> seen;
+    // device buffers of the streaming API
+    h264r_mb* d_mbs = nullptr; size_t c_mbs = 0;
+    int16_t* d_levels = nullptr; size_t c_levels = 0;
+    uint32_t* d_mv = nullptr; size_t c_mv = 0;
+    int8_t* d_ref = nullptr; size_t c_ref = 0;
+    h264r_slice* d_slices = nullptr; size_t c_slices = 0;
+    h264r_pic* d_pic = nullptr; size_t c_pic = 0;
+    h264r_quant* d_quant = nullptr; size_t c_quant = 0;
+    uint8_t* d_out = nullptr; size_t c_out = 0;
+    // timing
+    bool timing = false;
+    int debug = 0;
+    hipEvent_t ev[4] = {};
+    float last_ms[4] = {0, 0, 0, 0};
+};
+
+extern "C" {
+
+int h264r_abi_version(void) { return H264R_ABI_VERSION; }
+
+const char* h264r_strerror(int s)
+{
+    switch (s) {
+    case H264R_OK: return "ok";
+    case H264R_EINVAL: return "invalid argument";
+    case H264R_ENOMEM: return "out of memory";
+    case H264R_EDEVICE: return "HIP runtime error";
+    case H264R_ESTATE: return "call out of order";
+    case H264R_EUNSUPPORTED: return "unsupported configuration";
+    case H264R_ENODEVICE: return "no gfx950 device";
+    default: return "unknown status";
+    }
+}
+
+int h264r_device_count(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    int ok = 0;
+    for (int d = 0; d < n; ++d) {
+        hipDeviceProp_t p;
+        if (hipGetDeviceProperties(&p, d) == hipSuccess && strncmp(p.gcnArchName, "gfx950", 6) == 0) ++ok;
+    }
+    return ok;
+}
+
+int h264r_quant_init_flat(h264r_quant* q)
+{
+    if (!q) return H264R_EINVAL;
+    for (int t = 0; t < 2; ++t)
+        for (int pl = 0; pl < 3; ++pl)
+            for (int m = 0; m < 6; ++m) {
+                for (int k = 0; k < 16; ++k) q->scale4x4[t][pl][m][k] = (int16_t)(norm4(m, k / 4, k % 4) * 16);
+                for (int k = 0; k < 64; ++k) q->scale8x8[t][pl][m][k] = (int16_t)(norm8(m, k / 8, k % 8) * 16);
+            }
+    return H264R_OK;
+}
+
+int h264r_quant_init_lists(h264r_quant* q, const int32_t* const qm[12])
+{
+    // Transform::set_quant (transform.cc:259-302): InvLevelScale = dequant_coef x qmatrix.
+    if (!q || !qm) return H264R_EINVAL;
+    for (int i = 0; i < 12; ++i) if (!qm[i]) return H264R_EINVAL;
+    for (int pl = 0; pl < 3; ++pl)
+        for (int m = 0; m < 6; ++m) {
+            for (int k = 0; k < 16; ++k) {
+                q->scale4x4[0][pl][m][k] = (int16_t)(norm4(m, k / 4, k % 4) * qm[pl][k]);
+                q->scale4x4[1][pl][m][k] = (int16_t)(norm4(m, k / 4, k % 4) * qm[3 + pl][k]);
+            }
+            for (int k = 0; k < 64; ++k) {
+                // 8x8 lists: 6 Intra Y, 7 Inter Y, 8 Intra Cb, 9 Inter Cb, 10 Intra Cr, 11 Inter Cr
+                q->scale8x8[0][pl][m][k] = (int16_t)(norm8(m, k / 8, k % 8) * qm[6 + 2 * pl][k]);
+                q->scale8x8[1][pl][m][k] = (int16_t)(norm8(m, k / 8, k % 8) * qm[7 + 2 * pl][k]);
+            }
+        }
+    return H264R_OK;
+}
+
+int h264r_create(h264r_ctx** out, int device, int max_w, int max_h, int chroma_format_idc, int bit_depth)
+{
+    if (!out || max_w <= 0 || max_h <= 0 || max_w > 1024 || max_h > 1024) return H264R_EINVAL;
+    *out = nullptr;
+    if (chroma_format_idc != 1 || bit_depth != 8) return H264R_EUNSUPPORTED;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0 || device < 0 || device >= n) return H264R_ENODEVICE;
+    hipDeviceProp_t p;
+    if (hipGetDeviceProperties(&p, device) != hipSuccess || strncmp(p.gcnArchName, "gfx950", 6) != 0)
+        return H264R_ENODEVICE;
+    h264r_ctx* c = new (std::nothrow) h264r_ctx();
+    if (!c) return H264R_ENOMEM;
+    c->device = device; c->max_w = max_w; c->max_h = max_h;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&c->d_ref_planes), sizeof(uint8_t*) * 3 * H264R_MAX_SLOTS) != hipSuccess) {
+        delete c;
+        return H264R_EDEVICE;
+    }
+    for (int i = 0; i < 4; ++i) (void)hipEventCreate(&c->ev[i]);
+    (void)hipMemset(c->d_ref_planes, 0, sizeof(uint8_t*) * 3 * H264R_MAX_SLOTS);
+    *out = c;
+    return H264R_OK;
+}
+
+int h264r_destroy(h264r_ctx* c)
+{
+    if (!c) return H264R_EINVAL;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (int s = 0; s < H264R_MAX_SLOTS; ++s) if (c->slot[s][0]) (void)hipFree(c->slot[s][0]);
+    void* bufs[] = {c->d_ref_planes, c->d_mbs, c->d_levels, c->d_mv, c->d_ref, c->d_slices, c->d_pic, c->d_quant, c->d_out};
+    for (void* b : bufs) if (b) (void)hipFree(b);
+    for (int i = 0; i < 4; ++i) if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+    return H264R_OK;
+}
+
+static int ensure_slot(h264r_ctx* c, int slot, int w, int h)
+{
+    if (c->slot[slot][0] && c->slot_w[slot] == w && c->slot_h[slot] == h) return H264R_OK;
+    if (c->slot[slot][0]) { (void)hipFree(c->slot[slot][0]); c->slot[slot][0] = nullptr; }
+    size_t ys = (size_t)w * 16 * h * 16, cs = (size_t)w * 8 * h * 8;
+    uint8_t* base = nullptr;
+    if (hipMalloc(reinterpret_cast<void**>(&base), ys + 2 * cs) != hipSuccess) return H264R_ENOMEM;
+    c->slot[slot][0] = base; c->slot[slot][1] = base + ys; c->slot[slot][2] = base + ys + cs;
+    c->slot_w[slot] = w; c->slot_h[slot] = h;
+    HIP_OK(hipMemcpy(c->d_ref_planes + 3 * slot, c->slot[slot], 3 * sizeof(uint8_t*), hipMemcpyHostToDevice));
+    return H264R_OK;
+}
+
+int h264r_set_ref(h264r_ctx* c, int slot, const uint8_t* y, const uint8_t* u, const uint8_t* v, int w, int h)
+{
+    if (!c || slot < 0 || slot >= H264R_MAX_SLOTS || !y || !u || !v || w <= 0 || h <= 0 || w > c->max_w || h > c->max_h)
+        return H264R_EINVAL;
+    (void)hipSetDevice(c->device);
+    int st = ensure_slot(c, slot, w, h);
+    if (st) return st;
+    size_t ys = (size_t)w * 16 * h * 16, cs = (size_t)w * 8 * h * 8;
+    HIP_OK(hipMemcpyAsync(c->slot[slot][0], y, ys, hipMemcpyHostToDevice, c->stream));
+    HIP_OK(hipMemcpyAsync(c->slot[slot][1], u, cs, hipMemcpyHostToDevice, c->stream));
+    HIP_OK(hipMemcpyAsync(c->slot[slot][2], v, cs, hipMemcpyHostToDevice, c->stream));
+    HIP_OK(hipStreamSynchronize(c->stream));
+    return H264R_OK;
+}
+
+int h264r_ref_planes(h264r_ctx* c, int slot, uint8_t** y, uint8_t** u, uint8_t** v)
+{
+    if (!c || slot < 0 || slot >= H264R_MAX_SLOTS) return H264R_EINVAL;
+    if (y) *y = c->slot[slot][0];
+    if (u) *u = c->slot[slot][1];
+    if (v) *v = c->slot[slot][2];
+    return c->slot[slot][0] ? H264R_OK : H264R_ESTATE;
+}
+
+static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s)
+{
+    const int W = b.width_mbs, H = b.height_mbs, nsteps = (W - 1) + 2 * (H - 1) + 1;
+    if (c->timing) HIP_OK(hipEventRecord(c->ev[0], s));
+    hipLaunchKernelGGL(k_inter, dim3(W * H, b.num_pics), dim3(64), 0, s, b);
+    HIP_OK(hipGetLastError());
+    if (c->timing) HIP_OK(hipEventRecord(c->ev[1], s));
+    for (int t = 0; t < nsteps; ++t) {
+        int n = grid_diag(t, W, H);
+        if (n) hipLaunchKernelGGL(k_intra, dim3(n, b.num_pics), dim3(64), 0, s, b, t);
+    }
+    HIP_OK(hipGetLastError());
+    if (c->timing) HIP_OK(hipEventRecord(c->ev[2], s));
+    for (int t = 0; t < nsteps && !(c->debug & H264R_DBG_NO_DEBLOCK); ++t) {
+        int n = grid_diag(t, W, H);
+        if (n) hipLaunchKernelGGL(k_deblock, dim3(n, b.num_pics), dim3(64), 0, s, b, t);
+    }
+    HIP_OK(hipGetLastError());
+    if (c->timing) HIP_OK(hipEventRecord(c->ev[3], s));
+    return H264R_OK;
+}
+
+int h264r_decode_batch(h264r_ctx* c, const h264r_batch* b, void* stream)
+{
+    if (!c || !b || b->num_pics <= 0 || b->width_mbs <= 0 || b->height_mbs <= 0 ||
+        b->width_mbs > c->max_w || b->height_mbs > c->max_h || b->slice_stride <= 0 || !b->mbs || !b->levels ||
+        !b->mv || !b->ref_idx || !b->slices || !b->pics || !b->quant || !b->out_y || !b->out_u || !b->out_v)
+        return H264R_EINVAL;
+    (void)hipSetDevice(c->device);
+    h264r_batch bb = *b;
+    if (!bb.ref_planes) bb.ref_planes = c->d_ref_planes;
+    hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : c->stream;
+    return launch_all(c, bb, s);
+}
+
+int h264r_set_timing(h264r_ctx* c, int enable)
+{
+    if (!c) return H264R_EINVAL;
+    c->timing = enable != 0;
+    return H264R_OK;
+}
+
+int h264r_set_debug(h264r_ctx* c, int flags)
+{
+    if (!c) return H264R_EINVAL;
+    c->debug = flags;
+    return H264R_OK;
+}
+
+int h264r_last_timing(h264r_ctx* c, float out[4])
+{
+    if (!c || !out) return H264R_EINVAL;
+    if (!c->timing) return H264R_ESTATE;
+    HIP_OK(hipEventSynchronize(c->ev[3]));
+    HIP_OK(hipEventElapsedTime(&out[0], c->ev[0], c->ev[1]));
+    HIP_OK(hipEventElapsedTime(&out[1], c->ev[1], c->ev[2]));
+    HIP_OK(hipEventElapsedTime(&out[2], c->ev[2], c->ev[3]));
+    HIP_OK(hipEventElapsedTime(&out[3], c->ev[0], c->ev[3]));
+    return H264R_OK;
+}
+
+// ------------------------------------------------------------- streaming API
+int h264r_picture_begin(h264r_ctx* c, int w, int h, const h264r_pic* pic, const h264r_slice* slices,
+                        const h264r_quant* quant)
+{
+    if (!c || !pic || !slices || !quant || w <= 0 || h <= 0 || w > c->max_w || h > c->max_h ||
+        pic->num_slices <= 0 || pic->num_slices > H264R_MAX_SLICES)
+        return H264R_EINVAL;
+    c->pw = w; c->ph = h;
+    const size_t n = (size_t)w * h;
+    c->h_mbs.assign(n, h264r_mb{});
+    c->h_levels.clear();
+    c->h_mv.assign(2 * 16 * n, 0);
+    c->h_ref.assign(2 * 16 * n, -1);
+    c->h_slices.assign(slices, slices + pic->num_slices);
+    c->h_pic = *pic;
+    c->h_quant = *quant;
+    c->seen.assign(n, 0);
+    c->in_pic = true;
+    return H264R_OK;
+}
+
+int h264r_mb_submit(h264r_ctx* c, int addr, const h264r_mb* mb, const int16_t* levels, int n_levels,
+                    const uint32_t* mv, const int8_t* ref_idx)
+{
+    if (!c) return H264R_EINVAL;
+    if (!c->in_pic) return H264R_ESTATE;
+    const int n = c->pw * c->ph;
+    if (addr < 0 || addr >= n || !mb || n_levels < 0 || (n_levels && !levels) || !mv || !ref_idx) return H264R_EINVAL;
+    if (mb->flags & H264R_MBF_BYPASS) return H264R_EUNSUPPORTED;
+    if (mb->slice >= c->h_pic.num_slices) return H264R_EINVAL;
+    h264r_mb m = *mb;
+    // append the level block, 16-byte aligned
+    while (c->h_levels.size() % 8) c->h_levels.push_back(0);
+    m.coef_off = (uint32_t)c->h_levels.size();
+    c->h_levels.insert(c->h_levels.end(), levels, levels + n_levels);
+    c->h_mbs[addr] = m;
+    const int W4 = c->pw * 4, plane = W4 * c->ph * 4, x = addr % c->pw, y = addr / c->pw;
+    for (int l = 0; l < 2; ++l)
+        for (int k = 0; k < 16; ++k) {
+            int idx = (y * 4 + k / 4) * W4 + x * 4 + k % 4;
+            c->h_mv[(size_t)l * plane + idx] = mv[l * 16 + k];
+            c->h_ref[(size_t)l * plane + idx] = ref_idx[l * 16 + k];
+        }
+    c->seen[addr] = 1;
+    return H264R_OK;
+}
+
+int h264r_picture_end(h264r_ctx* c, uint8_t* y, uint8_t* u, uint8_t* v, int keep_slot)
+{
+    if (!c) return H264R_EINVAL;
+    if (!c->in_pic) return H264R_ESTATE;
+    c->in_pic = false;
+    for (uint8_t s : c->seen) if (!s) return H264R_ESTATE;      // every MB must be submitted
+    if (keep_slot >= H264R_MAX_SLOTS) return H264R_EINVAL;
+    (void)hipSetDevice(c->device);
+    const size_t n = (size_t)c->pw * c->ph, ys = n * 256, cs = n * 64;
+    if (c->h_levels.empty()) c->h_levels.push_back(0);
+    int st = 0;
+    if ((st = dev_resize(&c->d_mbs, &c->c_mbs, n)) || (st = dev_resize(&c->d_levels, &c->c_levels, c->h_levels.size())) ||
+        (st = dev_resize(&c->d_mv, &c->c_mv, c->h_mv.size())) || (st = dev_resize(&c->d_ref, &c->c_ref, c->h_ref.size())) ||
+        (st = dev_resize(&c->d_slices, &c->c_slices, c->h_slices.size())) || (st = dev_resize(&c->d_pic, &c->c_pic, 1)) ||
+        (st = dev_resize(&c->d_quant, &c->c_quant, 1)) || (st = dev_resize(&c->d_out, &c->c_out, ys + 2 * cs)))
+        return st;
+    hipStream_t s = c->stream;
+    HIP_OK(hipMemcpyAsync(c->d_mbs, c->h_mbs.data(), n * sizeof(h264r_mb), hipMemcpyHostToDevice, s));
+    HIP_OK(hipMemcpyAsync(c->d_levels, c->h_levels.data(), c->h_levels.size() * 2, hipMemcpyHostToDevice, s));
+    HIP_OK(hipMemcpyAsync(c->d_mv, c->h_mv.data(), c->h_mv.size() * 4, hipMemcpyHostToDevice, s));
+    HIP_OK(hipMemcpyAsync(c->d_ref, c->h_ref.data(), c->h_ref.size(), hipMemcpyHostToDevice, s));
+    HIP_OK(hipMemcpyAsync(c->d_slices, c->h_slices.data(), c->h_slices.size() * sizeof(h264r_slice), hipMemcpyHostToDevice, s));
+    HIP_OK(hipMemcpyAsync(c->d_pic, &c->h_pic, sizeof(h264r_pic), hipMemcpyHostToDevice, s));
+    HIP_OK(hipMemcpyAsync(c->d_quant, &c->h_quant, sizeof(h264r_quant), hipMemcpyHostToDevice, s));
+    // every referenced slot must be loaded
+    for (const h264r_slice& sl : c->h_slices)
+        for (int l = 0; l < 2; ++l)
+            for (int i = 0; i < sl.num_ref[l]; ++i) {
+                int slot = sl.ref_slot[l][i];
+                if (slot < 0 || slot >= H264R_MAX_SLOTS || !c->slot[slot][0] || c->slot_w[slot] != c->pw || c->slot_h[slot] != c->ph)
+                    return H264R_ESTATE;
+            }
+    h264r_batch b{};
+    b.num_pics = 1; b.width_mbs = c->pw; b.height_mbs = c->ph; b.slice_stride = (int)c->h_slices.size();
+    b.mbs = c->d_mbs; b.levels = c->d_levels; b.mv = c->d_mv; b.ref_idx = c->d_ref; b.slices = c->d_slices;
+    b.pics = c->d_pic; b.quant = c->d_quant; b.ref_planes = c->d_ref_planes;
+    b.out_y = c->d_out; b.out_u = c->d_out + ys; b.out_v = c->d_out + ys + cs;
+    if ((st = launch_all(c, b, s))) return st;
+    if (keep_slot >= 0) {
+        if ((st = ensure_slot(c, keep_slot, c->pw, c->ph))) return st;
+        HIP_OK(hipMemcpyAsync(c->slot[keep_slot][0], c->d_out, ys + 2 * cs, hipMemcpyDeviceToDevice, s));
+    }
+    if (y) HIP_OK(hipMemcpyAsync(y, b.out_y, ys, hipMemcpyDeviceToHost, s));
+    if (u) HIP_OK(hipMemcpyAsync(u, b.out_u, cs, hipMemcpyDeviceToHost, s));
+    if (v) HIP_OK(hipMemcpyAsync(v, b.out_v, cs, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    return H264R_OK;
+}
+
+}  // extern "C"

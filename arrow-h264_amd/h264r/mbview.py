@@ -1,0 +1,30 @@
+"""Per-macroblock views of a canonical picture (the unit Decoder.decode takes)."""
+from __future__ import annotations
+
+import numpy as np
+
+from . import _abi as A
+
+
+def level_count(rec) -> int:
+    """int16 entries of one MB's compacted level block (include/h264r.h)."""
+    if int(rec["mb_type"]) == A.I_PCM:
+        return 192
+    cbpl, cbpc = int(rec["cbp"]) & 15, int(rec["cbp"]) >> 4
+    n = 64 * bin(cbpl).count("1")
+    n += 128 if cbpc == 2 else 0
+    n += 16 if int(rec["mb_type"]) == A.I_16x16 else 0
+    n += 8 if cbpc else 0
+    return n
+
+
+def iter_mbs(p):
+    """Yield (addr, record[1], levels, mv[2,16], ref_idx[2,16]) in raster order."""
+    W, H = p.cfg.width_mbs, p.cfg.height_mbs
+    mv = p.mv.reshape(2, H, 4, W, 4).transpose(1, 3, 0, 2, 4).reshape(H, W, 2, 16)
+    rr = p.ref_idx.reshape(2, H, 4, W, 4).transpose(1, 3, 0, 2, 4).reshape(H, W, 2, 16)
+    for a in range(W * H):
+        rec = p.mbs[a:a + 1].copy()
+        off = int(rec["coef_off"][0])
+        lv = p.levels[off:off + level_count(rec[0])]
+        yield a, rec, lv, np.ascontiguousarray(mv[a // W, a % W]), np.ascontiguousarray(rr[a // W, a % W])

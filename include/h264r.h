@@ -225,6 +225,10 @@ int  h264r_ref_planes(h264r_ctx* ctx, int slot, uint8_t** y, uint8_t** u, uint8_
  * out[3] total.  Returns H264R_OK or an error. */
 int  h264r_last_timing(h264r_ctx* ctx, float out_ms[4]);
 int  h264r_set_timing(h264r_ctx* ctx, int enable);
+/* Debug hook: H264R_DBG_NO_DEBLOCK skips the loop filter (reconstruction only, to
+ * localise a mismatch against the oracle's pre-deblock planes). */
+#define H264R_DBG_NO_DEBLOCK 1
+int  h264r_set_debug(h264r_ctx* ctx, int flags);
 
 #ifdef __cplusplus
 }

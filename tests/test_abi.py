@@ -1,0 +1,99 @@
+"""C-ABI library: loads, exports every symbol include/h264r.h declares, struct
+layouts agree between C and the numpy/ctypes mirror, host helpers agree with the
+oracle.  No compute calls (no GPU needed)."""
+import ctypes as C
+import os
+import re
+import subprocess
+import tempfile
+
+import numpy as np
+import pytest
+
+import _oracle as O
+import h264r
+from h264r import _abi as A
+
+ROOT = O.ROOT
+
+
+@pytest.fixture(scope="module")
+def L():
+    h264r.build()
+    return h264r.lib()
+
+
+def header_symbols(name):
+    txt = open(os.path.join(ROOT, "include", name)).read()
+    return sorted(set(re.findall(r"\b(h264r_\w+)\s*\(", txt)))
+
+
+@pytest.mark.parametrize("hdr", ["h264r.h", "h264r_synth.h"])
+def test_exports_every_declared_symbol(L, hdr):
+    syms = header_symbols(hdr)
+    assert len(syms) >= 5
+    for s in syms:
+        assert hasattr(L, s), f"{s} declared in include/{hdr} but not exported"
+
+
+def test_struct_layouts_match_c():
+    src = r'''
+#include <stdio.h>
+#include <stddef.h>
+#include "h264r.h"
+#include "h264r_synth.h"
+int main(void) {
+  printf("%zu %zu %zu %zu %zu %zu\n", sizeof(h264r_mb), sizeof(h264r_slice), sizeof(h264r_quant),
+         sizeof(h264r_pic), sizeof(h264r_batch), sizeof(h264r_synth_cfg));
+  printf("%zu %zu %zu %zu\n", offsetof(h264r_mb, coef_off), offsetof(h264r_mb, ipred),
+         offsetof(h264r_slice, ref_slot), offsetof(h264r_slice, implicit_w1));
+  printf("%zu %zu\n", offsetof(h264r_batch, ref_planes), offsetof(h264r_synth_cfg, seed));
+  return 0; }
+'''
+    with tempfile.TemporaryDirectory() as td:
+        c = os.path.join(td, "l.c")
+        open(c, "w").write(src)
+        exe = os.path.join(td, "l")
+        subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), c, "-o", exe], check=True)
+        out = subprocess.run([exe], capture_output=True, text=True, check=True).stdout.split()
+    v = [int(x) for x in out]
+    assert v[0:6] == [A.MB_DTYPE.itemsize, A.SLICE_DTYPE.itemsize, A.QUANT_DTYPE.itemsize,
+                      A.PIC_DTYPE.itemsize, C.sizeof(A.Batch), C.sizeof(A.SynthCfg)]
+    assert v[6:10] == [A.MB_DTYPE.fields["coef_off"][1], A.MB_DTYPE.fields["ipred"][1],
+                       A.SLICE_DTYPE.fields["ref_slot"][1], A.SLICE_DTYPE.fields["implicit_w1"][1]]
+    assert v[10:12] == [A.Batch.ref_planes.offset, A.SynthCfg.seed.offset]
+
+
+def test_quant_flat_matches_oracle(L):
+    assert np.array_equal(h264r.quant_flat().view(np.uint8), O.quant_flat().view(np.uint8))
+
+
+def test_quant_lists_flat_equals_flat(L):
+    flat4 = (C.c_int32 * 16)(*([16] * 16))
+    flat8 = (C.c_int32 * 64)(*([16] * 64))
+    arr = (C.c_void_p * 12)(*([C.cast(flat4, C.c_void_p)] * 6 + [C.cast(flat8, C.c_void_p)] * 6))
+    q = np.zeros(1, A.QUANT_DTYPE)
+    assert L.h264r_quant_init_lists(A.ptr(q), arr) == 0
+    assert np.array_equal(q.view(np.uint8), h264r.quant_flat().view(np.uint8))
+
+
+def test_error_codes(L):
+    assert L.h264r_abi_version() == 1
+    assert L.h264r_strerror(A.EINVAL) == b"invalid argument"
+    h = C.c_void_p()
+    assert L.h264r_create(C.byref(h), 0, 0, 0, 1, 8) == A.EINVAL
+    assert L.h264r_create(C.byref(h), 0, 10, 10, 2, 8) == A.EUNSUPPORTED
+    assert L.h264r_create(C.byref(h), 0, 10, 10, 1, 10) == A.EUNSUPPORTED
+    assert L.h264r_quant_init_flat(None) == A.EINVAL
+    assert L.h264r_destroy(None) == A.EINVAL
+    assert L.h264r_mb_submit(None, 0, None, None, 0, None, None) == A.EINVAL
+
+
+def test_no_gpu_means_no_decoder(L):
+    """Without a gfx950 device the product refuses to run (no CPU fallback)."""
+    if L.h264r_device_count() > 0:
+        pytest.skip("a GPU is present")
+    h = C.c_void_p()
+    assert L.h264r_create(C.byref(h), 0, 10, 10, 1, 8) == A.ENODEVICE
+    with pytest.raises(h264r.H264RError):
+        h264r.Decoder()

@@ -1,0 +1,148 @@
+"""GPU path (lib/libh264r.so on gfx950) against the reference fixtures and the oracle.
+
+Bit-exact on every sample: this is integer work.  Full BASELINE sizes (1080p,
+2160p) are checked sample-for-sample against the oracle, which finishes them in
+seconds.
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+import _oracle as O
+import h264r
+from h264r import _abi as A
+from h264r import batch as B
+from h264r import synth
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "golden.json")))["fixtures"]
+
+
+def md5(a):
+    return hashlib.md5(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+@pytest.fixture(scope="module")
+def L():
+    h264r.build()
+    return h264r.lib()
+
+
+@pytest.fixture(scope="module")
+def dec(L):
+    d = h264r.Decoder(0, 240, 135)
+    yield d
+    d.close()
+
+
+def first_diff(a, b, n):
+    bad = np.argwhere(a != b)
+    if not len(bad):
+        return None
+    y, x = bad[0]
+    return f"{len(bad)} samples differ, first at (x={x}, y={y}) MB ({x // n}, {y // n}): gpu={a[y, x]} want={b[y, x]}"
+
+
+@pytest.mark.parametrize("fx", GOLDEN, ids=[f"{f['name']}[{f['index']}]" for f in GOLDEN])
+def test_gpu_matches_reference_fixture(L, dec, fx):
+    cfg = A.SynthCfg.from_dict(fx["cfg"])
+    p = synth.picture(L, cfg, fx["index"])
+    assert synth.input_digest(p) == fx["input_md5"]
+    refs = synth.refpics(L, cfg)
+    out = dec.decode_picture(p, refs)
+    got = {k: md5(out[i]) for i, k in enumerate("YUV")}
+    if got != fx["out_md5"]:
+        rec = dec.decode_picture(p, refs, no_deblock=True)
+        ref_rec = O.decode(p, refs, stage="recon")
+        ref_out = O.decode(p, refs)
+        msgs = []
+        for i, k in enumerate("YUV"):
+            n = 16 if i == 0 else 8
+            d = first_diff(rec[i], ref_rec[i], n)
+            if d:
+                msgs.append(f"recon {k}: {d}")
+            d = first_diff(out[i], ref_out[i], n)
+            if d:
+                msgs.append(f"final {k}: {d}")
+        pytest.fail("; ".join(msgs) or "md5 mismatch")
+
+
+def _batch_vs_oracle(L, dec, cidx, W, H, n, **over):
+    cfg = synth.default_cfg(L, cidx, W, H, **over)
+    pics = [synth.picture(L, cfg, i) for i in range(n)]
+    refs = synth.refpics(L, cfg)
+    for s, (y, u, v) in enumerate(refs):
+        dec.set_ref(s, y, u, v)
+    host = B.pack(pics, h264r.quant_flat())
+    db = B.to_device(host, n, None)
+    dec.decode_batch(db.batch)
+    import torch
+    torch.cuda.synchronize()
+    for i, p in enumerate(pics):
+        want = O.decode(p, refs)
+        got = db.planes(i)
+        for k in range(3):
+            d = first_diff(got[k], want[k], 16 if k == 0 else 8)
+            assert d is None, f"picture {i} plane {k}: {d}"
+
+
+def test_gpu_batch_cif_p(L, dec):
+    _batch_vs_oracle(L, dec, 3, 22, 18, 6)
+
+
+def test_gpu_batch_cif_b_explicit_cip(L, dec):
+    _batch_vs_oracle(L, dec, 4, 22, 18, 4, wp_mode=1, constrained_intra=1, num_refs=3, pcm_permille=20)
+
+
+def test_gpu_batch_1080p_p(L, dec):
+    """BASELINE config 3 size (1920x1088, IPPP Main distributions)."""
+    _batch_vs_oracle(L, dec, 3, 120, 68, 3)
+
+
+def test_gpu_batch_1080p_intra(L, dec):
+    """BASELINE config 2 size (all-intra, 4x4 + 8x8)."""
+    _batch_vs_oracle(L, dec, 2, 120, 68, 2)
+
+
+def test_gpu_2160p_b_8slices(L, dec):
+    """BASELINE config 5 size (3840x2160, 8 slices, idc 2)."""
+    _batch_vs_oracle(L, dec, 5, 240, 135, 1)
+
+
+@pytest.mark.parametrize("W,H", [(1, 1), (1, 7), (9, 1), (2, 2)])
+def test_gpu_degenerate_sizes(L, dec, W, H):
+    for cidx in (2, 3, 4):
+        cfg = synth.default_cfg(L, cidx, W, H, pcm_permille=50, num_slices=1)
+        p = synth.picture(L, cfg, 1)
+        refs = synth.refpics(L, cfg)
+        got = dec.decode_picture(p, refs)
+        want = O.decode(p, refs)
+        for k in range(3):
+            assert np.array_equal(got[k], want[k]), (cidx, k)
+
+
+def test_gpu_streaming_errors(L, dec):
+    cfg = synth.default_cfg(L, 3, 4, 3)
+    p = synth.picture(L, cfg, 0)
+    dec.init(4, 3, p.pic, p.slices)
+    with pytest.raises(h264r.H264RError) as e:
+        dec.deblock_filter()          # no MB submitted
+    assert e.value.status == A.ESTATE
+    with pytest.raises(h264r.H264RError) as e:
+        dec.deblock_filter()          # not inside a picture any more
+    assert e.value.status == A.ESTATE
+    with pytest.raises(h264r.H264RError) as e:
+        dec.decode(0, p.mbs[:1], p.levels[:0], p.mv[:, :1, :1].repeat(16).reshape(2, 16), np.zeros((2, 16), np.int8))
+    assert e.value.status == A.ESTATE
+
+
+def test_single_hip_runtime_in_process(L, dec):
+    """torch tensors and libh264r must share one HIP runtime (see h264r.lib())."""
+    maps = open("/proc/self/maps").read()
+    hip = {line.split()[-1] for line in maps.splitlines() if "libamdhip64" in line}
+    assert len(hip) == 1, hip
+    assert any("libh264r.so" in line for line in maps.splitlines())
