@@ -53,6 +53,17 @@ DEV h264r_mb load_mb(const h264r_mb* p)
     return m;
 }
 
+// Wave-level barrier for LDS scratch owned by one wave: orders this wave's LDS
+// accesses across lanes without a workgroup barrier (other waves of the
+// workgroup run independent work).
+DEV void wave_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_s_waitcnt(0xc07f);          // lgkmcnt(0): LDS ops of this wave done
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 DEV int mb_is_intra(const h264r_mb& m) { return (m.flags & H264R_MBF_INTRA) != 0; }
 
 // ----------------------------------------------------------- level block layout

@@ -6,6 +6,10 @@
 // The reconstruction itself never runs on the CPU: every entry point that
 // produces samples launches k_inter / k_intra / k_deblock and fails with
 // H264R_ENODEVICE when no gfx950 device is present.
+//
+// Launch sequence per batch: k_inter (every inter / PCM MB, fully parallel),
+// k_intra_pic (intra MBs, one workgroup per picture walking the
+// wavefront), k_deblock_pic (deblocking, same walk).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -16,9 +20,11 @@
 
 #include "h264r.h"
 
-extern "C" __global__ void k_inter(h264r_batch b);
-extern "C" __global__ void k_intra(h264r_batch b, int step);
-extern "C" __global__ void k_deblock(h264r_batch b, int step);
+namespace h264r { struct DbInfo; }
+extern "C" __global__ void k_inter(h264r_batch b, h264r::DbInfo* dbinfo);
+extern "C" __global__ void k_intra_pic(h264r_batch b, int* sync, int* err);
+extern "C" __global__ void k_deblock_pic(h264r_batch b, const h264r::DbInfo* dbinfo, int* sync, int* err);
+constexpr size_t DBINFO_BYTES = 48;
 
 namespace {
 
@@ -74,6 +80,7 @@ struct h264r_ctx {
     uint8_t* slot[H264R_MAX_SLOTS][3] = {};
     int slot_w[H264R_MAX_SLOTS] = {}, slot_h[H264R_MAX_SLOTS] = {};
     const uint8_t** d_ref_planes = nullptr;
+    int* d_err = nullptr;                 // device error word (bounded spin expired)
     // streaming-API staging
     bool in_pic = false;
     int pw = 0, ph = 0;
@@ -94,6 +101,9 @@ struct h264r_ctx {
     h264r_pic* d_pic = nullptr; size_t c_pic = 0;
     h264r_quant* d_quant = nullptr; size_t c_quant = 0;
     uint8_t* d_out = nullptr; size_t c_out = 0;
+    // per-batch scratch of the launch sequence
+    uint8_t* d_dbinfo = nullptr; size_t c_dbinfo = 0;
+    int* d_sync = nullptr; size_t c_sync = 0;
     // timing
     bool timing = false;
     int debug = 0;
@@ -177,12 +187,14 @@ int h264r_create(h264r_ctx** out, int device, int max_w, int max_h, int chroma_f
     if (!c) return H264R_ENOMEM;
     c->device = device; c->max_w = max_w; c->max_h = max_h;
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipMalloc(reinterpret_cast<void**>(&c->d_ref_planes), sizeof(uint8_t*) * 3 * H264R_MAX_SLOTS) != hipSuccess) {
+        hipMalloc(reinterpret_cast<void**>(&c->d_ref_planes), sizeof(uint8_t*) * 3 * H264R_MAX_SLOTS) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&c->d_err), sizeof(int)) != hipSuccess) {
         delete c;
         return H264R_EDEVICE;
     }
     for (int i = 0; i < 4; ++i) (void)hipEventCreate(&c->ev[i]);
     (void)hipMemset(c->d_ref_planes, 0, sizeof(uint8_t*) * 3 * H264R_MAX_SLOTS);
+    (void)hipMemset(c->d_err, 0, sizeof(int));
     *out = c;
     return H264R_OK;
 }
@@ -193,7 +205,7 @@ int h264r_destroy(h264r_ctx* c)
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (int s = 0; s < H264R_MAX_SLOTS; ++s) if (c->slot[s][0]) (void)hipFree(c->slot[s][0]);
-    void* bufs[] = {c->d_ref_planes, c->d_mbs, c->d_levels, c->d_mv, c->d_ref, c->d_slices, c->d_pic, c->d_quant, c->d_out};
+    void* bufs[] = {c->d_ref_planes, c->d_err, c->d_dbinfo, c->d_sync, c->d_mbs, c->d_levels, c->d_mv, c->d_ref, c->d_slices, c->d_pic, c->d_quant, c->d_out};
     for (void* b : bufs) if (b) (void)hipFree(b);
     for (int i = 0; i < 4; ++i) if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -240,21 +252,24 @@ int h264r_ref_planes(h264r_ctx* c, int slot, uint8_t** y, uint8_t** u, uint8_t**
 
 static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s)
 {
-    const int W = b.width_mbs, H = b.height_mbs, nsteps = (W - 1) + 2 * (H - 1) + 1;
+    const int W = b.width_mbs, H = b.height_mbs, P = b.num_pics;
+    const int nbands = (H + 15) / 16;
+    // scratch: per-MB deblocking records + two sync regions (ticket + per-row progress)
+    const size_t sync_ints = 1 + (size_t)P * H;
+    int st;
+    if ((st = dev_resize(&c->d_dbinfo, &c->c_dbinfo, (size_t)P * W * H * DBINFO_BYTES))) return st;
+    if ((st = dev_resize(&c->d_sync, &c->c_sync, 2 * sync_ints + 4))) return st;
+    HIP_OK(hipMemsetAsync(c->d_sync, 0, (2 * sync_ints + 4) * sizeof(int), s));
+    auto* dbinfo = reinterpret_cast<h264r::DbInfo*>(c->d_dbinfo);
     if (c->timing) HIP_OK(hipEventRecord(c->ev[0], s));
-    hipLaunchKernelGGL(k_inter, dim3(W * H, b.num_pics), dim3(64), 0, s, b);
+    hipLaunchKernelGGL(k_inter, dim3(W * H, P), dim3(64), 0, s, b, dbinfo);
     HIP_OK(hipGetLastError());
     if (c->timing) HIP_OK(hipEventRecord(c->ev[1], s));
-    for (int t = 0; t < nsteps; ++t) {
-        int n = grid_diag(t, W, H);
-        if (n) hipLaunchKernelGGL(k_intra, dim3(n, b.num_pics), dim3(64), 0, s, b, t);
-    }
+    hipLaunchKernelGGL(k_intra_pic, dim3(P * nbands), dim3(1024), 0, s, b, c->d_sync, c->d_err);
     HIP_OK(hipGetLastError());
     if (c->timing) HIP_OK(hipEventRecord(c->ev[2], s));
-    for (int t = 0; t < nsteps && !(c->debug & H264R_DBG_NO_DEBLOCK); ++t) {
-        int n = grid_diag(t, W, H);
-        if (n) hipLaunchKernelGGL(k_deblock, dim3(n, b.num_pics), dim3(64), 0, s, b, t);
-    }
+    if (!(c->debug & H264R_DBG_NO_DEBLOCK))
+        hipLaunchKernelGGL(k_deblock_pic, dim3(P * nbands), dim3(1024), 0, s, b, dbinfo, c->d_sync + sync_ints, c->d_err);
     HIP_OK(hipGetLastError());
     if (c->timing) HIP_OK(hipEventRecord(c->ev[3], s));
     return H264R_OK;
@@ -277,6 +292,18 @@ int h264r_set_timing(h264r_ctx* c, int enable)
 {
     if (!c) return H264R_EINVAL;
     c->timing = enable != 0;
+    return H264R_OK;
+}
+
+int h264r_check(h264r_ctx* c)
+{
+    if (!c) return H264R_EINVAL;
+    (void)hipSetDevice(c->device);
+    HIP_OK(hipStreamSynchronize(c->stream));
+    HIP_OK(hipDeviceSynchronize());
+    int e = 0;
+    HIP_OK(hipMemcpy(&e, c->d_err, sizeof(int), hipMemcpyDeviceToHost));
+    if (e) { (void)hipMemset(c->d_err, 0, sizeof(int)); return H264R_EDEVICE; }
     return H264R_OK;
 }
 
@@ -392,7 +419,7 @@ int h264r_picture_end(h264r_ctx* c, uint8_t* y, uint8_t* u, uint8_t* v, int keep
     if (u) HIP_OK(hipMemcpyAsync(u, b.out_u, cs, hipMemcpyDeviceToHost, s));
     if (v) HIP_OK(hipMemcpyAsync(v, b.out_v, cs, hipMemcpyDeviceToHost, s));
     HIP_OK(hipStreamSynchronize(s));
-    return H264R_OK;
+    return h264r_check(c);
 }
 
 }  // extern "C"

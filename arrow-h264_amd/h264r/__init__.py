@@ -74,6 +74,7 @@ def lib() -> C.CDLL:
         "h264r_ref_planes": ([P, I, C.POINTER(P), C.POINTER(P), C.POINTER(P)], I),
         "h264r_last_timing": ([P, C.POINTER(C.c_float)], I),
         "h264r_set_timing": ([P, I], I), "h264r_set_debug": ([P, I], I),
+        "h264r_check": ([P], I),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)
@@ -201,6 +202,10 @@ class Decoder:
 
     def decode_batch(self, batch: A.Batch, stream: int | None = None) -> None:
         _check("h264r_decode_batch", self._L.h264r_decode_batch(self._h, C.byref(batch), C.c_void_p(stream or 0)))
+
+    def check(self) -> None:
+        """Synchronise and raise if a device-side wavefront wait timed out."""
+        _check("h264r_check", self._L.h264r_check(self._h))
 
     def set_timing(self, on: bool) -> None:
         _check("h264r_set_timing", self._L.h264r_set_timing(self._h, 1 if on else 0))

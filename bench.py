@@ -1,0 +1,194 @@
+#!/usr/bin/env python3
+"""Benchmark: macroblocks/s of post-entropy reconstruction (MC + IDCT + intra +
+deblock) on MI355X, BASELINE.json's metric.
+
+A step = one h264r_decode_batch over a batch of synthetic pictures already
+resident in HBM (SURVEY 8(d) throughput mode: B independent pictures sharing a
+reference set).  Default workload: SURVEY config 3, 1080p (120x68 MBs) IPPP
+Main P pictures, B = 64.
+
+Multi-GPU (torchrun, one process per GPU): config 3 uses deblocking across the
+whole picture (disable_deblocking_filter_idc 0), which chains every MB of a
+picture (deblock.cc:547-551), so N > 1 runs N independent replicas (one stream
+per GPU, weak scaling, no data-path collective); see DESIGN.md.
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "arrow-h264_amd"))
+
+import numpy as np  # noqa: E402
+
+CONFIG_NAMES = {2: "1080p all-intra", 3: "1080p IPPP Main P-frames", 4: "1080p High IBBP B-frames, 4 slices",
+                5: "2160p High B-frames, 8 slices"}
+CONFIG_SIZE = {2: (120, 68), 3: (120, 68), 4: (120, 68), 5: (240, 135)}
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(cfg, refs, seconds: float):
+    """Oracle restatement (CPU port of the reference path), 1 thread, on a bounded
+    sample of the same workload: pictures are generated first, only decode is timed."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _oracle as O
+    from h264r import synth
+    L = O.lib()
+    nmb = cfg.width_mbs * cfg.height_mbs
+    t0 = time.perf_counter()
+    O.decode(synth.picture(L, cfg, 10_000), refs)
+    per_pic = max(time.perf_counter() - t0, 1e-3)
+    n = max(1, int(seconds / per_pic))
+    pics = [synth.picture(L, cfg, 10_001 + i) for i in range(n)]
+    t0 = time.perf_counter()
+    for p in pics:
+        O.decode(p, refs)
+    el = time.perf_counter() - t0
+    return n * nmb, el, n
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", type=int, default=3, choices=[2, 3, 4, 5])
+    ap.add_argument("--batch", type=int, default=0, help="pictures per GPU per step (default 64, 16 at 2160p)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-verify", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+    import torch.distributed as dist
+    import h264r
+    from h264r import batch as B
+    from h264r import synth
+
+    torch.cuda.set_device(local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    L = h264r.lib()
+    W, H = CONFIG_SIZE[args.config]
+    nb = args.batch or (16 if args.config == 5 else 64)
+    cfg = synth.default_cfg(L, args.config, W, H)
+    nmb = W * H
+
+    # inputs: this rank's stream of pictures (replicas: distinct picture indices per rank)
+    pics = [synth.picture(L, cfg, rank * nb + i) for i in range(nb)]
+    refs = synth.refpics(L, cfg)
+    rd = wr = 0
+    for p in pics:
+        r, w = synth.algo_bytes(L, p)
+        rd += r
+        wr += w
+
+    dec = h264r.Decoder(local, W, H)
+    for s, (y, u, v) in enumerate(refs):
+        dec.set_ref(s, y, u, v)
+    host = B.pack(pics, h264r.quant_flat())
+    db = B.to_device(host, nb, None)
+    stream = torch.cuda.current_stream().cuda_stream
+
+    for _ in range(args.warmup):
+        dec.decode_batch(db.batch, stream)
+    torch.cuda.synchronize()
+
+    # timed region: barrier + sync on both sides, exactly `steps` steps
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        dec.decode_batch(db.batch, stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    # phase breakdown: HIP events on the launch stream, outside the timed region
+    dec.set_timing(True)
+    phase = np.zeros(4)
+    reps = 3
+    for _ in range(reps):
+        dec.decode_batch(db.batch, stream)
+        phase += np.array(dec.last_timing())
+    phase /= reps
+    dec.set_timing(False)
+
+    verified = None
+    if not args.no_verify and rank == 0:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import _oracle as O
+        want = O.decode(pics[0], refs)
+        got = db.planes(0)
+        verified = all(np.array_equal(got[k], want[k]) for k in range(3))
+
+    total_mbs = world * nb * nmb * args.steps
+    value = total_mbs / dt
+    ms_per_step = dt / args.steps * 1e3
+    step_bytes = rd + wr
+    achieved = step_bytes / (ms_per_step * 1e-3) / 1e9
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        done, el, npics = cpu_baseline(cfg, refs, args.cpu_seconds)
+        cpu = {"value": done / el, "unit": "macroblocks/s", "cores": 1, "kind": "port",
+               "sample": f"{npics} pictures of the same {CONFIG_NAMES[args.config]} workload "
+                         f"({npics * nmb} MBs, {el:.1f} s) decoded by oracle/h264r_oracle.c (1 thread) "
+                         f"on {cpu_model()}"}
+
+    if rank == 0:
+        out = {
+            "metric": "macroblocks/s (decode reconstruct, post-entropy) 1080p P-frame; % HBM roofline",
+            "value": value, "unit": "macroblocks/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic (seeded SURVEY 8(d) generator, arrow-h264_amd/csrc/synth.c)",
+            "config": {"workload": CONFIG_NAMES[args.config], "survey_config": args.config,
+                       "width_mbs": W, "height_mbs": H, "pictures_per_gpu": nb,
+                       "parallelism": f"replicas{world}" if world > 1 else "single"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "whole step (k_inter + k_intra + k_deblock launches)",
+                         "algo_bytes_per_step": step_bytes, "algo_read_bytes_per_step": rd,
+                         "bytes_per_mb": step_bytes / (nb * nmb)},
+            "phase_ms": {"inter": phase[0], "intra": phase[1], "deblock": phase[2], "total": phase[3]},
+            "cpu_baseline": cpu,
+            "verified_vs_oracle": verified,
+        }
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

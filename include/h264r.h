@@ -229,6 +229,9 @@ int  h264r_set_timing(h264r_ctx* ctx, int enable);
  * localise a mismatch against the oracle's pre-deblock planes). */
 #define H264R_DBG_NO_DEBLOCK 1
 int  h264r_set_debug(h264r_ctx* ctx, int flags);
+/* Wait for the context's work and report a device-side failure (a wavefront wait
+ * that timed out): H264R_OK or H264R_EDEVICE. */
+int  h264r_check(h264r_ctx* ctx);
 
 #ifdef __cplusplus
 }
