@@ -140,14 +140,27 @@ DEV void db_info_mb(const h264r_batch& b, const Geom& g, int pic, int a, int lan
     }
 }
 
-constexpr int LP = 20;   // luma tile pitch: cols -4..15
-constexpr int CP = 12;   // chroma tile pitch: cols -4..7
+constexpr int LP = 20;    // luma tile: rows -4..15 x cols -4..15, 5 dwords per row
+constexpr int CP = 12;    // chroma tile: rows -4..7 x cols -4..7, 3 dwords per row
+constexpr int RING = 8;   // bottom-row ring entries (MBs) handed to the row below
+
+// Bottom rows of one MB for the row below: luma rows 12..15 (4 x 4 dwords) and
+// chroma rows 4..7 (2 planes x 4 x 2 dwords).
+struct alignas(16) RingEntry {
+    uint32_t y[4][4];
+    uint32_t c[2][4][2];
+};
 
 struct alignas(16) DbLds {
-    uint8_t lt[20 * LP];        // rows -4..15
-    uint8_t ct[2][12 * CP];     // rows -4..7
-    uint8_t bs[32];
+    uint32_t lt[20 * 5];          // luma tile, [row + 4][dword]
+    uint32_t ct[2][12 * 3];       // chroma tiles
+    uint8_t  bs[32];
+    uint32_t tail[4];             // DbInfo bytes 32..47
+    RingEntry ring[RING];
 };
+
+DEV uint8_t* ltb(DbLds& S) { return reinterpret_cast<uint8_t*>(S.lt); }
+DEV uint8_t* ctb(DbLds& S, int pl) { return reinterpret_cast<uint8_t*>(S.ct[pl]); }
 
 // alpha/beta/tc0 for one edge (filter_edge deblock.cc:469-480), 8-bit.
 DEV void edge_params(int qpp, int qpq, int offa, int offb, int& alpha, int& beta, int& idxA)
@@ -161,136 +174,85 @@ DEV void edge_params(int qpp, int qpq, int offa, int offb, int& alpha, int& beta
 
 DEV int tc0_of(int idxA, int bS) { return bS < 4 ? (int)((DB_TC0[idxA] >> (8 * (bS - 1))) & 255) : 0; }
 
-// Filter one line of N samples held in registers across the edges of one direction.
-// NE edges, edge k at v[4k+4] (q0); bs[k] its strength; qpp/qpq/params per edge.
-template <int NE, int N>
-DEV void filter_line(int (&v)[N], const int* bs, const int* alpha, const int* beta, const int* idxA, int chroma)
+// Filter one line held as packed bytes w[0..NE] (4 samples per dword; edge k sits
+// between dword k and dword k+1) across NE edges; edges are sequential because
+// neighbouring edges share samples (deblock.cc:459-485 per edge, :495-502 order).
+template <int NE>
+DEV void filter_line_packed(uint32_t (&w)[NE + 1], const uint8_t* bsrow, int seg, int qpP0, int qpQ, int offa, int offb,
+                            int chroma, int bsidx_step)
 {
 #pragma unroll
     for (int k = 0; k < NE; ++k) {
-        if (!bs[k]) continue;
-        filter_samples(v[4 * k + 0], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3],
-                       v[4 * k + 4], v[4 * k + 5], v[4 * k + 6], v[4 * k + 7],
-                       alpha[k], beta[k], bs[k], chroma, tc0_of(idxA[k], bs[k]));
+        const int bS = bsrow[k * bsidx_step * 4 + seg];
+        if (!bS) continue;
+        int alpha, beta, ia;
+        edge_params(k == 0 ? qpP0 : qpQ, qpQ, offa, offb, alpha, beta, ia);
+        const uint32_t a = w[k], c = w[k + 1];
+        int p3 = a & 255, p2 = (a >> 8) & 255, p1 = (a >> 16) & 255, p0 = a >> 24;
+        int q0 = c & 255, q1 = (c >> 8) & 255, q2 = (c >> 16) & 255, q3 = c >> 24;
+        filter_samples(p3, p2, p1, p0, q0, q1, q2, q3, alpha, beta, bS, chroma, tc0_of(ia, bS));
+        w[k] = (uint32_t)p3 | ((uint32_t)p2 << 8) | ((uint32_t)p1 << 16) | ((uint32_t)p0 << 24);
+        w[k + 1] = (uint32_t)q0 | ((uint32_t)q1 << 8) | ((uint32_t)q2 << 16) | ((uint32_t)q3 << 24);
     }
 }
 
-// Deblock MB (mbx, mby) of picture `pic`: vertical then horizontal edges
-// (filter_vertical / filter_horizontal deblock.cc:488-535); one wave.  Every MB
-// that precedes it in raster order and shares samples with it -- (x-1,y),
-// (x,y-1), (x+1,y-1) -- must already be filtered.
-DEV void deblock_mb(const h264r_batch& b, const Geom& g, int pic, int mbx, int mby, int lane, DbLds& S,
-                    const DbInfo* __restrict__ info_all)
+// The two filter passes of one MB on the LDS tiles: vertical edges with one lane per
+// sample row, then horizontal edges with one lane per column (filter_vertical /
+// filter_horizontal deblock.cc:488-535).  Lanes 0..15 luma, 16..31 chroma.
+DEV void filter_mb(DbLds& S, int lane)
 {
-    const int a = mby * g.wmb + mbx;
-    const DbInfo* info = info_all + (size_t)pic * g.nmb + a;
-    const int hasL = mbx > 0, hasU = mby > 0;
-    uint8_t* Y = b.out_y + (size_t)pic * g.ysz;
-    uint8_t* Cpl[2] = {b.out_u + (size_t)pic * g.csz, b.out_v + (size_t)pic * g.csz};
-    const int X0 = mbx * 16, Y0 = mby * 16, Xc = mbx * 8, Yc = mby * 8;
-
-    // ---- stage: strengths + samples (dword loads; rows/cols -4..-1 where a neighbour exists)
-    if (lane < 8) reinterpret_cast<uint32_t*>(S.bs)[lane] = reinterpret_cast<const uint32_t*>(info->bs)[lane];
-    for (int k = lane; k < 100; k += 64) {
-        int r = k / 5, d = k % 5;
-        if ((r < 4 && !hasU) || (d == 0 && !hasL)) continue;
-        reinterpret_cast<uint32_t*>(S.lt)[k] =
-            *reinterpret_cast<const uint32_t*>(Y + (size_t)(Y0 + r - 4) * g.W + X0 - 4 + 4 * d);
-    }
-    for (int k = lane; k < 72; k += 64) {
-        int pl = k / 36, r = (k % 36) / 3, d = k % 3;
-        if ((r < 4 && !hasU) || (d == 0 && !hasL)) continue;
-        reinterpret_cast<uint32_t*>(S.ct[pl])[r * 3 + d] =
-            *reinterpret_cast<const uint32_t*>(Cpl[pl] + (size_t)(Yc + r - 4) * g.Wc + Xc - 4 + 4 * d);
-    }
-    const uint4 tail = *reinterpret_cast<const uint4*>(&info->qpy[0]);
-    const int qpyQ = (int8_t)(tail.x & 255), qpyL = (int8_t)((tail.x >> 8) & 255), qpyU = (int8_t)((tail.x >> 16) & 255);
-    const int qpc[2][3] = {{(int8_t)(tail.x >> 24), (int8_t)(tail.y & 255), (int8_t)((tail.y >> 8) & 255)},
-                           {(int8_t)((tail.y >> 16) & 255), (int8_t)(tail.y >> 24), (int8_t)(tail.z & 255)}};
-    const int offa = (int8_t)((tail.z >> 8) & 255), offb = (int8_t)((tail.z >> 16) & 255);
-    wave_sync();
-
+    const uint32_t t0 = S.tail[0], t1 = S.tail[1], t2 = S.tail[2];
+    const int qpyQ = (int8_t)(t0 & 255), qpyL = (int8_t)((t0 >> 8) & 255), qpyU = (int8_t)((t0 >> 16) & 255);
+    const int offa = (int8_t)((t2 >> 8) & 255), offb = (int8_t)((t2 >> 16) & 255);
+#pragma unroll 1
     for (int hor = 0; hor < 2; ++hor) {
-        if (lane < 16) {                                       // luma line `lane`
-            int bs[4], al[4], be[4], ia[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                bs[e] = S.bs[hor * 16 + e * 4 + (lane >> 2)];
-                edge_params(e == 0 ? (hor ? qpyU : qpyL) : qpyQ, qpyQ, offa, offb, al[e], be[e], ia[e]);
-            }
-            int v[20];
+        if (lane < 16) {
+            uint32_t w[5];
+            uint8_t* lt = ltb(S);
             if (!hor) {
-                const uint32_t* row = reinterpret_cast<const uint32_t*>(S.lt + (lane + 4) * LP);
 #pragma unroll
-                for (int d = 0; d < 5; ++d) {
-                    uint32_t w = row[d];
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) v[4 * d + k] = (w >> (8 * k)) & 255;
-                }
+                for (int d = 0; d < 5; ++d) w[d] = S.lt[(lane + 4) * 5 + d];
             } else {
-#pragma unroll
-                for (int i = 0; i < 20; ++i) v[i] = S.lt[i * LP + lane + 4];
-            }
-            filter_line<4>(v, bs, al, be, ia, 0);
-            if (!hor) {
-                uint32_t* row = reinterpret_cast<uint32_t*>(S.lt + (lane + 4) * LP);
 #pragma unroll
                 for (int d = 0; d < 5; ++d)
-                    row[d] = (uint32_t)v[4 * d] | ((uint32_t)v[4 * d + 1] << 8) | ((uint32_t)v[4 * d + 2] << 16) |
-                             ((uint32_t)v[4 * d + 3] << 24);
+                    w[d] = (uint32_t)lt[(4 * d) * LP + lane + 4] | ((uint32_t)lt[(4 * d + 1) * LP + lane + 4] << 8) |
+                           ((uint32_t)lt[(4 * d + 2) * LP + lane + 4] << 16) | ((uint32_t)lt[(4 * d + 3) * LP + lane + 4] << 24);
+            }
+            filter_line_packed<4>(w, &S.bs[hor * 16], lane >> 2, hor ? qpyU : qpyL, qpyQ, offa, offb, 0, 1);
+            if (!hor) {
+#pragma unroll
+                for (int d = 0; d < 5; ++d) S.lt[(lane + 4) * 5 + d] = w[d];
             } else {
 #pragma unroll
-                for (int i = 1; i < 20; ++i) S.lt[i * LP + lane + 4] = (uint8_t)v[i];
+                for (int i = 1; i < 20; ++i) lt[i * LP + lane + 4] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
             }
-        } else if (lane < 32) {                                // chroma line
+        } else if (lane < 32) {
             const int pl = (lane - 16) >> 3, r = (lane - 16) & 7;
-            uint8_t* ct = S.ct[pl];
-            int bs[2], al[2], be[2], ia[2];
-#pragma unroll
-            for (int ce = 0; ce < 2; ++ce) {
-                bs[ce] = S.bs[hor * 16 + (ce ? 2 : 0) * 4 + (r >> 1)];     // StrengthIdx = pel << 1 (:460)
-                edge_params(ce == 0 ? qpc[pl][hor ? 2 : 1] : qpc[pl][0], qpc[pl][0], offa, offb, al[ce], be[ce], ia[ce]);
-            }
-            int v[12];
+            const int qcQ = pl ? (int8_t)((t1 >> 16) & 255) : (int8_t)(t0 >> 24);
+            const int qcL = pl ? (int8_t)(t1 >> 24) : (int8_t)(t1 & 255);
+            const int qcU = pl ? (int8_t)(t2 & 255) : (int8_t)((t1 >> 8) & 255);
+            uint32_t w[3];
+            uint8_t* ct = ctb(S, pl);
             if (!hor) {
-                const uint32_t* row = reinterpret_cast<const uint32_t*>(ct + (r + 4) * CP);
 #pragma unroll
-                for (int d = 0; d < 3; ++d) {
-                    uint32_t w = row[d];
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) v[4 * d + k] = (w >> (8 * k)) & 255;
-                }
+                for (int d = 0; d < 3; ++d) w[d] = S.ct[pl][(r + 4) * 3 + d];
             } else {
-#pragma unroll
-                for (int i = 0; i < 12; ++i) v[i] = ct[i * CP + r + 4];
-            }
-            filter_line<2>(v, bs, al, be, ia, 1);
-            if (!hor) {
-                uint32_t* row = reinterpret_cast<uint32_t*>(ct + (r + 4) * CP);
 #pragma unroll
                 for (int d = 0; d < 3; ++d)
-                    row[d] = (uint32_t)v[4 * d] | ((uint32_t)v[4 * d + 1] << 8) | ((uint32_t)v[4 * d + 2] << 16) |
-                             ((uint32_t)v[4 * d + 3] << 24);
+                    w[d] = (uint32_t)ct[(4 * d) * CP + r + 4] | ((uint32_t)ct[(4 * d + 1) * CP + r + 4] << 8) |
+                           ((uint32_t)ct[(4 * d + 2) * CP + r + 4] << 16) | ((uint32_t)ct[(4 * d + 3) * CP + r + 4] << 24);
+            }
+            // chroma edge 1 uses luma edge 2 (bsidx_step 2); StrengthIdx = pel << 1 (deblock.cc:460)
+            filter_line_packed<2>(w, &S.bs[hor * 16], r >> 1, hor ? qcU : qcL, qcQ, offa, offb, 1, 2);
+            if (!hor) {
+#pragma unroll
+                for (int d = 0; d < 3; ++d) S.ct[pl][(r + 4) * 3 + d] = w[d];
             } else {
 #pragma unroll
-                for (int i = 1; i < 12; ++i) ct[i * CP + r + 4] = (uint8_t)v[i];
+                for (int i = 1; i < 12; ++i) ct[i * CP + r + 4] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
             }
         }
         wave_sync();
-    }
-
-    // ---- write back: rows -3..15 (top rows only if the top MB exists), dwords from col -4
-    for (int k = lane; k < 95; k += 64) {
-        int r = k / 5 + 1, d = k % 5;
-        if ((r < 4 && !hasU) || (d == 0 && !hasL)) continue;
-        *reinterpret_cast<uint32_t*>(Y + (size_t)(Y0 + r - 4) * g.W + X0 - 4 + 4 * d) =
-            reinterpret_cast<const uint32_t*>(S.lt)[r * 5 + d];
-    }
-    for (int k = lane; k < 66; k += 64) {
-        int pl = k / 33, r = (k % 33) / 3 + 1, d = k % 3;
-        if ((r < 4 && !hasU) || (d == 0 && !hasL)) continue;
-        *reinterpret_cast<uint32_t*>(Cpl[pl] + (size_t)(Yc + r - 4) * g.Wc + Xc - 4 + 4 * d) =
-            reinterpret_cast<const uint32_t*>(S.ct[pl])[r * 3 + d];
     }
 }
 
