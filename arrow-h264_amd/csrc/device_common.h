@@ -73,6 +73,14 @@ struct LevelOffs {
     int cac, ldc, cdc;
 };
 
+// Offset of coded 8x8 luma block k inside the level block, or -1 (register-only form
+// of LevelOffs::b8 for a per-lane k).
+DEV int b8_offset(int cbp, int k)
+{
+    const int cbpl = cbp & 15;
+    return (cbpl >> k) & 1 ? 64 * __builtin_popcount(cbpl & ((1 << k) - 1)) : -1;
+}
+
 DEV LevelOffs level_offsets(const h264r_mb& m)
 {
     LevelOffs o;
@@ -150,6 +158,130 @@ DEV int luma_qpel(const uint8_t* __restrict__ img, int W, int H, int x, int y, i
 #undef S
 #undef B1
 #undef H1
+}
+
+// ------------------------------------------------------------ row-window MC
+// The per-sample forms above fetch one byte per tap.  The MC path proper loads
+// each reference row as three aligned dwords and extracts the samples it needs;
+// clamping (the padded-plane equivalence of inter_prediction.cc:185-186) is
+// applied to the row index always and to the column only for windows that
+// cross the picture edge.  Reads may run up to 11 bytes past the last sample
+// of a row: reference planes carry H264R_PLANE_SLACK bytes of slack.
+
+// Samples ref(x-2+k, y), k = 0..8, of the row whose dwords w0..w2 start at
+// a = clip(x-2) & ~3.
+DEV void row9(uint32_t w0, uint32_t w1, uint32_t w2, int x, int W, int (&p)[9])
+{
+    if (x - 2 >= 0 && x + 6 < W) {
+        const int s = (x - 2) & 3;
+        const uint32_t r0 = __builtin_amdgcn_alignbyte(w1, w0, s);
+        const uint32_t r1 = __builtin_amdgcn_alignbyte(w2, w1, s);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) { p[k] = (r0 >> (8 * k)) & 255; p[4 + k] = (r1 >> (8 * k)) & 255; }
+        p[8] = (w2 >> (8 * s)) & 255;
+    } else {
+        const int a = clip3(0, W - 1, x - 2) & ~3;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            const int idx = clip3(0, W - 1, x - 2 + k) - a;
+            const uint32_t d = idx < 4 ? w0 : (idx < 8 ? w1 : w2);
+            p[k] = (d >> (8 * (idx & 3))) & 255;
+        }
+    }
+}
+
+DEV const uint32_t* row_dwords(const uint8_t* __restrict__ img, int W, int H, int x, int y)
+{
+    const int a = clip3(0, W - 1, x - 2) & ~3;
+    return reinterpret_cast<const uint32_t*>(img + (size_t)clip3(0, H - 1, y) * W + a);
+}
+
+// Four luma prediction samples (x..x+3, y) at quarter-sample phase (xf, yf),
+// get_block_luma (inter_prediction.cc:158-340) in spec form (8.4.2.2.1): the
+// half-sample values b (horizontal), h (vertical), j (centre) and their
+// averages.  The 6 rows y-2..y+3 are streamed; each tap row is loaded once.
+DEV void luma_pred4(const uint8_t* __restrict__ img, int W, int H, int x, int y, int xf, int yf, int (&out)[4])
+{
+    constexpr int C6[6] = {1, -5, 20, 20, -5, 1};
+    if (yf == 0) {                                    // G, a, b, c: one row
+        const uint32_t* q = row_dwords(img, W, H, x, y);
+        int p[9];
+        row9(q[0], q[1], q[2], x, W, p);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            if (xf == 0) { out[c] = p[2 + c]; continue; }
+            const int b = clip255((tap6(p[c], p[c + 1], p[c + 2], p[c + 3], p[c + 4], p[c + 5]) + 16) >> 5);
+            out[c] = xf == 2 ? b : (b + (xf == 3 ? p[3 + c] : p[2 + c]) + 1) >> 1;
+        }
+        return;
+    }
+    uint32_t w[6][3];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        const uint32_t* q = row_dwords(img, W, H, x, y - 2 + k);
+        w[k][0] = q[0]; w[k][1] = q[1]; w[k][2] = q[2];
+    }
+    const bool jfam = xf == 2 || (yf == 2 && xf != 0);   // needs the centre sample j
+    const int hs = xf == 3 ? 1 : 0;                        // column of h / G for odd phases
+    const int brow = yf == 3 ? 3 : 2;                      // row of b / G (y or y+1)
+    int hacc[4] = {0, 0, 0, 0}, jacc[4] = {0, 0, 0, 0}, bsv[4] = {0, 0, 0, 0}, gsv[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        int p[9];
+        row9(w[k][0], w[k][1], w[k][2], x, W, p);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            hacc[c] += C6[k] * (hs ? p[3 + c] : p[2 + c]);
+            if (k == brow) gsv[c] = p[2 + c];
+            if (jfam || ((xf & 1) && k == brow)) {
+                const int b1 = tap6(p[c], p[c + 1], p[c + 2], p[c + 3], p[c + 4], p[c + 5]);
+                jacc[c] += C6[k] * b1;
+                if (k == brow) bsv[c] = b1;
+            }
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const int h = clip255((hacc[c] + 16) >> 5);
+        const int b = clip255((bsv[c] + 16) >> 5);
+        int v;
+        if (xf == 0) v = yf == 2 ? h : (h + gsv[c] + 1) >> 1;                 // d, h, n
+        else if (!jfam) v = (b + h + 1) >> 1;                                 // e, g, p, r
+        else {
+            const int j = clip255((jacc[c] + 512) >> 10);
+            if (xf == 2 && yf == 2) v = j;                                    // j
+            else if (xf == 2) v = (j + b + 1) >> 1;                           // f, q
+            else v = (j + h + 1) >> 1;                                        // i, k
+        }
+        out[c] = v;
+    }
+}
+
+// Two chroma prediction samples (xi, xi+1; yi) at eighth-sample phase (xf, yf),
+// get_block_chroma (inter_prediction.cc:380-404).
+DEV void chroma_pred2(const uint8_t* __restrict__ img, int W, int H, int xi, int yi, int xf, int yf, int (&out)[2])
+{
+    const int a = clip3(0, W - 1, xi) & ~3;
+    int p[2][3];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const uint32_t* q = reinterpret_cast<const uint32_t*>(img + (size_t)clip3(0, H - 1, yi + k) * W + a);
+        const uint32_t w0 = q[0], w1 = q[1];
+        if (xi >= 0 && xi + 2 < W) {
+            const uint32_t r = __builtin_amdgcn_alignbyte(w1, w0, xi & 3);
+            p[k][0] = r & 255; p[k][1] = (r >> 8) & 255; p[k][2] = (r >> 16) & 255;
+        } else {
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                const int idx = clip3(0, W - 1, xi + c) - a;
+                p[k][c] = ((idx < 4 ? w0 : w1) >> (8 * (idx & 3))) & 255;
+            }
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+        out[c] = ((8 - xf) * (8 - yf) * p[0][c] + xf * (8 - yf) * p[0][c + 1] + (8 - xf) * yf * p[1][c] +
+                  xf * yf * p[1][c + 1] + 32) >> 6;
 }
 
 // get_block_chroma sample (inter_prediction.cc:380-404).

@@ -8,8 +8,8 @@
 // H264R_ENODEVICE when no gfx950 device is present.
 //
 // Launch sequence per batch: k_inter (every inter / PCM MB, fully parallel),
-// k_intra_pic (intra MBs, one workgroup per picture walking the
-// wavefront), k_deblock_pic (deblocking, same walk).
+// k_intra_pic (intra MBs, banded workgroups walking the wavefront),
+// k_deblock (deblocking, one wave per pair of MB rows walking the wavefront).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -20,11 +20,13 @@
 
 #include "h264r.h"
 
-namespace h264r { struct DbInfo; }
+namespace h264r { struct DbInfo; struct RingEntry; }
 extern "C" __global__ void k_inter(h264r_batch b, h264r::DbInfo* dbinfo);
 extern "C" __global__ void k_intra_pic(h264r_batch b, int* sync, int* err);
-extern "C" __global__ void k_deblock_pic(h264r_batch b, const h264r::DbInfo* dbinfo, int* sync, int* err);
+extern "C" __global__ void k_deblock(h264r_batch b, const h264r::DbInfo* dbinfo, h264r::RingEntry* hb,
+                                     int* sync, int* err);
 constexpr size_t DBINFO_BYTES = 48;
+constexpr size_t HANDOFF_BYTES = 128;   // one RingEntry per MB
 
 namespace {
 
@@ -104,6 +106,7 @@ struct h264r_ctx {
     // per-batch scratch of the launch sequence
     uint8_t* d_dbinfo = nullptr; size_t c_dbinfo = 0;
     int* d_sync = nullptr; size_t c_sync = 0;
+    uint8_t* d_hb = nullptr; size_t c_hb = 0;
     // timing
     bool timing = false;
     int debug = 0;
@@ -205,7 +208,7 @@ int h264r_destroy(h264r_ctx* c)
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (int s = 0; s < H264R_MAX_SLOTS; ++s) if (c->slot[s][0]) (void)hipFree(c->slot[s][0]);
-    void* bufs[] = {c->d_ref_planes, c->d_err, c->d_dbinfo, c->d_sync, c->d_mbs, c->d_levels, c->d_mv, c->d_ref, c->d_slices, c->d_pic, c->d_quant, c->d_out};
+    void* bufs[] = {c->d_ref_planes, c->d_err, c->d_dbinfo, c->d_sync, c->d_hb, c->d_mbs, c->d_levels, c->d_mv, c->d_ref, c->d_slices, c->d_pic, c->d_quant, c->d_out};
     for (void* b : bufs) if (b) (void)hipFree(b);
     for (int i = 0; i < 4; ++i) if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -219,7 +222,7 @@ static int ensure_slot(h264r_ctx* c, int slot, int w, int h)
     if (c->slot[slot][0]) { (void)hipFree(c->slot[slot][0]); c->slot[slot][0] = nullptr; }
     size_t ys = (size_t)w * 16 * h * 16, cs = (size_t)w * 8 * h * 8;
     uint8_t* base = nullptr;
-    if (hipMalloc(reinterpret_cast<void**>(&base), ys + 2 * cs) != hipSuccess) return H264R_ENOMEM;
+    if (hipMalloc(reinterpret_cast<void**>(&base), ys + 2 * cs + H264R_PLANE_SLACK) != hipSuccess) return H264R_ENOMEM;
     c->slot[slot][0] = base; c->slot[slot][1] = base + ys; c->slot[slot][2] = base + ys + cs;
     c->slot_w[slot] = w; c->slot_h[slot] = h;
     HIP_OK(hipMemcpy(c->d_ref_planes + 3 * slot, c->slot[slot], 3 * sizeof(uint8_t*), hipMemcpyHostToDevice));
@@ -253,11 +256,13 @@ int h264r_ref_planes(h264r_ctx* c, int slot, uint8_t** y, uint8_t** u, uint8_t**
 static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s)
 {
     const int W = b.width_mbs, H = b.height_mbs, P = b.num_pics;
-    const int nbands = (H + 15) / 16;
-    // scratch: per-MB deblocking records + two sync regions (ticket + per-row progress)
+    const int nbands = (H + 15) / 16, npairs = (H + 1) / 2;
+    // scratch: per-MB deblocking records, row-pair hand-off records, two sync
+    // regions (ticket + per-row / per-pair progress)
     const size_t sync_ints = 1 + (size_t)P * H;
     int st;
     if ((st = dev_resize(&c->d_dbinfo, &c->c_dbinfo, (size_t)P * W * H * DBINFO_BYTES))) return st;
+    if ((st = dev_resize(&c->d_hb, &c->c_hb, (size_t)P * npairs * W * HANDOFF_BYTES))) return st;
     if ((st = dev_resize(&c->d_sync, &c->c_sync, 2 * sync_ints + 4))) return st;
     HIP_OK(hipMemsetAsync(c->d_sync, 0, (2 * sync_ints + 4) * sizeof(int), s));
     auto* dbinfo = reinterpret_cast<h264r::DbInfo*>(c->d_dbinfo);
@@ -269,7 +274,8 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s)
     HIP_OK(hipGetLastError());
     if (c->timing) HIP_OK(hipEventRecord(c->ev[2], s));
     if (!(c->debug & H264R_DBG_NO_DEBLOCK))
-        hipLaunchKernelGGL(k_deblock_pic, dim3(P * nbands), dim3(1024), 0, s, b, dbinfo, c->d_sync + sync_ints, c->d_err);
+        hipLaunchKernelGGL(k_deblock, dim3(P * npairs), dim3(64), 0, s, b, dbinfo,
+                           reinterpret_cast<h264r::RingEntry*>(c->d_hb), c->d_sync + sync_ints, c->d_err);
     HIP_OK(hipGetLastError());
     if (c->timing) HIP_OK(hipEventRecord(c->ev[3], s));
     return H264R_OK;

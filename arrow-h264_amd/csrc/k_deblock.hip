@@ -1,0 +1,231 @@
+// k_deblock.hip -- the in-loop deblocking filter of every picture of a batch.
+//
+// The reference filters MB by MB in raster order, vertical edges then
+// horizontal edges (Deblock::deblock_pic, deblock.cc:537-552), and the result
+// is order-dependent: MB (x,y)'s top edge reads samples that MB (x+1,y-1)'s
+// left edge wrote, so MB (x,y) may start only once (x+1,y-1) is done -- a
+// wavefront with a 2-MB lag per row.
+//
+// Work unit: one 64-lane wave owns a PAIR of MB rows (2p, 2p+1) of one
+// picture.  Lanes 0..31 walk row 2p ("half A"), lanes 32..63 walk row 2p+1
+// ("half B") two MBs behind, so every filter instruction works on two MBs
+// and all 64 lanes are busy (per half: lanes 0..15 luma lines, 16..31 chroma
+// lines).  Inside the pair, half A hands its bottom rows to half B through an
+// LDS ring; between pairs, half B publishes each MB's final-for-it bottom rows
+// as one 128-byte record (one cache line, stored write-through with `sc1`)
+// into a hand-off buffer and bumps a progress counter after `s_waitcnt
+// vmcnt(0)`; the pair below polls the counter and reads the records with
+// `sc1` loads (MI355X_MICROARCH.md, inter-workgroup hand-off with sc1 stores
+// and loads).  Pairs are taken as tickets from an atomic counter in
+// pair-major order, so a wave only ever waits on a ticket taken earlier by a
+// running wave: no deadlock under any dispatch order or residency; every spin
+// is bounded and flags the error word.
+//
+// Sample ownership: each MB row writes its rows 0..12 (chroma 0..4) and the
+// rows 13..15 (chroma 5..7) of the row above after filtering its top edge;
+// only the picture's last row writes its own bottom rows.  A sample is stored
+// once, when final, by exactly one wave.
+#include "mb_deblock.h"
+
+using namespace h264r;
+
+namespace {
+
+constexpr int PUB = 2;                      // progress publish granularity (MBs)
+constexpr int DRING = 4;                    // row A -> row B ring depth (lag is 2)
+constexpr unsigned SPIN_LIMIT = 1u << 22;   // ~0.3 s of polling, then flag an error
+
+struct alignas(16) PairLds {
+    DbLds t[2];                   // per half
+    RingEntry ring[2][DRING];     // per half: bottom rows of the last MBs
+};
+
+DEV uint32_t ld_cc(const uint32_t* p)       // coherent (L1-bypassing, sc1) load
+{
+    return __hip_atomic_load(const_cast<uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+DEV void st_cc(uint32_t* p, uint32_t v)     // write-through (sc1) store
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+}  // namespace
+
+// hb: hand-off records [pic][pair][W] (RingEntry); sync[0] ticket counter,
+// sync[1 + pic * npairs + pair] = number of complete records of that pair.
+extern "C" __global__ __launch_bounds__(64) void k_deblock(h264r_batch b, const DbInfo* __restrict__ dbinfo,
+                                                          RingEntry* hb, int* sync, int* err)
+{
+    __shared__ PairLds L;
+    const int lane = threadIdx.x, h = lane >> 5, hl = lane & 31;
+    const Geom g = make_geom(b.width_mbs, b.height_mbs);
+    const int W = g.wmb, H = g.hmb, npairs = (H + 1) >> 1;
+
+    int tk = 0;
+    if (lane == 0) tk = atomicAdd(&sync[0], 1);
+    const int ticket = __builtin_amdgcn_readfirstlane(tk);
+    const int rp = ticket / b.num_pics, pic = ticket % b.num_pics;
+    const int r = 2 * rp + h;                              // this half's MB row
+    const bool hasB = 2 * rp + 1 < H;
+    const bool half_on = r < H;
+    const bool last_row = r == H - 1;
+    const bool feeds_ring = h == 0 && hasB;                // A -> B through LDS
+    const bool feeds_hb = h == 1 && rp + 1 < npairs;       // B -> next pair through hb
+    const bool pair_feeds = rp + 1 < npairs && hasB;
+    int* prog_in = rp > 0 ? sync + 1 + (size_t)pic * npairs + (rp - 1) : nullptr;
+    int* prog_out = sync + 1 + (size_t)pic * npairs + rp;
+    const uint32_t* hb_in = rp > 0 ? reinterpret_cast<const uint32_t*>(hb + ((size_t)pic * npairs + rp - 1) * W) : nullptr;
+    uint32_t* hb_out = reinterpret_cast<uint32_t*>(hb + ((size_t)pic * npairs + rp) * W);
+
+    DbLds& S = L.t[h];
+    uint8_t* Y = b.out_y + (size_t)pic * g.ysz;
+    uint8_t* Cp[2] = {b.out_u + (size_t)pic * g.csz, b.out_v + (size_t)pic * g.csz};
+    const int Y0 = r * 16, Yc = r * 8;
+    const uint32_t* info_row = reinterpret_cast<const uint32_t*>(dbinfo + (size_t)pic * g.nmb + (size_t)r * W);
+
+    // per-lane roles inside a half (32 lanes)
+    const int by0 = hl >> 2, bd0 = hl & 3;                 // luma body dwords hl and hl + 32
+    const int cpl = hl >> 4, cy = (hl >> 1) & 7, cd = hl & 1;   // chroma body dword
+    const int steps = W + (hasB ? 2 : 0);
+
+    uint32_t pf_y0 = 0, pf_y1 = 0, pf_c = 0, pf_i = 0, pf_top = 0;
+    int seen = 0;          // last observed progress of the pair above
+    bool ok = true;
+
+    // Issue the loads of step t (this half's MB t - 2h): body, record and, for
+    // half A below another pair, the hand-off record of the MB above.
+    auto prefetch = [&](int t) {
+        if (rp > 0 && t < W) {
+            const int need = t + 1;                        // record t of the pair above
+            unsigned spins = 0;
+            while (seen < need) {
+                seen = __builtin_amdgcn_readfirstlane(
+                    (int)ld_cc(reinterpret_cast<const uint32_t*>(prog_in)));
+                if (seen >= need) break;
+                __builtin_amdgcn_s_sleep(1);
+                if (++spins > SPIN_LIMIT) {
+                    __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    ok = false;
+                    seen = W;
+                    break;
+                }
+            }
+        }
+        const int x = t - 2 * h;
+        if (half_on && x >= 0 && x < W) {
+            const uint8_t* yb = Y + (size_t)(Y0 + by0) * g.W + x * 16 + 4 * bd0;
+            pf_y0 = *reinterpret_cast<const uint32_t*>(yb);
+            pf_y1 = *reinterpret_cast<const uint32_t*>(yb + (size_t)8 * g.W);
+            pf_c = *reinterpret_cast<const uint32_t*>(Cp[cpl] + (size_t)(Yc + cy) * g.Wc + x * 8 + 4 * cd);
+            if (hl < 12) pf_i = info_row[x * 12 + hl];
+            if (h == 0 && rp > 0) pf_top = ld_cc(hb_in + (size_t)x * 32 + hl);
+        }
+    };
+
+    prefetch(0);
+    for (int t = 0; t < steps; ++t) {
+        const int x = t - 2 * h;
+        const bool act = half_on && x >= 0 && x < W;
+        const int X0 = x * 16, Xc = x * 8;
+
+        // ---- assemble this half's tile: body, record, top rows (left strip = carry)
+        if (act) {
+            S.lt[(4 + by0) * 5 + 1 + bd0] = pf_y0;
+            S.lt[(12 + by0) * 5 + 1 + bd0] = pf_y1;
+            S.ct[cpl][(4 + cy) * 3 + 1 + cd] = pf_c;
+            if (hl < 8) reinterpret_cast<uint32_t*>(S.bs)[hl] = pf_i;
+            else if (hl < 12) S.tail[hl - 8] = pf_i;
+            if (r > 0) {
+                const uint32_t v = h == 0 ? pf_top : reinterpret_cast<const uint32_t*>(&L.ring[0][x % DRING])[hl];
+                if (hl < 16) S.lt[(hl >> 2) * 5 + 1 + (hl & 3)] = v;
+                else {
+                    const int k = hl - 16, pl = k >> 3, i = (k >> 1) & 3, d = k & 1;
+                    S.ct[pl][i * 3 + 1 + d] = v;
+                }
+            }
+        }
+        if (t + 1 < steps) prefetch(t + 1);
+        if (!ok) break;
+        wave_sync();
+        filter_mb(S, hl, act);
+
+        // ---- write back what is final: enumerate luma rows -3..15 x dwords 0..4 (95)
+        //      and chroma 2 x rows -3..7 x dwords 0..2 (66); 6 slots per lane.
+        if (act) {
+#pragma unroll
+            for (int it = 0; it < 6; ++it) {
+                const int e = hl + 32 * it;
+                if (e < 95) {
+                    const int row = e / 5 - 3, dw = e % 5;
+                    bool v;
+                    if (row < 0) v = r > 0 && dw >= 1;
+                    else v = (row <= 12 || last_row) && (dw == 0 ? x > 0 : (dw < 4 || x == W - 1));
+                    if (v)
+                        *reinterpret_cast<uint32_t*>(Y + (size_t)(Y0 + row) * g.W + X0 + 4 * (dw - 1)) =
+                            S.lt[(row + 4) * 5 + dw];
+                } else if (e < 161) {
+                    const int k = e - 95, pl = k / 33, k2 = k - pl * 33, row = k2 / 3 - 3, dw = k2 % 3;
+                    bool v;
+                    if (row < 0) v = r > 0 && dw >= 1;
+                    else v = (row <= 4 || last_row) && (dw == 0 ? x > 0 : (dw < 2 || x == W - 1));
+                    if (v)
+                        *reinterpret_cast<uint32_t*>(Cp[pl] + (size_t)(Yc + row) * g.Wc + Xc + 4 * (dw - 1)) =
+                            S.ct[pl][(row + 4) * 3 + dw];
+                }
+            }
+        }
+        // ---- bottom rows of MB x (cols 0..11) and MB x-1 (cols 12..15) into this half's ring
+        if (act && (feeds_ring || feeds_hb)) {
+            RingEntry* ring = L.ring[h];
+#pragma unroll
+            for (int it = 0; it < 2; ++it) {
+                const int e = hl + 32 * it;
+                if (e < 20) {                              // luma rows 12..15 x dwords 0..4
+                    const int i = e / 5, dw = e % 5;
+                    const uint32_t v = S.lt[(16 + i) * 5 + dw];
+                    if (dw == 0) { if (x > 0) ring[(x + DRING - 1) % DRING].y[i][3] = v; }
+                    else if (dw < 4) ring[x % DRING].y[i][dw - 1] = v;
+                    else if (x == W - 1) ring[x % DRING].y[i][3] = v;
+                } else if (e < 44) {                       // chroma rows 4..7 x dwords 0..2
+                    const int k = e - 20, pl = k / 12, k2 = k - pl * 12, i = k2 / 3, dw = k2 % 3;
+                    const uint32_t v = S.ct[pl][(8 + i) * 3 + dw];
+                    if (dw == 0) { if (x > 0) ring[(x + DRING - 1) % DRING].c[pl][i][1] = v; }
+                    else if (dw == 1) ring[x % DRING].c[pl][i][0] = v;
+                    else if (x == W - 1) ring[x % DRING].c[pl][i][1] = v;
+                }
+            }
+        }
+        wave_sync();
+        // ---- half B: completed records (MB x-1, and MB x at the row end) to the hand-off buffer
+        if (act && feeds_hb) {
+            if (x > 0)
+                st_cc(hb_out + (size_t)(x - 1) * 32 + hl,
+                      reinterpret_cast<const uint32_t*>(&L.ring[1][(x + DRING - 1) % DRING])[hl]);
+            if (x == W - 1)
+                st_cc(hb_out + (size_t)x * 32 + hl, reinterpret_cast<const uint32_t*>(&L.ring[1][x % DRING])[hl]);
+        }
+        // ---- carry the right 4 columns into the left strip of the next tile
+        if (act) {
+#pragma unroll
+            for (int it = 0; it < 2; ++it) {
+                const int e = hl + 32 * it;
+                if (e < 20) S.lt[e * 5] = S.lt[e * 5 + 4];
+                else if (e < 44) { const int k = e - 20, pl = k / 12, i = k - pl * 12; S.ct[pl][i * 3] = S.ct[pl][i * 3 + 2]; }
+            }
+        }
+        wave_sync();
+        // ---- progress of the pair: records complete = MBs of row B finished, minus the last
+        if (pair_feeds) {
+            const int xb = t - 2;                          // row B's MB of this step
+            if (xb >= 0) {
+                const int done = xb == W - 1 ? W : xb;
+                if (done % PUB == 0 || done == W) {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    if (lane == 0) st_cc(reinterpret_cast<uint32_t*>(prog_out), (uint32_t)done);
+                }
+            }
+        }
+    }
+    if (!ok && pair_feeds && lane == 0)                     // release the pair below (error is flagged)
+        st_cc(reinterpret_cast<uint32_t*>(prog_out), (uint32_t)W);
+}

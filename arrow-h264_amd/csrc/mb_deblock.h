@@ -142,21 +142,22 @@ DEV void db_info_mb(const h264r_batch& b, const Geom& g, int pic, int a, int lan
 
 constexpr int LP = 20;    // luma tile: rows -4..15 x cols -4..15, 5 dwords per row
 constexpr int CP = 12;    // chroma tile: rows -4..7 x cols -4..7, 3 dwords per row
-constexpr int RING = 8;   // bottom-row ring entries (MBs) handed to the row below
 
 // Bottom rows of one MB for the row below: luma rows 12..15 (4 x 4 dwords) and
-// chroma rows 4..7 (2 planes x 4 x 2 dwords).
+// chroma rows 4..7 (2 planes x 4 x 2 dwords) -- 128 bytes, one cache line.
 struct alignas(16) RingEntry {
     uint32_t y[4][4];
     uint32_t c[2][4][2];
 };
+static_assert(sizeof(RingEntry) == 128, "RingEntry is one 128-B line");
 
+// One MB row's working set in LDS: the MB being filtered plus its 4-sample
+// left/top margins, and its deblocking record.
 struct alignas(16) DbLds {
     uint32_t lt[20 * 5];          // luma tile, [row + 4][dword]
     uint32_t ct[2][12 * 3];       // chroma tiles
     uint8_t  bs[32];
     uint32_t tail[4];             // DbInfo bytes 32..47
-    RingEntry ring[RING];
 };
 
 DEV uint8_t* ltb(DbLds& S) { return reinterpret_cast<uint8_t*>(S.lt); }
@@ -198,15 +199,17 @@ DEV void filter_line_packed(uint32_t (&w)[NE + 1], const uint8_t* bsrow, int seg
 
 // The two filter passes of one MB on the LDS tiles: vertical edges with one lane per
 // sample row, then horizontal edges with one lane per column (filter_vertical /
-// filter_horizontal deblock.cc:488-535).  Lanes 0..15 luma, 16..31 chroma.
-DEV void filter_mb(DbLds& S, int lane)
+// filter_horizontal deblock.cc:488-535).  Lanes 0..15 luma, 16..31 chroma;
+// every lane of the wave calls (the passes are separated by wave_sync).
+DEV void filter_mb(DbLds& S, int lane, bool act)
 {
     const uint32_t t0 = S.tail[0], t1 = S.tail[1], t2 = S.tail[2];
     const int qpyQ = (int8_t)(t0 & 255), qpyL = (int8_t)((t0 >> 8) & 255), qpyU = (int8_t)((t0 >> 16) & 255);
     const int offa = (int8_t)((t2 >> 8) & 255), offb = (int8_t)((t2 >> 16) & 255);
 #pragma unroll 1
     for (int hor = 0; hor < 2; ++hor) {
-        if (lane < 16) {
+        if (!act) {
+        } else if (lane < 16) {
             uint32_t w[5];
             uint8_t* lt = ltb(S);
             if (!hor) {

@@ -45,8 +45,9 @@ DEV void residual_mb(const h264r_mb& m, const int16_t* __restrict__ lv, const h2
         if (!t8) {
             int b = lane >> 2, r = lane & 3, bx = b & 3, by = b >> 2;
             int b8 = (by >> 1) * 2 + (bx >> 1), b4 = (by & 1) * 2 + (bx & 1);
-            if (o.b8[b8] >= 0) {
-                const int16_t* p = lv + o.b8[b8] + b4 * 16 + r * 4;
+            const int off = b8_offset(m.cbp, b8);
+            if (off >= 0) {
+                const int16_t* p = lv + off + b4 * 16 + r * 4;
                 const int16_t* sc = &q->scale4x4[inter][0][rem][r * 4];
                 for (int c = 0; c < 4; ++c) {
                     int pos = r * 4 + c;
@@ -57,8 +58,9 @@ DEV void residual_mb(const h264r_mb& m, const int16_t* __restrict__ lv, const h2
             }
         } else {
             int k = lane >> 4, row = (lane >> 1) & 7, half = lane & 1;
-            if (o.b8[k] >= 0) {
-                const int16_t* p = lv + o.b8[k] + row * 8 + half * 4;
+            const int off = b8_offset(m.cbp, k);
+            if (off >= 0) {
+                const int16_t* p = lv + off + row * 8 + half * 4;
                 const int16_t* sc = &q->scale8x8[inter][0][rem][row * 8 + half * 4];
                 for (int c = 0; c < 4; ++c) {
                     int lev = p[c];
@@ -238,8 +240,7 @@ DEV void inter_mb(const h264r_batch& b, const Geom& g, int pic, int a, int lane,
             if (!img) { for (int c = 0; c < 4; ++c) v[l][c] = 128; continue; }
             int vx = (mbx * 4 + bx) * 16 + (int16_t)(mm & 0xFFFF);
             int vy = (mby * 4 + by) * 16 + (int16_t)(mm >> 16);
-            for (int c = 0; c < 4; ++c)
-                v[l][c] = luma_qpel(img, g.W, g.H, (vx >> 2) + c, (vy >> 2) + r, vx & 3, vy & 3);
+            luma_pred4(img, g.W, g.H, vx >> 2, (vy >> 2) + r, vx & 3, vy & 3, v[l]);
         }
         for (int c = 0; c < 4; ++c) predL[c] = wp_combine(sl, dir, r0, r1, v[0][c], v[1][c], 0);
     }
@@ -260,8 +261,7 @@ DEV void inter_mb(const h264r_batch& b, const Geom& g, int pic, int a, int lane,
             if (!img) { v[l][0] = v[l][1] = 128; continue; }
             int vx = (mbx * 4 + bx) * 16 + (int16_t)(mm & 0xFFFF);
             int vy = (mby * 4 + by) * 16 + (int16_t)(mm >> 16);
-            for (int c = 0; c < 2; ++c)
-                v[l][c] = chroma_epel(img, g.Wc, g.Hc, (vx >> 3) + c, (vy >> 3) + r, vx & 7, vy & 7);
+            chroma_pred2(img, g.Wc, g.Hc, vx >> 3, (vy >> 3) + r, vx & 7, vy & 7, v[l]);
         }
         for (int c = 0; c < 2; ++c) predC[c] = wp_combine(sl, dir, r0, r1, v[0][c], v[1][c], 1 + pl);
     }

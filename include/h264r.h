@@ -150,7 +150,10 @@ typedef struct h264r_pic {
  * Per-picture strides: MBs W*H records; motion 2*(4H)*(4W) entries; slices
  * `slice_stride` entries; planes (16W)*(16H) bytes (Y) and (8W)*(8H) (Cb, Cr).
  * `ref_planes` is a device array of 3*H264R_MAX_SLOTS device pointers
- * (Y,Cb,Cr per DPB slot) to full-size planes. */
+ * (Y,Cb,Cr per DPB slot) to full-size planes; MC reads whole dwords, so each
+ * plane must be followed by H264R_PLANE_SLACK readable bytes (the slots of
+ * h264r_set_ref / h264r_ref_planes are). */
+#define H264R_PLANE_SLACK 64
 typedef struct h264r_batch {
     int32_t             num_pics;
     int32_t             width_mbs;
