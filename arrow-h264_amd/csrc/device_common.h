@@ -130,36 +130,6 @@ DEV int pxl(const uint8_t* __restrict__ img, int W, int H, int x, int y)
 }
 DEV int tap6(int a, int b, int c, int d, int e, int f) { return a - 5 * b + 20 * c + 20 * d - 5 * e + f; }
 
-// One luma quarter-pel sample, get_block_luma (inter_prediction.cc:158-340) in spec form.
-DEV int luma_qpel(const uint8_t* __restrict__ img, int W, int H, int x, int y, int xf, int yf)
-{
-#define S(dx, dy) pxl(img, W, H, x + (dx), y + (dy))
-#define B1(dy) tap6(S(-2, dy), S(-1, dy), S(0, dy), S(1, dy), S(2, dy), S(3, dy))
-#define H1(dx) tap6(S(dx, -2), S(dx, -1), S(dx, 0), S(dx, 1), S(dx, 2), S(dx, 3))
-    if (xf == 0 && yf == 0) return S(0, 0);
-    if (yf == 0) {
-        int b = clip255((B1(0) + 16) >> 5);
-        return xf == 2 ? b : (S(xf == 1 ? 0 : 1, 0) + b + 1) >> 1;
-    }
-    if (xf == 0) {
-        int h = clip255((H1(0) + 16) >> 5);
-        return yf == 2 ? h : (S(0, yf == 1 ? 0 : 1) + h + 1) >> 1;
-    }
-    if ((xf & 1) && (yf & 1)) {
-        int bb = clip255((B1(yf == 3 ? 1 : 0) + 16) >> 5);
-        int hh = clip255((H1(xf == 3 ? 1 : 0) + 16) >> 5);
-        return (bb + hh + 1) >> 1;
-    }
-    int j1 = tap6(B1(-2), B1(-1), B1(0), B1(1), B1(2), B1(3));
-    int j = clip255((j1 + 512) >> 10);
-    if (xf == 2 && yf == 2) return j;
-    if (xf == 2) return (j + clip255((B1(yf == 3 ? 1 : 0) + 16) >> 5) + 1) >> 1;
-    return (j + clip255((H1(xf == 3 ? 1 : 0) + 16) >> 5) + 1) >> 1;
-#undef S
-#undef B1
-#undef H1
-}
-
 // ------------------------------------------------------------ row-window MC
 // The per-sample forms above fetch one byte per tap.  The MC path proper loads
 // each reference row as three aligned dwords and extracts the samples it needs;
@@ -200,9 +170,13 @@ DEV const uint32_t* row_dwords(const uint8_t* __restrict__ img, int W, int H, in
 // get_block_luma (inter_prediction.cc:158-340) in spec form (8.4.2.2.1): the
 // half-sample values b (horizontal), h (vertical), j (centre) and their
 // averages.  The 6 rows y-2..y+3 are streamed; each tap row is loaded once.
-DEV void luma_pred4(const uint8_t* __restrict__ img, int W, int H, int x, int y, int xf, int yf, int (&out)[4])
+// XF/YF >= 0 fix the phase at compile time (wave-uniform MV phase: only that
+// case's arithmetic is emitted); -1 takes it from xf_rt/yf_rt per lane.
+template <int XF = -1, int YF = -1>
+DEV void luma_pred4(const uint8_t* __restrict__ img, int W, int H, int x, int y, int xf_rt, int yf_rt, int (&out)[4])
 {
     constexpr int C6[6] = {1, -5, 20, 20, -5, 1};
+    const int xf = XF >= 0 ? XF : xf_rt, yf = YF >= 0 ? YF : yf_rt;
     if (yf == 0) {                                    // G, a, b, c: one row
         const uint32_t* q = row_dwords(img, W, H, x, y);
         int p[9];
@@ -282,14 +256,6 @@ DEV void chroma_pred2(const uint8_t* __restrict__ img, int W, int H, int xi, int
     for (int c = 0; c < 2; ++c)
         out[c] = ((8 - xf) * (8 - yf) * p[0][c] + xf * (8 - yf) * p[0][c + 1] + (8 - xf) * yf * p[1][c] +
                   xf * yf * p[1][c + 1] + 32) >> 6;
-}
-
-// get_block_chroma sample (inter_prediction.cc:380-404).
-DEV int chroma_epel(const uint8_t* __restrict__ img, int W, int H, int xi, int yi, int xf, int yf)
-{
-    int A = pxl(img, W, H, xi, yi), B = pxl(img, W, H, xi + 1, yi);
-    int C = pxl(img, W, H, xi, yi + 1), D = pxl(img, W, H, xi + 1, yi + 1);
-    return ((8 - xf) * (8 - yf) * A + xf * (8 - yf) * B + (8 - xf) * yf * C + xf * yf * D + 32) >> 6;
 }
 
 DEV int rshift_rnd(int x, int a) { return a > 0 ? (x + (1 << (a - 1))) >> a : x; }  // inter_prediction.cc:35-38

@@ -21,7 +21,8 @@
 #include "h264r.h"
 
 namespace h264r { struct DbInfo; struct RingEntry; }
-extern "C" __global__ void k_inter(h264r_batch b, h264r::DbInfo* dbinfo);
+extern "C" __global__ void k_prep(h264r_batch b, uint2* mot);
+extern "C" __global__ void k_inter(h264r_batch b, const uint2* mot, h264r::DbInfo* dbinfo);
 extern "C" __global__ void k_intra_pic(h264r_batch b, int* sync, int* err);
 extern "C" __global__ void k_deblock(h264r_batch b, const h264r::DbInfo* dbinfo, h264r::RingEntry* hb,
                                      int* sync, int* err);
@@ -107,6 +108,7 @@ struct h264r_ctx {
     uint8_t* d_dbinfo = nullptr; size_t c_dbinfo = 0;
     int* d_sync = nullptr; size_t c_sync = 0;
     uint8_t* d_hb = nullptr; size_t c_hb = 0;
+    uint2* d_mot = nullptr; size_t c_mot = 0;
     // timing
     bool timing = false;
     int debug = 0;
@@ -208,7 +210,7 @@ int h264r_destroy(h264r_ctx* c)
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (int s = 0; s < H264R_MAX_SLOTS; ++s) if (c->slot[s][0]) (void)hipFree(c->slot[s][0]);
-    void* bufs[] = {c->d_ref_planes, c->d_err, c->d_dbinfo, c->d_sync, c->d_hb, c->d_mbs, c->d_levels, c->d_mv, c->d_ref, c->d_slices, c->d_pic, c->d_quant, c->d_out};
+    void* bufs[] = {c->d_ref_planes, c->d_err, c->d_dbinfo, c->d_sync, c->d_hb, c->d_mot, c->d_mbs, c->d_levels, c->d_mv, c->d_ref, c->d_slices, c->d_pic, c->d_quant, c->d_out};
     for (void* b : bufs) if (b) (void)hipFree(b);
     for (int i = 0; i < 4; ++i) if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -263,11 +265,15 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s)
     int st;
     if ((st = dev_resize(&c->d_dbinfo, &c->c_dbinfo, (size_t)P * W * H * DBINFO_BYTES))) return st;
     if ((st = dev_resize(&c->d_hb, &c->c_hb, (size_t)P * npairs * W * HANDOFF_BYTES))) return st;
+    const size_t mplane = (size_t)W * 4 * H * 4;
+    if ((st = dev_resize(&c->d_mot, &c->c_mot, (size_t)P * 2 * mplane))) return st;
     if ((st = dev_resize(&c->d_sync, &c->c_sync, 2 * sync_ints + 4))) return st;
     HIP_OK(hipMemsetAsync(c->d_sync, 0, (2 * sync_ints + 4) * sizeof(int), s));
     auto* dbinfo = reinterpret_cast<h264r::DbInfo*>(c->d_dbinfo);
     if (c->timing) HIP_OK(hipEventRecord(c->ev[0], s));
-    hipLaunchKernelGGL(k_inter, dim3(W * H, P), dim3(64), 0, s, b, dbinfo);
+    hipLaunchKernelGGL(k_prep, dim3((unsigned)((mplane + 255) / 256), P), dim3(256), 0, s, b, c->d_mot);
+    HIP_OK(hipGetLastError());
+    hipLaunchKernelGGL(k_inter, dim3(W * H, P), dim3(64), 0, s, b, c->d_mot, dbinfo);
     HIP_OK(hipGetLastError());
     if (c->timing) HIP_OK(hipEventRecord(c->ev[1], s));
     hipLaunchKernelGGL(k_intra_pic, dim3(P * nbands), dim3(1024), 0, s, b, c->d_sync, c->d_err);

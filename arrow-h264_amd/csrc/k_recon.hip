@@ -1,19 +1,46 @@
-// k_recon.hip -- k_inter: every MB of a batch, fully parallel, one 64-lane
-// workgroup (= one wave) per MB:
-//   - the per-MB deblocking record (boundary strengths + QPs, mb_deblock.h db_info_mb)
-//     for EVERY MB, so the order-dependent walk of k_deblock_pic loads 48 B per MB;
-//   - inter MBs and I_PCM reconstructed (mb_recon.h inter_mb / pcm_mb);
+// k_recon.hip -- the fully parallel part of a batch.
+//
+// k_prep   one lane per 4x4 block: resolves ref_idx to the DPB slot of
+//          RefPicList[l][ref_idx] (get_ref_pic dpb.cc:1046-1054 via the MB's
+//          slice) and packs {mv, ref_idx | slot << 8} per list, so the per-MB
+//          kernels never chase record -> slice -> slot -> plane.
+// k_inter  one 64-lane workgroup (= one wave) per MB:
+//   - the per-MB deblocking record (boundary strengths + QPs, mb_deblock.h
+//     db_info_mb) for EVERY MB, so the order-dependent walk of k_deblock loads
+//     48 B per MB;
+//   - inter MBs and I_PCM reconstructed (mb_inter.h inter_mb2);
 //   - intra MBs are left to k_intra_pic (they depend on their neighbours).
-#include "mb_recon.h"
+#include "mb_inter.h"
 #include "mb_deblock.h"
 
 using namespace h264r;
 
-extern "C" __global__ __launch_bounds__(64) void k_inter(h264r_batch b, DbInfo* dbinfo)
+extern "C" __global__ __launch_bounds__(256) void k_prep(h264r_batch b, uint2* __restrict__ mot)
+{
+    const Geom g = make_geom(b.width_mbs, b.height_mbs);
+    const int idx = blockIdx.x * 256 + threadIdx.x, pic = blockIdx.y;
+    if (idx >= g.motion_plane) return;
+    const int bx4 = idx % g.W4, by4 = idx / g.W4;
+    const h264r_mb* mb = &b.mbs[(size_t)pic * g.nmb + (by4 >> 2) * g.wmb + (bx4 >> 2)];
+    const h264r_slice* sl = &b.slices[(size_t)pic * b.slice_stride + mb->slice];
+    const size_t base = (size_t)pic * 2 * g.motion_plane;
+#pragma unroll
+    for (int l = 0; l < 2; ++l) {
+        const int ri = b.ref_idx[base + (size_t)l * g.motion_plane + idx];
+        const uint32_t mv = b.mv[base + (size_t)l * g.motion_plane + idx];
+        const int slot = ri >= 0 && ri < H264R_MAX_REFS ? sl->ref_slot[l][ri] : -1;
+        mot[base + (size_t)l * g.motion_plane + idx] = make_uint2(mv, (uint32_t)(uint8_t)ri | ((uint32_t)(uint8_t)slot << 8));
+    }
+}
+
+extern "C" __global__ __launch_bounds__(64) void k_inter(h264r_batch b, const uint2* __restrict__ mot, DbInfo* dbinfo)
 {
     __shared__ ResLds R;
     const Geom g = make_geom(b.width_mbs, b.height_mbs);
     const int pic = blockIdx.y, a = blockIdx.x, lane = threadIdx.x;
-    db_info_mb(b, g, pic, a, lane, dbinfo + (size_t)pic * g.nmb + a);
-    inter_mb(b, g, pic, a, lane, R);
+    const uint2* pm = mot + (size_t)pic * 2 * g.motion_plane;
+#ifndef H264R_EXP_NODBINFO
+    db_info_mb(b, g, pic, a, lane, pm, dbinfo + (size_t)pic * g.nmb + a);
+#endif
+    inter_mb2(b, g, pic, a, lane, pm, R);
 }

@@ -20,22 +20,19 @@ struct MotionRef {
     int mvx[2], mvy[2];
 };
 
-// pic_motion_params of a 4x4 block: ref_pic identity = DPB slot via the slice ref list
-// (interpret_mb.cc:611-623), or -1 when the list is unused.
-DEV MotionRef motion_at(const h264r_batch& b, const Geom& g, int pic, const h264r_mb* mbs,
-                        const h264r_slice* slices, int bx4, int by4)
+// Per-4x4-block motion as resolved by k_prep: {mv, ref_idx | slot << 8} per list.
+// ref identity = DPB slot of RefPicList[l][ref_idx] (pic_motion_params::ref_pic,
+// interpret_mb.cc:611-623), -1 when the list is unused.
+DEV MotionRef motion_of(uint2 w0, uint2 w1)
 {
     MotionRef r;
-    const size_t base = (size_t)pic * 2 * g.motion_plane;
-    const int idx = by4 * g.W4 + bx4;
-    const h264r_mb* mb = &mbs[(by4 >> 2) * g.wmb + (bx4 >> 2)];
-    const h264r_slice* sl = &slices[mb->slice];
+    const uint2 w[2] = {w0, w1};
+#pragma unroll
     for (int l = 0; l < 2; ++l) {
-        int ri = b.ref_idx[base + (size_t)l * g.motion_plane + idx];
-        uint32_t v = b.mv[base + (size_t)l * g.motion_plane + idx];
-        r.ref[l] = ri >= 0 ? sl->ref_slot[l][ri] : -1;
-        r.mvx[l] = (int16_t)(v & 0xFFFF);
-        r.mvy[l] = (int16_t)(v >> 16);
+        const int ri = (int8_t)(w[l].y & 255), slot = (int8_t)((w[l].y >> 8) & 255);
+        r.ref[l] = ri >= 0 ? slot : -1;
+        r.mvx[l] = (int16_t)(w[l].x & 0xFFFF);
+        r.mvy[l] = (int16_t)(w[l].x >> 16);
     }
     return r;
 }
@@ -75,23 +72,30 @@ struct DbInfo {
 static_assert(sizeof(DbInfo) == 48, "DbInfo layout");
 
 // Deblock::strength + strength_vertical/horizontal for MB `a` (deblock.cc:78-289).
-// All lanes call; lanes 0..31 compute one strength each, lane 32 the tail.
-DEV void db_info_mb(const h264r_batch& b, const Geom& g, int pic, int a, int lane, DbInfo* __restrict__ out)
+// All lanes call; lanes 0..31 compute one strength each, lane 32 the tail.  `mot`
+// is the picture's resolved motion (k_prep), [list][H4][W4]; every load is issued
+// before the first decision so the record and motion latencies overlap.
+DEV void db_info_mb(const h264r_batch& b, const Geom& g, int pic, int a, int lane, const uint2* __restrict__ mot,
+                    DbInfo* __restrict__ out)
 {
     const int mbx = a % g.wmb, mby = a / g.wmb;
     const h264r_mb* mbs = b.mbs + (size_t)pic * g.nmb;
     const h264r_slice* slices = b.slices + (size_t)pic * b.slice_stride;
+    const int hor = (lane >> 4) & 1, e = (lane >> 2) & 3, s = lane & 3;
+    const int qx = mbx * 4 + (hor ? s : e), qy = mby * 4 + (hor ? e : s);
+    const int px = max(qx - (hor ? 0 : 1), 0), py = max(qy - (hor ? 1 : 0), 0);
+    const uint2 q0 = mot[qy * g.W4 + qx], q1 = mot[g.motion_plane + qy * g.W4 + qx];
+    const uint2 p0 = mot[py * g.W4 + px], p1 = mot[g.motion_plane + py * g.W4 + px];
     const h264r_mb q = load_mb(&mbs[a]);
+    const int hasL = mbx > 0, hasU = mby > 0;
+    const h264r_mb L = load_mb(&mbs[hasL ? a - 1 : a]);
+    const h264r_mb U = load_mb(&mbs[hasU ? a - g.wmb : a]);
     const h264r_slice* qs = &slices[q.slice];
     const int idc = qs->deblock_idc;
-    const int hasL = mbx > 0, hasU = mby > 0;
-    const h264r_mb L = hasL ? load_mb(&mbs[a - 1]) : q;
-    const h264r_mb U = hasU ? load_mb(&mbs[a - g.wmb]) : q;
     const int fl = idc == 0 ? hasL : (idc == 2 && hasL && L.slice == q.slice);
     const int ft = idc == 0 ? hasU : (idc == 2 && hasU && U.slice == q.slice);
     const int t8 = (q.flags & H264R_MBF_T8x8) != 0;
     if (lane < 32) {
-        const int hor = lane >> 4, e = (lane >> 2) & 3, s = lane & 3;
         const int en = idc != 1 && (e == 0 ? (hor ? ft : fl) : ((e & 1) ? !t8 : 1));
         int v = 0;
         if (en) {
@@ -99,31 +103,26 @@ DEV void db_info_mb(const h264r_batch& b, const Geom& g, int pic, int a, int lan
             const int special = special_slice(slices[P.slice].slice_type) || special_slice(qs->slice_type);
             const int intra = mb_is_intra(q) || mb_is_intra(P);
             const int pskip = qs->slice_type == H264R_SLICE_P && q.mb_type == H264R_P_SKIP;
+            const int blkQ = hor ? 4 * e + s : 4 * s + e;
+            const int blkP = hor ? (e == 0 ? 12 : 4 * (e - 1)) + s : 4 * s + (e == 0 ? 3 : e - 1);
+            const int coded = ((q.cbp_blks >> blkQ) & 1) || ((P.cbp_blks >> blkP) & 1);
+            const int same_part = e > 0 && (q.mb_type == H264R_P_16x16 ||
+                                            q.mb_type == (hor ? H264R_P_8x16 : H264R_P_16x8));
             if (!hor) {
-                int blkQ = 4 * s + e, blkP = 4 * s + (e == 0 ? 3 : e - 1);
                 if (special) v = e == 0 ? 4 : 3;
                 else if (e > 0 && pskip) v = 0;
                 else if (e == 0 && intra) v = 4;
                 else if (intra) v = 3;
-                else if (((q.cbp_blks >> blkQ) & 1) || ((P.cbp_blks >> blkP) & 1)) v = 2;
-                else if (e > 0 && (q.mb_type == H264R_P_16x16 || q.mb_type == H264R_P_16x8)) v = 0;
-                else {
-                    MotionRef mq = motion_at(b, g, pic, mbs, slices, mbx * 4 + e, mby * 4 + s);
-                    MotionRef mp = motion_at(b, g, pic, mbs, slices, mbx * 4 + e - 1, mby * 4 + s);
-                    v = bs_compare(mq, mp);
-                }
+                else if (coded) v = 2;
+                else if (same_part) v = 0;
+                else v = bs_compare(motion_of(q0, q1), motion_of(p0, p1));
             } else {
-                int blkQ = 4 * e + s, blkP = (e == 0 ? 12 : 4 * (e - 1)) + s;
                 if (e == 0 && (special || intra)) v = 4;
                 else if (special || intra) v = 3;
                 else if (e > 0 && pskip) v = 0;
-                else if (((q.cbp_blks >> blkQ) & 1) || ((P.cbp_blks >> blkP) & 1)) v = 2;
-                else if (e > 0 && (q.mb_type == H264R_P_16x16 || q.mb_type == H264R_P_8x16)) v = 0;
-                else {
-                    MotionRef mq = motion_at(b, g, pic, mbs, slices, mbx * 4 + s, mby * 4 + e);
-                    MotionRef mp = motion_at(b, g, pic, mbs, slices, mbx * 4 + s, mby * 4 + e - 1);
-                    v = bs_compare(mq, mp);
-                }
+                else if (coded) v = 2;
+                else if (same_part) v = 0;
+                else v = bs_compare(motion_of(q0, q1), motion_of(p0, p1));
             }
         }
         out->bs[lane] = (uint8_t)v;

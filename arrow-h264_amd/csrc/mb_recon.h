@@ -4,8 +4,7 @@
 //
 //   residual_mb : dequant transform.cc:394-456, DC transforms :825-910,
 //                 inverse_4x4 :597-641, inverse_8x8 :643-733
-//   inter_mb    : Decoder::mb_pred_inter decoder.cc:217-262, InterPrediction
-//                 inter_prediction.cc:53-536, inverse_transform_inter transform.cc:1051-1095
+//   (inter MBs: mb_inter.h)
 //   intra_mb    : Decoder::mb_pred_intra decoder.cc:170-208, IntraPrediction
 //                 intra_prediction.cc:42-904, inverse_transform_{4x4,8x8,16x16,chroma}
 //                 transform.cc:986-1049
@@ -207,89 +206,6 @@ DEV void pcm_mb(const h264r_mb& m, const int16_t* __restrict__ lv, const Geom& g
         *reinterpret_cast<uint16_t*>(dst + (size_t)(mby * 8 + y) * g.Wc + mbx * 8 + x) = v;
     }
 }
-
-// Inter MB (or I_PCM) `a` of picture `pic`; one wave, R is that wave's LDS scratch.
-DEV void inter_mb(const h264r_batch& b, const Geom& g, int pic, int a, int lane, ResLds& R)
-{
-    const h264r_mb m = load_mb(&b.mbs[(size_t)pic * g.nmb + a]);
-    const int mbx = a % g.wmb, mby = a / g.wmb;
-    const PicPtrs o = out_planes(b, g, pic);
-    const int16_t* lv = b.levels + m.coef_off;
-
-    if (m.mb_type == H264R_I_PCM) { pcm_mb(m, lv, g, o, mbx, mby, lane); return; }
-    if (mb_is_intra(m)) return;
-
-    const h264r_slice* __restrict__ sl = &b.slices[(size_t)pic * b.slice_stride + m.slice];
-    const uint32_t* mvp = b.mv + (size_t)pic * 2 * g.motion_plane;
-    const int8_t* rip = b.ref_idx + (size_t)pic * 2 * g.motion_plane;
-
-    // ---- luma prediction: lane = (4x4 block b, row r), 4 samples
-    int predL[4];
-    {
-        int bi = lane >> 2, r = lane & 3, bx = bi & 3, by = bi >> 2;
-        int idx = (mby * 4 + by) * g.W4 + mbx * 4 + bx;
-        int r0 = rip[idx], r1 = rip[g.motion_plane + idx];
-        uint32_t m0 = mvp[idx], m1 = mvp[g.motion_plane + idx];
-        int dir = (r0 >= 0 && r1 >= 0) ? 2 : (r0 >= 0 ? 0 : 1);
-        int v[2][4];
-        for (int l = 0; l < 2; ++l) {
-            int rr = l ? r1 : r0;
-            if (rr < 0) continue;
-            uint32_t mm = l ? m1 : m0;
-            const uint8_t* img = ref_plane(b, sl, l, rr, 0);
-            if (!img) { for (int c = 0; c < 4; ++c) v[l][c] = 128; continue; }
-            int vx = (mbx * 4 + bx) * 16 + (int16_t)(mm & 0xFFFF);
-            int vy = (mby * 4 + by) * 16 + (int16_t)(mm >> 16);
-            luma_pred4(img, g.W, g.H, vx >> 2, (vy >> 2) + r, vx & 3, vy & 3, v[l]);
-        }
-        for (int c = 0; c < 4; ++c) predL[c] = wp_combine(sl, dir, r0, r1, v[0][c], v[1][c], 0);
-    }
-    // ---- chroma prediction: lane = (plane, 2x2 block, row), 2 samples
-    int predC[2];
-    {
-        int pl = lane >> 5, bi = (lane >> 1) & 15, r = lane & 1, bx = bi & 3, by = bi >> 2;
-        int idx = (mby * 4 + by) * g.W4 + mbx * 4 + bx;
-        int r0 = rip[idx], r1 = rip[g.motion_plane + idx];
-        uint32_t m0 = mvp[idx], m1 = mvp[g.motion_plane + idx];
-        int dir = (r0 >= 0 && r1 >= 0) ? 2 : (r0 >= 0 ? 0 : 1);
-        int v[2][2];
-        for (int l = 0; l < 2; ++l) {
-            int rr = l ? r1 : r0;
-            if (rr < 0) continue;
-            uint32_t mm = l ? m1 : m0;
-            const uint8_t* img = ref_plane(b, sl, l, rr, 1 + pl);
-            if (!img) { v[l][0] = v[l][1] = 128; continue; }
-            int vx = (mbx * 4 + bx) * 16 + (int16_t)(mm & 0xFFFF);
-            int vy = (mby * 4 + by) * 16 + (int16_t)(mm >> 16);
-            chroma_pred2(img, g.Wc, g.Hc, vx >> 3, (vy >> 3) + r, vx & 7, vy & 7, v[l]);
-        }
-        for (int c = 0; c < 2; ++c) predC[c] = wp_combine(sl, dir, r0, r1, v[0][c], v[1][c], 1 + pl);
-    }
-
-    // ---- residual + construction
-    const int cbpl = m.cbp & 15, cbpc = m.cbp >> 4;
-    if (cbpl | cbpc) residual_mb(m, lv, &b.quant[pic], R, lane);
-    {
-        int bi = lane >> 2, r = lane & 3, bx = bi & 3, by = bi >> 2;
-        uint32_t w = 0;
-        for (int c = 0; c < 4; ++c) {
-            int v = cbpl ? clip255(predL[c] + R.lum[by * 4 + r][bx * 4 + c]) : predL[c];
-            w |= (uint32_t)v << (8 * c);
-        }
-        *reinterpret_cast<uint32_t*>(o.y + (size_t)(mby * 16 + by * 4 + r) * g.W + mbx * 16 + bx * 4) = w;
-    }
-    {
-        int pl = lane >> 5, bi = (lane >> 1) & 15, r = lane & 1, bx = bi & 3, by = bi >> 2;
-        uint32_t w = 0;
-        for (int c = 0; c < 2; ++c) {
-            int v = cbpc ? clip255(predC[c] + R.chr[pl][by * 2 + r][bx * 2 + c]) : predC[c];
-            w |= (uint32_t)v << (8 * c);
-        }
-        uint8_t* dst = pl ? o.v : o.u;
-        *reinterpret_cast<uint16_t*>(dst + (size_t)(mby * 8 + by * 2 + r) * g.Wc + mbx * 8 + bx * 2) = (uint16_t)w;
-    }
-}
-
 
 // MB-level neighbour availability (get_neighbour + slice check + constrained intra,
 // intra_prediction.cc:142-168 / 629-651 / 753-777).  Neighbours on earlier diagonals

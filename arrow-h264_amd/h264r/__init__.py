@@ -24,7 +24,7 @@ from . import _abi as A
 from ._abi import MB_DTYPE, PIC_DTYPE, QUANT_DTYPE, SLICE_DTYPE  # noqa: F401
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libh264r.so")
+LIB_PATH = os.environ.get("H264R_LIB") or os.path.join(PKG_DIR, "lib", "libh264r.so")
 
 
 class H264RError(RuntimeError):
