@@ -14,20 +14,21 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <vector>
 
 #include "h264r.h"
 
-namespace h264r { struct DbInfo; struct RingEntry; }
+namespace h264r { struct DbInfo; }
 extern "C" __global__ void k_prep(h264r_batch b, uint2* mot);
 extern "C" __global__ void k_inter(h264r_batch b, const uint2* mot, h264r::DbInfo* dbinfo);
 extern "C" __global__ void k_intra_pic(h264r_batch b, int* sync, int* err);
-extern "C" __global__ void k_deblock(h264r_batch b, const h264r::DbInfo* dbinfo, h264r::RingEntry* hb,
-                                     int* sync, int* err);
-constexpr size_t DBINFO_BYTES = 48;
-constexpr size_t HANDOFF_BYTES = 128;   // one RingEntry per MB
+extern "C" __global__ void k_deblock(h264r_batch b, const h264r::DbInfo* dbinfo, uint64_t* hb,
+                                     int* sync, int* err, uint32_t epoch);
+constexpr size_t DBINFO_BYTES = 80;
+constexpr size_t HANDOFF_BYTES = 256;   // one tagged record (32 x {dword, epoch}) per MB
 
 namespace {
 
@@ -108,6 +109,7 @@ struct h264r_ctx {
     uint8_t* d_dbinfo = nullptr; size_t c_dbinfo = 0;
     int* d_sync = nullptr; size_t c_sync = 0;
     uint8_t* d_hb = nullptr; size_t c_hb = 0;
+    uint32_t epoch = 0;             // tag of the deblocking hand-off records of the last launch
     uint2* d_mot = nullptr; size_t c_mot = 0;
     // timing
     bool timing = false;
@@ -264,7 +266,18 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s)
     const size_t sync_ints = 1 + (size_t)P * H;
     int st;
     if ((st = dev_resize(&c->d_dbinfo, &c->c_dbinfo, (size_t)P * W * H * DBINFO_BYTES))) return st;
-    if ((st = dev_resize(&c->d_hb, &c->c_hb, (size_t)P * npairs * W * HANDOFF_BYTES))) return st;
+    {
+        const size_t cap_before = c->c_hb;
+        if ((st = dev_resize(&c->d_hb, &c->c_hb, (size_t)P * npairs * W * HANDOFF_BYTES))) return st;
+        if (c->c_hb != cap_before) {              // fresh memory: no record may carry a live epoch
+            HIP_OK(hipMemsetAsync(c->d_hb, 0, c->c_hb, s));
+            c->epoch = 0;
+        }
+        if (++c->epoch == 0) {                    // 2^32 launches: wrap without reusing an epoch
+            HIP_OK(hipMemsetAsync(c->d_hb, 0, c->c_hb, s));
+            c->epoch = 1;
+        }
+    }
     const size_t mplane = (size_t)W * 4 * H * 4;
     if ((st = dev_resize(&c->d_mot, &c->c_mot, (size_t)P * 2 * mplane))) return st;
     if ((st = dev_resize(&c->d_sync, &c->c_sync, 2 * sync_ints + 4))) return st;
@@ -281,11 +294,24 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s)
     if (c->timing) HIP_OK(hipEventRecord(c->ev[2], s));
     if (!(c->debug & H264R_DBG_NO_DEBLOCK))
         hipLaunchKernelGGL(k_deblock, dim3(P * npairs), dim3(64), 0, s, b, dbinfo,
-                           reinterpret_cast<h264r::RingEntry*>(c->d_hb), c->d_sync + sync_ints, c->d_err);
+                           reinterpret_cast<uint64_t*>(c->d_hb), c->d_sync + sync_ints, c->d_err, c->epoch);
     HIP_OK(hipGetLastError());
     if (c->timing) HIP_OK(hipEventRecord(c->ev[3], s));
     return H264R_OK;
 }
+
+#ifdef H264R_TRACE
+extern __device__ unsigned long long h264r_db_trace[1 << 16][8];
+static void dump_trace(hipStream_t s)
+{
+    const char* path = getenv("H264R_TRACE_OUT");
+    if (!path) return;
+    static std::vector<unsigned long long> buf((1 << 16) * 8);
+    (void)hipStreamSynchronize(s);
+    (void)hipMemcpyFromSymbol(buf.data(), HIP_SYMBOL(h264r_db_trace), buf.size() * 8);
+    if (FILE* f = fopen(path, "wb")) { fwrite(buf.data(), 8, buf.size(), f); fclose(f); }
+}
+#endif
 
 int h264r_decode_batch(h264r_ctx* c, const h264r_batch* b, void* stream)
 {
@@ -297,7 +323,13 @@ int h264r_decode_batch(h264r_ctx* c, const h264r_batch* b, void* stream)
     h264r_batch bb = *b;
     if (!bb.ref_planes) bb.ref_planes = c->d_ref_planes;
     hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : c->stream;
+#ifdef H264R_TRACE
+    int st = launch_all(c, bb, s);
+    dump_trace(s);
+    return st;
+#else
     return launch_all(c, bb, s);
+#endif
 }
 
 int h264r_set_timing(h264r_ctx* c, int enable)

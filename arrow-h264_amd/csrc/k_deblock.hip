@@ -12,11 +12,12 @@
 // and all 64 lanes are busy (per half: lanes 0..15 luma lines, 16..31 chroma
 // lines).  Inside the pair, half A hands its bottom rows to half B through an
 // LDS ring; between pairs, half B publishes each MB's final-for-it bottom rows
-// as one 128-byte record (one cache line, stored write-through with `sc1`)
-// into a hand-off buffer and bumps a progress counter after `s_waitcnt
-// vmcnt(0)`; the pair below polls the counter and reads the records with
-// `sc1` loads (MI355X_MICROARCH.md, inter-workgroup hand-off with sc1 stores
-// and loads).  Pairs are taken as tickets from an atomic counter in
+// as one self-validating record: 32 naturally aligned 8-byte granules {data
+// dword, launch epoch}, written by one write-through (`sc1`) store instruction.
+// The pair below reads the record with `sc1` loads and re-polls until every
+// granule carries this launch's epoch (MI355X_MICROARCH.md, R2 granule
+// hand-off): no progress counter, no `s_waitcnt vmcnt(0)` on the producer's
+// path.  Pairs are taken as tickets from an atomic counter in
 // pair-major order, so a wave only ever waits on a ticket taken earlier by a
 // running wave: no deadlock under any dispatch order or residency; every spin
 // is bounded and flags the error word.
@@ -31,7 +32,6 @@ using namespace h264r;
 
 namespace {
 
-constexpr int PUB = 2;                      // progress publish granularity (MBs)
 constexpr int DRING = 4;                    // row A -> row B ring depth (lag is 2)
 constexpr unsigned SPIN_LIMIT = 1u << 22;   // ~0.3 s of polling, then flag an error
 
@@ -44,17 +44,30 @@ DEV uint32_t ld_cc(const uint32_t* p)       // coherent (L1-bypassing, sc1) load
 {
     return __hip_atomic_load(const_cast<uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-DEV void st_cc(uint32_t* p, uint32_t v)     // write-through (sc1) store
+DEV uint64_t ld_cc64(const uint64_t* p)     // coherent (L1-bypassing, sc1) 8-byte load
+{
+    return __hip_atomic_load(const_cast<uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+DEV void st_cc64(uint64_t* p, uint64_t v)   // write-through (sc1) 8-byte store
 {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 }  // namespace
 
-// hb: hand-off records [pic][pair][W] (RingEntry); sync[0] ticket counter,
-// sync[1 + pic * npairs + pair] = number of complete records of that pair.
+#ifdef H264R_TRACE
+// Experimental timing trace (exp/ builds only): per ticket {start, first step,
+// end, cycles spent polling} in s_memrealtime ticks (100 MHz).
+__device__ unsigned long long h264r_db_trace[1 << 16][8];
+#define TRACE(...) __VA_ARGS__
+#else
+#define TRACE(...)
+#endif
+
+// hb: hand-off records [pic][pair][W][32] granules {RingEntry dword, epoch};
+// sync[0]: ticket counter; epoch: this launch's tag (never 0: hb is zeroed when allocated).
 extern "C" __global__ __launch_bounds__(64) void k_deblock(h264r_batch b, const DbInfo* __restrict__ dbinfo,
-                                                          RingEntry* hb, int* sync, int* err)
+                                                          uint64_t* hb, int* sync, int* err, uint32_t epoch)
 {
     __shared__ PairLds L;
     const int lane = threadIdx.x, h = lane >> 5, hl = lane & 31;
@@ -64,6 +77,7 @@ extern "C" __global__ __launch_bounds__(64) void k_deblock(h264r_batch b, const 
     int tk = 0;
     if (lane == 0) tk = atomicAdd(&sync[0], 1);
     const int ticket = __builtin_amdgcn_readfirstlane(tk);
+    TRACE(unsigned long long tr_start = __builtin_amdgcn_s_memrealtime();)
     const int rp = ticket / b.num_pics, pic = ticket % b.num_pics;
     const int r = 2 * rp + h;                              // this half's MB row
     const bool hasB = 2 * rp + 1 < H;
@@ -71,72 +85,74 @@ extern "C" __global__ __launch_bounds__(64) void k_deblock(h264r_batch b, const 
     const bool last_row = r == H - 1;
     const bool feeds_ring = h == 0 && hasB;                // A -> B through LDS
     const bool feeds_hb = h == 1 && rp + 1 < npairs;       // B -> next pair through hb
-    const bool pair_feeds = rp + 1 < npairs && hasB;
-    int* prog_in = rp > 0 ? sync + 1 + (size_t)pic * npairs + (rp - 1) : nullptr;
-    int* prog_out = sync + 1 + (size_t)pic * npairs + rp;
-    const uint32_t* hb_in = rp > 0 ? reinterpret_cast<const uint32_t*>(hb + ((size_t)pic * npairs + rp - 1) * W) : nullptr;
-    uint32_t* hb_out = reinterpret_cast<uint32_t*>(hb + ((size_t)pic * npairs + rp) * W);
+    const uint64_t* hb_in = rp > 0 ? hb + ((size_t)pic * npairs + rp - 1) * W * 32 : nullptr;
+    uint64_t* hb_out = hb + ((size_t)pic * npairs + rp) * W * 32;
 
     DbLds& S = L.t[h];
     uint8_t* Y = b.out_y + (size_t)pic * g.ysz;
     uint8_t* Cp[2] = {b.out_u + (size_t)pic * g.csz, b.out_v + (size_t)pic * g.csz};
     const int Y0 = r * 16, Yc = r * 8;
     const uint32_t* info_row = reinterpret_cast<const uint32_t*>(dbinfo + (size_t)pic * g.nmb + (size_t)r * W);
+    const uint64_t tag = (uint64_t)epoch << 32;
 
     // per-lane roles inside a half (32 lanes)
     const int by0 = hl >> 2, bd0 = hl & 3;                 // luma body dwords hl and hl + 32
     const int cpl = hl >> 4, cy = (hl >> 1) & 7, cd = hl & 1;   // chroma body dword
     const int steps = W + (hasB ? 2 : 0);
 
-    uint32_t pf_y0 = 0, pf_y1 = 0, pf_c = 0, pf_i = 0, pf_top = 0;
-    int seen = 0;          // last observed progress of the pair above
+    uint32_t pf_y0 = 0, pf_y1 = 0, pf_c = 0, pf_i = 0;
+    uint64_t pf_top = 0;
     bool ok = true;
+    TRACE(unsigned long long tr_wait = 0; unsigned long long tph[4] = {0, 0, 0, 0}; unsigned long long tm = 0;)
 
-    // Issue the loads of step t (this half's MB t - 2h): body, record and, for
-    // half A below another pair, the hand-off record of the MB above.
+    // Issue the loads of step t (this half's MB t - 2h): body, deblocking record
+    // and, for half A below another pair, the hand-off record of the MB above.
     auto prefetch = [&](int t) {
-        if (rp > 0 && t < W) {
-            const int need = t + 1;                        // record t of the pair above
-            unsigned spins = 0;
-            while (seen < need) {
-                seen = __builtin_amdgcn_readfirstlane(
-                    (int)ld_cc(reinterpret_cast<const uint32_t*>(prog_in)));
-                if (seen >= need) break;
-                __builtin_amdgcn_s_sleep(1);
-                if (++spins > SPIN_LIMIT) {
-                    __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    ok = false;
-                    seen = W;
-                    break;
-                }
-            }
-        }
         const int x = t - 2 * h;
         if (half_on && x >= 0 && x < W) {
             const uint8_t* yb = Y + (size_t)(Y0 + by0) * g.W + x * 16 + 4 * bd0;
             pf_y0 = *reinterpret_cast<const uint32_t*>(yb);
             pf_y1 = *reinterpret_cast<const uint32_t*>(yb + (size_t)8 * g.W);
             pf_c = *reinterpret_cast<const uint32_t*>(Cp[cpl] + (size_t)(Yc + cy) * g.Wc + x * 8 + 4 * cd);
-            if (hl < 12) pf_i = info_row[x * 12 + hl];
-            if (h == 0 && rp > 0) pf_top = ld_cc(hb_in + (size_t)x * 32 + hl);
+            if (hl < DBINFO_DWORDS) pf_i = info_row[x * DBINFO_DWORDS + hl];
+            if (h == 0 && rp > 0) pf_top = ld_cc64(hb_in + (size_t)x * 32 + hl);
         }
     };
 
     prefetch(0);
+    TRACE(const unsigned long long tr_first = __builtin_amdgcn_s_memrealtime();)
     for (int t = 0; t < steps; ++t) {
         const int x = t - 2 * h;
         const bool act = half_on && x >= 0 && x < W;
         const int X0 = x * 16, Xc = x * 8;
 
+        // ---- the record of the MB above (half A below another pair): wait for this epoch
+        if (rp > 0) {
+            const bool need = act && h == 0;
+            unsigned spins = 0;
+            TRACE(unsigned long long tw0 = 0;)
+            while (!__all(!need || (pf_top & 0xFFFFFFFF00000000ull) == tag)) {
+                TRACE(if (!tw0) tw0 = __builtin_amdgcn_s_memrealtime();)
+                __builtin_amdgcn_s_sleep(1);
+                if (need) pf_top = ld_cc64(hb_in + (size_t)x * 32 + hl);
+                if (++spins > SPIN_LIMIT) {
+                    if (lane == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    ok = false;
+                    break;
+                }
+            }
+            TRACE(if (tw0) tr_wait += __builtin_amdgcn_s_memrealtime() - tw0;)
+            if (!ok) break;
+        }
+        TRACE(unsigned long long ta = __builtin_amdgcn_s_memtime();)
         // ---- assemble this half's tile: body, record, top rows (left strip = carry)
         if (act) {
             S.lt[(4 + by0) * 5 + 1 + bd0] = pf_y0;
             S.lt[(12 + by0) * 5 + 1 + bd0] = pf_y1;
             S.ct[cpl][(4 + cy) * 3 + 1 + cd] = pf_c;
-            if (hl < 8) reinterpret_cast<uint32_t*>(S.bs)[hl] = pf_i;
-            else if (hl < 12) S.tail[hl - 8] = pf_i;
+            if (hl < DBINFO_DWORDS) S.info[hl] = pf_i;
             if (r > 0) {
-                const uint32_t v = h == 0 ? pf_top : reinterpret_cast<const uint32_t*>(&L.ring[0][x % DRING])[hl];
+                const uint32_t v = h == 0 ? (uint32_t)pf_top : reinterpret_cast<const uint32_t*>(&L.ring[0][x % DRING])[hl];
                 if (hl < 16) S.lt[(hl >> 2) * 5 + 1 + (hl & 3)] = v;
                 else {
                     const int k = hl - 16, pl = k >> 3, i = (k >> 1) & 3, d = k & 1;
@@ -144,10 +160,12 @@ extern "C" __global__ __launch_bounds__(64) void k_deblock(h264r_batch b, const 
                 }
             }
         }
+        TRACE(asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); tph[0] += __builtin_amdgcn_s_memtime() - ta;)
         if (t + 1 < steps) prefetch(t + 1);
-        if (!ok) break;
         wave_sync();
+        TRACE(tm = __builtin_amdgcn_s_memtime();)
         filter_mb(S, hl, act);
+        TRACE(asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); { unsigned long long t2 = __builtin_amdgcn_s_memtime(); tph[1] += t2 - tm; tm = t2; })
 
         // ---- write back what is final: enumerate luma rows -3..15 x dwords 0..4 (95)
         //      and chroma 2 x rows -3..7 x dwords 0..2 (66); 6 slots per lane.
@@ -196,13 +214,14 @@ extern "C" __global__ __launch_bounds__(64) void k_deblock(h264r_batch b, const 
             }
         }
         wave_sync();
+        TRACE({ unsigned long long t2 = __builtin_amdgcn_s_memtime(); tph[2] += t2 - tm; tm = t2; })
         // ---- half B: completed records (MB x-1, and MB x at the row end) to the hand-off buffer
         if (act && feeds_hb) {
             if (x > 0)
-                st_cc(hb_out + (size_t)(x - 1) * 32 + hl,
-                      reinterpret_cast<const uint32_t*>(&L.ring[1][(x + DRING - 1) % DRING])[hl]);
+                st_cc64(hb_out + (size_t)(x - 1) * 32 + hl,
+                        tag | reinterpret_cast<const uint32_t*>(&L.ring[1][(x + DRING - 1) % DRING])[hl]);
             if (x == W - 1)
-                st_cc(hb_out + (size_t)x * 32 + hl, reinterpret_cast<const uint32_t*>(&L.ring[1][x % DRING])[hl]);
+                st_cc64(hb_out + (size_t)x * 32 + hl, tag | reinterpret_cast<const uint32_t*>(&L.ring[1][x % DRING])[hl]);
         }
         // ---- carry the right 4 columns into the left strip of the next tile
         if (act) {
@@ -214,18 +233,12 @@ extern "C" __global__ __launch_bounds__(64) void k_deblock(h264r_batch b, const 
             }
         }
         wave_sync();
-        // ---- progress of the pair: records complete = MBs of row B finished, minus the last
-        if (pair_feeds) {
-            const int xb = t - 2;                          // row B's MB of this step
-            if (xb >= 0) {
-                const int done = xb == W - 1 ? W : xb;
-                if (done % PUB == 0 || done == W) {
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    if (lane == 0) st_cc(reinterpret_cast<uint32_t*>(prog_out), (uint32_t)done);
-                }
-            }
-        }
+        TRACE({ unsigned long long t2 = __builtin_amdgcn_s_memtime(); tph[3] += t2 - tm; })
     }
-    if (!ok && pair_feeds && lane == 0)                     // release the pair below (error is flagged)
-        st_cc(reinterpret_cast<uint32_t*>(prog_out), (uint32_t)W);
+    if (!ok && feeds_hb)                                   // release the pair below (the error is flagged)
+        for (int x = 0; x < W; ++x) st_cc64(hb_out + (size_t)x * 32 + hl, tag);
+    TRACE(if (lane == 0 && ticket < (1 << 16)) {
+        h264r_db_trace[ticket][0] = tr_start; h264r_db_trace[ticket][1] = tr_first;
+        h264r_db_trace[ticket][2] = __builtin_amdgcn_s_memrealtime(); h264r_db_trace[ticket][3] = tr_wait;
+        for (int i = 0; i < 4; ++i) h264r_db_trace[ticket][4 + i] = tph[i]; })
 }

@@ -9,7 +9,7 @@
 // row-to-row hand-off is an LDS counter with workgroup-scope release/acquire
 // (no inter-CU traffic).  Only the first row of a band waits on another
 // workgroup (the last row of the band above), through a progress counter in
-// global memory published with agent-scope release every PUB MBs
+// global memory published with agent-scope release after every intra MB
 // (MI355X_MICROARCH.md, Guideline 16 recipe).  Workgroups take (band, picture)
 // tickets in band-major order from an atomic counter, so every workgroup only
 // ever waits on a ticket taken earlier by a resident workgroup: no deadlock
@@ -21,7 +21,6 @@ using namespace h264r;
 namespace {
 
 constexpr int WAVES = 16;                   // rows per band
-constexpr int PUB = 4;                      // global publish granularity (MBs)
 constexpr unsigned SPIN_LIMIT = 1u << 24;   // bounded wait, then flag an error
 
 DEV void publish_lds(int* counter, int value, int lane)
@@ -81,27 +80,41 @@ DEV void picture_walk(const h264r_batch& b, int* sync, int* err, Scratch* scratc
     const h264r_mb* mbs = b.mbs + (size_t)pic * g.nmb;
     bool ok = true;
 
-    for (int x = 0; x < g.wmb && ok; ++x) {
-        const int need = min(x + 2, g.wmb);
-        const uint32_t w0 = __builtin_amdgcn_readfirstlane(*reinterpret_cast<const uint32_t*>(&mbs[r * g.wmb + x]));
-        const bool work = ((w0 >> 8) & H264R_MBF_INTRA) && (w0 & 255) != H264R_I_PCM;
-        if (work && r > 0) {
+    // Only intra MBs take part in the walk (inter and PCM MBs were reconstructed by
+    // k_inter).  Progress of a row = index of its first intra MB not yet done (W when
+    // none is left): MB x may start once the row above has progress >= x + 2.
+    const h264r_mb* row = mbs + (size_t)r * g.wmb;
+    auto next_intra = [&](int from) -> int {
+        for (int c = from & ~63; c < g.wmb; c += 64) {
+            const int m = c + lane;
+            bool in = false;
+            if (m >= from && m < g.wmb) {
+                const uint32_t w0 = *reinterpret_cast<const uint32_t*>(&row[m]);
+                in = ((w0 >> 8) & H264R_MBF_INTRA) && (w0 & 255) != H264R_I_PCM;
+            }
+            const uint64_t bits = __ballot(in);
+            if (bits) return c + __builtin_ctzll(bits);
+        }
+        return g.wmb;
+    };
+    auto publish = [&](int v) {
+        if (last_row) publish_global(&gprog[r], v, lane);
+        else publish_lds(&lprog[wave], v, lane);
+    };
+    int x = next_intra(0);
+    publish(x);
+    while (x < g.wmb && ok) {
+        if (r > 0) {
+            const int need = min(x + 2, g.wmb);
             if (wave == 0) ok = wait_for<true>(&gprog[r - 1], need, err);
             else ok = wait_for<false>(&lprog[wave - 1], need, err);
         }
-        if (work && ok) {
-            intra_mb(b, g, pic, x, r, lane, S);
-        }
-        if (last_row) {
-            if ((x + 1) % PUB == 0 || x + 1 == g.wmb) publish_global(&gprog[r], x + 1, lane);
-        } else {
-            publish_lds(&lprog[wave], x + 1, lane);
-        }
+        if (!ok) break;
+        intra_mb(b, g, pic, x, r, lane, S);
+        x = next_intra(x + 1);
+        publish(x);
     }
-    if (!ok) {   // let every waiter behind a failed wave finish (outputs are flagged invalid)
-        if (last_row) publish_global(&gprog[r], g.wmb, lane);
-        else publish_lds(&lprog[wave], g.wmb, lane);
-    }
+    if (!ok) publish(g.wmb);   // let every waiter behind a failed wave finish (outputs are flagged invalid)
 }
 
 extern "C" __global__ __launch_bounds__(1024) void k_intra_pic(h264r_batch b, int* sync, int* err)

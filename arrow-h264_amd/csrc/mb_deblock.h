@@ -63,16 +63,28 @@ DEV int special_slice(int t) { return t == H264R_SLICE_SP || t == H264R_SLICE_SI
 // disabled edge has bS 0.  bs[hor * 16 + edge * 4 + segment]; chroma edge 0 uses
 // luma edge 0, chroma edge 1 (sample 4) luma edge 2 (deblock.cc:430-433).
 struct DbInfo {
-    uint8_t bs[32];
-    int8_t  qpy[3];        // QpY of Q, left MB, top MB
-    int8_t  qpc[2][3];     // QpC[pl] of Q, left, top
-    int8_t  off_a, off_b;  // FilterOffsetA/B of Q's slice (deblock.cc:472-473)
-    uint8_t pad[5];
+    uint8_t  bs[32];
+    uint32_t par[9];       // [Y, Cb, Cr][left edge, top edge, internal edges]: edge_word()
+    uint32_t pad[3];
 };
-static_assert(sizeof(DbInfo) == 48, "DbInfo layout");
+static_assert(sizeof(DbInfo) == 80, "DbInfo layout");
+constexpr int DBINFO_DWORDS = 20;
+
+// alpha | beta << 8 | tc0(bS 1..3) << 16 / 21 / 26 for one edge: filter_edge
+// deblock.cc:469-480 (qPav of the two MBs' QPs, indexA/B with MbQ's slice offsets),
+// 8-bit tables (Tables 8-16 / 8-17, deblock.cc:294-324).
+DEV uint32_t edge_word(int qpp, int qpq, int offa, int offb)
+{
+    const int qPav = (qpp + qpq + 1) >> 1;
+    const int idxA = clip3(0, 51, qPav + offa), idxB = clip3(0, 51, qPav + offb);
+    const uint32_t t = DB_TC0[idxA];
+    return (DB_AB[idxA] & 255) | (DB_AB[idxB] & 0xFF00) | ((t & 31) << 16) | (((t >> 8) & 31) << 21) |
+           (((t >> 16) & 31) << 26);
+}
 
 // Deblock::strength + strength_vertical/horizontal for MB `a` (deblock.cc:78-289).
-// All lanes call; lanes 0..31 compute one strength each, lane 32 the tail.  `mot`
+// All lanes call; lanes 0..31 compute one strength each, lanes 32..40 the edge
+// parameters (alpha/beta/tc0 per plane and edge class).  `mot`
 // is the picture's resolved motion (k_prep), [list][H4][W4]; every load is issued
 // before the first decision so the record and motion latencies overlap.
 DEV void db_info_mb(const h264r_batch& b, const Geom& g, int pic, int a, int lane, const uint2* __restrict__ mot,
@@ -126,16 +138,14 @@ DEV void db_info_mb(const h264r_batch& b, const Geom& g, int pic, int a, int lan
             }
         }
         out->bs[lane] = (uint8_t)v;
-    } else if (lane == 32) {
-        uint32_t w[4];
-        w[0] = (uint8_t)q.qp_y | ((uint32_t)(uint8_t)L.qp_y << 8) | ((uint32_t)(uint8_t)U.qp_y << 16) |
-               ((uint32_t)(uint8_t)q.qp_c[0] << 24);
-        w[1] = (uint8_t)L.qp_c[0] | ((uint32_t)(uint8_t)U.qp_c[0] << 8) | ((uint32_t)(uint8_t)q.qp_c[1] << 16) |
-               ((uint32_t)(uint8_t)L.qp_c[1] << 24);
-        w[2] = (uint8_t)U.qp_c[1] | ((uint32_t)(uint8_t)qs->filter_offset_a << 8) |
-               ((uint32_t)(uint8_t)qs->filter_offset_b << 16);
-        w[3] = 0;
-        *reinterpret_cast<uint4*>(&out->qpy[0]) = make_uint4(w[0], w[1], w[2], w[3]);
+    } else if (lane < 32 + 9) {                        // edge parameters
+        const int k = lane - 32, pl = k / 3, which = k - pl * 3;
+        const int qyP = which == 0 ? L.qp_y : (which == 1 ? U.qp_y : q.qp_y);
+        const int qcP0 = which == 0 ? L.qp_c[0] : (which == 1 ? U.qp_c[0] : q.qp_c[0]);
+        const int qcP1 = which == 0 ? L.qp_c[1] : (which == 1 ? U.qp_c[1] : q.qp_c[1]);
+        const int qq = pl == 0 ? q.qp_y : (pl == 1 ? q.qp_c[0] : q.qp_c[1]);
+        const int qp = pl == 0 ? qyP : (pl == 1 ? qcP0 : qcP1);
+        out->par[k] = edge_word(qp, qq, qs->filter_offset_a, qs->filter_offset_b);
     }
 }
 
@@ -155,42 +165,30 @@ static_assert(sizeof(RingEntry) == 128, "RingEntry is one 128-B line");
 struct alignas(16) DbLds {
     uint32_t lt[20 * 5];          // luma tile, [row + 4][dword]
     uint32_t ct[2][12 * 3];       // chroma tiles
-    uint8_t  bs[32];
-    uint32_t tail[4];             // DbInfo bytes 32..47
+    uint32_t info[DBINFO_DWORDS]; // the MB's DbInfo
 };
 
 DEV uint8_t* ltb(DbLds& S) { return reinterpret_cast<uint8_t*>(S.lt); }
 DEV uint8_t* ctb(DbLds& S, int pl) { return reinterpret_cast<uint8_t*>(S.ct[pl]); }
 
-// alpha/beta/tc0 for one edge (filter_edge deblock.cc:469-480), 8-bit.
-DEV void edge_params(int qpp, int qpq, int offa, int offb, int& alpha, int& beta, int& idxA)
-{
-    int qPav = (qpp + qpq + 1) >> 1;
-    idxA = clip3(0, 51, qPav + offa);
-    int idxB = clip3(0, 51, qPav + offb);
-    alpha = DB_AB[idxA] & 255;
-    beta = (DB_AB[idxB] >> 8) & 255;
-}
-
-DEV int tc0_of(int idxA, int bS) { return bS < 4 ? (int)((DB_TC0[idxA] >> (8 * (bS - 1))) & 255) : 0; }
-
 // Filter one line held as packed bytes w[0..NE] (4 samples per dword; edge k sits
 // between dword k and dword k+1) across NE edges; edges are sequential because
 // neighbouring edges share samples (deblock.cc:459-485 per edge, :495-502 order).
 template <int NE>
-DEV void filter_line_packed(uint32_t (&w)[NE + 1], const uint8_t* bsrow, int seg, int qpP0, int qpQ, int offa, int offb,
+DEV void filter_line_packed(uint32_t (&w)[NE + 1], const uint8_t* bsrow, int seg, uint32_t par0, uint32_t pari,
                             int chroma, int bsidx_step)
 {
 #pragma unroll
     for (int k = 0; k < NE; ++k) {
         const int bS = bsrow[k * bsidx_step * 4 + seg];
         if (!bS) continue;
-        int alpha, beta, ia;
-        edge_params(k == 0 ? qpP0 : qpQ, qpQ, offa, offb, alpha, beta, ia);
+        const uint32_t par = k == 0 ? par0 : pari;
+        const int alpha = par & 255, beta = (par >> 8) & 255;
+        const int tc0 = bS < 4 ? (int)((par >> (16 + 5 * (bS - 1))) & 31) : 0;
         const uint32_t a = w[k], c = w[k + 1];
         int p3 = a & 255, p2 = (a >> 8) & 255, p1 = (a >> 16) & 255, p0 = a >> 24;
         int q0 = c & 255, q1 = (c >> 8) & 255, q2 = (c >> 16) & 255, q3 = c >> 24;
-        filter_samples(p3, p2, p1, p0, q0, q1, q2, q3, alpha, beta, bS, chroma, tc0_of(ia, bS));
+        filter_samples(p3, p2, p1, p0, q0, q1, q2, q3, alpha, beta, bS, chroma, tc0);
         w[k] = (uint32_t)p3 | ((uint32_t)p2 << 8) | ((uint32_t)p1 << 16) | ((uint32_t)p0 << 24);
         w[k + 1] = (uint32_t)q0 | ((uint32_t)q1 << 8) | ((uint32_t)q2 << 16) | ((uint32_t)q3 << 24);
     }
@@ -202,9 +200,7 @@ DEV void filter_line_packed(uint32_t (&w)[NE + 1], const uint8_t* bsrow, int seg
 // every lane of the wave calls (the passes are separated by wave_sync).
 DEV void filter_mb(DbLds& S, int lane, bool act)
 {
-    const uint32_t t0 = S.tail[0], t1 = S.tail[1], t2 = S.tail[2];
-    const int qpyQ = (int8_t)(t0 & 255), qpyL = (int8_t)((t0 >> 8) & 255), qpyU = (int8_t)((t0 >> 16) & 255);
-    const int offa = (int8_t)((t2 >> 8) & 255), offb = (int8_t)((t2 >> 16) & 255);
+    const uint8_t* bs = reinterpret_cast<const uint8_t*>(S.info);
 #pragma unroll 1
     for (int hor = 0; hor < 2; ++hor) {
         if (!act) {
@@ -220,7 +216,7 @@ DEV void filter_mb(DbLds& S, int lane, bool act)
                     w[d] = (uint32_t)lt[(4 * d) * LP + lane + 4] | ((uint32_t)lt[(4 * d + 1) * LP + lane + 4] << 8) |
                            ((uint32_t)lt[(4 * d + 2) * LP + lane + 4] << 16) | ((uint32_t)lt[(4 * d + 3) * LP + lane + 4] << 24);
             }
-            filter_line_packed<4>(w, &S.bs[hor * 16], lane >> 2, hor ? qpyU : qpyL, qpyQ, offa, offb, 0, 1);
+            filter_line_packed<4>(w, &bs[hor * 16], lane >> 2, S.info[8 + hor], S.info[10], 0, 1);
             if (!hor) {
 #pragma unroll
                 for (int d = 0; d < 5; ++d) S.lt[(lane + 4) * 5 + d] = w[d];
@@ -230,9 +226,6 @@ DEV void filter_mb(DbLds& S, int lane, bool act)
             }
         } else if (lane < 32) {
             const int pl = (lane - 16) >> 3, r = (lane - 16) & 7;
-            const int qcQ = pl ? (int8_t)((t1 >> 16) & 255) : (int8_t)(t0 >> 24);
-            const int qcL = pl ? (int8_t)(t1 >> 24) : (int8_t)(t1 & 255);
-            const int qcU = pl ? (int8_t)(t2 & 255) : (int8_t)((t1 >> 8) & 255);
             uint32_t w[3];
             uint8_t* ct = ctb(S, pl);
             if (!hor) {
@@ -245,7 +238,7 @@ DEV void filter_mb(DbLds& S, int lane, bool act)
                            ((uint32_t)ct[(4 * d + 2) * CP + r + 4] << 16) | ((uint32_t)ct[(4 * d + 3) * CP + r + 4] << 24);
             }
             // chroma edge 1 uses luma edge 2 (bsidx_step 2); StrengthIdx = pel << 1 (deblock.cc:460)
-            filter_line_packed<2>(w, &S.bs[hor * 16], r >> 1, hor ? qcU : qcL, qcQ, offa, offb, 1, 2);
+            filter_line_packed<2>(w, &bs[hor * 16], r >> 1, S.info[11 + 3 * pl + hor], S.info[13 + 3 * pl], 1, 2);
             if (!hor) {
 #pragma unroll
                 for (int d = 0; d < 3; ++d) S.ct[pl][(r + 4) * 3 + d] = w[d];
