@@ -111,11 +111,19 @@ struct h264r_ctx {
     uint8_t* d_hb = nullptr; size_t c_hb = 0;
     uint32_t epoch = 0;             // tag of the deblocking hand-off records of the last launch
     uint2* d_mot = nullptr; size_t c_mot = 0;
-    // timing
+    // pipelining: prep+inter on the caller's stream, intra and deblocking of each
+    // chunk of pictures on two more streams, chained by events
+    hipStream_t aux[2] = {};
+    std::vector<hipEvent_t> ev_chain;               // [2 * chunk + 0] inter done, [+1] intra done
+    hipEvent_t ev_end = nullptr;
+    // timing: every kernel of every launch bracketed by events on its stream
     bool timing = false;
     int debug = 0;
-    hipEvent_t ev[4] = {};
-    float last_ms[4] = {0, 0, 0, 0};
+    struct Span { int kind; hipEvent_t a, b; };
+    std::vector<hipEvent_t> ev_pool;
+    size_t ev_used = 0;
+    std::vector<Span> spans;
+    int timed_launches = 0;
 };
 
 extern "C" {
@@ -199,7 +207,13 @@ int h264r_create(h264r_ctx** out, int device, int max_w, int max_h, int chroma_f
         delete c;
         return H264R_EDEVICE;
     }
-    for (int i = 0; i < 4; ++i) (void)hipEventCreate(&c->ev[i]);
+    {   // the wavefront walks are latency-bound: their streams get the highest priority
+        int lo = 0, hi = 0;
+        (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+        for (int i = 0; i < 2; ++i)
+            if (hipStreamCreateWithPriority(&c->aux[i], hipStreamNonBlocking, hi) != hipSuccess) { delete c; return H264R_EDEVICE; }
+    }
+    (void)hipEventCreateWithFlags(&c->ev_end, hipEventDisableTiming);
     (void)hipMemset(c->d_ref_planes, 0, sizeof(uint8_t*) * 3 * H264R_MAX_SLOTS);
     (void)hipMemset(c->d_err, 0, sizeof(int));
     *out = c;
@@ -214,7 +228,10 @@ int h264r_destroy(h264r_ctx* c)
     for (int s = 0; s < H264R_MAX_SLOTS; ++s) if (c->slot[s][0]) (void)hipFree(c->slot[s][0]);
     void* bufs[] = {c->d_ref_planes, c->d_err, c->d_dbinfo, c->d_sync, c->d_hb, c->d_mot, c->d_mbs, c->d_levels, c->d_mv, c->d_ref, c->d_slices, c->d_pic, c->d_quant, c->d_out};
     for (void* b : bufs) if (b) (void)hipFree(b);
-    for (int i = 0; i < 4; ++i) if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
+    for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->ev_chain) (void)hipEventDestroy(e);
+    if (c->ev_end) (void)hipEventDestroy(c->ev_end);
+    for (int i = 0; i < 2; ++i) if (c->aux[i]) { (void)hipStreamSynchronize(c->aux[i]); (void)hipStreamDestroy(c->aux[i]); }
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return H264R_OK;
@@ -257,46 +274,138 @@ int h264r_ref_planes(h264r_ctx* c, int slot, uint8_t** y, uint8_t** u, uint8_t**
     return c->slot[slot][0] ? H264R_OK : H264R_ESTATE;
 }
 
+static hipEvent_t timing_event(h264r_ctx* c)
+{
+    if (c->ev_used == c->ev_pool.size()) {
+        hipEvent_t e = nullptr;
+        if (hipEventCreate(&e) != hipSuccess) return nullptr;
+        c->ev_pool.push_back(e);
+    }
+    return c->ev_pool[c->ev_used++];
+}
+
+// Bracket one launch with timing events on its stream (kind: 0 prep+inter, 1 intra,
+// 2 deblock, 3 whole batch).
+struct Timed {
+    h264r_ctx* c; int kind; hipStream_t s; hipEvent_t a = nullptr;
+    Timed(h264r_ctx* c_, int k, hipStream_t s_) : c(c_), kind(k), s(s_)
+    {
+        if (c->timing && (a = timing_event(c))) (void)hipEventRecord(a, s);
+    }
+    ~Timed()
+    {
+        if (!a) return;
+        hipEvent_t b = timing_event(c);
+        if (b) { (void)hipEventRecord(b, s); c->spans.push_back({kind, a, b}); }
+    }
+};
+
+// A batch restricted to pictures [p0, p0 + n).
+static h264r_batch chunk_of(const h264r_batch& b, int p0, int n)
+{
+    h264r_batch c = b;
+    const size_t nmb = (size_t)b.width_mbs * b.height_mbs, mp = nmb * 16;
+    const size_t ys = nmb * 256, cs = nmb * 64;
+    c.num_pics = n;
+    c.mbs = b.mbs + p0 * nmb;
+    c.mv = b.mv + p0 * 2 * mp;
+    c.ref_idx = b.ref_idx + p0 * 2 * mp;
+    c.slices = b.slices + (size_t)p0 * b.slice_stride;
+    c.pics = b.pics + p0;
+    c.quant = b.quant + p0;
+    c.out_y = b.out_y + p0 * ys;
+    c.out_u = b.out_u + p0 * cs;
+    c.out_v = b.out_v + p0 * cs;
+    return c;
+}
+
+// Pictures per pipelined chunk: the intra and deblocking walks of chunk i (latency-
+// bound wavefronts) run beside k_inter of chunk i+1 (throughput-bound).
+// Measured on MI355X (config 3, 1080p P): the walks are latency-bound, so a chunk's
+// walk takes about as long as the whole batch's -- chunking serialises them and loses
+// (64 pictures: 153 M MB/s unchunked vs 83 M with 16-picture chunks).  Off by default;
+// H264R_CHUNK=<pictures> enables it for experiments.
+static int chunk_pictures(int P)
+{
+    static const int env = [] { const char* e = getenv("H264R_CHUNK"); return e ? atoi(e) : 0; }();
+    return env > 0 ? env : P;
+}
+
 static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s)
 {
     const int W = b.width_mbs, H = b.height_mbs, P = b.num_pics;
     const int nbands = (H + 15) / 16, npairs = (H + 1) / 2;
-    // scratch: per-MB deblocking records, row-pair hand-off records, two sync
-    // regions (ticket + per-row / per-pair progress)
-    const size_t sync_ints = 1 + (size_t)P * H;
+    const int CP = std::min(chunk_pictures(P), P), K = (P + CP - 1) / CP;
+    // scratch: per-MB deblocking records and resolved motion (whole batch), tagged
+    // row-pair hand-off records (one chunk; chunks deblock in stream order), and per
+    // chunk a sync region: [intra ticket + per-row progress][deblock ticket]
+    const size_t sync_chunk = 1 + (size_t)CP * H + 4;
     int st;
     if ((st = dev_resize(&c->d_dbinfo, &c->c_dbinfo, (size_t)P * W * H * DBINFO_BYTES))) return st;
     {
         const size_t cap_before = c->c_hb;
-        if ((st = dev_resize(&c->d_hb, &c->c_hb, (size_t)P * npairs * W * HANDOFF_BYTES))) return st;
+        if ((st = dev_resize(&c->d_hb, &c->c_hb, (size_t)CP * npairs * W * HANDOFF_BYTES))) return st;
         if (c->c_hb != cap_before) {              // fresh memory: no record may carry a live epoch
             HIP_OK(hipMemsetAsync(c->d_hb, 0, c->c_hb, s));
             c->epoch = 0;
         }
-        if (++c->epoch == 0) {                    // 2^32 launches: wrap without reusing an epoch
+        if (c->epoch > 0xFFFFFF00u) {             // never reuse an epoch: restart from clean memory
             HIP_OK(hipMemsetAsync(c->d_hb, 0, c->c_hb, s));
-            c->epoch = 1;
+            c->epoch = 0;
         }
     }
     const size_t mplane = (size_t)W * 4 * H * 4;
     if ((st = dev_resize(&c->d_mot, &c->c_mot, (size_t)P * 2 * mplane))) return st;
-    if ((st = dev_resize(&c->d_sync, &c->c_sync, 2 * sync_ints + 4))) return st;
-    HIP_OK(hipMemsetAsync(c->d_sync, 0, (2 * sync_ints + 4) * sizeof(int), s));
-    auto* dbinfo = reinterpret_cast<h264r::DbInfo*>(c->d_dbinfo);
-    if (c->timing) HIP_OK(hipEventRecord(c->ev[0], s));
-    hipLaunchKernelGGL(k_prep, dim3((unsigned)((mplane + 255) / 256), P), dim3(256), 0, s, b, c->d_mot);
-    HIP_OK(hipGetLastError());
-    hipLaunchKernelGGL(k_inter, dim3(W * H, P), dim3(64), 0, s, b, c->d_mot, dbinfo);
-    HIP_OK(hipGetLastError());
-    if (c->timing) HIP_OK(hipEventRecord(c->ev[1], s));
-    hipLaunchKernelGGL(k_intra_pic, dim3(P * nbands), dim3(1024), 0, s, b, c->d_sync, c->d_err);
-    HIP_OK(hipGetLastError());
-    if (c->timing) HIP_OK(hipEventRecord(c->ev[2], s));
-    if (!(c->debug & H264R_DBG_NO_DEBLOCK))
-        hipLaunchKernelGGL(k_deblock, dim3(P * npairs), dim3(64), 0, s, b, dbinfo,
-                           reinterpret_cast<uint64_t*>(c->d_hb), c->d_sync + sync_ints, c->d_err, c->epoch);
-    HIP_OK(hipGetLastError());
-    if (c->timing) HIP_OK(hipEventRecord(c->ev[3], s));
+    if ((st = dev_resize(&c->d_sync, &c->c_sync, (size_t)K * sync_chunk))) return st;
+    while ((int)c->ev_chain.size() < 2 * K) {
+        hipEvent_t e = nullptr;
+        HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        c->ev_chain.push_back(e);
+    }
+    HIP_OK(hipMemsetAsync(c->d_sync, 0, (size_t)K * sync_chunk * sizeof(int), s));
+    auto dbinfo_at = [&](int p0) { return reinterpret_cast<h264r::DbInfo*>(c->d_dbinfo + (size_t)p0 * W * H * DBINFO_BYTES); };
+    const bool deblock = !(c->debug & H264R_DBG_NO_DEBLOCK);
+    Timed whole(c, 3, s);
+    if (c->timing) c->timed_launches++;
+    for (int k = 0; k < K; ++k) {
+        const int p0 = k * CP, n = std::min(CP, P - p0);
+        const h264r_batch cb = chunk_of(b, p0, n);
+        int* sync = c->d_sync + (size_t)k * sync_chunk;
+        // stream s: prep + inter of chunk k
+        {
+            Timed t(c, 0, s);
+            hipLaunchKernelGGL(k_prep, dim3((unsigned)((mplane + 255) / 256), n), dim3(256), 0, s, cb,
+                               c->d_mot + (size_t)p0 * 2 * mplane);
+            HIP_OK(hipGetLastError());
+            hipLaunchKernelGGL(k_inter, dim3(W * H, n), dim3(64), 0, s, cb, c->d_mot + (size_t)p0 * 2 * mplane,
+                               dbinfo_at(p0));
+            HIP_OK(hipGetLastError());
+        }
+        hipStream_t si = K > 1 ? c->aux[0] : s, sd = K > 1 ? c->aux[1] : s;
+        if (K > 1) {
+            HIP_OK(hipEventRecord(c->ev_chain[2 * k], s));
+            HIP_OK(hipStreamWaitEvent(si, c->ev_chain[2 * k], 0));
+        }
+        {
+            Timed t(c, 1, si);
+            hipLaunchKernelGGL(k_intra_pic, dim3(n * nbands), dim3(1024), 0, si, cb, sync, c->d_err);
+            HIP_OK(hipGetLastError());
+        }
+        if (K > 1) {
+            HIP_OK(hipEventRecord(c->ev_chain[2 * k + 1], si));
+            HIP_OK(hipStreamWaitEvent(sd, c->ev_chain[2 * k + 1], 0));
+        }
+        if (deblock) {
+            Timed t(c, 2, sd);
+            hipLaunchKernelGGL(k_deblock, dim3(n * npairs), dim3(64), 0, sd, cb, dbinfo_at(p0),
+                               reinterpret_cast<uint64_t*>(c->d_hb), sync + 1 + (size_t)CP * H, c->d_err, ++c->epoch);
+            HIP_OK(hipGetLastError());
+        }
+    }
+    if (K > 1) {                                   // the caller's stream sees the whole batch
+        HIP_OK(hipEventRecord(c->ev_end, c->aux[1]));
+        HIP_OK(hipStreamWaitEvent(s, c->ev_end, 0));
+    }
     return H264R_OK;
 }
 
@@ -336,6 +445,9 @@ int h264r_set_timing(h264r_ctx* c, int enable)
 {
     if (!c) return H264R_EINVAL;
     c->timing = enable != 0;
+    c->spans.clear();
+    c->ev_used = 0;
+    c->timed_launches = 0;
     return H264R_OK;
 }
 
@@ -344,6 +456,7 @@ int h264r_check(h264r_ctx* c)
     if (!c) return H264R_EINVAL;
     (void)hipSetDevice(c->device);
     HIP_OK(hipStreamSynchronize(c->stream));
+    for (int i = 0; i < 2; ++i) HIP_OK(hipStreamSynchronize(c->aux[i]));
     HIP_OK(hipDeviceSynchronize());
     int e = 0;
     HIP_OK(hipMemcpy(&e, c->d_err, sizeof(int), hipMemcpyDeviceToHost));
@@ -362,11 +475,18 @@ int h264r_last_timing(h264r_ctx* c, float out[4])
 {
     if (!c || !out) return H264R_EINVAL;
     if (!c->timing) return H264R_ESTATE;
-    HIP_OK(hipEventSynchronize(c->ev[3]));
-    HIP_OK(hipEventElapsedTime(&out[0], c->ev[0], c->ev[1]));
-    HIP_OK(hipEventElapsedTime(&out[1], c->ev[1], c->ev[2]));
-    HIP_OK(hipEventElapsedTime(&out[2], c->ev[2], c->ev[3]));
-    HIP_OK(hipEventElapsedTime(&out[3], c->ev[0], c->ev[3]));
+    if (c->timed_launches == 0) return H264R_ESTATE;
+    double sum[4] = {0, 0, 0, 0};
+    for (const auto& sp : c->spans) {
+        float ms = 0;
+        HIP_OK(hipEventSynchronize(sp.b));
+        HIP_OK(hipEventElapsedTime(&ms, sp.a, sp.b));
+        sum[sp.kind] += ms;
+    }
+    for (int k = 0; k < 4; ++k) out[k] = (float)(sum[k] / c->timed_launches);
+    c->spans.clear();
+    c->ev_used = 0;
+    c->timed_launches = 0;
     return H264R_OK;
 }
 

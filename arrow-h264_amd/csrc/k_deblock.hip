@@ -89,16 +89,76 @@ extern "C" __global__ __launch_bounds__(64) void k_deblock(h264r_batch b, const 
     uint64_t* hb_out = hb + ((size_t)pic * npairs + rp) * W * 32;
 
     DbLds& S = L.t[h];
+    uint32_t* Sw = reinterpret_cast<uint32_t*>(&S);        // tiles: Sw[p * TR * TP + (row + 4) * TP + dw]
+    if (hl == 0) S.zero = 0;
     uint8_t* Y = b.out_y + (size_t)pic * g.ysz;
     uint8_t* Cp[2] = {b.out_u + (size_t)pic * g.csz, b.out_v + (size_t)pic * g.csz};
     const int Y0 = r * 16, Yc = r * 8;
     const uint32_t* info_row = reinterpret_cast<const uint32_t*>(dbinfo + (size_t)pic * g.nmb + (size_t)r * W);
     const uint64_t tag = (uint64_t)epoch << 32;
+    const int steps = W + (hasB ? 2 : 0);
 
-    // per-lane roles inside a half (32 lanes)
+    // ---- per-lane roles (inside a half), computed once
     const int by0 = hl >> 2, bd0 = hl & 3;                 // luma body dwords hl and hl + 32
     const int cpl = hl >> 4, cy = (hl >> 1) & 7, cd = hl & 1;   // chroma body dword
-    const int steps = W + (hasB ? 2 : 0);
+    const int a_y0 = (4 + by0) * TP + 1 + bd0, a_y1 = a_y0 + 8 * TP;
+    const int a_c = (1 + cpl) * TR * TP + (4 + cy) * TP + 1 + cd;
+    const int a_top = hl < 16 ? (hl >> 2) * TP + 1 + (hl & 3)
+                              : (1 + ((hl - 16) >> 3)) * TR * TP + (((hl - 16) >> 1) & 3) * TP + 1 + (hl & 1);
+    // write-back slots: luma rows -3..15 x dwords 0..4 (95), chroma 2 x rows -3..7 x dwords 0..2 (66)
+    constexpr int NWB = 6;
+    int wb_word[NWB], wb_flags[NWB];                       // flags: 1 valid, 2 needs x > 0, 4 needs x == W-1, 8 chroma
+    uint8_t* wb_ptr[NWB];
+#pragma unroll
+    for (int it = 0; it < NWB; ++it) {
+        const int e = hl + 32 * it;
+        int f = 0, word = 0;
+        uint8_t* ptr = Y;
+        if (e < 95) {
+            const int row = e / 5 - 3, dw = e % 5;
+            const bool v = row < 0 ? (r > 0 && dw >= 1) : (row <= 12 || last_row);
+            f = (v ? 1 : 0) | (row >= 0 && dw == 0 ? 2 : 0) | (row >= 0 && dw == 4 ? 4 : 0);
+            word = (row + 4) * TP + dw;
+            ptr = Y + (ptrdiff_t)(Y0 + row) * g.W + 4 * (dw - 1);
+        } else if (e < 161) {
+            const int k = e - 95, pl = k / 33, k2 = k - pl * 33, row = k2 / 3 - 3, dw = k2 % 3;
+            const bool v = row < 0 ? (r > 0 && dw >= 1) : (row <= 4 || last_row);
+            f = (v ? 1 : 0) | (row >= 0 && dw == 0 ? 2 : 0) | (row >= 0 && dw == 2 ? 4 : 0) | 8;
+            word = (1 + pl) * TR * TP + (row + 4) * TP + dw;
+            ptr = Cp[pl] + (ptrdiff_t)(Yc + row) * g.Wc + 4 * (dw - 1);
+        }
+        wb_word[it] = word; wb_flags[it] = f; wb_ptr[it] = ptr;
+    }
+    // ring slots: luma rows 12..15 x dwords 0..4 (20), chroma 2 x rows 4..7 x dwords 0..2 (24)
+    int rg_src[2], rg_dst[2], rg_kind[2];                  // kind: 0 entry x, 1 entry x-1 if x > 0, 2 entry x if last, 3 none
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+        const int e = hl + 32 * it;
+        int src = 0, dst = 0, kind = 3;
+        if (e < 20) {
+            const int i = e / 5, dw = e % 5;
+            src = (16 + i) * TP + dw;
+            dst = i * 4 + (dw == 0 || dw == 4 ? 3 : dw - 1);
+            kind = dw == 0 ? 1 : (dw == 4 ? 2 : 0);
+        } else if (e < 44) {
+            const int k = e - 20, pl = k / 12, k2 = k - pl * 12, i = k2 / 3, dw = k2 % 3;
+            src = (1 + pl) * TR * TP + (8 + i) * TP + dw;
+            dst = 16 + pl * 8 + i * 2 + (dw == 1 ? 0 : 1);
+            kind = dw == 0 ? 1 : (dw == 2 ? 2 : 0);
+        }
+        rg_src[it] = src; rg_dst[it] = dst; rg_kind[it] = kind;
+    }
+    // carry slots: luma rows -4..15 (20), chroma 2 x rows -4..7 (24): dword 0 <- last dword
+    int cy_src[2], cy_dst[2];
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+        const int e = hl + 32 * it;
+        if (e < 20) { cy_dst[it] = e * TP; cy_src[it] = e * TP + 4; }
+        else if (e < 44) {
+            const int k = e - 20, pl = k / 12, row = k - pl * 12;
+            cy_dst[it] = (1 + pl) * TR * TP + row * TP; cy_src[it] = cy_dst[it] + 2;
+        } else { cy_dst[it] = -1; cy_src[it] = 0; }
+    }
 
     uint32_t pf_y0 = 0, pf_y1 = 0, pf_c = 0, pf_i = 0;
     uint64_t pf_top = 0;
@@ -124,7 +184,6 @@ extern "C" __global__ __launch_bounds__(64) void k_deblock(h264r_batch b, const 
     for (int t = 0; t < steps; ++t) {
         const int x = t - 2 * h;
         const bool act = half_on && x >= 0 && x < W;
-        const int X0 = x * 16, Xc = x * 8;
 
         // ---- the record of the MB above (half A below another pair): wait for this epoch
         if (rp > 0) {
@@ -145,93 +204,49 @@ extern "C" __global__ __launch_bounds__(64) void k_deblock(h264r_batch b, const 
             if (!ok) break;
         }
         TRACE(unsigned long long ta = __builtin_amdgcn_s_memtime();)
-        // ---- assemble this half's tile: body, record, top rows (left strip = carry)
-        if (act) {
-            S.lt[(4 + by0) * 5 + 1 + bd0] = pf_y0;
-            S.lt[(12 + by0) * 5 + 1 + bd0] = pf_y1;
-            S.ct[cpl][(4 + cy) * 3 + 1 + cd] = pf_c;
-            if (hl < DBINFO_DWORDS) S.info[hl] = pf_i;
-            if (r > 0) {
-                const uint32_t v = h == 0 ? (uint32_t)pf_top : reinterpret_cast<const uint32_t*>(&L.ring[0][x % DRING])[hl];
-                if (hl < 16) S.lt[(hl >> 2) * 5 + 1 + (hl & 3)] = v;
-                else {
-                    const int k = hl - 16, pl = k >> 3, i = (k >> 1) & 3, d = k & 1;
-                    S.ct[pl][i * 3 + 1 + d] = v;
-                }
-            }
-        }
+        // ---- assemble the tiles (an idle half scribbles on its own tiles only)
+        Sw[a_y0] = pf_y0;
+        Sw[a_y1] = pf_y1;
+        Sw[a_c] = pf_c;
+        if (hl < DBINFO_DWORDS) S.info[hl] = pf_i;
+        if (r > 0) Sw[a_top] = h == 0 ? (uint32_t)pf_top : reinterpret_cast<const uint32_t*>(&L.ring[0][x & (DRING - 1)])[hl];
         TRACE(asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); tph[0] += __builtin_amdgcn_s_memtime() - ta;)
         if (t + 1 < steps) prefetch(t + 1);
         wave_sync();
         TRACE(tm = __builtin_amdgcn_s_memtime();)
-        filter_mb(S, hl, act);
+        filter_mb(S, hl);
         TRACE(asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); { unsigned long long t2 = __builtin_amdgcn_s_memtime(); tph[1] += t2 - tm; tm = t2; })
 
-        // ---- write back what is final: enumerate luma rows -3..15 x dwords 0..4 (95)
-        //      and chroma 2 x rows -3..7 x dwords 0..2 (66); 6 slots per lane.
-        if (act) {
+        // ---- write back what is final (see the header comment)
+        const bool xl = x > 0, xr = x == W - 1;
 #pragma unroll
-            for (int it = 0; it < 6; ++it) {
-                const int e = hl + 32 * it;
-                if (e < 95) {
-                    const int row = e / 5 - 3, dw = e % 5;
-                    bool v;
-                    if (row < 0) v = r > 0 && dw >= 1;
-                    else v = (row <= 12 || last_row) && (dw == 0 ? x > 0 : (dw < 4 || x == W - 1));
-                    if (v)
-                        *reinterpret_cast<uint32_t*>(Y + (size_t)(Y0 + row) * g.W + X0 + 4 * (dw - 1)) =
-                            S.lt[(row + 4) * 5 + dw];
-                } else if (e < 161) {
-                    const int k = e - 95, pl = k / 33, k2 = k - pl * 33, row = k2 / 3 - 3, dw = k2 % 3;
-                    bool v;
-                    if (row < 0) v = r > 0 && dw >= 1;
-                    else v = (row <= 4 || last_row) && (dw == 0 ? x > 0 : (dw < 2 || x == W - 1));
-                    if (v)
-                        *reinterpret_cast<uint32_t*>(Cp[pl] + (size_t)(Yc + row) * g.Wc + Xc + 4 * (dw - 1)) =
-                            S.ct[pl][(row + 4) * 3 + dw];
-                }
-            }
+        for (int it = 0; it < NWB; ++it) {
+            const int f = wb_flags[it];
+            const bool v = act && (f & 1) && (xl || !(f & 2)) && (xr || !(f & 4));
+            if (v) *reinterpret_cast<uint32_t*>(wb_ptr[it] + x * ((f & 8) ? 8 : 16)) = Sw[wb_word[it]];
         }
         // ---- bottom rows of MB x (cols 0..11) and MB x-1 (cols 12..15) into this half's ring
         if (act && (feeds_ring || feeds_hb)) {
-            RingEntry* ring = L.ring[h];
+            uint32_t* ring = reinterpret_cast<uint32_t*>(L.ring[h]);
 #pragma unroll
             for (int it = 0; it < 2; ++it) {
-                const int e = hl + 32 * it;
-                if (e < 20) {                              // luma rows 12..15 x dwords 0..4
-                    const int i = e / 5, dw = e % 5;
-                    const uint32_t v = S.lt[(16 + i) * 5 + dw];
-                    if (dw == 0) { if (x > 0) ring[(x + DRING - 1) % DRING].y[i][3] = v; }
-                    else if (dw < 4) ring[x % DRING].y[i][dw - 1] = v;
-                    else if (x == W - 1) ring[x % DRING].y[i][3] = v;
-                } else if (e < 44) {                       // chroma rows 4..7 x dwords 0..2
-                    const int k = e - 20, pl = k / 12, k2 = k - pl * 12, i = k2 / 3, dw = k2 % 3;
-                    const uint32_t v = S.ct[pl][(8 + i) * 3 + dw];
-                    if (dw == 0) { if (x > 0) ring[(x + DRING - 1) % DRING].c[pl][i][1] = v; }
-                    else if (dw == 1) ring[x % DRING].c[pl][i][0] = v;
-                    else if (x == W - 1) ring[x % DRING].c[pl][i][1] = v;
-                }
+                const int k = rg_kind[it];
+                const int ent = k == 1 ? (x + DRING - 1) & (DRING - 1) : x & (DRING - 1);
+                if (k == 0 || (k == 1 && xl) || (k == 2 && xr)) ring[ent * 32 + rg_dst[it]] = Sw[rg_src[it]];
             }
         }
         wave_sync();
         TRACE({ unsigned long long t2 = __builtin_amdgcn_s_memtime(); tph[2] += t2 - tm; tm = t2; })
         // ---- half B: completed records (MB x-1, and MB x at the row end) to the hand-off buffer
         if (act && feeds_hb) {
-            if (x > 0)
-                st_cc64(hb_out + (size_t)(x - 1) * 32 + hl,
-                        tag | reinterpret_cast<const uint32_t*>(&L.ring[1][(x + DRING - 1) % DRING])[hl]);
-            if (x == W - 1)
-                st_cc64(hb_out + (size_t)x * 32 + hl, tag | reinterpret_cast<const uint32_t*>(&L.ring[1][x % DRING])[hl]);
+            const uint32_t* ring = reinterpret_cast<const uint32_t*>(L.ring[1]);
+            if (xl) st_cc64(hb_out + (size_t)(x - 1) * 32 + hl, tag | ring[((x + DRING - 1) & (DRING - 1)) * 32 + hl]);
+            if (xr) st_cc64(hb_out + (size_t)x * 32 + hl, tag | ring[(x & (DRING - 1)) * 32 + hl]);
         }
         // ---- carry the right 4 columns into the left strip of the next tile
-        if (act) {
 #pragma unroll
-            for (int it = 0; it < 2; ++it) {
-                const int e = hl + 32 * it;
-                if (e < 20) S.lt[e * 5] = S.lt[e * 5 + 4];
-                else if (e < 44) { const int k = e - 20, pl = k / 12, i = k - pl * 12; S.ct[pl][i * 3] = S.ct[pl][i * 3 + 2]; }
-            }
-        }
+        for (int it = 0; it < 2; ++it)
+            if (cy_dst[it] >= 0) Sw[cy_dst[it]] = Sw[cy_src[it]];
         wave_sync();
         TRACE({ unsigned long long t2 = __builtin_amdgcn_s_memtime(); tph[3] += t2 - tm; })
     }

@@ -149,8 +149,8 @@ DEV void db_info_mb(const h264r_batch& b, const Geom& g, int pic, int a, int lan
     }
 }
 
-constexpr int LP = 20;    // luma tile: rows -4..15 x cols -4..15, 5 dwords per row
-constexpr int CP = 12;    // chroma tile: rows -4..7 x cols -4..7, 3 dwords per row
+constexpr int TP = 5;     // tile pitch in dwords: left margin + 16 samples
+constexpr int TR = 20;    // tile rows: -4..15 (chroma uses -4..7)
 
 // Bottom rows of one MB for the row below: luma rows 12..15 (4 x 4 dwords) and
 // chroma rows 4..7 (2 planes x 4 x 2 dwords) -- 128 bytes, one cache line.
@@ -160,92 +160,107 @@ struct alignas(16) RingEntry {
 };
 static_assert(sizeof(RingEntry) == 128, "RingEntry is one 128-B line");
 
-// One MB row's working set in LDS: the MB being filtered plus its 4-sample
-// left/top margins, and its deblocking record.
+// One MB row's working set in LDS: three tiles of identical geometry (Y, Cb, Cr;
+// [row + 4][dword], dword 0 = the 4 samples left of the MB) and the MB's DbInfo.
+// The shared geometry lets luma and chroma lanes run the same instructions.
 struct alignas(16) DbLds {
-    uint32_t lt[20 * 5];          // luma tile, [row + 4][dword]
-    uint32_t ct[2][12 * 3];       // chroma tiles
-    uint32_t info[DBINFO_DWORDS]; // the MB's DbInfo
+    uint32_t t[3][TR * TP];
+    uint32_t info[DBINFO_DWORDS];
+    uint32_t zero;                // bS 0 of the edges a chroma line does not have
 };
 
-DEV uint8_t* ltb(DbLds& S) { return reinterpret_cast<uint8_t*>(S.lt); }
-DEV uint8_t* ctb(DbLds& S, int pl) { return reinterpret_cast<uint8_t*>(S.ct[pl]); }
-
-// Filter one line held as packed bytes w[0..NE] (4 samples per dword; edge k sits
-// between dword k and dword k+1) across NE edges; edges are sequential because
-// neighbouring edges share samples (deblock.cc:459-485 per edge, :495-502 order).
-template <int NE>
-DEV void filter_line_packed(uint32_t (&w)[NE + 1], const uint8_t* bsrow, int seg, uint32_t par0, uint32_t pari,
-                            int chroma, int bsidx_step)
+// One edge of one line, branch-free (filter_strong / filter_normal,
+// deblock.cc:327-415, as chosen by filter_edge :459-485): s[i0-4..i0+3] are
+// p3..p0 q0..q3; bS 0 leaves the line unchanged.  `par` is the edge's
+// edge_word(); chroma lines use tc0 + 1 and never touch p1/q1 or the strong
+// 3-tap outputs.
+DEV void filter_edge_line(int& p3, int& p2, int& p1, int& p0, int& q0, int& q1, int& q2, int& q3, int bS,
+                          uint32_t par, bool chroma)
 {
-#pragma unroll
-    for (int k = 0; k < NE; ++k) {
-        const int bS = bsrow[k * bsidx_step * 4 + seg];
-        if (!bS) continue;
-        const uint32_t par = k == 0 ? par0 : pari;
-        const int alpha = par & 255, beta = (par >> 8) & 255;
-        const int tc0 = bS < 4 ? (int)((par >> (16 + 5 * (bS - 1))) & 31) : 0;
-        const uint32_t a = w[k], c = w[k + 1];
-        int p3 = a & 255, p2 = (a >> 8) & 255, p1 = (a >> 16) & 255, p0 = a >> 24;
-        int q0 = c & 255, q1 = (c >> 8) & 255, q2 = (c >> 16) & 255, q3 = c >> 24;
-        filter_samples(p3, p2, p1, p0, q0, q1, q2, q3, alpha, beta, bS, chroma, tc0);
-        w[k] = (uint32_t)p3 | ((uint32_t)p2 << 8) | ((uint32_t)p1 << 16) | ((uint32_t)p0 << 24);
-        w[k + 1] = (uint32_t)q0 | ((uint32_t)q1 << 8) | ((uint32_t)q2 << 16) | ((uint32_t)q3 << 24);
+    const int alpha = par & 255, beta = (par >> 8) & 255;
+    const int tc0 = (bS >= 1 && bS <= 3) ? (int)((par >> (11 + 5 * bS)) & 31) : 0;
+    const bool filt = bS != 0 && iabs(p0 - q0) < alpha && iabs(p1 - p0) < beta && iabs(q1 - q0) < beta;
+    const bool apb = iabs(p2 - p0) < beta, aqb = iabs(q2 - q0) < beta;
+    // bS < 4 (filter_normal)
+    const int tc = chroma ? tc0 + 1 : tc0 + (int)apb + (int)aqb;
+    const int delta = clip3(-tc, tc, ((q0 - p0) * 4 + (p1 - q1) + 4) >> 3);
+    const int avg = (p0 + q0 + 1) >> 1;
+    const int n_p0 = clip255(p0 + delta), n_q0 = clip255(q0 - delta);
+    const int n_p1 = (!chroma && apb) ? p1 + clip3(-tc0, tc0, (p2 + avg - p1 * 2) >> 1) : p1;
+    const int n_q1 = (!chroma && aqb) ? q1 + clip3(-tc0, tc0, (q2 + avg - q1 * 2) >> 1) : q1;
+    // bS == 4 (filter_strong)
+    const bool strong = iabs(p0 - q0) < ((alpha >> 2) + 2);
+    const bool sp = !chroma && apb && strong, sq = !chroma && aqb && strong;
+    const int s_p0 = sp ? (p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3 : (2 * p1 + p0 + q1 + 2) >> 2;
+    const int s_p1 = sp ? (p2 + p1 + p0 + q0 + 2) >> 2 : p1;
+    const int s_p2 = sp ? (2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3 : p2;
+    const int s_q0 = sq ? (p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3 : (2 * q1 + q0 + p1 + 2) >> 2;
+    const int s_q1 = sq ? (p0 + q0 + q1 + q2 + 2) >> 2 : q1;
+    const int s_q2 = sq ? (2 * q3 + 3 * q2 + q1 + q0 + p0 + 4) >> 3 : q2;
+    const bool is4 = bS == 4;
+    if (filt) {
+        p2 = is4 ? s_p2 : p2; p1 = is4 ? s_p1 : n_p1; p0 = is4 ? s_p0 : n_p0;
+        q0 = is4 ? s_q0 : n_q0; q1 = is4 ? s_q1 : n_q1; q2 = is4 ? s_q2 : q2;
     }
 }
 
 // The two filter passes of one MB on the LDS tiles: vertical edges with one lane per
 // sample row, then horizontal edges with one lane per column (filter_vertical /
-// filter_horizontal deblock.cc:488-535).  Lanes 0..15 luma, 16..31 chroma;
-// every lane of the wave calls (the passes are separated by wave_sync).
-DEV void filter_mb(DbLds& S, int lane, bool act)
+// filter_horizontal deblock.cc:488-535).  Lanes 0..15 luma lines, 16..31 chroma
+// lines (Cb 16..23, Cr 24..31) run the same 4-edge code: a chroma line has its
+// edges at samples 0 and 4 (chroma edge 1 takes the bS of luma edge 2,
+// StrengthIdx = pel << 1, deblock.cc:430-433, :460) and bS 0 on the other two.
+// Edges no lane of the wave filters are skipped.  Every lane of the wave calls.
+DEV void filter_mb(DbLds& S, int lane)
 {
-    const uint8_t* bs = reinterpret_cast<const uint8_t*>(S.info);
+    const bool luma = lane < 16;
+    const int pl = luma ? 0 : 1 + ((lane - 16) >> 3), li = luma ? lane : (lane - 16) & 7;
+    const int seg = luma ? li >> 2 : li >> 1;
+    uint32_t* T = S.t[pl];
+    uint8_t* Tb = reinterpret_cast<uint8_t*>(T);
+    const uint8_t* ib = reinterpret_cast<const uint8_t*>(S.info);
+    const int zoff = (int)(reinterpret_cast<const uint8_t*>(&S.zero) - ib);
+    // byte offsets of this line's bS per edge (before + hor * 16), parameter words
+    int bso[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) bso[k] = luma ? k * 4 + seg : (k == 0 ? seg : (k == 1 ? 8 + seg : -1));
+    const int pe = luma ? 8 : 11 + 3 * (pl - 1), pi = luma ? 10 : 13 + 3 * (pl - 1);
 #pragma unroll 1
     for (int hor = 0; hor < 2; ++hor) {
-        if (!act) {
-        } else if (lane < 16) {
-            uint32_t w[5];
-            uint8_t* lt = ltb(S);
-            if (!hor) {
+        int bsk[4];
+        uint32_t park[4];
 #pragma unroll
-                for (int d = 0; d < 5; ++d) w[d] = S.lt[(lane + 4) * 5 + d];
-            } else {
+        for (int k = 0; k < 4; ++k) {
+            bsk[k] = ib[bso[k] >= 0 ? bso[k] + hor * 16 : zoff];
+            park[k] = S.info[k == 0 ? pe + hor : pi];
+        }
+        int v[20];
+        if (!hor) {
 #pragma unroll
-                for (int d = 0; d < 5; ++d)
-                    w[d] = (uint32_t)lt[(4 * d) * LP + lane + 4] | ((uint32_t)lt[(4 * d + 1) * LP + lane + 4] << 8) |
-                           ((uint32_t)lt[(4 * d + 2) * LP + lane + 4] << 16) | ((uint32_t)lt[(4 * d + 3) * LP + lane + 4] << 24);
+            for (int d = 0; d < 5; ++d) {
+                const uint32_t w = T[(li + 4) * TP + d];
+#pragma unroll
+                for (int c = 0; c < 4; ++c) v[4 * d + c] = (w >> (8 * c)) & 255;
             }
-            filter_line_packed<4>(w, &bs[hor * 16], lane >> 2, S.info[8 + hor], S.info[10], 0, 1);
-            if (!hor) {
+        } else {
 #pragma unroll
-                for (int d = 0; d < 5; ++d) S.lt[(lane + 4) * 5 + d] = w[d];
-            } else {
+            for (int i = 0; i < 20; ++i) v[i] = Tb[i * TP * 4 + li + 4];
+        }
 #pragma unroll
-                for (int i = 1; i < 20; ++i) lt[i * LP + lane + 4] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
-            }
-        } else if (lane < 32) {
-            const int pl = (lane - 16) >> 3, r = (lane - 16) & 7;
-            uint32_t w[3];
-            uint8_t* ct = ctb(S, pl);
-            if (!hor) {
+        for (int k = 0; k < 4; ++k) {
+            if (!__any(bsk[k] != 0)) continue;
+            const int i0 = 4 * k + 4;
+            filter_edge_line(v[i0 - 4], v[i0 - 3], v[i0 - 2], v[i0 - 1], v[i0], v[i0 + 1], v[i0 + 2], v[i0 + 3],
+                             bsk[k], park[k], !luma);
+        }
+        if (!hor) {
 #pragma unroll
-                for (int d = 0; d < 3; ++d) w[d] = S.ct[pl][(r + 4) * 3 + d];
-            } else {
+            for (int d = 0; d < 5; ++d)
+                T[(li + 4) * TP + d] = (uint32_t)v[4 * d] | ((uint32_t)v[4 * d + 1] << 8) |
+                                       ((uint32_t)v[4 * d + 2] << 16) | ((uint32_t)v[4 * d + 3] << 24);
+        } else {
 #pragma unroll
-                for (int d = 0; d < 3; ++d)
-                    w[d] = (uint32_t)ct[(4 * d) * CP + r + 4] | ((uint32_t)ct[(4 * d + 1) * CP + r + 4] << 8) |
-                           ((uint32_t)ct[(4 * d + 2) * CP + r + 4] << 16) | ((uint32_t)ct[(4 * d + 3) * CP + r + 4] << 24);
-            }
-            // chroma edge 1 uses luma edge 2 (bsidx_step 2); StrengthIdx = pel << 1 (deblock.cc:460)
-            filter_line_packed<2>(w, &bs[hor * 16], r >> 1, S.info[11 + 3 * pl + hor], S.info[13 + 3 * pl], 1, 2);
-            if (!hor) {
-#pragma unroll
-                for (int d = 0; d < 3; ++d) S.ct[pl][(r + 4) * 3 + d] = w[d];
-            } else {
-#pragma unroll
-                for (int i = 1; i < 12; ++i) ct[i * CP + r + 4] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
-            }
+            for (int i = 1; i < 20; ++i) Tb[i * TP * 4 + li + 4] = (uint8_t)v[i];
         }
         wave_sync();
     }
