@@ -5,7 +5,8 @@ deblock) on MI355X, BASELINE.json's metric.
 A step = one h264r_decode_batch over a batch of synthetic pictures already
 resident in HBM (SURVEY 8(d) throughput mode: B independent pictures sharing a
 reference set).  Default workload: SURVEY config 3, 1080p (120x68 MBs) IPPP
-Main P pictures, B = 64.
+Main P pictures, B = 256 per GPU (about 2 GB of HBM: the order-dependent walks
+need many pictures in flight to fill 256 CUs).
 
 Multi-GPU (torchrun, one process per GPU): config 3 uses deblocking across the
 whole picture (disable_deblocking_filter_idc 0), which chains every MB of a
@@ -50,6 +51,7 @@ def cpu_baseline(cfg, refs, seconds: float):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import _oracle as O
     from h264r import synth
+    from h264r import dist as D
     L = O.lib()
     nmb = cfg.width_mbs * cfg.height_mbs
     t0 = time.perf_counter()
@@ -96,7 +98,7 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", type=int, default=3, choices=[2, 3, 4, 5])
-    ap.add_argument("--batch", type=int, default=0, help="pictures per GPU per step (default 64, 16 at 2160p)")
+    ap.add_argument("--batch", type=int, default=0, help="pictures per GPU per step (default 256, 64 at 2160p)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
@@ -119,12 +121,12 @@ def main() -> int:
 
     L = h264r.lib()
     W, H = CONFIG_SIZE[args.config]
-    nb = args.batch or (16 if args.config == 5 else 64)
+    nb = args.batch or (64 if args.config == 5 else 256)
     cfg = synth.default_cfg(L, args.config, W, H)
     nmb = W * H
 
     # inputs: this rank's stream of pictures (replicas: distinct picture indices per rank)
-    pics = [synth.picture(L, cfg, rank * nb + i) for i in range(nb)]
+    pics = [synth.picture(L, cfg, i) for i in D.picture_share(rank, world, nb)]
     refs = synth.refpics(L, cfg)
     rd = wr = 0
     for p in pics:
@@ -159,10 +161,7 @@ def main() -> int:
     dt = time.perf_counter() - t0
     kern = np.array(dec.last_timing())          # ms per step: inter, intra, deblock, whole batch
     dec.set_timing(False)
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+    dt = D.max_over_ranks(dt, device="cuda")
 
     verified = None
     if not args.no_verify and rank == 0:
