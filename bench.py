@@ -113,6 +113,7 @@ def main() -> int:
     import h264r
     from h264r import batch as B
     from h264r import synth
+    from h264r import dist as D
 
     torch.cuda.set_device(local)
     if world > 1:
