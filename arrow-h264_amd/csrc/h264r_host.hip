@@ -24,7 +24,10 @@
 namespace h264r { struct DbInfo; }
 extern "C" __global__ void k_prep(h264r_batch b, uint2* mot);
 extern "C" __global__ void k_inter(h264r_batch b, const uint2* mot, h264r::DbInfo* dbinfo);
-extern "C" __global__ void k_intra_pic(h264r_batch b, int* sync, int* err);
+extern "C" __global__ void k_intra_pic(h264r_batch b, int* sync, int* err, const uint16_t* lvl, int lmax);
+extern "C" __global__ void k_level(h264r_batch b, uint16_t* lvl, int* lvsync);
+extern "C" __global__ void k_intra_levels(h264r_batch b, const uint16_t* lvl, int lmax, int* lvsync, int* err);
+constexpr int LEVEL_MAX_MBS = 65536;      // k_level's LDS bitmap (k_picture.hip)
 extern "C" __global__ void k_deblock(h264r_batch b, const h264r::DbInfo* dbinfo, uint64_t* hb,
                                      int* sync, int* err, uint32_t epoch);
 constexpr size_t DBINFO_BYTES = 80;
@@ -111,6 +114,8 @@ struct h264r_ctx {
     uint8_t* d_hb = nullptr; size_t c_hb = 0;
     uint32_t epoch = 0;             // tag of the deblocking hand-off records of the last launch
     uint2* d_mot = nullptr; size_t c_mot = 0;
+    uint16_t* d_lvl = nullptr; size_t c_lvl = 0;   // intra dependency level per MB
+    int levels_grid = 0;                           // resident workgroups of k_intra_levels
     // pipelining: prep+inter on the caller's stream, intra and deblocking of each
     // chunk of pictures on two more streams, chained by events
     hipStream_t aux[2] = {};
@@ -226,7 +231,7 @@ int h264r_destroy(h264r_ctx* c)
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (int s = 0; s < H264R_MAX_SLOTS; ++s) if (c->slot[s][0]) (void)hipFree(c->slot[s][0]);
-    void* bufs[] = {c->d_ref_planes, c->d_err, c->d_dbinfo, c->d_sync, c->d_hb, c->d_mot, c->d_mbs, c->d_levels, c->d_mv, c->d_ref, c->d_slices, c->d_pic, c->d_quant, c->d_out};
+    void* bufs[] = {c->d_ref_planes, c->d_err, c->d_dbinfo, c->d_sync, c->d_hb, c->d_mot, c->d_lvl, c->d_mbs, c->d_levels, c->d_mv, c->d_ref, c->d_slices, c->d_pic, c->d_quant, c->d_out};
     for (void* b : bufs) if (b) (void)hipFree(b);
     for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->ev_chain) (void)hipEventDestroy(e);
@@ -331,6 +336,16 @@ static int chunk_pictures(int P)
     return env > 0 ? env : P;
 }
 
+// Intra MBs are scheduled by dependency level (k_level, then k_intra_levels does levels
+// 1..N in one persistent launch); the wavefront walk k_intra_pic takes whatever lies deeper.  In P/B
+// pictures the deepest level is a handful; in all-intra pictures most MBs are deeper
+// than N and the walk does them.  H264R_LEVELS=<N> overrides (0: walk only).
+static int level_launches()
+{
+    static const int env = [] { const char* e = getenv("H264R_LEVELS"); return e ? atoi(e) : 16; }();
+    return std::max(0, std::min(env, 256));
+}
+
 static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s)
 {
     const int W = b.width_mbs, H = b.height_mbs, P = b.num_pics;
@@ -357,6 +372,18 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s)
     const size_t mplane = (size_t)W * 4 * H * 4;
     if ((st = dev_resize(&c->d_mot, &c->c_mot, (size_t)P * 2 * mplane))) return st;
     if ((st = dev_resize(&c->d_sync, &c->c_sync, (size_t)K * sync_chunk))) return st;
+    const bool levels = (size_t)W * H <= LEVEL_MAX_MBS && H <= 1024 && level_launches() > 0 &&
+                        !(c->debug & H264R_DBG_INTRA_WALK);
+    if (levels && !c->levels_grid) {
+        // every workgroup of the persistent level kernel must be resident at once: one
+        // block per CU below what the occupancy query reports (MI355X_MICROARCH.md,
+        // residency caveat), at least one per CU
+        int per_cu = 0, cus = 0;
+        HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(k_intra_levels), 256, 0));
+        HIP_OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
+        c->levels_grid = std::max(1, per_cu - 1) * std::max(1, cus);
+    }
+    if (levels && (st = dev_resize(&c->d_lvl, &c->c_lvl, (size_t)P * W * H))) return st;
     while ((int)c->ev_chain.size() < 2 * K) {
         hipEvent_t e = nullptr;
         HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -388,7 +415,18 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s)
         }
         {
             Timed t(c, 1, si);
-            hipLaunchKernelGGL(k_intra_pic, dim3(n * nbands), dim3(1024), 0, si, cb, sync, c->d_err);
+            uint16_t* lvl = levels ? c->d_lvl + (size_t)p0 * W * H : nullptr;
+            const int lmax = levels ? level_launches() : 0;
+            if (levels) {
+                int* lvsync = sync + 1 + (size_t)CP * H + 2;
+                hipLaunchKernelGGL(k_level, dim3(n), dim3(64 * ((H + 63) / 64)), 0, si, cb, lvl, lvsync);
+                HIP_OK(hipGetLastError());
+                hipLaunchKernelGGL(k_intra_levels, dim3(c->levels_grid), dim3(256), 0, si, cb, (const uint16_t*)lvl,
+                                   lmax, lvsync, c->d_err);
+                HIP_OK(hipGetLastError());
+            }
+            hipLaunchKernelGGL(k_intra_pic, dim3(n * nbands), dim3(1024), 0, si, cb, sync, c->d_err,
+                               (const uint16_t*)lvl, lmax);
             HIP_OK(hipGetLastError());
         }
         if (K > 1) {
@@ -587,3 +625,22 @@ int h264r_picture_end(h264r_ctx* c, uint8_t* y, uint8_t* u, uint8_t* v, int keep
 }
 
 }  // extern "C"
+
+#ifdef H264R_TRACE_INTRA
+// Diagnostic build only: copy the per-MB timing trace of k_intra_levels to the host.
+extern "C" __global__ void k_intra_trace_dump(unsigned long long* out, unsigned* n);
+extern "C" int h264r_trace_intra_dump(unsigned long long* out_host, unsigned* n_host)
+{
+    unsigned long long* d = nullptr;
+    unsigned* dn = nullptr;
+    HIP_OK(hipDeviceSynchronize());
+    HIP_OK(hipMalloc(&d, (size_t(1) << 20) * 32));
+    HIP_OK(hipMalloc(&dn, 4));
+    hipLaunchKernelGGL(k_intra_trace_dump, dim3(256), dim3(256), 0, nullptr, d, dn);
+    HIP_OK(hipDeviceSynchronize());
+    HIP_OK(hipMemcpy(n_host, dn, 4, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(out_host, d, (size_t)*n_host * 32, hipMemcpyDeviceToHost));
+    (void)hipFree(d); (void)hipFree(dn);
+    return 0;
+}
+#endif

@@ -14,7 +14,12 @@
 // tickets in band-major order from an atomic counter, so every workgroup only
 // ever waits on a ticket taken earlier by a resident workgroup: no deadlock
 // whatever the dispatch order or residency.  Every wait is bounded.
-#include "mb_recon.h"
+#include "mb_intra.h"
+
+#ifndef H264R_LVL_WAVES
+#define H264R_LVL_WAVES 4
+#endif
+#define H264R_LEVEL_MAX_MBS 65536           // k_level keeps a picture's intra bitmap in LDS
 
 using namespace h264r;
 
@@ -60,7 +65,7 @@ DEV bool wait_for(int* counter, int need, int* err)
 // sync: [0] ticket counter, [1 ..] per (picture, row) progress; zeroed before every launch.
 template <typename Scratch>
 DEV void picture_walk(const h264r_batch& b, int* sync, int* err, Scratch* scratch,
-                      int* lprog, int* ticket_lds)
+                      int* lprog, int* ticket_lds, const uint16_t* __restrict__ lvl, int lmax)
 {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const Geom g = make_geom(b.width_mbs, b.height_mbs);
@@ -84,6 +89,7 @@ DEV void picture_walk(const h264r_batch& b, int* sync, int* err, Scratch* scratc
     // k_inter).  Progress of a row = index of its first intra MB not yet done (W when
     // none is left): MB x may start once the row above has progress >= x + 2.
     const h264r_mb* row = mbs + (size_t)r * g.wmb;
+    const uint16_t* lrow = lvl ? lvl + (size_t)pic * g.nmb + (size_t)r * g.wmb : nullptr;
     auto next_intra = [&](int from) -> int {
         for (int c = from & ~63; c < g.wmb; c += 64) {
             const int m = c + lane;
@@ -91,6 +97,7 @@ DEV void picture_walk(const h264r_batch& b, int* sync, int* err, Scratch* scratc
             if (m >= from && m < g.wmb) {
                 const uint32_t w0 = *reinterpret_cast<const uint32_t*>(&row[m]);
                 in = ((w0 >> 8) & H264R_MBF_INTRA) && (w0 & 255) != H264R_I_PCM;
+                if (lrow && lrow[m] <= lmax) in = false;      // done by k_intra_lvl
             }
             const uint64_t bits = __ballot(in);
             if (bits) return c + __builtin_ctzll(bits);
@@ -110,17 +117,169 @@ DEV void picture_walk(const h264r_batch& b, int* sync, int* err, Scratch* scratc
             else ok = wait_for<false>(&lprog[wave - 1], need, err);
         }
         if (!ok) break;
-        intra_mb(b, g, pic, x, r, lane, S);
+        intra_mb2(b, g, pic, x, r, lane, S);
         x = next_intra(x + 1);
         publish(x);
     }
     if (!ok) publish(g.wmb);   // let every waiter behind a failed wave finish (outputs are flagged invalid)
 }
 
-extern "C" __global__ __launch_bounds__(1024) void k_intra_pic(h264r_batch b, int* sync, int* err)
+// lvl / lmax: intra MBs with lvl <= lmax were reconstructed by the k_intra_lvl
+// launches before this one (lvl == nullptr: the walk does every intra MB).
+extern "C" __global__ __launch_bounds__(1024) void k_intra_pic(h264r_batch b, int* sync, int* err,
+                                                              const uint16_t* lvl, int lmax)
 {
-    __shared__ IntraLds scratch[WAVES];
+    __shared__ IntraScratch scratch[WAVES];
     __shared__ int lprog[WAVES];
     __shared__ int ticket;
-    picture_walk(b, sync, err, scratch, lprog, &ticket);
+    picture_walk(b, sync, err, scratch, lprog, &ticket, lvl, lmax);
+}
+
+// ------------------------------------------------------------ level schedule
+// An intra MB reads the unfiltered samples of its neighbours A (x-1,y), B (x,y-1),
+// C (x+1,y-1) and D (x-1,y-1) (intra_prediction.cc:140-186, 683-695, 806-823).
+// Inter and I_PCM MBs are final after k_inter, so only intra -> intra edges
+// order the work: level(MB) = 0 for inter / I_PCM, else 1 + max(level of A, B, C,
+// D) (out of picture = 0).  Every MB of level L depends only on levels < L, so
+// one launch per level needs no in-kernel synchronisation at all.  In P / B
+// pictures (10 % intra MBs) the deepest chain is a handful of levels; in all-intra
+// pictures level(x, y) = x + 2y + 1 and the levels beyond `lmax` fall back to the
+// wavefront walk (k_intra_pic).  Slice boundaries are ignored here: that can only
+// raise a level, never break an order.
+//
+// k_level: one workgroup per picture, thread r = MB row r, which walks its row in
+// lock step: at step t thread r does MB x = t - 2r, after (x+1, r-1) was done at
+// step t-1.  Each row keeps its last four levels in an LDS ring.
+extern "C" __global__ __launch_bounds__(1024) void k_level(h264r_batch b, uint16_t* lvl, int* lvsync)
+{
+    __shared__ uint64_t bits[H264R_LEVEL_MAX_MBS / 64];   // intra (not PCM) MBs of the picture
+    __shared__ uint16_t ring[1024][4];
+    const Geom g = make_geom(b.width_mbs, b.height_mbs);
+    const int pic = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+    const h264r_mb* mbs = b.mbs + (size_t)pic * g.nmb;
+    for (int base = 0; base < g.nmb; base += blockDim.x) {
+        const int m = base + tid;
+        bool in = false;
+        if (m < g.nmb) {
+            const uint32_t w0 = *reinterpret_cast<const uint32_t*>(&mbs[m]);
+            in = ((w0 >> 8) & H264R_MBF_INTRA) && (w0 & 255) != H264R_I_PCM;
+        }
+        const uint64_t bl = __ballot(in);
+        if (lane == 0 && m < g.nmb) bits[(base + tid) >> 6] = bl;
+    }
+    __syncthreads();
+    const int r = tid;
+    uint16_t* out = lvl + (size_t)pic * g.nmb + (size_t)r * g.wmb;
+    int left = 0, deepest = 0;
+    const int steps = g.wmb + 2 * (g.hmb - 1);
+    for (int t = 0; t < steps; ++t) {
+        const int x = t - 2 * r;
+        if (r < g.hmb && x >= 0 && x < g.wmb) {
+            const int m = r * g.wmb + x;
+            int L = 0;
+            if ((bits[m >> 6] >> (m & 63)) & 1) {
+                int up = 0;
+                if (r > 0) {
+                    up = ring[r - 1][x & 3];
+                    if (x > 0) up = max(up, (int)ring[r - 1][(x - 1) & 3]);
+                    if (x + 1 < g.wmb) up = max(up, (int)ring[r - 1][(x + 1) & 3]);
+                }
+                L = 1 + max(up, left);
+            }
+            left = L;
+            deepest = max(deepest, L);
+            ring[r][x & 3] = (uint16_t)L;
+            out[x] = (uint16_t)L;
+        }
+        __syncthreads();
+    }
+    for (int d = 32; d >= 1; d >>= 1) deepest = max(deepest, __shfl_xor(deepest, d));
+    if (lane == 0 && deepest) atomicMax(&lvsync[1], deepest);
+}
+
+// k_intra_levels: the intra MBs of levels 1..min(lmax, deepest level), one level
+// after the other inside one persistent launch (a launch per level would pay a cold
+// instruction cache on every CU each time).  Every workgroup must be resident: the
+// host sizes the grid from the occupancy query.  Levels are separated by a grid
+// barrier (MI355X_MICROARCH.md price list 'barrier-counter': stores drained, agent
+// release, one counter, agent acquire).  Each wave scans 64 MBs at a time,
+// grid-stride, and reconstructs the ones at the current level one after the other.
+// lvsync: [0] barrier counter, [1] deepest level (k_level), both zeroed per batch.
+DEV bool grid_barrier(int* bar, int target, int* err)
+{
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    __shared__ int ok;
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_fetch_add(bar, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        unsigned spins = 0;
+        ok = 1;
+        while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            __builtin_amdgcn_s_sleep(2);
+            if (++spins > SPIN_LIMIT) {
+                __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ok = 0;
+                break;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    return ok;
+}
+
+#ifdef H264R_TRACE_INTRA
+__device__ unsigned long long h264r_intra_trace[1 << 20][4];
+__device__ unsigned h264r_intra_trace_n;
+extern "C" __global__ void k_intra_trace_dump(unsigned long long* out, unsigned* n)
+{
+    const unsigned cnt = h264r_intra_trace_n < (1u << 20) ? h264r_intra_trace_n : (1u << 20);
+    for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += gridDim.x * blockDim.x)
+        for (int j = 0; j < 4; ++j) out[i * 4 + j] = h264r_intra_trace[i][j];
+    if (blockIdx.x == 0 && threadIdx.x == 0) *n = cnt;
+}
+#endif
+
+extern "C" __global__ __launch_bounds__(256, H264R_LVL_WAVES) void k_intra_levels(h264r_batch b, const uint16_t* __restrict__ lvl,
+                                                                                int lmax, int* lvsync, int* err)
+{
+    __shared__ IntraScratch scratch[4];
+    const Geom g = make_geom(b.width_mbs, b.height_mbs);
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const size_t total = (size_t)g.nmb * b.num_pics;
+    const size_t gw = (size_t)blockIdx.x * 4 + wave, step = (size_t)gridDim.x * 4 * 64;
+    const int deepest = __hip_atomic_load(&lvsync[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int top = min(lmax, deepest);
+    for (int L = 1; L <= top; ++L) {
+        for (size_t base = gw * 64; base < total; base += step) {
+            const size_t e = base + lane;
+            const bool hit = e < total && lvl[e] == L;
+            uint64_t todo = __ballot(hit);
+            while (todo) {
+                const size_t k = base + __builtin_ctzll(todo);
+                todo &= todo - 1;
+                const int pic = (int)(k / g.nmb), a = (int)(k % g.nmb);
+#ifdef H264R_TRACE_INTRA
+                const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+#endif
+                intra_mb2(b, g, pic, a % g.wmb, a / g.wmb, lane, scratch[wave]);
+#ifdef H264R_TRACE_INTRA
+                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+                const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+                if (lane == 0) {
+                    const unsigned slot = atomicAdd(&h264r_intra_trace_n, 1u);
+                    if (slot < (1u << 20)) {
+                        h264r_intra_trace[slot][0] = t0; h264r_intra_trace[slot][1] = t1;
+                        h264r_intra_trace[slot][2] = ((unsigned long long)L << 32) | (unsigned)(b.mbs[k].mb_type);
+                        h264r_intra_trace[slot][3] = (unsigned long long)gw;
+                    }
+                }
+#endif
+            }
+        }
+        if (L < top && !grid_barrier(&lvsync[0], L * (int)gridDim.x, err)) return;
+    }
 }

@@ -1,0 +1,477 @@
+// mb_intra.h -- one intra macroblock per 64-lane wave (used by the level-scheduled
+// k_intra_lvl and by the wavefront walk k_intra_pic).
+//
+//   Decoder::mb_pred_intra decoder.cc:170-208
+//   IntraPrediction::intra_pred_{4x4,8x8,16x16,chroma} intra_prediction.cc:34-904
+//   Transform::inverse_transform_{4x4,8x8,16x16,chroma} transform.cc:986-1049,
+//   inverse_4x4 :597-641, inverse_8x8 :643-733, DC transforms :825-889.
+//
+// Structure (latency is what matters: the MBs of one dependency level run in
+// parallel, each as a short chain of wave-synchronous steps):
+//   1. every global load is issued up front: the MB record, the four neighbour
+//      records (availability), the neighbour samples (row above x = -4..23,
+//      column left, chroma likewise), the levels and scales;
+//   2. the residual is computed in registers (lane = 4x4 block * 4 + row, four
+//      samples per lane; rows in-lane, columns across the quad by DPP) -- the
+//      8x8 transform goes through LDS;
+//   3. I_16x16 and chroma predict in that same layout and store straight to the
+//      picture; I_4x4 walks its 16 blocks as a wavefront over the block grid
+//      (block (bx,by) at step bx + 2by: 10 steps, two blocks per step, one sample
+//      per lane), I_8x8 its 4 blocks in order (one sample per lane);
+//   4. every directional NxN mode is evaluated in one form: the neighbours along
+//      the edge form a 1-D array e[] (left column bottom-up, corner, top row),
+//      and each sample is a copy, a 2-tap or a [1,2,1] filter at an index of e[]
+//      that depends on (mode, x, y) only (intra_nxn_tap below; spec 8.3.1.2.x /
+//      8.3.2.2.x, intra_prediction.cc:189-346, 449-606).
+#pragma once
+#include "mb_inter.h"
+
+namespace h264r {
+
+constexpr int ITP = 32;   // luma tile pitch: x = -4..27 at byte x + 4, row y = -1..15 at (y + 1) * ITP
+constexpr int ICP = 16;   // chroma tile pitch: x = -4..11
+
+struct IntraScratch {
+    alignas(16) uint8_t tile[17 * ITP];
+    alignas(16) uint8_t ctile[2][9 * ICP];
+    alignas(16) int res[16][16];          // luma residual (I_4x4 / I_8x8)
+    alignas(16) uint8_t fs[32];           // I_8x8 filtered neighbours: [3] Q, [4 + x] T[x], [20 + y] L[y]
+};
+
+DEV int ti(int x, int y) { return (y + 1) * ITP + x + 4; }          // luma tile index
+DEV int ci(int x, int y) { return (y + 1) * ICP + x + 4; }          // chroma tile index
+
+// (kind, index) of prediction sample (x, y) of an NxN block in directional mode
+// `mode` (not DC): kind 0 = e[i], 1 = (e[i] + e[i+1] + 1) >> 1,
+// 2 = (e[i-1] + 2 e[i] + e[i+1] + 2) >> 2.  e[] (3N + 3 entries): e[N - k] = L[k]
+// (left column, k = 0..N-1), e[0] = L[N-1] again, e[N+1] = Q (corner),
+// e[N+2+k] = T[k] (row above, k = 0..2N-1), e[3N+2] = T[2N-1] again -- the
+// repeated ends give the (a + 3b + 2) >> 2 corner cases of modes 3 and 8.
+template <int N>
+DEV void intra_nxn_tap(int mode, int x, int y, int& kind, int& i)
+{
+    switch (mode) {
+    case 0: kind = 0; i = N + 2 + x; return;                                  // vertical
+    case 1: kind = 0; i = N - y; return;                                      // horizontal
+    case 3: kind = 2; i = N + 3 + x + y; return;                              // diagonal down left
+    case 4: kind = 2; i = N + 1 + x - y; return;                              // diagonal down right
+    case 5: {                                                                 // vertical right
+        const int z = 2 * x - y;
+        if (z >= 0) { kind = (z & 1) ? 2 : 1; i = N + 1 + x - (y >> 1); }
+        else if (z == -1) { kind = 2; i = N + 1; }
+        else { kind = 2; i = N + 2 + 2 * x - y; }
+        return;
+    }
+    case 6: {                                                                 // horizontal down
+        const int z = 2 * y - x;
+        if (z >= 0) { if (z & 1) { kind = 2; i = N + 1 - y + (x >> 1); } else { kind = 1; i = N - y + (x >> 1); } }
+        else if (z == -1) { kind = 2; i = N + 1; }
+        else { kind = 2; i = N + x - 2 * y; }
+        return;
+    }
+    case 7:                                                                   // vertical left
+        if (y & 1) { kind = 2; i = N + 3 + x + (y >> 1); } else { kind = 1; i = N + 2 + x + (y >> 1); }
+        return;
+    default: {                                                                // horizontal up
+        const int z = x + 2 * y;
+        if (z < 2 * N - 3) { kind = (z & 1) ? 2 : 1; i = N - 1 - y - (x >> 1); }
+        else if (z == 2 * N - 3) { kind = 2; i = 1; }
+        else { kind = 0; i = 1; }
+        return;
+    }
+    }
+}
+
+// The (kind, i) of intra_nxn_tap for all 9 modes at one sample position, packed one
+// byte per mode (i | kind << 5; DC entries unused), so a step looks its entry up with
+// a shift instead of branching over the modes.
+template <int N>
+DEV void intra_tap_table(int x, int y, uint32_t (&t)[3])
+{
+    t[0] = t[1] = t[2] = 0;
+#pragma unroll
+    for (int md = 0; md < 9; ++md) {
+        if (md == 2) continue;
+        int kind, i;
+        intra_nxn_tap<N>(md, x, y, kind, i);
+        t[md >> 2] |= (uint32_t)(i | (kind << 5)) << (8 * (md & 3));
+    }
+}
+DEV int intra_tap_entry(const uint32_t (&t)[3], int mode)
+{
+    const uint32_t w = mode < 4 ? t[0] : (mode < 8 ? t[1] : t[2]);
+    return (w >> (8 * (mode & 3))) & 255;
+}
+
+DEV int tap_apply(int kind, int a, int b, int c)
+{
+    return kind == 2 ? (a + 2 * b + c + 2) >> 2 : (kind == 1 ? (b + c + 1) >> 1 : b);
+}
+
+DEV uint32_t lds_u32(const uint8_t* p) { return *reinterpret_cast<const uint32_t*>(p); }
+DEV int sum4(uint32_t w) { return (int)__builtin_amdgcn_sad_u8(w, 0u, 0u); }   // sum of the 4 bytes
+
+// Chroma residual of one MB in the inter_mb2 lane layout (transform.cc:875-889 DC,
+// inverse_4x4 for the AC blocks): lane = plane << 5 | blk << 3 | half << 2 | row,
+// two samples (cols 2*half, +1).  `tab` = 0 intra, 1 inter scale tables.
+DEV void chroma_res2(const h264r_mb& m, const int16_t* __restrict__ lv, const h264r_quant* __restrict__ q, int tab,
+                     int lane, int (&resC)[2])
+{
+    const int cpl = lane >> 5, cb = (lane >> 3) & 3, chalf = (lane >> 2) & 1, crow = lane & 3;
+    const int cbpc = m.cbp >> 4;
+    resC[0] = resC[1] = 0;
+    if (!cbpc) return;
+    const LevelOffs lo = level_offsets(m);
+    const int qpc = m.qp_scaled[1 + cpl], per = qpc / 6;
+    const uint2 cdc = ld8(lv + lo.cdc + cpl * 4);
+    const int cdc_scale = q->scale4x4[tab][1 + cpl][qpc % 6][0];
+    int k0 = 0, k1 = 0;
+    if (cbpc == 2) {
+        const uint32_t clev = *reinterpret_cast<const uint32_t*>(lv + lo.cac + cpl * 64 + cb * 16 + crow * 4 + chalf * 2);
+        const uint32_t csc = *reinterpret_cast<const uint32_t*>(&q->scale4x4[tab][1 + cpl][qpc % 6][crow * 4 + chalf * 2]);
+        k0 = dq4((int16_t)(clev & 0xFFFF), (int16_t)(csc & 0xFFFF), per);
+        k1 = dq4((int16_t)(clev >> 16), (int16_t)(csc >> 16), per);
+    }
+    const int c00 = (int16_t)(cdc.x & 0xFFFF), c01 = (int16_t)(cdc.x >> 16);
+    const int c10 = (int16_t)(cdc.y & 0xFFFF), c11 = (int16_t)(cdc.y >> 16);
+    const int e00 = c00 + c01, e01 = c00 - c01, e10 = c10 + c11, e11 = c10 - c11;
+    const int f = cb == 0 ? e00 + e10 : cb == 1 ? e01 + e11 : cb == 2 ? e00 - e10 : e01 - e11;
+    if (crow == 0 && chalf == 0) k0 = ((f * cdc_scale) * (1 << per)) >> 5;
+    const int o0 = __shfl_xor(k0, 4), o1 = __shfl_xor(k1, 4);
+    const int d0 = chalf ? o0 : k0, d1 = chalf ? o1 : k1, d2 = chalf ? k0 : o0, d3 = chalf ? k1 : o1;
+    int t[4];
+    idct4(d0, d1, d2, d3, t[0], t[1], t[2], t[3]);
+    const int u0 = chalf ? t[2] : t[0], u1 = chalf ? t[3] : t[1];
+    resC[0] = idct4_col_row(quad_bcast<0>(u0), quad_bcast<1>(u0), quad_bcast<2>(u0), quad_bcast<3>(u0), crow);
+    resC[1] = idct4_col_row(quad_bcast<0>(u1), quad_bcast<1>(u1), quad_bcast<2>(u1), quad_bcast<3>(u1), crow);
+}
+
+// Luma residual of an I_4x4 / I_16x16 MB in registers: lane = blk * 4 + row (blk
+// raster over the 4x4 block grid), four samples.  I_16x16 DC: 4x4 Hadamard and
+// scaling of transform_luma_dc (transform.cc:825-856), evaluated per lane.
+DEV void luma_res4_intra(const h264r_mb& m, const int16_t* __restrict__ lv, const h264r_quant* __restrict__ q,
+                         int lane, int (&res)[4])
+{
+    const int blk = lane >> 2, r = lane & 3, bx = blk & 3, by = blk >> 2;
+    const int qp = m.qp_scaled[0], per = qp / 6, rem = qp % 6;
+    const bool i16 = m.mb_type == H264R_I_16x16;
+    const int loff = b8_offset(m.cbp, (by >> 1) * 2 + (bx >> 1));
+    uint2 lev = make_uint2(0, 0), sc = make_uint2(0, 0);
+    if (loff >= 0) {
+        lev = ld8(lv + loff + ((by & 1) * 2 + (bx & 1)) * 16 + r * 4);
+        sc = ld8(&q->scale4x4[0][0][rem][r * 4]);
+    }
+    int d[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const int l = (int16_t)((c & 2 ? lev.y : lev.x) >> (16 * (c & 1)));
+        const int s = (int16_t)((c & 2 ? sc.y : sc.x) >> (16 * (c & 1)));
+        d[c] = dq4(l, s, per);
+    }
+    if (i16) {
+        const int16_t* p = lv + level_offsets(m).ldc;     // 16 DC levels, raster, wave-uniform
+        const int mx = (0xA6C0 >> (4 * bx)) & 15, my = (0xA6C0 >> (4 * by)) & 15;   // Hadamard sign masks
+        int f = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            int s = 0;
+#pragma unroll
+            for (int l = 0; l < 4; ++l) s += ((mx >> l) & 1) ? -p[4 * k + l] : p[4 * k + l];
+            f += ((my >> k) & 1) ? -s : s;
+        }
+        const int scale = q->scale4x4[0][0][rem][0];
+        const int dc = qp >= 36 ? (f * scale) * (1 << (per - 6)) : (f * scale + (1 << (5 - per))) >> (6 - per);
+        if (r == 0) d[0] = dc;
+    }
+    int t[4];
+    idct4(d[0], d[1], d[2], d[3], t[0], t[1], t[2], t[3]);
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+        res[c] = idct4_col_row(quad_bcast<0>(t[c]), quad_bcast<1>(t[c]), quad_bcast<2>(t[c]), quad_bcast<3>(t[c]), r);
+}
+
+// Luma residual of an I_8x8 MB (inverse_8x8, transform.cc:643-733) into S.res.
+DEV void luma_res8_intra(const h264r_mb& m, const int16_t* __restrict__ lv, const h264r_quant* __restrict__ q,
+                         int lane, IntraScratch& S)
+{
+    const int k = lane >> 4, row = (lane >> 1) & 7, half = lane & 1;
+    const int qp = m.qp_scaled[0], per = qp / 6, rem = qp % 6;
+    const int off = b8_offset(m.cbp, k);
+    int d[4] = {0, 0, 0, 0};
+    if (off >= 0) {
+        const uint2 lev = ld8(lv + off + row * 8 + half * 4);
+        const uint2 sc = ld8(&q->scale8x8[0][0][rem][row * 8 + half * 4]);
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+            d[c] = dq8((int16_t)((c & 2 ? lev.y : lev.x) >> (16 * (c & 1))),
+                       (int16_t)((c & 2 ? sc.y : sc.x) >> (16 * (c & 1))), per);
+    }
+    // row pass: the other half of my row is in lane ^ 1
+    int in[8], out[8];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const int o = __shfl_xor(d[c], 1);
+        in[c] = half ? o : d[c];
+        in[4 + c] = half ? d[c] : o;
+    }
+    idct8(in, out);
+    int* dst = &S.res[(k >> 1) * 8 + row][(k & 1) * 8 + half * 4];
+    *reinterpret_cast<int4*>(dst) = make_int4(out[half * 4], out[half * 4 + 1], out[half * 4 + 2], out[half * 4 + 3]);
+    wave_sync();
+    // column pass: lane = k * 16 + col * 2 + hv, outputs rows hv*4 .. hv*4 + 3
+    {
+        const int col = (lane >> 1) & 7, hv = lane & 1;
+        const int x = (k & 1) * 8 + col, y0 = (k >> 1) * 8;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) in[i] = S.res[y0 + i][x];
+        idct8(in, out);
+        wave_sync();                                   // every lane has read its column
+#pragma unroll
+        for (int i = 0; i < 4; ++i) S.res[y0 + hv * 4 + i][x] = (out[hv * 4 + i] + 32) >> 6;
+    }
+    wave_sync();
+}
+
+// Intra MB (mbx, mby) of picture `pic` (no-op for inter / I_PCM MBs); one wave.
+DEV void intra_mb2(const h264r_batch& b, const Geom& g, int pic, int mbx, int mby, int lane, IntraScratch& S)
+{
+    const int a = mby * g.wmb + mbx;
+    const h264r_mb* mbs = b.mbs + (size_t)pic * g.nmb;
+    const PicPtrs o = out_planes(b, g, pic);
+    const int X = mbx * 16, Y = mby * 16, Xc = mbx * 8, Yc = mby * 8;
+
+    // ---- neighbour samples: issued before anything else (in-picture addresses only;
+    // availability decides later which of them are used)
+    uint32_t nb = 0;
+    {
+        if (lane < 7) {                                   // row above, x = -4..23
+            const int x = X - 4 + 4 * lane;
+            if (mby > 0 && x >= 0 && x < g.W) nb = *reinterpret_cast<const uint32_t*>(o.y + (size_t)(Y - 1) * g.W + x);
+        } else if (lane < 23) {                           // left column
+            if (mbx > 0) nb = o.y[(size_t)(Y + lane - 7) * g.W + X - 1];
+        } else if (lane < 29) {                           // chroma rows above, x = -4..7
+            const int k = lane - 23, pl = k / 3, x = Xc - 4 + 4 * (k % 3);
+            if (mby > 0 && x >= 0) nb = *reinterpret_cast<const uint32_t*>((pl ? o.v : o.u) + (size_t)(Yc - 1) * g.Wc + x);
+        } else if (lane < 45) {                           // chroma left columns
+            const int k = lane - 29, pl = k >> 3;
+            if (mbx > 0) nb = (pl ? o.v : o.u)[(size_t)(Yc + (k & 7)) * g.Wc + Xc - 1];
+        }
+    }
+    const h264r_mb m = load_mb(&mbs[a]);
+    if (!mb_is_intra(m) || m.mb_type == H264R_I_PCM) return;
+    const int cip = b.pics[pic].constrained_intra_pred;
+    const int avA = nb_avail(mbs, g, m, cip, mbx - 1, mby), avB = nb_avail(mbs, g, m, cip, mbx, mby - 1);
+    const int avC = nb_avail(mbs, g, m, cip, mbx + 1, mby - 1), avD = nb_avail(mbs, g, m, cip, mbx - 1, mby - 1);
+    const int16_t* lv = b.levels + m.coef_off;
+    const h264r_quant* __restrict__ q = &b.quant[pic];
+    const bool i16 = m.mb_type == H264R_I_16x16, i8 = m.mb_type == H264R_I_8x8;
+
+    // ---- residual (registers; 8x8 via LDS)
+    int resL[4] = {0, 0, 0, 0}, resC[2];
+    if (!i8) luma_res4_intra(m, lv, q, lane, resL);
+    chroma_res2(m, lv, q, 0, lane, resC);
+
+    // ---- neighbours into the tiles
+    if (lane < 7) *reinterpret_cast<uint32_t*>(&S.tile[4 * lane]) = nb;
+    else if (lane < 23) S.tile[ti(-1, lane - 7)] = (uint8_t)nb;
+    else if (lane < 29) { const int k = lane - 23; *reinterpret_cast<uint32_t*>(&S.ctile[k / 3][4 * (k % 3)]) = nb; }
+    else if (lane < 45) { const int k = lane - 29; S.ctile[k >> 3][ci(-1, k & 7)] = (uint8_t)nb; }
+    if (i8) luma_res8_intra(m, lv, q, lane, S);        // includes wave_syncs
+    else if (!i16) {
+        const int blk = lane >> 2, r = lane & 3;
+        *reinterpret_cast<int4*>(&S.res[(blk >> 2) * 4 + r][(blk & 3) * 4]) = make_int4(resL[0], resL[1], resL[2], resL[3]);
+    }
+    wave_sync();
+    const int cbpl = m.cbp & 15;
+
+    if (i16) {
+        // Intra16x16 (intra_prediction.cc:668-735) + construction_16x16 (transform.cc:940-959),
+        // in the residual layout: row y = by * 4 + r, cols x0 .. x0 + 3.
+        const int blk = lane >> 2, r = lane & 3, y = (blk >> 2) * 4 + r, x0 = (blk & 3) * 4;
+        const int mode = m.i16_mode;
+        int p[4];
+        if (mode == 0) {
+            const uint32_t w = lds_u32(&S.tile[ti(x0, -1)]);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) p[c] = (w >> (8 * c)) & 255;
+        } else if (mode == 1) {
+            p[0] = p[1] = p[2] = p[3] = S.tile[ti(-1, y)];
+        } else if (mode == 2) {
+            int sum = 0, dc = 128;
+            if (avB)
+#pragma unroll
+                for (int k = 0; k < 4; ++k) sum += sum4(lds_u32(&S.tile[ti(4 * k, -1)]));
+            if (avA)
+#pragma unroll
+                for (int k = 0; k < 16; ++k) sum += S.tile[ti(-1, k)];
+            if (avA || avB) dc = (sum + (avA ? 8 : 0) + (avB ? 8 : 0)) >> (3 + avA + avB);
+            p[0] = p[1] = p[2] = p[3] = dc;
+        } else {
+            int Hs = 0, Vs = 0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                Hs += (k + 1) * (S.tile[ti(8 + k, -1)] - S.tile[ti(6 - k, -1)]);
+                Vs += (k + 1) * (S.tile[ti(-1, 8 + k)] - S.tile[ti(-1, 6 - k)]);
+            }
+            const int pa = 16 * (S.tile[ti(-1, 15)] + S.tile[ti(15, -1)]);
+            const int pb = (5 * Hs + 32) >> 6, pc = (5 * Vs + 32) >> 6;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) p[c] = clip255((pa + pb * (x0 + c - 7) + pc * (y - 7) + 16) >> 5);
+        }
+        uint32_t w = 0;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) w |= (uint32_t)clip255(p[c] + resL[c]) << (8 * c);
+        *reinterpret_cast<uint32_t*>(o.y + (size_t)(Y + y) * g.W + X + x0) = w;
+    } else if (i8) {
+        uint32_t tab[3];
+        intra_tap_table<8>(lane & 7, lane >> 3, tab);
+#pragma unroll 1
+        for (int blk = 0; blk < 4; ++blk) {
+            const int xO = (blk & 1) * 8, yO = (blk >> 1) * 8;
+            const int aA = xO > 0 ? 1 : avA, aB = yO > 0 ? 1 : avB;
+            const int aD = (xO > 0 && yO > 0) ? 1 : (xO == 0 && yO == 0) ? avD : (xO == 0 ? avA : avB);
+            const int aC = yO > 0 ? (xO == 0) : (xO == 0 ? avB : avC);   // intra_prediction.cc:370-376
+            const int mode = (m.ipred[blk >> 1] >> ((blk & 1) * 4)) & 15;
+            // reference sample filtering (intra_prediction.cc:413-447) -> S.fs
+            auto po = [&](int x, int y) -> int {
+                if (y < 0 && x >= 8 && !aC) x = 7;                   // p(x,-1) substitution :404-407
+                return S.tile[ti(xO + x, yO + y)];
+            };
+            if (lane < 25) {
+                int v = 0, at;
+                if (lane == 0) {                                       // p(-1,-1)
+                    at = 3;
+                    if (aD) {
+                        if (aA && aB) v = (po(0, -1) + 2 * po(-1, -1) + po(-1, 0) + 2) >> 2;
+                        else if (aB) v = (3 * po(-1, -1) + po(0, -1) + 2) >> 2;
+                        else if (aA) v = (3 * po(-1, -1) + po(-1, 0) + 2) >> 2;
+                        else v = po(-1, -1);
+                    }
+                } else if (lane <= 16) {                               // p(x,-1), x = lane-1
+                    const int x = lane - 1;
+                    at = 4 + x;
+                    if (aB) {
+                        if (x == 0) v = aD ? (po(-1, -1) + 2 * po(0, -1) + po(1, -1) + 2) >> 2 : (3 * po(0, -1) + po(1, -1) + 2) >> 2;
+                        else if (x < 15) v = (po(x - 1, -1) + 2 * po(x, -1) + po(x + 1, -1) + 2) >> 2;
+                        else v = (po(14, -1) + 3 * po(15, -1) + 2) >> 2;
+                    }
+                } else {                                               // p(-1,y), y = lane-17
+                    const int y = lane - 17;
+                    at = 20 + y;
+                    if (aA) {
+                        if (y == 0) v = aD ? (po(-1, -1) + 2 * po(-1, 0) + po(-1, 1) + 2) >> 2 : (3 * po(-1, 0) + po(-1, 1) + 2) >> 2;
+                        else if (y < 7) v = (po(-1, y - 1) + 2 * po(-1, y) + po(-1, y + 1) + 2) >> 2;
+                        else v = (po(-1, 6) + 3 * po(-1, 7) + 2) >> 2;
+                    }
+                }
+                S.fs[at] = (uint8_t)v;
+            }
+            wave_sync();
+            {
+                const int x = lane & 7, y = lane >> 3;
+                int p;
+                if (mode == 2) {                                       // DC (intra_prediction.cc:480-497)
+                    const int st = sum4(lds_u32(&S.fs[4])) + sum4(lds_u32(&S.fs[8]));
+                    const int sl = sum4(lds_u32(&S.fs[20])) + sum4(lds_u32(&S.fs[24]));
+                    p = aA && aB ? (st + sl + 8) >> 4 : aB ? (st + 4) >> 3 : aA ? (sl + 4) >> 3 : 128;
+                } else {
+                    const int ent = intra_tap_entry(tab, mode), kind = ent >> 5, i = ent & 31;
+                    auto E = [&](int k) -> int {                       // e[k] from S.fs
+                        const int at = k <= 8 ? 20 + min(7, 8 - k) : (k == 9 ? 3 : 4 + min(k - 10, 15));
+                        return S.fs[at];
+                    };
+                    p = tap_apply(kind, E(max(i - 1, 0)), E(i), E(min(i + 1, 26)));
+                }
+                const int v = (cbpl >> blk) & 1 ? clip255(p + S.res[yO + y][xO + x]) : p;
+                S.tile[ti(xO + x, yO + y)] = (uint8_t)v;
+            }
+            wave_sync();
+        }
+    } else {
+        // I_4x4: block (bx, by) at step bx + 2 by; slot 0 takes the block with the larger bx
+        uint32_t tab[3];
+        intra_tap_table<4>(lane & 3, (lane >> 2) & 3, tab);
+#pragma unroll 1
+        for (int s = 0; s < 10; ++s) {
+            const int slot = lane >> 4, pix = lane & 15, x = pix & 3, y = pix >> 2;
+            const int by = (s >> 1) - 1 + slot, bx = s - 2 * by;
+            if (lane < 32 && by >= 0 && by <= 3 && bx <= 3) {
+                const int xO = bx * 4, yO = by * 4;
+                const int bk = (by >> 1) * 8 + (bx >> 1) * 4 + (by & 1) * 2 + (bx & 1);   // blkIdx
+                const int aA = xO > 0 ? 1 : avA, aB = yO > 0 ? 1 : avB;
+                int aC;
+                if (yO == 0) aC = xO + 4 < 16 ? avB : avC;
+                else aC = (xO + 4 < 16) && !(xO == 4 && (yO == 4 || yO == 12));      // :154
+                const int mode = (m.ipred[bk >> 1] >> ((bk & 1) * 4)) & 15;
+                int p;
+                if (mode == 2) {                                       // DC (intra_prediction.cc:214-229)
+                    const int st = sum4(lds_u32(&S.tile[ti(xO, yO - 1)]));
+                    int sl = 0;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) sl += S.tile[ti(xO - 1, yO + k)];
+                    p = aA && aB ? (st + sl + 4) >> 3 : aB ? (st + 2) >> 2 : aA ? (sl + 2) >> 2 : 128;
+                } else {
+                    const int ent = intra_tap_entry(tab, mode), kind = ent >> 5, i = ent & 31;
+                    const int tmax = aC ? 7 : 3;
+                    auto E = [&](int k) -> int {                       // e[k] from the tile
+                        return k <= 5 ? S.tile[ti(xO - 1, yO + min(3, 4 - k))] : S.tile[ti(xO + min(k - 6, tmax), yO - 1)];
+                    };
+                    p = tap_apply(kind, E(max(i - 1, 0)), E(i), E(min(i + 1, 14)));
+                }
+                const int v = (cbpl >> ((yO >> 3) * 2 + (xO >> 3))) & 1 ? clip255(p + S.res[yO + y][xO + x]) : p;
+                S.tile[ti(xO + x, yO + y)] = (uint8_t)v;
+            }
+            wave_sync();
+        }
+    }
+    if (!i16) {
+        const int y = lane >> 2, x0 = (lane & 3) * 4;
+        *reinterpret_cast<uint32_t*>(o.y + (size_t)(Y + y) * g.W + X + x0) = lds_u32(&S.tile[ti(x0, y)]);
+    }
+
+    // ---- chroma: IntraPrediction::Chroma (intra_prediction.cc:748-894) + construction_chroma,
+    // in the chroma residual layout
+    {
+        const int pl = lane >> 5, cb = (lane >> 3) & 3, chalf = (lane >> 2) & 1, crow = lane & 3;
+        const int y = (cb >> 1) * 4 + crow, x0 = (cb & 1) * 4 + chalf * 2;
+        const uint8_t* C = S.ctile[pl];
+        const int mode = m.chroma_mode;
+        int p[2];
+        if (mode == 0) {
+            const int xO = x0 & 4, yO = y & 4;
+            int aA, aB;
+            if ((xO == 0 && yO == 0) || (xO > 0 && yO > 0)) { aA = avA; aB = avB; }
+            else if (xO > 0) { aA = avB ? 0 : avA; aB = avB; }
+            else { aA = avA; aB = avA ? 0 : avB; }
+            int sum = 0, v = 128;
+            if (aA || aB) {
+                if (aA)
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) sum += C[ci(-1, yO + k)];
+                if (aB) sum += sum4(lds_u32(&C[ci(xO, -1)]));
+                v = (sum + (aA ? 2 : 0) + (aB ? 2 : 0)) >> (1 + aA + aB);
+            }
+            p[0] = p[1] = v;
+        } else if (mode == 1) {
+            p[0] = p[1] = C[ci(-1, y)];
+        } else if (mode == 2) {
+            p[0] = C[ci(x0, -1)];
+            p[1] = C[ci(x0 + 1, -1)];
+        } else {
+            int Hs = 0, Vs = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                Hs += (k + 1) * (C[ci(4 + k, -1)] - C[ci(2 - k, -1)]);
+                Vs += (k + 1) * (C[ci(-1, 4 + k)] - C[ci(-1, 2 - k)]);
+            }
+            const int pa = 16 * (C[ci(-1, 7)] + C[ci(7, -1)]);
+            const int pb = (34 * Hs + 32) >> 6, pc = (34 * Vs + 32) >> 6;
+#pragma unroll
+            for (int c = 0; c < 2; ++c) p[c] = clip255((pa + pb * (x0 + c - 3) + pc * (y - 3) + 16) >> 5);
+        }
+        const uint32_t w = (uint32_t)clip255(p[0] + resC[0]) | ((uint32_t)clip255(p[1] + resC[1]) << 8);
+        *reinterpret_cast<uint16_t*>((pl ? o.v : o.u) + (size_t)(Yc + y) * g.Wc + Xc + x0) = (uint16_t)w;
+    }
+}
+
+}  // namespace h264r

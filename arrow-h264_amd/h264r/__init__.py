@@ -179,7 +179,8 @@ class Decoder:
         _check("h264r_set_debug", self._L.h264r_set_debug(self._h, flags))
 
     # -- convenience ----------------------------------------------------------------
-    def decode_picture(self, p, refs=None, keep_slot: int = -1, no_deblock: bool = False):
+    def decode_picture(self, p, refs=None, keep_slot: int = -1, no_deblock: bool = False,
+                       intra_walk: bool = False):
         """Submit every MB of a synth.Picture (raster order) and return its planes."""
         from .mbview import iter_mbs
         if refs is not None:
@@ -189,7 +190,7 @@ class Decoder:
         self.init(W, H, p.pic, p.slices)
         for addr, rec, lv, mv, rr in iter_mbs(p):
             self.decode(addr, rec, lv, mv, rr)
-        self.set_debug(1 if no_deblock else 0)
+        self.set_debug((A.DBG_NO_DEBLOCK if no_deblock else 0) | (A.DBG_INTRA_WALK if intra_walk else 0))
         try:
             return self.deblock_filter(keep_slot)
         finally:

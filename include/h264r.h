@@ -231,6 +231,9 @@ int  h264r_set_timing(h264r_ctx* ctx, int enable);
 /* Debug hook: H264R_DBG_NO_DEBLOCK skips the loop filter (reconstruction only, to
  * localise a mismatch against the oracle's pre-deblock planes). */
 #define H264R_DBG_NO_DEBLOCK 1
+/* H264R_DBG_INTRA_WALK reconstructs every intra MB with the wavefront walk instead of
+ * the dependency-level schedule (both are bit-exact; this exercises the walk alone). */
+#define H264R_DBG_INTRA_WALK 2
 int  h264r_set_debug(h264r_ctx* ctx, int flags);
 /* Wait for the context's work and report a device-side failure (a wavefront wait
  * that timed out): H264R_OK or H264R_EDEVICE. */

@@ -71,7 +71,7 @@ def test_gpu_matches_reference_fixture(L, dec, fx):
         pytest.fail("; ".join(msgs) or "md5 mismatch")
 
 
-def _batch_vs_oracle(L, dec, cidx, W, H, n, **over):
+def _batch_vs_oracle(L, dec, cidx, W, H, n, debug=0, **over):
     cfg = synth.default_cfg(L, cidx, W, H, **over)
     pics = [synth.picture(L, cfg, i) for i in range(n)]
     refs = synth.refpics(L, cfg)
@@ -79,9 +79,12 @@ def _batch_vs_oracle(L, dec, cidx, W, H, n, **over):
         dec.set_ref(s, y, u, v)
     host = B.pack(pics, h264r.quant_flat())
     db = B.to_device(host, n, None)
-    dec.decode_batch(db.batch)
-    import torch
-    torch.cuda.synchronize()
+    dec.set_debug(debug)
+    try:
+        dec.decode_batch(db.batch)
+        dec.check()
+    finally:
+        dec.set_debug(0)
     for i, p in enumerate(pics):
         want = O.decode(p, refs)
         got = db.planes(i)
@@ -106,6 +109,17 @@ def test_gpu_batch_1080p_p(L, dec):
 def test_gpu_batch_1080p_intra(L, dec):
     """BASELINE config 2 size (all-intra, 4x4 + 8x8)."""
     _batch_vs_oracle(L, dec, 2, 120, 68, 2)
+
+
+def test_gpu_batch_1080p_p_intra_walk(L, dec):
+    """The wavefront walk alone (no dependency-level schedule) on config 3."""
+    _batch_vs_oracle(L, dec, 3, 120, 68, 2, debug=A.DBG_INTRA_WALK)
+
+
+def test_gpu_batch_dense_intra_levels(L, dec):
+    """P pictures with 60 % intra MBs: chains far deeper than the level launches, so
+    the level schedule and the walk both take part in one picture."""
+    _batch_vs_oracle(L, dec, 3, 40, 30, 3, intra_permille=600, pcm_permille=30)
 
 
 def test_gpu_2160p_b_8slices(L, dec):

@@ -1,0 +1,41 @@
+#!/usr/bin/env python3
+"""Diagnostic: per-MB latency trace of k_intra_levels (lib built with -DH264R_TRACE_INTRA)."""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "arrow-h264_amd"))
+import torch  # noqa: E402,F401
+import h264r  # noqa: E402
+from h264r import batch as B, synth  # noqa: E402
+
+L = h264r.lib()
+W, H, n = 120, 68, int(sys.argv[1]) if len(sys.argv) > 1 else 256
+cfg = synth.default_cfg(L, 3, W, H)
+pics = [synth.picture(L, cfg, i) for i in range(n)]
+refs = synth.refpics(L, cfg)
+dec = h264r.Decoder(0, W, H)
+for s, (y, u, v) in enumerate(refs):
+    dec.set_ref(s, y, u, v)
+db = B.to_device(B.pack(pics, h264r.quant_flat()), n, None)
+dec.decode_batch(db.batch)
+dec.check()
+out = np.zeros((1 << 20, 4), np.uint64)
+cnt = C.c_uint(0)
+L.h264r_trace_intra_dump(out.ctypes.data_as(C.c_void_p), C.byref(cnt))
+t = out[: cnt.value]
+t0 = t[:, 0].astype(np.int64)
+dur = (t[:, 1].astype(np.int64) - t0) / 100.0     # us (100 MHz)
+lvl = (t[:, 2] >> 32).astype(np.int64)
+typ = (t[:, 2] & 0xFFFFFFFF).astype(np.int64)
+start = (t0 - t0.min()) / 100.0
+print("MBs", cnt.value)
+for Lv in np.unique(lvl):
+    m = lvl == Lv
+    print(f"level {Lv}: n={m.sum()} start {start[m].min():.1f}..{start[m].max():.1f} us  end {(start[m] + dur[m]).max():.1f}  dur mean {dur[m].mean():.2f} p50 {np.median(dur[m]):.2f} max {dur[m].max():.2f}")
+for ty in np.unique(typ):
+    m = typ == ty
+    print(f"type {ty}: n={m.sum()} dur mean {dur[m].mean():.2f} p50 {np.median(dur[m]):.2f}")
