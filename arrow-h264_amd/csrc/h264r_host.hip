@@ -23,7 +23,9 @@
 
 namespace h264r { struct DbInfo; }
 extern "C" __global__ void k_prep(h264r_batch b, uint2* mot);
-extern "C" __global__ void k_inter(h264r_batch b, const uint2* mot, h264r::DbInfo* dbinfo);
+extern "C" __global__ void k_inter(h264r_batch b, const uint2* mot);
+extern "C" __global__ void k_dbinfo(h264r_batch b, const uint2* mot, h264r::DbInfo* dbinfo);
+extern "C" __global__ void k_inter4(h264r_batch b, const uint2* mot, h264r::DbInfo* dbinfo);
 extern "C" __global__ void k_intra_pic(h264r_batch b, int* sync, int* err, const uint16_t* lvl, int lmax);
 extern "C" __global__ void k_level(h264r_batch b, uint16_t* lvl, int* lvsync);
 extern "C" __global__ void k_intra_levels(h264r_batch b, const uint16_t* lvl, int lmax, int* lvsync, int* err);
@@ -346,6 +348,14 @@ static int level_launches()
     return std::max(0, std::min(env, 256));
 }
 
+// Inter MBs: k_inter4 (four MBs per wave, lane per 4x4 block, deblock records
+// folded in) unless H264R_INTER=1 selects the wave-per-MB k_inter + k_dbinfo pair.
+static bool inter4()
+{
+    static const bool v = [] { const char* e = getenv("H264R_INTER"); return !(e && atoi(e) == 1); }();
+    return v;
+}
+
 static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s)
 {
     const int W = b.width_mbs, H = b.height_mbs, P = b.num_pics;
@@ -404,9 +414,17 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s)
             hipLaunchKernelGGL(k_prep, dim3((unsigned)((mplane + 255) / 256), n), dim3(256), 0, s, cb,
                                c->d_mot + (size_t)p0 * 2 * mplane);
             HIP_OK(hipGetLastError());
-            hipLaunchKernelGGL(k_inter, dim3(W * H, n), dim3(64), 0, s, cb, c->d_mot + (size_t)p0 * 2 * mplane,
-                               dbinfo_at(p0));
-            HIP_OK(hipGetLastError());
+            if (inter4()) {
+                hipLaunchKernelGGL(k_inter4, dim3((W * H + 15) / 16, n), dim3(256), 0, s, cb,
+                                   c->d_mot + (size_t)p0 * 2 * mplane, dbinfo_at(p0));
+                HIP_OK(hipGetLastError());
+            } else {
+                hipLaunchKernelGGL(k_dbinfo, dim3((W * H + 3) / 4, n), dim3(256), 0, s, cb,
+                                   c->d_mot + (size_t)p0 * 2 * mplane, dbinfo_at(p0));
+                HIP_OK(hipGetLastError());
+                hipLaunchKernelGGL(k_inter, dim3(W * H, n), dim3(64), 0, s, cb, c->d_mot + (size_t)p0 * 2 * mplane);
+                HIP_OK(hipGetLastError());
+            }
         }
         hipStream_t si = K > 1 ? c->aux[0] : s, sd = K > 1 ? c->aux[1] : s;
         if (K > 1) {

@@ -1,0 +1,603 @@
+// mb_inter4.h -- inter (and I_PCM) macroblocks, FOUR per 64-lane wave, one lane per
+// 4x4 luma block (+ its 2x2 chroma sub-blocks in both planes), and the deblocking
+// record of every MB.
+//
+//   Decoder::mb_pred_inter decoder.cc:212-262 (partition walk = per-4x4 motion),
+//   InterPrediction::get_block_luma inter_prediction.cc:158-340 (6-tap qpel),
+//   get_block_chroma :342-406 (bilinear), mc_prediction :53-86 and bi_prediction
+//   :88-156 (weighted prediction), Transform::inverse_transform_inter
+//   transform.cc:1051-1095 (inverse_4x4 :597-641, inverse_8x8 :643-733, chroma DC
+//   :875-889, construction :913-984), mb_pred_ipcm decoder.cc:149-168,
+//   Deblock::strength deblock.cc:78-289 (boundary strengths, DbInfo).
+//
+// Why this shape: a wave per MB with a lane per sample row keeps one MB in flight
+// per wave, recomputes the 6-tap intermediates of every row in every lane, and
+// leaves the kernel latency-bound (a handful of dependent global round trips per MB,
+// at 5 waves per SIMD).  With a lane per 4x4 block a wave carries four MBs, each
+// lane filters its 9x9 reference window once (the horizontal intermediates of a row
+// feed both the half-sample b and the centre j of all four output rows), the 4x4
+// inverse transform runs entirely in-lane, and a 4x4 block's motion is exactly what
+// the boundary strengths of its left and top edges need.
+//
+// Lane roles: g = lane >> 4 picks the MB (a0 + g), blk = lane & 15 the 4x4 block in
+// raster order (bx = blk & 3, by = blk >> 2).  Chroma: the lane owns the 2x2 chroma
+// samples (2bx.., 2by..) of each plane (4:2:0: the chroma of a luma 4x4 block, with
+// the same motion vector).  A chroma 4x4 transform block is spread over the lanes
+// {blk, blk^1, blk^4, blk^5}; an 8x8 luma transform block likewise.
+#pragma once
+#include "mb_deblock.h"
+
+namespace h264r {
+
+constexpr int INTER4_MBS = 16;   // MBs per 256-thread workgroup (4 waves x 4)
+
+struct Inter4Lds {
+    const uint8_t* planes[3 * H264R_MAX_SLOTS];
+};
+
+DEV int sel16(uint32_t lo, uint32_t hi, int c) { return (int16_t)(((c & 2) ? hi : lo) >> (16 * (c & 1))); }
+
+// Two rows (y, y+1) of luma prediction samples of a 4-wide block at integer
+// position (x, y) and quarter phase (xf, yf), spec 8.4.2.2.1 / reference
+// get_block_luma.  Streams the 7 window rows y-2..y+4 once: the unrounded
+// horizontal 6-tap of each row feeds b (rows 2..4) and the centre j (all rows); the
+// vertical 6-tap h runs down column c + 2 (+1 for xf == 3, giving m).  out[i] packs
+// row i's four samples as bytes.  (A whole 4x4 block at once would share 5 of the
+// 9 window rows between its row pairs but needs twice the registers.)
+DEV void luma_rows2_pred(const uint8_t* __restrict__ img, int W, int H, int x, int y, int xf, int yf, uint32_t (&out)[2])
+{
+    const int hs = xf == 3 ? 1 : 0;                  // G/h column: c + 2 + hs
+    const int brow = yf == 3 ? 1 : 0;                // b/G row: i + 2 + brow
+    int hacc[2][4], jacc[2][4], bsv[2][4], gsv[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) hacc[i][c] = jacc[i][c] = bsv[i][c] = gsv[i][c] = 0;
+    uint32_t w[7][3];
+#pragma unroll
+    for (int r = 0; r < 7; ++r) {
+        const uint32_t* q = row_dwords(img, W, H, x, y - 2 + r);
+        w[r][0] = q[0]; w[r][1] = q[1]; w[r][2] = q[2];
+    }
+    constexpr int C6[6] = {1, -5, 20, 20, -5, 1};
+#pragma unroll
+    for (int r = 0; r < 7; ++r) {
+        int p[9];
+        row9(w[r][0], w[r][1], w[r][2], x, W, p);
+        int b1[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) b1[c] = tap6(p[c], p[c + 1], p[c + 2], p[c + 3], p[c + 4], p[c + 5]);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int k = r - i;                      // tap index of row r for output row i
+            if (k < 0 || k > 5) continue;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                hacc[i][c] += C6[k] * (hs ? p[3 + c] : p[2 + c]);
+                jacc[i][c] += C6[k] * b1[c];
+            }
+            if (k == 2 || k == 3) {                   // b / G of output row i: row i + 2 + brow
+                const bool take = k == 2 + brow;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    bsv[i][c] = take ? b1[c] : bsv[i][c];
+                    gsv[i][c] = take ? (hs ? p[3 + c] : p[2 + c]) : gsv[i][c];
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        uint32_t o = 0;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int G = gsv[i][c];
+            const int h = clip255((hacc[i][c] + 16) >> 5);
+            const int b = clip255((bsv[i][c] + 16) >> 5);
+            const int j = clip255((jacc[i][c] + 512) >> 10);
+            int v;
+            if (xf == 0) v = yf == 0 ? G : (yf == 2 ? h : (h + G + 1) >> 1);          // G, d, h, n
+            else if (yf == 0) v = xf == 2 ? b : (b + G + 1) >> 1;                      // a, b, c
+            else if (xf == 2) v = yf == 2 ? j : (j + b + 1) >> 1;                      // j, f, q
+            else if (yf == 2) v = (j + h + 1) >> 1;                                     // i, k
+            else v = (b + h + 1) >> 1;                                                  // e, g, p, r
+            o |= (uint32_t)v << (8 * c);
+        }
+        out[i] = o;
+    }
+}
+
+// ---------------------------------------------------------------- packed 16-bit helpers
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+DEV s16x2 as_s16x2(uint32_t v) { return __builtin_bit_cast(s16x2, v); }
+DEV uint32_t as_u32(s16x2 v) { return __builtin_bit_cast(uint32_t, v); }
+DEV s16x2 splat16(short v) { return (s16x2){v, v}; }
+DEV s16x2 pk_max(s16x2 a, s16x2 b) { return __builtin_elementwise_max(a, b); }
+DEV s16x2 pk_min(s16x2 a, s16x2 b) { return __builtin_elementwise_min(a, b); }
+DEV s16x2 pk_clip255(s16x2 a) { return pk_min(pk_max(a, splat16(0)), splat16(255)); }
+// (p[k], p[k+1]) of the 9 row samples held as bytes in r0 = p0..p3, r1 = p4..p7, r2 = p8
+template <int K>
+DEV s16x2 pair_at(uint32_t r0, uint32_t r1, uint32_t r2)
+{
+    constexpr uint32_t sel = K < 3 ? (0x0c000c00u | ((K + 1) << 16) | K)
+                           : K == 3 ? 0x0c040c03u
+                           : K < 7 ? (0x0c000c00u | ((K - 3) << 16) | (K - 4))
+                           : 0x0c040c03u;
+    return as_s16x2(K < 4 ? __builtin_amdgcn_perm(r1, r0, sel) : __builtin_amdgcn_perm(r2, r1, sel));
+}
+
+// The 16 luma prediction samples of one 4x4 block at integer position (x, y) and
+// quarter phase (xf, yf): spec 8.4.2.2.1 / reference get_block_luma
+// (inter_prediction.cc:158-340).  The 9 window rows y-2..y+6 are loaded at once and
+// streamed; per row the unrounded horizontal 6-tap b1 of columns 0..3 is computed
+// once (packed 16-bit pairs, exact: |b1| <= 10710) and feeds both b (rows 2..6) and
+// the centre j of every output row it is a tap of (32-bit); the vertical 6-tap h of
+// column c + 2 (+1 for xf == 3: m) accumulates in packed 16-bit.  Every output is
+// (X + Y + 1) >> 1 of two of {G, b, h, j}, chosen per lane from the phase.
+// out[i] packs row i's four samples as bytes.
+DEV void luma_block_pred(const uint8_t* __restrict__ img, int W, int H, int x, int y, int xf, int yf, uint32_t (&out)[4])
+{
+    const int hs = xf == 3 ? 1 : 0;                  // G / h column c + 2 + hs
+    const int brow = yf == 3 ? 1 : 0;                // b / G row i + 2 + brow
+    uint32_t w[9][3];
+#pragma unroll
+    for (int r = 0; r < 9; ++r) {
+        const uint32_t* q = row_dwords(img, W, H, x, y - 2 + r);
+        w[r][0] = q[0]; w[r][1] = q[1]; w[r][2] = q[2];
+    }
+    const bool inside = x - 2 >= 0 && x + 6 < W;
+    const int sh = (x - 2) & 3;
+    s16x2 hacc[4][2], bsv[4][2], gsv[4][2];
+    int jacc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) hacc[i][h2] = bsv[i][h2] = gsv[i][h2] = splat16(0);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) jacc[i][c] = 0;
+    }
+    constexpr short C6[6] = {1, -5, 20, 20, -5, 1};
+#pragma unroll
+    for (int r = 0; r < 9; ++r) {
+        uint32_t r0, r1, r2;
+        if (inside) {
+            r0 = __builtin_amdgcn_alignbyte(w[r][1], w[r][0], sh);
+            r1 = __builtin_amdgcn_alignbyte(w[r][2], w[r][1], sh);
+            r2 = w[r][2] >> (8 * sh);
+        } else {                                       // window crosses the picture edge: clamp per sample
+            int p[9];
+            row9(w[r][0], w[r][1], w[r][2], x, W, p);
+            r0 = p[0] | (p[1] << 8) | (p[2] << 16) | ((uint32_t)p[3] << 24);
+            r1 = p[4] | (p[5] << 8) | (p[6] << 16) | ((uint32_t)p[7] << 24);
+            r2 = p[8];
+        }
+        const s16x2 q0 = pair_at<0>(r0, r1, r2), q1 = pair_at<1>(r0, r1, r2), q2 = pair_at<2>(r0, r1, r2);
+        const s16x2 q3 = pair_at<3>(r0, r1, r2), q4 = pair_at<4>(r0, r1, r2), q5 = pair_at<5>(r0, r1, r2);
+        const s16x2 q6 = pair_at<6>(r0, r1, r2), q7 = pair_at<7>(r0, r1, r2);
+        const s16x2 b01 = (q0 + q5) + splat16(20) * (q2 + q3) - splat16(5) * (q1 + q4);   // b1 cols 0,1
+        const s16x2 b23 = (q2 + q7) + splat16(20) * (q4 + q5) - splat16(5) * (q3 + q6);   // b1 cols 2,3
+        const s16x2 g01 = hs ? q3 : q2, g23 = hs ? q5 : q4;                                // G column pairs
+        const int bc[4] = {(int)b01.x, (int)b01.y, (int)b23.x, (int)b23.y};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int k = r - i;                       // tap index of row r for output row i
+            if (k < 0 || k > 5) continue;
+            hacc[i][0] += splat16(C6[k]) * g01;
+            hacc[i][1] += splat16(C6[k]) * g23;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) jacc[i][c] += C6[k] * bc[c];
+            if (k == 2 || k == 3) {                    // b / G of output row i: row i + 2 + brow
+                const bool take = k == 2 + brow;
+                bsv[i][0] = take ? b01 : bsv[i][0];
+                bsv[i][1] = take ? b23 : bsv[i][1];
+                gsv[i][0] = take ? g01 : gsv[i][0];
+                gsv[i][1] = take ? g23 : gsv[i][1];
+            }
+        }
+    }
+    // output = (X + Y + 1) >> 1, X, Y in {0 G, 1 b, 2 h, 3 j}
+    int xs, ys;
+    if (xf == 0) { xs = yf == 2 ? 2 : 0; ys = yf == 0 ? 0 : 2; }
+    else if (yf == 0) { xs = xf == 2 ? 1 : 0; ys = 1; }
+    else if (xf == 2) { xs = yf == 2 ? 3 : 1; ys = 3; }
+    else if (yf == 2) { xs = 2; ys = 3; }
+    else { xs = 1; ys = 2; }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        uint32_t o2[2];
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) {
+            const s16x2 G = gsv[i][h2];
+            const s16x2 hh = pk_clip255((hacc[i][h2] + splat16(16)) >> splat16(5));
+            const s16x2 bb = pk_clip255((bsv[i][h2] + splat16(16)) >> splat16(5));
+            const int j0 = clip255((jacc[i][2 * h2] + 512) >> 10), j1 = clip255((jacc[i][2 * h2 + 1] + 512) >> 10);
+            const s16x2 jj = (s16x2){(short)j0, (short)j1};
+            const s16x2 X = xs == 0 ? G : (xs == 1 ? bb : (xs == 2 ? hh : jj));
+            const s16x2 Y = ys == 0 ? G : (ys == 1 ? bb : (ys == 2 ? hh : jj));
+            o2[h2] = as_u32((X + Y + splat16(1)) >> splat16(1));
+        }
+        out[i] = __builtin_amdgcn_perm(o2[1], o2[0], 0x06040200u);
+    }
+}
+
+// 2x2 chroma prediction samples at chroma integer position (xi, yi), eighth phase
+// (xf, yf): get_block_chroma inter_prediction.cc:380-404 with clamped coordinates.
+// Returns the four samples as bytes (row 0 in bits 0..15, row 1 in 16..31).
+DEV uint32_t chroma_block_pred(const uint8_t* __restrict__ img, int W, int H, int xi, int yi, int xf, int yf)
+{
+    const int a = clip3(0, W - 1, xi) & ~3;
+    int p[3][3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const uint32_t* q = reinterpret_cast<const uint32_t*>(img + (size_t)clip3(0, H - 1, yi + k) * W + a);
+        const uint32_t w0 = q[0], w1 = q[1];
+        if (xi >= 0 && xi + 2 < W) {
+            const uint32_t r = __builtin_amdgcn_alignbyte(w1, w0, xi & 3);
+            p[k][0] = r & 255; p[k][1] = (r >> 8) & 255; p[k][2] = (r >> 16) & 255;
+        } else {
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                const int idx = clip3(0, W - 1, xi + c) - a;
+                p[k][c] = ((idx < 4 ? w0 : w1) >> (8 * (idx & 3))) & 255;
+            }
+        }
+    }
+    const int wa = (8 - xf) * (8 - yf), wb = xf * (8 - yf), wc = (8 - xf) * yf, wd = xf * yf;
+    uint32_t o = 0;
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+            o |= (uint32_t)((wa * p[r][c] + wb * p[r][c + 1] + wc * p[r + 1][c] + wd * p[r + 1][c + 1] + 32) >> 6)
+                 << (16 * r + 8 * c);
+    return o;
+}
+
+// mc_prediction / bi_prediction combine (inter_prediction.cc:53-156) on 4 packed
+// samples of each list.
+DEV uint32_t wp_combine4(const h264r_slice* __restrict__ sl, int wp_mode, int dir, int r0, int r1, uint32_t v0,
+                         uint32_t v1, int pl)
+{
+    if (wp_mode == 0) {
+        if (dir == 0) return v0;
+        if (dir == 1) return v1;
+        // (a + b + 1) >> 1 per byte
+        return (v0 | v1) - (((v0 ^ v1) >> 1) & 0x7F7F7F7Fu);
+    }
+    uint32_t o = 0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+        o |= (uint32_t)wp_combine(sl, dir, r0, r1, (v0 >> (8 * c)) & 255, (v1 >> (8 * c)) & 255, pl) << (8 * c);
+    return o;
+}
+
+// 4-point inverse transform of one column / row held in registers, (x + 32) >> 6 at
+// the end of the second pass (inverse_4x4 transform.cc:597-641).
+DEV void idct4_inplace(int& a, int& b, int& c, int& d)
+{
+    int o0, o1, o2, o3;
+    idct4(a, b, c, d, o0, o1, o2, o3);
+    a = o0; b = o1; c = o2; d = o3;
+}
+
+// The inter / I_PCM macroblocks a0 .. a0+3 of picture `pic` and the deblocking
+// records of all four.  `mot`: the picture's resolved motion (k_prep).
+DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int lane, const uint2* __restrict__ mot,
+                    DbInfo* __restrict__ dbout, const Inter4Lds& S)
+{
+    const int grp = lane >> 4, blk = lane & 15, bx = blk & 3, by = blk >> 2;
+    const int a = a0 + grp;
+    const bool valid = a < g.nmb;
+    const int aa = valid ? a : g.nmb - 1;
+    const int mbx = aa % g.wmb, mby = aa / g.wmb;
+    const h264r_mb* mbs = b.mbs + (size_t)pic * g.nmb;
+    const h264r_slice* slices = b.slices + (size_t)pic * b.slice_stride;
+
+    // ---- motion of this block and of its left / upper neighbours (k_prep output)
+    const int X4 = mbx * 4 + bx, Y4 = mby * 4 + by;
+    const int mi = Y4 * g.W4 + X4;
+    const uint2 m0 = mot[mi], m1 = mot[g.motion_plane + mi];
+    const int li = X4 > 0 ? mi - 1 : mi, ui = Y4 > 0 ? mi - g.W4 : mi;
+    const uint2 l0 = mot[li], l1 = mot[g.motion_plane + li];
+    const uint2 u0 = mot[ui], u1 = mot[g.motion_plane + ui];
+    // ---- MB records (own, left, upper) and slice headers
+    const h264r_mb q = mbs[aa];
+    const int hasL = mbx > 0, hasU = mby > 0;
+    const h264r_mb L = mbs[hasL ? aa - 1 : aa];
+    const h264r_mb U = mbs[hasU ? aa - g.wmb : aa];
+    const h264r_slice* qs = &slices[q.slice];
+    const uint2 qsh = *reinterpret_cast<const uint2*>(qs);       // type, idc, offsets, wp, log2 wd
+    const int q_type = qsh.x & 255, idc = (qsh.x >> 8) & 255;
+    const int offa = (int8_t)((qsh.x >> 16) & 255), offb = (int8_t)(qsh.x >> 24);
+    const int wp_mode = qsh.y & 255;
+
+    // ---- deblocking record (Deblock::strength deblock.cc:78-289): this lane's
+    // left edge (vertical edge bx, segment by) and top edge (horizontal edge by,
+    // segment bx)
+    if (valid) {
+        const int fl = idc == 0 ? hasL : (idc == 2 && hasL && L.slice == q.slice);
+        const int ft = idc == 0 ? hasU : (idc == 2 && hasU && U.slice == q.slice);
+        const int t8 = (q.flags & H264R_MBF_T8x8) != 0;
+        const MotionRef mq = motion_of(m0, m1);
+        const int q_intra = mb_is_intra(q);
+        const int pskip = q_type == H264R_SLICE_P && q.mb_type == H264R_P_SKIP;
+        const int special_q = special_slice(q_type);
+        DbInfo* out = dbout + aa;
+#pragma unroll
+        for (int hor = 0; hor < 2; ++hor) {
+            const int e = hor ? by : bx, s = hor ? bx : by;
+            const int en = idc != 1 && (e == 0 ? (hor ? ft : fl) : ((e & 1) ? !t8 : 1));
+            int v = 0;
+            if (en) {
+                // MB P of the edge: the left / upper MB for edge 0, else this MB
+                const int p_slice = e == 0 ? (hor ? U.slice : L.slice) : q.slice;
+                const int p_flags = e == 0 ? (hor ? U.flags : L.flags) : q.flags;
+                const int p_cbp = e == 0 ? (hor ? U.cbp_blks : L.cbp_blks) : q.cbp_blks;
+                const int special = special_q || (e == 0 && special_slice(slices[p_slice].slice_type));
+                const int intra = q_intra || (p_flags & H264R_MBF_INTRA) != 0;
+                const int blkQ = 4 * by + bx;
+                const int blkP = hor ? (e == 0 ? 12 + bx : blkQ - 4) : (e == 0 ? blkQ + 3 : blkQ - 1);
+                const int coded = ((q.cbp_blks >> blkQ) & 1) || ((p_cbp >> blkP) & 1);
+                const int same_part = e > 0 && (q.mb_type == H264R_P_16x16 ||
+                                                q.mb_type == (hor ? H264R_P_8x16 : H264R_P_16x8));
+                if (!hor) {
+                    if (special) v = e == 0 ? 4 : 3;
+                    else if (e > 0 && pskip) v = 0;
+                    else if (e == 0 && intra) v = 4;
+                    else if (intra) v = 3;
+                    else if (coded) v = 2;
+                    else if (same_part) v = 0;
+                    else v = bs_compare(mq, motion_of(l0, l1));
+                } else {
+                    if (e == 0 && (special || intra)) v = 4;
+                    else if (special || intra) v = 3;
+                    else if (e > 0 && pskip) v = 0;
+                    else if (coded) v = 2;
+                    else if (same_part) v = 0;
+                    else v = bs_compare(mq, motion_of(u0, u1));
+                }
+            }
+            out->bs[hor * 16 + e * 4 + s] = (uint8_t)v;
+        }
+        if (blk < 9) {                                              // edge parameters
+            const int pl = blk / 3, which = blk - pl * 3;
+            const int py = which == 0 ? L.qp_y : (which == 1 ? U.qp_y : q.qp_y);
+            const int pc0 = which == 0 ? L.qp_c[0] : (which == 1 ? U.qp_c[0] : q.qp_c[0]);
+            const int pc1 = which == 0 ? L.qp_c[1] : (which == 1 ? U.qp_c[1] : q.qp_c[1]);
+            const int qp = pl == 0 ? py : (pl == 1 ? pc0 : pc1);
+            const int qq = pl == 0 ? q.qp_y : (pl == 1 ? q.qp_c[0] : q.qp_c[1]);
+            out->par[blk] = edge_word(qp, qq, offa, offb);
+        }
+    }
+
+    const bool pcm = q.mb_type == H264R_I_PCM;
+    if (!valid || (mb_is_intra(q) && !pcm)) return;              // intra: k_intra_* (lanes idle here)
+    const PicPtrs o = out_planes(b, g, pic);
+    const int16_t* lv = b.levels + q.coef_off;
+    uint8_t* ydst = o.y + (size_t)(mby * 16 + by * 4) * g.W + mbx * 16 + bx * 4;
+    const size_t coff = (size_t)(mby * 8 + by * 2) * g.Wc + mbx * 8 + bx * 2;
+    if (pcm) {                                                       // mb_pred_ipcm decoder.cc:149-168
+        const uint8_t* raw = reinterpret_cast<const uint8_t*>(lv);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            *reinterpret_cast<uint32_t*>(ydst + (size_t)r * g.W) =
+                *reinterpret_cast<const uint32_t*>(raw + (by * 4 + r) * 16 + bx * 4);
+#pragma unroll
+        for (int pl = 0; pl < 2; ++pl)
+#pragma unroll
+            for (int r = 0; r < 2; ++r)
+                *reinterpret_cast<uint16_t*>((pl ? o.v : o.u) + coff + (size_t)r * g.Wc) =
+                    *reinterpret_cast<const uint16_t*>(raw + 256 + pl * 64 + (by * 2 + r) * 8 + bx * 2);
+        return;
+    }
+
+    // ---- residual inputs, issued before motion compensation
+    const int cbpl = q.cbp & 15, cbpc = q.cbp >> 4;
+    const int t8 = (q.flags & H264R_MBF_T8x8) != 0;
+    const h264r_quant* __restrict__ qt = &b.quant[pic];
+    const int qpl = q.qp_scaled[0];
+    const int b8 = (by >> 1) * 2 + (bx >> 1);
+    const int loff = b8_offset(q.cbp, b8);
+    uint4 lev[2] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
+    uint4 lsc[2] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
+    if (loff >= 0) {
+        if (!t8) {                      // 4x4 block: 16 raster levels
+            const uint4* p = reinterpret_cast<const uint4*>(lv + loff + ((by & 1) * 2 + (bx & 1)) * 16);
+            lev[0] = p[0]; lev[1] = p[1];
+            const uint4* s = reinterpret_cast<const uint4*>(&qt->scale4x4[1][0][qpl % 6][0]);
+            lsc[0] = s[0]; lsc[1] = s[1];
+        } else {                        // my 4x4 quadrant of the 8x8 block: rows (by&1)*4.., cols (bx&1)*4..
+            const int16_t* p = lv + loff + (by & 1) * 32 + (bx & 1) * 4;
+            const int16_t* s = &qt->scale8x8[1][0][qpl % 6][(by & 1) * 32 + (bx & 1) * 4];
+            const uint2 r0 = ld8(p), r1 = ld8(p + 8), r2 = ld8(p + 16), r3 = ld8(p + 24);
+            lev[0] = make_uint4(r0.x, r0.y, r1.x, r1.y); lev[1] = make_uint4(r2.x, r2.y, r3.x, r3.y);
+            const uint2 s0 = ld8(s), s1 = ld8(s + 8), s2 = ld8(s + 16), s3 = ld8(s + 24);
+            lsc[0] = make_uint4(s0.x, s0.y, s1.x, s1.y); lsc[1] = make_uint4(s2.x, s2.y, s3.x, s3.y);
+        }
+    }
+    // chroma: my 2x2 quadrant of chroma 4x4 block cb of each plane + the plane's 4 DC levels
+    const int cb = (by >> 1) * 2 + (bx >> 1), cr = (by & 1) * 2, cc = (bx & 1) * 2;
+    uint32_t clev[2][2] = {{0, 0}, {0, 0}}, csc[2][2] = {{0, 0}, {0, 0}};
+    uint2 cdc[2] = {make_uint2(0, 0), make_uint2(0, 0)};
+    int cdcs[2] = {0, 0};
+    if (cbpc) {
+        const LevelOffs lo = level_offsets(q);
+#pragma unroll
+        for (int pl = 0; pl < 2; ++pl) {
+            const int qpc = q.qp_scaled[1 + pl];
+            cdc[pl] = ld8(lv + lo.cdc + pl * 4);
+            cdcs[pl] = qt->scale4x4[1][1 + pl][qpc % 6][0];
+            if (cbpc == 2) {
+#pragma unroll
+                for (int r = 0; r < 2; ++r) {
+                    clev[pl][r] = *reinterpret_cast<const uint32_t*>(lv + lo.cac + pl * 64 + cb * 16 + (cr + r) * 4 + cc);
+                    csc[pl][r] = *reinterpret_cast<const uint32_t*>(&qt->scale4x4[1][1 + pl][qpc % 6][(cr + r) * 4 + cc]);
+                }
+            }
+        }
+    }
+
+    // ---- prediction
+    const int r0 = (int8_t)(m0.y & 255), r1 = (int8_t)(m1.y & 255);
+    const int dir = (r0 >= 0 && r1 >= 0) ? 2 : (r0 >= 0 ? 0 : 1);
+    uint32_t pY[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}}, pC[2][2] = {{0, 0}, {0, 0}};
+#pragma unroll 1
+    for (int l = 0; l < 2; ++l) {
+        const uint2 mw = l ? m1 : m0;
+        const int rr = l ? r1 : r0;
+        const bool use = rr >= 0;
+        if (!__any(use)) continue;                                  // P pictures: list 1 never
+        if (!use) continue;
+        const int slot = (int8_t)((mw.y >> 8) & 255);
+        const bool ok = slot >= 0 && slot < H264R_MAX_SLOTS && rr < H264R_MAX_REFS && S.planes[slot * 3];
+        const int mvx = (int16_t)(mw.x & 0xFFFF), mvy = (int16_t)(mw.x >> 16);
+        const int vx = X4 * 16 + mvx, vy = Y4 * 16 + mvy;           // quarter luma / eighth chroma units
+        if (!ok) {                                                   // no_ref: 128 (inter_prediction.cc:164-167,366-369)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) pY[l][i] = 0x80808080u;
+            pC[l][0] = pC[l][1] = 0x80808080u;
+            continue;
+        }
+        luma_block_pred(S.planes[slot * 3], g.W, g.H, vx >> 2, vy >> 2, vx & 3, vy & 3, pY[l]);
+#pragma unroll
+        for (int pl = 0; pl < 2; ++pl)
+            pC[l][pl] = chroma_block_pred(S.planes[slot * 3 + 1 + pl], g.Wc, g.Hc, vx >> 3, vy >> 3, vx & 7, vy & 7);
+    }
+    uint32_t predY[4], predC[2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) predY[i] = wp_combine4(qs, wp_mode, dir, r0, r1, pY[0][i], pY[1][i], 0);
+#pragma unroll
+    for (int pl = 0; pl < 2; ++pl) predC[pl] = wp_combine4(qs, wp_mode, dir, r0, r1, pC[0][pl], pC[1][pl], 1 + pl);
+
+    // ---- luma residual (transform.cc:1058-1073)
+    int res[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) res[i][c] = 0;
+    if (__any(cbpl != 0)) {
+        const int per = qpl / 6;
+        int d[4][4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const uint4 lw = lev[i >> 1], sw = lsc[i >> 1];
+                const uint32_t lo_ = (i & 1) ? lw.z : lw.x, hi_ = (i & 1) ? lw.w : lw.y;
+                const uint32_t slo = (i & 1) ? sw.z : sw.x, shi = (i & 1) ? sw.w : sw.y;
+                const int lvv = sel16(lo_, hi_, c), scv = sel16(slo, shi, c);
+                d[i][c] = t8 ? dq8(lvv, scv, per) : dq4(lvv, scv, per);
+            }
+        if (!__any(t8 != 0)) {
+            // 4x4: rows then columns, all in-lane
+#pragma unroll
+            for (int i = 0; i < 4; ++i) idct4_inplace(d[i][0], d[i][1], d[i][2], d[i][3]);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) idct4_inplace(d[0][c], d[1][c], d[2][c], d[3][c]);
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) res[i][c] = (d[i][c] + 32) >> 6;
+        } else {
+            // 8x8 (only t8 MBs reach here with d != 0 for their lanes; 4x4 MBs of the same
+            // wave take the in-lane path below).  Rows: my 4 + the 4 of lane ^ 1.
+            int e4[4][4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                int in[8], outv[8];
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const int ov = __shfl_xor(d[i][c], 1);
+                    in[c] = (bx & 1) ? ov : d[i][c];
+                    in[4 + c] = (bx & 1) ? d[i][c] : ov;
+                }
+                idct8(in, outv);
+#pragma unroll
+                for (int c = 0; c < 4; ++c) e4[i][c] = (bx & 1) ? outv[4 + c] : outv[c];
+            }
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                int in[8], outv[8];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int ov = __shfl_xor(e4[i][c], 4);
+                    in[i] = (by & 1) ? ov : e4[i][c];
+                    in[4 + i] = (by & 1) ? e4[i][c] : ov;
+                }
+                idct8(in, outv);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) res[i][c] = t8 ? ((by & 1) ? outv[4 + i] : outv[i]) : 0;
+            }
+            if (!t8) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) idct4_inplace(d[i][0], d[i][1], d[i][2], d[i][3]);
+#pragma unroll
+                for (int c = 0; c < 4; ++c) idct4_inplace(d[0][c], d[1][c], d[2][c], d[3][c]);
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) res[i][c] = ((t8 ? res[i][c] : d[i][c]) + 32) >> 6;
+        }
+    }
+    // ---- construction + store, luma
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        uint32_t wv = 0;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) wv |= (uint32_t)clip255((int)((predY[i] >> (8 * c)) & 255) + res[i][c]) << (8 * c);
+        *reinterpret_cast<uint32_t*>(ydst + (size_t)i * g.W) = wv;
+    }
+
+    // ---- chroma residual (transform.cc:1081-1091, DC :875-889): chroma block cb is
+    // spread over lanes {blk, ^1, ^4, ^5}; my quadrant rows cr.., cols cc..
+#pragma unroll
+    for (int pl = 0; pl < 2; ++pl) {
+        int rc[2][2] = {{0, 0}, {0, 0}};
+        if (__any(cbpc != 0)) {
+            const int qpc = q.qp_scaled[1 + pl], per = qpc / 6;
+            int k[2][2];
+#pragma unroll
+            for (int r = 0; r < 2; ++r)
+#pragma unroll
+                for (int c = 0; c < 2; ++c)
+                    k[r][c] = dq4((int16_t)(clev[pl][r] >> (16 * c)), (int16_t)(csc[pl][r] >> (16 * c)), per);
+            const int c00 = (int16_t)(cdc[pl].x & 0xFFFF), c01 = (int16_t)(cdc[pl].x >> 16);
+            const int c10 = (int16_t)(cdc[pl].y & 0xFFFF), c11 = (int16_t)(cdc[pl].y >> 16);
+            const int e00 = c00 + c01, e01 = c00 - c01, e10 = c10 + c11, e11 = c10 - c11;
+            const int f = cb == 0 ? e00 + e10 : cb == 1 ? e01 + e11 : cb == 2 ? e00 - e10 : e01 - e11;
+            if (cr == 0 && cc == 0) k[0][0] = cbpc ? ((f * cdcs[pl]) * (1 << per)) >> 5 : 0;
+            // rows: my 2 columns + the 2 of lane ^ 1
+            int t[2][2];
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                const int o0 = __shfl_xor(k[r][0], 1), o1 = __shfl_xor(k[r][1], 1);
+                const int d0 = cc ? o0 : k[r][0], d1 = cc ? o1 : k[r][1], d2 = cc ? k[r][0] : o0, d3 = cc ? k[r][1] : o1;
+                int y0, y1, y2, y3;
+                idct4(d0, d1, d2, d3, y0, y1, y2, y3);
+                t[r][0] = cc ? y2 : y0;
+                t[r][1] = cc ? y3 : y1;
+            }
+            // columns: my 2 rows + the 2 of lane ^ 4
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                const int o0 = __shfl_xor(t[0][c], 4), o1 = __shfl_xor(t[1][c], 4);
+                const int d0 = cr ? o0 : t[0][c], d1 = cr ? o1 : t[1][c], d2 = cr ? t[0][c] : o0, d3 = cr ? t[1][c] : o1;
+                int y0, y1, y2, y3;
+                idct4(d0, d1, d2, d3, y0, y1, y2, y3);
+                rc[0][c] = ((cr ? y2 : y0) + 32) >> 6;
+                rc[1][c] = ((cr ? y3 : y1) + 32) >> 6;
+            }
+        }
+        uint8_t* cdst = (pl ? o.v : o.u) + coff;
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            const uint32_t pr = predC[pl] >> (16 * r);
+            const uint32_t wv = (uint32_t)clip255((int)(pr & 255) + rc[r][0]) |
+                                ((uint32_t)clip255((int)((pr >> 8) & 255) + rc[r][1]) << 8);
+            *reinterpret_cast<uint16_t*>(cdst + (size_t)r * g.Wc) = (uint16_t)wv;
+        }
+    }
+}
+
+}  // namespace h264r
