@@ -22,16 +22,16 @@
 #include "h264r.h"
 
 namespace h264r { struct DbInfo; }
-extern "C" __global__ void k_prep(h264r_batch b, uint2* mot);
+extern "C" __global__ void k_prep(h264r_batch b, uint2* mot, int2 rows);
 extern "C" __global__ void k_inter(h264r_batch b, const uint2* mot);
 extern "C" __global__ void k_dbinfo(h264r_batch b, const uint2* mot, h264r::DbInfo* dbinfo);
-extern "C" __global__ void k_inter4(h264r_batch b, const uint2* mot, h264r::DbInfo* dbinfo);
-extern "C" __global__ void k_intra_pic(h264r_batch b, int* sync, int* err, const uint16_t* lvl, int lmax);
-extern "C" __global__ void k_level(h264r_batch b, uint16_t* lvl, int* lvsync);
-extern "C" __global__ void k_intra_levels(h264r_batch b, const uint16_t* lvl, int lmax, int* lvsync, int* err);
+extern "C" __global__ void k_inter4(h264r_batch b, const uint2* mot, h264r::DbInfo* dbinfo, int2 rows);
+extern "C" __global__ void k_intra_pic(h264r_batch b, int* sync, int* err, const uint16_t* lvl, int lmax, int2 rows);
+extern "C" __global__ void k_level(h264r_batch b, uint16_t* lvl, int* lvsync, int2 rows);
+extern "C" __global__ void k_intra_levels(h264r_batch b, const uint16_t* lvl, int lmax, int* lvsync, int* err, int2 rows);
 constexpr int LEVEL_MAX_MBS = 65536;      // k_level's LDS bitmap (k_picture.hip)
 extern "C" __global__ void k_deblock(h264r_batch b, const h264r::DbInfo* dbinfo, uint64_t* hb,
-                                     int* sync, int* err, uint32_t epoch);
+                                     int* sync, int* err, uint32_t epoch, int2 rows);
 constexpr size_t DBINFO_BYTES = 80;
 constexpr size_t HANDOFF_BYTES = 256;   // one tagged record (32 x {dword, epoch}) per MB
 
@@ -356,10 +356,13 @@ static bool inter4()
     return v;
 }
 
-static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s)
+// rows [row0, row1): the MB rows of every picture this launch reconstructs and
+// deblocks (the whole picture, or a slice-aligned band: h264r_decode_batch_rows).
+static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row0, int row1)
 {
-    const int W = b.width_mbs, H = b.height_mbs, P = b.num_pics;
-    const int nbands = (H + 15) / 16, npairs = (H + 1) / 2;
+    const int W = b.width_mbs, H = b.height_mbs, P = b.num_pics, HB = row1 - row0;
+    const int2 rows = make_int2(row0, row1);
+    const int nbands = (HB + 15) / 16, npairs = (HB + 1) / 2;
     const int CP = std::min(chunk_pictures(P), P), K = (P + CP - 1) / CP;
     // scratch: per-MB deblocking records and resolved motion (whole batch), tagged
     // row-pair hand-off records (one chunk; chunks deblock in stream order), and per
@@ -411,12 +414,12 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s)
         // stream s: prep + inter of chunk k
         {
             Timed t(c, 0, s);
-            hipLaunchKernelGGL(k_prep, dim3((unsigned)((mplane + 255) / 256), n), dim3(256), 0, s, cb,
-                               c->d_mot + (size_t)p0 * 2 * mplane);
+            hipLaunchKernelGGL(k_prep, dim3((unsigned)((HB * 16 * W + 255) / 256), n), dim3(256), 0, s, cb,
+                               c->d_mot + (size_t)p0 * 2 * mplane, rows);
             HIP_OK(hipGetLastError());
-            if (inter4()) {
-                hipLaunchKernelGGL(k_inter4, dim3((W * H + 15) / 16, n), dim3(256), 0, s, cb,
-                                   c->d_mot + (size_t)p0 * 2 * mplane, dbinfo_at(p0));
+            if (inter4() || HB != H) {
+                hipLaunchKernelGGL(k_inter4, dim3((W * HB + 15) / 16, n), dim3(256), 0, s, cb,
+                                   c->d_mot + (size_t)p0 * 2 * mplane, dbinfo_at(p0), rows);
                 HIP_OK(hipGetLastError());
             } else {
                 hipLaunchKernelGGL(k_dbinfo, dim3((W * H + 3) / 4, n), dim3(256), 0, s, cb,
@@ -437,14 +440,14 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s)
             const int lmax = levels ? level_launches() : 0;
             if (levels) {
                 int* lvsync = sync + 1 + (size_t)CP * H + 2;
-                hipLaunchKernelGGL(k_level, dim3(n), dim3(64 * ((H + 63) / 64)), 0, si, cb, lvl, lvsync);
+                hipLaunchKernelGGL(k_level, dim3(n), dim3(64 * ((HB + 63) / 64)), 0, si, cb, lvl, lvsync, rows);
                 HIP_OK(hipGetLastError());
                 hipLaunchKernelGGL(k_intra_levels, dim3(c->levels_grid), dim3(256), 0, si, cb, (const uint16_t*)lvl,
-                                   lmax, lvsync, c->d_err);
+                                   lmax, lvsync, c->d_err, rows);
                 HIP_OK(hipGetLastError());
             }
             hipLaunchKernelGGL(k_intra_pic, dim3(n * nbands), dim3(1024), 0, si, cb, sync, c->d_err,
-                               (const uint16_t*)lvl, lmax);
+                               (const uint16_t*)lvl, lmax, rows);
             HIP_OK(hipGetLastError());
         }
         if (K > 1) {
@@ -454,7 +457,7 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s)
         if (deblock) {
             Timed t(c, 2, sd);
             hipLaunchKernelGGL(k_deblock, dim3(n * npairs), dim3(64), 0, sd, cb, dbinfo_at(p0),
-                               reinterpret_cast<uint64_t*>(c->d_hb), sync + 1 + (size_t)CP * H, c->d_err, ++c->epoch);
+                               reinterpret_cast<uint64_t*>(c->d_hb), sync + 1 + (size_t)CP * H, c->d_err, ++c->epoch, rows);
             HIP_OK(hipGetLastError());
         }
     }
@@ -489,12 +492,26 @@ int h264r_decode_batch(h264r_ctx* c, const h264r_batch* b, void* stream)
     if (!bb.ref_planes) bb.ref_planes = c->d_ref_planes;
     hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : c->stream;
 #ifdef H264R_TRACE
-    int st = launch_all(c, bb, s);
+    int st = launch_all(c, bb, s, 0, bb.height_mbs);
     dump_trace(s);
     return st;
 #else
-    return launch_all(c, bb, s);
+    return launch_all(c, bb, s, 0, bb.height_mbs);
 #endif
+}
+
+int h264r_decode_batch_rows(h264r_ctx* c, const h264r_batch* b, int row0, int row1, void* stream)
+{
+    if (!c || !b || row0 < 0 || row1 <= row0 || row1 > b->height_mbs) return H264R_EINVAL;
+    if (!b->mbs || !b->levels || !b->mv || !b->ref_idx || !b->slices || !b->pics || !b->quant || !b->out_y ||
+        !b->out_u || !b->out_v || b->num_pics <= 0 || b->width_mbs <= 0 || b->width_mbs > c->max_w ||
+        b->height_mbs > c->max_h || b->slice_stride <= 0)
+        return H264R_EINVAL;
+    (void)hipSetDevice(c->device);
+    h264r_batch bb = *b;
+    if (!bb.ref_planes) bb.ref_planes = c->d_ref_planes;
+    hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : c->stream;
+    return launch_all(c, bb, s, row0, row1);
 }
 
 int h264r_set_timing(h264r_ctx* c, int enable)
@@ -630,7 +647,7 @@ int h264r_picture_end(h264r_ctx* c, uint8_t* y, uint8_t* u, uint8_t* v, int keep
     b.mbs = c->d_mbs; b.levels = c->d_levels; b.mv = c->d_mv; b.ref_idx = c->d_ref; b.slices = c->d_slices;
     b.pics = c->d_pic; b.quant = c->d_quant; b.ref_planes = c->d_ref_planes;
     b.out_y = c->d_out; b.out_u = c->d_out + ys; b.out_v = c->d_out + ys + cs;
-    if ((st = launch_all(c, b, s))) return st;
+    if ((st = launch_all(c, b, s, 0, b.height_mbs))) return st;
     if (keep_slot >= 0) {
         if ((st = ensure_slot(c, keep_slot, c->pw, c->ph))) return st;
         HIP_OK(hipMemcpyAsync(c->slot[keep_slot][0], c->d_out, ys + 2 * cs, hipMemcpyDeviceToDevice, s));

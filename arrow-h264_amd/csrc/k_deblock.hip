@@ -67,20 +67,21 @@ __device__ unsigned long long h264r_db_trace[1 << 16][8];
 // hb: hand-off records [pic][pair][W][32] granules {RingEntry dword, epoch};
 // sync[0]: ticket counter; epoch: this launch's tag (never 0: hb is zeroed when allocated).
 extern "C" __global__ __launch_bounds__(64) void k_deblock(h264r_batch b, const DbInfo* __restrict__ dbinfo,
-                                                          uint64_t* hb, int* sync, int* err, uint32_t epoch)
+                                                          uint64_t* hb, int* sync, int* err, uint32_t epoch, int2 rows)
 {
     __shared__ PairLds L;
     const int lane = threadIdx.x, h = lane >> 5, hl = lane & 31;
     const Geom g = make_geom(b.width_mbs, b.height_mbs);
-    const int W = g.wmb, H = g.hmb, npairs = (H + 1) >> 1;
+    // rows [R0, H): the MB rows decoded by this launch (a slice-aligned band, h264r_decode_batch_rows)
+    const int W = g.wmb, R0 = rows.x, H = rows.y, npairs = (H - R0 + 1) >> 1;
 
     int tk = 0;
     if (lane == 0) tk = atomicAdd(&sync[0], 1);
     const int ticket = __builtin_amdgcn_readfirstlane(tk);
     TRACE(unsigned long long tr_start = __builtin_amdgcn_s_memrealtime();)
     const int rp = ticket / b.num_pics, pic = ticket % b.num_pics;
-    const int r = 2 * rp + h;                              // this half's MB row
-    const bool hasB = 2 * rp + 1 < H;
+    const int r = R0 + 2 * rp + h;                         // this half's MB row
+    const bool hasB = R0 + 2 * rp + 1 < H;
     const bool half_on = r < H;
     const bool last_row = r == H - 1;
     const bool feeds_ring = h == 0 && hasB;                // A -> B through LDS
@@ -116,13 +117,13 @@ extern "C" __global__ __launch_bounds__(64) void k_deblock(h264r_batch b, const 
         uint8_t* ptr = Y;
         if (e < 95) {
             const int row = e / 5 - 3, dw = e % 5;
-            const bool v = row < 0 ? (r > 0 && dw >= 1) : (row <= 12 || last_row);
+            const bool v = row < 0 ? (r > R0 && dw >= 1) : (row <= 12 || last_row);
             f = (v ? 1 : 0) | (row >= 0 && dw == 0 ? 2 : 0) | (row >= 0 && dw == 4 ? 4 : 0);
             word = (row + 4) * TP + dw;
             ptr = Y + (ptrdiff_t)(Y0 + row) * g.W + 4 * (dw - 1);
         } else if (e < 161) {
             const int k = e - 95, pl = k / 33, k2 = k - pl * 33, row = k2 / 3 - 3, dw = k2 % 3;
-            const bool v = row < 0 ? (r > 0 && dw >= 1) : (row <= 4 || last_row);
+            const bool v = row < 0 ? (r > R0 && dw >= 1) : (row <= 4 || last_row);
             f = (v ? 1 : 0) | (row >= 0 && dw == 0 ? 2 : 0) | (row >= 0 && dw == 2 ? 4 : 0) | 8;
             word = (1 + pl) * TR * TP + (row + 4) * TP + dw;
             ptr = Cp[pl] + (ptrdiff_t)(Yc + row) * g.Wc + 4 * (dw - 1);
@@ -209,7 +210,11 @@ extern "C" __global__ __launch_bounds__(64) void k_deblock(h264r_batch b, const 
         Sw[a_y1] = pf_y1;
         Sw[a_c] = pf_c;
         if (hl < DBINFO_DWORDS) S.info[hl] = pf_i;
-        if (r > 0) Sw[a_top] = h == 0 ? (uint32_t)pf_top : reinterpret_cast<const uint32_t*>(&L.ring[0][x & (DRING - 1)])[hl];
+        // a band that starts below row 0 must not be filtered across its top edge (idc 1 or
+        // a slice edge with idc 2): its top-edge strengths (bs[16..19] = info dword 4) are 0
+        if (r == R0 && R0 > 0 && act && hl == 4 && pf_i != 0)
+            __hip_atomic_store(err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (r > R0) Sw[a_top] = h == 0 ? (uint32_t)pf_top : reinterpret_cast<const uint32_t*>(&L.ring[0][x & (DRING - 1)])[hl];
         TRACE(asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); tph[0] += __builtin_amdgcn_s_memtime() - ta;)
         if (t + 1 < steps) prefetch(t + 1);
         wave_sync();

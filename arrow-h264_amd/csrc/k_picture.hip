@@ -65,22 +65,23 @@ DEV bool wait_for(int* counter, int need, int* err)
 // sync: [0] ticket counter, [1 ..] per (picture, row) progress; zeroed before every launch.
 template <typename Scratch>
 DEV void picture_walk(const h264r_batch& b, int* sync, int* err, Scratch* scratch,
-                      int* lprog, int* ticket_lds, const uint16_t* __restrict__ lvl, int lmax)
+                      int* lprog, int* ticket_lds, const uint16_t* __restrict__ lvl, int lmax, int2 rows)
 {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const Geom g = make_geom(b.width_mbs, b.height_mbs);
-    const int nbands = (g.hmb + WAVES - 1) / WAVES;
-    const int bh = (g.hmb + nbands - 1) / nbands;            // rows per band (<= 16)
+    const int R0 = rows.x, R1 = rows.y, HB = R1 - R0;         // MB rows of this launch
+    const int nbands = (HB + WAVES - 1) / WAVES;
+    const int bh = (HB + nbands - 1) / nbands;               // rows per band (<= 16)
     if (threadIdx.x == 0) *ticket_lds = atomicAdd(&sync[0], 1);
     if (threadIdx.x < WAVES) lprog[threadIdx.x] = 0;
     __syncthreads();
     const int ticket = *ticket_lds;
     const int band = ticket / b.num_pics, pic = ticket % b.num_pics;
-    const int r0 = band * bh, r1 = min(g.hmb, r0 + bh);
+    const int r0 = R0 + band * bh, r1 = min(R1, r0 + bh);
     const int r = r0 + wave;
     if (r >= r1) return;
     int* gprog = sync + 1 + (size_t)pic * g.hmb;
-    const bool last_row = r == r1 - 1 && r1 < g.hmb;
+    const bool last_row = r == r1 - 1 && r1 < R1;
     Scratch& S = scratch[wave];
     const h264r_mb* mbs = b.mbs + (size_t)pic * g.nmb;
     bool ok = true;
@@ -111,7 +112,7 @@ DEV void picture_walk(const h264r_batch& b, int* sync, int* err, Scratch* scratc
     int x = next_intra(0);
     publish(x);
     while (x < g.wmb && ok) {
-        if (r > 0) {
+        if (r > R0) {
             const int need = min(x + 2, g.wmb);
             if (wave == 0) ok = wait_for<true>(&gprog[r - 1], need, err);
             else ok = wait_for<false>(&lprog[wave - 1], need, err);
@@ -127,12 +128,12 @@ DEV void picture_walk(const h264r_batch& b, int* sync, int* err, Scratch* scratc
 // lvl / lmax: intra MBs with lvl <= lmax were reconstructed by the k_intra_lvl
 // launches before this one (lvl == nullptr: the walk does every intra MB).
 extern "C" __global__ __launch_bounds__(1024) void k_intra_pic(h264r_batch b, int* sync, int* err,
-                                                              const uint16_t* lvl, int lmax)
+                                                              const uint16_t* lvl, int lmax, int2 rows)
 {
     __shared__ IntraScratch scratch[WAVES];
     __shared__ int lprog[WAVES];
     __shared__ int ticket;
-    picture_walk(b, sync, err, scratch, lprog, &ticket, lvl, lmax);
+    picture_walk(b, sync, err, scratch, lprog, &ticket, lvl, lmax, rows);
 }
 
 // ------------------------------------------------------------ level schedule
@@ -150,32 +151,33 @@ extern "C" __global__ __launch_bounds__(1024) void k_intra_pic(h264r_batch b, in
 // k_level: one workgroup per picture, thread r = MB row r, which walks its row in
 // lock step: at step t thread r does MB x = t - 2r, after (x+1, r-1) was done at
 // step t-1.  Each row keeps its last four levels in an LDS ring.
-extern "C" __global__ __launch_bounds__(1024) void k_level(h264r_batch b, uint16_t* lvl, int* lvsync)
+extern "C" __global__ __launch_bounds__(1024) void k_level(h264r_batch b, uint16_t* lvl, int* lvsync, int2 rows)
 {
     __shared__ uint64_t bits[H264R_LEVEL_MAX_MBS / 64];   // intra (not PCM) MBs of the picture
     __shared__ uint16_t ring[1024][4];
     const Geom g = make_geom(b.width_mbs, b.height_mbs);
     const int pic = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
     const h264r_mb* mbs = b.mbs + (size_t)pic * g.nmb;
-    for (int base = 0; base < g.nmb; base += blockDim.x) {
+    const int R0 = rows.x, HB = rows.y - rows.x, mend = rows.y * g.wmb;   // rows above R0 count as level 0
+    for (int base = R0 * g.wmb; base < mend; base += blockDim.x) {
         const int m = base + tid;
         bool in = false;
-        if (m < g.nmb) {
+        if (m < mend) {
             const uint32_t w0 = *reinterpret_cast<const uint32_t*>(&mbs[m]);
             in = ((w0 >> 8) & H264R_MBF_INTRA) && (w0 & 255) != H264R_I_PCM;
         }
         const uint64_t bl = __ballot(in);
-        if (lane == 0 && m < g.nmb) bits[(base + tid) >> 6] = bl;
+        if (lane == 0 && m < mend) bits[(base + tid - R0 * g.wmb) >> 6] = bl;
     }
     __syncthreads();
-    const int r = tid;
-    uint16_t* out = lvl + (size_t)pic * g.nmb + (size_t)r * g.wmb;
+    const int r = tid;                                      // band row; MB row R0 + r
+    uint16_t* out = lvl + (size_t)pic * g.nmb + (size_t)(R0 + r) * g.wmb;
     int left = 0, deepest = 0;
-    const int steps = g.wmb + 2 * (g.hmb - 1);
+    const int steps = g.wmb + 2 * (HB - 1);
     for (int t = 0; t < steps; ++t) {
         const int x = t - 2 * r;
-        if (r < g.hmb && x >= 0 && x < g.wmb) {
-            const int m = r * g.wmb + x;
+        if (r < HB && x >= 0 && x < g.wmb) {
+            const int m = r * g.wmb + x;            // band-relative MB index
             int L = 0;
             if ((bits[m >> 6] >> (m & 63)) & 1) {
                 int up = 0;
@@ -244,24 +246,25 @@ extern "C" __global__ void k_intra_trace_dump(unsigned long long* out, unsigned*
 #endif
 
 extern "C" __global__ __launch_bounds__(256, H264R_LVL_WAVES) void k_intra_levels(h264r_batch b, const uint16_t* __restrict__ lvl,
-                                                                                int lmax, int* lvsync, int* err)
+                                                                                int lmax, int* lvsync, int* err, int2 rows)
 {
     __shared__ IntraScratch scratch[4];
     const Geom g = make_geom(b.width_mbs, b.height_mbs);
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const size_t total = (size_t)g.nmb * b.num_pics;
+    const int nb = (rows.y - rows.x) * g.wmb, m0 = rows.x * g.wmb;    // band MBs per picture
+    const size_t total = (size_t)nb * b.num_pics;
     const size_t gw = (size_t)blockIdx.x * 4 + wave, step = (size_t)gridDim.x * 4 * 64;
     const int deepest = __hip_atomic_load(&lvsync[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int top = min(lmax, deepest);
     for (int L = 1; L <= top; ++L) {
         for (size_t base = gw * 64; base < total; base += step) {
             const size_t e = base + lane;
-            const bool hit = e < total && lvl[e] == L;
+            const bool hit = e < total && lvl[(e / nb) * g.nmb + m0 + e % nb] == L;
             uint64_t todo = __ballot(hit);
             while (todo) {
                 const size_t k = base + __builtin_ctzll(todo);
                 todo &= todo - 1;
-                const int pic = (int)(k / g.nmb), a = (int)(k % g.nmb);
+                const int pic = (int)(k / nb), a = m0 + (int)(k % nb);
 #ifdef H264R_TRACE_INTRA
                 const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -273,7 +276,7 @@ extern "C" __global__ __launch_bounds__(256, H264R_LVL_WAVES) void k_intra_level
                     const unsigned slot = atomicAdd(&h264r_intra_trace_n, 1u);
                     if (slot < (1u << 20)) {
                         h264r_intra_trace[slot][0] = t0; h264r_intra_trace[slot][1] = t1;
-                        h264r_intra_trace[slot][2] = ((unsigned long long)L << 32) | (unsigned)(b.mbs[k].mb_type);
+                        h264r_intra_trace[slot][2] = ((unsigned long long)L << 32) | (unsigned)(b.mbs[(size_t)pic * g.nmb + a].mb_type);
                         h264r_intra_trace[slot][3] = (unsigned long long)gw;
                     }
                 }

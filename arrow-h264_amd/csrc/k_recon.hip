@@ -16,11 +16,11 @@
 
 using namespace h264r;
 
-extern "C" __global__ __launch_bounds__(256) void k_prep(h264r_batch b, uint2* __restrict__ mot)
+extern "C" __global__ __launch_bounds__(256) void k_prep(h264r_batch b, uint2* __restrict__ mot, int2 rows)
 {
     const Geom g = make_geom(b.width_mbs, b.height_mbs);
-    const int idx = blockIdx.x * 256 + threadIdx.x, pic = blockIdx.y;
-    if (idx >= g.motion_plane) return;
+    const int idx = rows.x * 4 * g.W4 + blockIdx.x * 256 + threadIdx.x, pic = blockIdx.y;
+    if (idx >= rows.y * 4 * g.W4) return;
     const int bx4 = idx % g.W4, by4 = idx / g.W4;
     const h264r_mb* mb = &b.mbs[(size_t)pic * g.nmb + (by4 >> 2) * g.wmb + (bx4 >> 2)];
     const h264r_slice* sl = &b.slices[(size_t)pic * b.slice_stride + mb->slice];
@@ -57,14 +57,16 @@ extern "C" __global__ __launch_bounds__(256) void k_dbinfo(h264r_batch b, const 
 
 // k_inter4: inter / I_PCM MBs and the deblocking record of every MB, four MBs per
 // wave, one lane per 4x4 block (mb_inter4.h).  Grid (ceil(nmb / 16), pictures).
-extern "C" __global__ __launch_bounds__(256) void k_inter4(h264r_batch b, const uint2* __restrict__ mot, DbInfo* dbinfo)
+extern "C" __global__ __launch_bounds__(256) void k_inter4(h264r_batch b, const uint2* __restrict__ mot, DbInfo* dbinfo,
+                                                           int2 rows)
 {
     __shared__ Inter4Lds S;
     if (threadIdx.x < 3 * H264R_MAX_SLOTS) S.planes[threadIdx.x] = b.ref_planes[threadIdx.x];
     __syncthreads();
     const Geom g = make_geom(b.width_mbs, b.height_mbs);
     const int pic = blockIdx.y, lane = threadIdx.x & 63;
-    const int a0 = (blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) * 4;
-    if (a0 >= g.nmb) return;
-    inter4_mbs(b, g, pic, a0, lane, mot + (size_t)pic * 2 * g.motion_plane, dbinfo + (size_t)pic * g.nmb, S);
+    const int a0 = rows.x * g.wmb + (blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) * 4;
+    const int aend = rows.y * g.wmb;
+    if (a0 >= aend) return;
+    inter4_mbs(b, g, pic, a0, aend, lane, mot + (size_t)pic * 2 * g.motion_plane, dbinfo + (size_t)pic * g.nmb, S);
 }

@@ -282,13 +282,13 @@ DEV void idct4_inplace(int& a, int& b, int& c, int& d)
 
 // The inter / I_PCM macroblocks a0 .. a0+3 of picture `pic` and the deblocking
 // records of all four.  `mot`: the picture's resolved motion (k_prep).
-DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int lane, const uint2* __restrict__ mot,
+DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int aend, int lane, const uint2* __restrict__ mot,
                     DbInfo* __restrict__ dbout, const Inter4Lds& S)
 {
     const int grp = lane >> 4, blk = lane & 15, bx = blk & 3, by = blk >> 2;
     const int a = a0 + grp;
-    const bool valid = a < g.nmb;
-    const int aa = valid ? a : g.nmb - 1;
+    const bool valid = a < aend;
+    const int aa = valid ? a : aend - 1;
     const int mbx = aa % g.wmb, mby = aa / g.wmb;
     const h264r_mb* mbs = b.mbs + (size_t)pic * g.nmb;
     const h264r_slice* slices = b.slices + (size_t)pic * b.slice_stride;

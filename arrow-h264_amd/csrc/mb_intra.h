@@ -403,22 +403,20 @@ DEV void intra_mb2(const h264r_batch& b, const Geom& g, int pic, int mbx, int mb
                 if (yO == 0) aC = xO + 4 < 16 ? avB : avC;
                 else aC = (xO + 4 < 16) && !(xO == 4 && (yO == 4 || yO == 12));      // :154
                 const int mode = (m.ipred[bk >> 1] >> ((bk & 1) * 4)) & 15;
-                int p;
-                if (mode == 2) {                                       // DC (intra_prediction.cc:214-229)
-                    const int st = sum4(lds_u32(&S.tile[ti(xO, yO - 1)]));
-                    int sl = 0;
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) sl += S.tile[ti(xO - 1, yO + k)];
-                    p = aA && aB ? (st + sl + 4) >> 3 : aB ? (st + 2) >> 2 : aA ? (sl + 2) >> 2 : 128;
-                } else {
-                    const int ent = intra_tap_entry(tab, mode), kind = ent >> 5, i = ent & 31;
-                    const int tmax = aC ? 7 : 3;
-                    auto E = [&](int k) -> int {                       // e[k] from the tile
-                        return k <= 5 ? S.tile[ti(xO - 1, yO + min(3, 4 - k))] : S.tile[ti(xO + min(k - 6, tmax), yO - 1)];
-                    };
-                    p = tap_apply(kind, E(max(i - 1, 0)), E(i), E(min(i + 1, 14)));
-                }
-                const int v = (cbpl >> ((yO >> 3) * 2 + (xO >> 3))) & 1 ? clip255(p + S.res[yO + y][xO + x]) : p;
+                // branch-free: the directional tap and DC are both evaluated, then selected
+                const int ent = intra_tap_entry(tab, mode), kind = ent >> 5, i = ent & 31;
+                const int tmax = aC ? 7 : 3;
+                const int base = ti(xO, yO);
+                auto eoff = [&](int k) -> int {                          // tile offset of e[k] from the block origin
+                    return k <= 5 ? min(3, 4 - k) * ITP - 1 : min(k - 6, tmax) - ITP;
+                };
+                const int e0 = S.tile[base + eoff(max(i - 1, 0))], e1 = S.tile[base + eoff(i)];
+                const int e2 = S.tile[base + eoff(min(i + 1, 14))];
+                const int st = sum4(lds_u32(&S.tile[base - ITP]));       // DC (intra_prediction.cc:214-229)
+                const int sl = S.tile[base - 1] + S.tile[base + ITP - 1] + S.tile[base + 2 * ITP - 1] + S.tile[base + 3 * ITP - 1];
+                const int dc = aA && aB ? (st + sl + 4) >> 3 : aB ? (st + 2) >> 2 : aA ? (sl + 2) >> 2 : 128;
+                const int p = mode == 2 ? dc : tap_apply(kind, e0, e1, e2);
+                const int v = clip255(p + S.res[yO + y][xO + x]);     // residual is 0 in uncoded blocks
                 S.tile[ti(xO + x, yO + y)] = (uint8_t)v;
             }
             wave_sync();

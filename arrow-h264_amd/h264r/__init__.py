@@ -71,6 +71,7 @@ def lib() -> C.CDLL:
         "h264r_mb_submit": ([P, I, P, P, I, P, P], I),
         "h264r_picture_end": ([P, P, P, P, I], I),
         "h264r_decode_batch": ([P, C.POINTER(A.Batch), P], I),
+        "h264r_decode_batch_rows": ([P, C.POINTER(A.Batch), I, I, P], I),
         "h264r_ref_planes": ([P, I, C.POINTER(P), C.POINTER(P), C.POINTER(P)], I),
         "h264r_last_timing": ([P, C.POINTER(C.c_float)], I),
         "h264r_set_timing": ([P, I], I), "h264r_set_debug": ([P, I], I),
@@ -201,8 +202,14 @@ class Decoder:
         _check("h264r_ref_planes", self._L.h264r_ref_planes(self._h, slot, C.byref(y), C.byref(u), C.byref(v)))
         return y.value, u.value, v.value
 
-    def decode_batch(self, batch: A.Batch, stream: int | None = None) -> None:
-        _check("h264r_decode_batch", self._L.h264r_decode_batch(self._h, C.byref(batch), C.c_void_p(stream or 0)))
+    def decode_batch(self, batch: A.Batch, stream: int | None = None, rows: tuple[int, int] | None = None) -> None:
+        """Reconstruct + deblock every picture of a device-resident batch; with `rows` =
+        (row0, row1) only that slice-aligned band of MB rows (h264r_decode_batch_rows)."""
+        if rows is None:
+            _check("h264r_decode_batch", self._L.h264r_decode_batch(self._h, C.byref(batch), C.c_void_p(stream or 0)))
+        else:
+            _check("h264r_decode_batch_rows", self._L.h264r_decode_batch_rows(
+                self._h, C.byref(batch), int(rows[0]), int(rows[1]), C.c_void_p(stream or 0)))
 
     def check(self) -> None:
         """Synchronise and raise if a device-side wavefront wait timed out."""

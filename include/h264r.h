@@ -219,6 +219,17 @@ int  h264r_picture_end(h264r_ctx* ctx, uint8_t* y, uint8_t* u, uint8_t* v,
 /* Launches recon + deblock for every picture of the batch on `stream`
  * (a hipStream_t, NULL = the context's stream).  Asynchronous. */
 int  h264r_decode_batch(h264r_ctx* ctx, const h264r_batch* batch, void* stream);
+
+/* Slice-sharded form of h264r_decode_batch (multi-GPU): reconstruct and
+ * deblock only MB rows [row0, row1) of every picture of the batch.  The band must start
+ * at a slice boundary and must not be deblocked across its top edge (its first slice has
+ * disable_deblocking_filter_idc 1, or 2 with a slice edge there; deblock.cc:247-253);
+ * slices never predict across each other (intra_prediction.cc:145-152), so the band is
+ * then independent of the rows outside it.  Motion compensation still reads whole
+ * reference pictures.  A band whose top edge would be filtered is reported by
+ * h264r_check() as H264R_EDEVICE.  Replaces nothing in the reference (its decoder is
+ * single-threaded); the slice walk it parallelises is slice_data.cc:640-650. */
+int  h264r_decode_batch_rows(h264r_ctx* ctx, const h264r_batch* batch, int row0, int row1, void* stream);
 /* Device pointer of DPB slot planes (for building h264r_batch.ref_planes). */
 int  h264r_ref_planes(h264r_ctx* ctx, int slot, uint8_t** y, uint8_t** u, uint8_t** v);
 

@@ -160,3 +160,60 @@ def test_single_hip_runtime_in_process(L, dec):
     hip = {line.split()[-1] for line in maps.splitlines() if "libamdhip64" in line}
     assert len(hip) == 1, hip
     assert any("libh264r.so" in line for line in maps.splitlines())
+
+
+def _slice_first_rows(p):
+    W, H = p.cfg.width_mbs, p.cfg.height_mbs
+    s = p.mbs["slice"].reshape(H, W)[:, 0]
+    return [0] + [r for r in range(1, H) if s[r] != s[r - 1]]
+
+
+@pytest.mark.parametrize("cidx,W,H,world", [(4, 120, 68, 4), (4, 120, 68, 2), (5, 240, 135, 8), (5, 240, 135, 3)])
+def test_gpu_slice_bands_match_whole_picture(L, dec, cidx, W, H, world):
+    """Slice-sharded decode (multi-GPU mode): each rank's band, decoded on
+    its own by h264r_decode_batch_rows, equals those rows of the oracle's whole-picture
+    decode and leaves every other row untouched."""
+    from h264r import dist as D
+    import torch
+    n = 2
+    cfg = synth.default_cfg(L, cidx, W, H)
+    pics = [synth.picture(L, cfg, i) for i in range(n)]
+    refs = synth.refpics(L, cfg)
+    for s, (y, u, v) in enumerate(refs):
+        dec.set_ref(s, y, u, v)
+    want = [O.decode(p, refs) for p in pics]
+    bands = D.slice_bands(_slice_first_rows(pics[0]), H, world)
+    host = B.pack(pics, h264r.quant_flat())
+    for r0, r1 in bands:
+        if r1 == r0:
+            continue
+        db = B.to_device(host, n, None)
+        dec.decode_batch(db.batch, rows=(r0, r1))
+        dec.check()
+        torch.cuda.synchronize()
+        for i in range(n):
+            got = db.planes(i)
+            for k in range(3):
+                m = 16 if k == 0 else 8
+                inside = slice(r0 * m, r1 * m)
+                d = first_diff(got[k][inside], want[i][k][inside], m)
+                assert d is None, f"band {r0}..{r1} picture {i} plane {k}: {d}"
+                outside = np.ones(got[k].shape[0], bool)
+                outside[inside] = False
+                assert not got[k][outside].any(), f"band {r0}..{r1} wrote outside its rows"
+
+
+def test_gpu_band_across_filtered_edge_is_reported(L, dec):
+    """Config 3 deblocks across the whole picture (idc 0): a band starting inside it
+    would need rows it does not have, and h264r_check says so."""
+    cfg = synth.default_cfg(L, 3, 22, 18, num_slices=2)
+    p = synth.picture(L, cfg, 0)
+    refs = synth.refpics(L, cfg)
+    for s, (y, u, v) in enumerate(refs):
+        dec.set_ref(s, y, u, v)
+    db = B.to_device(B.pack([p], h264r.quant_flat()), 1, None)
+    r0 = _slice_first_rows(p)[1]
+    dec.decode_batch(db.batch, rows=(r0, 18))
+    with pytest.raises(h264r.H264RError) as e:
+        dec.check()
+    assert e.value.status == A.EDEVICE
