@@ -413,10 +413,10 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
         int* sync = c->d_sync + (size_t)k * sync_chunk;
         // stream s: prep + inter of chunk k
         {
-            Timed t(c, 0, s);
             hipLaunchKernelGGL(k_prep, dim3((unsigned)((HB * 16 * W + 255) / 256), n), dim3(256), 0, s, cb,
                                c->d_mot + (size_t)p0 * 2 * mplane, rows);
             HIP_OK(hipGetLastError());
+            Timed t(c, 0, s);                      // phase 0 = the inter kernel alone (k_prep is in the total only)
             if (inter4() || HB != H) {
                 hipLaunchKernelGGL(k_inter4, dim3((W * HB + 15) / 16, n), dim3(256), 0, s, cb,
                                    c->d_mot + (size_t)p0 * 2 * mplane, dbinfo_at(p0), rows);

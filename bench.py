@@ -102,6 +102,9 @@ def main() -> int:
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--shard", choices=["replicas", "slices"], default=None,
+                    help="N>1 placement: independent pictures per GPU, or slice bands of shared pictures "
+                         "(default: slices for configs 4/5, replicas for 2/3)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -125,25 +128,80 @@ def main() -> int:
     nb = args.batch or (64 if args.config == 5 else 256)
     cfg = synth.default_cfg(L, args.config, W, H)
     nmb = W * H
+    shard = args.shard or ("slices" if world > 1 and cfg.deblock_idc != 0 and cfg.num_slices > 1 else "replicas")
+    if shard == "slices" and cfg.deblock_idc == 0:
+        raise SystemExit("slice sharding needs disable_deblocking_filter_idc 1/2 (configs 4, 5)")
 
-    # inputs: this rank's stream of pictures (replicas: distinct picture indices per rank)
-    pics = [synth.picture(L, cfg, i) for i in D.picture_share(rank, world, nb)]
+    # inputs.  replicas: this rank's own pictures.  slices (weak scaling): every rank
+    # holds the same world * nb pictures and reconstructs its band of slices of each.
+    if shard == "replicas":
+        pics = [synth.picture(L, cfg, i) for i in D.picture_share(rank, world, nb)]
+    else:
+        pics = [synth.picture(L, cfg, i) for i in range(world * nb)]
+    npics = len(pics)
     refs = synth.refpics(L, cfg)
     rd = wr = 0
     for p in pics:
         r, w = synth.algo_bytes(L, p)
         rd += r
         wr += w
+    band = (0, H)
+    if shard == "slices":
+        srow = pics[0].mbs["slice"].reshape(H, W)[:, 0]
+        first = [0] + [r for r in range(1, H) if srow[r] != srow[r - 1]]
+        bands = D.slice_bands(first, H, world)
+        band = bands[rank]
+        frac = (band[1] - band[0]) / H
+        rd, wr = int(rd * frac), int(wr * frac)          # this rank's share (rows are uniform)
 
     dec = h264r.Decoder(local, W, H)
-    for s, (y, u, v) in enumerate(refs):
-        dec.set_ref(s, y, u, v)
+    # DPB slots as torch tensors (+ H264R_PLANE_SLACK) so that the slice mode's exchange
+    # can write a decoded picture straight into reference slot 0 on every rank
+    slack = 64
+    slot_t = []
+    for (y, u, v) in refs:
+        slot_t.append([torch.from_numpy(np.concatenate([a.reshape(-1), np.zeros(slack, np.uint8)])).to("cuda")
+                       for a in (y, u, v)])
+    tab = np.zeros(3 * 32, np.int64)
+    for s_, planes in enumerate(slot_t):
+        for k in range(3):
+            tab[3 * s_ + k] = planes[k].data_ptr()
+    tab_t = torch.from_numpy(tab).to("cuda")
     host = B.pack(pics, h264r.quant_flat())
-    db = B.to_device(host, nb, None)
+    db = B.to_device(host, npics, tab_t.data_ptr())
     stream = torch.cuda.current_stream().cuda_stream
 
+    def exchange():
+        """slice mode: picture 0's bands all-gathered over RCCL (xGMI) into reference slot 0
+        of every rank -- the decoded picture becomes the next step's reference."""
+        if shard != "slices":
+            return
+        outs = (db.tensors["out_y"][0].view(16 * H, 16 * W), db.tensors["out_u"][0].view(8 * H, 8 * W),
+                db.tensors["out_v"][0].view(8 * H, 8 * W))
+        for k, (t, m) in enumerate(zip(outs, (16, 8, 8))):
+            D.allgather_rows(t, m, bands, rank)
+            slot_t[0][k][: t.numel()].copy_(t.view(-1))
+
+    def step():
+        if band[1] > band[0]:
+            dec.decode_batch(db.batch, stream, rows=None if band == (0, H) else band)
+        exchange()
+
+    # correctness first (refs as generated): rank 0 checks picture 0 after the exchange
+    verified = None
+    if not args.no_verify:
+        step()
+        torch.cuda.synchronize()
+        dec.check()
+        if rank == 0:
+            sys.path.insert(0, os.path.join(ROOT, "tests"))
+            import _oracle as O
+            want = O.decode(pics[0], refs)
+            got = db.planes(0)
+            verified = all(np.array_equal(got[k], want[k]) for k in range(3))
+
     for _ in range(args.warmup):
-        dec.decode_batch(db.batch, stream)
+        step()
     torch.cuda.synchronize()
 
     # timed region: barrier + sync on both sides, exactly `steps` steps.  Every kernel
@@ -155,39 +213,33 @@ def main() -> int:
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        dec.decode_batch(db.batch, stream)
+        step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    kern = np.array(dec.last_timing())          # ms per step: inter, intra, deblock, whole batch
+    kern = np.array(dec.last_timing()) if band[1] > band[0] else np.zeros(4)
     dec.set_timing(False)
     dt = D.max_over_ranks(dt, device="cuda")
 
-    verified = None
-    if not args.no_verify and rank == 0:
-        sys.path.insert(0, os.path.join(ROOT, "tests"))
-        import _oracle as O
-        want = O.decode(pics[0], refs)
-        got = db.planes(0)
-        verified = all(np.array_equal(got[k], want[k]) for k in range(3))
 
-    total_mbs = world * nb * nmb * args.steps
+    total_mbs = (world * nb if shard == "replicas" else npics) * nmb * args.steps
     value = total_mbs / dt
     ms_per_step = dt / args.steps * 1e3
     step_bytes = rd + wr
     # algorithmic bytes per launch of each kernel
-    kbytes = kernel_bytes(pics, nmb)
-    names = ["k_inter (with k_prep)", "k_intra_pic", "k_deblock"]
+    kbytes = [int(k * (band[1] - band[0]) / H) for k in kernel_bytes(pics, nmb)]
+    names = ["k_inter4", "intra (k_level + k_intra_levels + k_intra_pic)", "k_deblock"]
+    mbs_rank = (nb * nmb) if shard == "replicas" else int(npics * nmb * (band[1] - band[0]) / H)
     dom = int(np.argmax(kern[:3]))
     achieved = kbytes[dom] / (kern[dom] * 1e-3) / 1e9
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        done, el, npics = cpu_baseline(cfg, refs, args.cpu_seconds)
+        done, el, ncpu = cpu_baseline(cfg, refs, args.cpu_seconds)
         cpu = {"value": done / el, "unit": "macroblocks/s", "cores": 1, "kind": "port",
-               "sample": f"{npics} pictures of the same {CONFIG_NAMES[args.config]} workload "
-                         f"({npics * nmb} MBs, {el:.1f} s) decoded by oracle/h264r_oracle.c (1 thread) "
+               "sample": f"{ncpu} pictures of the same {CONFIG_NAMES[args.config]} workload "
+                         f"({ncpu * nmb} MBs, {el:.1f} s) decoded by oracle/h264r_oracle.c (1 thread) "
                          f"on {cpu_model()}"}
 
     if rank == 0:
@@ -199,13 +251,15 @@ def main() -> int:
             "data": "synthetic (seeded SURVEY 8(d) generator, arrow-h264_amd/csrc/synth.c)",
             "config": {"workload": CONFIG_NAMES[args.config], "survey_config": args.config,
                        "width_mbs": W, "height_mbs": H, "pictures_per_gpu": nb,
-                       "parallelism": f"replicas{world}" if world > 1 else "single"},
+                       "parallelism": (f"{shard}{world}" if world > 1 else "single"),
+                       "pictures_per_step": world * nb if shard == "replicas" else npics,
+                       "rows_this_rank": list(band)},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                          "kernel": names[dom], "kernel_ms": float(kern[dom]),
                          "kernel_algo_bytes": int(kbytes[dom]),
                          "step_algo_bytes": step_bytes, "step_achieved": step_bytes / (ms_per_step * 1e-3) / 1e9,
-                         "bytes_per_mb": step_bytes / (nb * nmb)},
+                         "bytes_per_mb": step_bytes / max(mbs_rank, 1)},
             "kernel_ms": {"inter": float(kern[0]), "intra": float(kern[1]), "deblock": float(kern[2]),
                           "batch_wall": float(kern[3])},
             "cpu_baseline": cpu,

@@ -234,9 +234,11 @@ int  h264r_decode_batch_rows(h264r_ctx* ctx, const h264r_batch* batch, int row0,
 int  h264r_ref_planes(h264r_ctx* ctx, int slot, uint8_t** y, uint8_t** u, uint8_t** v);
 
 /* ---- instrumentation ------------------------------------------------------------- */
-/* Average device time (ms) of the last h264r_decode_batch phases, measured with
- * HIP events on the launch stream: out[0] inter, out[1] intra, out[2] deblock,
- * out[3] total.  Returns H264R_OK or an error. */
+/* Average device time (ms) per h264r_decode_batch of the launches made since timing was
+ * enabled, measured with HIP events on each launch's stream: out[0] the inter kernel
+ * (k_inter4), out[1] the intra kernels (k_level + k_intra_levels + k_intra_pic),
+ * out[2] deblocking (k_deblock), out[3] the whole batch (also k_prep).  Returns
+ * H264R_OK or an error. */
 int  h264r_last_timing(h264r_ctx* ctx, float out_ms[4]);
 int  h264r_set_timing(h264r_ctx* ctx, int enable);
 /* Debug hook: H264R_DBG_NO_DEBLOCK skips the loop filter (reconstruction only, to
