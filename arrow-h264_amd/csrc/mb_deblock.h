@@ -174,6 +174,7 @@ struct alignas(16) DbLds {
 // p3..p0 q0..q3; bS 0 leaves the line unchanged.  `par` is the edge's
 // edge_word(); chroma lines use tc0 + 1 and never touch p1/q1 or the strong
 // 3-tap outputs.
+template <bool STRONG>
 DEV void filter_edge_line(int& p3, int& p2, int& p1, int& p0, int& q0, int& q1, int& q2, int& q3, int bS,
                           uint32_t par, bool chroma)
 {
@@ -188,6 +189,10 @@ DEV void filter_edge_line(int& p3, int& p2, int& p1, int& p0, int& q0, int& q1, 
     const int n_p0 = clip255(p0 + delta), n_q0 = clip255(q0 - delta);
     const int n_p1 = (!chroma && apb) ? p1 + clip3(-tc0, tc0, (p2 + avg - p1 * 2) >> 1) : p1;
     const int n_q1 = (!chroma && aqb) ? q1 + clip3(-tc0, tc0, (q2 + avg - q1 * 2) >> 1) : q1;
+    if (!STRONG) {            // no lane of the wave has bS 4 on this edge
+        if (filt) { p1 = n_p1; p0 = n_p0; q0 = n_q0; q1 = n_q1; }
+        return;
+    }
     // bS == 4 (filter_strong)
     const bool strong = iabs(p0 - q0) < ((alpha >> 2) + 2);
     const bool sp = !chroma && apb && strong, sq = !chroma && aqb && strong;
@@ -250,8 +255,12 @@ DEV void filter_mb(DbLds& S, int lane)
         for (int k = 0; k < 4; ++k) {
             if (!__any(bsk[k] != 0)) continue;
             const int i0 = 4 * k + 4;
-            filter_edge_line(v[i0 - 4], v[i0 - 3], v[i0 - 2], v[i0 - 1], v[i0], v[i0 + 1], v[i0 + 2], v[i0 + 3],
-                             bsk[k], park[k], !luma);
+            if (k == 0 && __any(bsk[k] == 4))
+                filter_edge_line<true>(v[i0 - 4], v[i0 - 3], v[i0 - 2], v[i0 - 1], v[i0], v[i0 + 1], v[i0 + 2], v[i0 + 3],
+                                       bsk[k], park[k], !luma);
+            else
+                filter_edge_line<false>(v[i0 - 4], v[i0 - 3], v[i0 - 2], v[i0 - 1], v[i0], v[i0 + 1], v[i0 + 2], v[i0 + 3],
+                                        bsk[k], park[k], !luma);
         }
         if (!hor) {
 #pragma unroll

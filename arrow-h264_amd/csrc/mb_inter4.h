@@ -25,6 +25,7 @@
 // the same motion vector).  A chroma 4x4 transform block is spread over the lanes
 // {blk, blk^1, blk^4, blk^5}; an 8x8 luma transform block likewise.
 #pragma once
+#include "mb_inter.h"
 #include "mb_deblock.h"
 
 namespace h264r {
