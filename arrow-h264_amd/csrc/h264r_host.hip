@@ -430,7 +430,7 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
                                c->d_mot + (size_t)p0 * 2 * mplane, rows);
             HIP_OK(hipGetLastError());
             Timed t(c, 0, s);                      // phase 0 = the inter kernel alone (k_prep is in the total only)
-            if (inter4() || HB != H) {
+            if ((inter4() && !(c->debug & H264R_DBG_INTER1)) || HB != H) {
                 hipLaunchKernelGGL(k_inter4, dim3((W * HB + 15) / 16, n), dim3(256), 0, s, cb,
                                    c->d_mot + (size_t)p0 * 2 * mplane, dbinfo_at(p0), rows);
                 HIP_OK(hipGetLastError());
@@ -469,7 +469,7 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
         }
         if (deblock) {
             Timed t(c, 2, sd);
-            if (deblock4())
+            if (deblock4() || (c->debug & H264R_DBG_DEBLOCK4))
                 hipLaunchKernelGGL(k_deblock4, dim3(n * nquads), dim3(64), 0, sd, cb, dbinfo_at(p0),
                                    reinterpret_cast<uint64_t*>(c->d_hb), sync + 1 + (size_t)CP * H, c->d_err, ++c->epoch, rows);
             else

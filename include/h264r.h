@@ -247,6 +247,11 @@ int  h264r_set_timing(h264r_ctx* ctx, int enable);
 /* H264R_DBG_INTRA_WALK reconstructs every intra MB with the wavefront walk instead of
  * the dependency-level schedule (both are bit-exact; this exercises the walk alone). */
 #define H264R_DBG_INTRA_WALK 2
+/* Alternative kernels, bit-exact, for tests and measurements: H264R_DBG_DEBLOCK4 the
+ * four-rows-per-wave packed deblocking walk, H264R_DBG_INTER1 the wave-per-MB inter
+ * kernel (k_inter + k_dbinfo). */
+#define H264R_DBG_DEBLOCK4   4
+#define H264R_DBG_INTER1     8
 int  h264r_set_debug(h264r_ctx* ctx, int flags);
 /* Wait for the context's work and report a device-side failure (a wavefront wait
  * that timed out): H264R_OK or H264R_EDEVICE. */
