@@ -102,6 +102,7 @@ def main() -> int:
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--traffic-json", default=None, help="PMC traffic summary (default profiles/traffic.json)")
     ap.add_argument("--shard", choices=["replicas", "slices"], default=None,
                     help="N>1 placement: independent pictures per GPU, or slice bands of shared pictures "
                          "(default: slices for configs 4/5, replicas for 2/3)")
@@ -233,6 +234,18 @@ def main() -> int:
     mbs_rank = (nb * nmb) if shard == "replicas" else int(npics * nmb * (band[1] - band[0]) / H)
     dom = int(np.argmax(kern[:3]))
     achieved = kbytes[dom] / (kern[dom] * 1e-3) / 1e9
+    # HBM traffic of the dominant kernel per launch, from the PMC counters of the
+    # committed profile run (tools/pmc.sh + tools/pmc_summary.py --json): per-MB
+    # FETCH_SIZE (doubled, gfx950) + WRITE_SIZE times the MBs this launch processed
+    traffic, traffic_src = None, None
+    tpath = args.traffic_json or os.path.join(ROOT, "profiles", "traffic.json")
+    kern_names = [["k_inter4"], ["k_level", "k_intra_levels", "k_intra_pic"], ["k_deblock"]][dom]
+    if os.path.exists(tpath):
+        tj = json.load(open(tpath))
+        per_mb = [tj["kernels"][k]["traffic_bytes_per_mb"] for k in kern_names if k in tj["kernels"]]
+        if per_mb:
+            traffic = sum(per_mb) * mbs_rank
+            traffic_src = f"{os.path.basename(tpath)} ({tj.get('source')}): {'+'.join(kern_names)}"
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -255,7 +268,7 @@ def main() -> int:
                        "pictures_per_step": world * nb if shard == "replicas" else npics,
                        "rows_this_rank": list(band)},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": names[dom], "kernel_ms": float(kern[dom]),
                          "kernel_algo_bytes": int(kbytes[dom]),
                          "step_algo_bytes": step_bytes, "step_achieved": step_bytes / (ms_per_step * 1e-3) / 1e9,
