@@ -55,11 +55,15 @@ DEV h264r_mb load_mb(const h264r_mb* p)
 
 // Wave-level barrier for LDS scratch owned by one wave: orders this wave's LDS
 // accesses across lanes without a workgroup barrier (other waves of the
-// workgroup run independent work).
+// workgroup run independent work).  H264R_SYNC_NODRAIN drops the lgkmcnt(0)
+// drain: a wave's LDS instructions execute in issue order, so only the compiler
+// has to be kept from moving accesses across the barrier (measurement variant).
 DEV void wave_sync()
 {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+#ifndef H264R_SYNC_NODRAIN
     __builtin_amdgcn_s_waitcnt(0xc07f);          // lgkmcnt(0): LDS ops of this wave done
+#endif
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }

@@ -66,7 +66,10 @@ __device__ unsigned long long h264r_db_trace[1 << 16][8];
 
 // hb: hand-off records [pic][pair][W][32] granules {RingEntry dword, epoch};
 // sync[0]: ticket counter; epoch: this launch's tag (never 0: hb is zeroed when allocated).
-extern "C" __global__ __launch_bounds__(64) void k_deblock(h264r_batch b, const DbInfo* __restrict__ dbinfo,
+#ifndef H264R_DB_WAVES
+#define H264R_DB_WAVES 1                    // minimum waves per SIMD asked of the register allocator
+#endif
+extern "C" __global__ __launch_bounds__(64, H264R_DB_WAVES) void k_deblock(h264r_batch b, const DbInfo* __restrict__ dbinfo,
                                                           uint64_t* hb, int* sync, int* err, uint32_t epoch, int2 rows)
 {
     __shared__ PairLds L;

@@ -57,7 +57,10 @@ extern "C" __global__ __launch_bounds__(256) void k_dbinfo(h264r_batch b, const 
 
 // k_inter4: inter / I_PCM MBs and the deblocking record of every MB, four MBs per
 // wave, one lane per 4x4 block (mb_inter4.h).  Grid (ceil(nmb / 16), pictures).
-extern "C" __global__ __launch_bounds__(256) void k_inter4(h264r_batch b, const uint2* __restrict__ mot, DbInfo* dbinfo,
+#ifndef H264R_INTER_WAVES
+#define H264R_INTER_WAVES 1                 // minimum waves per SIMD asked of the register allocator
+#endif
+extern "C" __global__ __launch_bounds__(256, H264R_INTER_WAVES) void k_inter4(h264r_batch b, const uint2* __restrict__ mot, DbInfo* dbinfo,
                                                            int2 rows)
 {
     __shared__ Inter4Lds S;
