@@ -407,7 +407,10 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
         int per_cu = 0, cus = 0;
         HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(k_intra_levels), 256, 0));
         HIP_OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
-        c->levels_grid = std::max(1, per_cu - 1) * std::max(1, cus);
+        static const int margin = [] { const char* e = getenv("H264R_LVL_MARGIN"); return e ? atoi(e) : 1; }();
+        c->levels_grid = std::max(1, per_cu - margin) * std::max(1, cus);
+        if (getenv("H264R_VERBOSE"))
+            fprintf(stderr, "h264r: k_intra_levels occupancy %d blocks/CU, %d CUs, grid %d\n", per_cu, cus, c->levels_grid);
     }
     if (levels && (st = dev_resize(&c->d_lvl, &c->c_lvl, (size_t)P * W * H))) return st;
     while ((int)c->ev_chain.size() < 2 * K) {

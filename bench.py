@@ -66,6 +66,40 @@ def cpu_baseline(cfg, refs, seconds: float):
     return n * nmb, el, n
 
 
+def cpu_baseline_threads(cfg, refs, seconds: float, threads: int):
+    """The same oracle with `threads` pthreads over independent pictures
+    (oracle_decode_pictures; BASELINE.md section 4, 'nproc threads'), bounded sample."""
+    import ctypes as C
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _oracle as O
+    from h264r import synth
+    L = O.lib()
+    W, H = cfg.width_mbs, cfg.height_mbs
+    q = O.quant_flat()
+    keep = []
+
+    def batch(first, count):
+        arr = (O.OraclePicture * count)()
+        for i in range(count):
+            p = synth.picture(L, cfg, first + i)
+            out = O.new_planes(W, H)
+            keep.append((p, out))
+            arr[i] = O.make_oracle_picture(p, refs, q, out)
+        return arr
+    probe = batch(20_000, threads)
+    t0 = time.perf_counter()
+    L.oracle_decode_pictures(probe, threads, threads)
+    per_round = max(time.perf_counter() - t0, 1e-3)
+    n = threads * max(1, int(seconds / per_round))
+    arr = batch(20_000 + threads, n)
+    t0 = time.perf_counter()
+    st = L.oracle_decode_pictures(arr, n, threads)
+    el = time.perf_counter() - t0
+    if st != 0:
+        raise RuntimeError(f"oracle_decode_pictures -> {st}")
+    return n * W * H, el, n
+
+
 def kernel_bytes(pics, nmb):
     """Algorithmic bytes per launch of k_inter, k_intra_pic and k_deblock over a batch
     (SURVEY 8(d) per-MB formula split by the kernel that reads / writes them):
@@ -101,6 +135,7 @@ def main() -> int:
     ap.add_argument("--batch", type=int, default=0, help="pictures per GPU per step (default 256, 64 at 2160p)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16, help="threads of the multi-threaded CPU baseline")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--traffic-json", default=None, help="PMC traffic summary (default profiles/traffic.json)")
     ap.add_argument("--shard", choices=["replicas", "slices"], default=None,
@@ -247,13 +282,19 @@ def main() -> int:
             traffic = sum(per_mb) * mbs_rank
             traffic_src = f"{os.path.basename(tpath)} ({tj.get('source')}): {'+'.join(kern_names)}"
 
-    cpu = None
+    cpu = cpu_mt = None
     if rank == 0 and world == 1 and not args.no_cpu:
         done, el, ncpu = cpu_baseline(cfg, refs, args.cpu_seconds)
         cpu = {"value": done / el, "unit": "macroblocks/s", "cores": 1, "kind": "port",
                "sample": f"{ncpu} pictures of the same {CONFIG_NAMES[args.config]} workload "
                          f"({ncpu * nmb} MBs, {el:.1f} s) decoded by oracle/h264r_oracle.c (1 thread) "
                          f"on {cpu_model()}"}
+        # the box gives one GPU's job a 16-CPU share (os.cpu_count() shows the whole machine)
+        thr = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+        done, el, ncpu = cpu_baseline_threads(cfg, refs, args.cpu_seconds / 2, thr)
+        cpu_mt = {"value": done / el, "unit": "macroblocks/s", "cores": thr, "kind": "port",
+                  "sample": f"{ncpu} pictures ({ncpu * nmb} MBs, {el:.1f} s) over {thr} threads, "
+                            f"oracle_decode_pictures, on {cpu_model()}"}
 
     if rank == 0:
         out = {
@@ -276,6 +317,7 @@ def main() -> int:
             "kernel_ms": {"inter": float(kern[0]), "intra": float(kern[1]), "deblock": float(kern[2]),
                           "batch_wall": float(kern[3])},
             "cpu_baseline": cpu,
+            "cpu_baseline_threads": cpu_mt,
             "verified_vs_oracle": verified,
         }
         print(json.dumps(out))
