@@ -164,10 +164,20 @@ DEV void row9(uint32_t w0, uint32_t w1, uint32_t w2, int x, int W, int (&p)[9])
     }
 }
 
-DEV const uint32_t* row_dwords(const uint8_t* __restrict__ img, int W, int H, int x, int y)
+// Global-address-space view of a pointer whose address space the compiler cannot
+// infer (a plane pointer read from LDS or picked per lane): loads through it are
+// `global_load`, not `flat_load`.  A flat load counts on lgkmcnt as well as vmcnt and
+// may return out of order, so every later LDS wait -- and every use of any load --
+// would also wait for it (a prefetch would stop overlapping anything).
+typedef const uint32_t __attribute__((address_space(1))) gdword;
+DEV const gdword* as_global(const void* p) { return (const gdword*)p; }
+template <typename T>
+DEV T load_global(const void* p) { return *(const __attribute__((address_space(1))) T*)p; }
+
+DEV const gdword* row_dwords(const uint8_t* __restrict__ img, int W, int H, int x, int y)
 {
     const int a = clip3(0, W - 1, x - 2) & ~3;
-    return reinterpret_cast<const uint32_t*>(img + (size_t)clip3(0, H - 1, y) * W + a);
+    return as_global(img + (size_t)clip3(0, H - 1, y) * W + a);
 }
 
 // Four luma prediction samples (x..x+3, y) at quarter-sample phase (xf, yf),
@@ -182,7 +192,7 @@ DEV void luma_pred4(const uint8_t* __restrict__ img, int W, int H, int x, int y,
     constexpr int C6[6] = {1, -5, 20, 20, -5, 1};
     const int xf = XF >= 0 ? XF : xf_rt, yf = YF >= 0 ? YF : yf_rt;
     if (yf == 0) {                                    // G, a, b, c: one row
-        const uint32_t* q = row_dwords(img, W, H, x, y);
+        const gdword* q = row_dwords(img, W, H, x, y);
         int p[9];
         row9(q[0], q[1], q[2], x, W, p);
 #pragma unroll
@@ -196,7 +206,7 @@ DEV void luma_pred4(const uint8_t* __restrict__ img, int W, int H, int x, int y,
     uint32_t w[6][3];
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
-        const uint32_t* q = row_dwords(img, W, H, x, y - 2 + k);
+        const gdword* q = row_dwords(img, W, H, x, y - 2 + k);
         w[k][0] = q[0]; w[k][1] = q[1]; w[k][2] = q[2];
     }
     const bool jfam = xf == 2 || (yf == 2 && xf != 0);   // needs the centre sample j
@@ -243,7 +253,7 @@ DEV void chroma_pred2(const uint8_t* __restrict__ img, int W, int H, int xi, int
     int p[2][3];
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
-        const uint32_t* q = reinterpret_cast<const uint32_t*>(img + (size_t)clip3(0, H - 1, yi + k) * W + a);
+        const gdword* q = as_global(img + (size_t)clip3(0, H - 1, yi + k) * W + a);
         const uint32_t w0 = q[0], w1 = q[1];
         if (xi >= 0 && xi + 2 < W) {
             const uint32_t r = __builtin_amdgcn_alignbyte(w1, w0, xi & 3);

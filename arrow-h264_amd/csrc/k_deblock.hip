@@ -177,7 +177,7 @@ extern "C" __global__ __launch_bounds__(64, H264R_DB_WAVES) void k_deblock(h264r
             const uint8_t* yb = Y + (size_t)(Y0 + by0) * g.W + x * 16 + 4 * bd0;
             pf_y0 = *reinterpret_cast<const uint32_t*>(yb);
             pf_y1 = *reinterpret_cast<const uint32_t*>(yb + (size_t)8 * g.W);
-            pf_c = *reinterpret_cast<const uint32_t*>(Cp[cpl] + (size_t)(Yc + cy) * g.Wc + x * 8 + 4 * cd);
+            pf_c = *as_global(Cp[cpl] + (size_t)(Yc + cy) * g.Wc + x * 8 + 4 * cd);
             if (hl < DBINFO_DWORDS) pf_i = info_row[x * DBINFO_DWORDS + hl];
             if (h == 0 && rp > 0) pf_top = ld_cc64(hb_in + (size_t)x * 32 + hl);
         }

@@ -184,7 +184,10 @@ extern "C" __global__ __launch_bounds__(64) void k_deblock4(h264r_batch b, const
         const int x = t - 2 * qd;
         if (row_on && x >= 0 && x < W) {
             pf_y = *reinterpret_cast<const uint4*>(Y + (size_t)(Y0 + ql) * g.W + x * 16);
-            pf_c = *reinterpret_cast<const uint2*>(Cp[ql >> 3] + (size_t)(Yc + (ql & 7)) * g.Wc + x * 8);
+            {
+                const unsigned long long v = load_global<unsigned long long>(Cp[ql >> 3] + (size_t)(Yc + (ql & 7)) * g.Wc + x * 8);
+                pf_c = make_uint2((uint32_t)v, (uint32_t)(v >> 32));
+            }
             if (ql < DBINFO_DWORDS / 2) pf_i = *reinterpret_cast<const uint2*>(info_row + x * DBINFO_DWORDS + 2 * ql);
             if (qd == 0 && wq > 0) {
                 pf_top[0] = ld_cc64(hb_in + (size_t)x * 32 + 2 * ql);

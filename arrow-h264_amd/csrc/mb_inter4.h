@@ -57,7 +57,7 @@ DEV void luma_rows2_pred(const uint8_t* __restrict__ img, int W, int H, int x, i
     uint32_t w[7][3];
 #pragma unroll
     for (int r = 0; r < 7; ++r) {
-        const uint32_t* q = row_dwords(img, W, H, x, y - 2 + r);
+        const gdword* q = row_dwords(img, W, H, x, y - 2 + r);
         w[r][0] = q[0]; w[r][1] = q[1]; w[r][2] = q[2];
     }
     constexpr int C6[6] = {1, -5, 20, 20, -5, 1};
@@ -143,7 +143,7 @@ DEV void luma_block_pred(const uint8_t* __restrict__ img, int W, int H, int x, i
     uint32_t w[9][3];
 #pragma unroll
     for (int r = 0; r < 9; ++r) {
-        const uint32_t* q = row_dwords(img, W, H, x, y - 2 + r);
+        const gdword* q = row_dwords(img, W, H, x, y - 2 + r);
         w[r][0] = q[0]; w[r][1] = q[1]; w[r][2] = q[2];
     }
     const bool inside = x - 2 >= 0 && x + 6 < W;
@@ -230,7 +230,7 @@ DEV uint32_t chroma_block_pred(const uint8_t* __restrict__ img, int W, int H, in
     int p[3][3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-        const uint32_t* q = reinterpret_cast<const uint32_t*>(img + (size_t)clip3(0, H - 1, yi + k) * W + a);
+        const gdword* q = as_global(img + (size_t)clip3(0, H - 1, yi + k) * W + a);
         const uint32_t w0 = q[0], w1 = q[1];
         if (xi >= 0 && xi + 2 < W) {
             const uint32_t r = __builtin_amdgcn_alignbyte(w1, w0, xi & 3);
