@@ -171,15 +171,20 @@ extern "C" __global__ __launch_bounds__(64, H264R_DB_WAVES) void k_deblock(h264r
 
     // Issue the loads of step t (this half's MB t - 2h): body, deblocking record
     // and, for half A below another pair, the hand-off record of the MB above.
+    // The hand-off record is loaded first and unconditionally (lanes that do not need
+    // it read their own output record): a conditional load merges into the
+    // loop-carried register through a copy, and the copy's vmcnt(0) would retire the
+    // whole prefetch at once instead of letting it overlap the filter work.
     auto prefetch = [&](int t) {
         const int x = t - 2 * h;
+        const int xs = min(max(x, 0), W - 1);
+        pf_top = ld_cc64(h == 0 && rp > 0 ? hb_in + (size_t)xs * 32 + hl : hb_out + hl);
         if (half_on && x >= 0 && x < W) {
             const uint8_t* yb = Y + (size_t)(Y0 + by0) * g.W + x * 16 + 4 * bd0;
             pf_y0 = *reinterpret_cast<const uint32_t*>(yb);
             pf_y1 = *reinterpret_cast<const uint32_t*>(yb + (size_t)8 * g.W);
             pf_c = *as_global(Cp[cpl] + (size_t)(Yc + cy) * g.Wc + x * 8 + 4 * cd);
             if (hl < DBINFO_DWORDS) pf_i = info_row[x * DBINFO_DWORDS + hl];
-            if (h == 0 && rp > 0) pf_top = ld_cc64(hb_in + (size_t)x * 32 + hl);
         }
     };
 
