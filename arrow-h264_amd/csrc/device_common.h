@@ -53,6 +53,19 @@ DEV h264r_mb load_mb(const h264r_mb* p)
     return m;
 }
 
+// Scalar (constant address space) load of data that no kernel of the batch writes
+// (MB records, slice headers): a wave-uniform address becomes an s_load, issued back
+// to back with the others and waited on lgkmcnt, not interleaved with vmcnt waits.
+DEV uint32_t ld_const(const void* p) { return *(const __attribute__((address_space(4))) uint32_t*)p; }
+DEV h264r_mb load_mb_const(const h264r_mb* p)
+{
+    h264r_mb m;
+    uint32_t* w = reinterpret_cast<uint32_t*>(&m);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = ld_const(reinterpret_cast<const uint32_t*>(p) + i);
+    return m;
+}
+
 // Wave-level barrier for LDS scratch owned by one wave: orders this wave's LDS
 // accesses across lanes without a workgroup barrier (other waves of the
 // workgroup run independent work).  H264R_SYNC_NODRAIN drops the lgkmcnt(0)

@@ -156,11 +156,12 @@ DEV void luma_res4_intra(const h264r_mb& m, const int16_t* __restrict__ lv, cons
     const int qp = m.qp_scaled[0], per = qp / 6, rem = qp % 6;
     const bool i16 = m.mb_type == H264R_I_16x16;
     const int loff = b8_offset(m.cbp, (by >> 1) * 2 + (bx >> 1));
-    uint2 lev = make_uint2(0, 0), sc = make_uint2(0, 0);
-    if (loff >= 0) {
-        lev = ld8(lv + loff + ((by & 1) * 2 + (bx & 1)) * 16 + r * 4);
-        sc = ld8(&q->scale4x4[0][0][rem][r * 4]);
-    }
+    // both loads issued unconditionally (a lane without levels reads the scale table
+    // and drops the value): a load inside a lane-divergent branch merges through a copy
+    // whose vmcnt(0) serialises it behind everything issued before
+    uint2 lev = ld8(loff >= 0 ? (const void*)(lv + loff + ((by & 1) * 2 + (bx & 1)) * 16 + r * 4) : (const void*)q);
+    const uint2 sc = ld8(&q->scale4x4[0][0][rem][r * 4]);
+    if (loff < 0) lev = make_uint2(0, 0);
     int d[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
@@ -198,9 +199,10 @@ DEV void luma_res8_intra(const h264r_mb& m, const int16_t* __restrict__ lv, cons
     const int qp = m.qp_scaled[0], per = qp / 6, rem = qp % 6;
     const int off = b8_offset(m.cbp, k);
     int d[4] = {0, 0, 0, 0};
-    if (off >= 0) {
-        const uint2 lev = ld8(lv + off + row * 8 + half * 4);
+    {
+        uint2 lev = ld8(off >= 0 ? (const void*)(lv + off + row * 8 + half * 4) : (const void*)q);   // unconditional
         const uint2 sc = ld8(&q->scale8x8[0][0][rem][row * 8 + half * 4]);
+        if (off < 0) lev = make_uint2(0, 0);
 #pragma unroll
         for (int c = 0; c < 4; ++c)
             d[c] = dq8((int16_t)((c & 2 ? lev.y : lev.x) >> (16 * (c & 1))),
@@ -242,26 +244,53 @@ DEV void intra_mb2(const h264r_batch& b, const Geom& g, int pic, int mbx, int mb
 
     // ---- neighbour samples: issued before anything else (in-picture addresses only;
     // availability decides later which of them are used)
+    // One dword load per lane, all issued at once (a left-column sample is the top byte
+    // of the aligned dword that ends at x - 1; lanes with nothing to fetch read their own
+    // MB's first row and drop it).  Loads in lane-divergent branches would each merge
+    // through a copy whose vmcnt(0) serialises them.
     uint32_t nb = 0;
     {
+        const uint8_t* src = o.y + (size_t)Y * g.W + X;
+        bool want = false, left = false;
         if (lane < 7) {                                   // row above, x = -4..23
             const int x = X - 4 + 4 * lane;
-            if (mby > 0 && x >= 0 && x < g.W) nb = *reinterpret_cast<const uint32_t*>(o.y + (size_t)(Y - 1) * g.W + x);
+            want = mby > 0 && x >= 0 && x < g.W;
+            src = want ? o.y + (size_t)(Y - 1) * g.W + x : src;
         } else if (lane < 23) {                           // left column
-            if (mbx > 0) nb = o.y[(size_t)(Y + lane - 7) * g.W + X - 1];
+            want = left = mbx > 0;
+            src = want ? o.y + (size_t)(Y + lane - 7) * g.W + X - 4 : src;
         } else if (lane < 29) {                           // chroma rows above, x = -4..7
             const int k = lane - 23, pl = k / 3, x = Xc - 4 + 4 * (k % 3);
-            if (mby > 0 && x >= 0) nb = *reinterpret_cast<const uint32_t*>((pl ? o.v : o.u) + (size_t)(Yc - 1) * g.Wc + x);
+            want = mby > 0 && x >= 0;
+            src = want ? (pl ? o.v : o.u) + (size_t)(Yc - 1) * g.Wc + x : src;
         } else if (lane < 45) {                           // chroma left columns
             const int k = lane - 29, pl = k >> 3;
-            if (mbx > 0) nb = (pl ? o.v : o.u)[(size_t)(Yc + (k & 7)) * g.Wc + Xc - 1];
+            want = left = mbx > 0;
+            src = want ? (pl ? o.v : o.u) + (size_t)(Yc + (k & 7)) * g.Wc + Xc - 4 : src;
         }
+        const uint32_t w = *as_global(src);
+        nb = (w >> (left ? 24 : 0)) & (0u - (uint32_t)want);   // arithmetic, not a select: no branch
     }
-    const h264r_mb m = load_mb(&mbs[a]);
+    // neighbour MB records A, B, C, D: dwords 0 (type, flags) and 2 (cbp_blks, slice), all
+    // loaded before any decision (get_neighbour + slice check + constrained intra,
+    // intra_prediction.cc:142-168 / 629-651 / 753-777)
+    uint32_t nw0[4], nw2[4];
+    bool nin[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int nx = mbx + (k == 0 || k == 3 ? -1 : (k == 2 ? 1 : 0)), ny = mby - (k == 0 ? 0 : 1);
+        nin[k] = nx >= 0 && ny >= 0 && nx < g.wmb && ny < g.hmb;
+        const uint32_t* p = reinterpret_cast<const uint32_t*>(&mbs[nin[k] ? ny * g.wmb + nx : a]);
+        nw0[k] = ld_const(p);
+        nw2[k] = ld_const(p + 2);
+    }
+    const h264r_mb m = load_mb_const(&mbs[a]);
     if (!mb_is_intra(m) || m.mb_type == H264R_I_PCM) return;
     const int cip = b.pics[pic].constrained_intra_pred;
-    const int avA = nb_avail(mbs, g, m, cip, mbx - 1, mby), avB = nb_avail(mbs, g, m, cip, mbx, mby - 1);
-    const int avC = nb_avail(mbs, g, m, cip, mbx + 1, mby - 1), avD = nb_avail(mbs, g, m, cip, mbx - 1, mby - 1);
+    auto avail = [&](int k) -> int {
+        return nin[k] && (int)(nw2[k] >> 16) == (int)m.slice && !(cip && !((nw0[k] >> 8) & H264R_MBF_INTRA));
+    };
+    const int avA = avail(0), avB = avail(1), avC = avail(2), avD = avail(3);
     const int16_t* lv = b.levels + m.coef_off;
     const h264r_quant* __restrict__ q = &b.quant[pic];
     const bool i16 = m.mb_type == H264R_I_16x16, i8 = m.mb_type == H264R_I_8x8;
