@@ -36,6 +36,16 @@ struct Inter4Lds {
     const uint8_t* planes[3 * H264R_MAX_SLOTS];
 };
 
+DEV h264r_mb mb_lane(const h264r_mb* p)          // per-lane 32-byte record, two 16-byte loads
+{
+    const uint4* q = reinterpret_cast<const uint4*>(p);
+    const uint4 w0 = q[0], w1 = q[1];
+    h264r_mb m;
+    uint32_t* w = reinterpret_cast<uint32_t*>(&m);
+    w[0] = w0.x; w[1] = w0.y; w[2] = w0.z; w[3] = w0.w; w[4] = w1.x; w[5] = w1.y; w[6] = w1.z; w[7] = w1.w;
+    return m;
+}
+
 DEV int sel16(uint32_t lo, uint32_t hi, int c) { return (int16_t)(((c & 2) ? hi : lo) >> (16 * (c & 1))); }
 
 // Two rows (y, y+1) of luma prediction samples of a 4-wide block at integer
@@ -302,12 +312,16 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
     const uint2 l0 = mot[li], l1 = mot[g.motion_plane + li];
     const uint2 u0 = mot[ui], u1 = mot[g.motion_plane + ui];
     // ---- MB records (own, left, upper) and slice headers
-    const h264r_mb q = mbs[aa];
+    // records as two 16-byte loads each (a struct copy becomes one byte load per field,
+    // each waited on its own); all three issued together
+    const h264r_mb q = mb_lane(&mbs[aa]);
     const int hasL = mbx > 0, hasU = mby > 0;
-    const h264r_mb L = mbs[hasL ? aa - 1 : aa];
-    const h264r_mb U = mbs[hasU ? aa - g.wmb : aa];
+    const h264r_mb L = mb_lane(&mbs[hasL ? aa - 1 : aa]);
+    const h264r_mb U = mb_lane(&mbs[hasU ? aa - g.wmb : aa]);
     const h264r_slice* qs = &slices[q.slice];
     const uint2 qsh = *reinterpret_cast<const uint2*>(qs);       // type, idc, offsets, wp, log2 wd
+    // slice types of the left / upper MBs' slices (SP/SI edges), loaded with qsh
+    const int l_type = slices[L.slice].slice_type, u_type = slices[U.slice].slice_type;
     const int q_type = qsh.x & 255, idc = (qsh.x >> 8) & 255;
     const int offa = (int8_t)((qsh.x >> 16) & 255), offb = (int8_t)(qsh.x >> 24);
     const int wp_mode = qsh.y & 255;
@@ -331,10 +345,9 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
             int v = 0;
             if (en) {
                 // MB P of the edge: the left / upper MB for edge 0, else this MB
-                const int p_slice = e == 0 ? (hor ? U.slice : L.slice) : q.slice;
                 const int p_flags = e == 0 ? (hor ? U.flags : L.flags) : q.flags;
                 const int p_cbp = e == 0 ? (hor ? U.cbp_blks : L.cbp_blks) : q.cbp_blks;
-                const int special = special_q || (e == 0 && special_slice(slices[p_slice].slice_type));
+                const int special = special_q || (e == 0 && special_slice(hor ? u_type : l_type));
                 const int intra = q_intra || (p_flags & H264R_MBF_INTRA) != 0;
                 const int blkQ = 4 * by + bx;
                 const int blkP = hor ? (e == 0 ? 12 + bx : blkQ - 4) : (e == 0 ? blkQ + 3 : blkQ - 1);
