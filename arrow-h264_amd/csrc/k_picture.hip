@@ -256,15 +256,25 @@ extern "C" __global__ __launch_bounds__(256, H264R_LVL_WAVES) void k_intra_level
     const size_t gw = (size_t)blockIdx.x * 4 + wave, step = (size_t)gridDim.x * 4 * 64;
     const int deepest = __hip_atomic_load(&lvsync[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int top = min(lmax, deepest);
+    // the level of batch MB e (32-bit index math: P * nmb < 2^31); the load is clamped,
+    // not conditional, so the next chunk's levels can be in flight while this chunk's
+    // MBs are reconstructed
+    const unsigned total32 = (unsigned)total, nbu = (unsigned)nb;
+    auto lvl_at = [&](size_t base) -> int {
+        const unsigned e = min((unsigned)base + (unsigned)lane, total32 - 1u);
+        return lvl[(size_t)(e / nbu) * g.nmb + m0 + e % nbu];
+    };
     for (int L = 1; L <= top; ++L) {
+        int cur = lvl_at(gw * 64);
         for (size_t base = gw * 64; base < total; base += step) {
-            const size_t e = base + lane;
-            const bool hit = e < total && lvl[(e / nb) * g.nmb + m0 + e % nb] == L;
+            const int nxt = lvl_at(base + step < total ? base + step : base);     // prefetch
+            const bool hit = base + lane < total && cur == L;
             uint64_t todo = __ballot(hit);
+            cur = nxt;
             while (todo) {
-                const size_t k = base + __builtin_ctzll(todo);
+                const unsigned k = (unsigned)base + (unsigned)__builtin_ctzll(todo);
                 todo &= todo - 1;
-                const int pic = (int)(k / nb), a = m0 + (int)(k % nb);
+                const int pic = (int)(k / nbu), a = m0 + (int)(k % nbu);
 #ifdef H264R_TRACE_INTRA
                 const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
 #endif
