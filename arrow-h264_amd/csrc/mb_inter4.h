@@ -308,24 +308,259 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
     const int X4 = mbx * 4 + bx, Y4 = mby * 4 + by;
     const int mi = Y4 * g.W4 + X4;
     const uint2 m0 = mot[mi], m1 = mot[g.motion_plane + mi];
-    const int li = X4 > 0 ? mi - 1 : mi, ui = Y4 > 0 ? mi - g.W4 : mi;
-    const uint2 l0 = mot[li], l1 = mot[g.motion_plane + li];
-    const uint2 u0 = mot[ui], u1 = mot[g.motion_plane + ui];
     // ---- MB records (own, left, upper) and slice headers
     // records as two 16-byte loads each (a struct copy becomes one byte load per field,
     // each waited on its own); all three issued together
     const h264r_mb q = mb_lane(&mbs[aa]);
     const int hasL = mbx > 0, hasU = mby > 0;
-    const h264r_mb L = mb_lane(&mbs[hasL ? aa - 1 : aa]);
-    const h264r_mb U = mb_lane(&mbs[hasU ? aa - g.wmb : aa]);
     const h264r_slice* qs = &slices[q.slice];
     const uint2 qsh = *reinterpret_cast<const uint2*>(qs);       // type, idc, offsets, wp, log2 wd
     // slice types of the left / upper MBs' slices (SP/SI edges), loaded with qsh
-    const int l_type = slices[L.slice].slice_type, u_type = slices[U.slice].slice_type;
     const int q_type = qsh.x & 255, idc = (qsh.x >> 8) & 255;
     const int offa = (int8_t)((qsh.x >> 16) & 255), offb = (int8_t)(qsh.x >> 24);
     const int wp_mode = qsh.y & 255;
 
+    // ---- reconstruction of inter / I_PCM MBs first (the motion-compensation loads go
+    // out as early as possible), the deblocking record of every MB after it
+    [&]() {
+        const bool pcm = q.mb_type == H264R_I_PCM;
+        if (!valid || (mb_is_intra(q) && !pcm)) return;              // intra: k_intra_* (lanes idle here)
+        const PicPtrs o = out_planes(b, g, pic);
+        const int16_t* lv = b.levels + q.coef_off;
+        uint8_t* ydst = o.y + (size_t)(mby * 16 + by * 4) * g.W + mbx * 16 + bx * 4;
+        const size_t coff = (size_t)(mby * 8 + by * 2) * g.Wc + mbx * 8 + bx * 2;
+        if (pcm) {                                                       // mb_pred_ipcm decoder.cc:149-168
+            const uint8_t* raw = reinterpret_cast<const uint8_t*>(lv);
+    #pragma unroll
+            for (int r = 0; r < 4; ++r)
+                *reinterpret_cast<uint32_t*>(ydst + (size_t)r * g.W) =
+                    *reinterpret_cast<const uint32_t*>(raw + (by * 4 + r) * 16 + bx * 4);
+    #pragma unroll
+            for (int pl = 0; pl < 2; ++pl)
+    #pragma unroll
+                for (int r = 0; r < 2; ++r)
+                    *reinterpret_cast<uint16_t*>((pl ? o.v : o.u) + coff + (size_t)r * g.Wc) =
+                        *reinterpret_cast<const uint16_t*>(raw + 256 + pl * 64 + (by * 2 + r) * 8 + bx * 2);
+            return;
+        }
+
+        // ---- residual inputs, issued before motion compensation
+        const int cbpl = q.cbp & 15, cbpc = q.cbp >> 4;
+        const int t8 = (q.flags & H264R_MBF_T8x8) != 0;
+        const h264r_quant* __restrict__ qt = &b.quant[pic];
+        const int qpl = q.qp_scaled[0];
+        const int b8 = (by >> 1) * 2 + (bx >> 1);
+        const int loff = b8_offset(q.cbp, b8);
+        uint4 lev[2] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
+        uint4 lsc[2] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
+        if (loff >= 0) {
+            if (!t8) {                      // 4x4 block: 16 raster levels
+                const uint4* p = reinterpret_cast<const uint4*>(lv + loff + ((by & 1) * 2 + (bx & 1)) * 16);
+                lev[0] = p[0]; lev[1] = p[1];
+                const uint4* s = reinterpret_cast<const uint4*>(&qt->scale4x4[1][0][qpl % 6][0]);
+                lsc[0] = s[0]; lsc[1] = s[1];
+            } else {                        // my 4x4 quadrant of the 8x8 block: rows (by&1)*4.., cols (bx&1)*4..
+                const int16_t* p = lv + loff + (by & 1) * 32 + (bx & 1) * 4;
+                const int16_t* s = &qt->scale8x8[1][0][qpl % 6][(by & 1) * 32 + (bx & 1) * 4];
+                const uint2 r0 = ld8(p), r1 = ld8(p + 8), r2 = ld8(p + 16), r3 = ld8(p + 24);
+                lev[0] = make_uint4(r0.x, r0.y, r1.x, r1.y); lev[1] = make_uint4(r2.x, r2.y, r3.x, r3.y);
+                const uint2 s0 = ld8(s), s1 = ld8(s + 8), s2 = ld8(s + 16), s3 = ld8(s + 24);
+                lsc[0] = make_uint4(s0.x, s0.y, s1.x, s1.y); lsc[1] = make_uint4(s2.x, s2.y, s3.x, s3.y);
+            }
+        }
+        // chroma: my 2x2 quadrant of chroma 4x4 block cb of each plane + the plane's 4 DC levels
+        const int cb = (by >> 1) * 2 + (bx >> 1), cr = (by & 1) * 2, cc = (bx & 1) * 2;
+        uint32_t clev[2][2] = {{0, 0}, {0, 0}}, csc[2][2] = {{0, 0}, {0, 0}};
+        uint2 cdc[2] = {make_uint2(0, 0), make_uint2(0, 0)};
+        int cdcs[2] = {0, 0};
+        if (cbpc) {
+            const LevelOffs lo = level_offsets(q);
+    #pragma unroll
+            for (int pl = 0; pl < 2; ++pl) {
+                const int qpc = q.qp_scaled[1 + pl];
+                cdc[pl] = ld8(lv + lo.cdc + pl * 4);
+                cdcs[pl] = qt->scale4x4[1][1 + pl][qpc % 6][0];
+                if (cbpc == 2) {
+    #pragma unroll
+                    for (int r = 0; r < 2; ++r) {
+                        clev[pl][r] = *reinterpret_cast<const uint32_t*>(lv + lo.cac + pl * 64 + cb * 16 + (cr + r) * 4 + cc);
+                        csc[pl][r] = *reinterpret_cast<const uint32_t*>(&qt->scale4x4[1][1 + pl][qpc % 6][(cr + r) * 4 + cc]);
+                    }
+                }
+            }
+        }
+
+        // ---- prediction
+        const int r0 = (int8_t)(m0.y & 255), r1 = (int8_t)(m1.y & 255);
+        const int dir = (r0 >= 0 && r1 >= 0) ? 2 : (r0 >= 0 ? 0 : 1);
+        uint32_t pY[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}}, pC[2][2] = {{0, 0}, {0, 0}};
+    #pragma unroll 1
+        for (int l = 0; l < 2; ++l) {
+            const uint2 mw = l ? m1 : m0;
+            const int rr = l ? r1 : r0;
+            const bool use = rr >= 0;
+            if (!__any(use)) continue;                                  // P pictures: list 1 never
+            if (!use) continue;
+            const int slot = (int8_t)((mw.y >> 8) & 255);
+            const bool ok = slot >= 0 && slot < H264R_MAX_SLOTS && rr < H264R_MAX_REFS && S.planes[slot * 3];
+            const int mvx = (int16_t)(mw.x & 0xFFFF), mvy = (int16_t)(mw.x >> 16);
+            const int vx = X4 * 16 + mvx, vy = Y4 * 16 + mvy;           // quarter luma / eighth chroma units
+            if (!ok) {                                                   // no_ref: 128 (inter_prediction.cc:164-167,366-369)
+    #pragma unroll
+                for (int i = 0; i < 4; ++i) pY[l][i] = 0x80808080u;
+                pC[l][0] = pC[l][1] = 0x80808080u;
+                continue;
+            }
+            luma_block_pred(S.planes[slot * 3], g.W, g.H, vx >> 2, vy >> 2, vx & 3, vy & 3, pY[l]);
+    #pragma unroll
+            for (int pl = 0; pl < 2; ++pl)
+                pC[l][pl] = chroma_block_pred(S.planes[slot * 3 + 1 + pl], g.Wc, g.Hc, vx >> 3, vy >> 3, vx & 7, vy & 7);
+        }
+        uint32_t predY[4], predC[2];
+    #pragma unroll
+        for (int i = 0; i < 4; ++i) predY[i] = wp_combine4(qs, wp_mode, dir, r0, r1, pY[0][i], pY[1][i], 0);
+    #pragma unroll
+        for (int pl = 0; pl < 2; ++pl) predC[pl] = wp_combine4(qs, wp_mode, dir, r0, r1, pC[0][pl], pC[1][pl], 1 + pl);
+
+        // ---- luma residual (transform.cc:1058-1073)
+        int res[4][4];
+    #pragma unroll
+        for (int i = 0; i < 4; ++i)
+    #pragma unroll
+            for (int c = 0; c < 4; ++c) res[i][c] = 0;
+        if (__any(cbpl != 0)) {
+            const int per = qpl / 6;
+            int d[4][4];
+    #pragma unroll
+            for (int i = 0; i < 4; ++i)
+    #pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const uint4 lw = lev[i >> 1], sw = lsc[i >> 1];
+                    const uint32_t lo_ = (i & 1) ? lw.z : lw.x, hi_ = (i & 1) ? lw.w : lw.y;
+                    const uint32_t slo = (i & 1) ? sw.z : sw.x, shi = (i & 1) ? sw.w : sw.y;
+                    const int lvv = sel16(lo_, hi_, c), scv = sel16(slo, shi, c);
+                    d[i][c] = t8 ? dq8(lvv, scv, per) : dq4(lvv, scv, per);
+                }
+            if (!__any(t8 != 0)) {
+                // 4x4: rows then columns, all in-lane
+    #pragma unroll
+                for (int i = 0; i < 4; ++i) idct4_inplace(d[i][0], d[i][1], d[i][2], d[i][3]);
+    #pragma unroll
+                for (int c = 0; c < 4; ++c) idct4_inplace(d[0][c], d[1][c], d[2][c], d[3][c]);
+    #pragma unroll
+                for (int i = 0; i < 4; ++i)
+    #pragma unroll
+                    for (int c = 0; c < 4; ++c) res[i][c] = (d[i][c] + 32) >> 6;
+            } else {
+                // 8x8 (only t8 MBs reach here with d != 0 for their lanes; 4x4 MBs of the same
+                // wave take the in-lane path below).  Rows: my 4 + the 4 of lane ^ 1.
+                int e4[4][4];
+    #pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    int in[8], outv[8];
+    #pragma unroll
+                    for (int c = 0; c < 4; ++c) {
+                        const int ov = __shfl_xor(d[i][c], 1);
+                        in[c] = (bx & 1) ? ov : d[i][c];
+                        in[4 + c] = (bx & 1) ? d[i][c] : ov;
+                    }
+                    idct8(in, outv);
+    #pragma unroll
+                    for (int c = 0; c < 4; ++c) e4[i][c] = (bx & 1) ? outv[4 + c] : outv[c];
+                }
+    #pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    int in[8], outv[8];
+    #pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int ov = __shfl_xor(e4[i][c], 4);
+                        in[i] = (by & 1) ? ov : e4[i][c];
+                        in[4 + i] = (by & 1) ? e4[i][c] : ov;
+                    }
+                    idct8(in, outv);
+    #pragma unroll
+                    for (int i = 0; i < 4; ++i) res[i][c] = t8 ? ((by & 1) ? outv[4 + i] : outv[i]) : 0;
+                }
+                if (!t8) {
+    #pragma unroll
+                    for (int i = 0; i < 4; ++i) idct4_inplace(d[i][0], d[i][1], d[i][2], d[i][3]);
+    #pragma unroll
+                    for (int c = 0; c < 4; ++c) idct4_inplace(d[0][c], d[1][c], d[2][c], d[3][c]);
+                }
+    #pragma unroll
+                for (int i = 0; i < 4; ++i)
+    #pragma unroll
+                    for (int c = 0; c < 4; ++c) res[i][c] = ((t8 ? res[i][c] : d[i][c]) + 32) >> 6;
+            }
+        }
+        // ---- construction + store, luma
+    #pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            uint32_t wv = 0;
+    #pragma unroll
+            for (int c = 0; c < 4; ++c) wv |= (uint32_t)clip255((int)((predY[i] >> (8 * c)) & 255) + res[i][c]) << (8 * c);
+            *reinterpret_cast<uint32_t*>(ydst + (size_t)i * g.W) = wv;
+        }
+
+        // ---- chroma residual (transform.cc:1081-1091, DC :875-889): chroma block cb is
+        // spread over lanes {blk, ^1, ^4, ^5}; my quadrant rows cr.., cols cc..
+    #pragma unroll
+        for (int pl = 0; pl < 2; ++pl) {
+            int rc[2][2] = {{0, 0}, {0, 0}};
+            if (__any(cbpc != 0)) {
+                const int qpc = q.qp_scaled[1 + pl], per = qpc / 6;
+                int k[2][2];
+    #pragma unroll
+                for (int r = 0; r < 2; ++r)
+    #pragma unroll
+                    for (int c = 0; c < 2; ++c)
+                        k[r][c] = dq4((int16_t)(clev[pl][r] >> (16 * c)), (int16_t)(csc[pl][r] >> (16 * c)), per);
+                const int c00 = (int16_t)(cdc[pl].x & 0xFFFF), c01 = (int16_t)(cdc[pl].x >> 16);
+                const int c10 = (int16_t)(cdc[pl].y & 0xFFFF), c11 = (int16_t)(cdc[pl].y >> 16);
+                const int e00 = c00 + c01, e01 = c00 - c01, e10 = c10 + c11, e11 = c10 - c11;
+                const int f = cb == 0 ? e00 + e10 : cb == 1 ? e01 + e11 : cb == 2 ? e00 - e10 : e01 - e11;
+                if (cr == 0 && cc == 0) k[0][0] = cbpc ? ((f * cdcs[pl]) * (1 << per)) >> 5 : 0;
+                // rows: my 2 columns + the 2 of lane ^ 1
+                int t[2][2];
+    #pragma unroll
+                for (int r = 0; r < 2; ++r) {
+                    const int o0 = __shfl_xor(k[r][0], 1), o1 = __shfl_xor(k[r][1], 1);
+                    const int d0 = cc ? o0 : k[r][0], d1 = cc ? o1 : k[r][1], d2 = cc ? k[r][0] : o0, d3 = cc ? k[r][1] : o1;
+                    int y0, y1, y2, y3;
+                    idct4(d0, d1, d2, d3, y0, y1, y2, y3);
+                    t[r][0] = cc ? y2 : y0;
+                    t[r][1] = cc ? y3 : y1;
+                }
+                // columns: my 2 rows + the 2 of lane ^ 4
+    #pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                    const int o0 = __shfl_xor(t[0][c], 4), o1 = __shfl_xor(t[1][c], 4);
+                    const int d0 = cr ? o0 : t[0][c], d1 = cr ? o1 : t[1][c], d2 = cr ? t[0][c] : o0, d3 = cr ? t[1][c] : o1;
+                    int y0, y1, y2, y3;
+                    idct4(d0, d1, d2, d3, y0, y1, y2, y3);
+                    rc[0][c] = ((cr ? y2 : y0) + 32) >> 6;
+                    rc[1][c] = ((cr ? y3 : y1) + 32) >> 6;
+                }
+            }
+            uint8_t* cdst = (pl ? o.v : o.u) + coff;
+    #pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                const uint32_t pr = predC[pl] >> (16 * r);
+                const uint32_t wv = (uint32_t)clip255((int)(pr & 255) + rc[r][0]) |
+                                    ((uint32_t)clip255((int)((pr >> 8) & 255) + rc[r][1]) << 8);
+                *reinterpret_cast<uint16_t*>(cdst + (size_t)r * g.Wc) = (uint16_t)wv;
+            }
+        }
+    }();
+
+    // neighbour motion and records: loaded here, after the reconstruction, so that
+    // they do not stay live across motion compensation (L2-hot by now)
+    const int li = X4 > 0 ? mi - 1 : mi, ui = Y4 > 0 ? mi - g.W4 : mi;
+    const uint2 l0 = mot[li], l1 = mot[g.motion_plane + li];
+    const uint2 u0 = mot[ui], u1 = mot[g.motion_plane + ui];
+    const h264r_mb L = mb_lane(&mbs[hasL ? aa - 1 : aa]);
+    const h264r_mb U = mb_lane(&mbs[hasU ? aa - g.wmb : aa]);
+    const int l_type = slices[L.slice].slice_type, u_type = slices[U.slice].slice_type;
     // ---- deblocking record (Deblock::strength deblock.cc:78-289): this lane's
     // left edge (vertical edge bx, segment by) and top edge (horizontal edge by,
     // segment bx)
@@ -384,234 +619,6 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
         }
     }
 
-    const bool pcm = q.mb_type == H264R_I_PCM;
-    if (!valid || (mb_is_intra(q) && !pcm)) return;              // intra: k_intra_* (lanes idle here)
-    const PicPtrs o = out_planes(b, g, pic);
-    const int16_t* lv = b.levels + q.coef_off;
-    uint8_t* ydst = o.y + (size_t)(mby * 16 + by * 4) * g.W + mbx * 16 + bx * 4;
-    const size_t coff = (size_t)(mby * 8 + by * 2) * g.Wc + mbx * 8 + bx * 2;
-    if (pcm) {                                                       // mb_pred_ipcm decoder.cc:149-168
-        const uint8_t* raw = reinterpret_cast<const uint8_t*>(lv);
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-            *reinterpret_cast<uint32_t*>(ydst + (size_t)r * g.W) =
-                *reinterpret_cast<const uint32_t*>(raw + (by * 4 + r) * 16 + bx * 4);
-#pragma unroll
-        for (int pl = 0; pl < 2; ++pl)
-#pragma unroll
-            for (int r = 0; r < 2; ++r)
-                *reinterpret_cast<uint16_t*>((pl ? o.v : o.u) + coff + (size_t)r * g.Wc) =
-                    *reinterpret_cast<const uint16_t*>(raw + 256 + pl * 64 + (by * 2 + r) * 8 + bx * 2);
-        return;
-    }
-
-    // ---- residual inputs, issued before motion compensation
-    const int cbpl = q.cbp & 15, cbpc = q.cbp >> 4;
-    const int t8 = (q.flags & H264R_MBF_T8x8) != 0;
-    const h264r_quant* __restrict__ qt = &b.quant[pic];
-    const int qpl = q.qp_scaled[0];
-    const int b8 = (by >> 1) * 2 + (bx >> 1);
-    const int loff = b8_offset(q.cbp, b8);
-    uint4 lev[2] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
-    uint4 lsc[2] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
-    if (loff >= 0) {
-        if (!t8) {                      // 4x4 block: 16 raster levels
-            const uint4* p = reinterpret_cast<const uint4*>(lv + loff + ((by & 1) * 2 + (bx & 1)) * 16);
-            lev[0] = p[0]; lev[1] = p[1];
-            const uint4* s = reinterpret_cast<const uint4*>(&qt->scale4x4[1][0][qpl % 6][0]);
-            lsc[0] = s[0]; lsc[1] = s[1];
-        } else {                        // my 4x4 quadrant of the 8x8 block: rows (by&1)*4.., cols (bx&1)*4..
-            const int16_t* p = lv + loff + (by & 1) * 32 + (bx & 1) * 4;
-            const int16_t* s = &qt->scale8x8[1][0][qpl % 6][(by & 1) * 32 + (bx & 1) * 4];
-            const uint2 r0 = ld8(p), r1 = ld8(p + 8), r2 = ld8(p + 16), r3 = ld8(p + 24);
-            lev[0] = make_uint4(r0.x, r0.y, r1.x, r1.y); lev[1] = make_uint4(r2.x, r2.y, r3.x, r3.y);
-            const uint2 s0 = ld8(s), s1 = ld8(s + 8), s2 = ld8(s + 16), s3 = ld8(s + 24);
-            lsc[0] = make_uint4(s0.x, s0.y, s1.x, s1.y); lsc[1] = make_uint4(s2.x, s2.y, s3.x, s3.y);
-        }
-    }
-    // chroma: my 2x2 quadrant of chroma 4x4 block cb of each plane + the plane's 4 DC levels
-    const int cb = (by >> 1) * 2 + (bx >> 1), cr = (by & 1) * 2, cc = (bx & 1) * 2;
-    uint32_t clev[2][2] = {{0, 0}, {0, 0}}, csc[2][2] = {{0, 0}, {0, 0}};
-    uint2 cdc[2] = {make_uint2(0, 0), make_uint2(0, 0)};
-    int cdcs[2] = {0, 0};
-    if (cbpc) {
-        const LevelOffs lo = level_offsets(q);
-#pragma unroll
-        for (int pl = 0; pl < 2; ++pl) {
-            const int qpc = q.qp_scaled[1 + pl];
-            cdc[pl] = ld8(lv + lo.cdc + pl * 4);
-            cdcs[pl] = qt->scale4x4[1][1 + pl][qpc % 6][0];
-            if (cbpc == 2) {
-#pragma unroll
-                for (int r = 0; r < 2; ++r) {
-                    clev[pl][r] = *reinterpret_cast<const uint32_t*>(lv + lo.cac + pl * 64 + cb * 16 + (cr + r) * 4 + cc);
-                    csc[pl][r] = *reinterpret_cast<const uint32_t*>(&qt->scale4x4[1][1 + pl][qpc % 6][(cr + r) * 4 + cc]);
-                }
-            }
-        }
-    }
-
-    // ---- prediction
-    const int r0 = (int8_t)(m0.y & 255), r1 = (int8_t)(m1.y & 255);
-    const int dir = (r0 >= 0 && r1 >= 0) ? 2 : (r0 >= 0 ? 0 : 1);
-    uint32_t pY[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}}, pC[2][2] = {{0, 0}, {0, 0}};
-#pragma unroll 1
-    for (int l = 0; l < 2; ++l) {
-        const uint2 mw = l ? m1 : m0;
-        const int rr = l ? r1 : r0;
-        const bool use = rr >= 0;
-        if (!__any(use)) continue;                                  // P pictures: list 1 never
-        if (!use) continue;
-        const int slot = (int8_t)((mw.y >> 8) & 255);
-        const bool ok = slot >= 0 && slot < H264R_MAX_SLOTS && rr < H264R_MAX_REFS && S.planes[slot * 3];
-        const int mvx = (int16_t)(mw.x & 0xFFFF), mvy = (int16_t)(mw.x >> 16);
-        const int vx = X4 * 16 + mvx, vy = Y4 * 16 + mvy;           // quarter luma / eighth chroma units
-        if (!ok) {                                                   // no_ref: 128 (inter_prediction.cc:164-167,366-369)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) pY[l][i] = 0x80808080u;
-            pC[l][0] = pC[l][1] = 0x80808080u;
-            continue;
-        }
-        luma_block_pred(S.planes[slot * 3], g.W, g.H, vx >> 2, vy >> 2, vx & 3, vy & 3, pY[l]);
-#pragma unroll
-        for (int pl = 0; pl < 2; ++pl)
-            pC[l][pl] = chroma_block_pred(S.planes[slot * 3 + 1 + pl], g.Wc, g.Hc, vx >> 3, vy >> 3, vx & 7, vy & 7);
-    }
-    uint32_t predY[4], predC[2];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) predY[i] = wp_combine4(qs, wp_mode, dir, r0, r1, pY[0][i], pY[1][i], 0);
-#pragma unroll
-    for (int pl = 0; pl < 2; ++pl) predC[pl] = wp_combine4(qs, wp_mode, dir, r0, r1, pC[0][pl], pC[1][pl], 1 + pl);
-
-    // ---- luma residual (transform.cc:1058-1073)
-    int res[4][4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) res[i][c] = 0;
-    if (__any(cbpl != 0)) {
-        const int per = qpl / 6;
-        int d[4][4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                const uint4 lw = lev[i >> 1], sw = lsc[i >> 1];
-                const uint32_t lo_ = (i & 1) ? lw.z : lw.x, hi_ = (i & 1) ? lw.w : lw.y;
-                const uint32_t slo = (i & 1) ? sw.z : sw.x, shi = (i & 1) ? sw.w : sw.y;
-                const int lvv = sel16(lo_, hi_, c), scv = sel16(slo, shi, c);
-                d[i][c] = t8 ? dq8(lvv, scv, per) : dq4(lvv, scv, per);
-            }
-        if (!__any(t8 != 0)) {
-            // 4x4: rows then columns, all in-lane
-#pragma unroll
-            for (int i = 0; i < 4; ++i) idct4_inplace(d[i][0], d[i][1], d[i][2], d[i][3]);
-#pragma unroll
-            for (int c = 0; c < 4; ++c) idct4_inplace(d[0][c], d[1][c], d[2][c], d[3][c]);
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int c = 0; c < 4; ++c) res[i][c] = (d[i][c] + 32) >> 6;
-        } else {
-            // 8x8 (only t8 MBs reach here with d != 0 for their lanes; 4x4 MBs of the same
-            // wave take the in-lane path below).  Rows: my 4 + the 4 of lane ^ 1.
-            int e4[4][4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                int in[8], outv[8];
-#pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    const int ov = __shfl_xor(d[i][c], 1);
-                    in[c] = (bx & 1) ? ov : d[i][c];
-                    in[4 + c] = (bx & 1) ? d[i][c] : ov;
-                }
-                idct8(in, outv);
-#pragma unroll
-                for (int c = 0; c < 4; ++c) e4[i][c] = (bx & 1) ? outv[4 + c] : outv[c];
-            }
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                int in[8], outv[8];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int ov = __shfl_xor(e4[i][c], 4);
-                    in[i] = (by & 1) ? ov : e4[i][c];
-                    in[4 + i] = (by & 1) ? e4[i][c] : ov;
-                }
-                idct8(in, outv);
-#pragma unroll
-                for (int i = 0; i < 4; ++i) res[i][c] = t8 ? ((by & 1) ? outv[4 + i] : outv[i]) : 0;
-            }
-            if (!t8) {
-#pragma unroll
-                for (int i = 0; i < 4; ++i) idct4_inplace(d[i][0], d[i][1], d[i][2], d[i][3]);
-#pragma unroll
-                for (int c = 0; c < 4; ++c) idct4_inplace(d[0][c], d[1][c], d[2][c], d[3][c]);
-            }
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int c = 0; c < 4; ++c) res[i][c] = ((t8 ? res[i][c] : d[i][c]) + 32) >> 6;
-        }
-    }
-    // ---- construction + store, luma
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        uint32_t wv = 0;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) wv |= (uint32_t)clip255((int)((predY[i] >> (8 * c)) & 255) + res[i][c]) << (8 * c);
-        *reinterpret_cast<uint32_t*>(ydst + (size_t)i * g.W) = wv;
-    }
-
-    // ---- chroma residual (transform.cc:1081-1091, DC :875-889): chroma block cb is
-    // spread over lanes {blk, ^1, ^4, ^5}; my quadrant rows cr.., cols cc..
-#pragma unroll
-    for (int pl = 0; pl < 2; ++pl) {
-        int rc[2][2] = {{0, 0}, {0, 0}};
-        if (__any(cbpc != 0)) {
-            const int qpc = q.qp_scaled[1 + pl], per = qpc / 6;
-            int k[2][2];
-#pragma unroll
-            for (int r = 0; r < 2; ++r)
-#pragma unroll
-                for (int c = 0; c < 2; ++c)
-                    k[r][c] = dq4((int16_t)(clev[pl][r] >> (16 * c)), (int16_t)(csc[pl][r] >> (16 * c)), per);
-            const int c00 = (int16_t)(cdc[pl].x & 0xFFFF), c01 = (int16_t)(cdc[pl].x >> 16);
-            const int c10 = (int16_t)(cdc[pl].y & 0xFFFF), c11 = (int16_t)(cdc[pl].y >> 16);
-            const int e00 = c00 + c01, e01 = c00 - c01, e10 = c10 + c11, e11 = c10 - c11;
-            const int f = cb == 0 ? e00 + e10 : cb == 1 ? e01 + e11 : cb == 2 ? e00 - e10 : e01 - e11;
-            if (cr == 0 && cc == 0) k[0][0] = cbpc ? ((f * cdcs[pl]) * (1 << per)) >> 5 : 0;
-            // rows: my 2 columns + the 2 of lane ^ 1
-            int t[2][2];
-#pragma unroll
-            for (int r = 0; r < 2; ++r) {
-                const int o0 = __shfl_xor(k[r][0], 1), o1 = __shfl_xor(k[r][1], 1);
-                const int d0 = cc ? o0 : k[r][0], d1 = cc ? o1 : k[r][1], d2 = cc ? k[r][0] : o0, d3 = cc ? k[r][1] : o1;
-                int y0, y1, y2, y3;
-                idct4(d0, d1, d2, d3, y0, y1, y2, y3);
-                t[r][0] = cc ? y2 : y0;
-                t[r][1] = cc ? y3 : y1;
-            }
-            // columns: my 2 rows + the 2 of lane ^ 4
-#pragma unroll
-            for (int c = 0; c < 2; ++c) {
-                const int o0 = __shfl_xor(t[0][c], 4), o1 = __shfl_xor(t[1][c], 4);
-                const int d0 = cr ? o0 : t[0][c], d1 = cr ? o1 : t[1][c], d2 = cr ? t[0][c] : o0, d3 = cr ? t[1][c] : o1;
-                int y0, y1, y2, y3;
-                idct4(d0, d1, d2, d3, y0, y1, y2, y3);
-                rc[0][c] = ((cr ? y2 : y0) + 32) >> 6;
-                rc[1][c] = ((cr ? y3 : y1) + 32) >> 6;
-            }
-        }
-        uint8_t* cdst = (pl ? o.v : o.u) + coff;
-#pragma unroll
-        for (int r = 0; r < 2; ++r) {
-            const uint32_t pr = predC[pl] >> (16 * r);
-            const uint32_t wv = (uint32_t)clip255((int)(pr & 255) + rc[r][0]) |
-                                ((uint32_t)clip255((int)((pr >> 8) & 255) + rc[r][1]) << 8);
-            *reinterpret_cast<uint16_t*>(cdst + (size_t)r * g.Wc) = (uint16_t)wv;
-        }
-    }
 }
 
 }  // namespace h264r
