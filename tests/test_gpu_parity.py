@@ -225,3 +225,28 @@ def test_gpu_band_across_filtered_edge_is_reported(L, dec):
     with pytest.raises(h264r.H264RError) as e:
         dec.check()
     assert e.value.status == A.EDEVICE
+
+
+def test_gpu_ippp_chain_yuv_compare(L, dec, tmp_path):
+    """Output/compare step over a dependent IPPP chain: each decoded
+    picture is kept as reference slot 0 of the next (picture_end keep_slot); the GPU's
+    frames are written cropped (output.cc:109-227) and compared per frame with the
+    oracle's by the harness protocol (model/__init__.py:119-183)."""
+    from h264r import output as OUT
+    W, H, n = 22, 18, 4
+    cfg = synth.default_cfg(L, 3, W, H)
+    refs = synth.refpics(L, cfg)
+    crop = OUT.Crop(left=1, right=2, top=0, bottom=4)
+    gpu_yuv, want = tmp_path / "gpu.yuv", []
+    oracle_refs = list(refs)
+    with OUT.YuvWriter(gpu_yuv, W, H, crop) as w:
+        for i in range(n):
+            p = synth.picture(L, cfg, i)
+            out = dec.decode_picture(p, refs if i == 0 else None, keep_slot=0)
+            w.write(*out)
+            ref_out = O.decode(p, oracle_refs)
+            oracle_refs = [ref_out] + oracle_refs[1:]
+            want.append(hashlib.md5(OUT.frame_bytes(*ref_out, w.geom)).hexdigest())
+    OUT.write_digests(tmp_path / "gpu.yuv.md5", want)
+    assert OUT.compare_yuv(gpu_yuv, tmp_path / "gpu.yuv.md5", "ippp") == want
+    assert gpu_yuv.stat().st_size == n * w.geom.frame_bytes
