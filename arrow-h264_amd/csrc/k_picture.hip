@@ -253,7 +253,12 @@ extern "C" __global__ __launch_bounds__(256, H264R_LVL_WAVES) void k_intra_level
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int nb = (rows.y - rows.x) * g.wmb, m0 = rows.x * g.wmb;    // band MBs per picture
     const size_t total = (size_t)nb * b.num_pics;
-    const size_t gw = (size_t)blockIdx.x * 4 + wave, step = (size_t)gridDim.x * 4 * 64;
+    // a wave scans `chunk` MBs at a time: 64 when the batch has work for every wave, fewer
+    // for small batches (the latency chain: one picture per launch), so that the intra MBs
+    // of a level spread over all waves instead of queueing behind one another in a few
+    const unsigned nw = gridDim.x * 4u;
+    const int chunk = (int)min((size_t)64, max((size_t)1, (total + nw - 1) / nw));
+    const size_t gw = (size_t)blockIdx.x * 4 + wave, step = (size_t)nw * chunk;
     const int deepest = __hip_atomic_load(&lvsync[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int top = min(lmax, deepest);
     // the level of batch MB e (32-bit index math: P * nmb < 2^31); the load is clamped,
@@ -265,10 +270,10 @@ extern "C" __global__ __launch_bounds__(256, H264R_LVL_WAVES) void k_intra_level
         return lvl[(size_t)(e / nbu) * g.nmb + m0 + e % nbu];
     };
     for (int L = 1; L <= top; ++L) {
-        int cur = lvl_at(gw * 64);
-        for (size_t base = gw * 64; base < total; base += step) {
+        int cur = lvl_at(gw * chunk);
+        for (size_t base = gw * chunk; base < total; base += step) {
             const int nxt = lvl_at(base + step < total ? base + step : base);     // prefetch
-            const bool hit = base + lane < total && cur == L;
+            const bool hit = lane < chunk && base + lane < total && cur == L;
             uint64_t todo = __ballot(hit);
             cur = nxt;
             while (todo) {

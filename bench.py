@@ -126,6 +126,62 @@ def kernel_bytes(pics, nmb):
     return [inter, intra, len(pics) * nmb * 768]
 
 
+def latency_chain(dec, L, cfg, refs, stream, n: int, verify: int):
+    """SURVEY 8(d) latency mode: a dependent IPPP chain decoded one picture per launch.
+    Picture i predicts from DPB slot 0 = the decoded picture i-1 (slot 1 keeps the
+    synthetic reference), so every launch waits for the previous one's output.  Returns
+    (ms per picture, pictures, verified): the first `verify` pictures are compared with
+    the oracle's chain."""
+    import torch
+    from h264r import batch as B
+    from h264r import synth
+    W, H = cfg.width_mbs, cfg.height_mbs
+    slack = 64
+    sizes = (256 * W * H, 64 * W * H, 64 * W * H)
+
+    def planes_t(src=None):
+        if src is None:
+            return [torch.zeros(n_ + slack, dtype=torch.uint8, device="cuda") for n_ in sizes]
+        return [torch.from_numpy(np.concatenate([a.reshape(-1), np.zeros(slack, np.uint8)])).to("cuda") for a in src]
+    bufs = [planes_t(refs[0])] + [planes_t() for _ in range(n)]
+    slot1 = [planes_t(r) for r in refs[1:]]
+    pics = [synth.picture(L, cfg, 50_000 + i) for i in range(n)]
+    keep, batches = [], []
+    for i, p in enumerate(pics):
+        tab = np.zeros(3 * 32, np.int64)
+        for s_, planes in enumerate([bufs[i]] + slot1):
+            for k in range(3):
+                tab[3 * s_ + k] = planes[k].data_ptr()
+        tab_t = torch.from_numpy(tab).to("cuda")
+        db = B.to_device(B.pack([p], __import__("h264r").quant_flat()), 1, tab_t.data_ptr())
+        db.batch.out_y, db.batch.out_u, db.batch.out_v = (t.data_ptr() for t in bufs[i + 1])
+        keep.append((tab_t, db))
+        batches.append(db.batch)
+
+    def chain():
+        for b in batches:
+            dec.decode_batch(b, stream)
+    chain()                                            # warm-up (and the verified run)
+    torch.cuda.synchronize()
+    dec.check()
+    verified = None
+    if verify:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import _oracle as O
+        oref = list(refs)
+        verified = True
+        for i in range(min(verify, n)):
+            want = O.decode(pics[i], oref)
+            got = [bufs[i + 1][k][: sizes[k]].cpu().numpy() for k in range(3)]
+            verified &= all(np.array_equal(got[k], want[k].reshape(-1)) for k in range(3))
+            oref = [want] + oref[1:]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    chain()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / n * 1e3, n, verified
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -137,6 +193,8 @@ def main() -> int:
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16, help="threads of the multi-threaded CPU baseline")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--latency-pictures", type=int, default=32,
+                    help="length of the dependent-chain latency run (rank 0, N=1; 0 = skip)")
     ap.add_argument("--traffic-json", default=None, help="PMC traffic summary (default profiles/traffic.json)")
     ap.add_argument("--shard", choices=["replicas", "slices"], default=None,
                     help="N>1 placement: independent pictures per GPU, or slice bands of shared pictures "
@@ -296,6 +354,15 @@ def main() -> int:
                   "sample": f"{ncpu} pictures ({ncpu * nmb} MBs, {el:.1f} s) over {thr} threads, "
                             f"oracle_decode_pictures, on {cpu_model()}"}
 
+    latency = None
+    if rank == 0 and world == 1 and args.latency_pictures > 0 and shard == "replicas":
+        ms, nl, lver = latency_chain(dec, L, cfg, refs, stream, args.latency_pictures,
+                                     0 if args.no_verify else 3)
+        latency = {"ms_per_picture": ms, "pictures": nl, "macroblocks_per_s": nmb / (ms * 1e-3),
+                   "verified_vs_oracle": lver,
+                   "workload": f"dependent chain of {CONFIG_NAMES[args.config]}, one picture per launch "
+                               "(slot 0 = previous decoded picture)"}
+
     if rank == 0:
         out = {
             "metric": "macroblocks/s (decode reconstruct, post-entropy) 1080p P-frame; % HBM roofline",
@@ -318,6 +385,7 @@ def main() -> int:
                           "batch_wall": float(kern[3])},
             "cpu_baseline": cpu,
             "cpu_baseline_threads": cpu_mt,
+            "latency": latency,
             "verified_vs_oracle": verified,
         }
         print(json.dumps(out))
