@@ -5,7 +5,7 @@ deblock) on MI355X, BASELINE.json's metric.
 A step = one h264r_decode_batch over a batch of synthetic pictures already
 resident in HBM (SURVEY 8(d) throughput mode: B independent pictures sharing a
 reference set).  Default workload: SURVEY config 3, 1080p (120x68 MBs) IPPP
-Main P pictures, B = 256 per GPU (about 2 GB of HBM: the order-dependent walks
+Main P pictures, B = 1024 per GPU (about 8 GB of HBM: the order-dependent walks
 need many pictures in flight to fill 256 CUs).
 
 Multi-GPU (torchrun, one process per GPU): config 3 uses deblocking across the
@@ -188,7 +188,7 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", type=int, default=3, choices=[2, 3, 4, 5])
-    ap.add_argument("--batch", type=int, default=0, help="pictures per GPU per step (default 256, 64 at 2160p)")
+    ap.add_argument("--batch", type=int, default=0, help="pictures per GPU per step (default 1024 for configs 2/3, 256 for 4, 64 at 2160p)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16, help="threads of the multi-threaded CPU baseline")
@@ -219,7 +219,11 @@ def main() -> int:
 
     L = h264r.lib()
     W, H = CONFIG_SIZE[args.config]
-    nb = args.batch or (64 if args.config == 5 else 256)
+    # pictures per GPU per step: the order-dependent walks (deblocking wavefront, intra
+    # levels) need many pictures in flight; 1080p config 2/3 batches of 1024 pictures
+    # (~8 GB of HBM) beat 256 by ~12 % (profiles/r01_batch_sweep.txt).  Slice mode
+    # holds world x nb pictures per rank, so configs 4/5 stay smaller.
+    nb = args.batch or {2: 1024, 3: 1024, 4: 256, 5: 64}[args.config]
     cfg = synth.default_cfg(L, args.config, W, H)
     nmb = W * H
     shard = args.shard or ("slices" if world > 1 and cfg.deblock_idc != 0 and cfg.num_slices > 1 else "replicas")
