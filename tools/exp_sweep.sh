@@ -5,7 +5,7 @@
 set -e
 OUT=$(realpath -m "$1"); shift
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
-ARGS=${BENCH_ARGS:-"--steps 10 --warmup 2 --no-cpu"}
+ARGS=${BENCH_ARGS:-"--steps 10 --warmup 2 --no-cpu --latency-pictures 0"}
 mkdir -p "$OUT"
 for spec in "$@"; do
   name=${spec%%:*}; envs=${spec#*:}

@@ -5,7 +5,7 @@
 set -e
 OUT=$(realpath -m "$1"); shift
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
-ARGS=${*:-"--batch 64 --steps 3 --warmup 1 --no-cpu --no-verify"}
+ARGS=${*:-"--batch 64 --steps 3 --warmup 1 --no-cpu --no-verify --latency-pictures 0"}
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 timeout -s KILL 120 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/stats" -o run -- python3 "$ROOT/bench.py" $ARGS > "$OUT/stats.log" 2>&1

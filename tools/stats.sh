@@ -2,7 +2,7 @@
 # tools/stats.sh <outdir> [bench args] -- rocprofv3 kernel-trace stats of a short bench run (GPU box)
 OUT=$(realpath -m "$1"); shift
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
-ARGS=${*:-"--steps 3 --warmup 1 --no-cpu --no-verify"}
+ARGS=${*:-"--steps 3 --warmup 1 --no-cpu --no-verify --latency-pictures 0"}
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 timeout -s KILL 150 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT" -o run -- python3 "$ROOT/bench.py" $ARGS > "$OUT/bench.log" 2>&1
