@@ -133,6 +133,7 @@ def latency_chain(dec, L, cfg, refs, stream, n: int, verify: int):
     (ms per picture, pictures, verified): the first `verify` pictures are compared with
     the oracle's chain."""
     import torch
+    import h264r
     from h264r import batch as B
     from h264r import synth
     W, H = cfg.width_mbs, cfg.height_mbs
@@ -153,7 +154,7 @@ def latency_chain(dec, L, cfg, refs, stream, n: int, verify: int):
             for k in range(3):
                 tab[3 * s_ + k] = planes[k].data_ptr()
         tab_t = torch.from_numpy(tab).to("cuda")
-        db = B.to_device(B.pack([p], __import__("h264r").quant_flat()), 1, tab_t.data_ptr())
+        db = B.to_device(B.pack([p], h264r.quant_flat()), 1, tab_t.data_ptr())
         db.batch.out_y, db.batch.out_u, db.batch.out_v = (t.data_ptr() for t in bufs[i + 1])
         keep.append((tab_t, db))
         batches.append(db.batch)
