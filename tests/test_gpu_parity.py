@@ -250,3 +250,18 @@ def test_gpu_ippp_chain_yuv_compare(L, dec, tmp_path):
     OUT.write_digests(tmp_path / "gpu.yuv.md5", want)
     assert OUT.compare_yuv(gpu_yuv, tmp_path / "gpu.yuv.md5", "ippp") == want
     assert gpu_yuv.stat().st_size == n * w.geom.frame_bytes
+
+
+def test_gpu_batch_latency_chain(L, dec):
+    """bench.py's latency mode: a dependent chain through h264r_decode_batch, one picture
+    per launch, each writing straight into the DPB slot the next one predicts from;
+    the chain is compared with the oracle's (the same function bench.py times)."""
+    import sys
+    import torch
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    cfg = synth.default_cfg(L, 3, 22, 18)
+    refs = synth.refpics(L, cfg)
+    ms, n, ok = bench.latency_chain(dec, L, cfg, refs, torch.cuda.current_stream().cuda_stream, 4, 4)
+    assert n == 4 and ms > 0
+    assert ok is True
