@@ -39,20 +39,6 @@ DEV int clip3(int lo, int hi, int x) { return x < lo ? lo : (x > hi ? hi : x); }
 DEV int clip255(int x) { return clip3(0, 255, x); }                                 // clip1, defines.h:54-58
 DEV int iabs(int x) { return x < 0 ? -x : x; }
 
-// Load the 32-byte MB record into SGPR-friendly registers (wave-uniform address).
-DEV h264r_mb load_mb(const h264r_mb* p)
-{
-    const uint4* q = reinterpret_cast<const uint4*>(p);
-    uint4 a = q[0], b = q[1];
-    h264r_mb m;
-    uint32_t* w = reinterpret_cast<uint32_t*>(&m);
-    w[0] = __builtin_amdgcn_readfirstlane(a.x); w[1] = __builtin_amdgcn_readfirstlane(a.y);
-    w[2] = __builtin_amdgcn_readfirstlane(a.z); w[3] = __builtin_amdgcn_readfirstlane(a.w);
-    w[4] = __builtin_amdgcn_readfirstlane(b.x); w[5] = __builtin_amdgcn_readfirstlane(b.y);
-    w[6] = __builtin_amdgcn_readfirstlane(b.z); w[7] = __builtin_amdgcn_readfirstlane(b.w);
-    return m;
-}
-
 // Scalar (constant address space) load of data that no kernel of the batch writes
 // (MB records, slice headers): a wave-uniform address becomes an s_load, issued back
 // to back with the others and waited on lgkmcnt, not interleaved with vmcnt waits.
@@ -140,12 +126,6 @@ DEV void idct8(const int* in, int* out)
 }
 
 // ---------------------------------------------------------------- motion comp.
-// Clamped sample fetch (equivalent to the reference's padded planes, picture.cc:182-205).
-DEV int pxl(const uint8_t* __restrict__ img, int W, int H, int x, int y)
-{
-    return img[clip3(0, H - 1, y) * W + clip3(0, W - 1, x)];
-}
-DEV int tap6(int a, int b, int c, int d, int e, int f) { return a - 5 * b + 20 * c + 20 * d - 5 * e + f; }
 
 // ------------------------------------------------------------ row-window MC
 // The per-sample forms above fetch one byte per tap.  The MC path proper loads
@@ -191,98 +171,6 @@ DEV const gdword* row_dwords(const uint8_t* __restrict__ img, int W, int H, int 
 {
     const int a = clip3(0, W - 1, x - 2) & ~3;
     return as_global(img + (size_t)clip3(0, H - 1, y) * W + a);
-}
-
-// Four luma prediction samples (x..x+3, y) at quarter-sample phase (xf, yf),
-// get_block_luma (inter_prediction.cc:158-340) in spec form (8.4.2.2.1): the
-// half-sample values b (horizontal), h (vertical), j (centre) and their
-// averages.  The 6 rows y-2..y+3 are streamed; each tap row is loaded once.
-// XF/YF >= 0 fix the phase at compile time (wave-uniform MV phase: only that
-// case's arithmetic is emitted); -1 takes it from xf_rt/yf_rt per lane.
-template <int XF = -1, int YF = -1>
-DEV void luma_pred4(const uint8_t* __restrict__ img, int W, int H, int x, int y, int xf_rt, int yf_rt, int (&out)[4])
-{
-    constexpr int C6[6] = {1, -5, 20, 20, -5, 1};
-    const int xf = XF >= 0 ? XF : xf_rt, yf = YF >= 0 ? YF : yf_rt;
-    if (yf == 0) {                                    // G, a, b, c: one row
-        const gdword* q = row_dwords(img, W, H, x, y);
-        int p[9];
-        row9(q[0], q[1], q[2], x, W, p);
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            if (xf == 0) { out[c] = p[2 + c]; continue; }
-            const int b = clip255((tap6(p[c], p[c + 1], p[c + 2], p[c + 3], p[c + 4], p[c + 5]) + 16) >> 5);
-            out[c] = xf == 2 ? b : (b + (xf == 3 ? p[3 + c] : p[2 + c]) + 1) >> 1;
-        }
-        return;
-    }
-    uint32_t w[6][3];
-#pragma unroll
-    for (int k = 0; k < 6; ++k) {
-        const gdword* q = row_dwords(img, W, H, x, y - 2 + k);
-        w[k][0] = q[0]; w[k][1] = q[1]; w[k][2] = q[2];
-    }
-    const bool jfam = xf == 2 || (yf == 2 && xf != 0);   // needs the centre sample j
-    const int hs = xf == 3 ? 1 : 0;                        // column of h / G for odd phases
-    const int brow = yf == 3 ? 3 : 2;                      // row of b / G (y or y+1)
-    int hacc[4] = {0, 0, 0, 0}, jacc[4] = {0, 0, 0, 0}, bsv[4] = {0, 0, 0, 0}, gsv[4] = {0, 0, 0, 0};
-#pragma unroll
-    for (int k = 0; k < 6; ++k) {
-        int p[9];
-        row9(w[k][0], w[k][1], w[k][2], x, W, p);
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            hacc[c] += C6[k] * (hs ? p[3 + c] : p[2 + c]);
-            if (k == brow) gsv[c] = p[2 + c];
-            if (jfam || ((xf & 1) && k == brow)) {
-                const int b1 = tap6(p[c], p[c + 1], p[c + 2], p[c + 3], p[c + 4], p[c + 5]);
-                jacc[c] += C6[k] * b1;
-                if (k == brow) bsv[c] = b1;
-            }
-        }
-    }
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        const int h = clip255((hacc[c] + 16) >> 5);
-        const int b = clip255((bsv[c] + 16) >> 5);
-        int v;
-        if (xf == 0) v = yf == 2 ? h : (h + gsv[c] + 1) >> 1;                 // d, h, n
-        else if (!jfam) v = (b + h + 1) >> 1;                                 // e, g, p, r
-        else {
-            const int j = clip255((jacc[c] + 512) >> 10);
-            if (xf == 2 && yf == 2) v = j;                                    // j
-            else if (xf == 2) v = (j + b + 1) >> 1;                           // f, q
-            else v = (j + h + 1) >> 1;                                        // i, k
-        }
-        out[c] = v;
-    }
-}
-
-// Two chroma prediction samples (xi, xi+1; yi) at eighth-sample phase (xf, yf),
-// get_block_chroma (inter_prediction.cc:380-404).
-DEV void chroma_pred2(const uint8_t* __restrict__ img, int W, int H, int xi, int yi, int xf, int yf, int (&out)[2])
-{
-    const int a = clip3(0, W - 1, xi) & ~3;
-    int p[2][3];
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        const gdword* q = as_global(img + (size_t)clip3(0, H - 1, yi + k) * W + a);
-        const uint32_t w0 = q[0], w1 = q[1];
-        if (xi >= 0 && xi + 2 < W) {
-            const uint32_t r = __builtin_amdgcn_alignbyte(w1, w0, xi & 3);
-            p[k][0] = r & 255; p[k][1] = (r >> 8) & 255; p[k][2] = (r >> 16) & 255;
-        } else {
-#pragma unroll
-            for (int c = 0; c < 3; ++c) {
-                const int idx = clip3(0, W - 1, xi + c) - a;
-                p[k][c] = ((idx < 4 ? w0 : w1) >> (8 * (idx & 3))) & 255;
-            }
-        }
-    }
-#pragma unroll
-    for (int c = 0; c < 2; ++c)
-        out[c] = ((8 - xf) * (8 - yf) * p[0][c] + xf * (8 - yf) * p[0][c + 1] + (8 - xf) * yf * p[1][c] +
-                  xf * yf * p[1][c + 1] + 32) >> 6;
 }
 
 DEV int rshift_rnd(int x, int a) { return a > 0 ? (x + (1 << (a - 1))) >> a : x; }  // inter_prediction.cc:35-38
@@ -334,36 +222,38 @@ __device__ static const uint32_t DB_TC0[52] = {
 #undef T
 };
 
-// filter_strong / filter_normal (deblock.cc:327-415) on 8 samples p3..p0 q0..q3 held in
-// registers; returns the updated samples in place.
-DEV void filter_samples(int& p3, int& p2, int& p1, int& p0, int& q0, int& q1, int& q2, int& q3,
-                        int alpha, int beta, int bS, int chroma, int tc0)
+// ------------------------------------------------------------- shared helpers
+template <int K>
+DEV int quad_bcast(int v)       // value of lane K of this lane's quad
 {
-    if (!(iabs(p0 - q0) < alpha && iabs(p1 - p0) < beta && iabs(q1 - q0) < beta)) return;
-    int ap = iabs(p2 - p0), aq = iabs(q2 - q0);
-    if (bS == 4) {
-        int np0, np1, np2, nq0, nq1, nq2;
-        int strong = iabs(p0 - q0) < (alpha >> 2) + 2;
-        if (!chroma && ap < beta && strong) {
-            np0 = (p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3;
-            np1 = (p2 + p1 + p0 + q0 + 2) >> 2;
-            np2 = (2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3;
-        } else { np0 = (2 * p1 + p0 + q1 + 2) >> 2; np1 = p1; np2 = p2; }
-        if (!chroma && aq < beta && strong) {
-            nq0 = (p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3;
-            nq1 = (p0 + q0 + q1 + q2 + 2) >> 2;
-            nq2 = (2 * q3 + 3 * q2 + q1 + q0 + p0 + 4) >> 3;
-        } else { nq0 = (2 * q1 + q0 + p1 + 2) >> 2; nq1 = q1; nq2 = q2; }
-        p0 = np0; p1 = np1; p2 = np2; q0 = nq0; q1 = nq1; q2 = nq2;
-    } else {
-        int tc = chroma ? tc0 + 1 : tc0 + (ap < beta) + (aq < beta);
-        int delta = clip3(-tc, tc, (((q0 - p0) * 4) + (p1 - q1) + 4) >> 3);
-        int np1 = p1, nq1 = q1;
-        if (!chroma && ap < beta) np1 = p1 + clip3(-tc0, tc0, (p2 + ((p0 + q0 + 1) >> 1) - (p1 * 2)) >> 1);
-        if (!chroma && aq < beta) nq1 = q1 + clip3(-tc0, tc0, (q2 + ((p0 + q0 + 1) >> 1) - (q1 * 2)) >> 1);
-        p0 = clip255(p0 + delta); q0 = clip255(q0 - delta);
-        p1 = np1; q1 = nq1;
-    }
+    return __builtin_amdgcn_update_dpp(0, v, K * 0x55, 0xF, 0xF, false);
+}
+
+// Column pass of inverse_4x4 (transform.cc:619-640) for the lane holding row r of
+// the block: t[k] = row k's value in this column.  Returns ((o_r + 32) >> 6).
+DEV int idct4_col_row(int t0, int t1, int t2, int t3, int r)
+{
+    const int e0 = t0 + t2, e1 = t0 - t2, e2 = (t1 >> 1) - t3, e3 = t1 + (t3 >> 1);
+    const bool outer = r == 0 || r == 3;
+    const int x = outer ? e0 : e1, y = outer ? e3 : e2;
+    return ((r < 2 ? x + y : x - y) + 32) >> 6;
+}
+
+DEV uint2 ld8(const void* p) { return *reinterpret_cast<const uint2*>(p); }
+
+struct PicPtrs {
+    uint8_t* y;
+    uint8_t* u;
+    uint8_t* v;
+};
+
+DEV PicPtrs out_planes(const h264r_batch& b, const Geom& g, int pic)
+{
+    PicPtrs p;
+    p.y = b.out_y + (size_t)pic * g.ysz;
+    p.u = b.out_u + (size_t)pic * g.csz;
+    p.v = b.out_v + (size_t)pic * g.csz;
+    return p;
 }
 
 }  // namespace h264r

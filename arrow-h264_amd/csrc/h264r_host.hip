@@ -23,8 +23,6 @@
 
 namespace h264r { struct DbInfo; }
 extern "C" __global__ void k_prep(h264r_batch b, uint2* mot, int2 rows);
-extern "C" __global__ void k_inter(h264r_batch b, const uint2* mot);
-extern "C" __global__ void k_dbinfo(h264r_batch b, const uint2* mot, h264r::DbInfo* dbinfo);
 extern "C" __global__ void k_inter4(h264r_batch b, const uint2* mot, h264r::DbInfo* dbinfo, int2 rows);
 extern "C" __global__ void k_intra_pic(h264r_batch b, int* sync, int* err, const uint16_t* lvl, int lmax, int2 rows);
 extern "C" __global__ void k_level(h264r_batch b, uint16_t* lvl, int* lvsync, int2 rows);
@@ -32,8 +30,6 @@ extern "C" __global__ void k_intra_levels(h264r_batch b, const uint16_t* lvl, in
 constexpr int LEVEL_MAX_MBS = 65536;      // k_level's LDS bitmap (k_picture.hip)
 extern "C" __global__ void k_deblock(h264r_batch b, const h264r::DbInfo* dbinfo, uint64_t* hb,
                                      int* sync, int* err, uint32_t epoch, int2 rows);
-extern "C" __global__ void k_deblock4(h264r_batch b, const h264r::DbInfo* dbinfo, uint64_t* hb,
-                                      int* sync, int* err, uint32_t epoch, int2 rows);
 constexpr size_t DBINFO_BYTES = 80;
 constexpr size_t HANDOFF_BYTES = 256;   // one tagged record (32 x {dword, epoch}) per MB
 
@@ -120,11 +116,10 @@ struct h264r_ctx {
     uint2* d_mot = nullptr; size_t c_mot = 0;
     uint16_t* d_lvl = nullptr; size_t c_lvl = 0;   // intra dependency level per MB
     int levels_grid = 0;                           // resident workgroups of k_intra_levels
-    // pipelining: prep+inter on the caller's stream, intra and deblocking of each
-    // chunk of pictures on two more streams, chained by events
-    hipStream_t aux[2] = {};
-    std::vector<hipEvent_t> ev_chain;               // [2 * chunk + 0] inter done, [+1] intra done
-    hipEvent_t ev_end = nullptr;
+    // the per-batch scratch above is reused by every launch: a launch on a stream other
+    // than the previous one first waits for the previous launch (ev_last)
+    hipStream_t last_stream = nullptr;
+    hipEvent_t ev_last = nullptr;
     // timing: every kernel of every launch bracketed by events on its stream
     bool timing = false;
     int debug = 0;
@@ -210,19 +205,15 @@ int h264r_create(h264r_ctx** out, int device, int max_w, int max_h, int chroma_f
     h264r_ctx* c = new (std::nothrow) h264r_ctx();
     if (!c) return H264R_ENOMEM;
     c->device = device; c->max_w = max_w; c->max_h = max_h;
-    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+    // the context's own stream is a BLOCKING stream: work on the legacy NULL stream (torch's
+    // default stream) and this stream are ordered with each other
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamDefault) != hipSuccess ||
         hipMalloc(reinterpret_cast<void**>(&c->d_ref_planes), sizeof(uint8_t*) * 3 * H264R_MAX_SLOTS) != hipSuccess ||
         hipMalloc(reinterpret_cast<void**>(&c->d_err), sizeof(int)) != hipSuccess) {
         delete c;
         return H264R_EDEVICE;
     }
-    {   // the wavefront walks are latency-bound: their streams get the highest priority
-        int lo = 0, hi = 0;
-        (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
-        for (int i = 0; i < 2; ++i)
-            if (hipStreamCreateWithPriority(&c->aux[i], hipStreamNonBlocking, hi) != hipSuccess) { delete c; return H264R_EDEVICE; }
-    }
-    (void)hipEventCreateWithFlags(&c->ev_end, hipEventDisableTiming);
+    if (hipEventCreateWithFlags(&c->ev_last, hipEventDisableTiming) != hipSuccess) { delete c; return H264R_EDEVICE; }
     (void)hipMemset(c->d_ref_planes, 0, sizeof(uint8_t*) * 3 * H264R_MAX_SLOTS);
     (void)hipMemset(c->d_err, 0, sizeof(int));
     *out = c;
@@ -238,9 +229,7 @@ int h264r_destroy(h264r_ctx* c)
     void* bufs[] = {c->d_ref_planes, c->d_err, c->d_dbinfo, c->d_sync, c->d_hb, c->d_mot, c->d_lvl, c->d_mbs, c->d_levels, c->d_mv, c->d_ref, c->d_slices, c->d_pic, c->d_quant, c->d_out};
     for (void* b : bufs) if (b) (void)hipFree(b);
     for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
-    for (hipEvent_t e : c->ev_chain) (void)hipEventDestroy(e);
-    if (c->ev_end) (void)hipEventDestroy(c->ev_end);
-    for (int i = 0; i < 2; ++i) if (c->aux[i]) { (void)hipStreamSynchronize(c->aux[i]); (void)hipStreamDestroy(c->aux[i]); }
+    if (c->ev_last) (void)hipEventDestroy(c->ev_last);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return H264R_OK;
@@ -309,37 +298,6 @@ struct Timed {
     }
 };
 
-// A batch restricted to pictures [p0, p0 + n).
-static h264r_batch chunk_of(const h264r_batch& b, int p0, int n)
-{
-    h264r_batch c = b;
-    const size_t nmb = (size_t)b.width_mbs * b.height_mbs, mp = nmb * 16;
-    const size_t ys = nmb * 256, cs = nmb * 64;
-    c.num_pics = n;
-    c.mbs = b.mbs + p0 * nmb;
-    c.mv = b.mv + p0 * 2 * mp;
-    c.ref_idx = b.ref_idx + p0 * 2 * mp;
-    c.slices = b.slices + (size_t)p0 * b.slice_stride;
-    c.pics = b.pics + p0;
-    c.quant = b.quant + p0;
-    c.out_y = b.out_y + p0 * ys;
-    c.out_u = b.out_u + p0 * cs;
-    c.out_v = b.out_v + p0 * cs;
-    return c;
-}
-
-// Pictures per pipelined chunk: the intra and deblocking walks of chunk i (latency-
-// bound wavefronts) run beside k_inter of chunk i+1 (throughput-bound).
-// Measured on MI355X (config 3, 1080p P): the walks are latency-bound, so a chunk's
-// walk takes about as long as the whole batch's -- chunking serialises them and loses
-// (64 pictures: 153 M MB/s unchunked vs 83 M with 16-picture chunks).  Off by default;
-// H264R_CHUNK=<pictures> enables it for experiments.
-static int chunk_pictures(int P)
-{
-    static const int env = [] { const char* e = getenv("H264R_CHUNK"); return e ? atoi(e) : 0; }();
-    return env > 0 ? env : P;
-}
-
 // Intra MBs are scheduled by dependency level (k_level, then k_intra_levels does levels
 // 1..N in one persistent launch); the wavefront walk k_intra_pic takes whatever lies deeper.  In P/B
 // pictures the deepest level is a handful; in all-intra pictures most MBs are deeper
@@ -350,42 +308,31 @@ static int level_launches()
     return std::max(0, std::min(env, 256));
 }
 
-// Inter MBs: k_inter4 (four MBs per wave, lane per 4x4 block, deblock records
-// folded in) unless H264R_INTER=1 selects the wave-per-MB k_inter + k_dbinfo pair.
-static bool inter4()
-{
-    static const bool v = [] { const char* e = getenv("H264R_INTER"); return !(e && atoi(e) == 1); }();
-    return v;
-}
-
 // rows [row0, row1): the MB rows of every picture this launch reconstructs and
 // deblocks (the whole picture, or a slice-aligned band: h264r_decode_batch_rows).
-// Deblocking: k_deblock (two MB rows per wave, one line per lane) unless
-// H264R_DEBLOCK=4 selects k_deblock4 (four rows per wave, packed 16-bit lines).
-// Measured on MI355X (config 3, 1080p P): both bit-exact; k_deblock4 issues 20 %
-// fewer VALU and half the SALU per MB but its longer per-step chain makes the
-// wavefront slower (batch 240: 3.41 ms vs 2.92 ms), so it is not the default.
-static bool deblock4()
-{
-    static const bool v = [] { const char* e = getenv("H264R_DEBLOCK"); return e && atoi(e) == 4; }();
-    return v;
-}
-
+// Six launches on stream s: k_prep, k_inter4 (inter / PCM MBs + deblocking records),
+// k_level + k_intra_levels + k_intra_pic (intra MBs), k_deblock.
 static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row0, int row1)
 {
     const int W = b.width_mbs, H = b.height_mbs, P = b.num_pics, HB = row1 - row0;
     const int2 rows = make_int2(row0, row1);
-    const int nbands = (HB + 15) / 16, npairs = (HB + 1) / 2, nquads = (HB + 3) / 4;
-    const int CP = std::min(chunk_pictures(P), P), K = (P + CP - 1) / CP;
-    // scratch: per-MB deblocking records and resolved motion (whole batch), tagged
-    // row-pair hand-off records (one chunk; chunks deblock in stream order), and per
-    // chunk a sync region: [intra ticket + per-row progress][deblock ticket]
-    const size_t sync_chunk = 1 + (size_t)CP * H + 4;
+    const int nbands = (HB + 15) / 16, npairs = (HB + 1) / 2;
+    // scratch: per-MB deblocking records and resolved motion, tagged row-pair hand-off
+    // records, and a sync region [intra ticket + per-(picture,row) progress][deblock
+    // ticket][level barrier, deepest level]
+    const size_t sync_n = 1 + (size_t)P * H + 4;
+    // the scratch is shared by every launch of this context: a launch on another stream
+    // than the previous one waits for it first
+    if (c->last_stream && c->last_stream != s) {
+        HIP_OK(hipEventRecord(c->ev_last, c->last_stream));
+        HIP_OK(hipStreamWaitEvent(s, c->ev_last, 0));
+    }
+    c->last_stream = s;
     int st;
     if ((st = dev_resize(&c->d_dbinfo, &c->c_dbinfo, (size_t)P * W * H * DBINFO_BYTES))) return st;
     {
         const size_t cap_before = c->c_hb;
-        if ((st = dev_resize(&c->d_hb, &c->c_hb, (size_t)CP * std::max(npairs, nquads) * W * HANDOFF_BYTES))) return st;
+        if ((st = dev_resize(&c->d_hb, &c->c_hb, (size_t)P * npairs * W * HANDOFF_BYTES))) return st;
         if (c->c_hb != cap_before) {              // fresh memory: no record may carry a live epoch
             HIP_OK(hipMemsetAsync(c->d_hb, 0, c->c_hb, s));
             c->epoch = 0;
@@ -397,7 +344,7 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
     }
     const size_t mplane = (size_t)W * 4 * H * 4;
     if ((st = dev_resize(&c->d_mot, &c->c_mot, (size_t)P * 2 * mplane))) return st;
-    if ((st = dev_resize(&c->d_sync, &c->c_sync, (size_t)K * sync_chunk))) return st;
+    if ((st = dev_resize(&c->d_sync, &c->c_sync, sync_n))) return st;
     const bool levels = (size_t)W * H <= LEVEL_MAX_MBS && H <= 1024 && level_launches() > 0 &&
                         !(c->debug & H264R_DBG_INTRA_WALK);
     if (levels && !c->levels_grid) {
@@ -413,77 +360,39 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
             fprintf(stderr, "h264r: k_intra_levels occupancy %d blocks/CU, %d CUs, grid %d\n", per_cu, cus, c->levels_grid);
     }
     if (levels && (st = dev_resize(&c->d_lvl, &c->c_lvl, (size_t)P * W * H))) return st;
-    while ((int)c->ev_chain.size() < 2 * K) {
-        hipEvent_t e = nullptr;
-        HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        c->ev_chain.push_back(e);
-    }
-    HIP_OK(hipMemsetAsync(c->d_sync, 0, (size_t)K * sync_chunk * sizeof(int), s));
-    auto dbinfo_at = [&](int p0) { return reinterpret_cast<h264r::DbInfo*>(c->d_dbinfo + (size_t)p0 * W * H * DBINFO_BYTES); };
-    const bool deblock = !(c->debug & H264R_DBG_NO_DEBLOCK);
+    HIP_OK(hipMemsetAsync(c->d_sync, 0, sync_n * sizeof(int), s));
+    h264r::DbInfo* dbinfo = reinterpret_cast<h264r::DbInfo*>(c->d_dbinfo);
+    int* sync = c->d_sync;
     Timed whole(c, 3, s);
     if (c->timing) c->timed_launches++;
-    for (int k = 0; k < K; ++k) {
-        const int p0 = k * CP, n = std::min(CP, P - p0);
-        const h264r_batch cb = chunk_of(b, p0, n);
-        int* sync = c->d_sync + (size_t)k * sync_chunk;
-        // stream s: prep + inter of chunk k
-        {
-            hipLaunchKernelGGL(k_prep, dim3((unsigned)((HB * 16 * W + 255) / 256), n), dim3(256), 0, s, cb,
-                               c->d_mot + (size_t)p0 * 2 * mplane, rows);
-            HIP_OK(hipGetLastError());
-            Timed t(c, 0, s);                      // phase 0 = the inter kernel alone (k_prep is in the total only)
-            if ((inter4() && !(c->debug & H264R_DBG_INTER1)) || HB != H) {
-                hipLaunchKernelGGL(k_inter4, dim3((W * HB + 15) / 16, n), dim3(256), 0, s, cb,
-                                   c->d_mot + (size_t)p0 * 2 * mplane, dbinfo_at(p0), rows);
-                HIP_OK(hipGetLastError());
-            } else {
-                hipLaunchKernelGGL(k_dbinfo, dim3((W * H + 3) / 4, n), dim3(256), 0, s, cb,
-                                   c->d_mot + (size_t)p0 * 2 * mplane, dbinfo_at(p0));
-                HIP_OK(hipGetLastError());
-                hipLaunchKernelGGL(k_inter, dim3(W * H, n), dim3(64), 0, s, cb, c->d_mot + (size_t)p0 * 2 * mplane);
-                HIP_OK(hipGetLastError());
-            }
-        }
-        hipStream_t si = K > 1 ? c->aux[0] : s, sd = K > 1 ? c->aux[1] : s;
-        if (K > 1) {
-            HIP_OK(hipEventRecord(c->ev_chain[2 * k], s));
-            HIP_OK(hipStreamWaitEvent(si, c->ev_chain[2 * k], 0));
-        }
-        {
-            Timed t(c, 1, si);
-            uint16_t* lvl = levels ? c->d_lvl + (size_t)p0 * W * H : nullptr;
-            const int lmax = levels ? level_launches() : 0;
-            if (levels) {
-                int* lvsync = sync + 1 + (size_t)CP * H + 2;
-                hipLaunchKernelGGL(k_level, dim3(n), dim3(64 * ((HB + 63) / 64)), 0, si, cb, lvl, lvsync, rows);
-                HIP_OK(hipGetLastError());
-                hipLaunchKernelGGL(k_intra_levels, dim3(c->levels_grid), dim3(256), 0, si, cb, (const uint16_t*)lvl,
-                                   lmax, lvsync, c->d_err, rows);
-                HIP_OK(hipGetLastError());
-            }
-            hipLaunchKernelGGL(k_intra_pic, dim3(n * nbands), dim3(1024), 0, si, cb, sync, c->d_err,
-                               (const uint16_t*)lvl, lmax, rows);
-            HIP_OK(hipGetLastError());
-        }
-        if (K > 1) {
-            HIP_OK(hipEventRecord(c->ev_chain[2 * k + 1], si));
-            HIP_OK(hipStreamWaitEvent(sd, c->ev_chain[2 * k + 1], 0));
-        }
-        if (deblock) {
-            Timed t(c, 2, sd);
-            if (deblock4() || (c->debug & H264R_DBG_DEBLOCK4))
-                hipLaunchKernelGGL(k_deblock4, dim3(n * nquads), dim3(64), 0, sd, cb, dbinfo_at(p0),
-                                   reinterpret_cast<uint64_t*>(c->d_hb), sync + 1 + (size_t)CP * H, c->d_err, ++c->epoch, rows);
-            else
-                hipLaunchKernelGGL(k_deblock, dim3(n * npairs), dim3(64), 0, sd, cb, dbinfo_at(p0),
-                               reinterpret_cast<uint64_t*>(c->d_hb), sync + 1 + (size_t)CP * H, c->d_err, ++c->epoch, rows);
-            HIP_OK(hipGetLastError());
-        }
+    hipLaunchKernelGGL(k_prep, dim3((unsigned)((HB * 16 * W + 255) / 256), P), dim3(256), 0, s, b, c->d_mot, rows);
+    HIP_OK(hipGetLastError());
+    {
+        Timed t(c, 0, s);                         // phase 0 = the inter kernel alone (k_prep is in the total only)
+        hipLaunchKernelGGL(k_inter4, dim3((W * HB + 15) / 16, P), dim3(256), 0, s, b, c->d_mot, dbinfo, rows);
+        HIP_OK(hipGetLastError());
     }
-    if (K > 1) {                                   // the caller's stream sees the whole batch
-        HIP_OK(hipEventRecord(c->ev_end, c->aux[1]));
-        HIP_OK(hipStreamWaitEvent(s, c->ev_end, 0));
+    {
+        Timed t(c, 1, s);
+        uint16_t* lvl = levels ? c->d_lvl : nullptr;
+        const int lmax = levels ? level_launches() : 0;
+        if (levels) {
+            int* lvsync = sync + 1 + (size_t)P * H + 2;
+            hipLaunchKernelGGL(k_level, dim3(P), dim3(64 * ((HB + 63) / 64)), 0, s, b, lvl, lvsync, rows);
+            HIP_OK(hipGetLastError());
+            hipLaunchKernelGGL(k_intra_levels, dim3(c->levels_grid), dim3(256), 0, s, b, (const uint16_t*)lvl,
+                               lmax, lvsync, c->d_err, rows);
+            HIP_OK(hipGetLastError());
+        }
+        hipLaunchKernelGGL(k_intra_pic, dim3(P * nbands), dim3(1024), 0, s, b, sync, c->d_err,
+                           (const uint16_t*)lvl, lmax, rows);
+        HIP_OK(hipGetLastError());
+    }
+    if (!(c->debug & H264R_DBG_NO_DEBLOCK)) {
+        Timed t(c, 2, s);
+        hipLaunchKernelGGL(k_deblock, dim3(P * npairs), dim3(64), 0, s, b, dbinfo,
+                           reinterpret_cast<uint64_t*>(c->d_hb), sync + 1 + (size_t)P * H, c->d_err, ++c->epoch, rows);
+        HIP_OK(hipGetLastError());
     }
     return H264R_OK;
 }
@@ -549,8 +458,7 @@ int h264r_check(h264r_ctx* c)
     if (!c) return H264R_EINVAL;
     (void)hipSetDevice(c->device);
     HIP_OK(hipStreamSynchronize(c->stream));
-    for (int i = 0; i < 2; ++i) HIP_OK(hipStreamSynchronize(c->aux[i]));
-    HIP_OK(hipDeviceSynchronize());
+    if (c->last_stream) HIP_OK(hipStreamSynchronize(c->last_stream));
     int e = 0;
     HIP_OK(hipMemcpy(&e, c->d_err, sizeof(int), hipMemcpyDeviceToHost));
     if (e) { (void)hipMemset(c->d_err, 0, sizeof(int)); return H264R_EDEVICE; }

@@ -4,14 +4,10 @@
 //          RefPicList[l][ref_idx] (get_ref_pic dpb.cc:1046-1054 via the MB's
 //          slice) and packs {mv, ref_idx | slot << 8} per list, so the per-MB
 //          kernels never chase record -> slice -> slot -> plane.
-// k_inter  one 64-lane workgroup (= one wave) per MB: inter MBs and I_PCM
-//          reconstructed (mb_inter.h inter_mb2); intra MBs are left to the intra
-//          kernels (they depend on their neighbours).
-// k_dbinfo the per-MB deblocking record (boundary strengths + QPs, mb_deblock.h
-//          db_info_mb) for EVERY MB, so the order-dependent walk of k_deblock
-//          loads 80 B per MB.
-#include "mb_inter.h"
-#include "mb_deblock.h"
+// k_inter4 four MBs per wave, one lane per 4x4 block: inter MBs and I_PCM
+//          reconstructed (mb_inter4.h), and the per-MB deblocking record DbInfo of
+//          every MB; intra MBs are left to the intra kernels (they depend on their
+//          neighbours).
 #include "mb_inter4.h"
 
 using namespace h264r;
@@ -32,27 +28,6 @@ extern "C" __global__ __launch_bounds__(256) void k_prep(h264r_batch b, uint2* _
         const int slot = ri >= 0 && ri < H264R_MAX_REFS ? sl->ref_slot[l][ri] : -1;
         mot[base + (size_t)l * g.motion_plane + idx] = make_uint2(mv, (uint32_t)(uint8_t)ri | ((uint32_t)(uint8_t)slot << 8));
     }
-}
-
-extern "C" __global__ __launch_bounds__(64) void k_inter(h264r_batch b, const uint2* __restrict__ mot)
-{
-    __shared__ ResLds R;
-    const Geom g = make_geom(b.width_mbs, b.height_mbs);
-    const int pic = blockIdx.y, a = blockIdx.x, lane = threadIdx.x;
-    inter_mb2(b, g, pic, a, lane, mot + (size_t)pic * 2 * g.motion_plane, R);
-}
-
-// k_dbinfo: the deblocking record of every MB (mb_deblock.h db_info_mb), four MBs
-// per workgroup, one wave each.  Kept out of k_inter: it is small, fully parallel
-// work whose loads (three MB records, eight motion entries per lane) would otherwise
-// lengthen every inter MB's dependency chain.
-extern "C" __global__ __launch_bounds__(256) void k_dbinfo(h264r_batch b, const uint2* __restrict__ mot, DbInfo* dbinfo)
-{
-    const Geom g = make_geom(b.width_mbs, b.height_mbs);
-    const int pic = blockIdx.y, lane = threadIdx.x & 63;
-    const int a = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (a >= g.nmb) return;
-    db_info_mb(b, g, pic, a, lane, mot + (size_t)pic * 2 * g.motion_plane, dbinfo + (size_t)pic * g.nmb + a);
 }
 
 // k_inter4: inter / I_PCM MBs and the deblocking record of every MB, four MBs per

@@ -82,73 +82,6 @@ DEV uint32_t edge_word(int qpp, int qpq, int offa, int offb)
            (((t >> 16) & 31) << 26);
 }
 
-// Deblock::strength + strength_vertical/horizontal for MB `a` (deblock.cc:78-289).
-// All lanes call; lanes 0..31 compute one strength each, lanes 32..40 the edge
-// parameters (alpha/beta/tc0 per plane and edge class).  `mot`
-// is the picture's resolved motion (k_prep), [list][H4][W4]; every load is issued
-// before the first decision so the record and motion latencies overlap.
-DEV void db_info_mb(const h264r_batch& b, const Geom& g, int pic, int a, int lane, const uint2* __restrict__ mot,
-                    DbInfo* __restrict__ out)
-{
-    const int mbx = a % g.wmb, mby = a / g.wmb;
-    const h264r_mb* mbs = b.mbs + (size_t)pic * g.nmb;
-    const h264r_slice* slices = b.slices + (size_t)pic * b.slice_stride;
-    const int hor = (lane >> 4) & 1, e = (lane >> 2) & 3, s = lane & 3;
-    const int qx = mbx * 4 + (hor ? s : e), qy = mby * 4 + (hor ? e : s);
-    const int px = max(qx - (hor ? 0 : 1), 0), py = max(qy - (hor ? 1 : 0), 0);
-    const uint2 q0 = mot[qy * g.W4 + qx], q1 = mot[g.motion_plane + qy * g.W4 + qx];
-    const uint2 p0 = mot[py * g.W4 + px], p1 = mot[g.motion_plane + py * g.W4 + px];
-    const h264r_mb q = load_mb(&mbs[a]);
-    const int hasL = mbx > 0, hasU = mby > 0;
-    const h264r_mb L = load_mb(&mbs[hasL ? a - 1 : a]);
-    const h264r_mb U = load_mb(&mbs[hasU ? a - g.wmb : a]);
-    const h264r_slice* qs = &slices[q.slice];
-    const int idc = qs->deblock_idc;
-    const int fl = idc == 0 ? hasL : (idc == 2 && hasL && L.slice == q.slice);
-    const int ft = idc == 0 ? hasU : (idc == 2 && hasU && U.slice == q.slice);
-    const int t8 = (q.flags & H264R_MBF_T8x8) != 0;
-    if (lane < 32) {
-        const int en = idc != 1 && (e == 0 ? (hor ? ft : fl) : ((e & 1) ? !t8 : 1));
-        int v = 0;
-        if (en) {
-            const h264r_mb& P = e == 0 ? (hor ? U : L) : q;
-            const int special = special_slice(slices[P.slice].slice_type) || special_slice(qs->slice_type);
-            const int intra = mb_is_intra(q) || mb_is_intra(P);
-            const int pskip = qs->slice_type == H264R_SLICE_P && q.mb_type == H264R_P_SKIP;
-            const int blkQ = hor ? 4 * e + s : 4 * s + e;
-            const int blkP = hor ? (e == 0 ? 12 : 4 * (e - 1)) + s : 4 * s + (e == 0 ? 3 : e - 1);
-            const int coded = ((q.cbp_blks >> blkQ) & 1) || ((P.cbp_blks >> blkP) & 1);
-            const int same_part = e > 0 && (q.mb_type == H264R_P_16x16 ||
-                                            q.mb_type == (hor ? H264R_P_8x16 : H264R_P_16x8));
-            if (!hor) {
-                if (special) v = e == 0 ? 4 : 3;
-                else if (e > 0 && pskip) v = 0;
-                else if (e == 0 && intra) v = 4;
-                else if (intra) v = 3;
-                else if (coded) v = 2;
-                else if (same_part) v = 0;
-                else v = bs_compare(motion_of(q0, q1), motion_of(p0, p1));
-            } else {
-                if (e == 0 && (special || intra)) v = 4;
-                else if (special || intra) v = 3;
-                else if (e > 0 && pskip) v = 0;
-                else if (coded) v = 2;
-                else if (same_part) v = 0;
-                else v = bs_compare(motion_of(q0, q1), motion_of(p0, p1));
-            }
-        }
-        out->bs[lane] = (uint8_t)v;
-    } else if (lane < 32 + 9) {                        // edge parameters
-        const int k = lane - 32, pl = k / 3, which = k - pl * 3;
-        const int qyP = which == 0 ? L.qp_y : (which == 1 ? U.qp_y : q.qp_y);
-        const int qcP0 = which == 0 ? L.qp_c[0] : (which == 1 ? U.qp_c[0] : q.qp_c[0]);
-        const int qcP1 = which == 0 ? L.qp_c[1] : (which == 1 ? U.qp_c[1] : q.qp_c[1]);
-        const int qq = pl == 0 ? q.qp_y : (pl == 1 ? q.qp_c[0] : q.qp_c[1]);
-        const int qp = pl == 0 ? qyP : (pl == 1 ? qcP0 : qcP1);
-        out->par[k] = edge_word(qp, qq, qs->filter_offset_a, qs->filter_offset_b);
-    }
-}
-
 constexpr int TP = 5;     // tile pitch in dwords: left margin + 16 samples
 constexpr int TR = 20;    // tile rows: -4..15 (chroma uses -4..7)
 

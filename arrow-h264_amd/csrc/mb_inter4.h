@@ -25,7 +25,6 @@
 // the same motion vector).  A chroma 4x4 transform block is spread over the lanes
 // {blk, blk^1, blk^4, blk^5}; an 8x8 luma transform block likewise.
 #pragma once
-#include "mb_inter.h"
 #include "mb_deblock.h"
 
 namespace h264r {
@@ -47,76 +46,6 @@ DEV h264r_mb mb_lane(const h264r_mb* p)          // per-lane 32-byte record, two
 }
 
 DEV int sel16(uint32_t lo, uint32_t hi, int c) { return (int16_t)(((c & 2) ? hi : lo) >> (16 * (c & 1))); }
-
-// Two rows (y, y+1) of luma prediction samples of a 4-wide block at integer
-// position (x, y) and quarter phase (xf, yf), spec 8.4.2.2.1 / reference
-// get_block_luma.  Streams the 7 window rows y-2..y+4 once: the unrounded
-// horizontal 6-tap of each row feeds b (rows 2..4) and the centre j (all rows); the
-// vertical 6-tap h runs down column c + 2 (+1 for xf == 3, giving m).  out[i] packs
-// row i's four samples as bytes.  (A whole 4x4 block at once would share 5 of the
-// 9 window rows between its row pairs but needs twice the registers.)
-DEV void luma_rows2_pred(const uint8_t* __restrict__ img, int W, int H, int x, int y, int xf, int yf, uint32_t (&out)[2])
-{
-    const int hs = xf == 3 ? 1 : 0;                  // G/h column: c + 2 + hs
-    const int brow = yf == 3 ? 1 : 0;                // b/G row: i + 2 + brow
-    int hacc[2][4], jacc[2][4], bsv[2][4], gsv[2][4];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) hacc[i][c] = jacc[i][c] = bsv[i][c] = gsv[i][c] = 0;
-    uint32_t w[7][3];
-#pragma unroll
-    for (int r = 0; r < 7; ++r) {
-        const gdword* q = row_dwords(img, W, H, x, y - 2 + r);
-        w[r][0] = q[0]; w[r][1] = q[1]; w[r][2] = q[2];
-    }
-    constexpr int C6[6] = {1, -5, 20, 20, -5, 1};
-#pragma unroll
-    for (int r = 0; r < 7; ++r) {
-        int p[9];
-        row9(w[r][0], w[r][1], w[r][2], x, W, p);
-        int b1[4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) b1[c] = tap6(p[c], p[c + 1], p[c + 2], p[c + 3], p[c + 4], p[c + 5]);
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int k = r - i;                      // tap index of row r for output row i
-            if (k < 0 || k > 5) continue;
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                hacc[i][c] += C6[k] * (hs ? p[3 + c] : p[2 + c]);
-                jacc[i][c] += C6[k] * b1[c];
-            }
-            if (k == 2 || k == 3) {                   // b / G of output row i: row i + 2 + brow
-                const bool take = k == 2 + brow;
-#pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    bsv[i][c] = take ? b1[c] : bsv[i][c];
-                    gsv[i][c] = take ? (hs ? p[3 + c] : p[2 + c]) : gsv[i][c];
-                }
-            }
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        uint32_t o = 0;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const int G = gsv[i][c];
-            const int h = clip255((hacc[i][c] + 16) >> 5);
-            const int b = clip255((bsv[i][c] + 16) >> 5);
-            const int j = clip255((jacc[i][c] + 512) >> 10);
-            int v;
-            if (xf == 0) v = yf == 0 ? G : (yf == 2 ? h : (h + G + 1) >> 1);          // G, d, h, n
-            else if (yf == 0) v = xf == 2 ? b : (b + G + 1) >> 1;                      // a, b, c
-            else if (xf == 2) v = yf == 2 ? j : (j + b + 1) >> 1;                      // j, f, q
-            else if (yf == 2) v = (j + h + 1) >> 1;                                     // i, k
-            else v = (b + h + 1) >> 1;                                                  // e, g, p, r
-            o |= (uint32_t)v << (8 * c);
-        }
-        out[i] = o;
-    }
-}
 
 // ---------------------------------------------------------------- packed 16-bit helpers
 typedef short s16x2 __attribute__((ext_vector_type(2)));

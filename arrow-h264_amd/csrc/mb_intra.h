@@ -24,7 +24,7 @@
 //      that depends on (mode, x, y) only (intra_nxn_tap below; spec 8.3.1.2.x /
 //      8.3.2.2.x, intra_prediction.cc:189-346, 449-606).
 #pragma once
-#include "mb_inter.h"
+#include "device_common.h"
 
 namespace h264r {
 

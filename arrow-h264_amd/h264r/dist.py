@@ -41,27 +41,49 @@ def slice_bands(slice_first_rows: Sequence[int], height_mbs: int, world: int) ->
     return [(cuts[k], cuts[k + 1]) for k in range(world)]
 
 
-def allgather_rows(plane, rows_per_mb: int, bands: Sequence[tuple[int, int]], rank: int, group=None):
-    """Exchange step of slice mode: every rank holds the rows of its own band of `plane`
-    (a [H, W] tensor, filled in place); after the call every rank holds the full plane.
-    One all-gather of equal-sized (padded) bands; on ROCm with the nccl backend this is
-    RCCL over xGMI."""
+def uniform_span(bands: Sequence[tuple[int, int]]) -> int:
+    """MB rows per rank if band k starts at k * span for every rank (only the last band
+    may be shorter), else 0.  Equal slices (configs 4/5) give such bands; then the
+    concatenation of every rank's span-row chunk IS the picture, and the exchange can
+    all-gather straight into the DPB slot."""
+    span = bands[0][1] - bands[0][0]
+    if span <= 0:
+        return 0
+    for k, (b0, b1) in enumerate(bands):
+        if b0 != min(k * span, bands[-1][1]) or b1 - b0 > span:
+            return 0
+    return span
+
+
+def slot_capacity(rows: int, row_bytes: int, bands: Sequence[tuple[int, int]], rows_per_mb: int) -> int:
+    """Bytes a DPB slot plane needs so that allgather_into_slot can land every rank's
+    span-row chunk in place (a short last band still receives a full chunk)."""
+    span = uniform_span(bands) or max(b1 - b0 for b0, b1 in bands)
+    return max(rows, len(bands) * span * rows_per_mb) * row_bytes
+
+
+def allgather_into_slot(send, dst, bands: Sequence[tuple[int, int]], rank: int, rows_per_mb: int, row_bytes: int,
+                        group=None) -> None:
+    """Exchange step of slice mode, one RCCL all-gather per plane.  `send` holds this
+    rank's band of the decoded plane from offset 0 (rows of `row_bytes`; at least as many
+    rows as the widest band); `dst` is the flat DPB-slot plane in which every rank
+    receives the whole picture (sized by slot_capacity).  With uniform bands the
+    collective writes the slot directly; otherwise each band is padded to the widest one
+    and copied into place after the gather."""
     import torch
     import torch.distributed as dist
-    H, W = plane.shape
     world = len(bands)
-    span = max(b1 - b0 for b0, b1 in bands) * rows_per_mb
-    if span == 0:
-        return plane
-    send = torch.zeros((span, W), dtype=plane.dtype, device=plane.device)
-    r0, r1 = bands[rank][0] * rows_per_mb, bands[rank][1] * rows_per_mb
-    send[: r1 - r0] = plane[r0:r1]
-    recv = [torch.empty_like(send) for _ in range(world)]
-    dist.all_gather(recv, send, group=group)
+    span = uniform_span(bands)
+    if span:
+        n = span * rows_per_mb * row_bytes
+        dist.all_gather_into_tensor(dst[: world * n], send[:n], group=group)
+        return
+    wide = max(b1 - b0 for b0, b1 in bands) * rows_per_mb * row_bytes
+    recv = torch.empty(world * wide, dtype=send.dtype, device=send.device)
+    dist.all_gather_into_tensor(recv, send[:wide], group=group)
     for k, (b0, b1) in enumerate(bands):
-        a0, a1 = b0 * rows_per_mb, b1 * rows_per_mb
-        plane[a0:a1] = recv[k][: a1 - a0]
-    return plane
+        a0, a1 = b0 * rows_per_mb * row_bytes, b1 * rows_per_mb * row_bytes
+        dst[a0:a1] = recv[k * wide: k * wide + (a1 - a0)]
 
 
 def max_over_ranks(seconds: float, device=None) -> float:

@@ -217,7 +217,15 @@ int  h264r_picture_end(h264r_ctx* ctx, uint8_t* y, uint8_t* u, uint8_t* v,
 
 /* ---- batch API (bench / throughput mode): arrays already on the device ---------- */
 /* Launches recon + deblock for every picture of the batch on `stream`
- * (a hipStream_t, NULL = the context's stream).  Asynchronous. */
+ * (a hipStream_t, NULL = the context's stream, a blocking stream: ordered with the
+ * legacy NULL stream).  Asynchronous.
+ * Threading / residency contract: a context is driven by one host thread; its scratch
+ * is reused by every launch, so a launch on a different stream than the previous one
+ * first waits for the previous one (an event, inserted by the library).  The intra
+ * kernel k_intra_levels is persistent and separates dependency levels with a grid
+ * barrier sized from the occupancy query: kernels of OTHER contexts or libraries
+ * running concurrently on the same device may delay it (every wait is bounded; an
+ * expired wait is reported by h264r_check as H264R_EDEVICE, never silently). */
 int  h264r_decode_batch(h264r_ctx* ctx, const h264r_batch* batch, void* stream);
 
 /* Slice-sharded form of h264r_decode_batch (multi-GPU): reconstruct and
@@ -247,11 +255,6 @@ int  h264r_set_timing(h264r_ctx* ctx, int enable);
 /* H264R_DBG_INTRA_WALK reconstructs every intra MB with the wavefront walk instead of
  * the dependency-level schedule (both are bit-exact; this exercises the walk alone). */
 #define H264R_DBG_INTRA_WALK 2
-/* Alternative kernels, bit-exact, for tests and measurements: H264R_DBG_DEBLOCK4 the
- * four-rows-per-wave packed deblocking walk, H264R_DBG_INTER1 the wave-per-MB inter
- * kernel (k_inter + k_dbinfo). */
-#define H264R_DBG_DEBLOCK4   4
-#define H264R_DBG_INTER1     8
 int  h264r_set_debug(h264r_ctx* ctx, int flags);
 /* Wait for the context's work and report a device-side failure (a wavefront wait
  * that timed out): H264R_OK or H264R_EDEVICE. */

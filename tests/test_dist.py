@@ -43,23 +43,39 @@ def test_slice_bands(starts, H, world, want):
         assert [b1 - b0 for b0, b1 in bands] == [17, 17, 17, 17, 17, 17, 16, 17]
 
 
+@pytest.mark.parametrize("bands,span", [([(0, 17), (17, 34), (34, 51), (51, 68)], 17),
+                                        ([(0, 34), (34, 67)], 34), ([(0, 34), (34, 68)], 34),
+                                        ([(0, 17), (17, 35)], 0), ([(0, 20), (20, 34)], 20), ([(0, 10), (10, 30)], 0),
+                                        ([(0, 68), (68, 68)], 68)])
+def test_uniform_span(bands, span):
+    assert D.uniform_span(bands) == span
+
+
 def _worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        H, W = 6, 5                        # MB rows / MB cols of a toy picture
-        bands = D.slice_bands([0, 2, 3, 5], H, world)
-        plane = torch.zeros((H * 16, W * 16), dtype=torch.uint8)
-        r0, r1 = bands[rank]
-        plane[r0 * 16:r1 * 16] = 10 + rank            # this rank's decoded band
-        D.allgather_rows(plane, 16, bands, rank)
-        want = torch.zeros_like(plane)
-        for k, (b0, b1) in enumerate(bands):
-            want[b0 * 16:b1 * 16] = 10 + k
-        ok_rows = bool(torch.equal(plane, want))
+        W = 5                              # MB columns of a toy picture
+        # the in-place exchange into a DPB slot: uniform bands (one chunk per rank lands
+        # straight in the slot) and non-uniform ones (padded + copied)
+        ok_slot = []
+        for starts, Hs in (([0, 3], 5), ([0, 2, 3, 5], 6), ([0, 4], 7)):
+            bands2 = D.slice_bands(starts, Hs, world)
+            Wb = W * 16
+            src = torch.zeros(Hs * 16 * Wb, dtype=torch.uint8)
+            a0, a1 = bands2[rank]
+            for y in range(a0 * 16, a1 * 16):
+                src[y * Wb:(y + 1) * Wb] = (y * 7 + 1) % 251
+            cap = D.slot_capacity(Hs * 16, Wb, bands2, 16) + 64
+            dst = torch.full((cap,), 0xEE, dtype=torch.uint8)
+            send = torch.zeros(max(b1 - b0 for b0, b1 in bands2) * 16 * Wb, dtype=torch.uint8)
+            send[: (a1 - a0) * 16 * Wb] = src[a0 * 16 * Wb: a1 * 16 * Wb]
+            D.allgather_into_slot(send, dst, bands2, rank, 16, Wb)
+            exp = torch.tensor([(y * 7 + 1) % 251 for y in range(Hs * 16)], dtype=torch.uint8).repeat_interleave(Wb)
+            ok_slot.append(bool(torch.equal(dst[: Hs * 16 * Wb], exp)) and bool((dst[-64:] == 0xEE).all()))
         t = D.max_over_ranks(1.0 + rank)
         share = list(D.picture_share(rank, world, 3))
-        q.put((rank, ok_rows, t, share))
+        q.put((rank, all(ok_slot), t, share))
     finally:
         dist.destroy_process_group()
 

@@ -116,14 +116,6 @@ def test_gpu_batch_1080p_p_intra_walk(L, dec):
     _batch_vs_oracle(L, dec, 3, 120, 68, 2, debug=A.DBG_INTRA_WALK)
 
 
-@pytest.mark.parametrize("flag", ["DBG_DEBLOCK4", "DBG_INTER1"])
-@pytest.mark.parametrize("cidx,W,H,n,over", [(3, 120, 68, 2, {}), (4, 40, 30, 2, dict(wp_mode=1, num_slices=3)),
-                                             (2, 22, 18, 2, dict(deblock_idc=0)), (5, 33, 21, 1, dict(pcm_permille=30))])
-def test_gpu_alternative_kernels(L, dec, flag, cidx, W, H, n, over):
-    """The alternative (non-default) kernels are bit-exact too."""
-    _batch_vs_oracle(L, dec, cidx, W, H, n, debug=getattr(A, flag), **over)
-
-
 def test_gpu_batch_dense_intra_levels(L, dec):
     """P pictures with 60 % intra MBs: chains far deeper than the level launches, so
     the level schedule and the walk both take part in one picture."""
