@@ -144,7 +144,7 @@ def latency_chain(dec, L, cfg, refs, stream, n: int, verify: int):
         if src is None:
             return [torch.zeros(n_ + slack, dtype=torch.uint8, device="cuda") for n_ in sizes]
         return [torch.from_numpy(np.concatenate([a.reshape(-1), np.zeros(slack, np.uint8)])).to("cuda") for a in src]
-    bufs = [planes_t(refs[0])] + [planes_t() for _ in range(n)]
+    bufs = [planes_t(refs[0]) if refs else planes_t()] + [planes_t() for _ in range(n)]
     slot1 = [planes_t(r) for r in refs[1:]]
     pics = [synth.picture(L, cfg, 50_000 + i) for i in range(n)]
     keep, batches = [], []
@@ -175,7 +175,7 @@ def latency_chain(dec, L, cfg, refs, stream, n: int, verify: int):
             want = O.decode(pics[i], oref)
             got = [bufs[i + 1][k][: sizes[k]].cpu().numpy() for k in range(3)]
             verified &= all(np.array_equal(got[k], want[k].reshape(-1)) for k in range(3))
-            oref = [want] + oref[1:]
+            oref = [want] + oref[1:] if refs else []
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     chain()
@@ -276,7 +276,9 @@ def main() -> int:
             t[: a.size].copy_(torch.from_numpy(np.ascontiguousarray(a).reshape(-1)))
             out.append(t)
         return out
-    if shard == "slices":
+    if not refs:                                   # all-intra (config 2): no reference picture
+        ring = [[]]
+    elif shard == "slices":
         caps = [D.slot_capacity(plane_rows[k], row_bytes[k], bands, (16, 8, 8)[k]) for k in range(3)]
         ring = [slot_planes(refs[0], caps) for _ in range(3)]
     else:
@@ -285,7 +287,7 @@ def main() -> int:
     tabs = []
     for e in ring:
         tab = np.zeros(3 * 32, np.int64)
-        for s_, planes in enumerate([e] + others):
+        for s_, planes in enumerate(([e] if e else []) + others):
             for k in range(3):
                 tab[3 * s_ + k] = planes[k].data_ptr()
         tabs.append(torch.from_numpy(tab).to("cuda"))
