@@ -1,0 +1,629 @@
+"""h264_writer -- the repo's own tiny H.264 bitstream writer (TEST INFRASTRUCTURE).
+
+SURVEY.md 8(c) item 2: the conformance streams the reference's harness decodes are not
+in the container, so stream-level parity is pinned on streams this module generates.
+It writes Annex-B byte streams (CAVLC only) that exercise the reconstruction path:
+
+* SPS (Baseline 66 or High 100 with CAVLC), PPS, IDR + P pictures, several slices per
+  picture, per-slice deblocking control (disable_deblocking_filter_idc 0/1/2, alpha/beta
+  offsets), chroma_qp_index_offset, constrained_intra_pred, frame cropping, multiple
+  reference frames, explicit weighted prediction;
+* macroblocks I_PCM, I_16x16 (4 modes, every CBP), I_4x4 (9 modes, predicted-mode
+  coding), I_8x8 (High: transform_size_8x8_flag), P_L0_16x16 / 16x8 / 8x16 / 8x8 (all
+  sub-partitions) and P_8x8ref0, P_Skip runs, intra MBs in P slices, mb_qp_delta;
+* CAVLC residuals (coeff_token / levels with suffix-length adaptation and escapes /
+  total_zeros / run_before) for luma DC/AC/4x4/8x8 (interleaved) and chroma DC/AC, with
+  the decoder's nC prediction from neighbouring blocks.
+
+The encoder never needs the reconstruction: motion vector differences and QP deltas are
+drawn at random and the decoder derives the rest.  Intra modes are drawn only among
+those the neighbour availability allows (the reference asserts otherwise,
+intra_prediction.cc:191-873), and the predicted intra mode is derived exactly as the
+decoder does (neighbour.cc:318-360) so the chosen mode is what gets decoded.
+
+The VLC tables come from tests/golden/cavlc_tables.json, probed from the reference's
+own readers (oracle/probe_cavlc.cc).  Syntax follows the reference parser:
+slice header interpret_rbsp.cc:625-765, MB layer interpret_mb.cc:180-316 and 506-744,
+residual interpret_residual.cc:64-174 and 421-494.
+"""
+from __future__ import annotations
+
+import json
+import os
+import random
+from dataclasses import dataclass, field
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+_T = json.load(open(os.path.join(HERE, "golden", "cavlc_tables.json")))
+
+COEFF_TOKEN = {int(nc): {(tc, t1): (ln, code) for tc, t1, ln, code in ent} for nc, ent in _T["coeff_token"].items()}
+TOTAL_ZEROS = {int(y): {int(t): {v: (ln, code) for v, ln, code in ent} for t, ent in d.items()}
+               for y, d in _T["total_zeros"].items()}
+RUN_BEFORE = {int(z): {v: (ln, code) for v, ln, code in ent} for z, ent in _T["run_before"].items()}
+CBP_CODE = {k: {cbp: code for code, cbp in enumerate(v)} for k, v in _T["cbp_me"].items()}
+
+# 4x4 / 8x8 frame zig-zag scans: raster index of scan position k (spec Tables 8-12/8-13)
+def _zigzag(n):
+    out = []
+    for s in range(2 * n - 1):
+        cells = [(s - x, x) for x in range(n) if 0 <= s - x < n]    # (y, x) along the anti-diagonal
+        cells = sorted(cells, key=lambda c: c[1]) if s % 2 else sorted(cells, key=lambda c: -c[1])
+        out += [y * n + x for y, x in cells]
+    return out
+
+
+ZZ4 = _zigzag(4)
+ZZ8 = _zigzag(8)
+
+SKIP, INTER, I4, I8, I16, PCM = range(6)
+
+
+class BitWriter:
+    def __init__(self):
+        self.bits: list[int] = []
+
+    def u(self, n: int, v: int) -> None:
+        for k in range(n - 1, -1, -1):
+            self.bits.append((v >> k) & 1)
+
+    def ue(self, v: int) -> None:
+        v += 1
+        nb = v.bit_length() - 1
+        self.u(nb, 0)
+        self.u(nb + 1, v)
+
+    def se(self, v: int) -> None:
+        self.ue(2 * v - 1 if v > 0 else -2 * v)
+
+    def code(self, lc) -> None:
+        self.u(lc[0], lc[1])
+
+    def aligned(self) -> bool:
+        return len(self.bits) % 8 == 0
+
+    def trailing(self) -> None:
+        self.bits.append(1)
+        while len(self.bits) % 8:
+            self.bits.append(0)
+
+    def bytes(self) -> bytes:
+        assert len(self.bits) % 8 == 0
+        return bytes(int("".join(map(str, self.bits[i:i + 8])), 2) for i in range(0, len(self.bits), 8))
+
+
+def nal_unit(ref_idc: int, typ: int, rbsp: bytes) -> bytes:
+    """Annex-B NAL unit: start code, header, emulation-prevention bytes (7.4.1)."""
+    out = bytearray([0, 0, 0, 1, (ref_idc << 5) | typ])
+    zeros = 0
+    for b in rbsp:
+        if zeros >= 2 and b <= 3:
+            out.append(3)
+            zeros = 0
+        out.append(b)
+        zeros = zeros + 1 if b == 0 else 0
+    return bytes(out)
+
+
+@dataclass
+class StreamCfg:
+    width_mbs: int = 11
+    height_mbs: int = 9
+    frames: int = 4
+    seed: int = 1
+    profile: int = 66                # 66 Baseline, 100 High (CAVLC)
+    num_refs: int = 1                # max_num_ref_frames
+    slices: int = 1                  # slices per picture (random first_mb_in_slice)
+    qp: tuple = (18, 38)
+    chroma_qp_offset: int = 0
+    second_chroma_qp_offset: int | None = None
+    cip: int = 0                     # constrained_intra_pred_flag
+    deblock: tuple = (0,)            # disable_deblocking_filter_idc choices per slice
+    offsets: int = 0                 # max |alpha/beta offset_div2|
+    crop: tuple = (0, 0, 0, 0)       # left, right, top, bottom (luma samples / 2)
+    weighted: int = 0                # weighted_pred_flag (explicit WP in P slices)
+    transform8x8: int = 0            # High: transform_8x8_mode_flag
+    pcm: float = 0.02
+    skip: float = 0.15
+    intra_in_p: float = 0.10
+    level_max: int = 6               # typical |level|; escapes drawn now and then
+    all_intra: bool = False          # every picture an IDR / I picture
+    mv_range: int = 24               # |mvd| bound (quarter samples)
+    scaling: int = 0                 # High: 1 SPS scaling matrix, 2 PPS matrix, 3 both
+
+
+@dataclass
+class _Mb:
+    kind: int = SKIP
+    slice: int = -1
+    intra: bool = False
+    i4: list = field(default_factory=lambda: [2] * 16)   # Intra4x4PredMode, blkIdx order
+    i8: list = field(default_factory=lambda: [2] * 4)
+    t8: bool = False
+    nz: list = field(default_factory=lambda: [[[0] * 4 for _ in range(4)] for _ in range(3)])
+
+
+def _blk_xy(blk: int):
+    """(x, y) in 4x4 units of luma4x4BlkIdx (6.4.3)."""
+    return ((blk // 4) % 2) * 2 + (blk % 4) % 2, ((blk // 4) // 2) * 2 + (blk % 4) // 2
+
+
+class Encoder:
+    def __init__(self, cfg: StreamCfg):
+        self.c = cfg
+        self.rng = random.Random(cfg.seed)
+        self.W, self.H = cfg.width_mbs, cfg.height_mbs
+        self.log2_max_frame_num = 4
+
+    # ------------------------------------------------------------------ parameter sets
+    def sps(self) -> bytes:
+        c, w = self.c, BitWriter()
+        w.u(8, c.profile)
+        w.u(8, 0)                                   # constraint flags
+        w.u(8, 51)                                  # level_idc (largest DPB)
+        w.ue(0)                                     # seq_parameter_set_id
+        if c.profile == 100:
+            w.ue(1)                                 # chroma_format_idc 4:2:0
+            w.ue(0); w.ue(0)                        # bit depths 8
+            w.u(1, 0)                               # qpprime_y_zero_transform_bypass_flag
+            w.u(1, c.scaling & 1)                   # seq_scaling_matrix_present_flag
+            if c.scaling & 1:
+                self._scaling_matrix(w, 8)
+        w.ue(self.log2_max_frame_num - 4)
+        w.ue(2)                                     # pic_order_cnt_type 2 (output = decode order)
+        w.ue(c.num_refs)                            # max_num_ref_frames
+        w.u(1, 0)                                   # gaps_in_frame_num_value_allowed_flag
+        w.ue(self.W - 1)
+        w.ue(self.H - 1)
+        w.u(1, 1)                                   # frame_mbs_only_flag
+        w.u(1, 1)                                   # direct_8x8_inference_flag
+        crop = any(c.crop)
+        w.u(1, 1 if crop else 0)
+        if crop:
+            for v in c.crop:
+                w.ue(v)
+        w.u(1, 0)                                   # vui_parameters_present_flag
+        w.trailing()
+        return nal_unit(3, 7, w.bytes())
+
+    def pps(self) -> bytes:
+        c, w = self.c, BitWriter()
+        w.ue(0); w.ue(0)
+        w.u(1, 0)                                   # entropy_coding_mode_flag: CAVLC
+        w.u(1, 0)                                   # bottom_field_pic_order_in_frame_present_flag
+        w.ue(0)                                     # num_slice_groups_minus1
+        w.ue(0); w.ue(0)                            # num_ref_idx_l0/l1_default_active_minus1
+        w.u(1, c.weighted)                          # weighted_pred_flag
+        w.u(2, 0)                                   # weighted_bipred_idc
+        w.se(0); w.se(0)                            # pic_init_qp/qs_minus26
+        w.se(c.chroma_qp_offset)
+        w.u(1, 1)                                   # deblocking_filter_control_present_flag
+        w.u(1, c.cip)
+        w.u(1, 0)                                   # redundant_pic_cnt_present_flag
+        if c.profile == 100:
+            w.u(1, c.transform8x8)
+            w.u(1, 1 if c.scaling & 2 else 0)       # pic_scaling_matrix_present_flag
+            if c.scaling & 2:
+                self._scaling_matrix(w, 6 + 2 * c.transform8x8)
+            w.se(c.chroma_qp_offset if c.second_chroma_qp_offset is None else c.second_chroma_qp_offset)
+        w.trailing()
+        return nal_unit(3, 8, w.bytes())
+
+    def _scaling_matrix(self, w: BitWriter, n: int) -> None:
+        """scaling_list_present_flag + scaling_list() for n lists (7.3.2.1.1.1): absent
+        (fall-back rules), "use default" (first delta makes nextScale 0), explicit values
+        in zig-zag order, or explicit values cut short (nextScale 0 repeats the last)."""
+        r = self.rng
+        for i in range(n):
+            kind = r.choice(["absent", "default", "explicit", "short"])
+            w.u(1, 0 if kind == "absent" else 1)
+            if kind == "absent":
+                continue
+            size = 16 if i < 6 else 64
+            if kind == "default":
+                w.se(-8)                            # nextScale = (8 - 8) % 256 = 0 at j = 0
+                continue
+            last = 8
+            stop = r.randint(1, size - 1) if kind == "short" else size
+            for j in range(size):
+                if j == stop:
+                    w.se((0 - last + 128) % 256 - 128)   # nextScale 0: the rest repeats `last`
+                    break
+                v = r.randint(4, 64)
+                w.se((v - last + 128) % 256 - 128)
+                last = v
+
+    # ------------------------------------------------------------------ availability
+    def _mb_at(self, x: int, y: int, cur_slice: int):
+        if x < 0 or y < 0 or x >= self.W or y >= self.H:
+            return None
+        m = self.mbs[y * self.W + x]
+        return m if m.slice == cur_slice else None
+
+    def _intra_avail(self, x, y, s):
+        """Availability for intra prediction (same slice, constrained_intra_pred)."""
+        m = self._mb_at(x, y, s)
+        if m is None or (self.c.cip and not m.intra):
+            return None
+        return m
+
+    # ------------------------------------------------------------------ CAVLC residual
+    def _nc(self, a: int, pl: int, bx: int, by: int, s: int) -> int:
+        """nC of the block at (bx, by) (4x4 units, plane pl), neighbour.cc:263-314."""
+        mx, my = a % self.W, a // self.W
+        n = 4 if pl == 0 else 2
+        def nz_of(dx, dy):
+            x, y = bx + dx, by + dy
+            ox, oy = mx + (x // n if x >= 0 else -1), my + (y // n if y >= 0 else -1)
+            if x >= 0 and y >= 0:
+                return self.mbs[a].nz[pl][y][x]
+            m = self._mb_at(ox, oy, s)
+            if m is None:
+                return None
+            return m.nz[pl][y % n][x % n]
+        na, nb = nz_of(-1, 0), nz_of(0, -1)
+        if na is not None and nb is not None:
+            return (na + nb + 1) >> 1
+        return (na or 0) + (nb or 0)
+
+    def _levels(self, n: int):
+        """Random coefficient levels of one block (scan order, n coefficients)."""
+        r = self.rng
+        tc = min(n, int(r.expovariate(0.35))) if r.random() < 0.8 else r.randint(0, n)
+        pos = sorted(r.sample(range(n), tc))
+        out = [0] * n
+        for p in pos:
+            if r.random() < 0.03:
+                v = r.randint(self.c.level_max, 60)
+            else:
+                v = 1 if r.random() < 0.55 else min(self.c.level_max, 1 + int(r.expovariate(0.6)))
+            out[p] = v if r.random() < 0.5 else -v
+        return out
+
+    def _block(self, w: BitWriter, coeffs: list, nc: int, max_num: int) -> int:
+        """residual_block_cavlc (9.2, interpret_residual.cc:64-174) of coefficients in
+        scan order; returns TotalCoeff."""
+        nzp = [k for k, v in enumerate(coeffs) if v]
+        tc = len(nzp)
+        lv = [coeffs[k] for k in nzp]                   # levelVal[0..tc-1], low to high frequency
+        t1 = 0
+        for v in reversed(lv):
+            if abs(v) == 1 and t1 < 3:
+                t1 += 1
+            else:
+                break
+        if nc >= 8:
+            w.u(6, 3 if tc == 0 else ((tc - 1) << 2) | t1)
+        else:
+            cls = -1 if nc == -1 else (-2 if nc == -2 else (0 if nc < 2 else (2 if nc < 4 else 4)))
+            w.code(COEFF_TOKEN[cls][(tc, t1)])
+        if tc == 0:
+            return 0
+        for k in range(tc - 1, tc - 1 - t1, -1):
+            w.u(1, 1 if lv[k] < 0 else 0)
+        suffix_len = 1 if tc > 10 and t1 < 3 else 0
+        for k in range(tc - 1 - t1, -1, -1):
+            v = lv[k]
+            code = 2 * v - 2 if v > 0 else -2 * v - 1
+            if k == tc - 1 - t1 and t1 < 3:
+                code -= 2
+            if suffix_len == 0:
+                if code < 14:
+                    w.u(code, 0); w.u(1, 1)
+                elif code < 30:
+                    w.u(14, 0); w.u(1, 1); w.u(4, code - 14)
+                else:
+                    assert code - 30 < 4096
+                    w.u(15, 0); w.u(1, 1); w.u(12, code - 30)
+            else:
+                if code < (15 << suffix_len):
+                    w.u(code >> suffix_len, 0); w.u(1, 1); w.u(suffix_len, code & ((1 << suffix_len) - 1))
+                else:
+                    assert code - (15 << suffix_len) < 4096
+                    w.u(15, 0); w.u(1, 1); w.u(12, code - (15 << suffix_len))
+            if suffix_len == 0:
+                suffix_len = 1
+            if abs(v) > (3 << (suffix_len - 1)) and suffix_len < 6:
+                suffix_len += 1
+        total_zeros = nzp[-1] + 1 - tc
+        if tc < max_num:
+            yuv = 0 if max_num == 4 else (1 if max_num == 8 else 2)
+            w.code(TOTAL_ZEROS[yuv][tc][total_zeros])
+        zl = total_zeros
+        for k in range(tc - 1, 0, -1):
+            if zl <= 0:
+                break
+            run = nzp[k] - nzp[k - 1] - 1
+            w.code(RUN_BEFORE[min(zl, 7)][run])
+            zl -= run
+        return tc
+
+    def _residual(self, w: BitWriter, a: int, m: _Mb, cbp: int, s: int) -> None:
+        """residual_luma + residual_chroma (interpret_residual.cc:421-494)."""
+        cbpl, cbpc = cbp & 15, cbp >> 4
+        if m.kind == I16:
+            self._block(w, self._levels(16), self._nc(a, 0, 0, 0, s), 16)
+        for b8 in range(4):
+            if m.t8 and (cbpl >> b8) & 1:
+                l8 = self._levels(64)
+                for b4 in range(4):
+                    bx, by = _blk_xy(b8 * 4 + b4)
+                    m.nz[0][by][bx] = self._block(w, [l8[4 * k + b4] for k in range(16)], self._nc(a, 0, bx, by, s), 16)
+                continue
+            for b4 in range(4):
+                bx, by = _blk_xy(b8 * 4 + b4)
+                if (cbpl >> b8) & 1:
+                    if m.kind == I16:
+                        m.nz[0][by][bx] = self._block(w, self._levels(15), self._nc(a, 0, bx, by, s), 15)
+                    else:
+                        m.nz[0][by][bx] = self._block(w, self._levels(16), self._nc(a, 0, bx, by, s), 16)
+                else:
+                    m.nz[0][by][bx] = 0
+        if cbpc & 3:
+            for _pl in (1, 2):
+                self._block(w, self._levels(4), -1, 4)
+        for pl in (1, 2):
+            for b in range(4):
+                bx, by = b % 2, b // 2
+                if cbpc & 2:
+                    m.nz[pl][by][bx] = self._block(w, self._levels(15), self._nc(a, pl, bx, by, s), 15)
+                else:
+                    m.nz[pl][by][bx] = 0
+
+    # ------------------------------------------------------------------ intra modes
+    def _pred_mode(self, a: int, m: _Mb, bx: int, by: int, s: int, n8: bool) -> int:
+        """predIntra4x4PredMode / predIntra8x8PredMode (neighbour.cc:318-400)."""
+        mx, my = a % self.W, a // self.W
+        def mode_of(dx, dy):
+            x, y = bx + dx, by + dy
+            if x >= 0 and y >= 0:
+                nb, lx, ly = m, x, y
+            else:
+                nb = self._intra_avail(mx + (-1 if x < 0 else 0), my + (-1 if y < 0 else 0), s)
+                if nb is None:
+                    return None
+                lx, ly = x % 4, y % 4
+            if nb.kind == I8:
+                return nb.i8[(ly // 2) * 2 + lx // 2]
+            if nb.kind == I4:
+                blk = (ly // 2) * 8 + (lx // 2) * 4 + (ly % 2) * 2 + lx % 2
+                return nb.i4[blk]
+            return 2
+        # the 4x4 blocks left of / above the block's top-left 4x4 (also for 8x8 blocks:
+        # the reference looks at samples (x-1, y) and (x, y-1), neighbour.cc:367-391)
+        ma, mb_ = mode_of(-1, 0), mode_of(0, -1)
+        if ma is None or mb_ is None:
+            return 2
+        return min(ma, mb_)
+
+    def _avail_abd(self, a: int, bx: int, by: int, n: int, s: int):
+        """Availability of neighbours A, B, D of an n-wide block at (bx, by) (4x4 units)."""
+        mx, my = a % self.W, a // self.W
+        av = lambda dx, dy: self._intra_avail(mx + dx, my + dy, s) is not None
+        A = bx > 0 or av(-1, 0)
+        B = by > 0 or av(0, -1)
+        if bx > 0 and by > 0:
+            D = True
+        elif bx == 0 and by > 0:
+            D = av(-1, 0)
+        elif bx > 0 and by == 0:
+            D = av(0, -1)
+        else:
+            D = av(-1, -1)
+        return A, B, D
+
+    @staticmethod
+    def _valid_nxn(A, B, D):
+        need = {0: "B", 1: "A", 2: "", 3: "B", 4: "ABD", 5: "ABD", 6: "ABD", 7: "B", 8: "A"}
+        have = {"A": A, "B": B, "D": D}
+        return [md for md, req in need.items() if all(have[ch] for ch in req)]
+
+    # ------------------------------------------------------------------ one macroblock
+    def _mb(self, w: BitWriter, a: int, ptype: str, s: int, nref: int):
+        c, r = self.c, self.rng
+        m = self.mbs[a]
+        m.slice = s
+        roll = r.random()
+        if ptype == "P" and roll < c.skip:
+            m.kind, m.intra = SKIP, False
+            m.nz = [[[0] * 4 for _ in range(4)] for _ in range(3)]
+            return False
+        intra = ptype == "I" or r.random() < c.intra_in_p
+        base = 5 if ptype == "P" else 0
+        if intra:
+            m.intra = True
+            k = r.random()
+            if k < c.pcm:
+                m.kind = PCM
+            elif k < 0.4:
+                m.kind = I16
+            elif c.transform8x8 and k < 0.7:
+                m.kind = I8
+            else:
+                m.kind = I4
+        else:
+            m.intra = False
+            m.kind = INTER
+        mx, my = a % self.W, a // self.W
+        A, B, D = self._avail_abd(a, 0, 0, 4, s)
+        if m.kind == PCM:
+            w.ue(base + 25)
+            while not w.aligned():
+                w.u(1, 0)
+            for _ in range(384):
+                w.u(8, r.randint(1, 255))
+            m.nz = [[[16] * 4 for _ in range(4)] for _ in range(3)]
+            return True
+        cmodes = [0] + ([1] if A else []) + ([2] if B else []) + ([3] if A and B and D else [])
+        if m.kind == I16:
+            modes = ([0] if B else []) + ([1] if A else []) + [2] + ([3] if A and B and D else [])
+            mode = r.choice(modes)
+            cbpc = r.randint(0, 2)
+            cbpl = 15 if r.random() < 0.5 else 0
+            w.ue(base + 1 + mode + 4 * cbpc + (12 if cbpl else 0))
+            w.ue(r.choice(cmodes))
+            cbp = cbpl | cbpc << 4
+        elif m.kind in (I4, I8):
+            w.ue(base + 0)
+            m.t8 = m.kind == I8
+            if c.transform8x8:
+                w.u(1, 1 if m.t8 else 0)
+            if m.kind == I4:
+                for blk in range(16):
+                    bx, by = _blk_xy(blk)
+                    mode = r.choice(self._valid_nxn(*self._avail_abd(a, bx, by, 1, s)))
+                    pred = self._pred_mode(a, m, bx, by, s, False)
+                    m.i4[blk] = mode
+                    if mode == pred:
+                        w.u(1, 1)
+                    else:
+                        w.u(1, 0); w.u(3, mode if mode < pred else mode - 1)
+            else:
+                for b8 in range(4):
+                    bx, by = (b8 % 2) * 2, (b8 // 2) * 2
+                    mode = r.choice(self._valid_nxn(*self._avail_abd(a, bx, by, 2, s)))
+                    pred = self._pred_mode(a, m, bx, by, s, True)
+                    m.i8[b8] = mode
+                    if mode == pred:
+                        w.u(1, 1)
+                    else:
+                        w.u(1, 0); w.u(3, mode if mode < pred else mode - 1)
+            w.ue(r.choice(cmodes))
+            cbp = r.randint(0, 47)
+            w.ue(CBP_CODE["intra"][cbp])
+        else:
+            mbt = r.choices([0, 1, 2, 3, 4], weights=[45, 12, 12, 21, 10])[0]
+            w.ue(mbt)
+            def ref_idx():
+                v = r.randrange(nref)
+                if nref == 2:
+                    w.u(1, 1 - v)
+                elif nref > 2:
+                    w.ue(v)
+            def mvd():
+                w.se(r.randint(-c.mv_range, c.mv_range)); w.se(r.randint(-c.mv_range, c.mv_range))
+            small = False
+            if mbt in (0, 1, 2):
+                for _ in range(1 if mbt == 0 else 2):
+                    ref_idx()
+                for _ in range(1 if mbt == 0 else 2):
+                    mvd()
+            else:
+                subs = [r.choice([0, 0, 1, 2, 3]) for _ in range(4)]
+                small = any(sb != 0 for sb in subs)
+                for sb in subs:
+                    w.ue(sb)
+                if mbt == 3:
+                    for _ in range(4):
+                        ref_idx()
+                for sb in subs:
+                    for _ in range({0: 1, 1: 2, 2: 2, 3: 4}[sb]):
+                        mvd()
+            cbp = r.randint(0, 47)
+            w.ue(CBP_CODE["inter"][cbp])
+            m.t8 = False
+            if (cbp & 15) and c.transform8x8 and not small:
+                m.t8 = r.random() < 0.5
+                w.u(1, 1 if m.t8 else 0)
+        if cbp or m.kind == I16:
+            lo, hi = c.qp
+            target = r.randint(lo, hi)
+            d = (target - self.qp_pred + 26) % 52 - 26
+            w.se(d)
+            self.qp_pred = (self.qp_pred + d + 52) % 52
+        self._residual(w, a, m, cbp, s)
+        return True
+
+    # ------------------------------------------------------------------ pictures
+    def picture(self, idx: int, idr: bool):
+        """NAL units of picture idx: one per slice."""
+        c, r = self.c, self.rng
+        n = self.W * self.H
+        self.mbs = [_Mb() for _ in range(n)]
+        ptype = "I" if idr else "P"
+        starts = sorted({0} | set(r.sample(range(1, n), min(c.slices - 1, n - 1)))) if c.slices > 1 else [0]
+        frame_num = 0 if idr else (self.frame_num + 1) % (1 << self.log2_max_frame_num)
+        self.frame_num = frame_num
+        self.refs = 0 if idr else min(self.refs + 1, c.num_refs)
+        out = []
+        for s, first in enumerate(starts):
+            end = starts[s + 1] if s + 1 < len(starts) else n
+            w = BitWriter()
+            w.ue(first)
+            w.ue(7 if ptype == "I" else 5)          # slice_type (all slices of the picture alike)
+            w.ue(0)                                 # pic_parameter_set_id
+            w.u(self.log2_max_frame_num, frame_num)
+            if idr:
+                w.ue(idx % 2)                       # idr_pic_id
+            nref = self.refs
+            if ptype == "P":
+                w.u(1, 1)                           # num_ref_idx_active_override_flag
+                w.ue(nref - 1)
+                w.u(1, 0)                           # ref_pic_list_modification_flag_l0
+                if c.weighted:
+                    ld, cd = r.randint(0, 7), r.randint(0, 7)
+                    w.ue(ld); w.ue(cd)
+                    for _ in range(nref):
+                        if r.random() < 0.7:
+                            w.u(1, 1); w.se(r.randint(-min(64, 1 << ld), min(127, 2 << ld))); w.se(r.randint(-20, 20))
+                        else:
+                            w.u(1, 0)
+                        if r.random() < 0.7:
+                            w.u(1, 1)
+                            for _ in range(2):
+                                w.se(r.randint(-min(64, 1 << cd), min(127, 2 << cd))); w.se(r.randint(-20, 20))
+                        else:
+                            w.u(1, 0)
+            if idr:
+                w.u(1, 0); w.u(1, 0)                # no_output_of_prior_pics_flag, long_term_reference_flag
+            else:
+                w.u(1, 0)                           # adaptive_ref_pic_marking_mode_flag
+            lo, hi = c.qp
+            sqp = r.randint(lo, hi)
+            w.se(sqp - 26)
+            self.qp_pred = sqp
+            idc = r.choice(c.deblock)
+            w.ue(idc)
+            if idc != 1:
+                w.se(r.randint(-c.offsets, c.offsets)); w.se(r.randint(-c.offsets, c.offsets))
+            skip_run = 0
+            for a in range(first, end):
+                coded = self._mb(w if ptype == "I" else _Deferred(w, skip_run), a, ptype, s, nref)
+                if ptype == "P":
+                    skip_run = 0 if coded else skip_run + 1
+            if ptype == "P" and skip_run:
+                w.ue(skip_run)
+            w.trailing()
+            out.append(nal_unit(3, 5 if idr else 1, w.bytes()))
+        return out
+
+    def stream(self) -> bytes:
+        c = self.c
+        out = [self.sps(), self.pps()]
+        self.frame_num, self.refs = 0, 0
+        for i in range(c.frames):
+            out += self.picture(i, idr=(i == 0 or c.all_intra))
+        return b"".join(out)
+
+
+class _Deferred:
+    """Writes mb_skip_run (ue) just before the first syntax element of a coded MB in a P
+    slice; a skipped MB writes nothing."""
+
+    def __init__(self, w: BitWriter, run: int):
+        self.w, self.run, self.done = w, run, False
+
+    def _flush(self):
+        if not self.done:
+            self.w.ue(self.run)
+            self.done = True
+
+    def __getattr__(self, name):
+        self._flush()
+        return getattr(self.w, name)
+
+
+def write_stream(path: str, cfg: StreamCfg) -> bytes:
+    data = Encoder(cfg).stream()
+    with open(path, "wb") as f:
+        f.write(data)
+    return data

@@ -1,0 +1,158 @@
+"""Stream-level parity fixtures (TEST INFRASTRUCTURE).
+
+SURVEY.md 8(c) items 2-3 and 8(f) rank 1.  A fixed set of H.264 streams written by the
+repo's own bitstream writer (tests/h264_writer.py) is committed under
+tests/golden/streams/, together with, per stream:
+
+* the reference's per-frame MD5s of its decoded YUV: the unmodified reference decoder
+  (oracle/_ref/ldecod, built from /root/reference) run in this container, digested with
+  the reference harness's protocol (script/test/model/__init__.py:119-183,
+  h264r.output.digest_by_frames);
+* the MB records captured at the C-ABI boundary while the reference's own parser drives
+  the drop-in Decoder shim (oracle/_ref/ldecod_shim, shim/decoder_h264r.cc): for every
+  picture the h264r_mb records, level pool, motion, slice table, picture parameters,
+  quantisation tables and DPB slot it is kept in (<name>.cap.npz).  The GPU tests
+  replay them through libh264r.so, where the reference cannot run.
+
+tests/golden/make_streams.py regenerates everything (this container only).
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+GOLDEN = os.path.join(HERE, "golden")
+STREAM_DIR = os.path.join(GOLDEN, "streams")
+STREAMS_JSON = os.path.join(GOLDEN, "streams.json")
+sys.path.insert(0, os.path.join(ROOT, "arrow-h264_amd"))
+
+from h264r import _abi as A  # noqa: E402
+from h264r import output as OUT  # noqa: E402
+
+# name -> tests/h264_writer.StreamCfg fields
+STREAMS = {
+    "bp_qcif_ippp": dict(width_mbs=11, height_mbs=9, frames=4, seed=101),
+    "bp_qcif_slices_cip": dict(width_mbs=11, height_mbs=9, frames=5, seed=102, slices=3, deblock=(0, 1, 2),
+                               offsets=6, num_refs=3, cip=1, chroma_qp_offset=-5),
+    "bp_cif_wp_pcm": dict(width_mbs=22, height_mbs=18, frames=4, seed=103, weighted=1, num_refs=2, pcm=0.1,
+                          skip=0.3),
+    "bp_qcif_intra_qp0_51": dict(width_mbs=11, height_mbs=9, frames=3, seed=104, all_intra=True, qp=(0, 51),
+                                 level_max=3),
+    "hp_cif_8x8": dict(width_mbs=22, height_mbs=18, frames=4, seed=105, profile=100, transform8x8=1, slices=2,
+                       deblock=(0, 2), offsets=3, chroma_qp_offset=4, second_chroma_qp_offset=-3),
+    "hp_qcif_scaling_lists": dict(width_mbs=11, height_mbs=9, frames=4, seed=106, profile=100, transform8x8=1,
+                                  scaling=3, qp=(10, 34)),
+    "hp_qcif_scaling_pps_4x4": dict(width_mbs=11, height_mbs=9, frames=3, seed=107, profile=100, transform8x8=0,
+                                    scaling=2),
+    "bp_vga_crop_8slices": dict(width_mbs=40, height_mbs=30, frames=3, seed=108, crop=(1, 2, 0, 4), slices=8,
+                                deblock=(0, 1, 2), offsets=6, intra_in_p=0.3, num_refs=2),
+    "hp_720p_4slices": dict(width_mbs=80, height_mbs=45, frames=2, seed=109, profile=100, transform8x8=1,
+                            slices=4, deblock=(0, 2), scaling=1, num_refs=1),
+}
+
+CAP_MAGIC = 0x43523448
+QUANT_BYTES = A.QUANT_DTYPE.itemsize
+
+
+def stream_path(name: str) -> str:
+    return os.path.join(STREAM_DIR, name + ".264")
+
+
+def capture_path(name: str) -> str:
+    return os.path.join(STREAM_DIR, name + ".cap.npz")
+
+
+def crop_of(cfg: dict) -> OUT.Crop:
+    l, r, t, b = cfg.get("crop", (0, 0, 0, 0))
+    return OUT.Crop(left=l, right=r, top=t, bottom=b)
+
+
+def frame_md5s(planes, cfg: dict) -> list[str]:
+    """Per-frame MD5 of cropped output frames (write_out_picture + digest_by_frames)."""
+    geom = OUT.geometry(cfg["width_mbs"], cfg["height_mbs"], crop_of(cfg))
+    return [hashlib.md5(OUT.frame_bytes(y, u, v, geom)).hexdigest() for (y, u, v) in planes]
+
+
+def read_capture_file(path: str) -> list[dict]:
+    """Parse the raw capture written by oracle/h264r_cpu_abi.c (H264R_CAPTURE)."""
+    raw = open(path, "rb").read()
+    off, pics = 0, []
+    while off < len(raw):
+        hdr = np.frombuffer(raw, np.int32, 8, off)
+        off += 32
+        magic, W, H, ns, nl, keep = (int(v) for v in hdr[:6])
+        assert magic == CAP_MAGIC, "capture: bad record"
+        n = W * H
+
+        def take(dtype, count):
+            nonlocal off
+            a = np.frombuffer(raw, dtype, count, off).copy()
+            off += a.nbytes
+            return a
+        p = dict(W=W, H=H, keep=keep)
+        p["mbs"] = take(A.MB_DTYPE, n)
+        p["levels"] = take(np.int16, nl)
+        p["mv"] = take(np.uint32, 2 * 16 * n).reshape(2, 4 * H, 4 * W)
+        p["ref_idx"] = take(np.int8, 2 * 16 * n).reshape(2, 4 * H, 4 * W)
+        p["slices"] = take(A.SLICE_DTYPE, ns)
+        p["pic"] = take(A.PIC_DTYPE, 1)
+        p["quant"] = take(A.QUANT_DTYPE, 1)
+        y = take(np.uint8, 256 * n).reshape(16 * H, 16 * W)
+        u = take(np.uint8, 64 * n).reshape(8 * H, 8 * W)
+        v = take(np.uint8, 64 * n).reshape(8 * H, 8 * W)
+        p["plane_md5"] = [hashlib.md5(a.tobytes()).hexdigest() for a in (y, u, v)]
+        pics.append(p)
+    return pics
+
+
+def save_capture(path: str, pics: list[dict]) -> None:
+    arrs = {}
+    for i, p in enumerate(pics):
+        for k in ("mbs", "levels", "mv", "ref_idx", "slices", "pic", "quant"):
+            a = p[k]
+            arrs[f"{i}_{k}"] = a.view(np.uint8) if a.dtype.names else a
+        arrs[f"{i}_meta"] = np.array([p["W"], p["H"], p["keep"]], np.int32)
+        arrs[f"{i}_plane_md5"] = np.array(p["plane_md5"])
+    np.savez_compressed(path, n=np.array([len(pics)]), **arrs)
+
+
+def load_capture(path: str) -> list[dict]:
+    z = np.load(path, allow_pickle=False)
+    dt = {"mbs": A.MB_DTYPE, "slices": A.SLICE_DTYPE, "pic": A.PIC_DTYPE, "quant": A.QUANT_DTYPE}
+    pics = []
+    for i in range(int(z["n"][0])):
+        W, H, keep = (int(v) for v in z[f"{i}_meta"])
+        p = dict(W=W, H=H, keep=keep)
+        for k in ("mbs", "levels", "mv", "ref_idx", "slices", "pic", "quant"):
+            a = z[f"{i}_{k}"]
+            p[k] = a.view(dt[k]) if k in dt else a
+        p["plane_md5"] = [str(s) for s in z[f"{i}_plane_md5"]]
+        pics.append(p)
+    return pics
+
+
+def golden() -> dict:
+    return json.load(open(STREAMS_JSON))
+
+
+def iter_mbs(p: dict):
+    """(addr, record, levels, mv[2,16], ref_idx[2,16]) of every MB of a captured picture,
+    in the form Decoder.decode / h264r_mb_submit take."""
+    W, H = p["W"], p["H"]
+    mv = p["mv"].reshape(2, H, 4, W, 4).transpose(0, 1, 3, 2, 4).reshape(2, H * W, 16)
+    ri = p["ref_idx"].reshape(2, H, 4, W, 4).transpose(0, 1, 3, 2, 4).reshape(2, H * W, 16)
+    mbs = p["mbs"]
+    offs = mbs["coef_off"].astype(np.int64)
+    order = np.argsort(offs, kind="stable")
+    ends = np.empty_like(offs)
+    ends[order] = np.append(offs[order][1:], len(p["levels"]))
+    for a in range(W * H):
+        rec = mbs[a:a + 1].copy()
+        rec["coef_off"] = 0
+        yield a, rec, p["levels"][offs[a]:ends[a]], mv[:, a], ri[:, a]
