@@ -112,8 +112,15 @@ Shim& shim()
     return s;
 }
 
+bool trace()
+{
+    static const bool t = getenv("H264R_SHIM_TRACE") != nullptr;
+    return t;
+}
+
 void check(int st, const char* what)
 {
+    if (trace()) fprintf(stderr, "h264r shim: %s -> %d\n", what, st);
     if (st != H264R_OK) error(500, "h264r: %s failed: %s", what, h264r_strerror(st));
 }
 
