@@ -30,8 +30,11 @@ extern "C" __global__ void k_intra_levels(h264r_batch b, const uint16_t* lvl, in
 constexpr int LEVEL_MAX_MBS = 65536;      // k_level's LDS bitmap (k_picture.hip)
 extern "C" __global__ void k_deblock(h264r_batch b, const h264r::DbInfo* dbinfo, uint64_t* hb,
                                      int* sync, int* err, uint32_t epoch, int2 rows);
+extern "C" __global__ void k_deblock2(h264r_batch b, const h264r::DbInfo* dbinfo, uint64_t* hb,
+                                      int* sync, int* err, uint32_t epoch, int2 rows);
 constexpr size_t DBINFO_BYTES = 80;
 constexpr size_t HANDOFF_BYTES = 256;   // one tagged record (32 x {dword, epoch}) per MB
+constexpr size_t HANDOFF2_BYTES = 384;  // k_deblock2: 2 row slots x 24 x {dword, tag} per MB column
 
 namespace {
 
@@ -113,6 +116,8 @@ struct h264r_ctx {
     int* d_sync = nullptr; size_t c_sync = 0;
     uint8_t* d_hb = nullptr; size_t c_hb = 0;
     uint32_t epoch = 0;             // tag of the deblocking hand-off records of the last launch
+    uint8_t* d_hb2 = nullptr; size_t c_hb2 = 0;
+    uint32_t epoch2 = 0;            // the same for k_deblock2 (< 2^20: its tags carry the row)
     uint2* d_mot = nullptr; size_t c_mot = 0;
     uint16_t* d_lvl = nullptr; size_t c_lvl = 0;   // intra dependency level per MB
     int levels_grid = 0;                           // resident workgroups of k_intra_levels
@@ -226,7 +231,7 @@ int h264r_destroy(h264r_ctx* c)
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (int s = 0; s < H264R_MAX_SLOTS; ++s) if (c->slot[s][0]) (void)hipFree(c->slot[s][0]);
-    void* bufs[] = {c->d_ref_planes, c->d_err, c->d_dbinfo, c->d_sync, c->d_hb, c->d_mot, c->d_lvl, c->d_mbs, c->d_levels, c->d_mv, c->d_ref, c->d_slices, c->d_pic, c->d_quant, c->d_out};
+    void* bufs[] = {c->d_ref_planes, c->d_err, c->d_dbinfo, c->d_sync, c->d_hb, c->d_hb2, c->d_mot, c->d_lvl, c->d_mbs, c->d_levels, c->d_mv, c->d_ref, c->d_slices, c->d_pic, c->d_quant, c->d_out};
     for (void* b : bufs) if (b) (void)hipFree(b);
     for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
     if (c->ev_last) (void)hipEventDestroy(c->ev_last);
@@ -330,16 +335,21 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
     c->last_stream = s;
     int st;
     if ((st = dev_resize(&c->d_dbinfo, &c->c_dbinfo, (size_t)P * W * H * DBINFO_BYTES))) return st;
+    static const int rows_min = [] { const char* e = getenv("H264R_DEBLOCK2_MIN"); return e ? atoi(e) : (1 << 30); }();
+    const bool by_rows = (c->debug & H264R_DBG_DEBLOCK_ROWS) || (!(c->debug & H264R_DBG_DEBLOCK_MB) && P >= rows_min);
+    // hand-off records of the chosen deblocking kernel; fresh memory or a wrapping epoch
+    // restarts from zeroed records, so no record may carry a live tag
+    uint8_t** hb = by_rows ? &c->d_hb2 : &c->d_hb;
+    size_t* hcap = by_rows ? &c->c_hb2 : &c->c_hb;
+    uint32_t* ep = by_rows ? &c->epoch2 : &c->epoch;
+    const uint32_t ep_max = by_rows ? (1u << 20) - 2 : 0xFFFFFF00u;
     {
-        const size_t cap_before = c->c_hb;
-        if ((st = dev_resize(&c->d_hb, &c->c_hb, (size_t)P * npairs * W * HANDOFF_BYTES))) return st;
-        if (c->c_hb != cap_before) {              // fresh memory: no record may carry a live epoch
-            HIP_OK(hipMemsetAsync(c->d_hb, 0, c->c_hb, s));
-            c->epoch = 0;
-        }
-        if (c->epoch > 0xFFFFFF00u) {             // never reuse an epoch: restart from clean memory
-            HIP_OK(hipMemsetAsync(c->d_hb, 0, c->c_hb, s));
-            c->epoch = 0;
+        const size_t cap_before = *hcap;
+        const size_t need = by_rows ? (size_t)P * W * HANDOFF2_BYTES : (size_t)P * npairs * W * HANDOFF_BYTES;
+        if ((st = dev_resize(hb, hcap, need))) return st;
+        if (*hcap != cap_before || *ep > ep_max) {
+            HIP_OK(hipMemsetAsync(*hb, 0, *hcap, s));
+            *ep = 0;
         }
     }
     const size_t mplane = (size_t)W * 4 * H * 4;
@@ -390,8 +400,12 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
     }
     if (!(c->debug & H264R_DBG_NO_DEBLOCK)) {
         Timed t(c, 2, s);
-        hipLaunchKernelGGL(k_deblock, dim3(P * npairs), dim3(64), 0, s, b, dbinfo,
-                           reinterpret_cast<uint64_t*>(c->d_hb), sync + 1 + (size_t)P * H, c->d_err, ++c->epoch, rows);
+        if (by_rows)
+            hipLaunchKernelGGL(k_deblock2, dim3(((P + 31) / 32) * HB), dim3(64), 0, s, b, dbinfo,
+                               reinterpret_cast<uint64_t*>(c->d_hb2), sync + 1 + (size_t)P * H, c->d_err, ++c->epoch2, rows);
+        else
+            hipLaunchKernelGGL(k_deblock, dim3(P * npairs), dim3(64), 0, s, b, dbinfo,
+                               reinterpret_cast<uint64_t*>(c->d_hb), sync + 1 + (size_t)P * H, c->d_err, ++c->epoch, rows);
         HIP_OK(hipGetLastError());
     }
     return H264R_OK;

@@ -181,8 +181,9 @@ class Decoder:
 
     # -- convenience ----------------------------------------------------------------
     def decode_picture(self, p, refs=None, keep_slot: int = -1, no_deblock: bool = False,
-                       intra_walk: bool = False):
-        """Submit every MB of a synth.Picture (raster order) and return its planes."""
+                       intra_walk: bool = False, debug: int = 0):
+        """Submit every MB of a synth.Picture (raster order) and return its planes
+        (debug: further h264r_set_debug flags for this picture)."""
         from .mbview import iter_mbs
         if refs is not None:
             for s, (y, u, v) in enumerate(refs):
@@ -191,7 +192,7 @@ class Decoder:
         self.init(W, H, p.pic, p.slices)
         for addr, rec, lv, mv, rr in iter_mbs(p):
             self.decode(addr, rec, lv, mv, rr)
-        self.set_debug((A.DBG_NO_DEBLOCK if no_deblock else 0) | (A.DBG_INTRA_WALK if intra_walk else 0))
+        self.set_debug((A.DBG_NO_DEBLOCK if no_deblock else 0) | (A.DBG_INTRA_WALK if intra_walk else 0) | debug)
         try:
             return self.deblock_filter(keep_slot)
         finally:

@@ -255,6 +255,12 @@ int  h264r_set_timing(h264r_ctx* ctx, int enable);
 /* H264R_DBG_INTRA_WALK reconstructs every intra MB with the wavefront walk instead of
  * the dependency-level schedule (both are bit-exact; this exercises the walk alone). */
 #define H264R_DBG_INTRA_WALK 2
+/* The loop filter has two schedules (both bit-exact): k_deblock spreads one MB over 32
+ * lanes (short latency, small batches), k_deblock2 gives each (picture, MB row) a lane
+ * pair (batches of >= H264R_DEBLOCK2_MIN pictures; off by default).  These flags
+ * force one of them. */
+#define H264R_DBG_DEBLOCK_MB   4
+#define H264R_DBG_DEBLOCK_ROWS 8
 int  h264r_set_debug(h264r_ctx* ctx, int flags);
 /* Wait for the context's work and report a device-side failure (a wavefront wait
  * that timed out): H264R_OK or H264R_EDEVICE. */

@@ -5,6 +5,7 @@ Bit-exact on every sample: this is integer work.  Full BASELINE sizes (1080p,
 seconds.
 """
 import hashlib
+import itertools
 import json
 import os
 
@@ -71,26 +72,33 @@ def test_gpu_matches_reference_fixture(L, dec, fx):
         pytest.fail("; ".join(msgs) or "md5 mismatch")
 
 
-def _batch_vs_oracle(L, dec, cidx, W, H, n, debug=0, **over):
+# both deblocking schedules (include/h264r.h): one MB per 32 lanes / a lane pair per MB row
+DEBLOCKS = (A.DBG_DEBLOCK_MB, A.DBG_DEBLOCK_ROWS)
+
+
+def _batch_vs_oracle(L, dec, cidx, W, H, n, debug=0, deblocks=DEBLOCKS, **over):
+    """Decode n synthetic pictures in one batch under each deblocking schedule and compare
+    every plane with the oracle's decode."""
     cfg = synth.default_cfg(L, cidx, W, H, **over)
     pics = [synth.picture(L, cfg, i) for i in range(n)]
     refs = synth.refpics(L, cfg)
     for s, (y, u, v) in enumerate(refs):
         dec.set_ref(s, y, u, v)
     host = B.pack(pics, h264r.quant_flat())
-    db = B.to_device(host, n, None)
-    dec.set_debug(debug)
-    try:
-        dec.decode_batch(db.batch)
-        dec.check()
-    finally:
-        dec.set_debug(0)
-    for i, p in enumerate(pics):
-        want = O.decode(p, refs)
-        got = db.planes(i)
-        for k in range(3):
-            d = first_diff(got[k], want[k], 16 if k == 0 else 8)
-            assert d is None, f"picture {i} plane {k}: {d}"
+    want = [O.decode(p, refs) for p in pics]
+    for db_flag in deblocks:
+        db = B.to_device(host, n, None)
+        dec.set_debug(debug | db_flag)
+        try:
+            dec.decode_batch(db.batch)
+            dec.check()
+        finally:
+            dec.set_debug(0)
+        for i in range(n):
+            got = db.planes(i)
+            for k in range(3):
+                d = first_diff(got[k], want[i][k], 16 if k == 0 else 8)
+                assert d is None, f"deblock flag {db_flag} picture {i} plane {k}: {d}"
 
 
 def test_gpu_batch_cif_p(L, dec):
@@ -122,6 +130,13 @@ def test_gpu_batch_dense_intra_levels(L, dec):
     _batch_vs_oracle(L, dec, 3, 40, 30, 3, intra_permille=600, pcm_permille=30)
 
 
+@pytest.mark.parametrize("n", [33, 70])
+def test_gpu_batch_picture_groups(L, dec, n):
+    """Batches spanning several 32-picture groups of k_deblock2 (the last one ragged);
+    n = 70 is above the default H264R_DEBLOCK2_MIN, so flag 0 takes the row schedule too."""
+    _batch_vs_oracle(L, dec, 3, 11, 9, n, deblocks=(0, A.DBG_DEBLOCK_MB, A.DBG_DEBLOCK_ROWS), pcm_permille=20)
+
+
 def test_gpu_2160p_b_8slices(L, dec):
     """BASELINE config 5 size (3840x2160, 8 slices, idc 2)."""
     _batch_vs_oracle(L, dec, 5, 240, 135, 1)
@@ -133,10 +148,11 @@ def test_gpu_degenerate_sizes(L, dec, W, H):
         cfg = synth.default_cfg(L, cidx, W, H, pcm_permille=50, num_slices=1)
         p = synth.picture(L, cfg, 1)
         refs = synth.refpics(L, cfg)
-        got = dec.decode_picture(p, refs)
         want = O.decode(p, refs)
-        for k in range(3):
-            assert np.array_equal(got[k], want[k]), (cidx, k)
+        for flag in DEBLOCKS:
+            got = dec.decode_picture(p, refs, debug=flag)
+            for k in range(3):
+                assert np.array_equal(got[k], want[k]), (cidx, flag, k)
 
 
 def test_gpu_streaming_errors(L, dec):
@@ -184,12 +200,16 @@ def test_gpu_slice_bands_match_whole_picture(L, dec, cidx, W, H, world):
     want = [O.decode(p, refs) for p in pics]
     bands = D.slice_bands(_slice_first_rows(pics[0]), H, world)
     host = B.pack(pics, h264r.quant_flat())
-    for r0, r1 in bands:
+    for (r0, r1), flag in itertools.product(bands, DEBLOCKS):
         if r1 == r0:
             continue
         db = B.to_device(host, n, None)
-        dec.decode_batch(db.batch, rows=(r0, r1))
-        dec.check()
+        dec.set_debug(flag)
+        try:
+            dec.decode_batch(db.batch, rows=(r0, r1))
+            dec.check()
+        finally:
+            dec.set_debug(0)
         torch.cuda.synchronize()
         for i in range(n):
             got = db.planes(i)
@@ -197,7 +217,7 @@ def test_gpu_slice_bands_match_whole_picture(L, dec, cidx, W, H, world):
                 m = 16 if k == 0 else 8
                 inside = slice(r0 * m, r1 * m)
                 d = first_diff(got[k][inside], want[i][k][inside], m)
-                assert d is None, f"band {r0}..{r1} picture {i} plane {k}: {d}"
+                assert d is None, f"band {r0}..{r1} flag {flag} picture {i} plane {k}: {d}"
                 outside = np.ones(got[k].shape[0], bool)
                 outside[inside] = False
                 assert not got[k][outside].any(), f"band {r0}..{r1} wrote outside its rows"
@@ -211,12 +231,17 @@ def test_gpu_band_across_filtered_edge_is_reported(L, dec):
     refs = synth.refpics(L, cfg)
     for s, (y, u, v) in enumerate(refs):
         dec.set_ref(s, y, u, v)
-    db = B.to_device(B.pack([p], h264r.quant_flat()), 1, None)
     r0 = _slice_first_rows(p)[1]
-    dec.decode_batch(db.batch, rows=(r0, 18))
-    with pytest.raises(h264r.H264RError) as e:
-        dec.check()
-    assert e.value.status == A.EDEVICE
+    for flag in DEBLOCKS:
+        db = B.to_device(B.pack([p], h264r.quant_flat()), 1, None)
+        dec.set_debug(flag)
+        try:
+            dec.decode_batch(db.batch, rows=(r0, 18))
+            with pytest.raises(h264r.H264RError) as e:
+                dec.check()
+        finally:
+            dec.set_debug(0)
+        assert e.value.status == A.EDEVICE, flag
 
 
 def test_gpu_ippp_chain_yuv_compare(L, dec, tmp_path):

@@ -124,16 +124,19 @@ def test_reference_and_shim_reproduce_golden(name, tmp_path):
 
 # ---------------------------------------------------------------------------- MI355X
 @pytest.mark.gpu
+@pytest.mark.parametrize("flag", [A.DBG_DEBLOCK_MB, A.DBG_DEBLOCK_ROWS], ids=["deblock_mb", "deblock_rows"])
 @pytest.mark.parametrize("name", NAMES)
-def test_gpu_replay_of_captures_matches_reference(name):
+def test_gpu_replay_of_captures_matches_reference(name, flag):
     """The MB records the reference parser handed the shim, replayed through the C ABI
     of libh264r.so on MI355X (streaming API, each reference picture kept on the device
-    in the shim's DPB slot), reproduce the reference's per-frame MD5s bit for bit."""
+    in the shim's DPB slot), reproduce the reference's per-frame MD5s bit for bit --
+    under both deblocking schedules."""
     import h264r
     cfg = S.STREAMS[name]
     pics = S.load_capture(S.capture_path(name))
     W, H = cfg["width_mbs"], cfg["height_mbs"]
     with h264r.Decoder(0, W, H) as dec:
+        dec.set_debug(flag)
         def run(p):
             dec.assign_quant_params(p["quant"])
             dec.init(W, H, p["pic"], p["slices"])
