@@ -35,6 +35,7 @@ extern "C" __global__ void k_deblock2(h264r_batch b, const h264r::DbInfo* dbinfo
 constexpr size_t DBINFO_BYTES = 80;
 constexpr size_t HANDOFF_BYTES = 256;   // one tagged record (32 x {dword, epoch}) per MB
 constexpr size_t HANDOFF2_BYTES = 384;  // k_deblock2: 2 row slots x 24 x {dword, tag} per MB column
+constexpr int DEBLOCK2_UNITS = 16;      // k_deblock2: pictures per wave (mb_deblock.h)
 
 namespace {
 
@@ -401,7 +402,7 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
     if (!(c->debug & H264R_DBG_NO_DEBLOCK)) {
         Timed t(c, 2, s);
         if (by_rows)
-            hipLaunchKernelGGL(k_deblock2, dim3(((P + 31) / 32) * HB), dim3(64), 0, s, b, dbinfo,
+            hipLaunchKernelGGL(k_deblock2, dim3(((P + DEBLOCK2_UNITS - 1) / DEBLOCK2_UNITS) * HB), dim3(64), 0, s, b, dbinfo,
                                reinterpret_cast<uint64_t*>(c->d_hb2), sync + 1 + (size_t)P * H, c->d_err, ++c->epoch2, rows);
         else
             hipLaunchKernelGGL(k_deblock, dim3(P * npairs), dim3(64), 0, s, b, dbinfo,

@@ -69,6 +69,7 @@ struct DbInfo {
 };
 static_assert(sizeof(DbInfo) == 80, "DbInfo layout");
 constexpr int DBINFO_DWORDS = 20;
+constexpr int DEBLOCK2_UNITS = 16;   // k_deblock2: (picture, MB row) units per wave
 
 // alpha | beta << 8 | tc0(bS 1..3) << 16 / 21 / 26 for one edge: filter_edge
 // deblock.cc:469-480 (qPav of the two MBs' QPs, indexA/B with MbQ's slice offsets),

@@ -17,6 +17,12 @@
  * usage: ref_driver W H kind nslices idc offA offB t8 wp cip nrefs qpmin qpmax
  *                   pcm_permille intra_permille mvx mvy seed index out.yuv [recon_only]
  * Output: Y plane then Cb then Cr, 8-bit, unpadded.
+ *
+ * Timing mode (H264R_TIME_REPS=<n>): the reconstruction of the picture -- the
+ * coefficient push (inverse scan + dequantisation), Decoder::decode of every MB and
+ * deblock_filter -- runs n times back to back on one thread (every pass rewrites every
+ * MB, so each pass decodes the same picture), and "ref_time <MBs> <seconds>" goes to
+ * stderr.  The output file holds the last pass.
  */
 #include "global.h"
 #include "slice.h"
@@ -24,6 +30,7 @@
 #include "macroblock.h"
 #include "decoder.h"
 
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -193,6 +200,15 @@ int main(int argc, char** argv)
     zigzag(4, inv4);
     zigzag(8, inv8);
 
+    const char* reps_env = getenv("H264R_TIME_REPS");
+    const int reps = reps_env ? atoi(reps_env) : 1;
+    /* every pass starts from the parser's state of mb_data (reset_mbs) */
+    std::vector<char> mb_pristine(sizeof(mb_t) * NMB);
+    memcpy(mb_pristine.data(), (void*)mb_data, mb_pristine.size());
+    double sec = 0;
+    for (int rep = 0; rep < reps; ++rep) {
+    if (rep) memcpy((void*)mb_data, mb_pristine.data(), mb_pristine.size());
+    const auto t0 = std::chrono::steady_clock::now();
     for (int a = 0; a < NMB; ++a) {
         const h264r_mb& c = mbs[a];
         slice_t& s = *sl[c.slice];
@@ -310,6 +326,11 @@ int main(int argc, char** argv)
         }
     }
     if (!recon_only) sl[0]->decoder.deblock_filter(*sl[0]);
+    sec += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    }
+    if (reps_env) {
+        fprintf(stderr, "ref_time %lld %.6f\n", (long long)NMB * reps, sec);
+    }
 
     FILE* f = fopen(out_path, "wb");
     if (!f) return 5;

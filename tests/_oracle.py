@@ -110,8 +110,10 @@ def decode(p: synth.Picture, refs=None, stage: str = "full"):
     return out
 
 
-def run_reference(cfg: A.SynthCfg, index: int, recon_only: bool = False):
-    """Planes produced by the compiled reference decoder (this container only)."""
+def run_reference(cfg: A.SynthCfg, index: int, recon_only: bool = False, time_reps: int = 0):
+    """Planes produced by the compiled reference decoder (this container only).  With
+    time_reps > 0 the driver reconstructs the picture that many times on one thread and
+    (planes, macroblocks, seconds) is returned (ref_driver.cc timing mode)."""
     drv = build_ref()
     W, H = cfg.width_mbs, cfg.height_mbs
     with tempfile.TemporaryDirectory() as td:
@@ -120,10 +122,15 @@ def run_reference(cfg: A.SynthCfg, index: int, recon_only: bool = False):
                 cfg.filter_offset_b, cfg.transform8x8, cfg.wp_mode, cfg.constrained_intra,
                 cfg.num_refs, cfg.qp_min, cfg.qp_max, cfg.pcm_permille, cfg.intra_permille,
                 cfg.mv_range_x, cfg.mv_range_y, hex(cfg.seed), index, out, int(recon_only)]
-        r = subprocess.run([str(a) for a in args], capture_output=True, text=True)
+        env = dict(os.environ, H264R_TIME_REPS=str(time_reps)) if time_reps else None
+        r = subprocess.run([str(a) for a in args], capture_output=True, text=True, env=env)
         if r.returncode != 0:
             raise RuntimeError(f"ref_driver failed ({r.returncode}): {r.stderr[-2000:]}")
         raw = np.fromfile(out, np.uint8)
     ny, nc = 256 * W * H, 64 * W * H
-    return (raw[:ny].reshape(16 * H, 16 * W), raw[ny:ny + nc].reshape(8 * H, 8 * W),
-            raw[ny + nc:].reshape(8 * H, 8 * W))
+    planes = (raw[:ny].reshape(16 * H, 16 * W), raw[ny:ny + nc].reshape(8 * H, 8 * W),
+              raw[ny + nc:].reshape(8 * H, 8 * W))
+    if not time_reps:
+        return planes
+    line = [ln for ln in r.stderr.splitlines() if ln.startswith("ref_time ")][-1].split()
+    return planes, int(line[1]), float(line[2])

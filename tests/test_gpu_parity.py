@@ -133,7 +133,7 @@ def test_gpu_batch_dense_intra_levels(L, dec):
 @pytest.mark.parametrize("n", [33, 70])
 def test_gpu_batch_picture_groups(L, dec, n):
     """Batches spanning several 32-picture groups of k_deblock2 (the last one ragged);
-    n = 70 is above the default H264R_DEBLOCK2_MIN, so flag 0 takes the row schedule too."""
+    flag 0 takes whichever schedule H264R_DEBLOCK2_MIN selects for the batch size."""
     _batch_vs_oracle(L, dec, 3, 11, 9, n, deblocks=(0, A.DBG_DEBLOCK_MB, A.DBG_DEBLOCK_ROWS), pcm_permille=20)
 
 
