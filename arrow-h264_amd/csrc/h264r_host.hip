@@ -17,6 +17,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <new>
+#include <string>
 #include <vector>
 
 #include "h264r.h"
@@ -336,7 +337,7 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
     c->last_stream = s;
     int st;
     if ((st = dev_resize(&c->d_dbinfo, &c->c_dbinfo, (size_t)P * W * H * DBINFO_BYTES))) return st;
-    static const int rows_min = [] { const char* e = getenv("H264R_DEBLOCK2_MIN"); return e ? atoi(e) : (1 << 30); }();
+    static const int rows_min = [] { const char* e = getenv("H264R_DEBLOCK2_MIN"); return e ? atoi(e) : 128; }();
     const bool by_rows = (c->debug & H264R_DBG_DEBLOCK_ROWS) || (!(c->debug & H264R_DBG_DEBLOCK_MB) && P >= rows_min);
     // hand-off records of the chosen deblocking kernel; fresh memory or a wrapping epoch
     // restarts from zeroed records, so no record may carry a live tag
@@ -413,15 +414,19 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
 }
 
 #ifdef H264R_TRACE
-extern __device__ unsigned long long h264r_db_trace[1 << 16][8];
+void h264r_db_trace_copy(void* dst);    // k_deblock.hip / k_deblock2.hip (trace builds)
+void h264r_db2_trace_copy(void* dst);
+// H264R_TRACE_OUT=<path>: k_deblock's trace to <path>, k_deblock2's to <path>.2
 static void dump_trace(hipStream_t s)
 {
     const char* path = getenv("H264R_TRACE_OUT");
     if (!path) return;
     static std::vector<unsigned long long> buf((1 << 16) * 8);
     (void)hipStreamSynchronize(s);
-    (void)hipMemcpyFromSymbol(buf.data(), HIP_SYMBOL(h264r_db_trace), buf.size() * 8);
+    h264r_db_trace_copy(buf.data());
     if (FILE* f = fopen(path, "wb")) { fwrite(buf.data(), 8, buf.size(), f); fclose(f); }
+    h264r_db2_trace_copy(buf.data());
+    if (FILE* f = fopen((std::string(path) + ".2").c_str(), "wb")) { fwrite(buf.data(), 8, buf.size(), f); fclose(f); }
 }
 #endif
 

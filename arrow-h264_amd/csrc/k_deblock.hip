@@ -60,6 +60,7 @@ DEV void st_cc64(uint64_t* p, uint64_t v)   // write-through (sc1) 8-byte store
 // end, cycles spent polling} in s_memrealtime ticks (100 MHz).
 __device__ unsigned long long h264r_db_trace[1 << 16][8];
 #define TRACE(...) __VA_ARGS__
+extern "C" void h264r_db_trace_copy(void* dst) { (void)hipMemcpyFromSymbol(dst, HIP_SYMBOL(h264r_db_trace), sizeof(h264r_db_trace)); }
 #else
 #define TRACE(...)
 #endif

@@ -1,0 +1,54 @@
+#!/usr/bin/env python3
+"""Diagnostic (GPU box): per-wave timing of the deblocking walk from a trace build,
+    make -C arrow-h264_amd OBJ=build_trace LIBDIR=lib_trace EXTRA=-DH264R_TRACE
+    H264R_LIB=arrow-h264_amd/lib_trace/libh264r.so python tools/trace_deblock.py [pictures] [flag]
+(flag 8 = k_deblock2, 4 = k_deblock).  k_deblock2 records per ticket {start, end} in
+100 MHz ticks and the core cycles of its four phases summed over the walk."""
+import os
+import sys
+import tempfile
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "arrow-h264_amd"))
+import torch  # noqa: E402,F401
+import h264r  # noqa: E402
+from h264r import batch as B, synth  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 256
+flag = int(sys.argv[2]) if len(sys.argv) > 2 else 8
+L = h264r.lib()
+W, H = 120, 68
+cfg = synth.default_cfg(L, 3, W, H)
+pics = [synth.picture(L, cfg, i % 8) for i in range(n)]
+refs = synth.refpics(L, cfg)
+out = os.path.join(tempfile.mkdtemp(), "tr.bin")
+with h264r.Decoder(0, W, H) as dec:
+    for s, (y, u, v) in enumerate(refs):
+        dec.set_ref(s, y, u, v)
+    host = B.pack(pics, h264r.quant_flat())
+    dec.set_debug(flag)
+    for it in range(3):                       # the last launch is the one traced
+        db = B.to_device(host, n, None)
+        if it == 2:
+            os.environ["H264R_TRACE_OUT"] = out
+        dec.decode_batch(db.batch)
+        dec.check()
+t = np.fromfile(out + ".2", np.uint64).reshape(-1, 8).astype(np.int64)
+ng = (n + 15) // 16
+k = ng * H
+t = t[:k]
+t0 = t[:, 0].min()
+start, end = (t[:, 0] - t0) / 100.0, (t[:, 1] - t0) / 100.0       # microseconds
+print(f"{n} pictures, {k} waves: kernel span {end.max():.0f} us; wave duration mean {np.mean(end - start):.0f} us, "
+      f"start spread {start.min():.0f}..{start.max():.0f} us")
+ph = t[:, 2:6].astype(np.float64)
+tot = ph.sum(1, keepdims=True)
+print("phase share (V, record wait, H, publish/stores/switch):", np.round((ph / tot).mean(0), 3))
+print("cycles per step by phase:", np.round(ph.mean(0) / W, 0))
+rows = np.arange(k) // ng
+for r in (0, 1, 2, H // 2, H - 1):
+    sel = rows == r
+    print(f"row {r:3d}: start {start[sel].mean():8.1f} us end {end[sel].mean():8.1f} us, wait share "
+          f"{(ph[sel, 1] / tot[sel, 0]).mean():.3f}, cycles/step by phase {np.round(ph[sel].mean(0) / W, 0)}")
