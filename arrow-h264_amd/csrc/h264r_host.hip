@@ -23,8 +23,7 @@
 #include "h264r.h"
 
 namespace h264r { struct DbInfo; }
-extern "C" __global__ void k_prep(h264r_batch b, uint2* mot, int2 rows);
-extern "C" __global__ void k_inter4(h264r_batch b, const uint2* mot, h264r::DbInfo* dbinfo, int2 rows);
+extern "C" __global__ void k_inter4(h264r_batch b, h264r::DbInfo* dbinfo, int2 rows);
 extern "C" __global__ void k_intra_pic(h264r_batch b, int* sync, int* err, const uint16_t* lvl, int lmax, int2 rows);
 extern "C" __global__ void k_level(h264r_batch b, uint16_t* lvl, int* lvsync, int2 rows);
 extern "C" __global__ void k_intra_levels(h264r_batch b, const uint16_t* lvl, int lmax, int* lvsync, int* err, int2 rows);
@@ -120,7 +119,6 @@ struct h264r_ctx {
     uint32_t epoch = 0;             // tag of the deblocking hand-off records of the last launch
     uint8_t* d_hb2 = nullptr; size_t c_hb2 = 0;
     uint32_t epoch2 = 0;            // the same for k_deblock2 (< 2^20: its tags carry the row)
-    uint2* d_mot = nullptr; size_t c_mot = 0;
     uint16_t* d_lvl = nullptr; size_t c_lvl = 0;   // intra dependency level per MB
     int levels_grid = 0;                           // resident workgroups of k_intra_levels
     // the per-batch scratch above is reused by every launch: a launch on a stream other
@@ -233,7 +231,7 @@ int h264r_destroy(h264r_ctx* c)
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (int s = 0; s < H264R_MAX_SLOTS; ++s) if (c->slot[s][0]) (void)hipFree(c->slot[s][0]);
-    void* bufs[] = {c->d_ref_planes, c->d_err, c->d_dbinfo, c->d_sync, c->d_hb, c->d_hb2, c->d_mot, c->d_lvl, c->d_mbs, c->d_levels, c->d_mv, c->d_ref, c->d_slices, c->d_pic, c->d_quant, c->d_out};
+    void* bufs[] = {c->d_ref_planes, c->d_err, c->d_dbinfo, c->d_sync, c->d_hb, c->d_hb2, c->d_lvl, c->d_mbs, c->d_levels, c->d_mv, c->d_ref, c->d_slices, c->d_pic, c->d_quant, c->d_out};
     for (void* b : bufs) if (b) (void)hipFree(b);
     for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
     if (c->ev_last) (void)hipEventDestroy(c->ev_last);
@@ -317,14 +315,14 @@ static int level_launches()
 
 // rows [row0, row1): the MB rows of every picture this launch reconstructs and
 // deblocks (the whole picture, or a slice-aligned band: h264r_decode_batch_rows).
-// Six launches on stream s: k_prep, k_inter4 (inter / PCM MBs + deblocking records),
-// k_level + k_intra_levels + k_intra_pic (intra MBs), k_deblock.
+// Five launches on stream s: k_inter4 (inter / PCM MBs + deblocking records), k_level +
+// k_intra_levels + k_intra_pic (intra MBs), k_deblock or k_deblock2 (by batch size).
 static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row0, int row1)
 {
     const int W = b.width_mbs, H = b.height_mbs, P = b.num_pics, HB = row1 - row0;
     const int2 rows = make_int2(row0, row1);
     const int nbands = (HB + 15) / 16, npairs = (HB + 1) / 2;
-    // scratch: per-MB deblocking records and resolved motion, tagged row-pair hand-off
+    // scratch: per-MB deblocking records, tagged hand-off
     // records, and a sync region [intra ticket + per-(picture,row) progress][deblock
     // ticket][level barrier, deepest level]
     const size_t sync_n = 1 + (size_t)P * H + 4;
@@ -354,8 +352,6 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
             *ep = 0;
         }
     }
-    const size_t mplane = (size_t)W * 4 * H * 4;
-    if ((st = dev_resize(&c->d_mot, &c->c_mot, (size_t)P * 2 * mplane))) return st;
     if ((st = dev_resize(&c->d_sync, &c->c_sync, sync_n))) return st;
     const bool levels = (size_t)W * H <= LEVEL_MAX_MBS && H <= 1024 && level_launches() > 0 &&
                         !(c->debug & H264R_DBG_INTRA_WALK);
@@ -377,11 +373,9 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
     int* sync = c->d_sync;
     Timed whole(c, 3, s);
     if (c->timing) c->timed_launches++;
-    hipLaunchKernelGGL(k_prep, dim3((unsigned)((HB * 16 * W + 255) / 256), P), dim3(256), 0, s, b, c->d_mot, rows);
-    HIP_OK(hipGetLastError());
     {
-        Timed t(c, 0, s);                         // phase 0 = the inter kernel alone (k_prep is in the total only)
-        hipLaunchKernelGGL(k_inter4, dim3((W * HB + 15) / 16, P), dim3(256), 0, s, b, c->d_mot, dbinfo, rows);
+        Timed t(c, 0, s);
+        hipLaunchKernelGGL(k_inter4, dim3((W * HB + 15) / 16, P), dim3(256), 0, s, b, dbinfo, rows);
         HIP_OK(hipGetLastError());
     }
     {

@@ -20,7 +20,7 @@ struct MotionRef {
     int mvx[2], mvy[2];
 };
 
-// Per-4x4-block motion as resolved by k_prep: {mv, ref_idx | slot << 8} per list.
+// Per-4x4-block motion as resolved in k_inter4 (block_motion): {mv, ref_idx | slot << 8} per list.
 // ref identity = DPB slot of RefPicList[l][ref_idx] (pic_motion_params::ref_pic,
 // interpret_mb.cc:611-623), -1 when the list is unused.
 DEV MotionRef motion_of(uint2 w0, uint2 w1)

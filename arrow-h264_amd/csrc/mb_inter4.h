@@ -30,10 +30,25 @@
 namespace h264r {
 
 constexpr int INTER4_MBS = 16;   // MBs per 256-thread workgroup (4 waves x 4)
+constexpr int INTER4_LDS_SLICES = 64;   // slices whose ref tables the workgroup keeps in LDS
 
 struct Inter4Lds {
     const uint8_t* planes[3 * H264R_MAX_SLOTS];
+    int8_t ref_slot[INTER4_LDS_SLICES][2][H264R_MAX_REFS];   // h264r_slice::ref_slot of the picture's slices
 };
+
+// Motion of one 4x4 block as {mv, ref_idx | slot << 8} per list: RefPicList[l][ref_idx]
+// of the block's slice resolved to its DPB slot (get_ref_pic dpb.cc:1046-1054;
+// pic_motion_params::ref_pic interpret_mb.cc:611-623), slot -1 when the list is unused.
+DEV uint2 block_motion(const h264r_batch& b, const h264r_slice* slices, const Inter4Lds& S, size_t at, int slice, int l)
+{
+    const uint32_t mv = b.mv[at];
+    const int ri = b.ref_idx[at];
+    int slot = -1;
+    if (ri >= 0 && ri < H264R_MAX_REFS)
+        slot = slice < INTER4_LDS_SLICES ? S.ref_slot[slice][l][ri] : slices[slice].ref_slot[l][ri];
+    return make_uint2(mv, (uint32_t)(uint8_t)ri | ((uint32_t)(uint8_t)slot << 8));
+}
 
 DEV h264r_mb mb_lane(const h264r_mb* p)          // per-lane 32-byte record, two 16-byte loads
 {
@@ -221,9 +236,9 @@ DEV void idct4_inplace(int& a, int& b, int& c, int& d)
 }
 
 // The inter / I_PCM macroblocks a0 .. a0+3 of picture `pic` and the deblocking
-// records of all four.  `mot`: the picture's resolved motion (k_prep).
-DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int aend, int lane, const uint2* __restrict__ mot,
-                    DbInfo* __restrict__ dbout, const Inter4Lds& S)
+// records of all four.
+DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int aend, int lane, DbInfo* __restrict__ dbout,
+                    const Inter4Lds& S)
 {
     const int grp = lane >> 4, blk = lane & 15, bx = blk & 3, by = blk >> 2;
     const int a = a0 + grp;
@@ -233,14 +248,14 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
     const h264r_mb* mbs = b.mbs + (size_t)pic * g.nmb;
     const h264r_slice* slices = b.slices + (size_t)pic * b.slice_stride;
 
-    // ---- motion of this block and of its left / upper neighbours (k_prep output)
+    // ---- MB record (two 16-byte loads: a struct copy becomes one byte load per field,
+    // each waited on its own) and the motion of this block
     const int X4 = mbx * 4 + bx, Y4 = mby * 4 + by;
     const int mi = Y4 * g.W4 + X4;
-    const uint2 m0 = mot[mi], m1 = mot[g.motion_plane + mi];
-    // ---- MB records (own, left, upper) and slice headers
-    // records as two 16-byte loads each (a struct copy becomes one byte load per field,
-    // each waited on its own); all three issued together
+    const size_t mbase = (size_t)pic * 2 * g.motion_plane;
     const h264r_mb q = mb_lane(&mbs[aa]);
+    const uint2 m0 = block_motion(b, slices, S, mbase + mi, q.slice, 0);
+    const uint2 m1 = block_motion(b, slices, S, mbase + g.motion_plane + mi, q.slice, 1);
     const int hasL = mbx > 0, hasU = mby > 0;
     const h264r_slice* qs = &slices[q.slice];
     const uint2 qsh = *reinterpret_cast<const uint2*>(qs);       // type, idc, offsets, wp, log2 wd
@@ -485,10 +500,12 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
     // neighbour motion and records: loaded here, after the reconstruction, so that
     // they do not stay live across motion compensation (L2-hot by now)
     const int li = X4 > 0 ? mi - 1 : mi, ui = Y4 > 0 ? mi - g.W4 : mi;
-    const uint2 l0 = mot[li], l1 = mot[g.motion_plane + li];
-    const uint2 u0 = mot[ui], u1 = mot[g.motion_plane + ui];
     const h264r_mb L = mb_lane(&mbs[hasL ? aa - 1 : aa]);
     const h264r_mb U = mb_lane(&mbs[hasU ? aa - g.wmb : aa]);
+    // the neighbour block belongs to this MB or to the left / upper one (its slice resolves it)
+    const int lsl = bx > 0 ? q.slice : L.slice, usl = by > 0 ? q.slice : U.slice;
+    const uint2 l0 = block_motion(b, slices, S, mbase + li, lsl, 0), l1 = block_motion(b, slices, S, mbase + g.motion_plane + li, lsl, 1);
+    const uint2 u0 = block_motion(b, slices, S, mbase + ui, usl, 0), u1 = block_motion(b, slices, S, mbase + g.motion_plane + ui, usl, 1);
     const int l_type = slices[L.slice].slice_type, u_type = slices[U.slice].slice_type;
     // ---- deblocking record (Deblock::strength deblock.cc:78-289): this lane's
     // left edge (vertical edge bx, segment by) and top edge (horizontal edge by,

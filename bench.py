@@ -400,7 +400,7 @@ def main() -> int:
     # k_deblock2, smaller ones with k_deblock (include/h264r.h)
     dbk = "k_deblock2" if npics >= int(os.environ.get("H264R_DEBLOCK2_MIN", "128")) else "k_deblock"
     names = ["k_inter4", "intra (k_level + k_intra_levels + k_intra_pic)", dbk]
-    kern_names = [["k_prep", "k_inter4"], ["k_level", "k_intra_levels", "k_intra_pic"], [dbk]]
+    kern_names = [["k_inter4"], ["k_level", "k_intra_levels", "k_intra_pic"], [dbk]]
     # HBM traffic per launch sequence from the PMC counters of the committed profile run
     # (tools/pmc.sh + tools/pmc_summary.py --json): per-MB FETCH_SIZE (doubled, gfx950) +
     # WRITE_SIZE of every kernel of the sequence, times the MBs this rank processed
@@ -456,7 +456,7 @@ def main() -> int:
                        "rows_this_rank": list(band)},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": "h264r_decode_batch launch sequence (k_prep, k_inter4, k_level, "
+                         "kernel": "h264r_decode_batch launch sequence (k_inter4, k_level, "
                                    f"k_intra_levels, k_intra_pic, {dbk})",
                          "kernel_ms": float(kern[3]), "kernel_algo_bytes": int(step_bytes),
                          "bytes_per_mb": step_bytes / max(mbs_rank, 1),

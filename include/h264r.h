@@ -245,7 +245,7 @@ int  h264r_ref_planes(h264r_ctx* ctx, int slot, uint8_t** y, uint8_t** u, uint8_
 /* Average device time (ms) per h264r_decode_batch of the launches made since timing was
  * enabled, measured with HIP events on each launch's stream: out[0] the inter kernel
  * (k_inter4), out[1] the intra kernels (k_level + k_intra_levels + k_intra_pic),
- * out[2] deblocking (k_deblock), out[3] the whole batch (also k_prep).  Returns
+ * out[2] deblocking (k_deblock / k_deblock2), out[3] the whole batch.  Returns
  * H264R_OK or an error. */
 int  h264r_last_timing(h264r_ctx* ctx, float out_ms[4]);
 int  h264r_set_timing(h264r_ctx* ctx, int enable);
