@@ -25,9 +25,14 @@
 namespace h264r { struct DbInfo; }
 extern "C" __global__ void k_inter4(h264r_batch b, h264r::DbInfo* dbinfo, int2 rows);
 extern "C" __global__ void k_intra_pic(h264r_batch b, int* sync, int* err, const uint16_t* lvl, int lmax, int2 rows);
-extern "C" __global__ void k_level(h264r_batch b, uint16_t* lvl, int* lvsync, int2 rows);
-extern "C" __global__ void k_intra_levels(h264r_batch b, const uint16_t* lvl, int lmax, int* lvsync, int* err, int2 rows);
+extern "C" __global__ void k_level(h264r_batch b, uint16_t* lvl, int* lvsync, int* lcount, int2 rows);
+extern "C" __global__ void k_level_scan(const int* lcount, int* lbase);
+extern "C" __global__ void k_level_scatter(h264r_batch b, const uint16_t* lvl, const int* lbase, int* lcursor,
+                                           uint32_t* list, int2 rows);
+extern "C" __global__ void k_intra_levels(h264r_batch b, const int* lcount, const int* lbase, const uint32_t* list,
+                                          int lmax, int* lvsync, int* err);
 constexpr int LEVEL_MAX_MBS = 65536;      // k_level's LDS bitmap (k_picture.hip)
+constexpr int LEVEL_LISTS = 64;           // levels with MB lists (H264R_LEVEL_LISTS, k_picture.hip)
 extern "C" __global__ void k_deblock(h264r_batch b, const h264r::DbInfo* dbinfo, uint64_t* hb,
                                      int* sync, int* err, uint32_t epoch, int2 rows);
 extern "C" __global__ void k_deblock2(h264r_batch b, const h264r::DbInfo* dbinfo, uint64_t* hb,
@@ -120,6 +125,8 @@ struct h264r_ctx {
     uint8_t* d_hb2 = nullptr; size_t c_hb2 = 0;
     uint32_t epoch2 = 0;            // the same for k_deblock2 (< 2^20: its tags carry the row)
     uint16_t* d_lvl = nullptr; size_t c_lvl = 0;   // intra dependency level per MB
+    uint32_t* d_list = nullptr; size_t c_list = 0; // intra MBs by level (pic * nmb + addr)
+    int* d_lcnt = nullptr; size_t c_lcnt = 0;      // [count | base | cursor] x (LEVEL_LISTS + 2)
     int levels_grid = 0;                           // resident workgroups of k_intra_levels
     // the per-batch scratch above is reused by every launch: a launch on a stream other
     // than the previous one first waits for the previous launch (ev_last)
@@ -231,7 +238,7 @@ int h264r_destroy(h264r_ctx* c)
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (int s = 0; s < H264R_MAX_SLOTS; ++s) if (c->slot[s][0]) (void)hipFree(c->slot[s][0]);
-    void* bufs[] = {c->d_ref_planes, c->d_err, c->d_dbinfo, c->d_sync, c->d_hb, c->d_hb2, c->d_lvl, c->d_mbs, c->d_levels, c->d_mv, c->d_ref, c->d_slices, c->d_pic, c->d_quant, c->d_out};
+    void* bufs[] = {c->d_ref_planes, c->d_err, c->d_dbinfo, c->d_sync, c->d_hb, c->d_hb2, c->d_lvl, c->d_list, c->d_lcnt, c->d_mbs, c->d_levels, c->d_mv, c->d_ref, c->d_slices, c->d_pic, c->d_quant, c->d_out};
     for (void* b : bufs) if (b) (void)hipFree(b);
     for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
     if (c->ev_last) (void)hipEventDestroy(c->ev_last);
@@ -303,14 +310,19 @@ struct Timed {
     }
 };
 
-// Intra MBs are scheduled by dependency level (k_level, then k_intra_levels does levels
-// 1..N in one persistent launch); the wavefront walk k_intra_pic takes whatever lies deeper.  In P/B
-// pictures the deepest level is a handful; in all-intra pictures most MBs are deeper
-// than N and the walk does them.  H264R_LEVELS=<N> overrides (0: walk only).
+// Intra MBs are scheduled by dependency level: k_level computes every MB's level and
+// counts them, k_level_scan + k_level_scatter build one MB list per level, and
+// k_intra_levels does levels 1..N from those lists in one persistent cooperative launch
+// (a grid barrier between levels); the wavefront walk k_intra_pic takes whatever lies
+// deeper.  N = 16 by default: P / B pictures rarely go deeper, and in all-intra pictures
+// (levels x + 2y + 1) a level holds a few MBs per picture, so the walk's row-to-row
+// hand-off beats one grid barrier per level (config 2: 36.6 ms of intra walking vs 44.9
+// with every level from lists).  H264R_LEVELS=<N> overrides N (0: walk only; at most
+// LEVEL_LISTS).
 static int level_launches()
 {
     static const int env = [] { const char* e = getenv("H264R_LEVELS"); return e ? atoi(e) : 16; }();
-    return std::max(0, std::min(env, 256));
+    return std::max(0, std::min(env, LEVEL_LISTS));
 }
 
 // rows [row0, row1): the MB rows of every picture this launch reconstructs and
@@ -367,7 +379,11 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
         if (getenv("H264R_VERBOSE"))
             fprintf(stderr, "h264r: k_intra_levels occupancy %d blocks/CU, %d CUs, grid %d\n", per_cu, cus, c->levels_grid);
     }
-    if (levels && (st = dev_resize(&c->d_lvl, &c->c_lvl, (size_t)P * W * H))) return st;
+    if (levels && ((st = dev_resize(&c->d_lvl, &c->c_lvl, (size_t)P * W * H)) ||
+                   (st = dev_resize(&c->d_list, &c->c_list, (size_t)P * W * H)) ||
+                   (st = dev_resize(&c->d_lcnt, &c->c_lcnt, 3 * (size_t)(LEVEL_LISTS + 2)))))
+        return st;
+    if (levels) HIP_OK(hipMemsetAsync(c->d_lcnt, 0, 3 * (size_t)(LEVEL_LISTS + 2) * sizeof(int), s));
     HIP_OK(hipMemsetAsync(c->d_sync, 0, sync_n * sizeof(int), s));
     h264r::DbInfo* dbinfo = reinterpret_cast<h264r::DbInfo*>(c->d_dbinfo);
     int* sync = c->d_sync;
@@ -384,11 +400,36 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
         const int lmax = levels ? level_launches() : 0;
         if (levels) {
             int* lvsync = sync + 1 + (size_t)P * H + 2;
-            hipLaunchKernelGGL(k_level, dim3(P), dim3(64 * ((HB + 63) / 64)), 0, s, b, lvl, lvsync, rows);
+            int* lcount = c->d_lcnt;
+            int* lbase = lcount + (LEVEL_LISTS + 2);
+            int* lcursor = lbase + (LEVEL_LISTS + 2);
+            hipLaunchKernelGGL(k_level, dim3(P), dim3(64 * ((HB + 63) / 64)), 0, s, b, lvl, lvsync, lcount, rows);
             HIP_OK(hipGetLastError());
-            hipLaunchKernelGGL(k_intra_levels, dim3(c->levels_grid), dim3(256), 0, s, b, (const uint16_t*)lvl,
-                               lmax, lvsync, c->d_err, rows);
+            hipLaunchKernelGGL(k_level_scan, dim3(1), dim3(1024), 0, s, (const int*)lcount, lbase);
             HIP_OK(hipGetLastError());
+            hipLaunchKernelGGL(k_level_scatter, dim3(P), dim3(1024), 0, s, b, (const uint16_t*)lvl, (const int*)lbase,
+                               lcursor, c->d_list, rows);
+            HIP_OK(hipGetLastError());
+            // the grid is one block per CU below the occupancy answer (residency margin);
+            // H264R_COOP=1 launches it cooperatively instead, so that the runtime checks the
+            // grid against the occupancy query (off by default: rocprofv3 7.2 crashes at
+            // process exit after a cooperative launch)
+            static const bool coop = [] { const char* e = getenv("H264R_COOP"); return e && atoi(e) != 0; }();
+            if (coop) {
+                const int* lcount_c = lcount;
+                const int* lbase_c = lbase;
+                const uint32_t* list_c = c->d_list;
+                int lmax_v = lmax;
+                int* err_p = c->d_err;
+                void* args[] = {(void*)&b, (void*)&lcount_c, (void*)&lbase_c, (void*)&list_c, (void*)&lmax_v,
+                                (void*)&lvsync, (void*)&err_p};
+                HIP_OK(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(k_intra_levels), dim3(c->levels_grid),
+                                                  dim3(256), args, 0, s));
+            } else {
+                hipLaunchKernelGGL(k_intra_levels, dim3(c->levels_grid), dim3(256), 0, s, b, (const int*)lcount,
+                                   (const int*)lbase, (const uint32_t*)c->d_list, lmax, lvsync, c->d_err);
+                HIP_OK(hipGetLastError());
+            }
         }
         hipLaunchKernelGGL(k_intra_pic, dim3(P * nbands), dim3(1024), 0, s, b, sync, c->d_err,
                            (const uint16_t*)lvl, lmax, rows);

@@ -20,6 +20,7 @@
 #define H264R_LVL_WAVES 4
 #endif
 #define H264R_LEVEL_MAX_MBS 65536           // k_level keeps a picture's intra bitmap in LDS
+#define H264R_LEVEL_LISTS 64                // levels 1 .. this many get per-level MB lists
 
 using namespace h264r;
 
@@ -151,10 +152,14 @@ extern "C" __global__ __launch_bounds__(1024) void k_intra_pic(h264r_batch b, in
 // k_level: one workgroup per picture, thread r = MB row r, which walks its row in
 // lock step: at step t thread r does MB x = t - 2r, after (x+1, r-1) was done at
 // step t-1.  Each row keeps its last four levels in an LDS ring.
-extern "C" __global__ __launch_bounds__(1024) void k_level(h264r_batch b, uint16_t* lvl, int* lvsync, int2 rows)
+// lcount[L] (L = 1 .. H264R_LEVEL_LISTS): intra MBs of level L over the batch (zeroed per
+// batch); k_level_lists turns them into one MB list per level.
+extern "C" __global__ __launch_bounds__(1024) void k_level(h264r_batch b, uint16_t* lvl, int* lvsync, int* lcount, int2 rows)
 {
     __shared__ uint64_t bits[H264R_LEVEL_MAX_MBS / 64];   // intra (not PCM) MBs of the picture
     __shared__ uint16_t ring[1024][4];
+    __shared__ int hist[H264R_LEVEL_LISTS + 1];
+    for (int i = threadIdx.x; i <= H264R_LEVEL_LISTS; i += blockDim.x) hist[i] = 0;
     const Geom g = make_geom(b.width_mbs, b.height_mbs);
     const int pic = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
     const h264r_mb* mbs = b.mbs + (size_t)pic * g.nmb;
@@ -192,11 +197,85 @@ extern "C" __global__ __launch_bounds__(1024) void k_level(h264r_batch b, uint16
             deepest = max(deepest, L);
             ring[r][x & 3] = (uint16_t)L;
             out[x] = (uint16_t)L;
+            if (L >= 1 && L <= H264R_LEVEL_LISTS) atomicAdd(&hist[L], 1);
         }
         __syncthreads();
     }
     for (int d = 32; d >= 1; d >>= 1) deepest = max(deepest, __shfl_xor(deepest, d));
     if (lane == 0 && deepest) atomicMax(&lvsync[1], deepest);
+    for (int i = threadIdx.x + 1; i <= H264R_LEVEL_LISTS; i += blockDim.x)
+        if (hist[i]) atomicAdd(&lcount[i], hist[i]);
+}
+
+// The per-level MB lists: lbase[L] = exclusive prefix of lcount over levels (one
+// workgroup, k_level_scan), then every intra MB of level 1 .. H264R_LEVEL_LISTS appends
+// pic * nmb + addr to its level's list (k_level_scatter: a workgroup counts its MBs per
+// level in LDS and reserves each level's range with one global atomic).
+// lcount, lbase, lcursor: H264R_LEVEL_LISTS + 2 ints each.
+extern "C" __global__ __launch_bounds__(1024) void k_level_scan(const int* lcount, int* lbase)
+{
+    __shared__ int part[1024];
+    constexpr int PER = (H264R_LEVEL_LISTS + 2 + 1023) / 1024;
+    const int t = threadIdx.x;
+    int v[PER], sum = 0;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        const int i = t * PER + k;
+        v[k] = i <= H264R_LEVEL_LISTS ? lcount[i] : 0;
+        sum += v[k];
+    }
+    part[t] = sum;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {                  // inclusive scan of the per-thread sums
+        const int add = t >= o ? part[t - o] : 0;
+        __syncthreads();
+        part[t] += add;
+        __syncthreads();
+    }
+    int run = part[t] - sum;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        const int i = t * PER + k;
+        if (i <= H264R_LEVEL_LISTS + 1) lbase[i] = run;
+        run += v[k];
+    }
+}
+
+// One workgroup per picture: an LDS count per level over the picture's MBs, one global
+// atomic per (picture, level) to reserve its range, then the entries (a workgroup per
+// 256 MBs reserved per (workgroup, level) instead: 130 k atomics on a few counters,
+// 375 us per 1024 1080p pictures).
+constexpr int SCATTER_PER = 16;             // MBs per thread (1024 threads: pictures up to 16 k MBs per pass)
+extern "C" __global__ __launch_bounds__(1024) void k_level_scatter(h264r_batch b, const uint16_t* __restrict__ lvl,
+                                                                   const int* __restrict__ lbase, int* lcursor,
+                                                                   uint32_t* __restrict__ list, int2 rows)
+{
+    __shared__ int cnt[H264R_LEVEL_LISTS + 1];
+    __shared__ int res[H264R_LEVEL_LISTS + 1];
+    const Geom g = make_geom(b.width_mbs, b.height_mbs);
+    const int pic = blockIdx.x, tid = threadIdx.x;
+    const int m0 = rows.x * g.wmb, m1 = rows.y * g.wmb;
+    const uint16_t* lp = lvl + (size_t)pic * g.nmb;
+    for (int base = m0; base < m1; base += 1024 * SCATTER_PER) {
+        if (tid <= H264R_LEVEL_LISTS) cnt[tid] = 0;
+        __syncthreads();
+        int L[SCATTER_PER], rank[SCATTER_PER];
+#pragma unroll
+        for (int k = 0; k < SCATTER_PER; ++k) {
+            const int m = base + k * 1024 + tid;
+            L[k] = m < m1 ? lp[m] : 0;
+            if (L[k] < 1 || L[k] > H264R_LEVEL_LISTS) L[k] = 0;
+        }
+#pragma unroll
+        for (int k = 0; k < SCATTER_PER; ++k) rank[k] = L[k] ? atomicAdd(&cnt[L[k]], 1) : 0;
+        __syncthreads();
+        if (tid >= 1 && tid <= H264R_LEVEL_LISTS && cnt[tid]) res[tid] = atomicAdd(&lcursor[tid], cnt[tid]);
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < SCATTER_PER; ++k)
+            if (L[k]) list[lbase[L[k]] + res[L[k]] + rank[k]] = (uint32_t)((size_t)pic * g.nmb + base + k * 1024 + tid);
+        __syncthreads();
+    }
 }
 
 // k_intra_levels: the intra MBs of levels 1..min(lmax, deepest level), one level
@@ -245,58 +324,46 @@ extern "C" __global__ void k_intra_trace_dump(unsigned long long* out, unsigned*
 }
 #endif
 
-extern "C" __global__ __launch_bounds__(256, H264R_LVL_WAVES) void k_intra_levels(h264r_batch b, const uint16_t* __restrict__ lvl,
-                                                                                int lmax, int* lvsync, int* err, int2 rows)
+extern "C" __global__ __launch_bounds__(256, H264R_LVL_WAVES) void k_intra_levels(h264r_batch b, const int* __restrict__ lcount,
+                                                                                const int* __restrict__ lbase,
+                                                                                const uint32_t* __restrict__ list,
+                                                                                int lmax, int* lvsync, int* err)
 {
     __shared__ IntraScratch scratch[4];
     const Geom g = make_geom(b.width_mbs, b.height_mbs);
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const int nb = (rows.y - rows.x) * g.wmb, m0 = rows.x * g.wmb;    // band MBs per picture
-    const size_t total = (size_t)nb * b.num_pics;
-    // a wave scans `chunk` MBs at a time: 64 when the batch has work for every wave, fewer
-    // for small batches (the latency chain: one picture per launch), so that the intra MBs
-    // of a level spread over all waves instead of queueing behind one another in a few
-    const unsigned nw = gridDim.x * 4u;
-    const int chunk = (int)min((size_t)64, max((size_t)1, (total + nw - 1) / nw));
-    const size_t gw = (size_t)blockIdx.x * 4 + wave, step = (size_t)nw * chunk;
+    const int nw = (int)gridDim.x * 4, gw = (int)blockIdx.x * 4 + wave;
     const int deepest = __hip_atomic_load(&lvsync[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int top = min(lmax, deepest);
-    // the level of batch MB e (32-bit index math: P * nmb < 2^31); the load is clamped,
-    // not conditional, so the next chunk's levels can be in flight while this chunk's
-    // MBs are reconstructed
-    const unsigned total32 = (unsigned)total, nbu = (unsigned)nb;
-    auto lvl_at = [&](size_t base) -> int {
-        const unsigned e = min((unsigned)base + (unsigned)lane, total32 - 1u);
-        return lvl[(size_t)(e / nbu) * g.nmb + m0 + e % nbu];
-    };
     for (int L = 1; L <= top; ++L) {
-        int cur = lvl_at(gw * chunk);
-        for (size_t base = gw * chunk; base < total; base += step) {
-            const int nxt = lvl_at(base + step < total ? base + step : base);     // prefetch
-            const bool hit = lane < chunk && base + lane < total && cur == L;
-            uint64_t todo = __ballot(hit);
-            cur = nxt;
-            while (todo) {
-                const unsigned k = (unsigned)base + (unsigned)__builtin_ctzll(todo);
-                todo &= todo - 1;
-                const int pic = (int)(k / nbu), a = m0 + (int)(k % nbu);
+        // the MBs of level L, wave-strided over the list (entry = pic * nmb + addr)
+        const int n = lcount[L], base = lbase[L];
+        for (int e = gw; e < n; e += nw) {
+            const uint32_t k = list[base + e];
+            const int pic = (int)(k / (unsigned)g.nmb), a = (int)(k % (unsigned)g.nmb);
 #ifdef H264R_TRACE_INTRA
-                const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-#endif
-                intra_mb2(b, g, pic, a % g.wmb, a / g.wmb, lane, scratch[wave]);
-#ifdef H264R_TRACE_INTRA
-                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-                const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
-                if (lane == 0) {
-                    const unsigned slot = atomicAdd(&h264r_intra_trace_n, 1u);
-                    if (slot < (1u << 20)) {
-                        h264r_intra_trace[slot][0] = t0; h264r_intra_trace[slot][1] = t1;
-                        h264r_intra_trace[slot][2] = ((unsigned long long)L << 32) | (unsigned)(b.mbs[(size_t)pic * g.nmb + a].mb_type);
-                        h264r_intra_trace[slot][3] = (unsigned long long)gw;
+            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime(), c0 = __builtin_amdgcn_s_memtime();
+            unsigned long long tph[5] = {c0, c0, c0, c0, c0};
+            intra_mb2(b, g, pic, a % g.wmb, a / g.wmb, lane, scratch[wave], tph);
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+            if (lane == 0) {
+                const unsigned slot = atomicAdd(&h264r_intra_trace_n, 1u);
+                if (slot < (1u << 20)) {
+                    // [3]: core cycles / 16 of the phases (record, residual, tiles, prediction), 16 bits each
+                    unsigned long long ph = 0, prev = c0;
+                    for (int q = 0; q < 4; ++q) {
+                        ph |= (unsigned long long)min((tph[q] - prev) >> 4, 65535ull) << (16 * q);
+                        prev = tph[q];
                     }
+                    h264r_intra_trace[slot][0] = t0; h264r_intra_trace[slot][1] = t1;
+                    h264r_intra_trace[slot][2] = ((unsigned long long)L << 32) | (unsigned)(b.mbs[(size_t)pic * g.nmb + a].mb_type);
+                    h264r_intra_trace[slot][3] = ph;
                 }
-#endif
             }
+#else
+            intra_mb2(b, g, pic, a % g.wmb, a / g.wmb, lane, scratch[wave]);
+#endif
         }
         if (L < top && !grid_barrier(&lvsync[0], L * (int)gridDim.x, err)) return;
     }

@@ -111,32 +111,75 @@ DEV int tap_apply(int kind, int a, int b, int c)
 DEV uint32_t lds_u32(const uint8_t* p) { return *reinterpret_cast<const uint32_t*>(p); }
 DEV int sum4(uint32_t w) { return (int)__builtin_amdgcn_sad_u8(w, 0u, 0u); }   // sum of the 4 bytes
 
-// Chroma residual of one MB in the inter_mb2 lane layout (transform.cc:875-889 DC,
-// inverse_4x4 for the AC blocks): lane = plane << 5 | blk << 3 | half << 2 | row,
-// two samples (cols 2*half, +1).  `tab` = 0 intra, 1 inter scale tables.
-DEV void chroma_res2(const h264r_mb& m, const int16_t* __restrict__ lv, const h264r_quant* __restrict__ q, int tab,
-                     int lane, int (&resC)[2])
+// Every level and scale an intra MB's residual needs, loaded in ONE batch right after
+// the MB record (the residual used to take two or three dependent round trips:
+// luma levels, then the I_16x16 DC levels, then chroma -- profiles/r02_intra_phases.txt).
+// Every load is unconditional: a lane without data reads the quant table and drops it
+// (a load in a lane-divergent branch merges through a copy that waits for everything).
+// (plain dwords: HIP's uint2 / uint4 unions in a struct passed around end up on the stack)
+struct IntraLoads {
+    uint32_t lev[2], sc[2]; // luma: 4x4 layout (lane = blk * 4 + row) or, I_8x8, (k, row, half)
+    uint32_t dc[8];         // I_16x16: the 16 DC levels (raster)
+    int dc_scale;           // I_16x16: scale4x4[0][0][qp % 6][0]
+    uint32_t cdc[2];        // chroma: the plane's 4 DC levels
+    int cdc_scale;
+    uint32_t clev, csc;     // chroma AC: two levels and their scales
+    bool lev_ok;            // lev holds coded levels (else: use 0)
+};
+
+// Branch-free: every address is a select, every load is issued, and a lane's "no data"
+// case is applied where the value is used -- a load under a branch, or a select on a
+// loaded value right after it, makes the compiler wait for it there.
+DEV IntraLoads intra_loads(const h264r_mb& m, const int16_t* __restrict__ lv, const h264r_quant* __restrict__ q, int lane)
+{
+    IntraLoads L;
+    const int qp = m.qp_scaled[0], rem = qp % 6;
+    const LevelOffs lo = level_offsets(m);
+    const int16_t* dummy = &q->scale4x4[0][0][0][0];
+    const bool i8 = m.mb_type == H264R_I_8x8;
+    // I_8x8 layout: k = lane >> 4, row, half; 4x4 layout: blk = lane >> 2, row
+    const int k8 = lane >> 4, row8 = (lane >> 1) & 7, half8 = lane & 1;
+    const int blk = lane >> 2, r4 = lane & 3, bx = blk & 3, by = blk >> 2;
+    const int off = b8_offset(m.cbp, i8 ? k8 : (by >> 1) * 2 + (bx >> 1));
+    const int within = i8 ? row8 * 8 + half8 * 4 : ((by & 1) * 2 + (bx & 1)) * 16 + r4 * 4;
+    L.lev_ok = off >= 0;
+    const uint2 lv2 = ld8(off >= 0 ? lv + off + within : dummy);
+    const uint2 sc2 = ld8(i8 ? &q->scale8x8[0][0][rem][row8 * 8 + half8 * 4] : &q->scale4x4[0][0][rem][r4 * 4]);
+    L.lev[0] = lv2.x; L.lev[1] = lv2.y; L.sc[0] = sc2.x; L.sc[1] = sc2.y;
+    const uint4* dcp = reinterpret_cast<const uint4*>(lo.ldc >= 0 ? lv + lo.ldc : dummy);
+    const uint4 d0 = dcp[0], d1 = dcp[1];
+    L.dc[0] = d0.x; L.dc[1] = d0.y; L.dc[2] = d0.z; L.dc[3] = d0.w;
+    L.dc[4] = d1.x; L.dc[5] = d1.y; L.dc[6] = d1.z; L.dc[7] = d1.w;
+    L.dc_scale = q->scale4x4[0][0][rem][0];
+    const int cpl = lane >> 5, cb = (lane >> 3) & 3, chalf = (lane >> 2) & 1, crow = lane & 3;
+    const int qpc = (cpl ? m.qp_scaled[2] : m.qp_scaled[1]);
+    const uint2 cd = ld8(lo.cdc >= 0 ? lv + lo.cdc + cpl * 4 : dummy);
+    L.cdc[0] = cd.x; L.cdc[1] = cd.y;
+    L.cdc_scale = q->scale4x4[0][1 + cpl][qpc % 6][0];
+    L.clev = *reinterpret_cast<const uint32_t*>(lo.cac >= 0 ? lv + lo.cac + cpl * 64 + cb * 16 + crow * 4 + chalf * 2 : dummy);
+    L.csc = *reinterpret_cast<const uint32_t*>(&q->scale4x4[0][1 + cpl][qpc % 6][crow * 4 + chalf * 2]);
+    return L;
+}
+
+// Chroma residual of one MB (transform.cc:875-889 DC, inverse_4x4 for the AC blocks):
+// lane = plane << 5 | blk << 3 | half << 2 | row, two samples (cols 2*half, +1).
+DEV void chroma_res2(const h264r_mb& m, const IntraLoads& L, int lane, int (&resC)[2])
 {
     const int cpl = lane >> 5, cb = (lane >> 3) & 3, chalf = (lane >> 2) & 1, crow = lane & 3;
     const int cbpc = m.cbp >> 4;
     resC[0] = resC[1] = 0;
     if (!cbpc) return;
-    const LevelOffs lo = level_offsets(m);
-    const int qpc = m.qp_scaled[1 + cpl], per = qpc / 6;
-    const uint2 cdc = ld8(lv + lo.cdc + cpl * 4);
-    const int cdc_scale = q->scale4x4[tab][1 + cpl][qpc % 6][0];
+    const int qpc = (cpl ? m.qp_scaled[2] : m.qp_scaled[1]), per = qpc / 6;
     int k0 = 0, k1 = 0;
     if (cbpc == 2) {
-        const uint32_t clev = *reinterpret_cast<const uint32_t*>(lv + lo.cac + cpl * 64 + cb * 16 + crow * 4 + chalf * 2);
-        const uint32_t csc = *reinterpret_cast<const uint32_t*>(&q->scale4x4[tab][1 + cpl][qpc % 6][crow * 4 + chalf * 2]);
-        k0 = dq4((int16_t)(clev & 0xFFFF), (int16_t)(csc & 0xFFFF), per);
-        k1 = dq4((int16_t)(clev >> 16), (int16_t)(csc >> 16), per);
+        k0 = dq4((int16_t)(L.clev & 0xFFFF), (int16_t)(L.csc & 0xFFFF), per);
+        k1 = dq4((int16_t)(L.clev >> 16), (int16_t)(L.csc >> 16), per);
     }
-    const int c00 = (int16_t)(cdc.x & 0xFFFF), c01 = (int16_t)(cdc.x >> 16);
-    const int c10 = (int16_t)(cdc.y & 0xFFFF), c11 = (int16_t)(cdc.y >> 16);
+    const int c00 = (int16_t)(L.cdc[0] & 0xFFFF), c01 = (int16_t)(L.cdc[0] >> 16);
+    const int c10 = (int16_t)(L.cdc[1] & 0xFFFF), c11 = (int16_t)(L.cdc[1] >> 16);
     const int e00 = c00 + c01, e01 = c00 - c01, e10 = c10 + c11, e11 = c10 - c11;
     const int f = cb == 0 ? e00 + e10 : cb == 1 ? e01 + e11 : cb == 2 ? e00 - e10 : e01 - e11;
-    if (crow == 0 && chalf == 0) k0 = ((f * cdc_scale) * (1 << per)) >> 5;
+    if (crow == 0 && chalf == 0) k0 = ((f * L.cdc_scale) * (1 << per)) >> 5;
     const int o0 = __shfl_xor(k0, 4), o1 = __shfl_xor(k1, 4);
     const int d0 = chalf ? o0 : k0, d1 = chalf ? o1 : k1, d2 = chalf ? k0 : o0, d3 = chalf ? k1 : o1;
     int t[4];
@@ -149,38 +192,34 @@ DEV void chroma_res2(const h264r_mb& m, const int16_t* __restrict__ lv, const h2
 // Luma residual of an I_4x4 / I_16x16 MB in registers: lane = blk * 4 + row (blk
 // raster over the 4x4 block grid), four samples.  I_16x16 DC: 4x4 Hadamard and
 // scaling of transform_luma_dc (transform.cc:825-856), evaluated per lane.
-DEV void luma_res4_intra(const h264r_mb& m, const int16_t* __restrict__ lv, const h264r_quant* __restrict__ q,
-                         int lane, int (&res)[4])
+DEV void luma_res4_intra(const h264r_mb& m, const IntraLoads& L, int lane, int (&res)[4])
 {
     const int blk = lane >> 2, r = lane & 3, bx = blk & 3, by = blk >> 2;
-    const int qp = m.qp_scaled[0], per = qp / 6, rem = qp % 6;
+    const int qp = m.qp_scaled[0], per = qp / 6;
     const bool i16 = m.mb_type == H264R_I_16x16;
-    const int loff = b8_offset(m.cbp, (by >> 1) * 2 + (bx >> 1));
-    // both loads issued unconditionally (a lane without levels reads the scale table
-    // and drops the value): a load inside a lane-divergent branch merges through a copy
-    // whose vmcnt(0) serialises it behind everything issued before
-    uint2 lev = ld8(loff >= 0 ? (const void*)(lv + loff + ((by & 1) * 2 + (bx & 1)) * 16 + r * 4) : (const void*)q);
-    const uint2 sc = ld8(&q->scale4x4[0][0][rem][r * 4]);
-    if (loff < 0) lev = make_uint2(0, 0);
+    const uint32_t lev0 = L.lev_ok ? L.lev[0] : 0u, lev1 = L.lev_ok ? L.lev[1] : 0u;
     int d[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-        const int l = (int16_t)((c & 2 ? lev.y : lev.x) >> (16 * (c & 1)));
-        const int s = (int16_t)((c & 2 ? sc.y : sc.x) >> (16 * (c & 1)));
+        const int l = (int16_t)((c & 2 ? lev1 : lev0) >> (16 * (c & 1)));
+        const int s = (int16_t)((c & 2 ? L.sc[1] : L.sc[0]) >> (16 * (c & 1)));
         d[c] = dq4(l, s, per);
     }
     if (i16) {
-        const int16_t* p = lv + level_offsets(m).ldc;     // 16 DC levels, raster, wave-uniform
+        const uint32_t (&w)[8] = L.dc;
         const int mx = (0xA6C0 >> (4 * bx)) & 15, my = (0xA6C0 >> (4 * by)) & 15;   // Hadamard sign masks
         int f = 0;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             int s = 0;
 #pragma unroll
-            for (int l = 0; l < 4; ++l) s += ((mx >> l) & 1) ? -p[4 * k + l] : p[4 * k + l];
+            for (int l = 0; l < 4; ++l) {
+                const int v = (int16_t)(w[(4 * k + l) >> 1] >> (16 * (l & 1)));
+                s += ((mx >> l) & 1) ? -v : v;
+            }
             f += ((my >> k) & 1) ? -s : s;
         }
-        const int scale = q->scale4x4[0][0][rem][0];
+        const int scale = L.dc_scale;
         const int dc = qp >= 36 ? (f * scale) * (1 << (per - 6)) : (f * scale + (1 << (5 - per))) >> (6 - per);
         if (r == 0) d[0] = dc;
     }
@@ -192,22 +231,16 @@ DEV void luma_res4_intra(const h264r_mb& m, const int16_t* __restrict__ lv, cons
 }
 
 // Luma residual of an I_8x8 MB (inverse_8x8, transform.cc:643-733) into S.res.
-DEV void luma_res8_intra(const h264r_mb& m, const int16_t* __restrict__ lv, const h264r_quant* __restrict__ q,
-                         int lane, IntraScratch& S)
+DEV void luma_res8_intra(const h264r_mb& m, const IntraLoads& L, int lane, IntraScratch& S)
 {
     const int k = lane >> 4, row = (lane >> 1) & 7, half = lane & 1;
-    const int qp = m.qp_scaled[0], per = qp / 6, rem = qp % 6;
-    const int off = b8_offset(m.cbp, k);
-    int d[4] = {0, 0, 0, 0};
-    {
-        uint2 lev = ld8(off >= 0 ? (const void*)(lv + off + row * 8 + half * 4) : (const void*)q);   // unconditional
-        const uint2 sc = ld8(&q->scale8x8[0][0][rem][row * 8 + half * 4]);
-        if (off < 0) lev = make_uint2(0, 0);
+    const int qp = m.qp_scaled[0], per = qp / 6;
+    const uint32_t lev0 = L.lev_ok ? L.lev[0] : 0u, lev1 = L.lev_ok ? L.lev[1] : 0u;
+    int d[4];
 #pragma unroll
-        for (int c = 0; c < 4; ++c)
-            d[c] = dq8((int16_t)((c & 2 ? lev.y : lev.x) >> (16 * (c & 1))),
-                       (int16_t)((c & 2 ? sc.y : sc.x) >> (16 * (c & 1))), per);
-    }
+    for (int c = 0; c < 4; ++c)
+        d[c] = dq8((int16_t)((c & 2 ? lev1 : lev0) >> (16 * (c & 1))),
+                   (int16_t)((c & 2 ? L.sc[1] : L.sc[0]) >> (16 * (c & 1))), per);
     // row pass: the other half of my row is in lane ^ 1
     int in[8], out[8];
 #pragma unroll
@@ -234,21 +267,32 @@ DEV void luma_res8_intra(const h264r_mb& m, const int16_t* __restrict__ lv, cons
     wave_sync();
 }
 
-// Intra MB (mbx, mby) of picture `pic` (no-op for inter / I_PCM MBs); one wave.
-DEV void intra_mb2(const h264r_batch& b, const Geom& g, int pic, int mbx, int mby, int lane, IntraScratch& S)
+// The loads of one intra MB, in two stages: IntraHead needs nothing (neighbour samples,
+// neighbour records, the MB record), IntraLoads needs the MB record (levels, scales).
+// (Issuing both for the next MB while the current one is reconstructed held two MBs'
+// records in SGPRs and spilled: 120 SGPRs, 55 VGPRs at 4 waves/SIMD.)
+// The records are wave-uniform scalar loads (constant address space: immutable during
+// a batch).
+struct IntraHead {
+    uint32_t nb;                 // this lane's neighbour sample dword (masked)
+    uint32_t nw0[4], nw2[4];     // neighbour records A, B, C, D: dwords 0 (type, flags) and 2 (cbp_blks, slice)
+    h264r_mb m;
+    int cip;
+    uint32_t nin;                // bit k: neighbour k inside the picture
+};
+
+DEV IntraHead intra_head(const h264r_batch& b, const Geom& g, int pic, int mbx, int mby, int lane)
 {
+    IntraHead h;
     const int a = mby * g.wmb + mbx;
     const h264r_mb* mbs = b.mbs + (size_t)pic * g.nmb;
     const PicPtrs o = out_planes(b, g, pic);
     const int X = mbx * 16, Y = mby * 16, Xc = mbx * 8, Yc = mby * 8;
-
-    // ---- neighbour samples: issued before anything else (in-picture addresses only;
-    // availability decides later which of them are used)
-    // One dword load per lane, all issued at once (a left-column sample is the top byte
-    // of the aligned dword that ends at x - 1; lanes with nothing to fetch read their own
+    // ---- neighbour samples (in-picture addresses only; availability decides later which
+    // of them are used): one dword load per lane (a left-column sample is the top byte of
+    // the aligned dword that ends at x - 1; lanes with nothing to fetch read their own
     // MB's first row and drop it).  Loads in lane-divergent branches would each merge
     // through a copy whose vmcnt(0) serialises them.
-    uint32_t nb = 0;
     {
         const uint8_t* src = o.y + (size_t)Y * g.W + X;
         bool want = false, left = false;
@@ -269,48 +313,72 @@ DEV void intra_mb2(const h264r_batch& b, const Geom& g, int pic, int mbx, int mb
             src = want ? (pl ? o.v : o.u) + (size_t)(Yc + (k & 7)) * g.Wc + Xc - 4 : src;
         }
         const uint32_t w = *as_global(src);
-        nb = (w >> (left ? 24 : 0)) & (0u - (uint32_t)want);   // arithmetic, not a select: no branch
+        h.nb = (w >> (left ? 24 : 0)) & (0u - (uint32_t)want);   // arithmetic, not a select: no branch
     }
-    // neighbour MB records A, B, C, D: dwords 0 (type, flags) and 2 (cbp_blks, slice), all
-    // loaded before any decision (get_neighbour + slice check + constrained intra,
-    // intra_prediction.cc:142-168 / 629-651 / 753-777)
-    uint32_t nw0[4], nw2[4];
-    bool nin[4];
+    // neighbour records (get_neighbour + slice check + constrained intra,
+    // intra_prediction.cc:142-168 / 629-651 / 753-777) and the MB record
+    h.nin = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const int nx = mbx + (k == 0 || k == 3 ? -1 : (k == 2 ? 1 : 0)), ny = mby - (k == 0 ? 0 : 1);
-        nin[k] = nx >= 0 && ny >= 0 && nx < g.wmb && ny < g.hmb;
-        const uint32_t* p = reinterpret_cast<const uint32_t*>(&mbs[nin[k] ? ny * g.wmb + nx : a]);
-        nw0[k] = ld_const(p);
-        nw2[k] = ld_const(p + 2);
+        const bool in = nx >= 0 && ny >= 0 && nx < g.wmb && ny < g.hmb;
+        h.nin |= (uint32_t)in << k;
+        const uint32_t* p = reinterpret_cast<const uint32_t*>(&mbs[in ? ny * g.wmb + nx : a]);
+        h.nw0[k] = ld_const(p);
+        h.nw2[k] = ld_const(p + 2);
     }
-    const h264r_mb m = load_mb_const(&mbs[a]);
+    h.cip = ld_const(&b.pics[pic].constrained_intra_pred);
+    h.m = load_mb_const(&mbs[a]);
+    return h;
+}
+
+DEV IntraLoads intra_body_loads(const h264r_batch& b, int pic, const IntraHead& h, int lane)
+{
+    return intra_loads(h.m, b.levels + h.m.coef_off, &b.quant[pic], lane);
+}
+
+// Intra MB (mbx, mby) of picture `pic` from its loads (no-op for inter / I_PCM MBs); one
+// wave.  tph (trace builds): s_memtime at the phase boundaries [record known, residual,
+// tiles, prediction, end].
+DEV void intra_mb_compute(const h264r_batch& b, const Geom& g, int pic, int mbx, int mby, int lane, IntraScratch& S,
+                          const IntraHead& hd, const IntraLoads& ld, unsigned long long* tph = nullptr)
+{
+#define INTRA_STAMP(k) do { if (tph) tph[k] = __builtin_amdgcn_s_memtime(); } while (0)
+    const PicPtrs o = out_planes(b, g, pic);
+    const int X = mbx * 16, Y = mby * 16, Xc = mbx * 8, Yc = mby * 8;
+    const h264r_mb& m = hd.m;
+    const uint32_t nb = hd.nb;
+    // the 16 intra 4x4 / 4 intra 8x8 modes as one 64-bit word (h264r_mb::ipred, dwords 5-6):
+    // indexed per lane by shifts, not through the record's bytes (that puts it on the stack)
+    const uint64_t ipw = (uint64_t)reinterpret_cast<const uint32_t*>(&m)[5] |
+                         ((uint64_t)reinterpret_cast<const uint32_t*>(&m)[6] << 32);
     if (!mb_is_intra(m) || m.mb_type == H264R_I_PCM) return;
-    const int cip = b.pics[pic].constrained_intra_pred;
+    INTRA_STAMP(0);
     auto avail = [&](int k) -> int {
-        return nin[k] && (int)(nw2[k] >> 16) == (int)m.slice && !(cip && !((nw0[k] >> 8) & H264R_MBF_INTRA));
+        return ((hd.nin >> k) & 1) && (int)(hd.nw2[k] >> 16) == (int)m.slice && !(hd.cip && !((hd.nw0[k] >> 8) & H264R_MBF_INTRA));
     };
     const int avA = avail(0), avB = avail(1), avC = avail(2), avD = avail(3);
-    const int16_t* lv = b.levels + m.coef_off;
-    const h264r_quant* __restrict__ q = &b.quant[pic];
     const bool i16 = m.mb_type == H264R_I_16x16, i8 = m.mb_type == H264R_I_8x8;
 
     // ---- residual (registers; 8x8 via LDS)
     int resL[4] = {0, 0, 0, 0}, resC[2];
-    if (!i8) luma_res4_intra(m, lv, q, lane, resL);
-    chroma_res2(m, lv, q, 0, lane, resC);
+    if (!i8) luma_res4_intra(m, ld, lane, resL);
+    chroma_res2(m, ld, lane, resC);
+    if (tph) { asm volatile("; stamp after residual" ::"v"(resL[0]), "v"(resC[0])); }
+    INTRA_STAMP(1);
 
     // ---- neighbours into the tiles
     if (lane < 7) *reinterpret_cast<uint32_t*>(&S.tile[4 * lane]) = nb;
     else if (lane < 23) S.tile[ti(-1, lane - 7)] = (uint8_t)nb;
     else if (lane < 29) { const int k = lane - 23; *reinterpret_cast<uint32_t*>(&S.ctile[k / 3][4 * (k % 3)]) = nb; }
     else if (lane < 45) { const int k = lane - 29; S.ctile[k >> 3][ci(-1, k & 7)] = (uint8_t)nb; }
-    if (i8) luma_res8_intra(m, lv, q, lane, S);        // includes wave_syncs
+    if (i8) luma_res8_intra(m, ld, lane, S);           // includes wave_syncs
     else if (!i16) {
         const int blk = lane >> 2, r = lane & 3;
         *reinterpret_cast<int4*>(&S.res[(blk >> 2) * 4 + r][(blk & 3) * 4]) = make_int4(resL[0], resL[1], resL[2], resL[3]);
     }
     wave_sync();
+    INTRA_STAMP(2);
     const int cbpl = m.cbp & 15;
 
     if (i16) {
@@ -360,7 +428,7 @@ DEV void intra_mb2(const h264r_batch& b, const Geom& g, int pic, int mbx, int mb
             const int aA = xO > 0 ? 1 : avA, aB = yO > 0 ? 1 : avB;
             const int aD = (xO > 0 && yO > 0) ? 1 : (xO == 0 && yO == 0) ? avD : (xO == 0 ? avA : avB);
             const int aC = yO > 0 ? (xO == 0) : (xO == 0 ? avB : avC);   // intra_prediction.cc:370-376
-            const int mode = (m.ipred[blk >> 1] >> ((blk & 1) * 4)) & 15;
+            const int mode = (int)((ipw >> (4 * blk)) & 15);
             // reference sample filtering (intra_prediction.cc:413-447) -> S.fs
             auto po = [&](int x, int y) -> int {
                 if (y < 0 && x >= 8 && !aC) x = 7;                   // p(x,-1) substitution :404-407
@@ -431,7 +499,7 @@ DEV void intra_mb2(const h264r_batch& b, const Geom& g, int pic, int mbx, int mb
                 int aC;
                 if (yO == 0) aC = xO + 4 < 16 ? avB : avC;
                 else aC = (xO + 4 < 16) && !(xO == 4 && (yO == 4 || yO == 12));      // :154
-                const int mode = (m.ipred[bk >> 1] >> ((bk & 1) * 4)) & 15;
+                const int mode = (int)((ipw >> (4 * bk)) & 15);
                 // branch-free: the directional tap and DC are both evaluated, then selected
                 const int ent = intra_tap_entry(tab, mode), kind = ent >> 5, i = ent & 31;
                 const int tmax = aC ? 7 : 3;
@@ -451,6 +519,7 @@ DEV void intra_mb2(const h264r_batch& b, const Geom& g, int pic, int mbx, int mb
             wave_sync();
         }
     }
+    INTRA_STAMP(3);
     if (!i16) {
         const int y = lane >> 2, x0 = (lane & 3) * 4;
         *reinterpret_cast<uint32_t*>(o.y + (size_t)(Y + y) * g.W + X + x0) = lds_u32(&S.tile[ti(x0, y)]);
@@ -499,6 +568,18 @@ DEV void intra_mb2(const h264r_batch& b, const Geom& g, int pic, int mbx, int mb
         const uint32_t w = (uint32_t)clip255(p[0] + resC[0]) | ((uint32_t)clip255(p[1] + resC[1]) << 8);
         *reinterpret_cast<uint16_t*>((pl ? o.v : o.u) + (size_t)(Yc + y) * g.Wc + Xc + x0) = (uint16_t)w;
     }
+    INTRA_STAMP(4);
+#undef INTRA_STAMP
+}
+
+// Loads then reconstruction of one intra MB (the walk, k_intra_pic).
+DEV void intra_mb2(const h264r_batch& b, const Geom& g, int pic, int mbx, int mby, int lane, IntraScratch& S,
+                   unsigned long long* tph = nullptr)
+{
+    const IntraHead hd = intra_head(b, g, pic, mbx, mby, lane);
+    if (!mb_is_intra(hd.m) || hd.m.mb_type == H264R_I_PCM) return;
+    const IntraLoads ld = intra_body_loads(b, pic, hd, lane);
+    intra_mb_compute(b, g, pic, mbx, mby, lane, S, hd, ld, tph);
 }
 
 }  // namespace h264r

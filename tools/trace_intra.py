@@ -36,6 +36,8 @@ print("MBs", cnt.value)
 for Lv in np.unique(lvl):
     m = lvl == Lv
     print(f"level {Lv}: n={m.sum()} start {start[m].min():.1f}..{start[m].max():.1f} us  end {(start[m] + dur[m]).max():.1f}  dur mean {dur[m].mean():.2f} p50 {np.median(dur[m]):.2f} max {dur[m].max():.2f}")
+ph = np.stack([((t[:, 3] >> (16 * k)) & 0xFFFF).astype(np.int64) * 16 for k in range(4)], 1)   # core cycles
 for ty in np.unique(typ):
     m = typ == ty
-    print(f"type {ty}: n={m.sum()} dur mean {dur[m].mean():.2f} p50 {np.median(dur[m]):.2f}")
+    print(f"type {ty}: n={m.sum()} dur mean {dur[m].mean():.2f} p50 {np.median(dur[m]):.2f}  "
+          f"cycles to record / residual / tiles / prediction: {np.round(ph[m].mean(0), 0)}")
