@@ -11,6 +11,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("dir")
 ap.add_argument("--mbs", type=float, default=0, help="macroblocks per dispatch (for per-MB figures)")
 ap.add_argument("--json", default=None, help="write per-kernel HBM traffic per MB (bytes) to this file")
+ap.add_argument("--config", type=int, default=3, help="SURVEY config of the profiled bench run (bench.py matches it)")
 a = ap.parse_args()
 
 for f in glob.glob(os.path.join(a.dir, "stats", "**", "*kernel_stats.csv"), recursive=True):
@@ -33,7 +34,7 @@ for k, cs in vals.items():
 
 if a.json and a.mbs:
     import json
-    out = {"source": os.path.basename(os.path.normpath(a.dir)), "mbs_per_dispatch": a.mbs,
+    out = {"source": os.path.basename(os.path.normpath(a.dir)), "survey_config": a.config, "mbs_per_dispatch": a.mbs,
            "note": "FETCH_SIZE / WRITE_SIZE are KiB per dispatch (rocprofv3, separate --pmc passes). "
                    "gfx950 reports half the bytes of wide coalesced reads (MI355X_MICROARCH.md, HBM): "
                    "read_bytes_per_mb doubles FETCH_SIZE (an upper bound for narrower access), "
