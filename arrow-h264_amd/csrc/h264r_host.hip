@@ -574,8 +574,10 @@ int h264r_mb_submit(h264r_ctx* c, int addr, const h264r_mb* mb, const int16_t* l
     if (!c->in_pic) return H264R_ESTATE;
     const int n = c->pw * c->ph;
     if (addr < 0 || addr >= n || !mb || n_levels < 0 || (n_levels && !levels) || !mv || !ref_idx) return H264R_EINVAL;
-    if (mb->flags & H264R_MBF_BYPASS) return H264R_EUNSUPPORTED;
     if (mb->slice >= c->h_pic.num_slices) return H264R_EINVAL;
+    // lossless inter MBs: the kernels take intra_chroma_pred_mode as DC, which is what the
+    // parser leaves in an inter MB (macroblock_t::init, slice_data.cc:482)
+    if ((mb->flags & H264R_MBF_BYPASS) && !(mb->flags & H264R_MBF_INTRA) && mb->chroma_mode != 0) return H264R_EINVAL;
     h264r_mb m = *mb;
     // append the level block, 16-byte aligned
     while (c->h_levels.size() % 8) c->h_levels.push_back(0);

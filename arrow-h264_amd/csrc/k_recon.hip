@@ -12,7 +12,7 @@ using namespace h264r;
 
 // Grid (ceil(nmb / 16), pictures).
 #ifndef H264R_INTER_WAVES
-#define H264R_INTER_WAVES 1                 // minimum waves per SIMD asked of the register allocator
+#define H264R_INTER_WAVES 3                 // minimum waves per SIMD asked of the register allocator (<= 168 VGPRs)
 #endif
 extern "C" __global__ __launch_bounds__(256, H264R_INTER_WAVES) void k_inter4(h264r_batch b, DbInfo* dbinfo, int2 rows)
 {

@@ -372,6 +372,7 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
         for (int i = 0; i < 4; ++i)
     #pragma unroll
             for (int c = 0; c < 4; ++c) res[i][c] = 0;
+        const bool byp = (q.flags & H264R_MBF_BYPASS) != 0;
         if (__any(cbpl != 0)) {
             const int per = qpl / 6;
             int d[4][4];
@@ -383,8 +384,46 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
                     const uint32_t lo_ = (i & 1) ? lw.z : lw.x, hi_ = (i & 1) ? lw.w : lw.y;
                     const uint32_t slo = (i & 1) ? sw.z : sw.x, shi = (i & 1) ? sw.w : sw.y;
                     const int lvv = sel16(lo_, hi_, c), scv = sel16(slo, shi, c);
-                    d[i][c] = t8 ? dq8(lvv, scv, per) : dq4(lvv, scv, per);
+                    d[i][c] = byp ? lvv : (t8 ? dq8(lvv, scv, per) : dq4(lvv, scv, per));
                 }
+            // lossless MBs (TransformBypassModeFlag): the levels are the residual, DPCM'd in
+            // place down the columns / along the rows when the block's Intra4x4PredMode /
+            // Intra8x8PredMode is vertical / horizontal (bypass_4x4 / bypass_8x8
+            // transform.cc:736-778; inverse_transform_4x4 / _8x8 :986-1016 read those modes
+            // for inter MBs too: whatever the parser's mb_t slot holds).  The flag is
+            // uniform over an MB's 16 lanes, so the cross-lane carries stay inside the branch.
+            if (byp) {
+                const uint32_t* qw = reinterpret_cast<const uint32_t*>(&q);
+                const uint64_t ipw = (uint64_t)qw[5] | ((uint64_t)qw[6] << 32);
+                const int bk = t8 ? b8 : (by >> 1) * 8 + (bx >> 1) * 4 + (by & 1) * 2 + (bx & 1);
+                const int mode = (int)((ipw >> (4 * bk)) & 15);
+                const bool vert = mode == 0, horz = mode == 1;
+    #pragma unroll
+                for (int i = 1; i < 4; ++i)
+    #pragma unroll
+                    for (int c = 0; c < 4; ++c) d[i][c] += vert ? d[i - 1][c] : 0;
+    #pragma unroll
+                for (int c = 1; c < 4; ++c)
+    #pragma unroll
+                    for (int i = 0; i < 4; ++i) d[i][c] += horz ? d[i][c - 1] : 0;
+                // 8x8: the quadrant above (lane ^ 4) / to the left (lane ^ 1) carries in
+    #pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const int up = __shfl_xor(d[3][c], 4);
+    #pragma unroll
+                    for (int i = 0; i < 4; ++i) d[i][c] += (t8 && vert && (by & 1)) ? up : 0;
+                }
+    #pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int left = __shfl_xor(d[i][3], 1);
+    #pragma unroll
+                    for (int c = 0; c < 4; ++c) d[i][c] += (t8 && horz && (bx & 1)) ? left : 0;
+                }
+    #pragma unroll
+                for (int i = 0; i < 4; ++i)
+    #pragma unroll
+                    for (int c = 0; c < 4; ++c) res[i][c] = d[i][c];
+            } else
             if (!__any(t8 != 0)) {
                 // 4x4: rows then columns, all in-lane
     #pragma unroll
@@ -453,12 +492,14 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
             int rc[2][2] = {{0, 0}, {0, 0}};
             if (__any(cbpc != 0)) {
                 const int qpc = q.qp_scaled[1 + pl], per = qpc / 6;
-                int k[2][2];
+                int k[2][2], raw[2][2];
     #pragma unroll
                 for (int r = 0; r < 2; ++r)
     #pragma unroll
-                    for (int c = 0; c < 2; ++c)
-                        k[r][c] = dq4((int16_t)(clev[pl][r] >> (16 * c)), (int16_t)(csc[pl][r] >> (16 * c)), per);
+                    for (int c = 0; c < 2; ++c) {
+                        raw[r][c] = (int16_t)(clev[pl][r] >> (16 * c));
+                        k[r][c] = dq4(raw[r][c], (int16_t)(csc[pl][r] >> (16 * c)), per);
+                    }
                 const int c00 = (int16_t)(cdc[pl].x & 0xFFFF), c01 = (int16_t)(cdc[pl].x >> 16);
                 const int c10 = (int16_t)(cdc[pl].y & 0xFFFF), c11 = (int16_t)(cdc[pl].y >> 16);
                 const int e00 = c00 + c01, e01 = c00 - c01, e10 = c10 + c11, e11 = c10 - c11;
@@ -484,6 +525,16 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
                     idct4(d0, d1, d2, d3, y0, y1, y2, y3);
                     rc[0][c] = ((cr ? y2 : y0) + 32) >> 6;
                     rc[1][c] = ((cr ? y3 : y1) + 32) >> 6;
+                }
+                // lossless: the raw levels, DC at (0,0) (transform.cc:453-455,860); an inter MB's
+                // intra_chroma_pred_mode is DC (macroblock_t::init slice_data.cc:482), so
+                // bypass_chroma (:802-822) copies
+                if (byp) {
+                    const int dcl = cb == 0 ? c00 : cb == 1 ? c01 : cb == 2 ? c10 : c11;
+    #pragma unroll
+                    for (int r = 0; r < 2; ++r)
+    #pragma unroll
+                        for (int c = 0; c < 2; ++c) rc[r][c] = (cr == 0 && cc == 0 && r == 0 && c == 0) ? dcl : raw[r][c];
                 }
             }
             uint8_t* cdst = (pl ? o.v : o.u) + coff;

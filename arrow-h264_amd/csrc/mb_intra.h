@@ -34,7 +34,8 @@ constexpr int ICP = 16;   // chroma tile pitch: x = -4..11
 struct IntraScratch {
     alignas(16) uint8_t tile[17 * ITP];
     alignas(16) uint8_t ctile[2][9 * ICP];
-    alignas(16) int res[16][16];          // luma residual (I_4x4 / I_8x8)
+    alignas(16) int res[16][16];          // luma residual (I_4x4 / I_8x8; every type when lossless)
+    alignas(16) int cres[2][8][8];        // chroma residual of lossless MBs
     alignas(16) uint8_t fs[32];           // I_8x8 filtered neighbours: [3] Q, [4 + x] T[x], [20 + y] L[y]
 };
 
@@ -267,6 +268,93 @@ DEV void luma_res8_intra(const h264r_mb& m, const IntraLoads& L, int lane, Intra
     wave_sync();
 }
 
+// Lossless DPCM of one line of n residual samples in place (transform.cc:736-822: a vertical
+// mode accumulates down a column, a horizontal mode along a row; `step` is the distance of
+// consecutive samples of the line).
+DEV void dpcm_line(int* p, int step, int n)
+{
+    int acc = 0;
+    for (int i = 0; i < n; ++i) { acc += p[i * step]; p[i * step] = acc; }
+}
+
+// Residual of a TransformBypassModeFlag MB (interpret_mb.cc:804): the levels are the
+// residual (coeff_luma_ac / coeff_chroma_ac skip inverse_quantize, transform.cc:439-455; the
+// DC transforms do nothing, :827,860), DPCM'd along the prediction direction of each block
+// (bypass_4x4/8x8/16x16/chroma, :736-822, chosen by inverse_transform_* :986-1049).  The
+// final luma residual is left in S.res (every MB type), I_16x16's also in resL (its
+// register layout), chroma in resC.
+DEV void intra_bypass_res(const h264r_mb& m, const int16_t* __restrict__ lv, int lane, IntraScratch& S, uint64_t ipw,
+                          int (&resL)[4], int (&resC)[2])
+{
+    // the raw levels are loaded again here (rare MBs, L2-hot): keeping IntraLoads live into
+    // this branch spilled the kernel
+    const bool i8 = m.mb_type == H264R_I_8x8, i16 = m.mb_type == H264R_I_16x16;
+    const LevelOffs lo = level_offsets(m);
+    const int blk = lane >> 2, r = lane & 3, bx = blk & 3, by = blk >> 2;
+    {
+        const int k8 = lane >> 4, row8 = (lane >> 1) & 7, half8 = lane & 1;
+        const int off = b8_offset(m.cbp, i8 ? k8 : (by >> 1) * 2 + (bx >> 1));
+        const int within = i8 ? row8 * 8 + half8 * 4 : ((by & 1) * 2 + (bx & 1)) * 16 + r * 4;
+        uint2 w = ld8(lv + (off >= 0 ? off + within : 0));
+        if (off < 0) w = make_uint2(0, 0);
+        int v[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) v[c] = (int16_t)((c & 2 ? w.y : w.x) >> (16 * (c & 1)));
+        if (i8) {
+            *reinterpret_cast<int4*>(&S.res[(k8 >> 1) * 8 + row8][(k8 & 1) * 8 + half8 * 4]) = make_int4(v[0], v[1], v[2], v[3]);
+        } else {
+            if (i16 && r == 0) v[0] = lv[lo.ldc + 4 * by + bx];          // DC at (0,0)
+            *reinterpret_cast<int4*>(&S.res[by * 4 + r][bx * 4]) = make_int4(v[0], v[1], v[2], v[3]);
+        }
+    }
+    const int cpl = lane >> 5, cb = (lane >> 3) & 3, chalf = (lane >> 2) & 1, crow = lane & 3;
+    const int cbpc = m.cbp >> 4;
+    int c0 = 0, c1 = 0;
+    if (cbpc == 2) {
+        const uint32_t w = *reinterpret_cast<const uint32_t*>(lv + lo.cac + cpl * 64 + cb * 16 + crow * 4 + chalf * 2);
+        c0 = (int16_t)(w & 0xFFFF);
+        c1 = (int16_t)(w >> 16);
+    }
+    if (cbpc && crow == 0 && chalf == 0) c0 = lv[lo.cdc + cpl * 4 + cb];
+    const int cy = (cb >> 1) * 4 + crow, cx = (cb & 1) * 4 + chalf * 2;
+    S.cres[cpl][cy][cx] = c0;
+    S.cres[cpl][cy][cx + 1] = c1;
+    wave_sync();
+    // one line per lane: vertical = 0 / horizontal = 1 for luma, 2 / 1 for chroma
+    if (i8) {
+        if (lane < 32) {
+            const int b = lane >> 3, t = lane & 7, mode = (int)((ipw >> (4 * b)) & 15);
+            int* o = &S.res[(b >> 1) * 8][(b & 1) * 8];
+            if (mode == 0) dpcm_line(o + t, 16, 8);
+            else if (mode == 1) dpcm_line(o + t * 16, 1, 8);
+        }
+    } else if (i16) {
+        if (lane < 16) {
+            if (m.i16_mode == 0) dpcm_line(&S.res[0][lane], 16, 16);
+            else if (m.i16_mode == 1) dpcm_line(&S.res[lane][0], 1, 16);
+        }
+    } else {
+        const int bk = (by >> 1) * 8 + (bx >> 1) * 4 + (by & 1) * 2 + (bx & 1);   // blkIdx
+        const int mode = (int)((ipw >> (4 * bk)) & 15);
+        int* o = &S.res[by * 4][bx * 4];
+        if (mode == 0) dpcm_line(o + r, 16, 4);
+        else if (mode == 1) dpcm_line(o + r * 16, 1, 4);
+    }
+    if (lane < 16) {
+        int* o = &S.cres[lane >> 3][0][0];
+        const int t = lane & 7;
+        if (m.chroma_mode == 2) dpcm_line(o + t, 8, 8);
+        else if (m.chroma_mode == 1) dpcm_line(o + t * 8, 1, 8);
+    }
+    wave_sync();
+    if (i16) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) resL[c] = S.res[by * 4 + r][bx * 4 + c];
+    }
+    resC[0] = S.cres[cpl][cy][cx];
+    resC[1] = S.cres[cpl][cy][cx + 1];
+}
+
 // The loads of one intra MB, in two stages: IntraHead needs nothing (neighbour samples,
 // neighbour records, the MB record), IntraLoads needs the MB record (levels, scales).
 // (Issuing both for the next MB while the current one is reconstructed held two MBs'
@@ -360,19 +448,28 @@ DEV void intra_mb_compute(const h264r_batch& b, const Geom& g, int pic, int mbx,
     const int avA = avail(0), avB = avail(1), avC = avail(2), avD = avail(3);
     const bool i16 = m.mb_type == H264R_I_16x16, i8 = m.mb_type == H264R_I_8x8;
 
-    // ---- residual (registers; 8x8 via LDS)
-    int resL[4] = {0, 0, 0, 0}, resC[2];
+    // ---- residual (registers; 8x8 via LDS; lossless MBs via LDS)
+    const bool byp = (m.flags & H264R_MBF_BYPASS) != 0;
+    int resL[4] = {0, 0, 0, 0}, resC[2] = {0, 0};
     if (!i8) luma_res4_intra(m, ld, lane, resL);
     chroma_res2(m, ld, lane, resC);
     if (tph) { asm volatile("; stamp after residual" ::"v"(resL[0]), "v"(resC[0])); }
     INTRA_STAMP(1);
 
     // ---- neighbours into the tiles
-    if (lane < 7) *reinterpret_cast<uint32_t*>(&S.tile[4 * lane]) = nb;
-    else if (lane < 23) S.tile[ti(-1, lane - 7)] = (uint8_t)nb;
-    else if (lane < 29) { const int k = lane - 23; *reinterpret_cast<uint32_t*>(&S.ctile[k / 3][4 * (k % 3)]) = nb; }
-    else if (lane < 45) { const int k = lane - 29; S.ctile[k >> 3][ci(-1, k & 7)] = (uint8_t)nb; }
-    if (i8) luma_res8_intra(m, ld, lane, S);           // includes wave_syncs
+    {
+        // one LDS byte offset per lane (one live register, not four hoisted addresses)
+        const int kc = lane < 29 ? lane - 23 : lane - 29;
+        const int at = lane < 7 ? 4 * lane
+                     : lane < 23 ? ti(-1, lane - 7)
+                     : lane < 29 ? (int)offsetof(IntraScratch, ctile) + (kc / 3) * 9 * ICP + 4 * (kc % 3)
+                                 : (int)offsetof(IntraScratch, ctile) + (kc >> 3) * 9 * ICP + ci(-1, kc & 7);
+        uint8_t* base = reinterpret_cast<uint8_t*>(&S);
+        if (lane < 7 || (lane >= 23 && lane < 29)) *reinterpret_cast<uint32_t*>(base + at) = nb;
+        else if (lane < 45) base[at] = (uint8_t)nb;
+    }
+    if (byp) intra_bypass_res(m, b.levels + m.coef_off, lane, S, ipw, resL, resC);   // S.res too
+    else if (i8) luma_res8_intra(m, ld, lane, S);      // includes wave_syncs
     else if (!i16) {
         const int blk = lane >> 2, r = lane & 3;
         *reinterpret_cast<int4*>(&S.res[(blk >> 2) * 4 + r][(blk & 3) * 4]) = make_int4(resL[0], resL[1], resL[2], resL[3]);

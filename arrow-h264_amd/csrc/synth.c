@@ -247,6 +247,10 @@ int h264r_synth_picture(const h264r_synth_cfg* c, int index, h264r_mb* mbs, int1
 
         int qp = rrange(&r, c->qp_min, c->qp_max);
         if (pcm) qp = 0;
+        else if (c->lossless_permille && rnd(&r, 1000) < c->lossless_permille) qp = 0;
+        /* TransformBypassModeFlag = qpprime_y_zero_transform_bypass_flag && qp_scaled[0] == 0
+           (interpret_mb.cc:804); I_PCM ignores it */
+        const int bypass = c->lossless_permille > 0 && qp == 0 && !pcm;
         m->qp_y = (int8_t)qp;
         int qc = clip3i(0, 51, qp);   /* chroma_qp_index_offset 0 (update_qp :784-805) */
         qc = qc < 30 ? qc : QP_SCALE_CR[qc];
@@ -340,6 +344,14 @@ int h264r_synth_picture(const h264r_synth_cfg* c, int index, h264r_mb* mbs, int1
             if (mt == H264R_P_SKIP && !bslice) t8 = 0;
         }
         if (t8) m->flags |= H264R_MBF_T8x8;
+        if (bypass) {
+            m->flags |= H264R_MBF_BYPASS;
+            /* an inter MB's Intra4x4PredMode / Intra8x8PredMode are whatever the mb_t slot
+               held (macroblock_t::init, slice_data.cc:455-503, does not reset them), and the
+               reference's bypass reads them for the DPCM direction (transform.cc:993,1008) */
+            if (!is_intra)
+                for (int b = 0; b < 8; ++b) m->ipred[b] = (uint8_t)(rnd(&r, 9) | (rnd(&r, 9) << 4));
+        }
         m->cbp = (uint8_t)(cbpl | (cbpc << 4));
 
         /* levels, in the compacted layout of include/h264r.h */

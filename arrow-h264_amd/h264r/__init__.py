@@ -102,6 +102,17 @@ def quant_flat() -> np.ndarray:
     return q
 
 
+def quant_lists(m4: np.ndarray, m8: np.ndarray) -> np.ndarray:
+    """h264r_quant_init_lists from resolved scaling matrices: m4 [6][16] (Intra Y/Cb/Cr, Inter
+    Y/Cb/Cr), m8 [6][64] (Intra Y, Inter Y, Intra Cb, Inter Cb, Intra Cr, Inter Cr), raster."""
+    m4 = np.ascontiguousarray(m4, np.int32).reshape(6, 16)
+    m8 = np.ascontiguousarray(m8, np.int32).reshape(6, 64)
+    arr = (C.c_void_p * 12)(*([m4[i].ctypes.data for i in range(6)] + [m8[i].ctypes.data for i in range(6)]))
+    q = np.zeros(1, QUANT_DTYPE)
+    _check("h264r_quant_init_lists", lib().h264r_quant_init_lists(A.ptr(q), arr))
+    return q
+
+
 class Decoder:
     """One reconstruction context on one GPU (reference: one Decoder per slice_t)."""
 

@@ -56,7 +56,7 @@ class SynthCfg(C.Structure):
         ("constrained_intra", C.c_int32), ("num_refs", C.c_int32),
         ("qp_min", C.c_int32), ("qp_max", C.c_int32), ("pcm_permille", C.c_int32),
         ("intra_permille", C.c_int32), ("mv_range_x", C.c_int32),
-        ("mv_range_y", C.c_int32), ("seed", C.c_uint64),
+        ("mv_range_y", C.c_int32), ("lossless_permille", C.c_int32), ("seed", C.c_uint64),
     ]
 
     def as_dict(self) -> dict:

@@ -94,7 +94,10 @@ extern "C" {
 /* ---- h264r_mb.flags ---------------------------------------------------------- */
 #define H264R_MBF_INTRA   0x01   /* mb_t::is_intra_block            */
 #define H264R_MBF_T8x8    0x02   /* mb_t::transform_size_8x8_flag   */
-#define H264R_MBF_BYPASS  0x04   /* mb_t::TransformBypassModeFlag (unsupported -> EUNSUPPORTED) */
+#define H264R_MBF_BYPASS  0x04   /* mb_t::TransformBypassModeFlag (lossless: levels are the residual,
+                                    DPCM by the block's ipred mode -- for inter MBs too, as the
+                                    reference reads Intra4x4/8x8PredMode there, transform.cc:993,1008;
+                                    an inter MB's chroma_mode must be 0, the parser's value) */
 
 /* 32-byte macroblock record (fields named after mb_t, macroblock.h:78-135). */
 typedef struct h264r_mb {

@@ -41,6 +41,11 @@ typedef struct h264r_synth_cfg {
     int32_t  pcm_permille;       /* I_PCM MBs per 1000 MBs (0 for the bench configs)      */
     int32_t  intra_permille;     /* intra MBs in P/B pictures (default 100)               */
     int32_t  mv_range_x, mv_range_y;   /* integer-pel MV range (default 64 / 32)          */
+    int32_t  lossless_permille;  /* sps.qpprime_y_zero_transform_bypass_flag when > 0: this
+                                    many MBs per 1000 get QP'Y 0, and every MB at QP'Y 0 is a
+                                    TransformBypassModeFlag MB (interpret_mb.cc:804); inter
+                                    bypass MBs carry random Intra4x4/8x8PredMode values, which
+                                    the reference's bypass DPCM reads for them (transform.cc:993,1008) */
     uint64_t seed;
 } h264r_synth_cfg;
 

@@ -63,6 +63,24 @@ void oracle_quant_init_flat(h264r_quant* q)
             }
 }
 
+/* Explicit scaling matrices qmatrix[0..11] (already resolved, raster order: 4x4 lists
+ * Intra Y/Cb/Cr, Inter Y/Cb/Cr; 8x8 lists Intra Y, Inter Y, Intra Cb, Inter Cb, Intra Cr,
+ * Inter Cr) x dequant_coef, as Transform::set_quant does (transform.cc:259-302). */
+void oracle_quant_init_lists(h264r_quant* q, const int32_t* m4 /*[6][16]*/, const int32_t* m8 /*[6][64]*/)
+{
+    for (int pl = 0; pl < 3; ++pl)
+        for (int m = 0; m < 6; ++m) {
+            for (int k = 0; k < 16; ++k) {
+                q->scale4x4[0][pl][m][k] = (int16_t)(dequant_coef[m][k / 4][k % 4] * m4[pl * 16 + k]);
+                q->scale4x4[1][pl][m][k] = (int16_t)(dequant_coef[m][k / 4][k % 4] * m4[(3 + pl) * 16 + k]);
+            }
+            for (int k = 0; k < 64; ++k) {
+                q->scale8x8[0][pl][m][k] = (int16_t)(dq8(m, k / 8, k % 8) * m8[(2 * pl) * 64 + k]);
+                q->scale8x8[1][pl][m][k] = (int16_t)(dq8(m, k / 8, k % 8) * m8[(2 * pl + 1) * 64 + k]);
+            }
+        }
+}
+
 /* --------------------------------------------- level block layout (include/h264r.h) */
 typedef struct {
     const int16_t* b8[4];   /* NULL when the 8x8 is not coded */
@@ -157,11 +175,62 @@ static void inverse_8x8(int d[16][16], int r[16][16], int py, int px)   /* trans
     }
 }
 
+/* Lossless residual DPCM (transform.cc:736-822): a vertical mode accumulates down the
+ * columns, a horizontal mode along the rows, any other mode copies.  `vert` / `horz` are
+ * the mode values of the block size (0 / 1 for 4x4, 8x8, 16x16; 2 / 1 for chroma). */
+static void bypass_block(int r[16][16], int f[16][16], int x0, int y0, int w, int h, int mode, int vert, int horz)
+{
+    for (int y = 0; y < h; ++y)
+        for (int x = 0; x < w; ++x) {
+            int v = r[y0 + y][x0 + x];
+            if (mode == vert && y > 0) v += f[y0 + y - 1][x0 + x];
+            else if (mode == horz && x > 0) v += f[y0 + y][x0 + x - 1];
+            f[y0 + y][x0 + x] = v;
+        }
+}
+
+/* TransformBypassModeFlag MBs: levels stay raw (coeff_luma_ac / coeff_chroma_ac skip
+ * inverse_quantize, transform.cc:439-441,453-455; transform_luma_dc / transform_chroma_dc
+ * do nothing, :827,860), DC levels at the (0,0) of their 4x4 blocks. */
+static void load_cof_bypass(const h264r_mb* mb, const int16_t* pool, int cof[3][16][16])
+{
+    levels_view v = view_levels(mb, pool);
+    int t8 = (mb->flags & H264R_MBF_T8x8) != 0;
+    if (v.ldc)
+        for (int i = 0; i < 4; ++i)
+            for (int j = 0; j < 4; ++j) cof[0][i * 4][j * 4] = v.ldc[i * 4 + j];
+    for (int b8 = 0; b8 < 4; ++b8) {
+        const int16_t* blk = v.b8[b8];
+        if (!blk) continue;
+        for (int b4 = 0; b4 < 4; ++b4)
+            for (int pos = 0; pos < 16; ++pos) {
+                if (v.ldc && pos == 0 && !t8) continue;
+                if (t8) {
+                    int k = b4 * 16 + pos;
+                    cof[0][(b8 >> 1) * 8 + k / 8][(b8 & 1) * 8 + k % 8] = blk[k];
+                } else {
+                    int bx = (b8 & 1) * 2 + (b4 & 1), by = (b8 >> 1) * 2 + (b4 >> 1);
+                    cof[0][by * 4 + pos / 4][bx * 4 + pos % 4] = blk[b4 * 16 + pos];
+                }
+            }
+    }
+    for (int pl = 1; pl <= 2; ++pl) {
+        if (v.cdc)
+            for (int i = 0; i < 2; ++i)
+                for (int j = 0; j < 2; ++j) cof[pl][i * 4][j * 4] = v.cdc[(pl - 1) * 4 + i * 2 + j];
+        if (v.cac)
+            for (int b = 0; b < 4; ++b)
+                for (int pos = 1; pos < 16; ++pos)
+                    cof[pl][(b / 2) * 4 + pos / 4][(b % 2) * 4 + pos % 4] = v.cac[(pl - 1) * 64 + b * 16 + pos];
+    }
+}
+
 /* Coefficient push: coeff_luma_ac/coeff_chroma_ac + inverse_quantize (transform.cc:394-456),
  * transform_luma_dc (:825-856), transform_chroma_dc (:858-910). */
 static void load_cof(const h264r_mb* mb, const int16_t* pool, const h264r_quant* q, int cof[3][16][16])
 {
     memset(cof, 0, sizeof(int) * 3 * 16 * 16);
+    if (mb->flags & H264R_MBF_BYPASS) { load_cof_bypass(mb, pool, cof); return; }
     levels_view v = view_levels(mb, pool);
     int inter = (mb->flags & H264R_MBF_INTRA) ? 0 : 1;
     int t8 = (mb->flags & H264R_MBF_T8x8) != 0;
@@ -660,6 +729,28 @@ static void construct(const pstate* s, int addr, int pl, int x0, int y0, int w, 
 
 static int intra4_mode(const h264r_mb* mb, int blk) { return (mb->ipred[blk >> 1] >> ((blk & 1) * 4)) & 15; }
 
+/* inverse_transform_4x4 / _8x8 of one coded block (transform.cc:986-1016): the inverse
+ * transform, or for TransformBypassModeFlag MBs the DPCM of the block's Intra4x4PredMode /
+ * Intra8x8PredMode (read for inter MBs too, :993,1008). */
+static void luma_block_res(const h264r_mb* mb, int cof[16][16], int rres[16][16], int x, int y, int n)
+{
+    int bk = n == 4 ? ((y / 4) / 2) * 8 + ((y / 4) % 2) * 2 + ((x / 4) / 2) * 4 + ((x / 4) % 2)
+                    : (y / 8) * 2 + x / 8;
+    if (mb->flags & H264R_MBF_BYPASS) bypass_block(cof, rres, x, y, n, n, intra4_mode(mb, bk), 0, 1);
+    else if (n == 4) inverse_4x4(cof, rres, y, x);
+    else inverse_8x8(cof, rres, y, x);
+}
+
+/* inverse_transform_16x16 / inverse_transform_chroma residual (transform.cc:1018-1049) */
+static void mb_res(const h264r_mb* mb, int pl, int cof[16][16], int rres[16][16])
+{
+    int n = pl ? 8 : 16;
+    if (mb->flags & H264R_MBF_BYPASS)
+        bypass_block(cof, rres, 0, 0, n, n, pl ? mb->chroma_mode : mb->i16_mode, pl ? 2 : 0, 1);
+    else
+        for (int y = 0; y < n; y += 4) for (int x = 0; x < n; x += 4) inverse_4x4(cof, rres, y, x);
+}
+
 /* Decoder::decode (decoder.cc:65-262) for one MB. */
 static int decode_mb(pstate* s, int addr)
 {
@@ -668,7 +759,6 @@ static int decode_mb(pstate* s, int addr)
     int mbx = addr % s->wmb, mby = addr / s->wmb;
     static __thread int cof[3][16][16], rres[3][16][16], mbp[3][16][16];
     s->slice_nr[addr] = (int16_t)mb->slice;               /* mb.init, slice_data.cc:465 */
-    if (mb->flags & H264R_MBF_BYPASS) return H264R_EUNSUPPORTED;
 
     if (mb->mb_type == H264R_I_PCM) {                      /* mb_pred_ipcm decoder.cc:149-168 */
         const uint8_t* raw = (const uint8_t*)(p->levels + mb->coef_off);
@@ -694,7 +784,7 @@ static int decode_mb(pstate* s, int addr)
                 gather_nxn(s, addr, 4, ioff, joff, img, s->W, &n);
                 pred_4x4(&n, intra4_mode(mb, b), mbp[0], ioff, joff);
                 int coded = cbpl & (1 << ((joff / 8) * 2 + ioff / 8));
-                if (coded) inverse_4x4(cof[0], rres[0], joff, ioff);
+                if (coded) luma_block_res(mb, cof[0], rres[0], ioff, joff, 4);
                 construct(s, addr, 0, ioff, joff, 4, 4, coded, rres[0], mbp[0]);
             } else if (mb->mb_type == H264R_I_8x8) {
                 nbr_t n, f;
@@ -702,11 +792,11 @@ static int decode_mb(pstate* s, int addr)
                 filter_8x8(&n, &f);
                 pred_8x8(&f, intra4_mode(mb, b / 4), mbp[0], ioff, joff);
                 int coded = cbpl & (1 << ((joff / 8) * 2 + ioff / 8));
-                if (coded) inverse_8x8(cof[0], rres[0], joff, ioff);
+                if (coded) luma_block_res(mb, cof[0], rres[0], ioff, joff, 8);
                 construct(s, addr, 0, ioff, joff, 8, 8, coded, rres[0], mbp[0]);
             } else {
                 pred_mb(s, addr, 0, mb->i16_mode, img, s->W, mbp[0]);
-                for (int y = 0; y < 16; y += 4) for (int x = 0; x < 16; x += 4) inverse_4x4(cof[0], rres[0], y, x);
+                mb_res(mb, 0, cof[0], rres[0]);
                 construct(s, addr, 0, 0, 0, 16, 16, 1, rres[0], mbp[0]);
             }
         }
@@ -714,7 +804,7 @@ static int decode_mb(pstate* s, int addr)
             pred_mb(s, addr, 1, mb->chroma_mode, p->out[pl], s->Wc, mbp[pl]);
         }
         for (int pl = 1; pl <= 2; ++pl) {                  /* inverse_transform_chroma :1033-1049 */
-            for (int y = 0; y < 8; y += 4) for (int x = 0; x < 8; x += 4) inverse_4x4(cof[pl], rres[pl], y, x);
+            mb_res(mb, pl, cof[pl], rres[pl]);
             construct(s, addr, pl, 0, 0, 8, 8, 1, rres[pl], mbp[pl]);
         }
         return 0;
@@ -728,21 +818,21 @@ static int decode_mb(pstate* s, int addr)
             for (int y = 0; y < 16; y += 4)
                 for (int x = 0; x < 16; x += 4) {
                     int coded = cbpl & (1 << ((y / 8) * 2 + x / 8));
-                    if (coded) inverse_4x4(cof[0], rres[0], y, x);
+                    if (coded) luma_block_res(mb, cof[0], rres[0], x, y, 4);
                     construct(s, addr, 0, x, y, 4, 4, coded, rres[0], mbp[0]);
                 }
         } else {
             for (int y = 0; y < 16; y += 8)
                 for (int x = 0; x < 16; x += 8) {
                     int coded = cbpl & (1 << ((y / 8) * 2 + x / 8));
-                    if (coded) inverse_8x8(cof[0], rres[0], y, x);
+                    if (coded) luma_block_res(mb, cof[0], rres[0], x, y, 8);
                     construct(s, addr, 0, x, y, 8, 8, coded, rres[0], mbp[0]);
                 }
         }
     } else construct(s, addr, 0, 0, 0, 16, 16, 0, rres[0], mbp[0]);
     for (int pl = 1; pl <= 2; ++pl) {
         if (cbpc) {
-            for (int y = 0; y < 8; y += 4) for (int x = 0; x < 8; x += 4) inverse_4x4(cof[pl], rres[pl], y, x);
+            mb_res(mb, pl, cof[pl], rres[pl]);
             construct(s, addr, pl, 0, 0, 8, 8, 1, rres[pl], mbp[pl]);
         } else construct(s, addr, pl, 0, 0, 8, 8, 0, rres[pl], mbp[pl]);
     }

@@ -15,7 +15,10 @@
  * Reference pictures are padded with the reference's own pad_buf (picture.cc:182).
  *
  * usage: ref_driver W H kind nslices idc offA offB t8 wp cip nrefs qpmin qpmax
- *                   pcm_permille intra_permille mvx mvy seed index out.yuv [recon_only]
+ *                   pcm_permille intra_permille mvx mvy seed index out.yuv [recon_only
+ *                   [lossless_permille]]
+ * lossless_permille > 0 sets sps.qpprime_y_zero_transform_bypass_flag (the synthetic
+ * pictures then hold TransformBypassModeFlag MBs, interpret_mb.cc:804).
  * Output: Y plane then Cb then Cr, 8-bit, unpadded.
  *
  * Timing mode (H264R_TIME_REPS=<n>): the reconstruction of the picture -- the
@@ -78,6 +81,7 @@ int main(int argc, char** argv)
     int index = atoi(argv[k++]);
     const char* out_path = argv[k++];
     bool recon_only = argc > k && atoi(argv[k]) != 0;
+    if (argc > k + 1) cfg.lossless_permille = atoi(argv[k + 1]);
 
     const int W = cfg.width_mbs, H = cfg.height_mbs, NMB = W * H, W4 = W * 4, PL = W4 * H * 4;
     std::vector<h264r_mb> mbs(NMB);
@@ -104,6 +108,22 @@ int main(int argc, char** argv)
     sps->PicWidthInMbs = W; sps->FrameHeightInMbs = H;
     sps->PicWidthInSamplesL = W * 16; sps->PicWidthInSamplesC = W * 8;
     sps->PicHeightInMapUnits = H; sps->PicSizeInMapUnits = W * H;
+    sps->qpprime_y_zero_transform_bypass_flag = cfg.lossless_permille > 0;
+    /* H264R_QMATRIX=<file>: 6x16 + 6x64 int32 raster scaling lists, every one present in
+     * the SPS (Transform::init then takes them as they are, transform.cc:183-214) */
+    if (const char* qm = getenv("H264R_QMATRIX")) {
+        FILE* f = fopen(qm, "rb");
+        int32_t v[6 * 16 + 6 * 64];
+        if (!f || fread(v, sizeof(v), 1, f) != 1) { fprintf(stderr, "cannot read %s\n", qm); return 2; }
+        fclose(f);
+        sps->seq_scaling_matrix_present_flag = 1;
+        for (int i = 0; i < 12; ++i) sps->seq_scaling_list_present_flag[i] = 1;
+        for (int i = 0; i < 6; ++i) {
+            sps->UseDefaultScalingMatrix4x4Flag[i] = 0; sps->UseDefaultScalingMatrix8x8Flag[i] = 0;
+            for (int k = 0; k < 16; ++k) sps->ScalingList4x4[i][k] = v[i * 16 + k];
+            for (int k = 0; k < 64; ++k) sps->ScalingList8x8[i][k] = v[96 + i * 64 + k];
+        }
+    }
     pps->entropy_coding_mode_flag = 0;
     pps->weighted_pred_flag = cfg.kind == H264R_SYNTH_P && cfg.wp_mode == 1;
     pps->weighted_bipred_idc = cfg.kind == H264R_SYNTH_B ? cfg.wp_mode : 0;
@@ -227,7 +247,12 @@ int main(int argc, char** argv)
         mb.CodedBlockPatternChroma = c.cbp >> 4;
         mb.QpY = c.qp_y; mb.QpC[0] = c.qp_c[0]; mb.QpC[1] = c.qp_c[1];
         mb.qp_scaled[0] = c.qp_scaled[0]; mb.qp_scaled[1] = c.qp_scaled[1]; mb.qp_scaled[2] = c.qp_scaled[2];
-        mb.TransformBypassModeFlag = 0;
+        /* interpret_mb.cc:804 */
+        mb.TransformBypassModeFlag = sps->qpprime_y_zero_transform_bypass_flag && mb.qp_scaled[0] == 0;
+        if (mb.TransformBypassModeFlag != ((c.flags & H264R_MBF_BYPASS) != 0) && c.mb_type != H264R_I_PCM) {
+            fprintf(stderr, "bypass flag mismatch at MB %d\n", a);
+            return 4;
+        }
         memset(mb.cbp_blks, 0, sizeof(mb.cbp_blks));
         /* partition shape for the reference's own partition walk (decoder.cc:217-254) */
         if (!mb.is_intra_block) {

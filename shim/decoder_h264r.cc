@@ -357,7 +357,6 @@ void Decoder::decode(mb_t& mb)
     slice_t& slice = *mb.p_Slice;
     Shim& S = shim();
     const int (*cof)[16][16] = this->transform->cof;
-    if (mb.TransformBypassModeFlag) check(H264R_EUNSUPPORTED, "lossless (TransformBypassModeFlag) macroblocks");
     const int si = slice_index(S, &slice);
     if (si < 0) check(H264R_ESTATE, "decode() before init() of its slice");
 
@@ -365,7 +364,8 @@ void Decoder::decode(mb_t& mb)
     h264r_mb& r = st.rec;
     memset(&r, 0, sizeof(r));
     r.mb_type = mb.mb_type;
-    r.flags = (mb.is_intra_block ? H264R_MBF_INTRA : 0) | (mb.transform_size_8x8_flag ? H264R_MBF_T8x8 : 0);
+    r.flags = (mb.is_intra_block ? H264R_MBF_INTRA : 0) | (mb.transform_size_8x8_flag ? H264R_MBF_T8x8 : 0) |
+              (mb.TransformBypassModeFlag ? H264R_MBF_BYPASS : 0);
     const int cbpl = mb.CodedBlockPatternLuma, cbpc = mb.CodedBlockPatternChroma;
     r.cbp = (uint8_t)(cbpl | cbpc << 4);
     r.qp_y = mb.QpY;
@@ -379,6 +379,15 @@ void Decoder::decode(mb_t& mb)
         for (int b = 0; b < 4; ++b) r.ipred[b >> 1] |= (uint8_t)((mb.Intra8x8PredMode[b] & 15) << ((b & 1) * 4));
     else if (mb.mb_type == I_4x4)
         for (int b = 0; b < 16; ++b) r.ipred[b >> 1] |= (uint8_t)((mb.Intra4x4PredMode[b] & 15) << ((b & 1) * 4));
+    else if (mb.TransformBypassModeFlag && !mb.is_intra_block) {
+        // a lossless inter MB: the reference's bypass DPCM reads the mb_t slot's
+        // Intra4x4PredMode / Intra8x8PredMode (transform.cc:993,1008), which the parser does
+        // not reset for inter MBs -- pass on whatever they hold
+        if (mb.transform_size_8x8_flag)
+            for (int b = 0; b < 4; ++b) r.ipred[b >> 1] |= (uint8_t)((mb.Intra8x8PredMode[b] & 15) << ((b & 1) * 4));
+        else
+            for (int b = 0; b < 16; ++b) r.ipred[b >> 1] |= (uint8_t)((mb.Intra4x4PredMode[b] & 15) << ((b & 1) * 4));
+    }
 
     // the level block (include/h264r.h layout) from the raw levels in cof
     std::vector<int16_t>& lv = st.levels;

@@ -64,6 +64,8 @@ def lib() -> C.CDLL:
         for f in ("oracle_decode_picture", "oracle_reconstruct_picture", "oracle_deblock_picture"):
             getattr(L, f).argtypes = [C.POINTER(OraclePicture)]
             getattr(L, f).restype = C.c_int
+        L.oracle_quant_init_lists.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+        L.oracle_quant_init_lists.restype = None
         L.oracle_decode_pictures.argtypes = [C.POINTER(OraclePicture), C.c_int, C.c_int]
         L.oracle_decode_pictures.restype = C.c_int
         _lib = L
@@ -73,6 +75,21 @@ def lib() -> C.CDLL:
 def quant_flat() -> np.ndarray:
     q = np.zeros(1, A.QUANT_DTYPE)
     lib().oracle_quant_init_flat(A.ptr(q))
+    return q
+
+
+def qmatrix(seed: int):
+    """Deterministic explicit scaling lists for the synthetic fixtures: (m4 [6][16], m8 [6][64])
+    int32, raster order, values 4..64 (7.4.2.1.1.1 allows 1..255)."""
+    rng = np.random.default_rng(seed)
+    return (rng.integers(4, 65, (6, 16)).astype(np.int32), rng.integers(4, 65, (6, 64)).astype(np.int32))
+
+
+def quant_lists(m4: np.ndarray, m8: np.ndarray) -> np.ndarray:
+    q = np.zeros(1, A.QUANT_DTYPE)
+    a4 = np.ascontiguousarray(m4, np.int32)          # kept alive across the call
+    a8 = np.ascontiguousarray(m8, np.int32)
+    lib().oracle_quant_init_lists(A.ptr(q), A.ptr(a4), A.ptr(a8))
     return q
 
 
@@ -95,12 +112,13 @@ def new_planes(W: int, H: int):
             np.zeros((8 * H, 8 * W), np.uint8))
 
 
-def decode(p: synth.Picture, refs=None, stage: str = "full"):
-    """Oracle output planes (Y, Cb, Cr) for one synthetic picture."""
+def decode(p: synth.Picture, refs=None, stage: str = "full", quant=None):
+    """Oracle output planes (Y, Cb, Cr) for one synthetic picture (flat scaling
+    matrices unless `quant` is given)."""
     L = lib()
     if refs is None:
         refs = synth.refpics(L, p.cfg)
-    q = quant_flat()
+    q = quant_flat() if quant is None else quant
     out = new_planes(p.cfg.width_mbs, p.cfg.height_mbs)
     o = make_oracle_picture(p, refs, q, out)
     fn = {"full": L.oracle_decode_picture, "recon": L.oracle_reconstruct_picture}[stage]
@@ -110,10 +128,11 @@ def decode(p: synth.Picture, refs=None, stage: str = "full"):
     return out
 
 
-def run_reference(cfg: A.SynthCfg, index: int, recon_only: bool = False, time_reps: int = 0):
+def run_reference(cfg: A.SynthCfg, index: int, recon_only: bool = False, time_reps: int = 0, qm=None):
     """Planes produced by the compiled reference decoder (this container only).  With
     time_reps > 0 the driver reconstructs the picture that many times on one thread and
-    (planes, macroblocks, seconds) is returned (ref_driver.cc timing mode)."""
+    (planes, macroblocks, seconds) is returned (ref_driver.cc timing mode).  qm = (m4, m8):
+    explicit SPS scaling lists (all present)."""
     drv = build_ref()
     W, H = cfg.width_mbs, cfg.height_mbs
     with tempfile.TemporaryDirectory() as td:
@@ -121,8 +140,16 @@ def run_reference(cfg: A.SynthCfg, index: int, recon_only: bool = False, time_re
         args = [drv, W, H, cfg.kind, cfg.num_slices, cfg.deblock_idc, cfg.filter_offset_a,
                 cfg.filter_offset_b, cfg.transform8x8, cfg.wp_mode, cfg.constrained_intra,
                 cfg.num_refs, cfg.qp_min, cfg.qp_max, cfg.pcm_permille, cfg.intra_permille,
-                cfg.mv_range_x, cfg.mv_range_y, hex(cfg.seed), index, out, int(recon_only)]
-        env = dict(os.environ, H264R_TIME_REPS=str(time_reps)) if time_reps else None
+                cfg.mv_range_x, cfg.mv_range_y, hex(cfg.seed), index, out, int(recon_only),
+                cfg.lossless_permille]
+        env = dict(os.environ)
+        if time_reps:
+            env["H264R_TIME_REPS"] = str(time_reps)
+        if qm is not None:
+            qf = os.path.join(td, "qm.bin")
+            np.concatenate([np.ascontiguousarray(qm[0], np.int32).ravel(),
+                            np.ascontiguousarray(qm[1], np.int32).ravel()]).tofile(qf)
+            env["H264R_QMATRIX"] = qf
         r = subprocess.run([str(a) for a in args], capture_output=True, text=True, env=env)
         if r.returncode != 0:
             raise RuntimeError(f"ref_driver failed ({r.returncode}): {r.stderr[-2000:]}")

@@ -62,6 +62,19 @@ CASES = [
     ("intra_1080p", 2, 120, 68, {}, [0]),
     ("p_1080p", 3, 120, 68, {}, [0]),
     ("b_1080p_4slices", 4, 120, 68, {}, [0]),
+    ("b_2160p_strip", 5, 240, 8, dict(num_slices=2), [0]),
+    # lossless (qpprime_y_zero_transform_bypass_flag, TransformBypassModeFlag MBs; F12)
+    ("intra_qcif_lossless", 2, 11, 9, dict(qp_min=0, qp_max=30, lossless_permille=400, pcm_permille=20), [0, 1]),
+    ("intra_qcif_lossless_4x4", 2, 11, 9, dict(qp_min=0, qp_max=10, transform8x8=0, lossless_permille=300), [0]),
+    ("p_qcif_lossless_t8", 3, 11, 9, dict(qp_min=0, qp_max=30, lossless_permille=400, transform8x8=1,
+                                          intra_permille=300), [0, 1]),
+    ("b_qcif_lossless", 4, 11, 9, dict(qp_min=0, qp_max=20, lossless_permille=500), [0]),
+    # explicit scaling matrices (SPS lists, all present; Transform::init/set_quant transform.cc:173-302)
+    ("intra_qcif_scaling", 2, 11, 9, dict(qm=14), [0]),
+    ("p_qcif_scaling_t8", 3, 11, 9, dict(transform8x8=1, qm=15), [0]),
+    ("b_qcif_scaling", 4, 11, 9, dict(qm=11), [0]),
+    ("b_1080p_4slices_scaling", 4, 120, 68, dict(qm=12), [0]),
+    ("b_2160p_strip_scaling", 5, 240, 8, dict(num_slices=2, qm=13), [0]),
 ]
 
 
@@ -76,15 +89,21 @@ def main() -> int:
     L = O.lib()
     fixtures = []
     for name, cidx, W, H, over, indices in CASES:
+        over = dict(over)
+        qseed = over.pop("qm", None)
         cfg = synth.default_cfg(L, cidx, W, H, **over)
+        qm = O.qmatrix(qseed) if qseed is not None else None
+        quant = O.quant_lists(*qm) if qm is not None else None
         for idx in indices:
             t0 = time.time()
             p = synth.picture(L, cfg, idx)
             entry = {"name": name, "config": cidx, "cfg": cfg.as_dict(), "index": idx,
                      "input_md5": synth.input_digest(p)}
+            if qm is not None:
+                entry["qmatrix"] = {"m4": qm[0].tolist(), "m8": qm[1].tolist()}
             for stage, recon_only in (("recon", True), ("out", False)):
-                ref = O.run_reference(cfg, idx, recon_only=recon_only)
-                ora = O.decode(p, stage="recon" if recon_only else "full")
+                ref = O.run_reference(cfg, idx, recon_only=recon_only, qm=qm)
+                ora = O.decode(p, stage="recon" if recon_only else "full", quant=quant)
                 for k, pl in enumerate("YUV"):
                     if not np.array_equal(ref[k], ora[k]):
                         bad = np.argwhere(ref[k] != ora[k])

@@ -110,7 +110,7 @@ class StreamCfg:
     height_mbs: int = 9
     frames: int = 4
     seed: int = 1
-    profile: int = 66                # 66 Baseline, 100 High (CAVLC)
+    profile: int = 66                # 66 Baseline, 100 High, 244 High 4:4:4 Predictive (4:2:0, CAVLC)
     num_refs: int = 1                # max_num_ref_frames
     slices: int = 1                  # slices per picture (random first_mb_in_slice)
     qp: tuple = (18, 38)
@@ -129,6 +129,10 @@ class StreamCfg:
     all_intra: bool = False          # every picture an IDR / I picture
     mv_range: int = 24               # |mvd| bound (quarter samples)
     scaling: int = 0                 # High: 1 SPS scaling matrix, 2 PPS matrix, 3 both
+    lossless: float = 0.0            # 244: qpprime_y_zero_transform_bypass_flag; share of coded intra
+                                     # MBs sent to QP 0 (TransformBypassModeFlag, interpret_mb.cc:804).
+                                     # Coded inter MBs keep QP >= 1: the reference's inter bypass
+                                     # reads stale Intra4x4PredMode (transform.cc:993)
 
 
 @dataclass
@@ -161,10 +165,10 @@ class Encoder:
         w.u(8, 0)                                   # constraint flags
         w.u(8, 51)                                  # level_idc (largest DPB)
         w.ue(0)                                     # seq_parameter_set_id
-        if c.profile == 100:
+        if c.profile in (100, 244):
             w.ue(1)                                 # chroma_format_idc 4:2:0
             w.ue(0); w.ue(0)                        # bit depths 8
-            w.u(1, 0)                               # qpprime_y_zero_transform_bypass_flag
+            w.u(1, 1 if c.lossless else 0)          # qpprime_y_zero_transform_bypass_flag
             w.u(1, c.scaling & 1)                   # seq_scaling_matrix_present_flag
             if c.scaling & 1:
                 self._scaling_matrix(w, 8)
@@ -199,7 +203,7 @@ class Encoder:
         w.u(1, 1)                                   # deblocking_filter_control_present_flag
         w.u(1, c.cip)
         w.u(1, 0)                                   # redundant_pic_cnt_present_flag
-        if c.profile == 100:
+        if c.profile in (100, 244):
             w.u(1, c.transform8x8)
             w.u(1, 1 if c.scaling & 2 else 0)       # pic_scaling_matrix_present_flag
             if c.scaling & 2:
@@ -526,7 +530,9 @@ class Encoder:
                 w.u(1, 1 if m.t8 else 0)
         if cbp or m.kind == I16:
             lo, hi = c.qp
-            target = r.randint(lo, hi)
+            if c.lossless and not m.intra:
+                lo = max(lo, 1)
+            target = 0 if (c.lossless and m.intra and r.random() < c.lossless) else r.randint(lo, hi)
             d = (target - self.qp_pred + 26) % 52 - 26
             w.se(d)
             self.qp_pred = (self.qp_pred + d + 52) % 52

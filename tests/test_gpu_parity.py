@@ -54,12 +54,19 @@ def test_gpu_matches_reference_fixture(L, dec, fx):
     p = synth.picture(L, cfg, fx["index"])
     assert synth.input_digest(p) == fx["input_md5"]
     refs = synth.refpics(L, cfg)
-    out = dec.decode_picture(p, refs)
-    got = {k: md5(out[i]) for i, k in enumerate("YUV")}
+    qm = fx.get("qmatrix")
+    quant = h264r.quant_lists(qm["m4"], qm["m8"]) if qm else h264r.quant_flat()
+    oquant = O.quant_lists(qm["m4"], qm["m8"]) if qm else None
+    dec.assign_quant_params(quant)
+    try:
+        out = dec.decode_picture(p, refs)
+        got = {k: md5(out[i]) for i, k in enumerate("YUV")}
+        rec = dec.decode_picture(p, refs, no_deblock=True) if got != fx["out_md5"] else None
+    finally:
+        dec.assign_quant_params(h264r.quant_flat())
     if got != fx["out_md5"]:
-        rec = dec.decode_picture(p, refs, no_deblock=True)
-        ref_rec = O.decode(p, refs, stage="recon")
-        ref_out = O.decode(p, refs)
+        ref_rec = O.decode(p, refs, stage="recon", quant=oquant)
+        ref_out = O.decode(p, refs, quant=oquant)
         msgs = []
         for i, k in enumerate("YUV"):
             n = 16 if i == 0 else 8
@@ -76,16 +83,17 @@ def test_gpu_matches_reference_fixture(L, dec, fx):
 DEBLOCKS = (A.DBG_DEBLOCK_MB, A.DBG_DEBLOCK_ROWS)
 
 
-def _batch_vs_oracle(L, dec, cidx, W, H, n, debug=0, deblocks=DEBLOCKS, **over):
+def _batch_vs_oracle(L, dec, cidx, W, H, n, debug=0, deblocks=DEBLOCKS, qm=None, **over):
     """Decode n synthetic pictures in one batch under each deblocking schedule and compare
-    every plane with the oracle's decode."""
+    every plane with the oracle's decode (qm: seed of explicit scaling lists)."""
     cfg = synth.default_cfg(L, cidx, W, H, **over)
     pics = [synth.picture(L, cfg, i) for i in range(n)]
     refs = synth.refpics(L, cfg)
     for s, (y, u, v) in enumerate(refs):
         dec.set_ref(s, y, u, v)
-    host = B.pack(pics, h264r.quant_flat())
-    want = [O.decode(p, refs) for p in pics]
+    lists = O.qmatrix(qm) if qm is not None else None
+    host = B.pack(pics, h264r.quant_lists(*lists) if lists else h264r.quant_flat())
+    want = [O.decode(p, refs, quant=O.quant_lists(*lists) if lists else None) for p in pics]
     for db_flag in deblocks:
         db = B.to_device(host, n, None)
         dec.set_debug(debug | db_flag)
@@ -135,6 +143,27 @@ def test_gpu_batch_picture_groups(L, dec, n):
     """Batches spanning several 32-picture groups of k_deblock2 (the last one ragged);
     flag 0 takes whichever schedule H264R_DEBLOCK2_MIN selects for the batch size."""
     _batch_vs_oracle(L, dec, 3, 11, 9, n, deblocks=(0, A.DBG_DEBLOCK_MB, A.DBG_DEBLOCK_ROWS), pcm_permille=20)
+
+
+@pytest.mark.parametrize("cidx,over", [
+    (2, dict(qp_min=0, qp_max=20, lossless_permille=500, pcm_permille=20)),
+    (3, dict(qp_min=0, qp_max=20, lossless_permille=500, intra_permille=400, transform8x8=1)),
+    (4, dict(qp_min=0, qp_max=20, lossless_permille=500)),
+])
+def test_gpu_batch_lossless(L, dec, cidx, over):
+    """TransformBypassModeFlag MBs (F12, transform.cc:736-822) in every MB kind, CIF batches,
+    through the level schedule and (all-intra) the walk."""
+    _batch_vs_oracle(L, dec, cidx, 22, 18, 3, **over)
+
+
+def test_gpu_batch_lossless_walk(L, dec):
+    _batch_vs_oracle(L, dec, 3, 22, 18, 2, debug=A.DBG_INTRA_WALK, qp_min=0, qp_max=10, lossless_permille=600,
+                     intra_permille=500, transform8x8=1)
+
+
+def test_gpu_batch_1080p_b_scaling(L, dec):
+    """Config 4 size with explicit (non-flat) scaling matrices."""
+    _batch_vs_oracle(L, dec, 4, 120, 68, 2, qm=21)
 
 
 def test_gpu_2160p_b_8slices(L, dec):

@@ -28,9 +28,10 @@ def test_oracle_matches_reference_fixture(fx):
     cfg = synth.A.SynthCfg.from_dict(fx["cfg"])
     p = synth.picture(L, cfg, fx["index"])
     assert synth.input_digest(p) == fx["input_md5"], "synthetic generator drifted from the fixture"
-    rec = O.decode(p, stage="recon")
+    quant = O.quant_lists(fx["qmatrix"]["m4"], fx["qmatrix"]["m8"]) if "qmatrix" in fx else None
+    rec = O.decode(p, stage="recon", quant=quant)
     assert {k: md5(rec[i]) for i, k in enumerate("YUV")} == fx["recon_md5"]
-    out = O.decode(p, stage="full")
+    out = O.decode(p, stage="full", quant=quant)
     assert {k: md5(out[i]) for i, k in enumerate("YUV")} == fx["out_md5"]
 
 
@@ -47,6 +48,9 @@ def test_fixture_coverage():
     assert any(c["num_slices"] > 1 for c in cfgs)
     assert any(c["filter_offset_a"] != 0 for c in cfgs)
     assert "p_1080p" in names and "intra_1080p" in names
+    assert any(c.get("lossless_permille") for c in cfgs)                      # F12
+    assert any("qmatrix" in f and f["cfg"]["kind"] == 2 for f in GOLDEN)        # scaling lists, B
+    assert any(c["width_mbs"] == 240 for c in cfgs)                            # a 2160p-wide strip
 
 
 @pytest.mark.reference
