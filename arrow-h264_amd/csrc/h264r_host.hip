@@ -23,7 +23,8 @@
 #include "h264r.h"
 
 namespace h264r { struct DbInfo; }
-extern "C" __global__ void k_inter4(h264r_batch b, h264r::DbInfo* dbinfo, int2 rows);
+extern "C" __global__ void k_inter4(h264r_batch b, h264r::DbInfo* dbinfo, int2 rows, int* sp_flag);
+extern "C" __global__ void k_inter_sp(h264r_batch b, int2 rows, const int* sp_flag);
 extern "C" __global__ void k_intra_pic(h264r_batch b, int* sync, int* err, const uint16_t* lvl, int lmax, int2 rows);
 extern "C" __global__ void k_level(h264r_batch b, uint16_t* lvl, int* lvsync, int* lcount, int2 rows);
 extern "C" __global__ void k_level_scan(const int* lcount, int* lbase);
@@ -336,8 +337,8 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
     const int nbands = (HB + 15) / 16, npairs = (HB + 1) / 2;
     // scratch: per-MB deblocking records, tagged hand-off
     // records, and a sync region [intra ticket + per-(picture,row) progress][deblock
-    // ticket][level barrier, deepest level]
-    const size_t sync_n = 1 + (size_t)P * H + 4;
+    // ticket][level barrier, deepest level][SP inter MBs seen]
+    const size_t sync_n = 1 + (size_t)P * H + 5;
     // the scratch is shared by every launch of this context: a launch on another stream
     // than the previous one waits for it first
     if (c->last_stream && c->last_stream != s) {
@@ -391,7 +392,11 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
     if (c->timing) c->timed_launches++;
     {
         Timed t(c, 0, s);
-        hipLaunchKernelGGL(k_inter4, dim3((W * HB + 15) / 16, P), dim3(256), 0, s, b, dbinfo, rows);
+        int* sp_flag = sync + 1 + (size_t)P * H + 4;
+        hipLaunchKernelGGL(k_inter4, dim3((W * HB + 15) / 16, P), dim3(256), 0, s, b, dbinfo, rows, sp_flag);
+        HIP_OK(hipGetLastError());
+        // inter MBs of SP slices (a short launch when the batch has none)
+        hipLaunchKernelGGL(k_inter_sp, dim3(1024), dim3(256), 0, s, b, rows, (const int*)sp_flag);
         HIP_OK(hipGetLastError());
     }
     {
@@ -575,6 +580,7 @@ int h264r_mb_submit(h264r_ctx* c, int addr, const h264r_mb* mb, const int16_t* l
     const int n = c->pw * c->ph;
     if (addr < 0 || addr >= n || !mb || n_levels < 0 || (n_levels && !levels) || !mv || !ref_idx) return H264R_EINVAL;
     if (mb->slice >= c->h_pic.num_slices) return H264R_EINVAL;
+    if (mb->mb_type == H264R_SI) return H264R_EUNSUPPORTED;        // see include/h264r.h
     // lossless inter MBs: the kernels take intra_chroma_pred_mode as DC, which is what the
     // parser leaves in an inter MB (macroblock_t::init, slice_data.cc:482)
     if ((mb->flags & H264R_MBF_BYPASS) && !(mb->flags & H264R_MBF_INTRA) && mb->chroma_mode != 0) return H264R_EINVAL;

@@ -14,24 +14,51 @@ using namespace h264r;
 #ifndef H264R_INTER_WAVES
 #define H264R_INTER_WAVES 3                 // minimum waves per SIMD asked of the register allocator (<= 168 VGPRs)
 #endif
-extern "C" __global__ __launch_bounds__(256, H264R_INTER_WAVES) void k_inter4(h264r_batch b, DbInfo* dbinfo, int2 rows)
+// The workgroup's copy of the DPB plane table and of picture `pic`'s slice ref tables.
+DEV void inter4_lds(const h264r_batch& b, int pic, Inter4Lds& S)
+{
+    if (threadIdx.x < 3 * H264R_MAX_SLOTS) S.planes[threadIdx.x] = b.ref_planes[threadIdx.x];
+    // the picture's ref tables: 32 bytes per slice, 8 per thread
+    const int nsl = min(b.slice_stride, INTER4_LDS_SLICES);
+    const h264r_slice* sl = b.slices + (size_t)pic * b.slice_stride;
+    for (int i = threadIdx.x; i < nsl * 4; i += blockDim.x)
+        *reinterpret_cast<uint2*>(&S.ref_slot[i >> 2][0][0] + 8 * (i & 3)) =
+            *reinterpret_cast<const uint2*>(&sl[i >> 2].ref_slot[0][0] + 8 * (i & 3));
+}
+
+// sp_flag: set when an inter MB of an SP slice was met (k_inter_sp then runs).
+extern "C" __global__ __launch_bounds__(256, H264R_INTER_WAVES) void k_inter4(h264r_batch b, DbInfo* dbinfo, int2 rows,
+                                                                             int* sp_flag)
 {
     __shared__ Inter4Lds S;
     const int pic = blockIdx.y;
-    if (threadIdx.x < 3 * H264R_MAX_SLOTS) S.planes[threadIdx.x] = b.ref_planes[threadIdx.x];
-    {
-        // the picture's ref tables: 32 bytes per slice, 8 per thread
-        const int nsl = min(b.slice_stride, INTER4_LDS_SLICES);
-        const h264r_slice* sl = b.slices + (size_t)pic * b.slice_stride;
-        for (int i = threadIdx.x; i < nsl * 4; i += blockDim.x)
-            *reinterpret_cast<uint2*>(&S.ref_slot[i >> 2][0][0] + 8 * (i & 3)) =
-                *reinterpret_cast<const uint2*>(&sl[i >> 2].ref_slot[0][0] + 8 * (i & 3));
-    }
+    inter4_lds(b, pic, S);
     __syncthreads();
     const Geom g = make_geom(b.width_mbs, b.height_mbs);
     const int lane = threadIdx.x & 63;
     const int a0 = rows.x * g.wmb + (blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) * 4;
     const int aend = rows.y * g.wmb;
     if (a0 >= aend) return;
-    inter4_mbs(b, g, pic, a0, aend, lane, dbinfo + (size_t)pic * g.nmb, S);
+    inter4_mbs<false>(b, g, pic, a0, aend, lane, dbinfo + (size_t)pic * g.nmb, S, sp_flag);
+}
+
+// k_inter_sp: the inter MBs of SP slices (inverse_transform_sp), after k_inter4.  A
+// persistent grid that leaves at once unless k_inter4 set sp_flag (so a batch without SP
+// slices pays one short launch), then strides over (16-MB group, picture).
+extern "C" __global__ __launch_bounds__(256) void k_inter_sp(h264r_batch b, int2 rows, const int* sp_flag)
+{
+    if (!__hip_atomic_load(sp_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+    __shared__ Inter4Lds S;
+    const Geom g = make_geom(b.width_mbs, b.height_mbs);
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int groups = (g.wmb * (rows.y - rows.x) + 15) / 16;
+    const int aend = rows.y * g.wmb;
+    for (int w = blockIdx.x; w < groups * b.num_pics; w += gridDim.x) {
+        const int pic = w / groups, grp = w % groups;
+        __syncthreads();                              // the previous item's readers are done with S
+        inter4_lds(b, pic, S);
+        __syncthreads();
+        const int a0 = rows.x * g.wmb + (grp * 4 + wave) * 4;
+        if (a0 < aend) inter4_mbs<true>(b, g, pic, a0, aend, lane, nullptr, S, nullptr);
+    }
 }

@@ -235,10 +235,56 @@ DEV void idct4_inplace(int& a, int& b, int& c, int& d)
     a = o0; b = o1; c = o2; d = o3;
 }
 
+// ------------------------------------------------------------------ SP slices
+// Transform::itrans_sp / itrans_sp_cr (transform.cc:1098-1265), the arithmetic of the
+// reference as it stands (see oracle/h264r_oracle.c sp_mb for its quirks).
+__device__ static const uint8_t SP_A[16] = {16, 20, 16, 20, 20, 25, 20, 25, 16, 20, 16, 20, 20, 25, 20, 25};
+DEV int sp_sgn(int x) { return (x >= 0) - (x < 0); }                                   // defines.h:73-77
+DEV int sp_ls2(int m, int j, int i)                                                     // LevelScale2 :1105-1130
+{
+    const int cls = (j & 1) + (i & 1);
+    constexpr int v0[6] = {13107, 11916, 10082, 9362, 8192, 7282};
+    constexpr int v1[6] = {8066, 7490, 6554, 5825, 5243, 4559};
+    constexpr int v2[6] = {5243, 4660, 4194, 3647, 3355, 2893};
+    return cls == 0 ? v0[m] : (cls == 1 ? v1[m] : v2[m]);
+}
+DEV int sp_dq(int m, int j, int i)                                                      // dequant_coef :93-100
+{
+    constexpr int v0[6] = {10, 11, 13, 14, 16, 18};
+    constexpr int v1[6] = {13, 14, 16, 18, 20, 23};
+    constexpr int v2[6] = {16, 18, 20, 23, 25, 29};
+    const int cls = (j & 1) + (i & 1);
+    return cls == 0 ? v0[m] : (cls == 1 ? v1[m] : v2[m]);
+}
+// One coefficient of itrans_sp (luma, :1158-1178): cr the dequantised level, cp the
+// transformed prediction; returns the re-dequantised coefficient.
+DEV int sp_luma_coef(int cr, int cp, int j, int i, int qp, int qs, int sw)
+{
+    const int ls = sp_ls2(qs % 6, j, i);
+    int cij;
+    if (sw) {
+        cij = cr + sp_sgn(cp) * ((iabs(cp) * ls + (1 << (14 + qs / 6))) >> (15 + qs / 6));
+    } else {
+        const int cs = cp + ((int)((unsigned)(cr * sp_dq(qp % 6, j, i) * SP_A[j * 4 + i]) << (qp / 6)) >> 10);
+        cij = sp_sgn(cs) * ((iabs(cs) * ls + (1 << (14 + qs / 6))) >> (15 + qs / 6));
+    }
+    const int dq = sp_dq(qs % 6, j, i);
+    return qs >= 24 ? (int)((unsigned)(cij * dq) << (qs / 6 - 4)) : (cij * dq + (1 << (3 - qs / 6))) >> (4 - qs / 6);
+}
+// 4-point forward core transform (forward_4x4 rows / columns, :560-594)
+DEV void fwd4(int p0, int p1, int p2, int p3, int& c0, int& c1, int& c2, int& c3)
+{
+    const int e0 = p0 + p3, e1 = p1 + p2, e2 = p1 - p2, e3 = p0 - p3;
+    c0 = e0 + e1; c1 = e2 + (e3 << 1); c2 = e0 - e1; c3 = e3 - (e2 << 1);
+}
+
 // The inter / I_PCM macroblocks a0 .. a0+3 of picture `pic` and the deblocking
-// records of all four.
+// records of all four.  SP = false (k_inter4): inter MBs of SP slices are left out and
+// flagged in *sp_flag; SP = true (k_inter_sp): only those are reconstructed, with
+// inverse_transform_sp (decoder.cc:256-257, transform.cc:1267-1300), and no records.
+template <bool SP>
 DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int aend, int lane, DbInfo* __restrict__ dbout,
-                    const Inter4Lds& S)
+                    const Inter4Lds& S, int* sp_flag)
 {
     const int grp = lane >> 4, blk = lane & 15, bx = blk & 3, by = blk >> 2;
     const int a = a0 + grp;
@@ -269,6 +315,12 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
     [&]() {
         const bool pcm = q.mb_type == H264R_I_PCM;
         if (!valid || (mb_is_intra(q) && !pcm)) return;              // intra: k_intra_* (lanes idle here)
+        const bool sp_mb = q_type == H264R_SLICE_SP && !mb_is_intra(q);
+        if constexpr (!SP) {
+            if (sp_mb) { *sp_flag = 1; return; }                     // k_inter_sp's
+        } else {
+            if (!sp_mb) return;
+        }
         const PicPtrs o = out_planes(b, g, pic);
         const int16_t* lv = b.levels + q.coef_off;
         uint8_t* ydst = o.y + (size_t)(mby * 16 + by * 4) * g.W + mbx * 16 + bx * 4;
@@ -366,6 +418,159 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
     #pragma unroll
         for (int pl = 0; pl < 2; ++pl) predC[pl] = wp_combine4(qs, wp_mode, dir, r0, r1, pC[0][pl], pC[1][pl], 1 + pl);
 
+        if constexpr (SP) {
+            // ---- itrans_sp of this lane's 4x4 block (:1132-1187): the prediction is
+            // transformed, combined with the level and re-quantised at QsY; the
+            // reconstruction is the clipped inverse transform alone
+            const int qp = q.qp_y, qsy = qs->qs_y, sw = qs->sp_switch;
+            const int per = qpl / 6;
+            int cf[4][4];
+    #pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int p0 = predY[i] & 255, p1 = (predY[i] >> 8) & 255, p2 = (predY[i] >> 16) & 255, p3 = predY[i] >> 24;
+                fwd4(p0, p1, p2, p3, cf[i][0], cf[i][1], cf[i][2], cf[i][3]);
+            }
+    #pragma unroll
+            for (int c = 0; c < 4; ++c) fwd4(cf[0][c], cf[1][c], cf[2][c], cf[3][c], cf[0][c], cf[1][c], cf[2][c], cf[3][c]);
+    #pragma unroll
+            for (int i = 0; i < 4; ++i)
+    #pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const uint4 lw = lev[i >> 1], sw4 = lsc[i >> 1];
+                    const uint32_t lo_ = (i & 1) ? lw.z : lw.x, hi_ = (i & 1) ? lw.w : lw.y;
+                    const uint32_t slo = (i & 1) ? sw4.z : sw4.x, shi = (i & 1) ? sw4.w : sw4.y;
+                    const int cr = dq4(sel16(lo_, hi_, c), sel16(slo, shi, c), per);   // inverse_quantize :409-413
+                    cf[i][c] = sp_luma_coef(cr, cf[i][c], i, c, qp, qsy, sw);
+                }
+    #pragma unroll
+            for (int i = 0; i < 4; ++i) idct4_inplace(cf[i][0], cf[i][1], cf[i][2], cf[i][3]);
+    #pragma unroll
+            for (int c = 0; c < 4; ++c) idct4_inplace(cf[0][c], cf[1][c], cf[2][c], cf[3][c]);
+    #pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                uint32_t wv = 0;
+    #pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    int v = (cf[i][c] + 32) >> 6;
+                    // opaque: shift + clamp + byte packing otherwise becomes v_ashr_pk_u8_i32, whose
+                    // upper result half the compiler takes as zero -- on MI355X it kept the old
+                    // register's upper bits (bytes 2-3 = 0xFF after a negative input), measured
+                    asm volatile("" : "+v"(v));
+                    wv |= (uint32_t)clip255(v) << (8 * c);
+                }
+                *reinterpret_cast<uint32_t*>(ydst + (size_t)i * g.W) = wv;
+            }
+            // ---- itrans_sp_cr (:1190-1265) then inverse_transform_chroma (:1033-1049):
+            // chroma block cb is spread over lanes {blk, ^1, ^4, ^5}; my 2x2 quadrant
+            // (rows cr.., cols cc..).  The DC pass takes the raw DC levels (transform_chroma_dc
+            // skips SP inter MBs, :865-875), the AC pass the PREDICTION SAMPLES (:1246)
+    #pragma unroll
+            for (int pl = 0; pl < 2; ++pl) {
+                const int qpc = q.qp_c[pl], qsc = qs->qs_c[pl];
+                int pr[2][2], f[2][2];
+    #pragma unroll
+                for (int r = 0; r < 2; ++r)
+    #pragma unroll
+                    for (int c = 0; c < 2; ++c) pr[r][c] = (predC[pl] >> (16 * r + 8 * c)) & 255;
+                // forward transform: rows (my 2 columns + the 2 of lane ^ 1), then columns
+                // (my 2 rows + the 2 of lane ^ 4)
+                int t[2][2];
+    #pragma unroll
+                for (int r = 0; r < 2; ++r) {
+                    const int o0 = __shfl_xor(pr[r][0], 1), o1 = __shfl_xor(pr[r][1], 1);
+                    const int q0 = cc ? o0 : pr[r][0], q1 = cc ? o1 : pr[r][1], q2 = cc ? pr[r][0] : o0, q3 = cc ? pr[r][1] : o1;
+                    int y0, y1, y2, y3;
+                    fwd4(q0, q1, q2, q3, y0, y1, y2, y3);
+                    t[r][0] = cc ? y2 : y0;
+                    t[r][1] = cc ? y3 : y1;
+                }
+    #pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                    const int o0 = __shfl_xor(t[0][c], 4), o1 = __shfl_xor(t[1][c], 4);
+                    const int q0 = cr ? o0 : t[0][c], q1 = cr ? o1 : t[1][c], q2 = cr ? t[0][c] : o0, q3 = cr ? t[1][c] : o1;
+                    int y0, y1, y2, y3;
+                    fwd4(q0, q1, q2, q3, y0, y1, y2, y3);
+                    f[0][c] = cr ? y2 : y0;
+                    f[1][c] = cr ? y3 : y1;
+                }
+                // the four blocks' DC coefficients (lanes 0, 2, 8, 10 of the MB's 16)
+                const int gb = lane & ~15;
+                const int d00 = __shfl(f[0][0], gb + 0), d01 = __shfl(f[0][0], gb + 2);
+                const int d10 = __shfl(f[0][0], gb + 8), d11 = __shfl(f[0][0], gb + 10);
+                int mp[4] = {d00 + d10 + d01 + d11, d00 - d10 + d01 - d11, d00 + d10 - d01 - d11, d00 - d10 - d01 + d11};
+                const int c00 = (int16_t)(cdc[pl].x & 0xFFFF), c01 = (int16_t)(cdc[pl].x >> 16);
+                const int c10 = (int16_t)(cdc[pl].y & 0xFFFF), c11 = (int16_t)(cdc[pl].y >> 16);
+                const int crd[4] = {c00, c01, c10, c11};
+                const int ls0 = sp_ls2(qsc % 6, 0, 0);
+    #pragma unroll
+                for (int n = 0; n < 4; ++n) {
+                    const int cp = mp[n];
+                    int cij;
+                    if (qs->sp_switch) {
+                        cij = ((sp_sgn(cp) * (iabs(cp) * ls0 + (1 << (15 + qsc / 6)))) >> (16 + qsc / 6)) + cp;
+                    } else {
+                        const int cs = cp + ((int)((unsigned)(crd[n] * sp_dq(qpc % 6, 0, 0) * 16) << (qpc / 6)) >> 9);
+                        cij = (sp_sgn(cs) * (iabs(cs) * ls0 + (1 << (15 + qsc / 6)))) >> (16 + qsc / 6);
+                    }
+                    mp[n] = (int)((unsigned)(cij * sp_dq(qsc % 6, 0, 0)) << (qpc / 6));
+                }
+                // AC (every position; (0,0) is replaced by the DC result below)
+                int k[2][2];
+    #pragma unroll
+                for (int r = 0; r < 2; ++r)
+    #pragma unroll
+                    for (int c = 0; c < 2; ++c) {
+                        const int j = cr + r, i = cc + c;
+                        const int crv = dq4((int16_t)(clev[pl][r] >> (16 * c)), (int16_t)(csc[pl][r] >> (16 * c)), qpc / 6);
+                        const int cp = pr[r][c], ls = sp_ls2(qsc % 6, j, i);
+                        int cij;
+                        if (qs->sp_switch) {
+                            cij = crv + ((sp_sgn(cp) * (iabs(cp) * ls + (1 << (14 + qsc / 6)))) >> (15 + qsc / 6));
+                        } else {
+                            const int cs = cp + ((int)((unsigned)(crv * sp_dq(qpc % 6, j, i) * SP_A[j * 4 + i]) << (qpc / 6)) >> 9);
+                            cij = (sp_sgn(cs) * (iabs(cs) * ls + (1 << (14 + qsc / 6)))) >> (15 + qsc / 6);
+                        }
+                        k[r][c] = (int)((unsigned)(cij * sp_dq(qsc % 6, j, i)) << (qpc / 6));
+                    }
+                if (cr == 0 && cc == 0) {
+                    const int dcv = cb == 0 ? (mp[0] + mp[1] + mp[2] + mp[3]) >> 1
+                                  : cb == 1 ? (mp[0] + mp[1] - mp[2] - mp[3]) >> 1
+                                  : cb == 2 ? (mp[0] - mp[1] + mp[2] - mp[3]) >> 1
+                                            : (mp[0] - mp[1] - mp[2] + mp[3]) >> 1;
+                    k[0][0] = dcv;
+                }
+                // inverse transform (as below) and construction with the prediction
+                int rcv[2][2];
+                {
+                    int tt[2][2];
+    #pragma unroll
+                    for (int r = 0; r < 2; ++r) {
+                        const int o0 = __shfl_xor(k[r][0], 1), o1 = __shfl_xor(k[r][1], 1);
+                        const int d0 = cc ? o0 : k[r][0], d1 = cc ? o1 : k[r][1], d2 = cc ? k[r][0] : o0, d3 = cc ? k[r][1] : o1;
+                        int y0, y1, y2, y3;
+                        idct4(d0, d1, d2, d3, y0, y1, y2, y3);
+                        tt[r][0] = cc ? y2 : y0;
+                        tt[r][1] = cc ? y3 : y1;
+                    }
+    #pragma unroll
+                    for (int c = 0; c < 2; ++c) {
+                        const int o0 = __shfl_xor(tt[0][c], 4), o1 = __shfl_xor(tt[1][c], 4);
+                        const int d0 = cr ? o0 : tt[0][c], d1 = cr ? o1 : tt[1][c], d2 = cr ? tt[0][c] : o0, d3 = cr ? tt[1][c] : o1;
+                        int y0, y1, y2, y3;
+                        idct4(d0, d1, d2, d3, y0, y1, y2, y3);
+                        rcv[0][c] = ((cr ? y2 : y0) + 32) >> 6;
+                        rcv[1][c] = ((cr ? y3 : y1) + 32) >> 6;
+                    }
+                }
+                uint8_t* cdst = (pl ? o.v : o.u) + coff;
+    #pragma unroll
+                for (int r = 0; r < 2; ++r) {
+                    const uint32_t wv = (uint32_t)clip255(pr[r][0] + rcv[r][0]) | ((uint32_t)clip255(pr[r][1] + rcv[r][1]) << 8);
+                    *reinterpret_cast<uint16_t*>(cdst + (size_t)r * g.Wc) = (uint16_t)wv;
+                }
+            }
+            return;
+        }
         // ---- luma residual (transform.cc:1058-1073)
         int res[4][4];
     #pragma unroll
@@ -548,6 +753,7 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
         }
     }();
 
+    if constexpr (SP) return;
     // neighbour motion and records: loaded here, after the reconstruction, so that
     // they do not stay live across motion compensation (L2-hot by now)
     const int li = X4 > 0 ? mi - 1 : mi, ui = Y4 > 0 ? mi - g.W4 : mi;

@@ -82,6 +82,12 @@ static void make_slices(const h264r_synth_cfg* c, rng_t* r, h264r_slice* sl)
         x->wp_mode = (uint8_t)c->wp_mode;
         x->luma_log2_wd = 5; x->chroma_log2_wd = 5;
         if (c->kind == H264R_SYNTH_INTRA) continue;
+        if (c->kind == H264R_SYNTH_P && c->sp_slices) {
+            x->slice_type = H264R_SLICE_SP;
+            x->qs_y = (uint8_t)rrange(r, 0, 5);
+            x->sp_switch = (uint8_t)rrange(r, 0, 1);
+            x->qs_c[0] = x->qs_c[1] = (int8_t)x->qs_y;     /* chroma_qp_index_offset 0, QsY < 30 */
+        }
         /* L0: descending POC below cur then ascending above; L1: the reverse (8.2.4.2.3 style) */
         int l0[H264R_MAX_REFS], l1[H264R_MAX_REFS], k0 = 0, k1 = 0;
         for (int k = n - 1; k >= 0; --k) if (h264r_synth_slot_poc(k) < cur) l0[k0++] = k;

@@ -34,7 +34,8 @@ assert MB_DTYPE.itemsize == 32
 SLICE_DTYPE = np.dtype([
     ("slice_type", "u1"), ("deblock_idc", "u1"), ("filter_offset_a", "i1"),
     ("filter_offset_b", "i1"), ("wp_mode", "u1"), ("luma_log2_wd", "u1"),
-    ("chroma_log2_wd", "u1"), ("num_ref", "u1", (2,)), ("pad", "u1", (7,)),
+    ("chroma_log2_wd", "u1"), ("num_ref", "u1", (2,)), ("qs_y", "u1"), ("sp_switch", "u1"),
+    ("qs_c", "i1", (2,)), ("pad", "u1", (3,)),
     ("ref_slot", "i1", (2, MAX_REFS)), ("wp_weight", "i1", (2, MAX_REFS, 3)),
     ("wp_offset", "i1", (2, MAX_REFS, 3)), ("implicit_w1", "<i2", (MAX_REFS, MAX_REFS)),
 ])
@@ -56,7 +57,8 @@ class SynthCfg(C.Structure):
         ("constrained_intra", C.c_int32), ("num_refs", C.c_int32),
         ("qp_min", C.c_int32), ("qp_max", C.c_int32), ("pcm_permille", C.c_int32),
         ("intra_permille", C.c_int32), ("mv_range_x", C.c_int32),
-        ("mv_range_y", C.c_int32), ("lossless_permille", C.c_int32), ("seed", C.c_uint64),
+        ("mv_range_y", C.c_int32), ("lossless_permille", C.c_int32), ("sp_slices", C.c_int32),
+        ("seed", C.c_uint64),
     ]
 
     def as_dict(self) -> dict:

@@ -88,8 +88,10 @@ extern "C" {
 #define H264R_SLICE_P   0
 #define H264R_SLICE_B   1
 #define H264R_SLICE_I   2
-#define H264R_SLICE_SP  3
-#define H264R_SLICE_SI  4
+#define H264R_SLICE_SP  3   /* inverse_transform_sp (transform.cc:1267-1300); QsC < 6 only: the reference
+                               indexes LevelScale2[QsC] unreduced (:1230,1235), undefined beyond */
+#define H264R_SLICE_SI  4   /* SI MBs (mb_type H264R_SI): EUNSUPPORTED -- the reference sends them through
+                               mb_pred_inter with an out-of-range BLOCK_STEP row (decoder.cc:141-146,212-225) */
 
 /* ---- h264r_mb.flags ---------------------------------------------------------- */
 #define H264R_MBF_INTRA   0x01   /* mb_t::is_intra_block            */
@@ -128,7 +130,10 @@ typedef struct h264r_slice {
     uint8_t  luma_log2_wd;         /* luma_log2_weight_denom (5 when not explicit, interpret_rbsp.cc:722) */
     uint8_t  chroma_log2_wd;       /* chroma_log2_weight_denom                           */
     uint8_t  num_ref[2];
-    uint8_t  pad[7];
+    uint8_t  qs_y;                 /* SP slices: QsY (slice_qs_delta, interpret_rbsp.cc:740-748)           */
+    uint8_t  sp_switch;            /* SP slices: sp_for_switch_flag                                        */
+    int8_t   qs_c[2];              /* SP slices: QsC[] of the slice's MBs (interpret_mb.cc:799-801)       */
+    uint8_t  pad[3];
     int8_t   ref_slot[2][H264R_MAX_REFS];       /* RefPicList[l][i] -> DPB slot       */
     int8_t   wp_weight[2][H264R_MAX_REFS][3];   /* pred_weight_l[l][pl][i].weight     */
     int8_t   wp_offset[2][H264R_MAX_REFS][3];   /* pred_weight_l[l][pl][i].offset     */

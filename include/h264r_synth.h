@@ -46,6 +46,9 @@ typedef struct h264r_synth_cfg {
                                     TransformBypassModeFlag MB (interpret_mb.cc:804); inter
                                     bypass MBs carry random Intra4x4/8x8PredMode values, which
                                     the reference's bypass DPCM reads for them (transform.cc:993,1008) */
+    int32_t  sp_slices;          /* P pictures: every slice an SP slice (QsY 0..5 -- the reference's
+                                    itrans_sp_cr indexes LevelScale2 by QsC unreduced, transform.cc:1230,
+                                    so only QsC < 6 has defined results -- sp_for_switch_flag random)   */
     uint64_t seed;
 } h264r_synth_cfg;
 

@@ -185,6 +185,7 @@ int h264r_mb_submit(h264r_ctx* c, int addr, const h264r_mb* mb, const int16_t* l
     const int n = c->pw * c->ph;
     if (addr < 0 || addr >= n || !mb || n_levels < 0 || (n_levels && !levels) || !mv || !ref_idx) return H264R_EINVAL;
     if (mb->slice >= c->pic.num_slices) return H264R_EINVAL;
+    if (mb->mb_type == H264R_SI) return H264R_EUNSUPPORTED;
     size_t off = (c->n_levels + 7) & ~(size_t)7;
     if (off + (size_t)n_levels + 8 > c->cap_levels) {
         size_t cap = (off + n_levels + 8) * 2;

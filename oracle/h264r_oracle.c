@@ -751,6 +751,122 @@ static void mb_res(const h264r_mb* mb, int pl, int cof[16][16], int rres[16][16]
         for (int y = 0; y < n; y += 4) for (int x = 0; x < n; x += 4) inverse_4x4(cof, rres, y, x);
 }
 
+/* ------------------------------------------------------- SP slices (transform.cc:1098-1300) */
+static const int A_SP[4][4] = {{16, 20, 16, 20}, {20, 25, 20, 25}, {16, 20, 16, 20}, {20, 25, 20, 25}};   /* :1098-1103 */
+
+/* LevelScale2 (transform.cc:1105-1130): the forward quantisation scale, by position class */
+static int level_scale2(int m, int j, int i)
+{
+    static const int v[6][3] = {{13107, 8066, 5243}, {11916, 7490, 4660}, {10082, 6554, 4194},
+                                {9362, 5825, 3647}, {8192, 5243, 3355}, {7282, 4559, 2893}};
+    return v[m][(j & 1) + (i & 1)];
+}
+
+static inline int sgn(int x) { return (x >= 0) - (x < 0); }                          /* defines.h:73-77 */
+static inline int shl(int x, int s) { return (int)((unsigned)x << s); }              /* C++ << on negatives */
+
+static void forward_4x4(int p[16][16], int c[16][16], int py, int px)               /* transform.cc:556-595 */
+{
+    int f[4][4];
+    for (int i = 0; i < 4; ++i) {
+        int e0 = p[py + i][px + 0] + p[py + i][px + 3], e1 = p[py + i][px + 1] + p[py + i][px + 2];
+        int e2 = p[py + i][px + 1] - p[py + i][px + 2], e3 = p[py + i][px + 0] - p[py + i][px + 3];
+        f[i][0] = e0 + e1; f[i][1] = e2 + (e3 << 1); f[i][2] = e0 - e1; f[i][3] = e3 - (e2 << 1);
+    }
+    for (int j = 0; j < 4; ++j) {
+        int g0 = f[0][j] + f[3][j], g1 = f[1][j] + f[2][j], g2 = f[1][j] - f[2][j], g3 = f[0][j] - f[3][j];
+        c[py + 0][px + j] = g0 + g1; c[py + 1][px + j] = g2 + (g3 << 1);
+        c[py + 2][px + j] = g0 - g1; c[py + 3][px + j] = g3 - (g2 << 1);
+    }
+}
+
+/* An inter MB of an SP slice: Transform::inverse_transform_sp (transform.cc:1267-1300) --
+ * itrans_sp per luma 4x4 block (:1132-1187; reconstruction = clip1 of the residual, the
+ * prediction enters in the transform domain), then per chroma plane itrans_sp_cr
+ * (:1190-1265) and inverse_transform_chroma (which adds the prediction once more, as the
+ * reference does: itrans_sp_cr keeps mb_pred, :1209).  cof holds what the coefficient push
+ * left: dequantised AC levels and, chroma DC, the raw levels (transform_chroma_dc skips SP
+ * inter MBs, :865-875).  Luma QP: the MB's QpY (slice.parser.QpY at decode time). */
+static void sp_mb(const pstate* s, int addr, const h264r_mb* mb, int cof[3][16][16], int mbp[3][16][16])
+{
+    const h264r_slice* sl = slice_of(s, mb);
+    static __thread int c[16][16], rres[16][16];
+    const int sw = sl->sp_switch;
+    {
+        const int qp = mb->qp_y, qs = sl->qs_y;
+        for (int by = 0; by < 16; by += 4)
+            for (int bx = 0; bx < 16; bx += 4) {
+                forward_4x4(mbp[0], c, by, bx);
+                for (int j = 0; j < 4; ++j)
+                    for (int i = 0; i < 4; ++i) {
+                        int crij = cof[0][by + j][bx + i], cpij = c[by + j][bx + i], cij;
+                        int ls = level_scale2(qs % 6, j, i);
+                        if (sw) {
+                            int csij = sgn(cpij) * ((iabs(cpij) * ls + (1 << (14 + qs / 6))) >> (15 + qs / 6));
+                            cij = crij + csij;
+                        } else {
+                            int csij = cpij + (shl(crij * dequant_coef[qp % 6][j][i] * A_SP[j][i], qp / 6) >> 10);
+                            cij = sgn(csij) * ((iabs(csij) * ls + (1 << (14 + qs / 6))) >> (15 + qs / 6));
+                        }
+                        int dq = dequant_coef[qs % 6][j][i];
+                        cof[0][by + j][bx + i] = qs >= 24 ? shl(cij * dq, qs / 6 - 4) : (cij * dq + (1 << (3 - qs / 6))) >> (4 - qs / 6);
+                    }
+                inverse_4x4(cof[0], rres, by, bx);
+                for (int j = 0; j < 4; ++j)
+                    for (int i = 0; i < 4; ++i) mbp[0][by + j][bx + i] = clip1(255, rres[by + j][bx + i]);
+            }
+        construct(s, addr, 0, 0, 0, 16, 16, 0, rres, mbp[0]);      /* the reconstruction itself */
+    }
+    levels_view v = view_levels(mb, s->p->levels);
+    for (int pl = 1; pl <= 2; ++pl) {
+        const int qp = mb->qp_c[pl - 1], qs = sl->qs_c[pl - 1];     /* QsC < 6 (see h264r_synth.h) */
+        int (*cf)[16] = cof[pl];
+        for (int n2 = 0; n2 < 2; ++n2)                              /* raw DC levels */
+            for (int n1 = 0; n1 < 2; ++n1) cf[n2 * 4][n1 * 4] = v.cdc ? v.cdc[(pl - 1) * 4 + n2 * 2 + n1] : 0;
+        for (int y = 0; y < 8; y += 4) for (int x = 0; x < 8; x += 4) forward_4x4(mbp[pl], c, y, x);
+        int mp1[2][2];
+        mp1[0][0] = c[0][0] + c[4][0] + c[0][4] + c[4][4];
+        mp1[0][1] = c[0][0] - c[4][0] + c[0][4] - c[4][4];
+        mp1[1][0] = c[0][0] + c[4][0] - c[0][4] - c[4][4];
+        mp1[1][1] = c[0][0] - c[4][0] - c[0][4] + c[4][4];
+        for (int n2 = 0; n2 < 2; ++n2)
+            for (int n1 = 0; n1 < 2; ++n1) {
+                int crij = cf[n2 * 4][n1 * 4], cpij = mp1[n2][n1], cij;
+                int ls = level_scale2(qs % 6, 0, 0);
+                if (sw) {
+                    int csij = (sgn(cpij) * (iabs(cpij) * ls + (1 << (15 + qs / 6)))) >> (16 + qs / 6);
+                    cij = csij + cpij;
+                } else {
+                    int csij = cpij + (shl(crij * dequant_coef[qp % 6][0][0] * A_SP[0][0], qp / 6) >> 9);
+                    cij = (sgn(csij) * (iabs(csij) * ls + (1 << (15 + qs / 6)))) >> (16 + qs / 6);
+                }
+                mp1[n2][n1] = shl(cij * dequant_coef[qs % 6][0][0], qp / 6);
+            }
+        for (int n2 = 0; n2 < 8; n2 += 4)
+            for (int n1 = 0; n1 < 8; n1 += 4)
+                for (int j = 0; j < 4; ++j)
+                    for (int i = 0; i < 4; ++i) {
+                        /* the prediction SAMPLE, not its transform (transform.cc:1246) */
+                        int crij = cf[n2 + j][n1 + i], cpij = mbp[pl][n2 + j][n1 + i], cij;
+                        int ls = level_scale2(qs % 6, j, i);
+                        if (sw) {
+                            int csij = (sgn(cpij) * (iabs(cpij) * ls + (1 << (14 + qs / 6)))) >> (15 + qs / 6);
+                            cij = crij + csij;
+                        } else {
+                            int csij = cpij + (shl(crij * dequant_coef[qp % 6][j][i] * A_SP[j][i], qp / 6) >> 9);
+                            cij = (sgn(csij) * (iabs(csij) * ls + (1 << (14 + qs / 6)))) >> (15 + qs / 6);
+                        }
+                        cf[n2 + j][n1 + i] = shl(cij * dequant_coef[qs % 6][j][i], qp / 6);
+                    }
+        cf[0][0] = (mp1[0][0] + mp1[0][1] + mp1[1][0] + mp1[1][1]) >> 1;
+        cf[0][4] = (mp1[0][0] + mp1[0][1] - mp1[1][0] - mp1[1][1]) >> 1;
+        cf[4][0] = (mp1[0][0] - mp1[0][1] + mp1[1][0] - mp1[1][1]) >> 1;
+        cf[4][4] = (mp1[0][0] - mp1[0][1] - mp1[1][0] + mp1[1][1]) >> 1;
+        for (int y = 0; y < 8; y += 4) for (int x = 0; x < 8; x += 4) inverse_4x4(cf, rres, y, x);
+        construct(s, addr, pl, 0, 0, 8, 8, 1, rres, mbp[pl]);
+    }
+}
+
 /* Decoder::decode (decoder.cc:65-262) for one MB. */
 static int decode_mb(pstate* s, int addr)
 {
@@ -812,6 +928,11 @@ static int decode_mb(pstate* s, int addr)
 
     int st = inter_pred_mb(s, addr, mbp);
     if (st) return st;
+    if (slice_of(s, mb)->slice_type == H264R_SLICE_SP) {          /* decoder.cc:256-257 */
+        if (mb->flags & H264R_MBF_T8x8) return H264R_EUNSUPPORTED;  /* no 8x8 transform in SP (Extended) */
+        sp_mb(s, addr, mb, cof, mbp);
+        return 0;
+    }
     /* inverse_transform_inter transform.cc:1051-1095 */
     if (cbpl) {
         if (!(mb->flags & H264R_MBF_T8x8)) {

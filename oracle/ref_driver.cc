@@ -16,7 +16,7 @@
  *
  * usage: ref_driver W H kind nslices idc offA offB t8 wp cip nrefs qpmin qpmax
  *                   pcm_permille intra_permille mvx mvy seed index out.yuv [recon_only
- *                   [lossless_permille]]
+ *                   [lossless_permille [sp_slices]]]
  * lossless_permille > 0 sets sps.qpprime_y_zero_transform_bypass_flag (the synthetic
  * pictures then hold TransformBypassModeFlag MBs, interpret_mb.cc:804).
  * Output: Y plane then Cb then Cr, 8-bit, unpadded.
@@ -82,6 +82,7 @@ int main(int argc, char** argv)
     const char* out_path = argv[k++];
     bool recon_only = argc > k && atoi(argv[k]) != 0;
     if (argc > k + 1) cfg.lossless_permille = atoi(argv[k + 1]);
+    if (argc > k + 2) cfg.sp_slices = atoi(argv[k + 2]);
 
     const int W = cfg.width_mbs, H = cfg.height_mbs, NMB = W * H, W4 = W * 4, PL = W4 * H * 4;
     std::vector<h264r_mb> mbs(NMB);
@@ -177,6 +178,7 @@ int main(int argc, char** argv)
         h.luma_log2_weight_denom = c.luma_log2_wd; h.chroma_log2_weight_denom = c.chroma_log2_wd;
         h.PicOrderCnt = h.TopFieldOrderCnt = h.BottomFieldOrderCnt = pic.poc;
         h.direct_spatial_mv_pred_flag = 0;
+        h.QsY = (int8_t)c.qs_y; h.sp_for_switch_flag = c.sp_switch;      /* SP slices (interpret_rbsp.cc:738-748) */
         for (int l = 0; l < 2; ++l)
             for (int pl = 0; pl < 3; ++pl) {
                 h.pred_weight_l[l][pl].resize(H264R_MAX_REFS);
@@ -246,6 +248,8 @@ int main(int argc, char** argv)
         mb.CodedBlockPatternLuma = c.cbp & 15;
         mb.CodedBlockPatternChroma = c.cbp >> 4;
         mb.QpY = c.qp_y; mb.QpC[0] = c.qp_c[0]; mb.QpC[1] = c.qp_c[1];
+        mb.QsC[0] = slices[c.slice].qs_c[0]; mb.QsC[1] = slices[c.slice].qs_c[1];   /* interpret_mb.cc:799-801 */
+        s.parser.QpY = c.qp_y;                   /* itrans_sp reads the parser's running QpY (transform.cc:1138) */
         mb.qp_scaled[0] = c.qp_scaled[0]; mb.qp_scaled[1] = c.qp_scaled[1]; mb.qp_scaled[2] = c.qp_scaled[2];
         /* interpret_mb.cc:804 */
         mb.TransformBypassModeFlag = sps->qpprime_y_zero_transform_bypass_flag && mb.qp_scaled[0] == 0;

@@ -164,7 +164,12 @@ h264r_slice slice_record(Shim& S, slice_t& slice)
     h264r_slice r;
     memset(&r, 0, sizeof(r));
     if (shr.MbaffFrameFlag || shr.field_pic_flag) check(H264R_EUNSUPPORTED, "MBAFF / field slices");
+    // SI MBs go through mb_pred_inter in the reference with an out-of-range BLOCK_STEP row
+    // (decoder.cc:141-146, 212-225): nothing defined to reproduce
+    if (shr.slice_type == SI_slice) check(H264R_EUNSUPPORTED, "SI slices");
     r.slice_type = shr.slice_type;
+    r.qs_y = (uint8_t)shr.QsY;                        // SP (interpret_rbsp.cc:738-748)
+    r.sp_switch = shr.sp_for_switch_flag ? 1 : 0;
     r.deblock_idc = shr.disable_deblocking_filter_idc;
     r.filter_offset_a = shr.FilterOffsetA;
     r.filter_offset_b = shr.FilterOffsetB;
@@ -360,6 +365,15 @@ void Decoder::decode(mb_t& mb)
     const int si = slice_index(S, &slice);
     if (si < 0) check(H264R_ESTATE, "decode() before init() of its slice");
 
+    if (slice.header.slice_type == SP_slice && !mb.is_intra_block) {
+        // itrans_sp_cr indexes LevelScale2 with QsC unreduced (transform.cc:1230,1235): the
+        // reference reads past the table for QsC >= 6, so only QsC < 6 has defined output
+        if (mb.QsC[0] >= 6 || mb.QsC[1] >= 6 || mb.QsC[0] < 0 || mb.QsC[1] < 0)
+            check(H264R_EUNSUPPORTED, "SP slice with QsC >= 6");
+        if (mb.transform_size_8x8_flag) check(H264R_EUNSUPPORTED, "8x8 transform in an SP slice");
+        S.slice_tab[si].qs_c[0] = mb.QsC[0];          // interpret_mb.cc:799-801 (one value per slice)
+        S.slice_tab[si].qs_c[1] = mb.QsC[1];
+    }
     StagedMb& st = S.mbs[mb.mbAddrX];
     h264r_mb& r = st.rec;
     memset(&r, 0, sizeof(r));

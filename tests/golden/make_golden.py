@@ -69,6 +69,10 @@ CASES = [
     ("p_qcif_lossless_t8", 3, 11, 9, dict(qp_min=0, qp_max=30, lossless_permille=400, transform8x8=1,
                                           intra_permille=300), [0, 1]),
     ("b_qcif_lossless", 4, 11, 9, dict(qp_min=0, qp_max=20, lossless_permille=500), [0]),
+    # SP slices (inverse_transform_sp transform.cc:1267-1300; F13): switching and not, QsY 0..5
+    ("p_qcif_sp", 3, 11, 9, dict(sp_slices=1), [0, 1, 2]),
+    ("p_cif_sp_3slices", 3, 22, 18, dict(sp_slices=1, num_slices=3, deblock_idc=2, intra_permille=200), [0]),
+    ("p_qcif_sp_qp0_51", 3, 11, 9, dict(sp_slices=1, qp_min=0, qp_max=51, num_refs=3), [0, 1]),
     # explicit scaling matrices (SPS lists, all present; Transform::init/set_quant transform.cc:173-302)
     ("intra_qcif_scaling", 2, 11, 9, dict(qm=14), [0]),
     ("p_qcif_scaling_t8", 3, 11, 9, dict(transform8x8=1, qm=15), [0]),

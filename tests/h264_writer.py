@@ -110,7 +110,7 @@ class StreamCfg:
     height_mbs: int = 9
     frames: int = 4
     seed: int = 1
-    profile: int = 66                # 66 Baseline, 100 High, 244 High 4:4:4 Predictive (4:2:0, CAVLC)
+    profile: int = 66                # 66 Baseline, 88 Extended, 100 High, 244 High 4:4:4 Predictive (4:2:0, CAVLC)
     num_refs: int = 1                # max_num_ref_frames
     slices: int = 1                  # slices per picture (random first_mb_in_slice)
     qp: tuple = (18, 38)
@@ -129,6 +129,8 @@ class StreamCfg:
     all_intra: bool = False          # every picture an IDR / I picture
     mv_range: int = 24               # |mvd| bound (quarter samples)
     scaling: int = 0                 # High: 1 SPS scaling matrix, 2 PPS matrix, 3 both
+    sp: float = 0.0                  # 88: share of P pictures coded as SP pictures (every slice SP)
+    qs: tuple = (0, 5)               # QsY range of SP slices (the reference's itrans_sp_cr is defined for QsC < 6)
     lossless: float = 0.0            # 244: qpprime_y_zero_transform_bypass_flag; share of coded intra
                                      # MBs sent to QP 0 (TransformBypassModeFlag, interpret_mb.cc:804).
                                      # Coded inter MBs keep QP >= 1: the reference's inter bypass
@@ -546,6 +548,7 @@ class Encoder:
         n = self.W * self.H
         self.mbs = [_Mb() for _ in range(n)]
         ptype = "I" if idr else "P"
+        sp = ptype == "P" and c.sp > 0 and r.random() < c.sp   # (no draw otherwise: fixed streams stay)
         starts = sorted({0} | set(r.sample(range(1, n), min(c.slices - 1, n - 1)))) if c.slices > 1 else [0]
         frame_num = 0 if idr else (self.frame_num + 1) % (1 << self.log2_max_frame_num)
         self.frame_num = frame_num
@@ -555,7 +558,7 @@ class Encoder:
             end = starts[s + 1] if s + 1 < len(starts) else n
             w = BitWriter()
             w.ue(first)
-            w.ue(7 if ptype == "I" else 5)          # slice_type (all slices of the picture alike)
+            w.ue(7 if ptype == "I" else (8 if sp else 5))   # slice_type (all slices of the picture alike)
             w.ue(0)                                 # pic_parameter_set_id
             w.u(self.log2_max_frame_num, frame_num)
             if idr:
@@ -587,6 +590,9 @@ class Encoder:
             sqp = r.randint(lo, hi)
             w.se(sqp - 26)
             self.qp_pred = sqp
+            if sp:
+                w.u(1, r.randint(0, 1))             # sp_for_switch_flag
+                w.se(r.randint(*c.qs) - 26)         # slice_qs_delta (pic_init_qs 26)
             idc = r.choice(c.deblock)
             w.ue(idc)
             if idc != 1:

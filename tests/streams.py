@@ -54,6 +54,8 @@ STREAMS = {
                                 deblock=(0, 1, 2), offsets=6, intra_in_p=0.3, num_refs=2),
     "hi444_qcif_lossless": dict(width_mbs=11, height_mbs=9, frames=4, seed=110, profile=244, transform8x8=1,
                                 lossless=0.5, qp=(0, 30), intra_in_p=0.4, deblock=(0, 2), offsets=4),
+    "xp_qcif_sp": dict(width_mbs=11, height_mbs=9, frames=5, seed=111, profile=88, sp=0.8, num_refs=2,
+                       intra_in_p=0.2, slices=2, deblock=(0, 1, 2), offsets=3),
     "hp_720p_4slices": dict(width_mbs=80, height_mbs=45, frames=2, seed=109, profile=100, transform8x8=1,
                             slices=4, deblock=(0, 2), scaling=1, num_refs=1),
 }

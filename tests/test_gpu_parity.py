@@ -161,6 +161,16 @@ def test_gpu_batch_lossless_walk(L, dec):
                      intra_permille=500, transform8x8=1)
 
 
+@pytest.mark.parametrize("W,H,n,over", [
+    (22, 18, 3, dict(num_slices=2, intra_permille=200, pcm_permille=20)),
+    (120, 68, 2, dict(qp_min=0, qp_max=51)),
+])
+def test_gpu_batch_sp(L, dec, W, H, n, over):
+    """SP pictures (F13: k_inter_sp, inverse_transform_sp transform.cc:1267-1300), switching and
+    not, mixed with intra / PCM MBs, at CIF and config-3 size."""
+    _batch_vs_oracle(L, dec, 3, W, H, n, sp_slices=1, **over)
+
+
 def test_gpu_batch_1080p_b_scaling(L, dec):
     """Config 4 size with explicit (non-flat) scaling matrices."""
     _batch_vs_oracle(L, dec, 4, 120, 68, 2, qm=21)

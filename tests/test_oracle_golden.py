@@ -49,6 +49,7 @@ def test_fixture_coverage():
     assert any(c["filter_offset_a"] != 0 for c in cfgs)
     assert "p_1080p" in names and "intra_1080p" in names
     assert any(c.get("lossless_permille") for c in cfgs)                      # F12
+    assert any(c.get("sp_slices") for c in cfgs)                              # F13 (SP)
     assert any("qmatrix" in f and f["cfg"]["kind"] == 2 for f in GOLDEN)        # scaling lists, B
     assert any(c["width_mbs"] == 240 for c in cfgs)                            # a 2160p-wide strip
 
