@@ -407,10 +407,14 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
                 pC[l][0] = pC[l][1] = 0x80808080u;
                 continue;
             }
+#ifndef H264R_EXP_NO_LUMA           // (measurement-only knobs: tools/exp_sweep.sh ablations)
             luma_block_pred(S.planes[slot * 3], g.W, g.H, vx >> 2, vy >> 2, vx & 3, vy & 3, pY[l]);
+#endif
+#ifndef H264R_EXP_NO_CHROMA
     #pragma unroll
             for (int pl = 0; pl < 2; ++pl)
                 pC[l][pl] = chroma_block_pred(S.planes[slot * 3 + 1 + pl], g.Wc, g.Hc, vx >> 3, vy >> 3, vx & 7, vy & 7);
+#endif
         }
         uint32_t predY[4], predC[2];
     #pragma unroll
@@ -578,7 +582,11 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
     #pragma unroll
             for (int c = 0; c < 4; ++c) res[i][c] = 0;
         const bool byp = (q.flags & H264R_MBF_BYPASS) != 0;
+#ifdef H264R_EXP_NO_RES
+        if (false) {
+#else
         if (__any(cbpl != 0)) {
+#endif
             const int per = qpl / 6;
             int d[4][4];
     #pragma unroll
@@ -695,7 +703,11 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
     #pragma unroll
         for (int pl = 0; pl < 2; ++pl) {
             int rc[2][2] = {{0, 0}, {0, 0}};
+#ifdef H264R_EXP_NO_RES
+            if (false) {
+#else
             if (__any(cbpc != 0)) {
+#endif
                 const int qpc = q.qp_scaled[1 + pl], per = qpc / 6;
                 int k[2][2], raw[2][2];
     #pragma unroll
@@ -756,6 +768,9 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
     if constexpr (SP) return;
     // neighbour motion and records: loaded here, after the reconstruction, so that
     // they do not stay live across motion compensation (L2-hot by now)
+#ifdef H264R_EXP_NO_DBINFO
+    return;
+#endif
     const int li = X4 > 0 ? mi - 1 : mi, ui = Y4 > 0 ? mi - g.W4 : mi;
     const h264r_mb L = mb_lane(&mbs[hasL ? aa - 1 : aa]);
     const h264r_mb U = mb_lane(&mbs[hasU ? aa - g.wmb : aa]);
