@@ -213,6 +213,11 @@ def main() -> int:
     from h264r import synth
     from h264r import dist as D
 
+    # H264R_BENCH_REHEARSE=1 (testing the N > 1 code path on a one-GPU box): every rank on
+    # device 0, gloo instead of RCCL (RCCL refuses two ranks on one GPU); never a measurement
+    rehearse = os.environ.get("H264R_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local = 0
     torch.cuda.set_device(local)
     # every device operation of this process (allocations, uploads, decode, exchange,
     # checks) goes on ONE explicit stream, which is also the stream the library launches
@@ -222,7 +227,10 @@ def main() -> int:
     torch.cuda.set_stream(cs)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     L = h264r.lib()
     W, H = CONFIG_SIZE[args.config]
@@ -380,7 +388,7 @@ def main() -> int:
     dec.check()
     kern = np.array(dec.last_timing()) if band[1] > band[0] else np.zeros(4)
     dec.set_timing(False)
-    dt = D.max_over_ranks(dt, device="cuda")
+    dt = D.max_over_ranks(dt, device="cpu" if rehearse else "cuda")
 
     total_mbs = (world * nb if shard == "replicas" else npics) * nmb * args.steps
     value = total_mbs / dt
