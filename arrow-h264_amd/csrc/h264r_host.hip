@@ -393,7 +393,8 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
     {
         Timed t(c, 0, s);
         int* sp_flag = sync + 1 + (size_t)P * H + 4;
-        hipLaunchKernelGGL(k_inter4, dim3((W * HB + 15) / 16, P), dim3(256), 0, s, b, dbinfo, rows, sp_flag);
+        const int groups = (W * HB + 15) / 16;
+        hipLaunchKernelGGL(k_inter4, dim3(8 * ((groups + 7) / 8), P), dim3(256), 0, s, b, dbinfo, rows, sp_flag);
         HIP_OK(hipGetLastError());
         // inter MBs of SP slices (a short launch when the batch has none)
         hipLaunchKernelGGL(k_inter_sp, dim3(1024), dim3(256), 0, s, b, rows, (const int*)sp_flag);

@@ -27,16 +27,24 @@ DEV void inter4_lds(const h264r_batch& b, int pic, Inter4Lds& S)
 }
 
 // sp_flag: set when an inter MB of an SP slice was met (k_inter_sp then runs).
+// Grid (8 * ceil(groups / 8), pictures), XCD-aware: workgroups go round-robin to the 8
+// XCDs in launch order, so blockIdx.x % 8 is the XCD and it takes the 16-MB groups of band
+// blockIdx.x % 8 (one eighth of the MB rows) of every picture: an XCD's motion
+// compensation reads only its band of the reference pictures (+ the MV reach), which its
+// 4 MB L2 holds, instead of every XCD streaming whole references through its L2.
 extern "C" __global__ __launch_bounds__(256, H264R_INTER_WAVES) void k_inter4(h264r_batch b, DbInfo* dbinfo, int2 rows,
                                                                              int* sp_flag)
 {
     __shared__ Inter4Lds S;
     const int pic = blockIdx.y;
+    const Geom g = make_geom(b.width_mbs, b.height_mbs);
+    const int groups = (g.wmb * (rows.y - rows.x) + 15) / 16, gb = (groups + 7) / 8;
+    const int grp = (blockIdx.x & 7) * gb + (blockIdx.x >> 3);
+    if (grp >= groups) return;
     inter4_lds(b, pic, S);
     __syncthreads();
-    const Geom g = make_geom(b.width_mbs, b.height_mbs);
     const int lane = threadIdx.x & 63;
-    const int a0 = rows.x * g.wmb + (blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) * 4;
+    const int a0 = rows.x * g.wmb + (grp * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) * 4;
     const int aend = rows.y * g.wmb;
     if (a0 >= aend) return;
     inter4_mbs<false>(b, g, pic, a0, aend, lane, dbinfo + (size_t)pic * g.nmb, S, sp_flag);

@@ -100,7 +100,11 @@ DEV void luma_block_pred(const uint8_t* __restrict__ img, int W, int H, int x, i
         const gdword* q = row_dwords(img, W, H, x, y - 2 + r);
         w[r][0] = q[0]; w[r][1] = q[1]; w[r][2] = q[2];
     }
+#ifdef H264R_EXP_NO_EDGE
+    const bool inside = true;
+#else
     const bool inside = x - 2 >= 0 && x + 6 < W;
+#endif
     const int sh = (x - 2) & 3;
     s16x2 hacc[4][2], bsv[4][2], gsv[4][2];
     int jacc[4][4];
@@ -137,10 +141,14 @@ DEV void luma_block_pred(const uint8_t* __restrict__ img, int W, int H, int x, i
         for (int i = 0; i < 4; ++i) {
             const int k = r - i;                       // tap index of row r for output row i
             if (k < 0 || k > 5) continue;
+#ifndef H264R_EXP_NO_H
             hacc[i][0] += splat16(C6[k]) * g01;
             hacc[i][1] += splat16(C6[k]) * g23;
+#endif
+#ifndef H264R_EXP_NO_J
 #pragma unroll
             for (int c = 0; c < 4; ++c) jacc[i][c] += C6[k] * bc[c];
+#endif
             if (k == 2 || k == 3) {                    // b / G of output row i: row i + 2 + brow
                 const bool take = k == 2 + brow;
                 bsv[i][0] = take ? b01 : bsv[i][0];
