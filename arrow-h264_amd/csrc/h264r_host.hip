@@ -420,6 +420,11 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
             // H264R_COOP=1 launches it cooperatively instead, so that the runtime checks the
             // grid against the occupancy query (off by default: rocprofv3 7.2 crashes at
             // process exit after a cooperative launch)
+            // small batches (the latency chain: one picture) take a grid sized to their MBs,
+            // 64 per workgroup: most workgroups of the full grid would only attend the grid
+            // barriers, whose cost grows with the number of arrivals (MI355X_MICROARCH.md
+            // price list 'barrier-xcd')
+            const int lgrid = std::min(c->levels_grid, std::max(8, (int)(((size_t)P * W * HB + 63) / 64)));
             static const bool coop = [] { const char* e = getenv("H264R_COOP"); return e && atoi(e) != 0; }();
             if (coop) {
                 const int* lcount_c = lcount;
@@ -429,10 +434,10 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
                 int* err_p = c->d_err;
                 void* args[] = {(void*)&b, (void*)&lcount_c, (void*)&lbase_c, (void*)&list_c, (void*)&lmax_v,
                                 (void*)&lvsync, (void*)&err_p};
-                HIP_OK(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(k_intra_levels), dim3(c->levels_grid),
+                HIP_OK(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(k_intra_levels), dim3(lgrid),
                                                   dim3(256), args, 0, s));
             } else {
-                hipLaunchKernelGGL(k_intra_levels, dim3(c->levels_grid), dim3(256), 0, s, b, (const int*)lcount,
+                hipLaunchKernelGGL(k_intra_levels, dim3(lgrid), dim3(256), 0, s, b, (const int*)lcount,
                                    (const int*)lbase, (const uint32_t*)c->d_list, lmax, lvsync, c->d_err);
                 HIP_OK(hipGetLastError());
             }
