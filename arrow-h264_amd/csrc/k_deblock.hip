@@ -8,19 +8,25 @@
 //
 // Work unit: one 64-lane wave owns a PAIR of MB rows (2p, 2p+1) of one
 // picture.  Lanes 0..31 walk row 2p ("half A"), lanes 32..63 walk row 2p+1
-// ("half B") two MBs behind, so every filter instruction works on two MBs
+// ("half B") one MB behind, so every filter instruction works on two MBs
 // and all 64 lanes are busy (per half: lanes 0..15 luma lines, 16..31 chroma
-// lines).  Inside the pair, half A hands its bottom rows to half B through an
+// lines).  One MB behind is the least lag the reference's order allows: MB
+// (x, y)'s horizontal edges need (x+1, y-1)'s vertical edges only (they change
+// columns 13..15 of (x, y-1)), so a step runs the vertical edges of both halves,
+// then hands the bottom rows of the MB above to each half, then the horizontal
+// edges.  Inside the pair, half A hands its bottom rows to half B through an
 // LDS ring; between pairs, half B publishes each MB's final-for-it bottom rows
 // as one self-validating record: 32 naturally aligned 8-byte granules {data
-// dword, launch epoch}, written by one write-through (`sc1`) store instruction.
+// dword, launch epoch}, written by one write-through (`sc1`) store instruction,
+// as soon as the vertical edges of the MB to its right are done.
 // The pair below reads the record with `sc1` loads and re-polls until every
 // granule carries this launch's epoch (MI355X_MICROARCH.md, R2 granule
 // hand-off): no progress counter, no `s_waitcnt vmcnt(0)` on the producer's
 // path.  Pairs are taken as tickets from an atomic counter in
 // pair-major order, so a wave only ever waits on a ticket taken earlier by a
 // running wave: no deadlock under any dispatch order or residency; every spin
-// is bounded and flags the error word.
+// is bounded and flags the error word.  A pair trails the pair above by two
+// steps plus the hand-off (profiles/r02_deblock_lone_trace.txt).
 //
 // Sample ownership: each MB row writes its rows 0..12 (chroma 0..4) and the
 // rows 13..15 (chroma 5..7) of the row above after filtering its top edge;
@@ -32,7 +38,7 @@ using namespace h264r;
 
 namespace {
 
-constexpr int DRING = 4;                    // row A -> row B ring depth (lag is 2)
+constexpr int DRING = 4;                    // row A -> row B ring depth (lag is 1)
 constexpr unsigned SPIN_LIMIT = 1u << 22;   // ~0.3 s of polling, then flag an error
 
 struct alignas(16) PairLds {
@@ -101,7 +107,7 @@ extern "C" __global__ __launch_bounds__(64, H264R_DB_WAVES) void k_deblock(h264r
     const int Y0 = r * 16, Yc = r * 8;
     const uint32_t* info_row = reinterpret_cast<const uint32_t*>(dbinfo + (size_t)pic * g.nmb + (size_t)r * W);
     const uint64_t tag = (uint64_t)epoch << 32;
-    const int steps = W + (hasB ? 2 : 0);
+    const int steps = W + (hasB ? 1 : 0);
 
     // ---- per-lane roles (inside a half), computed once
     const int by0 = hl >> 2, bd0 = hl & 3;                 // luma body dwords hl and hl + 32
@@ -166,20 +172,13 @@ extern "C" __global__ __launch_bounds__(64, H264R_DB_WAVES) void k_deblock(h264r
     }
 
     uint32_t pf_y0 = 0, pf_y1 = 0, pf_c = 0, pf_i = 0;
-    uint64_t pf_top = 0;
+    uint64_t top = 0;
     bool ok = true;
     TRACE(unsigned long long tr_wait = 0; unsigned long long tph[4] = {0, 0, 0, 0}; unsigned long long tm = 0;)
 
-    // Issue the loads of step t (this half's MB t - 2h): body, deblocking record
-    // and, for half A below another pair, the hand-off record of the MB above.
-    // The hand-off record is loaded first and unconditionally (lanes that do not need
-    // it read their own output record): a conditional load merges into the
-    // loop-carried register through a copy, and the copy's vmcnt(0) would retire the
-    // whole prefetch at once instead of letting it overlap the filter work.
+    // The body loads of step t (this half's MB t - h): samples and deblocking record.
     auto prefetch = [&](int t) {
-        const int x = t - 2 * h;
-        const int xs = min(max(x, 0), W - 1);
-        pf_top = ld_cc64(h == 0 && rp > 0 ? hb_in + (size_t)xs * 32 + hl : hb_out + hl);
+        const int x = t - h;
         if (half_on && x >= 0 && x < W) {
             const uint8_t* yb = Y + (size_t)(Y0 + by0) * g.W + x * 16 + 4 * bd0;
             pf_y0 = *reinterpret_cast<const uint32_t*>(yb);
@@ -188,22 +187,68 @@ extern "C" __global__ __launch_bounds__(64, H264R_DB_WAVES) void k_deblock(h264r
             if (hl < DBINFO_DWORDS) pf_i = info_row[x * DBINFO_DWORDS + hl];
         }
     };
+    // The hand-off record of MB x above (half A below another pair), loaded first in a
+    // step and unconditionally (lanes that do not need it read their own output
+    // record): a conditional load merges into its register through a copy, whose
+    // vmcnt(0) would retire the body prefetch with it.  The vertical edges cover it.
+    auto load_top = [&](int x) {
+        const int xs = min(max(x, 0), W - 1);
+        top = ld_cc64(h == 0 && rp > 0 ? hb_in + (size_t)xs * 32 + hl : hb_out + hl);
+    };
+    uint32_t* ring_mine = reinterpret_cast<uint32_t*>(L.ring[h]);
+    const uint32_t* ring_a = reinterpret_cast<const uint32_t*>(L.ring[0]);
+    const uint32_t* ring_b = reinterpret_cast<const uint32_t*>(L.ring[1]);
+    // ring slots of the given kind for MB x (see rg_kind)
+    auto feed_ring = [&](int x, bool left) {
+#pragma unroll
+        for (int it = 0; it < 2; ++it) {
+            const int k = rg_kind[it];
+            if (left ? k == 1 : (k == 0 || (k == 2 && x == W - 1))) {
+                const int ent = k == 1 ? (x + DRING - 1) & (DRING - 1) : x & (DRING - 1);
+                ring_mine[ent * 32 + rg_dst[it]] = Sw[rg_src[it]];
+            }
+        }
+    };
 
     prefetch(0);
     TRACE(const unsigned long long tr_first = __builtin_amdgcn_s_memrealtime();)
     for (int t = 0; t < steps; ++t) {
-        const int x = t - 2 * h;
+        const int x = t - h;
         const bool act = half_on && x >= 0 && x < W;
+        const bool xl = x > 0, xr = x == W - 1;
+        TRACE(unsigned long long ta = __builtin_amdgcn_s_memtime();)
+        if (rp > 0) load_top(x);
+
+        // ---- assemble the MB's own rows (an idle half scribbles on its own tiles only)
+        Sw[a_y0] = pf_y0;
+        Sw[a_y1] = pf_y1;
+        Sw[a_c] = pf_c;
+        if (hl < DBINFO_DWORDS) S.info[hl] = pf_i;
+        // a band that starts below row 0 must not be filtered across its top edge (idc 1 or
+        // a slice edge with idc 2): its top-edge strengths (bs[16..19] = info dword 4) are 0
+        if (r == R0 && R0 > 0 && act && hl == 4 && pf_i != 0)
+            __hip_atomic_store(err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (t + 1 < steps) prefetch(t + 1);
+        wave_sync();
+        TRACE({ asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); const unsigned long long t2 = __builtin_amdgcn_s_memtime(); tph[0] += t2 - ta; tm = t2; })
+
+        // ---- vertical edges of both halves (deblock.cc:488-504)
+        filter_pass(S, hl, 0);
+        wave_sync();
+        // MB x-1's columns 12..15 (the left strip) are final for this row now: its ring entry
+        // is complete
+        if (act && xl && (feeds_ring || feeds_hb)) feed_ring(x, true);
+        TRACE({ asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); const unsigned long long t2 = __builtin_amdgcn_s_memtime(); tph[1] += t2 - tm; tm = t2; })
 
         // ---- the record of the MB above (half A below another pair): wait for this epoch
         if (rp > 0) {
             const bool need = act && h == 0;
             unsigned spins = 0;
             TRACE(unsigned long long tw0 = 0;)
-            while (!__all(!need || (pf_top & 0xFFFFFFFF00000000ull) == tag)) {
+            while (!__all(!need || (top & 0xFFFFFFFF00000000ull) == tag)) {
                 TRACE(if (!tw0) tw0 = __builtin_amdgcn_s_memrealtime();)
                 __builtin_amdgcn_s_sleep(1);
-                if (need) pf_top = ld_cc64(hb_in + (size_t)x * 32 + hl);
+                if (need) top = ld_cc64(hb_in + (size_t)x * 32 + hl);
                 if (++spins > SPIN_LIMIT) {
                     if (lane == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     ok = false;
@@ -213,50 +258,32 @@ extern "C" __global__ __launch_bounds__(64, H264R_DB_WAVES) void k_deblock(h264r
             TRACE(if (tw0) tr_wait += __builtin_amdgcn_s_memrealtime() - tw0;)
             if (!ok) break;
         }
-        TRACE(unsigned long long ta = __builtin_amdgcn_s_memtime();)
-        // ---- assemble the tiles (an idle half scribbles on its own tiles only)
-        Sw[a_y0] = pf_y0;
-        Sw[a_y1] = pf_y1;
-        Sw[a_c] = pf_c;
-        if (hl < DBINFO_DWORDS) S.info[hl] = pf_i;
-        // a band that starts below row 0 must not be filtered across its top edge (idc 1 or
-        // a slice edge with idc 2): its top-edge strengths (bs[16..19] = info dword 4) are 0
-        if (r == R0 && R0 > 0 && act && hl == 4 && pf_i != 0)
-            __hip_atomic_store(err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (r > R0) Sw[a_top] = h == 0 ? (uint32_t)pf_top : reinterpret_cast<const uint32_t*>(&L.ring[0][x & (DRING - 1)])[hl];
-        TRACE(asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); tph[0] += __builtin_amdgcn_s_memtime() - ta;)
-        if (t + 1 < steps) prefetch(t + 1);
         wave_sync();
         TRACE(tm = __builtin_amdgcn_s_memtime();)
-        filter_mb(S, hl);
-        TRACE(asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); { unsigned long long t2 = __builtin_amdgcn_s_memtime(); tph[1] += t2 - tm; tm = t2; })
+        // ---- the rows above: half A from the record, half B from half A's ring entry x
+        // (A's MB x: columns 0..11 after H(x), 12..15 after V(x+1), this step)
+        if (r > R0) Sw[a_top] = h == 0 ? (uint32_t)top : ring_a[(x & (DRING - 1)) * 32 + hl];
+        // half B: the record of MB x-1 is complete
+        if (act && feeds_hb && xl) st_cc64(hb_out + (size_t)(x - 1) * 32 + hl, tag | ring_b[((x + DRING - 1) & (DRING - 1)) * 32 + hl]);
+        wave_sync();
+
+        // ---- horizontal edges of both halves (deblock.cc:506-535)
+        filter_pass(S, hl, 1);
+        wave_sync();
+        TRACE({ asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); const unsigned long long t2 = __builtin_amdgcn_s_memtime(); tph[2] += t2 - tm; tm = t2; })
 
         // ---- write back what is final (see the header comment)
-        const bool xl = x > 0, xr = x == W - 1;
 #pragma unroll
         for (int it = 0; it < NWB; ++it) {
             const int f = wb_flags[it];
             const bool v = act && (f & 1) && (xl || !(f & 2)) && (xr || !(f & 4));
             if (v) *reinterpret_cast<uint32_t*>(wb_ptr[it] + x * ((f & 8) ? 8 : 16)) = Sw[wb_word[it]];
         }
-        // ---- bottom rows of MB x (cols 0..11) and MB x-1 (cols 12..15) into this half's ring
-        if (act && (feeds_ring || feeds_hb)) {
-            uint32_t* ring = reinterpret_cast<uint32_t*>(L.ring[h]);
-#pragma unroll
-            for (int it = 0; it < 2; ++it) {
-                const int k = rg_kind[it];
-                const int ent = k == 1 ? (x + DRING - 1) & (DRING - 1) : x & (DRING - 1);
-                if (k == 0 || (k == 1 && xl) || (k == 2 && xr)) ring[ent * 32 + rg_dst[it]] = Sw[rg_src[it]];
-            }
-        }
+        // ---- bottom rows of MB x, columns 0..11 (all 16 at the row end), into this half's ring
+        if (act && (feeds_ring || feeds_hb)) feed_ring(x, false);
         wave_sync();
-        TRACE({ unsigned long long t2 = __builtin_amdgcn_s_memtime(); tph[2] += t2 - tm; tm = t2; })
-        // ---- half B: completed records (MB x-1, and MB x at the row end) to the hand-off buffer
-        if (act && feeds_hb) {
-            const uint32_t* ring = reinterpret_cast<const uint32_t*>(L.ring[1]);
-            if (xl) st_cc64(hb_out + (size_t)(x - 1) * 32 + hl, tag | ring[((x + DRING - 1) & (DRING - 1)) * 32 + hl]);
-            if (xr) st_cc64(hb_out + (size_t)x * 32 + hl, tag | ring[(x & (DRING - 1)) * 32 + hl]);
-        }
+        // ---- half B at the row end: the last record
+        if (act && feeds_hb && xr) st_cc64(hb_out + (size_t)x * 32 + hl, tag | ring_b[(x & (DRING - 1)) * 32 + hl]);
         // ---- carry the right 4 columns into the left strip of the next tile
 #pragma unroll
         for (int it = 0; it < 2; ++it)

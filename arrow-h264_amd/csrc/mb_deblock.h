@@ -149,8 +149,9 @@ DEV void filter_edge_line(int& p3, int& p2, int& p1, int& p0, int& q0, int& q1, 
 // lines (Cb 16..23, Cr 24..31) run the same 4-edge code: a chroma line has its
 // edges at samples 0 and 4 (chroma edge 1 takes the bS of luma edge 2,
 // StrengthIdx = pel << 1, deblock.cc:430-433, :460) and bS 0 on the other two.
-// Edges no lane of the wave filters are skipped.  Every lane of the wave calls.
-DEV void filter_mb(DbLds& S, int lane)
+// Edges no lane of the wave filters are skipped.  Every lane of the wave calls, and
+// separates the two passes (and whatever it does between them) with wave_sync().
+DEV void filter_pass(DbLds& S, int lane, const int hor)
 {
     const bool luma = lane < 16;
     const int pl = luma ? 0 : 1 + ((lane - 16) >> 3), li = luma ? lane : (lane - 16) & 7;
@@ -164,8 +165,7 @@ DEV void filter_mb(DbLds& S, int lane)
 #pragma unroll
     for (int k = 0; k < 4; ++k) bso[k] = luma ? k * 4 + seg : (k == 0 ? seg : (k == 1 ? 8 + seg : -1));
     const int pe = luma ? 8 : 11 + 3 * (pl - 1), pi = luma ? 10 : 13 + 3 * (pl - 1);
-#pragma unroll 1
-    for (int hor = 0; hor < 2; ++hor) {
+    {
         int bsk[4];
         uint32_t park[4];
 #pragma unroll
@@ -205,7 +205,6 @@ DEV void filter_mb(DbLds& S, int lane)
 #pragma unroll
             for (int i = 1; i < 20; ++i) Tb[i * TP * 4 + li + 4] = (uint8_t)v[i];
         }
-        wave_sync();
     }
 }
 

@@ -35,6 +35,26 @@ with h264r.Decoder(0, W, H) as dec:
             os.environ["H264R_TRACE_OUT"] = out
         dec.decode_batch(db.batch)
         dec.check()
+if flag == 4:
+    # k_deblock: per ticket (pair-major: ticket = pair * n + pic) {start, first step, end,
+    # polling ticks} in 100 MHz ticks, then core cycles of: tile assembly, vertical pass,
+    # horizontal pass (with the rows above), write-back + ring + carry -- summed over the
+    # walk's W + 1 steps
+    t = np.fromfile(out, np.uint64).reshape(-1, 8).astype(np.int64)
+    k = n * ((H + 1) // 2)
+    t = t[:k]
+    t0 = t[:, 0].min()
+    start, end = (t[:, 0] - t0) / 100.0, (t[:, 2] - t0) / 100.0
+    print(f"{n} pictures, {k} waves: kernel span {end.max():.0f} us; wave duration mean {np.mean(end - start):.0f} us")
+    steps = W + 1
+    print(f"polling share {np.mean(t[:, 3] / np.maximum(t[:, 2] - t[:, 0], 1)):.3f}; "
+          f"us per step {np.mean((t[:, 2] - t[:, 1]) / 100.0 / steps):.2f}")
+    print("cycles per step (assemble, V pass, H pass, write-back):", np.round(t[:, 4:8].mean(0) / steps, 0))
+    for p in (0, 1, k // n // 2, k // n - 1):
+        sel = np.arange(k) // n == p
+        print(f"pair {p:3d}: start {start[sel].mean():8.1f} us end {end[sel].mean():8.1f} us, poll "
+              f"{t[sel, 3].mean() / 100.0:8.1f} us, cycles/step {np.round(t[sel, 4:8].mean(0) / steps, 0)}")
+    sys.exit(0)
 t = np.fromfile(out + ".2", np.uint64).reshape(-1, 8).astype(np.int64)
 ng = (n + 15) // 16
 k = ng * H
