@@ -173,31 +173,6 @@ DEV const gdword* row_dwords(const uint8_t* __restrict__ img, int W, int H, int 
     return as_global(img + (size_t)clip3(0, H - 1, y) * W + a);
 }
 
-DEV int rshift_rnd(int x, int a) { return a > 0 ? (x + (1 << (a - 1))) >> a : x; }  // inter_prediction.cc:35-38
-
-// mc_prediction / bi_prediction combine (inter_prediction.cc:53-156) for one sample.
-DEV int wp_combine(const h264r_slice* __restrict__ sl, int dir, int r0, int r1, int v0, int v1, int pl)
-{
-    int mode = sl->wp_mode;
-    if (dir != 2) {
-        if (mode != 1) return dir == 0 ? v0 : v1;
-        int r = dir == 0 ? r0 : r1, v = dir == 0 ? v0 : v1;
-        int w = sl->wp_weight[dir][r][pl], o = sl->wp_offset[dir][r][pl];
-        int d = pl ? sl->chroma_log2_wd : sl->luma_log2_wd;
-        return clip255(rshift_rnd(w * v, d) + o);
-    }
-    if (mode == 0) return (v0 + v1 + 1) >> 1;
-    int w0, w1, o0, o1;
-    if (mode == 1) {
-        w0 = sl->wp_weight[0][r0][pl]; w1 = sl->wp_weight[1][r1][pl];
-        o0 = sl->wp_offset[0][r0][pl]; o1 = sl->wp_offset[1][r1][pl];
-    } else {
-        w1 = sl->implicit_w1[r0][r1]; w0 = 64 - w1; o0 = o1 = 0;
-    }
-    int d = (pl ? sl->chroma_log2_wd : sl->luma_log2_wd) + 1;
-    return clip255(rshift_rnd(w0 * v0 + w1 * v1, d) + ((o0 + o1 + 1) >> 1));
-}
-
 // ---------------------------------------------------------------- deblocking
 // Tables 8-16 / 8-17 (deblock.cc:294-324), packed alpha | beta<<8 | tc0[3]<<16.. in one word.
 __device__ static const uint32_t DB_AB[52] = {

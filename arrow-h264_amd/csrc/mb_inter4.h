@@ -216,10 +216,52 @@ DEV uint32_t chroma_block_pred(const uint8_t* __restrict__ img, int W, int H, in
     return o;
 }
 
-// mc_prediction / bi_prediction combine (inter_prediction.cc:53-156) on 4 packed
-// samples of each list.
-DEV uint32_t wp_combine4(const h264r_slice* __restrict__ sl, int wp_mode, int dir, int r0, int r1, uint32_t v0,
-                         uint32_t v1, int pl)
+// mc_prediction / bi_prediction combine (inter_prediction.cc:53-156) of one lane and
+// plane as w0 * v0 + w1 * v1, rounded right shift by d (rshift_rnd :35-38), + o, with the
+// reference's case split resolved once per plane instead of per sample: one list unweighted
+// {1, 0 | 0, 1; d 0}, one list explicit {w, 0 | 0, w; logWD; o}, both lists unweighted
+// {1, 1; 1}, explicit {w0, w1; logWD + 1; (o0 + o1 + 1) >> 1}, implicit {64 - w1, w1;
+// logWD + 1 = 6}.  The slice's weights are loaded together, not per sample behind branches.
+struct WpPar {
+    int w0, w1, o, d, rnd;
+};
+DEV WpPar wp_params(const h264r_slice* __restrict__ sl, int wp_mode, int dir, int r0, int r1, int pl)
+{
+    const int ra = clip3(0, H264R_MAX_REFS - 1, r0), rb = clip3(0, H264R_MAX_REFS - 1, r1);   // unused list: any entry
+    const int lwd = pl ? sl->chroma_log2_wd : sl->luma_log2_wd;
+    const int wa = sl->wp_weight[0][ra][pl], wb = sl->wp_weight[1][rb][pl];
+    const int oa = sl->wp_offset[0][ra][pl], ob = sl->wp_offset[1][rb][pl];
+    const int iw = sl->implicit_w1[ra][rb];
+    WpPar p;
+    if (dir != 2) {
+        const bool ex = wp_mode == 1;
+        p.w0 = dir == 0 ? (ex ? wa : 1) : 0;
+        p.w1 = dir == 1 ? (ex ? wb : 1) : 0;
+        p.o = ex ? (dir == 0 ? oa : ob) : 0;
+        p.d = ex ? lwd : 0;
+    } else if (wp_mode == 0) {
+        p.w0 = p.w1 = 1; p.o = 0; p.d = 1;
+    } else if (wp_mode == 1) {
+        p.w0 = wa; p.w1 = wb; p.o = (oa + ob + 1) >> 1; p.d = lwd + 1;
+    } else {
+        p.w1 = iw; p.w0 = 64 - iw; p.o = 0; p.d = lwd + 1;
+    }
+    p.rnd = p.d > 0 ? 1 << (p.d - 1) : 0;
+    return p;
+}
+// 4 packed samples of each list
+DEV uint32_t wp_apply4(const WpPar& p, uint32_t v0, uint32_t v1)
+{
+    uint32_t o = 0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const int x = p.w0 * (int)((v0 >> (8 * c)) & 255) + p.w1 * (int)((v1 >> (8 * c)) & 255);
+        o |= (uint32_t)clip255(((x + p.rnd) >> p.d) + p.o) << (8 * c);
+    }
+    return o;
+}
+// The combine of 4 packed samples: weighted prediction off is byte-wise SWAR.
+DEV uint32_t wp_combine4(const WpPar& p, int wp_mode, int dir, uint32_t v0, uint32_t v1)
 {
     if (wp_mode == 0) {
         if (dir == 0) return v0;
@@ -227,11 +269,7 @@ DEV uint32_t wp_combine4(const h264r_slice* __restrict__ sl, int wp_mode, int di
         // (a + b + 1) >> 1 per byte
         return (v0 | v1) - (((v0 ^ v1) >> 1) & 0x7F7F7F7Fu);
     }
-    uint32_t o = 0;
-#pragma unroll
-    for (int c = 0; c < 4; ++c)
-        o |= (uint32_t)wp_combine(sl, dir, r0, r1, (v0 >> (8 * c)) & 255, (v1 >> (8 * c)) & 255, pl) << (8 * c);
-    return o;
+    return wp_apply4(p, v0, v1);
 }
 
 // 4-point inverse transform of one column / row held in registers, (x + 32) >> 6 at
@@ -425,10 +463,15 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
 #endif
         }
         uint32_t predY[4], predC[2];
+        WpPar wpp[3] = {};
+        if (wp_mode != 0) {
     #pragma unroll
-        for (int i = 0; i < 4; ++i) predY[i] = wp_combine4(qs, wp_mode, dir, r0, r1, pY[0][i], pY[1][i], 0);
+            for (int pl = 0; pl < 3; ++pl) wpp[pl] = wp_params(qs, wp_mode, dir, r0, r1, pl);
+        }
     #pragma unroll
-        for (int pl = 0; pl < 2; ++pl) predC[pl] = wp_combine4(qs, wp_mode, dir, r0, r1, pC[0][pl], pC[1][pl], 1 + pl);
+        for (int i = 0; i < 4; ++i) predY[i] = wp_combine4(wpp[0], wp_mode, dir, pY[0][i], pY[1][i]);
+    #pragma unroll
+        for (int pl = 0; pl < 2; ++pl) predC[pl] = wp_combine4(wpp[1 + pl], wp_mode, dir, pC[0][pl], pC[1][pl]);
 
         if constexpr (SP) {
             // ---- itrans_sp of this lane's 4x4 block (:1132-1187): the prediction is
