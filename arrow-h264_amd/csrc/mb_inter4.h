@@ -40,13 +40,20 @@ struct Inter4Lds {
 // Motion of one 4x4 block as {mv, ref_idx | slot << 8} per list: RefPicList[l][ref_idx]
 // of the block's slice resolved to its DPB slot (get_ref_pic dpb.cc:1046-1054;
 // pic_motion_params::ref_pic interpret_mb.cc:611-623), slot -1 when the list is unused.
+// The table of a slice past the LDS copy is read through a buffer load: a select between
+// the LDS and the global byte became one flat load, whose wait covers every outstanding
+// load of both kinds.
 DEV uint2 block_motion(const h264r_batch& b, const h264r_slice* slices, const Inter4Lds& S, size_t at, int slice, int l)
 {
     const uint32_t mv = b.mv[at];
     const int ri = b.ref_idx[at];
-    int slot = -1;
-    if (ri >= 0 && ri < H264R_MAX_REFS)
-        slot = slice < INTER4_LDS_SLICES ? S.ref_slot[slice][l][ri] : slices[slice].ref_slot[l][ri];
+    const bool has = ri >= 0 && ri < H264R_MAX_REFS;
+    int slot = has ? S.ref_slot[min(slice, INTER4_LDS_SLICES - 1)][l][ri] : -1;
+    if (has && slice >= INTER4_LDS_SLICES) {
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<h264r_slice*>(slices + slice), 0,
+                                                                            (int)sizeof(h264r_slice), 0x00020000);
+        slot = (int8_t)__builtin_amdgcn_raw_buffer_load_b8(rs, (int)offsetof(h264r_slice, ref_slot) + l * H264R_MAX_REFS + ri, 0, 0);
+    }
     return make_uint2(mv, (uint32_t)(uint8_t)ri | ((uint32_t)(uint8_t)slot << 8));
 }
 
@@ -346,11 +353,11 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
     const int mi = Y4 * g.W4 + X4;
     const size_t mbase = (size_t)pic * 2 * g.motion_plane;
     const h264r_mb q = mb_lane(&mbs[aa]);
+    const h264r_slice* qs = &slices[q.slice];
+    const uint2 qsh = *reinterpret_cast<const uint2*>(qs);       // type, idc, offsets, wp, log2 wd
     const uint2 m0 = block_motion(b, slices, S, mbase + mi, q.slice, 0);
     const uint2 m1 = block_motion(b, slices, S, mbase + g.motion_plane + mi, q.slice, 1);
     const int hasL = mbx > 0, hasU = mby > 0;
-    const h264r_slice* qs = &slices[q.slice];
-    const uint2 qsh = *reinterpret_cast<const uint2*>(qs);       // type, idc, offsets, wp, log2 wd
     // slice types of the left / upper MBs' slices (SP/SI edges), loaded with qsh
     const int q_type = qsh.x & 255, idc = (qsh.x >> 8) & 255;
     const int offa = (int8_t)((qsh.x >> 16) & 255), offb = (int8_t)(qsh.x >> 24);
