@@ -348,7 +348,7 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
     c->last_stream = s;
     int st;
     if ((st = dev_resize(&c->d_dbinfo, &c->c_dbinfo, (size_t)P * W * H * DBINFO_BYTES))) return st;
-    static const int rows_min = [] { const char* e = getenv("H264R_DEBLOCK2_MIN"); return e ? atoi(e) : 128; }();
+    static const int rows_min = [] { const char* e = getenv("H264R_DEBLOCK2_MIN"); return e ? atoi(e) : 192; }();
     const bool by_rows = (c->debug & H264R_DBG_DEBLOCK_ROWS) || (!(c->debug & H264R_DBG_DEBLOCK_MB) && P >= rows_min);
     // hand-off records of the chosen deblocking kernel; fresh memory or a wrapping epoch
     // restarts from zeroed records, so no record may carry a live tag

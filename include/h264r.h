@@ -265,7 +265,7 @@ int  h264r_set_timing(h264r_ctx* ctx, int enable);
 #define H264R_DBG_INTRA_WALK 2
 /* The loop filter has two schedules (both bit-exact): k_deblock spreads one MB over 32
  * lanes (short latency, small batches), k_deblock2 gives each (picture, MB row) four
- * lanes (batches of >= H264R_DEBLOCK2_MIN pictures, default 128).  These flags
+ * lanes (batches of >= H264R_DEBLOCK2_MIN pictures, default 192).  These flags
  * force one of them. */
 #define H264R_DBG_DEBLOCK_MB   4
 #define H264R_DBG_DEBLOCK_ROWS 8
