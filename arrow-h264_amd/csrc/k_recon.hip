@@ -41,13 +41,14 @@ extern "C" __global__ __launch_bounds__(256, H264R_INTER_WAVES) void k_inter4(h2
     const int groups = (g.wmb * (rows.y - rows.x) + 15) / 16, gb = (groups + 7) / 8;
     const int grp = (blockIdx.x & 7) * gb + (blockIdx.x >> 3);
     if (grp >= groups) return;
-    inter4_lds(b, pic, S);
-    __syncthreads();
     const int lane = threadIdx.x & 63;
     const int a0 = rows.x * g.wmb + (grp * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) * 4;
     const int aend = rows.y * g.wmb;
+    const Inter4Pre pre = inter4_pre(b, g, pic, a0, aend, lane);
+    inter4_lds(b, pic, S);
+    __syncthreads();
     if (a0 >= aend) return;
-    inter4_mbs<false>(b, g, pic, a0, aend, lane, dbinfo + (size_t)pic * g.nmb, S, sp_flag);
+    inter4_mbs<false>(b, g, pic, a0, aend, lane, dbinfo + (size_t)pic * g.nmb, S, sp_flag, pre);
 }
 
 // k_inter_sp: the inter MBs of SP slices (inverse_transform_sp), after k_inter4.  A
@@ -67,6 +68,6 @@ extern "C" __global__ __launch_bounds__(256) void k_inter_sp(h264r_batch b, int2
         inter4_lds(b, pic, S);
         __syncthreads();
         const int a0 = rows.x * g.wmb + (grp * 4 + wave) * 4;
-        if (a0 < aend) inter4_mbs<true>(b, g, pic, a0, aend, lane, nullptr, S, nullptr);
+        if (a0 < aend) inter4_mbs<true>(b, g, pic, a0, aend, lane, nullptr, S, nullptr, inter4_pre(b, g, pic, a0, aend, lane));
     }
 }

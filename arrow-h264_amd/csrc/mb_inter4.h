@@ -43,10 +43,8 @@ struct Inter4Lds {
 // The table of a slice past the LDS copy is read through a buffer load: a select between
 // the LDS and the global byte became one flat load, whose wait covers every outstanding
 // load of both kinds.
-DEV uint2 block_motion(const h264r_batch& b, const h264r_slice* slices, const Inter4Lds& S, size_t at, int slice, int l)
+DEV uint2 motion_word(uint32_t mv, int ri, const h264r_slice* slices, const Inter4Lds& S, int slice, int l)
 {
-    const uint32_t mv = b.mv[at];
-    const int ri = b.ref_idx[at];
     const bool has = ri >= 0 && ri < H264R_MAX_REFS;
     int slot = has ? S.ref_slot[min(slice, INTER4_LDS_SLICES - 1)][l][ri] : -1;
     if (has && slice >= INTER4_LDS_SLICES) {
@@ -55,6 +53,10 @@ DEV uint2 block_motion(const h264r_batch& b, const h264r_slice* slices, const In
         slot = (int8_t)__builtin_amdgcn_raw_buffer_load_b8(rs, (int)offsetof(h264r_slice, ref_slot) + l * H264R_MAX_REFS + ri, 0, 0);
     }
     return make_uint2(mv, (uint32_t)(uint8_t)ri | ((uint32_t)(uint8_t)slot << 8));
+}
+DEV uint2 block_motion(const h264r_batch& b, const h264r_slice* slices, const Inter4Lds& S, size_t at, int slice, int l)
+{
+    return motion_word(b.mv[at], b.ref_idx[at], slices, S, slice, l);
 }
 
 DEV h264r_mb mb_lane(const h264r_mb* p)          // per-lane 32-byte record, two 16-byte loads
@@ -65,6 +67,33 @@ DEV h264r_mb mb_lane(const h264r_mb* p)          // per-lane 32-byte record, two
     uint32_t* w = reinterpret_cast<uint32_t*>(&m);
     w[0] = w0.x; w[1] = w0.y; w[2] = w0.z; w[3] = w0.w; w[4] = w1.x; w[5] = w1.y; w[6] = w1.z; w[7] = w1.w;
     return m;
+}
+
+// A lane's MB record, its block's motion ({mv, ref_idx} per list) and the slice header:
+// none depends on the workgroup's LDS tables, so the kernels issue them before filling
+// those tables (one global round trip less in front of the motion compensation).
+struct Inter4Pre {
+    h264r_mb q;
+    uint32_t mv[2];
+    int ri[2];
+    uint2 qsh;      // type, idc, offsets, wp, log2 wd
+};
+DEV Inter4Pre inter4_pre(const h264r_batch& b, const Geom& g, int pic, int a0, int aend, int lane)
+{
+    const int blk = lane & 15, a = a0 + (lane >> 4);
+    const int aa = a < aend ? a : aend - 1;
+    const int mbx = aa % g.wmb, mby = aa / g.wmb;
+    const int mi = (mby * 4 + (blk >> 2)) * g.W4 + mbx * 4 + (blk & 3);
+    const size_t mbase = (size_t)pic * 2 * g.motion_plane;
+    Inter4Pre p;
+    p.q = mb_lane(&b.mbs[(size_t)pic * g.nmb + aa]);
+#pragma unroll
+    for (int l = 0; l < 2; ++l) {
+        p.mv[l] = b.mv[mbase + l * g.motion_plane + mi];
+        p.ri[l] = b.ref_idx[mbase + l * g.motion_plane + mi];
+    }
+    p.qsh = *reinterpret_cast<const uint2*>(&b.slices[(size_t)pic * b.slice_stride + p.q.slice]);
+    return p;
 }
 
 DEV int sel16(uint32_t lo, uint32_t hi, int c) { return (int16_t)(((c & 2) ? hi : lo) >> (16 * (c & 1))); }
@@ -337,7 +366,7 @@ DEV void fwd4(int p0, int p1, int p2, int p3, int& c0, int& c1, int& c2, int& c3
 // inverse_transform_sp (decoder.cc:256-257, transform.cc:1267-1300), and no records.
 template <bool SP>
 DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int aend, int lane, DbInfo* __restrict__ dbout,
-                    const Inter4Lds& S, int* sp_flag)
+                    const Inter4Lds& S, int* sp_flag, const Inter4Pre& pre)
 {
     const int grp = lane >> 4, blk = lane & 15, bx = blk & 3, by = blk >> 2;
     const int a = a0 + grp;
@@ -352,11 +381,11 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
     const int X4 = mbx * 4 + bx, Y4 = mby * 4 + by;
     const int mi = Y4 * g.W4 + X4;
     const size_t mbase = (size_t)pic * 2 * g.motion_plane;
-    const h264r_mb q = mb_lane(&mbs[aa]);
+    const h264r_mb q = pre.q;
     const h264r_slice* qs = &slices[q.slice];
-    const uint2 qsh = *reinterpret_cast<const uint2*>(qs);       // type, idc, offsets, wp, log2 wd
-    const uint2 m0 = block_motion(b, slices, S, mbase + mi, q.slice, 0);
-    const uint2 m1 = block_motion(b, slices, S, mbase + g.motion_plane + mi, q.slice, 1);
+    const uint2 qsh = pre.qsh;
+    const uint2 m0 = motion_word(pre.mv[0], pre.ri[0], slices, S, q.slice, 0);
+    const uint2 m1 = motion_word(pre.mv[1], pre.ri[1], slices, S, q.slice, 1);
     const int hasL = mbx > 0, hasU = mby > 0;
     // slice types of the left / upper MBs' slices (SP/SI edges), loaded with qsh
     const int q_type = qsh.x & 255, idc = (qsh.x >> 8) & 255;
