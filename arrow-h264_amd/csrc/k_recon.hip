@@ -14,7 +14,8 @@ using namespace h264r;
 #ifndef H264R_INTER_WAVES
 #define H264R_INTER_WAVES 3                 // minimum waves per SIMD asked of the register allocator (<= 168 VGPRs)
 #endif
-// The workgroup's copy of the DPB plane table and of picture `pic`'s slice ref tables.
+// The workgroup's copy of the DPB plane table and of picture `pic`'s slice ref tables and
+// slice types.
 DEV void inter4_lds(const h264r_batch& b, int pic, Inter4Lds& S)
 {
     if (threadIdx.x < 3 * H264R_MAX_SLOTS) S.planes[threadIdx.x] = b.ref_planes[threadIdx.x];
@@ -24,6 +25,7 @@ DEV void inter4_lds(const h264r_batch& b, int pic, Inter4Lds& S)
     for (int i = threadIdx.x; i < nsl * 4; i += blockDim.x)
         *reinterpret_cast<uint2*>(&S.ref_slot[i >> 2][0][0] + 8 * (i & 3)) =
             *reinterpret_cast<const uint2*>(&sl[i >> 2].ref_slot[0][0] + 8 * (i & 3));
+    if (threadIdx.x >= 64 && threadIdx.x - 64 < nsl) S.slice_type[threadIdx.x - 64] = sl[threadIdx.x - 64].slice_type;
 }
 
 // sp_flag: set when an inter MB of an SP slice was met (k_inter_sp then runs).

@@ -35,23 +35,35 @@ constexpr int INTER4_LDS_SLICES = 64;   // slices whose ref tables the workgroup
 struct Inter4Lds {
     const uint8_t* planes[3 * H264R_MAX_SLOTS];
     int8_t ref_slot[INTER4_LDS_SLICES][2][H264R_MAX_REFS];   // h264r_slice::ref_slot of the picture's slices
+    uint8_t slice_type[INTER4_LDS_SLICES];                   // h264r_slice::slice_type of the same slices
 };
+
+// Byte `off` of slice `slice`'s h264r_slice, for the slices past the LDS copy: a buffer
+// load (a select between an LDS and a global byte became one flat load, whose wait covers
+// every outstanding load of both kinds).
+DEV int slice_byte(const h264r_slice* slices, int slice, int off)
+{
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<h264r_slice*>(slices + slice), 0,
+                                                                        (int)sizeof(h264r_slice), 0x00020000);
+    return __builtin_amdgcn_raw_buffer_load_b8(rs, off, 0, 0);
+}
+// slice_type of a slice: the LDS copy, else the slice table
+DEV int slice_type_of(const h264r_slice* slices, const Inter4Lds& S, int slice)
+{
+    int t = S.slice_type[min(slice, INTER4_LDS_SLICES - 1)];
+    if (slice >= INTER4_LDS_SLICES) t = slice_byte(slices, slice, (int)offsetof(h264r_slice, slice_type));
+    return t;
+}
 
 // Motion of one 4x4 block as {mv, ref_idx | slot << 8} per list: RefPicList[l][ref_idx]
 // of the block's slice resolved to its DPB slot (get_ref_pic dpb.cc:1046-1054;
 // pic_motion_params::ref_pic interpret_mb.cc:611-623), slot -1 when the list is unused.
-// The table of a slice past the LDS copy is read through a buffer load: a select between
-// the LDS and the global byte became one flat load, whose wait covers every outstanding
-// load of both kinds.
 DEV uint2 motion_word(uint32_t mv, int ri, const h264r_slice* slices, const Inter4Lds& S, int slice, int l)
 {
     const bool has = ri >= 0 && ri < H264R_MAX_REFS;
     int slot = has ? S.ref_slot[min(slice, INTER4_LDS_SLICES - 1)][l][ri] : -1;
-    if (has && slice >= INTER4_LDS_SLICES) {
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<h264r_slice*>(slices + slice), 0,
-                                                                            (int)sizeof(h264r_slice), 0x00020000);
-        slot = (int8_t)__builtin_amdgcn_raw_buffer_load_b8(rs, (int)offsetof(h264r_slice, ref_slot) + l * H264R_MAX_REFS + ri, 0, 0);
-    }
+    if (has && slice >= INTER4_LDS_SLICES)
+        slot = (int8_t)slice_byte(slices, slice, (int)offsetof(h264r_slice, ref_slot) + l * H264R_MAX_REFS + ri);
     return make_uint2(mv, (uint32_t)(uint8_t)ri | ((uint32_t)(uint8_t)slot << 8));
 }
 DEV uint2 block_motion(const h264r_batch& b, const h264r_slice* slices, const Inter4Lds& S, size_t at, int slice, int l)
@@ -865,7 +877,7 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
     const int lsl = bx > 0 ? q.slice : L.slice, usl = by > 0 ? q.slice : U.slice;
     const uint2 l0 = block_motion(b, slices, S, mbase + li, lsl, 0), l1 = block_motion(b, slices, S, mbase + g.motion_plane + li, lsl, 1);
     const uint2 u0 = block_motion(b, slices, S, mbase + ui, usl, 0), u1 = block_motion(b, slices, S, mbase + g.motion_plane + ui, usl, 1);
-    const int l_type = slices[L.slice].slice_type, u_type = slices[U.slice].slice_type;
+    const int l_type = slice_type_of(slices, S, L.slice), u_type = slice_type_of(slices, S, U.slice);
     // ---- deblocking record (Deblock::strength deblock.cc:78-289): this lane's
     // left edge (vertical edge bx, segment by) and top edge (horizontal edge by,
     // segment bx)
