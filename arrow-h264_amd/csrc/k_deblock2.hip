@@ -128,8 +128,16 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2
     const __amdgpu_buffer_rsrc_t hrs = __builtin_amdgcn_make_buffer_rsrc(hb, 0, hb_bytes, 0x00020000);
     const uint32_t rec_out = (uint32_t)(((size_t)pic * 2 + (ry & 1)) * W * RECG * 8);
     const uint32_t rec_in = (uint32_t)(((size_t)pic * 2 + ((ry + 1) & 1)) * W * RECG * 8);
-    // pair k (granules 2k, 2k+1) of consumer lane c of MB m
-    auto pair_off = [&](uint32_t base, int m, int c, int k) -> uint32_t { return base + (uint32_t)(m * RECG + c * 6 + 2 * k) * 8u; };
+    // pair k (granules 2k, 2k+1) of consumer lane c of MB m.  An MB's 12 pairs form three
+    // 64-byte blocks, each stored by ONE instruction of the unit's four lanes (one whole
+    // write-through segment instead of four partial ones): block 0 = the early pairs
+    // (0,0) (0,1) (0,2) (1,0), block 1 = the early (2,0) (2,1) (2,2) (1,1), block 2 = the
+    // late (1,2) (3,0) (3,1) (3,2).
+    auto pair_off = [&](uint32_t base, int m, int c, int k) -> uint32_t {
+        const int blk = c == 0 ? 0 : c == 2 ? 1 : c == 3 ? 2 : (k < 2 ? k : 2);
+        const int slot = c == 0 || c == 2 ? k : c == 3 ? k + 1 : (k < 2 ? 3 : 0);
+        return base + (uint32_t)(m * RECG) * 8u + (uint32_t)(blk * 4 + slot) * 16u;
+    };
     auto load_pair = [&](int m, int k) -> v4u {
         return __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(hrs, pair_off(rec_in, m, q, k), 0, AUX_SC1));
     };
@@ -225,11 +233,11 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, v), hrs,
                                                pair_off(rec_out, m, c, k), 0, AUX_SC1);
     };
-    // early pairs: 8, two per lane; late pairs: 4, one per lane
-    auto early_c = [&](int j) { return j < 6 ? (j < 3 ? 0 : 2) : 1; };
-    auto early_k = [&](int j) { return j < 6 ? j % 3 : j - 6; };
-    auto late_c = [&](int j) { return j == 0 ? 1 : 3; };
-    auto late_k = [&](int j) { return j == 0 ? 2 : j - 1; };
+    // early pairs: 8, block j slot q from lane q; late pairs: 4, block 2 slot q from lane q
+    auto early_c = [&](int lq, int j) { return lq < 3 ? (j ? 2 : 0) : 1; };
+    auto early_k = [&](int lq, int j) { return lq < 3 ? lq : j; };
+    auto late_c = [&](int lq) { return lq == 0 ? 1 : 3; };
+    auto late_k = [&](int lq) { return lq == 0 ? 2 : lq - 1; };
     // DbInfo of MB m: 5 pieces of 16 bytes, piece q and (every lane) piece 4
     v4u ninf[2];
     auto load_info = [&](int m) {
@@ -430,7 +438,7 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2
         // 6. publish / store what is final now: the 16 granules of MB x that MB x+1 cannot
         // change, four per lane (at the row end the late ones are final too)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) publish_pair(x, early_c(2 * q + j), early_k(2 * q + j), tag32);
+        for (int j = 0; j < 2; ++j) publish_pair(x, early_c(q, j), early_k(q, j), tag32);
         if (x == W - 1) publish_pair(x, late_c(q), late_k(q), tag32);
         if (above) {
             // rows 13..15 of MB (x, y-1), my luma dword; chroma row 7 of my plane, my dword
