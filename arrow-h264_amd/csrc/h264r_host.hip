@@ -22,10 +22,15 @@
 
 #include "h264r.h"
 
+#ifndef H264R_WALK_ROWS
+#define H264R_WALK_ROWS 8       // k_intra_pic: MB rows per band = waves per workgroup (k_picture.hip)
+#endif
+
 namespace h264r { struct DbInfo; }
 extern "C" __global__ void k_inter4(h264r_batch b, h264r::DbInfo* dbinfo, int2 rows, int* sp_flag);
 extern "C" __global__ void k_inter_sp(h264r_batch b, int2 rows, const int* sp_flag);
-extern "C" __global__ void k_intra_pic(h264r_batch b, int* sync, int* err, const uint16_t* lvl, int lmax, int2 rows);
+extern "C" __global__ void k_intra_pic(h264r_batch b, int* sync, int* err, const uint16_t* lvl, int lmax, int2 rows,
+                                      int gstep);
 extern "C" __global__ void k_level(h264r_batch b, uint16_t* lvl, int* lvsync, int* lcount, int2 rows);
 extern "C" __global__ void k_level_scan(const int* lcount, int* lbase);
 extern "C" __global__ void k_level_scatter(h264r_batch b, const uint16_t* lvl, const int* lbase, int* lcursor,
@@ -334,7 +339,7 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
 {
     const int W = b.width_mbs, H = b.height_mbs, P = b.num_pics, HB = row1 - row0;
     const int2 rows = make_int2(row0, row1);
-    const int nbands = (HB + 15) / 16, npairs = (HB + 1) / 2;
+    const int nbands = (HB + H264R_WALK_ROWS - 1) / H264R_WALK_ROWS, npairs = (HB + 1) / 2;
     // scratch: per-MB deblocking records, tagged hand-off
     // records, and a sync region [intra ticket + per-(picture,row) progress][deblock
     // ticket][level barrier, deepest level][SP inter MBs seen]
@@ -442,8 +447,12 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
                 HIP_OK(hipGetLastError());
             }
         }
-        hipLaunchKernelGGL(k_intra_pic, dim3(P * nbands), dim3(1024), 0, s, b, sync, c->d_err,
-                           (const uint16_t*)lvl, lmax, rows);
+        // the walk's band-to-band hand-off: global progress every gstep MBs (k_picture.hip);
+        // H264R_WALK_GSTEP overrides
+        static const int gstep_env = [] { const char* e = getenv("H264R_WALK_GSTEP"); return e ? atoi(e) : 0; }();
+        const int gstep = gstep_env > 0 ? gstep_env : (P >= 128 ? 64 : 1);
+        hipLaunchKernelGGL(k_intra_pic, dim3(P * nbands), dim3(64 * H264R_WALK_ROWS), 0, s, b, sync, c->d_err,
+                           (const uint16_t*)lvl, lmax, rows, gstep);
         HIP_OK(hipGetLastError());
     }
     if (!(c->debug & H264R_DBG_NO_DEBLOCK)) {

@@ -4,12 +4,12 @@
 // (intra_prediction.cc:140-186), so MB (x,y) depends on (x-1,y), (x,y-1) and
 // (x+1,y-1): a wavefront with a 2-MB lag per row.
 //
-// A picture is cut into bands of <= 16 MB rows; one 1024-thread workgroup owns a
-// band and each wave owns one row, walking it left to right.  Inside a band the
+// A picture is cut into bands of <= 8 MB rows (H264R_WALK_ROWS); one 512-thread workgroup
+// owns a band and each wave owns one row, walking it left to right.  Inside a band the
 // row-to-row hand-off is an LDS counter with workgroup-scope release/acquire
 // (no inter-CU traffic).  Only the first row of a band waits on another
 // workgroup (the last row of the band above), through a progress counter in
-// global memory published with agent-scope release after every intra MB
+// global memory published with agent-scope release every `gstep` intra MBs
 // (MI355X_MICROARCH.md, Guideline 16 recipe).  Workgroups take (band, picture)
 // tickets in band-major order from an atomic counter, so every workgroup only
 // ever waits on a ticket taken earlier by a resident workgroup: no deadlock
@@ -26,7 +26,13 @@ using namespace h264r;
 
 namespace {
 
-constexpr int WAVES = 16;                   // rows per band
+#ifndef H264R_WALK_ROWS
+#define H264R_WALK_ROWS 8                   // MB rows per band (h264r_host.hip sizes the launch with it)
+#endif
+#ifndef H264R_WALK_WAVES
+#define H264R_WALK_WAVES 4                  // minimum waves per SIMD asked of the register allocator (<= 128 VGPRs)
+#endif
+constexpr int WAVES = H264R_WALK_ROWS;      // rows per band, one wave each
 constexpr unsigned SPIN_LIMIT = 1u << 24;   // bounded wait, then flag an error
 
 DEV void publish_lds(int* counter, int value, int lane)
@@ -63,20 +69,17 @@ DEV bool wait_for(int* counter, int need, int* err)
 
 }  // namespace
 
+// One (band, picture) ticket: wave `wave` walks MB row r0 + wave of the band.
 // sync: [0] ticket counter, [1 ..] per (picture, row) progress; zeroed before every launch.
 template <typename Scratch>
-DEV void picture_walk(const h264r_batch& b, int* sync, int* err, Scratch* scratch,
-                      int* lprog, int* ticket_lds, const uint16_t* __restrict__ lvl, int lmax, int2 rows)
+DEV void walk_ticket(const h264r_batch& b, int* sync, int* err, Scratch* scratch, int* lprog, int ticket,
+                     const uint16_t* __restrict__ lvl, int lmax, int2 rows, int gstep)
 {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const Geom g = make_geom(b.width_mbs, b.height_mbs);
     const int R0 = rows.x, R1 = rows.y, HB = R1 - R0;         // MB rows of this launch
     const int nbands = (HB + WAVES - 1) / WAVES;
-    const int bh = (HB + nbands - 1) / nbands;               // rows per band (<= 16)
-    if (threadIdx.x == 0) *ticket_lds = atomicAdd(&sync[0], 1);
-    if (threadIdx.x < WAVES) lprog[threadIdx.x] = 0;
-    __syncthreads();
-    const int ticket = *ticket_lds;
+    const int bh = (HB + nbands - 1) / nbands;               // rows per band (<= WAVES)
     const int band = ticket / b.num_pics, pic = ticket % b.num_pics;
     const int r0 = R0 + band * bh, r1 = min(R1, r0 + bh);
     const int r = r0 + wave;
@@ -106,12 +109,30 @@ DEV void picture_walk(const h264r_batch& b, int* sync, int* err, Scratch* scratc
         }
         return g.wmb;
     };
-    auto publish = [&](int v) {
-        if (last_row) publish_global(&gprog[r], v, lane);
-        else publish_lds(&lprog[wave], v, lane);
+    // The band's last row publishes to the next band through global memory, an agent-scope
+    // release (L2 write-back of the XCD's dirty lines) each time: every `gstep` MBs and at
+    // the row end.  With band-major tickets the next band of a picture comes a batch's worth
+    // of tickets later, so large batches take a coarse gstep (the next band's first row is
+    // not waiting; one release per MB on every band's last row cost config 2 a quarter of its
+    // walk time, profiles/r02_intra_walk_gstep.txt), small ones 1.
+    // A row that stored nothing since its last global publish (no intra MB) skips the
+    // release: the relaxed flag store alone.
+    int gpub = -1;
+    bool dirty = false;
+    auto publish = [&](int v, bool force) {
+        if (last_row) {
+            if (force || v >= g.wmb || v - gpub >= gstep) {
+                if (dirty) publish_global(&gprog[r], v, lane);
+                else if (lane == 0) __hip_atomic_store(&gprog[r], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                gpub = v;
+                dirty = false;
+            }
+        } else {
+            publish_lds(&lprog[wave], v, lane);
+        }
     };
     int x = next_intra(0);
-    publish(x);
+    publish(x, true);
     while (x < g.wmb && ok) {
         if (r > R0) {
             const int need = min(x + 2, g.wmb);
@@ -120,21 +141,25 @@ DEV void picture_walk(const h264r_batch& b, int* sync, int* err, Scratch* scratc
         }
         if (!ok) break;
         intra_mb2(b, g, pic, x, r, lane, S);
+        dirty = true;
         x = next_intra(x + 1);
-        publish(x);
+        publish(x, false);
     }
-    if (!ok) publish(g.wmb);   // let every waiter behind a failed wave finish (outputs are flagged invalid)
+    if (!ok) { dirty = true; publish(g.wmb, true); }   // let every waiter behind a failed wave finish (outputs are flagged invalid)
 }
 
 // lvl / lmax: intra MBs with lvl <= lmax were reconstructed by the k_intra_lvl
 // launches before this one (lvl == nullptr: the walk does every intra MB).
-extern "C" __global__ __launch_bounds__(1024) void k_intra_pic(h264r_batch b, int* sync, int* err,
-                                                              const uint16_t* lvl, int lmax, int2 rows)
+extern "C" __global__ __launch_bounds__(64 * H264R_WALK_ROWS, H264R_WALK_WAVES) void k_intra_pic(h264r_batch b, int* sync, int* err,
+                                                              const uint16_t* lvl, int lmax, int2 rows, int gstep)
 {
     __shared__ IntraScratch scratch[WAVES];
     __shared__ int lprog[WAVES];
     __shared__ int ticket;
-    picture_walk(b, sync, err, scratch, lprog, &ticket, lvl, lmax, rows);
+    if (threadIdx.x == 0) ticket = atomicAdd(&sync[0], 1);
+    if (threadIdx.x < WAVES) lprog[threadIdx.x] = 0;
+    __syncthreads();
+    walk_ticket(b, sync, err, scratch, lprog, ticket, lvl, lmax, rows, gstep);
 }
 
 // ------------------------------------------------------------ level schedule
