@@ -48,13 +48,16 @@ DEV void publish_global(int* counter, int value, int lane)
     if (lane == 0) __hip_atomic_store(counter, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// seen: the progress value observed (and acquired); a later need <= seen needs no new wait:
+// what was published before that value was visible after the acquire that followed it.
 template <bool GLOBAL>
-DEV bool wait_for(int* counter, int need, int* err)
+DEV bool wait_for(int* counter, int need, int* err, int& seen)
 {
     unsigned spins = 0;
     for (;;) {
         int v = GLOBAL ? __hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                        : __hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        seen = v;
         if (v >= need) break;
         __builtin_amdgcn_s_sleep(1);
         if (++spins > SPIN_LIMIT) {
@@ -133,11 +136,12 @@ DEV void walk_ticket(const h264r_batch& b, int* sync, int* err, Scratch* scratch
     };
     int x = next_intra(0);
     publish(x, true);
+    int seen = 0;                                            // progress of the row above, acquired
     while (x < g.wmb && ok) {
-        if (r > R0) {
-            const int need = min(x + 2, g.wmb);
-            if (wave == 0) ok = wait_for<true>(&gprog[r - 1], need, err);
-            else ok = wait_for<false>(&lprog[wave - 1], need, err);
+        const int need = min(x + 2, g.wmb);
+        if (r > R0 && need > seen) {
+            if (wave == 0) ok = wait_for<true>(&gprog[r - 1], need, err, seen);
+            else ok = wait_for<false>(&lprog[wave - 1], need, err, seen);
         }
         if (!ok) break;
         intra_mb2(b, g, pic, x, r, lane, S);
