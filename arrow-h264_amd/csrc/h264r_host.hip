@@ -42,7 +42,7 @@ constexpr int LEVEL_LISTS = 64;           // levels with MB lists (H264R_LEVEL_L
 extern "C" __global__ void k_deblock(h264r_batch b, const h264r::DbInfo* dbinfo, uint64_t* hb,
                                      int* sync, int* err, uint32_t epoch, int2 rows);
 extern "C" __global__ void k_deblock2(h264r_batch b, const h264r::DbInfo* dbinfo, uint64_t* hb,
-                                      int* sync, int* err, uint32_t epoch, int2 rows);
+                                      int* sync, int* err, uint32_t epoch, int2 rows, int nx);
 constexpr size_t DBINFO_BYTES = 80;
 constexpr size_t HANDOFF_BYTES = 256;   // one tagged record (32 x {dword, epoch}) per MB
 constexpr size_t HANDOFF2_BYTES = 384;  // k_deblock2: 2 row slots x 24 x {dword, tag} per MB column
@@ -134,6 +134,7 @@ struct h264r_ctx {
     uint32_t* d_list = nullptr; size_t c_list = 0; // intra MBs by level (pic * nmb + addr)
     int* d_lcnt = nullptr; size_t c_lcnt = 0;      // [count | base | cursor] x (LEVEL_LISTS + 2)
     int levels_grid = 0;                           // resident workgroups of k_intra_levels
+    int nxcc = 0;                                  // XCDs of the device (k_deblock2's placement)
     // the per-batch scratch above is reused by every launch: a launch on a stream other
     // than the previous one first waits for the previous launch (ev_last)
     hipStream_t last_stream = nullptr;
@@ -343,7 +344,7 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
     // scratch: per-MB deblocking records, tagged hand-off
     // records, and a sync region [intra ticket + per-(picture,row) progress][deblock
     // ticket][level barrier, deepest level][SP inter MBs seen]
-    const size_t sync_n = 1 + (size_t)P * H + 5;
+    const size_t sync_n = 1 + (size_t)P * H + 5 + 8;   // + k_deblock2's per-XCD ticket counters
     // the scratch is shared by every launch of this context: a launch on another stream
     // than the previous one waits for it first
     if (c->last_stream && c->last_stream != s) {
@@ -458,8 +459,20 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
     if (!(c->debug & H264R_DBG_NO_DEBLOCK)) {
         Timed t(c, 2, s);
         if (by_rows)
-            hipLaunchKernelGGL(k_deblock2, dim3(((P + DEBLOCK2_UNITS - 1) / DEBLOCK2_UNITS) * HB), dim3(64), 0, s, b, dbinfo,
-                               reinterpret_cast<uint64_t*>(c->d_hb2), sync + 1 + (size_t)P * H, c->d_err, ++c->epoch2, rows);
+        {
+            // k_deblock2 keeps a 16-picture group on one XCD (g % nx): nx counters
+            if (!c->nxcc) {
+                int nx = 1;
+                if (hipDeviceGetAttribute(&nx, hipDeviceAttributeNumberOfXccs, c->device) != hipSuccess) nx = 1;
+                c->nxcc = std::max(1, std::min(nx, 8));
+            }
+            int grid = ((P + DEBLOCK2_UNITS - 1) / DEBLOCK2_UNITS) * HB;
+            const int nx = grid >= 64 * c->nxcc ? c->nxcc : 1;
+            grid = (grid + nx - 1) / nx * nx;
+            hipLaunchKernelGGL(k_deblock2, dim3(grid), dim3(64), 0, s, b, dbinfo,
+                               reinterpret_cast<uint64_t*>(c->d_hb2), sync + 1 + (size_t)P * H + 5, c->d_err, ++c->epoch2, rows,
+                               nx);
+        }
         else
             hipLaunchKernelGGL(k_deblock, dim3(P * npairs), dim3(64), 0, s, b, dbinfo,
                                reinterpret_cast<uint64_t*>(c->d_hb), sync + 1 + (size_t)P * H, c->d_err, ++c->epoch, rows);

@@ -94,18 +94,48 @@ extern "C" void h264r_db2_trace_copy(void* dst) { (void)hipMemcpyFromSymbol(dst,
 // (two granules; each 8-byte half observed untorn on gfx950, MI355X_MICROARCH.md
 // visibility: the tag check stays per granule); sync[0]: ticket counter;
 // epoch < 2^20 (the host restarts from zeroed records before it wraps).
+// XCD-local hand-off (H264R_DB2_XCD, default): the rows of a 16-picture group all run on
+// one XCD -- group g on XCD g % nx, each XCD with its own ticket counter (the XCD read
+// from the hardware register, so the placement holds whatever the dispatch order) -- and
+// the hand-off records are plain stores, which stay in that XCD's L2, read back by `sc1`
+// loads (L1 bypassed, L2 hit) instead of write-through stores and loads served from the
+// fabric.  Each wave takes tickets until its XCD's run out, so an XCD finishes its groups
+// as long as any wave lands on it: the host asks for this mode (nx > 1) only for grids of
+// >= 64 waves per XCD, rounded up to whole round-robin cycles.
+#ifndef H264R_DB2_XCD
+#define H264R_DB2_XCD 1
+#endif
 extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_deblock2(
-    h264r_batch b, const DbInfo* __restrict__ dbinfo, uint64_t* hb, int* sync, int* err, uint32_t epoch, int2 rows)
+    h264r_batch b, const DbInfo* __restrict__ dbinfo, uint64_t* hb, int* sync, int* err, uint32_t epoch, int2 rows, int nx)
 {
     __shared__ UnitLds S[UNITS];
-    const int lane = threadIdx.x, u = lane >> 2, q = lane & 3;
     const Geom g = make_geom(b.width_mbs, b.height_mbs);
     const int W = g.wmb, R0 = rows.x, R1 = rows.y;
     const int ngroups = (b.num_pics + UNITS - 1) / UNITS;
+    // nx == 1 (small grids, one-XCD partitions, H264R_DB2_XCD=0): one counter, write-through
+    // records, any wave on any XCD
+#if !H264R_DB2_XCD
+    nx = 1;
+#endif
+    unsigned xcc_reg = 0;
+    if (nx > 1) asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc_reg));
+    const int xcc = (int)(xcc_reg & 15u) % nx;
+    const int ngx = (ngroups - xcc + nx - 1) / nx;           // groups xcc, xcc + nx, ...
+    int* counter = &sync[xcc];
+    const bool local = nx > 1;                                // records: plain stores, kept in the XCD's L2
+    const int items = ngx * (R1 - R0);
+    for (;;) {
+    __syncthreads();                                          // the previous item's LDS reads are done
     int tk = 0;
-    if (lane == 0) tk = atomicAdd(&sync[0], 1);
+    if (threadIdx.x == 0) tk = atomicAdd(counter, 1);
     const int ticket = __builtin_amdgcn_readfirstlane(tk);
-    const int ry = ticket / ngroups, grp = ticket - ry * ngroups;
+    if (ticket >= items) return;
+    const int ry = ticket / ngx, grp = (ticket - ry * ngx) * nx + xcc;
+    // lane, opaque per item: what derives from it is recomputed per item, not hoisted out of
+    // the ticket loop and kept live across it (that spilled 31 VGPRs)
+    int lane = threadIdx.x;
+    asm volatile("" : "+v"(lane));
+    const int u = lane >> 2, q = lane & 3;
     const int y = R0 + ry;
     const int pic_raw = grp * UNITS + u;
     const bool active = pic_raw < b.num_pics;
@@ -230,8 +260,9 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2
     // chroma dword 1, lane 3's three with luma dword 3 / chroma dword 1).
     auto publish_pair = [&](int m, int c, int k, uint32_t t) {
         const v4u v = {granule(m, c, 2 * k), t, granule(m, c, 2 * k + 1), t};
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, v), hrs,
-                                               pair_off(rec_out, m, c, k), 0, AUX_SC1);
+        const auto w = __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, v);
+        if (local) __builtin_amdgcn_raw_buffer_store_b128(w, hrs, pair_off(rec_out, m, c, k), 0, 0);
+        else __builtin_amdgcn_raw_buffer_store_b128(w, hrs, pair_off(rec_out, m, c, k), 0, AUX_SC1);
     };
     // early pairs: 8, block j slot q from lane q; late pairs: 4, block 2 slot q from lane q
     auto early_c = [&](int lq, int j) { return lq < 3 ? (j ? 2 : 0) : 1; };
@@ -480,12 +511,14 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2
         for (int x = 0; x < W; ++x)
             for (int k = 0; k < 3; ++k) {
                 const v4u v = {0u, tag32, 0u, tag32};
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, v), hrs,
-                                                       pair_off(rec_out, x, q, k), 0, AUX_SC1);
+                const auto w = __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, v);
+                if (local) __builtin_amdgcn_raw_buffer_store_b128(w, hrs, pair_off(rec_out, x, q, k), 0, 0);
+                else __builtin_amdgcn_raw_buffer_store_b128(w, hrs, pair_off(rec_out, x, q, k), 0, AUX_SC1);
             }
     }
     TRACE(if (lane == 0 && ticket < (1 << 16)) {
         h264r_db2_trace[ticket][0] = tr_start; h264r_db2_trace[ticket][1] = __builtin_amdgcn_s_memrealtime();
         for (int i = 0; i < 4; ++i) h264r_db2_trace[ticket][2 + i] = tph[i];
         h264r_db2_trace[ticket][6] = (unsigned long long)W; })
+    }
 }

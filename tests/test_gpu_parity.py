@@ -109,6 +109,38 @@ def _batch_vs_oracle(L, dec, cidx, W, H, n, debug=0, deblocks=DEBLOCKS, qm=None,
                 assert d is None, f"deblock flag {db_flag} picture {i} plane {k}: {d}"
 
 
+def _large_batch_vs_oracle(L, dec, cidx, W, H, n, nbase=8):
+    """n pictures = nbase distinct ones repeated: every output is compared with the oracle's
+    decode of its base picture (a large batch at little oracle cost)."""
+    cfg = synth.default_cfg(L, cidx, W, H)
+    base = [synth.picture(L, cfg, i) for i in range(nbase)]
+    refs = synth.refpics(L, cfg)
+    for s, (y, u, v) in enumerate(refs):
+        dec.set_ref(s, y, u, v)
+    want = [O.decode(p, refs) for p in base]
+    host = B.pack([base[i % nbase] for i in range(n)], h264r.quant_flat())
+    db = B.to_device(host, n, None)
+    dec.set_debug(A.DBG_DEBLOCK_ROWS)
+    try:
+        dec.decode_batch(db.batch)
+        dec.check()
+    finally:
+        dec.set_debug(0)
+    for i in range(n):
+        got = db.planes(i)
+        for k in range(3):
+            d = first_diff(got[k], want[i % nbase][k], 16 if k == 0 else 8)
+            assert d is None, f"picture {i} plane {k}: {d}"
+
+
+@pytest.mark.parametrize("cidx", [2, 3])
+def test_gpu_large_batch_xcd_groups(L, dec, cidx):
+    """464 CIF pictures (29 groups of 16 x 18 MB rows = 522 k_deblock2 waves): k_deblock2 in
+    its XCD-local mode (groups on XCD g % 8, plain-store records) and the walk's coarse
+    band hand-off (batches >= 128 pictures); every picture checked."""
+    _large_batch_vs_oracle(L, dec, cidx, 22, 18, 464)
+
+
 def test_gpu_batch_cif_p(L, dec):
     _batch_vs_oracle(L, dec, 3, 22, 18, 6)
 
