@@ -40,7 +40,7 @@ extern "C" __global__ void k_intra_levels(h264r_batch b, const int* lcount, cons
 constexpr int LEVEL_MAX_MBS = 65536;      // k_level's LDS bitmap (k_picture.hip)
 constexpr int LEVEL_LISTS = 64;           // levels with MB lists (H264R_LEVEL_LISTS, k_picture.hip)
 extern "C" __global__ void k_deblock(h264r_batch b, const h264r::DbInfo* dbinfo, uint64_t* hb,
-                                     int* sync, int* err, uint32_t epoch, int2 rows);
+                                     int* sync, int* err, uint32_t epoch, int2 rows, int nx);
 extern "C" __global__ void k_deblock2(h264r_batch b, const h264r::DbInfo* dbinfo, uint64_t* hb,
                                       int* sync, int* err, uint32_t epoch, int2 rows, int nx);
 constexpr size_t DBINFO_BYTES = 80;
@@ -338,6 +338,11 @@ static int level_launches()
 // k_intra_levels + k_intra_pic (intra MBs), k_deblock or k_deblock2 (by batch size).
 static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row0, int row1)
 {
+    // H264R_DEBUG=<flags>: h264r_set_debug flags OR-ed into every launch (measurement A/B)
+    static const int env_debug = [] { const char* e = getenv("H264R_DEBUG"); return e ? atoi(e) : 0; }();
+    const int debug_saved = c->debug;
+    c->debug |= env_debug;
+    struct Restore { h264r_ctx* c; int d; ~Restore() { c->debug = d; } } restore{c, debug_saved};
     const int W = b.width_mbs, H = b.height_mbs, P = b.num_pics, HB = row1 - row0;
     const int2 rows = make_int2(row0, row1);
     const int nbands = (HB + H264R_WALK_ROWS - 1) / H264R_WALK_ROWS, npairs = (HB + 1) / 2;
@@ -458,24 +463,30 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
     }
     if (!(c->debug & H264R_DBG_NO_DEBLOCK)) {
         Timed t(c, 2, s);
+        if (!c->nxcc) {                  // XCDs of the device: the deblocking kernels' placement
+            int nx = 1;
+            if (hipDeviceGetAttribute(&nx, hipDeviceAttributeNumberOfXccs, c->device) != hipSuccess) nx = 1;
+            c->nxcc = std::max(1, std::min(nx, 8));
+        }
         if (by_rows)
         {
             // k_deblock2 keeps a 16-picture group on one XCD (g % nx): nx counters
-            if (!c->nxcc) {
-                int nx = 1;
-                if (hipDeviceGetAttribute(&nx, hipDeviceAttributeNumberOfXccs, c->device) != hipSuccess) nx = 1;
-                c->nxcc = std::max(1, std::min(nx, 8));
-            }
             int grid = ((P + DEBLOCK2_UNITS - 1) / DEBLOCK2_UNITS) * HB;
-            const int nx = grid >= 64 * c->nxcc ? c->nxcc : 1;
+            const int nx = grid >= 64 * c->nxcc && !(c->debug & H264R_DBG_DEBLOCK_GLOBAL) ? c->nxcc : 1;
             grid = (grid + nx - 1) / nx * nx;
             hipLaunchKernelGGL(k_deblock2, dim3(grid), dim3(64), 0, s, b, dbinfo,
                                reinterpret_cast<uint64_t*>(c->d_hb2), sync + 1 + (size_t)P * H + 5, c->d_err, ++c->epoch2, rows,
                                nx);
         }
-        else
-            hipLaunchKernelGGL(k_deblock, dim3(P * npairs), dim3(64), 0, s, b, dbinfo,
-                               reinterpret_cast<uint64_t*>(c->d_hb), sync + 1 + (size_t)P * H, c->d_err, ++c->epoch, rows);
+        else {
+            // k_deblock keeps a picture's pairs on one XCD (p % nx): nx times the largest
+            // XCD share of waves, so every XCD runs all its pairs at once
+            const int nx = c->nxcc > 1 && !(c->debug & H264R_DBG_DEBLOCK_GLOBAL) ? c->nxcc : 1;
+            const int grid = nx * ((P + nx - 1) / nx) * npairs;
+            hipLaunchKernelGGL(k_deblock, dim3(grid), dim3(64), 0, s, b, dbinfo,
+                               reinterpret_cast<uint64_t*>(c->d_hb), sync + 1 + (size_t)P * H + 5, c->d_err, ++c->epoch, rows,
+                               nx);
+        }
         HIP_OK(hipGetLastError());
     }
     return H264R_OK;

@@ -58,6 +58,13 @@ DEV void st_cc64(uint64_t* p, uint64_t v)   // write-through (sc1) 8-byte store
 {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// a hand-off record granule: plain (kept in the XCD's L2) when producer and consumer share
+// the XCD (local), else write-through
+DEV void st_rec(uint64_t* p, uint64_t v, bool local)
+{
+    if (local) *(__attribute__((address_space(1))) uint64_t*)p = v;
+    else st_cc64(p, v);
+}
 
 }  // namespace
 
@@ -76,20 +83,36 @@ extern "C" void h264r_db_trace_copy(void* dst) { (void)hipMemcpyFromSymbol(dst, 
 #ifndef H264R_DB_WAVES
 #define H264R_DB_WAVES 1                    // minimum waves per SIMD asked of the register allocator
 #endif
+// nx > 1: XCD-local hand-off, as in k_deblock2 -- every pair of a picture on one XCD
+// (picture p on XCD p % nx, per-XCD ticket counters sync[0 .. nx-1], the XCD read from
+// HW_REG_XCC_ID; waves take tickets until their XCD's run out) and the records as plain
+// stores kept in that XCD's L2.  The host launches nx times the pairs of the largest XCD
+// share, so each XCD's pairs all run at once whatever the round-robin start.
 extern "C" __global__ __launch_bounds__(64, H264R_DB_WAVES) void k_deblock(h264r_batch b, const DbInfo* __restrict__ dbinfo,
-                                                          uint64_t* hb, int* sync, int* err, uint32_t epoch, int2 rows)
+                                                          uint64_t* hb, int* sync, int* err, uint32_t epoch, int2 rows,
+                                                          int nx)
 {
     __shared__ PairLds L;
-    const int lane = threadIdx.x, h = lane >> 5, hl = lane & 31;
     const Geom g = make_geom(b.width_mbs, b.height_mbs);
     // rows [R0, H): the MB rows decoded by this launch (a slice-aligned band, h264r_decode_batch_rows)
     const int W = g.wmb, R0 = rows.x, H = rows.y, npairs = (H - R0 + 1) >> 1;
-
+    unsigned xcc_reg = 0;
+    if (nx > 1) asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc_reg));
+    const int xcc = (int)(xcc_reg & 15u) % nx;
+    const int npx = (b.num_pics - xcc + nx - 1) / nx;          // pictures xcc, xcc + nx, ...
+    const bool local = nx > 1;
+    const int items = npx * npairs;
+    for (;;) {
+    __syncthreads();                                          // the previous item's LDS use is over
+    int lane = threadIdx.x;
+    asm volatile("" : "+v"(lane));                            // per item: no hoisted lane-derived state
+    const int h = lane >> 5, hl = lane & 31;
     int tk = 0;
-    if (lane == 0) tk = atomicAdd(&sync[0], 1);
+    if (lane == 0) tk = atomicAdd(&sync[xcc], 1);
     const int ticket = __builtin_amdgcn_readfirstlane(tk);
+    if (ticket >= items) return;
     TRACE(unsigned long long tr_start = __builtin_amdgcn_s_memrealtime();)
-    const int rp = ticket / b.num_pics, pic = ticket % b.num_pics;
+    const int rp = ticket / npx, pic = (ticket - rp * npx) * nx + xcc;
     const int r = R0 + 2 * rp + h;                         // this half's MB row
     const bool hasB = R0 + 2 * rp + 1 < H;
     const bool half_on = r < H;
@@ -264,7 +287,7 @@ extern "C" __global__ __launch_bounds__(64, H264R_DB_WAVES) void k_deblock(h264r
         // (A's MB x: columns 0..11 after H(x), 12..15 after V(x+1), this step)
         if (r > R0) Sw[a_top] = h == 0 ? (uint32_t)top : ring_a[(x & (DRING - 1)) * 32 + hl];
         // half B: the record of MB x-1 is complete
-        if (act && feeds_hb && xl) st_cc64(hb_out + (size_t)(x - 1) * 32 + hl, tag | ring_b[((x + DRING - 1) & (DRING - 1)) * 32 + hl]);
+        if (act && feeds_hb && xl) st_rec(hb_out + (size_t)(x - 1) * 32 + hl, tag | ring_b[((x + DRING - 1) & (DRING - 1)) * 32 + hl], local);
         wave_sync();
 
         // ---- horizontal edges of both halves (deblock.cc:506-535)
@@ -283,7 +306,7 @@ extern "C" __global__ __launch_bounds__(64, H264R_DB_WAVES) void k_deblock(h264r
         if (act && (feeds_ring || feeds_hb)) feed_ring(x, false);
         wave_sync();
         // ---- half B at the row end: the last record
-        if (act && feeds_hb && xr) st_cc64(hb_out + (size_t)x * 32 + hl, tag | ring_b[(x & (DRING - 1)) * 32 + hl]);
+        if (act && feeds_hb && xr) st_rec(hb_out + (size_t)x * 32 + hl, tag | ring_b[(x & (DRING - 1)) * 32 + hl], local);
         // ---- carry the right 4 columns into the left strip of the next tile
 #pragma unroll
         for (int it = 0; it < 2; ++it)
@@ -292,9 +315,10 @@ extern "C" __global__ __launch_bounds__(64, H264R_DB_WAVES) void k_deblock(h264r
         TRACE({ unsigned long long t2 = __builtin_amdgcn_s_memtime(); tph[3] += t2 - tm; })
     }
     if (!ok && feeds_hb)                                   // release the pair below (the error is flagged)
-        for (int x = 0; x < W; ++x) st_cc64(hb_out + (size_t)x * 32 + hl, tag);
+        for (int x = 0; x < W; ++x) st_rec(hb_out + (size_t)x * 32 + hl, tag, local);
     TRACE(if (lane == 0 && ticket < (1 << 16)) {
         h264r_db_trace[ticket][0] = tr_start; h264r_db_trace[ticket][1] = tr_first;
         h264r_db_trace[ticket][2] = __builtin_amdgcn_s_memrealtime(); h264r_db_trace[ticket][3] = tr_wait;
         for (int i = 0; i < 4; ++i) h264r_db_trace[ticket][4 + i] = tph[i]; })
+    }
 }

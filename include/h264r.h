@@ -269,6 +269,10 @@ int  h264r_set_timing(h264r_ctx* ctx, int enable);
  * force one of them. */
 #define H264R_DBG_DEBLOCK_MB   4
 #define H264R_DBG_DEBLOCK_ROWS 8
+/* Both schedules keep a picture's (k_deblock) or a 16-picture group's (k_deblock2) rows on
+ * one XCD and hand records over in that XCD's L2; H264R_DBG_DEBLOCK_GLOBAL uses one
+ * ticket counter and write-through records instead (any wave on any XCD). */
+#define H264R_DBG_DEBLOCK_GLOBAL 16
 int  h264r_set_debug(h264r_ctx* ctx, int flags);
 /* Wait for the context's work and report a device-side failure (a wavefront wait
  * that timed out): H264R_OK or H264R_EDEVICE. */

@@ -80,7 +80,7 @@ def test_gpu_matches_reference_fixture(L, dec, fx):
 
 
 # both deblocking schedules (include/h264r.h): one MB per 32 lanes / a lane pair per MB row
-DEBLOCKS = (A.DBG_DEBLOCK_MB, A.DBG_DEBLOCK_ROWS)
+DEBLOCKS = (A.DBG_DEBLOCK_MB, A.DBG_DEBLOCK_ROWS, A.DBG_DEBLOCK_MB | A.DBG_DEBLOCK_GLOBAL)
 
 
 def _batch_vs_oracle(L, dec, cidx, W, H, n, debug=0, deblocks=DEBLOCKS, qm=None, **over):
