@@ -67,7 +67,49 @@ DEV void wave_sync()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// XCD-local schedules (k_deblock, k_deblock2): a wave takes tickets only from its own
+// XCD's counter tickets[k], so an XCD that no wave of the launch reached (a CU-masked
+// stream, XCC ids that are not contiguous modulo nx) would leave its pictures unfiltered.
+// Every wave passes here once, when its XCD's tickets have run out; the last one checks
+// that every XCD's tickets were all taken (a counter that was reached ends past its item
+// count) and flags err[0] = 3 otherwise -- a failure is never silent.  One-wave workgroups.
+template <typename ItemsOf>
+DEV void xcd_drain_check(const int* tickets, int* done, int nx, ItemsOf items_of, int* err)
+{
+    if (nx <= 1 || threadIdx.x != 0) return;
+    const int prev = __hip_atomic_fetch_add(done, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev != (int)gridDim.x - 1) return;
+    for (int k = 0; k < nx; ++k)
+        if (__hip_atomic_load(&tickets[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < items_of(k))
+            __hip_atomic_store(err, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 DEV int mb_is_intra(const h264r_mb& m) { return (m.flags & H264R_MBF_INTRA) != 0; }
+
+// ---------------------------------------------------------------- bounded waits
+// Every cross-wave wait of the kernels (row hand-offs, the level barrier) is bounded in
+// WALL time, not in polls: err[0] is the context's error word (h264r_check), err[1] the
+// bound in s_memrealtime ticks (100 MHz), written by the host.  A wait gives up when its
+// own bound has passed (it then flags err[0] = 1) or as soon as another wave has flagged
+// an error, so one expired wait drains the whole grid within a few polls instead of
+// every waiter behind it serving its own full bound (the round-2 hang: chained
+// poll-count bounds of ~17 s each).  Checked every 64 polls (one scalar clock read).
+struct WaitClock {
+    uint64_t t0 = 0;
+    uint32_t n = 0;
+};
+// true: stop waiting (the error is flagged)
+DEV bool wait_give_up(int* err, WaitClock& c)
+{
+    if ((++c.n & 63u) != 1u) return false;
+    const uint64_t now = __builtin_amdgcn_s_memrealtime();
+    if (c.n == 1u) { c.t0 = now; return false; }
+    if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return true;
+    const uint32_t lim = (uint32_t)__hip_atomic_load(err + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (now - c.t0 <= (uint64_t)lim) return false;
+    __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return true;
+}
 
 // ----------------------------------------------------------- level block layout
 // Section offsets of the compacted level block (include/h264r.h), int16 units.

@@ -102,7 +102,8 @@ struct h264r_ctx {
     uint8_t* slot[H264R_MAX_SLOTS][3] = {};
     int slot_w[H264R_MAX_SLOTS] = {}, slot_h[H264R_MAX_SLOTS] = {};
     const uint8_t** d_ref_planes = nullptr;
-    int* d_err = nullptr;                 // device error word (bounded spin expired)
+    int* d_err = nullptr;                 // [0] device error word (a bounded wait expired), [1] wait bound
+    uint32_t wait_ticks = 0;              // err[1] as last written (s_memrealtime ticks, 100 MHz)
     // streaming-API staging
     bool in_pic = false;
     int pw = 0, ph = 0;
@@ -211,6 +212,26 @@ int h264r_quant_init_lists(h264r_quant* q, const int32_t* const qm[12])
     return H264R_OK;
 }
 
+// The wall-time bound of every device-side wait (device_common.h wait_give_up): 2 s, or
+// H264R_WAIT_MS.  A launch of the slowest kernel over the largest batch takes ~10 ms, and
+// a wait only ever waits on work that is already running, so 2 s means a lost wave.
+static uint32_t wait_bound_ticks()
+{
+    static const uint32_t t = [] {
+        const char* e = getenv("H264R_WAIT_MS");
+        const double ms = e ? atof(e) : 2000.0;
+        return (uint32_t)std::min(4.0e9, std::max(1.0, ms * 1.0e5));
+    }();
+    return t;
+}
+static int set_wait_bound(h264r_ctx* c, uint32_t ticks)
+{
+    if (c->wait_ticks == ticks) return H264R_OK;
+    HIP_OK(hipMemcpy(c->d_err + 1, &ticks, sizeof(uint32_t), hipMemcpyHostToDevice));
+    c->wait_ticks = ticks;
+    return H264R_OK;
+}
+
 int h264r_create(h264r_ctx** out, int device, int max_w, int max_h, int chroma_format_idc, int bit_depth)
 {
     if (!out || max_w <= 0 || max_h <= 0 || max_w > 1024 || max_h > 1024) return H264R_EINVAL;
@@ -228,13 +249,14 @@ int h264r_create(h264r_ctx** out, int device, int max_w, int max_h, int chroma_f
     // default stream) and this stream are ordered with each other
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamDefault) != hipSuccess ||
         hipMalloc(reinterpret_cast<void**>(&c->d_ref_planes), sizeof(uint8_t*) * 3 * H264R_MAX_SLOTS) != hipSuccess ||
-        hipMalloc(reinterpret_cast<void**>(&c->d_err), sizeof(int)) != hipSuccess) {
+        hipMalloc(reinterpret_cast<void**>(&c->d_err), 2 * sizeof(int)) != hipSuccess) {
         delete c;
         return H264R_EDEVICE;
     }
     if (hipEventCreateWithFlags(&c->ev_last, hipEventDisableTiming) != hipSuccess) { delete c; return H264R_EDEVICE; }
     (void)hipMemset(c->d_ref_planes, 0, sizeof(uint8_t*) * 3 * H264R_MAX_SLOTS);
-    (void)hipMemset(c->d_err, 0, sizeof(int));
+    (void)hipMemset(c->d_err, 0, 2 * sizeof(int));
+    if (set_wait_bound(c, wait_bound_ticks()) != H264R_OK) { (void)h264r_destroy(c); return H264R_EDEVICE; }
     *out = c;
     return H264R_OK;
 }
@@ -338,8 +360,13 @@ static int level_launches()
 // k_intra_levels + k_intra_pic (intra MBs), k_deblock or k_deblock2 (by batch size).
 static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row0, int row1)
 {
-    // H264R_DEBUG=<flags>: h264r_set_debug flags OR-ed into every launch (measurement A/B)
-    static const int env_debug = [] { const char* e = getenv("H264R_DEBUG"); return e ? atoi(e) : 0; }();
+    // H264R_DEBUG=<flags>: the deblocking-schedule flags of h264r_set_debug OR-ed into every
+    // launch (measurement A/B); flags that change or skip work (H264R_DBG_NO_DEBLOCK, the
+    // wait test) are API-only, so a stray variable cannot alter the output
+    static const int env_debug = [] {
+        const char* e = getenv("H264R_DEBUG");
+        return e ? atoi(e) & (H264R_DBG_INTRA_WALK | H264R_DBG_DEBLOCK_MB | H264R_DBG_DEBLOCK_ROWS | H264R_DBG_DEBLOCK_GLOBAL) : 0;
+    }();
     const int debug_saved = c->debug;
     c->debug |= env_debug;
     struct Restore { h264r_ctx* c; int d; ~Restore() { c->debug = d; } } restore{c, debug_saved};
@@ -349,7 +376,7 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
     // scratch: per-MB deblocking records, tagged hand-off
     // records, and a sync region [intra ticket + per-(picture,row) progress][deblock
     // ticket][level barrier, deepest level][SP inter MBs seen]
-    const size_t sync_n = 1 + (size_t)P * H + 5 + 8;   // + k_deblock2's per-XCD ticket counters
+    const size_t sync_n = 1 + (size_t)P * H + 5 + 9;   // + the deblocking kernels' per-XCD ticket counters, done count
     // the scratch is shared by every launch of this context: a launch on another stream
     // than the previous one waits for it first
     if (c->last_stream && c->last_stream != s) {
@@ -377,8 +404,12 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
         }
     }
     if ((st = dev_resize(&c->d_sync, &c->c_sync, sync_n))) return st;
+    // H264R_DBG_WAIT_TEST: every intra-walk wait asks for progress no row reaches, under a
+    // 10 ms bound -- the launch must drain and h264r_check report H264R_EDEVICE
+    const bool wait_test = (c->debug & H264R_DBG_WAIT_TEST) != 0;
+    if ((st = set_wait_bound(c, wait_test ? 1000000u : wait_bound_ticks()))) return st;
     const bool levels = (size_t)W * H <= LEVEL_MAX_MBS && H <= 1024 && level_launches() > 0 &&
-                        !(c->debug & H264R_DBG_INTRA_WALK);
+                        !(c->debug & (H264R_DBG_INTRA_WALK | H264R_DBG_WAIT_TEST));
     if (levels && !c->levels_grid) {
         // every workgroup of the persistent level kernel must be resident at once: one
         // block per CU below what the occupancy query reports (MI355X_MICROARCH.md,
@@ -427,16 +458,17 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
             hipLaunchKernelGGL(k_level_scatter, dim3(P), dim3(1024), 0, s, b, (const uint16_t*)lvl, (const int*)lbase,
                                lcursor, c->d_list, rows);
             HIP_OK(hipGetLastError());
-            // the grid is one block per CU below the occupancy answer (residency margin);
-            // H264R_COOP=1 launches it cooperatively instead, so that the runtime checks the
-            // grid against the occupancy query (off by default: rocprofv3 7.2 crashes at
-            // process exit after a cooperative launch)
+            // a cooperative launch (the runtime checks that the whole grid is resident at
+            // once, or refuses it: the grid barrier's contract, include/h264r.h), the grid
+            // one block per CU below the occupancy answer; H264R_COOP=0 takes a plain launch
+            // (rocprofv3 7.2 crashes at process exit after a cooperative launch: profiling
+            // runs set it; throughput is the same, profiles/r02_intra_levels_launch.txt)
             // small batches (the latency chain: one picture) take a grid sized to their MBs,
             // 64 per workgroup: most workgroups of the full grid would only attend the grid
             // barriers, whose cost grows with the number of arrivals (MI355X_MICROARCH.md
             // price list 'barrier-xcd')
             const int lgrid = std::min(c->levels_grid, std::max(8, (int)(((size_t)P * W * HB + 63) / 64)));
-            static const bool coop = [] { const char* e = getenv("H264R_COOP"); return e && atoi(e) != 0; }();
+            static const bool coop = [] { const char* e = getenv("H264R_COOP"); return !e || atoi(e) != 0; }();
             if (coop) {
                 const int* lcount_c = lcount;
                 const int* lbase_c = lbase;
@@ -456,7 +488,7 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
         // the walk's band-to-band hand-off: global progress every gstep MBs (k_picture.hip);
         // H264R_WALK_GSTEP overrides
         static const int gstep_env = [] { const char* e = getenv("H264R_WALK_GSTEP"); return e ? atoi(e) : 0; }();
-        const int gstep = gstep_env > 0 ? gstep_env : (P >= 128 ? 64 : 1);
+        const int gstep = wait_test ? -1 : gstep_env > 0 ? gstep_env : (P >= 128 ? 64 : 1);
         hipLaunchKernelGGL(k_intra_pic, dim3(P * nbands), dim3(64 * H264R_WALK_ROWS), 0, s, b, sync, c->d_err,
                            (const uint16_t*)lvl, lmax, rows, gstep);
         HIP_OK(hipGetLastError());

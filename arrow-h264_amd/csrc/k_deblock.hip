@@ -39,7 +39,6 @@ using namespace h264r;
 namespace {
 
 constexpr int DRING = 4;                    // row A -> row B ring depth (lag is 1)
-constexpr unsigned SPIN_LIMIT = 1u << 22;   // ~0.3 s of polling, then flag an error
 
 struct alignas(16) PairLds {
     DbLds t[2];                   // per half
@@ -110,7 +109,10 @@ extern "C" __global__ __launch_bounds__(64, H264R_DB_WAVES) void k_deblock(h264r
     int tk = 0;
     if (lane == 0) tk = atomicAdd(&sync[xcc], 1);
     const int ticket = __builtin_amdgcn_readfirstlane(tk);
-    if (ticket >= items) return;
+    if (ticket >= items) {
+        xcd_drain_check(sync, sync + 8, nx, [&](int k) { return (b.num_pics - k + nx - 1) / nx * npairs; }, err);
+        return;
+    }
     TRACE(unsigned long long tr_start = __builtin_amdgcn_s_memrealtime();)
     const int rp = ticket / npx, pic = (ticket - rp * npx) * nx + xcc;
     const int r = R0 + 2 * rp + h;                         // this half's MB row
@@ -266,14 +268,13 @@ extern "C" __global__ __launch_bounds__(64, H264R_DB_WAVES) void k_deblock(h264r
         // ---- the record of the MB above (half A below another pair): wait for this epoch
         if (rp > 0) {
             const bool need = act && h == 0;
-            unsigned spins = 0;
+            WaitClock wc;
             TRACE(unsigned long long tw0 = 0;)
             while (!__all(!need || (top & 0xFFFFFFFF00000000ull) == tag)) {
                 TRACE(if (!tw0) tw0 = __builtin_amdgcn_s_memrealtime();)
                 __builtin_amdgcn_s_sleep(1);
                 if (need) top = ld_cc64(hb_in + (size_t)x * 32 + hl);
-                if (++spins > SPIN_LIMIT) {
-                    if (lane == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (wait_give_up(err, wc)) {                     // bounded (device_common.h)
                     ok = false;
                     break;
                 }

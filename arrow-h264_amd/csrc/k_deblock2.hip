@@ -52,7 +52,6 @@ using namespace h264r;
 
 namespace {
 
-constexpr unsigned SPIN2 = 1u << 22;   // bounded polling, then flag an error
 constexpr int UNITS = DEBLOCK2_UNITS;  // (picture, MB row) units per wave, 4 lanes each
 constexpr int RECG = 24;               // granules per MB record: [consumer lane c 0..3][i 0..5]
 constexpr int AUX_SC1 = 16;            // buffer-op cache policy: sc1 (write-through store, L2-served load)
@@ -129,7 +128,10 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2
     int tk = 0;
     if (threadIdx.x == 0) tk = atomicAdd(counter, 1);
     const int ticket = __builtin_amdgcn_readfirstlane(tk);
-    if (ticket >= items) return;
+    if (ticket >= items) {
+        xcd_drain_check(sync, sync + 8, nx, [&](int k) { return (ngroups - k + nx - 1) / nx * (R1 - R0); }, err);
+        return;
+    }
     const int ry = ticket / ngx, grp = (ticket - ry * ngx) * nx + xcc;
     // lane, opaque per item: what derives from it is recomputed per item, not hoisted out of
     // the ticket loop and kept live across it (that spilled 31 VGPRs)
@@ -388,13 +390,12 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2
             // the first check stands outside the re-poll loop, so that its wait covers the
             // record loads only (the loads issued after them stay in flight)
             if (!ready()) {
-                unsigned spins = 0;
+                WaitClock wc;
                 do {
                     __builtin_amdgcn_s_sleep(1);
 #pragma unroll
                     for (int k = 0; k < 3; ++k) { const v4u v = load_pair(x, k); rin[2 * k] = v.x | (uint64_t)v.y << 32; rin[2 * k + 1] = v.z | (uint64_t)v.w << 32; }
-                    if (++spins > SPIN2) {
-                        if (lane == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (wait_give_up(err, wc)) {                 // bounded (device_common.h)
                         ok = false;
                         consume_window();
                         return;

@@ -33,7 +33,6 @@ namespace {
 #define H264R_WALK_WAVES 4                  // minimum waves per SIMD asked of the register allocator (<= 128 VGPRs)
 #endif
 constexpr int WAVES = H264R_WALK_ROWS;      // rows per band, one wave each
-constexpr unsigned SPIN_LIMIT = 1u << 24;   // bounded wait, then flag an error
 
 DEV void publish_lds(int* counter, int value, int lane)
 {
@@ -53,17 +52,14 @@ DEV void publish_global(int* counter, int value, int lane)
 template <bool GLOBAL>
 DEV bool wait_for(int* counter, int need, int* err, int& seen)
 {
-    unsigned spins = 0;
+    WaitClock wc;
     for (;;) {
         int v = GLOBAL ? __hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                        : __hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         seen = v;
         if (v >= need) break;
         __builtin_amdgcn_s_sleep(1);
-        if (++spins > SPIN_LIMIT) {
-            __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            return false;
-        }
+        if (wait_give_up(err, wc)) return false;     // bounded (device_common.h)
     }
     if (GLOBAL) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     else __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
@@ -138,7 +134,8 @@ DEV void walk_ticket(const h264r_batch& b, int* sync, int* err, Scratch* scratch
     publish(x, true);
     int seen = 0;                                            // progress of the row above, acquired
     while (x < g.wmb && ok) {
-        const int need = min(x + 2, g.wmb);
+        // gstep < 0: the host's wait test (H264R_DBG_WAIT_TEST) -- a need no row ever meets
+        const int need = gstep < 0 ? g.wmb + 1 : min(x + 2, g.wmb);
         if (r > R0 && need > seen) {
             if (wave == 0) ok = wait_for<true>(&gprog[r - 1], need, err, seen);
             else ok = wait_for<false>(&lprog[wave - 1], need, err, seen);
@@ -324,15 +321,11 @@ DEV bool grid_barrier(int* bar, int target, int* err)
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __hip_atomic_fetch_add(bar, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        unsigned spins = 0;
+        WaitClock wc;
         ok = 1;
         while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
             __builtin_amdgcn_s_sleep(2);
-            if (++spins > SPIN_LIMIT) {
-                __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                ok = 0;
-                break;
-            }
+            if (wait_give_up(err, wc)) { ok = 0; break; }
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -273,6 +273,11 @@ int  h264r_set_timing(h264r_ctx* ctx, int enable);
  * one XCD and hand records over in that XCD's L2; H264R_DBG_DEBLOCK_GLOBAL uses one
  * ticket counter and write-through records instead (any wave on any XCD). */
 #define H264R_DBG_DEBLOCK_GLOBAL 16
+/* Test hook for the bounded waits: every intra MB goes through the wavefront walk, whose
+ * row-to-row waits then ask for progress that never comes, under a 10 ms bound.  The
+ * launch drains and h264r_check returns H264R_EDEVICE (the output is invalid).  The
+ * bound of every wait is wall time: 2 s by default (environment H264R_WAIT_MS). */
+#define H264R_DBG_WAIT_TEST 32
 int  h264r_set_debug(h264r_ctx* ctx, int flags);
 /* Wait for the context's work and report a device-side failure (a wavefront wait
  * that timed out): H264R_OK or H264R_EDEVICE. */

@@ -185,8 +185,12 @@ h264r_slice slice_record(Shim& S, slice_t& slice)
         for (int i = 0; i < H264R_MAX_REFS; ++i) {
             r.ref_slot[l][i] = -1;
             if (i < n && slice.RefPicList[l][i]) {
+                // every picture of a reference list must be resident: a missing one would be
+                // predicted as the reference's no_ref grey (inter_prediction.cc:164-167) --
+                // fail loudly instead
                 auto it = S.slot_of.find(slice.RefPicList[l][i]);
-                if (it != S.slot_of.end()) r.ref_slot[l][i] = (int8_t)it->second;
+                if (it == S.slot_of.end()) check(H264R_ESTATE, "reference picture not resident in a device DPB slot");
+                r.ref_slot[l][i] = (int8_t)it->second;
             }
             for (int pl = 0; pl < 3; ++pl) {
                 const auto& v = shr.pred_weight_l[l][pl];
@@ -490,8 +494,25 @@ void Decoder::deblock_filter(slice_t& slice)
     }
     int keep = -1;
     if (pic->used_for_reference) {
-        keep = S.next_slot;                 // round robin over 32 slots: a DPB holds <= 16 references
-        S.next_slot = (S.next_slot + 1) % H264R_MAX_SLOTS;
+        // a device slot no reference of the DPB holds: the frames of fs_ref / fs_ltref
+        // (dpb.h:30-36) as they stand before this picture is stored (exit_picture ->
+        // store_picture, picture.cc:253-269; its own marking can only free more), searched
+        // round robin from the last slot given out.  The DPB holds <= 16 reference frames,
+        // so one of the 32 slots is always free -- a long-term reference keeps its slot for
+        // as long as it stays in the DPB.
+        bool busy[H264R_MAX_SLOTS] = {};
+        const dpb_t* dpb = slice.p_Dpb;
+        auto mark = [&](pic_t* fs) {
+            if (!fs || !fs->frame) return;
+            auto it = S.slot_of.find(fs->frame);
+            if (it != S.slot_of.end()) busy[it->second] = true;
+        };
+        for (unsigned i = 0; dpb && i < dpb->ref_frames_in_buffer; ++i) mark(dpb->fs_ref[i]);
+        for (unsigned i = 0; dpb && i < dpb->ltref_frames_in_buffer; ++i) mark(dpb->fs_ltref[i]);
+        for (int k = 0; k < H264R_MAX_SLOTS && keep < 0; ++k)
+            if (!busy[(S.next_slot + k) % H264R_MAX_SLOTS]) keep = (S.next_slot + k) % H264R_MAX_SLOTS;
+        if (keep < 0) check(H264R_EUNSUPPORTED, "more than 32 reference frames resident");
+        S.next_slot = (keep + 1) % H264R_MAX_SLOTS;
         for (auto it = S.slot_of.begin(); it != S.slot_of.end();)
             it = it->second == keep ? S.slot_of.erase(it) : std::next(it);
     }

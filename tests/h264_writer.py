@@ -135,6 +135,16 @@ class StreamCfg:
                                      # MBs sent to QP 0 (TransformBypassModeFlag, interpret_mb.cc:804).
                                      # Coded inter MBs keep QP >= 1: the reference's inter bypass
                                      # reads stale Intra4x4PredMode (transform.cc:993)
+    bframes: int = 0                 # B pictures between anchors (IBBP...; pic_order_cnt_type 0, B pictures
+                                     # decoded after the anchor that follows them in output order)
+    bipred: int = 0                  # weighted_bipred_idc: 0 default, 1 explicit, 2 implicit (POC distances)
+    direct: tuple = (0, 1)           # direct_spatial_mv_pred_flag choices per B slice (0 temporal, 1 spatial)
+    b_ref: float = 0.0               # share of B pictures kept as references (nal_ref_idc != 0)
+    l1_refs: int = 2                 # max num_ref_idx_l1_active of B slices
+    long_term: int = 0               # the IDR is a long-term reference (LongTermFrameIdx 0) kept for the
+                                     # whole stream, and P picture `long_term` becomes a second one by
+                                     # MMCO 4 + 6 (LongTermFrameIdx 1); P pictures predict from them
+                                     # (list 0: short-term by PicNum, then long-term, 8.2.4.2.1)
 
 
 @dataclass
@@ -159,6 +169,7 @@ class Encoder:
         self.rng = random.Random(cfg.seed)
         self.W, self.H = cfg.width_mbs, cfg.height_mbs
         self.log2_max_frame_num = 4
+        self.log2_max_poc_lsb = 8
 
     # ------------------------------------------------------------------ parameter sets
     def sps(self) -> bytes:
@@ -175,7 +186,11 @@ class Encoder:
             if c.scaling & 1:
                 self._scaling_matrix(w, 8)
         w.ue(self.log2_max_frame_num - 4)
-        w.ue(2)                                     # pic_order_cnt_type 2 (output = decode order)
+        if c.bframes:
+            w.ue(0)                                 # pic_order_cnt_type 0: B pictures reorder
+            w.ue(self.log2_max_poc_lsb - 4)
+        else:
+            w.ue(2)                                 # pic_order_cnt_type 2 (output = decode order)
         w.ue(c.num_refs)                            # max_num_ref_frames
         w.u(1, 0)                                   # gaps_in_frame_num_value_allowed_flag
         w.ue(self.W - 1)
@@ -199,7 +214,7 @@ class Encoder:
         w.ue(0)                                     # num_slice_groups_minus1
         w.ue(0); w.ue(0)                            # num_ref_idx_l0/l1_default_active_minus1
         w.u(1, c.weighted)                          # weighted_pred_flag
-        w.u(2, 0)                                   # weighted_bipred_idc
+        w.u(2, c.bipred)                            # weighted_bipred_idc
         w.se(0); w.se(0)                            # pic_init_qp/qs_minus26
         w.se(c.chroma_qp_offset)
         w.u(1, 1)                                   # deblocking_filter_control_present_flag
@@ -429,12 +444,12 @@ class Encoder:
         m = self.mbs[a]
         m.slice = s
         roll = r.random()
-        if ptype == "P" and roll < c.skip:
+        if ptype in ("P", "B") and roll < c.skip:
             m.kind, m.intra = SKIP, False
             m.nz = [[[0] * 4 for _ in range(4)] for _ in range(3)]
             return False
         intra = ptype == "I" or r.random() < c.intra_in_p
-        base = 5 if ptype == "P" else 0
+        base = 5 if ptype == "P" else (23 if ptype == "B" else 0)
         if intra:
             m.intra = True
             k = r.random()
@@ -496,6 +511,12 @@ class Encoder:
             w.ue(r.choice(cmodes))
             cbp = r.randint(0, 47)
             w.ue(CBP_CODE["intra"][cbp])
+        elif ptype == "B":
+            cbp, small = self._b_inter(w, nref)
+            m.t8 = False
+            if (cbp & 15) and c.transform8x8 and not small:
+                m.t8 = r.random() < 0.5
+                w.u(1, 1 if m.t8 else 0)
         else:
             mbt = r.choices([0, 1, 2, 3, 4], weights=[45, 12, 12, 21, 10])[0]
             w.ue(mbt)
@@ -541,29 +562,135 @@ class Encoder:
         self._residual(w, a, m, cbp, s)
         return True
 
+    # B partitions: mb_type 1..21 -> prediction of partition 0 / 1 (Table 7-14); sub_mb_type
+    # -> (prediction, sub-partitions) (Table 7-18); None = direct
+    B_PARTS = {1: ("L0",), 2: ("L1",), 3: ("Bi",)}
+    B_PARTS.update({4 + k: pr for k, pr in enumerate(
+        [("L0", "L0")] * 2 + [("L1", "L1")] * 2 + [("L0", "L1")] * 2 + [("L1", "L0")] * 2 + [("L0", "Bi")] * 2 +
+        [("L1", "Bi")] * 2 + [("Bi", "L0")] * 2 + [("Bi", "L1")] * 2 + [("Bi", "Bi")] * 2)})
+    B_SUBS = {0: (None, 0), 1: ("L0", 1), 2: ("L1", 1), 3: ("Bi", 1), 4: ("L0", 2), 5: ("L0", 2), 6: ("L1", 2),
+              7: ("L1", 2), 8: ("Bi", 2), 9: ("Bi", 2), 10: ("L0", 4), 11: ("L1", 4), 12: ("Bi", 4)}
+
+    def _b_inter(self, w: BitWriter, nref: tuple):
+        """An inter MB of a B slice (CAVLC, 7.3.5.1-7.3.5.2; interpret_mb.cc:392-404, 480-503,
+        636-700): mb_type B_Direct_16x16 / 16x16 / 16x8 / 8x16 / B_8x8 with direct and every
+        sub-partition, then ref_idx of list 0, of list 1, mvd of list 0, of list 1.  Returns
+        (cbp, has sub-partitions smaller than 8x8)."""
+        c, r = self.c, self.rng
+        n0, n1 = nref
+
+        def ref_idx(n):
+            v = r.randrange(n)
+            if n == 2:
+                w.u(1, 1 - v)
+            elif n > 2:
+                w.ue(v)
+
+        def mvd():
+            w.se(r.randint(-c.mv_range, c.mv_range)); w.se(r.randint(-c.mv_range, c.mv_range))
+        k = r.random()
+        mbt = 0 if k < 0.15 else (r.randint(1, 3) if k < 0.55 else (r.randint(4, 21) if k < 0.8 else 22))
+        w.ue(mbt)
+        small = False
+        if 1 <= mbt <= 21:
+            preds = self.B_PARTS[mbt]
+            for lst, n in (("L0", n0), ("L1", n1)):
+                for pr in preds:
+                    if pr in (lst, "Bi"):
+                        ref_idx(n)
+            for lst in ("L0", "L1"):
+                for pr in preds:
+                    if pr in (lst, "Bi"):
+                        mvd()
+        elif mbt == 22:
+            subs = [0 if r.random() < 0.3 else r.randint(1, 12) for _ in range(4)]
+            small = any(self.B_SUBS[sb][1] > 1 for sb in subs)
+            for sb in subs:
+                w.ue(sb)
+            for lst, n in (("L0", n0), ("L1", n1)):
+                for sb in subs:
+                    if sb and self.B_SUBS[sb][0] in (lst, "Bi"):
+                        ref_idx(n)
+            for lst in ("L0", "L1"):
+                for sb in subs:
+                    if sb and self.B_SUBS[sb][0] in (lst, "Bi"):
+                        for _ in range(self.B_SUBS[sb][1]):
+                            mvd()
+        cbp = r.randint(0, 47)
+        w.ue(CBP_CODE["inter"][cbp])
+        return cbp, small
+
     # ------------------------------------------------------------------ pictures
-    def picture(self, idx: int, idr: bool):
-        """NAL units of picture idx: one per slice."""
+    def _pred_weight_table(self, w: BitWriter, nrefs: tuple, bi: bool) -> None:
+        """pred_weight_table (7.3.3.2; interpret_rbsp.cc): per list and reference a luma and
+        a chroma flag with weights / offsets.  For B slices the weights stay inside the
+        bi-prediction constraint -128 <= w0 + w1 <= 128 (8.4.2.3)."""
+        r = self.rng
+        ld, cd = r.randint(0, 7), r.randint(0, 7)
+        w.ue(ld); w.ue(cd)
+        for n in nrefs:
+            for _ in range(n):
+                if r.random() < 0.7:
+                    w.u(1, 1)
+                    w.se(r.randint(-min(64, 1 << ld), min(127, 2 << ld)) if not bi else r.randint(-32, 64))
+                    w.se(r.randint(-20, 20))
+                else:
+                    w.u(1, 0)
+                if r.random() < 0.7:
+                    w.u(1, 1)
+                    for _ in range(2):
+                        w.se(r.randint(-min(64, 1 << cd), min(127, 2 << cd)) if not bi else r.randint(-32, 64))
+                        w.se(r.randint(-20, 20))
+                else:
+                    w.u(1, 0)
+
+    def picture(self, idx: int, idr: bool, kind: str | None = None, ref_idc: int = 3, poc: int = 0):
+        """NAL units of picture idx: one per slice.  kind None = I (idr) or P; "B" writes a
+        B picture (nal_ref_idc = ref_idc, POC lsb from poc)."""
         c, r = self.c, self.rng
         n = self.W * self.H
         self.mbs = [_Mb() for _ in range(n)]
-        ptype = "I" if idr else "P"
+        ptype = kind or ("I" if idr else "P")
         sp = ptype == "P" and c.sp > 0 and r.random() < c.sp   # (no draw otherwise: fixed streams stay)
         starts = sorted({0} | set(r.sample(range(1, n), min(c.slices - 1, n - 1)))) if c.slices > 1 else [0]
         frame_num = 0 if idr else (self.frame_num + 1) % (1 << self.log2_max_frame_num)
+        tracked = bool(c.bframes or c.long_term)           # DPB bookkeeping of the IBBP / long-term streams
+        if tracked and not idr:
+            frame_num = (self.prev_ref_fn + 1) % (1 << self.log2_max_frame_num)
         self.frame_num = frame_num
-        self.refs = 0 if idr else min(self.refs + 1, c.num_refs)
+        if ref_idc:
+            self.prev_ref_fn = frame_num
+        avail = self.st + self.lt                            # reference frames in the DPB before this picture
+        mmco_lt = c.long_term and ptype == "P" and idx == c.long_term
+        if ptype == "B":
+            nref_b = (avail, min(avail, c.l1_refs))
+        elif c.bframes:
+            # a P picture leaves one reference out of its list: the pictures its motion
+            # points to stay in the DPB for the B pictures' temporal direct (the co-located
+            # reference must be in their list 0, 8.4.1.2.3)
+            self.refs_p = max(1, min(avail, c.num_refs - 1))
+        if not tracked:
+            self.refs = 0 if idr else min(self.refs + 1, c.num_refs)
         out = []
         for s, first in enumerate(starts):
             end = starts[s + 1] if s + 1 < len(starts) else n
             w = BitWriter()
             w.ue(first)
-            w.ue(7 if ptype == "I" else (8 if sp else 5))   # slice_type (all slices of the picture alike)
+            w.ue(7 if ptype == "I" else (8 if sp else (6 if ptype == "B" else 5)))   # slice_type (all slices alike)
             w.ue(0)                                 # pic_parameter_set_id
             w.u(self.log2_max_frame_num, frame_num)
             if idr:
                 w.ue(idx % 2)                       # idr_pic_id
-            nref = self.refs
+            if c.bframes:
+                w.u(self.log2_max_poc_lsb, poc % (1 << self.log2_max_poc_lsb))   # pic_order_cnt_lsb
+            nref = self.refs if not tracked else (self.refs_p if c.bframes else avail)
+            if ptype == "B":
+                w.u(1, r.choice(c.direct))          # direct_spatial_mv_pred_flag
+                w.u(1, 1)                           # num_ref_idx_active_override_flag
+                w.ue(nref_b[0] - 1); w.ue(nref_b[1] - 1)
+                w.u(1, 0); w.u(1, 0)                # ref_pic_list_modification_flag_l0 / _l1
+                if c.bipred == 1:
+                    self._pred_weight_table(w, nref_b, True)
             if ptype == "P":
                 w.u(1, 1)                           # num_ref_idx_active_override_flag
                 w.ue(nref - 1)
@@ -583,8 +710,14 @@ class Encoder:
                         else:
                             w.u(1, 0)
             if idr:
-                w.u(1, 0); w.u(1, 0)                # no_output_of_prior_pics_flag, long_term_reference_flag
-            else:
+                w.u(1, 0)                           # no_output_of_prior_pics_flag
+                w.u(1, 1 if c.long_term else 0)     # long_term_reference_flag (LongTermFrameIdx 0)
+            elif mmco_lt:
+                w.u(1, 1)                           # adaptive_ref_pic_marking_mode_flag
+                w.ue(4); w.ue(2)                    # MMCO 4: MaxLongTermFrameIdx = 1
+                w.ue(6); w.ue(1)                    # MMCO 6: this picture long-term, LongTermFrameIdx 1
+                w.ue(0)                             # end
+            elif ref_idc:
                 w.u(1, 0)                           # adaptive_ref_pic_marking_mode_flag
             lo, hi = c.qp
             sqp = r.randint(lo, hi)
@@ -599,21 +732,45 @@ class Encoder:
                 w.se(r.randint(-c.offsets, c.offsets)); w.se(r.randint(-c.offsets, c.offsets))
             skip_run = 0
             for a in range(first, end):
-                coded = self._mb(w if ptype == "I" else _Deferred(w, skip_run), a, ptype, s, nref)
-                if ptype == "P":
+                coded = self._mb(w if ptype == "I" else _Deferred(w, skip_run), a, ptype, s,
+                                 nref_b if ptype == "B" else nref)
+                if ptype != "I":
                     skip_run = 0 if coded else skip_run + 1
-            if ptype == "P" and skip_run:
+            if ptype != "I" and skip_run:
                 w.ue(skip_run)
             w.trailing()
-            out.append(nal_unit(3, 5 if idr else 1, w.bytes()))
+            out.append(nal_unit(ref_idc, 5 if idr else 1, w.bytes()))
+        if ref_idc:                                          # marking after the picture (8.2.5)
+            if idr:
+                self.st, self.lt = (0, 1) if c.long_term else (1, 0)
+            elif mmco_lt:
+                self.lt += 1
+            else:
+                self.st = min(self.st + 1, c.num_refs - self.lt)   # sliding window: short-term only
         return out
 
     def stream(self) -> bytes:
         c = self.c
         out = [self.sps(), self.pps()]
-        self.frame_num, self.refs = 0, 0
-        for i in range(c.frames):
-            out += self.picture(i, idr=(i == 0 or c.all_intra))
+        self.frame_num, self.refs, self.prev_ref_fn, self.st, self.lt = 0, 0, 0, 0, 0
+        if not c.bframes:
+            for i in range(c.frames):
+                out += self.picture(i, idr=(i == 0 or c.all_intra))
+            return b"".join(out)
+        # IBBP: anchors (I / P) every bframes + 1 pictures in output order, each sent before
+        # the B pictures that precede it; trailing pictures past the last anchor are P.
+        # POC = 2 x output index (frames).
+        order, k = [(0, None)], 0
+        while k + 1 < c.frames:
+            anchor = min(k + c.bframes + 1, c.frames - 1)
+            order.append((anchor, None))
+            order += [(b, "B") for b in range(k + 1, anchor)]
+            k = anchor
+        for i, (disp, kind) in enumerate(order):
+            ref_idc = 3
+            if kind == "B":
+                ref_idc = 2 if self.rng.random() < c.b_ref else 0
+            out += self.picture(i, idr=(i == 0), kind=kind, ref_idc=ref_idc, poc=2 * disp)
         return b"".join(out)
 
 

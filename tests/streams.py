@@ -58,6 +58,20 @@ STREAMS = {
                        intra_in_p=0.2, slices=2, deblock=(0, 1, 2), offsets=3),
     "hp_720p_4slices": dict(width_mbs=80, height_mbs=45, frames=2, seed=109, profile=100, transform8x8=1,
                             slices=4, deblock=(0, 2), scaling=1, num_refs=1),
+    # B pictures (IBBP, output order != decoding order): temporal + spatial direct, B_8x8 with direct
+    # sub-blocks, every B partition; default / implicit (POC distances) / explicit bi-prediction weights
+    "mp_qcif_ibbp_direct": dict(width_mbs=11, height_mbs=9, frames=7, seed=201, profile=77, bframes=2, num_refs=3),
+    "mp_qcif_ibbp_implicit": dict(width_mbs=11, height_mbs=9, frames=7, seed=202, profile=77, bframes=2, num_refs=3,
+                                  direct=(1,), bipred=2),
+    "hp_qcif_ibbp_explicit_8x8": dict(width_mbs=11, height_mbs=9, frames=7, seed=203, profile=100, transform8x8=1,
+                                      bframes=2, num_refs=3, direct=(0,), bipred=1),
+    "hp_cif_ibbbp_bref_slices": dict(width_mbs=22, height_mbs=18, frames=10, seed=205, profile=100, transform8x8=1,
+                                     bframes=3, b_ref=0.5, direct=(1,), bipred=2, num_refs=4, slices=3,
+                                     deblock=(0, 1, 2), offsets=4, cip=1, intra_in_p=0.15),
+    # 40 pictures with two long-term references (the IDR, and picture 2 by MMCO 4 + 6) used all
+    # along: more reference pictures than device DPB slots over the stream's life
+    "bp_qcif_longterm_40": dict(width_mbs=11, height_mbs=9, frames=40, seed=204, num_refs=4, long_term=2, skip=0.3,
+                                intra_in_p=0.05),
 }
 
 CAP_MAGIC = 0x43523448
@@ -75,6 +89,19 @@ def capture_path(name: str) -> str:
 def crop_of(cfg: dict) -> OUT.Crop:
     l, r, t, b = cfg.get("crop", (0, 0, 0, 0))
     return OUT.Crop(left=l, right=r, top=t, bottom=b)
+
+
+def output_order(pics: list[dict]) -> list[int]:
+    """Decoding-order indices of captured pictures in output order: POC order inside each
+    IDR period (a new period at every POC 0 after the first picture) -- the order the
+    reference's DPB writes them (dpb.cc output process)."""
+    keys, period = [], 0
+    for i, p in enumerate(pics):
+        poc = int(p["pic"]["poc"][0])
+        if i and poc == 0:
+            period += 1
+        keys.append((period, poc, i))
+    return [k[2] for k in sorted(keys)]
 
 
 def frame_md5s(planes, cfg: dict) -> list[str]:

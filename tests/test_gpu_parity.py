@@ -134,6 +134,14 @@ def _large_batch_vs_oracle(L, dec, cidx, W, H, n, nbase=8):
 
 
 @pytest.mark.parametrize("cidx", [2, 3])
+def test_gpu_large_batch_wide_rows(L, dec, cidx):
+    """1080p-wide rows (W = 120 > 64) in a 256-picture batch of 32-row pictures: k_deblock2's
+    XCD-local mode (16 groups x 32 rows = 512 waves, 64 per XCD) and, all-intra, the walk's
+    coarse band hand-off publishing mid-row (gstep 64 < W); every picture checked."""
+    _large_batch_vs_oracle(L, dec, cidx, 120, 32, 256)
+
+
+@pytest.mark.parametrize("cidx", [2, 3])
 def test_gpu_large_batch_xcd_groups(L, dec, cidx):
     """464 CIF pictures (29 groups of 16 x 18 MB rows = 522 k_deblock2 waves): k_deblock2 in
     its XCD-local mode (groups on XCD g % 8, plain-store records) and the walk's coarse
@@ -172,8 +180,9 @@ def test_gpu_batch_dense_intra_levels(L, dec):
 
 @pytest.mark.parametrize("n", [33, 70])
 def test_gpu_batch_picture_groups(L, dec, n):
-    """Batches spanning several 32-picture groups of k_deblock2 (the last one ragged);
-    flag 0 takes whichever schedule H264R_DEBLOCK2_MIN selects for the batch size."""
+    """Batches spanning several 16-picture groups of k_deblock2 (the last one ragged) under
+    both schedules; flag 0 takes the default for these sizes (k_deblock, below
+    H264R_DEBLOCK2_MIN) -- k_deblock2's default selection is covered by the large batches."""
     _batch_vs_oracle(L, dec, 3, 11, 9, n, deblocks=(0, A.DBG_DEBLOCK_MB, A.DBG_DEBLOCK_ROWS), pcm_permille=20)
 
 
@@ -353,3 +362,24 @@ def test_gpu_batch_latency_chain(L, dec):
     ms, n, ok = bench.latency_chain(dec, L, cfg, refs, torch.cuda.current_stream().cuda_stream, 4, 4)
     assert n == 4 and ms > 0
     assert ok is True
+
+
+def test_gpu_expired_wait_reports_edevice(L, dec):
+    """Every device-side wait is bounded in wall time (device_common.h wait_give_up): under
+    H264R_DBG_WAIT_TEST every intra-walk wait asks for progress that never comes (10 ms
+    bound); the launch drains, h264r_picture_end reports H264R_EDEVICE within that bound
+    plus the drain, and the context decodes bit-exact again afterwards."""
+    import time
+    cfg = synth.default_cfg(L, 2, 22, 18)                 # all-intra: every row waits on the one above
+    p = synth.picture(L, cfg, 0)
+    refs = synth.refpics(L, cfg)
+    want = O.decode(p, refs)
+    for flag in (A.DBG_DEBLOCK_MB, A.DBG_DEBLOCK_ROWS):
+        t0 = time.time()
+        with pytest.raises(h264r.H264RError) as e:
+            dec.decode_picture(p, refs, debug=A.DBG_WAIT_TEST | flag)
+        assert e.value.status == A.EDEVICE
+        assert time.time() - t0 < 5.0
+        got = dec.decode_picture(p, refs, debug=flag)
+        for k in range(3):
+            assert np.array_equal(got[k], want[k]), (flag, k)

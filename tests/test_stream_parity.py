@@ -30,13 +30,10 @@ REF_BIN = os.path.join(S.ROOT, "oracle", "_ref")
 
 
 def _replay(pics, decode_picture):
-    """Decode captured pictures in order, keeping each reference picture in the DPB slot
-    the shim gave it; returns the output planes per picture."""
-    outs = []
-    for p in pics:
-        out = decode_picture(p)
-        outs.append(out)
-    return outs
+    """Decode captured pictures in decoding order, keeping each reference picture in the
+    DPB slot the shim gave it; returns the output planes in output order (POC)."""
+    outs = [decode_picture(p) for p in pics]
+    return [outs[i] for i in S.output_order(pics)]
 
 
 def test_stream_set_matches_writer_and_golden_table():
@@ -59,6 +56,7 @@ def test_captures_cover_the_path():
     sizes, every CBP class, explicit WP, deblocking idc 0/1/2 with offsets, multi-slice
     pictures, scaling lists (non-flat quantisation tables)."""
     types, t8, wp, idc, offs, multi, nonflat, chroma = set(), False, False, set(), False, False, False, set()
+    stypes, bwp, l1, t8b = set(), set(), False, False
     flat = O.quant_flat()
     for name in NAMES:
         for p in S.load_capture(S.capture_path(name)):
@@ -67,6 +65,11 @@ def test_captures_cover_the_path():
             t8 |= bool((m["flags"] & A.MBF_T8x8).any())
             chroma |= set(int(c) for c in np.unique(m["cbp"] >> 4))
             sl = p["slices"]
+            stypes |= set(int(v) for v in sl["slice_type"])
+            if (sl["slice_type"] == A.SLICE_B).any():
+                bwp |= set(int(v) for v in sl["wp_mode"])
+                l1 |= bool((p["ref_idx"][1] >= 0).any())
+                t8b |= bool((m["flags"] & A.MBF_T8x8).any())
             wp |= bool((sl["wp_mode"] == 1).any())
             idc |= set(int(v) for v in sl["deblock_idc"])
             offs |= bool((sl["filter_offset_a"] != 0).any() or (sl["filter_offset_b"] != 0).any())
@@ -74,6 +77,8 @@ def test_captures_cover_the_path():
             nonflat |= p["quant"].tobytes() != flat.tobytes()
     assert {A.P_SKIP, A.P_16x16, A.P_16x8, A.P_8x16, A.P_8x8, A.I_4x4, A.I_8x8, A.I_16x16, A.I_PCM} <= types
     assert t8 and wp and idc == {0, 1, 2} and offs and multi and nonflat and chroma == {0, 1, 2}
+    # B slices with list-1 prediction under every bi-prediction weighting, 8x8 transforms in B
+    assert {A.SLICE_P, A.SLICE_B, A.SLICE_I, A.SLICE_SP} <= stypes and bwp == {0, 1, 2} and l1 and t8b
 
 
 @pytest.mark.parametrize("name", NAMES)
