@@ -33,6 +33,8 @@ import os
 import random
 from dataclasses import dataclass, field
 
+import h264_cabac as CB
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 _T = json.load(open(os.path.join(HERE, "golden", "cavlc_tables.json")))
 
@@ -141,6 +143,8 @@ class StreamCfg:
     direct: tuple = (0, 1)           # direct_spatial_mv_pred_flag choices per B slice (0 temporal, 1 spatial)
     b_ref: float = 0.0               # share of B pictures kept as references (nal_ref_idc != 0)
     l1_refs: int = 2                 # max num_ref_idx_l1_active of B slices
+    cabac: int = 0                   # entropy_coding_mode_flag (CABAC, tests/h264_cabac.py; Main / High)
+    cabac_init: tuple = (0, 1, 2)    # cabac_init_idc choices per P / B slice
     long_term: int = 0               # the IDR is a long-term reference (LongTermFrameIdx 0) kept for the
                                      # whole stream, and P picture `long_term` becomes a second one by
                                      # MMCO 4 + 6 (LongTermFrameIdx 1); P pictures predict from them
@@ -156,6 +160,16 @@ class _Mb:
     i8: list = field(default_factory=lambda: [2] * 4)
     t8: bool = False
     nz: list = field(default_factory=lambda: [[[0] * 4 for _ in range(4)] for _ in range(3)])
+    # what the CABAC context selection reads of a decoded MB (mb_t fields, macroblock.h:78-135)
+    skip: bool = False
+    mbt_ref: int = 0                 # mb_t::mb_type (0 skip / direct, 1..4 partitions, 8 I_4x4, 9 I_8x8, 10 I_16x16, 12 I_PCM)
+    cbpl: int = 0
+    cbpc: int = 0
+    cmode: int = 0
+    cbp_bits: int = 0
+    sub_direct: list = field(default_factory=lambda: [False] * 4)
+    ref: list = field(default_factory=lambda: [[-1] * 16, [-1] * 16])
+    mvd: list = field(default_factory=lambda: [[(0, 0)] * 16, [(0, 0)] * 16])
 
 
 def _blk_xy(blk: int):
@@ -170,6 +184,7 @@ class Encoder:
         self.W, self.H = cfg.width_mbs, cfg.height_mbs
         self.log2_max_frame_num = 4
         self.log2_max_poc_lsb = 8
+        self.cab = None                  # the CABAC sink of the slice being written (CABAC streams)
 
     # ------------------------------------------------------------------ parameter sets
     def sps(self) -> bytes:
@@ -209,7 +224,7 @@ class Encoder:
     def pps(self) -> bytes:
         c, w = self.c, BitWriter()
         w.ue(0); w.ue(0)
-        w.u(1, 0)                                   # entropy_coding_mode_flag: CAVLC
+        w.u(1, c.cabac)                             # entropy_coding_mode_flag
         w.u(1, 0)                                   # bottom_field_pic_order_in_frame_present_flag
         w.ue(0)                                     # num_slice_groups_minus1
         w.ue(0); w.ue(0)                            # num_ref_idx_l0/l1_default_active_minus1
@@ -361,6 +376,9 @@ class Encoder:
     def _residual(self, w: BitWriter, a: int, m: _Mb, cbp: int, s: int) -> None:
         """residual_luma + residual_chroma (interpret_residual.cc:421-494)."""
         cbpl, cbpc = cbp & 15, cbp >> 4
+        if self.cab:
+            self._residual_cabac(m, cbpl, cbpc)
+            return
         if m.kind == I16:
             self._block(w, self._levels(16), self._nc(a, 0, 0, 0, s), 16)
         for b8 in range(4):
@@ -389,6 +407,34 @@ class Encoder:
                     m.nz[pl][by][bx] = self._block(w, self._levels(15), self._nc(a, pl, bx, by, s), 15)
                 else:
                     m.nz[pl][by][bx] = 0
+
+    def _residual_cabac(self, m: _Mb, cbpl: int, cbpc: int) -> None:
+        """The same blocks and level draws as the CAVLC path, as residual_block_cabac calls:
+        an 8x8 transform block is one 64-coefficient block (interpret_residual.cc:453-456)."""
+        cab = self.cab
+        if m.kind == I16:
+            cab.block(CB.LUMA_16DC, 0, 0, self._levels(16))
+        for b8 in range(4):
+            if not (cbpl >> b8) & 1:
+                continue
+            if m.t8:
+                l8 = self._levels(64)
+                if not any(l8):                  # no coded_block_flag for 8x8 blocks: >= 1 coefficient
+                    l8[0] = 1
+                cab.block(CB.LUMA_8x8, 0, b8 * 4, l8)
+                continue
+            for b4 in range(4):
+                if m.kind == I16:
+                    cab.block(CB.LUMA_16AC, 0, b8 * 4 + b4, self._levels(15))
+                else:
+                    cab.block(CB.LUMA_4x4, 0, b8 * 4 + b4, self._levels(16))
+        if cbpc & 3:
+            for pl in (1, 2):
+                cab.block(CB.CHROMA_DC, pl, 0, self._levels(4))
+        if cbpc & 2:
+            for pl in (1, 2):
+                for b in range(4):
+                    cab.block(CB.CHROMA_AC, pl, b, self._levels(15))
 
     # ------------------------------------------------------------------ intra modes
     def _pred_mode(self, a: int, m: _Mb, bx: int, by: int, s: int, n8: bool) -> int:
@@ -439,15 +485,25 @@ class Encoder:
         return [md for md, req in need.items() if all(have[ch] for ch in req)]
 
     # ------------------------------------------------------------------ one macroblock
-    def _mb(self, w: BitWriter, a: int, ptype: str, s: int, nref: int):
+    def _mb(self, w: BitWriter, a: int, ptype: str, s: int, nref):
+        """One macroblock: every random decision is drawn here in a fixed order; the syntax
+        goes out as CAVLC bits into `w`, or as CABAC bins through self.cab (a CabacSink)
+        when the stream is CABAC.  Returns False for a skipped MB."""
         c, r = self.c, self.rng
+        cab = self.cab
         m = self.mbs[a]
         m.slice = s
+        if cab:
+            cab.start_mb(a)
         roll = r.random()
         if ptype in ("P", "B") and roll < c.skip:
-            m.kind, m.intra = SKIP, False
+            m.kind, m.intra, m.skip, m.mbt_ref = SKIP, False, True, 0
             m.nz = [[[0] * 4 for _ in range(4)] for _ in range(3)]
+            if cab:
+                cab.skip_flag(True)
             return False
+        if cab and ptype != "I":
+            cab.skip_flag(False)
         intra = ptype == "I" or r.random() < c.intra_in_p
         base = 5 if ptype == "P" else (23 if ptype == "B" else 0)
         if intra:
@@ -467,11 +523,16 @@ class Encoder:
         mx, my = a % self.W, a // self.W
         A, B, D = self._avail_abd(a, 0, 0, 4, s)
         if m.kind == PCM:
-            w.ue(base + 25)
-            while not w.aligned():
-                w.u(1, 0)
-            for _ in range(384):
-                w.u(8, r.randint(1, 255))
+            m.mbt_ref = 12
+            if cab:
+                cab.mb_type_intra(25)
+                cab.pcm([r.randint(1, 255) for _ in range(384)])
+            else:
+                w.ue(base + 25)
+                while not w.aligned():
+                    w.u(1, 0)
+                for _ in range(384):
+                    w.u(8, r.randint(1, 255))
             m.nz = [[[16] * 4 for _ in range(4)] for _ in range(3)]
             return True
         cmodes = [0] + ([1] if A else []) + ([2] if B else []) + ([3] if A and B and D else [])
@@ -480,21 +541,36 @@ class Encoder:
             mode = r.choice(modes)
             cbpc = r.randint(0, 2)
             cbpl = 15 if r.random() < 0.5 else 0
-            w.ue(base + 1 + mode + 4 * cbpc + (12 if cbpl else 0))
-            w.ue(r.choice(cmodes))
+            m.mbt_ref, m.cbpl, m.cbpc = 10, cbpl, cbpc
+            cm = r.choice(cmodes)
+            if cab:
+                cab.mb_type_intra(1 + mode + 4 * cbpc + (12 if cbpl else 0))
+                m.cmode = cm
+                cab.chroma_mode(cm)
+            else:
+                w.ue(base + 1 + mode + 4 * cbpc + (12 if cbpl else 0))
+                w.ue(cm)
             cbp = cbpl | cbpc << 4
         elif m.kind in (I4, I8):
-            w.ue(base + 0)
             m.t8 = m.kind == I8
-            if c.transform8x8:
-                w.u(1, 1 if m.t8 else 0)
+            m.mbt_ref = 9 if m.t8 else 8
+            if cab:
+                cab.mb_type_intra(0)
+                if c.transform8x8:
+                    cab.transform8x8(m.t8)
+            else:
+                w.ue(base + 0)
+                if c.transform8x8:
+                    w.u(1, 1 if m.t8 else 0)
             if m.kind == I4:
                 for blk in range(16):
                     bx, by = _blk_xy(blk)
                     mode = r.choice(self._valid_nxn(*self._avail_abd(a, bx, by, 1, s)))
                     pred = self._pred_mode(a, m, bx, by, s, False)
                     m.i4[blk] = mode
-                    if mode == pred:
+                    if cab:
+                        cab.intra_mode(mode, pred)
+                    elif mode == pred:
                         w.u(1, 1)
                     else:
                         w.u(1, 0); w.u(3, mode if mode < pred else mode - 1)
@@ -504,63 +580,117 @@ class Encoder:
                     mode = r.choice(self._valid_nxn(*self._avail_abd(a, bx, by, 2, s)))
                     pred = self._pred_mode(a, m, bx, by, s, True)
                     m.i8[b8] = mode
-                    if mode == pred:
+                    if cab:
+                        cab.intra_mode(mode, pred)
+                    elif mode == pred:
                         w.u(1, 1)
                     else:
                         w.u(1, 0); w.u(3, mode if mode < pred else mode - 1)
-            w.ue(r.choice(cmodes))
+            cm = r.choice(cmodes)
             cbp = r.randint(0, 47)
-            w.ue(CBP_CODE["intra"][cbp])
+            m.cbpl, m.cbpc = cbp & 15, cbp >> 4
+            if cab:
+                m.cmode = cm
+                cab.chroma_mode(cm)
+                cab.cbp(cbp)
+            else:
+                w.ue(cm)
+                w.ue(CBP_CODE["intra"][cbp])
         elif ptype == "B":
-            cbp, small = self._b_inter(w, nref)
+            cbp, small = self._b_inter(w, nref, a)
             m.t8 = False
             if (cbp & 15) and c.transform8x8 and not small:
                 m.t8 = r.random() < 0.5
-                w.u(1, 1 if m.t8 else 0)
+                if cab:
+                    cab.transform8x8(m.t8)
+                else:
+                    w.u(1, 1 if m.t8 else 0)
         else:
             mbt = r.choices([0, 1, 2, 3, 4], weights=[45, 12, 12, 21, 10])[0]
-            w.ue(mbt)
-            def ref_idx():
+            if cab and mbt == 4:
+                mbt = 3                                  # no P_8x8ref0 in CABAC (Table 9-37)
+            m.mbt_ref = (1, 2, 3, 4, 4)[mbt]
+            if cab:
+                cab.mb_type_p(mbt)
+            else:
+                w.ue(mbt)
+            parts = {0: [(0, 0, 4, 4)], 1: [(0, 0, 4, 2), (0, 2, 4, 2)], 2: [(0, 0, 2, 4), (2, 0, 2, 4)]}
+            def ref_idx(x0, y0, pw, ph):
                 v = r.randrange(nref)
-                if nref == 2:
+                if cab:
+                    cab.ref_idx(v, nref, 0, x0, y0)
+                    self._set_ref(m, 0, x0, y0, pw, ph, v)
+                elif nref == 2:
                     w.u(1, 1 - v)
                 elif nref > 2:
                     w.ue(v)
-            def mvd():
-                w.se(r.randint(-c.mv_range, c.mv_range)); w.se(r.randint(-c.mv_range, c.mv_range))
+            def mvd(x0, y0, pw, ph):
+                dx, dy = r.randint(-c.mv_range, c.mv_range), r.randint(-c.mv_range, c.mv_range)
+                if cab:
+                    cab.mvd(dx, 0, 0, x0, y0); cab.mvd(dy, 0, 1, x0, y0)
+                    self._set_mvd(m, 0, x0, y0, pw, ph, (dx, dy))
+                else:
+                    w.se(dx); w.se(dy)
             small = False
             if mbt in (0, 1, 2):
-                for _ in range(1 if mbt == 0 else 2):
-                    ref_idx()
-                for _ in range(1 if mbt == 0 else 2):
-                    mvd()
+                for p in parts[mbt]:
+                    ref_idx(*p)
+                for p in parts[mbt]:
+                    mvd(*p)
             else:
                 subs = [r.choice([0, 0, 1, 2, 3]) for _ in range(4)]
                 small = any(sb != 0 for sb in subs)
                 for sb in subs:
-                    w.ue(sb)
+                    if cab:
+                        cab.sub_p(sb)
+                    else:
+                        w.ue(sb)
                 if mbt == 3:
-                    for _ in range(4):
-                        ref_idx()
-                for sb in subs:
-                    for _ in range({0: 1, 1: 2, 2: 2, 3: 4}[sb]):
-                        mvd()
+                    for b8 in range(4):
+                        ref_idx((b8 % 2) * 2, (b8 // 2) * 2, 2, 2)
+                for b8, sb in enumerate(subs):
+                    x8, y8 = (b8 % 2) * 2, (b8 // 2) * 2
+                    for sp in {0: [(0, 0, 2, 2)], 1: [(0, 0, 2, 1), (0, 1, 2, 1)], 2: [(0, 0, 1, 2), (1, 0, 1, 2)],
+                               3: [(0, 0, 1, 1), (1, 0, 1, 1), (0, 1, 1, 1), (1, 1, 1, 1)]}[sb]:
+                        mvd(x8 + sp[0], y8 + sp[1], sp[2], sp[3])
             cbp = r.randint(0, 47)
-            w.ue(CBP_CODE["inter"][cbp])
+            m.cbpl, m.cbpc = cbp & 15, cbp >> 4
+            if cab:
+                cab.cbp(cbp)
+            else:
+                w.ue(CBP_CODE["inter"][cbp])
             m.t8 = False
             if (cbp & 15) and c.transform8x8 and not small:
                 m.t8 = r.random() < 0.5
-                w.u(1, 1 if m.t8 else 0)
+                if cab:
+                    cab.transform8x8(m.t8)
+                else:
+                    w.u(1, 1 if m.t8 else 0)
         if cbp or m.kind == I16:
             lo, hi = c.qp
             if c.lossless and not m.intra:
                 lo = max(lo, 1)
             target = 0 if (c.lossless and m.intra and r.random() < c.lossless) else r.randint(lo, hi)
             d = (target - self.qp_pred + 26) % 52 - 26
-            w.se(d)
+            if cab:
+                cab.qp_delta(d)
+            else:
+                w.se(d)
             self.qp_pred = (self.qp_pred + d + 52) % 52
         self._residual(w, a, m, cbp, s)
         return True
+
+    @staticmethod
+    def _set_ref(m, lst, x0, y0, pw, ph, v):
+        for y in range(y0, y0 + ph):
+            for x in range(x0, x0 + pw):
+                m.ref[lst][y * 4 + x] = v
+
+    @staticmethod
+    def _set_mvd(m, lst, x0, y0, pw, ph, v):
+        for y in range(y0, y0 + ph):
+            for x in range(x0, x0 + pw):
+                m.mvd[lst][y * 4 + x] = v
 
     # B partitions: mb_type 1..21 -> prediction of partition 0 / 1 (Table 7-14); sub_mb_type
     # -> (prediction, sub-partitions) (Table 7-18); None = direct
@@ -571,53 +701,87 @@ class Encoder:
     B_SUBS = {0: (None, 0), 1: ("L0", 1), 2: ("L1", 1), 3: ("Bi", 1), 4: ("L0", 2), 5: ("L0", 2), 6: ("L1", 2),
               7: ("L1", 2), 8: ("Bi", 2), 9: ("Bi", 2), 10: ("L0", 4), 11: ("L1", 4), 12: ("Bi", 4)}
 
-    def _b_inter(self, w: BitWriter, nref: tuple):
-        """An inter MB of a B slice (CAVLC, 7.3.5.1-7.3.5.2; interpret_mb.cc:392-404, 480-503,
+    def _b_inter(self, w: BitWriter, nref: tuple, a: int):
+        """An inter MB of a B slice (7.3.5.1-7.3.5.2; interpret_mb.cc:392-404, 480-503,
         636-700): mb_type B_Direct_16x16 / 16x16 / 16x8 / 8x16 / B_8x8 with direct and every
-        sub-partition, then ref_idx of list 0, of list 1, mvd of list 0, of list 1.  Returns
-        (cbp, has sub-partitions smaller than 8x8)."""
-        c, r = self.c, self.rng
+        sub-partition, then ref_idx of list 0, of list 1, mvd of list 0, of list 1 (CAVLC
+        bits, or CABAC bins through self.cab).  Returns (cbp, has sub-partitions smaller
+        than 8x8)."""
+        c, r, cab = self.c, self.rng, self.cab
+        m = self.mbs[a]
         n0, n1 = nref
 
-        def ref_idx(n):
+        def ref_idx(n, lst, x0, y0, pw, ph):
             v = r.randrange(n)
-            if n == 2:
+            if cab:
+                cab.ref_idx(v, n, lst, x0, y0)
+                self._set_ref(m, lst, x0, y0, pw, ph, v)
+            elif n == 2:
                 w.u(1, 1 - v)
             elif n > 2:
                 w.ue(v)
 
-        def mvd():
-            w.se(r.randint(-c.mv_range, c.mv_range)); w.se(r.randint(-c.mv_range, c.mv_range))
+        def mvd(lst, x0, y0, pw, ph):
+            dx, dy = r.randint(-c.mv_range, c.mv_range), r.randint(-c.mv_range, c.mv_range)
+            if cab:
+                cab.mvd(dx, lst, 0, x0, y0); cab.mvd(dy, lst, 1, x0, y0)
+                self._set_mvd(m, lst, x0, y0, pw, ph, (dx, dy))
+            else:
+                w.se(dx); w.se(dy)
         k = r.random()
         mbt = 0 if k < 0.15 else (r.randint(1, 3) if k < 0.55 else (r.randint(4, 21) if k < 0.8 else 22))
-        w.ue(mbt)
+        m.mbt_ref = 0 if mbt == 0 else (1 if mbt <= 3 else (4 if mbt == 22 else (2 if mbt % 2 == 0 else 3)))
+        m.sub_direct = [mbt == 0] * 4
+        if cab:
+            cab.mb_type_b(mbt)
+        else:
+            w.ue(mbt)
         small = False
         if 1 <= mbt <= 21:
             preds = self.B_PARTS[mbt]
-            for lst, n in (("L0", n0), ("L1", n1)):
-                for pr in preds:
-                    if pr in (lst, "Bi"):
-                        ref_idx(n)
-            for lst in ("L0", "L1"):
-                for pr in preds:
-                    if pr in (lst, "Bi"):
-                        mvd()
+            geo = [(0, 0, 4, 4)] if mbt <= 3 else ([(0, 0, 4, 2), (0, 2, 4, 2)] if mbt % 2 == 0 else [(0, 0, 2, 4), (2, 0, 2, 4)])
+            for lst, (name, n) in enumerate((("L0", n0), ("L1", n1))):
+                for pr, g in zip(preds, geo):
+                    if pr in (name, "Bi"):
+                        ref_idx(n, lst, *g)
+            for lst, name in enumerate(("L0", "L1")):
+                for pr, g in zip(preds, geo):
+                    if pr in (name, "Bi"):
+                        mvd(lst, *g)
         elif mbt == 22:
             subs = [0 if r.random() < 0.3 else r.randint(1, 12) for _ in range(4)]
             small = any(self.B_SUBS[sb][1] > 1 for sb in subs)
+            m.sub_direct = [sb == 0 for sb in subs]
             for sb in subs:
-                w.ue(sb)
-            for lst, n in (("L0", n0), ("L1", n1)):
-                for sb in subs:
-                    if sb and self.B_SUBS[sb][0] in (lst, "Bi"):
-                        ref_idx(n)
-            for lst in ("L0", "L1"):
-                for sb in subs:
-                    if sb and self.B_SUBS[sb][0] in (lst, "Bi"):
-                        for _ in range(self.B_SUBS[sb][1]):
-                            mvd()
+                if cab:
+                    cab.sub_b(sb)
+                else:
+                    w.ue(sb)
+            for lst, (name, n) in enumerate((("L0", n0), ("L1", n1))):
+                for b8, sb in enumerate(subs):
+                    if sb and self.B_SUBS[sb][0] in (name, "Bi"):
+                        ref_idx(n, lst, (b8 % 2) * 2, (b8 // 2) * 2, 2, 2)
+            for lst, name in enumerate(("L0", "L1")):
+                for b8, sb in enumerate(subs):
+                    if sb and self.B_SUBS[sb][0] in (name, "Bi"):
+                        x8, y8 = (b8 % 2) * 2, (b8 // 2) * 2
+                        nparts = self.B_SUBS[sb][1]
+                        if nparts == 1:
+                            sps = [(0, 0, 2, 2)]
+                        elif nparts == 4:
+                            sps = [(0, 0, 1, 1), (1, 0, 1, 1), (0, 1, 1, 1), (1, 1, 1, 1)]
+                        elif sb in (4, 6, 8):            # 8x4
+                            sps = [(0, 0, 2, 1), (0, 1, 2, 1)]
+                        else:                            # 4x8
+                            sps = [(0, 0, 1, 2), (1, 0, 1, 2)]
+                        for sp in sps:
+                            mvd(lst, x8 + sp[0], y8 + sp[1], sp[2], sp[3])
         cbp = r.randint(0, 47)
-        w.ue(CBP_CODE["inter"][cbp])
+        m.cbpl, m.cbpc = cbp & 15, cbp >> 4
+        if cab:
+            cab.cbp(cbp)
+        else:
+            w.ue(CBP_CODE["inter"][cbp])
         return cbp, small
 
     # ------------------------------------------------------------------ pictures
@@ -719,6 +883,10 @@ class Encoder:
                 w.ue(0)                             # end
             elif ref_idc:
                 w.u(1, 0)                           # adaptive_ref_pic_marking_mode_flag
+            init_idc = 0
+            if c.cabac and ptype != "I":
+                init_idc = r.choice(c.cabac_init)
+                w.ue(init_idc)                      # cabac_init_idc
             lo, hi = c.qp
             sqp = r.randint(lo, hi)
             w.se(sqp - 26)
@@ -730,15 +898,26 @@ class Encoder:
             w.ue(idc)
             if idc != 1:
                 w.se(r.randint(-c.offsets, c.offsets)); w.se(r.randint(-c.offsets, c.offsets))
-            skip_run = 0
-            for a in range(first, end):
-                coded = self._mb(w if ptype == "I" else _Deferred(w, skip_run), a, ptype, s,
-                                 nref_b if ptype == "B" else nref)
-                if ptype != "I":
-                    skip_run = 0 if coded else skip_run + 1
-            if ptype != "I" and skip_run:
-                w.ue(skip_run)
-            w.trailing()
+            if c.cabac:
+                while not w.aligned():
+                    w.u(1, 1)                       # cabac_alignment_one_bit
+                self.cab = CB.CabacSink(self, w.bits, ptype, sqp, init_idc, s)
+                for a in range(first, end):
+                    self._mb(w, a, ptype, s, nref_b if ptype == "B" else nref)
+                    self.cab.end_of_slice(a == end - 1)   # the flush's last bit is rbsp_stop_one_bit
+                self.cab = None
+                while not w.aligned():
+                    w.u(1, 0)                       # rbsp_alignment_zero_bit
+            else:
+                skip_run = 0
+                for a in range(first, end):
+                    coded = self._mb(w if ptype == "I" else _Deferred(w, skip_run), a, ptype, s,
+                                     nref_b if ptype == "B" else nref)
+                    if ptype != "I":
+                        skip_run = 0 if coded else skip_run + 1
+                if ptype != "I" and skip_run:
+                    w.ue(skip_run)
+                w.trailing()
             out.append(nal_unit(ref_idc, 5 if idr else 1, w.bytes()))
         if ref_idc:                                          # marking after the picture (8.2.5)
             if idr:

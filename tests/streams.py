@@ -68,6 +68,21 @@ STREAMS = {
     "hp_cif_ibbbp_bref_slices": dict(width_mbs=22, height_mbs=18, frames=10, seed=205, profile=100, transform8x8=1,
                                      bframes=3, b_ref=0.5, direct=(1,), bipred=2, num_refs=4, slices=3,
                                      deblock=(0, 1, 2), offsets=4, cip=1, intra_in_p=0.15),
+    # CABAC (entropy_coding_mode_flag 1, tests/h264_cabac.py): every cabac_init_idc, PCM inside CABAC
+    # slices, 8x8 transform blocks as one 64-coefficient block (interpret_residual.cc:453-456)
+    "mp_cif_cabac_ippp_slices": dict(width_mbs=22, height_mbs=18, frames=4, seed=401, profile=77, cabac=1, slices=3,
+                                     deblock=(0, 1, 2), offsets=6, pcm=0.05, num_refs=2, weighted=1, cip=1),
+    "hp_cif_cabac_ibbp_4slices": dict(width_mbs=22, height_mbs=18, frames=7, seed=402, profile=100, transform8x8=1,
+                                      cabac=1, bframes=2, num_refs=3, bipred=2, slices=4, deblock=(2,), offsets=3),
+    "hp_qcif_cabac_intra_qp0_51": dict(width_mbs=11, height_mbs=9, frames=2, seed=403, profile=100, transform8x8=1,
+                                       cabac=1, all_intra=True, qp=(0, 51), pcm=0.05, level_max=3),
+    "hp_cif_cabac_bref_explicit_scaling": dict(width_mbs=22, height_mbs=18, frames=8, seed=404, profile=100,
+                                               transform8x8=1, cabac=1, bframes=3, b_ref=0.5, direct=(1,), bipred=1,
+                                               num_refs=4, scaling=3, chroma_qp_offset=3, second_chroma_qp_offset=-2),
+    # BASELINE config 4's shape as a real stream: 1080p High, IBBP, 8x8 transform, CABAC, 4 slices, idc 2
+    "hp_1080p_cabac_ibbp_4slices": dict(width_mbs=120, height_mbs=68, frames=4, seed=405, profile=100, transform8x8=1,
+                                        cabac=1, bframes=2, num_refs=3, bipred=2, slices=4, deblock=(2,), offsets=2,
+                                        crop=(0, 0, 0, 4)),
     # 40 pictures with two long-term references (the IDR, and picture 2 by MMCO 4 + 6) used all
     # along: more reference pictures than device DPB slots over the stream's life
     "bp_qcif_longterm_40": dict(width_mbs=11, height_mbs=9, frames=40, seed=204, num_refs=4, long_term=2, skip=0.3,

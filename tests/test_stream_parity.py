@@ -11,6 +11,8 @@ and every decode must reproduce the reference's per-frame MD5s (the reference ha
 compare protocol, script/test/model/__init__.py:119-183).
 """
 import ctypes as C
+import json
+import sys
 import hashlib
 import os
 import subprocess
@@ -171,3 +173,21 @@ def test_gpu_reference_parser_with_shim_end_to_end(name, tmp_path):
                        capture_output=True, text=True, timeout=300, cwd=tmp_path)
     assert r.returncode == 0, r.stdout[-800:] + r.stderr[-800:]
     assert OUT.digest_by_frames(str(out), cfg["frames"]) == GOLD[name]["frame_md5"]
+
+
+CABAC_TRACED = [n for n, c in S.STREAMS.items() if c.get("cabac") and c["width_mbs"] * c["height_mbs"] <= 400]
+
+
+@pytest.mark.skipif(not O.reference_available(), reason="needs /root/reference (this container only)")
+@pytest.mark.parametrize("name", CABAC_TRACED)
+def test_reference_parser_reads_what_the_cabac_writer_wrote(name):
+    """Every syntax element the reference parser decodes from a CABAC stream (mb_skip_flag,
+    mb_type, sub_mb_type, transform_size_8x8_flag, intra modes, ref_idx, mvd, CBP,
+    mb_qp_delta and every coefficient it pushes through Decoder::coeff_*; traced by
+    oracle/_ref/ldecod_trace) is the one the writer meant -- the MD5 agreement above could
+    otherwise hide a stream both decoders misread alike."""
+    O.build_ref()
+    r = subprocess.run([sys.executable, os.path.join(S.ROOT, "tools", "cabac_trace_diff.py"),
+                        json.dumps(S.STREAMS[name])], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "syntax elements agree" in r.stdout
