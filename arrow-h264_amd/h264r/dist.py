@@ -95,3 +95,54 @@ def max_over_ranks(seconds: float, device=None) -> float:
     t = torch.tensor([seconds], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+# ------------------------------------------------------------------ dependent chains
+# Slice mode over a real stream (bench.py --chain): every picture of a chain predicts from
+# the chain's previous decoded picture, so each reference picture crosses the ranks once,
+# before the next picture of its chain may start -- the exchange is on the dependency
+# path (slice walk slice_data.cc:640-650, idc 2 stopping the filter at slice edges
+# deblock.cc:247-253).  K chains advance together: their pictures form one batch, chain k
+# predicting from DPB slot k, and one all-gather per plane moves every rank's band of all
+# K pictures at once.
+
+def chain_slots(slices, chain: int, nchains: int):
+    """Slice tables of a chain's picture: reference slot 0 (the picture's first list-0
+    reference) becomes the chain's own slot `chain`, slot s >= 1 the shared static slot
+    nchains + s - 1; unused entries (-1) stay."""
+    import numpy as np
+    out = slices.copy()
+    rs = out["ref_slot"]
+    rs[...] = np.where(rs == 0, chain, np.where(rs > 0, nchains + rs.astype(np.int16) - 1, rs)).astype(np.int8)
+    if nchains + int(slices["ref_slot"].max()) - 1 >= 32:
+        raise ValueError("chain slots exceed the 32 DPB slots of a batch")
+    return out
+
+
+def chain_exchange(out, slots, bands: Sequence[tuple[int, int]], rank: int, plane_bytes: int, slot_stride: int,
+                   rows_per_mb: int, row_bytes: int, group=None) -> None:
+    """Exchange of one plane in chain mode: `out` holds the K decoded planes of this rank
+    ([K][plane_bytes], only this rank's band rows valid); `slots` the K chains' DPB slot
+    planes ([K][slot_stride]).  Every rank's band of all K pictures travels in ONE
+    all-gather (bands padded to the widest); each rank then lands every band in every
+    chain's slot.  World 1: a local copy."""
+    import torch
+    import torch.distributed as dist
+    world = len(bands)
+    K = out.numel() // plane_bytes
+    rb = rows_per_mb * row_bytes
+    src = out.reshape(-1)[:K * plane_bytes].view(K, plane_bytes)
+    dst = slots.reshape(-1)[:K * slot_stride].view(K, slot_stride)
+    if world == 1 or not (dist.is_available() and dist.is_initialized()):
+        dst[:, :plane_bytes].copy_(src)
+        return
+    wide = max(b1 - b0 for b0, b1 in bands) * rb
+    a0, a1 = bands[rank][0] * rb, bands[rank][1] * rb
+    send = torch.zeros((K, wide), dtype=out.dtype, device=out.device)
+    if a1 > a0:
+        send[:, :a1 - a0].copy_(src[:, a0:a1])
+    recv = torch.empty((world, K, wide), dtype=out.dtype, device=out.device)
+    dist.all_gather_into_tensor(recv.view(-1), send.view(-1), group=group)
+    for r, (b0, b1) in enumerate(bands):
+        if b1 > b0:
+            dst[:, b0 * rb:b1 * rb].copy_(recv[r, :, :(b1 - b0) * rb])

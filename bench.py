@@ -101,10 +101,13 @@ def cpu_baseline_threads(cfg, refs, seconds: float, threads: int):
 
 
 def kernel_bytes(pics, nmb):
-    """Algorithmic bytes per launch of k_inter, k_intra_pic and k_deblock over a batch
-    (SURVEY 8(d) per-MB formula split by the kernel that reads / writes them):
-    inter/PCM MBs R + 384 W in k_inter, intra MBs R + 384 W in k_intra_pic, and every
-    sample read once and written once by k_deblock."""
+    """The path's algorithmic bytes (R + W per MB, summed over the batch) split
+    over the kernels without double counting: an MB's R (record, levels, motion, reference
+    samples) to the kernel that reconstructs it (inter / PCM MBs k_inter4, intra MBs the
+    intra kernels), every MB's W (384 final samples) to the deblocking kernel that stores
+    them.  The three parts add up to the path's bytes; the unfiltered samples the
+    reconstruction kernels write and the deblocking kernel reads back are not algorithmic
+    (a fused design keeps them on chip), so they appear only in the PMC traffic."""
     from h264r import _abi as A
     inter = intra = 0
     pop4 = np.array([bin(v).count("1") for v in range(16)])
@@ -121,9 +124,9 @@ def kernel_bytes(pics, nmb):
         nl = used.sum(axis=0)
         r = 32 + 128 * pop4[cbpl] + 32 * i16 + 16 * (cbpc != 0) + 256 * (cbpc == 2) + 464 * np.where(is_intra, 0, nl)
         r = np.where(pcm, 416, r)
-        intra += int((r + 384)[is_intra & ~pcm].sum())
-        inter += int((r + 384)[~is_intra | pcm].sum())
-    return [inter, intra, len(pics) * nmb * 768]
+        intra += int(r[is_intra & ~pcm].sum())
+        inter += int(r[~is_intra | pcm].sum())
+    return [inter, intra, len(pics) * nmb * 384]
 
 
 def latency_chain(dec, L, cfg, refs, stream, n: int, verify: int):
@@ -183,6 +186,165 @@ def latency_chain(dec, L, cfg, refs, stream, n: int, verify: int):
     return (time.perf_counter() - t0) / n * 1e3, n, verified
 
 
+def chain_bench(args, rank: int, world: int, local: int, cs, rehearse: bool) -> dict:
+    """--chain K: K dependent chains per step, slice-sharded over the ranks (DESIGN
+    section 6).  Chain k's picture t predicts from its picture t-1 (DPB slot k): a rank decodes
+    its slice band of the K pictures, then ONE all-gather per plane brings every rank's band
+    of all K pictures into every rank's chain slots before any chain's next picture may
+    start -- one exchange per reference picture, on the dependency path.  The chains are
+    split into two groups whose batches alternate on the decode stream, so the exchange of
+    one group (communication stream) overlaps the decode of the other.  Each group keeps
+    two slot sets (ping-pong: step t reads set t % 2, its exchange fills set (t+1) % 2)."""
+    import torch
+    import h264r
+    from h264r import batch as B
+    from h264r import synth
+    from h264r import dist as D
+    L = h264r.lib()
+    W, H = CONFIG_SIZE[args.config]
+    cfg = synth.default_cfg(L, args.config, W, H)
+    refs = synth.refpics(L, cfg)
+    if not refs:
+        raise SystemExit("--chain needs inter pictures (configs 3, 4, 5)")
+    kg = args.chain // 2
+    nmb = W * H
+    base = [synth.picture(L, cfg, i) for i in range(2 * kg)]
+    srow = base[0].mbs["slice"].reshape(H, W)[:, 0]
+    first = [0] + [r for r in range(1, H) if srow[r] != srow[r - 1]]
+    bands = D.slice_bands(first, H, world) if world > 1 else [(0, H)]
+    band = bands[rank]
+    if world > 1 and cfg.deblock_idc == 0:
+        raise SystemExit("slice sharding needs disable_deblocking_filter_idc 1/2 (configs 4, 5)")
+    slack = 64
+    pbytes = (256 * nmb, 64 * nmb, 64 * nmb)
+    rows_per_mb, row_bytes = (16, 8, 8), (16 * W, 8 * W, 8 * W)
+    dec = h264r.Decoder(local, W, H)
+    static = []
+    for r in refs[1:]:
+        static.append([torch.from_numpy(np.concatenate([a.reshape(-1), np.zeros(slack, np.uint8)])).to("cuda")
+                       for a in r])
+    groups = []
+    for g in range(2):
+        pics = []
+        for k in range(kg):
+            p = base[g * kg + k]
+            p.slices = D.chain_slots(p.slices, k, kg)
+            pics.append(p)
+        # two slot sets per plane: [kg][plane + slack], every chain starting from refs[0]
+        sets = []
+        for _ in range(2):
+            planes = []
+            for k3 in range(3):
+                t = torch.zeros((kg, pbytes[k3] + slack), dtype=torch.uint8, device="cuda")
+                t[:, :pbytes[k3]].copy_(torch.from_numpy(refs[0][k3].reshape(1, -1)).expand(kg, -1))
+                planes.append(t)
+            sets.append(planes)
+        tabs = []
+        for si in range(2):
+            tab = np.zeros(3 * 32, np.int64)
+            for k in range(kg):
+                for k3 in range(3):
+                    tab[3 * k + k3] = sets[si][k3][k].data_ptr()
+            for j, planes in enumerate(static):
+                for k3 in range(3):
+                    tab[3 * (kg + j) + k3] = planes[k3].data_ptr()
+            tabs.append(torch.from_numpy(tab).to("cuda"))
+        db = B.to_device(B.pack(pics, h264r.quant_flat()), kg, tabs[0].data_ptr())
+        groups.append(dict(pics=pics, sets=sets, tabs=tabs, db=db, ev_ex=[]))
+    comm = torch.cuda.Stream(device=local)
+    stream = cs.cuda_stream
+    nstep = [0]
+
+    def step():
+        t = nstep[0]
+        nstep[0] += 1
+        for G in groups:
+            if t >= 1:
+                cs.wait_event(G["ev_ex"][t - 1])       # this chain group's previous pictures are in place
+            G["db"].batch.ref_planes = G["tabs"][t % 2].data_ptr()
+            if band[1] > band[0]:
+                dec.decode_batch(G["db"].batch, stream, rows=None if band == (0, H) else band)
+            ev = torch.cuda.Event()
+            ev.record(cs)
+            comm.wait_event(ev)
+            with torch.cuda.stream(comm):
+                outs = (G["db"].tensors["out_y"], G["db"].tensors["out_u"], G["db"].tensors["out_v"])
+                for k3 in range(3):
+                    D.chain_exchange(outs[k3], G["sets"][(t + 1) % 2][k3], bands, rank, pbytes[k3],
+                                     pbytes[k3] + slack, rows_per_mb[k3], row_bytes[k3])
+                ex = torch.cuda.Event()
+                ex.record(comm)
+            G["ev_ex"].append(ex)
+
+    verified = None
+    if not args.no_verify:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import _oracle as O
+        verified = True
+        G = groups[0]
+        prev = refs[0]
+        for t in range(2):                             # chain 0 of group 0, two dependent pictures
+            step()
+            torch.cuda.synchronize()
+            dec.check()
+            if rank == 0:
+                slot_refs = [prev] + [refs[0]] * (kg - 1) + list(refs[1:])
+                want = O.decode(G["pics"][0], slot_refs)
+                got = [G["sets"][(t + 1) % 2][k3][0, :pbytes[k3]].cpu().numpy() for k3 in range(3)]
+                verified &= all(np.array_equal(got[k3], want[k3].reshape(-1)) for k3 in range(3))
+                prev = want
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    dec.set_timing(True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    dec.check()
+    kern = np.array(dec.last_timing()) * 2 if band[1] > band[0] else np.zeros(4)   # two launches per step
+    dec.set_timing(False)
+    dt = D.max_over_ranks(dt, device="cpu" if rehearse else "cuda")
+    rd = wr = 0
+    for p in base:
+        r, w = synth.algo_bytes(L, p)
+        rd, wr = rd + r, wr + w
+    total_mbs = 2 * kg * nmb * args.steps
+    value = total_mbs / dt
+    frac_rows = (band[1] - band[0]) / H
+    step_bytes = int((rd + wr) * frac_rows)
+    achieved = step_bytes / (kern[3] * 1e-3) / 1e9 if kern[3] > 0 else 0.0
+    return {
+        "metric": "macroblocks/s (decode reconstruct, post-entropy) 1080p P-frame; % HBM roofline",
+        "value": value, "unit": "macroblocks/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "u8", "data": "synthetic (seeded SURVEY 8(d) generator, arrow-h264_amd/csrc/synth.c)",
+        "config": {"workload": f"{CONFIG_NAMES[args.config]}, {2 * kg} dependent chains (each picture predicts "
+                               "from its chain's previous decoded picture; one all-gather per plane per step)",
+                   "survey_config": args.config, "width_mbs": W, "height_mbs": H, "mode": "chain",
+                   "chains": 2 * kg, "parallelism": f"slices{world}" if world > 1 else "single",
+                   "rows_this_rank": list(band), "bands": [list(b) for b in bands]},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "kernel": "h264r_decode_batch launch sequences of the two chain groups",
+                     "kernel_ms": float(kern[3]), "kernel_algo_bytes": step_bytes,
+                     "numerator": "SURVEY 8(d) R+W of this rank's band of the step's pictures"},
+        "kernel_ms": {"inter": float(kern[0]), "intra": float(kern[1]), "deblock": float(kern[2]),
+                      "batch_wall": float(kern[3])},
+        "exchange_per_step": {"collectives": 3 if world > 1 else 0,
+                              "bytes_per_rank": int(sum(pbytes) * 2 * kg * frac_rows)},
+        "cpu_baseline": None,
+        "verified_vs_oracle": verified,
+    }
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -197,6 +359,9 @@ def main() -> int:
     ap.add_argument("--latency-pictures", type=int, default=32,
                     help="length of the dependent-chain latency run (rank 0, N=1; 0 = skip)")
     ap.add_argument("--traffic-json", default=None, help="PMC traffic summary (default profiles/traffic.json)")
+    ap.add_argument("--chain", type=int, default=0,
+                    help="dependent-chain mode: this many chains (even, <= 60) advance one picture per step, "
+                         "slice-sharded with one all-gather per reference picture (see chain_bench)")
     ap.add_argument("--shard", choices=["replicas", "slices"], default=None,
                     help="N>1 placement: independent pictures per GPU, or slice bands of shared pictures "
                          "(default: slices for configs 4/5, replicas for 2/3)")
@@ -231,6 +396,16 @@ def main() -> int:
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    if args.chain:
+        if args.chain % 2 or not 2 <= args.chain <= 60:
+            raise SystemExit("--chain takes an even number of chains, 2..60")
+        out = chain_bench(args, rank, world, local, cs, rehearse)
+        if rank == 0:
+            print(json.dumps(out))
+        if world > 1:
+            dist.destroy_process_group()
+        return 0
 
     L = h264r.lib()
     W, H = CONFIG_SIZE[args.config]
@@ -400,9 +575,8 @@ def main() -> int:
     # batch), divided by the sequence's device time (HIP events around the whole launch
     # sequence on its stream, averaged over the timed steps)
     achieved = step_bytes / (kern[3] * 1e-3) / 1e9 if kern[3] > 0 else 0.0
-    # per-kernel split: the same 8(d) bytes attributed to the kernel that reads / writes
-    # them (inter/PCM MBs -> k_inter4, intra MBs -> intra kernels, every final sample
-    # read + written once -> k_deblock), over that kernel's own event time
+    # per-kernel split of the same 8(d) bytes (kernel_bytes: R to the reconstructing kernel,
+    # W to deblocking; the parts add up to the path's bytes), over each kernel's own event time
     kbytes = [int(k * (band[1] - band[0]) / H) for k in kbytes_all]
     # the library deblocks batches of >= H264R_DEBLOCK2_MIN pictures (default 192) with
     # k_deblock2, smaller ones with k_deblock (include/h264r.h)

@@ -73,6 +73,23 @@ def _worker(rank, world, port, q):
             D.allgather_into_slot(send, dst, bands2, rank, 16, Wb)
             exp = torch.tensor([(y * 7 + 1) % 251 for y in range(Hs * 16)], dtype=torch.uint8).repeat_interleave(Wb)
             ok_slot.append(bool(torch.equal(dst[: Hs * 16 * Wb], exp)) and bool((dst[-64:] == 0xEE).all()))
+        # chain mode: K pictures' bands in one all-gather, landed in K chain slots
+        ok_chain = []
+        for starts, Hs in (([0, 2, 4], 6), ([0, 3], 5)):
+            bands3 = D.slice_bands(starts, Hs, world)
+            K, Wb = 3, W * 16
+            plane = Hs * 16 * Wb
+            stride = plane + 64
+            out = torch.zeros(K * plane, dtype=torch.uint8)
+            a0, a1 = bands3[rank]
+            full = torch.stack([torch.tensor([(k * 31 + y * 7 + 1) % 251 for y in range(Hs * 16)],
+                                             dtype=torch.uint8).repeat_interleave(Wb) for k in range(K)])
+            out.view(K, plane)[:, a0 * 16 * Wb:a1 * 16 * Wb] = full[:, a0 * 16 * Wb:a1 * 16 * Wb]
+            slots = torch.full((K * stride,), 0xEE, dtype=torch.uint8)
+            D.chain_exchange(out, slots, bands3, rank, plane, stride, 16, Wb)
+            got = slots.view(K, stride)
+            ok_chain.append(bool(torch.equal(got[:, :plane], full)) and bool((got[:, plane:] == 0xEE).all()))
+        ok_slot.append(all(ok_chain))
         t = D.max_over_ranks(1.0 + rank)
         share = list(D.picture_share(rank, world, 3))
         q.put((rank, all(ok_slot), t, share))
@@ -94,3 +111,18 @@ def test_gloo_world2_allgather_and_max():
     assert [r[1] for r in res] == [True, True]
     assert [r[2] for r in res] == [2.0, 2.0]           # the slowest rank's time on every rank
     assert res[0][3] == [0, 1, 2] and res[1][3] == [3, 4, 5]
+
+
+def test_chain_slots():
+    import numpy as np
+    from h264r import _abi as A
+    sl = np.zeros(2, A.SLICE_DTYPE)
+    sl["ref_slot"][:] = -1
+    sl["ref_slot"][0, 0, :3] = [0, 1, 2]
+    sl["ref_slot"][0, 1, :2] = [1, 0]
+    out = D.chain_slots(sl, 5, 8)
+    assert out["ref_slot"][0, 0, :4].tolist() == [5, 8, 9, -1]
+    assert out["ref_slot"][0, 1, :3].tolist() == [8, 5, -1]
+    assert (sl["ref_slot"][0, 0, :3] == [0, 1, 2]).all()          # input untouched
+    with pytest.raises(ValueError):
+        D.chain_slots(sl, 0, 31)
