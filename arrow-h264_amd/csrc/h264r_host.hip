@@ -94,6 +94,26 @@ int dev_resize(T** p, size_t* cap, size_t n)
 
 }  // namespace
 
+// Per-batch scratch of one launch sequence (a context has one per pipeline stage,
+// h264r_decode_batch's sub-batches).
+struct Scratch {
+    uint8_t* d_dbinfo = nullptr; size_t c_dbinfo = 0;
+    int* d_sync = nullptr; size_t c_sync = 0;
+    uint8_t* d_hb = nullptr; size_t c_hb = 0;
+    uint32_t epoch = 0;             // tag of the deblocking hand-off records of the last launch
+    uint8_t* d_hb2 = nullptr; size_t c_hb2 = 0;
+    uint32_t epoch2 = 0;            // the same for k_deblock2 (< 2^20: its tags carry the row)
+    uint16_t* d_lvl = nullptr; size_t c_lvl = 0;   // intra dependency level per MB
+    uint32_t* d_list = nullptr; size_t c_list = 0; // intra MBs by level (pic * nmb + addr)
+    int* d_lcnt = nullptr; size_t c_lcnt = 0;      // [count | base | cursor] x (LEVEL_LISTS + 2)
+    void release()
+    {
+        void* bufs[] = {d_dbinfo, d_sync, d_hb, d_hb2, d_lvl, d_list, d_lcnt};
+        for (void* b : bufs) if (b) (void)hipFree(b);
+    }
+};
+constexpr int MAX_PIPES = 4;
+
 struct h264r_ctx {
     int device = 0;
     int max_w = 0, max_h = 0;
@@ -124,16 +144,10 @@ struct h264r_ctx {
     h264r_pic* d_pic = nullptr; size_t c_pic = 0;
     h264r_quant* d_quant = nullptr; size_t c_quant = 0;
     uint8_t* d_out = nullptr; size_t c_out = 0;
-    // per-batch scratch of the launch sequence
-    uint8_t* d_dbinfo = nullptr; size_t c_dbinfo = 0;
-    int* d_sync = nullptr; size_t c_sync = 0;
-    uint8_t* d_hb = nullptr; size_t c_hb = 0;
-    uint32_t epoch = 0;             // tag of the deblocking hand-off records of the last launch
-    uint8_t* d_hb2 = nullptr; size_t c_hb2 = 0;
-    uint32_t epoch2 = 0;            // the same for k_deblock2 (< 2^20: its tags carry the row)
-    uint16_t* d_lvl = nullptr; size_t c_lvl = 0;   // intra dependency level per MB
-    uint32_t* d_list = nullptr; size_t c_list = 0; // intra MBs by level (pic * nmb + addr)
-    int* d_lcnt = nullptr; size_t c_lcnt = 0;      // [count | base | cursor] x (LEVEL_LISTS + 2)
+    // per-batch scratch of the launch sequence: one per pipeline stage (sub-batch)
+    Scratch sc[MAX_PIPES];
+    hipStream_t pipe_stream[MAX_PIPES] = {};
+    hipEvent_t ev_fork = nullptr, ev_join[MAX_PIPES] = {}, ev_stage[2][MAX_PIPES] = {};
     int levels_grid = 0;                           // resident workgroups of k_intra_levels
     int nxcc = 0;                                  // XCDs of the device (k_deblock2's placement)
     // the per-batch scratch above is reused by every launch: a launch on a stream other
@@ -267,8 +281,15 @@ int h264r_destroy(h264r_ctx* c)
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (int s = 0; s < H264R_MAX_SLOTS; ++s) if (c->slot[s][0]) (void)hipFree(c->slot[s][0]);
-    void* bufs[] = {c->d_ref_planes, c->d_err, c->d_dbinfo, c->d_sync, c->d_hb, c->d_hb2, c->d_lvl, c->d_list, c->d_lcnt, c->d_mbs, c->d_levels, c->d_mv, c->d_ref, c->d_slices, c->d_pic, c->d_quant, c->d_out};
+    void* bufs[] = {c->d_ref_planes, c->d_err, c->d_mbs, c->d_levels, c->d_mv, c->d_ref, c->d_slices, c->d_pic, c->d_quant, c->d_out};
     for (void* b : bufs) if (b) (void)hipFree(b);
+    for (int k = 0; k < MAX_PIPES; ++k) {
+        c->sc[k].release();
+        if (c->pipe_stream[k]) (void)hipStreamDestroy(c->pipe_stream[k]);
+        if (c->ev_join[k]) (void)hipEventDestroy(c->ev_join[k]);
+        for (int j = 0; j < 2; ++j) if (c->ev_stage[j][k]) (void)hipEventDestroy(c->ev_stage[j][k]);
+    }
+    if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
     for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
     if (c->ev_last) (void)hipEventDestroy(c->ev_last);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -329,7 +350,7 @@ struct Timed {
     h264r_ctx* c; int kind; hipStream_t s; hipEvent_t a = nullptr;
     Timed(h264r_ctx* c_, int k, hipStream_t s_) : c(c_), kind(k), s(s_)
     {
-        if (c->timing && (a = timing_event(c))) (void)hipEventRecord(a, s);
+        if (c && c->timing && (a = timing_event(c))) (void)hipEventRecord(a, s);
     }
     ~Timed()
     {
@@ -358,7 +379,16 @@ static int level_launches()
 // deblocks (the whole picture, or a slice-aligned band: h264r_decode_batch_rows).
 // Five launches on stream s: k_inter4 (inter / PCM MBs + deblocking records), k_level +
 // k_intra_levels + k_intra_pic (intra MBs), k_deblock or k_deblock2 (by batch size).
-static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row0, int row1)
+// Pipeline hooks of one launch sequence (h264r_decode_batch's sub-batches): the inter
+// kernels of stage k start after stage k-1's (`after_inter`), its intra kernels after stage
+// k-1's intra kernels (`after_intra`: at most one grid-barrier kernel runs at a time), and it
+// records `inter_done` / `intra_done` for stage k+1.
+struct PipeHooks {
+    hipEvent_t after_inter = nullptr, after_intra = nullptr, inter_done = nullptr, intra_done = nullptr;
+};
+
+static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row0, int row1, Scratch& X,
+                      const PipeHooks& hk = PipeHooks(), bool timed_whole = true)
 {
     // H264R_DEBUG=<flags>: the deblocking-schedule flags of h264r_set_debug OR-ed into every
     // launch (measurement A/B); flags that change or skip work (H264R_DBG_NO_DEBLOCK, the
@@ -379,20 +409,16 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
     const size_t sync_n = 1 + (size_t)P * H + 5 + 9;   // + the deblocking kernels' per-XCD ticket counters, done count
     // the scratch is shared by every launch of this context: a launch on another stream
     // than the previous one waits for it first
-    if (c->last_stream && c->last_stream != s) {
-        HIP_OK(hipEventRecord(c->ev_last, c->last_stream));
-        HIP_OK(hipStreamWaitEvent(s, c->ev_last, 0));
-    }
-    c->last_stream = s;
     int st;
-    if ((st = dev_resize(&c->d_dbinfo, &c->c_dbinfo, (size_t)P * W * H * DBINFO_BYTES))) return st;
+    if ((st = dev_resize(&X.d_dbinfo, &X.c_dbinfo, (size_t)P * W * H * DBINFO_BYTES))) return st;
     static const int rows_min = [] { const char* e = getenv("H264R_DEBLOCK2_MIN"); return e ? atoi(e) : 192; }();
     const bool by_rows = (c->debug & H264R_DBG_DEBLOCK_ROWS) || (!(c->debug & H264R_DBG_DEBLOCK_MB) && P >= rows_min);
+    (void)rows_min;
     // hand-off records of the chosen deblocking kernel; fresh memory or a wrapping epoch
     // restarts from zeroed records, so no record may carry a live tag
-    uint8_t** hb = by_rows ? &c->d_hb2 : &c->d_hb;
-    size_t* hcap = by_rows ? &c->c_hb2 : &c->c_hb;
-    uint32_t* ep = by_rows ? &c->epoch2 : &c->epoch;
+    uint8_t** hb = by_rows ? &X.d_hb2 : &X.d_hb;
+    size_t* hcap = by_rows ? &X.c_hb2 : &X.c_hb;
+    uint32_t* ep = by_rows ? &X.epoch2 : &X.epoch;
     const uint32_t ep_max = by_rows ? (1u << 20) - 2 : 0xFFFFFF00u;
     {
         const size_t cap_before = *hcap;
@@ -403,7 +429,7 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
             *ep = 0;
         }
     }
-    if ((st = dev_resize(&c->d_sync, &c->c_sync, sync_n))) return st;
+    if ((st = dev_resize(&X.d_sync, &X.c_sync, sync_n))) return st;
     // H264R_DBG_WAIT_TEST: every intra-walk wait asks for progress no row reaches, under a
     // 10 ms bound -- the launch must drain and h264r_check report H264R_EDEVICE
     const bool wait_test = (c->debug & H264R_DBG_WAIT_TEST) != 0;
@@ -422,16 +448,17 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
         if (getenv("H264R_VERBOSE"))
             fprintf(stderr, "h264r: k_intra_levels occupancy %d blocks/CU, %d CUs, grid %d\n", per_cu, cus, c->levels_grid);
     }
-    if (levels && ((st = dev_resize(&c->d_lvl, &c->c_lvl, (size_t)P * W * H)) ||
-                   (st = dev_resize(&c->d_list, &c->c_list, (size_t)P * W * H)) ||
-                   (st = dev_resize(&c->d_lcnt, &c->c_lcnt, 3 * (size_t)(LEVEL_LISTS + 2)))))
+    if (levels && ((st = dev_resize(&X.d_lvl, &X.c_lvl, (size_t)P * W * H)) ||
+                   (st = dev_resize(&X.d_list, &X.c_list, (size_t)P * W * H)) ||
+                   (st = dev_resize(&X.d_lcnt, &X.c_lcnt, 3 * (size_t)(LEVEL_LISTS + 2)))))
         return st;
-    if (levels) HIP_OK(hipMemsetAsync(c->d_lcnt, 0, 3 * (size_t)(LEVEL_LISTS + 2) * sizeof(int), s));
-    HIP_OK(hipMemsetAsync(c->d_sync, 0, sync_n * sizeof(int), s));
-    h264r::DbInfo* dbinfo = reinterpret_cast<h264r::DbInfo*>(c->d_dbinfo);
-    int* sync = c->d_sync;
-    Timed whole(c, 3, s);
-    if (c->timing) c->timed_launches++;
+    if (levels) HIP_OK(hipMemsetAsync(X.d_lcnt, 0, 3 * (size_t)(LEVEL_LISTS + 2) * sizeof(int), s));
+    HIP_OK(hipMemsetAsync(X.d_sync, 0, sync_n * sizeof(int), s));
+    h264r::DbInfo* dbinfo = reinterpret_cast<h264r::DbInfo*>(X.d_dbinfo);
+    int* sync = X.d_sync;
+    Timed whole(timed_whole ? c : nullptr, 3, s);
+    if (c->timing && timed_whole) c->timed_launches++;
+    if (hk.after_inter) HIP_OK(hipStreamWaitEvent(s, hk.after_inter, 0));
     {
         Timed t(c, 0, s);
         int* sp_flag = sync + 1 + (size_t)P * H + 4;
@@ -442,13 +469,15 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
         hipLaunchKernelGGL(k_inter_sp, dim3(1024), dim3(256), 0, s, b, rows, (const int*)sp_flag);
         HIP_OK(hipGetLastError());
     }
+    if (hk.inter_done) HIP_OK(hipEventRecord(hk.inter_done, s));
+    if (hk.after_intra) HIP_OK(hipStreamWaitEvent(s, hk.after_intra, 0));
     {
         Timed t(c, 1, s);
-        uint16_t* lvl = levels ? c->d_lvl : nullptr;
+        uint16_t* lvl = levels ? X.d_lvl : nullptr;
         const int lmax = levels ? level_launches() : 0;
         if (levels) {
             int* lvsync = sync + 1 + (size_t)P * H + 2;
-            int* lcount = c->d_lcnt;
+            int* lcount = X.d_lcnt;
             int* lbase = lcount + (LEVEL_LISTS + 2);
             int* lcursor = lbase + (LEVEL_LISTS + 2);
             hipLaunchKernelGGL(k_level, dim3(P), dim3(64 * ((HB + 63) / 64)), 0, s, b, lvl, lvsync, lcount, rows);
@@ -456,7 +485,7 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
             hipLaunchKernelGGL(k_level_scan, dim3(1), dim3(1024), 0, s, (const int*)lcount, lbase);
             HIP_OK(hipGetLastError());
             hipLaunchKernelGGL(k_level_scatter, dim3(P), dim3(1024), 0, s, b, (const uint16_t*)lvl, (const int*)lbase,
-                               lcursor, c->d_list, rows);
+                               lcursor, X.d_list, rows);
             HIP_OK(hipGetLastError());
             // a cooperative launch (the runtime checks that the whole grid is resident at
             // once, or refuses it: the grid barrier's contract, include/h264r.h), the grid
@@ -472,7 +501,7 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
             if (coop) {
                 const int* lcount_c = lcount;
                 const int* lbase_c = lbase;
-                const uint32_t* list_c = c->d_list;
+                const uint32_t* list_c = X.d_list;
                 int lmax_v = lmax;
                 int* err_p = c->d_err;
                 void* args[] = {(void*)&b, (void*)&lcount_c, (void*)&lbase_c, (void*)&list_c, (void*)&lmax_v,
@@ -481,7 +510,7 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
                                                   dim3(256), args, 0, s));
             } else {
                 hipLaunchKernelGGL(k_intra_levels, dim3(lgrid), dim3(256), 0, s, b, (const int*)lcount,
-                                   (const int*)lbase, (const uint32_t*)c->d_list, lmax, lvsync, c->d_err);
+                                   (const int*)lbase, (const uint32_t*)X.d_list, lmax, lvsync, c->d_err);
                 HIP_OK(hipGetLastError());
             }
         }
@@ -493,6 +522,7 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
                            (const uint16_t*)lvl, lmax, rows, gstep);
         HIP_OK(hipGetLastError());
     }
+    if (hk.intra_done) HIP_OK(hipEventRecord(hk.intra_done, s));
     if (!(c->debug & H264R_DBG_NO_DEBLOCK)) {
         Timed t(c, 2, s);
         if (!c->nxcc) {                  // XCDs of the device: the deblocking kernels' placement
@@ -507,7 +537,7 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
             const int nx = grid >= 64 * c->nxcc && !(c->debug & H264R_DBG_DEBLOCK_GLOBAL) ? c->nxcc : 1;
             grid = (grid + nx - 1) / nx * nx;
             hipLaunchKernelGGL(k_deblock2, dim3(grid), dim3(64), 0, s, b, dbinfo,
-                               reinterpret_cast<uint64_t*>(c->d_hb2), sync + 1 + (size_t)P * H + 5, c->d_err, ++c->epoch2, rows,
+                               reinterpret_cast<uint64_t*>(X.d_hb2), sync + 1 + (size_t)P * H + 5, c->d_err, ++X.epoch2, rows,
                                nx);
         }
         else {
@@ -516,11 +546,82 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
             const int nx = c->nxcc > 1 && !(c->debug & H264R_DBG_DEBLOCK_GLOBAL) ? c->nxcc : 1;
             const int grid = nx * ((P + nx - 1) / nx) * npairs;
             hipLaunchKernelGGL(k_deblock, dim3(grid), dim3(64), 0, s, b, dbinfo,
-                               reinterpret_cast<uint64_t*>(c->d_hb), sync + 1 + (size_t)P * H + 5, c->d_err, ++c->epoch, rows,
+                               reinterpret_cast<uint64_t*>(X.d_hb), sync + 1 + (size_t)P * H + 5, c->d_err, ++X.epoch, rows,
                                nx);
         }
         HIP_OK(hipGetLastError());
     }
+    return H264R_OK;
+}
+
+// h264r_decode_batch's pipeline: a batch of >= 2 x H264R_PIPE_MIN pictures (default 256) is
+// cut into H264R_PIPES sub-batches (default 2, at most MAX_PIPES) launched on the context's
+// pipeline streams, so that one sub-batch's latency-bound kernels (the intra walk, the
+// deblocking row walk, whose waves mostly wait on the row above) share the CUs with the next
+// sub-batch's fully parallel k_inter4: stage k's inter kernels start after stage k-1's, its
+// intra kernels after stage k-1's (never two grid-barrier kernels at once), deblocking
+// whenever its own intra kernels are done.  The caller's stream forks into the stages and
+// joins them; the results are those of one launch sequence over the whole batch.
+static int pipe_count(int P)
+{
+    static const int pipes = [] { const char* e = getenv("H264R_PIPES"); return e ? atoi(e) : 2; }();
+    static const int pmin = [] { const char* e = getenv("H264R_PIPE_MIN"); return e ? atoi(e) : 256; }();
+    return std::max(1, std::min(std::min(pipes, MAX_PIPES), P / std::max(1, pmin)));
+}
+
+static h264r_batch sub_batch(const h264r_batch& b, int p0, int p1)
+{
+    const size_t nmb = (size_t)b.width_mbs * b.height_mbs;
+    h264r_batch x = b;
+    x.num_pics = p1 - p0;
+    x.mbs = b.mbs + (size_t)p0 * nmb;
+    x.mv = b.mv + (size_t)p0 * 32 * nmb;
+    x.ref_idx = b.ref_idx + (size_t)p0 * 32 * nmb;
+    x.slices = b.slices + (size_t)p0 * b.slice_stride;
+    x.pics = b.pics + p0;
+    x.quant = b.quant + p0;
+    x.out_y = b.out_y + (size_t)p0 * 256 * nmb;
+    x.out_u = b.out_u + (size_t)p0 * 64 * nmb;
+    x.out_v = b.out_v + (size_t)p0 * 64 * nmb;
+    return x;
+}
+
+static int run_batch(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row0, int row1)
+{
+    // the scratch is shared by every launch of this context: a launch on another stream
+    // than the previous one waits for it first
+    if (c->last_stream && c->last_stream != s) {
+        HIP_OK(hipEventRecord(c->ev_last, c->last_stream));
+        HIP_OK(hipStreamWaitEvent(s, c->ev_last, 0));
+    }
+    c->last_stream = s;
+    const int n = pipe_count(b.num_pics);
+    if (n == 1) return launch_all(c, b, s, row0, row1, c->sc[0]);
+    if (!c->ev_fork) {
+        HIP_OK(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
+        for (int k = 0; k < MAX_PIPES; ++k) {
+            HIP_OK(hipStreamCreateWithFlags(&c->pipe_stream[k], hipStreamNonBlocking));
+            HIP_OK(hipEventCreateWithFlags(&c->ev_join[k], hipEventDisableTiming));
+            for (int j = 0; j < 2; ++j) HIP_OK(hipEventCreateWithFlags(&c->ev_stage[j][k], hipEventDisableTiming));
+        }
+    }
+    Timed whole(c, 3, s);
+    if (c->timing) c->timed_launches++;
+    HIP_OK(hipEventRecord(c->ev_fork, s));
+    for (int k = 0; k < n; ++k) {
+        const int p0 = (int)((long long)b.num_pics * k / n), p1 = (int)((long long)b.num_pics * (k + 1) / n);
+        hipStream_t sk = c->pipe_stream[k];
+        HIP_OK(hipStreamWaitEvent(sk, c->ev_fork, 0));
+        PipeHooks hk;
+        hk.after_inter = k ? c->ev_stage[0][k - 1] : nullptr;
+        hk.after_intra = k ? c->ev_stage[1][k - 1] : nullptr;
+        hk.inter_done = c->ev_stage[0][k];
+        hk.intra_done = c->ev_stage[1][k];
+        int st = launch_all(c, sub_batch(b, p0, p1), sk, row0, row1, c->sc[k], hk, false);
+        if (st) return st;
+        HIP_OK(hipEventRecord(c->ev_join[k], sk));
+    }
+    for (int k = 0; k < n; ++k) HIP_OK(hipStreamWaitEvent(s, c->ev_join[k], 0));
     return H264R_OK;
 }
 
@@ -552,11 +653,11 @@ int h264r_decode_batch(h264r_ctx* c, const h264r_batch* b, void* stream)
     if (!bb.ref_planes) bb.ref_planes = c->d_ref_planes;
     hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : c->stream;
 #ifdef H264R_TRACE
-    int st = launch_all(c, bb, s, 0, bb.height_mbs);
+    int st = run_batch(c, bb, s, 0, bb.height_mbs);
     dump_trace(s);
     return st;
 #else
-    return launch_all(c, bb, s, 0, bb.height_mbs);
+    return run_batch(c, bb, s, 0, bb.height_mbs);
 #endif
 }
 
@@ -571,7 +672,7 @@ int h264r_decode_batch_rows(h264r_ctx* c, const h264r_batch* b, int row0, int ro
     h264r_batch bb = *b;
     if (!bb.ref_planes) bb.ref_planes = c->d_ref_planes;
     hipStream_t s = stream ? reinterpret_cast<hipStream_t>(stream) : c->stream;
-    return launch_all(c, bb, s, row0, row1);
+    return run_batch(c, bb, s, row0, row1);
 }
 
 int h264r_set_timing(h264r_ctx* c, int enable)
@@ -709,7 +810,7 @@ int h264r_picture_end(h264r_ctx* c, uint8_t* y, uint8_t* u, uint8_t* v, int keep
     b.mbs = c->d_mbs; b.levels = c->d_levels; b.mv = c->d_mv; b.ref_idx = c->d_ref; b.slices = c->d_slices;
     b.pics = c->d_pic; b.quant = c->d_quant; b.ref_planes = c->d_ref_planes;
     b.out_y = c->d_out; b.out_u = c->d_out + ys; b.out_v = c->d_out + ys + cs;
-    if ((st = launch_all(c, b, s, 0, b.height_mbs))) return st;
+    if ((st = run_batch(c, b, s, 0, b.height_mbs))) return st;
     if (keep_slot >= 0) {
         if ((st = ensure_slot(c, keep_slot, c->pw, c->ph))) return st;
         HIP_OK(hipMemcpyAsync(c->slot[keep_slot][0], c->d_out, ys + 2 * cs, hipMemcpyDeviceToDevice, s));

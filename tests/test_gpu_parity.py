@@ -141,6 +141,14 @@ def test_gpu_large_batch_wide_rows(L, dec, cidx):
     _large_batch_vs_oracle(L, dec, cidx, 120, 32, 256)
 
 
+@pytest.mark.parametrize("cidx", [2, 3, 4])
+def test_gpu_pipelined_sub_batches(L, dec, cidx):
+    """A batch of >= 2 x H264R_PIPE_MIN pictures (1100 CIF pictures) runs as sub-batches on
+    the context's pipeline streams (h264r_host.hip run_batch: inter / intra / deblocking of
+    consecutive sub-batches overlapping); every picture checked."""
+    _large_batch_vs_oracle(L, dec, cidx, 22, 18, 1100)
+
+
 @pytest.mark.parametrize("cidx", [2, 3])
 def test_gpu_large_batch_xcd_groups(L, dec, cidx):
     """464 CIF pictures (29 groups of 16 x 18 MB rows = 522 k_deblock2 waves): k_deblock2 in
