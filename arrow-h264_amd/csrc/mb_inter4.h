@@ -483,6 +483,8 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
         // ---- prediction
         const int r0 = (int8_t)(m0.y & 255), r1 = (int8_t)(m1.y & 255);
         const int dir = (r0 >= 0 && r1 >= 0) ? 2 : (r0 >= 0 ? 0 : 1);
+        // the prediction of each list in named registers: an array indexed by the (not
+        // unrolled) list loop was promoted to LDS by the compiler (48 B per lane)
         uint32_t pY[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}}, pC[2][2] = {{0, 0}, {0, 0}};
     #pragma unroll 1
         for (int l = 0; l < 2; ++l) {
@@ -490,25 +492,35 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
             const int rr = l ? r1 : r0;
             const bool use = rr >= 0;
             if (!__any(use)) continue;                                  // P pictures: list 1 never
-            if (!use) continue;
-            const int slot = (int8_t)((mw.y >> 8) & 255);
-            const bool ok = slot >= 0 && slot < H264R_MAX_SLOTS && rr < H264R_MAX_REFS && S.planes[slot * 3];
-            const int mvx = (int16_t)(mw.x & 0xFFFF), mvy = (int16_t)(mw.x >> 16);
-            const int vx = X4 * 16 + mvx, vy = Y4 * 16 + mvy;           // quarter luma / eighth chroma units
-            if (!ok) {                                                   // no_ref: 128 (inter_prediction.cc:164-167,366-369)
-    #pragma unroll
-                for (int i = 0; i < 4; ++i) pY[l][i] = 0x80808080u;
-                pC[l][0] = pC[l][1] = 0x80808080u;
-                continue;
-            }
+            uint32_t tY[4] = {0x80808080u, 0x80808080u, 0x80808080u, 0x80808080u};
+            uint32_t tC[2] = {0x80808080u, 0x80808080u};                // no_ref: 128 (inter_prediction.cc:164-167,366-369)
+            if (use) {
+                const int slot = (int8_t)((mw.y >> 8) & 255);
+                const bool ok = slot >= 0 && slot < H264R_MAX_SLOTS && rr < H264R_MAX_REFS && S.planes[slot * 3];
+                const int mvx = (int16_t)(mw.x & 0xFFFF), mvy = (int16_t)(mw.x >> 16);
+                const int vx = X4 * 16 + mvx, vy = Y4 * 16 + mvy;       // quarter luma / eighth chroma units
+                if (ok) {
 #ifndef H264R_EXP_NO_LUMA           // (measurement-only knobs: tools/exp_sweep.sh ablations)
-            luma_block_pred(S.planes[slot * 3], g.W, g.H, vx >> 2, vy >> 2, vx & 3, vy & 3, pY[l]);
+                    luma_block_pred(S.planes[slot * 3], g.W, g.H, vx >> 2, vy >> 2, vx & 3, vy & 3, tY);
 #endif
 #ifndef H264R_EXP_NO_CHROMA
     #pragma unroll
-            for (int pl = 0; pl < 2; ++pl)
-                pC[l][pl] = chroma_block_pred(S.planes[slot * 3 + 1 + pl], g.Wc, g.Hc, vx >> 3, vy >> 3, vx & 7, vy & 7);
+                    for (int pl = 0; pl < 2; ++pl)
+                        tC[pl] = chroma_block_pred(S.planes[slot * 3 + 1 + pl], g.Wc, g.Hc, vx >> 3, vy >> 3, vx & 7, vy & 7);
 #endif
+                }
+            }
+            const bool l1 = l != 0;
+    #pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                pY[0][i] = (use && !l1) ? tY[i] : pY[0][i];
+                pY[1][i] = (use && l1) ? tY[i] : pY[1][i];
+            }
+    #pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                pC[0][k] = (use && !l1) ? tC[k] : pC[0][k];
+                pC[1][k] = (use && l1) ? tC[k] : pC[1][k];
+            }
         }
         uint32_t predY[4], predC[2];
         WpPar wpp[3] = {};
@@ -760,8 +772,11 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
                         in[4 + c] = (bx & 1) ? d[i][c] : ov;
                     }
                     idct8(in, outv);
+                    // mask select: a ternary over the two halves became a lane-indexed array
+                    // read, which the compiler placed in LDS (32 B per lane)
+                    const int mx = -(bx & 1);
     #pragma unroll
-                    for (int c = 0; c < 4; ++c) e4[i][c] = (bx & 1) ? outv[4 + c] : outv[c];
+                    for (int c = 0; c < 4; ++c) e4[i][c] = (outv[c] & ~mx) | (outv[4 + c] & mx);
                 }
     #pragma unroll
                 for (int c = 0; c < 4; ++c) {
@@ -773,8 +788,9 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
                         in[4 + i] = (by & 1) ? e4[i][c] : ov;
                     }
                     idct8(in, outv);
+                    const int my = -(by & 1);
     #pragma unroll
-                    for (int i = 0; i < 4; ++i) res[i][c] = t8 ? ((by & 1) ? outv[4 + i] : outv[i]) : 0;
+                    for (int i = 0; i < 4; ++i) res[i][c] = t8 ? ((outv[i] & ~my) | (outv[4 + i] & my)) : 0;
                 }
                 if (!t8) {
     #pragma unroll
