@@ -27,22 +27,23 @@
 #endif
 
 namespace h264r { struct DbInfo; }
-extern "C" __global__ void k_inter4(h264r_batch b, h264r::DbInfo* dbinfo, int2 rows, int* sp_flag);
-extern "C" __global__ void k_inter_sp(h264r_batch b, int2 rows, const int* sp_flag);
+extern "C" __global__ void k_inter4(h264r_batch b, h264r::DbInfo* dbinfo, int2 rows, int* sp_flag, uint8_t* recon);
+extern "C" __global__ void k_inter_sp(h264r_batch b, int2 rows, const int* sp_flag, uint8_t* recon);
+extern "C" __global__ void k_untile(h264r_batch b, int2 rows, const uint8_t* recon);
 extern "C" __global__ void k_intra_pic(h264r_batch b, int* sync, int* err, const uint16_t* lvl, int lmax, int2 rows,
-                                      int gstep);
+                                      int gstep, uint8_t* recon);
 extern "C" __global__ void k_level(h264r_batch b, uint16_t* lvl, int* lvsync, int* lcount, int2 rows);
 extern "C" __global__ void k_level_scan(const int* lcount, int* lbase);
 extern "C" __global__ void k_level_scatter(h264r_batch b, const uint16_t* lvl, const int* lbase, int* lcursor,
                                            uint32_t* list, int2 rows);
 extern "C" __global__ void k_intra_levels(h264r_batch b, const int* lcount, const int* lbase, const uint32_t* list,
-                                          int lmax, int* lvsync, int* err);
+                                          int lmax, int* lvsync, int* err, uint8_t* recon);
 constexpr int LEVEL_MAX_MBS = 65536;      // k_level's LDS bitmap (k_picture.hip)
 constexpr int LEVEL_LISTS = 64;           // levels with MB lists (H264R_LEVEL_LISTS, k_picture.hip)
 extern "C" __global__ void k_deblock(h264r_batch b, const h264r::DbInfo* dbinfo, uint64_t* hb,
-                                     int* sync, int* err, uint32_t epoch, int2 rows, int nx);
+                                     int* sync, int* err, uint32_t epoch, int2 rows, int nx, uint8_t* recon);
 extern "C" __global__ void k_deblock2(h264r_batch b, const h264r::DbInfo* dbinfo, uint64_t* hb,
-                                      int* sync, int* err, uint32_t epoch, int2 rows, int nx);
+                                      int* sync, int* err, uint32_t epoch, int2 rows, int nx, const uint8_t* recon);
 constexpr size_t DBINFO_BYTES = 80;
 constexpr size_t HANDOFF_BYTES = 256;   // one tagged record (32 x {dword, epoch}) per MB
 constexpr size_t HANDOFF2_BYTES = 384;  // k_deblock2: 2 row slots x 24 x {dword, tag} per MB column
@@ -106,9 +107,10 @@ struct Scratch {
     uint16_t* d_lvl = nullptr; size_t c_lvl = 0;   // intra dependency level per MB
     uint32_t* d_list = nullptr; size_t c_list = 0; // intra MBs by level (pic * nmb + addr)
     int* d_lcnt = nullptr; size_t c_lcnt = 0;      // [count | base | cursor] x (LEVEL_LISTS + 2)
+    uint8_t* d_recon = nullptr; size_t c_recon = 0; // MB-tiled reconstruction, 384 B per (picture, MB)
     void release()
     {
-        void* bufs[] = {d_dbinfo, d_sync, d_hb, d_hb2, d_lvl, d_list, d_lcnt};
+        void* bufs[] = {d_dbinfo, d_sync, d_hb, d_hb2, d_lvl, d_list, d_lcnt, d_recon};
         for (void* b : bufs) if (b) (void)hipFree(b);
     }
 };
@@ -411,6 +413,10 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
     // than the previous one waits for it first
     int st;
     if ((st = dev_resize(&X.d_dbinfo, &X.c_dbinfo, (size_t)P * W * H * DBINFO_BYTES))) return st;
+    // the reconstruction kernels write the MB-tiled samples (device_common.h), the
+    // deblocking kernel (or k_untile) turns them into the output planes
+    if ((st = dev_resize(&X.d_recon, &X.c_recon, (size_t)P * W * H * 384))) return st;
+    uint8_t* recon = X.d_recon;
     static const int rows_min = [] { const char* e = getenv("H264R_DEBLOCK2_MIN"); return e ? atoi(e) : 192; }();
     const bool by_rows = (c->debug & H264R_DBG_DEBLOCK_ROWS) || (!(c->debug & H264R_DBG_DEBLOCK_MB) && P >= rows_min);
     (void)rows_min;
@@ -463,10 +469,10 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
         Timed t(c, 0, s);
         int* sp_flag = sync + 1 + (size_t)P * H + 4;
         const int groups = (W * HB + 15) / 16;
-        hipLaunchKernelGGL(k_inter4, dim3(8 * ((groups + 7) / 8), P), dim3(256), 0, s, b, dbinfo, rows, sp_flag);
+        hipLaunchKernelGGL(k_inter4, dim3(8 * ((groups + 7) / 8), P), dim3(256), 0, s, b, dbinfo, rows, sp_flag, recon);
         HIP_OK(hipGetLastError());
         // inter MBs of SP slices (a short launch when the batch has none)
-        hipLaunchKernelGGL(k_inter_sp, dim3(1024), dim3(256), 0, s, b, rows, (const int*)sp_flag);
+        hipLaunchKernelGGL(k_inter_sp, dim3(1024), dim3(256), 0, s, b, rows, (const int*)sp_flag, recon);
         HIP_OK(hipGetLastError());
     }
     if (hk.inter_done) HIP_OK(hipEventRecord(hk.inter_done, s));
@@ -505,12 +511,12 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
                 int lmax_v = lmax;
                 int* err_p = c->d_err;
                 void* args[] = {(void*)&b, (void*)&lcount_c, (void*)&lbase_c, (void*)&list_c, (void*)&lmax_v,
-                                (void*)&lvsync, (void*)&err_p};
+                                (void*)&lvsync, (void*)&err_p, (void*)&recon};
                 HIP_OK(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(k_intra_levels), dim3(lgrid),
                                                   dim3(256), args, 0, s));
             } else {
                 hipLaunchKernelGGL(k_intra_levels, dim3(lgrid), dim3(256), 0, s, b, (const int*)lcount,
-                                   (const int*)lbase, (const uint32_t*)X.d_list, lmax, lvsync, c->d_err);
+                                   (const int*)lbase, (const uint32_t*)X.d_list, lmax, lvsync, c->d_err, recon);
                 HIP_OK(hipGetLastError());
             }
         }
@@ -519,7 +525,7 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
         static const int gstep_env = [] { const char* e = getenv("H264R_WALK_GSTEP"); return e ? atoi(e) : 0; }();
         const int gstep = wait_test ? -1 : gstep_env > 0 ? gstep_env : (P >= 128 ? 64 : 1);
         hipLaunchKernelGGL(k_intra_pic, dim3(P * nbands), dim3(64 * H264R_WALK_ROWS), 0, s, b, sync, c->d_err,
-                           (const uint16_t*)lvl, lmax, rows, gstep);
+                           (const uint16_t*)lvl, lmax, rows, gstep, recon);
         HIP_OK(hipGetLastError());
     }
     if (hk.intra_done) HIP_OK(hipEventRecord(hk.intra_done, s));
@@ -538,7 +544,7 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
             grid = (grid + nx - 1) / nx * nx;
             hipLaunchKernelGGL(k_deblock2, dim3(grid), dim3(64), 0, s, b, dbinfo,
                                reinterpret_cast<uint64_t*>(X.d_hb2), sync + 1 + (size_t)P * H + 5, c->d_err, ++X.epoch2, rows,
-                               nx);
+                               nx, (const uint8_t*)recon);
         }
         else {
             // k_deblock keeps a picture's pairs on one XCD (p % nx): nx times the largest
@@ -547,25 +553,33 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
             const int grid = nx * ((P + nx - 1) / nx) * npairs;
             hipLaunchKernelGGL(k_deblock, dim3(grid), dim3(64), 0, s, b, dbinfo,
                                reinterpret_cast<uint64_t*>(X.d_hb), sync + 1 + (size_t)P * H + 5, c->d_err, ++X.epoch, rows,
-                               nx);
+                               nx, recon);
         }
+        HIP_OK(hipGetLastError());
+    } else {
+        hipLaunchKernelGGL(k_untile, dim3((W * HB * 32 + 255) / 256, P), dim3(256), 0, s, b, rows, (const uint8_t*)recon);
         HIP_OK(hipGetLastError());
     }
     return H264R_OK;
 }
 
-// h264r_decode_batch's pipeline: a batch of >= 2 x H264R_PIPE_MIN pictures (default 256) is
-// cut into H264R_PIPES sub-batches (default 2, at most MAX_PIPES) launched on the context's
-// pipeline streams, so that one sub-batch's latency-bound kernels (the intra walk, the
-// deblocking row walk, whose waves mostly wait on the row above) share the CUs with the next
-// sub-batch's fully parallel k_inter4: stage k's inter kernels start after stage k-1's, its
-// intra kernels after stage k-1's (never two grid-barrier kernels at once), deblocking
-// whenever its own intra kernels are done.  The caller's stream forks into the stages and
-// joins them; the results are those of one launch sequence over the whole batch.
+// h264r_decode_batch's pipeline (opt-in): with H264R_PIPES = n > 1, a batch of >= 2 x
+// H264R_PIPE_MIN pictures (default 256) is cut into n sub-batches (at most MAX_PIPES)
+// launched on the context's pipeline streams, so that one sub-batch's latency-bound kernels
+// (the intra walk, the deblocking row walk) could share the CUs with the next sub-batch's
+// fully parallel k_inter4: stage k's inter kernels start after stage k-1's, its intra
+// kernels after stage k-1's (never two grid-barrier kernels at once), deblocking whenever
+// its own intra kernels are done.  The caller's stream forks into the stages and joins
+// them; the results are those of one launch sequence over the whole batch.  Default 1:
+// measured on MI355X (profiles/r03_pipes.txt) every depth > 1 is slower -- config 3 at
+// batch 1024 406.8 -> 372.5 / 352.1 / 336.4 Mmb/s at 2 / 3 / 4 sub-batches, config 4
+// unchanged -- each kernel already fills the chip, and the overlap only adds contention.
+// Read per call (tests switch it).
 static int pipe_count(int P)
 {
-    static const int pipes = [] { const char* e = getenv("H264R_PIPES"); return e ? atoi(e) : 2; }();
-    static const int pmin = [] { const char* e = getenv("H264R_PIPE_MIN"); return e ? atoi(e) : 256; }();
+    const char* e = getenv("H264R_PIPES");
+    const char* m = getenv("H264R_PIPE_MIN");
+    const int pipes = e ? atoi(e) : 1, pmin = m ? atoi(m) : 256;
     return std::max(1, std::min(std::min(pipes, MAX_PIPES), P / std::max(1, pmin)));
 }
 

@@ -89,7 +89,7 @@ extern "C" void h264r_db_trace_copy(void* dst) { (void)hipMemcpyFromSymbol(dst, 
 // share, so each XCD's pairs all run at once whatever the round-robin start.
 extern "C" __global__ __launch_bounds__(64, H264R_DB_WAVES) void k_deblock(h264r_batch b, const DbInfo* __restrict__ dbinfo,
                                                           uint64_t* hb, int* sync, int* err, uint32_t epoch, int2 rows,
-                                                          int nx)
+                                                          int nx, uint8_t* recon)
 {
     __shared__ PairLds L;
     const Geom g = make_geom(b.width_mbs, b.height_mbs);
@@ -201,14 +201,15 @@ extern "C" __global__ __launch_bounds__(64, H264R_DB_WAVES) void k_deblock(h264r
     bool ok = true;
     TRACE(unsigned long long tr_wait = 0; unsigned long long tph[4] = {0, 0, 0, 0}; unsigned long long tm = 0;)
 
-    // The body loads of step t (this half's MB t - h): samples and deblocking record.
+    // The body loads of step t (this half's MB t - h): samples (the MB-tiled reconstruction,
+    // device_common.h) and deblocking record.
     auto prefetch = [&](int t) {
         const int x = t - h;
         if (half_on && x >= 0 && x < W) {
-            const uint8_t* yb = Y + (size_t)(Y0 + by0) * g.W + x * 16 + 4 * bd0;
-            pf_y0 = *reinterpret_cast<const uint32_t*>(yb);
-            pf_y1 = *reinterpret_cast<const uint32_t*>(yb + (size_t)8 * g.W);
-            pf_c = *as_global(Cp[cpl] + (size_t)(Yc + cy) * g.Wc + x * 8 + 4 * cd);
+            const uint8_t* mb = recon_mb(recon, g, pic, r * W + x);
+            pf_y0 = load_global<uint32_t>(mb + by0 * 16 + 4 * bd0);
+            pf_y1 = load_global<uint32_t>(mb + (by0 + 8) * 16 + 4 * bd0);
+            pf_c = load_global<uint32_t>(mb + RECON_CB + cpl * 64 + cy * 8 + 4 * cd);
             if (hl < DBINFO_DWORDS) pf_i = info_row[x * DBINFO_DWORDS + hl];
         }
     };

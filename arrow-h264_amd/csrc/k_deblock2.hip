@@ -105,7 +105,8 @@ extern "C" void h264r_db2_trace_copy(void* dst) { (void)hipMemcpyFromSymbol(dst,
 #define H264R_DB2_XCD 1
 #endif
 extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_deblock2(
-    h264r_batch b, const DbInfo* __restrict__ dbinfo, uint64_t* hb, int* sync, int* err, uint32_t epoch, int2 rows, int nx)
+    h264r_batch b, const DbInfo* __restrict__ dbinfo, uint64_t* hb, int* sync, int* err, uint32_t epoch, int2 rows, int nx,
+    const uint8_t* __restrict__ recon)
 {
     __shared__ UnitLds S[UNITS];
     const Geom g = make_geom(b.width_mbs, b.height_mbs);
@@ -174,25 +175,19 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2
         return __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(hrs, pair_off(rec_in, m, q, k), 0, AUX_SC1));
     };
 
-    // ---- window fetch: MBs m, m+1 as 32-byte luma / 16-byte chroma row pieces
+    // ---- window fetch: MBs m, m+1 -- 768 contiguous bytes of the MB-tiled reconstruction
+    // (device_common.h), 16 bytes per load: luma rows 2i + p of MB m + d, and the chroma
+    // chunk k = 4i + q (MB m + k / 8, plane (k / 4) & 1, rows 2 (k & 3) and 2 (k & 3) + 1)
+    const uint8_t* rrow = recon + ((size_t)pic * g.nmb + (size_t)y * W) * RECON_MB;
     v4u wl[8], wc[4];
     auto fetch = [&](int m) {
-        const int xa = min(m + d, W - 1);
+        const uint8_t* ma = rrow + (size_t)min(m + d, W - 1) * RECON_MB;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) wl[i] = *reinterpret_cast<const v4u*>(Y + (size_t)(2 * i + p) * Wl + xa * 16);
-        if (m + 1 < W) {
+        for (int i = 0; i < 8; ++i) wl[i] = load_global<v4u>(ma + (2 * i + p) * 16);
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int pr = 4 * i + q;                                               // plane * 8 + row
-                wc[i] = *reinterpret_cast<const v4u*>((pr >> 3 ? Cr : Cb) + (size_t)(pr & 7) * Wc + m * 8);
-            }
-        } else {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int pr = 4 * i + q;
-                const v2u v = *reinterpret_cast<const v2u*>((pr >> 3 ? Cr : Cb) + (size_t)(pr & 7) * Wc + m * 8);
-                wc[i] = (v4u){v.x, v.y, 0u, 0u};
-            }
+        for (int i = 0; i < 4; ++i) {
+            const int k = 4 * i + q;
+            wc[i] = load_global<v4u>(rrow + (size_t)min(m + (k >> 3), W - 1) * RECON_MB + RECON_CB + (k & 7) * 16);
         }
     };
     auto fill = [&](int m) {                                                            // registers -> ring slots
@@ -201,9 +196,9 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2
         for (int i = 0; i < 8; ++i) *reinterpret_cast<v4u*>(&U.y[2 * i + p][4 * s]) = wl[i];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const int pr = 4 * i + q;
-            *reinterpret_cast<v2u*>(&U.c[pr >> 3][pr & 7][2 * sa]) = wc[i].xy;
-            *reinterpret_cast<v2u*>(&U.c[pr >> 3][pr & 7][2 * sb]) = wc[i].zw;
+            const int k = 4 * i + q, sk = i < 2 ? sa : sb, pl = (k >> 2) & 1, r = 2 * (k & 3);
+            *reinterpret_cast<v2u*>(&U.c[pl][r][2 * sk]) = wc[i].xy;
+            *reinterpret_cast<v2u*>(&U.c[pl][r + 1][2 * sk]) = wc[i].zw;
         }
     };
     // the fetch registers read on the paths that do not fill (the last window, a failed

@@ -72,7 +72,7 @@ DEV bool wait_for(int* counter, int need, int* err, int& seen)
 // sync: [0] ticket counter, [1 ..] per (picture, row) progress; zeroed before every launch.
 template <typename Scratch>
 DEV void walk_ticket(const h264r_batch& b, int* sync, int* err, Scratch* scratch, int* lprog, int ticket,
-                     const uint16_t* __restrict__ lvl, int lmax, int2 rows, int gstep)
+                     const uint16_t* __restrict__ lvl, int lmax, int2 rows, int gstep, uint8_t* recon)
 {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const Geom g = make_geom(b.width_mbs, b.height_mbs);
@@ -141,7 +141,7 @@ DEV void walk_ticket(const h264r_batch& b, int* sync, int* err, Scratch* scratch
             else ok = wait_for<false>(&lprog[wave - 1], need, err, seen);
         }
         if (!ok) break;
-        intra_mb2(b, g, pic, x, r, lane, S);
+        intra_mb2(b, g, pic, x, r, lane, S, recon);
         dirty = true;
         x = next_intra(x + 1);
         publish(x, false);
@@ -152,7 +152,8 @@ DEV void walk_ticket(const h264r_batch& b, int* sync, int* err, Scratch* scratch
 // lvl / lmax: intra MBs with lvl <= lmax were reconstructed by the k_intra_lvl
 // launches before this one (lvl == nullptr: the walk does every intra MB).
 extern "C" __global__ __launch_bounds__(64 * H264R_WALK_ROWS, H264R_WALK_WAVES) void k_intra_pic(h264r_batch b, int* sync, int* err,
-                                                              const uint16_t* lvl, int lmax, int2 rows, int gstep)
+                                                              const uint16_t* lvl, int lmax, int2 rows, int gstep,
+                                                              uint8_t* recon)
 {
     __shared__ IntraScratch scratch[WAVES];
     __shared__ int lprog[WAVES];
@@ -160,7 +161,7 @@ extern "C" __global__ __launch_bounds__(64 * H264R_WALK_ROWS, H264R_WALK_WAVES) 
     if (threadIdx.x == 0) ticket = atomicAdd(&sync[0], 1);
     if (threadIdx.x < WAVES) lprog[threadIdx.x] = 0;
     __syncthreads();
-    walk_ticket(b, sync, err, scratch, lprog, ticket, lvl, lmax, rows, gstep);
+    walk_ticket(b, sync, err, scratch, lprog, ticket, lvl, lmax, rows, gstep, recon);
 }
 
 // ------------------------------------------------------------ level schedule
@@ -349,7 +350,7 @@ extern "C" __global__ void k_intra_trace_dump(unsigned long long* out, unsigned*
 extern "C" __global__ __launch_bounds__(256, H264R_LVL_WAVES) void k_intra_levels(h264r_batch b, const int* __restrict__ lcount,
                                                                                 const int* __restrict__ lbase,
                                                                                 const uint32_t* __restrict__ list,
-                                                                                int lmax, int* lvsync, int* err)
+                                                                                int lmax, int* lvsync, int* err, uint8_t* recon)
 {
     __shared__ IntraScratch scratch[4];
     const Geom g = make_geom(b.width_mbs, b.height_mbs);
@@ -366,7 +367,7 @@ extern "C" __global__ __launch_bounds__(256, H264R_LVL_WAVES) void k_intra_level
 #ifdef H264R_TRACE_INTRA
             const unsigned long long t0 = __builtin_amdgcn_s_memrealtime(), c0 = __builtin_amdgcn_s_memtime();
             unsigned long long tph[5] = {c0, c0, c0, c0, c0};
-            intra_mb2(b, g, pic, a % g.wmb, a / g.wmb, lane, scratch[wave], tph);
+            intra_mb2(b, g, pic, a % g.wmb, a / g.wmb, lane, scratch[wave], recon, tph);
             asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
             const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
             if (lane == 0) {
@@ -384,7 +385,7 @@ extern "C" __global__ __launch_bounds__(256, H264R_LVL_WAVES) void k_intra_level
                 }
             }
 #else
-            intra_mb2(b, g, pic, a % g.wmb, a / g.wmb, lane, scratch[wave]);
+            intra_mb2(b, g, pic, a % g.wmb, a / g.wmb, lane, scratch[wave], recon);
 #endif
         }
         if (L < top && !grid_barrier(&lvsync[0], L * (int)gridDim.x, err)) return;

@@ -35,9 +35,10 @@ DEV void inter4_lds(const h264r_batch& b, int pic, Inter4Lds& S)
 // compensation reads only its band of the reference pictures (+ the MV reach), which its
 // 4 MB L2 holds, instead of every XCD streaming whole references through its L2.
 extern "C" __global__ __launch_bounds__(256, H264R_INTER_WAVES) void k_inter4(h264r_batch b, DbInfo* dbinfo, int2 rows,
-                                                                             int* sp_flag)
+                                                                             int* sp_flag, uint8_t* recon)
 {
     __shared__ Inter4Lds S;
+    __shared__ QuadTile tiles[4][INTER4_TILES];
     const int pic = blockIdx.y;
     const Geom g = make_geom(b.width_mbs, b.height_mbs);
     const int groups = (g.wmb * (rows.y - rows.x) + 15) / 16, gb = (groups + 7) / 8;
@@ -50,16 +51,18 @@ extern "C" __global__ __launch_bounds__(256, H264R_INTER_WAVES) void k_inter4(h2
     inter4_lds(b, pic, S);
     __syncthreads();
     if (a0 >= aend) return;
-    inter4_mbs<false>(b, g, pic, a0, aend, lane, dbinfo + (size_t)pic * g.nmb, S, sp_flag, pre);
+    inter4_mbs<false>(b, g, pic, a0, aend, lane, dbinfo + (size_t)pic * g.nmb, S, sp_flag, pre,
+                      tiles[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)], recon);
 }
 
 // k_inter_sp: the inter MBs of SP slices (inverse_transform_sp), after k_inter4.  A
 // persistent grid that leaves at once unless k_inter4 set sp_flag (so a batch without SP
 // slices pays one short launch), then strides over (16-MB group, picture).
-extern "C" __global__ __launch_bounds__(256) void k_inter_sp(h264r_batch b, int2 rows, const int* sp_flag)
+extern "C" __global__ __launch_bounds__(256) void k_inter_sp(h264r_batch b, int2 rows, const int* sp_flag, uint8_t* recon)
 {
     if (!__hip_atomic_load(sp_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
     __shared__ Inter4Lds S;
+    __shared__ QuadTile tiles[4][INTER4_TILES];
     const Geom g = make_geom(b.width_mbs, b.height_mbs);
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int groups = (g.wmb * (rows.y - rows.x) + 15) / 16;
@@ -70,6 +73,28 @@ extern "C" __global__ __launch_bounds__(256) void k_inter_sp(h264r_batch b, int2
         inter4_lds(b, pic, S);
         __syncthreads();
         const int a0 = rows.x * g.wmb + (grp * 4 + wave) * 4;
-        if (a0 < aend) inter4_mbs<true>(b, g, pic, a0, aend, lane, nullptr, S, nullptr, inter4_pre(b, g, pic, a0, aend, lane));
+        if (a0 < aend) inter4_mbs<true>(b, g, pic, a0, aend, lane, nullptr, S, nullptr, inter4_pre(b, g, pic, a0, aend, lane),
+                                         tiles[wave], recon);
+    }
+}
+
+// k_untile: the MB-tiled reconstruction copied into the output planes as it stands (the
+// launch sequence without deblocking, H264R_DBG_NO_DEBLOCK).  One thread per luma row
+// (16 B) or chroma row (8 B) of an MB: 32 per MB.  Grid (ceil(32 * MBs / 256), pictures).
+extern "C" __global__ __launch_bounds__(256) void k_untile(h264r_batch b, int2 rows, const uint8_t* __restrict__ recon)
+{
+    const Geom g = make_geom(b.width_mbs, b.height_mbs);
+    const int pic = blockIdx.y;
+    const int t = blockIdx.x * 256 + threadIdx.x, a = rows.x * g.wmb + (t >> 5), k = t & 31;
+    if (a >= rows.y * g.wmb) return;
+    const int mbx = a % g.wmb, mby = a / g.wmb;
+    const uint8_t* mb = recon + ((size_t)pic * g.nmb + a) * RECON_MB;
+    if (k < 16) {
+        *reinterpret_cast<uint4*>(b.out_y + (size_t)pic * g.ysz + (size_t)(mby * 16 + k) * g.W + mbx * 16) =
+            *reinterpret_cast<const uint4*>(mb + k * 16);
+    } else {
+        const int pl = (k - 16) >> 3, r = k & 7;
+        uint8_t* dst = (pl ? b.out_v : b.out_u) + (size_t)pic * g.csz + (size_t)(mby * 8 + r) * g.Wc + mbx * 8;
+        *reinterpret_cast<uint2*>(dst) = *reinterpret_cast<const uint2*>(mb + RECON_CB + pl * 64 + r * 8);
     }
 }

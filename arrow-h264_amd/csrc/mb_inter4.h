@@ -138,16 +138,36 @@ DEV s16x2 pair_at(uint32_t r0, uint32_t r1, uint32_t r2)
 // column c + 2 (+1 for xf == 3: m) accumulates in packed 16-bit.  Every output is
 // (X + Y + 1) >> 1 of two of {G, b, h, j}, chosen per lane from the phase.
 // out[i] packs row i's four samples as bytes.
-DEV void luma_block_pred(const uint8_t* __restrict__ img, int W, int H, int x, int y, int xf, int yf, uint32_t (&out)[4])
+// The 9 window rows of one lane straight from the reference plane (three aligned dwords
+// per row from clip(x - 2) & ~3, row index clamped).
+DEV void luma_window_global(const uint8_t* __restrict__ img, int W, int H, int x, int y, uint32_t (&w)[9][3])
 {
-    const int hs = xf == 3 ? 1 : 0;                  // G / h column c + 2 + hs
-    const int brow = yf == 3 ? 1 : 0;                // b / G row i + 2 + brow
-    uint32_t w[9][3];
 #pragma unroll
     for (int r = 0; r < 9; ++r) {
         const gdword* q = row_dwords(img, W, H, x, y - 2 + r);
         w[r][0] = q[0]; w[r][1] = q[1]; w[r][2] = q[2];
     }
+}
+
+// Reference tiles in LDS (north_star: "LDS staging of reference-block tiles"): the four
+// 4x4 blocks of an 8x8 quadrant that share one motion vector read one 13-row x 16-byte tile
+// of the reference (rows y-2 .. y+10, aligned dwords from (x-2) & ~3), which the quadrant's
+// four lanes fetch together by LDS-DMA (global_load_lds_dwordx4, no VGPR staging: k_inter4
+// sits at its VGPR cap) -- at most four 16-byte rows per lane -- instead of each lane
+// fetching its own 9 rows x 12 bytes.  Partitions of 8x8 and larger (16x16, 16x8, 8x16,
+// P/B_8x8 with 8x8 sub-blocks, direct with 8x8 inference) are uniform per quadrant; 8x4 /
+// 4x8 / 4x4 sub-blocks and windows crossing the left / right picture edge keep the
+// per-lane fetch.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+struct alignas(16) QuadTile {
+    u32x4 slot[64];                  // one wave-instruction of LDS-DMA: 16 B per lane
+};
+constexpr int INTER4_TILES = 4;      // per wave: tile rows ql, ql + 4, ql + 8, 12 of every quadrant
+
+DEV void luma_block_pred(const uint32_t (&w)[9][3], int W, int x, int xf, int yf, uint32_t (&out)[4])
+{
+    const int hs = xf == 3 ? 1 : 0;                  // G / h column c + 2 + hs
+    const int brow = yf == 3 ? 1 : 0;                // b / G row i + 2 + brow
 #ifdef H264R_EXP_NO_EDGE
     const bool inside = true;
 #else
@@ -378,7 +398,8 @@ DEV void fwd4(int p0, int p1, int p2, int p3, int& c0, int& c1, int& c2, int& c3
 // inverse_transform_sp (decoder.cc:256-257, transform.cc:1267-1300), and no records.
 template <bool SP>
 DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int aend, int lane, DbInfo* __restrict__ dbout,
-                    const Inter4Lds& S, int* sp_flag, const Inter4Pre& pre)
+                    const Inter4Lds& S, int* sp_flag, const Inter4Pre& pre, QuadTile* __restrict__ tiles,
+                    uint8_t* __restrict__ recon)
 {
     const int grp = lane >> 4, blk = lane & 15, bx = blk & 3, by = blk >> 2;
     const int a = a0 + grp;
@@ -415,21 +436,22 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
         } else {
             if (!sp_mb) return;
         }
-        const PicPtrs o = out_planes(b, g, pic);
         const int16_t* lv = b.levels + q.coef_off;
-        uint8_t* ydst = o.y + (size_t)(mby * 16 + by * 4) * g.W + mbx * 16 + bx * 4;
-        const size_t coff = (size_t)(mby * 8 + by * 2) * g.Wc + mbx * 8 + bx * 2;
+        // my 4x4 block in the MB-tiled reconstruction (device_common.h): rows of 16 / 8 bytes
+        uint8_t* const rmb = recon_mb(recon, g, pic, aa);
+        uint8_t* ydst = rmb + (by * 4) * 16 + bx * 4;
+        const int coff = RECON_CB + (by * 2) * 8 + bx * 2;          // Cb; Cr 64 bytes on
         if (pcm) {                                                       // mb_pred_ipcm decoder.cc:149-168
             const uint8_t* raw = reinterpret_cast<const uint8_t*>(lv);
     #pragma unroll
             for (int r = 0; r < 4; ++r)
-                *reinterpret_cast<uint32_t*>(ydst + (size_t)r * g.W) =
+                *reinterpret_cast<uint32_t*>(ydst + r * 16) =
                     *reinterpret_cast<const uint32_t*>(raw + (by * 4 + r) * 16 + bx * 4);
     #pragma unroll
             for (int pl = 0; pl < 2; ++pl)
     #pragma unroll
                 for (int r = 0; r < 2; ++r)
-                    *reinterpret_cast<uint16_t*>((pl ? o.v : o.u) + coff + (size_t)r * g.Wc) =
+                    *reinterpret_cast<uint16_t*>(rmb + coff + pl * 64 + r * 8) =
                         *reinterpret_cast<const uint16_t*>(raw + 256 + pl * 64 + (by * 2 + r) * 8 + bx * 2);
             return;
         }
@@ -494,22 +516,67 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
             if (!__any(use)) continue;                                  // P pictures: list 1 never
             uint32_t tY[4] = {0x80808080u, 0x80808080u, 0x80808080u, 0x80808080u};
             uint32_t tC[2] = {0x80808080u, 0x80808080u};                // no_ref: 128 (inter_prediction.cc:164-167,366-369)
-            if (use) {
-                const int slot = (int8_t)((mw.y >> 8) & 255);
-                const bool ok = slot >= 0 && slot < H264R_MAX_SLOTS && rr < H264R_MAX_REFS && S.planes[slot * 3];
-                const int mvx = (int16_t)(mw.x & 0xFFFF), mvy = (int16_t)(mw.x >> 16);
-                const int vx = X4 * 16 + mvx, vy = Y4 * 16 + mvy;       // quarter luma / eighth chroma units
-                if (ok) {
+            const int slot = (int8_t)((mw.y >> 8) & 255);
+            const bool ok = use && slot >= 0 && slot < H264R_MAX_SLOTS && rr < H264R_MAX_REFS && S.planes[slot * 3];
+            const int mvx = (int16_t)(mw.x & 0xFFFF), mvy = (int16_t)(mw.x >> 16);
+            const int vx = X4 * 16 + mvx, vy = Y4 * 16 + mvy;           // quarter luma / eighth chroma units
+            const int x = vx >> 2, y = vy >> 2;
 #ifndef H264R_EXP_NO_LUMA           // (measurement-only knobs: tools/exp_sweep.sh ablations)
-                    luma_block_pred(S.planes[slot * 3], g.W, g.H, vx >> 2, vy >> 2, vx & 3, vy & 3, tY);
+            {
+                // quadrant tile (QuadTile): the four lanes of my 8x8 quadrant (blk ^ 1, ^ 4, ^ 5)
+                // predict from one slot with one vector, and the tile stays inside the picture
+                const uint32_t key = ok ? mw.x : 0xFFFFFFFFu;
+                const int skey = ok ? slot : -1;
+                const bool uni = ok && key == (uint32_t)__shfl_xor((int)key, 1) && key == (uint32_t)__shfl_xor((int)key, 4) &&
+                                 key == (uint32_t)__shfl_xor((int)key, 5) && skey == __shfl_xor(skey, 1) &&
+                                 skey == __shfl_xor(skey, 4) && skey == __shfl_xor(skey, 5);
+                const int xq = x - 4 * (bx & 1), yq = y - 4 * (by & 1);
+#ifdef H264R_NO_QTILE                // A/B build (tools/ab_lib.sh): per-lane fetch only
+                const bool tile = false && uni;
+#else
+                const bool tile = uni && xq - 2 >= 0 && xq + 10 < g.W;
+#endif
+                // tile row t * 4 + ql (row 12: t = 3, ql = 0) of a quadrant lands, by LDS-DMA, in
+                // the 16-byte slot of the quadrant's lane ql of its wave-instruction t
+                const int qbase = grp * 16 + (by & 2) * 4 + (bx & 2);          // lane of ql = 0
+                if (__any(tile)) {
+                    const int ql = (by & 1) * 2 + (bx & 1);
+                    const uint8_t* img = S.planes[(tile ? slot : 0) * 3] + ((xq - 2) & ~3);
+#pragma unroll
+                    for (int t = 0; t < 4; ++t)
+                        if (tile && (t < 3 || ql == 0))
+                            __builtin_amdgcn_global_load_lds(
+                                (const __attribute__((address_space(1))) void*)(img + (size_t)clip3(0, g.H - 1, yq - 2 + ql + 4 * t) * g.W),
+                                (__attribute__((address_space(3))) void*)(tiles + t), 16, 0, 0);
+                    __builtin_amdgcn_s_waitcnt(0x0F70);                       // vmcnt(0): this wave's tiles landed
+                    __builtin_amdgcn_wave_barrier();
+                }
+                // the 9 window rows: tile rows (by & 1) * 4 + r from dword (bx & 1), or the
+                // lane's own rows of the plane -- one generic (flat) load per row either way
+                uint32_t w[9][3];
+                if (tile) {
+                    const uint32_t* tb = reinterpret_cast<const uint32_t*>(tiles) + (bx & 1);
+#pragma unroll
+                    for (int r = 0; r < 9; ++r) {
+                        const int jr = (by & 1) * 4 + r;                        // tile row
+                        const int src = qbase + ((jr & 2) << 1) + (jr & 1);    // lane that fetched it
+                        const uint32_t* q = tb + (jr >> 2) * 256 + src * 4;
+                        w[r][0] = q[0]; w[r][1] = q[1]; w[r][2] = q[2];
+                    }
+                } else if (ok) {
+                    luma_window_global(S.planes[slot * 3], g.W, g.H, x, y, w);
+                }
+                if (ok) luma_block_pred(w, g.W, x, vx & 3, vy & 3, tY);
+                if (__any(tile)) wave_sync();                      // read before the next list's tiles
+            }
 #endif
 #ifndef H264R_EXP_NO_CHROMA
+            if (ok) {
     #pragma unroll
-                    for (int pl = 0; pl < 2; ++pl)
-                        tC[pl] = chroma_block_pred(S.planes[slot * 3 + 1 + pl], g.Wc, g.Hc, vx >> 3, vy >> 3, vx & 7, vy & 7);
-#endif
-                }
+                for (int pl = 0; pl < 2; ++pl)
+                    tC[pl] = chroma_block_pred(S.planes[slot * 3 + 1 + pl], g.Wc, g.Hc, vx >> 3, vy >> 3, vx & 7, vy & 7);
             }
+#endif
             const bool l1 = l != 0;
     #pragma unroll
             for (int i = 0; i < 4; ++i) {
@@ -573,7 +640,7 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
                     asm volatile("" : "+v"(v));
                     wv |= (uint32_t)clip255(v) << (8 * c);
                 }
-                *reinterpret_cast<uint32_t*>(ydst + (size_t)i * g.W) = wv;
+                *reinterpret_cast<uint32_t*>(ydst + i * 16) = wv;
             }
             // ---- itrans_sp_cr (:1190-1265) then inverse_transform_chroma (:1033-1049):
             // chroma block cb is spread over lanes {blk, ^1, ^4, ^5}; my 2x2 quadrant
@@ -677,11 +744,11 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
                         rcv[1][c] = ((cr ? y3 : y1) + 32) >> 6;
                     }
                 }
-                uint8_t* cdst = (pl ? o.v : o.u) + coff;
+                uint8_t* cdst = rmb + coff + pl * 64;
     #pragma unroll
                 for (int r = 0; r < 2; ++r) {
                     const uint32_t wv = (uint32_t)clip255(pr[r][0] + rcv[r][0]) | ((uint32_t)clip255(pr[r][1] + rcv[r][1]) << 8);
-                    *reinterpret_cast<uint16_t*>(cdst + (size_t)r * g.Wc) = (uint16_t)wv;
+                    *reinterpret_cast<uint16_t*>(cdst + r * 8) = (uint16_t)wv;
                 }
             }
             return;
@@ -810,7 +877,7 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
             uint32_t wv = 0;
     #pragma unroll
             for (int c = 0; c < 4; ++c) wv |= (uint32_t)clip255((int)((predY[i] >> (8 * c)) & 255) + res[i][c]) << (8 * c);
-            *reinterpret_cast<uint32_t*>(ydst + (size_t)i * g.W) = wv;
+            *reinterpret_cast<uint32_t*>(ydst + i * 16) = wv;
         }
 
         // ---- chroma residual (transform.cc:1081-1091, DC :875-889): chroma block cb is
@@ -869,13 +936,13 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
                         for (int c = 0; c < 2; ++c) rc[r][c] = (cr == 0 && cc == 0 && r == 0 && c == 0) ? dcl : raw[r][c];
                 }
             }
-            uint8_t* cdst = (pl ? o.v : o.u) + coff;
+            uint8_t* cdst = rmb + coff + pl * 64;
     #pragma unroll
             for (int r = 0; r < 2; ++r) {
                 const uint32_t pr = predC[pl] >> (16 * r);
                 const uint32_t wv = (uint32_t)clip255((int)(pr & 255) + rc[r][0]) |
                                     ((uint32_t)clip255((int)((pr >> 8) & 255) + rc[r][1]) << 8);
-                *reinterpret_cast<uint16_t*>(cdst + (size_t)r * g.Wc) = (uint16_t)wv;
+                *reinterpret_cast<uint16_t*>(cdst + r * 8) = (uint16_t)wv;
             }
         }
     }();

@@ -369,12 +369,11 @@ struct IntraHead {
     uint32_t nin;                // bit k: neighbour k inside the picture
 };
 
-DEV IntraHead intra_head(const h264r_batch& b, const Geom& g, int pic, int mbx, int mby, int lane)
+DEV IntraHead intra_head(const h264r_batch& b, const Geom& g, int pic, int mbx, int mby, int lane, uint8_t* recon)
 {
     IntraHead h;
     const int a = mby * g.wmb + mbx;
     const h264r_mb* mbs = b.mbs + (size_t)pic * g.nmb;
-    const PicPtrs o = out_planes(b, g, pic);
     const int X = mbx * 16, Y = mby * 16, Xc = mbx * 8, Yc = mby * 8;
     // ---- neighbour samples (in-picture addresses only; availability decides later which
     // of them are used): one dword load per lane (a left-column sample is the top byte of
@@ -382,23 +381,24 @@ DEV IntraHead intra_head(const h264r_batch& b, const Geom& g, int pic, int mbx, 
     // MB's first row and drop it).  Loads in lane-divergent branches would each merge
     // through a copy whose vmcnt(0) serialises them.
     {
-        const uint8_t* src = o.y + (size_t)Y * g.W + X;
+        // (MB-tiled reconstruction, device_common.h: a dword never crosses an MB)
+        const uint8_t* src = recon_mb(recon, g, pic, mby * g.wmb + mbx);
         bool want = false, left = false;
         if (lane < 7) {                                   // row above, x = -4..23
             const int x = X - 4 + 4 * lane;
             want = mby > 0 && x >= 0 && x < g.W;
-            src = want ? o.y + (size_t)(Y - 1) * g.W + x : src;
+            src = want ? recon_y(recon, g, pic, x, Y - 1) : src;
         } else if (lane < 23) {                           // left column
             want = left = mbx > 0;
-            src = want ? o.y + (size_t)(Y + lane - 7) * g.W + X - 4 : src;
+            src = want ? recon_y(recon, g, pic, X - 4, Y + lane - 7) : src;
         } else if (lane < 29) {                           // chroma rows above, x = -4..7
             const int k = lane - 23, pl = k / 3, x = Xc - 4 + 4 * (k % 3);
             want = mby > 0 && x >= 0;
-            src = want ? (pl ? o.v : o.u) + (size_t)(Yc - 1) * g.Wc + x : src;
+            src = want ? recon_c(recon, g, pic, pl, x, Yc - 1) : src;
         } else if (lane < 45) {                           // chroma left columns
             const int k = lane - 29, pl = k >> 3;
             want = left = mbx > 0;
-            src = want ? (pl ? o.v : o.u) + (size_t)(Yc + (k & 7)) * g.Wc + Xc - 4 : src;
+            src = want ? recon_c(recon, g, pic, pl, Xc - 4, Yc + (k & 7)) : src;
         }
         const uint32_t w = *as_global(src);
         h.nb = (w >> (left ? 24 : 0)) & (0u - (uint32_t)want);   // arithmetic, not a select: no branch
@@ -429,11 +429,10 @@ DEV IntraLoads intra_body_loads(const h264r_batch& b, int pic, const IntraHead& 
 // wave.  tph (trace builds): s_memtime at the phase boundaries [record known, residual,
 // tiles, prediction, end].
 DEV void intra_mb_compute(const h264r_batch& b, const Geom& g, int pic, int mbx, int mby, int lane, IntraScratch& S,
-                          const IntraHead& hd, const IntraLoads& ld, unsigned long long* tph = nullptr)
+                          const IntraHead& hd, const IntraLoads& ld, uint8_t* recon, unsigned long long* tph = nullptr)
 {
 #define INTRA_STAMP(k) do { if (tph) tph[k] = __builtin_amdgcn_s_memtime(); } while (0)
-    const PicPtrs o = out_planes(b, g, pic);
-    const int X = mbx * 16, Y = mby * 16, Xc = mbx * 8, Yc = mby * 8;
+    uint8_t* const rmb = recon_mb(recon, g, pic, mby * g.wmb + mbx);      // MB-tiled (device_common.h)
     const h264r_mb& m = hd.m;
     const uint32_t nb = hd.nb;
     // the 16 intra 4x4 / 4 intra 8x8 modes as one 64-bit word (h264r_mb::ipred, dwords 5-6):
@@ -515,7 +514,7 @@ DEV void intra_mb_compute(const h264r_batch& b, const Geom& g, int pic, int mbx,
         uint32_t w = 0;
 #pragma unroll
         for (int c = 0; c < 4; ++c) w |= (uint32_t)clip255(p[c] + resL[c]) << (8 * c);
-        *reinterpret_cast<uint32_t*>(o.y + (size_t)(Y + y) * g.W + X + x0) = w;
+        *reinterpret_cast<uint32_t*>(rmb + y * 16 + x0) = w;
     } else if (i8) {
         uint32_t tab[3];
         intra_tap_table<8>(lane & 7, lane >> 3, tab);
@@ -619,7 +618,7 @@ DEV void intra_mb_compute(const h264r_batch& b, const Geom& g, int pic, int mbx,
     INTRA_STAMP(3);
     if (!i16) {
         const int y = lane >> 2, x0 = (lane & 3) * 4;
-        *reinterpret_cast<uint32_t*>(o.y + (size_t)(Y + y) * g.W + X + x0) = lds_u32(&S.tile[ti(x0, y)]);
+        *reinterpret_cast<uint32_t*>(rmb + y * 16 + x0) = lds_u32(&S.tile[ti(x0, y)]);
     }
 
     // ---- chroma: IntraPrediction::Chroma (intra_prediction.cc:748-894) + construction_chroma,
@@ -663,7 +662,7 @@ DEV void intra_mb_compute(const h264r_batch& b, const Geom& g, int pic, int mbx,
             for (int c = 0; c < 2; ++c) p[c] = clip255((pa + pb * (x0 + c - 3) + pc * (y - 3) + 16) >> 5);
         }
         const uint32_t w = (uint32_t)clip255(p[0] + resC[0]) | ((uint32_t)clip255(p[1] + resC[1]) << 8);
-        *reinterpret_cast<uint16_t*>((pl ? o.v : o.u) + (size_t)(Yc + y) * g.Wc + Xc + x0) = (uint16_t)w;
+        *reinterpret_cast<uint16_t*>(rmb + RECON_CB + pl * 64 + y * 8 + x0) = (uint16_t)w;
     }
     INTRA_STAMP(4);
 #undef INTRA_STAMP
@@ -671,12 +670,12 @@ DEV void intra_mb_compute(const h264r_batch& b, const Geom& g, int pic, int mbx,
 
 // Loads then reconstruction of one intra MB (the walk, k_intra_pic).
 DEV void intra_mb2(const h264r_batch& b, const Geom& g, int pic, int mbx, int mby, int lane, IntraScratch& S,
-                   unsigned long long* tph = nullptr)
+                   uint8_t* recon, unsigned long long* tph = nullptr)
 {
-    const IntraHead hd = intra_head(b, g, pic, mbx, mby, lane);
+    const IntraHead hd = intra_head(b, g, pic, mbx, mby, lane, recon);
     if (!mb_is_intra(hd.m) || hd.m.mb_type == H264R_I_PCM) return;
     const IntraLoads ld = intra_body_loads(b, pic, hd, lane);
-    intra_mb_compute(b, g, pic, mbx, mby, lane, S, hd, ld, tph);
+    intra_mb_compute(b, g, pic, mbx, mby, lane, S, hd, ld, recon, tph);
 }
 
 }  // namespace h264r

@@ -142,10 +142,11 @@ def test_gpu_large_batch_wide_rows(L, dec, cidx):
 
 
 @pytest.mark.parametrize("cidx", [2, 3, 4])
-def test_gpu_pipelined_sub_batches(L, dec, cidx):
-    """A batch of >= 2 x H264R_PIPE_MIN pictures (1100 CIF pictures) runs as sub-batches on
-    the context's pipeline streams (h264r_host.hip run_batch: inter / intra / deblocking of
-    consecutive sub-batches overlapping); every picture checked."""
+def test_gpu_pipelined_sub_batches(L, dec, cidx, monkeypatch):
+    """With H264R_PIPES=3 a batch of >= 2 x H264R_PIPE_MIN pictures (1100 CIF pictures) runs
+    as sub-batches on the context's pipeline streams (h264r_host.hip run_batch: inter /
+    intra / deblocking of consecutive sub-batches overlapping); every picture checked."""
+    monkeypatch.setenv("H264R_PIPES", "3")
     _large_batch_vs_oracle(L, dec, cidx, 22, 18, 1100)
 
 
