@@ -149,15 +149,18 @@ DEV void luma_window_global(const uint8_t* __restrict__ img, int W, int H, int x
     }
 }
 
-// Reference tiles in LDS (north_star: "LDS staging of reference-block tiles"): the four
-// 4x4 blocks of an 8x8 quadrant that share one motion vector read one 13-row x 16-byte tile
-// of the reference (rows y-2 .. y+10, aligned dwords from (x-2) & ~3), which the quadrant's
-// four lanes fetch together by LDS-DMA (global_load_lds_dwordx4, no VGPR staging: k_inter4
-// sits at its VGPR cap) -- at most four 16-byte rows per lane -- instead of each lane
-// fetching its own 9 rows x 12 bytes.  Partitions of 8x8 and larger (16x16, 16x8, 8x16,
-// P/B_8x8 with 8x8 sub-blocks, direct with 8x8 inference) are uniform per quadrant; 8x4 /
-// 4x8 / 4x4 sub-blocks and windows crossing the left / right picture edge keep the
-// per-lane fetch.
+// Reference tiles in LDS (north_star: "LDS staging of reference-block tiles"), built and
+// measured, OFF by default (-DH264R_QTILE builds it): the four 4x4 blocks of an 8x8
+// quadrant that share one motion vector read one 13-row x 16-byte tile of the reference
+// (rows y-2 .. y+10, aligned dwords from (x-2) & ~3), which the quadrant's four lanes fetch
+// together by LDS-DMA (global_load_lds_dwordx4, no VGPR staging: k_inter4 sits at its VGPR
+// cap) -- at most four 16-byte rows per lane -- instead of each lane fetching its own 9
+// rows x 12 bytes.  Bit-exact (154 GPU tests), but k_inter4 9.41 -> 11.00 ms per 1024
+// config-3 pictures and 3.75 -> 4.23 ms on config 4 (profiles/r03_e_ab.txt): the fill's
+// vmcnt(0) also retires the residual loads issued before it, the per-lane window reads
+// from LDS are no cheaper than the L1/L2-served global ones (the quadrant's rows were
+// already shared in L1), and the extra live state spilled (84 B/lane of scratch at the
+// 168-VGPR cap).  Register staging instead of LDS-DMA spilled 140 B/lane.
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 struct alignas(16) QuadTile {
     u32x4 slot[64];                  // one wave-instruction of LDS-DMA: 16 B per lane
@@ -531,10 +534,10 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
                                  key == (uint32_t)__shfl_xor((int)key, 5) && skey == __shfl_xor(skey, 1) &&
                                  skey == __shfl_xor(skey, 4) && skey == __shfl_xor(skey, 5);
                 const int xq = x - 4 * (bx & 1), yq = y - 4 * (by & 1);
-#ifdef H264R_NO_QTILE                // A/B build (tools/ab_lib.sh): per-lane fetch only
-                const bool tile = false && uni;
-#else
+#ifdef H264R_QTILE                   // measured slower: off (QuadTile above)
                 const bool tile = uni && xq - 2 >= 0 && xq + 10 < g.W;
+#else
+                const bool tile = false && uni && xq >= 0;
 #endif
                 // tile row t * 4 + ql (row 12: t = 3, ql = 0) of a quadrant lands, by LDS-DMA, in
                 // the 16-byte slot of the quadrant's lane ql of its wave-instruction t
