@@ -28,6 +28,8 @@
 
 namespace h264r { struct DbInfo; }
 extern "C" __global__ void k_inter4(h264r_batch b, h264r::DbInfo* dbinfo, int2 rows, int* sp_flag, uint8_t* recon);
+extern "C" __global__ void k_inter4r(h264r_batch b, h264r::DbInfo* dbinfo, int2 rows, int* sp_flag, uint8_t* recon);
+extern "C" __global__ void k_dbinfo(h264r_batch b, h264r::DbInfo* dbinfo, int2 rows);
 extern "C" __global__ void k_inter_sp(h264r_batch b, int2 rows, const int* sp_flag, uint8_t* recon);
 extern "C" __global__ void k_untile(h264r_batch b, int2 rows, const uint8_t* recon);
 extern "C" __global__ void k_intra_pic(h264r_batch b, int* sync, int* err, const uint16_t* lvl, int lmax, int2 rows,
@@ -108,10 +110,16 @@ struct Scratch {
     uint32_t* d_list = nullptr; size_t c_list = 0; // intra MBs by level (pic * nmb + addr)
     int* d_lcnt = nullptr; size_t c_lcnt = 0;      // [count | base | cursor] x (LEVEL_LISTS + 2)
     uint8_t* d_recon = nullptr; size_t c_recon = 0; // MB-tiled reconstruction, 384 B per (picture, MB)
+    // k_dbinfo beside the reconstruction (H264R_DBINFO=2): its stream and fork / join events
+    hipStream_t side = nullptr;
+    hipEvent_t ev_side_start = nullptr, ev_side_done = nullptr;
     void release()
     {
         void* bufs[] = {d_dbinfo, d_sync, d_hb, d_hb2, d_lvl, d_list, d_lcnt, d_recon};
         for (void* b : bufs) if (b) (void)hipFree(b);
+        if (side) (void)hipStreamDestroy(side);
+        if (ev_side_start) (void)hipEventDestroy(ev_side_start);
+        if (ev_side_done) (void)hipEventDestroy(ev_side_done);
     }
 };
 constexpr int MAX_PIPES = 4;
@@ -464,12 +472,35 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
     int* sync = X.d_sync;
     Timed whole(timed_whole ? c : nullptr, 3, s);
     if (c->timing && timed_whole) c->timed_launches++;
+    // the deblocking records: inside k_inter4 (H264R_DBINFO=0), k_dbinfo before k_inter4r on
+    // this stream (1), or k_dbinfo on the scratch's side stream beside the reconstruction
+    // kernels, joined before deblocking (2)
+    const char* dbe = getenv("H264R_DBINFO");
+    const int db_mode = dbe ? atoi(dbe) : 0;
+    const int groups = (W * HB + 15) / 16;
+    const dim3 igrid(8 * ((groups + 7) / 8), P);
+    if (db_mode == 2) {
+        if (!X.side) {
+            HIP_OK(hipStreamCreateWithFlags(&X.side, hipStreamNonBlocking));
+            HIP_OK(hipEventCreateWithFlags(&X.ev_side_start, hipEventDisableTiming));
+            HIP_OK(hipEventCreateWithFlags(&X.ev_side_done, hipEventDisableTiming));
+        }
+        HIP_OK(hipEventRecord(X.ev_side_start, s));                 // the previous launch's deblocking read dbinfo
+        HIP_OK(hipStreamWaitEvent(X.side, X.ev_side_start, 0));
+        hipLaunchKernelGGL(k_dbinfo, igrid, dim3(256), 0, X.side, b, dbinfo, rows);
+        HIP_OK(hipGetLastError());
+        HIP_OK(hipEventRecord(X.ev_side_done, X.side));
+    }
     if (hk.after_inter) HIP_OK(hipStreamWaitEvent(s, hk.after_inter, 0));
     {
         Timed t(c, 0, s);
         int* sp_flag = sync + 1 + (size_t)P * H + 4;
-        const int groups = (W * HB + 15) / 16;
-        hipLaunchKernelGGL(k_inter4, dim3(8 * ((groups + 7) / 8), P), dim3(256), 0, s, b, dbinfo, rows, sp_flag, recon);
+        if (db_mode == 1) {
+            hipLaunchKernelGGL(k_dbinfo, igrid, dim3(256), 0, s, b, dbinfo, rows);
+            HIP_OK(hipGetLastError());
+        }
+        if (db_mode == 0) hipLaunchKernelGGL(k_inter4, igrid, dim3(256), 0, s, b, dbinfo, rows, sp_flag, recon);
+        else hipLaunchKernelGGL(k_inter4r, igrid, dim3(256), 0, s, b, dbinfo, rows, sp_flag, recon);
         HIP_OK(hipGetLastError());
         // inter MBs of SP slices (a short launch when the batch has none)
         hipLaunchKernelGGL(k_inter_sp, dim3(1024), dim3(256), 0, s, b, rows, (const int*)sp_flag, recon);
@@ -529,6 +560,7 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
         HIP_OK(hipGetLastError());
     }
     if (hk.intra_done) HIP_OK(hipEventRecord(hk.intra_done, s));
+    if (db_mode == 2) HIP_OK(hipStreamWaitEvent(s, X.ev_side_done, 0));
     if (!(c->debug & H264R_DBG_NO_DEBLOCK)) {
         Timed t(c, 2, s);
         if (!c->nxcc) {                  // XCDs of the device: the deblocking kernels' placement

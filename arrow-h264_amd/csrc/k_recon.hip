@@ -28,17 +28,27 @@ DEV void inter4_lds(const h264r_batch& b, int pic, Inter4Lds& S)
     if (threadIdx.x >= 64 && threadIdx.x - 64 < nsl) S.slice_type[threadIdx.x - 64] = sl[threadIdx.x - 64].slice_type;
 }
 
+// the wave's QuadTile rows (H264R_QTILE builds only: mb_inter4.h)
+DEV QuadTile* wave_tiles()
+{
+#ifdef H264R_QTILE
+    __shared__ QuadTile tiles[4][INTER4_TILES];
+    return tiles[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)];
+#else
+    return nullptr;
+#endif
+}
+
 // sp_flag: set when an inter MB of an SP slice was met (k_inter_sp then runs).
 // Grid (8 * ceil(groups / 8), pictures), XCD-aware: workgroups go round-robin to the 8
 // XCDs in launch order, so blockIdx.x % 8 is the XCD and it takes the 16-MB groups of band
 // blockIdx.x % 8 (one eighth of the MB rows) of every picture: an XCD's motion
 // compensation reads only its band of the reference pictures (+ the MV reach), which its
 // 4 MB L2 holds, instead of every XCD streaming whole references through its L2.
-extern "C" __global__ __launch_bounds__(256, H264R_INTER_WAVES) void k_inter4(h264r_batch b, DbInfo* dbinfo, int2 rows,
-                                                                             int* sp_flag, uint8_t* recon)
+// DB: the deblocking records too (k_inter4), or not (k_inter4r, with k_dbinfo beside it).
+template <bool DB>
+DEV void inter4_kernel(const h264r_batch& b, DbInfo* dbinfo, int2 rows, int* sp_flag, uint8_t* recon, Inter4Lds& S)
 {
-    __shared__ Inter4Lds S;
-    __shared__ QuadTile tiles[4][INTER4_TILES];
     const int pic = blockIdx.y;
     const Geom g = make_geom(b.width_mbs, b.height_mbs);
     const int groups = (g.wmb * (rows.y - rows.x) + 15) / 16, gb = (groups + 7) / 8;
@@ -51,8 +61,46 @@ extern "C" __global__ __launch_bounds__(256, H264R_INTER_WAVES) void k_inter4(h2
     inter4_lds(b, pic, S);
     __syncthreads();
     if (a0 >= aend) return;
-    inter4_mbs<false>(b, g, pic, a0, aend, lane, dbinfo + (size_t)pic * g.nmb, S, sp_flag, pre,
-                      tiles[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)], recon);
+    inter4_mbs<false, DB>(b, g, pic, a0, aend, lane, dbinfo + (size_t)pic * g.nmb, S, sp_flag, pre, wave_tiles(), recon);
+}
+extern "C" __global__ __launch_bounds__(256, H264R_INTER_WAVES) void k_inter4(h264r_batch b, DbInfo* dbinfo, int2 rows,
+                                                                             int* sp_flag, uint8_t* recon)
+{
+    __shared__ Inter4Lds S;
+    inter4_kernel<true>(b, dbinfo, rows, sp_flag, recon, S);
+}
+extern "C" __global__ __launch_bounds__(256, H264R_INTER_WAVES) void k_inter4r(h264r_batch b, DbInfo* dbinfo, int2 rows,
+                                                                              int* sp_flag, uint8_t* recon)
+{
+    __shared__ Inter4Lds S;
+    inter4_kernel<false>(b, dbinfo, rows, sp_flag, recon, S);
+}
+
+// k_dbinfo: the deblocking records DbInfo of every MB (dbinfo_block, mb_inter4.h) on their
+// own -- they depend on the MB records and motion only, not on any sample, so the host
+// launches this beside k_inter4r on a second stream.  Same grid and lane roles as k_inter4.
+extern "C" __global__ __launch_bounds__(256) void k_dbinfo(h264r_batch b, DbInfo* dbinfo, int2 rows)
+{
+    __shared__ Inter4Lds S;
+    const int pic = blockIdx.y;
+    const Geom g = make_geom(b.width_mbs, b.height_mbs);
+    const int groups = (g.wmb * (rows.y - rows.x) + 15) / 16, gb = (groups + 7) / 8;
+    const int grp = (blockIdx.x & 7) * gb + (blockIdx.x >> 3);
+    if (grp >= groups) return;
+    const int lane = threadIdx.x & 63;
+    const int a0 = rows.x * g.wmb + (grp * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) * 4;
+    const int aend = rows.y * g.wmb;
+    const Inter4Pre pre = inter4_pre(b, g, pic, a0, aend, lane);
+    inter4_lds(b, pic, S);
+    __syncthreads();
+    if (a0 >= aend) return;
+    const int a = a0 + (lane >> 4);
+    const bool valid = a < aend;
+    const int aa = valid ? a : aend - 1;
+    const h264r_slice* slices = b.slices + (size_t)pic * b.slice_stride;
+    const uint2 m0 = motion_word(pre.mv[0], pre.ri[0], slices, S, pre.q.slice, 0);
+    const uint2 m1 = motion_word(pre.mv[1], pre.ri[1], slices, S, pre.q.slice, 1);
+    dbinfo_block(b, g, pic, aa, valid, lane & 15, S, pre.q, m0, m1, pre.qsh, dbinfo + (size_t)pic * g.nmb);
 }
 
 // k_inter_sp: the inter MBs of SP slices (inverse_transform_sp), after k_inter4.  A
@@ -62,7 +110,6 @@ extern "C" __global__ __launch_bounds__(256) void k_inter_sp(h264r_batch b, int2
 {
     if (!__hip_atomic_load(sp_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
     __shared__ Inter4Lds S;
-    __shared__ QuadTile tiles[4][INTER4_TILES];
     const Geom g = make_geom(b.width_mbs, b.height_mbs);
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int groups = (g.wmb * (rows.y - rows.x) + 15) / 16;
@@ -73,8 +120,8 @@ extern "C" __global__ __launch_bounds__(256) void k_inter_sp(h264r_batch b, int2
         inter4_lds(b, pic, S);
         __syncthreads();
         const int a0 = rows.x * g.wmb + (grp * 4 + wave) * 4;
-        if (a0 < aend) inter4_mbs<true>(b, g, pic, a0, aend, lane, nullptr, S, nullptr, inter4_pre(b, g, pic, a0, aend, lane),
-                                         tiles[wave], recon);
+        if (a0 < aend) inter4_mbs<true, false>(b, g, pic, a0, aend, lane, nullptr, S, nullptr, inter4_pre(b, g, pic, a0, aend, lane),
+                                               wave_tiles(), recon);
     }
 }
 

@@ -395,11 +395,104 @@ DEV void fwd4(int p0, int p1, int p2, int p3, int& c0, int& c1, int& c2, int& c3
     c0 = e0 + e1; c1 = e2 + (e3 << 1); c2 = e0 - e1; c3 = e3 - (e2 << 1);
 }
 
-// The inter / I_PCM macroblocks a0 .. a0+3 of picture `pic` and the deblocking
+// QpY (pl 0) / QpC[pl - 1] of a record, from its dwords 0 and 1
+DEV int mb_qp(const h264r_mb& m, int pl)
+{
+    const uint32_t w0 = reinterpret_cast<const uint32_t*>(&m)[0], w1 = reinterpret_cast<const uint32_t*>(&m)[1];
+    return pl == 0 ? (int)(int8_t)(w0 >> 24) : (int)(int8_t)(w1 >> (8 * (pl - 1)));
+}
+
+// The deblocking record of one MB's 4x4 block (Deblock::strength deblock.cc:78-289,
+// edge parameters :469-480): the block's left edge (vertical edge bx, segment by) and top
+// edge (horizontal edge by, segment bx), and for blk < 9 one alpha/beta/tc0 word.  Inside
+// k_inter4 after the reconstruction (DB = true), or its own kernel k_dbinfo.
+DEV void dbinfo_block(const h264r_batch& b, const Geom& g, int pic, int aa, bool valid, int blk, const Inter4Lds& S,
+                      const h264r_mb& q, uint2 m0, uint2 m1, uint2 qsh, DbInfo* __restrict__ dbout)
+{
+    const int bx = blk & 3, by = blk >> 2;
+    const int mbx = aa % g.wmb, mby = aa / g.wmb;
+    const h264r_mb* mbs = b.mbs + (size_t)pic * g.nmb;
+    const h264r_slice* slices = b.slices + (size_t)pic * b.slice_stride;
+    const int X4 = mbx * 4 + bx, Y4 = mby * 4 + by;
+    const int mi = Y4 * g.W4 + X4;
+    const size_t mbase = (size_t)pic * 2 * g.motion_plane;
+    const int hasL = mbx > 0, hasU = mby > 0;
+    const int q_type = qsh.x & 255, idc = (qsh.x >> 8) & 255;
+    const int offa = (int8_t)((qsh.x >> 16) & 255), offb = (int8_t)(qsh.x >> 24);
+    // neighbour motion and records (in k_inter4: loaded after the reconstruction, so that
+    // they do not stay live across motion compensation; L2-hot by then)
+    const int li = X4 > 0 ? mi - 1 : mi, ui = Y4 > 0 ? mi - g.W4 : mi;
+    const h264r_mb L = mb_lane(&mbs[hasL ? aa - 1 : aa]);
+    const h264r_mb U = mb_lane(&mbs[hasU ? aa - g.wmb : aa]);
+    // the neighbour block belongs to this MB or to the left / upper one (its slice resolves it)
+    const int lsl = bx > 0 ? q.slice : L.slice, usl = by > 0 ? q.slice : U.slice;
+    const uint2 l0 = block_motion(b, slices, S, mbase + li, lsl, 0), l1 = block_motion(b, slices, S, mbase + g.motion_plane + li, lsl, 1);
+    const uint2 u0 = block_motion(b, slices, S, mbase + ui, usl, 0), u1 = block_motion(b, slices, S, mbase + g.motion_plane + ui, usl, 1);
+    const int l_type = slice_type_of(slices, S, L.slice), u_type = slice_type_of(slices, S, U.slice);
+    // ---- deblocking record (Deblock::strength deblock.cc:78-289): this lane's
+    // left edge (vertical edge bx, segment by) and top edge (horizontal edge by,
+    // segment bx)
+    if (valid) {
+        const int fl = idc == 0 ? hasL : (idc == 2 && hasL && L.slice == q.slice);
+        const int ft = idc == 0 ? hasU : (idc == 2 && hasU && U.slice == q.slice);
+        const int t8 = (q.flags & H264R_MBF_T8x8) != 0;
+        const MotionRef mq = motion_of(m0, m1);
+        const int q_intra = mb_is_intra(q);
+        const int pskip = q_type == H264R_SLICE_P && q.mb_type == H264R_P_SKIP;
+        const int special_q = special_slice(q_type);
+        DbInfo* out = dbout + aa;
+#pragma unroll
+        for (int hor = 0; hor < 2; ++hor) {
+            const int e = hor ? by : bx, s = hor ? bx : by;
+            const int en = idc != 1 && (e == 0 ? (hor ? ft : fl) : ((e & 1) ? !t8 : 1));
+            int v = 0;
+            if (en) {
+                // MB P of the edge: the left / upper MB for edge 0, else this MB
+                const int p_flags = e == 0 ? (hor ? U.flags : L.flags) : q.flags;
+                const int p_cbp = e == 0 ? (hor ? U.cbp_blks : L.cbp_blks) : q.cbp_blks;
+                const int special = special_q || (e == 0 && special_slice(hor ? u_type : l_type));
+                const int intra = q_intra || (p_flags & H264R_MBF_INTRA) != 0;
+                const int blkQ = 4 * by + bx;
+                const int blkP = hor ? (e == 0 ? 12 + bx : blkQ - 4) : (e == 0 ? blkQ + 3 : blkQ - 1);
+                const int coded = ((q.cbp_blks >> blkQ) & 1) || ((p_cbp >> blkP) & 1);
+                const int same_part = e > 0 && (q.mb_type == H264R_P_16x16 ||
+                                                q.mb_type == (hor ? H264R_P_8x16 : H264R_P_16x8));
+                if (!hor) {
+                    if (special) v = e == 0 ? 4 : 3;
+                    else if (e > 0 && pskip) v = 0;
+                    else if (e == 0 && intra) v = 4;
+                    else if (intra) v = 3;
+                    else if (coded) v = 2;
+                    else if (same_part) v = 0;
+                    else v = bs_compare(mq, motion_of(l0, l1));
+                } else {
+                    if (e == 0 && (special || intra)) v = 4;
+                    else if (special || intra) v = 3;
+                    else if (e > 0 && pskip) v = 0;
+                    else if (coded) v = 2;
+                    else if (same_part) v = 0;
+                    else v = bs_compare(mq, motion_of(u0, u1));
+                }
+            }
+            out->bs[hor * 16 + e * 4 + s] = (uint8_t)v;
+        }
+        if (blk < 9) {                                              // edge parameters
+            const int pl = blk / 3, which = blk - pl * 3;
+            // QP of plane pl from the record's dwords 0 / 1 (a select between the byte fields
+            // became a select of their addresses: the record went to memory, promoted to LDS)
+            const h264r_mb& P = which == 0 ? L : (which == 1 ? U : q);
+            const int qp = mb_qp(P, pl), qq = mb_qp(q, pl);
+            out->par[blk] = edge_word(qp, qq, offa, offb);
+        }
+    }
+
+}
+
+// The inter / I_PCM macroblocks a0 .. a0+3 of picture `pic` and (DB) the deblocking
 // records of all four.  SP = false (k_inter4): inter MBs of SP slices are left out and
 // flagged in *sp_flag; SP = true (k_inter_sp): only those are reconstructed, with
 // inverse_transform_sp (decoder.cc:256-257, transform.cc:1267-1300), and no records.
-template <bool SP>
+template <bool SP, bool DB>
 DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int aend, int lane, DbInfo* __restrict__ dbout,
                     const Inter4Lds& S, int* sp_flag, const Inter4Pre& pre, QuadTile* __restrict__ tiles,
                     uint8_t* __restrict__ recon)
@@ -409,23 +502,17 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
     const bool valid = a < aend;
     const int aa = valid ? a : aend - 1;
     const int mbx = aa % g.wmb, mby = aa / g.wmb;
-    const h264r_mb* mbs = b.mbs + (size_t)pic * g.nmb;
     const h264r_slice* slices = b.slices + (size_t)pic * b.slice_stride;
 
-    // ---- MB record (two 16-byte loads: a struct copy becomes one byte load per field,
-    // each waited on its own) and the motion of this block
+    // ---- MB record (inter4_pre: two 16-byte loads -- a struct copy becomes one byte load
+    // per field, each waited on its own) and the motion of this block
     const int X4 = mbx * 4 + bx, Y4 = mby * 4 + by;
-    const int mi = Y4 * g.W4 + X4;
-    const size_t mbase = (size_t)pic * 2 * g.motion_plane;
     const h264r_mb q = pre.q;
     const h264r_slice* qs = &slices[q.slice];
     const uint2 qsh = pre.qsh;
     const uint2 m0 = motion_word(pre.mv[0], pre.ri[0], slices, S, q.slice, 0);
     const uint2 m1 = motion_word(pre.mv[1], pre.ri[1], slices, S, q.slice, 1);
-    const int hasL = mbx > 0, hasU = mby > 0;
-    // slice types of the left / upper MBs' slices (SP/SI edges), loaded with qsh
-    const int q_type = qsh.x & 255, idc = (qsh.x >> 8) & 255;
-    const int offa = (int8_t)((qsh.x >> 16) & 255), offb = (int8_t)(qsh.x >> 24);
+    const int q_type = qsh.x & 255;
     const int wp_mode = qsh.y & 255;
 
     // ---- reconstruction of inter / I_PCM MBs first (the motion-compensation loads go
@@ -950,78 +1037,11 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
         }
     }();
 
-    if constexpr (SP) return;
-    // neighbour motion and records: loaded here, after the reconstruction, so that
-    // they do not stay live across motion compensation (L2-hot by now)
+    if constexpr (SP || !DB) return;
 #ifdef H264R_EXP_NO_DBINFO
     return;
 #endif
-    const int li = X4 > 0 ? mi - 1 : mi, ui = Y4 > 0 ? mi - g.W4 : mi;
-    const h264r_mb L = mb_lane(&mbs[hasL ? aa - 1 : aa]);
-    const h264r_mb U = mb_lane(&mbs[hasU ? aa - g.wmb : aa]);
-    // the neighbour block belongs to this MB or to the left / upper one (its slice resolves it)
-    const int lsl = bx > 0 ? q.slice : L.slice, usl = by > 0 ? q.slice : U.slice;
-    const uint2 l0 = block_motion(b, slices, S, mbase + li, lsl, 0), l1 = block_motion(b, slices, S, mbase + g.motion_plane + li, lsl, 1);
-    const uint2 u0 = block_motion(b, slices, S, mbase + ui, usl, 0), u1 = block_motion(b, slices, S, mbase + g.motion_plane + ui, usl, 1);
-    const int l_type = slice_type_of(slices, S, L.slice), u_type = slice_type_of(slices, S, U.slice);
-    // ---- deblocking record (Deblock::strength deblock.cc:78-289): this lane's
-    // left edge (vertical edge bx, segment by) and top edge (horizontal edge by,
-    // segment bx)
-    if (valid) {
-        const int fl = idc == 0 ? hasL : (idc == 2 && hasL && L.slice == q.slice);
-        const int ft = idc == 0 ? hasU : (idc == 2 && hasU && U.slice == q.slice);
-        const int t8 = (q.flags & H264R_MBF_T8x8) != 0;
-        const MotionRef mq = motion_of(m0, m1);
-        const int q_intra = mb_is_intra(q);
-        const int pskip = q_type == H264R_SLICE_P && q.mb_type == H264R_P_SKIP;
-        const int special_q = special_slice(q_type);
-        DbInfo* out = dbout + aa;
-#pragma unroll
-        for (int hor = 0; hor < 2; ++hor) {
-            const int e = hor ? by : bx, s = hor ? bx : by;
-            const int en = idc != 1 && (e == 0 ? (hor ? ft : fl) : ((e & 1) ? !t8 : 1));
-            int v = 0;
-            if (en) {
-                // MB P of the edge: the left / upper MB for edge 0, else this MB
-                const int p_flags = e == 0 ? (hor ? U.flags : L.flags) : q.flags;
-                const int p_cbp = e == 0 ? (hor ? U.cbp_blks : L.cbp_blks) : q.cbp_blks;
-                const int special = special_q || (e == 0 && special_slice(hor ? u_type : l_type));
-                const int intra = q_intra || (p_flags & H264R_MBF_INTRA) != 0;
-                const int blkQ = 4 * by + bx;
-                const int blkP = hor ? (e == 0 ? 12 + bx : blkQ - 4) : (e == 0 ? blkQ + 3 : blkQ - 1);
-                const int coded = ((q.cbp_blks >> blkQ) & 1) || ((p_cbp >> blkP) & 1);
-                const int same_part = e > 0 && (q.mb_type == H264R_P_16x16 ||
-                                                q.mb_type == (hor ? H264R_P_8x16 : H264R_P_16x8));
-                if (!hor) {
-                    if (special) v = e == 0 ? 4 : 3;
-                    else if (e > 0 && pskip) v = 0;
-                    else if (e == 0 && intra) v = 4;
-                    else if (intra) v = 3;
-                    else if (coded) v = 2;
-                    else if (same_part) v = 0;
-                    else v = bs_compare(mq, motion_of(l0, l1));
-                } else {
-                    if (e == 0 && (special || intra)) v = 4;
-                    else if (special || intra) v = 3;
-                    else if (e > 0 && pskip) v = 0;
-                    else if (coded) v = 2;
-                    else if (same_part) v = 0;
-                    else v = bs_compare(mq, motion_of(u0, u1));
-                }
-            }
-            out->bs[hor * 16 + e * 4 + s] = (uint8_t)v;
-        }
-        if (blk < 9) {                                              // edge parameters
-            const int pl = blk / 3, which = blk - pl * 3;
-            const int py = which == 0 ? L.qp_y : (which == 1 ? U.qp_y : q.qp_y);
-            const int pc0 = which == 0 ? L.qp_c[0] : (which == 1 ? U.qp_c[0] : q.qp_c[0]);
-            const int pc1 = which == 0 ? L.qp_c[1] : (which == 1 ? U.qp_c[1] : q.qp_c[1]);
-            const int qp = pl == 0 ? py : (pl == 1 ? pc0 : pc1);
-            const int qq = pl == 0 ? q.qp_y : (pl == 1 ? q.qp_c[0] : q.qp_c[1]);
-            out->par[blk] = edge_word(qp, qq, offa, offb);
-        }
-    }
-
+    dbinfo_block(b, g, pic, aa, valid, blk, S, q, m0, m1, qsh, dbout);
 }
 
 }  // namespace h264r
