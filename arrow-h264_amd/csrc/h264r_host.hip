@@ -34,7 +34,7 @@ extern "C" __global__ void k_inter_sp(h264r_batch b, int2 rows, const int* sp_fl
 extern "C" __global__ void k_untile(h264r_batch b, int2 rows, const uint8_t* recon);
 extern "C" __global__ void k_intra_pic(h264r_batch b, int* sync, int* err, const uint16_t* lvl, int lmax, int2 rows,
                                       int gstep, uint8_t* recon);
-extern "C" __global__ void k_level(h264r_batch b, uint16_t* lvl, int* lvsync, int* lcount, int2 rows);
+extern "C" __global__ void k_level(h264r_batch b, uint16_t* lvl, int* lvsync, int* lcount, int2 rows, int deep_cut);
 extern "C" __global__ void k_level_scan(const int* lcount, int* lbase);
 extern "C" __global__ void k_level_scatter(h264r_batch b, const uint16_t* lvl, const int* lbase, int* lcursor,
                                            uint32_t* list, int2 rows);
@@ -517,7 +517,8 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
             int* lcount = X.d_lcnt;
             int* lbase = lcount + (LEVEL_LISTS + 2);
             int* lcursor = lbase + (LEVEL_LISTS + 2);
-            hipLaunchKernelGGL(k_level, dim3(P), dim3(64 * ((HB + 63) / 64)), 0, s, b, lvl, lvsync, lcount, rows);
+            // pictures deeper than 4 x lmax levels (all-intra) are left to the walk whole
+            hipLaunchKernelGGL(k_level, dim3(P), dim3(64 * ((HB + 63) / 64)), 0, s, b, lvl, lvsync, lcount, rows, 4 * lmax);
             HIP_OK(hipGetLastError());
             hipLaunchKernelGGL(k_level_scan, dim3(1), dim3(1024), 0, s, (const int*)lcount, lbase);
             HIP_OK(hipGetLastError());

@@ -181,7 +181,8 @@ extern "C" __global__ __launch_bounds__(64 * H264R_WALK_ROWS, H264R_WALK_WAVES) 
 // step t-1.  Each row keeps its last four levels in an LDS ring.
 // lcount[L] (L = 1 .. H264R_LEVEL_LISTS): intra MBs of level L over the batch (zeroed per
 // batch); k_level_lists turns them into one MB list per level.
-extern "C" __global__ __launch_bounds__(1024) void k_level(h264r_batch b, uint16_t* lvl, int* lvsync, int* lcount, int2 rows)
+extern "C" __global__ __launch_bounds__(1024) void k_level(h264r_batch b, uint16_t* lvl, int* lvsync, int* lcount, int2 rows,
+                                                          int deep_cut)
 {
     __shared__ uint64_t bits[H264R_LEVEL_MAX_MBS / 64];   // intra (not PCM) MBs of the picture
     __shared__ uint16_t ring[1024][4];
@@ -229,6 +230,17 @@ extern "C" __global__ __launch_bounds__(1024) void k_level(h264r_batch b, uint16
         __syncthreads();
     }
     for (int d = 32; d >= 1; d >>= 1) deepest = max(deepest, __shfl_xor(deepest, d));
+    // a picture deeper than deep_cut (all-intra: level x + 2y + 1) goes to the walk whole:
+    // its few MBs per level would only make k_intra_levels wait at its grid barriers
+    __shared__ int pdeep;
+    if (tid == 0) pdeep = 0;
+    __syncthreads();
+    if (lane == 0 && deepest) atomicMax(&pdeep, deepest);
+    __syncthreads();
+    if (pdeep > deep_cut) {
+        for (int m = R0 * g.wmb + tid; m < mend; m += blockDim.x) lvl[(size_t)pic * g.nmb + m] = 0xFFFF;
+        return;
+    }
     if (lane == 0 && deepest) atomicMax(&lvsync[1], deepest);
     for (int i = threadIdx.x + 1; i <= H264R_LEVEL_LISTS; i += blockDim.x)
         if (hist[i]) atomicAdd(&lcount[i], hist[i]);

@@ -546,7 +546,8 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
             return;
         }
 
-        // ---- residual inputs, issued before motion compensation
+        // ---- residual inputs: issued before motion compensation, or (H264R_RES_LATE) after
+        // it, so that they are not live across it (30 VGPRs)
         const int cbpl = q.cbp & 15, cbpc = q.cbp >> 4;
         const int t8 = (q.flags & H264R_MBF_T8x8) != 0;
         const h264r_quant* __restrict__ qt = &b.quant[pic];
@@ -555,42 +556,47 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
         const int loff = b8_offset(q.cbp, b8);
         uint4 lev[2] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
         uint4 lsc[2] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
-        if (loff >= 0) {
-            if (!t8) {                      // 4x4 block: 16 raster levels
-                const uint4* p = reinterpret_cast<const uint4*>(lv + loff + ((by & 1) * 2 + (bx & 1)) * 16);
-                lev[0] = p[0]; lev[1] = p[1];
-                const uint4* s = reinterpret_cast<const uint4*>(&qt->scale4x4[1][0][qpl % 6][0]);
-                lsc[0] = s[0]; lsc[1] = s[1];
-            } else {                        // my 4x4 quadrant of the 8x8 block: rows (by&1)*4.., cols (bx&1)*4..
-                const int16_t* p = lv + loff + (by & 1) * 32 + (bx & 1) * 4;
-                const int16_t* s = &qt->scale8x8[1][0][qpl % 6][(by & 1) * 32 + (bx & 1) * 4];
-                const uint2 r0 = ld8(p), r1 = ld8(p + 8), r2 = ld8(p + 16), r3 = ld8(p + 24);
-                lev[0] = make_uint4(r0.x, r0.y, r1.x, r1.y); lev[1] = make_uint4(r2.x, r2.y, r3.x, r3.y);
-                const uint2 s0 = ld8(s), s1 = ld8(s + 8), s2 = ld8(s + 16), s3 = ld8(s + 24);
-                lsc[0] = make_uint4(s0.x, s0.y, s1.x, s1.y); lsc[1] = make_uint4(s2.x, s2.y, s3.x, s3.y);
-            }
-        }
         // chroma: my 2x2 quadrant of chroma 4x4 block cb of each plane + the plane's 4 DC levels
         const int cb = (by >> 1) * 2 + (bx >> 1), cr = (by & 1) * 2, cc = (bx & 1) * 2;
         uint32_t clev[2][2] = {{0, 0}, {0, 0}}, csc[2][2] = {{0, 0}, {0, 0}};
         uint2 cdc[2] = {make_uint2(0, 0), make_uint2(0, 0)};
         int cdcs[2] = {0, 0};
-        if (cbpc) {
-            const LevelOffs lo = level_offsets(q);
+        auto load_residual = [&]() {
+            if (loff >= 0) {
+                if (!t8) {                      // 4x4 block: 16 raster levels
+                    const uint4* p = reinterpret_cast<const uint4*>(lv + loff + ((by & 1) * 2 + (bx & 1)) * 16);
+                    lev[0] = p[0]; lev[1] = p[1];
+                    const uint4* s = reinterpret_cast<const uint4*>(&qt->scale4x4[1][0][qpl % 6][0]);
+                    lsc[0] = s[0]; lsc[1] = s[1];
+                } else {                        // my 4x4 quadrant of the 8x8 block: rows (by&1)*4.., cols (bx&1)*4..
+                    const int16_t* p = lv + loff + (by & 1) * 32 + (bx & 1) * 4;
+                    const int16_t* s = &qt->scale8x8[1][0][qpl % 6][(by & 1) * 32 + (bx & 1) * 4];
+                    const uint2 r0 = ld8(p), r1 = ld8(p + 8), r2 = ld8(p + 16), r3 = ld8(p + 24);
+                    lev[0] = make_uint4(r0.x, r0.y, r1.x, r1.y); lev[1] = make_uint4(r2.x, r2.y, r3.x, r3.y);
+                    const uint2 s0 = ld8(s), s1 = ld8(s + 8), s2 = ld8(s + 16), s3 = ld8(s + 24);
+                    lsc[0] = make_uint4(s0.x, s0.y, s1.x, s1.y); lsc[1] = make_uint4(s2.x, s2.y, s3.x, s3.y);
+                }
+            }
+            if (cbpc) {
+                const LevelOffs lo = level_offsets(q);
     #pragma unroll
-            for (int pl = 0; pl < 2; ++pl) {
-                const int qpc = q.qp_scaled[1 + pl];
-                cdc[pl] = ld8(lv + lo.cdc + pl * 4);
-                cdcs[pl] = qt->scale4x4[1][1 + pl][qpc % 6][0];
-                if (cbpc == 2) {
+                for (int pl = 0; pl < 2; ++pl) {
+                    const int qpc = q.qp_scaled[1 + pl];
+                    cdc[pl] = ld8(lv + lo.cdc + pl * 4);
+                    cdcs[pl] = qt->scale4x4[1][1 + pl][qpc % 6][0];
+                    if (cbpc == 2) {
     #pragma unroll
-                    for (int r = 0; r < 2; ++r) {
-                        clev[pl][r] = *reinterpret_cast<const uint32_t*>(lv + lo.cac + pl * 64 + cb * 16 + (cr + r) * 4 + cc);
-                        csc[pl][r] = *reinterpret_cast<const uint32_t*>(&qt->scale4x4[1][1 + pl][qpc % 6][(cr + r) * 4 + cc]);
+                        for (int r = 0; r < 2; ++r) {
+                            clev[pl][r] = *reinterpret_cast<const uint32_t*>(lv + lo.cac + pl * 64 + cb * 16 + (cr + r) * 4 + cc);
+                            csc[pl][r] = *reinterpret_cast<const uint32_t*>(&qt->scale4x4[1][1 + pl][qpc % 6][(cr + r) * 4 + cc]);
+                        }
                     }
                 }
             }
-        }
+        };
+#ifndef H264R_RES_LATE
+        load_residual();
+#endif
 
         // ---- prediction
         const int r0 = (int8_t)(m0.y & 255), r1 = (int8_t)(m1.y & 255);
@@ -689,6 +695,9 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
         for (int i = 0; i < 4; ++i) predY[i] = wp_combine4(wpp[0], wp_mode, dir, pY[0][i], pY[1][i]);
     #pragma unroll
         for (int pl = 0; pl < 2; ++pl) predC[pl] = wp_combine4(wpp[1 + pl], wp_mode, dir, pC[0][pl], pC[1][pl]);
+#ifdef H264R_RES_LATE
+        load_residual();
+#endif
 
         if constexpr (SP) {
             // ---- itrans_sp of this lane's 4x4 block (:1132-1187): the prediction is
