@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "h264r.h"
+#include "launch_cfg.h"
 
 #ifndef H264R_WALK_ROWS
 #define H264R_WALK_ROWS 8       // k_intra_pic: MB rows per band = waves per workgroup (k_picture.hip)
@@ -472,13 +473,16 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
     int* sync = X.d_sync;
     Timed whole(timed_whole ? c : nullptr, 3, s);
     if (c->timing && timed_whole) c->timed_launches++;
-    // the deblocking records: inside k_inter4 (H264R_DBINFO=0), k_dbinfo before k_inter4r on
-    // this stream (1), or k_dbinfo on the scratch's side stream beside the reconstruction
-    // kernels, joined before deblocking (2)
+    // the deblocking records: k_dbinfo before k_inter4r on this stream (H264R_DBINFO=1, the
+    // default: k_inter4r then fits 4 waves/SIMD), inside k_inter4 (0), or k_dbinfo on the
+    // scratch's side stream beside the reconstruction kernels, joined before deblocking (2)
+    // (profiles/r03_f_dbinfo_ab.txt, r03_h_inter_ab.txt)
     const char* dbe = getenv("H264R_DBINFO");
-    const int db_mode = dbe ? atoi(dbe) : 0;
+    const int db_mode = dbe ? atoi(dbe) : 1;
     const int groups = (W * HB + 15) / 16;
-    const dim3 igrid(8 * ((groups + 7) / 8), P);
+    // groups per workgroup (launch_cfg.h), 8 XCD bands (k_recon.hip inter4_groups)
+    const dim3 igrid(8 * ((groups + 8 * H264R_INTER_GROUPS - 1) / (8 * H264R_INTER_GROUPS)), P);
+    const dim3 dgrid(8 * ((groups + 8 * H264R_DBINFO_GROUPS - 1) / (8 * H264R_DBINFO_GROUPS)), P);
     if (db_mode == 2) {
         if (!X.side) {
             HIP_OK(hipStreamCreateWithFlags(&X.side, hipStreamNonBlocking));
@@ -487,7 +491,7 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
         }
         HIP_OK(hipEventRecord(X.ev_side_start, s));                 // the previous launch's deblocking read dbinfo
         HIP_OK(hipStreamWaitEvent(X.side, X.ev_side_start, 0));
-        hipLaunchKernelGGL(k_dbinfo, igrid, dim3(256), 0, X.side, b, dbinfo, rows);
+        hipLaunchKernelGGL(k_dbinfo, dgrid, dim3(256), 0, X.side, b, dbinfo, rows);
         HIP_OK(hipGetLastError());
         HIP_OK(hipEventRecord(X.ev_side_done, X.side));
     }
@@ -496,7 +500,7 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
         Timed t(c, 0, s);
         int* sp_flag = sync + 1 + (size_t)P * H + 4;
         if (db_mode == 1) {
-            hipLaunchKernelGGL(k_dbinfo, igrid, dim3(256), 0, s, b, dbinfo, rows);
+            hipLaunchKernelGGL(k_dbinfo, dgrid, dim3(256), 0, s, b, dbinfo, rows);
             HIP_OK(hipGetLastError());
         }
         if (db_mode == 0) hipLaunchKernelGGL(k_inter4, igrid, dim3(256), 0, s, b, dbinfo, rows, sp_flag, recon);

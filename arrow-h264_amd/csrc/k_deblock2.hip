@@ -512,9 +512,11 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2
                 else __builtin_amdgcn_raw_buffer_store_b128(w, hrs, pair_off(rec_out, x, q, k), 0, AUX_SC1);
             }
     }
-    TRACE(if (lane == 0 && ticket < (1 << 16)) {
-        h264r_db2_trace[ticket][0] = tr_start; h264r_db2_trace[ticket][1] = __builtin_amdgcn_s_memrealtime();
-        for (int i = 0; i < 4; ++i) h264r_db2_trace[ticket][2 + i] = tph[i];
-        h264r_db2_trace[ticket][6] = (unsigned long long)W; })
+    // (indexed row-major over (row, group) whatever the XCD-local ticket numbering)
+    TRACE(const int tix = ry * ngroups + grp;
+          if (lane == 0 && tix < (1 << 16)) {
+        h264r_db2_trace[tix][0] = tr_start; h264r_db2_trace[tix][1] = __builtin_amdgcn_s_memrealtime();
+        for (int i = 0; i < 4; ++i) h264r_db2_trace[tix][2 + i] = tph[i];
+        h264r_db2_trace[tix][6] = (unsigned long long)W; })
     }
 }

@@ -6,13 +6,20 @@
 //          neighbours).  Motion is read as the parser left it ({mv, ref_idx} per list)
 //          and RefPicList[l][ref_idx] resolved to a DPB slot through an LDS copy of the
 //          picture's slice tables.
+#include "launch_cfg.h"
 #include "mb_inter4.h"
 
 using namespace h264r;
 
 // Grid (ceil(nmb / 16), pictures).
+// minimum waves per SIMD asked of the register allocator: k_inter4r 4 (<= 128 VGPRs, its
+// natural size with the residual loaded after the motion compensation), the fused
+// k_inter4 3 (<= 168)
 #ifndef H264R_INTER_WAVES
-#define H264R_INTER_WAVES 3                 // minimum waves per SIMD asked of the register allocator (<= 168 VGPRs)
+#define H264R_INTER_WAVES 4
+#endif
+#ifndef H264R_INTER4_WAVES
+#define H264R_INTER4_WAVES 3
 #endif
 // The workgroup's copy of the DPB plane table and of picture `pic`'s slice ref tables and
 // slice types.
@@ -39,8 +46,21 @@ DEV QuadTile* wave_tiles()
 #endif
 }
 
+// The 16-MB groups [grp, gend) of one k_inter4 / k_dbinfo workgroup: XCD-aware (below),
+// `per` (H264R_INTER_GROUPS / H264R_DBINFO_GROUPS, launch_cfg.h) consecutive groups of its
+// XCD's band per workgroup, so that the workgroup's LDS tables are filled once for several
+// groups.
+DEV bool inter4_groups(const Geom& g, int2 rows, int per, int& grp, int& gend)
+{
+    const int groups = (g.wmb * (rows.y - rows.x) + 15) / 16, gb = (groups + 7) / 8;
+    const int band = blockIdx.x & 7;
+    grp = band * gb + (blockIdx.x >> 3) * per;
+    gend = min(min(grp + per, (band + 1) * gb), groups);
+    return grp < gend;
+}
+
 // sp_flag: set when an inter MB of an SP slice was met (k_inter_sp then runs).
-// Grid (8 * ceil(groups / 8), pictures), XCD-aware: workgroups go round-robin to the 8
+// Grid (8 * ceil(groups / (8 * per)), pictures), XCD-aware: workgroups go round-robin to the 8
 // XCDs in launch order, so blockIdx.x % 8 is the XCD and it takes the 16-MB groups of band
 // blockIdx.x % 8 (one eighth of the MB rows) of every picture: an XCD's motion
 // compensation reads only its band of the reference pictures (+ the MV reach), which its
@@ -51,19 +71,29 @@ DEV void inter4_kernel(const h264r_batch& b, DbInfo* dbinfo, int2 rows, int* sp_
 {
     const int pic = blockIdx.y;
     const Geom g = make_geom(b.width_mbs, b.height_mbs);
-    const int groups = (g.wmb * (rows.y - rows.x) + 15) / 16, gb = (groups + 7) / 8;
-    const int grp = (blockIdx.x & 7) * gb + (blockIdx.x >> 3);
-    if (grp >= groups) return;
-    const int lane = threadIdx.x & 63;
-    const int a0 = rows.x * g.wmb + (grp * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) * 4;
+    int grp, gend;
+    if (!inter4_groups(g, rows, H264R_INTER_GROUPS, grp, gend)) return;
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int aend = rows.y * g.wmb;
-    const Inter4Pre pre = inter4_pre(b, g, pic, a0, aend, lane);
+    int a0 = rows.x * g.wmb + (grp * 4 + wave) * 4;
+    Inter4Pre pre = inter4_pre(b, g, pic, a0, aend, lane);
     inter4_lds(b, pic, S);
     __syncthreads();
-    if (a0 >= aend) return;
-    inter4_mbs<false, DB>(b, g, pic, a0, aend, lane, dbinfo + (size_t)pic * g.nmb, S, sp_flag, pre, wave_tiles(), recon);
+    for (;;) {
+        if (a0 >= aend) return;
+        // the lane, opaque per group: what derives from it is recomputed per group, not
+        // hoisted out of the loop and kept live across it (that spilled 144 B per lane)
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        inter4_mbs<false, DB>(b, g, pic, a0, aend, ln, dbinfo + (size_t)pic * g.nmb, S, sp_flag, pre, wave_tiles(), recon);
+        if (++grp >= gend) return;
+        a0 = rows.x * g.wmb + (grp * 4 + wave) * 4;
+        int ln2 = lane;
+        asm volatile("" : "+v"(ln2));
+        pre = inter4_pre(b, g, pic, a0, aend, ln2);
+    }
 }
-extern "C" __global__ __launch_bounds__(256, H264R_INTER_WAVES) void k_inter4(h264r_batch b, DbInfo* dbinfo, int2 rows,
+extern "C" __global__ __launch_bounds__(256, H264R_INTER4_WAVES) void k_inter4(h264r_batch b, DbInfo* dbinfo, int2 rows,
                                                                              int* sp_flag, uint8_t* recon)
 {
     __shared__ Inter4Lds S;
@@ -84,23 +114,24 @@ extern "C" __global__ __launch_bounds__(256) void k_dbinfo(h264r_batch b, DbInfo
     __shared__ Inter4Lds S;
     const int pic = blockIdx.y;
     const Geom g = make_geom(b.width_mbs, b.height_mbs);
-    const int groups = (g.wmb * (rows.y - rows.x) + 15) / 16, gb = (groups + 7) / 8;
-    const int grp = (blockIdx.x & 7) * gb + (blockIdx.x >> 3);
-    if (grp >= groups) return;
-    const int lane = threadIdx.x & 63;
-    const int a0 = rows.x * g.wmb + (grp * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6)) * 4;
+    int grp, gend;
+    if (!inter4_groups(g, rows, H264R_DBINFO_GROUPS, grp, gend)) return;
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int aend = rows.y * g.wmb;
-    const Inter4Pre pre = inter4_pre(b, g, pic, a0, aend, lane);
     inter4_lds(b, pic, S);
     __syncthreads();
-    if (a0 >= aend) return;
-    const int a = a0 + (lane >> 4);
-    const bool valid = a < aend;
-    const int aa = valid ? a : aend - 1;
     const h264r_slice* slices = b.slices + (size_t)pic * b.slice_stride;
-    const uint2 m0 = motion_word(pre.mv[0], pre.ri[0], slices, S, pre.q.slice, 0);
-    const uint2 m1 = motion_word(pre.mv[1], pre.ri[1], slices, S, pre.q.slice, 1);
-    dbinfo_block(b, g, pic, aa, valid, lane & 15, S, pre.q, m0, m1, pre.qsh, dbinfo + (size_t)pic * g.nmb);
+    for (; grp < gend; ++grp) {
+        const int a0 = rows.x * g.wmb + (grp * 4 + wave) * 4;
+        if (a0 >= aend) return;
+        const Inter4Pre pre = inter4_pre(b, g, pic, a0, aend, lane);
+        const int a = a0 + (lane >> 4);
+        const bool valid = a < aend;
+        const int aa = valid ? a : aend - 1;
+        const uint2 m0 = motion_word(pre.mv[0], pre.ri[0], slices, S, pre.q.slice, 0);
+        const uint2 m1 = motion_word(pre.mv[1], pre.ri[1], slices, S, pre.q.slice, 1);
+        dbinfo_block(b, g, pic, aa, valid, lane & 15, S, pre.q, m0, m1, pre.qsh, dbinfo + (size_t)pic * g.nmb);
+    }
 }
 
 // k_inter_sp: the inter MBs of SP slices (inverse_transform_sp), after k_inter4.  A

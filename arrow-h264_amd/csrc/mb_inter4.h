@@ -546,8 +546,10 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
             return;
         }
 
-        // ---- residual inputs: issued before motion compensation, or (H264R_RES_LATE) after
-        // it, so that they are not live across it (30 VGPRs)
+        // ---- residual inputs: issued after the motion compensation, so that they are not
+        // live across it (30 VGPRs: k_inter4r fits 128 VGPRs = 4 waves/SIMD; config 3
+        // 475 -> 493 M MB/s with k_dbinfo, profiles/r03_h_inter_ab.txt), or before it
+        // (H264R_RES_EARLY)
         const int cbpl = q.cbp & 15, cbpc = q.cbp >> 4;
         const int t8 = (q.flags & H264R_MBF_T8x8) != 0;
         const h264r_quant* __restrict__ qt = &b.quant[pic];
@@ -594,7 +596,7 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
                 }
             }
         };
-#ifndef H264R_RES_LATE
+#ifdef H264R_RES_EARLY
         load_residual();
 #endif
 
@@ -695,7 +697,7 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
         for (int i = 0; i < 4; ++i) predY[i] = wp_combine4(wpp[0], wp_mode, dir, pY[0][i], pY[1][i]);
     #pragma unroll
         for (int pl = 0; pl < 2; ++pl) predC[pl] = wp_combine4(wpp[1 + pl], wp_mode, dir, pC[0][pl], pC[1][pl]);
-#ifdef H264R_RES_LATE
+#ifndef H264R_RES_EARLY
         load_residual();
 #endif
 
