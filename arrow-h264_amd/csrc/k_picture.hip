@@ -24,6 +24,29 @@
 
 using namespace h264r;
 
+#ifdef H264R_TRACE_INTRA
+// per-MB trace (trace builds only: tools/trace_intra.py): {start, end} in 100 MHz ticks,
+// [2] = level << 32 | mb_type (k_intra_levels) or 1 << 31 | wait ticks << 8 | mb_type (the
+// walk: the wait for the row above, then the MB), [3] = phase cycles / 16 (16 bits each)
+__device__ unsigned long long h264r_intra_trace[1 << 20][4];
+__device__ unsigned h264r_intra_trace_n;
+DEV void intra_trace_put(unsigned long long t0, unsigned long long w, const unsigned long long (&tph)[5], unsigned long long c0, int lane)
+{
+    const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+    if (lane) return;
+    const unsigned slot = atomicAdd(&h264r_intra_trace_n, 1u);
+    if (slot >= (1u << 20)) return;
+    unsigned long long ph = 0, prev = c0;
+    for (int q = 0; q < 4; ++q) {
+        ph |= (unsigned long long)min((tph[q] - prev) >> 4, 65535ull) << (16 * q);
+        prev = tph[q];
+    }
+    h264r_intra_trace[slot][0] = t0; h264r_intra_trace[slot][1] = t1;
+    h264r_intra_trace[slot][2] = w;
+    h264r_intra_trace[slot][3] = ph;
+}
+#endif
+
 namespace {
 
 #ifndef H264R_WALK_ROWS
@@ -136,12 +159,26 @@ DEV void walk_ticket(const h264r_batch& b, int* sync, int* err, Scratch* scratch
     while (x < g.wmb && ok) {
         // gstep < 0: the host's wait test (H264R_DBG_WAIT_TEST) -- a need no row ever meets
         const int need = gstep < 0 ? g.wmb + 1 : min(x + 2, g.wmb);
+#ifdef H264R_TRACE_INTRA
+        const unsigned long long t_wait0 = __builtin_amdgcn_s_memrealtime();
+#endif
         if (r > R0 && need > seen) {
             if (wave == 0) ok = wait_for<true>(&gprog[r - 1], need, err, seen);
             else ok = wait_for<false>(&lprog[wave - 1], need, err, seen);
         }
         if (!ok) break;
+#ifdef H264R_TRACE_INTRA
+        {
+            const unsigned long long tw = __builtin_amdgcn_s_memrealtime(), c0 = __builtin_amdgcn_s_memtime();
+            unsigned long long tph[5] = {c0, c0, c0, c0, c0};
+            intra_mb2(b, g, pic, x, r, lane, S, recon, tph);
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            const unsigned long long wait = min((tw - t_wait0) , 0xFFFFFull);
+            intra_trace_put(t_wait0, (1ull << 31) | (wait << 8) | (unsigned)row[x].mb_type, tph, c0, lane);
+        }
+#else
         intra_mb2(b, g, pic, x, r, lane, S, recon);
+#endif
         dirty = true;
         x = next_intra(x + 1);
         publish(x, false);
@@ -348,8 +385,6 @@ DEV bool grid_barrier(int* bar, int target, int* err)
 }
 
 #ifdef H264R_TRACE_INTRA
-__device__ unsigned long long h264r_intra_trace[1 << 20][4];
-__device__ unsigned h264r_intra_trace_n;
 extern "C" __global__ void k_intra_trace_dump(unsigned long long* out, unsigned* n)
 {
     const unsigned cnt = h264r_intra_trace_n < (1u << 20) ? h264r_intra_trace_n : (1u << 20);

@@ -426,8 +426,13 @@ DEV void dbinfo_block(const h264r_batch& b, const Geom& g, int pic, int aa, bool
     const h264r_mb U = mb_lane(&mbs[hasU ? aa - g.wmb : aa]);
     // the neighbour block belongs to this MB or to the left / upper one (its slice resolves it)
     const int lsl = bx > 0 ? q.slice : L.slice, usl = by > 0 ? q.slice : U.slice;
-    const uint2 l0 = block_motion(b, slices, S, mbase + li, lsl, 0), l1 = block_motion(b, slices, S, mbase + g.motion_plane + li, lsl, 1);
-    const uint2 u0 = block_motion(b, slices, S, mbase + ui, usl, 0), u1 = block_motion(b, slices, S, mbase + g.motion_plane + ui, usl, 1);
+    // the neighbours' motion matters only to an inter MB (an intra one has bS 3 / 4 on every
+    // edge): a wave of intra MBs (all-intra pictures) skips its loads
+    uint2 l0 = make_uint2(0, 0), l1 = l0, u0 = l0, u1 = l0;
+    if (__builtin_amdgcn_readfirstlane(__any(!mb_is_intra(q)))) {
+        l0 = block_motion(b, slices, S, mbase + li, lsl, 0); l1 = block_motion(b, slices, S, mbase + g.motion_plane + li, lsl, 1);
+        u0 = block_motion(b, slices, S, mbase + ui, usl, 0); u1 = block_motion(b, slices, S, mbase + g.motion_plane + ui, usl, 1);
+    }
     const int l_type = slice_type_of(slices, S, L.slice), u_type = slice_type_of(slices, S, U.slice);
     // ---- deblocking record (Deblock::strength deblock.cc:78-289): this lane's
     // left edge (vertical edge bx, segment by) and top edge (horizontal edge by,

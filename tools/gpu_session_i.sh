@@ -8,4 +8,5 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 180 --timeout
 timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err &&
 tools/stats.sh $O/stats --steps 5 --warmup 1 --no-cpu --no-verify --latency-pictures 0 &&
 H264R_LIB=varlib/trace/libh264r.so timeout -k 10 200 python tools/trace_deblock.py 1024 8 > $O/trace_db2_1024.txt 2>&1 &&
-tools/pmc.sh $O/pmc3 --config 3 --batch 256 --steps 3 --warmup 1 --no-cpu --no-verify --latency-pictures 0
+tools/pmc.sh $O/pmc3 --config 3 --batch 256 --steps 3 --warmup 1 --no-cpu --no-verify --latency-pictures 0 &&
+H264R_LIB=varlib/trace_intra/libh264r.so timeout -k 10 200 python tools/trace_intra.py 120 2 > $O/trace_intra_c2.txt 2>&1

@@ -1,5 +1,7 @@
 #!/usr/bin/env python3
-"""Diagnostic: per-MB latency trace of k_intra_levels (lib built with -DH264R_TRACE_INTRA)."""
+"""Diagnostic: per-MB latency trace of k_intra_levels and the walk k_intra_pic (lib built
+with -DH264R_TRACE_INTRA):
+    H264R_LIB=<trace lib> python tools/trace_intra.py [pictures] [config]"""
 import ctypes as C
 import os
 import sys
@@ -14,7 +16,8 @@ from h264r import batch as B, synth  # noqa: E402
 
 L = h264r.lib()
 W, H, n = 120, 68, int(sys.argv[1]) if len(sys.argv) > 1 else 256
-cfg = synth.default_cfg(L, 3, W, H)
+config = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+cfg = synth.default_cfg(L, config, W, H)
 pics = [synth.picture(L, cfg, i) for i in range(n)]
 refs = synth.refpics(L, cfg)
 dec = h264r.Decoder(0, W, H)
@@ -29,10 +32,15 @@ L.h264r_trace_intra_dump(out.ctypes.data_as(C.c_void_p), C.byref(cnt))
 t = out[: cnt.value]
 t0 = t[:, 0].astype(np.int64)
 dur = (t[:, 1].astype(np.int64) - t0) / 100.0     # us (100 MHz)
-lvl = (t[:, 2] >> 32).astype(np.int64)
-typ = (t[:, 2] & 0xFFFFFFFF).astype(np.int64)
+walk = ((t[:, 2] >> 31) & 1).astype(bool) & ((t[:, 2] >> 32) == 0)
+lvl = np.where(walk, -1, (t[:, 2] >> 32).astype(np.int64))
+typ = np.where(walk, (t[:, 2] & 0xFF).astype(np.int64), (t[:, 2] & 0xFFFFFFFF).astype(np.int64))
+wait = np.where(walk, ((t[:, 2] >> 8) & 0xFFFFF).astype(np.int64) / 100.0, 0.0)
 start = (t0 - t0.min()) / 100.0
-print("MBs", cnt.value)
+print("MBs", cnt.value, "walk MBs", int(walk.sum()))
+if walk.any():
+    print(f"walk: span {(start[walk] + dur[walk]).max():.1f} us, per MB {dur[walk].mean():.2f} us of which waiting for "
+          f"the row above {wait[walk].mean():.2f} us")
 for Lv in np.unique(lvl):
     m = lvl == Lv
     print(f"level {Lv}: n={m.sum()} start {start[m].min():.1f}..{start[m].max():.1f} us  end {(start[m] + dur[m]).max():.1f}  dur mean {dur[m].mean():.2f} p50 {np.median(dur[m]):.2f} max {dur[m].max():.2f}")
