@@ -47,10 +47,13 @@ extern "C" __global__ void k_deblock(h264r_batch b, const h264r::DbInfo* dbinfo,
                                      int* sync, int* err, uint32_t epoch, int2 rows, int nx, uint8_t* recon);
 extern "C" __global__ void k_deblock2(h264r_batch b, const h264r::DbInfo* dbinfo, uint64_t* hb,
                                       int* sync, int* err, uint32_t epoch, int2 rows, int nx, const uint8_t* recon);
+extern "C" __global__ void k_deblock3(h264r_batch b, const h264r::DbInfo* dbinfo, uint64_t* hb,
+                                      int* sync, int* err, uint32_t epoch, int2 rows, int nx, const uint8_t* recon);
 constexpr size_t DBINFO_BYTES = 80;
 constexpr size_t HANDOFF_BYTES = 256;   // one tagged record (32 x {dword, epoch}) per MB
 constexpr size_t HANDOFF2_BYTES = 384;  // k_deblock2: 2 row slots x 24 x {dword, tag} per MB column
 constexpr int DEBLOCK2_UNITS = 16;      // k_deblock2: pictures per wave (mb_deblock.h)
+constexpr int DEBLOCK3_UNITS = 8;       // k_deblock3: pictures per wave (k_deblock3.hip)
 
 namespace {
 
@@ -575,11 +578,15 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
         }
         if (by_rows)
         {
-            // k_deblock2 keeps a 16-picture group on one XCD (g % nx): nx counters
-            int grid = ((P + DEBLOCK2_UNITS - 1) / DEBLOCK2_UNITS) * HB;
+            // k_deblock2 keeps a 16-picture group on one XCD (g % nx): nx counters;
+            // H264R_DEBLOCK3=1: k_deblock3, the same walk with 8 lanes per picture-row (A/B)
+            const char* d3e = getenv("H264R_DEBLOCK3");
+            const bool d3 = d3e && atoi(d3e) != 0;
+            const int units = d3 ? DEBLOCK3_UNITS : DEBLOCK2_UNITS;
+            int grid = ((P + units - 1) / units) * HB;
             const int nx = grid >= 64 * c->nxcc && !(c->debug & H264R_DBG_DEBLOCK_GLOBAL) ? c->nxcc : 1;
             grid = (grid + nx - 1) / nx * nx;
-            hipLaunchKernelGGL(k_deblock2, dim3(grid), dim3(64), 0, s, b, dbinfo,
+            hipLaunchKernelGGL(d3 ? k_deblock3 : k_deblock2, dim3(grid), dim3(64), 0, s, b, dbinfo,
                                reinterpret_cast<uint64_t*>(X.d_hb2), sync + 1 + (size_t)P * H + 5, c->d_err, ++X.epoch2, rows,
                                nx, (const uint8_t*)recon);
         }
