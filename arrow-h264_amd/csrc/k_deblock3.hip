@@ -74,9 +74,10 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(H
     const int ry = ticket / ngx, grp = (ticket - ry * ngx) * nx + xcc;
     int lane = threadIdx.x;
     asm volatile("" : "+v"(lane));
-    const int u = lane >> 3, q = lane & 7;
-    const int c4 = q >> 1, j = q & 1;                          // consumer lane of k_deblock2, column pair
-    const int p = q >> 2;                                      // my chroma plane
+    const int u = lane >> 3;
+    int q = lane & 7;
+    int c4 = q >> 1, j = q & 1;                                // consumer lane of k_deblock2, column pair
+    int p = q >> 2;                                            // my chroma plane
     const int y = R0 + ry;
     const int pic_raw = grp * UNITS3 + u;
     const bool active = pic_raw < b.num_pics;
@@ -199,6 +200,10 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(H
     __syncthreads();
     auto step = [&](const int x, auto odd_tag) {
         constexpr bool ODD = decltype(odd_tag)::value;
+        // the lane role, opaque per step: what derives from it (addresses) is recomputed per
+        // step, not kept live across the walk
+        asm volatile("" : "+v"(q));
+        c4 = q >> 1; j = q & 1; p = q >> 2;
         const int sc = x % 3, sl = (x + 2) % 3;
         // 1. the record of MB (x, y-1) (checked after the vertical edges)
         uint64_t rin[6];
