@@ -177,7 +177,13 @@ DEV void walk_ticket(const h264r_batch& b, int* sync, int* err, Scratch* scratch
             intra_trace_put(t_wait0, (1ull << 31) | (wait << 8) | (unsigned)row[x].mb_type, tph, c0, lane);
         }
 #else
-        intra_mb2(b, g, pic, x, r, lane, S, recon);
+        {
+            // the lane, opaque per MB: what derives from it is recomputed per MB, not hoisted
+            // out of the walk and kept live across it
+            int ln = lane;
+            asm volatile("" : "+v"(ln));
+            intra_mb2(b, g, pic, x, r, ln, S, recon);
+        }
 #endif
         dirty = true;
         x = next_intra(x + 1);
@@ -432,7 +438,9 @@ extern "C" __global__ __launch_bounds__(256, H264R_LVL_WAVES) void k_intra_level
                 }
             }
 #else
-            intra_mb2(b, g, pic, a % g.wmb, a / g.wmb, lane, scratch[wave], recon);
+            int ln = lane;                                 // opaque per MB (see walk_ticket)
+            asm volatile("" : "+v"(ln));
+            intra_mb2(b, g, pic, a % g.wmb, a / g.wmb, ln, scratch[wave], recon);
 #endif
         }
         if (L < top && !grid_barrier(&lvsync[0], L * (int)gridDim.x, err)) return;
