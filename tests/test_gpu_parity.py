@@ -158,6 +158,15 @@ def test_gpu_large_batch_xcd_groups(L, dec, cidx):
     _large_batch_vs_oracle(L, dec, cidx, 22, 18, 464)
 
 
+@pytest.mark.parametrize("cidx,W,H,n", [(3, 22, 18, 464), (2, 120, 32, 256), (4, 22, 18, 203)])
+def test_gpu_large_batch_deblock3(L, dec, cidx, W, H, n, monkeypatch):
+    """k_deblock3 (H264R_DEBLOCK3=1: the row walk with 8 lanes per picture-row, 8 pictures
+    per wave): XCD-local groups of 8 pictures, 1080p-wide rows, a ragged last group;
+    every picture checked."""
+    monkeypatch.setenv("H264R_DEBLOCK3", "1")
+    _large_batch_vs_oracle(L, dec, cidx, W, H, n)
+
+
 def test_gpu_batch_cif_p(L, dec):
     _batch_vs_oracle(L, dec, 3, 22, 18, 6)
 
