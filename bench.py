@@ -580,9 +580,14 @@ def main() -> int:
     kbytes = [int(k * (band[1] - band[0]) / H) for k in kbytes_all]
     # the library deblocks batches of >= H264R_DEBLOCK2_MIN pictures (default 192) with
     # k_deblock2, smaller ones with k_deblock (include/h264r.h)
-    dbk = "k_deblock2" if npics >= int(os.environ.get("H264R_DEBLOCK2_MIN", "192")) else "k_deblock"
-    names = ["k_inter4", "intra (k_level + k_intra_levels + k_intra_pic)", dbk]
-    kern_names = [["k_inter4"], ["k_level", "k_intra_levels", "k_intra_pic"], [dbk]]
+    # (k_deblock3 under H264R_DEBLOCK3=1); the deblocking records come from k_dbinfo before
+    # k_inter4r (H264R_DBINFO=1, the default) or from k_inter4 itself (0)
+    row_walk = "k_deblock3" if os.environ.get("H264R_DEBLOCK3", "0") not in ("", "0") else "k_deblock2"
+    dbk = row_walk if npics >= int(os.environ.get("H264R_DEBLOCK2_MIN", "192")) else "k_deblock"
+    inter_k = ["k_inter4"] if os.environ.get("H264R_DBINFO", "1") == "0" else ["k_dbinfo", "k_inter4r"]
+    names = [" + ".join(inter_k), "intra (k_level + k_intra_levels + k_intra_pic)", dbk]
+    kern_names = [inter_k + ["k_inter_sp"], ["k_level", "k_level_scan", "k_level_scatter", "k_intra_levels", "k_intra_pic"],
+                  [dbk]]
     # HBM traffic per launch sequence from the PMC counters of the committed profile run
     # (tools/pmc.sh + tools/pmc_summary.py --json): per-MB FETCH_SIZE (doubled, gfx950) +
     # WRITE_SIZE of every kernel of the sequence, times the MBs this rank processed
@@ -656,8 +661,8 @@ def main() -> int:
                        "rows_this_rank": list(band)},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": "h264r_decode_batch launch sequence (k_inter4, k_level, "
-                                   f"k_intra_levels, k_intra_pic, {dbk})",
+                         "kernel": f"h264r_decode_batch launch sequence ({', '.join(inter_k)}, k_inter_sp, "
+                                   f"k_level, k_intra_levels, k_intra_pic, {dbk})",
                          "kernel_ms": float(kern[3]), "kernel_algo_bytes": int(step_bytes),
                          "bytes_per_mb": step_bytes / max(mbs_rank, 1),
                          "numerator": "SURVEY 8(d) R+W summed exactly over the batch's MBs",
