@@ -399,6 +399,10 @@ static int level_launches()
 // records `inter_done` / `intra_done` for stage k+1.
 struct PipeHooks {
     hipEvent_t after_inter = nullptr, after_intra = nullptr, inter_done = nullptr, intra_done = nullptr;
+    // a stage of a pipelined batch: other kernels share the device, so no grid barrier (the
+    // level kernel's whole grid need not be resident while they run: the walk does every
+    // intra MB)
+    bool pipelined = false;
 };
 
 static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row0, int row1, Scratch& X,
@@ -452,7 +456,7 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
     // 10 ms bound -- the launch must drain and h264r_check report H264R_EDEVICE
     const bool wait_test = (c->debug & H264R_DBG_WAIT_TEST) != 0;
     if ((st = set_wait_bound(c, wait_test ? 1000000u : wait_bound_ticks()))) return st;
-    const bool levels = (size_t)W * H <= LEVEL_MAX_MBS && H <= 1024 && level_launches() > 0 &&
+    const bool levels = !hk.pipelined && (size_t)W * H <= LEVEL_MAX_MBS && H <= 1024 && level_launches() > 0 &&
                         !(c->debug & (H264R_DBG_INTRA_WALK | H264R_DBG_WAIT_TEST));
     if (levels && !c->levels_grid) {
         // every workgroup of the persistent level kernel must be resident at once: one
@@ -675,6 +679,7 @@ static int run_batch(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row0
         hk.after_intra = k ? c->ev_stage[1][k - 1] : nullptr;
         hk.inter_done = c->ev_stage[0][k];
         hk.intra_done = c->ev_stage[1][k];
+        hk.pipelined = true;
         int st = launch_all(c, sub_batch(b, p0, p1), sk, row0, row1, c->sc[k], hk, false);
         if (st) return st;
         HIP_OK(hipEventRecord(c->ev_join[k], sk));
