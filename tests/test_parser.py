@@ -1,0 +1,109 @@
+"""The repo's own CPU entropy / syntax stage (include/h264p.h,
+arrow-h264_amd/parser/h264p.cc).
+
+The parser replaces the reference's parser (interpret_*.cc, slice_*.cc, dpb.cc) on the
+caller side of the reconstruction ABI.  It is pinned two ways on the committed writer
+streams (tests/streams.py):
+
+* its decode reproduces the UNMODIFIED reference's per-frame MD5s (tests/golden/streams.json)
+  -- on the CPU implementation of the h264r ABI here (oracle/_cpu/h264dec_cpu), and on
+  MI355X through libh264r.so (arrow-h264_amd/lib/h264dec);
+* what it hands the ABI is byte-identical to what the reference parser + drop-in shim handed
+  it (the committed captures, tests/golden/streams/*.cap.npz): every MB record, level block,
+  motion entry, slice table, picture record, quantisation table and DPB slot.
+
+CABAC streams are refused with H264R_EUNSUPPORTED (the parser reads CAVLC).
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import _oracle as O
+import streams as S
+from h264r import output as OUT
+
+GOLD = S.golden()["streams"]
+CAVLC = [n for n, c in S.STREAMS.items() if not c.get("cabac")]
+CABAC = [n for n, c in S.STREAMS.items() if c.get("cabac")]
+CPU_DEC = os.path.join(S.ROOT, "oracle", "_cpu", "h264dec_cpu")
+GPU_DEC = os.path.join(S.ROOT, "arrow-h264_amd", "lib", "h264dec")
+
+
+def _cpu_dec():
+    O.build_oracle()
+    assert os.path.exists(CPU_DEC)
+    return CPU_DEC
+
+
+def _run(binary, name, out, env=None):
+    return subprocess.run([binary, "-i", S.stream_path(name), "-o", str(out)], capture_output=True, text=True,
+                          timeout=600, env=dict(os.environ, **(env or {})))
+
+
+@pytest.mark.parametrize("name", CAVLC)
+def test_parser_decodes_to_reference_md5s(name, tmp_path):
+    """Own parser + the CPU implementation of the reconstruction ABI == the unmodified
+    reference decoder, frame by frame (the reference harness's protocol,
+    script/test/model/__init__.py:119-183)."""
+    out = tmp_path / "out.yuv"
+    r = _run(_cpu_dec(), name, out)
+    assert r.returncode == 0, r.stderr[-800:]
+    assert OUT.digest_by_frames(str(out), S.STREAMS[name]["frames"]) == GOLD[name]["frame_md5"]
+
+
+@pytest.mark.parametrize("name", CAVLC)
+def test_parser_hands_the_abi_what_the_reference_parser_did(name, tmp_path):
+    """Every array the parser passes through the C ABI equals the capture of the reference
+    parser + shim (the same h264r_picture_begin / h264r_mb_submit / h264r_picture_end
+    traffic, in the same order, with the same DPB slots)."""
+    cap = tmp_path / "cap.bin"
+    r = _run(_cpu_dec(), name, tmp_path / "out.yuv", {"H264R_CAPTURE": str(cap)})
+    assert r.returncode == 0, r.stderr[-800:]
+    mine = S.read_capture_file(str(cap))
+    ref = S.load_capture(S.capture_path(name))
+    assert len(mine) == len(ref)
+    for i, (a, b) in enumerate(zip(mine, ref)):
+        assert a["keep"] == b["keep"], f"picture {i}: DPB slot"
+        for k in ("mbs", "levels", "mv", "ref_idx", "slices", "pic", "quant"):
+            if a[k].dtype.names:
+                for f in a[k].dtype.names:
+                    assert np.array_equal(a[k][f], b[k][f]), f"picture {i}: {k}.{f}"
+            else:
+                assert np.array_equal(a[k], b[k]), f"picture {i}: {k}"
+        assert a["plane_md5"] == b["plane_md5"], f"picture {i}: reconstructed planes"
+
+
+@pytest.mark.parametrize("name", CABAC[:1])
+def test_parser_refuses_cabac(name, tmp_path):
+    r = _run(_cpu_dec(), name, tmp_path / "out.yuv")
+    assert r.returncode != 0 and "CABAC" in r.stderr
+
+
+def test_parser_rejects_garbage(tmp_path):
+    """A stream whose slice names no PPS, and a truncated slice: errors, not crashes."""
+    bad = tmp_path / "bad.264"
+    bad.write_bytes(bytes([0, 0, 0, 1, 0x65, 0x88, 0x84, 0x00]))
+    r = subprocess.run([_cpu_dec(), "-i", str(bad), "-o", str(tmp_path / "o.yuv")], capture_output=True, text=True,
+                       timeout=60)
+    assert r.returncode != 0 and "h264dec:" in r.stderr
+    data = open(S.stream_path("bp_qcif_ippp"), "rb").read()
+    cut = tmp_path / "cut.264"
+    cut.write_bytes(data[: len(data) // 3])
+    r = subprocess.run([_cpu_dec(), "-i", str(cut), "-o", str(tmp_path / "o.yuv")], capture_output=True, text=True,
+                       timeout=60)
+    assert r.returncode != 0 and "h264dec:" in r.stderr
+
+
+# ---------------------------------------------------------------------------- MI355X
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", CAVLC)
+def test_gpu_parser_decodes_to_reference_md5s(name, tmp_path):
+    """The standalone decoder of the GPU box (no reference code anywhere): own parser +
+    libh264r.so on MI355X reproduces the unmodified reference's per-frame MD5s."""
+    assert os.path.exists(GPU_DEC), "arrow-h264_amd/lib/h264dec not built"
+    out = tmp_path / "out.yuv"
+    r = _run(GPU_DEC, name, out)
+    assert r.returncode == 0, r.stderr[-800:]
+    assert OUT.digest_by_frames(str(out), S.STREAMS[name]["frames"]) == GOLD[name]["frame_md5"]
