@@ -1,6 +1,6 @@
 // h264p.cc -- the repo's own CPU entropy / syntax stage.
 //
-// Annex-B stream -> NAL units -> SPS / PPS / slice headers -> CAVLC macroblock layer ->
+// Annex-B stream -> NAL units -> SPS / PPS / slice headers -> CAVLC / CABAC macroblock layer ->
 // per-picture staging -> the h264r reconstruction ABI (include/h264r.h), with the same
 // records, levels, motion, slice tables, quantisation tables and DPB slots the reference
 // parser + drop-in shim hand it (shim/decoder_h264r.cc).  Every function follows the
@@ -18,6 +18,7 @@
 #include <string>
 #include <vector>
 
+#include "cabac_tables.h"
 #include "cavlc_tables.h"
 #include "h264r.h"
 
@@ -145,6 +146,101 @@ const Tables& tables()
     static const Tables t;
     return t;
 }
+
+// ------------------------------------------------------------------ CABAC engine
+// cabac_engine_t (interpret.cc:308-432): 9-bit codIOffset read bit by bit from the RBSP, so
+// the bit position after a terminating bin is exactly where the spec puts it (I_PCM samples
+// and the slice end follow it); the contexts in the reference's layout (cabac_tables.h).
+struct Cabac {
+    Bits* b = nullptr;
+    uint32_t range = 510, offset = 0;
+    uint8_t state[CABAC_CONTEXTS], mps[CABAC_CONTEXTS];
+
+    // cabac_contexts_t::init (bitstream_cabac.cc:1215-1264): kind 0 = I, 1..3 = P idc, 4..6 = B idc
+    void init_contexts(int kind, int qp)
+    {
+        qp = clip3(0, 51, qp);
+        for (int i = 0; i < CABAC_CONTEXTS; ++i) {
+            const int pre = clip3(1, 126, ((CABAC_MN[kind][i][0] * qp) >> 4) + CABAC_MN[kind][i][1]);
+            if (pre <= 63) { state[i] = (uint8_t)(63 - pre); mps[i] = 0; }
+            else { state[i] = (uint8_t)(pre - 64); mps[i] = 1; }
+        }
+    }
+    void init_engine(Bits& bits)                       // cabac_engine_t::init: byte-align, 9 bits
+    {
+        b = &bits;
+        while (!b->aligned()) b->u(1);
+        range = 510;
+        offset = b->u(9);
+    }
+    int dec(int ctx)
+    {
+        const uint32_t lps = RANGE_LPS[state[ctx]][(range >> 6) & 3];
+        int bin;
+        range -= lps;
+        if (offset < range) {
+            bin = mps[ctx];
+            state[ctx] = TRANS_MPS[state[ctx]];
+        } else {
+            bin = !mps[ctx];
+            offset -= range;
+            range = lps;
+            if (state[ctx] == 0) mps[ctx] = (uint8_t)(1 - mps[ctx]);
+            state[ctx] = TRANS_LPS[state[ctx]];
+        }
+        while (range < 256) {
+            range <<= 1;
+            offset = (offset << 1) | b->u(1);
+        }
+        return bin;
+    }
+    int bypass()
+    {
+        offset = (offset << 1) | b->u(1);
+        if (offset < range) return 0;
+        offset -= range;
+        return 1;
+    }
+    int term()
+    {
+        range -= 2;
+        if (offset >= range) return 1;
+        while (range < 256) {
+            range <<= 1;
+            offset = (offset << 1) | b->u(1);
+        }
+        return 0;
+    }
+    // u / tu / ueg / fl binarisations (interpret.cc:383-432); inc[k] = ctxIdxInc of bin k
+    // (the last entry for every later bin)
+    int unary(int ctx, const int* inc, int ninc)
+    {
+        int n = 0;
+        while (dec(ctx + inc[std::min(n, ninc - 1)])) {
+            if (++n > 4096) fail(H264R_EINVAL, "CABAC: unary code too long");
+        }
+        return n;
+    }
+    int tu(int ctx, const int* inc, int ninc, int cmax)
+    {
+        int n = 0;
+        while (n < cmax && dec(ctx + inc[std::min(n, ninc - 1)])) ++n;
+        return n;
+    }
+    int ueg(int ctx, const int* inc, int ninc, int cmax, int k, bool sign)
+    {
+        int v = tu(ctx, inc, ninc, cmax);
+        if (v == cmax) {
+            while (bypass()) {
+                v += 1 << k++;
+                if (k > 24) fail(H264R_EINVAL, "CABAC: exp-Golomb suffix too long");
+            }
+            while (k--) v += bypass() << k;
+        }
+        if (sign && v && bypass()) v = -v;
+        return v;
+    }
+};
 
 // zig-zag scans (frame): raster index of scan position k (Tables 8-12 / 8-13)
 const uint8_t ZZ4[16] = {0, 1, 4, 8, 5, 2, 3, 6, 9, 12, 13, 10, 7, 11, 14, 15};
@@ -408,6 +504,7 @@ struct SliceHeader {
     int weight[2][32][3] = {}, offset[2][32][3] = {};
     bool no_output_of_prior_pics = false, long_term_reference = false, adaptive = false;
     std::vector<Mmco> mmco;
+    int cabac_init_idc = 0;
     int qp = 26, qs = 0;
     bool sp_switch = false;
     int deblock_idc = 0, offset_a = 0, offset_b = 0;
@@ -422,8 +519,13 @@ struct MbState {
     uint8_t mb_type = 0;
     bool t8 = false;
     uint8_t i4[16] = {}, i8[4] = {}, i16 = 0;
-    uint8_t nz[3][4][4] = {};
+    uint8_t nz[3][4][4] = {};             // CAVLC TotalCoeff per 4x4 block (nz_coeff)
     uint8_t sub_type[4] = {}, sub_pred[4] = {};
+    // read by the CABAC context selection (neighbour.cc:415-764)
+    bool skip = false;
+    uint8_t cbpl = 0, cbpc = 0, cmode = 0;
+    uint64_t cbp_bits = 0;                // coded_block_flag bits (update_coded_block_flag)
+    int16_t mvd[2][16][2] = {};           // mvd_l0 / mvd_l1 per 4x4 block (raster)
 };
 
 struct StagedMb {
@@ -446,6 +548,8 @@ struct SliceCtx {
     int W, H;
     int qp;                     // slice.parser.QpY
     int skip_run = -1;
+    Cabac* cab = nullptr;       // CABAC slices (entropy_coding_mode_flag)
+    int last_dquant = 0;
     // the current MB
     int addr = 0, mbx = 0, mby = 0;
     MbState* cur = nullptr;
@@ -474,7 +578,23 @@ struct SliceCtx {
     int nnz_pred(int pl, int i, int j);
     int block_cavlc(int pl, bool chroma, bool ac, int blk, int start, int max_coeff, int32_t* coeff_pos_level,
                     int* npos);
+    // CABAC syntax elements (interpret_se.cc, contexts neighbour.cc:415-764)
+    MbState* nb_cur(int dx, int dy);
+    int cabac_mb_type(bool I, bool B);
+    int cabac_sub_mb_type(bool B);
+    int cabac_cbp();
+    int cabac_ref_idx(int list, int x4, int y4);
+    int cabac_mvd(int list, int x4, int y4, int comp);
+    int cbf_inc(int pl, bool chroma, bool ac, int blk);
+    int block_cabac(int cat, int pl, bool chroma, bool ac, int blk, int start, int max_coeff, int32_t* out, int* nout);
+    int block(int cat, int pl, bool chroma, bool ac, int blk, int start, int max_coeff, int32_t* out, int* nout)
+    {
+        return cab ? block_cabac(cat, pl, chroma, ac, blk, start, max_coeff, out, nout)
+                   : block_cavlc(pl, chroma, ac, blk, start, max_coeff, out, nout);
+    }
     void stage();
+    bool read_t8();
+    void set_cbp_state();
 };
 
 class Decoder {
@@ -601,7 +721,6 @@ void Decoder::parse_slice_header(Bits& b, SliceHeader& h)
     require(h.pps_id < 256 && pps_[h.pps_id].valid, "slice: pic_parameter_set_id of no PPS");
     const Pps& pps = pps_[h.pps_id];
     const Sps& sps = sps_[pps.sps_id];
-    unsupported(pps.cabac, "CABAC entropy coding (this parser reads CAVLC)");
     unsupported(sps.chroma_format_idc != 1 || sps.bit_depth_y != 8 || sps.bit_depth_c != 8,
                 "picture format (4:2:0, 8-bit only)");
     unsupported(!sps.frame_mbs_only, "field / MBAFF coding");
@@ -675,6 +794,10 @@ void Decoder::parse_slice_header(Bits& b, SliceHeader& h)
                     h.mmco.push_back(m);
                 }
         }
+    }
+    if (pps.cabac && h.slice_type != H264R_SLICE_I) {
+        h.cabac_init_idc = b.ue();
+        require(h.cabac_init_idc <= 2, "slice: cabac_init_idc");
     }
     h.qp = pps.init_qp + b.se();
     if (h.slice_type == H264R_SLICE_SP) {
@@ -1077,6 +1200,22 @@ void SliceCtx::run()
     const bool I = sh.slice_type == H264R_SLICE_I;
     addr = sh.first_mb;
     require(addr < W * H, "slice: first_mb_in_slice");
+    if (pps.cabac) {
+        // Parser::init / slice_t::init (interpret_mb.cc:138-156, slice_data.cc:602-604); the
+        // end_of_slice_flag after every MB but the picture's last (macroblock_t::close :526-565)
+        static thread_local Cabac engine;
+        cab = &engine;
+        const int kind = I ? 0 : (sh.slice_type == H264R_SLICE_B ? 4 : 1) + sh.cabac_init_idc;
+        cab->init_contexts(kind, sh.qp);
+        cab->init_engine(b);
+        for (;;) {
+            macroblock();
+            if (addr == W * H - 1) return;
+            const int eos = cab->term();
+            ++addr;
+            if (eos) return;
+        }
+    }
     for (;;) {
         macroblock();
         if (addr == W * H - 1) return;
@@ -1124,17 +1263,28 @@ void SliceCtx::macroblock()
     chroma_mode = 0;
     cbpl = cbpc = 0;
     cbp_blks = 0;
+    m.cbp_bits = 0;
+    if (sh.slice_type != H264R_SLICE_I) memset(m.mvd, 0, sizeof(m.mvd));
     memset(cof, 0, sizeof(cof));
     allrefzero = false;
     const bool I = sh.slice_type == H264R_SLICE_I, B = sh.slice_type == H264R_SLICE_B;
     int mb_type;
     skip = false;
     if (!I) {
-        if (skip_run == -1) skip_run = b.ue();
-        skip = skip_run > 0;
-        --skip_run;
+        if (cab) {
+            // mb_skip_flag: ctxIdxInc = A / B available and not skipped
+            int inc = 0;
+            for (MbState* n : {nb_cur(-1, 0), nb_cur(0, -1)}) inc += n && !n->skip;
+            skip = cab->dec(CTX_SKIP_CONTEXTS + inc);
+            if (skip) last_dquant = 0;
+        } else {
+            if (skip_run == -1) skip_run = b.ue();
+            skip = skip_run > 0;
+            --skip_run;
+        }
     }
-    mb_type = skip ? 0 : (int)(uint8_t)b.ue() + ((!I && !B) ? 1 : 0);
+    m.skip = skip;
+    mb_type = skip ? 0 : (cab ? cabac_mb_type(I, B) : (int)(uint8_t)b.ue()) + ((!I && !B) ? 1 : 0);
     // mb_type tables (interpret_mb.cc:318-406)
     int itype = -1;
     if (I) itype = mb_type;
@@ -1191,12 +1341,17 @@ void SliceCtx::macroblock()
         memset(m.nz, 16, sizeof(m.nz));
         cbp_blks = 0xFFFF;
         reset_motion();
+        m.skip = false;
+        last_dquant = 0;
+        m.cbpl = m.cbpc = 0;
+        m.cmode = 0;
         while (!b.aligned()) b.u(1);
         for (int y = 0; y < 16; ++y)
             for (int x = 0; x < 16; ++x) cof[0][y][x] = b.u(8);
         for (int c = 1; c <= 2; ++c)
             for (int y = 0; y < 8; ++y)
                 for (int x = 0; x < 8; ++x) cof[c][y][x] = b.u(8);
+        if (cab) cab->init_engine(b);
         stage();
         return;
     }
@@ -1206,7 +1361,7 @@ void SliceCtx::macroblock()
         m.t8 = false;
         if (m.mb_type == H264R_P_8x8) {
             for (int k = 0; k < 4; ++k) {
-                const uint32_t t = b.ue();
+                const uint32_t t = cab ? (uint32_t)cabac_sub_mb_type(B) : b.ue();
                 if (!B) {
                     require(t < 4, "sub_mb_type (P)");
                     m.sub_type[k] = (uint8_t)(4 + t);        // P_8x8, P_8x4, P_4x8, P_4x4
@@ -1228,32 +1383,64 @@ void SliceCtx::macroblock()
     update_qp(qp);
     if (m.mb_type == 0) {
         m.t8 = false;
-        if (sh.slice_type != H264R_SLICE_B) { stage(); return; }      // P_Skip (nz cleared by skip_p)
-        if (skip_run >= 0) {                                          // B_Skip
+        if (sh.slice_type != H264R_SLICE_B) { set_cbp_state(); stage(); return; }   // P_Skip (nz cleared by skip_p)
+        if (skip) {                                                                 // B_Skip
             memset(m.nz, 0, sizeof(m.nz));
+            set_cbp_state();
             stage();
             return;
         }
     }
     // coded_block_pattern (interpret_mb.cc:707-729)
     if (m.mb_type != H264R_I_16x16) {
-        const uint32_t code = b.ue();
-        require(code < 48, "coded_block_pattern");
-        const int cbp = m.intra ? CBP_ME_INTRA[code] : CBP_ME_INTER[code];
+        int cbp;
+        if (cab) {
+            cbp = cabac_cbp();
+            if (!cbp) last_dquant = 0;
+        } else {
+            const uint32_t code = b.ue();
+            require(code < 48, "coded_block_pattern");
+            cbp = m.intra ? CBP_ME_INTRA[code] : CBP_ME_INTER[code];
+        }
         cbpl = cbp % 16;
         cbpc = cbp / 16;
         const bool direct = m.mb_type == 0 && B;
         if (cbpl > 0 && pps.transform_8x8 && !m.intra && no_sub_lt8 && (!direct || sps.direct_8x8_inference))
-            m.t8 = b.u(1);
+            m.t8 = read_t8();
     }
+    set_cbp_state();
     if (cbpl > 0 || cbpc > 0 || m.mb_type == H264R_I_16x16) {
-        const int dq = (int8_t)b.se();
+        int dq;
+        if (cab) {
+            // unary at {last_dquant != 0, 2, 3}, mapped to the signed value (interpret_se.cc:441-460)
+            const int inc[3] = {last_dquant != 0 ? 1 : 0, 2, 3};
+            const int v = cab->unary(CTX_DELTA_QP_CONTEXTS, inc, 3);
+            dq = (int8_t)((v & 1) ? (v + 1) >> 1 : -((v + 1) >> 1));
+            last_dquant = dq;
+        } else
+            dq = (int8_t)b.se();
         require(dq >= -26 && dq <= 25, "mb_qp_delta");
         qp = (qp + dq + 52) % 52;
     }
     update_qp(qp);
     residual();
     stage();
+}
+
+// transform_size_8x8_flag: ctxIdxInc = A / B available with the 8x8 transform
+bool SliceCtx::read_t8()
+{
+    if (!cab) return b.u(1);
+    int inc = 0;
+    for (MbState* n : {nb_cur(-1, 0), nb_cur(0, -1)}) inc += n && n->t8;
+    return cab->dec(CTX_TRANSFORM_SIZE_CONTEXTS + inc);
+}
+
+void SliceCtx::set_cbp_state()
+{
+    cur->cbpl = (uint8_t)cbpl;
+    cur->cbpc = (uint8_t)cbpc;
+    cur->cmode = chroma_mode;
 }
 
 // mb_pred for intra MBs (interpret_mb.cc:506-569)
@@ -1263,26 +1450,46 @@ void SliceCtx::intra_pred_modes()
     reset_motion();
     m.t8 = false;
     if (pps.transform_8x8 && m.mb_type == H264R_I_4x4) {
-        m.t8 = b.u(1);
+        m.t8 = read_t8();
         m.mb_type = m.t8 ? H264R_I_8x8 : H264R_I_4x4;
     }
+    // prev_intra_pred_mode_flag + rem_intra_pred_mode (interpret_se.cc:302-323: CABAC rem as 3
+    // bins, LSB first, at ipr_contexts[1])
+    auto read_mode = [&](bool& prev) -> int {
+        if (!cab) {
+            prev = b.u(1);
+            return prev ? 0 : (int)b.u(3);
+        }
+        prev = cab->dec(CTX_IPR_CONTEXTS);
+        if (prev) return 0;
+        int r = 0;
+        for (int k = 0; k < 3; ++k) r |= cab->dec(CTX_IPR_CONTEXTS + 1) << k;
+        return r;
+    };
     if (m.mb_type == H264R_I_4x4) {
         for (int k = 0; k < 16; ++k) {
             const int bx = ((k / 4) % 2) * 8 + ((k % 4) % 2) * 4, by = ((k / 4) / 2) * 8 + ((k % 4) / 2) * 4;
-            const bool prev = b.u(1);
-            const int rem = prev ? 0 : b.u(3);
+            bool prev;
+            const int rem = read_mode(prev);
             const int pred = pred_mode(bx, by, false);
             m.i4[k] = (uint8_t)(prev ? pred : rem < pred ? rem : rem + 1);
         }
     } else if (m.mb_type == H264R_I_8x8) {
         for (int k = 0; k < 4; ++k) {
-            const bool prev = b.u(1);
-            const int rem = prev ? 0 : b.u(3);
+            bool prev;
+            const int rem = read_mode(prev);
             const int pred = pred_mode((k % 2) * 8, (k / 2) * 8, true);
             m.i8[k] = (uint8_t)(prev ? pred : rem < pred ? rem : rem + 1);
         }
     }
-    chroma_mode = (uint8_t)b.ue();
+    if (cab) {
+        // TU cMax 3: bin 0 at A / B available with a non-DC chroma mode (not I_PCM), then 3
+        int inc0 = 0;
+        for (MbState* n : {nb_cur(-1, 0), nb_cur(0, -1)}) inc0 += n && n->cmode != 0 && n->mb_type != H264R_I_PCM;
+        const int inc[2] = {inc0, 3};
+        chroma_mode = (uint8_t)cab->tu(CTX_CIPR_CONTEXTS, inc, 2, 3);
+    } else
+        chroma_mode = (uint8_t)b.ue();
     require(chroma_mode <= 3, "intra_chroma_pred_mode");
 }
 
@@ -1548,7 +1755,7 @@ void SliceCtx::inter_pred()
                     const bool present = B || !allrefzero || m.mb_type != H264R_P_8x8;
                     const int n = sh.nref[l];
                     int r = 0;
-                    if (present && n > 1) r = n == 2 ? 1 - (int)b.u(1) : (int)b.ue();
+                    if (present && n > 1) r = cab ? cabac_ref_idx(l, x8, y8) : n == 2 ? 1 - (int)b.u(1) : (int)b.ue();
                     require(r < n, "ref_idx out of range");
                     for (int y4 = 0; y4 < sv0; ++y4)
                         for (int x4 = 0; x4 < sh0; ++x4) M.ref_idx[l][M.at(mbx * 4 + x8 + x4, mby * 4 + y8 + y4)] = (int8_t)r;
@@ -1564,7 +1771,8 @@ void SliceCtx::inter_pred()
                 const int cref = M.ref_idx[l][M.at(mbx * 4 + x8, mby * 4 + y8)];
                 for (int y4 = 0; y4 < sv0; y4 += sv4)
                     for (int x4 = 0; x4 < sh0; x4 += sh4) {
-                        const int dx = (int16_t)b.se(), dy = (int16_t)b.se();
+                        const int dx = (int16_t)(cab ? cabac_mvd(l, x8 + x4, y8 + y4, 0) : b.se());
+                        const int dy = (int16_t)(cab ? cabac_mvd(l, x8 + x4, y8 + y4, 1) : b.se());
                         bool av[3];
                         int ref[3], mv[3][2], p[2];
                         neighbour_mv(l, x8 + x4, y8 + y4, sh4 * 4, sv4 * 4, av, ref, mv);
@@ -1575,6 +1783,9 @@ void SliceCtx::inter_pred()
                                 const size_t e = M.at(mbx * 4 + x8 + x4 + x2, mby * 4 + y8 + y4 + y2);
                                 M.mvx[l][e] = vx;
                                 M.mvy[l][e] = vy;
+                                int16_t* d = m.mvd[l][(y8 + y4 + y2) * 4 + x8 + x4 + x2];
+                                d[0] = (int16_t)dx;
+                                d[1] = (int16_t)dy;
                             }
                     }
             }
@@ -1675,25 +1886,40 @@ int SliceCtx::block_cavlc(int pl, bool chroma, bool ac, int blk, int start, int 
 
 // residual_luma / residual_chroma (interpret_residual.cc:421-494) + the coefficient push
 // of the shim (decoder_h264r.cc:328-354): raw levels at raster positions in cof
+enum { LUMA_16DC, LUMA_16AC, LUMA_4x4, CHROMA_DC, CHROMA_AC, LUMA_8x8 };
+
 void SliceCtx::residual()
 {
     MbState& m = *cur;
-    int32_t pl_[64];
+    int32_t pl_[128];
     int n;
-    if (m.mb_type == H264R_I_16x16) {
-        block_cavlc(0, false, false, 0, 0, 16, pl_, &n);
+    const bool i16 = m.mb_type == H264R_I_16x16;
+    if (i16) {
+        block(LUMA_16DC, 0, false, false, 0, 0, 16, pl_, &n);
         for (int k = 0; k < n; ++k) {
             const int r = ZZ4[pl_[2 * k]];
             cof[0][(r / 4) * 4][(r % 4) * 4] = pl_[2 * k + 1];
         }
     }
-    for (int i8 = 0; i8 < 4; ++i8)
+    for (int i8 = 0; i8 < 4; ++i8) {
+        if (cab && m.t8) {
+            // one 64-coefficient block per coded 8x8 (CABAC, :449-450)
+            if (!(cbpl & (1 << i8))) continue;
+            const int i = (i8 % 2) * 2, j = (i8 / 2) * 2;
+            block(LUMA_8x8, 0, false, true, i8 * 4, 0, 64, pl_, &n);
+            for (int k = 0; k < n; ++k) {
+                cbp_blks |= (uint16_t)(0x33u << (j * 4 + i));
+                const int r = ZZ8[pl_[2 * k]];
+                cof[0][j * 4 + r / 8][i * 4 + r % 8] = pl_[2 * k + 1];
+            }
+            continue;
+        }
         for (int i4 = 0; i4 < 4; ++i4) {
             const int blk = i8 * 4 + i4;
             const int i = ((blk / 4) % 2) * 2 + (blk % 4) % 2, j = ((blk / 4) / 2) * 2 + (blk % 4) / 2;
-            if (!(cbpl & (1 << i8))) { m.nz[0][j][i] = 0; continue; }
-            if (m.mb_type == H264R_I_16x16) block_cavlc(0, false, true, blk, 1, 15, pl_, &n);
-            else block_cavlc(0, false, true, blk, 0, 16, pl_, &n);
+            if (!(cbpl & (1 << i8))) { if (!cab) m.nz[0][j][i] = 0; continue; }
+            if (i16) block(LUMA_16AC, 0, false, true, blk, 1, 15, pl_, &n);
+            else block(LUMA_4x4, 0, false, true, blk, 0, 16, pl_, &n);
             for (int k = 0; k < n; ++k) {
                 const int c = pl_[2 * k], lev = pl_[2 * k + 1];
                 if (!m.t8) {
@@ -1709,9 +1935,10 @@ void SliceCtx::residual()
                 }
             }
         }
+    }
     if (cbpc & 3)
         for (int c = 1; c <= 2; ++c) {
-            block_cavlc(c, true, false, 0, 0, 4, pl_, &n);
+            block(CHROMA_DC, c, true, false, 0, 0, 4, pl_, &n);
             for (int k = 0; k < n; ++k) {
                 const int q = pl_[2 * k];
                 cof[c][(q / 2) * 4][(q % 2) * 4] = pl_[2 * k + 1];
@@ -1719,13 +1946,264 @@ void SliceCtx::residual()
         }
     for (int c = 1; c <= 2; ++c)
         for (int blk = 0; blk < 4; ++blk) {
-            if (!(cbpc & 2)) { m.nz[c][blk / 2][blk % 2] = 0; continue; }
-            block_cavlc(c, true, true, blk, 1, 15, pl_, &n);
+            if (!(cbpc & 2)) { if (!cab) m.nz[c][blk / 2][blk % 2] = 0; continue; }
+            block(CHROMA_AC, c, true, true, blk, 1, 15, pl_, &n);
             for (int k = 0; k < n; ++k) {
                 const int r = ZZ4[pl_[2 * k]];
                 cof[c][(blk / 2) * 4 + r / 4][(blk % 2) * 4 + r % 4] = pl_[2 * k + 1];
             }
         }
+}
+
+// ------------------------------------------------------------------ CABAC syntax elements
+// the MB at (dx, dy) MBs from the current one if it is in the current slice (get_mb + the
+// slice_nr check of every CtxIdxInc function)
+MbState* SliceCtx::nb_cur(int dx, int dy)
+{
+    int ax, ay;
+    return nb_mb(false, dx * 16, dy * 16, ax, ay);
+}
+
+// mb_type (interpret_se.cc:113-227): I-slice numbering 0..25 for I, P 0..3 (inter) / 5 + I,
+// B 0..22 / 23 + I
+int SliceCtx::cabac_mb_type(bool I, bool B)
+{
+    Cabac& c = *cab;
+    auto i_suffix = [&](int base, bool islice) -> int {          // the I mb_type after the prefix bin
+        if (c.term()) return 25;
+        int t = 1;
+        t += c.dec(base + (islice ? 3 : 1)) * 12;
+        if (c.dec(base + (islice ? 4 : 2))) t += c.dec(base + (islice ? 5 : 2)) * 4 + 4;
+        t += c.dec(base + (islice ? 6 : 3)) * 2;
+        t += c.dec(base + (islice ? 7 : 3));
+        return t;
+    };
+    if (I) {
+        int inc = 0;
+        for (MbState* n : {nb_cur(-1, 0), nb_cur(0, -1)}) inc += n && n->mb_type != H264R_I_4x4 && n->mb_type != H264R_I_8x8;
+        const int base = CTX_MB_TYPE_CONTEXTS + 3;
+        if (!c.dec(base + inc)) return 0;
+        return i_suffix(base, true);
+    }
+    if (!B) {
+        const int ctx = CTX_MB_TYPE_CONTEXTS;
+        if (!c.dec(ctx + 0)) {
+            if (!c.dec(ctx + 1)) return c.dec(ctx + 2) * 3;
+            return 2 - c.dec(ctx + 3);
+        }
+        const int base = CTX_MB_TYPE_CONTEXTS + 3;
+        if (!c.dec(base)) return 5;
+        return 5 + i_suffix(base, false);
+    }
+    const int ctx = CTX_MB_TYPE_CONTEXTS;
+    int inc = 0;
+    for (MbState* n : {nb_cur(-1, 0), nb_cur(0, -1)}) inc += n && n->mb_type != 0;
+    int t = 0;
+    if (c.dec(ctx + inc)) {
+        t = 1;
+        if (!c.dec(ctx + 3)) t += c.dec(ctx + 5);
+        else {
+            t += 2;
+            if (!c.dec(ctx + 4)) {
+                t += c.dec(ctx + 5) * 4;
+                t += c.dec(ctx + 5) * 2;
+                t += c.dec(ctx + 5);
+            } else {
+                t += 9;
+                t += c.dec(ctx + 5) * 8;
+                t += c.dec(ctx + 5) * 4;
+                t += c.dec(ctx + 5) * 2;
+                if (t < 22) t += c.dec(ctx + 5);
+                if (t == 22) t = 23;
+                else if (t == 24) t = 11;
+                else if (t == 26) t = 22;
+            }
+        }
+    }
+    if (t == 23) {
+        const int base = CTX_MB_TYPE_CONTEXTS + 5;
+        if (!c.dec(base)) return 23;
+        return 23 + i_suffix(base, false);
+    }
+    return t;
+}
+
+// sub_mb_type (interpret_se.cc:247-285)
+int SliceCtx::cabac_sub_mb_type(bool B)
+{
+    Cabac& c = *cab;
+    const int ctx = CTX_B8_TYPE_CONTEXTS;
+    int t = 0;
+    if (!B) {
+        if (!c.dec(ctx)) {
+            t = 1;
+            if (c.dec(ctx + 1)) t += c.dec(ctx + 2) ? 1 : 2;
+        }
+        return t;
+    }
+    if (c.dec(ctx)) {
+        t = 1;
+        if (c.dec(ctx + 1)) {
+            t += 2;
+            if (c.dec(ctx + 2)) {
+                t += 4;
+                if (c.dec(ctx + 3)) t += 4;
+                else t += c.dec(ctx + 3) * 2;
+            } else
+                t += c.dec(ctx + 3) * 2;
+        }
+        t += c.dec(ctx + 3);
+    }
+    return t;
+}
+
+// coded_block_pattern (interpret_se.cc:419-435, neighbour.cc:635-686)
+int SliceCtx::cabac_cbp()
+{
+    Cabac& c = *cab;
+    int cbp = 0;
+    MbState* A = nb_cur(-1, 0);
+    MbState* Bm = nb_cur(0, -1);
+    for (int y0 = 0; y0 < 4; y0 += 2)
+        for (int x0 = 0; x0 < 4; x0 += 2) {
+            int ca = 0x3F, cb = 0x3F, ia = 0, ib = 0;
+            if (x0 == 0) {
+                if (A && A->mb_type != H264R_I_PCM) { ca = A->cbpl; ia = (y0 & ~1) + 1; }
+            } else { ca = cbp; ia = y0; }
+            if (y0 == 0) {
+                if (Bm && Bm->mb_type != H264R_I_PCM) { cb = Bm->cbpl; ib = x0 / 2 + 2; }
+            } else { cb = cbp; ib = x0 / 2; }
+            const int inc = ((ca & (1 << ia)) == 0 ? 1 : 0) + 2 * ((cb & (1 << ib)) == 0 ? 1 : 0);
+            if (c.dec(CTX_CBP_L_CONTEXTS + inc)) cbp += 1 << (y0 + (x0 >> 1));
+        }
+    auto f = [](MbState* n, bool two) { return n && (n->mb_type == H264R_I_PCM || (two ? n->cbpc == 2 : n->cbpc != 0)); };
+    const int inc0 = f(A, false) + 2 * f(Bm, false), inc1 = f(A, true) + 2 * f(Bm, true) + 4;
+    if (c.dec(CTX_CBP_C_CONTEXTS + inc0)) cbp += c.dec(CTX_CBP_C_CONTEXTS + inc1) ? 32 : 16;
+    return cbp;
+}
+
+// ref_idx_lX (interpret_se.cc:341-370, ctxIdxInc neighbour.cc:517-572): unary at {inc, 4, 5}
+int SliceCtx::cabac_ref_idx(int list, int x4, int y4)
+{
+    const bool B = sh.slice_type == H264R_SLICE_B;
+    const Motion& M = *D.mot_;
+    int inc = 0;
+    const int off[2][2] = {{x4 * 4 - 1, y4 * 4}, {x4 * 4, y4 * 4 - 1}};
+    for (int k = 0; k < 2; ++k) {
+        int ax, ay;
+        MbState* n = nb_mb(false, off[k][0], off[k][1], ax, ay);
+        if (!n) continue;
+        const int r = M.ref_idx[list][M.at(ax / 4, ay / 4)];
+        const int part = ((ay / 4) & 2) + ((ax / 8) & 1);
+        const bool pred_eq = !((n->mb_type == 0 && B) || n->sub_type[part] == 0);
+        const bool cond = !(n->mb_type == 0 || n->intra || !pred_eq || r <= 0);
+        inc += cond ? (k ? 2 : 1) : 0;
+    }
+    const int incs[3] = {inc, 4, 5};
+    return cab->unary(CTX_REF_NO_CONTEXTS, incs, 3);
+}
+
+// mvd_lX (interpret_se.cc:372-387, ctxIdxInc neighbour.cc:574-633): UEG3, signed, cMax 9
+int SliceCtx::cabac_mvd(int list, int x4, int y4, int comp)
+{
+    const bool B = sh.slice_type == H264R_SLICE_B;
+    int sum = 0;
+    const int off[2][2] = {{x4 * 4 - 1, y4 * 4}, {x4 * 4, y4 * 4 - 1}};
+    for (int k = 0; k < 2; ++k) {
+        int ax, ay;
+        MbState* n = nb_mb(false, off[k][0], off[k][1], ax, ay);
+        if (!n) continue;
+        const int part = ((ay / 4) & 2) + ((ax / 8) & 1);
+        const bool pred_eq = !((n->mb_type == 0 && B) || n->sub_type[part] == 0);
+        if (!(n->mb_type == 0 || n->intra || !pred_eq))
+            sum += std::abs((int)n->mvd[list][((ay & 15) / 4) * 4 + (ax & 15) / 4][comp]);
+    }
+    const int inc[5] = {sum < 3 ? 0 : sum <= 32 ? 1 : 2, 3, 4, 5, 6};
+    return cab->ueg(comp ? CTX_MVD_Y_CONTEXTS : CTX_MVD_X_CONTEXTS, inc, 5, 9, 3, true);
+}
+
+// coded_block_flag ctxIdxInc (neighbour.cc:689-742)
+int SliceCtx::cbf_inc(int pl, bool chroma, bool ac, int blk)
+{
+    const int i = chroma ? blk % 2 : ((blk / 4) % 2) * 2 + (blk % 4) % 2;
+    const int j = chroma ? blk / 2 : ((blk / 4) / 2) * 2 + (blk % 4) / 2;
+    const int bit = !chroma ? (ac ? 1 : 0) : !ac ? (pl == 1 ? 17 : 18) : (pl == 1 ? 19 : 35);
+    const int nw = chroma ? 8 : 16;
+    int inc = 0;
+    const int off[2][2] = {{i * 4 - 1, j * 4}, {i * 4, j * 4 - 1}};
+    for (int k = 0; k < 2; ++k) {
+        int ax, ay;
+        MbState* n = nb_mb(chroma, off[k][0], off[k][1], ax, ay);
+        int cond = cur->intra ? 1 : 0;
+        if (n) {
+            if (n->mb_type == H264R_I_PCM) cond = 1;
+            else {
+                const int pos = ac ? ((ay % nw) & 12) + (ax % nw) / 4 : 0;
+                cond = (int)((n->cbp_bits >> (bit + pos)) & 1);
+            }
+        }
+        inc += cond << k;
+    }
+    return inc;
+}
+
+// residual_block_cabac (interpret_residual.cc:315-419): (position, level) pairs, positions
+// counted from 0 like the CAVLC reader's
+int SliceCtx::block_cabac(int cat, int pl, bool chroma, bool ac, int blk, int start, int max_coeff, int32_t* out, int* nout)
+{
+    Cabac& c = *cab;
+    *nout = 0;
+    bool coded = true;                                    // always one for 8x8 blocks (4:2:0)
+    if (cat != LUMA_8x8) coded = c.dec(CTX_BCBP_CONTEXTS + TYPE2CTX_BCBP[cat] + cbf_inc(pl, chroma, ac, blk));
+    if (!coded) return 0;
+    {                                                     // update_coded_block_flag (neighbour.cc:744-764)
+        const int i = chroma ? blk % 2 : ((blk / 4) % 2) * 2 + (blk % 4) % 2;
+        const int j = chroma ? blk / 2 : ((blk / 4) / 2) * 2 + (blk % 4) / 2;
+        const int bit = (!chroma ? (ac ? 1 : 0) : !ac ? (pl == 1 ? 17 : 18) : (pl == 1 ? 19 : 35)) + (ac ? j * 4 + i : 0);
+        cur->cbp_bits |= (uint64_t)(cur->t8 && !chroma && ac ? 0x33 : 0x01) << bit;
+    }
+    const uint8_t* pmap = cat == LUMA_8x8 ? POS2CTX_MAP8X8 : POS2CTX_MAP4X4;
+    const uint8_t* plast = cat == LUMA_8x8 ? POS2CTX_LAST8X8 : POS2CTX_LAST4X4;
+    const int map = CTX_MAP_CONTEXTS + TYPE2CTX_MAP[cat], last = CTX_LAST_CONTEXTS + TYPE2CTX_MAP[cat];
+    int sig[64];
+    int num = max_coeff;
+    int ii = 0;
+    for (; ii < num - 1; ++ii) {
+        sig[ii] = c.dec(map + pmap[ii]);
+        if (sig[ii] && c.dec(last + plast[ii])) num = ii + 1;
+    }
+    sig[num - 1] = 1;
+    const int one = CTX_ONE_CONTEXTS + TYPE2CTX_ONE[cat];
+    int eq1 = 0, gt1 = 0, n = 0;
+    for (int k = num - 1; k >= 0; --k) {
+        if (!sig[k]) continue;
+        const int inc0 = gt1 ? 0 : std::min(4, 1 + eq1);
+        const int inc1 = 5 + std::min(4 - (cat == CHROMA_DC ? 1 : 0), gt1);
+        int am1 = 0;
+        if (c.dec(one + inc0)) {
+            // unary_exp_golomb_level_decode (:291-312): up to 13 more bins at inc1, then EG0
+            int ones = 0;
+            while (ones < 13 && c.dec(one + inc1)) ++ones;
+            if (ones < 13) am1 = ones + 1;
+            else {
+                int v = 0, kk = 0;
+                while (c.bypass()) {
+                    v += 1 << kk++;
+                    if (kk > 24) fail(H264R_EINVAL, "CABAC: level suffix too long");
+                }
+                while (kk--) v += c.bypass() << kk;
+                am1 = 14 + v;
+            }
+        }
+        const int level = c.bypass() ? -(am1 + 1) : am1 + 1;
+        out[2 * n] = k + start;
+        out[2 * n + 1] = level;
+        ++n;
+        eq1 += am1 == 0;
+        gt1 += am1 != 0;
+    }
+    *nout = n;
+    return n;
 }
 
 // The MB's record, level block and motion as the shim's decode(mb) snapshots them

@@ -2,8 +2,8 @@
  * h264p.h -- C ABI of the repo's own CPU entropy / syntax stage.
  *
  * The caller side of the reconstruction boundary (include/h264r.h): an Annex-B byte
- * stream is parsed on the host -- NAL units, SPS / PPS, slice headers, the CAVLC
- * macroblock layer and residuals, motion-vector prediction (P_Skip, B direct spatial /
+ * stream is parsed on the host -- NAL units, SPS / PPS, slice headers, the CAVLC and
+ * CABAC macroblock layer and residuals, motion-vector prediction (P_Skip, B direct spatial /
  * temporal), reference picture marking and list construction -- and every picture is
  * handed to the h264r ABI exactly as the reference parser + drop-in shim hand it
  * (shim/decoder_h264r.cc): h264r_picture_begin, h264r_mb_submit per MB, h264r_picture_end.
@@ -13,17 +13,20 @@
  *   ldecod.cc decode_one_frame, slice_data.cc:636-660  h264p_decode (NAL loop, picture boundary)
  *   interpret_rbsp.cc:625-777 slice_header              parse_slice_header
  *   interpret_rbsp.cc seq/pic_parameter_set_rbsp        parse_sps / parse_pps
- *   interpret_mb.cc:180-316 Macroblock::parse           Slice::macroblock
- *   interpret_mv.cc:27-434 MV prediction, direct        Slice::neighbour_mv / predict_mv / direct_*
- *   interpret_residual.cc:64-174, 421-494 (CAVLC)       Slice::residual_block / residual
+ *   interpret_mb.cc:180-316 Macroblock::parse           SliceCtx::macroblock
+ *   interpret_mv.cc:27-434 MV prediction, direct        SliceCtx::neighbour_mv / predict_mv / direct_*
+ *   interpret_residual.cc:64-174 (CAVLC), 315-419        SliceCtx::block_cavlc / block_cabac / residual
+ *     (CABAC), 421-494
+ *   interpret.cc:308-432 cabac_engine_t                Cabac (dec / bypass / term, u / tu / ueg)
+ *   interpret_se.cc, neighbour.cc:415-764 (CABAC ctx)   SliceCtx::cabac_* / cbf_inc
  *   slice_ref_list.cc:88-341, 885-964 ref lists         Decoder::init_lists / modify_list
  *   framebuf/dpb.cc marking (sliding window, MMCO)      Decoder::mark_picture
  *
  * The reconstruction calls are resolved at link time: against libh264r.so (MI355X) for the
  * product, against the CPU implementation of the same ABI in tests.  Status codes are the
- * h264r ones (H264R_OK / H264R_E*).  Entropy coding: CAVLC (CABAC streams return
- * H264R_EUNSUPPORTED, as do MBAFF / field pictures, FMO, data partitioning, formats other
- * than 4:2:0 8-bit, POC type 1, MMCO 5 and SI slices).
+ * h264r ones (H264R_OK / H264R_E*).  H264R_EUNSUPPORTED: MBAFF / field pictures, FMO,
+ * data partitioning, formats other than 4:2:0 8-bit, POC type 1, MMCO 5, SI slices (as in
+ * the reconstruction path).
  */
 #ifndef H264P_H_
 #define H264P_H_

@@ -12,7 +12,9 @@ streams (tests/streams.py):
   it (the committed captures, tests/golden/streams/*.cap.npz): every MB record, level block,
   motion entry, slice table, picture record, quantisation table and DPB slot.
 
-CABAC streams are refused with H264R_EUNSUPPORTED (the parser reads CAVLC).
+Both entropy coders are covered: 16 CAVLC streams (I / P / B / SP, lossless, long-term
+references) and 5 CABAC streams (every cabac_init_idc, I_PCM inside CABAC slices, B
+pictures with 8x8 transforms, BASELINE config 4's 1080p High IBBP 4-slice shape).
 """
 import os
 import subprocess
@@ -25,8 +27,7 @@ import streams as S
 from h264r import output as OUT
 
 GOLD = S.golden()["streams"]
-CAVLC = [n for n, c in S.STREAMS.items() if not c.get("cabac")]
-CABAC = [n for n, c in S.STREAMS.items() if c.get("cabac")]
+NAMES = list(S.STREAMS)
 CPU_DEC = os.path.join(S.ROOT, "oracle", "_cpu", "h264dec_cpu")
 GPU_DEC = os.path.join(S.ROOT, "arrow-h264_amd", "lib", "h264dec")
 
@@ -42,7 +43,7 @@ def _run(binary, name, out, env=None):
                           timeout=600, env=dict(os.environ, **(env or {})))
 
 
-@pytest.mark.parametrize("name", CAVLC)
+@pytest.mark.parametrize("name", NAMES)
 def test_parser_decodes_to_reference_md5s(name, tmp_path):
     """Own parser + the CPU implementation of the reconstruction ABI == the unmodified
     reference decoder, frame by frame (the reference harness's protocol,
@@ -53,7 +54,7 @@ def test_parser_decodes_to_reference_md5s(name, tmp_path):
     assert OUT.digest_by_frames(str(out), S.STREAMS[name]["frames"]) == GOLD[name]["frame_md5"]
 
 
-@pytest.mark.parametrize("name", CAVLC)
+@pytest.mark.parametrize("name", NAMES)
 def test_parser_hands_the_abi_what_the_reference_parser_did(name, tmp_path):
     """Every array the parser passes through the C ABI equals the capture of the reference
     parser + shim (the same h264r_picture_begin / h264r_mb_submit / h264r_picture_end
@@ -75,10 +76,8 @@ def test_parser_hands_the_abi_what_the_reference_parser_did(name, tmp_path):
         assert a["plane_md5"] == b["plane_md5"], f"picture {i}: reconstructed planes"
 
 
-@pytest.mark.parametrize("name", CABAC[:1])
-def test_parser_refuses_cabac(name, tmp_path):
-    r = _run(_cpu_dec(), name, tmp_path / "out.yuv")
-    assert r.returncode != 0 and "CABAC" in r.stderr
+def test_parser_covers_both_entropy_coders():
+    assert {bool(c.get("cabac")) for c in S.STREAMS.values()} == {False, True}
 
 
 def test_parser_rejects_garbage(tmp_path):
@@ -98,7 +97,7 @@ def test_parser_rejects_garbage(tmp_path):
 
 # ---------------------------------------------------------------------------- MI355X
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", CAVLC)
+@pytest.mark.parametrize("name", NAMES)
 def test_gpu_parser_decodes_to_reference_md5s(name, tmp_path):
     """The standalone decoder of the GPU box (no reference code anywhere): own parser +
     libh264r.so on MI355X reproduces the unmodified reference's per-frame MD5s."""
