@@ -31,7 +31,11 @@ _lib = None
 
 
 def build_oracle() -> None:
-    subprocess.run(["make", "-s", "-C", ORACLE_DIR, "all"], check=True)
+    # one make at a time (pytest-xdist workers): a binary being relinked must not be run
+    import fcntl
+    with open(os.path.join(ORACLE_DIR, ".build.lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        subprocess.run(["make", "-s", "-C", ORACLE_DIR, "all"], check=True)
 
 
 def reference_available() -> bool:
