@@ -33,6 +33,8 @@ DEV void inter4_lds(const h264r_batch& b, int pic, Inter4Lds& S)
         *reinterpret_cast<uint2*>(&S.ref_slot[i >> 2][0][0] + 8 * (i & 3)) =
             *reinterpret_cast<const uint2*>(&sl[i >> 2].ref_slot[0][0] + 8 * (i & 3));
     if (threadIdx.x >= 64 && threadIdx.x - 64 < nsl) S.slice_type[threadIdx.x - 64] = sl[threadIdx.x - 64].slice_type;
+    if (threadIdx.x >= 128 && threadIdx.x - 128 < nsl)
+        S.hdr[threadIdx.x - 128] = *reinterpret_cast<const uint2*>(&sl[threadIdx.x - 128]);
 }
 
 // the wave's QuadTile rows (H264R_QTILE builds only: mb_inter4.h)
@@ -118,19 +120,27 @@ extern "C" __global__ __launch_bounds__(256) void k_dbinfo(h264r_batch b, DbInfo
     if (!inter4_groups(g, rows, H264R_DBINFO_GROUPS, grp, gend)) return;
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int aend = rows.y * g.wmb;
+    const h264r_slice* slices = b.slices + (size_t)pic * b.slice_stride;
+    // the first group's record, motion and neighbour loads go out before the LDS tables are
+    // filled; every later group's right after the previous group's use
+    int a0 = rows.x * g.wmb + (grp * 4 + wave) * 4;
+    Inter4Pre pre = inter4_pre(b, g, pic, a0, aend, lane);
+    DbNb nb = dbinfo_pre(b, g, pic, a0, aend, lane);
     inter4_lds(b, pic, S);
     __syncthreads();
-    const h264r_slice* slices = b.slices + (size_t)pic * b.slice_stride;
-    for (; grp < gend; ++grp) {
-        const int a0 = rows.x * g.wmb + (grp * 4 + wave) * 4;
+    for (;;) {
         if (a0 >= aend) return;
-        const Inter4Pre pre = inter4_pre(b, g, pic, a0, aend, lane);
         const int a = a0 + (lane >> 4);
         const bool valid = a < aend;
         const int aa = valid ? a : aend - 1;
         const uint2 m0 = motion_word(pre.mv[0], pre.ri[0], slices, S, pre.q.slice, 0);
         const uint2 m1 = motion_word(pre.mv[1], pre.ri[1], slices, S, pre.q.slice, 1);
-        dbinfo_block(b, g, pic, aa, valid, lane & 15, S, pre.q, m0, m1, pre.qsh, dbinfo + (size_t)pic * g.nmb);
+        dbinfo_block(b, g, pic, aa, valid, lane & 15, S, pre.q, m0, m1, slice_hdr(slices, S, pre.q.slice), nb,
+                     dbinfo + (size_t)pic * g.nmb);
+        if (++grp >= gend) return;
+        a0 = rows.x * g.wmb + (grp * 4 + wave) * 4;
+        pre = inter4_pre(b, g, pic, a0, aend, lane);
+        nb = dbinfo_pre(b, g, pic, a0, aend, lane);
     }
 }
 

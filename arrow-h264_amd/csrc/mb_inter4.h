@@ -34,6 +34,7 @@ constexpr int INTER4_LDS_SLICES = 64;   // slices whose ref tables the workgroup
 
 struct Inter4Lds {
     const uint8_t* planes[3 * H264R_MAX_SLOTS];
+    uint2 hdr[INTER4_LDS_SLICES];                            // dwords 0..1 of the picture's slices (type, idc, offsets, wp)
     int8_t ref_slot[INTER4_LDS_SLICES][2][H264R_MAX_REFS];   // h264r_slice::ref_slot of the picture's slices
     uint8_t slice_type[INTER4_LDS_SLICES];                   // h264r_slice::slice_type of the same slices
 };
@@ -53,6 +54,14 @@ DEV int slice_type_of(const h264r_slice* slices, const Inter4Lds& S, int slice)
     int t = S.slice_type[min(slice, INTER4_LDS_SLICES - 1)];
     if (slice >= INTER4_LDS_SLICES) t = slice_byte(slices, slice, (int)offsetof(h264r_slice, slice_type));
     return t;
+}
+
+// Dwords 0..1 of slice `slice` (type, idc, filter offsets, wp mode, log2 wd): the LDS copy,
+// else the slice table
+DEV uint2 slice_hdr(const h264r_slice* slices, const Inter4Lds& S, int slice)
+{
+    if (slice < INTER4_LDS_SLICES) return S.hdr[slice];
+    return *reinterpret_cast<const uint2*>(&slices[slice]);
 }
 
 // Motion of one 4x4 block as {mv, ref_idx | slot << 8} per list: RefPicList[l][ref_idx]
@@ -88,7 +97,6 @@ struct Inter4Pre {
     h264r_mb q;
     uint32_t mv[2];
     int ri[2];
-    uint2 qsh;      // type, idc, offsets, wp, log2 wd
 };
 DEV Inter4Pre inter4_pre(const h264r_batch& b, const Geom& g, int pic, int a0, int aend, int lane)
 {
@@ -104,8 +112,39 @@ DEV Inter4Pre inter4_pre(const h264r_batch& b, const Geom& g, int pic, int a0, i
         p.mv[l] = b.mv[mbase + l * g.motion_plane + mi];
         p.ri[l] = b.ref_idx[mbase + l * g.motion_plane + mi];
     }
-    p.qsh = *reinterpret_cast<const uint2*>(&b.slices[(size_t)pic * b.slice_stride + p.q.slice]);
     return p;
+}
+
+// What the deblocking record of a lane's block reads besides its own MB: the left and upper
+// MB records and the motion of the blocks left of and above it (the MB's own blocks or the
+// neighbours'), loaded unconditionally and with no dependence on the MB record, so k_dbinfo
+// issues them together with inter4_pre's loads (one global round trip per group).
+struct DbNb {
+    h264r_mb L, U;
+    uint32_t lmv[2], umv[2];
+    int lri[2], uri[2];
+};
+DEV DbNb dbinfo_pre(const h264r_batch& b, const Geom& g, int pic, int a0, int aend, int lane)
+{
+    const int blk = lane & 15, a = a0 + (lane >> 4);
+    const int aa = a < aend ? a : aend - 1;
+    const int mbx = aa % g.wmb, mby = aa / g.wmb;
+    const int X4 = mbx * 4 + (blk & 3), Y4 = mby * 4 + (blk >> 2);
+    const int mi = Y4 * g.W4 + X4;
+    const int li = X4 > 0 ? mi - 1 : mi, ui = Y4 > 0 ? mi - g.W4 : mi;
+    const size_t mbase = (size_t)pic * 2 * g.motion_plane;
+    const h264r_mb* mbs = b.mbs + (size_t)pic * g.nmb;
+    DbNb n;
+    n.L = mb_lane(&mbs[mbx > 0 ? aa - 1 : aa]);
+    n.U = mb_lane(&mbs[mby > 0 ? aa - g.wmb : aa]);
+#pragma unroll
+    for (int l = 0; l < 2; ++l) {
+        n.lmv[l] = b.mv[mbase + l * g.motion_plane + li];
+        n.lri[l] = b.ref_idx[mbase + l * g.motion_plane + li];
+        n.umv[l] = b.mv[mbase + l * g.motion_plane + ui];
+        n.uri[l] = b.ref_idx[mbase + l * g.motion_plane + ui];
+    }
+    return n;
 }
 
 DEV int sel16(uint32_t lo, uint32_t hi, int c) { return (int16_t)(((c & 2) ? hi : lo) >> (16 * (c & 1))); }
@@ -407,32 +446,20 @@ DEV int mb_qp(const h264r_mb& m, int pl)
 // edge (horizontal edge by, segment bx), and for blk < 9 one alpha/beta/tc0 word.  Inside
 // k_inter4 after the reconstruction (DB = true), or its own kernel k_dbinfo.
 DEV void dbinfo_block(const h264r_batch& b, const Geom& g, int pic, int aa, bool valid, int blk, const Inter4Lds& S,
-                      const h264r_mb& q, uint2 m0, uint2 m1, uint2 qsh, DbInfo* __restrict__ dbout)
+                      const h264r_mb& q, uint2 m0, uint2 m1, uint2 qsh, const DbNb& nb, DbInfo* __restrict__ dbout)
 {
     const int bx = blk & 3, by = blk >> 2;
     const int mbx = aa % g.wmb, mby = aa / g.wmb;
-    const h264r_mb* mbs = b.mbs + (size_t)pic * g.nmb;
     const h264r_slice* slices = b.slices + (size_t)pic * b.slice_stride;
-    const int X4 = mbx * 4 + bx, Y4 = mby * 4 + by;
-    const int mi = Y4 * g.W4 + X4;
-    const size_t mbase = (size_t)pic * 2 * g.motion_plane;
     const int hasL = mbx > 0, hasU = mby > 0;
     const int q_type = qsh.x & 255, idc = (qsh.x >> 8) & 255;
     const int offa = (int8_t)((qsh.x >> 16) & 255), offb = (int8_t)(qsh.x >> 24);
-    // neighbour motion and records (in k_inter4: loaded after the reconstruction, so that
-    // they do not stay live across motion compensation; L2-hot by then)
-    const int li = X4 > 0 ? mi - 1 : mi, ui = Y4 > 0 ? mi - g.W4 : mi;
-    const h264r_mb L = mb_lane(&mbs[hasL ? aa - 1 : aa]);
-    const h264r_mb U = mb_lane(&mbs[hasU ? aa - g.wmb : aa]);
+    const h264r_mb& L = nb.L;
+    const h264r_mb& U = nb.U;
     // the neighbour block belongs to this MB or to the left / upper one (its slice resolves it)
     const int lsl = bx > 0 ? q.slice : L.slice, usl = by > 0 ? q.slice : U.slice;
-    // the neighbours' motion matters only to an inter MB (an intra one has bS 3 / 4 on every
-    // edge): a wave of intra MBs (all-intra pictures) skips its loads
-    uint2 l0 = make_uint2(0, 0), l1 = l0, u0 = l0, u1 = l0;
-    if (__builtin_amdgcn_readfirstlane(__any(!mb_is_intra(q)))) {
-        l0 = block_motion(b, slices, S, mbase + li, lsl, 0); l1 = block_motion(b, slices, S, mbase + g.motion_plane + li, lsl, 1);
-        u0 = block_motion(b, slices, S, mbase + ui, usl, 0); u1 = block_motion(b, slices, S, mbase + g.motion_plane + ui, usl, 1);
-    }
+    const uint2 l0 = motion_word(nb.lmv[0], nb.lri[0], slices, S, lsl, 0), l1 = motion_word(nb.lmv[1], nb.lri[1], slices, S, lsl, 1);
+    const uint2 u0 = motion_word(nb.umv[0], nb.uri[0], slices, S, usl, 0), u1 = motion_word(nb.umv[1], nb.uri[1], slices, S, usl, 1);
     const int l_type = slice_type_of(slices, S, L.slice), u_type = slice_type_of(slices, S, U.slice);
     // ---- deblocking record (Deblock::strength deblock.cc:78-289): this lane's
     // left edge (vertical edge bx, segment by) and top edge (horizontal edge by,
@@ -490,7 +517,6 @@ DEV void dbinfo_block(const h264r_batch& b, const Geom& g, int pic, int aa, bool
             out->par[blk] = edge_word(qp, qq, offa, offb);
         }
     }
-
 }
 
 // The inter / I_PCM macroblocks a0 .. a0+3 of picture `pic` and (DB) the deblocking
@@ -514,7 +540,7 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
     const int X4 = mbx * 4 + bx, Y4 = mby * 4 + by;
     const h264r_mb q = pre.q;
     const h264r_slice* qs = &slices[q.slice];
-    const uint2 qsh = pre.qsh;
+    const uint2 qsh = slice_hdr(slices, S, q.slice);
     const uint2 m0 = motion_word(pre.mv[0], pre.ri[0], slices, S, q.slice, 0);
     const uint2 m1 = motion_word(pre.mv[1], pre.ri[1], slices, S, q.slice, 1);
     const int q_type = qsh.x & 255;
@@ -1057,7 +1083,10 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
 #ifdef H264R_EXP_NO_DBINFO
     return;
 #endif
-    dbinfo_block(b, g, pic, aa, valid, blk, S, q, m0, m1, qsh, dbout);
+    // neighbour records and motion loaded only now, so that they do not stay live across the
+    // motion compensation (L2-hot by then)
+    const DbNb nb = dbinfo_pre(b, g, pic, a0, aend, lane);
+    dbinfo_block(b, g, pic, aa, valid, blk, S, q, m0, m1, qsh, nb, dbout);
 }
 
 }  // namespace h264r
