@@ -73,6 +73,13 @@ struct Bits {
         pos += n;
         if (pos > nbits) fail(H264R_EINVAL, "bitstream: read past the end of a NAL unit");
     }
+    uint32_t bit()
+    {
+        if (pos >= nbits) fail(H264R_EINVAL, "bitstream: read past the end of a NAL unit");
+        const uint32_t v = (buf[pos >> 3] >> (7 - (pos & 7))) & 1;
+        ++pos;
+        return v;
+    }
     uint32_t u(int n)
     {
         if (n == 0) return 0;
@@ -84,7 +91,7 @@ struct Bits {
     uint32_t ue()
     {
         int lz = 0;
-        while (!u(1))
+        while (!bit())
             if (++lz > 31) fail(H264R_EINVAL, "bitstream: ue(v) longer than 32 bits");
         return lz ? (uint32_t)((1ull << lz) - 1 + u(lz)) : 0;
     }
@@ -188,15 +195,20 @@ struct Cabac {
             if (state[ctx] == 0) mps[ctx] = (uint8_t)(1 - mps[ctx]);
             state[ctx] = TRANS_LPS[state[ctx]];
         }
-        while (range < 256) {
-            range <<= 1;
-            offset = (offset << 1) | b->u(1);
-        }
+        renorm();
         return bin;
+    }
+    void renorm()                                      // RenormD: range back to 9 bits at once
+    {
+        if (range < 256) {
+            const int sh = __builtin_clz(range) - 23;
+            range <<= sh;
+            offset = (offset << sh) | b->u(sh);
+        }
     }
     int bypass()
     {
-        offset = (offset << 1) | b->u(1);
+        offset = (offset << 1) | b->bit();
         if (offset < range) return 0;
         offset -= range;
         return 1;
@@ -205,10 +217,7 @@ struct Cabac {
     {
         range -= 2;
         if (offset >= range) return 1;
-        while (range < 256) {
-            range <<= 1;
-            offset = (offset << 1) | b->u(1);
-        }
+        renorm();
         return 0;
     }
     // u / tu / ueg / fl binarisations (interpret.cc:383-432); inc[k] = ctxIdxInc of bin k
@@ -1846,7 +1855,7 @@ int SliceCtx::block_cavlc(int pl, bool chroma, bool ac, int blk, int start, int 
         for (int k = tc - 1 - t1; k >= 0; --k) {
             int prefix = -1;
             for (int bit = 0; !bit; ++prefix) {
-                bit = b.u(1);
+                bit = b.bit();
                 if (prefix > 32) fail(H264R_EINVAL, "level_prefix too long");
             }
             const int ssize = (prefix == 14 && suffix == 0) ? 4 : prefix >= 15 ? prefix - 3 : suffix;
