@@ -53,7 +53,7 @@ namespace {
 #define H264R_WALK_ROWS 8                   // MB rows per band (h264r_host.hip sizes the launch with it)
 #endif
 #ifndef H264R_WALK_WAVES
-#define H264R_WALK_WAVES 8                  // minimum waves per SIMD asked of the register allocator (<= 64 VGPRs; profiles/r03_b_ab.txt)
+#define H264R_WALK_WAVES 8                  // minimum waves per SIMD asked of the register allocator (<= 64 VGPRs; profiles/r03s2_b_ab.txt)
 #endif
 constexpr int WAVES = H264R_WALK_ROWS;      // rows per band, one wave each
 
