@@ -21,21 +21,37 @@ using namespace h264r;
 #ifndef H264R_INTER4_WAVES
 #define H264R_INTER4_WAVES 3
 #endif
-// The workgroup's copy of the DPB plane table and of picture `pic`'s slice ref tables and
-// slice types.
-DEV void inter4_lds(const h264r_batch& b, int pic, Inter4Lds& S)
+// The workgroup's copy of the DPB plane table and of picture `pic`'s slice ref tables, slice
+// types and slice headers.  Every thread issues its loads first (clamped indices, no branch)
+// and writes LDS after: three loads in flight instead of one round trip per table.
+struct LdsRegs {
+    const uint8_t* plane;
+    uint2 refs, hdr;
+};
+DEV LdsRegs inter4_lds_load(const h264r_batch& b, int pic)
 {
-    if (threadIdx.x < 3 * H264R_MAX_SLOTS) S.planes[threadIdx.x] = b.ref_planes[threadIdx.x];
-    // the picture's ref tables: 32 bytes per slice, 8 per thread
+    const int t = threadIdx.x;
     const int nsl = min(b.slice_stride, INTER4_LDS_SLICES);
     const h264r_slice* sl = b.slices + (size_t)pic * b.slice_stride;
-    for (int i = threadIdx.x; i < nsl * 4; i += blockDim.x)
-        *reinterpret_cast<uint2*>(&S.ref_slot[i >> 2][0][0] + 8 * (i & 3)) =
-            *reinterpret_cast<const uint2*>(&sl[i >> 2].ref_slot[0][0] + 8 * (i & 3));
-    if (threadIdx.x >= 64 && threadIdx.x - 64 < nsl) S.slice_type[threadIdx.x - 64] = sl[threadIdx.x - 64].slice_type;
-    if (threadIdx.x >= 128 && threadIdx.x - 128 < nsl)
-        S.hdr[threadIdx.x - 128] = *reinterpret_cast<const uint2*>(&sl[threadIdx.x - 128]);
+    LdsRegs r;
+    r.plane = b.ref_planes[min(t, 3 * H264R_MAX_SLOTS - 1)];
+    const int ri = min(t, nsl * 4 - 1);                      // ref tables: 32 bytes per slice, 8 per thread
+    r.refs = *reinterpret_cast<const uint2*>(&sl[ri >> 2].ref_slot[0][0] + 8 * (ri & 3));
+    r.hdr = *reinterpret_cast<const uint2*>(&sl[min(t, nsl - 1)]);
+    return r;
 }
+DEV void inter4_lds_store(const h264r_batch& b, const LdsRegs& r, Inter4Lds& S)
+{
+    const int t = threadIdx.x;
+    const int nsl = min(b.slice_stride, INTER4_LDS_SLICES);
+    if (t < 3 * H264R_MAX_SLOTS) S.planes[t] = r.plane;
+    if (t < nsl * 4) *reinterpret_cast<uint2*>(&S.ref_slot[t >> 2][0][0] + 8 * (t & 3)) = r.refs;
+    if (t < nsl) {
+        S.hdr[t] = r.hdr;
+        S.slice_type[t] = (uint8_t)(r.hdr.x & 255);
+    }
+}
+DEV void inter4_lds(const h264r_batch& b, int pic, Inter4Lds& S) { inter4_lds_store(b, inter4_lds_load(b, pic), S); }
 
 // the wave's QuadTile rows (H264R_QTILE builds only: mb_inter4.h)
 DEV QuadTile* wave_tiles()
@@ -79,7 +95,8 @@ DEV void inter4_kernel(const h264r_batch& b, DbInfo* dbinfo, int2 rows, int* sp_
     const int aend = rows.y * g.wmb;
     int a0 = rows.x * g.wmb + (grp * 4 + wave) * 4;
     Inter4Pre pre = inter4_pre(b, g, pic, a0, aend, lane);
-    inter4_lds(b, pic, S);
+    const LdsRegs lr = inter4_lds_load(b, pic);
+    inter4_lds_store(b, lr, S);
     __syncthreads();
     for (;;) {
         if (a0 >= aend) return;

@@ -299,22 +299,29 @@ DEV void luma_block_pred(const uint32_t (&w)[9][3], int W, int x, int xf, int yf
 DEV uint32_t chroma_block_pred(const uint8_t* __restrict__ img, int W, int H, int xi, int yi, int xf, int yf)
 {
     const int a = clip3(0, W - 1, xi) & ~3;
-    int p[3][3];
+    // the three rows' dwords first, then byte selection without branches: a lane-divergent
+    // interior / edge split made every row's load wait for the previous row's use (the
+    // compiler joined the paths with a full vmcnt wait before issuing the next load)
+    uint32_t w[3][2];
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
         const gdword* q = as_global(img + (size_t)clip3(0, H - 1, yi + k) * W + a);
-        const uint32_t w0 = q[0], w1 = q[1];
-        if (xi >= 0 && xi + 2 < W) {
-            const uint32_t r = __builtin_amdgcn_alignbyte(w1, w0, xi & 3);
-            p[k][0] = r & 255; p[k][1] = (r >> 8) & 255; p[k][2] = (r >> 16) & 255;
-        } else {
-#pragma unroll
-            for (int c = 0; c < 3; ++c) {
-                const int idx = clip3(0, W - 1, xi + c) - a;
-                p[k][c] = ((idx < 4 ? w0 : w1) >> (8 * (idx & 3))) & 255;
-            }
-        }
+        w[k][0] = q[0];
+        w[k][1] = q[1];
     }
+    int sh[3];
+    bool hi[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {                       // column c, clamped to the picture
+        const int idx = clip3(0, W - 1, xi + c) - a;
+        hi[c] = idx >= 4;
+        sh[c] = 8 * (idx & 3);
+    }
+    int p[3][3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) p[k][c] = ((hi[c] ? w[k][1] : w[k][0]) >> sh[c]) & 255;
     const int wa = (8 - xf) * (8 - yf), wb = xf * (8 - yf), wc = (8 - xf) * yf, wd = xf * yf;
     uint32_t o = 0;
 #pragma unroll
@@ -335,13 +342,34 @@ DEV uint32_t chroma_block_pred(const uint8_t* __restrict__ img, int W, int H, in
 struct WpPar {
     int w0, w1, o, d, rnd;
 };
-DEV WpPar wp_params(const h264r_slice* __restrict__ sl, int wp_mode, int dir, int r0, int r1, int pl)
+// The slice's weights and offsets of both lists' references, all three planes, loaded
+// together (per-plane loads behind the case split below waited for each other: three round
+// trips per MB in weighted slices)
+struct WpRaw {
+    int lwd[2];
+    int wa[3], wb[3], oa[3], ob[3];
+    int iw;
+};
+DEV WpRaw wp_raw(const h264r_slice* __restrict__ sl, int r0, int r1)
 {
     const int ra = clip3(0, H264R_MAX_REFS - 1, r0), rb = clip3(0, H264R_MAX_REFS - 1, r1);   // unused list: any entry
-    const int lwd = pl ? sl->chroma_log2_wd : sl->luma_log2_wd;
-    const int wa = sl->wp_weight[0][ra][pl], wb = sl->wp_weight[1][rb][pl];
-    const int oa = sl->wp_offset[0][ra][pl], ob = sl->wp_offset[1][rb][pl];
-    const int iw = sl->implicit_w1[ra][rb];
+    WpRaw w;
+    w.lwd[0] = sl->luma_log2_wd;
+    w.lwd[1] = sl->chroma_log2_wd;
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) {
+        w.wa[pl] = sl->wp_weight[0][ra][pl];
+        w.wb[pl] = sl->wp_weight[1][rb][pl];
+        w.oa[pl] = sl->wp_offset[0][ra][pl];
+        w.ob[pl] = sl->wp_offset[1][rb][pl];
+    }
+    w.iw = sl->implicit_w1[ra][rb];
+    return w;
+}
+DEV WpPar wp_params(const WpRaw& w, int wp_mode, int dir, int pl)
+{
+    const int lwd = w.lwd[pl ? 1 : 0];
+    const int wa = w.wa[pl], wb = w.wb[pl], oa = w.oa[pl], ob = w.ob[pl], iw = w.iw;
     WpPar p;
     if (dir != 2) {
         const bool ex = wp_mode == 1;
@@ -721,8 +749,9 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
         uint32_t predY[4], predC[2];
         WpPar wpp[3] = {};
         if (wp_mode != 0) {
+            const WpRaw wr = wp_raw(qs, r0, r1);
     #pragma unroll
-            for (int pl = 0; pl < 3; ++pl) wpp[pl] = wp_params(qs, wp_mode, dir, r0, r1, pl);
+            for (int pl = 0; pl < 3; ++pl) wpp[pl] = wp_params(wr, wp_mode, dir, pl);
         }
     #pragma unroll
         for (int i = 0; i < 4; ++i) predY[i] = wp_combine4(wpp[0], wp_mode, dir, pY[0][i], pY[1][i]);

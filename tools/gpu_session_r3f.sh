@@ -1,7 +1,8 @@
 #!/bin/bash
 # tools/gpu_session_r3f.sh -- every GPU test at the working tree (branch-free chroma MC with
-# its six row loads in flight together; the workgroup's LDS tables from loads issued
-# together), then A/B against HEAD (varlib/head) on configs 3, 4, 2.
+# its six row loads in flight together; the workgroup LDS tables from loads issued
+# together; the WP parameters of all planes in one batch), then A/B against HEAD
+# (varlib/head) on configs 3, 4, 5.
 set -o pipefail
 O=gpurun_out/r3f; mkdir -p $O
 L=arrow-h264_amd/lib/libh264r.so; H=varlib/head/libh264r.so
