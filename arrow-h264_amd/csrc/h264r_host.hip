@@ -92,7 +92,8 @@ template <typename T>
 int dev_resize(T** p, size_t* cap, size_t n)
 {
     if (n <= *cap && *p) return H264R_OK;
-    if (*p) (void)hipFree(*p);
+    // work still queued may read the old buffer (h264r_picture_end_async): drain it first
+    if (*p) { (void)hipDeviceSynchronize(); (void)hipFree(*p); }
     *p = nullptr; *cap = 0;
     if (hipMalloc(reinterpret_cast<void**>(p), std::max<size_t>(n, 1) * sizeof(T)) != hipSuccess) return H264R_ENOMEM;
     *cap = n;
@@ -138,17 +139,25 @@ struct h264r_ctx {
     const uint8_t** d_ref_planes = nullptr;
     int* d_err = nullptr;                 // [0] device error word (a bounded wait expired), [1] wait bound
     uint32_t wait_ticks = 0;              // err[1] as last written (s_memrealtime ticks, 100 MHz)
-    // streaming-API staging
+    // streaming-API staging: two pictures, so that one is parsed (h264r_picture_begin /
+    // h264r_mb_submit) while the other is reconstructed (h264r_picture_end_async)
+    struct StreamPic {
+        int pw = 0, ph = 0;
+        std::vector<h264r_mb> h_mbs;
+        std::vector<int16_t> h_levels;
+        std::vector<uint32_t> h_mv;
+        std::vector<int8_t> h_ref;
+        std::vector<h264r_slice> h_slices;
+        h264r_pic h_pic{};
+        h264r_quant h_quant{};
+        std::vector<uint8_t> seen;
+        uint8_t* out = nullptr; size_t c_out = 0;   // pinned planes Y | Cb | Cr, then the error word
+        hipEvent_t done = nullptr;                 // its uploads, launches and readback
+        bool pending = false;
+    };
+    StreamPic sp[2];
+    int sp_fill = 0, sp_wait = 0, sp_pending = 0;
     bool in_pic = false;
-    int pw = 0, ph = 0;
-    std::vector<h264r_mb> h_mbs;
-    std::vector<int16_t> h_levels;
-    std::vector<uint32_t> h_mv;
-    std::vector<int8_t> h_ref;
-    std::vector<h264r_slice> h_slices;
-    h264r_pic h_pic{};
-    h264r_quant h_quant{};
-    std::vector<uint8_t> seen;
     // device buffers of the streaming API
     h264r_mb* d_mbs = nullptr; size_t c_mbs = 0;
     int16_t* d_levels = nullptr; size_t c_levels = 0;
@@ -297,6 +306,10 @@ int h264r_destroy(h264r_ctx* c)
     for (int s = 0; s < H264R_MAX_SLOTS; ++s) if (c->slot[s][0]) (void)hipFree(c->slot[s][0]);
     void* bufs[] = {c->d_ref_planes, c->d_err, c->d_mbs, c->d_levels, c->d_mv, c->d_ref, c->d_slices, c->d_pic, c->d_quant, c->d_out};
     for (void* b : bufs) if (b) (void)hipFree(b);
+    for (auto& p : c->sp) {
+        if (p.out) (void)hipHostFree(p.out);
+        if (p.done) (void)hipEventDestroy(p.done);
+    }
     for (int k = 0; k < MAX_PIPES; ++k) {
         c->sc[k].release();
         if (c->pipe_stream[k]) (void)hipStreamDestroy(c->pipe_stream[k]);
@@ -314,7 +327,11 @@ int h264r_destroy(h264r_ctx* c)
 static int ensure_slot(h264r_ctx* c, int slot, int w, int h)
 {
     if (c->slot[slot][0] && c->slot_w[slot] == w && c->slot_h[slot] == h) return H264R_OK;
-    if (c->slot[slot][0]) { (void)hipFree(c->slot[slot][0]); c->slot[slot][0] = nullptr; }
+    if (c->slot[slot][0]) {
+        (void)hipDeviceSynchronize();
+        (void)hipFree(c->slot[slot][0]);
+        c->slot[slot][0] = nullptr;
+    }
     size_t ys = (size_t)w * 16 * h * 16, cs = (size_t)w * 8 * h * 8;
     uint8_t* base = nullptr;
     if (hipMalloc(reinterpret_cast<void**>(&base), ys + 2 * cs + H264R_PLANE_SLACK) != hipSuccess) return H264R_ENOMEM;
@@ -793,16 +810,19 @@ int h264r_picture_begin(h264r_ctx* c, int w, int h, const h264r_pic* pic, const 
     if (!c || !pic || !slices || !quant || w <= 0 || h <= 0 || w > c->max_w || h > c->max_h ||
         pic->num_slices <= 0 || pic->num_slices > H264R_MAX_SLICES)
         return H264R_EINVAL;
-    c->pw = w; c->ph = h;
+    // both staging pictures in flight: the caller collects one first (h264r_picture_wait)
+    if (c->sp_pending == 2) return H264R_ESTATE;
+    auto& P = c->sp[c->sp_fill];
+    P.pw = w; P.ph = h;
     const size_t n = (size_t)w * h;
-    c->h_mbs.assign(n, h264r_mb{});
-    c->h_levels.clear();
-    c->h_mv.assign(2 * 16 * n, 0);
-    c->h_ref.assign(2 * 16 * n, -1);
-    c->h_slices.assign(slices, slices + pic->num_slices);
-    c->h_pic = *pic;
-    c->h_quant = *quant;
-    c->seen.assign(n, 0);
+    P.h_mbs.assign(n, h264r_mb{});
+    P.h_levels.clear();
+    P.h_mv.assign(2 * 16 * n, 0);
+    P.h_ref.assign(2 * 16 * n, -1);
+    P.h_slices.assign(slices, slices + pic->num_slices);
+    P.h_pic = *pic;
+    P.h_quant = *quant;
+    P.seen.assign(n, 0);
     c->in_pic = true;
     return H264R_OK;
 }
@@ -812,77 +832,120 @@ int h264r_mb_submit(h264r_ctx* c, int addr, const h264r_mb* mb, const int16_t* l
 {
     if (!c) return H264R_EINVAL;
     if (!c->in_pic) return H264R_ESTATE;
-    const int n = c->pw * c->ph;
+    auto& P = c->sp[c->sp_fill];
+    const int n = P.pw * P.ph;
     if (addr < 0 || addr >= n || !mb || n_levels < 0 || (n_levels && !levels) || !mv || !ref_idx) return H264R_EINVAL;
-    if (mb->slice >= c->h_pic.num_slices) return H264R_EINVAL;
+    if (mb->slice >= P.h_pic.num_slices) return H264R_EINVAL;
     if (mb->mb_type == H264R_SI) return H264R_EUNSUPPORTED;        // see include/h264r.h
     // lossless inter MBs: the kernels take intra_chroma_pred_mode as DC, which is what the
     // parser leaves in an inter MB (macroblock_t::init, slice_data.cc:482)
     if ((mb->flags & H264R_MBF_BYPASS) && !(mb->flags & H264R_MBF_INTRA) && mb->chroma_mode != 0) return H264R_EINVAL;
     h264r_mb m = *mb;
     // append the level block, 16-byte aligned
-    while (c->h_levels.size() % 8) c->h_levels.push_back(0);
-    m.coef_off = (uint32_t)c->h_levels.size();
-    c->h_levels.insert(c->h_levels.end(), levels, levels + n_levels);
-    c->h_mbs[addr] = m;
-    const int W4 = c->pw * 4, plane = W4 * c->ph * 4, x = addr % c->pw, y = addr / c->pw;
+    while (P.h_levels.size() % 8) P.h_levels.push_back(0);
+    m.coef_off = (uint32_t)P.h_levels.size();
+    P.h_levels.insert(P.h_levels.end(), levels, levels + n_levels);
+    P.h_mbs[addr] = m;
+    const int W4 = P.pw * 4, plane = W4 * P.ph * 4, x = addr % P.pw, y = addr / P.pw;
     for (int l = 0; l < 2; ++l)
         for (int k = 0; k < 16; ++k) {
             int idx = (y * 4 + k / 4) * W4 + x * 4 + k % 4;
-            c->h_mv[(size_t)l * plane + idx] = mv[l * 16 + k];
-            c->h_ref[(size_t)l * plane + idx] = ref_idx[l * 16 + k];
+            P.h_mv[(size_t)l * plane + idx] = mv[l * 16 + k];
+            P.h_ref[(size_t)l * plane + idx] = ref_idx[l * 16 + k];
         }
-    c->seen[addr] = 1;
+    P.seen[addr] = 1;
     return H264R_OK;
 }
 
-int h264r_picture_end(h264r_ctx* c, uint8_t* y, uint8_t* u, uint8_t* v, int keep_slot)
+int h264r_picture_end_async(h264r_ctx* c, int keep_slot)
 {
     if (!c) return H264R_EINVAL;
     if (!c->in_pic) return H264R_ESTATE;
     c->in_pic = false;
-    for (uint8_t s : c->seen) if (!s) return H264R_ESTATE;      // every MB must be submitted
+    auto& P = c->sp[c->sp_fill];
+    for (uint8_t s : P.seen) if (!s) return H264R_ESTATE;      // every MB must be submitted
     if (keep_slot >= H264R_MAX_SLOTS) return H264R_EINVAL;
     (void)hipSetDevice(c->device);
-    const size_t n = (size_t)c->pw * c->ph, ys = n * 256, cs = n * 64;
-    if (c->h_levels.empty()) c->h_levels.push_back(0);
-    int st = 0;
-    if ((st = dev_resize(&c->d_mbs, &c->c_mbs, n)) || (st = dev_resize(&c->d_levels, &c->c_levels, c->h_levels.size())) ||
-        (st = dev_resize(&c->d_mv, &c->c_mv, c->h_mv.size())) || (st = dev_resize(&c->d_ref, &c->c_ref, c->h_ref.size())) ||
-        (st = dev_resize(&c->d_slices, &c->c_slices, c->h_slices.size())) || (st = dev_resize(&c->d_pic, &c->c_pic, 1)) ||
-        (st = dev_resize(&c->d_quant, &c->c_quant, 1)) || (st = dev_resize(&c->d_out, &c->c_out, ys + 2 * cs)))
-        return st;
-    hipStream_t s = c->stream;
-    HIP_OK(hipMemcpyAsync(c->d_mbs, c->h_mbs.data(), n * sizeof(h264r_mb), hipMemcpyHostToDevice, s));
-    HIP_OK(hipMemcpyAsync(c->d_levels, c->h_levels.data(), c->h_levels.size() * 2, hipMemcpyHostToDevice, s));
-    HIP_OK(hipMemcpyAsync(c->d_mv, c->h_mv.data(), c->h_mv.size() * 4, hipMemcpyHostToDevice, s));
-    HIP_OK(hipMemcpyAsync(c->d_ref, c->h_ref.data(), c->h_ref.size(), hipMemcpyHostToDevice, s));
-    HIP_OK(hipMemcpyAsync(c->d_slices, c->h_slices.data(), c->h_slices.size() * sizeof(h264r_slice), hipMemcpyHostToDevice, s));
-    HIP_OK(hipMemcpyAsync(c->d_pic, &c->h_pic, sizeof(h264r_pic), hipMemcpyHostToDevice, s));
-    HIP_OK(hipMemcpyAsync(c->d_quant, &c->h_quant, sizeof(h264r_quant), hipMemcpyHostToDevice, s));
+    const size_t n = (size_t)P.pw * P.ph, ys = n * 256, cs = n * 64;
+    if (P.h_levels.empty()) P.h_levels.push_back(0);
     // every referenced slot must be loaded
-    for (const h264r_slice& sl : c->h_slices)
+    for (const h264r_slice& sl : P.h_slices)
         for (int l = 0; l < 2; ++l)
             for (int i = 0; i < sl.num_ref[l]; ++i) {
                 int slot = sl.ref_slot[l][i];
-                if (slot < 0 || slot >= H264R_MAX_SLOTS || !c->slot[slot][0] || c->slot_w[slot] != c->pw || c->slot_h[slot] != c->ph)
+                if (slot < 0 || slot >= H264R_MAX_SLOTS || !c->slot[slot][0] || c->slot_w[slot] != P.pw || c->slot_h[slot] != P.ph)
                     return H264R_ESTATE;
             }
+    int st = 0;
+    // the device inputs are one set, reused in stream order (dev_resize drains before it frees)
+    if ((st = dev_resize(&c->d_mbs, &c->c_mbs, n)) || (st = dev_resize(&c->d_levels, &c->c_levels, P.h_levels.size())) ||
+        (st = dev_resize(&c->d_mv, &c->c_mv, P.h_mv.size())) || (st = dev_resize(&c->d_ref, &c->c_ref, P.h_ref.size())) ||
+        (st = dev_resize(&c->d_slices, &c->c_slices, P.h_slices.size())) || (st = dev_resize(&c->d_pic, &c->c_pic, 1)) ||
+        (st = dev_resize(&c->d_quant, &c->c_quant, 1)) || (st = dev_resize(&c->d_out, &c->c_out, ys + 2 * cs)))
+        return st;
+    if (P.c_out < ys + 2 * cs + 16) {
+        if (P.out) (void)hipHostFree(P.out);
+        P.out = nullptr; P.c_out = 0;
+        if (hipHostMalloc(reinterpret_cast<void**>(&P.out), ys + 2 * cs + 16) != hipSuccess) return H264R_ENOMEM;
+        P.c_out = ys + 2 * cs + 16;
+    }
+    if (!P.done) HIP_OK(hipEventCreateWithFlags(&P.done, hipEventDisableTiming));
+    hipStream_t s = c->stream;
+    HIP_OK(hipMemcpyAsync(c->d_mbs, P.h_mbs.data(), n * sizeof(h264r_mb), hipMemcpyHostToDevice, s));
+    HIP_OK(hipMemcpyAsync(c->d_levels, P.h_levels.data(), P.h_levels.size() * 2, hipMemcpyHostToDevice, s));
+    HIP_OK(hipMemcpyAsync(c->d_mv, P.h_mv.data(), P.h_mv.size() * 4, hipMemcpyHostToDevice, s));
+    HIP_OK(hipMemcpyAsync(c->d_ref, P.h_ref.data(), P.h_ref.size(), hipMemcpyHostToDevice, s));
+    HIP_OK(hipMemcpyAsync(c->d_slices, P.h_slices.data(), P.h_slices.size() * sizeof(h264r_slice), hipMemcpyHostToDevice, s));
+    HIP_OK(hipMemcpyAsync(c->d_pic, &P.h_pic, sizeof(h264r_pic), hipMemcpyHostToDevice, s));
+    HIP_OK(hipMemcpyAsync(c->d_quant, &P.h_quant, sizeof(h264r_quant), hipMemcpyHostToDevice, s));
     h264r_batch b{};
-    b.num_pics = 1; b.width_mbs = c->pw; b.height_mbs = c->ph; b.slice_stride = (int)c->h_slices.size();
+    b.num_pics = 1; b.width_mbs = P.pw; b.height_mbs = P.ph; b.slice_stride = (int)P.h_slices.size();
     b.mbs = c->d_mbs; b.levels = c->d_levels; b.mv = c->d_mv; b.ref_idx = c->d_ref; b.slices = c->d_slices;
     b.pics = c->d_pic; b.quant = c->d_quant; b.ref_planes = c->d_ref_planes;
     b.out_y = c->d_out; b.out_u = c->d_out + ys; b.out_v = c->d_out + ys + cs;
     if ((st = run_batch(c, b, s, 0, b.height_mbs))) return st;
     if (keep_slot >= 0) {
-        if ((st = ensure_slot(c, keep_slot, c->pw, c->ph))) return st;
+        if ((st = ensure_slot(c, keep_slot, P.pw, P.ph))) return st;
         HIP_OK(hipMemcpyAsync(c->slot[keep_slot][0], c->d_out, ys + 2 * cs, hipMemcpyDeviceToDevice, s));
     }
-    if (y) HIP_OK(hipMemcpyAsync(y, b.out_y, ys, hipMemcpyDeviceToHost, s));
-    if (u) HIP_OK(hipMemcpyAsync(u, b.out_u, cs, hipMemcpyDeviceToHost, s));
-    if (v) HIP_OK(hipMemcpyAsync(v, b.out_v, cs, hipMemcpyDeviceToHost, s));
-    HIP_OK(hipStreamSynchronize(s));
-    return h264r_check(c);
+    // planes and the device error word into this picture's pinned staging; the error word is
+    // cleared behind it, so each picture reports its own failures
+    HIP_OK(hipMemcpyAsync(P.out, c->d_out, ys + 2 * cs, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipMemcpyAsync(P.out + ys + 2 * cs, c->d_err, sizeof(int), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipMemsetAsync(c->d_err, 0, sizeof(int), s));
+    HIP_OK(hipEventRecord(P.done, s));
+    P.pending = true;
+    ++c->sp_pending;
+    c->sp_fill = 1 - c->sp_fill;
+    return H264R_OK;
+}
+
+int h264r_picture_wait(h264r_ctx* c, uint8_t* y, uint8_t* u, uint8_t* v)
+{
+    if (!c) return H264R_EINVAL;
+    auto& P = c->sp[c->sp_wait];
+    if (!c->sp_pending || !P.pending) return H264R_ESTATE;
+    (void)hipSetDevice(c->device);
+    HIP_OK(hipEventSynchronize(P.done));
+    P.pending = false;
+    --c->sp_pending;
+    c->sp_wait = 1 - c->sp_wait;
+    const size_t n = (size_t)P.pw * P.ph, ys = n * 256, cs = n * 64;
+    if (y) memcpy(y, P.out, ys);
+    if (u) memcpy(u, P.out + ys, cs);
+    if (v) memcpy(v, P.out + ys + cs, cs);
+    int e = 0;
+    memcpy(&e, P.out + ys + 2 * cs, sizeof(int));
+    return e ? H264R_EDEVICE : H264R_OK;
+}
+
+int h264r_picture_end(h264r_ctx* c, uint8_t* y, uint8_t* u, uint8_t* v, int keep_slot)
+{
+    if (!c) return H264R_EINVAL;
+    if (c->sp_pending) return H264R_ESTATE;        // collect the asynchronous pictures first
+    int st = h264r_picture_end_async(c, keep_slot);
+    if (st) return st;
+    return h264r_picture_wait(c, y, u, v);
 }
 
 }  // extern "C"

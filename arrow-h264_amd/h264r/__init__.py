@@ -70,6 +70,8 @@ def lib() -> C.CDLL:
         "h264r_picture_begin": ([P, I, I, P, P, P], I),
         "h264r_mb_submit": ([P, I, P, P, I, P, P], I),
         "h264r_picture_end": ([P, P, P, P, I], I),
+        "h264r_picture_end_async": ([P, I], I),
+        "h264r_picture_wait": ([P, P, P, P], I),
         "h264r_decode_batch": ([P, C.POINTER(A.Batch), P], I),
         "h264r_decode_batch_rows": ([P, C.POINTER(A.Batch), I, I, P], I),
         "h264r_ref_planes": ([P, I, C.POINTER(P), C.POINTER(P), C.POINTER(P)], I),
@@ -185,6 +187,21 @@ class Decoder:
         u = np.empty((8 * H, 8 * W), np.uint8)
         v = np.empty((8 * H, 8 * W), np.uint8)
         _check("h264r_picture_end", self._L.h264r_picture_end(self._h, A.ptr(y), A.ptr(u), A.ptr(v), keep_slot))
+        return y, u, v
+
+    def deblock_filter_async(self, keep_slot: int = -1) -> None:
+        """h264r_picture_end_async: the picture is reconstructed while the caller stages
+        the next one; its planes come from wait() (oldest first)."""
+        _check("h264r_picture_end_async", self._L.h264r_picture_end_async(self._h, keep_slot))
+        self._waiting = getattr(self, "_waiting", []) + [self._dims]
+
+    def wait(self):
+        """h264r_picture_wait: planes of the oldest picture handed to deblock_filter_async."""
+        W, H = self._waiting.pop(0)
+        y = np.empty((16 * H, 16 * W), np.uint8)
+        u = np.empty((8 * H, 8 * W), np.uint8)
+        v = np.empty((8 * H, 8 * W), np.uint8)
+        _check("h264r_picture_wait", self._L.h264r_picture_wait(self._h, A.ptr(y), A.ptr(u), A.ptr(v)))
         return y, u, v
 
     def set_debug(self, flags: int) -> None:

@@ -4,6 +4,9 @@
 // order, cropped to the SPS window, 8-bit planar 4:2:0 (write_out_picture, output.cc:109-227).
 // Linked against libh264r.so it decodes on MI355X; the test build links the CPU
 // implementation of the same ABI instead (oracle/Makefile h264dec_cpu).
+// `-r N`: decode the stream N more times after the written pass and print the wall time per
+// frame of those passes (parse + reconstruction + readback, no file output) to stderr.
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -28,14 +31,15 @@ static int write_frame(void* user, const h264p_frame* f)
 int main(int argc, char** argv)
 {
     const char *in = nullptr, *outp = nullptr;
-    int device = 0;
+    int device = 0, repeat = 0;
     for (int i = 1; i + 1 < argc; i += 2) {
         if (!strcmp(argv[i], "-i")) in = argv[i + 1];
         else if (!strcmp(argv[i], "-o")) outp = argv[i + 1];
         else if (!strcmp(argv[i], "-d")) device = atoi(argv[i + 1]);
+        else if (!strcmp(argv[i], "-r")) repeat = atoi(argv[i + 1]);
     }
     if (!in || !outp) {
-        fprintf(stderr, "usage: %s -i stream.264 -o out.yuv [-d device]\n", argv[0]);
+        fprintf(stderr, "usage: %s -i stream.264 -o out.yuv [-d device] [-r repeats]\n", argv[0]);
         return 2;
     }
     FILE* f = fopen(in, "rb");
@@ -50,6 +54,14 @@ int main(int argc, char** argv)
     h264p_dec* dec = nullptr;
     int st = h264p_create(&dec, device);
     if (st == H264R_OK) st = h264p_decode(dec, data.data(), data.size(), write_frame, out);
+    if (st == H264R_OK && repeat > 0) {
+        long frames = 0;
+        auto count = [](void* u, const h264p_frame*) { ++*static_cast<long*>(u); return 0; };
+        const auto t0 = std::chrono::steady_clock::now();
+        for (int r = 0; r < repeat && st == H264R_OK; ++r) st = h264p_decode(dec, data.data(), data.size(), count, &frames);
+        const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        if (st == H264R_OK) fprintf(stderr, "h264dec: %ld frames, %.3f ms per frame\n", frames, ms / frames);
+    }
     if (st != H264R_OK)
         fprintf(stderr, "h264dec: %s (%s)\n", h264r_strerror(st), dec ? h264p_last_error(dec) : "");
     h264p_destroy(dec);

@@ -645,7 +645,8 @@ private:
     h264p_output_fn out_ = nullptr;
     void* user_ = nullptr;
     int stop_ = 0;
-    std::vector<uint8_t> y8_, u8_, v8_;
+    int inflight_ = -1;                        // pending_ entry whose planes are still on the GPU
+    bool sync_ = getenv("H264P_SYNC") != nullptr;   // A/B switch: h264r_picture_end per picture
 
     void nal(const uint8_t* p, size_t n);
     void slice(Bits& b, int nal_ref_idc, int nal_type);
@@ -657,6 +658,7 @@ private:
     h264r_slice slice_record(const SliceHeader& h);
     void mark_picture();
     void flush_output();
+    void collect();
 };
 
 // ------------------------------------------------------------------ NAL / slice layer
@@ -666,6 +668,9 @@ int Decoder::decode(const uint8_t* data, size_t size, h264p_output_fn out, void*
     user_ = user;
     stop_ = 0;
     err.clear();
+    if (inflight_ >= 0) (void)h264r_picture_wait(ctx_, nullptr, nullptr, nullptr);  // left by a failed call
+    inflight_ = -1;
+    pending_.clear();
     try {
         // Annex-B: start codes 0x000001 (B.2); a NAL ends at the next start code (its
         // trailing_zero_8bits dropped)
@@ -1096,13 +1101,22 @@ void Decoder::finish_picture()
         for (auto& q : dpb_)
             if (q->slot == keep) q->slot = -1;
     }
-    y8_.resize((size_t)W * H * 256);
-    u8_.resize((size_t)W * H * 64);
-    v8_.resize((size_t)W * H * 64);
-    check(h264r_picture_end(ctx_, y8_.data(), u8_.data(), v8_.data(), keep), "h264r_picture_end");
+    pending_.push_back(Output{period_, cur_->poc, {}, {}, {}});
+    if (sync_) {
+        Output& o = pending_.back();
+        o.y.resize((size_t)W * H * 256);
+        o.u.resize((size_t)W * H * 64);
+        o.v.resize((size_t)W * H * 64);
+        check(h264r_picture_end(ctx_, o.y.data(), o.u.data(), o.v.data(), keep), "h264r_picture_end");
+    } else {
+        // this picture is reconstructed while the next one is parsed; the previous one is
+        // collected now (the h264r ABI stages two pictures)
+        check(h264r_picture_end_async(ctx_, keep), "h264r_picture_end_async");
+        collect();
+        inflight_ = (int)pending_.size() - 1;
+    }
     cur_->slot = keep;
     mark_picture();
-    pending_.push_back(Output{period_, cur_->poc, y8_, u8_, v8_});
     // pictures no longer used for reference leave the DPB (their motion with them)
     dpb_.erase(std::remove_if(dpb_.begin(), dpb_.end(), [](const std::unique_ptr<Picture>& q) { return !q->ref; }),
                dpb_.end());
@@ -1177,8 +1191,22 @@ void Decoder::mark_picture()
     (void)cur_lt;
 }
 
+// Planes of the picture still on the GPU into its output entry.
+void Decoder::collect()
+{
+    if (inflight_ < 0) return;
+    Output& o = pending_[inflight_];
+    inflight_ = -1;
+    const size_t n = (size_t)psps_->W * psps_->H;
+    o.y.resize(n * 256);
+    o.u.resize(n * 64);
+    o.v.resize(n * 64);
+    check(h264r_picture_wait(ctx_, o.y.data(), o.u.data(), o.v.data()), "h264r_picture_wait");
+}
+
 void Decoder::flush_output()
 {
+    collect();
     std::stable_sort(pending_.begin(), pending_.end(),
                      [](const Output& a, const Output& b) { return a.period != b.period ? a.period < b.period : a.poc < b.poc; });
     const Sps& s = psps_ ? *psps_ : sps_[0];

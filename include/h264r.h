@@ -219,9 +219,20 @@ int  h264r_mb_submit(h264r_ctx* ctx, int mb_addr, const h264r_mb* mb,
                      const int16_t* levels, int n_levels,
                      const uint32_t* mv /*[2][16]*/, const int8_t* ref_idx /*[2][16]*/);
 /* Decoder::deblock_filter: reconstruct + deblock on the GPU, copy planes back.
- * If keep_as_ref_slot >= 0 the result also stays on the device as that DPB slot. */
+ * If keep_as_ref_slot >= 0 the result also stays on the device as that DPB slot.
+ * (H264R_ESTATE while a picture of the asynchronous form below is outstanding.) */
 int  h264r_picture_end(h264r_ctx* ctx, uint8_t* y, uint8_t* u, uint8_t* v,
                        int keep_as_ref_slot);
+/* The same, split so that the host parses the next picture while the GPU reconstructs this
+ * one: h264r_picture_end_async enqueues the upload, the reconstruction, the DPB-slot copy and
+ * the readback into pinned staging on the context's stream and returns; the next
+ * h264r_picture_begin may follow at once (two pictures are staged; a third begin before a
+ * wait is H264R_ESTATE).  A later picture may reference keep_as_ref_slot right away (stream
+ * order).  h264r_picture_wait blocks until the OLDEST outstanding picture is done and copies
+ * its planes out (NULL skips a plane); it reports that picture's device-side failures
+ * (H264R_EDEVICE), as h264r_check does for the synchronous form. */
+int  h264r_picture_end_async(h264r_ctx* ctx, int keep_as_ref_slot);
+int  h264r_picture_wait(h264r_ctx* ctx, uint8_t* y, uint8_t* u, uint8_t* v);
 
 /* ---- batch API (bench / throughput mode): arrays already on the device ---------- */
 /* Launches recon + deblock for every picture of the batch on `stream`

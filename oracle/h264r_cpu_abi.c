@@ -33,6 +33,9 @@ struct h264r_ctx {
     h264r_slice* slices;
     h264r_pic pic;
     h264r_quant quant;
+    uint8_t* async_out[2];      /* h264r_picture_end_async staging, Y | Cb | Cr */
+    size_t async_n[2];
+    int async_head, n_async;
 };
 
 static const int DQ4[6][3] = {{10, 13, 16}, {11, 14, 18}, {13, 16, 20}, {14, 18, 23}, {16, 20, 25}, {18, 23, 29}};
@@ -117,6 +120,8 @@ int h264r_destroy(h264r_ctx* c)
 {
     if (!c) return H264R_EINVAL;
     for (int s = 0; s < H264R_MAX_SLOTS; ++s) free(c->slot[s][0]);
+    free(c->async_out[0]);
+    free(c->async_out[1]);
     free_pic(c);
     free(c);
     return H264R_OK;
@@ -234,9 +239,8 @@ static void capture(const h264r_ctx* c, int keep, uint8_t* const out[3])
     fclose(f);
 }
 
-int h264r_picture_end(h264r_ctx* c, uint8_t* y, uint8_t* u, uint8_t* v, int keep)
+static int picture_end(h264r_ctx* c, uint8_t* y, uint8_t* u, uint8_t* v, int keep)
 {
-    if (!c) return H264R_EINVAL;
     if (!c->in_pic) return H264R_ESTATE;
     c->in_pic = 0;
     const int n = c->pw * c->ph;
@@ -260,6 +264,46 @@ int h264r_picture_end(h264r_ctx* c, uint8_t* y, uint8_t* u, uint8_t* v, int keep
         if ((st = h264r_set_ref(c, keep, y, u, v, c->pw, c->ph))) return st;
     }
     return H264R_OK;
+}
+
+/* The asynchronous form: the CPU computes the picture at once into one of two staging sets,
+ * h264r_picture_wait hands them out oldest first (the GPU library's contract). */
+int h264r_picture_end_async(h264r_ctx* c, int keep)
+{
+    if (!c) return H264R_EINVAL;
+    if (c->n_async == 2) return H264R_ESTATE;
+    const size_t n = (size_t)c->pw * c->ph;
+    const int k = (c->async_head + c->n_async) % 2;
+    uint8_t* buf = (uint8_t*)realloc(c->async_out[k], n * 384);
+    if (!buf) return H264R_ENOMEM;
+    c->async_out[k] = buf;
+    c->async_n[k] = n;
+    int st = picture_end(c, buf, buf + n * 256, buf + n * 320, keep);
+    if (st) return st;
+    ++c->n_async;
+    return H264R_OK;
+}
+
+int h264r_picture_wait(h264r_ctx* c, uint8_t* y, uint8_t* u, uint8_t* v)
+{
+    if (!c) return H264R_EINVAL;
+    if (!c->n_async) return H264R_ESTATE;
+    const int k = c->async_head;
+    const size_t n = c->async_n[k];
+    const uint8_t* buf = c->async_out[k];
+    if (y) memcpy(y, buf, n * 256);
+    if (u) memcpy(u, buf + n * 256, n * 64);
+    if (v) memcpy(v, buf + n * 320, n * 64);
+    c->async_head = (k + 1) % 2;
+    --c->n_async;
+    return H264R_OK;
+}
+
+int h264r_picture_end(h264r_ctx* c, uint8_t* y, uint8_t* u, uint8_t* v, int keep)
+{
+    if (!c) return H264R_EINVAL;
+    if (c->n_async) return H264R_ESTATE;
+    return picture_end(c, y, u, v, keep);
 }
 
 int h264r_check(h264r_ctx* c) { return c ? H264R_OK : H264R_EINVAL; }

@@ -401,3 +401,48 @@ def test_gpu_expired_wait_reports_edevice(L, dec):
         got = dec.decode_picture(p, refs, debug=flag)
         for k in range(3):
             assert np.array_equal(got[k], want[k]), (flag, k)
+
+
+def test_gpu_async_pictures_overlap(L, dec):
+    """h264r_picture_end_async / h264r_picture_wait: picture i+1 is staged and enqueued while
+    picture i is still on the GPU, referencing the DPB slot picture i is written into (stream
+    order); every picture equals the oracle's, the waits hand them out oldest first, a third
+    picture before a wait and a synchronous end with pictures outstanding are H264R_ESTATE."""
+    from h264r.mbview import iter_mbs
+    W, H, n = 22, 18, 5
+    cfg = synth.default_cfg(L, 3, W, H)
+    refs = synth.refpics(L, cfg)
+    for s, (y, u, v) in enumerate(refs):
+        dec.set_ref(s, y, u, v)
+    pics = [synth.picture(L, cfg, i) for i in range(n)]
+    want, oracle_refs = [], list(refs)
+    for p in pics:
+        out = O.decode(p, oracle_refs)
+        oracle_refs = [out] + oracle_refs[1:]
+        want.append(out)
+
+    def stage(p):
+        dec.init(W, H, p.pic, p.slices)
+        for addr, rec, lv, mv, rr in iter_mbs(p):
+            dec.decode(addr, rec, lv, mv, rr)
+
+    got = []
+    stage(pics[0])
+    dec.deblock_filter_async(keep_slot=0)
+    for i in range(1, n):
+        stage(pics[i])
+        dec.deblock_filter_async(keep_slot=0)
+        if i == 2:
+            with pytest.raises(h264r.H264RError) as e:
+                dec.init(W, H, pics[0].pic, pics[0].slices)     # two pictures outstanding
+            assert e.value.status == A.ESTATE
+        got.append(dec.wait())
+    with pytest.raises(h264r.H264RError) as e:
+        stage(pics[0])
+        dec.deblock_filter()                                   # one picture outstanding
+    assert e.value.status == A.ESTATE
+    got.append(dec.wait())
+    for i in range(n):
+        for k in range(3):
+            d = first_diff(got[i][k], want[i][k], 16 if k == 0 else 8)
+            assert d is None, f"picture {i} plane {k}: {d}"

@@ -76,6 +76,16 @@ def test_parser_hands_the_abi_what_the_reference_parser_did(name, tmp_path):
         assert a["plane_md5"] == b["plane_md5"], f"picture {i}: reconstructed planes"
 
 
+@pytest.mark.parametrize("name", ["bp_qcif_ippp", "hp_cif_cabac_ibbp_4slices"])
+def test_parser_synchronous_mode_matches(name, tmp_path):
+    """H264P_SYNC=1 (h264r_picture_end per picture instead of the overlapped
+    h264r_picture_end_async / h264r_picture_wait pair): the same frames."""
+    out = tmp_path / "out.yuv"
+    r = _run(_cpu_dec(), name, out, {"H264P_SYNC": "1"})
+    assert r.returncode == 0, r.stderr[-800:]
+    assert OUT.digest_by_frames(str(out), S.STREAMS[name]["frames"]) == GOLD[name]["frame_md5"]
+
+
 def test_parser_covers_both_entropy_coders():
     assert {bool(c.get("cabac")) for c in S.STREAMS.values()} == {False, True}
 
