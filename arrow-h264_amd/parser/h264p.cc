@@ -61,13 +61,21 @@ struct Bits {
         buf.insert(buf.end(), 8, 0);
         pos = 0;
     }
-    uint32_t peek(int n) const
+    // the n (1..32) bits at bit position p, zeros past the end (one big-endian 8-byte load
+    // inside the buffer, which ends in 8 zero bytes)
+    uint32_t peek_at(size_t p, int n) const
     {
-        const size_t b = pos >> 3;
+        const size_t b = p >> 3;
         uint64_t w = 0;
-        for (int k = 0; k < 5; ++k) w = w << 8 | buf[b + k];
-        return (uint32_t)((w >> (40 - (pos & 7) - n)) & ((1ull << n) - 1));
+        if (b + 8 <= buf.size()) {
+            memcpy(&w, &buf[b], 8);
+            w = __builtin_bswap64(w);
+        } else {
+            for (size_t k = 0; k < 8; ++k) w = w << 8 | (b + k < buf.size() ? buf[b + k] : 0);
+        }
+        return (uint32_t)((w << (p & 7)) >> (64 - n));
     }
+    uint32_t peek(int n) const { return peek_at(pos, n); }
     void skip(int n)
     {
         pos += n;
@@ -160,8 +168,32 @@ const Tables& tables()
 // and the slice end follow it); the contexts in the reference's layout (cabac_tables.h).
 struct Cabac {
     Bits* b = nullptr;
-    uint32_t range = 510, offset = 0;
-    uint8_t state[CABAC_CONTEXTS], mps[CABAC_CONTEXTS];
+    uint32_t range = 510;
+    // codIOffset with k look-ahead bits below it: value = codIOffset << k | the next k bits of
+    // the RBSP (loaded up to bit lpos), so RenormD only lowers k and the RBSP is read 32 bits
+    // at a time; the exact bit position (lpos - k) is handed back to the RBSP where the spec
+    // reads raw bits after a terminating bin (I_PCM samples)
+    uint64_t value = 0;
+    int k = 0;
+    size_t lpos = 0;
+    uint8_t st[CABAC_CONTEXTS];                        // pStateIdx << 1 | valMPS
+
+    struct Trans {
+        uint8_t mps[128], lps[128];
+        Trans()
+        {
+            for (int s = 0; s < 64; ++s)
+                for (int m = 0; m < 2; ++m) {
+                    mps[s << 1 | m] = (uint8_t)(TRANS_MPS[s] << 1 | m);
+                    lps[s << 1 | m] = (uint8_t)(TRANS_LPS[s] << 1 | (s == 0 ? 1 - m : m));
+                }
+        }
+    };
+    static const Trans& trans()
+    {
+        static const Trans t;
+        return t;
+    }
 
     // cabac_contexts_t::init (bitstream_cabac.cc:1215-1264): kind 0 = I, 1..3 = P idc, 4..6 = B idc
     void init_contexts(int kind, int qp)
@@ -169,31 +201,40 @@ struct Cabac {
         qp = clip3(0, 51, qp);
         for (int i = 0; i < CABAC_CONTEXTS; ++i) {
             const int pre = clip3(1, 126, ((CABAC_MN[kind][i][0] * qp) >> 4) + CABAC_MN[kind][i][1]);
-            if (pre <= 63) { state[i] = (uint8_t)(63 - pre); mps[i] = 0; }
-            else { state[i] = (uint8_t)(pre - 64); mps[i] = 1; }
+            st[i] = pre <= 63 ? (uint8_t)((63 - pre) << 1) : (uint8_t)((pre - 64) << 1 | 1);
         }
+    }
+    void refill()
+    {
+        value = value << 32 | b->peek_at(lpos, 32);
+        lpos += 32;
+        k += 32;
     }
     void init_engine(Bits& bits)                       // cabac_engine_t::init: byte-align, 9 bits
     {
         b = &bits;
         while (!b->aligned()) b->u(1);
         range = 510;
-        offset = b->u(9);
+        value = b->u(9);
+        lpos = b->pos;
+        k = 0;
+        refill();
     }
     int dec(int ctx)
     {
-        const uint32_t lps = RANGE_LPS[state[ctx]][(range >> 6) & 3];
-        int bin;
+        const int s = st[ctx];
+        const uint32_t lps = RANGE_LPS[s >> 1][(range >> 6) & 3];
         range -= lps;
-        if (offset < range) {
-            bin = mps[ctx];
-            state[ctx] = TRANS_MPS[state[ctx]];
+        const uint64_t r = (uint64_t)range << k;
+        int bin;
+        if (value < r) {
+            bin = s & 1;
+            st[ctx] = trans().mps[s];
         } else {
-            bin = !mps[ctx];
-            offset -= range;
+            bin = !(s & 1);
+            value -= r;
             range = lps;
-            if (state[ctx] == 0) mps[ctx] = (uint8_t)(1 - mps[ctx]);
-            state[ctx] = TRANS_LPS[state[ctx]];
+            st[ctx] = trans().lps[s];
         }
         renorm();
         return bin;
@@ -203,20 +244,34 @@ struct Cabac {
         if (range < 256) {
             const int sh = __builtin_clz(range) - 23;
             range <<= sh;
-            offset = (offset << sh) | b->u(sh);
+            k -= sh;
+            if (k < 16) refill();
         }
     }
     int bypass()
     {
-        offset = (offset << 1) | b->bit();
-        if (offset < range) return 0;
-        offset -= range;
-        return 1;
+        --k;
+        const uint64_t r = (uint64_t)range << k;
+        int bin = 0;
+        if (value >= r) {
+            value -= r;
+            bin = 1;
+        }
+        if (k < 16) refill();
+        return bin;
+    }
+    void check_end() const
+    {
+        if (lpos - k > b->nbits) fail(H264R_EINVAL, "bitstream: read past the end of a NAL unit");
     }
     int term()
     {
         range -= 2;
-        if (offset >= range) return 1;
+        check_end();
+        if (value >= (uint64_t)range << k) {
+            b->pos = lpos - k;                         // the RBSP continues here (I_PCM samples)
+            return 1;
+        }
         renorm();
         return 0;
     }
@@ -1247,7 +1302,7 @@ void SliceCtx::run()
         cab->init_engine(b);
         for (;;) {
             macroblock();
-            if (addr == W * H - 1) return;
+            if (addr == W * H - 1) { cab->check_end(); return; }
             const int eos = cab->term();
             ++addr;
             if (eos) return;
