@@ -98,9 +98,10 @@ struct Bits {
     }
     uint32_t ue()
     {
-        int lz = 0;
-        while (!bit())
-            if (++lz > 31) fail(H264R_EINVAL, "bitstream: ue(v) longer than 32 bits");
+        const uint32_t w = peek_at(pos, 32);
+        if (!w) fail(H264R_EINVAL, "bitstream: ue(v) longer than 32 bits");
+        const int lz = __builtin_clz(w);                // the leading zeros, then the 1
+        skip(lz + 1);
         return lz ? (uint32_t)((1ull << lz) - 1 + u(lz)) : 0;
     }
     int32_t se()
@@ -112,28 +113,29 @@ struct Bits {
     bool more_rbsp_data() const { return pos < stop; }
 };
 
-// A VLC table as a 16-bit prefix lookup: value and length of the codeword the next 16 bits
-// start with (len 0: no codeword).
+// A VLC table as a prefix lookup over its longest codeword: value | length << 8 of the
+// codeword the next `bits` bits start with (length 0: no codeword).  Sized per table (total_zeros
+// 9 bits, run_before 11, coeff_token up to 16), so the tables the residual reads stay in cache.
 struct Vlc {
-    std::vector<uint16_t> val;
-    std::vector<uint8_t> len;
+    int bits = 1;
+    std::vector<uint16_t> e;
     template <typename E, typename F>
-    void build(const E* e, int n, F value)
+    void build(const E* c, int n, F value)
     {
-        val.assign(1 << 16, 0);
-        len.assign(1 << 16, 0);
+        bits = 1;
+        for (int i = 0; i < n; ++i) bits = std::max(bits, (int)c[i].len);
+        e.assign((size_t)1 << bits, 0);
         for (int i = 0; i < n; ++i) {
-            const int l = e[i].len, c = e[i].code;
-            const int lo = c << (16 - l), hi = lo + (1 << (16 - l));
-            for (int k = lo; k < hi; ++k) { val[k] = (uint16_t)value(e[i]); len[k] = (uint8_t)l; }
+            const int l = c[i].len, lo = c[i].code << (bits - l), hi = lo + (1 << (bits - l));
+            for (int k = lo; k < hi; ++k) e[k] = (uint16_t)(value(c[i]) | l << 8);
         }
     }
     int read(Bits& b, const char* what) const
     {
-        const uint32_t w = b.peek(16);
-        if (!len[w]) fail(H264R_EINVAL, std::string("bitstream: no ") + what + " codeword");
-        b.skip(len[w]);
-        return val[w];
+        const uint16_t v = e[b.peek(bits)];
+        if (!(v >> 8)) fail(H264R_EINVAL, std::string("bitstream: no ") + what + " codeword");
+        b.skip(v >> 8);
+        return v & 255;
     }
 };
 
