@@ -37,6 +37,7 @@ struct IntraScratch {
     alignas(16) int res[16][16];          // luma residual (I_4x4 / I_8x8; every type when lossless)
     alignas(16) int cres[2][8][8];        // chroma residual of lossless MBs
     alignas(16) uint8_t fs[32];           // I_8x8 filtered neighbours: [3] Q, [4 + x] T[x], [20 + y] L[y]
+    alignas(16) uint8_t fe[32];           // the same in e[] order: e[k] at [k + 1] (intra_nxn_tap)
 };
 
 DEV int ti(int x, int y) { return (y + 1) * ITP + x + 4; }          // luma tile index
@@ -516,49 +517,42 @@ DEV void intra_mb_compute(const h264r_batch& b, const Geom& g, int pic, int mbx,
         for (int c = 0; c < 4; ++c) w |= (uint32_t)clip255(p[c] + resL[c]) << (8 * c);
         *reinterpret_cast<uint32_t*>(rmb + y * 16 + x0) = w;
     } else if (i8) {
+        // I_8x8, its 4 blocks in order (unrolled: each block's availability and mode are
+        // wave-uniform).  The reference sample filter (intra_prediction.cc:413-447) runs on
+        // lanes 0..24 over the sequence s = L[7..0], Q, T[0..15] (s[j] = e[j + 1]): every
+        // filtered sample is (A + 2 B + C + 2) >> 2 of its two sequence neighbours, a
+        // neighbour outside the sequence or unavailable being B itself -- one form, selects
+        // instead of lane-divergent branches.  The result goes to S.fe in e[] order (e[k] at
+        // fe[k + 1], the repeated ends included; the taps read fe[i .. i + 2]) and to S.fs
+        // (the DC sums).
         uint32_t tab[3];
         intra_tap_table<8>(lane & 7, lane >> 3, tab);
-#pragma unroll 1
+        const int j = min(lane, 24);
+        const int at_e = lane < 25 ? j + 2 : 31, at_dup = lane == 0 ? 1 : (lane == 24 ? 27 : 31);
+        const int at_fs = lane >= 25 ? 31 : (j < 8 ? 27 - j : (j == 8 ? 3 : j - 5));
+#pragma unroll
         for (int blk = 0; blk < 4; ++blk) {
             const int xO = (blk & 1) * 8, yO = (blk >> 1) * 8;
             const int aA = xO > 0 ? 1 : avA, aB = yO > 0 ? 1 : avB;
             const int aD = (xO > 0 && yO > 0) ? 1 : (xO == 0 && yO == 0) ? avD : (xO == 0 ? avA : avB);
             const int aC = yO > 0 ? (xO == 0) : (xO == 0 ? avB : avC);   // intra_prediction.cc:370-376
             const int mode = (int)((ipw >> (4 * blk)) & 15);
-            // reference sample filtering (intra_prediction.cc:413-447) -> S.fs
-            auto po = [&](int x, int y) -> int {
-                if (y < 0 && x >= 8 && !aC) x = 7;                   // p(x,-1) substitution :404-407
-                return S.tile[ti(xO + x, yO + y)];
+            const int tcap = aC ? 15 : 7;                                // p(x,-1) substitution :404-407
+            const int bo = ti(xO, yO);
+            auto off = [&](int k) -> int {                               // tile offset of s[k] from the block origin
+                int l = (7 - k) * ITP - 1, t = min(k - 9, tcap) - ITP;
+                asm volatile("" : "+v"(l), "+v"(t));
+                return k < 8 ? l : t;
             };
-            if (lane < 25) {
-                int v = 0, at;
-                if (lane == 0) {                                       // p(-1,-1)
-                    at = 3;
-                    if (aD) {
-                        if (aA && aB) v = (po(0, -1) + 2 * po(-1, -1) + po(-1, 0) + 2) >> 2;
-                        else if (aB) v = (3 * po(-1, -1) + po(0, -1) + 2) >> 2;
-                        else if (aA) v = (3 * po(-1, -1) + po(-1, 0) + 2) >> 2;
-                        else v = po(-1, -1);
-                    }
-                } else if (lane <= 16) {                               // p(x,-1), x = lane-1
-                    const int x = lane - 1;
-                    at = 4 + x;
-                    if (aB) {
-                        if (x == 0) v = aD ? (po(-1, -1) + 2 * po(0, -1) + po(1, -1) + 2) >> 2 : (3 * po(0, -1) + po(1, -1) + 2) >> 2;
-                        else if (x < 15) v = (po(x - 1, -1) + 2 * po(x, -1) + po(x + 1, -1) + 2) >> 2;
-                        else v = (po(14, -1) + 3 * po(15, -1) + 2) >> 2;
-                    }
-                } else {                                               // p(-1,y), y = lane-17
-                    const int y = lane - 17;
-                    at = 20 + y;
-                    if (aA) {
-                        if (y == 0) v = aD ? (po(-1, -1) + 2 * po(-1, 0) + po(-1, 1) + 2) >> 2 : (3 * po(-1, 0) + po(-1, 1) + 2) >> 2;
-                        else if (y < 7) v = (po(-1, y - 1) + 2 * po(-1, y) + po(-1, y + 1) + 2) >> 2;
-                        else v = (po(-1, 6) + 3 * po(-1, 7) + 2) >> 2;
-                    }
-                }
-                S.fs[at] = (uint8_t)v;
-            }
+            const int B = S.tile[bo + off(j)];
+            int A = S.tile[bo + off(max(j - 1, 0))], C = S.tile[bo + off(min(j + 1, 24))];
+            A = (j == 9 && !aD) || (j == 8 && !aA) ? B : A;
+            C = (j == 7 && !aD) || (j == 8 && !aB) ? B : C;
+            const bool valid = j < 8 ? aA : (j == 8 ? aD : aB);
+            const int v = valid ? (A + 2 * B + C + 2) >> 2 : 0;
+            S.fe[at_e] = (uint8_t)v;
+            S.fe[at_dup] = (uint8_t)v;
+            S.fs[at_fs] = (uint8_t)v;
             wave_sync();
             {
                 const int x = lane & 7, y = lane >> 3;
@@ -569,11 +563,8 @@ DEV void intra_mb_compute(const h264r_batch& b, const Geom& g, int pic, int mbx,
                     p = aA && aB ? (st + sl + 8) >> 4 : aB ? (st + 4) >> 3 : aA ? (sl + 4) >> 3 : 128;
                 } else {
                     const int ent = intra_tap_entry(tab, mode), kind = ent >> 5, i = ent & 31;
-                    auto E = [&](int k) -> int {                       // e[k] from S.fs
-                        const int at = k <= 8 ? 20 + min(7, 8 - k) : (k == 9 ? 3 : 4 + min(k - 10, 15));
-                        return S.fs[at];
-                    };
-                    p = tap_apply(kind, E(max(i - 1, 0)), E(i), E(min(i + 1, 26)));
+                    const uint8_t* e = &S.fe[i];                       // e[i - 1], e[i], e[i + 1]
+                    p = tap_apply(kind, e[0], e[1], e[2]);
                 }
                 const int v = (cbpl >> blk) & 1 ? clip255(p + S.res[yO + y][xO + x]) : p;
                 S.tile[ti(xO + x, yO + y)] = (uint8_t)v;
@@ -581,37 +572,55 @@ DEV void intra_mb_compute(const h264r_batch& b, const Geom& g, int pic, int mbx,
             wave_sync();
         }
     } else {
-        // I_4x4: block (bx, by) at step bx + 2 by; slot 0 takes the block with the larger bx
+        // I_4x4: block (bx, by) at step bx + 2 by, two blocks per step: lanes 0..15 (slot 0) the
+        // one with the larger bx, lanes 16..31 (slot 1) the other.  The steps are unrolled, so
+        // each slot's block, availability and mode are wave-uniform (scalar) and a lane only
+        // selects between the two slots' values; every per-lane expression is a select, not a
+        // branch (a lane-divergent branch runs both sides anyway, plus the exec-mask work).
         uint32_t tab[3];
         intra_tap_table<4>(lane & 3, (lane >> 2) & 3, tab);
-#pragma unroll 1
+        const int slot = (lane >> 4) & 1, x = lane & 3, y = (lane >> 2) & 3;
+        const bool half = lane < 32;
+#pragma unroll
         for (int s = 0; s < 10; ++s) {
-            const int slot = lane >> 4, pix = lane & 15, x = pix & 3, y = pix >> 2;
-            const int by = (s >> 1) - 1 + slot, bx = s - 2 * by;
-            if (lane < 32 && by >= 0 && by <= 3 && bx <= 3) {
+            // compile-time block coordinates of the two slots
+            const int by0 = (s >> 1) - 1, bx0 = (s & 1) + 2, by1 = s >> 1, bx1 = s & 1;
+            const bool ok0 = by0 >= 0, ok1 = by1 <= 3;
+            auto blk_par = [&](int bx, int by, int& mode, int& aA, int& aB, int& tmax, int& base) {
                 const int xO = bx * 4, yO = by * 4;
                 const int bk = (by >> 1) * 8 + (bx >> 1) * 4 + (by & 1) * 2 + (bx & 1);   // blkIdx
-                const int aA = xO > 0 ? 1 : avA, aB = yO > 0 ? 1 : avB;
-                int aC;
-                if (yO == 0) aC = xO + 4 < 16 ? avB : avC;
-                else aC = (xO + 4 < 16) && !(xO == 4 && (yO == 4 || yO == 12));      // :154
-                const int mode = (int)((ipw >> (4 * bk)) & 15);
-                // branch-free: the directional tap and DC are both evaluated, then selected
-                const int ent = intra_tap_entry(tab, mode), kind = ent >> 5, i = ent & 31;
-                const int tmax = aC ? 7 : 3;
-                const int base = ti(xO, yO);
-                auto eoff = [&](int k) -> int {                          // tile offset of e[k] from the block origin
-                    return k <= 5 ? min(3, 4 - k) * ITP - 1 : min(k - 6, tmax) - ITP;
-                };
-                const int e0 = S.tile[base + eoff(max(i - 1, 0))], e1 = S.tile[base + eoff(i)];
-                const int e2 = S.tile[base + eoff(min(i + 1, 14))];
-                const int st = sum4(lds_u32(&S.tile[base - ITP]));       // DC (intra_prediction.cc:214-229)
-                const int sl = S.tile[base - 1] + S.tile[base + ITP - 1] + S.tile[base + 2 * ITP - 1] + S.tile[base + 3 * ITP - 1];
-                const int dc = aA && aB ? (st + sl + 4) >> 3 : aB ? (st + 2) >> 2 : aA ? (sl + 2) >> 2 : 128;
-                const int p = mode == 2 ? dc : tap_apply(kind, e0, e1, e2);
-                const int v = clip255(p + S.res[yO + y][xO + x]);     // residual is 0 in uncoded blocks
-                S.tile[ti(xO + x, yO + y)] = (uint8_t)v;
-            }
+                aA = xO > 0 ? 1 : avA;
+                aB = yO > 0 ? 1 : avB;
+                const int aC = yO == 0 ? (xO + 4 < 16 ? avB : avC) : ((xO + 4 < 16) && !(xO == 4 && (yO == 4 || yO == 12)));   // :154
+                tmax = aC ? 7 : 3;
+                mode = (int)((ipw >> (4 * bk)) & 15);
+                base = ti(xO, yO);
+            };
+            int m0 = 2, a0 = 0, b0 = 0, t0 = 3, base0 = 0, m1 = 2, a1 = 0, b1 = 0, t1 = 3, base1 = 0;
+            if (ok0) blk_par(bx0, by0, m0, a0, b0, t0, base0);
+            if (ok1) blk_par(bx1, by1, m1, a1, b1, t1, base1);
+            const bool on = half && (slot ? ok1 : ok0);
+            const int mode = slot ? m1 : m0, aA = slot ? a1 : a0, aB = slot ? b1 : b0;
+            const int tmax = slot ? t1 : t0, base = slot ? base1 : base0;
+            const int ent = intra_tap_entry(tab, mode), kind = ent >> 5, i = ent & 31;
+            // tile offset of e[k] from the block origin: the left column bottom-up (k <= 5, the
+            // corner at 5), then the row above clamped at tmax; both forms computed, one selected
+            auto eoff = [&](int k) -> int {
+                int l = (3 - max(k - 1, 0)) * ITP - 1, t = min(k - 6, tmax) - ITP;
+                asm volatile("" : "+v"(l), "+v"(t));
+                return k <= 5 ? l : t;
+            };
+            // lanes without a block read around an interior origin (every offset inside the tile)
+            const int pb = on ? base : ti(4, 4);
+            const int e0 = S.tile[pb + eoff(max(i - 1, 0))], e1 = S.tile[pb + eoff(i)];
+            const int e2 = S.tile[pb + eoff(min(i + 1, 14))];
+            const int st = sum4(lds_u32(&S.tile[pb - ITP]));       // DC (intra_prediction.cc:214-229)
+            const int sl = S.tile[pb - 1] + S.tile[pb + ITP - 1] + S.tile[pb + 2 * ITP - 1] + S.tile[pb + 3 * ITP - 1];
+            const int dc = aA && aB ? (st + sl + 4) >> 3 : aB ? (st + 2) >> 2 : aA ? (sl + 2) >> 2 : 128;
+            const int p = mode == 2 ? dc : tap_apply(kind, e0, e1, e2);
+            // residual (0 in uncoded blocks) at tile position pb + y * ITP + x
+            const int v = clip255(p + S.res[(pb >> 5) - 1 + y][(pb & 31) - 4 + x]);
+            if (on) S.tile[pb + y * ITP + x] = (uint8_t)v;
             wave_sync();
         }
     }
@@ -630,19 +639,15 @@ DEV void intra_mb_compute(const h264r_batch& b, const Geom& g, int pic, int mbx,
         const int mode = m.chroma_mode;
         int p[2];
         if (mode == 0) {
+            // per 4x4 block: both sums read, the available ones selected (no lane-divergent branch)
             const int xO = x0 & 4, yO = y & 4;
-            int aA, aB;
-            if ((xO == 0 && yO == 0) || (xO > 0 && yO > 0)) { aA = avA; aB = avB; }
-            else if (xO > 0) { aA = avB ? 0 : avA; aB = avB; }
-            else { aA = avA; aB = avA ? 0 : avB; }
-            int sum = 0, v = 128;
-            if (aA || aB) {
-                if (aA)
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) sum += C[ci(-1, yO + k)];
-                if (aB) sum += sum4(lds_u32(&C[ci(xO, -1)]));
-                v = (sum + (aA ? 2 : 0) + (aB ? 2 : 0)) >> (1 + aA + aB);
-            }
+            const bool diag = (xO == 0) == (yO == 0);                  // blocks (0,0) and (4,4)
+            const int aA = diag || xO == 0 ? avA : (avB ? 0 : avA);
+            const int aB = diag || xO > 0 ? avB : (avA ? 0 : avB);
+            const int sl = C[ci(-1, yO)] + C[ci(-1, yO + 1)] + C[ci(-1, yO + 2)] + C[ci(-1, yO + 3)];
+            const int st = sum4(lds_u32(&C[ci(xO, -1)]));
+            const int sum = (aA ? sl : 0) + (aB ? st : 0) + (aA ? 2 : 0) + (aB ? 2 : 0);
+            const int v = aA || aB ? sum >> (1 + aA + aB) : 128;
             p[0] = p[1] = v;
         } else if (mode == 1) {
             p[0] = p[1] = C[ci(-1, y)];
