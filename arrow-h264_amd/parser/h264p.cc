@@ -11,11 +11,13 @@
 #include "h264p.h"
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "cabac_tables.h"
@@ -625,7 +627,12 @@ struct SliceCtx {
     uint16_t cbp_blks = 0;
     int32_t cof[3][16][16];
 
-    SliceCtx(Decoder& d, const Sps& s, const Pps& p, const SliceHeader& h, int nr, Bits& bits);
+    Picture* const (*list_)[33];  // RefPicList of this slice (the slices of a picture may run in parallel)
+    const int* list_n_;
+    int end_mb;                   // the next slice's first MB (a slice running into it is malformed)
+
+    SliceCtx(Decoder& d, const Sps& s, const Pps& p, const SliceHeader& h, int nr, Bits& bits,
+             Picture* const (*lists)[33], const int* list_n, int end);
     void run();
     void macroblock();
     MbState* nb_mb(bool chroma, int xN, int yN, int& ax, int& ay);
@@ -684,6 +691,20 @@ public:
     std::vector<h264r_slice> slice_tab_;
     h264r_quant quant_;
     bool have_quant_ = false;
+    // the picture's slices, parsed when the picture ends: on several threads when it has
+    // several (slices never read each other's syntax: every neighbour across a slice edge is
+    // "not available"), H264P_THREADS (default: up to 8) threads
+    struct PendingSlice {
+        SliceHeader h;
+        Bits b;
+        int nr;
+        const Sps* sps;
+        const Pps* pps;
+        Picture* list[2][33];
+        int list_n[2];
+    };
+    std::vector<std::unique_ptr<PendingSlice>> pslices_;
+    void run_slices();
 
 private:
     int device_;
@@ -728,6 +749,7 @@ int Decoder::decode(const uint8_t* data, size_t size, h264p_output_fn out, void*
     if (inflight_ >= 0) (void)h264r_picture_wait(ctx_, nullptr, nullptr, nullptr);  // left by a failed call
     inflight_ = -1;
     pending_.clear();
+    pslices_.clear();
     try {
         // Annex-B: start codes 0x000001 (B.2); a NAL ends at the next start code (its
         // trailing_zero_8bits dropped)
@@ -768,10 +790,12 @@ void Decoder::nal(const uint8_t* p, size_t n)
     case 2: case 3: case 4:
         fail(H264R_EUNSUPPORTED, "data partitioning (NAL types 2-4)");
     case 7:
+        run_slices();                                  // the pending slices refer to the current sets
         b.load(p + 1, n - 1);
         parse_sps(b, sps_);
         return;
     case 8:
+        run_slices();
         b.load(p + 1, n - 1);
         parse_pps(b, pps_, sps_);
         return;
@@ -914,8 +938,72 @@ void Decoder::slice(Bits& b, int nal_ref_idc, int nal_type)
         fail(H264R_EUNSUPPORTED, "scaling matrices differing between slices of one picture");
     quant_ = q;
     have_quant_ = true;
-    SliceCtx sc(*this, sps, pps, h, (int)slice_tab_.size() - 1, b);
-    sc.run();
+    auto ps = std::make_unique<PendingSlice>();
+    ps->h = h;
+    ps->b = std::move(b);
+    ps->nr = (int)slice_tab_.size() - 1;
+    ps->sps = &sps;
+    ps->pps = &pps;
+    memcpy(ps->list, list_, sizeof(list_));
+    memcpy(ps->list_n, list_n_, sizeof(list_n_));
+    pslices_.push_back(std::move(ps));
+}
+
+void Decoder::run_slices()
+{
+    const size_t n = pslices_.size();
+    if (!n) return;
+    const int W = psps_->W, H = psps_->H;
+    static const int env_threads = [] {
+        const char* e = getenv("H264P_THREADS");
+        return e ? std::max(1, atoi(e)) : 0;
+    }();
+    const int hw = std::max(1, (int)std::thread::hardware_concurrency());
+    // threads pay off on large pictures; H264P_THREADS forces them (the tests use it)
+    int threads = env_threads ? env_threads : (W * H >= 1200 ? std::min(8, hw) : 1);
+    threads = std::min<int>(threads, (int)n);
+    bool ordered = true;
+    for (size_t k = 1; k < n; ++k) ordered &= pslices_[k - 1]->h.first_mb < pslices_[k]->h.first_mb;
+    auto end_of = [&](size_t k) { return k + 1 < n ? pslices_[k + 1]->h.first_mb : W * H; };
+    auto run_one = [&](size_t k, int end) {
+        PendingSlice& p = *pslices_[k];
+        SliceCtx sc(*this, *p.sps, *p.pps, p.h, p.nr, p.b, p.list, p.list_n, end);
+        sc.run();
+    };
+    if (threads <= 1 || !ordered) {
+        for (size_t k = 0; k < n; ++k) run_one(k, W * H);
+        pslices_.clear();
+        return;
+    }
+    // every MB's slice before the slices run, so an availability check never reads a slice
+    // number another thread is writing (the neighbours of an MB precede it in raster order)
+    for (size_t k = 0; k < n; ++k)
+        for (int a = std::min(pslices_[k]->h.first_mb, W * H); a < std::min(end_of(k), W * H); ++a) mbs_[a].slice_nr = pslices_[k]->nr;
+    std::atomic<size_t> next{0};
+    std::vector<Error> errs(n);
+    std::vector<uint8_t> failed(n, 0);
+    auto worker = [&]() {
+        for (;;) {
+            const size_t k = next++;
+            if (k >= n) return;
+            try {
+                run_one(k, end_of(k));
+            } catch (const Error& e) {
+                errs[k] = e;
+                failed[k] = 1;
+            } catch (const std::bad_alloc&) {
+                errs[k] = Error{H264R_ENOMEM, "out of memory"};
+                failed[k] = 1;
+            }
+        }
+    };
+    std::vector<std::thread> pool;
+    for (int t = 1; t < threads; ++t) pool.emplace_back(worker);
+    worker();
+    for (auto& t : pool) t.join();
+    pslices_.clear();
+    for (size_t k = 0; k < n; ++k)
+        if (failed[k]) throw errs[k];                 // the first slice's error, as the sequential order
 }
 
 // POC (8.2.1.1 type 0, 8.2.1.3 type 2) and the per-picture state (slice_data.cc init_picture)
@@ -1129,6 +1217,7 @@ h264r_slice Decoder::slice_record(const SliceHeader& h)
 // decoder_h264r.cc:470-533), then marking (8.2.5) and output.
 void Decoder::finish_picture()
 {
+    run_slices();
     in_picture_ = false;
     const int W = psps_->W, H = psps_->H;
     if (!have_quant_) check(h264r_quant_init_flat(&quant_), "h264r_quant_init_flat");
@@ -1283,8 +1372,10 @@ void Decoder::flush_output()
 }
 
 // ------------------------------------------------------------------ macroblock layer
-SliceCtx::SliceCtx(Decoder& d, const Sps& s, const Pps& p, const SliceHeader& h, int nr, Bits& bits)
-    : D(d), sps(s), pps(p), sh(h), slice_nr(nr), b(bits), W(s.W), H(s.H), qp(h.qp)
+SliceCtx::SliceCtx(Decoder& d, const Sps& s, const Pps& p, const SliceHeader& h, int nr, Bits& bits,
+                   Picture* const (*lists)[33], const int* list_n, int end)
+    : D(d), sps(s), pps(p), sh(h), slice_nr(nr), b(bits), W(s.W), H(s.H), qp(h.qp), list_(lists), list_n_(list_n),
+      end_mb(end)
 {
 }
 
@@ -1308,14 +1399,15 @@ void SliceCtx::run()
             const int eos = cab->term();
             ++addr;
             if (eos) return;
+            require(addr < end_mb, "slice: runs into the next slice");
         }
     }
     for (;;) {
         macroblock();
         if (addr == W * H - 1) return;
         ++addr;
-        if (b.more_rbsp_data()) continue;
-        if (I || skip_run <= 0) return;
+        if (!b.more_rbsp_data() && (I || skip_run <= 0)) return;
+        require(addr < end_mb, "slice: runs into the next slice");
     }
 }
 
@@ -1690,7 +1782,7 @@ void SliceCtx::skip_p()
           (ref[1] == 0 && mv[1][0] == 0 && mv[1][1] == 0)))
         predict_mv(av, ref, mv, 0, 0, 0, 16, 16, p);
     Motion& M = *D.mot_;
-    const int pic = D.list_[0][0] ? D.list_[0][0]->id : -1;
+    const int pic = list_[0][0] ? list_[0][0]->id : -1;
     for (int y = 0; y < 4; ++y)
         for (int x = 0; x < 4; ++x) {
             const size_t i = M.at(mbx * 4 + x, mby * 4 + y);
@@ -1725,7 +1817,7 @@ void SliceCtx::direct_spatial()
     predict_mv(av0, r0, mv0, ref0, 0, 0, 16, 16, p0);
     predict_mv(av1, r1, mv1, ref1, 0, 0, 16, 16, p1);
     Motion& M = *D.mot_;
-    Picture* col = D.list_[1][0];
+    Picture* col = list_[1][0];
     require(col != nullptr, "direct prediction without RefPicList1[0]");
     const int step = sps.direct_8x8_inference ? 4 : 1;
     for (int blk = 0; blk < 16; blk += step) {
@@ -1742,8 +1834,8 @@ void SliceCtx::direct_spatial()
                        std::abs(C.mvy[1][e]) >> 1 == 0);
         }
         const size_t e = M.at(mbx * 4 + i, mby * 4 + j);
-        M.ref_pic[0][e] = ref0 == -1 ? -1 : (D.list_[0][ref0] ? D.list_[0][ref0]->id : -1);
-        M.ref_pic[1][e] = ref1 == -1 ? -1 : (D.list_[1][ref1] ? D.list_[1][ref1]->id : -1);
+        M.ref_pic[0][e] = ref0 == -1 ? -1 : (list_[0][ref0] ? list_[0][ref0]->id : -1);
+        M.ref_pic[1][e] = ref1 == -1 ? -1 : (list_[1][ref1] ? list_[1][ref1]->id : -1);
         M.ref_idx[0][e] = (int8_t)ref0;
         M.ref_idx[1][e] = (int8_t)ref1;
         const bool z0 = zero || ref0 < 0 || (ref0 == 0 && colzero), z1 = zero || ref1 < 0 || (ref1 == 0 && colzero);
@@ -1770,7 +1862,7 @@ void SliceCtx::direct_temporal()
     MbState& m = *cur;
     if (m.sub_type[0] && m.sub_type[1] && m.sub_type[2] && m.sub_type[3]) return;
     Motion& M = *D.mot_;
-    Picture* col = D.list_[1][0];
+    Picture* col = list_[1][0];
     require(col != nullptr, "direct prediction without RefPicList1[0]");
     const Motion& C = *col->mot;
     for (int blk = 0; blk < 16; ++blk) {
@@ -1791,13 +1883,13 @@ void SliceCtx::direct_temporal()
             // MapColToList0 (:242-285): the list-0 index of the picture the co-located block used
             const int cpic = C.ref_pic[rl][c];
             int mapped = -1;
-            const int nref = std::min(sh.nref[0], D.list_n_[0]);
+            const int nref = std::min(sh.nref[0], list_n_[0]);
             for (int k = 0; k < nref; ++k)
-                if (D.list_[0][k] && D.list_[0][k]->id == cpic) { mapped = k; break; }
+                if (list_[0][k] && list_[0][k]->id == cpic) { mapped = k; break; }
             require(mapped >= 0, "temporal direct: co-located block's reference is unavailable");
             // DistScaleFactor (:287-311)
-            const Picture* p0 = D.list_[0][mapped];
-            const Picture* p1 = D.list_[1][0];
+            const Picture* p0 = list_[0][mapped];
+            const Picture* p1 = list_[1][0];
             int scale = 9999;
             if (!p0->long_term) {
                 const int tb = clip3(-128, 127, D.cur_->poc - p0->poc), td = clip3(-128, 127, p1->poc - p0->poc);
@@ -1819,8 +1911,8 @@ void SliceCtx::direct_temporal()
             }
         }
         M.ref_idx[1][e] = 0;
-        M.ref_pic[0][e] = D.list_[0][M.ref_idx[0][e]] ? D.list_[0][M.ref_idx[0][e]]->id : -1;
-        M.ref_pic[1][e] = D.list_[1][0] ? D.list_[1][0]->id : -1;
+        M.ref_pic[0][e] = list_[0][M.ref_idx[0][e]] ? list_[0][M.ref_idx[0][e]]->id : -1;
+        M.ref_pic[1][e] = list_[1][0] ? list_[1][0]->id : -1;
     }
 }
 
@@ -1889,7 +1981,7 @@ void SliceCtx::inter_pred()
             const size_t e = M.at(mbx * 4 + x, mby * 4 + y);
             for (int l = 0; l < nlists; ++l) {
                 const int r = M.ref_idx[l][e];
-                M.ref_pic[l][e] = (r >= 0 && D.list_[l][r]) ? D.list_[l][r]->id : -1;
+                M.ref_pic[l][e] = (r >= 0 && list_[l][r]) ? list_[l][r]->id : -1;
             }
         }
 }

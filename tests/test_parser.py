@@ -86,6 +86,27 @@ def test_parser_synchronous_mode_matches(name, tmp_path):
     assert OUT.digest_by_frames(str(out), S.STREAMS[name]["frames"]) == GOLD[name]["frame_md5"]
 
 
+@pytest.mark.parametrize("name", [n for n in NAMES if "slices" in n])
+def test_parser_parallel_slices_hand_the_abi_the_same(name, tmp_path):
+    """The slices of a picture parsed on 4 threads (H264P_THREADS=4): the ABI traffic and the
+    frames are those of the sequential parse, i.e. the reference parser + shim's."""
+    cap = tmp_path / "cap.bin"
+    out = tmp_path / "out.yuv"
+    r = _run(_cpu_dec(), name, out, {"H264R_CAPTURE": str(cap), "H264P_THREADS": "4"})
+    assert r.returncode == 0, r.stderr[-800:]
+    assert OUT.digest_by_frames(str(out), S.STREAMS[name]["frames"]) == GOLD[name]["frame_md5"]
+    mine = S.read_capture_file(str(cap))
+    ref = S.load_capture(S.capture_path(name))
+    assert len(mine) == len(ref)
+    for i, (a, b) in enumerate(zip(mine, ref)):
+        for k in ("mbs", "levels", "mv", "ref_idx", "slices", "pic", "quant"):
+            if a[k].dtype.names:
+                for f in a[k].dtype.names:
+                    assert np.array_equal(a[k][f], b[k][f]), f"picture {i}: {k}.{f}"
+            else:
+                assert np.array_equal(a[k], b[k]), f"picture {i}: {k}"
+
+
 def test_parser_covers_both_entropy_coders():
     assert {bool(c.get("cabac")) for c in S.STREAMS.values()} == {False, True}
 
