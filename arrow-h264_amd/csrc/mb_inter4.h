@@ -69,10 +69,14 @@ DEV uint2 slice_hdr(const h264r_slice* slices, const Inter4Lds& S, int slice)
 // pic_motion_params::ref_pic interpret_mb.cc:611-623), slot -1 when the list is unused.
 DEV uint2 motion_word(uint32_t mv, int ri, const h264r_slice* slices, const Inter4Lds& S, int slice, int l)
 {
+    // the table read at a clamped index and the "no list" case selected afterwards: an LDS
+    // read under the lane's `has` compiled to a lane-divergent branch
     const bool has = ri >= 0 && ri < H264R_MAX_REFS;
-    int slot = has ? S.ref_slot[min(slice, INTER4_LDS_SLICES - 1)][l][ri] : -1;
-    if (has && slice >= INTER4_LDS_SLICES)
-        slot = (int8_t)slice_byte(slices, slice, (int)offsetof(h264r_slice, ref_slot) + l * H264R_MAX_REFS + ri);
+    const int ric = has ? ri : 0;
+    int slot = S.ref_slot[min(slice, INTER4_LDS_SLICES - 1)][l][ric];
+    if (slice >= INTER4_LDS_SLICES)
+        slot = (int8_t)slice_byte(slices, slice, (int)offsetof(h264r_slice, ref_slot) + l * H264R_MAX_REFS + ric);
+    slot = has ? slot : -1;
     return make_uint2(mv, (uint32_t)(uint8_t)ri | ((uint32_t)(uint8_t)slot << 8));
 }
 DEV uint2 block_motion(const h264r_batch& b, const h264r_slice* slices, const Inter4Lds& S, size_t at, int slice, int l)
@@ -268,13 +272,19 @@ DEV void luma_block_pred(const uint32_t (&w)[9][3], int W, int x, int xf, int yf
             }
         }
     }
-    // output = (X + Y + 1) >> 1, X, Y in {0 G, 1 b, 2 h, 3 j}
-    int xs, ys;
-    if (xf == 0) { xs = yf == 2 ? 2 : 0; ys = yf == 0 ? 0 : 2; }
-    else if (yf == 0) { xs = xf == 2 ? 1 : 0; ys = 1; }
-    else if (xf == 2) { xs = yf == 2 ? 3 : 1; ys = 3; }
-    else if (yf == 2) { xs = 2; ys = 3; }
-    else { xs = 1; ys = 2; }
+    // output = (X + Y + 1) >> 1, X, Y in {0 G, 1 b, 2 h, 3 j}: (xs, ys) of the 16 phases as a
+    // 64-bit table (an if-chain on the lane's phase compiled to lane-divergent branches)
+    // XSYS nibble 4 xf + yf = xs | ys << 2:  xf 0: (0,0) (0,2) (2,2) (0,2); yf 0: (0,1) (1,1)
+    // (0,1); xf 2: (1,3) (3,3) (1,3); yf 2: (2,3); else (1,2)
+    constexpr uint64_t XSYS = 0x9e94dfd59e948a80ull;
+    const int xsys = (int)(XSYS >> (4 * (xf * 4 + yf))) & 15, xs = xsys & 3, ys = xsys >> 2;
+    // one of four by masks (a ternary chain became a branch tree)
+    const uint32_t mx1 = 0u - (uint32_t)(xs & 1), mx2 = 0u - (uint32_t)(xs >> 1);
+    const uint32_t my1 = 0u - (uint32_t)(ys & 1), my2 = 0u - (uint32_t)(ys >> 1);
+    auto pick = [](uint32_t m1, uint32_t m2, uint32_t a, uint32_t b, uint32_t c, uint32_t d) -> uint32_t {
+        const uint32_t lo = a ^ ((a ^ b) & m1), hi = c ^ ((c ^ d) & m1);
+        return lo ^ ((lo ^ hi) & m2);
+    };
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         uint32_t o2[2];
@@ -284,9 +294,10 @@ DEV void luma_block_pred(const uint32_t (&w)[9][3], int W, int x, int xf, int yf
             const s16x2 hh = pk_clip255((hacc[i][h2] + splat16(16)) >> splat16(5));
             const s16x2 bb = pk_clip255((bsv[i][h2] + splat16(16)) >> splat16(5));
             const int j0 = clip255((jacc[i][2 * h2] + 512) >> 10), j1 = clip255((jacc[i][2 * h2 + 1] + 512) >> 10);
-            const s16x2 jj = (s16x2){(short)j0, (short)j1};
-            const s16x2 X = xs == 0 ? G : (xs == 1 ? bb : (xs == 2 ? hh : jj));
-            const s16x2 Y = ys == 0 ? G : (ys == 1 ? bb : (ys == 2 ? hh : jj));
+            // all four computed, then picked per lane (the phase differs between lanes)
+            const uint32_t g32 = as_u32(G), b32 = as_u32(bb), h32 = as_u32(hh), j32 = (uint32_t)j0 | ((uint32_t)j1 << 16);
+            const s16x2 X = as_s16x2(pick(mx1, mx2, g32, b32, h32, j32));
+            const s16x2 Y = as_s16x2(pick(my1, my2, g32, b32, h32, j32));
             o2[h2] = as_u32((X + Y + splat16(1)) >> splat16(1));
         }
         out[i] = __builtin_amdgcn_perm(o2[1], o2[0], 0x06040200u);
@@ -370,20 +381,14 @@ DEV WpPar wp_params(const WpRaw& w, int wp_mode, int dir, int pl)
 {
     const int lwd = w.lwd[pl ? 1 : 0];
     const int wa = w.wa[pl], wb = w.wb[pl], oa = w.oa[pl], ob = w.ob[pl], iw = w.iw;
+    // selects, not branches (dir and the slice's mode differ between a wave's lanes): one
+    // list (explicit weights or plain), both lists averaged, explicit or implicit
     WpPar p;
-    if (dir != 2) {
-        const bool ex = wp_mode == 1;
-        p.w0 = dir == 0 ? (ex ? wa : 1) : 0;
-        p.w1 = dir == 1 ? (ex ? wb : 1) : 0;
-        p.o = ex ? (dir == 0 ? oa : ob) : 0;
-        p.d = ex ? lwd : 0;
-    } else if (wp_mode == 0) {
-        p.w0 = p.w1 = 1; p.o = 0; p.d = 1;
-    } else if (wp_mode == 1) {
-        p.w0 = wa; p.w1 = wb; p.o = (oa + ob + 1) >> 1; p.d = lwd + 1;
-    } else {
-        p.w1 = iw; p.w0 = 64 - iw; p.o = 0; p.d = lwd + 1;
-    }
+    const bool ex = wp_mode == 1, im = wp_mode == 2, bi = dir == 2;
+    p.w0 = bi ? (ex ? wa : (im ? 64 - iw : 1)) : (dir == 0 ? (ex ? wa : 1) : 0);
+    p.w1 = bi ? (ex ? wb : (im ? iw : 1)) : (dir == 1 ? (ex ? wb : 1) : 0);
+    p.o = bi ? (ex ? (oa + ob + 1) >> 1 : 0) : (ex ? (dir == 0 ? oa : ob) : 0);
+    p.d = bi ? (wp_mode == 0 ? 1 : lwd + 1) : (ex ? lwd : 0);
     p.rnd = p.d > 0 ? 1 << (p.d - 1) : 0;
     return p;
 }
@@ -402,10 +407,9 @@ DEV uint32_t wp_apply4(const WpPar& p, uint32_t v0, uint32_t v1)
 DEV uint32_t wp_combine4(const WpPar& p, int wp_mode, int dir, uint32_t v0, uint32_t v1)
 {
     if (wp_mode == 0) {
-        if (dir == 0) return v0;
-        if (dir == 1) return v1;
-        // (a + b + 1) >> 1 per byte
-        return (v0 | v1) - (((v0 ^ v1) >> 1) & 0x7F7F7F7Fu);
+        // one list or (a + b + 1) >> 1 per byte, selected (dir differs between a wave's lanes)
+        const uint32_t avg = (v0 | v1) - (((v0 ^ v1) >> 1) & 0x7F7F7F7Fu);
+        return dir == 0 ? v0 : (dir == 1 ? v1 : avg);
     }
     return wp_apply4(p, v0, v1);
 }
@@ -927,6 +931,10 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
         if (__any(cbpl != 0)) {
 #endif
             const int per = qpl / 6;
+            // dq4 / dq8 (transform.cc:394-419) as one form, rounding and shift per lane: the
+            // lanes of a wave mix 4x4 and 8x8 MBs, and a select per value (not a branch) keeps
+            // the 16 values free of exec-mask work
+            const int drnd = t8 ? 32 : 8, dsh = t8 ? 6 : 4;
             int d[4][4];
     #pragma unroll
             for (int i = 0; i < 4; ++i)
@@ -936,7 +944,8 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
                     const uint32_t lo_ = (i & 1) ? lw.z : lw.x, hi_ = (i & 1) ? lw.w : lw.y;
                     const uint32_t slo = (i & 1) ? sw.z : sw.x, shi = (i & 1) ? sw.w : sw.y;
                     const int lvv = sel16(lo_, hi_, c), scv = sel16(slo, shi, c);
-                    d[i][c] = byp ? lvv : (t8 ? dq8(lvv, scv, per) : dq4(lvv, scv, per));
+                    const int dqv = ((lvv * scv) * (1 << per) + drnd) >> dsh;
+                    d[i][c] = byp ? lvv : dqv;
                 }
             // lossless MBs (TransformBypassModeFlag): the levels are the residual, DPCM'd in
             // place down the columns / along the rows when the block's Intra4x4PredMode /
@@ -1063,7 +1072,9 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
                 const int c00 = (int16_t)(cdc[pl].x & 0xFFFF), c01 = (int16_t)(cdc[pl].x >> 16);
                 const int c10 = (int16_t)(cdc[pl].y & 0xFFFF), c11 = (int16_t)(cdc[pl].y >> 16);
                 const int e00 = c00 + c01, e01 = c00 - c01, e10 = c10 + c11, e11 = c10 - c11;
-                const int f = cb == 0 ? e00 + e10 : cb == 1 ? e01 + e11 : cb == 2 ? e00 - e10 : e01 - e11;
+                // f = (e00 or e01) +/- (e10 or e11) by cb's bits: arithmetic, not a branch tree
+                const int ea = (cb & 1) ? e01 : e00, eb = (cb & 1) ? e11 : e10;
+                const int f = ea + (eb ^ -(cb >> 1)) + (cb >> 1);
                 if (cr == 0 && cc == 0) k[0][0] = cbpc ? ((f * cdcs[pl]) * (1 << per)) >> 5 : 0;
                 // rows: my 2 columns + the 2 of lane ^ 1
                 int t[2][2];

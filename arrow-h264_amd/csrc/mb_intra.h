@@ -105,9 +105,13 @@ DEV int intra_tap_entry(const uint32_t (&t)[3], int mode)
     return (w >> (8 * (mode & 3))) & 255;
 }
 
+// kind 0 / 1 / 2 of intra_nxn_tap: all three forms, one kept by masks (a ternary chain on the
+// lane's kind compiled to a tree of lane-divergent branches)
 DEV int tap_apply(int kind, int a, int b, int c)
 {
-    return kind == 2 ? (a + 2 * b + c + 2) >> 2 : (kind == 1 ? (b + c + 1) >> 1 : b);
+    const int t1 = (b + c + 1) >> 1, t2 = (a + 2 * b + c + 2) >> 2;
+    const int m1 = -(kind & 1), m2 = -(kind >> 1);
+    return ((b ^ ((b ^ t1) & m1)) & ~m2) | (t2 & m2);
 }
 
 DEV uint32_t lds_u32(const uint8_t* p) { return *reinterpret_cast<const uint32_t*>(p); }
@@ -616,8 +620,11 @@ DEV void intra_mb_compute(const h264r_batch& b, const Geom& g, int pic, int mbx,
             const int e2 = S.tile[pb + eoff(min(i + 1, 14))];
             const int st = sum4(lds_u32(&S.tile[pb - ITP]));       // DC (intra_prediction.cc:214-229)
             const int sl = S.tile[pb - 1] + S.tile[pb + ITP - 1] + S.tile[pb + 2 * ITP - 1] + S.tile[pb + 3 * ITP - 1];
-            const int dc = aA && aB ? (st + sl + 4) >> 3 : aB ? (st + 2) >> 2 : aA ? (sl + 2) >> 2 : 128;
-            const int p = mode == 2 ? dc : tap_apply(kind, e0, e1, e2);
+            // DC by masks: the available sums, shifted by 2 or 3, 128 when neither side is
+            const int mA = -aA, mB = -aB, dsh = 1 + aA + aB;
+            const int dc = (((sl & mA) + (st & mB) + (1 << (dsh - 1))) >> dsh) + (128 & ~(mA | mB));
+            const int tp = tap_apply(kind, e0, e1, e2), m2 = -(int)(mode == 2);
+            const int p = tp ^ ((tp ^ dc) & m2);
             // residual (0 in uncoded blocks) at tile position pb + y * ITP + x
             const int v = clip255(p + S.res[(pb >> 5) - 1 + y][(pb & 31) - 4 + x]);
             if (on) S.tile[pb + y * ITP + x] = (uint8_t)v;

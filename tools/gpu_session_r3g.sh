@@ -1,10 +1,10 @@
 #!/bin/bash
-# tools/gpu_session_r3g.sh -- final measurement at HEAD: every GPU test, smoke(), the default
+# tools/gpu_session_r3g.sh [outdir name] -- final measurement at HEAD: every GPU test, smoke(), the default
 # bench line (config 3), rocprofv3 kernel stats, configs 2/4/5, PMC passes at batch 1024, a
 # per-phase trace of k_deblock2 (trace build, arrow-h264_amd/lib_trace), the standalone decoder's
 # wall time per frame on the 1080p CABAC stream with and without the overlapped picture end.
 set -o pipefail
-O=gpurun_out/r3g; mkdir -p $O
+O=gpurun_out/${1:-r3g}; mkdir -p $O
 timeout -k 10 420 python -u -m pytest tests -m gpu -x -v --timeout 180 --timeout-method thread > $O/gputest.log 2>&1 &&
 timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 &&
 timeout -k 10 300 python -u bench.py > $O/bench.json 2> $O/bench.err &&
