@@ -166,10 +166,12 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2
     // write-through segment instead of four partial ones): block 0 = the early pairs
     // (0,0) (0,1) (0,2) (1,0), block 1 = the early (2,0) (2,1) (2,2) (1,1), block 2 = the
     // late (1,2) (3,0) (3,1) (3,2).
+    // blk * 4 + slot of pair k of lane c, nibble 3c + k of PAIR_POS (a select chain on the lane's
+    // c compiled to a branch tree at every use)
+    constexpr uint64_t PAIR_POS = 0xba9654873210ull;
     auto pair_off = [&](uint32_t base, int m, int c, int k) -> uint32_t {
-        const int blk = c == 0 ? 0 : c == 2 ? 1 : c == 3 ? 2 : (k < 2 ? k : 2);
-        const int slot = c == 0 || c == 2 ? k : c == 3 ? k + 1 : (k < 2 ? 3 : 0);
-        return base + (uint32_t)(m * RECG) * 8u + (uint32_t)(blk * 4 + slot) * 16u;
+        const uint32_t bs = (uint32_t)(PAIR_POS >> (4 * (c * 3 + k))) & 15u;
+        return base + (uint32_t)(m * RECG) * 8u + bs * 16u;
     };
     auto load_pair = [&](int m, int k) -> v4u {
         return __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(hrs, pair_off(rec_in, m, q, k), 0, AUX_SC1));

@@ -113,34 +113,41 @@ DEV void filter_edge_line(int& p3, int& p2, int& p1, int& p0, int& q0, int& q1, 
                           uint32_t par, bool chroma)
 {
     const int alpha = par & 255, beta = (par >> 8) & 255;
-    const int tc0 = (bS >= 1 && bS <= 3) ? (int)((par >> (11 + 5 * bS)) & 31) : 0;
-    const bool filt = bS != 0 && iabs(p0 - q0) < alpha && iabs(p1 - p0) < beta && iabs(q1 - q0) < beta;
+    // every candidate computed, then selected: the compiler otherwise sinks each into a
+    // lane-divergent branch of its own (bS and the decisions differ between a wave's lines)
+    int tc0r = (int)((par >> (11 + 5 * min(max(bS, 1), 3))) & 31);
+    asm volatile("" : "+v"(tc0r));
+    const int tc0 = (bS >= 1 && bS <= 3) ? tc0r : 0;
+    // all four tests evaluated (a short-circuit && on lane-varying operands becomes branches)
+    const bool filt = ((int)(bS != 0) & (int)(iabs(p0 - q0) < alpha) & (int)(iabs(p1 - p0) < beta) &
+                       (int)(iabs(q1 - q0) < beta)) != 0;
     const bool apb = iabs(p2 - p0) < beta, aqb = iabs(q2 - q0) < beta;
     // bS < 4 (filter_normal)
-    const int tc = chroma ? tc0 + 1 : tc0 + (int)apb + (int)aqb;
+    const int tc = tc0 + (chroma ? 1 : (int)apb + (int)aqb);
     const int delta = clip3(-tc, tc, ((q0 - p0) * 4 + (p1 - q1) + 4) >> 3);
     const int avg = (p0 + q0 + 1) >> 1;
     const int n_p0 = clip255(p0 + delta), n_q0 = clip255(q0 - delta);
-    const int n_p1 = (!chroma && apb) ? p1 + clip3(-tc0, tc0, (p2 + avg - p1 * 2) >> 1) : p1;
-    const int n_q1 = (!chroma && aqb) ? q1 + clip3(-tc0, tc0, (q2 + avg - q1 * 2) >> 1) : q1;
+    int t_p1 = p1 + clip3(-tc0, tc0, (p2 + avg - p1 * 2) >> 1), t_q1 = q1 + clip3(-tc0, tc0, (q2 + avg - q1 * 2) >> 1);
+    asm volatile("" : "+v"(t_p1), "+v"(t_q1));
+    const int n_p1 = (!chroma && apb) ? t_p1 : p1;
+    const int n_q1 = (!chroma && aqb) ? t_q1 : q1;
     if (!STRONG) {            // no lane of the wave has bS 4 on this edge
-        if (filt) { p1 = n_p1; p0 = n_p0; q0 = n_q0; q1 = n_q1; }
+        p1 = filt ? n_p1 : p1; p0 = filt ? n_p0 : p0; q0 = filt ? n_q0 : q0; q1 = filt ? n_q1 : q1;
         return;
     }
     // bS == 4 (filter_strong)
     const bool strong = iabs(p0 - q0) < ((alpha >> 2) + 2);
     const bool sp = !chroma && apb && strong, sq = !chroma && aqb && strong;
-    const int s_p0 = sp ? (p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3 : (2 * p1 + p0 + q1 + 2) >> 2;
-    const int s_p1 = sp ? (p2 + p1 + p0 + q0 + 2) >> 2 : p1;
-    const int s_p2 = sp ? (2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3 : p2;
-    const int s_q0 = sq ? (p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3 : (2 * q1 + q0 + p1 + 2) >> 2;
-    const int s_q1 = sq ? (p0 + q0 + q1 + q2 + 2) >> 2 : q1;
-    const int s_q2 = sq ? (2 * q3 + 3 * q2 + q1 + q0 + p0 + 4) >> 3 : q2;
-    const bool is4 = bS == 4;
-    if (filt) {
-        p2 = is4 ? s_p2 : p2; p1 = is4 ? s_p1 : n_p1; p0 = is4 ? s_p0 : n_p0;
-        q0 = is4 ? s_q0 : n_q0; q1 = is4 ? s_q1 : n_q1; q2 = is4 ? s_q2 : q2;
-    }
+    int a_p0 = (p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3, b_p0 = (2 * p1 + p0 + q1 + 2) >> 2;
+    int a_p1 = (p2 + p1 + p0 + q0 + 2) >> 2, a_p2 = (2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3;
+    int a_q0 = (p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3, b_q0 = (2 * q1 + q0 + p1 + 2) >> 2;
+    int a_q1 = (p0 + q0 + q1 + q2 + 2) >> 2, a_q2 = (2 * q3 + 3 * q2 + q1 + q0 + p0 + 4) >> 3;
+    asm volatile("" : "+v"(a_p0), "+v"(b_p0), "+v"(a_p1), "+v"(a_p2), "+v"(a_q0), "+v"(b_q0), "+v"(a_q1), "+v"(a_q2));
+    const int s_p0 = sp ? a_p0 : b_p0, s_p1 = sp ? a_p1 : p1, s_p2 = sp ? a_p2 : p2;
+    const int s_q0 = sq ? a_q0 : b_q0, s_q1 = sq ? a_q1 : q1, s_q2 = sq ? a_q2 : q2;
+    const bool is4 = bS == 4, f4 = filt && is4, fn = filt && !is4;
+    p2 = f4 ? s_p2 : p2; p1 = f4 ? s_p1 : (fn ? n_p1 : p1); p0 = f4 ? s_p0 : (fn ? n_p0 : p0);
+    q0 = f4 ? s_q0 : (fn ? n_q0 : q0); q1 = f4 ? s_q1 : (fn ? n_q1 : q1); q2 = f4 ? s_q2 : q2;
 }
 
 // The two filter passes of one MB on the LDS tiles: vertical edges with one lane per
