@@ -306,20 +306,24 @@ DEV void luma_block_pred(const uint32_t (&w)[9][3], int W, int x, int xf, int yf
 
 // 2x2 chroma prediction samples at chroma integer position (xi, yi), eighth phase
 // (xf, yf): get_block_chroma inter_prediction.cc:380-404 with clamped coordinates.
-// Returns the four samples as bytes (row 0 in bits 0..15, row 1 in 16..31).
-DEV uint32_t chroma_block_pred(const uint8_t* __restrict__ img, int W, int H, int xi, int yi, int xf, int yf)
+// Both planes; each plane's four samples as bytes (row 0 in bits 0..15, row 1 in 16..31).
+DEV void chroma_block_pred2(const uint8_t* __restrict__ cb, const uint8_t* __restrict__ cr, int W, int H, int xi, int yi,
+                            int xf, int yf, uint32_t (&out)[2])
 {
     const int a = clip3(0, W - 1, xi) & ~3;
-    // the three rows' dwords first, then byte selection without branches: a lane-divergent
-    // interior / edge split made every row's load wait for the previous row's use (the
-    // compiler joined the paths with a full vmcnt wait before issuing the next load)
-    uint32_t w[3][2];
+    // both planes' three rows first (12 dwords in flight), then byte selection without
+    // branches: a lane-divergent interior / edge split made every row's load wait for the
+    // previous row's use, and one plane at a time left the second plane's last row behind a
+    // full vmcnt wait
+    uint32_t w[2][3][2];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        const gdword* q = as_global(img + (size_t)clip3(0, H - 1, yi + k) * W + a);
-        w[k][0] = q[0];
-        w[k][1] = q[1];
-    }
+    for (int pl = 0; pl < 2; ++pl)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const gdword* q = as_global((pl ? cr : cb) + (size_t)clip3(0, H - 1, yi + k) * W + a);
+            w[pl][k][0] = q[0];
+            w[pl][k][1] = q[1];
+        }
     int sh[3];
     bool hi[3];
 #pragma unroll
@@ -328,20 +332,23 @@ DEV uint32_t chroma_block_pred(const uint8_t* __restrict__ img, int W, int H, in
         hi[c] = idx >= 4;
         sh[c] = 8 * (idx & 3);
     }
-    int p[3][3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k)
-#pragma unroll
-        for (int c = 0; c < 3; ++c) p[k][c] = ((hi[c] ? w[k][1] : w[k][0]) >> sh[c]) & 255;
     const int wa = (8 - xf) * (8 - yf), wb = xf * (8 - yf), wc = (8 - xf) * yf, wd = xf * yf;
-    uint32_t o = 0;
 #pragma unroll
-    for (int r = 0; r < 2; ++r)
+    for (int pl = 0; pl < 2; ++pl) {
+        int p[3][3];
 #pragma unroll
-        for (int c = 0; c < 2; ++c)
-            o |= (uint32_t)((wa * p[r][c] + wb * p[r][c + 1] + wc * p[r + 1][c] + wd * p[r + 1][c + 1] + 32) >> 6)
-                 << (16 * r + 8 * c);
-    return o;
+        for (int k = 0; k < 3; ++k)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) p[k][c] = ((hi[c] ? w[pl][k][1] : w[pl][k][0]) >> sh[c]) & 255;
+        uint32_t o = 0;
+#pragma unroll
+        for (int r = 0; r < 2; ++r)
+#pragma unroll
+            for (int c = 0; c < 2; ++c)
+                o |= (uint32_t)((wa * p[r][c] + wb * p[r][c + 1] + wc * p[r + 1][c] + wd * p[r + 1][c + 1] + 32) >> 6)
+                     << (16 * r + 8 * c);
+        out[pl] = o;
+    }
 }
 
 // mc_prediction / bi_prediction combine (inter_prediction.cc:53-156) of one lane and
@@ -732,11 +739,7 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
             }
 #endif
 #ifndef H264R_EXP_NO_CHROMA
-            if (ok) {
-    #pragma unroll
-                for (int pl = 0; pl < 2; ++pl)
-                    tC[pl] = chroma_block_pred(S.planes[slot * 3 + 1 + pl], g.Wc, g.Hc, vx >> 3, vy >> 3, vx & 7, vy & 7);
-            }
+            if (ok) chroma_block_pred2(S.planes[slot * 3 + 1], S.planes[slot * 3 + 2], g.Wc, g.Hc, vx >> 3, vy >> 3, vx & 7, vy & 7, tC);
 #endif
             const bool l1 = l != 0;
     #pragma unroll
