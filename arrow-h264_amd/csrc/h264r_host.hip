@@ -29,8 +29,9 @@
 
 namespace h264r { struct DbInfo; }
 extern "C" __global__ void k_inter4(h264r_batch b, h264r::DbInfo* dbinfo, int2 rows, int* sp_flag, uint8_t* recon);
-extern "C" __global__ void k_inter4r(h264r_batch b, h264r::DbInfo* dbinfo, int2 rows, int* sp_flag, uint8_t* recon);
-extern "C" __global__ void k_dbinfo(h264r_batch b, h264r::DbInfo* dbinfo, int2 rows);
+extern "C" __global__ void k_inter4r(h264r_batch b, h264r::DbInfo* dbinfo, int2 rows, int* sp_flag, uint8_t* recon,
+                                     const int* inter_cnt);
+extern "C" __global__ void k_dbinfo(h264r_batch b, h264r::DbInfo* dbinfo, int2 rows, int* inter_cnt);
 extern "C" __global__ void k_inter_sp(h264r_batch b, int2 rows, const int* sp_flag, uint8_t* recon);
 extern "C" __global__ void k_untile(h264r_batch b, int2 rows, const uint8_t* recon);
 extern "C" __global__ void k_intra_pic(h264r_batch b, int* sync, int* err, const uint16_t* lvl, int lmax, int2 rows,
@@ -441,7 +442,9 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
     // scratch: per-MB deblocking records, tagged hand-off
     // records, and a sync region [intra ticket + per-(picture,row) progress][deblock
     // ticket][level barrier, deepest level][SP inter MBs seen]
-    const size_t sync_n = 1 + (size_t)P * H + 5 + 9;   // + the deblocking kernels' per-XCD ticket counters, done count
+    // + the deblocking kernels' per-XCD ticket counters, done count, then per picture the waves
+    // of k_dbinfo that met an inter or I_PCM MB (k_inter4r skips the pictures without one)
+    const size_t sync_n = 1 + (size_t)P * H + 5 + 9 + P;
     // the scratch is shared by every launch of this context: a launch on another stream
     // than the previous one waits for it first
     int st;
@@ -515,7 +518,7 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
         }
         HIP_OK(hipEventRecord(X.ev_side_start, s));                 // the previous launch's deblocking read dbinfo
         HIP_OK(hipStreamWaitEvent(X.side, X.ev_side_start, 0));
-        hipLaunchKernelGGL(k_dbinfo, dgrid, dim3(256), 0, X.side, b, dbinfo, rows);
+        hipLaunchKernelGGL(k_dbinfo, dgrid, dim3(256), 0, X.side, b, dbinfo, rows, (int*)nullptr);
         HIP_OK(hipGetLastError());
         HIP_OK(hipEventRecord(X.ev_side_done, X.side));
     }
@@ -523,12 +526,14 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
     {
         Timed t(c, 0, s);
         int* sp_flag = sync + 1 + (size_t)P * H + 4;
+        // per-picture inter counts: only when k_dbinfo runs before k_inter4r on this stream
+        int* inter_cnt = db_mode == 1 ? sync + 1 + (size_t)P * H + 14 : nullptr;
         if (db_mode == 1) {
-            hipLaunchKernelGGL(k_dbinfo, dgrid, dim3(256), 0, s, b, dbinfo, rows);
+            hipLaunchKernelGGL(k_dbinfo, dgrid, dim3(256), 0, s, b, dbinfo, rows, inter_cnt);
             HIP_OK(hipGetLastError());
         }
         if (db_mode == 0) hipLaunchKernelGGL(k_inter4, igrid, dim3(256), 0, s, b, dbinfo, rows, sp_flag, recon);
-        else hipLaunchKernelGGL(k_inter4r, igrid, dim3(256), 0, s, b, dbinfo, rows, sp_flag, recon);
+        else hipLaunchKernelGGL(k_inter4r, igrid, dim3(256), 0, s, b, dbinfo, rows, sp_flag, recon, (const int*)inter_cnt);
         HIP_OK(hipGetLastError());
         // inter MBs of SP slices (a short launch when the batch has none)
         hipLaunchKernelGGL(k_inter_sp, dim3(1024), dim3(256), 0, s, b, rows, (const int*)sp_flag, recon);

@@ -85,7 +85,8 @@ DEV bool inter4_groups(const Geom& g, int2 rows, int per, int& grp, int& gend)
 // 4 MB L2 holds, instead of every XCD streaming whole references through its L2.
 // DB: the deblocking records too (k_inter4), or not (k_inter4r, with k_dbinfo beside it).
 template <bool DB>
-DEV void inter4_kernel(const h264r_batch& b, DbInfo* dbinfo, int2 rows, int* sp_flag, uint8_t* recon, Inter4Lds& S)
+DEV void inter4_kernel(const h264r_batch& b, DbInfo* dbinfo, int2 rows, int* sp_flag, uint8_t* recon, Inter4Lds& S,
+                       const int* inter_cnt)
 {
     const int pic = blockIdx.y;
     const Geom g = make_geom(b.width_mbs, b.height_mbs);
@@ -95,7 +96,11 @@ DEV void inter4_kernel(const h264r_batch& b, DbInfo* dbinfo, int2 rows, int* sp_
     const int aend = rows.y * g.wmb;
     int a0 = rows.x * g.wmb + (grp * 4 + wave) * 4;
     Inter4Pre pre = inter4_pre(b, g, pic, a0, aend, lane);
+    // a picture k_dbinfo found no inter or I_PCM MB in (all-intra) has nothing for this kernel;
+    // the flag is loaded with the records, so it adds no round trip
+    const int has_inter = inter_cnt ? inter_cnt[pic] : 1;
     const LdsRegs lr = inter4_lds_load(b, pic);
+    if (__builtin_amdgcn_readfirstlane(has_inter) == 0) return;
     inter4_lds_store(b, lr, S);
     __syncthreads();
     for (;;) {
@@ -116,19 +121,20 @@ extern "C" __global__ __launch_bounds__(256, H264R_INTER4_WAVES) void k_inter4(h
                                                                              int* sp_flag, uint8_t* recon)
 {
     __shared__ Inter4Lds S;
-    inter4_kernel<true>(b, dbinfo, rows, sp_flag, recon, S);
+    inter4_kernel<true>(b, dbinfo, rows, sp_flag, recon, S, nullptr);
 }
 extern "C" __global__ __launch_bounds__(256, H264R_INTER_WAVES) void k_inter4r(h264r_batch b, DbInfo* dbinfo, int2 rows,
-                                                                              int* sp_flag, uint8_t* recon)
+                                                                              int* sp_flag, uint8_t* recon,
+                                                                              const int* inter_cnt)
 {
     __shared__ Inter4Lds S;
-    inter4_kernel<false>(b, dbinfo, rows, sp_flag, recon, S);
+    inter4_kernel<false>(b, dbinfo, rows, sp_flag, recon, S, inter_cnt);
 }
 
 // k_dbinfo: the deblocking records DbInfo of every MB (dbinfo_block, mb_inter4.h) on their
 // own -- they depend on the MB records and motion only, not on any sample, so the host
 // launches this beside k_inter4r on a second stream.  Same grid and lane roles as k_inter4.
-extern "C" __global__ __launch_bounds__(256) void k_dbinfo(h264r_batch b, DbInfo* dbinfo, int2 rows)
+extern "C" __global__ __launch_bounds__(256) void k_dbinfo(h264r_batch b, DbInfo* dbinfo, int2 rows, int* inter_cnt)
 {
     __shared__ Inter4Lds S;
     const int pic = blockIdx.y;
@@ -145,20 +151,23 @@ extern "C" __global__ __launch_bounds__(256) void k_dbinfo(h264r_batch b, DbInfo
     DbNb nb = dbinfo_pre(b, g, pic, a0, aend, lane);
     inter4_lds(b, pic, S);
     __syncthreads();
+    bool inter = false;                      // an inter or I_PCM MB met (k_inter4r has work)
     for (;;) {
-        if (a0 >= aend) return;
+        if (a0 >= aend) break;
         const int a = a0 + (lane >> 4);
         const bool valid = a < aend;
         const int aa = valid ? a : aend - 1;
+        inter |= __any(valid && (!mb_is_intra(pre.q) || pre.q.mb_type == H264R_I_PCM)) != 0;
         const uint2 m0 = motion_word(pre.mv[0], pre.ri[0], slices, S, pre.q.slice, 0);
         const uint2 m1 = motion_word(pre.mv[1], pre.ri[1], slices, S, pre.q.slice, 1);
         dbinfo_block(b, g, pic, aa, valid, lane & 15, S, pre.q, m0, m1, slice_hdr(slices, S, pre.q.slice), nb,
                      dbinfo + (size_t)pic * g.nmb);
-        if (++grp >= gend) return;
+        if (++grp >= gend) break;
         a0 = rows.x * g.wmb + (grp * 4 + wave) * 4;
         pre = inter4_pre(b, g, pic, a0, aend, lane);
         nb = dbinfo_pre(b, g, pic, a0, aend, lane);
     }
+    if (inter_cnt && inter && lane == 0) inter_cnt[pic] = 1;         // every writer stores 1
 }
 
 // k_inter_sp: the inter MBs of SP slices (inverse_transform_sp), after k_inter4.  A
