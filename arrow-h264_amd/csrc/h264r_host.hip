@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cerrno>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -28,7 +29,6 @@
 #endif
 
 namespace h264r { struct DbInfo; }
-extern "C" __global__ void k_inter4(h264r_batch b, h264r::DbInfo* dbinfo, int2 rows, int* sp_flag, uint8_t* recon);
 extern "C" __global__ void k_inter4r(h264r_batch b, h264r::DbInfo* dbinfo, int2 rows, int* sp_flag, uint8_t* recon,
                                      const int* inter_cnt);
 extern "C" __global__ void k_dbinfo(h264r_batch b, h264r::DbInfo* dbinfo, int2 rows, int* inter_cnt);
@@ -48,13 +48,10 @@ extern "C" __global__ void k_deblock(h264r_batch b, const h264r::DbInfo* dbinfo,
                                      int* sync, int* err, uint32_t epoch, int2 rows, int nx, uint8_t* recon);
 extern "C" __global__ void k_deblock2(h264r_batch b, const h264r::DbInfo* dbinfo, uint64_t* hb,
                                       int* sync, int* err, uint32_t epoch, int2 rows, int nx, const uint8_t* recon);
-extern "C" __global__ void k_deblock3(h264r_batch b, const h264r::DbInfo* dbinfo, uint64_t* hb,
-                                      int* sync, int* err, uint32_t epoch, int2 rows, int nx, const uint8_t* recon);
 constexpr size_t DBINFO_BYTES = 80;
 constexpr size_t HANDOFF_BYTES = 256;   // one tagged record (32 x {dword, epoch}) per MB
 constexpr size_t HANDOFF2_BYTES = 384;  // k_deblock2: 2 row slots x 24 x {dword, tag} per MB column
 constexpr int DEBLOCK2_UNITS = 16;      // k_deblock2: pictures per wave (mb_deblock.h)
-constexpr int DEBLOCK3_UNITS = 8;       // k_deblock3: pictures per wave (k_deblock3.hip)
 
 namespace {
 
@@ -103,8 +100,7 @@ int dev_resize(T** p, size_t* cap, size_t n)
 
 }  // namespace
 
-// Per-batch scratch of one launch sequence (a context has one per pipeline stage,
-// h264r_decode_batch's sub-batches).
+// Per-batch scratch of one launch sequence.
 struct Scratch {
     uint8_t* d_dbinfo = nullptr; size_t c_dbinfo = 0;
     int* d_sync = nullptr; size_t c_sync = 0;
@@ -116,19 +112,12 @@ struct Scratch {
     uint32_t* d_list = nullptr; size_t c_list = 0; // intra MBs by level (pic * nmb + addr)
     int* d_lcnt = nullptr; size_t c_lcnt = 0;      // [count | base | cursor] x (LEVEL_LISTS + 2)
     uint8_t* d_recon = nullptr; size_t c_recon = 0; // MB-tiled reconstruction, 384 B per (picture, MB)
-    // k_dbinfo beside the reconstruction (H264R_DBINFO=2): its stream and fork / join events
-    hipStream_t side = nullptr;
-    hipEvent_t ev_side_start = nullptr, ev_side_done = nullptr;
     void release()
     {
         void* bufs[] = {d_dbinfo, d_sync, d_hb, d_hb2, d_lvl, d_list, d_lcnt, d_recon};
         for (void* b : bufs) if (b) (void)hipFree(b);
-        if (side) (void)hipStreamDestroy(side);
-        if (ev_side_start) (void)hipEventDestroy(ev_side_start);
-        if (ev_side_done) (void)hipEventDestroy(ev_side_done);
     }
 };
-constexpr int MAX_PIPES = 4;
 
 struct h264r_ctx {
     int device = 0;
@@ -140,6 +129,7 @@ struct h264r_ctx {
     const uint8_t** d_ref_planes = nullptr;
     int* d_err = nullptr;                 // [0] device error word (a bounded wait expired), [1] wait bound
     uint32_t wait_ticks = 0;              // err[1] as last written (s_memrealtime ticks, 100 MHz)
+    uint32_t wait_val = 0;                // its host copy, the source of the async write
     // streaming-API staging: two pictures, so that one is parsed (h264r_picture_begin /
     // h264r_mb_submit) while the other is reconstructed (h264r_picture_end_async)
     struct StreamPic {
@@ -168,10 +158,8 @@ struct h264r_ctx {
     h264r_pic* d_pic = nullptr; size_t c_pic = 0;
     h264r_quant* d_quant = nullptr; size_t c_quant = 0;
     uint8_t* d_out = nullptr; size_t c_out = 0;
-    // per-batch scratch of the launch sequence: one per pipeline stage (sub-batch)
-    Scratch sc[MAX_PIPES];
-    hipStream_t pipe_stream[MAX_PIPES] = {};
-    hipEvent_t ev_fork = nullptr, ev_join[MAX_PIPES] = {}, ev_stage[2][MAX_PIPES] = {};
+    // per-batch scratch of the launch sequence
+    Scratch sc;
     int levels_grid = 0;                           // resident workgroups of k_intra_levels
     int nxcc = 0;                                  // XCDs of the device (k_deblock2's placement)
     // the per-batch scratch above is reused by every launch: a launch on a stream other
@@ -250,22 +238,67 @@ int h264r_quant_init_lists(h264r_quant* q, const int32_t* const qm[12])
     return H264R_OK;
 }
 
-// The wall-time bound of every device-side wait (device_common.h wait_give_up): 2 s, or
-// H264R_WAIT_MS.  A launch of the slowest kernel over the largest batch takes ~10 ms, and
-// a wait only ever waits on work that is already running, so 2 s means a lost wave.
-static uint32_t wait_bound_ticks()
+// Environment knobs, read and validated once (at the first h264r_create).  Each one only
+// chooses between bit-exact schedules or bounds a wait; a value out of its range fails
+// h264r_create with H264R_EINVAL (stderr names it) instead of being taken for another setting.
+struct Knobs {
+    bool ok = true;
+    int debug = 0;             // H264R_DEBUG: schedule flags of h264r_set_debug OR-ed into every launch
+    uint32_t wait_ticks = 0;   // H264R_WAIT_MS: bound of every device-side wait (below)
+    int levels = 16;           // H264R_LEVELS: dependency levels from lists (level_launches)
+    int deblock2_min = 192;    // H264R_DEBLOCK2_MIN: batches from this size deblock with k_deblock2
+    int lvl_margin = 1;        // H264R_LVL_MARGIN: k_intra_levels' grid, blocks per CU below occupancy
+    bool coop = true;          // H264R_COOP: k_intra_levels by hipLaunchCooperativeKernel
+    int walk_gstep = 0;        // H264R_WALK_GSTEP: the walk's band hand-off period (0: by batch size)
+    bool verbose = false;      // H264R_VERBOSE
+};
+static bool env_long(const char* name, long lo, long hi, long* out)
 {
-    static const uint32_t t = [] {
-        const char* e = getenv("H264R_WAIT_MS");
-        const double ms = e ? atof(e) : 2000.0;
-        return (uint32_t)std::min(4.0e9, std::max(1.0, ms * 1.0e5));
-    }();
-    return t;
+    const char* e = getenv(name);
+    if (!e) return true;
+    char* end = nullptr;
+    errno = 0;
+    const long v = strtol(e, &end, 10);
+    if (end == e || *end != '\0' || errno != 0 || v < lo || v > hi) {
+        fprintf(stderr, "h264r: %s=\"%s\" is not an integer in [%ld, %ld]\n", name, e, lo, hi);
+        return false;
+    }
+    *out = v;
+    return true;
 }
-static int set_wait_bound(h264r_ctx* c, uint32_t ticks)
+constexpr int SCHEDULE_FLAGS = H264R_DBG_INTRA_WALK | H264R_DBG_DEBLOCK_MB | H264R_DBG_DEBLOCK_ROWS | H264R_DBG_DEBLOCK_GLOBAL;
+static const Knobs& knobs()
+{
+    static const Knobs k = [] {
+        Knobs n;
+        long v;
+        // flags that change or skip work (H264R_DBG_NO_DEBLOCK, the wait test) are API-only
+        v = 0; n.ok &= env_long("H264R_DEBUG", 0, SCHEDULE_FLAGS, &v);
+        if (v & ~SCHEDULE_FLAGS) { fprintf(stderr, "h264r: H264R_DEBUG=%ld: only schedule flags (%d)\n", v, SCHEDULE_FLAGS); n.ok = false; }
+        n.debug = (int)(v & SCHEDULE_FLAGS);
+        // a launch of the slowest kernel over the largest batch takes ~10 ms, and a wait only
+        // ever waits on work that is already running: 2 s means a lost wave
+        v = 2000; n.ok &= env_long("H264R_WAIT_MS", 1, 40000, &v);
+        n.wait_ticks = (uint32_t)(v * 100000);                     // s_memrealtime, 100 MHz
+        v = 16; n.ok &= env_long("H264R_LEVELS", 0, LEVEL_LISTS, &v); n.levels = (int)v;
+        v = 192; n.ok &= env_long("H264R_DEBLOCK2_MIN", 1, 1L << 30, &v); n.deblock2_min = (int)v;
+        v = 1; n.ok &= env_long("H264R_LVL_MARGIN", 0, 7, &v); n.lvl_margin = (int)v;
+        v = 1; n.ok &= env_long("H264R_COOP", 0, 1, &v); n.coop = v != 0;
+        v = 0; n.ok &= env_long("H264R_WALK_GSTEP", 0, 1 << 20, &v); n.walk_gstep = (int)v;
+        v = 0; n.ok &= env_long("H264R_VERBOSE", 0, 1, &v); n.verbose = v != 0;
+        return n;
+    }();
+    return k;
+}
+static uint32_t wait_bound_ticks() { return knobs().wait_ticks; }
+// err[1] is rewritten in stream order on the launch stream s (a launch still running on
+// another stream keeps the bound it started with only if it is ordered before -- run_batch
+// orders every launch of the context after the previous one)
+static int set_wait_bound(h264r_ctx* c, uint32_t ticks, hipStream_t s)
 {
     if (c->wait_ticks == ticks) return H264R_OK;
-    HIP_OK(hipMemcpy(c->d_err + 1, &ticks, sizeof(uint32_t), hipMemcpyHostToDevice));
+    c->wait_val = ticks;
+    HIP_OK(hipMemcpyAsync(c->d_err + 1, &c->wait_val, sizeof(uint32_t), hipMemcpyHostToDevice, s));
     c->wait_ticks = ticks;
     return H264R_OK;
 }
@@ -274,6 +307,7 @@ int h264r_create(h264r_ctx** out, int device, int max_w, int max_h, int chroma_f
 {
     if (!out || max_w <= 0 || max_h <= 0 || max_w > 1024 || max_h > 1024) return H264R_EINVAL;
     *out = nullptr;
+    if (!knobs().ok) return H264R_EINVAL;            // an environment knob out of range (stderr)
     if (chroma_format_idc != 1 || bit_depth != 8) return H264R_EUNSUPPORTED;
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0 || device < 0 || device >= n) return H264R_ENODEVICE;
@@ -294,7 +328,10 @@ int h264r_create(h264r_ctx** out, int device, int max_w, int max_h, int chroma_f
     if (hipEventCreateWithFlags(&c->ev_last, hipEventDisableTiming) != hipSuccess) { delete c; return H264R_EDEVICE; }
     (void)hipMemset(c->d_ref_planes, 0, sizeof(uint8_t*) * 3 * H264R_MAX_SLOTS);
     (void)hipMemset(c->d_err, 0, 2 * sizeof(int));
-    if (set_wait_bound(c, wait_bound_ticks()) != H264R_OK) { (void)h264r_destroy(c); return H264R_EDEVICE; }
+    if (set_wait_bound(c, wait_bound_ticks(), c->stream) != H264R_OK || hipStreamSynchronize(c->stream) != hipSuccess) {
+        (void)h264r_destroy(c);
+        return H264R_EDEVICE;
+    }
     *out = c;
     return H264R_OK;
 }
@@ -311,13 +348,7 @@ int h264r_destroy(h264r_ctx* c)
         if (p.out) (void)hipHostFree(p.out);
         if (p.done) (void)hipEventDestroy(p.done);
     }
-    for (int k = 0; k < MAX_PIPES; ++k) {
-        c->sc[k].release();
-        if (c->pipe_stream[k]) (void)hipStreamDestroy(c->pipe_stream[k]);
-        if (c->ev_join[k]) (void)hipEventDestroy(c->ev_join[k]);
-        for (int j = 0; j < 2; ++j) if (c->ev_stage[j][k]) (void)hipEventDestroy(c->ev_stage[j][k]);
-    }
-    if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+    c->sc.release();
     for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
     if (c->ev_last) (void)hipEventDestroy(c->ev_last);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -401,40 +432,20 @@ struct Timed {
 // hand-off beats one grid barrier per level (config 2: 36.6 ms of intra walking vs 44.9
 // with every level from lists).  H264R_LEVELS=<N> overrides N (0: walk only; at most
 // LEVEL_LISTS).
-static int level_launches()
-{
-    static const int env = [] { const char* e = getenv("H264R_LEVELS"); return e ? atoi(e) : 16; }();
-    return std::max(0, std::min(env, LEVEL_LISTS));
-}
+static int level_launches() { return knobs().levels; }
 
 // rows [row0, row1): the MB rows of every picture this launch reconstructs and
 // deblocks (the whole picture, or a slice-aligned band: h264r_decode_batch_rows).
-// Five launches on stream s: k_inter4 (inter / PCM MBs + deblocking records), k_level +
-// k_intra_levels + k_intra_pic (intra MBs), k_deblock or k_deblock2 (by batch size).
-// Pipeline hooks of one launch sequence (h264r_decode_batch's sub-batches): the inter
-// kernels of stage k start after stage k-1's (`after_inter`), its intra kernels after stage
-// k-1's intra kernels (`after_intra`: at most one grid-barrier kernel runs at a time), and it
-// records `inter_done` / `intra_done` for stage k+1.
-struct PipeHooks {
-    hipEvent_t after_inter = nullptr, after_intra = nullptr, inter_done = nullptr, intra_done = nullptr;
-    // a stage of a pipelined batch: other kernels share the device, so no grid barrier (the
-    // level kernel's whole grid need not be resident while they run: the walk does every
-    // intra MB)
-    bool pipelined = false;
-};
-
-static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row0, int row1, Scratch& X,
-                      const PipeHooks& hk = PipeHooks(), bool timed_whole = true)
+// The launches on stream s: k_dbinfo + k_inter4r + k_inter_sp (inter / PCM MBs and the
+// deblocking records), k_level + k_level_scan + k_level_scatter + k_intra_levels + k_intra_pic
+// (intra MBs), k_deblock or k_deblock2 (by batch size).
+static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row0, int row1, Scratch& X)
 {
-    // H264R_DEBUG=<flags>: the deblocking-schedule flags of h264r_set_debug OR-ed into every
-    // launch (measurement A/B); flags that change or skip work (H264R_DBG_NO_DEBLOCK, the
-    // wait test) are API-only, so a stray variable cannot alter the output
-    static const int env_debug = [] {
-        const char* e = getenv("H264R_DEBUG");
-        return e ? atoi(e) & (H264R_DBG_INTRA_WALK | H264R_DBG_DEBLOCK_MB | H264R_DBG_DEBLOCK_ROWS | H264R_DBG_DEBLOCK_GLOBAL) : 0;
-    }();
+    const Knobs& K = knobs();
+    // H264R_DEBUG: the deblocking-schedule flags of h264r_set_debug OR-ed into every launch
+    // (measurement A/B; validated in knobs(): schedule flags only, so the output is unchanged)
     const int debug_saved = c->debug;
-    c->debug |= env_debug;
+    c->debug |= K.debug;
     struct Restore { h264r_ctx* c; int d; ~Restore() { c->debug = d; } } restore{c, debug_saved};
     const int W = b.width_mbs, H = b.height_mbs, P = b.num_pics, HB = row1 - row0;
     const int2 rows = make_int2(row0, row1);
@@ -445,17 +456,13 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
     // + the deblocking kernels' per-XCD ticket counters, done count, then per picture the waves
     // of k_dbinfo that met an inter or I_PCM MB (k_inter4r skips the pictures without one)
     const size_t sync_n = 1 + (size_t)P * H + 5 + 9 + P;
-    // the scratch is shared by every launch of this context: a launch on another stream
-    // than the previous one waits for it first
     int st;
     if ((st = dev_resize(&X.d_dbinfo, &X.c_dbinfo, (size_t)P * W * H * DBINFO_BYTES))) return st;
     // the reconstruction kernels write the MB-tiled samples (device_common.h), the
     // deblocking kernel (or k_untile) turns them into the output planes
     if ((st = dev_resize(&X.d_recon, &X.c_recon, (size_t)P * W * H * 384))) return st;
     uint8_t* recon = X.d_recon;
-    static const int rows_min = [] { const char* e = getenv("H264R_DEBLOCK2_MIN"); return e ? atoi(e) : 192; }();
-    const bool by_rows = (c->debug & H264R_DBG_DEBLOCK_ROWS) || (!(c->debug & H264R_DBG_DEBLOCK_MB) && P >= rows_min);
-    (void)rows_min;
+    const bool by_rows = (c->debug & H264R_DBG_DEBLOCK_ROWS) || (!(c->debug & H264R_DBG_DEBLOCK_MB) && P >= K.deblock2_min);
     // hand-off records of the chosen deblocking kernel; fresh memory or a wrapping epoch
     // restarts from zeroed records, so no record may carry a live tag
     uint8_t** hb = by_rows ? &X.d_hb2 : &X.d_hb;
@@ -475,8 +482,8 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
     // H264R_DBG_WAIT_TEST: every intra-walk wait asks for progress no row reaches, under a
     // 10 ms bound -- the launch must drain and h264r_check report H264R_EDEVICE
     const bool wait_test = (c->debug & H264R_DBG_WAIT_TEST) != 0;
-    if ((st = set_wait_bound(c, wait_test ? 1000000u : wait_bound_ticks()))) return st;
-    const bool levels = !hk.pipelined && (size_t)W * H <= LEVEL_MAX_MBS && H <= 1024 && level_launches() > 0 &&
+    if ((st = set_wait_bound(c, wait_test ? 1000000u : wait_bound_ticks(), s))) return st;
+    const bool levels = (size_t)W * H <= LEVEL_MAX_MBS && H <= 1024 && level_launches() > 0 &&
                         !(c->debug & (H264R_DBG_INTRA_WALK | H264R_DBG_WAIT_TEST));
     if (levels && !c->levels_grid) {
         // every workgroup of the persistent level kernel must be resident at once: one
@@ -485,9 +492,8 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
         int per_cu = 0, cus = 0;
         HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(k_intra_levels), 256, 0));
         HIP_OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
-        static const int margin = [] { const char* e = getenv("H264R_LVL_MARGIN"); return e ? atoi(e) : 1; }();
-        c->levels_grid = std::max(1, per_cu - margin) * std::max(1, cus);
-        if (getenv("H264R_VERBOSE"))
+        c->levels_grid = std::max(1, per_cu - K.lvl_margin) * std::max(1, cus);
+        if (K.verbose)
             fprintf(stderr, "h264r: k_intra_levels occupancy %d blocks/CU, %d CUs, grid %d\n", per_cu, cus, c->levels_grid);
     }
     if (levels && ((st = dev_resize(&X.d_lvl, &X.c_lvl, (size_t)P * W * H)) ||
@@ -498,49 +504,26 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
     HIP_OK(hipMemsetAsync(X.d_sync, 0, sync_n * sizeof(int), s));
     h264r::DbInfo* dbinfo = reinterpret_cast<h264r::DbInfo*>(X.d_dbinfo);
     int* sync = X.d_sync;
-    Timed whole(timed_whole ? c : nullptr, 3, s);
-    if (c->timing && timed_whole) c->timed_launches++;
-    // the deblocking records: k_dbinfo before k_inter4r on this stream (H264R_DBINFO=1, the
-    // default: k_inter4r then fits 4 waves/SIMD), inside k_inter4 (0), or k_dbinfo on the
-    // scratch's side stream beside the reconstruction kernels, joined before deblocking (2)
-    // (profiles/r03_f_dbinfo_ab.txt, r03_h_inter_ab.txt)
-    const char* dbe = getenv("H264R_DBINFO");
-    const int db_mode = dbe ? atoi(dbe) : 1;
+    Timed whole(c, 3, s);
+    if (c->timing) c->timed_launches++;
     const int groups = (W * HB + 15) / 16;
     // groups per workgroup (launch_cfg.h), 8 XCD bands (k_recon.hip inter4_groups)
     const dim3 igrid(8 * ((groups + 8 * H264R_INTER_GROUPS - 1) / (8 * H264R_INTER_GROUPS)), P);
     const dim3 dgrid(8 * ((groups + 8 * H264R_DBINFO_GROUPS - 1) / (8 * H264R_DBINFO_GROUPS)), P);
-    if (db_mode == 2) {
-        if (!X.side) {
-            HIP_OK(hipStreamCreateWithFlags(&X.side, hipStreamNonBlocking));
-            HIP_OK(hipEventCreateWithFlags(&X.ev_side_start, hipEventDisableTiming));
-            HIP_OK(hipEventCreateWithFlags(&X.ev_side_done, hipEventDisableTiming));
-        }
-        HIP_OK(hipEventRecord(X.ev_side_start, s));                 // the previous launch's deblocking read dbinfo
-        HIP_OK(hipStreamWaitEvent(X.side, X.ev_side_start, 0));
-        hipLaunchKernelGGL(k_dbinfo, dgrid, dim3(256), 0, X.side, b, dbinfo, rows, (int*)nullptr);
-        HIP_OK(hipGetLastError());
-        HIP_OK(hipEventRecord(X.ev_side_done, X.side));
-    }
-    if (hk.after_inter) HIP_OK(hipStreamWaitEvent(s, hk.after_inter, 0));
     {
         Timed t(c, 0, s);
         int* sp_flag = sync + 1 + (size_t)P * H + 4;
-        // per-picture inter counts: only when k_dbinfo runs before k_inter4r on this stream
-        int* inter_cnt = db_mode == 1 ? sync + 1 + (size_t)P * H + 14 : nullptr;
-        if (db_mode == 1) {
-            hipLaunchKernelGGL(k_dbinfo, dgrid, dim3(256), 0, s, b, dbinfo, rows, inter_cnt);
-            HIP_OK(hipGetLastError());
-        }
-        if (db_mode == 0) hipLaunchKernelGGL(k_inter4, igrid, dim3(256), 0, s, b, dbinfo, rows, sp_flag, recon);
-        else hipLaunchKernelGGL(k_inter4r, igrid, dim3(256), 0, s, b, dbinfo, rows, sp_flag, recon, (const int*)inter_cnt);
+        // the deblocking records first (k_inter4r then fits 4 waves/SIMD), with per picture
+        // a flag that an inter or I_PCM MB was met (profiles/r03_f_dbinfo_ab.txt, r03_h_inter_ab.txt)
+        int* inter_cnt = sync + 1 + (size_t)P * H + 14;
+        hipLaunchKernelGGL(k_dbinfo, dgrid, dim3(256), 0, s, b, dbinfo, rows, inter_cnt);
+        HIP_OK(hipGetLastError());
+        hipLaunchKernelGGL(k_inter4r, igrid, dim3(256), 0, s, b, dbinfo, rows, sp_flag, recon, (const int*)inter_cnt);
         HIP_OK(hipGetLastError());
         // inter MBs of SP slices (a short launch when the batch has none)
         hipLaunchKernelGGL(k_inter_sp, dim3(1024), dim3(256), 0, s, b, rows, (const int*)sp_flag, recon);
         HIP_OK(hipGetLastError());
     }
-    if (hk.inter_done) HIP_OK(hipEventRecord(hk.inter_done, s));
-    if (hk.after_intra) HIP_OK(hipStreamWaitEvent(s, hk.after_intra, 0));
     {
         Timed t(c, 1, s);
         uint16_t* lvl = levels ? X.d_lvl : nullptr;
@@ -568,8 +551,7 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
             // barriers, whose cost grows with the number of arrivals (MI355X_MICROARCH.md
             // price list 'barrier-xcd')
             const int lgrid = std::min(c->levels_grid, std::max(8, (int)(((size_t)P * W * HB + 63) / 64)));
-            static const bool coop = [] { const char* e = getenv("H264R_COOP"); return !e || atoi(e) != 0; }();
-            if (coop) {
+            if (K.coop) {
                 const int* lcount_c = lcount;
                 const int* lbase_c = lbase;
                 const uint32_t* list_c = X.d_list;
@@ -587,14 +569,11 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
         }
         // the walk's band-to-band hand-off: global progress every gstep MBs (k_picture.hip);
         // H264R_WALK_GSTEP overrides
-        static const int gstep_env = [] { const char* e = getenv("H264R_WALK_GSTEP"); return e ? atoi(e) : 0; }();
-        const int gstep = wait_test ? -1 : gstep_env > 0 ? gstep_env : (P >= 128 ? 64 : 1);
+        const int gstep = wait_test ? -1 : K.walk_gstep > 0 ? K.walk_gstep : (P >= 128 ? 64 : 1);
         hipLaunchKernelGGL(k_intra_pic, dim3(P * nbands), dim3(64 * H264R_WALK_ROWS), 0, s, b, sync, c->d_err,
                            (const uint16_t*)lvl, lmax, rows, gstep, recon);
         HIP_OK(hipGetLastError());
     }
-    if (hk.intra_done) HIP_OK(hipEventRecord(hk.intra_done, s));
-    if (db_mode == 2) HIP_OK(hipStreamWaitEvent(s, X.ev_side_done, 0));
     if (!(c->debug & H264R_DBG_NO_DEBLOCK)) {
         Timed t(c, 2, s);
         if (!c->nxcc) {                  // XCDs of the device: the deblocking kernels' placement
@@ -604,15 +583,11 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
         }
         if (by_rows)
         {
-            // k_deblock2 keeps a 16-picture group on one XCD (g % nx): nx counters;
-            // H264R_DEBLOCK3=1: k_deblock3, the same walk with 8 lanes per picture-row (A/B)
-            const char* d3e = getenv("H264R_DEBLOCK3");
-            const bool d3 = d3e && atoi(d3e) != 0;
-            const int units = d3 ? DEBLOCK3_UNITS : DEBLOCK2_UNITS;
-            int grid = ((P + units - 1) / units) * HB;
+            // k_deblock2 keeps a 16-picture group on one XCD (g % nx): nx counters
+            int grid = ((P + DEBLOCK2_UNITS - 1) / DEBLOCK2_UNITS) * HB;
             const int nx = grid >= 64 * c->nxcc && !(c->debug & H264R_DBG_DEBLOCK_GLOBAL) ? c->nxcc : 1;
             grid = (grid + nx - 1) / nx * nx;
-            hipLaunchKernelGGL(d3 ? k_deblock3 : k_deblock2, dim3(grid), dim3(64), 0, s, b, dbinfo,
+            hipLaunchKernelGGL(k_deblock2, dim3(grid), dim3(64), 0, s, b, dbinfo,
                                reinterpret_cast<uint64_t*>(X.d_hb2), sync + 1 + (size_t)P * H + 5, c->d_err, ++X.epoch2, rows,
                                nx, (const uint8_t*)recon);
         }
@@ -633,43 +608,6 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
     return H264R_OK;
 }
 
-// h264r_decode_batch's pipeline (opt-in): with H264R_PIPES = n > 1, a batch of >= 2 x
-// H264R_PIPE_MIN pictures (default 256) is cut into n sub-batches (at most MAX_PIPES)
-// launched on the context's pipeline streams, so that one sub-batch's latency-bound kernels
-// (the intra walk, the deblocking row walk) could share the CUs with the next sub-batch's
-// fully parallel k_inter4: stage k's inter kernels start after stage k-1's, its intra
-// kernels after stage k-1's (never two grid-barrier kernels at once), deblocking whenever
-// its own intra kernels are done.  The caller's stream forks into the stages and joins
-// them; the results are those of one launch sequence over the whole batch.  Default 1:
-// measured on MI355X (profiles/r03_pipes.txt) every depth > 1 is slower -- config 3 at
-// batch 1024 406.8 -> 372.5 / 352.1 / 336.4 Mmb/s at 2 / 3 / 4 sub-batches, config 4
-// unchanged -- each kernel already fills the chip, and the overlap only adds contention.
-// Read per call (tests switch it).
-static int pipe_count(int P)
-{
-    const char* e = getenv("H264R_PIPES");
-    const char* m = getenv("H264R_PIPE_MIN");
-    const int pipes = e ? atoi(e) : 1, pmin = m ? atoi(m) : 256;
-    return std::max(1, std::min(std::min(pipes, MAX_PIPES), P / std::max(1, pmin)));
-}
-
-static h264r_batch sub_batch(const h264r_batch& b, int p0, int p1)
-{
-    const size_t nmb = (size_t)b.width_mbs * b.height_mbs;
-    h264r_batch x = b;
-    x.num_pics = p1 - p0;
-    x.mbs = b.mbs + (size_t)p0 * nmb;
-    x.mv = b.mv + (size_t)p0 * 32 * nmb;
-    x.ref_idx = b.ref_idx + (size_t)p0 * 32 * nmb;
-    x.slices = b.slices + (size_t)p0 * b.slice_stride;
-    x.pics = b.pics + p0;
-    x.quant = b.quant + p0;
-    x.out_y = b.out_y + (size_t)p0 * 256 * nmb;
-    x.out_u = b.out_u + (size_t)p0 * 64 * nmb;
-    x.out_v = b.out_v + (size_t)p0 * 64 * nmb;
-    return x;
-}
-
 static int run_batch(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row0, int row1)
 {
     // the scratch is shared by every launch of this context: a launch on another stream
@@ -679,35 +617,7 @@ static int run_batch(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row0
         HIP_OK(hipStreamWaitEvent(s, c->ev_last, 0));
     }
     c->last_stream = s;
-    const int n = pipe_count(b.num_pics);
-    if (n == 1) return launch_all(c, b, s, row0, row1, c->sc[0]);
-    if (!c->ev_fork) {
-        HIP_OK(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
-        for (int k = 0; k < MAX_PIPES; ++k) {
-            HIP_OK(hipStreamCreateWithFlags(&c->pipe_stream[k], hipStreamNonBlocking));
-            HIP_OK(hipEventCreateWithFlags(&c->ev_join[k], hipEventDisableTiming));
-            for (int j = 0; j < 2; ++j) HIP_OK(hipEventCreateWithFlags(&c->ev_stage[j][k], hipEventDisableTiming));
-        }
-    }
-    Timed whole(c, 3, s);
-    if (c->timing) c->timed_launches++;
-    HIP_OK(hipEventRecord(c->ev_fork, s));
-    for (int k = 0; k < n; ++k) {
-        const int p0 = (int)((long long)b.num_pics * k / n), p1 = (int)((long long)b.num_pics * (k + 1) / n);
-        hipStream_t sk = c->pipe_stream[k];
-        HIP_OK(hipStreamWaitEvent(sk, c->ev_fork, 0));
-        PipeHooks hk;
-        hk.after_inter = k ? c->ev_stage[0][k - 1] : nullptr;
-        hk.after_intra = k ? c->ev_stage[1][k - 1] : nullptr;
-        hk.inter_done = c->ev_stage[0][k];
-        hk.intra_done = c->ev_stage[1][k];
-        hk.pipelined = true;
-        int st = launch_all(c, sub_batch(b, p0, p1), sk, row0, row1, c->sc[k], hk, false);
-        if (st) return st;
-        HIP_OK(hipEventRecord(c->ev_join[k], sk));
-    }
-    for (int k = 0; k < n; ++k) HIP_OK(hipStreamWaitEvent(s, c->ev_join[k], 0));
-    return H264R_OK;
+    return launch_all(c, b, s, row0, row1, c->sc);
 }
 
 #ifdef H264R_TRACE
@@ -727,11 +637,18 @@ static void dump_trace(hipStream_t s)
 }
 #endif
 
+// ref_planes_stride: 0 (one table) or whole tables apart; per-picture tables need the caller's own
+static bool stride_ok(const h264r_batch* b)
+{
+    return b->ref_planes_stride == 0 || (b->ref_planes_stride >= 3 * H264R_MAX_SLOTS && b->ref_planes);
+}
+
 int h264r_decode_batch(h264r_ctx* c, const h264r_batch* b, void* stream)
 {
     if (!c || !b || b->num_pics <= 0 || b->width_mbs <= 0 || b->height_mbs <= 0 ||
         b->width_mbs > c->max_w || b->height_mbs > c->max_h || b->slice_stride <= 0 || !b->mbs || !b->levels ||
-        !b->mv || !b->ref_idx || !b->slices || !b->pics || !b->quant || !b->out_y || !b->out_u || !b->out_v)
+        !b->mv || !b->ref_idx || !b->slices || !b->pics || !b->quant || !b->out_y || !b->out_u || !b->out_v ||
+        !stride_ok(b))
         return H264R_EINVAL;
     (void)hipSetDevice(c->device);
     h264r_batch bb = *b;
@@ -751,7 +668,7 @@ int h264r_decode_batch_rows(h264r_ctx* c, const h264r_batch* b, int row0, int ro
     if (!c || !b || row0 < 0 || row1 <= row0 || row1 > b->height_mbs) return H264R_EINVAL;
     if (!b->mbs || !b->levels || !b->mv || !b->ref_idx || !b->slices || !b->pics || !b->quant || !b->out_y ||
         !b->out_u || !b->out_v || b->num_pics <= 0 || b->width_mbs <= 0 || b->width_mbs > c->max_w ||
-        b->height_mbs > c->max_h || b->slice_stride <= 0)
+        b->height_mbs > c->max_h || b->slice_stride <= 0 || !stride_ok(b))
         return H264R_EINVAL;
     (void)hipSetDevice(c->device);
     h264r_batch bb = *b;

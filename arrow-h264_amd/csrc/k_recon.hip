@@ -1,25 +1,20 @@
 // k_recon.hip -- the fully parallel part of a batch.
 //
-// k_inter4 four MBs per wave, one lane per 4x4 block: inter MBs and I_PCM
-//          reconstructed (mb_inter4.h), and the per-MB deblocking record DbInfo of
-//          every MB; intra MBs are left to the intra kernels (they depend on their
-//          neighbours).  Motion is read as the parser left it ({mv, ref_idx} per list)
-//          and RefPicList[l][ref_idx] resolved to a DPB slot through an LDS copy of the
-//          picture's slice tables.
+// k_dbinfo  the per-MB deblocking record DbInfo of every MB (mb_inter4.h dbinfo_block).
+// k_inter4r four MBs per wave, one lane per 4x4 block: inter MBs and I_PCM reconstructed
+//           (mb_inter4.h); intra MBs are left to the intra kernels (they depend on their
+//           neighbours).  Motion is read as the parser left it ({mv, ref_idx} per list) and
+//           RefPicList[l][ref_idx] resolved to a DPB slot through an LDS copy of the
+//           picture's slice tables.
 #include "launch_cfg.h"
 #include "mb_inter4.h"
 
 using namespace h264r;
 
-// Grid (ceil(nmb / 16), pictures).
 // minimum waves per SIMD asked of the register allocator: k_inter4r 4 (<= 128 VGPRs, its
-// natural size with the residual loaded after the motion compensation), the fused
-// k_inter4 3 (<= 168)
+// natural size with the residual loaded after the motion compensation)
 #ifndef H264R_INTER_WAVES
 #define H264R_INTER_WAVES 4
-#endif
-#ifndef H264R_INTER4_WAVES
-#define H264R_INTER4_WAVES 3
 #endif
 // The workgroup's copy of the DPB plane table and of picture `pic`'s slice ref tables, slice
 // types and slice headers.  Every thread issues its loads first (clamped indices, no branch)
@@ -34,7 +29,8 @@ DEV LdsRegs inter4_lds_load(const h264r_batch& b, int pic)
     const int nsl = min(b.slice_stride, INTER4_LDS_SLICES);
     const h264r_slice* sl = b.slices + (size_t)pic * b.slice_stride;
     LdsRegs r;
-    r.plane = b.ref_planes[min(t, 3 * H264R_MAX_SLOTS - 1)];
+    // the batch's one DPB table, or picture pic's own (ref_planes_stride, include/h264r.h)
+    r.plane = b.ref_planes[(size_t)pic * b.ref_planes_stride + min(t, 3 * H264R_MAX_SLOTS - 1)];
     const int ri = min(t, nsl * 4 - 1);                      // ref tables: 32 bytes per slice, 8 per thread
     r.refs = *reinterpret_cast<const uint2*>(&sl[ri >> 2].ref_slot[0][0] + 8 * (ri & 3));
     r.hdr = *reinterpret_cast<const uint2*>(&sl[min(t, nsl - 1)]);
@@ -52,17 +48,6 @@ DEV void inter4_lds_store(const h264r_batch& b, const LdsRegs& r, Inter4Lds& S)
     }
 }
 DEV void inter4_lds(const h264r_batch& b, int pic, Inter4Lds& S) { inter4_lds_store(b, inter4_lds_load(b, pic), S); }
-
-// the wave's QuadTile rows (H264R_QTILE builds only: mb_inter4.h)
-DEV QuadTile* wave_tiles()
-{
-#ifdef H264R_QTILE
-    __shared__ QuadTile tiles[4][INTER4_TILES];
-    return tiles[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)];
-#else
-    return nullptr;
-#endif
-}
 
 // The 16-MB groups [grp, gend) of one k_inter4 / k_dbinfo workgroup: XCD-aware (below),
 // `per` (H264R_INTER_GROUPS / H264R_DBINFO_GROUPS, launch_cfg.h) consecutive groups of its
@@ -83,11 +68,12 @@ DEV bool inter4_groups(const Geom& g, int2 rows, int per, int& grp, int& gend)
 // blockIdx.x % 8 (one eighth of the MB rows) of every picture: an XCD's motion
 // compensation reads only its band of the reference pictures (+ the MV reach), which its
 // 4 MB L2 holds, instead of every XCD streaming whole references through its L2.
-// DB: the deblocking records too (k_inter4), or not (k_inter4r, with k_dbinfo beside it).
-template <bool DB>
-DEV void inter4_kernel(const h264r_batch& b, DbInfo* dbinfo, int2 rows, int* sp_flag, uint8_t* recon, Inter4Lds& S,
-                       const int* inter_cnt)
+extern "C" __global__ __launch_bounds__(256, H264R_INTER_WAVES) void k_inter4r(h264r_batch b, DbInfo* dbinfo, int2 rows,
+                                                                              int* sp_flag, uint8_t* recon,
+                                                                              const int* inter_cnt)
 {
+    (void)dbinfo;
+    __shared__ Inter4Lds S;
     const int pic = blockIdx.y;
     const Geom g = make_geom(b.width_mbs, b.height_mbs);
     int grp, gend;
@@ -109,7 +95,7 @@ DEV void inter4_kernel(const h264r_batch& b, DbInfo* dbinfo, int2 rows, int* sp_
         // hoisted out of the loop and kept live across it (that spilled 144 B per lane)
         int ln = lane;
         asm volatile("" : "+v"(ln));
-        inter4_mbs<false, DB>(b, g, pic, a0, aend, ln, dbinfo + (size_t)pic * g.nmb, S, sp_flag, pre, wave_tiles(), recon);
+        inter4_mbs<false>(b, g, pic, a0, aend, ln, S, sp_flag, pre, recon);
         if (++grp >= gend) return;
         a0 = rows.x * g.wmb + (grp * 4 + wave) * 4;
         int ln2 = lane;
@@ -117,23 +103,10 @@ DEV void inter4_kernel(const h264r_batch& b, DbInfo* dbinfo, int2 rows, int* sp_
         pre = inter4_pre(b, g, pic, a0, aend, ln2);
     }
 }
-extern "C" __global__ __launch_bounds__(256, H264R_INTER4_WAVES) void k_inter4(h264r_batch b, DbInfo* dbinfo, int2 rows,
-                                                                             int* sp_flag, uint8_t* recon)
-{
-    __shared__ Inter4Lds S;
-    inter4_kernel<true>(b, dbinfo, rows, sp_flag, recon, S, nullptr);
-}
-extern "C" __global__ __launch_bounds__(256, H264R_INTER_WAVES) void k_inter4r(h264r_batch b, DbInfo* dbinfo, int2 rows,
-                                                                              int* sp_flag, uint8_t* recon,
-                                                                              const int* inter_cnt)
-{
-    __shared__ Inter4Lds S;
-    inter4_kernel<false>(b, dbinfo, rows, sp_flag, recon, S, inter_cnt);
-}
 
 // k_dbinfo: the deblocking records DbInfo of every MB (dbinfo_block, mb_inter4.h) on their
-// own -- they depend on the MB records and motion only, not on any sample, so the host
-// launches this beside k_inter4r on a second stream.  Same grid and lane roles as k_inter4.
+// own -- they depend on the MB records and motion only, not on any sample; launched before
+// k_inter4r.  Same grid and lane roles as k_inter4r.
 extern "C" __global__ __launch_bounds__(256) void k_dbinfo(h264r_batch b, DbInfo* dbinfo, int2 rows, int* inter_cnt)
 {
     __shared__ Inter4Lds S;
@@ -187,8 +160,7 @@ extern "C" __global__ __launch_bounds__(256) void k_inter_sp(h264r_batch b, int2
         inter4_lds(b, pic, S);
         __syncthreads();
         const int a0 = rows.x * g.wmb + (grp * 4 + wave) * 4;
-        if (a0 < aend) inter4_mbs<true, false>(b, g, pic, a0, aend, lane, nullptr, S, nullptr, inter4_pre(b, g, pic, a0, aend, lane),
-                                               wave_tiles(), recon);
+        if (a0 < aend) inter4_mbs<true>(b, g, pic, a0, aend, lane, S, nullptr, inter4_pre(b, g, pic, a0, aend, lane), recon);
     }
 }
 

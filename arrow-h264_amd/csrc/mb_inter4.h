@@ -192,33 +192,11 @@ DEV void luma_window_global(const uint8_t* __restrict__ img, int W, int H, int x
     }
 }
 
-// Reference tiles in LDS (north_star: "LDS staging of reference-block tiles"), built and
-// measured, OFF by default (-DH264R_QTILE builds it): the four 4x4 blocks of an 8x8
-// quadrant that share one motion vector read one 13-row x 16-byte tile of the reference
-// (rows y-2 .. y+10, aligned dwords from (x-2) & ~3), which the quadrant's four lanes fetch
-// together by LDS-DMA (global_load_lds_dwordx4, no VGPR staging: k_inter4 sits at its VGPR
-// cap) -- at most four 16-byte rows per lane -- instead of each lane fetching its own 9
-// rows x 12 bytes.  Bit-exact (154 GPU tests), but k_inter4 9.41 -> 11.00 ms per 1024
-// config-3 pictures and 3.75 -> 4.23 ms on config 4 (profiles/r03_e_ab.txt): the fill's
-// vmcnt(0) also retires the residual loads issued before it, the per-lane window reads
-// from LDS are no cheaper than the L1/L2-served global ones (the quadrant's rows were
-// already shared in L1), and the extra live state spilled (84 B/lane of scratch at the
-// 168-VGPR cap).  Register staging instead of LDS-DMA spilled 140 B/lane.
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-struct alignas(16) QuadTile {
-    u32x4 slot[64];                  // one wave-instruction of LDS-DMA: 16 B per lane
-};
-constexpr int INTER4_TILES = 4;      // per wave: tile rows ql, ql + 4, ql + 8, 12 of every quadrant
-
 DEV void luma_block_pred(const uint32_t (&w)[9][3], int W, int x, int xf, int yf, uint32_t (&out)[4])
 {
     const int hs = xf == 3 ? 1 : 0;                  // G / h column c + 2 + hs
     const int brow = yf == 3 ? 1 : 0;                // b / G row i + 2 + brow
-#ifdef H264R_EXP_NO_EDGE
-    const bool inside = true;
-#else
     const bool inside = x - 2 >= 0 && x + 6 < W;
-#endif
     const int sh = (x - 2) & 3;
     s16x2 hacc[4][2], bsv[4][2], gsv[4][2];
     int jacc[4][4];
@@ -255,14 +233,10 @@ DEV void luma_block_pred(const uint32_t (&w)[9][3], int W, int x, int xf, int yf
         for (int i = 0; i < 4; ++i) {
             const int k = r - i;                       // tap index of row r for output row i
             if (k < 0 || k > 5) continue;
-#ifndef H264R_EXP_NO_H
             hacc[i][0] += splat16(C6[k]) * g01;
             hacc[i][1] += splat16(C6[k]) * g23;
-#endif
-#ifndef H264R_EXP_NO_J
 #pragma unroll
             for (int c = 0; c < 4; ++c) jacc[i][c] += C6[k] * bc[c];
-#endif
             if (k == 2 || k == 3) {                    // b / G of output row i: row i + 2 + brow
                 const bool take = k == 2 + brow;
                 bsv[i][0] = take ? b01 : bsv[i][0];
@@ -558,14 +532,13 @@ DEV void dbinfo_block(const h264r_batch& b, const Geom& g, int pic, int aa, bool
     }
 }
 
-// The inter / I_PCM macroblocks a0 .. a0+3 of picture `pic` and (DB) the deblocking
-// records of all four.  SP = false (k_inter4): inter MBs of SP slices are left out and
-// flagged in *sp_flag; SP = true (k_inter_sp): only those are reconstructed, with
-// inverse_transform_sp (decoder.cc:256-257, transform.cc:1267-1300), and no records.
-template <bool SP, bool DB>
-DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int aend, int lane, DbInfo* __restrict__ dbout,
-                    const Inter4Lds& S, int* sp_flag, const Inter4Pre& pre, QuadTile* __restrict__ tiles,
-                    uint8_t* __restrict__ recon)
+// The inter / I_PCM macroblocks a0 .. a0+3 of picture `pic` (their deblocking records come
+// from k_dbinfo).  SP = false (k_inter4r): inter MBs of SP slices are left out and flagged in
+// *sp_flag; SP = true (k_inter_sp): only those are reconstructed, with inverse_transform_sp
+// (decoder.cc:256-257, transform.cc:1267-1300).
+template <bool SP>
+DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int aend, int lane,
+                    const Inter4Lds& S, int* sp_flag, const Inter4Pre& pre, uint8_t* __restrict__ recon)
 {
     const int grp = lane >> 4, blk = lane & 15, bx = blk & 3, by = blk >> 2;
     const int a = a0 + grp;
@@ -585,8 +558,7 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
     const int q_type = qsh.x & 255;
     const int wp_mode = qsh.y & 255;
 
-    // ---- reconstruction of inter / I_PCM MBs first (the motion-compensation loads go
-    // out as early as possible), the deblocking record of every MB after it
+    // ---- reconstruction of inter / I_PCM MBs (intra MBs: the lanes idle here)
     [&]() {
         const bool pcm = q.mb_type == H264R_I_PCM;
         if (!valid || (mb_is_intra(q) && !pcm)) return;              // intra: k_intra_* (lanes idle here)
@@ -618,8 +590,7 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
 
         // ---- residual inputs: issued after the motion compensation, so that they are not
         // live across it (30 VGPRs: k_inter4r fits 128 VGPRs = 4 waves/SIMD; config 3
-        // 475 -> 493 M MB/s with k_dbinfo, profiles/r03_h_inter_ab.txt), or before it
-        // (H264R_RES_EARLY)
+        // 475 -> 493 M MB/s, profiles/r03_h_inter_ab.txt)
         const int cbpl = q.cbp & 15, cbpc = q.cbp >> 4;
         const int t8 = (q.flags & H264R_MBF_T8x8) != 0;
         const h264r_quant* __restrict__ qt = &b.quant[pic];
@@ -666,9 +637,6 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
                 }
             }
         };
-#ifdef H264R_RES_EARLY
-        load_residual();
-#endif
 
         // ---- prediction
         const int r0 = (int8_t)(m0.y & 255), r1 = (int8_t)(m1.y & 255);
@@ -689,58 +657,14 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
             const int mvx = (int16_t)(mw.x & 0xFFFF), mvy = (int16_t)(mw.x >> 16);
             const int vx = X4 * 16 + mvx, vy = Y4 * 16 + mvy;           // quarter luma / eighth chroma units
             const int x = vx >> 2, y = vy >> 2;
-#ifndef H264R_EXP_NO_LUMA           // (measurement-only knobs: tools/exp_sweep.sh ablations)
             {
-                // quadrant tile (QuadTile): the four lanes of my 8x8 quadrant (blk ^ 1, ^ 4, ^ 5)
-                // predict from one slot with one vector, and the tile stays inside the picture
-                const uint32_t key = ok ? mw.x : 0xFFFFFFFFu;
-                const int skey = ok ? slot : -1;
-                const bool uni = ok && key == (uint32_t)__shfl_xor((int)key, 1) && key == (uint32_t)__shfl_xor((int)key, 4) &&
-                                 key == (uint32_t)__shfl_xor((int)key, 5) && skey == __shfl_xor(skey, 1) &&
-                                 skey == __shfl_xor(skey, 4) && skey == __shfl_xor(skey, 5);
-                const int xq = x - 4 * (bx & 1), yq = y - 4 * (by & 1);
-#ifdef H264R_QTILE                   // measured slower: off (QuadTile above)
-                const bool tile = uni && xq - 2 >= 0 && xq + 10 < g.W;
-#else
-                const bool tile = false && uni && xq >= 0;
-#endif
-                // tile row t * 4 + ql (row 12: t = 3, ql = 0) of a quadrant lands, by LDS-DMA, in
-                // the 16-byte slot of the quadrant's lane ql of its wave-instruction t
-                const int qbase = grp * 16 + (by & 2) * 4 + (bx & 2);          // lane of ql = 0
-                if (__any(tile)) {
-                    const int ql = (by & 1) * 2 + (bx & 1);
-                    const uint8_t* img = S.planes[(tile ? slot : 0) * 3] + ((xq - 2) & ~3);
-#pragma unroll
-                    for (int t = 0; t < 4; ++t)
-                        if (tile && (t < 3 || ql == 0))
-                            __builtin_amdgcn_global_load_lds(
-                                (const __attribute__((address_space(1))) void*)(img + (size_t)clip3(0, g.H - 1, yq - 2 + ql + 4 * t) * g.W),
-                                (__attribute__((address_space(3))) void*)(tiles + t), 16, 0, 0);
-                    __builtin_amdgcn_s_waitcnt(0x0F70);                       // vmcnt(0): this wave's tiles landed
-                    __builtin_amdgcn_wave_barrier();
-                }
-                // the 9 window rows: tile rows (by & 1) * 4 + r from dword (bx & 1), or the
-                // lane's own rows of the plane -- one generic (flat) load per row either way
                 uint32_t w[9][3];
-                if (tile) {
-                    const uint32_t* tb = reinterpret_cast<const uint32_t*>(tiles) + (bx & 1);
-#pragma unroll
-                    for (int r = 0; r < 9; ++r) {
-                        const int jr = (by & 1) * 4 + r;                        // tile row
-                        const int src = qbase + ((jr & 2) << 1) + (jr & 1);    // lane that fetched it
-                        const uint32_t* q = tb + (jr >> 2) * 256 + src * 4;
-                        w[r][0] = q[0]; w[r][1] = q[1]; w[r][2] = q[2];
-                    }
-                } else if (ok) {
+                if (ok) {
                     luma_window_global(S.planes[slot * 3], g.W, g.H, x, y, w);
+                    luma_block_pred(w, g.W, x, vx & 3, vy & 3, tY);
                 }
-                if (ok) luma_block_pred(w, g.W, x, vx & 3, vy & 3, tY);
-                if (__any(tile)) wave_sync();                      // read before the next list's tiles
             }
-#endif
-#ifndef H264R_EXP_NO_CHROMA
             if (ok) chroma_block_pred2(S.planes[slot * 3 + 1], S.planes[slot * 3 + 2], g.Wc, g.Hc, vx >> 3, vy >> 3, vx & 7, vy & 7, tC);
-#endif
             const bool l1 = l != 0;
     #pragma unroll
             for (int i = 0; i < 4; ++i) {
@@ -764,9 +688,7 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
         for (int i = 0; i < 4; ++i) predY[i] = wp_combine4(wpp[0], wp_mode, dir, pY[0][i], pY[1][i]);
     #pragma unroll
         for (int pl = 0; pl < 2; ++pl) predC[pl] = wp_combine4(wpp[1 + pl], wp_mode, dir, pC[0][pl], pC[1][pl]);
-#ifndef H264R_RES_EARLY
         load_residual();
-#endif
 
         if constexpr (SP) {
             // ---- itrans_sp of this lane's 4x4 block (:1132-1187): the prediction is
@@ -928,11 +850,7 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
     #pragma unroll
             for (int c = 0; c < 4; ++c) res[i][c] = 0;
         const bool byp = (q.flags & H264R_MBF_BYPASS) != 0;
-#ifdef H264R_EXP_NO_RES
-        if (false) {
-#else
         if (__any(cbpl != 0)) {
-#endif
             const int per = qpl / 6;
             // dq4 / dq8 (transform.cc:394-419) as one form, rounding and shift per lane: the
             // lanes of a wave mix 4x4 and 8x8 MBs, and a select per value (not a branch) keeps
@@ -1058,11 +976,7 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
     #pragma unroll
         for (int pl = 0; pl < 2; ++pl) {
             int rc[2][2] = {{0, 0}, {0, 0}};
-#ifdef H264R_EXP_NO_RES
-            if (false) {
-#else
             if (__any(cbpc != 0)) {
-#endif
                 const int qpc = q.qp_scaled[1 + pl], per = qpc / 6;
                 int k[2][2], raw[2][2];
     #pragma unroll
@@ -1121,15 +1035,6 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
             }
         }
     }();
-
-    if constexpr (SP || !DB) return;
-#ifdef H264R_EXP_NO_DBINFO
-    return;
-#endif
-    // neighbour records and motion loaded only now, so that they do not stay live across the
-    // motion compensation (L2-hot by then)
-    const DbNb nb = dbinfo_pre(b, g, pic, a0, aend, lane);
-    dbinfo_block(b, g, pic, aa, valid, blk, S, q, m0, m1, qsh, nb, dbout);
 }
 
 }  // namespace h264r

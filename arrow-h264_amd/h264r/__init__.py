@@ -83,7 +83,7 @@ def lib() -> C.CDLL:
         f = getattr(L, name)
         f.argtypes, f.restype = args, res
     A.bind_synth(L)
-    if L.h264r_abi_version() != 1:
+    if L.h264r_abi_version() != A.ABI_VERSION:
         raise ImportError("libh264r ABI version mismatch")
     _lib = L
     return L

@@ -14,6 +14,7 @@ OK, EINVAL, ENOMEM, EDEVICE, ESTATE, EUNSUPPORTED, ENODEVICE = 0, -1, -2, -3, -4
 DBG_NO_DEBLOCK, DBG_INTRA_WALK, DBG_DEBLOCK_MB, DBG_DEBLOCK_ROWS, DBG_DEBLOCK_GLOBAL = 1, 2, 4, 8, 16   # h264r_set_debug flags (include/h264r.h)
 DBG_WAIT_TEST = 32
 MAX_REFS, MAX_SLOTS, MAX_SLICES = 16, 32, 256
+ABI_VERSION = 2
 
 P_SKIP, P_16x16, P_16x8, P_8x16, P_8x8, P_8x4, P_4x8, P_4x4 = range(8)
 I_4x4, I_8x8, I_16x16, SI, I_PCM = 8, 9, 10, 11, 12
@@ -81,6 +82,7 @@ class Batch(C.Structure):
         ("mv", C.c_void_p), ("ref_idx", C.c_void_p), ("slices", C.c_void_p),
         ("pics", C.c_void_p), ("quant", C.c_void_p), ("ref_planes", C.c_void_p),
         ("out_y", C.c_void_p), ("out_u", C.c_void_p), ("out_v", C.c_void_p),
+        ("ref_planes_stride", C.c_int64),
     ]
 
 

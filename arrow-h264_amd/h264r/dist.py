@@ -97,52 +97,158 @@ def max_over_ranks(seconds: float, device=None) -> float:
     return float(t.item())
 
 
-# ------------------------------------------------------------------ dependent chains
-# Slice mode over a real stream (bench.py --chain): every picture of a chain predicts from
-# the chain's previous decoded picture, so each reference picture crosses the ranks once,
-# before the next picture of its chain may start -- the exchange is on the dependency
-# path (slice walk slice_data.cc:640-650, idc 2 stopping the filter at slice edges
-# deblock.cc:247-253).  K chains advance together: their pictures form one batch, chain k
-# predicting from DPB slot k, and one all-gather per plane moves every rank's band of all
-# K pictures at once.
-
-def chain_slots(slices, chain: int, nchains: int):
-    """Slice tables of a chain's picture: reference slot 0 (the picture's first list-0
-    reference) becomes the chain's own slot `chain`, slot s >= 1 the shared static slot
-    nchains + s - 1; unused entries (-1) stay."""
-    import numpy as np
-    out = slices.copy()
-    rs = out["ref_slot"]
-    rs[...] = np.where(rs == 0, chain, np.where(rs > 0, nchains + rs.astype(np.int16) - 1, rs)).astype(np.int8)
-    if nchains + int(slices["ref_slot"].max()) - 1 >= 32:
-        raise ValueError("chain slots exceed the 32 DPB slots of a batch")
-    return out
-
-
-def chain_exchange(out, slots, bands: Sequence[tuple[int, int]], rank: int, plane_bytes: int, slot_stride: int,
-                   rows_per_mb: int, row_bytes: int, group=None) -> None:
-    """Exchange of one plane in chain mode: `out` holds the K decoded planes of this rank
-    ([K][plane_bytes], only this rank's band rows valid); `slots` the K chains' DPB slot
-    planes ([K][slot_stride]).  Every rank's band of all K pictures travels in ONE
-    all-gather (bands padded to the widest); each rank then lands every band in every
-    chain's slot.  World 1: a local copy."""
+def min_over_ranks(value: float, device=None) -> float:
+    """The smallest value over the ranks (a verification flag: 1.0 on a rank that passed)."""
     import torch
     import torch.distributed as dist
-    world = len(bands)
-    K = out.numel() // plane_bytes
-    rb = rows_per_mb * row_bytes
-    src = out.reshape(-1)[:K * plane_bytes].view(K, plane_bytes)
-    dst = slots.reshape(-1)[:K * slot_stride].view(K, slot_stride)
-    if world == 1 or not (dist.is_available() and dist.is_initialized()):
-        dst[:, :plane_bytes].copy_(src)
-        return
-    wide = max(b1 - b0 for b0, b1 in bands) * rb
-    a0, a1 = bands[rank][0] * rb, bands[rank][1] * rb
-    send = torch.zeros((K, wide), dtype=out.dtype, device=out.device)
-    if a1 > a0:
-        send[:, :a1 - a0].copy_(src[:, a0:a1])
-    recv = torch.empty((world, K, wide), dtype=out.dtype, device=out.device)
-    dist.all_gather_into_tensor(recv.view(-1), send.view(-1), group=group)
-    for r, (b0, b1) in enumerate(bands):
-        if b1 > b0:
-            dst[:, b0 * rb:b1 * rb].copy_(recv[r, :, :(b1 - b0) * rb])
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return value
+    t = torch.tensor([value], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return float(t.item())
+
+
+# ------------------------------------------------------ chain mode over per-picture DPBs
+# bench.py's chain mode (DESIGN.md section 6, round 4): every picture of a batch carries its own
+# DPB table (h264r_batch.ref_planes_stride), so one launch decodes the next picture of any
+# number of chains; the decoded planes of step t ARE the chains' references of step t+1 (two
+# output sets per group, alternating), and the exchange only has to bring in the rows of the
+# other ranks' bands that this rank's motion compensation can reach.
+
+ROW_BYTES_PER_MB_COL = (256, 64, 64)       # bytes of one MB row per MB column: Y, Cb, Cr
+
+
+def halo_mb_rows(max_abs_mvy_qpel: int) -> int:
+    """MB rows of a reference picture above / below a band that the band's motion
+    compensation can read, for vertical motion vectors |mv_y| <= max_abs_mvy_qpel.
+    Luma (get_block_luma, inter_prediction.cc:158-340): a 4x4 block at rows Y..Y+3 reads
+    rows y-2 .. y+6 with y = Y + floor(mv_y / 4): ceil(m / 4) + 2 rows above the band,
+    floor(m / 4) + 3 below.  Chroma (get_block_chroma :342-406, 4:2:0): rows yc .. yc+2 with
+    yc = Yc + floor(mv_y / 8): at most ceil(m / 8) + 1 chroma rows = ceil(m / 4) + 2 luma rows.
+    Rows past the picture edge are clamped (:185-186), i.e. read inside the picture."""
+    m = max(0, int(max_abs_mvy_qpel))
+    return -(-((m + 3) // 4 + 3) // 16)
+
+
+def halo_plan(bands, rank: int, halo: int):
+    """Rows this rank receives from / sends to each other rank in halo mode:
+    (need {peer: (row0, row1)}, give {peer: (row0, row1)}), MB rows, empty ranges left out."""
+    b0, b1 = bands[rank]
+    need, give = {}, {}
+    if b1 <= b0:
+        return need, give
+    for r, (r0, r1) in enumerate(bands):
+        if r == rank or r1 <= r0:
+            continue
+        n0, n1 = max(b0 - halo, r0), min(b1 + halo, r1)
+        if n1 > n0:
+            need[r] = (n0, n1)
+        g0, g1 = max(r0 - halo, b0), min(r1 + halo, b1)
+        if g1 > g0:
+            give[r] = (g0, g1)
+    return need, give
+
+
+class BandExchange:
+    """The exchange step of chain mode for one group of `nk` pictures decoded as slice bands:
+    after rank `rank` has decoded MB rows bands[rank] of every picture into a set of output
+    planes (Y, Cb, Cr: flat tensors holding [nk][plane] + slack), bring in the rows of the
+    other bands it will read as references of the next step:
+
+    * mode "halo": the rows within `halo` MB rows of its band (halo_mb_rows), one send and
+      one receive per neighbouring rank -- point-to-point over xGMI (batch_isend_irecv),
+      every plane of all nk pictures packed into one buffer per peer;
+    * mode "allgather": every other band whole, one all-gather of all nk pictures' bands
+      (padded to the widest band).
+
+    With gloo (CPU rehearsal) device tensors are staged through host memory."""
+
+    def __init__(self, bands, rank: int, width_mbs: int, height_mbs: int, nk: int, mode: str, halo: int,
+                 device, group=None):
+        import torch
+        self.bands, self.rank, self.nk, self.mode, self.group = list(bands), rank, nk, mode, group
+        self.W, self.H = width_mbs, height_mbs
+        self.rb = [c * width_mbs for c in ROW_BYTES_PER_MB_COL]           # bytes per MB row, per plane
+        self.mbrow = sum(self.rb)
+        self.psz = [r * height_mbs for r in self.rb]                      # plane bytes
+        self.world = len(self.bands)
+        if mode not in ("halo", "allgather"):
+            raise ValueError(mode)
+        if mode == "halo":
+            self.need, self.give = halo_plan(self.bands, rank, halo)
+        else:
+            self.need = {r: b for r, b in enumerate(self.bands) if r != rank and b[1] > b[0]}
+            self.give = {r: self.bands[rank] for r in range(self.world) if r != rank}
+        self.wide = max(b1 - b0 for b0, b1 in self.bands)
+        self.device = device
+
+        def buf(rows):
+            return torch.empty(nk * rows * self.mbrow, dtype=torch.uint8, device=device)
+        if mode == "halo":
+            self.sbuf = {r: buf(g1 - g0) for r, (g0, g1) in self.give.items()}
+            self.rbuf = {r: buf(n1 - n0) for r, (n0, n1) in self.need.items()}
+        else:
+            self.sbuf = {0: buf(self.wide)}
+            self.rbuf = {0: torch.empty(self.world * nk * self.wide * self.mbrow, dtype=torch.uint8, device=device)}
+
+    def bytes_in(self) -> int:
+        """Bytes this rank receives per exchange (the padding of the all-gather included)."""
+        return sum(t.numel() for t in self.rbuf.values()) - (self.sbuf[0].numel() if self.mode == "allgather" else 0)
+
+    def _views(self, planes):
+        return [planes[k].reshape(-1)[: self.nk * self.psz[k]].view(self.nk, self.psz[k]) for k in range(3)]
+
+    def _pack(self, views, b, rows, r0, r1):
+        """Rows [r0, r1) of every picture into buffer b ([nk][rows * mbrow], Y then Cb then Cr)."""
+        bv = b.view(self.nk, rows * self.mbrow)
+        o = 0
+        for k in range(3):
+            n = (r1 - r0) * self.rb[k]
+            bv[:, o:o + n].copy_(views[k][:, r0 * self.rb[k]:r1 * self.rb[k]])
+            o += rows * self.rb[k]
+
+    def _unpack(self, views, b, rows, r0, r1):
+        bv = b.view(self.nk, rows * self.mbrow)
+        o = 0
+        for k in range(3):
+            n = (r1 - r0) * self.rb[k]
+            views[k][:, r0 * self.rb[k]:r1 * self.rb[k]].copy_(bv[:, o:o + n])
+            o += rows * self.rb[k]
+
+    def run(self, planes) -> None:
+        import torch.distributed as dist
+        if self.world == 1 or not (dist.is_available() and dist.is_initialized()):
+            return
+        views = self._views(planes)
+        gloo = dist.get_backend(self.group) == "gloo" and self.device != "cpu" and str(self.device) != "cpu"
+        if self.mode == "allgather":
+            b0, b1 = self.bands[self.rank]
+            self._pack(views, self.sbuf[0], self.wide, b0, b1)
+            send, recv = self.sbuf[0], self.rbuf[0]
+            if gloo:
+                hs, hr = send.cpu(), recv.cpu()
+                dist.all_gather_into_tensor(hr, hs, group=self.group)
+                recv.copy_(hr)
+            else:
+                dist.all_gather_into_tensor(recv, send, group=self.group)
+            per = self.nk * self.wide * self.mbrow
+            for r, (n0, n1) in self.need.items():
+                self._unpack(views, recv[r * per:(r + 1) * per], self.wide, n0, n1)
+            return
+        for r, (g0, g1) in self.give.items():
+            self._pack(views, self.sbuf[r], g1 - g0, g0, g1)
+        if gloo:
+            hs = {r: t.cpu() for r, t in self.sbuf.items()}
+            hr = {r: t.cpu() for r, t in self.rbuf.items()}
+            ops = [dist.P2POp(dist.isend, hs[r], r, self.group) for r in sorted(hs)] + \
+                  [dist.P2POp(dist.irecv, hr[r], r, self.group) for r in sorted(hr)]
+        else:
+            ops = [dist.P2POp(dist.isend, self.sbuf[r], r, self.group) for r in sorted(self.sbuf)] + \
+                  [dist.P2POp(dist.irecv, self.rbuf[r], r, self.group) for r in sorted(self.rbuf)]
+        if ops:
+            for q in dist.batch_isend_irecv(ops):
+                q.wait()
+        for r, (n0, n1) in self.need.items():
+            if gloo:
+                self.rbuf[r].copy_(hr[r])
+            self._unpack(views, self.rbuf[r], n1 - n0, n0, n1)

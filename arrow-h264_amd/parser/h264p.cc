@@ -11,6 +11,7 @@
 #include "h264p.h"
 
 #include <algorithm>
+#include <bitset>
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
@@ -110,6 +111,20 @@ struct Bits {
     {
         const uint32_t k = ue();
         return (k & 1) ? (int32_t)((k + 1) / 2) : -(int32_t)(k / 2);
+    }
+    // ue(v) / se(v) of a syntax element with a range: out of it the stream is malformed (the
+    // value never reaches an int field, where 2^31 and more would turn negative)
+    int ue_max(uint32_t max, const char* what)
+    {
+        const uint32_t v = ue();
+        require(v <= max, what);
+        return (int)v;
+    }
+    int se_in(int lo, int hi, const char* what)
+    {
+        const int32_t v = se();
+        require(v >= lo && v <= hi, what);
+        return v;
     }
     bool aligned() const { return (pos & 7) == 0; }
     bool more_rbsp_data() const { return pos < stop; }
@@ -399,67 +414,71 @@ struct Pps {
     ScalingLists sc;
 };
 
-// seq_parameter_set_rbsp (7.3.2.1.1; interpret_rbsp.cc)
-void parse_sps(Bits& b, Sps* sets)
+// seq_parameter_set_rbsp (7.3.2.1.1; interpret_rbsp.cc): the set and its id
+int parse_sps(Bits& b, Sps& s)
 {
-    Sps s;
+    s = Sps();
     s.profile = b.u(8);
     b.u(16);                                  // constraint flags, level_idc
-    const uint32_t id = b.ue();
-    require(id < 32, "SPS: seq_parameter_set_id");
+    const int id = b.ue_max(31, "SPS: seq_parameter_set_id");
     if (s.profile == 100 || s.profile == 110 || s.profile == 122 || s.profile == 244 || s.profile == 44 ||
         s.profile == 83 || s.profile == 86 || s.profile == 118 || s.profile == 128 || s.profile == 138 ||
         s.profile == 139 || s.profile == 134 || s.profile == 135) {
-        s.chroma_format_idc = b.ue();
+        s.chroma_format_idc = b.ue_max(3, "SPS: chroma_format_idc");
         if (s.chroma_format_idc == 3) b.u(1);                    // separate_colour_plane_flag
-        s.bit_depth_y = 8 + b.ue();
-        s.bit_depth_c = 8 + b.ue();
+        s.bit_depth_y = 8 + b.ue_max(6, "SPS: bit_depth_luma_minus8");
+        s.bit_depth_c = 8 + b.ue_max(6, "SPS: bit_depth_chroma_minus8");
         s.bypass = b.u(1);
         s.sc.matrix_present = b.u(1);
         if (s.sc.matrix_present) scaling_matrix(b, s.sc, s.chroma_format_idc != 3 ? 8 : 12);
     }
-    s.log2_max_frame_num = b.ue() + 4;
-    s.poc_type = b.ue();
-    if (s.poc_type == 0) s.log2_max_poc_lsb = b.ue() + 4;
+    // the reference asserts log2_max_frame_num_minus4 <= 12 (interpret_rbsp.cc); the same range
+    // bounds log2_max_pic_order_cnt_lsb_minus4 (7.4.2.1.1)
+    s.log2_max_frame_num = b.ue_max(12, "SPS: log2_max_frame_num_minus4") + 4;
+    s.poc_type = b.ue_max(2, "SPS: pic_order_cnt_type");
+    if (s.poc_type == 0) s.log2_max_poc_lsb = b.ue_max(12, "SPS: log2_max_pic_order_cnt_lsb_minus4") + 4;
     else if (s.poc_type == 1) {
         b.u(1); b.se(); b.se();
-        const uint32_t n = b.ue();
-        for (uint32_t i = 0; i < n; ++i) b.se();
+        const int n = b.ue_max(255, "SPS: num_ref_frames_in_pic_order_cnt_cycle");
+        for (int i = 0; i < n; ++i) b.se();
     }
-    s.max_num_ref_frames = b.ue();
+    s.max_num_ref_frames = b.ue_max(16, "SPS: max_num_ref_frames");
     s.gaps = b.u(1);
-    s.W = b.ue() + 1;
-    const int map_h = b.ue() + 1;
+    // picture sizes beyond the library's (1024 x 1024 MBs, include/h264r.h) are refused here,
+    // before any buffer is sized from them
+    s.W = b.ue_max(1023, "SPS: pic_width_in_mbs_minus1") + 1;
+    const int map_h = b.ue_max(1023, "SPS: pic_height_in_map_units_minus1") + 1;
     s.frame_mbs_only = b.u(1);
     if (!s.frame_mbs_only) s.mbaff = b.u(1);
     s.H = map_h * (2 - s.frame_mbs_only);
     s.direct_8x8_inference = b.u(1);
     if (b.u(1))
-        for (int k = 0; k < 4; ++k) s.crop[k] = b.ue();
+        for (int k = 0; k < 4; ++k) s.crop[k] = b.ue_max(8 * 1024, "SPS: frame_crop offset");
+    require(2 * (s.crop[0] + s.crop[1]) < 16 * s.W && 2 * (s.crop[2] + s.crop[3]) < 16 * s.H, "SPS: cropping window empty");
     // vui_parameters: nothing the path reads
     s.valid = true;
-    sets[id] = s;
+    return id;
 }
 
-// pic_parameter_set_rbsp (7.3.2.2)
-void parse_pps(Bits& b, Pps* sets, const Sps* spss)
+// pic_parameter_set_rbsp (7.3.2.2): the set and its id
+int parse_pps(Bits& b, Pps& p, const Sps* spss)
 {
-    Pps p;
-    const uint32_t id = b.ue();
-    require(id < 256, "PPS: pic_parameter_set_id");
-    p.sps_id = b.ue();
-    require(p.sps_id < 32 && spss[p.sps_id].valid, "PPS: seq_parameter_set_id of no SPS");
+    p = Pps();
+    const int id = b.ue_max(255, "PPS: pic_parameter_set_id");
+    p.sps_id = b.ue_max(31, "PPS: seq_parameter_set_id");
+    require(spss[p.sps_id].valid, "PPS: seq_parameter_set_id of no SPS");
     p.cabac = b.u(1);
     p.bottom_field_poc = b.u(1);
-    p.num_slice_groups = b.ue() + 1;
+    p.num_slice_groups = b.ue_max(7, "PPS: num_slice_groups_minus1") + 1;
     unsupported(p.num_slice_groups > 1, "slice groups (FMO)");
-    p.nref_default[0] = b.ue() + 1;
-    p.nref_default[1] = b.ue() + 1;
+    p.nref_default[0] = b.ue_max(31, "PPS: num_ref_idx_l0_default_active_minus1") + 1;
+    p.nref_default[1] = b.ue_max(31, "PPS: num_ref_idx_l1_default_active_minus1") + 1;
     p.weighted_pred = b.u(1);
     p.weighted_bipred_idc = b.u(2);
-    p.init_qp = 26 + b.se();
-    p.init_qs = 26 + b.se();
-    p.cqp_offset[0] = b.se();
+    require(p.weighted_bipred_idc <= 2, "PPS: weighted_bipred_idc");
+    p.init_qp = 26 + b.se_in(-26, 25, "PPS: pic_init_qp_minus26");
+    p.init_qs = 26 + b.se_in(-26, 25, "PPS: pic_init_qs_minus26");
+    p.cqp_offset[0] = b.se_in(-12, 12, "PPS: chroma_qp_index_offset");
     p.deblocking_control = b.u(1);
     p.cip = b.u(1);
     p.redundant_pic_cnt = b.u(1);
@@ -469,10 +488,10 @@ void parse_pps(Bits& b, Pps* sets, const Sps* spss)
         p.sc.matrix_present = b.u(1);
         if (p.sc.matrix_present)
             scaling_matrix(b, p.sc, 6 + (spss[p.sps_id].chroma_format_idc != 3 ? 2 : 6) * p.transform_8x8);
-        p.cqp_offset[1] = b.se();
+        p.cqp_offset[1] = b.se_in(-12, 12, "PPS: second_chroma_qp_index_offset");
     }
     p.valid = true;
-    sets[id] = p;
+    return id;
 }
 
 // Transform::init fall-back rules A / B (transform.cc:173-257), as restated by the shim
@@ -549,6 +568,7 @@ struct Picture {
 
 struct Output {
     int period, poc;
+    int W, H, crop[4];              // its SPS's, at the time it was decoded (a later SPS may differ)
     std::vector<uint8_t> y, u, v;
 };
 
@@ -680,6 +700,8 @@ public:
     // state the slice layer reads
     Sps sps_[32];
     Pps pps_[256];
+    std::vector<uint8_t> sps_raw_[32], pps_raw_[256];   // RBSP bytes of each stored set (repeats are no-ops)
+    std::bitset<256> pps_used_;                       // PPS ids the open picture's slices refer to
     std::vector<MbState> mbs_;
     std::vector<StagedMb> staged_;
     std::vector<uint8_t> seen_;
@@ -789,16 +811,32 @@ void Decoder::nal(const uint8_t* p, size_t n)
         return;
     case 2: case 3: case 4:
         fail(H264R_EUNSUPPORTED, "data partitioning (NAL types 2-4)");
-    case 7:
+    case 7: {
         run_slices();                                  // the pending slices refer to the current sets
         b.load(p + 1, n - 1);
-        parse_sps(b, sps_);
+        Sps s;
+        const int id = parse_sps(b, s);
+        std::vector<uint8_t> raw(p + 1, p + n);
+        if (sps_[id].valid && raw == sps_raw_[id]) return;          // a repeat of the stored set
+        // a different set under the active id ends the open picture first, as the reference
+        // calls exit_picture before activating it (slice_header.cc:392-423)
+        if (in_picture_ && psps_ == &sps_[id]) finish_picture();
+        sps_[id] = s;
+        sps_raw_[id] = std::move(raw);
         return;
-    case 8:
+    }
+    case 8: {
         run_slices();
         b.load(p + 1, n - 1);
-        parse_pps(b, pps_, sps_);
+        Pps q;
+        const int id = parse_pps(b, q, sps_);
+        std::vector<uint8_t> raw(p + 1, p + n);
+        if (pps_[id].valid && raw == pps_raw_[id]) return;
+        if (in_picture_ && pps_used_[id]) finish_picture();
+        pps_[id] = q;
+        pps_raw_[id] = std::move(raw);
         return;
+    }
     case 11:                                      // end of stream
         if (in_picture_) finish_picture();
         return;
@@ -810,10 +848,10 @@ void Decoder::nal(const uint8_t* p, size_t n)
 // slice_header (7.3.3; interpret_rbsp.cc:625-777)
 void Decoder::parse_slice_header(Bits& b, SliceHeader& h)
 {
-    h.first_mb = b.ue();
-    h.slice_type = b.ue() % 5;
-    h.pps_id = b.ue();
-    require(h.pps_id < 256 && pps_[h.pps_id].valid, "slice: pic_parameter_set_id of no PPS");
+    h.first_mb = b.ue_max(1024 * 1024 - 1, "slice: first_mb_in_slice");
+    h.slice_type = b.ue_max(9, "slice: slice_type") % 5;
+    h.pps_id = b.ue_max(255, "slice: pic_parameter_set_id");
+    require(pps_[h.pps_id].valid, "slice: pic_parameter_set_id of no PPS");
     const Pps& pps = pps_[h.pps_id];
     const Sps& sps = sps_[pps.sps_id];
     unsupported(sps.chroma_format_idc != 1 || sps.bit_depth_y != 8 || sps.bit_depth_c != 8,
@@ -822,22 +860,24 @@ void Decoder::parse_slice_header(Bits& b, SliceHeader& h)
     unsupported(sps.poc_type == 1, "pic_order_cnt_type 1");
     unsupported(h.slice_type == H264R_SLICE_SI, "SI slices");
     h.frame_num = b.u(sps.log2_max_frame_num);
-    if (h.idr) h.idr_pic_id = b.ue();
+    if (h.idr) h.idr_pic_id = b.ue_max(65535, "slice: idr_pic_id");
     if (sps.poc_type == 0) {
         h.poc_lsb = b.u(sps.log2_max_poc_lsb);
         if (pps.bottom_field_poc) h.delta_poc_bottom = b.se();
     }
-    if (pps.redundant_pic_cnt) unsupported(b.ue() != 0, "redundant pictures");
+    if (pps.redundant_pic_cnt) unsupported(b.ue_max(127, "slice: redundant_pic_cnt") != 0, "redundant pictures");
     const bool P = h.slice_type == H264R_SLICE_P || h.slice_type == H264R_SLICE_SP, B = h.slice_type == H264R_SLICE_B;
     if (B) h.direct_spatial = b.u(1);
     h.nref[0] = pps.nref_default[0];
     h.nref[1] = pps.nref_default[1];
     if (P || B) {
         if (b.u(1)) {
-            h.nref[0] = b.ue() + 1;
-            if (B) h.nref[1] = b.ue() + 1;
+            h.nref[0] = b.ue_max(31, "slice: num_ref_idx_l0_active_minus1") + 1;
+            if (B) h.nref[1] = b.ue_max(31, "slice: num_ref_idx_l1_active_minus1") + 1;
         }
-        require(h.nref[0] <= 32 && h.nref[1] <= 32, "slice: num_ref_idx_active");
+        // frames: at most 16 per list (the reference asserts it, interpret_rbsp.cc:710;
+        // H264R_MAX_REFS): a larger count would be clamped downstream, not decoded
+        require(h.nref[0] <= 16 && (!B || h.nref[1] <= 16), "slice: num_ref_idx_active above 16 (frames)");
     }
     if (!B) h.nref[1] = 0;
     if (!P && !B) h.nref[0] = 0;
@@ -846,26 +886,34 @@ void Decoder::parse_slice_header(Bits& b, SliceHeader& h)
         h.mod_flag[l] = b.u(1);
         if (h.mod_flag[l])
             for (;;) {
-                const int idc = b.ue();
+                const int idc = b.ue_max(3, "slice: modification_of_pic_nums_idc");
                 if (idc == 3) break;
-                require(idc < 3, "slice: modification_of_pic_nums_idc");
-                h.mods[l].push_back({idc, (int)b.ue()});
+                // at most num_ref_idx_active entries (the reference asserts it,
+                // interpret_rbsp.cc:803): each one writes a list entry
+                require((int)h.mods[l].size() < h.nref[l], "slice: more list modifications than active references");
+                h.mods[l].push_back({idc, b.ue_max(1u << 17, "slice: abs_diff_pic_num_minus1 / long_term_pic_num")});
             }
     }
     // pred_weight_table (7.3.3.2; interpret_rbsp.cc:832-905)
     if ((pps.weighted_pred && P) || (pps.weighted_bipred_idc == 1 && B)) {
-        h.luma_log2_wd = b.ue();
-        h.chroma_log2_wd = b.ue();
+        h.luma_log2_wd = b.ue_max(7, "slice: luma_log2_weight_denom");
+        h.chroma_log2_wd = b.ue_max(7, "slice: chroma_log2_weight_denom");
         for (int l = 0; l < (B ? 2 : 1); ++l)
             for (int i = 0; i < h.nref[l]; ++i) {
                 h.weight[l][i][0] = 1 << h.luma_log2_wd;
                 h.offset[l][i][0] = 0;
-                if (b.u(1)) { h.weight[l][i][0] = b.se(); h.offset[l][i][0] = b.se(); }
+                if (b.u(1)) {
+                    h.weight[l][i][0] = b.se_in(-128, 127, "slice: luma_weight");
+                    h.offset[l][i][0] = b.se_in(-128, 127, "slice: luma_offset");
+                }
                 const bool cf = b.u(1);
                 for (int j = 1; j < 3; ++j) {
                     h.weight[l][i][j] = 1 << h.chroma_log2_wd;
                     h.offset[l][i][j] = 0;
-                    if (cf) { h.weight[l][i][j] = b.se(); h.offset[l][i][j] = b.se(); }
+                    if (cf) {
+                        h.weight[l][i][j] = b.se_in(-128, 127, "slice: chroma_weight");
+                        h.offset[l][i][j] = b.se_in(-128, 127, "slice: chroma_offset");
+                    }
                 }
             }
     }
@@ -878,34 +926,33 @@ void Decoder::parse_slice_header(Bits& b, SliceHeader& h)
             h.adaptive = b.u(1);
             if (h.adaptive)
                 for (;;) {
-                    Mmco m{(int)b.ue(), 0, 0};
+                    Mmco m{b.ue_max(6, "slice: memory_management_control_operation"), 0, 0};
                     if (m.op == 0) break;
-                    require(m.op <= 6, "slice: memory_management_control_operation");
                     unsupported(m.op == 5, "MMCO 5");
-                    if (m.op == 1 || m.op == 3) m.a = b.ue();          // difference_of_pic_nums_minus1
-                    if (m.op == 2) m.a = b.ue();                       // long_term_pic_num
-                    if (m.op == 3 || m.op == 6) m.b = b.ue();          // long_term_frame_idx
-                    if (m.op == 4) m.a = b.ue();                       // max_long_term_frame_idx_plus1
+                    require(h.mmco.size() < 64, "slice: memory_management_control_operation count");
+                    if (m.op == 1 || m.op == 3) m.a = b.ue_max(1u << 17, "slice: difference_of_pic_nums_minus1");
+                    if (m.op == 2) m.a = b.ue_max(1u << 17, "slice: long_term_pic_num");
+                    if (m.op == 3 || m.op == 6) m.b = b.ue_max(15, "slice: long_term_frame_idx");
+                    if (m.op == 4) m.a = b.ue_max(16, "slice: max_long_term_frame_idx_plus1");
                     h.mmco.push_back(m);
                 }
         }
     }
     if (pps.cabac && h.slice_type != H264R_SLICE_I) {
-        h.cabac_init_idc = b.ue();
-        require(h.cabac_init_idc <= 2, "slice: cabac_init_idc");
+        h.cabac_init_idc = b.ue_max(2, "slice: cabac_init_idc");
     }
-    h.qp = pps.init_qp + b.se();
+    h.qp = pps.init_qp + b.se_in(-51, 51, "slice: slice_qp_delta");
     if (h.slice_type == H264R_SLICE_SP) {
         h.sp_switch = b.u(1);
-        h.qs = pps.init_qs + b.se();
+        h.qs = pps.init_qs + b.se_in(-51, 51, "slice: slice_qs_delta");
     }
     require(h.qp >= 0 && h.qp <= 51 && h.qs >= 0 && h.qs <= 51, "slice: QP out of range");
     if (pps.deblocking_control) {
-        h.deblock_idc = b.ue();
-        require(h.deblock_idc <= 2, "slice: disable_deblocking_filter_idc");
+        h.deblock_idc = b.ue_max(2, "slice: disable_deblocking_filter_idc");
         if (h.deblock_idc != 1) {
-            h.offset_a = b.se() * 2;
-            h.offset_b = b.se() * 2;
+            // the reference asserts -6..6 (interpret_rbsp.cc:760-765)
+            h.offset_a = b.se_in(-6, 6, "slice: slice_alpha_c0_offset_div2") * 2;
+            h.offset_b = b.se_in(-6, 6, "slice: slice_beta_offset_div2") * 2;
         }
     }
 }
@@ -930,6 +977,7 @@ void Decoder::slice(Bits& b, int nal_ref_idc, int nal_type)
     const Pps& pps = pps_[h.pps_id];
     const Sps& sps = sps_[pps.sps_id];
     require(&sps == psps_, "slice: SPS changes inside a picture");
+    pps_used_[h.pps_id] = true;
     unsupported((int)slice_tab_.size() >= H264R_MAX_SLICES, "slices per picture");
     init_lists(h);
     slice_tab_.push_back(slice_record(h));
@@ -1011,11 +1059,15 @@ void Decoder::begin_picture(const SliceHeader& h)
 {
     const Pps& pps = pps_[h.pps_id];
     const Sps& sps = sps_[pps.sps_id];
+    const int W = sps.W, H = sps.H;
+    // the picture still on the GPU leaves the context (at its own size, Output::W/H) before the
+    // context is replaced for a larger picture size
+    if (!ctx_ || W > ctx_w_ || H > ctx_h_) collect();
     psps_ = &sps;
     ppps_ = &pps;
     first_ = h;
     in_picture_ = true;
-    const int W = sps.W, H = sps.H;
+    pps_used_.reset();
     if (!ctx_ || W > ctx_w_ || H > ctx_h_) {
         if (ctx_) h264r_destroy(ctx_);
         ctx_ = nullptr;
@@ -1247,7 +1299,8 @@ void Decoder::finish_picture()
         for (auto& q : dpb_)
             if (q->slot == keep) q->slot = -1;
     }
-    pending_.push_back(Output{period_, cur_->poc, {}, {}, {}});
+    pending_.push_back(Output{period_, cur_->poc, W, H, {psps_->crop[0], psps_->crop[1], psps_->crop[2], psps_->crop[3]},
+                              {}, {}, {}});
     if (sync_) {
         Output& o = pending_.back();
         o.y.resize((size_t)W * H * 256);
@@ -1343,7 +1396,7 @@ void Decoder::collect()
     if (inflight_ < 0) return;
     Output& o = pending_[inflight_];
     inflight_ = -1;
-    const size_t n = (size_t)psps_->W * psps_->H;
+    const size_t n = (size_t)o.W * o.H;
     o.y.resize(n * 256);
     o.u.resize(n * 64);
     o.v.resize(n * 64);
@@ -1355,15 +1408,14 @@ void Decoder::flush_output()
     collect();
     std::stable_sort(pending_.begin(), pending_.end(),
                      [](const Output& a, const Output& b) { return a.period != b.period ? a.period < b.period : a.poc < b.poc; });
-    const Sps& s = psps_ ? *psps_ : sps_[0];
     for (Output& o : pending_) {
         if (stop_) break;
         h264p_frame f;
         f.y = o.y.data(); f.u = o.u.data(); f.v = o.v.data();
-        f.width = s.W * 16;
-        f.height = s.H * 16;
-        f.crop_left = 2 * s.crop[0]; f.crop_right = 2 * s.crop[1];
-        f.crop_top = 2 * s.crop[2]; f.crop_bottom = 2 * s.crop[3];
+        f.width = o.W * 16;
+        f.height = o.H * 16;
+        f.crop_left = 2 * o.crop[0]; f.crop_right = 2 * o.crop[1];
+        f.crop_top = 2 * o.crop[2]; f.crop_bottom = 2 * o.crop[3];
         f.poc = o.poc;
         f.period = o.period;
         if (out_) stop_ = out_(user_, &f);
@@ -1464,13 +1516,13 @@ void SliceCtx::macroblock()
             skip = cab->dec(CTX_SKIP_CONTEXTS + inc);
             if (skip) last_dquant = 0;
         } else {
-            if (skip_run == -1) skip_run = b.ue();
+            if (skip_run == -1) skip_run = b.ue_max(W * H, "mb_skip_run");
             skip = skip_run > 0;
             --skip_run;
         }
     }
     m.skip = skip;
-    mb_type = skip ? 0 : (cab ? cabac_mb_type(I, B) : (int)(uint8_t)b.ue()) + ((!I && !B) ? 1 : 0);
+    mb_type = skip ? 0 : (cab ? cabac_mb_type(I, B) : b.ue_max(48, "mb_type")) + ((!I && !B) ? 1 : 0);
     // mb_type tables (interpret_mb.cc:318-406)
     int itype = -1;
     if (I) itype = mb_type;
@@ -1584,8 +1636,7 @@ void SliceCtx::macroblock()
             cbp = cabac_cbp();
             if (!cbp) last_dquant = 0;
         } else {
-            const uint32_t code = b.ue();
-            require(code < 48, "coded_block_pattern");
+            const int code = b.ue_max(47, "coded_block_pattern");
             cbp = m.intra ? CBP_ME_INTRA[code] : CBP_ME_INTER[code];
         }
         cbpl = cbp % 16;
@@ -1604,7 +1655,7 @@ void SliceCtx::macroblock()
             dq = (int8_t)((v & 1) ? (v + 1) >> 1 : -((v + 1) >> 1));
             last_dquant = dq;
         } else
-            dq = (int8_t)b.se();
+            dq = b.se_in(-26, 25, "mb_qp_delta");
         require(dq >= -26 && dq <= 25, "mb_qp_delta");
         qp = (qp + dq + 52) % 52;
     }
@@ -1675,7 +1726,7 @@ void SliceCtx::intra_pred_modes()
         const int inc[2] = {inc0, 3};
         chroma_mode = (uint8_t)cab->tu(CTX_CIPR_CONTEXTS, inc, 2, 3);
     } else
-        chroma_mode = (uint8_t)b.ue();
+        chroma_mode = (uint8_t)b.ue_max(3, "intra_chroma_pred_mode");
     require(chroma_mode <= 3, "intra_chroma_pred_mode");
 }
 
@@ -1941,8 +1992,8 @@ void SliceCtx::inter_pred()
                     const bool present = B || !allrefzero || m.mb_type != H264R_P_8x8;
                     const int n = sh.nref[l];
                     int r = 0;
-                    if (present && n > 1) r = cab ? cabac_ref_idx(l, x8, y8) : n == 2 ? 1 - (int)b.u(1) : (int)b.ue();
-                    require(r < n, "ref_idx out of range");
+                    if (present && n > 1) r = cab ? cabac_ref_idx(l, x8, y8) : n == 2 ? 1 - (int)b.u(1) : b.ue_max(31, "ref_idx");
+                    require(r >= 0 && r < n, "ref_idx out of range");
                     for (int y4 = 0; y4 < sv0; ++y4)
                         for (int x4 = 0; x4 < sh0; ++x4) M.ref_idx[l][M.at(mbx * 4 + x8 + x4, mby * 4 + y8 + y4)] = (int8_t)r;
                 }
@@ -2021,6 +2072,7 @@ int SliceCtx::block_cavlc(int pl, bool chroma, bool ac, int blk, int start, int 
         t1 = v & 3;
     }
     require(tc <= max_coeff, "coeff_token: TotalCoeff above the block size");
+    require(t1 <= tc, "coeff_token: TrailingOnes above TotalCoeff");       // the 6-bit FLC (nC >= 8) can say so
     int level[16], run[16];
     if (tc > 0) {
         int suffix = tc > 10 && t1 < 3 ? 1 : 0;

@@ -2,16 +2,21 @@
 """Benchmark: macroblocks/s of post-entropy reconstruction (MC + IDCT + intra +
 deblock) on MI355X, BASELINE.json's metric.
 
-A step = one h264r_decode_batch over a batch of synthetic pictures already
-resident in HBM (SURVEY 8(d) throughput mode: B independent pictures sharing a
-reference set).  Default workload: SURVEY config 3, 1080p (120x68 MBs) IPPP
-Main P pictures, B = 1024 per GPU (about 8 GB of HBM: the order-dependent walks
-need many pictures in flight to fill 256 CUs).
+One GPU (default): throughput mode, the headline.  A step = one h264r_decode_batch over a
+batch of synthetic pictures already resident in HBM (B independent pictures
+sharing a reference set).  Workload: SURVEY config 3, 1080p (120x68 MBs) IPPP Main P
+pictures, B = 1024 per GPU (the order-dependent walks need many pictures in flight).
 
-Multi-GPU (torchrun, one process per GPU): config 3 uses deblocking across the
-whole picture (disable_deblocking_filter_idc 0), which chains every MB of a
-picture (deblock.cc:547-551), so N > 1 runs N independent replicas (one stream
-per GPU, weak scaling, no data-path collective); see DESIGN.md.
+N > 1 GPUs (default): chain mode on config 5 (2160p High B pictures, 8 slices,
+disable_deblocking_filter_idc 2), slice-sharded: K = 32 x N dependent chains advance one
+picture per step, each rank decodes its band of slices of every picture, and the rows of
+the other bands that its next motion compensation can reach come in by point-to-point RCCL
+transfers over xGMI (or --exchange allgather: every band).  Weak scaling; the JSON also
+carries the one-GPU line of the same mode (`same_mode_n1`).  `--gpus N` without a launcher
+starts the N ranks itself (torch.distributed.run as a child process); under
+`torch.distributed.run` one process per GPU reads RANK / LOCAL_RANK / WORLD_SIZE.
+Config 3 (idc 0) chains every MB of a picture through the loop filter
+(deblock.cc:547-551): `--mode throughput --shard replicas` runs N independent replicas.
 
 Prints ONE JSON line on rank 0.
 """
@@ -186,72 +191,85 @@ def latency_chain(dec, L, cfg, refs, stream, n: int, verify: int):
     return (time.perf_counter() - t0) / n * 1e3, n, verified
 
 
-def chain_bench(args, rank: int, world: int, local: int, cs, rehearse: bool) -> dict:
-    """--chain K: K dependent chains per step, slice-sharded over the ranks (DESIGN
-    section 6).  Chain k's picture t predicts from its picture t-1 (DPB slot k): a rank decodes
-    its slice band of the K pictures, then ONE all-gather per plane brings every rank's band
-    of all K pictures into every rank's chain slots before any chain's next picture may
-    start -- one exchange per reference picture, on the dependency path.  The chains are
-    split into two groups whose batches alternate on the decode stream, so the exchange of
-    one group (communication stream) overlaps the decode of the other.  Each group keeps
-    two slot sets (ping-pong: step t reads set t % 2, its exchange fills set (t+1) % 2)."""
+def chain_run(args, rank: int, world: int, local: int, cs, rehearse: bool, nchains: int, cfg_idx: int,
+              exchange: str) -> dict:
+    """Dependent chains, slice-sharded.  `nchains` chains advance
+    one picture per step; chain k's picture t predicts from its own picture t-1, so every decoded
+    picture is a reference the next step needs on every rank that reads it.
+
+    * Every picture of a batch has its own DPB table (h264r_batch.ref_planes_stride): slot 0 =
+      its chain's previous picture, slots 1.. = static references shared by all chains.  The
+      chains are split into two groups, one launch each per step.
+    * A group keeps two output sets; step t decodes into set t % 2 and reads set (t+1) % 2 -- the
+      previous step's output IS the reference, nothing is copied on a rank.
+    * Each rank decodes its slice band (MB rows of whole slices, disable_deblocking_filter_idc 2:
+      deblock.cc:247-253; slices never predict across each other: intra_prediction.cc:145-152),
+      then the exchange brings in the rows of other bands its next motion compensation can reach:
+      `halo` (default) = the rows within halo_mb_rows(max |mv_y|) of its band from the
+      neighbouring ranks, point-to-point (RCCL send/recv over xGMI); `allgather` = every band of
+      every picture (one all-gather per group and step).  The exchange of one group (communication
+      stream) overlaps the decode of the other (decode stream); each is on its chains' dependency
+      path.  The slice walk this parallelises is slice_data.cc:640-650."""
     import torch
     import h264r
     from h264r import batch as B
     from h264r import synth
     from h264r import dist as D
     L = h264r.lib()
-    W, H = CONFIG_SIZE[args.config]
-    cfg = synth.default_cfg(L, args.config, W, H)
+    W, H = CONFIG_SIZE[cfg_idx]
+    cfg = synth.default_cfg(L, cfg_idx, W, H)
     refs = synth.refpics(L, cfg)
     if not refs:
-        raise SystemExit("--chain needs inter pictures (configs 3, 4, 5)")
-    kg = args.chain // 2
+        raise SystemExit("chain mode needs inter pictures (configs 3, 4, 5)")
+    if nchains < 2 or nchains % 2:
+        raise SystemExit("chain mode takes an even number of chains >= 2")
+    nk = nchains // 2
     nmb = W * H
-    base = [synth.picture(L, cfg, i) for i in range(2 * kg)]
-    srow = base[0].mbs["slice"].reshape(H, W)[:, 0]
+    # distinct synthetic pictures: up to 16 per group (chains beyond reuse them; every chain
+    # still decodes its own picture from its own reference every step)
+    nbase = min(nk, 16)
+    base = [[synth.picture(L, cfg, g * 1000 + i) for i in range(nbase)] for g in range(2)]
+    srow = base[0][0].mbs["slice"].reshape(H, W)[:, 0]
     first = [0] + [r for r in range(1, H) if srow[r] != srow[r - 1]]
     bands = D.slice_bands(first, H, world) if world > 1 else [(0, H)]
     band = bands[rank]
     if world > 1 and cfg.deblock_idc == 0:
         raise SystemExit("slice sharding needs disable_deblocking_filter_idc 1/2 (configs 4, 5)")
+    # the halo: every vertical motion vector of every picture (a decoder knows its next
+    # picture's vectors before reconstructing it: the parser runs ahead of the GPU)
+    mvy = max(int(np.abs((p.mv >> 16).astype(np.int16)).max()) for g in base for p in g)
+    halo = D.halo_mb_rows(mvy)
     slack = 64
-    pbytes = (256 * nmb, 64 * nmb, 64 * nmb)
-    rows_per_mb, row_bytes = (16, 8, 8), (16 * W, 8 * W, 8 * W)
+    psz = (256 * nmb, 64 * nmb, 64 * nmb)
     dec = h264r.Decoder(local, W, H)
-    static = []
-    for r in refs[1:]:
-        static.append([torch.from_numpy(np.concatenate([a.reshape(-1), np.zeros(slack, np.uint8)])).to("cuda")
-                       for a in r])
+    static = [[torch.from_numpy(np.concatenate([a.reshape(-1), np.zeros(slack, np.uint8)])).to("cuda") for a in r]
+              for r in refs[1:]]
     groups = []
     for g in range(2):
-        pics = []
-        for k in range(kg):
-            p = base[g * kg + k]
-            p.slices = D.chain_slots(p.slices, k, kg)
-            pics.append(p)
-        # two slot sets per plane: [kg][plane + slack], every chain starting from refs[0]
-        sets = []
-        for _ in range(2):
-            planes = []
-            for k3 in range(3):
-                t = torch.zeros((kg, pbytes[k3] + slack), dtype=torch.uint8, device="cuda")
-                t[:, :pbytes[k3]].copy_(torch.from_numpy(refs[0][k3].reshape(1, -1)).expand(kg, -1))
-                planes.append(t)
-            sets.append(planes)
+        pics = [base[g][k % nbase] for k in range(nk)]
+        # two output sets [nk][plane] + slack; set 1 starts as every chain's first reference
+        sets = [[torch.zeros(nk * psz[k3] + slack, dtype=torch.uint8, device="cuda") for k3 in range(3)]
+                for _ in range(2)]
+        for k3 in range(3):
+            sets[1][k3][: nk * psz[k3]].view(nk, psz[k3]).copy_(
+                torch.from_numpy(refs[0][k3].reshape(1, -1)).expand(nk, -1))
         tabs = []
-        for si in range(2):
-            tab = np.zeros(3 * 32, np.int64)
-            for k in range(kg):
+        for si in range(2):                        # the table of a step that READS set si
+            tab = np.zeros((nk, 3 * 32), np.int64)
+            for k in range(nk):
                 for k3 in range(3):
-                    tab[3 * k + k3] = sets[si][k3][k].data_ptr()
-            for j, planes in enumerate(static):
-                for k3 in range(3):
-                    tab[3 * (kg + j) + k3] = planes[k3].data_ptr()
-            tabs.append(torch.from_numpy(tab).to("cuda"))
-        db = B.to_device(B.pack(pics, h264r.quant_flat()), kg, tabs[0].data_ptr())
-        groups.append(dict(pics=pics, sets=sets, tabs=tabs, db=db, ev_ex=[]))
-    comm = torch.cuda.Stream(device=local)
+                    tab[k, k3] = sets[si][k3].data_ptr() + k * psz[k3]
+                for j, planes in enumerate(static):
+                    for k3 in range(3):
+                        tab[k, 3 * (1 + j) + k3] = planes[k3].data_ptr()
+            tabs.append(torch.from_numpy(tab.reshape(-1)).to("cuda"))
+        db = B.to_device(B.pack(pics, h264r.quant_flat()), nk, tabs[1].data_ptr())
+        db.batch.ref_planes_stride = 3 * 32
+        for t_ in ("out_y", "out_u", "out_v"):          # the sets replace the batch's own outputs
+            del db.tensors[t_]
+        xch = D.BandExchange(bands, rank, W, H, nk, exchange, halo, "cuda") if world > 1 else None
+        groups.append(dict(pics=pics, sets=sets, tabs=tabs, db=db, xch=xch, ev_ex=[]))
+    comm = torch.cuda.Stream(device=local) if world > 1 else None
     stream = cs.cuda_stream
     nstep = [0]
 
@@ -259,40 +277,51 @@ def chain_bench(args, rank: int, world: int, local: int, cs, rehearse: bool) -> 
         t = nstep[0]
         nstep[0] += 1
         for G in groups:
-            if t >= 1:
-                cs.wait_event(G["ev_ex"][t - 1])       # this chain group's previous pictures are in place
-            G["db"].batch.ref_planes = G["tabs"][t % 2].data_ptr()
+            if t >= 1 and comm is not None:
+                cs.wait_event(G["ev_ex"][t - 1])       # the references of this step are complete
+            wr, rd_ = G["sets"][t % 2], t % 2 ^ 1
+            b = G["db"].batch
+            b.out_y, b.out_u, b.out_v = (x.data_ptr() for x in wr)
+            b.ref_planes = G["tabs"][rd_].data_ptr()
             if band[1] > band[0]:
-                dec.decode_batch(G["db"].batch, stream, rows=None if band == (0, H) else band)
+                dec.decode_batch(b, stream, rows=None if band == (0, H) else band)
+            if comm is None:
+                continue
             ev = torch.cuda.Event()
             ev.record(cs)
             comm.wait_event(ev)
             with torch.cuda.stream(comm):
-                outs = (G["db"].tensors["out_y"], G["db"].tensors["out_u"], G["db"].tensors["out_v"])
-                for k3 in range(3):
-                    D.chain_exchange(outs[k3], G["sets"][(t + 1) % 2][k3], bands, rank, pbytes[k3],
-                                     pbytes[k3] + slack, rows_per_mb[k3], row_bytes[k3])
+                G["xch"].run(wr)
                 ex = torch.cuda.Event()
                 ex.record(comm)
             G["ev_ex"].append(ex)
 
     verified = None
     if not args.no_verify:
+        # two steps, then chain 0 of group 0 against the oracle's chain: its second picture read
+        # the first one through the exchange, so the band (and the halo rows received) must equal
+        # the oracle's whole-picture decode
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import _oracle as O
-        verified = True
+        step()
+        step()
+        torch.cuda.synchronize()
+        dec.check()
         G = groups[0]
-        prev = refs[0]
-        for t in range(2):                             # chain 0 of group 0, two dependent pictures
-            step()
-            torch.cuda.synchronize()
-            dec.check()
-            if rank == 0:
-                slot_refs = [prev] + [refs[0]] * (kg - 1) + list(refs[1:])
-                want = O.decode(G["pics"][0], slot_refs)
-                got = [G["sets"][(t + 1) % 2][k3][0, :pbytes[k3]].cpu().numpy() for k3 in range(3)]
-                verified &= all(np.array_equal(got[k3], want[k3].reshape(-1)) for k3 in range(3))
-                prev = want
+        want0 = O.decode(G["pics"][0], refs)
+        want1 = O.decode(G["pics"][0], [want0] + list(refs[1:]))
+        rows = (16, 8, 8)
+        ok = True
+        for t, want, lo, hi in ((0, want0, max(band[0] - halo, 0), min(band[1] + halo, H)), (1, want1, band[0], band[1])):
+            if exchange == "allgather" and t == 0:
+                lo, hi = 0, H
+            if hi <= lo:
+                continue
+            for k3 in range(3):
+                got = G["sets"][t][k3][: psz[k3]].cpu().numpy().reshape(want[k3].shape)
+                ok &= bool(np.array_equal(got[lo * rows[k3]:hi * rows[k3]], want[k3][lo * rows[k3]:hi * rows[k3]]))
+        verified = bool(ok) if world == 1 else \
+            bool(D.min_over_ranks(1.0 if ok else 0.0, device="cpu" if rehearse else "cuda") == 1.0)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -311,25 +340,31 @@ def chain_bench(args, rank: int, world: int, local: int, cs, rehearse: bool) -> 
     dec.check()
     kern = np.array(dec.last_timing()) * 2 if band[1] > band[0] else np.zeros(4)   # two launches per step
     dec.set_timing(False)
-    dt = D.max_over_ranks(dt, device="cpu" if rehearse else "cuda")
+    if world > 1:
+        dt = D.max_over_ranks(dt, device="cpu" if rehearse else "cuda")
     rd = wr = 0
-    for p in base:
-        r, w = synth.algo_bytes(L, p)
-        rd, wr = rd + r, wr + w
-    total_mbs = 2 * kg * nmb * args.steps
+    for g in range(2):
+        for k in range(nk):
+            r, w = synth.algo_bytes(L, base[g][k % nbase])
+            rd, wr = rd + r, wr + w
+    total_mbs = nchains * nmb * args.steps
     value = total_mbs / dt
     frac_rows = (band[1] - band[0]) / H
     step_bytes = int((rd + wr) * frac_rows)
     achieved = step_bytes / (kern[3] * 1e-3) / 1e9 if kern[3] > 0 else 0.0
+    xin = groups[0]["xch"].bytes_in() * 2 if world > 1 else 0
+    del groups, dec
+    torch.cuda.empty_cache()
     return {
         "metric": "macroblocks/s (decode reconstruct, post-entropy) 1080p P-frame; % HBM roofline",
         "value": value, "unit": "macroblocks/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "u8", "data": "synthetic (seeded SURVEY 8(d) generator, arrow-h264_amd/csrc/synth.c)",
-        "config": {"workload": f"{CONFIG_NAMES[args.config]}, {2 * kg} dependent chains (each picture predicts "
-                               "from its chain's previous decoded picture; one all-gather per plane per step)",
-                   "survey_config": args.config, "width_mbs": W, "height_mbs": H, "mode": "chain",
-                   "chains": 2 * kg, "parallelism": f"slices{world}" if world > 1 else "single",
+        "config": {"workload": f"{CONFIG_NAMES[cfg_idx]}, {nchains} dependent chains ({nchains // world} per GPU; "
+                               "each picture predicts from its chain's previous decoded picture)",
+                   "survey_config": cfg_idx, "width_mbs": W, "height_mbs": H, "mode": "chain",
+                   "chains": nchains, "chains_per_gpu": nchains // world,
+                   "parallelism": f"slices{world}" if world > 1 else "single",
                    "rows_this_rank": list(band), "bands": [list(b) for b in bands]},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
@@ -338,20 +373,47 @@ def chain_bench(args, rank: int, world: int, local: int, cs, rehearse: bool) -> 
                      "numerator": "SURVEY 8(d) R+W of this rank's band of the step's pictures"},
         "kernel_ms": {"inter": float(kern[0]), "intra": float(kern[1]), "deblock": float(kern[2]),
                       "batch_wall": float(kern[3])},
-        "exchange_per_step": {"collectives": 3 if world > 1 else 0,
-                              "bytes_per_rank": int(sum(pbytes) * 2 * kg * frac_rows)},
+        "exchange": {"mode": exchange if world > 1 else None, "halo_mb_rows": halo, "max_abs_mvy_qpel": mvy,
+                     "bytes_in_per_rank_per_step": xin,
+                     "ops_per_step": (0 if world == 1 else 2 * (1 if exchange == "allgather" else
+                                                                 len(groups_peers(bands, rank, halo))))},
         "cpu_baseline": None,
         "verified_vs_oracle": verified,
     }
 
 
+def groups_peers(bands, rank, halo):
+    from h264r import dist as D
+    need, give = D.halo_plan(bands, rank, halo)
+    return sorted(set(need) | set(give))
+
+
+def spawn_ranks(args) -> int:
+    """`bench.py --gpus N` without a launcher (WORLD_SIZE unset): start N ranks through
+    torch.distributed.run as a CHILD process (nothing here has touched the GPU), wait, and exit
+    with its status; rank 0 prints the JSON line on the inherited stdout."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="GPUs = ranks; without WORLD_SIZE in the environment bench.py starts them itself")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", type=int, default=3, choices=[2, 3, 4, 5])
-    ap.add_argument("--batch", type=int, default=0, help="pictures per GPU per step (default 1024 for configs 2/3, 256 for 4, 64 at 2160p)")
+    ap.add_argument("--config", type=int, default=None, choices=[2, 3, 4, 5],
+                    help="SURVEY 8(d) workload (default: 3 at one GPU, 5 at N > 1)")
+    ap.add_argument("--mode", choices=["throughput", "chain"], default=None,
+                    help="throughput: independent pictures sharing a reference set (default at one GPU); "
+                         "chain: dependent chains, slice-sharded over the ranks (default at N > 1)")
+    ap.add_argument("--batch", type=int, default=0, help="throughput mode: pictures per GPU per step (default 1024 for configs 2/3, 256 for 4, 64 at 2160p)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16, help="threads of the multi-threaded CPU baseline")
@@ -360,16 +422,28 @@ def main() -> int:
                     help="length of the dependent-chain latency run (rank 0, N=1; 0 = skip)")
     ap.add_argument("--traffic-json", default=None, help="PMC traffic summary (default profiles/traffic.json)")
     ap.add_argument("--chain", type=int, default=0,
-                    help="dependent-chain mode: this many chains (even, <= 60) advance one picture per step, "
-                         "slice-sharded with one all-gather per reference picture (see chain_bench)")
+                    help="chain mode with this many chains in all (even); default chains-per-gpu x N")
+    ap.add_argument("--chains-per-gpu", type=int, default=32,
+                    help="chain mode: chains per GPU (weak scaling: the job holds chains-per-gpu x N chains)")
+    ap.add_argument("--exchange", choices=["halo", "allgather"], default="halo",
+                    help="chain mode at N > 1: rows within the motion vectors' reach from the neighbouring "
+                         "bands (point-to-point), or every band (all-gather)")
+    ap.add_argument("--no-n1", action="store_true", help="chain mode at N > 1: skip the one-GPU line of the same mode")
     ap.add_argument("--shard", choices=["replicas", "slices"], default=None,
-                    help="N>1 placement: independent pictures per GPU, or slice bands of shared pictures "
+                    help="throughput mode at N>1: independent pictures per GPU, or slice bands of shared pictures "
                          "(default: slices for configs 4/5, replicas for 2/3)")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return spawn_ranks(args)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
+    mode = "chain" if args.chain else (args.mode or ("throughput" if world == 1 or args.shard else "chain"))
+    if args.config is None:
+        args.config = 5 if (world > 1 and mode == "chain") else 3
 
     import torch
     import torch.distributed as dist
@@ -390,17 +464,32 @@ def main() -> int:
     # the context's own stream (unordered with torch's fills and copies)
     cs = torch.cuda.Stream(device=local)
     torch.cuda.set_stream(cs)
+    backend = None
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if rehearse:
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = dist.get_backend()
+        assert dist.get_world_size() == args.gpus, (dist.get_world_size(), args.gpus)
+        dist.barrier()                                  # communicators up before any P2P
+    ranks = {"backend": backend, "rccl_ranks": dist.get_world_size() if backend == "nccl" else 0,
+             "ranks": world, "rehearsal": rehearse}
 
-    if args.chain:
-        if args.chain % 2 or not 2 <= args.chain <= 60:
-            raise SystemExit("--chain takes an even number of chains, 2..60")
-        out = chain_bench(args, rank, world, local, cs, rehearse)
+    if mode == "chain":
+        nch = args.chain or args.chains_per_gpu * world
+        out = chain_run(args, rank, world, local, cs, rehearse, nch, args.config, args.exchange)
+        out["distributed"] = ranks
+        if world > 1 and not args.no_n1:
+            # the one-GPU line of the same mode and per-GPU load (weak scaling reference), on
+            # rank 0 alone after the N-rank run; the other ranks wait at the barrier
+            if rank == 0:
+                n1 = chain_run(args, 0, 1, local, cs, rehearse, nch // world, args.config, args.exchange)
+                out["same_mode_n1"] = {k: n1[k] for k in ("value", "ms_per_step", "verified_vs_oracle", "kernel_ms")}
+                out["same_mode_n1"]["chains"] = n1["config"]["chains"]
+                out["scaling_vs_same_mode_n1"] = out["value"] / (world * n1["value"])
+            dist.barrier()
         if rank == 0:
             print(json.dumps(out))
         if world > 1:
@@ -584,11 +673,8 @@ def main() -> int:
     kbytes = [int(k * (band[1] - band[0]) / H) for k in kbytes_all]
     # the library deblocks batches of >= H264R_DEBLOCK2_MIN pictures (default 192) with
     # k_deblock2, smaller ones with k_deblock (include/h264r.h)
-    # (k_deblock3 under H264R_DEBLOCK3=1); the deblocking records come from k_dbinfo before
-    # k_inter4r (H264R_DBINFO=1, the default) or from k_inter4 itself (0)
-    row_walk = "k_deblock3" if os.environ.get("H264R_DEBLOCK3", "0") not in ("", "0") else "k_deblock2"
-    dbk = row_walk if npics >= int(os.environ.get("H264R_DEBLOCK2_MIN", "192")) else "k_deblock"
-    inter_k = ["k_inter4"] if os.environ.get("H264R_DBINFO", "1") == "0" else ["k_dbinfo", "k_inter4r"]
+    dbk = "k_deblock2" if npics >= int(os.environ.get("H264R_DEBLOCK2_MIN", "192")) else "k_deblock"
+    inter_k = ["k_dbinfo", "k_inter4r"]
     names = [" + ".join(inter_k), "intra (k_level + k_intra_levels + k_intra_pic)", dbk]
     kern_names = [inter_k + ["k_inter_sp"], ["k_level", "k_level_scan", "k_level_scatter", "k_intra_levels", "k_intra_pic"],
                   [dbk]]
@@ -681,6 +767,7 @@ def main() -> int:
             "cpu_baseline_threads": cpu_mt,
             "latency": latency,
             "verified_vs_oracle": verified,
+            "distributed": ranks,
         }
         print(json.dumps(out))
     if world > 1:

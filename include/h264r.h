@@ -53,7 +53,7 @@
 extern "C" {
 #endif
 
-#define H264R_ABI_VERSION 1
+#define H264R_ABI_VERSION 2
 
 /* ---- status codes ---------------------------------------------------------- */
 #define H264R_OK               0
@@ -160,7 +160,11 @@ typedef struct h264r_pic {
  * `ref_planes` is a device array of 3*H264R_MAX_SLOTS device pointers
  * (Y,Cb,Cr per DPB slot) to full-size planes; MC reads whole dwords, so each
  * plane must be followed by H264R_PLANE_SLACK readable bytes (the slots of
- * h264r_set_ref / h264r_ref_planes are). */
+ * h264r_set_ref / h264r_ref_planes are).  `ref_planes_stride` (ABI 2): 0 = that one
+ * table serves every picture of the batch; otherwise picture p reads its own table at
+ * ref_planes + p * ref_planes_stride (>= 3*H264R_MAX_SLOTS pointers apart) -- a batch of
+ * pictures from different streams, each with its own DPB (the reference keeps one DPB per
+ * decoder, dpb.cc:1046-1054 get_ref_pic; bench.py's dependent chains). */
 #define H264R_PLANE_SLACK 64
 typedef struct h264r_batch {
     int32_t             num_pics;
@@ -178,6 +182,7 @@ typedef struct h264r_batch {
     uint8_t*            out_y;
     uint8_t*            out_u;
     uint8_t*            out_v;
+    int64_t             ref_planes_stride;   /* pointers; 0 = one table for the batch (above) */
 } h264r_batch;
 
 typedef struct h264r_ctx h264r_ctx;

@@ -5,6 +5,7 @@ import ctypes as C
 import os
 import re
 import subprocess
+import sys
 import tempfile
 
 import numpy as np
@@ -47,7 +48,8 @@ int main(void) {
          sizeof(h264r_pic), sizeof(h264r_batch), sizeof(h264r_synth_cfg));
   printf("%zu %zu %zu %zu\n", offsetof(h264r_mb, coef_off), offsetof(h264r_mb, ipred),
          offsetof(h264r_slice, ref_slot), offsetof(h264r_slice, implicit_w1));
-  printf("%zu %zu\n", offsetof(h264r_batch, ref_planes), offsetof(h264r_synth_cfg, seed));
+  printf("%zu %zu %zu\n", offsetof(h264r_batch, ref_planes), offsetof(h264r_synth_cfg, seed),
+         offsetof(h264r_batch, ref_planes_stride));
   return 0; }
 '''
     with tempfile.TemporaryDirectory() as td:
@@ -61,7 +63,7 @@ int main(void) {
                       A.PIC_DTYPE.itemsize, C.sizeof(A.Batch), C.sizeof(A.SynthCfg)]
     assert v[6:10] == [A.MB_DTYPE.fields["coef_off"][1], A.MB_DTYPE.fields["ipred"][1],
                        A.SLICE_DTYPE.fields["ref_slot"][1], A.SLICE_DTYPE.fields["implicit_w1"][1]]
-    assert v[10:12] == [A.Batch.ref_planes.offset, A.SynthCfg.seed.offset]
+    assert v[10:13] == [A.Batch.ref_planes.offset, A.SynthCfg.seed.offset, A.Batch.ref_planes_stride.offset]
 
 
 def test_quant_flat_matches_oracle(L):
@@ -78,7 +80,7 @@ def test_quant_lists_flat_equals_flat(L):
 
 
 def test_error_codes(L):
-    assert L.h264r_abi_version() == 1
+    assert L.h264r_abi_version() == A.ABI_VERSION
     assert L.h264r_strerror(A.EINVAL) == b"invalid argument"
     h = C.c_void_p()
     assert L.h264r_create(C.byref(h), 0, 0, 0, 1, 8) == A.EINVAL
@@ -97,3 +99,19 @@ def test_no_gpu_means_no_decoder(L):
     assert L.h264r_create(C.byref(h), 0, 10, 10, 1, 8) == A.ENODEVICE
     with pytest.raises(h264r.H264RError):
         h264r.Decoder()
+
+
+@pytest.mark.parametrize("env", [{"H264R_DEBLOCK2_MIN": "abc"}, {"H264R_LEVELS": "99"}, {"H264R_COOP": "2"},
+                                 {"H264R_DEBUG": "1"}, {"H264R_WAIT_MS": "0"}])
+def test_env_knob_out_of_range_is_refused(env):
+    """Every environment knob of the library is validated once: a value outside its range makes
+    h264r_create fail with H264R_EINVAL (before any device query, so this runs without a GPU)
+    instead of being taken for another setting.  H264R_DEBUG may carry
+    schedule flags only: DBG_NO_DEBLOCK (1) would change the output."""
+    code = ("import ctypes as C, sys; sys.path.insert(0, %r); import h264r; L = h264r.lib(); h = C.c_void_p(); "
+            "print(L.h264r_create(C.byref(h), 0, 10, 10, 1, 8))" % os.path.join(ROOT, "arrow-h264_amd"))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, **env))
+    assert r.returncode == 0, r.stderr[-1000:]
+    assert int(r.stdout.split()[-1]) == A.EINVAL
+    assert list(env)[0] in r.stderr

@@ -73,23 +73,6 @@ def _worker(rank, world, port, q):
             D.allgather_into_slot(send, dst, bands2, rank, 16, Wb)
             exp = torch.tensor([(y * 7 + 1) % 251 for y in range(Hs * 16)], dtype=torch.uint8).repeat_interleave(Wb)
             ok_slot.append(bool(torch.equal(dst[: Hs * 16 * Wb], exp)) and bool((dst[-64:] == 0xEE).all()))
-        # chain mode: K pictures' bands in one all-gather, landed in K chain slots
-        ok_chain = []
-        for starts, Hs in (([0, 2, 4], 6), ([0, 3], 5)):
-            bands3 = D.slice_bands(starts, Hs, world)
-            K, Wb = 3, W * 16
-            plane = Hs * 16 * Wb
-            stride = plane + 64
-            out = torch.zeros(K * plane, dtype=torch.uint8)
-            a0, a1 = bands3[rank]
-            full = torch.stack([torch.tensor([(k * 31 + y * 7 + 1) % 251 for y in range(Hs * 16)],
-                                             dtype=torch.uint8).repeat_interleave(Wb) for k in range(K)])
-            out.view(K, plane)[:, a0 * 16 * Wb:a1 * 16 * Wb] = full[:, a0 * 16 * Wb:a1 * 16 * Wb]
-            slots = torch.full((K * stride,), 0xEE, dtype=torch.uint8)
-            D.chain_exchange(out, slots, bands3, rank, plane, stride, 16, Wb)
-            got = slots.view(K, stride)
-            ok_chain.append(bool(torch.equal(got[:, :plane], full)) and bool((got[:, plane:] == 0xEE).all()))
-        ok_slot.append(all(ok_chain))
         t = D.max_over_ranks(1.0 + rank)
         share = list(D.picture_share(rank, world, 3))
         q.put((rank, all(ok_slot), t, share))
@@ -113,16 +96,69 @@ def test_gloo_world2_allgather_and_max():
     assert res[0][3] == [0, 1, 2] and res[1][3] == [3, 4, 5]
 
 
-def test_chain_slots():
-    import numpy as np
-    from h264r import _abi as A
-    sl = np.zeros(2, A.SLICE_DTYPE)
-    sl["ref_slot"][:] = -1
-    sl["ref_slot"][0, 0, :3] = [0, 1, 2]
-    sl["ref_slot"][0, 1, :2] = [1, 0]
-    out = D.chain_slots(sl, 5, 8)
-    assert out["ref_slot"][0, 0, :4].tolist() == [5, 8, 9, -1]
-    assert out["ref_slot"][0, 1, :3].tolist() == [8, 5, -1]
-    assert (sl["ref_slot"][0, 0, :3] == [0, 1, 2]).all()          # input untouched
-    with pytest.raises(ValueError):
-        D.chain_slots(sl, 0, 31)
+def test_halo_rows():
+    # luma window rows y-2 .. y+6, y = Y + floor(mv_y / 4); chroma rows yc .. yc+2
+    assert D.halo_mb_rows(0) == 1
+    assert D.halo_mb_rows(4 * 13) == 1              # 13 + 3 = 16 rows
+    assert D.halo_mb_rows(4 * 13 + 1) == 2
+    assert D.halo_mb_rows(131) == 3                 # config 5: |mv_y| <= 32.75 px
+    assert D.halo_plan([(0, 17), (17, 34), (34, 51)], 1, 3) == ({0: (14, 17), 2: (34, 37)}, {0: (17, 20), 2: (31, 34)})
+    assert D.halo_plan([(0, 2), (2, 4), (4, 9)], 0, 3) == ({1: (2, 4), 2: (4, 5)}, {1: (0, 2), 2: (1, 2)})
+    assert D.halo_plan([(0, 9), (9, 9)], 1, 3) == ({}, {})
+
+
+def _band_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        ok = []
+        W, H, nk, slack = 3, 7, 3, 64
+        for starts in ([0, 2, 3, 5], [0, 1, 4, 6], [0, 3]):
+            bands = D.slice_bands(starts, H, world)
+            for mode, halo in (("halo", 1), ("halo", 2), ("allgather", 0)):
+                psz = [c * W * H for c in D.ROW_BYTES_PER_MB_COL]
+                rb = [c * W for c in D.ROW_BYTES_PER_MB_COL]
+
+                def value(k, pl, row):          # a byte per (picture, plane, MB row, offset)
+                    n = rb[pl]
+                    return (torch.arange(n, dtype=torch.int64) * 3 + k * 101 + pl * 37 + row * 13) % 251
+                planes = [torch.full((nk * psz[pl] + slack,), 0xEE, dtype=torch.uint8) for pl in range(3)]
+                b0, b1 = bands[rank]
+                for pl in range(3):
+                    v = planes[pl][: nk * psz[pl]].view(nk, psz[pl])
+                    for k in range(nk):
+                        for r in range(b0, b1):
+                            v[k, r * rb[pl]:(r + 1) * rb[pl]] = value(k, pl, r).to(torch.uint8)
+                X = D.BandExchange(bands, rank, W, H, nk, mode, halo, "cpu")
+                X.run(planes)
+                lo, hi = (0, H) if mode == "allgather" else (max(b0 - halo, 0), min(b1 + halo, H))
+                if b1 <= b0 and mode == "halo":
+                    lo, hi = b0, b0
+                good = True
+                for pl in range(3):
+                    v = planes[pl][: nk * psz[pl]].view(nk, psz[pl])
+                    for k in range(nk):
+                        for r in range(H):
+                            seg = v[k, r * rb[pl]:(r + 1) * rb[pl]]
+                            want = value(k, pl, r).to(torch.uint8) if lo <= r < hi else torch.full_like(seg, 0xEE)
+                            good &= bool(torch.equal(seg, want))
+                    good &= bool((planes[pl][nk * psz[pl]:] == 0xEE).all())
+                ok.append(good)
+        q.put((rank, all(ok)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_band_exchange(world):
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_band_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert [r[1] for r in res] == [True] * world

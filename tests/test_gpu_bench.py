@@ -1,11 +1,12 @@
 """bench.py's modes on MI355X, checked end to end (each run compares its own output with the
 oracle before timing and reports `verified_vs_oracle`).
 
-The dependent-chain mode (--chain) is the multi-GPU path with an
-exchange on the dependency path: run here with one rank, and rehearsed with two ranks on
-the one GPU of the box (H264R_BENCH_REHEARSE=1: gloo in place of RCCL, which refuses two
-ranks on one device) -- the exchange moves real bands between processes, and chain 0's
-pictures after two exchanges must equal the oracle's chain."""
+The dependent-chain mode is the multi-GPU path with an exchange on the
+dependency path: run here with one rank, and rehearsed with two ranks on the one GPU of the box
+(H264R_BENCH_REHEARSE=1: gloo in place of RCCL, which refuses two ranks on one device) -- the
+exchange moves real rows between processes, and chain 0's second picture (which read its first
+through the exchange) must equal the oracle's chain.  `bench.py --gpus 2` with no launcher starts
+its two ranks itself."""
 import json
 import os
 import subprocess
@@ -37,7 +38,26 @@ def test_gpu_bench_chain_one_rank():
 def test_gpu_bench_chain_two_ranks_rehearsal():
     d = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
               "--master-addr", "127.0.0.1", "--master-port", "29517", "bench.py", "--gpus", "2", "--config", "4",
-              "--chain", "4", "--steps", "2", "--warmup", "1"], env={"H264R_BENCH_REHEARSE": "1"})
+              "--chain", "4", "--steps", "2", "--warmup", "1", "--no-n1"], env={"H264R_BENCH_REHEARSE": "1"})
     assert d["verified_vs_oracle"] is True
     assert d["n_gpus"] == 2 and d["config"]["bands"] == [[0, 34], [34, 68]]
-    assert d["exchange_per_step"]["collectives"] == 3
+    assert d["exchange"]["mode"] == "halo" and d["exchange"]["halo_mb_rows"] >= 1
+    assert d["exchange"]["ops_per_step"] == 2
+
+
+def test_gpu_bench_gpus2_spawns_its_ranks():
+    """`bench.py --gpus 2` with no torchrun: the default N > 1 line (config 5 chain mode,
+    slice-sharded), with the one-GPU line of the same mode beside it."""
+    d = _run([sys.executable, "bench.py", "--gpus", "2", "--chains-per-gpu", "2", "--steps", "2", "--warmup", "1"],
+             env={"H264R_BENCH_REHEARSE": "1"})
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "slices2"
+    assert d["config"]["survey_config"] == 5 and d["config"]["mode"] == "chain" and d["config"]["chains"] == 4
+    assert d["verified_vs_oracle"] is True
+    assert d["distributed"]["ranks"] == 2 and d["distributed"]["backend"] == "gloo"
+    assert d["same_mode_n1"]["verified_vs_oracle"] is True and d["same_mode_n1"]["chains"] == 2
+
+
+def test_gpu_bench_chain_allgather_rehearsal():
+    d = _run([sys.executable, "bench.py", "--gpus", "2", "--config", "4", "--chains-per-gpu", "2", "--exchange",
+              "allgather", "--steps", "2", "--warmup", "1", "--no-n1"], env={"H264R_BENCH_REHEARSE": "1"})
+    assert d["verified_vs_oracle"] is True and d["exchange"]["mode"] == "allgather"

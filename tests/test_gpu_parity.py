@@ -141,15 +141,6 @@ def test_gpu_large_batch_wide_rows(L, dec, cidx):
     _large_batch_vs_oracle(L, dec, cidx, 120, 32, 256)
 
 
-@pytest.mark.parametrize("cidx", [2, 3, 4])
-def test_gpu_pipelined_sub_batches(L, dec, cidx, monkeypatch):
-    """With H264R_PIPES=3 a batch of >= 2 x H264R_PIPE_MIN pictures (1100 CIF pictures) runs
-    as sub-batches on the context's pipeline streams (h264r_host.hip run_batch: inter /
-    intra / deblocking of consecutive sub-batches overlapping); every picture checked."""
-    monkeypatch.setenv("H264R_PIPES", "3")
-    _large_batch_vs_oracle(L, dec, cidx, 22, 18, 1100)
-
-
 @pytest.mark.parametrize("cidx", [2, 3])
 def test_gpu_large_batch_xcd_groups(L, dec, cidx):
     """464 CIF pictures (29 groups of 16 x 18 MB rows = 522 k_deblock2 waves): k_deblock2 in
@@ -158,13 +149,14 @@ def test_gpu_large_batch_xcd_groups(L, dec, cidx):
     _large_batch_vs_oracle(L, dec, cidx, 22, 18, 464)
 
 
-@pytest.mark.parametrize("cidx,W,H,n", [(3, 22, 18, 464), (2, 120, 32, 256), (4, 22, 18, 203)])
-def test_gpu_large_batch_deblock3(L, dec, cidx, W, H, n, monkeypatch):
-    """k_deblock3 (H264R_DEBLOCK3=1: the row walk with 8 lanes per picture-row, 8 pictures
-    per wave): XCD-local groups of 8 pictures, 1080p-wide rows, a ragged last group;
-    every picture checked."""
-    monkeypatch.setenv("H264R_DEBLOCK3", "1")
-    _large_batch_vs_oracle(L, dec, cidx, W, H, n)
+def test_gpu_stray_env_selectors_are_inert(L, dec, monkeypatch):
+    """The round-3 selectors that chose kernel variants (H264R_DBINFO, H264R_DEBLOCK3, H264R_PIPES)
+    are gone from the library: set to values that once launched no deblocking records, they
+    change nothing (a stale DbInfo must never be filtered with)."""
+    for k, v in (("H264R_DBINFO", "3"), ("H264R_DEBLOCK3", "on"), ("H264R_PIPES", "4")):
+        monkeypatch.setenv(k, v)
+    _batch_vs_oracle(L, dec, 3, 22, 18, 3)
+    _batch_vs_oracle(L, dec, 4, 22, 18, 2)
 
 
 def test_gpu_batch_cif_p(L, dec):

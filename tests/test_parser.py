@@ -137,3 +137,65 @@ def test_gpu_parser_decodes_to_reference_md5s(name, tmp_path):
     r = _run(GPU_DEC, name, out)
     assert r.returncode == 0, r.stderr[-800:]
     assert OUT.digest_by_frames(str(out), S.STREAMS[name]["frames"]) == GOLD[name]["frame_md5"]
+
+
+def _decode_bytes(binary, data: bytes, tmp_path, tag: str, timeout=120):
+    src = tmp_path / f"{tag}.264"
+    src.write_bytes(data)
+    out = tmp_path / f"{tag}.yuv"
+    r = subprocess.run([binary, "-i", str(src), "-o", str(out)], capture_output=True, text=True, timeout=timeout)
+    return r, (out.read_bytes() if out.exists() else b"")
+
+
+@pytest.mark.parametrize("names", [("bp_qcif_ippp", "bp_cif_wp_pcm"), ("bp_cif_wp_pcm", "bp_qcif_ippp"),
+                                   ("hp_cif_cabac_ibbp_4slices", "bp_qcif_longterm_40", "hp_720p_4slices")])
+def test_parser_resolution_change_at_idr(names, tmp_path):
+    """Streams of different picture sizes back to back (every one opens with its SPS / PPS, ids 0,
+    and an IDR): the decode is each stream's own decode in turn -- a replaced active SPS ends the
+    open picture first (slice_header.cc:392-423), the picture still on the device leaves the
+    context at its own size, and every output frame keeps its own size and cropping
+    (a resolution decrease overflowed the host copy, an increase lost a picture)."""
+    dec = _cpu_dec()
+    whole, parts = b"", []
+    for n in names:
+        data = open(S.stream_path(n), "rb").read()
+        whole += data
+        r, y = _decode_bytes(dec, data, tmp_path, n)
+        assert r.returncode == 0, r.stderr[-800:]
+        parts.append(y)
+    r, y = _decode_bytes(dec, whole, tmp_path, "all")
+    assert r.returncode == 0, r.stderr[-800:]
+    assert y == b"".join(parts)
+
+
+def test_parser_malformed_streams_under_asan(tmp_path):
+    """Malformed headers and slice data (bytes of the committed streams flipped at random, seeded)
+    through the parser built with AddressSanitizer + UBSan: every run ends in a decoded stream or
+    a reported error, never an out-of-bounds access or undefined behaviour (ue(v)
+    values >= 2^31 turned negative in int fields, unbounded list modifications, unchecked SPS /
+    slice-header ranges)."""
+    O.build_oracle()
+    subprocess.run(["make", "-s", "-C", os.path.join(S.ROOT, "oracle"), "asan"], check=True)
+    asan = os.path.join(S.ROOT, "oracle", "_cpu", "h264dec_cpu_asan")
+    rng = np.random.default_rng(0x264A)
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=0", UBSAN_OPTIONS="print_stacktrace=1")
+    bad = []
+    for name in ("bp_qcif_ippp", "mp_qcif_ibbp_direct", "hp_qcif_cabac_intra_qp0_51", "hp_qcif_scaling_lists",
+                 "hp_qcif_ibbp_explicit_8x8", "xp_qcif_sp", "bp_qcif_slices_cip", "hi444_qcif_lossless"):
+        base = bytearray(open(S.stream_path(name), "rb").read())
+        for k in range(60):
+            data = bytearray(base)
+            # the first bytes hold SPS / PPS / the first slice header; later flips hit MB data
+            for _ in range(int(rng.integers(1, 4))):
+                pos = int(rng.integers(4, min(len(data), 96))) if k % 2 == 0 else int(rng.integers(4, len(data)))
+                data[pos] ^= 1 << int(rng.integers(0, 8))
+            if k % 6 == 5:                    # an oversized ue(v): 31 zero bits in the first slice header
+                pos = int(rng.integers(8, 40))
+                data[pos:pos + 4] = b"\x00\x00\x00\x01"[:3] + b"\x80"
+            src = tmp_path / f"{name}_{k}.264"
+            src.write_bytes(bytes(data))
+            r = subprocess.run([asan, "-i", str(src), "-o", str(tmp_path / "o.yuv")], capture_output=True, text=True,
+                               timeout=120, env=env)
+            if "Sanitizer" in r.stderr or "runtime error" in r.stderr or r.returncode < 0:
+                bad.append((name, k, r.returncode, r.stderr[-1500:]))
+    assert not bad, bad[0]
