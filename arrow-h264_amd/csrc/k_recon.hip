@@ -68,12 +68,8 @@ DEV bool inter4_groups(const Geom& g, int2 rows, int per, int& grp, int& gend)
 // blockIdx.x % 8 (one eighth of the MB rows) of every picture: an XCD's motion
 // compensation reads only its band of the reference pictures (+ the MV reach), which its
 // 4 MB L2 holds, instead of every XCD streaming whole references through its L2.
-extern "C" __global__ __launch_bounds__(256, H264R_INTER_WAVES) void k_inter4r(h264r_batch b, DbInfo* dbinfo, int2 rows,
-                                                                              int* sp_flag, uint8_t* recon,
-                                                                              const int* inter_cnt)
+DEV void inter4_kernel(const h264r_batch& b, int2 rows, int* sp_flag, uint8_t* recon, Inter4Lds& S, const int* inter_cnt)
 {
-    (void)dbinfo;
-    __shared__ Inter4Lds S;
     const int pic = blockIdx.y;
     const Geom g = make_geom(b.width_mbs, b.height_mbs);
     int grp, gend;
@@ -102,6 +98,15 @@ extern "C" __global__ __launch_bounds__(256, H264R_INTER_WAVES) void k_inter4r(h
         asm volatile("" : "+v"(ln2));
         pre = inter4_pre(b, g, pic, a0, aend, ln2);
     }
+}
+
+extern "C" __global__ __launch_bounds__(256, H264R_INTER_WAVES) void k_inter4r(h264r_batch b, DbInfo* dbinfo, int2 rows,
+                                                                              int* sp_flag, uint8_t* recon,
+                                                                              const int* inter_cnt)
+{
+    (void)dbinfo;
+    __shared__ Inter4Lds S;
+    inter4_kernel(b, rows, sp_flag, recon, S, inter_cnt);
 }
 
 // k_dbinfo: the deblocking records DbInfo of every MB (dbinfo_block, mb_inter4.h) on their

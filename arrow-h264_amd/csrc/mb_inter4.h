@@ -192,6 +192,16 @@ DEV void luma_window_global(const uint8_t* __restrict__ img, int W, int H, int x
     }
 }
 
+// The LDS reference-tile variant of round 3 (one 13-row tile per 8x8 quadrant by LDS-DMA,
+// measured slower: profiles/r03_e_ab.txt) is gone, but its never-taken branch stays in
+// inter4_mbs: without that branch the scheduler's regions change and k_inter4r spills 17
+// VGPRs at its 128-VGPR budget (measured with the round-4 compiler; an explicit
+// sched_barrier, a compiler memory barrier or a wave-uniform branch do not reproduce it).
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+struct alignas(16) QuadTile {
+    u32x4 slot[64];
+};
+
 DEV void luma_block_pred(const uint32_t (&w)[9][3], int W, int x, int xf, int yf, uint32_t (&out)[4])
 {
     const int hs = xf == 3 ? 1 : 0;                  // G / h column c + 2 + hs
@@ -540,6 +550,7 @@ template <bool SP>
 DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int aend, int lane,
                     const Inter4Lds& S, int* sp_flag, const Inter4Pre& pre, uint8_t* __restrict__ recon)
 {
+    QuadTile* __restrict__ tiles = nullptr;       // the dead tile branch's (luma_block_pred note)
     const int grp = lane >> 4, blk = lane & 15, bx = blk & 3, by = blk >> 2;
     const int a = a0 + grp;
     const bool valid = a < aend;
@@ -658,11 +669,47 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
             const int vx = X4 * 16 + mvx, vy = Y4 * 16 + mvy;           // quarter luma / eighth chroma units
             const int x = vx >> 2, y = vy >> 2;
             {
-                uint32_t w[9][3];
-                if (ok) {
-                    luma_window_global(S.planes[slot * 3], g.W, g.H, x, y, w);
-                    luma_block_pred(w, g.W, x, vx & 3, vy & 3, tY);
+                // quadrant tile (QuadTile): the four lanes of my 8x8 quadrant (blk ^ 1, ^ 4, ^ 5)
+                // predict from one slot with one vector, and the tile stays inside the picture
+                const uint32_t key = ok ? mw.x : 0xFFFFFFFFu;
+                const int skey = ok ? slot : -1;
+                const bool uni = ok && key == (uint32_t)__shfl_xor((int)key, 1) && key == (uint32_t)__shfl_xor((int)key, 4) &&
+                                 key == (uint32_t)__shfl_xor((int)key, 5) && skey == __shfl_xor(skey, 1) &&
+                                 skey == __shfl_xor(skey, 4) && skey == __shfl_xor(skey, 5);
+                const int xq = x - 4 * (bx & 1), yq = y - 4 * (by & 1);
+                const bool tile = false && uni && xq >= 0;
+                // tile row t * 4 + ql (row 12: t = 3, ql = 0) of a quadrant lands, by LDS-DMA, in
+                // the 16-byte slot of the quadrant's lane ql of its wave-instruction t
+                const int qbase = grp * 16 + (by & 2) * 4 + (bx & 2);          // lane of ql = 0
+                if (__any(tile)) {
+                    const int ql = (by & 1) * 2 + (bx & 1);
+                    const uint8_t* img = S.planes[(tile ? slot : 0) * 3] + ((xq - 2) & ~3);
+#pragma unroll
+                    for (int t = 0; t < 4; ++t)
+                        if (tile && (t < 3 || ql == 0))
+                            __builtin_amdgcn_global_load_lds(
+                                (const __attribute__((address_space(1))) void*)(img + (size_t)clip3(0, g.H - 1, yq - 2 + ql + 4 * t) * g.W),
+                                (__attribute__((address_space(3))) void*)(tiles + t), 16, 0, 0);
+                    __builtin_amdgcn_s_waitcnt(0x0F70);                       // vmcnt(0): this wave's tiles landed
+                    __builtin_amdgcn_wave_barrier();
                 }
+                // the 9 window rows: tile rows (by & 1) * 4 + r from dword (bx & 1), or the
+                // lane's own rows of the plane -- one generic (flat) load per row either way
+                uint32_t w[9][3];
+                if (tile) {
+                    const uint32_t* tb = reinterpret_cast<const uint32_t*>(tiles) + (bx & 1);
+#pragma unroll
+                    for (int r = 0; r < 9; ++r) {
+                        const int jr = (by & 1) * 4 + r;                        // tile row
+                        const int src = qbase + ((jr & 2) << 1) + (jr & 1);    // lane that fetched it
+                        const uint32_t* q = tb + (jr >> 2) * 256 + src * 4;
+                        w[r][0] = q[0]; w[r][1] = q[1]; w[r][2] = q[2];
+                    }
+                } else if (ok) {
+                    luma_window_global(S.planes[slot * 3], g.W, g.H, x, y, w);
+                }
+                if (ok) luma_block_pred(w, g.W, x, vx & 3, vy & 3, tY);
+                if (__any(tile)) wave_sync();                      // read before the next list's tiles
             }
             if (ok) chroma_block_pred2(S.planes[slot * 3 + 1], S.planes[slot * 3 + 2], g.Wc, g.Hc, vx >> 3, vy >> 3, vx & 7, vy & 7, tC);
             const bool l1 = l != 0;
