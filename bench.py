@@ -38,6 +38,7 @@ CONFIG_NAMES = {2: "1080p all-intra", 3: "1080p IPPP Main P-frames", 4: "1080p H
                 5: "2160p High B-frames, 8 slices"}
 CONFIG_SIZE = {2: (120, 68), 3: (120, 68), 4: (120, 68), 5: (240, 135)}
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
+VALU_ISSUE_PER_S = 256 * 4 * 2.4e9 / 2   # wave64 VALU instructions per second: 256 CUs x 4 SIMD-32 at 2.4 GHz, 2 cycles each
 
 
 def cpu_model() -> str:
@@ -682,6 +683,7 @@ def main() -> int:
     # (tools/pmc.sh + tools/pmc_summary.py --json): per-MB FETCH_SIZE (doubled, gfx950) +
     # WRITE_SIZE of every kernel of the sequence, times the MBs this rank processed
     traffic, traffic_src, ktraffic = None, None, [None, None, None]
+    kvalu = [None, None, None]
     tpath = args.traffic_json or os.path.join(ROOT, "profiles", "traffic.json")
     if os.path.exists(tpath):
         tj = json.load(open(tpath))
@@ -690,11 +692,22 @@ def main() -> int:
             traffic = int(sum(per.values()) * mbs_rank)
             ktraffic = [int(sum(per.get(n, 0) for n in kn) * mbs_rank) for kn in kern_names]
             traffic_src = f"{os.path.basename(tpath)} ({tj.get('source')}): all kernels of the sequence"
+            vper = {k: v.get("valu_per_mb") for k, v in tj["kernels"].items()}
+            if all(vper.get(n) is not None for kn in kern_names for n in kn if n in vper):
+                kvalu = [sum(vper.get(n) or 0.0 for n in kn) for kn in kern_names]
     kernels = {}
     for i, nme in enumerate(names):
         ach = kbytes[i] / (kern[i] * 1e-3) / 1e9 if kern[i] > 0 else 0.0
         kernels[nme] = {"ms": float(kern[i]), "algo_bytes": kbytes[i], "achieved": ach,
                         "frac": ach / HBM_PEAK_GBS, "traffic": ktraffic[i]}
+        # the second roof: VALU issue.  A wave64 VALU instruction occupies
+        # its SIMD-32 for 2 cycles (MI355X_MICROARCH.md, wave scheduling), so the chip issues at
+        # most 256 CUs x 4 SIMDs x 2.4 GHz / 2 wave-instructions per second; valu_floor_ms is
+        # the kernel's PMC VALU count (profiles/traffic.json) at that rate
+        if kvalu[i] is not None and kern[i] > 0:
+            floor_ms = kvalu[i] * mbs_rank / VALU_ISSUE_PER_S * 1e3
+            kernels[nme].update({"valu_per_mb": kvalu[i], "valu_floor_ms": floor_ms,
+                                 "valu_frac": floor_ms / float(kern[i])})
 
     # a measured copy-kernel peak beside the spec peak (device-to-device copy
     # of 1 GiB, read + write bytes over its HIP-event time, best of 5), outside the timed region
@@ -758,6 +771,8 @@ def main() -> int:
                          "numerator": "SURVEY 8(d) R+W summed exactly over the batch's MBs",
                          "path_frac_wall": value / world * step_bytes / max(mbs_rank, 1) / (HBM_PEAK_GBS * 1e9),
                          "read_frac": (rd / (kern[3] * 1e-3) / 1e9 / HBM_PEAK_GBS) if kern[3] > 0 else 0.0,
+                         "valu_floor_ms": (sum(k["valu_floor_ms"] for k in kernels.values())
+                                           if all("valu_floor_ms" in k for k in kernels.values()) else None),
                          "copy_peak_measured": copy_peak,
                          "frac_of_copy_peak": (achieved / copy_peak) if copy_peak else None,
                          "kernels": kernels},
@@ -769,6 +784,11 @@ def main() -> int:
             "verified_vs_oracle": verified,
             "distributed": ranks,
         }
+        vf = out["roofline"]["valu_floor_ms"]
+        if vf:
+            # the HBM fraction the path could reach if every kernel issued VALU back to back at
+            # today's instruction counts (the ceiling the second roof puts on the first)
+            out["roofline"]["frac_ceiling_at_valu_floor"] = step_bytes / (vf * 1e-3) / 1e9 / HBM_PEAK_GBS
         print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()

@@ -47,4 +47,10 @@ if a.json and a.mbs:
         w = sum(cs["WRITE_SIZE"]) / len(cs["WRITE_SIZE"]) * 1024 / a.mbs
         out["kernels"][k] = {"read_bytes_per_mb": 2 * f, "read_bytes_per_mb_raw": f, "write_bytes_per_mb": w,
                              "traffic_bytes_per_mb": 2 * f + w}
+        # issue counts per MB (the second roof: bench.py turns VALU per MB into valu_frac)
+        for c, key in (("SQ_INSTS_VALU", "valu_per_mb"), ("SQ_INSTS_SALU", "salu_per_mb"), ("SQ_INSTS_LDS", "lds_per_mb")):
+            if c in cs:
+                out["kernels"][k][key] = sum(cs[c]) / len(cs[c]) / a.mbs
+        if "GRBM_GUI_ACTIVE" in cs:
+            out["kernels"][k]["grbm_gui_active"] = sum(cs["GRBM_GUI_ACTIVE"]) / len(cs["GRBM_GUI_ACTIVE"])
     json.dump(out, open(a.json, "w"), indent=1)
