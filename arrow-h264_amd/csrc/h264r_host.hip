@@ -51,7 +51,8 @@ extern "C" __global__ void k_deblock2(h264r_batch b, const h264r::DbInfo* dbinfo
 constexpr size_t DBINFO_BYTES = 80;
 constexpr size_t HANDOFF_BYTES = 256;   // one tagged record (32 x {dword, epoch}) per MB
 constexpr size_t HANDOFF2_BYTES = 384;  // k_deblock2: 2 row slots x 24 x {dword, tag} per MB column
-constexpr int DEBLOCK2_UNITS = 16;      // k_deblock2: pictures per wave (mb_deblock.h)
+constexpr int DEBLOCK2_UNITS = 16;      // k_deblock2: (picture, MB row) units per wave (mb_deblock.h)
+constexpr int DEBLOCK2_PICS = DEBLOCK2_UNITS / H264R_DB2_BAND;   // pictures per wave
 
 namespace {
 
@@ -583,8 +584,8 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
         }
         if (by_rows)
         {
-            // k_deblock2 keeps a 16-picture group on one XCD (g % nx): nx counters
-            int grid = ((P + DEBLOCK2_UNITS - 1) / DEBLOCK2_UNITS) * HB;
+            // k_deblock2 keeps a picture group on one XCD (g % nx): nx counters
+            int grid = ((P + DEBLOCK2_PICS - 1) / DEBLOCK2_PICS) * ((HB + H264R_DB2_BAND - 1) / H264R_DB2_BAND);
             const int nx = grid >= 64 * c->nxcc && !(c->debug & H264R_DBG_DEBLOCK_GLOBAL) ? c->nxcc : 1;
             grid = (grid + nx - 1) / nx * nx;
             hipLaunchKernelGGL(k_deblock2, dim3(grid), dim3(64), 0, s, b, dbinfo,

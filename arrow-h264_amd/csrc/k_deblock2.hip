@@ -1,13 +1,16 @@
-// k_deblock2.hip -- the in-loop deblocking filter for large batches: MB-row walks of
-// 16 pictures per wave, 4 lanes per (picture, MB row), packed 16-bit filters, LDS windows.
+// k_deblock2.hip -- the in-loop deblocking filter for large batches: bands of MB rows
+// walked in lock step, 4 lanes per (picture, MB row), packed 16-bit filters, LDS rings.
 //
 // The reference filters MB by MB in raster order, vertical edges then horizontal edges
 // (Deblock::deblock_pic, deblock.cc:537-552): along a row MB x needs MB x-1 finished,
-// and MB (x, y) needs MB (x+1, y-1) finished -- a wavefront with a 2-MB lag per row.
-// k_deblock (k_deblock.hip) spreads one MB over 32 lanes; its steps are short but
-// latency-bound.  Here the parallelism comes from the pictures of the batch: a 64-lane
-// wave owns MB row y of 16 pictures, four lanes per picture ("unit"), and walks
-// x = 0 .. W-1 with every unit in lock step.
+// and MB (x, y) needs the samples MB (x+1, y-1)'s left edge wrote.  k_deblock
+// (k_deblock.hip) spreads one MB over 32 lanes; its steps are short but latency-bound.
+// Here the parallelism comes from the pictures of the batch: a 64-lane wave owns a BAND
+// of H264R_DB2_BAND consecutive MB rows of 16 / BAND pictures, four lanes per (picture,
+// row) "unit", and walks them in lock step, row rb of the band one MB behind row rb-1
+// (the least lag the reference's order allows: within one step every unit runs its
+// vertical edges before any runs its horizontal edges, so MB x of the upper row has had
+// MB x+1's left edge filtered when the lower row filters its top edge).
 //
 //   vertical edges   lane q filters luma rows 4q .. 4q+3 as the pairs (r, r+2) and
 //                    chroma plane q/2, rows 4(q&1) .. +3 -- filter_vertical deblock.cc:488-504
@@ -16,35 +19,38 @@
 //
 // Every operand is an s16x2 of two lines (mb_deblock2.h); the transposition between
 // the two passes is free, since both read the MB from LDS.  Each unit's MB row lives
-// in LDS as a ring of three MB slots (MB x in slot x % 3: the left neighbour stays
-// while the next two MBs arrive); the two MBs of a window are fetched one window ahead
-// into registers as 32-byte row pieces and stored back the same way, so global traffic
-// stays in whole sectors (a lane-pair walk with 16-byte scattered accesses missed L2:
-// profiles/r02_deblock2_v1_pmc_b256.txt).
+// in LDS as two MB slots (MB x in slot x & 1: the left neighbour and the current MB).
+// Between a step's vertical and horizontal edges MB x-1 (final once MB x's left edge is
+// filtered) is stored and MB x+1, fetched into registers during the previous step, takes
+// its slot; the step ends by fetching MB x+2.
+// Two slots instead of three keep a unit at 848 B of LDS: three waves per SIMD instead of
+// two, which is what the walk needs -- at two, a 1080p batch of 1024 pictures takes 2.1
+// rounds of resident waves and its last band ran alone for a third of the kernel
+// (profiles/r04_d_trace_db2.txt).
 //
-// The row below needs each MB's bottom rows (luma 12..15, chroma 6..7) after the MB's
-// right neighbour filtered its left edge: 24 naturally aligned 8-byte granules {data
-// dword, tag} per MB, laid out so that lane q of the row below polls exactly the six
-// it filters with (luma dword q of rows 12..15, chroma plane q/2 dword q&1 of rows 6..7)
-// and the producing lane publishes exactly the six it holds after its horizontal pass
-// -- no LDS exchange on either side.  Luma dword 3 and chroma dword 1 change again
-// with MB x+1's vertical edges and are published after them.  Write-through `sc1`
-// stores, `sc1` polling loads until every granule carries this launch's tag
-// (MI355X_MICROARCH.md R2 granule hand-off).  Waves take tickets row-major, so a wave
-// only waits on tickets taken earlier by running waves; every spin is bounded and
-// flags the error word.
+// Inside the band the row below reads MB x's bottom rows straight from the upper unit's
+// ring slot (the upper row is on MB x+1 then: MB x is its left neighbour).  Only the
+// band's bottom row hands its bottom rows to the next band (a wave of a later ticket):
+// 24 naturally aligned 8-byte granules {data dword, tag} per MB, laid out so that lane q
+// of the consuming row polls exactly the six it filters with (luma dword q of rows
+// 12..15, chroma plane q/2 dword q&1 of rows 6..7) and the producing lane publishes
+// exactly the six it holds after its horizontal pass.  Luma dword 3 and chroma dword 1
+// change again with MB x+1's vertical edges and are published after them.  `sc1`
+// polling loads until every granule carries this launch's tag (MI355X_MICROARCH.md R2
+// granule hand-off).  Waves take tickets band-major, so a wave only waits on tickets
+// taken earlier by running waves; every spin is bounded and flags the error word.
 //
-// Memory operations are issued in the order their waits need (vmcnt is in order and
-// counts stores): the record loads first, then the next MB's DbInfo and the next
-// window, whose registers are not needed before the end of the step (DbInfo goes
-// through LDS, so no loaded register is carried into the next step's filters).
+// Rows start and end one step apart, so at a given step some units are before their
+// row's first MB or past its last: their filters run with bS 0 (no change) and their
+// stores and publishes go to an out-of-range buffer offset (dropped by the buffer unit).
+// Every memory operation is issued by every lane on every path, so the waitcnt pass can
+// count the operations younger than a load it waits for.
 //
 // Sample ownership (each sample stored once, when final): a row stores MB x's rows
 // 0..12 (chroma 0..6) once MB x+1's vertical edges are done, and the rows 13..15
-// (chroma 7) of MB (x, y-1) after filtering its own top edge.  The last row of the
-// band stores its own bottom rows.
-#include <type_traits>
-
+// (chroma 7) of MB (x, y-1) after filtering its own top edge.  The launch's last row
+// stores its own bottom rows.
+#include "launch_cfg.h"
 #include "mb_deblock.h"
 #include "mb_deblock2.h"
 
@@ -53,22 +59,27 @@ using namespace h264r;
 namespace {
 
 constexpr int UNITS = DEBLOCK2_UNITS;  // (picture, MB row) units per wave, 4 lanes each
+constexpr int BAND = H264R_DB2_BAND;   // MB rows per wave
+constexpr int PICS = UNITS / BAND;     // pictures per wave
+static_assert(UNITS % BAND == 0, "a band divides the wave's units");
 constexpr int RECG = 24;               // granules per MB record: [consumer lane c 0..3][i 0..5]
 constexpr int AUX_SC1 = 16;            // buffer-op cache policy: sc1 (write-through store, L2-served load)
+constexpr int RSRC_W3 = 0x00020000;    // buffer descriptor word 3 (gfx9 raw buffer, range-checked)
+constexpr uint32_t OOB = 0x80000000u;  // added to an offset: past every range (loads 0, stores dropped)
 
-// One unit's MB row in LDS (1264 B: a unit stride of 316 dwords spreads the 8 units of
-// a half-wave over distinct banks for the column reads of the horizontal pass).
+// One unit's MB row in LDS: two MB slots and the DbInfo -- 848 B, so 16 units (13.25 KiB)
+// leave room for three waves per SIMD (12 per CU).  The unit stride of 212 dwords puts the
+// 8 units of a half-wave 20 banks apart (mod 32): the column reads of the horizontal pass
+// are conflict-free.
 struct alignas(16) UnitLds {
-    uint32_t y[16][12];       // luma rows 0..15; MB x in slot s = x % 3: dwords 4s .. 4s+3
-    uint32_t c[2][8][6];      // chroma plane, rows 0..7; slot s = dwords 2s, 2s+1
-    uint32_t info[20];        // DbInfo of the MB being filtered
-    uint32_t pad[8];
+    uint32_t y[16][8];        // luma rows 0..15; MB x in slot s = x & 1: dwords 4s .. 4s+3
+    uint32_t c[2][8][4];      // chroma plane, rows 0..7; slot s = dwords 2s, 2s+1
+    uint32_t info[20];        // DbInfo of the MB being filtered (zeros: no MB this step)
 };
-static_assert(sizeof(UnitLds) == 1264, "UnitLds layout");
+static_assert(sizeof(UnitLds) == 848, "UnitLds layout");
 
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));   // native vectors: registers, not stack
 typedef uint32_t v2u __attribute__((ext_vector_type(2)));
-
 
 // {byte j, byte j + 2} of one dword as an s16x2 (the column pair (j, j+2)).
 DEV s2 unpack_cols(uint32_t w, int j) { return as_s2(__builtin_amdgcn_perm(w, w, 0x0C000C00u | ((uint32_t)(j + 2) << 16) | (uint32_t)j)); }
@@ -76,12 +87,23 @@ DEV s2 unpack_cols(uint32_t w, int j) { return as_s2(__builtin_amdgcn_perm(w, w,
 DEV uint32_t pack_cols(s2 c0, s2 c1) { return __builtin_amdgcn_perm(as_w(c1), as_w(c0), 0x06020400u); }
 DEV s2 bs_pair(uint32_t w, int slo, int shi) { return (s2){(short)((w >> (8 * slo)) & 255), (short)((w >> (8 * shi)) & 255)}; }
 
+template <int AUX = 0>
+DEV void st16(__amdgpu_buffer_rsrc_t r, uint32_t off, v4u v)
+{
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, v), r, off, 0, AUX);
+}
+DEV void st8(__amdgpu_buffer_rsrc_t r, uint32_t off, v2u v)
+{
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned int, v), r, off, 0, 0);
+}
+DEV void st4(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t v) { __builtin_amdgcn_raw_buffer_store_b32(v, r, off, 0, 0); }
+
 }  // namespace
 
 #ifdef H264R_TRACE
 // Timing trace (trace builds only: make EXTRA=-DH264R_TRACE): per ticket {start, end
-// (s_memrealtime, 100 MHz), then s_memtime cycles spent in: V pass, record wait,
-// H pass, publish + stores + window switch}.
+// (s_memrealtime, 100 MHz), then s_memtime cycles spent in: V pass + fill, record wait,
+// H pass, publish + stores}.
 __device__ unsigned long long h264r_db2_trace[1 << 16][8];
 #define TRACE(...) __VA_ARGS__
 extern "C" void h264r_db2_trace_copy(void* dst) { (void)hipMemcpyFromSymbol(dst, HIP_SYMBOL(h264r_db2_trace), sizeof(h264r_db2_trace)); }
@@ -89,11 +111,11 @@ extern "C" void h264r_db2_trace_copy(void* dst) { (void)hipMemcpyFromSymbol(dst,
 #define TRACE(...)
 #endif
 
-// hb: records [pic][row & 1][W][RECG] granules {dword, tag}, moved as 16-byte `sc1` pairs
-// (two granules; each 8-byte half observed untorn on gfx950, MI355X_MICROARCH.md
-// visibility: the tag check stays per granule); sync[0]: ticket counter;
-// epoch < 2^20 (the host restarts from zeroed records before it wraps).
-// XCD-local hand-off (H264R_DB2_XCD, default): the rows of a 16-picture group all run on
+// hb: records [pic][band & 1][W][RECG] granules {dword, tag}, moved as 16-byte pairs (two
+// granules; each 8-byte half observed untorn on gfx950, MI355X_MICROARCH.md visibility:
+// the tag check stays per granule); sync[0..nx): ticket counters; epoch < 2^20 (the host
+// restarts from zeroed records before it wraps).
+// XCD-local hand-off (H264R_DB2_XCD, default): the bands of a picture group all run on
 // one XCD -- group g on XCD g % nx, each XCD with its own ticket counter (the XCD read
 // from the hardware register, so the placement holds whatever the dispatch order) -- and
 // the hand-off records are plain stores, which stay in that XCD's L2, read back by `sc1`
@@ -104,14 +126,18 @@ extern "C" void h264r_db2_trace_copy(void* dst) { (void)hipMemcpyFromSymbol(dst,
 #ifndef H264R_DB2_XCD
 #define H264R_DB2_XCD 1
 #endif
-extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_deblock2(
+#ifndef H264R_DB2_DIAG
+#define H264R_DB2_DIAG 0   // diagnostic builds only (wrong output): bit 0 drops the output stores, bit 1 fetches MB 0
+#endif
+extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_deblock2(
     h264r_batch b, const DbInfo* __restrict__ dbinfo, uint64_t* hb, int* sync, int* err, uint32_t epoch, int2 rows, int nx,
     const uint8_t* __restrict__ recon)
 {
     __shared__ UnitLds S[UNITS];
     const Geom g = make_geom(b.width_mbs, b.height_mbs);
     const int W = g.wmb, R0 = rows.x, R1 = rows.y;
-    const int ngroups = (b.num_pics + UNITS - 1) / UNITS;
+    const int ngroups = (b.num_pics + PICS - 1) / PICS;
+    const int nbands = (R1 - R0 + BAND - 1) / BAND;
     // nx == 1 (small grids, one-XCD partitions, H264R_DB2_XCD=0): one counter, write-through
     // records, any wave on any XCD
 #if !H264R_DB2_XCD
@@ -123,147 +149,120 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2
     const int ngx = (ngroups - xcc + nx - 1) / nx;           // groups xcc, xcc + nx, ...
     int* counter = &sync[xcc];
     const bool local = nx > 1;                                // records: plain stores, kept in the XCD's L2
-    const int items = ngx * (R1 - R0);
+    const int items = ngx * nbands;
     for (;;) {
     __syncthreads();                                          // the previous item's LDS reads are done
     int tk = 0;
     if (threadIdx.x == 0) tk = atomicAdd(counter, 1);
     const int ticket = __builtin_amdgcn_readfirstlane(tk);
     if (ticket >= items) {
-        xcd_drain_check(sync, sync + 8, nx, [&](int k) { return (ngroups - k + nx - 1) / nx * (R1 - R0); }, err);
+        xcd_drain_check(sync, sync + 8, nx, [&](int k) { return (ngroups - k + nx - 1) / nx * nbands; }, err);
         return;
     }
-    const int ry = ticket / ngx, grp = (ticket - ry * ngx) * nx + xcc;
+    const int band = ticket / ngx, grp = (ticket - band * ngx) * nx + xcc;
     // lane, opaque per item: what derives from it is recomputed per item, not hoisted out of
-    // the ticket loop and kept live across it (that spilled 31 VGPRs)
+    // the ticket loop and kept live across it
     int lane = threadIdx.x;
     asm volatile("" : "+v"(lane));
     const int u = lane >> 2, q = lane & 3;
-    const int y = R0 + ry;
-    const int pic_raw = grp * UNITS + u;
-    const bool active = pic_raw < b.num_pics;
-    const int pic = active ? pic_raw : b.num_pics - 1;
+    const int rb = u / PICS, pu = u - rb * PICS;              // row in the band, picture in the group
+    const int y = R0 + band * BAND + rb;
+    const int pic0 = grp * PICS, npg = min(PICS, b.num_pics - pic0);
+    const bool active = pu < npg && y < R1;                  // units past the batch or the rows: no MB
+    const int pic = pic0 + min(pu, npg - 1), yc = min(y, R1 - 1);
     const bool above = y > R0, last_row = y == R1 - 1;
-    // records live in two slots per picture (rows alternate); the tag names launch and row
-    const uint32_t tag32 = (epoch << 12) | ((uint32_t)ry & 0xFFFu);
-    const uint64_t tag_in = (uint64_t)((epoch << 12) | ((uint32_t)(ry - 1) & 0xFFFu)) << 32;   // rows alternate slots
+    // records live in two slots per picture (bands alternate); the tag names launch and band
+    const uint32_t tag32 = (epoch << 12) | ((uint32_t)band & 0xFFFu);
+    const uint64_t tag_in = (uint64_t)((epoch << 12) | ((uint32_t)(band - 1) & 0xFFFu)) << 32;
+    const bool polls = active && rb == 0 && above;            // the band above's records
+    const bool publishes = active && rb == BAND - 1 && !last_row;
 
     UnitLds& U = S[u];
-    const size_t Wl = (size_t)g.W, Wc = (size_t)g.Wc;
-    uint8_t* Y = b.out_y + (size_t)pic * g.ysz + (size_t)(y * 16) * Wl;               // MB row y
-    uint8_t* Cb = b.out_u + (size_t)pic * g.csz + (size_t)(y * 8) * Wc;
-    uint8_t* Cr = b.out_v + (size_t)pic * g.csz + (size_t)(y * 8) * Wc;
+    const UnitLds& A = S[rb ? u - PICS : u];                  // the unit of the row above (rb > 0)
+    const uint32_t Wl = (uint32_t)g.W, Wc = (uint32_t)g.Wc;
+    const uint32_t ysz = (uint32_t)g.ysz, csz = (uint32_t)g.csz;
+    // the group's output planes through wave-uniform descriptors; per-lane byte offsets of
+    // row 0 of MB row y (OOB for units without an MB)
+    const __amdgpu_buffer_rsrc_t rY = __builtin_amdgcn_make_buffer_rsrc(b.out_y + (size_t)pic0 * g.ysz, 0, (int)(npg * ysz), RSRC_W3);
+    const __amdgpu_buffer_rsrc_t rU = __builtin_amdgcn_make_buffer_rsrc(b.out_u + (size_t)pic0 * g.csz, 0, (int)(npg * csz), RSRC_W3);
+    const __amdgpu_buffer_rsrc_t rV = __builtin_amdgcn_make_buffer_rsrc(b.out_v + (size_t)pic0 * g.csz, 0, (int)(npg * csz), RSRC_W3);
+    const uint32_t yrow = active ? (uint32_t)(pic - pic0) * ysz + (uint32_t)y * 16u * Wl : OOB;
+    const uint32_t crow = active ? (uint32_t)(pic - pic0) * csz + (uint32_t)y * 8u * Wc : OOB;
     const int p = q >> 1, d = q & 1;                                                    // my chroma plane / dword
-    uint8_t* Cp = p ? Cr : Cb;
-    const v4u* info_row = reinterpret_cast<const v4u*>(dbinfo + (size_t)pic * g.nmb + (size_t)y * W);
+    const v4u* info_row = reinterpret_cast<const v4u*>(dbinfo + (size_t)pic * g.nmb + (size_t)yc * W);
     // byte offsets of this unit's record rows in hb, through one wave-uniform descriptor
     const uint32_t hb_bytes = (uint32_t)b.num_pics * 2u * (uint32_t)W * RECG * 8u;
-    const __amdgpu_buffer_rsrc_t hrs = __builtin_amdgcn_make_buffer_rsrc(hb, 0, hb_bytes, 0x00020000);
-    const uint32_t rec_out = (uint32_t)(((size_t)pic * 2 + (ry & 1)) * W * RECG * 8);
-    const uint32_t rec_in = (uint32_t)(((size_t)pic * 2 + ((ry + 1) & 1)) * W * RECG * 8);
+    const __amdgpu_buffer_rsrc_t hrs = __builtin_amdgcn_make_buffer_rsrc(hb, 0, (int)hb_bytes, RSRC_W3);
+    const uint32_t rec_out = publishes ? (uint32_t)(((size_t)pic * 2 + (band & 1)) * W * RECG * 8) : OOB;
+    const uint32_t rec_in = polls ? (uint32_t)(((size_t)pic * 2 + ((band + 1) & 1)) * W * RECG * 8) : OOB;
     // pair k (granules 2k, 2k+1) of consumer lane c of MB m.  An MB's 12 pairs form three
-    // 64-byte blocks, each stored by ONE instruction of the unit's four lanes (one whole
-    // write-through segment instead of four partial ones): block 0 = the early pairs
-    // (0,0) (0,1) (0,2) (1,0), block 1 = the early (2,0) (2,1) (2,2) (1,1), block 2 = the
-    // late (1,2) (3,0) (3,1) (3,2).
-    // blk * 4 + slot of pair k of lane c, nibble 3c + k of PAIR_POS (a select chain on the lane's
-    // c compiled to a branch tree at every use)
+    // 64-byte blocks, each stored by ONE instruction of the unit's four lanes: block 0 =
+    // the early pairs (0,0) (0,1) (0,2) (1,0), block 1 = the early (2,0) (2,1) (2,2) (1,1),
+    // block 2 = the late (1,2) (3,0) (3,1) (3,2).  blk * 4 + slot of pair k of lane c is
+    // nibble 3c + k of PAIR_POS.
     constexpr uint64_t PAIR_POS = 0xba9654873210ull;
     auto pair_off = [&](uint32_t base, int m, int c, int k) -> uint32_t {
         const uint32_t bs = (uint32_t)(PAIR_POS >> (4 * (c * 3 + k))) & 15u;
         return base + (uint32_t)(m * RECG) * 8u + bs * 16u;
     };
-    auto load_pair = [&](int m, int k) -> v4u {
-        return __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(hrs, pair_off(rec_in, m, q, k), 0, AUX_SC1));
-    };
 
-    // ---- window fetch: MBs m, m+1 -- 768 contiguous bytes of the MB-tiled reconstruction
-    // (device_common.h), 16 bytes per load: luma rows 2i + p of MB m + d, and the chroma
-    // chunk k = 4i + q (MB m + k / 8, plane (k / 4) & 1, rows 2 (k & 3) and 2 (k & 3) + 1)
-    const uint8_t* rrow = recon + ((size_t)pic * g.nmb + (size_t)y * W) * RECON_MB;
-    v4u wl[8], wc[4];
+    // ---- one MB of the MB-tiled reconstruction (device_common.h), 16 bytes per load:
+    // luma rows 4i + q, chroma chunks 4j + q (plane j, rows 2q and 2q + 1)
+    const uint8_t* rrow = recon + ((size_t)pic * g.nmb + (size_t)yc * W) * RECON_MB;
+    v4u wl[4], wc[2];
     auto fetch = [&](int m) {
-        const uint8_t* ma = rrow + (size_t)min(m + d, W - 1) * RECON_MB;
+#if H264R_DB2_DIAG & 2
+        m = 0;                           // diagnostic build: every fetch reads MB 0 (L2-resident)
+#endif
+        const uint8_t* ma = rrow + (size_t)min(max(m, 0), W - 1) * RECON_MB;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) wl[i] = load_global<v4u>(ma + (2 * i + p) * 16);
+        for (int i = 0; i < 4; ++i) wl[i] = load_global<v4u>(ma + (4 * i + q) * 16);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int k = 4 * i + q;
-            wc[i] = load_global<v4u>(rrow + (size_t)min(m + (k >> 3), W - 1) * RECON_MB + RECON_CB + (k & 7) * 16);
+        for (int j = 0; j < 2; ++j) wc[j] = load_global<v4u>(ma + RECON_CB + (4 * j + q) * 16);
+    };
+    auto fill = [&](int s) {                                                            // registers -> ring slot s
+#pragma unroll
+        for (int i = 0; i < 4; ++i) *reinterpret_cast<v4u*>(&U.y[4 * i + q][4 * s]) = wl[i];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            *reinterpret_cast<v2u*>(&U.c[j][2 * q][2 * s]) = wc[j].xy;
+            *reinterpret_cast<v2u*>(&U.c[j][2 * q + 1][2 * s]) = wc[j].zw;
         }
     };
-    auto fill = [&](int m) {                                                            // registers -> ring slots
-        const int sa = m % 3, sb = (m + 1) % 3, s = d ? sb : sa;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) *reinterpret_cast<v4u*>(&U.y[2 * i + p][4 * s]) = wl[i];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int k = 4 * i + q, sk = i < 2 ? sa : sb, pl = (k >> 2) & 1, r = 2 * (k & 3);
-            *reinterpret_cast<v2u*>(&U.c[pl][r][2 * sk]) = wc[i].xy;
-            *reinterpret_cast<v2u*>(&U.c[pl][r + 1][2 * sk]) = wc[i].zw;
-        }
-    };
-    // the fetch registers read on the paths that do not fill (the last window, a failed
-    // wait), so that no path reaches the loop head with their loads pending
-    auto consume_window = [&]() {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) asm volatile("" ::"v"(wl[i]));
-#pragma unroll
-        for (int i = 0; i < 4; ++i) asm volatile("" ::"v"(wc[i]));
-    };
-    // Stores are issued by every lane on every path (the same count whatever the lane or the
-    // picture), so that the waitcnt pass can count the operations younger than a load it
-    // waits for.  Rows the row below still changes (luma 13..15, chroma 7) become a second
-    // store of row 12 / 6 with the same bytes; units past the batch end store exactly what
-    // the unit of the picture they duplicate stores.
+    // Rows the row below still changes (luma 13..15, chroma 7) become a second store of row
+    // 12 / 6 with the same bytes.
     const int ylast = last_row ? 15 : 12, clast = last_row ? 7 : 6;
-    // final MBs m, m+1 (adjacent): luma rows as two 16-byte halves from a lane pair, chroma
-    // rows as two 8-byte halves
-    auto store_pair = [&](int m) {
-        const int sa = m % 3, sb = (m + 1) % 3, s = d ? sb : sa;
+    // final MB m (slot s): luma rows 4i + q; chroma instruction i: plane i / 2, row 4 (i & 1) + q
+    auto store_mb = [&](int m, int s, bool ok) {
+#if H264R_DB2_DIAG & 1
+        ok = false;                      // diagnostic build: output stores dropped
+#endif
+        const uint32_t yb = (ok ? yrow : OOB) + (uint32_t)max(m, 0) * 16u;
+        const uint32_t cb = (ok ? crow : OOB) + (uint32_t)max(m, 0) * 8u;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int r = min(2 * i + p, ylast);
-            *reinterpret_cast<v4u*>(Y + (size_t)r * Wl + (m + d) * 16) = *reinterpret_cast<const v4u*>(&U.y[r][4 * s]);
+        for (int i = 0; i < 4; ++i) {
+            const int r = min(4 * i + q, ylast);
+            st16(rY, yb + (uint32_t)r * Wl, *reinterpret_cast<const v4u*>(&U.y[r][4 * s]));
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const int pr = 4 * i + q, r = min(pr & 7, clast);
-            uint8_t* dst = (pr >> 3 ? Cr : Cb) + (size_t)r * Wc + m * 8;
-            *reinterpret_cast<v2u*>(dst) = *reinterpret_cast<const v2u*>(&U.c[pr >> 3][r][2 * sa]);
-            *reinterpret_cast<v2u*>(dst + 8) = *reinterpret_cast<const v2u*>(&U.c[pr >> 3][r][2 * sb]);
+            const int pl = i >> 1, r = min(4 * (i & 1) + q, clast);
+            st8(pl ? rV : rU, cb + (uint32_t)r * Wc, *reinterpret_cast<const v2u*>(&U.c[pl][r][2 * s]));
         }
     };
-    // one final MB: my luma rows 4q..4q+3 and chroma rows 4(q&1)..+3 of plane p
-    auto store_one = [&](int m) {
-        const int s = m % 3;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int r = min(4 * q + i, ylast);
-            *reinterpret_cast<v4u*>(Y + (size_t)r * Wl + m * 16) = *reinterpret_cast<const v4u*>(&U.y[r][4 * s]);
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int r = min(4 * d + i, clast);
-            *reinterpret_cast<v2u*>(Cp + (size_t)r * Wc + m * 8) = *reinterpret_cast<const v2u*>(&U.c[p][r][2 * s]);
-        }
-    };
-    // granule i of consumer lane c of MB m, from the ring: luma row 12+i dword c (i < 4),
-    // chroma plane c/2 row 2+i dword c&1 (i = 4, 5)
-    auto granule = [&](int m, int c, int i) -> uint32_t {
-        const int s = m % 3;
+    // granule i of consumer lane c of MB m in slot s: luma row 12+i dword c (i < 4), chroma
+    // plane c/2 row 2+i dword c&1 (i = 4, 5)
+    auto granule = [&](int s, int c, int i) -> uint32_t {
         return i < 4 ? U.y[12 + i][4 * s + c] : U.c[c >> 1][2 + i][2 * s + (c & 1)];
     };
-    // publish pair k of consumer lane c of MB m.  Pairs are final either after H(m) ("early":
-    // lanes 0 and 2, lane 1's pairs 0-1) or only after V(m+1) ("late": lane 1's pair 2 with
-    // chroma dword 1, lane 3's three with luma dword 3 / chroma dword 1).
-    auto publish_pair = [&](int m, int c, int k, uint32_t t) {
-        const v4u v = {granule(m, c, 2 * k), t, granule(m, c, 2 * k + 1), t};
-        const auto w = __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, v);
-        if (local) __builtin_amdgcn_raw_buffer_store_b128(w, hrs, pair_off(rec_out, m, c, k), 0, 0);
-        else __builtin_amdgcn_raw_buffer_store_b128(w, hrs, pair_off(rec_out, m, c, k), 0, AUX_SC1);
+    // publish pair k of consumer lane c of MB m (slot s).  Pairs are final either after H(m)
+    // ("early": lanes 0 and 2, lane 1's pairs 0-1) or only after V(m+1) ("late": lane 1's
+    // pair 2 with chroma dword 1, lane 3's three with luma dword 3 / chroma dword 1).
+    auto publish_pair = [&](uint32_t base, int m, int s, int c, int k) {
+        const v4u v = {granule(s, c, 2 * k), tag32, granule(s, c, 2 * k + 1), tag32};
+        if (local) st16(hrs, pair_off(base, m, c, k), v);
+        else st16<AUX_SC1>(hrs, pair_off(base, m, c, k), v);
     };
-    // early pairs: 8, block j slot q from lane q; late pairs: 4, block 2 slot q from lane q
     auto early_c = [&](int lq, int j) { return lq < 3 ? (j ? 2 : 0) : 1; };
     auto early_k = [&](int lq, int j) { return lq < 3 ? lq : j; };
     auto late_c = [&](int lq) { return lq == 0 ? 1 : 3; };
@@ -271,36 +270,42 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2
     // DbInfo of MB m: 5 pieces of 16 bytes, piece q and (every lane) piece 4
     v4u ninf[2];
     auto load_info = [&](int m) {
-        const v4u* src = info_row + (size_t)min(m, W - 1) * 5;
+        const v4u* src = info_row + (size_t)min(max(m, 0), W - 1) * 5;
         ninf[0] = src[q];
         ninf[1] = src[4];
     };
-    auto put_info = [&]() {
-        *reinterpret_cast<v4u*>(&U.info[4 * q]) = ninf[0];
-        *reinterpret_cast<v4u*>(&U.info[16]) = ninf[1];
+    auto put_info = [&](bool ok) {      // zeros (bS 0: no edge filtered) when there is no MB
+        const v4u z = {0u, 0u, 0u, 0u};
+        *reinterpret_cast<v4u*>(&U.info[4 * q]) = ok ? ninf[0] : z;
+        *reinterpret_cast<v4u*>(&U.info[16]) = ok ? ninf[1] : z;
     };
 
     TRACE(const unsigned long long tr_start = __builtin_amdgcn_s_memrealtime(); unsigned long long tph[4] = {0, 0, 0, 0};
           unsigned long long tm = __builtin_amdgcn_s_memtime();)
     bool ok = true;
-    fetch(0);
-    load_info(0);
-    fill(0);
-    put_info();
-    __syncthreads();
-    // one step; ODD is x's parity, known at each call site, so that a window's fetch (even
-    // step) and fill (odd step) sit in one loop iteration and no load is pending across
-    // the back edge (the waitcnt pass then needs no conservative waits)
-    auto step = [&](const int x, auto odd_tag) {
-        constexpr bool ODD = decltype(odd_tag)::value;
-        const int sc = x % 3, sl = (x + 2) % 3;
-        // 1. the record of MB (x, y-1) (checked after the vertical edges)
-        uint64_t rin[6];
-        if (above) {
+    // row rb filters MB x = s - rb at step s; steps -2 and -1 bring MBs 0 and 1 in, the last
+    // step (x = W on the band's last row) stores MB W-1
+    const int s0 = -2, s1 = W + BAND - 1;
+    int x = s0 - rb;
+    // the record of MB (m, y-1) from the band above, as {data, tag} granules (OOB: zeros)
+    uint64_t rin[6];
+    auto load_record = [&](int m) {
+        const uint32_t base = active && m >= 0 && m < W ? rec_in : OOB;
 #pragma unroll
-            for (int k = 0; k < 3; ++k) { const v4u v = load_pair(x, k); rin[2 * k] = v.x | (uint64_t)v.y << 32; rin[2 * k + 1] = v.z | (uint64_t)v.w << 32; }
+        for (int k = 0; k < 3; ++k) {
+            const v4u v = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(hrs, pair_off(base, max(m, 0), q, k), 0, AUX_SC1));
+            rin[2 * k] = v.x | (uint64_t)v.y << 32; rin[2 * k + 1] = v.z | (uint64_t)v.w << 32;
         }
-        load_info(x + 1);                        // (clamped) younger than the record loads: not waited for there
+    };
+    put_info(false);                     // the first step has no MB
+    wave_sync();
+    // the loads every step ends with, in the same order, so that the loop head sees one state
+    fetch(x + 1);
+    load_info(x + 1);
+    for (int s = s0; s <= s1; ++s, ++x) {
+        const bool xok = active && x >= 0 && x < W;
+        const int sl = (x + 1) & 1, sc = x & 1;          // slots of MBs x-1 and x
+        // 1. this MB's DbInfo
         uint32_t inf[20];
 #pragma unroll
         for (int k = 0; k < 5; ++k) {
@@ -311,7 +316,6 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2
         const uint32_t cpar[3] = {p ? inf[14] : inf[11], p ? inf[15] : inf[12], p ? inf[16] : inf[13]};
 
         // 2. vertical edges of MB x (deblock.cc:488-504)
-        uint32_t lcv[2];                         // chroma: left dwords of rows 4d+2+i after V(x)
         {
             // luma rows (4q + i, 4q + i + 2): bS of V edge e, segment q = byte 4e + q
             EdgeP ev[4];
@@ -319,11 +323,11 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2
             for (int e = 0; e < 4; ++e) ev[e] = edge_params(inf[8 + (e == 0 ? 0 : 2)], bs_pair(inf[e], q, q));
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
-                const int ra = 4 * q + i, rb = ra + 2;
-                uint32_t la = U.y[ra][4 * sl + 3], lb = U.y[rb][4 * sl + 3];
-                const v4u A = *reinterpret_cast<const v4u*>(&U.y[ra][4 * sc]);
-                const v4u B = *reinterpret_cast<const v4u*>(&U.y[rb][4 * sc]);
-                uint32_t a[4] = {A.x, A.y, A.z, A.w}, bb[4] = {B.x, B.y, B.z, B.w};
+                const int ra = 4 * q + i, rb2 = ra + 2;
+                uint32_t la = U.y[ra][4 * sl + 3], lb = U.y[rb2][4 * sl + 3];
+                const v4u Av = *reinterpret_cast<const v4u*>(&U.y[ra][4 * sc]);
+                const v4u Bv = *reinterpret_cast<const v4u*>(&U.y[rb2][4 * sc]);
+                uint32_t a[4] = {Av.x, Av.y, Av.z, Av.w}, bb[4] = {Bv.x, Bv.y, Bv.z, Bv.w};
                 s2 c[20];
 #pragma unroll
                 for (int k = 0; k < 4; ++k) c[k] = unpack2(la, lb, k);
@@ -338,23 +342,27 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2
 #pragma unroll
                 for (int k = 0; k < 4; ++k) pack4(c[4 + 4 * k], c[5 + 4 * k], c[6 + 4 * k], c[7 + 4 * k], a[k], bb[k]);
                 U.y[ra][4 * sl + 3] = la;
-                U.y[rb][4 * sl + 3] = lb;
+                U.y[rb2][4 * sl + 3] = lb;
                 *reinterpret_cast<v4u*>(&U.y[ra][4 * sc]) = (v4u){a[0], a[1], a[2], a[3]};
-                *reinterpret_cast<v4u*>(&U.y[rb][4 * sc]) = (v4u){bb[0], bb[1], bb[2], bb[3]};
+                *reinterpret_cast<v4u*>(&U.y[rb2][4 * sc]) = (v4u){bb[0], bb[1], bb[2], bb[3]};
             }
+            // the record of MB (x, y-1) from the band above, checked after the vertical edges
+            // (issued here rather than at the step head: live across the luma pass its registers
+            // spilled at three waves per SIMD)
+            load_record(x);
             // chroma plane p rows (4d + i, +2); chroma edge 0 = luma edge 0, edge 1 (col 4) =
             // luma edge 2; row j takes the bS of luma row 2j: segment j / 2 (deblock.cc:430-433, 460)
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
-                const int ra = 4 * d + i, rb = ra + 2;
+                const int ra = 4 * d + i, rb2 = ra + 2;
                 EdgeP ec[2];
 #pragma unroll
                 for (int e = 0; e < 2; ++e)
-                    ec[e] = edge_params(cpar[e == 0 ? 0 : 2], bs_pair(inf[2 * e], ra >> 1, rb >> 1));
-                uint32_t la = U.c[p][ra][2 * sl + 1], lb = U.c[p][rb][2 * sl + 1];
-                const v2u A = *reinterpret_cast<const v2u*>(&U.c[p][ra][2 * sc]);
-                const v2u B = *reinterpret_cast<const v2u*>(&U.c[p][rb][2 * sc]);
-                uint32_t a[2] = {A.x, A.y}, bb[2] = {B.x, B.y};
+                    ec[e] = edge_params(cpar[e == 0 ? 0 : 2], bs_pair(inf[2 * e], ra >> 1, rb2 >> 1));
+                uint32_t la = U.c[p][ra][2 * sl + 1], lb = U.c[p][rb2][2 * sl + 1];
+                const v2u Av = *reinterpret_cast<const v2u*>(&U.c[p][ra][2 * sc]);
+                const v2u Bv = *reinterpret_cast<const v2u*>(&U.c[p][rb2][2 * sc]);
+                uint32_t a[2] = {Av.x, Av.y}, bb[2] = {Bv.x, Bv.y};
                 s2 c[12];
 #pragma unroll
                 for (int k = 0; k < 4; ++k) c[k] = unpack2(la, lb, k);
@@ -366,55 +374,60 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2
                 pack4(c[4], c[5], c[6], c[7], a[0], bb[0]);
                 pack4(c[8], c[9], c[10], c[11], a[1], bb[1]);
                 U.c[p][ra][2 * sl + 1] = la;
-                U.c[p][rb][2 * sl + 1] = lb;
+                U.c[p][rb2][2 * sl + 1] = lb;
                 *reinterpret_cast<v2u*>(&U.c[p][ra][2 * sc]) = (v2u){a[0], a[1]};
-                *reinterpret_cast<v2u*>(&U.c[p][rb][2 * sc]) = (v2u){bb[0], bb[1]};
-                lcv[i] = lb;                     // chroma rows 6 + i (lanes with d = 1)
+                *reinterpret_cast<v2u*>(&U.c[p][rb2][2 * sc]) = (v2u){bb[0], bb[1]};
             }
         }
         TRACE({ const unsigned long long t2 = __builtin_amdgcn_s_memtime(); tph[0] += t2 - tm; tm = t2; })
-        // 3. what the next step needs, behind the record loads in issue order
-        if (!ODD) fetch(min(x + 2, W - 1));                                             // next window
 
-        // 4. the record of MB (x, y-1) from the row above: wait for this launch
-        if (above) {
-            auto ready = [&]() {
-                bool r = true;
+        // 4. the record of MB (x, y-1) from the band above: wait for this launch
+        auto ready = [&]() {
+            bool r = true;
 #pragma unroll
-                for (int i = 0; i < 6; ++i) r &= (rin[i] & 0xFFFFFFFF00000000ull) == tag_in;
-                return __builtin_amdgcn_readfirstlane(__all(r || !active)) != 0;   // wave-uniform
-            };
-            // the first check stands outside the re-poll loop, so that its wait covers the
-            // record loads only (the loads issued after them stay in flight)
-            if (!ready()) {
-                WaitClock wc;
-                do {
-                    __builtin_amdgcn_s_sleep(1);
-#pragma unroll
-                    for (int k = 0; k < 3; ++k) { const v4u v = load_pair(x, k); rin[2 * k] = v.x | (uint64_t)v.y << 32; rin[2 * k + 1] = v.z | (uint64_t)v.w << 32; }
-                    if (wait_give_up(err, wc)) {                 // bounded (device_common.h)
-                        ok = false;
-                        consume_window();
-                        return;
-                    }
-                } while (!ready());
+            for (int i = 0; i < 6; ++i) r &= (rin[i] & 0xFFFFFFFF00000000ull) == tag_in;
+            return __builtin_amdgcn_readfirstlane(__all(r || !(polls && xok))) != 0;   // wave-uniform
+        };
+        if (!ready()) {
+            // every reload is checked before any exit of the loop, so that no path leaves it
+            // with a load pending (the waitcnt pass would otherwise drain at the step head)
+            WaitClock wclk;
+            bool give_up = false;
+            for (;;) {
+                __builtin_amdgcn_s_sleep(1);
+                load_record(x);
+                if (ready()) break;
+                if (wait_give_up(err, wclk)) { give_up = true; break; }   // bounded (device_common.h)
             }
+            if (give_up) { ok = false; break; }
         }
-        // a band that starts below row 0 must not be filtered across its top edge (idc 1, or a
+        // a launch that starts below row 0 must not be filtered across its top edge (idc 1, or a
         // slice edge with idc 2): its top-edge strengths (bs[16..19] = info dword 4) are 0
-        if (y == R0 && R0 > 0 && __builtin_amdgcn_readfirstlane(__any(active && inf[4] != 0)))
+        if (R0 > 0 && band == 0 && __builtin_amdgcn_readfirstlane(__any(rb == 0 && xok && inf[4] != 0)))
             __hip_atomic_store(err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __syncthreads();
+        wave_sync();                             // V(x) of every unit is in LDS
         TRACE({ const unsigned long long t2 = __builtin_amdgcn_s_memtime(); tph[1] += t2 - tm; tm = t2; })
-        // the late pairs of MB x-1 (luma dword 3, chroma dword 1), final after V(x): one per
-        // lane.  At x = 0 the same store carries tag 0 -- never taken for ready -- onto MB 0's
-        // pair, which step 1 overwrites.
-        publish_pair(max(x - 1, 0), late_c(q), late_k(q), x ? tag32 : 0u);
+        // the late pairs of MB x-1 (luma dword 3, chroma dword 1), final after V(x) (at x = W:
+        // after H(W-1)): one per lane
+        publish_pair(active && x >= 1 && x <= W ? rec_out : OOB, max(x - 1, 0), sl, late_c(q), late_k(q));
+        // rows -4..-1 (chroma -2..-1) of MB x's top edge for rows 1.. of the band: the upper unit's
+        // left slot (the upper row is on MB x+1), read before that slot is refilled below
+        if (rb) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) rin[r] = A.y[12 + r][4 * sc + q];
+#pragma unroll
+            for (int r = 0; r < 2; ++r) rin[4 + r] = A.c[p][6 + r][2 * sc + d];
+        }
+        // 5. MB x-1 is final (V(x) done): it leaves the ring, and MB x+1 (fetched during the
+        // previous step) takes its slot with its DbInfo
+        store_mb(x - 1, sl, active && x >= 1 && x <= W);
+        wave_sync();                             // every lane has read slot sl
+        fill(sl);
+        put_info(active && x + 1 >= 0 && x + 1 < W);
 
-        // 5. horizontal edges of MB x (deblock.cc:506-535)
+        // 6. horizontal edges of MB x (deblock.cc:506-535); rows -4..-1 from the record
         uint32_t wy[20], wcv[10];
         {
-            // luma columns 4q .. 4q+3 (dword q), rows -4..15 (rows -4..-1: the record), pairs (j, j+2)
 #pragma unroll
             for (int r = 0; r < 4; ++r) wy[r] = (uint32_t)rin[r];
 #pragma unroll
@@ -464,58 +477,39 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2
         }
         TRACE({ const unsigned long long t2 = __builtin_amdgcn_s_memtime(); tph[2] += t2 - tm; tm = t2; })
 
-        // 6. publish / store what is final now: the 16 granules of MB x that MB x+1 cannot
-        // change, four per lane (at the row end the late ones are final too)
+        // 7. publish / store what is final now: the 16 granules of MB x that MB x+1 cannot
+        // change, four per lane; rows 13..15 (chroma 7) of MB (x, y-1)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) publish_pair(x, early_c(q, j), early_k(q, j), tag32);
-        if (x == W - 1) publish_pair(x, late_c(q), late_k(q), tag32);
-        if (above) {
-            // rows 13..15 of MB (x, y-1), my luma dword; chroma row 7 of my plane, my dword
+        for (int j = 0; j < 2; ++j) publish_pair(xok ? rec_out : OOB, max(x, 0), sc, early_c(q, j), early_k(q, j));
+        {
+#if H264R_DB2_DIAG & 1
+            const uint32_t yb = OOB + (uint32_t)max(x, 0) * 16u + 4u * (uint32_t)q;
+#else
+            const uint32_t yb = (xok && above ? yrow : OOB) + (uint32_t)max(x, 0) * 16u + 4u * (uint32_t)q;
 #pragma unroll
-            for (int r = 1; r < 4; ++r) *reinterpret_cast<uint32_t*>(Y - (size_t)(4 - r) * Wl + x * 16 + 4 * q) = wy[r];
-            *reinterpret_cast<uint32_t*>(Cp - Wc + x * 8 + 4 * d) = wcv[1];
+#endif
+            for (int r = 1; r < 4; ++r) st4(rY, yb - (uint32_t)(4 - r) * Wl, wy[r]);
+            const uint32_t cb = (xok && above ? crow : OOB) + (uint32_t)max(x, 0) * 8u + 4u * (uint32_t)d - Wc;
+            st4(rU, p ? OOB : cb, wcv[1]);
+            st4(rV, p ? cb : OOB, wcv[1]);
         }
-        __syncthreads();
-        if (ODD) {
-            if (x + 1 < W) {
-                // window switch: MBs x-2, x-1 are final and leave the ring; x+1, x+2 come in
-                store_pair(max(x - 2, 0));           // (x = 1: MB 1 again at x = 3)
-                __syncthreads();                     // every lane has read the slots fill() reuses
-                fill(x + 1);
-            } else {
-                consume_window();
-            }
-        }
-        put_info();                                  // (stale after the last MB: never read)
-        __syncthreads();
+        // 8. what the next step fills: MB x+2 and its DbInfo
+        fetch(x + 2);
+        load_info(x + 2);
+        wave_sync();                             // H(x) of every unit is in LDS
         TRACE({ const unsigned long long t2 = __builtin_amdgcn_s_memtime(); tph[3] += t2 - tm; tm = t2; })
-    };
-    // the back edge follows an odd step only: no path reaches the loop head with a load
-    // of the even step pending
-    for (int x = 0;; x += 2) {
-        step(x, std::false_type());
-        if (!ok || x + 1 >= W) break;
-        step(x + 1, std::true_type());
-        if (!ok || x + 2 >= W) break;
     }
-    if (ok) {
-        // the row end: the MBs the last window switch left in the ring (W-3 .. W-1 for even
-        // W, W-2 .. W-1 for odd W)
-        const int m0 = max(W - ((W & 1) ? 2 : 3), 0);
-        if (W - m0 == 3) { store_pair(m0); store_one(m0 + 2); }
-        else if (W - m0 == 2) store_pair(m0);
-        else store_one(m0);
-    } else if (!last_row) {                          // release the row below (the error is flagged)
-        for (int x = 0; x < W; ++x)
+    if (!ok) {
+        // release the band below (the error is flagged)
+        for (int m = 0; m < W; ++m)
             for (int k = 0; k < 3; ++k) {
                 const v4u v = {0u, tag32, 0u, tag32};
-                const auto w = __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, v);
-                if (local) __builtin_amdgcn_raw_buffer_store_b128(w, hrs, pair_off(rec_out, x, q, k), 0, 0);
-                else __builtin_amdgcn_raw_buffer_store_b128(w, hrs, pair_off(rec_out, x, q, k), 0, AUX_SC1);
+                if (local) st16(hrs, pair_off(rec_out, m, q, k), v);
+                else st16<AUX_SC1>(hrs, pair_off(rec_out, m, q, k), v);
             }
     }
-    // (indexed row-major over (row, group) whatever the XCD-local ticket numbering)
-    TRACE(const int tix = ry * ngroups + grp;
+    // (indexed band-major over (band, group) whatever the XCD-local ticket numbering)
+    TRACE(const int tix = band * ngroups + grp;
           if (lane == 0 && tix < (1 << 16)) {
         h264r_db2_trace[tix][0] = tr_start; h264r_db2_trace[tix][1] = __builtin_amdgcn_s_memrealtime();
         for (int i = 0; i < 4; ++i) h264r_db2_trace[tix][2 + i] = tph[i];

@@ -11,3 +11,9 @@
 #ifndef H264R_DBINFO_GROUPS
 #define H264R_DBINFO_GROUPS 8
 #endif
+
+// k_deblock2: MB rows per wave, walked in lock step one MB apart (k_deblock2.hip); the
+// wave's 16 (picture, row) units cover 16 / H264R_DB2_BAND pictures
+#ifndef H264R_DB2_BAND
+#define H264R_DB2_BAND 4
+#endif

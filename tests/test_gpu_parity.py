@@ -136,15 +136,17 @@ def _large_batch_vs_oracle(L, dec, cidx, W, H, n, nbase=8):
 @pytest.mark.parametrize("cidx", [2, 3])
 def test_gpu_large_batch_wide_rows(L, dec, cidx):
     """1080p-wide rows (W = 120 > 64) in a 256-picture batch of 32-row pictures: k_deblock2's
-    XCD-local mode (16 groups x 32 rows = 512 waves, 64 per XCD) and, all-intra, the walk's
+    XCD-local mode (64 groups of 4 pictures x 8 bands of 4 rows = 512 waves, 64 per XCD) and,
+    all-intra, the walk's
     coarse band hand-off publishing mid-row (gstep 64 < W); every picture checked."""
     _large_batch_vs_oracle(L, dec, cidx, 120, 32, 256)
 
 
 @pytest.mark.parametrize("cidx", [2, 3])
 def test_gpu_large_batch_xcd_groups(L, dec, cidx):
-    """464 CIF pictures (29 groups of 16 x 18 MB rows = 522 k_deblock2 waves): k_deblock2 in
-    its XCD-local mode (groups on XCD g % 8, plain-store records) and the walk's coarse
+    """464 CIF pictures (116 groups of 4 pictures x 5 bands of 4 MB rows, the last band 2 rows
+    = 580 k_deblock2 waves): k_deblock2 in its XCD-local mode (groups on XCD g % 8,
+    plain-store records) and the walk's coarse
     band hand-off (batches >= 128 pictures); every picture checked."""
     _large_batch_vs_oracle(L, dec, cidx, 22, 18, 464)
 
@@ -190,7 +192,8 @@ def test_gpu_batch_dense_intra_levels(L, dec):
 
 @pytest.mark.parametrize("n", [33, 70])
 def test_gpu_batch_picture_groups(L, dec, n):
-    """Batches spanning several 16-picture groups of k_deblock2 (the last one ragged) under
+    """Batches spanning several 4-picture groups of k_deblock2 (the last one ragged; 9 MB rows
+    = bands of 4, 4 and 1 row) under
     both schedules; flag 0 takes the default for these sizes (k_deblock, below
     H264R_DEBLOCK2_MIN) -- k_deblock2's default selection is covered by the large batches."""
     _batch_vs_oracle(L, dec, 3, 11, 9, n, deblocks=(0, A.DBG_DEBLOCK_MB, A.DBG_DEBLOCK_ROWS), pcm_permille=20)
