@@ -92,11 +92,17 @@ DEV void st16(__amdgpu_buffer_rsrc_t r, uint32_t off, v4u v)
 {
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, v), r, off, 0, AUX);
 }
+template <int AUX = 0>
 DEV void st8(__amdgpu_buffer_rsrc_t r, uint32_t off, v2u v)
 {
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned int, v), r, off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned int, v), r, off, 0, AUX);
 }
-DEV void st4(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t v) { __builtin_amdgcn_raw_buffer_store_b32(v, r, off, 0, 0); }
+template <int AUX = 0>
+DEV void st4(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t v) { __builtin_amdgcn_raw_buffer_store_b32(v, r, off, 0, AUX); }
+#ifndef H264R_DB2_OUT_AUX
+#define H264R_DB2_OUT_AUX 0                // cache policy of the output-plane stores (measurement knob)
+#endif
+constexpr int OUT_AUX = H264R_DB2_OUT_AUX;
 
 }  // namespace
 
@@ -242,12 +248,12 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int r = min(4 * i + q, ylast);
-            st16(rY, yb + (uint32_t)r * Wl, *reinterpret_cast<const v4u*>(&U.y[r][4 * s]));
+            st16<OUT_AUX>(rY, yb + (uint32_t)r * Wl, *reinterpret_cast<const v4u*>(&U.y[r][4 * s]));
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int pl = i >> 1, r = min(4 * (i & 1) + q, clast);
-            st8(pl ? rV : rU, cb + (uint32_t)r * Wc, *reinterpret_cast<const v2u*>(&U.c[pl][r][2 * s]));
+            st8<OUT_AUX>(pl ? rV : rU, cb + (uint32_t)r * Wc, *reinterpret_cast<const v2u*>(&U.c[pl][r][2 * s]));
         }
     };
     // granule i of consumer lane c of MB m in slot s: luma row 12+i dword c (i < 4), chroma
@@ -488,10 +494,10 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3
             const uint32_t yb = (xok && above ? yrow : OOB) + (uint32_t)max(x, 0) * 16u + 4u * (uint32_t)q;
 #pragma unroll
 #endif
-            for (int r = 1; r < 4; ++r) st4(rY, yb - (uint32_t)(4 - r) * Wl, wy[r]);
+            for (int r = 1; r < 4; ++r) st4<OUT_AUX>(rY, yb - (uint32_t)(4 - r) * Wl, wy[r]);
             const uint32_t cb = (xok && above ? crow : OOB) + (uint32_t)max(x, 0) * 8u + 4u * (uint32_t)d - Wc;
-            st4(rU, p ? OOB : cb, wcv[1]);
-            st4(rV, p ? cb : OOB, wcv[1]);
+            st4<OUT_AUX>(rU, p ? OOB : cb, wcv[1]);
+            st4<OUT_AUX>(rV, p ? cb : OOB, wcv[1]);
         }
         // 8. what the next step fills: MB x+2 and its DbInfo
         fetch(x + 2);

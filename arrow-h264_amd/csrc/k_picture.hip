@@ -157,6 +157,14 @@ DEV void walk_ticket(const h264r_batch& b, int* sync, int* err, Scratch* scratch
     publish(x, true);
     int seen = 0;                                            // progress of the row above, acquired
     while (x < g.wmb && ok) {
+        // the lane, opaque per MB: what derives from it is recomputed per MB, not hoisted out of
+        // the walk and kept live across it
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        // the MB's records and levels do not depend on the row above: in flight during the wait
+        IntraHead hd;
+        intra_head_records(b, g, pic, x, r, ln, hd);
+        const IntraLoads ld = intra_body_loads(b, pic, hd, ln);
         // gstep < 0: the host's wait test (H264R_DBG_WAIT_TEST) -- a need no row ever meets
         const int need = gstep < 0 ? g.wmb + 1 : min(x + 2, g.wmb);
 #ifdef H264R_TRACE_INTRA
@@ -167,23 +175,18 @@ DEV void walk_ticket(const h264r_batch& b, int* sync, int* err, Scratch* scratch
             else ok = wait_for<false>(&lprog[wave - 1], need, err, seen);
         }
         if (!ok) break;
+        hd.nb = intra_head_samples(g, pic, x, r, ln, recon);
 #ifdef H264R_TRACE_INTRA
         {
             const unsigned long long tw = __builtin_amdgcn_s_memrealtime(), c0 = __builtin_amdgcn_s_memtime();
             unsigned long long tph[5] = {c0, c0, c0, c0, c0};
-            intra_mb2(b, g, pic, x, r, lane, S, recon, tph);
+            intra_mb_compute(b, g, pic, x, r, ln, S, hd, ld, recon, tph);
             asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
             const unsigned long long wait = min((tw - t_wait0) , 0xFFFFFull);
             intra_trace_put(t_wait0, (1ull << 31) | (wait << 8) | (unsigned)row[x].mb_type, tph, c0, lane);
         }
 #else
-        {
-            // the lane, opaque per MB: what derives from it is recomputed per MB, not hoisted
-            // out of the walk and kept live across it
-            int ln = lane;
-            asm volatile("" : "+v"(ln));
-            intra_mb2(b, g, pic, x, r, ln, S, recon);
-        }
+        intra_mb_compute(b, g, pic, x, r, ln, S, hd, ld, recon);
 #endif
         dirty = true;
         x = next_intra(x + 1);

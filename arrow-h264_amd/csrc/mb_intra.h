@@ -368,60 +368,71 @@ DEV void intra_bypass_res(const h264r_mb& m, const int16_t* __restrict__ lv, int
 // a batch).
 struct IntraHead {
     uint32_t nb;                 // this lane's neighbour sample dword (masked)
-    uint32_t nw0[4], nw2[4];     // neighbour records A, B, C, D: dwords 0 (type, flags) and 2 (cbp_blks, slice)
+    uint32_t nw0, nw2;           // lanes 0..3: neighbour record A, B, C, D (lane k): dwords 0 (type, flags) and 2 (cbp_blks, slice)
+    bool nin;                    // lanes 0..3: that neighbour lies inside the picture
     h264r_mb m;
     int cip;
-    uint32_t nin;                // bit k: neighbour k inside the picture
 };
 
-DEV IntraHead intra_head(const h264r_batch& b, const Geom& g, int pic, int mbx, int mby, int lane, uint8_t* recon)
+// The neighbour samples of MB (mbx, mby) for this lane: written by other waves (the row
+// above) or by this one (the MB to the left), so loaded only once they are final.
+DEV uint32_t intra_head_samples(const Geom& g, int pic, int mbx, int mby, int lane, uint8_t* recon)
 {
-    IntraHead h;
-    const int a = mby * g.wmb + mbx;
-    const h264r_mb* mbs = b.mbs + (size_t)pic * g.nmb;
     const int X = mbx * 16, Y = mby * 16, Xc = mbx * 8, Yc = mby * 8;
     // ---- neighbour samples (in-picture addresses only; availability decides later which
     // of them are used): one dword load per lane (a left-column sample is the top byte of
     // the aligned dword that ends at x - 1; lanes with nothing to fetch read their own
     // MB's first row and drop it).  Loads in lane-divergent branches would each merge
     // through a copy whose vmcnt(0) serialises them.
-    {
-        // (MB-tiled reconstruction, device_common.h: a dword never crosses an MB)
-        const uint8_t* src = recon_mb(recon, g, pic, mby * g.wmb + mbx);
-        bool want = false, left = false;
-        if (lane < 7) {                                   // row above, x = -4..23
-            const int x = X - 4 + 4 * lane;
-            want = mby > 0 && x >= 0 && x < g.W;
-            src = want ? recon_y(recon, g, pic, x, Y - 1) : src;
-        } else if (lane < 23) {                           // left column
-            want = left = mbx > 0;
-            src = want ? recon_y(recon, g, pic, X - 4, Y + lane - 7) : src;
-        } else if (lane < 29) {                           // chroma rows above, x = -4..7
-            const int k = lane - 23, pl = k / 3, x = Xc - 4 + 4 * (k % 3);
-            want = mby > 0 && x >= 0;
-            src = want ? recon_c(recon, g, pic, pl, x, Yc - 1) : src;
-        } else if (lane < 45) {                           // chroma left columns
-            const int k = lane - 29, pl = k >> 3;
-            want = left = mbx > 0;
-            src = want ? recon_c(recon, g, pic, pl, Xc - 4, Yc + (k & 7)) : src;
-        }
-        const uint32_t w = *as_global(src);
-        h.nb = (w >> (left ? 24 : 0)) & (0u - (uint32_t)want);   // arithmetic, not a select: no branch
+    // (MB-tiled reconstruction, device_common.h: a dword never crosses an MB)
+    const uint8_t* src = recon_mb(recon, g, pic, mby * g.wmb + mbx);
+    bool want = false, left = false;
+    if (lane < 7) {                                   // row above, x = -4..23
+        const int x = X - 4 + 4 * lane;
+        want = mby > 0 && x >= 0 && x < g.W;
+        src = want ? recon_y(recon, g, pic, x, Y - 1) : src;
+    } else if (lane < 23) {                           // left column
+        want = left = mbx > 0;
+        src = want ? recon_y(recon, g, pic, X - 4, Y + lane - 7) : src;
+    } else if (lane < 29) {                           // chroma rows above, x = -4..7
+        const int k = lane - 23, pl = k / 3, x = Xc - 4 + 4 * (k % 3);
+        want = mby > 0 && x >= 0;
+        src = want ? recon_c(recon, g, pic, pl, x, Yc - 1) : src;
+    } else if (lane < 45) {                           // chroma left columns
+        const int k = lane - 29, pl = k >> 3;
+        want = left = mbx > 0;
+        src = want ? recon_c(recon, g, pic, pl, Xc - 4, Yc + (k & 7)) : src;
     }
+    const uint32_t w = *as_global(src);
+    return (w >> (left ? 24 : 0)) & (0u - (uint32_t)want);   // arithmetic, not a select: no branch
+}
+
+// The records of MB (mbx, mby) and its neighbours: immutable during a batch, so the walk
+// loads them (and the levels they point to) before it waits for the row above.  The
+// neighbour records A, B, C, D go to lanes 0..3 by one vector load each (as scalar loads
+// they took SGPRs the walk does not have: the compiler issued them one at a time, each
+// behind its own wait).
+DEV void intra_head_records(const h264r_batch& b, const Geom& g, int pic, int mbx, int mby, int lane, IntraHead& h)
+{
+    const int a = mby * g.wmb + mbx;
+    const h264r_mb* mbs = b.mbs + (size_t)pic * g.nmb;
     // neighbour records (get_neighbour + slice check + constrained intra,
     // intra_prediction.cc:142-168 / 629-651 / 753-777) and the MB record
-    h.nin = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int nx = mbx + (k == 0 || k == 3 ? -1 : (k == 2 ? 1 : 0)), ny = mby - (k == 0 ? 0 : 1);
-        const bool in = nx >= 0 && ny >= 0 && nx < g.wmb && ny < g.hmb;
-        h.nin |= (uint32_t)in << k;
-        const uint32_t* p = reinterpret_cast<const uint32_t*>(&mbs[in ? ny * g.wmb + nx : a]);
-        h.nw0[k] = ld_const(p);
-        h.nw2[k] = ld_const(p + 2);
-    }
+    const int k = lane & 3;
+    const int nx = mbx + (k == 0 || k == 3 ? -1 : (k == 2 ? 1 : 0)), ny = mby - (k == 0 ? 0 : 1);
+    h.nin = nx >= 0 && ny >= 0 && nx < g.wmb && ny < g.hmb;
+    const uint2 w = *reinterpret_cast<const uint2*>(&mbs[h.nin ? ny * g.wmb + nx : a]);   // dwords 0, 1
+    h.nw0 = w.x;
+    h.nw2 = reinterpret_cast<const uint32_t*>(&mbs[h.nin ? ny * g.wmb + nx : a])[2];
     h.cip = ld_const(&b.pics[pic].constrained_intra_pred);
     h.m = load_mb_const(&mbs[a]);
+}
+
+DEV IntraHead intra_head(const h264r_batch& b, const Geom& g, int pic, int mbx, int mby, int lane, uint8_t* recon)
+{
+    IntraHead h;
+    h.nb = intra_head_samples(g, pic, mbx, mby, lane, recon);
+    intra_head_records(b, g, pic, mbx, mby, lane, h);
     return h;
 }
 
@@ -446,10 +457,11 @@ DEV void intra_mb_compute(const h264r_batch& b, const Geom& g, int pic, int mbx,
                          ((uint64_t)reinterpret_cast<const uint32_t*>(&m)[6] << 32);
     if (!mb_is_intra(m) || m.mb_type == H264R_I_PCM) return;
     INTRA_STAMP(0);
-    auto avail = [&](int k) -> int {
-        return ((hd.nin >> k) & 1) && (int)(hd.nw2[k] >> 16) == (int)m.slice && !(hd.cip && !((hd.nw0[k] >> 8) & H264R_MBF_INTRA));
-    };
-    const int avA = avail(0), avB = avail(1), avC = avail(2), avD = avail(3);
+    // availability of neighbour k from lane k's record, all four in one mask (wave-uniform)
+    const bool av = lane < 4 && hd.nin && (int)(hd.nw2 >> 16) == (int)m.slice &&
+                    !(hd.cip && !((hd.nw0 >> 8) & H264R_MBF_INTRA));
+    const uint32_t avm = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)__ballot(av));
+    const int avA = avm & 1, avB = (avm >> 1) & 1, avC = (avm >> 2) & 1, avD = (avm >> 3) & 1;
     const bool i16 = m.mb_type == H264R_I_16x16, i8 = m.mb_type == H264R_I_8x8;
 
     // ---- residual (registers; 8x8 via LDS; lossless MBs via LDS)
