@@ -421,7 +421,8 @@ def main() -> int:
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--latency-pictures", type=int, default=32,
                     help="length of the dependent-chain latency run (rank 0, N=1; 0 = skip)")
-    ap.add_argument("--traffic-json", default=None, help="PMC traffic summary (default profiles/traffic.json)")
+    ap.add_argument("--traffic-json", default=None, help="PMC traffic summary (default profiles/traffic.json, "
+                    "profiles/traffic_c<config>.json for other configs when present)")
     ap.add_argument("--chain", type=int, default=0,
                     help="chain mode with this many chains in all (even); default chains-per-gpu x N")
     ap.add_argument("--chains-per-gpu", type=int, default=32,
@@ -685,6 +686,8 @@ def main() -> int:
     traffic, traffic_src, ktraffic = None, None, [None, None, None]
     kvalu = [None, None, None]
     tpath = args.traffic_json or os.path.join(ROOT, "profiles", "traffic.json")
+    if not args.traffic_json and args.config != 3 and os.path.exists(os.path.join(ROOT, "profiles", f"traffic_c{args.config}.json")):
+        tpath = os.path.join(ROOT, "profiles", f"traffic_c{args.config}.json")
     if os.path.exists(tpath):
         tj = json.load(open(tpath))
         if tj.get("survey_config", 3) == args.config:
