@@ -247,7 +247,7 @@ struct Knobs {
     int debug = 0;             // H264R_DEBUG: schedule flags of h264r_set_debug OR-ed into every launch
     uint32_t wait_ticks = 0;   // H264R_WAIT_MS: bound of every device-side wait (below)
     int levels = 16;           // H264R_LEVELS: dependency levels from lists (level_launches)
-    int deblock2_min = 192;    // H264R_DEBLOCK2_MIN: batches from this size deblock with k_deblock2
+    int deblock2_min = 192;    // H264R_DEBLOCK2_MIN: batches of this many 68-row pictures' worth of MB rows deblock with k_deblock2
     int lvl_margin = 1;        // H264R_LVL_MARGIN: k_intra_levels' grid, blocks per CU below occupancy
     bool coop = true;          // H264R_COOP: k_intra_levels by hipLaunchCooperativeKernel
     int walk_gstep = 0;        // H264R_WALK_GSTEP: the walk's band hand-off period (0: by batch size)
@@ -463,7 +463,11 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
     // deblocking kernel (or k_untile) turns them into the output planes
     if ((st = dev_resize(&X.d_recon, &X.c_recon, (size_t)P * W * H * 384))) return st;
     uint8_t* recon = X.d_recon;
-    const bool by_rows = (c->debug & H264R_DBG_DEBLOCK_ROWS) || (!(c->debug & H264R_DBG_DEBLOCK_MB) && P >= K.deblock2_min);
+    // k_deblock2 needs many (picture group, band) walks in flight: H264R_DEBLOCK2_MIN is the
+    // crossover measured on whole 1080p pictures (68 MB rows), so a launch qualifies by its
+    // picture-rows (a 2160p picture counts twice, a 17-row slice band a quarter)
+    const bool by_rows = (c->debug & H264R_DBG_DEBLOCK_ROWS) ||
+                         (!(c->debug & H264R_DBG_DEBLOCK_MB) && (int64_t)P * HB >= (int64_t)K.deblock2_min * 68);
     // hand-off records of the chosen deblocking kernel; fresh memory or a wrapping epoch
     // restarts from zeroed records, so no record may carry a live tag
     uint8_t** hb = by_rows ? &X.d_hb2 : &X.d_hb;

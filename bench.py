@@ -200,7 +200,7 @@ def chain_run(args, rank: int, world: int, local: int, cs, rehearse: bool, nchai
 
     * Every picture of a batch has its own DPB table (h264r_batch.ref_planes_stride): slot 0 =
       its chain's previous picture, slots 1.. = static references shared by all chains.  The
-      chains are split into two groups, one launch each per step.
+      chains form `--chain-groups` groups (default 1), one launch each per step.
     * A group keeps two output sets; step t decodes into set t % 2 and reads set (t+1) % 2 -- the
       previous step's output IS the reference, nothing is copied on a rank.
     * Each rank decodes its slice band (MB rows of whole slices, disable_deblocking_filter_idc 2:
@@ -208,9 +208,12 @@ def chain_run(args, rank: int, world: int, local: int, cs, rehearse: bool, nchai
       then the exchange brings in the rows of other bands its next motion compensation can reach:
       `halo` (default) = the rows within halo_mb_rows(max |mv_y|) of its band from the
       neighbouring ranks, point-to-point (RCCL send/recv over xGMI); `allgather` = every band of
-      every picture (one all-gather per group and step).  The exchange of one group (communication
-      stream) overlaps the decode of the other (decode stream); each is on its chains' dependency
-      path.  The slice walk this parallelises is slice_data.cc:640-650."""
+      every picture (one all-gather per group and step).  With two or more groups the exchange of
+      one group (communication stream) overlaps the decode of the next (decode stream); each is
+      on its chains' dependency path.  One group (the default) decodes all chains in one launch:
+      the deblocking walks, latency-bound at these batch sizes, then run side by side, which
+      outweighs hiding an exchange of a few MB rows.  The slice walk this parallelises is
+      slice_data.cc:640-650."""
     import torch
     import h264r
     from h264r import batch as B
@@ -222,14 +225,15 @@ def chain_run(args, rank: int, world: int, local: int, cs, rehearse: bool, nchai
     refs = synth.refpics(L, cfg)
     if not refs:
         raise SystemExit("chain mode needs inter pictures (configs 3, 4, 5)")
-    if nchains < 2 or nchains % 2:
-        raise SystemExit("chain mode takes an even number of chains >= 2")
-    nk = nchains // 2
+    ng = max(1, int(getattr(args, "chain_groups", 1) or 1))
+    if nchains < ng or nchains % ng:
+        raise SystemExit(f"chain mode takes a multiple of --chain-groups ({ng}) chains")
+    nk = nchains // ng
     nmb = W * H
     # distinct synthetic pictures: up to 16 per group (chains beyond reuse them; every chain
     # still decodes its own picture from its own reference every step)
     nbase = min(nk, 16)
-    base = [[synth.picture(L, cfg, g * 1000 + i) for i in range(nbase)] for g in range(2)]
+    base = [[synth.picture(L, cfg, g * 1000 + i) for i in range(nbase)] for g in range(ng)]
     srow = base[0][0].mbs["slice"].reshape(H, W)[:, 0]
     first = [0] + [r for r in range(1, H) if srow[r] != srow[r - 1]]
     bands = D.slice_bands(first, H, world) if world > 1 else [(0, H)]
@@ -246,7 +250,7 @@ def chain_run(args, rank: int, world: int, local: int, cs, rehearse: bool, nchai
     static = [[torch.from_numpy(np.concatenate([a.reshape(-1), np.zeros(slack, np.uint8)])).to("cuda") for a in r]
               for r in refs[1:]]
     groups = []
-    for g in range(2):
+    for g in range(ng):
         pics = [base[g][k % nbase] for k in range(nk)]
         # two output sets [nk][plane] + slack; set 1 starts as every chain's first reference
         sets = [[torch.zeros(nk * psz[k3] + slack, dtype=torch.uint8, device="cuda") for k3 in range(3)]
@@ -339,12 +343,12 @@ def chain_run(args, rank: int, world: int, local: int, cs, rehearse: bool, nchai
         dist.barrier()
     dt = time.perf_counter() - t0
     dec.check()
-    kern = np.array(dec.last_timing()) * 2 if band[1] > band[0] else np.zeros(4)   # two launches per step
+    kern = np.array(dec.last_timing()) * ng if band[1] > band[0] else np.zeros(4)  # ng launches per step
     dec.set_timing(False)
     if world > 1:
         dt = D.max_over_ranks(dt, device="cpu" if rehearse else "cuda")
     rd = wr = 0
-    for g in range(2):
+    for g in range(ng):
         for k in range(nk):
             r, w = synth.algo_bytes(L, base[g][k % nbase])
             rd, wr = rd + r, wr + w
@@ -353,7 +357,7 @@ def chain_run(args, rank: int, world: int, local: int, cs, rehearse: bool, nchai
     frac_rows = (band[1] - band[0]) / H
     step_bytes = int((rd + wr) * frac_rows)
     achieved = step_bytes / (kern[3] * 1e-3) / 1e9 if kern[3] > 0 else 0.0
-    xin = groups[0]["xch"].bytes_in() * 2 if world > 1 else 0
+    xin = groups[0]["xch"].bytes_in() * ng if world > 1 else 0
     del groups, dec
     torch.cuda.empty_cache()
     return {
@@ -364,19 +368,19 @@ def chain_run(args, rank: int, world: int, local: int, cs, rehearse: bool, nchai
         "config": {"workload": f"{CONFIG_NAMES[cfg_idx]}, {nchains} dependent chains ({nchains // world} per GPU; "
                                "each picture predicts from its chain's previous decoded picture)",
                    "survey_config": cfg_idx, "width_mbs": W, "height_mbs": H, "mode": "chain",
-                   "chains": nchains, "chains_per_gpu": nchains // world,
+                   "chains": nchains, "chains_per_gpu": nchains // world, "chain_groups": ng,
                    "parallelism": f"slices{world}" if world > 1 else "single",
                    "rows_this_rank": list(band), "bands": [list(b) for b in bands]},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": "h264r_decode_batch launch sequences of the two chain groups",
+                     "kernel": "h264r_decode_batch launch sequences of the chain groups (one per group)",
                      "kernel_ms": float(kern[3]), "kernel_algo_bytes": step_bytes,
                      "numerator": "SURVEY 8(d) R+W of this rank's band of the step's pictures"},
         "kernel_ms": {"inter": float(kern[0]), "intra": float(kern[1]), "deblock": float(kern[2]),
                       "batch_wall": float(kern[3])},
         "exchange": {"mode": exchange if world > 1 else None, "halo_mb_rows": halo, "max_abs_mvy_qpel": mvy,
                      "bytes_in_per_rank_per_step": xin,
-                     "ops_per_step": (0 if world == 1 else 2 * (1 if exchange == "allgather" else
+                     "ops_per_step": (0 if world == 1 else ng * (1 if exchange == "allgather" else
                                                                  len(groups_peers(bands, rank, halo))))},
         "cpu_baseline": None,
         "verified_vs_oracle": verified,
@@ -424,7 +428,11 @@ def main() -> int:
     ap.add_argument("--traffic-json", default=None, help="PMC traffic summary (default profiles/traffic.json, "
                     "profiles/traffic_c<config>.json for other configs when present)")
     ap.add_argument("--chain", type=int, default=0,
-                    help="chain mode with this many chains in all (even); default chains-per-gpu x N")
+                    help="chain mode with this many chains in all (a multiple of --chain-groups); "
+                         "default chains-per-gpu x N")
+    ap.add_argument("--chain-groups", type=int, default=1,
+                    help="chain mode: launches per step (groups of chains); with 2 or more the exchange of one "
+                         "group overlaps the decode of the next")
     ap.add_argument("--chains-per-gpu", type=int, default=32,
                     help="chain mode: chains per GPU (weak scaling: the job holds chains-per-gpu x N chains)")
     ap.add_argument("--exchange", choices=["halo", "allgather"], default="halo",
@@ -673,9 +681,10 @@ def main() -> int:
     # per-kernel split of the same 8(d) bytes (kernel_bytes: R to the reconstructing kernel,
     # W to deblocking; the parts add up to the path's bytes), over each kernel's own event time
     kbytes = [int(k * (band[1] - band[0]) / H) for k in kbytes_all]
-    # the library deblocks batches of >= H264R_DEBLOCK2_MIN pictures (default 192) with
-    # k_deblock2, smaller ones with k_deblock (include/h264r.h)
-    dbk = "k_deblock2" if npics >= int(os.environ.get("H264R_DEBLOCK2_MIN", "192")) else "k_deblock"
+    # the library deblocks launches of >= H264R_DEBLOCK2_MIN (default 192) x 68 picture-MB-rows
+    # with k_deblock2, smaller ones with k_deblock (include/h264r.h)
+    dbk = ("k_deblock2" if npics * (band[1] - band[0]) >= int(os.environ.get("H264R_DEBLOCK2_MIN", "192")) * 68
+           else "k_deblock")
     inter_k = ["k_dbinfo", "k_inter4r"]
     names = [" + ".join(inter_k), "intra (k_level + k_intra_levels + k_intra_pic)", dbk]
     kern_names = [inter_k + ["k_inter_sp"], ["k_level", "k_level_scan", "k_level_scatter", "k_intra_levels", "k_intra_pic"],

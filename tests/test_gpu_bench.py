@@ -5,7 +5,8 @@ The dependent-chain mode is the multi-GPU path with an exc
 dependency path: run here with one rank, and rehearsed with two ranks on the one GPU of the box
 (H264R_BENCH_REHEARSE=1: gloo in place of RCCL, which refuses two ranks on one device) -- the
 exchange moves real rows between processes, and chain 0's second picture (which read its first
-through the exchange) must equal the oracle's chain.  `bench.py --gpus 2` with no launcher starts
+through the exchange) must equal the oracle's chain.  The default is one group of chains per step;
+`--chain-groups 2` overlaps one group's exchange with the next one's decode.  `bench.py --gpus 2` with no launcher starts
 its two ranks itself."""
 import json
 import os
@@ -38,11 +39,13 @@ def test_gpu_bench_chain_one_rank():
 def test_gpu_bench_chain_two_ranks_rehearsal():
     d = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
               "--master-addr", "127.0.0.1", "--master-port", "29517", "bench.py", "--gpus", "2", "--config", "4",
-              "--chain", "4", "--steps", "2", "--warmup", "1", "--no-n1"], env={"H264R_BENCH_REHEARSE": "1"})
+              "--chain", "4", "--chain-groups", "2", "--steps", "2", "--warmup", "1", "--no-n1"],
+             env={"H264R_BENCH_REHEARSE": "1"})
     assert d["verified_vs_oracle"] is True
     assert d["n_gpus"] == 2 and d["config"]["bands"] == [[0, 34], [34, 68]]
+    assert d["config"]["chain_groups"] == 2          # the exchange of one group beside the next one's decode
     assert d["exchange"]["mode"] == "halo" and d["exchange"]["halo_mb_rows"] >= 1
-    assert d["exchange"]["ops_per_step"] == 2
+    assert d["exchange"]["ops_per_step"] == 2        # one peer, two groups
 
 
 def test_gpu_bench_gpus2_spawns_its_ranks():
@@ -52,6 +55,7 @@ def test_gpu_bench_gpus2_spawns_its_ranks():
              env={"H264R_BENCH_REHEARSE": "1"})
     assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "slices2"
     assert d["config"]["survey_config"] == 5 and d["config"]["mode"] == "chain" and d["config"]["chains"] == 4
+    assert d["config"]["chain_groups"] == 1 and d["exchange"]["ops_per_step"] == 1
     assert d["verified_vs_oracle"] is True
     assert d["distributed"]["ranks"] == 2 and d["distributed"]["backend"] == "gloo"
     assert d["same_mode_n1"]["verified_vs_oracle"] is True and d["same_mode_n1"]["chains"] == 2
