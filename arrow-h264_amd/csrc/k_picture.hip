@@ -94,7 +94,7 @@ DEV bool wait_for(int* counter, int need, int* err, int& seen)
 // One (band, picture) ticket: wave `wave` walks MB row r0 + wave of the band.
 // sync: [0] ticket counter, [1 ..] per (picture, row) progress; zeroed before every launch.
 template <typename Scratch>
-DEV void walk_ticket(const h264r_batch& b, int* sync, int* err, Scratch* scratch, int* lprog, int ticket,
+DEV void walk_ticket(const h264r_batch& b, int* sync, int* err, Scratch* scratch, const uint32_t* tap4, int* lprog, int ticket,
                      const uint16_t* __restrict__ lvl, int lmax, int2 rows, int gstep, uint8_t* recon)
 {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -180,13 +180,13 @@ DEV void walk_ticket(const h264r_batch& b, int* sync, int* err, Scratch* scratch
         {
             const unsigned long long tw = __builtin_amdgcn_s_memrealtime(), c0 = __builtin_amdgcn_s_memtime();
             unsigned long long tph[5] = {c0, c0, c0, c0, c0};
-            intra_mb_compute(b, g, pic, x, r, ln, S, hd, ld, recon, tph);
+            intra_mb_compute(b, g, pic, x, r, ln, S, tap4, hd, ld, recon, tph);
             asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
             const unsigned long long wait = min((tw - t_wait0) , 0xFFFFFull);
             intra_trace_put(t_wait0, (1ull << 31) | (wait << 8) | (unsigned)row[x].mb_type, tph, c0, lane);
         }
 #else
-        intra_mb_compute(b, g, pic, x, r, ln, S, hd, ld, recon);
+        intra_mb_compute(b, g, pic, x, r, ln, S, tap4, hd, ld, recon);
 #endif
         dirty = true;
         x = next_intra(x + 1);
@@ -202,12 +202,14 @@ extern "C" __global__ __launch_bounds__(64 * H264R_WALK_ROWS, H264R_WALK_WAVES) 
                                                               uint8_t* recon)
 {
     __shared__ IntraScratch scratch[WAVES];
+    __shared__ uint32_t tap4[INTRA4_TAPS];
     __shared__ int lprog[WAVES];
     __shared__ int ticket;
     if (threadIdx.x == 0) ticket = atomicAdd(&sync[0], 1);
     if (threadIdx.x < WAVES) lprog[threadIdx.x] = 0;
+    intra4_tap_fill(tap4, threadIdx.x, blockDim.x);
     __syncthreads();
-    walk_ticket(b, sync, err, scratch, lprog, ticket, lvl, lmax, rows, gstep, recon);
+    walk_ticket(b, sync, err, scratch, tap4, lprog, ticket, lvl, lmax, rows, gstep, recon);
 }
 
 // ------------------------------------------------------------ level schedule
@@ -409,6 +411,9 @@ extern "C" __global__ __launch_bounds__(256, H264R_LVL_WAVES) void k_intra_level
                                                                                 int lmax, int* lvsync, int* err, uint8_t* recon)
 {
     __shared__ IntraScratch scratch[4];
+    __shared__ uint32_t tap4[INTRA4_TAPS];
+    intra4_tap_fill(tap4, threadIdx.x, blockDim.x);
+    __syncthreads();
     const Geom g = make_geom(b.width_mbs, b.height_mbs);
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int nw = (int)gridDim.x * 4, gw = (int)blockIdx.x * 4 + wave;
@@ -423,7 +428,7 @@ extern "C" __global__ __launch_bounds__(256, H264R_LVL_WAVES) void k_intra_level
 #ifdef H264R_TRACE_INTRA
             const unsigned long long t0 = __builtin_amdgcn_s_memrealtime(), c0 = __builtin_amdgcn_s_memtime();
             unsigned long long tph[5] = {c0, c0, c0, c0, c0};
-            intra_mb2(b, g, pic, a % g.wmb, a / g.wmb, lane, scratch[wave], recon, tph);
+            intra_mb2(b, g, pic, a % g.wmb, a / g.wmb, lane, scratch[wave], tap4, recon, tph);
             asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
             const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
             if (lane == 0) {
@@ -443,7 +448,7 @@ extern "C" __global__ __launch_bounds__(256, H264R_LVL_WAVES) void k_intra_level
 #else
             int ln = lane;                                 // opaque per MB (see walk_ticket)
             asm volatile("" : "+v"(ln));
-            intra_mb2(b, g, pic, a % g.wmb, a / g.wmb, ln, scratch[wave], recon);
+            intra_mb2(b, g, pic, a % g.wmb, a / g.wmb, ln, scratch[wave], tap4, recon);
 #endif
         }
         if (L < top && !grid_barrier(&lvsync[0], L * (int)gridDim.x, err)) return;

@@ -105,6 +105,30 @@ DEV int intra_tap_entry(const uint32_t (&t)[3], int mode)
     return (w >> (8 * (mode & 3))) & 255;
 }
 
+// The I_4x4 taps as tile offsets, one table per workgroup in LDS (INTRA4_TAPS uint32):
+// entry mode * 32 + tv * 16 + (y * 4 + x) holds, for sample (x, y) of a 4x4 block in
+// directional mode `mode`, the tile offsets (from the block origin, int8) of e[i - 1],
+// e[i], e[i + 1] in bytes 0..2 and the kind in byte 3 (intra_nxn_tap<4>); tv = 1 when the
+// block's upper-right neighbours are available (the row above reaches x = 7, else it
+// stops at 3).  e[k]: the left column bottom-up for k <= 5 (the corner at 5), then the row
+// above.  DC entries are 0.
+constexpr int INTRA4_TAPS = 9 * 2 * 16;
+DEV void intra4_tap_fill(uint32_t* tap4, int tid, int nthreads)
+{
+    for (int e = tid; e < INTRA4_TAPS; e += nthreads) {
+        const int mode = e >> 5, tmax = (e & 16) ? 7 : 3, x = e & 3, y = (e >> 2) & 3;
+        uint32_t v = 0;
+        if (mode != 2) {
+            int kind, i;
+            intra_nxn_tap<4>(mode, x, y, kind, i);
+            auto eoff = [&](int k) -> int { return k <= 5 ? (3 - max(k - 1, 0)) * ITP - 1 : min(k - 6, tmax) - ITP; };
+            v = (uint32_t)(uint8_t)eoff(max(i - 1, 0)) | ((uint32_t)(uint8_t)eoff(i) << 8) |
+                ((uint32_t)(uint8_t)eoff(min(i + 1, 14)) << 16) | ((uint32_t)kind << 24);
+        }
+        tap4[e] = v;
+    }
+}
+
 // kind 0 / 1 / 2 of intra_nxn_tap: all three forms, one kept by masks (a ternary chain on the
 // lane's kind compiled to a tree of lane-divergent branches)
 DEV int tap_apply(int kind, int a, int b, int c)
@@ -445,7 +469,8 @@ DEV IntraLoads intra_body_loads(const h264r_batch& b, int pic, const IntraHead& 
 // wave.  tph (trace builds): s_memtime at the phase boundaries [record known, residual,
 // tiles, prediction, end].
 DEV void intra_mb_compute(const h264r_batch& b, const Geom& g, int pic, int mbx, int mby, int lane, IntraScratch& S,
-                          const IntraHead& hd, const IntraLoads& ld, uint8_t* recon, unsigned long long* tph = nullptr)
+                          const uint32_t* tap4, const IntraHead& hd, const IntraLoads& ld, uint8_t* recon,
+                          unsigned long long* tph = nullptr)
 {
 #define INTRA_STAMP(k) do { if (tph) tph[k] = __builtin_amdgcn_s_memtime(); } while (0)
     uint8_t* const rmb = recon_mb(recon, g, pic, mby * g.wmb + mbx);      // MB-tiled (device_common.h)
@@ -593,53 +618,52 @@ DEV void intra_mb_compute(const h264r_batch& b, const Geom& g, int pic, int mbx,
         // each slot's block, availability and mode are wave-uniform (scalar) and a lane only
         // selects between the two slots' values; every per-lane expression is a select, not a
         // branch (a lane-divergent branch runs both sides anyway, plus the exec-mask work).
-        uint32_t tab[3];
-        intra_tap_table<4>(lane & 3, (lane >> 2) & 3, tab);
+        // A sample's three e[] taps come as tile offsets from the workgroup's table (tap4:
+        // intra4_tap_fill), the DC sums and the directional taps each run only when a slot of
+        // the step needs them (scalar branches on the two modes).
         const int slot = (lane >> 4) & 1, x = lane & 3, y = (lane >> 2) & 3;
         const bool half = lane < 32;
+        const int soff = y * ITP + x, roff = y * 16 + x, pos = lane & 15;
 #pragma unroll
         for (int s = 0; s < 10; ++s) {
             // compile-time block coordinates of the two slots
             const int by0 = (s >> 1) - 1, bx0 = (s & 1) + 2, by1 = s >> 1, bx1 = s & 1;
             const bool ok0 = by0 >= 0, ok1 = by1 <= 3;
-            auto blk_par = [&](int bx, int by, int& mode, int& aA, int& aB, int& tmax, int& base) {
+            auto blk_par = [&](int bx, int by, int& mode, int& aA, int& aB, int& tv) {
                 const int xO = bx * 4, yO = by * 4;
                 const int bk = (by >> 1) * 8 + (bx >> 1) * 4 + (by & 1) * 2 + (bx & 1);   // blkIdx
                 aA = xO > 0 ? 1 : avA;
                 aB = yO > 0 ? 1 : avB;
-                const int aC = yO == 0 ? (xO + 4 < 16 ? avB : avC) : ((xO + 4 < 16) && !(xO == 4 && (yO == 4 || yO == 12)));   // :154
-                tmax = aC ? 7 : 3;
+                tv = yO == 0 ? (xO + 4 < 16 ? avB : avC) : ((xO + 4 < 16) && !(xO == 4 && (yO == 4 || yO == 12)));   // :154
                 mode = (int)((ipw >> (4 * bk)) & 15);
-                base = ti(xO, yO);
             };
-            int m0 = 2, a0 = 0, b0 = 0, t0 = 3, base0 = 0, m1 = 2, a1 = 0, b1 = 0, t1 = 3, base1 = 0;
-            if (ok0) blk_par(bx0, by0, m0, a0, b0, t0, base0);
-            if (ok1) blk_par(bx1, by1, m1, a1, b1, t1, base1);
+            // an absent slot: mode 0 (no DC work), its lanes read around an interior origin
+            int m0 = 0, a0 = 0, b0 = 0, t0 = 0, m1 = 0, a1 = 0, b1 = 0, t1 = 0;
+            if (ok0) blk_par(bx0, by0, m0, a0, b0, t0);
+            if (ok1) blk_par(bx1, by1, m1, a1, b1, t1);
+            const int base0 = ok0 ? ti(bx0 * 4, by0 * 4) : ti(4, 4), base1 = ok1 ? ti(bx1 * 4, by1 * 4) : ti(4, 4);
+            const int rb0 = ok0 ? by0 * 64 + bx0 * 4 : 0, rb1 = ok1 ? by1 * 64 + bx1 * 4 : 0;
             const bool on = half && (slot ? ok1 : ok0);
-            const int mode = slot ? m1 : m0, aA = slot ? a1 : a0, aB = slot ? b1 : b0;
-            const int tmax = slot ? t1 : t0, base = slot ? base1 : base0;
-            const int ent = intra_tap_entry(tab, mode), kind = ent >> 5, i = ent & 31;
-            // tile offset of e[k] from the block origin: the left column bottom-up (k <= 5, the
-            // corner at 5), then the row above clamped at tmax; both forms computed, one selected
-            auto eoff = [&](int k) -> int {
-                int l = (3 - max(k - 1, 0)) * ITP - 1, t = min(k - 6, tmax) - ITP;
-                asm volatile("" : "+v"(l), "+v"(t));
-                return k <= 5 ? l : t;
-            };
-            // lanes without a block read around an interior origin (every offset inside the tile)
-            const int pb = on ? base : ti(4, 4);
-            const int e0 = S.tile[pb + eoff(max(i - 1, 0))], e1 = S.tile[pb + eoff(i)];
-            const int e2 = S.tile[pb + eoff(min(i + 1, 14))];
-            const int st = sum4(lds_u32(&S.tile[pb - ITP]));       // DC (intra_prediction.cc:214-229)
-            const int sl = S.tile[pb - 1] + S.tile[pb + ITP - 1] + S.tile[pb + 2 * ITP - 1] + S.tile[pb + 3 * ITP - 1];
-            // DC by masks: the available sums, shifted by 2 or 3, 128 when neither side is
-            const int mA = -aA, mB = -aB, dsh = 1 + aA + aB;
-            const int dc = (((sl & mA) + (st & mB) + (1 << (dsh - 1))) >> dsh) + (128 & ~(mA | mB));
-            const int tp = tap_apply(kind, e0, e1, e2), m2 = -(int)(mode == 2);
-            const int p = tp ^ ((tp ^ dc) & m2);
-            // residual (0 in uncoded blocks) at tile position pb + y * ITP + x
-            const int v = clip255(p + S.res[(pb >> 5) - 1 + y][(pb & 31) - 4 + x]);
-            if (on) S.tile[pb + y * ITP + x] = (uint8_t)v;
+            const int mode = slot ? m1 : m0, pb = slot ? base1 : base0;
+            int tp = 0, dc = 0;
+            if (m0 != 2 || m1 != 2) {
+                const uint32_t ent = tap4[(slot ? m1 * 32 + t1 * 16 : m0 * 32 + t0 * 16) + pos];
+                const int e0 = S.tile[pb + (int)(int8_t)ent], e1 = S.tile[pb + (int)(int8_t)(ent >> 8)];
+                const int e2 = S.tile[pb + (int)(int8_t)(ent >> 16)];
+                tp = tap_apply((int)(ent >> 24), e0, e1, e2);
+            }
+            if (m0 == 2 || m1 == 2) {                                // DC (intra_prediction.cc:214-229)
+                const int aA = slot ? a1 : a0, aB = slot ? b1 : b0;
+                const int st = sum4(lds_u32(&S.tile[pb - ITP]));
+                const int sl = S.tile[pb - 1] + S.tile[pb + ITP - 1] + S.tile[pb + 2 * ITP - 1] + S.tile[pb + 3 * ITP - 1];
+                // by masks: the available sums, shifted by 2 or 3, 128 when neither side is
+                const int mA = -aA, mB = -aB, dsh = 1 + aA + aB;
+                dc = (((sl & mA) + (st & mB) + (1 << (dsh - 1))) >> dsh) + (128 & ~(mA | mB));
+            }
+            const int p = mode == 2 ? dc : tp;
+            // residual (0 in uncoded blocks)
+            const int v = clip255(p + (&S.res[0][0])[(slot ? rb1 : rb0) + roff]);
+            if (on) S.tile[pb + soff] = (uint8_t)v;
             wave_sync();
         }
     }
@@ -694,12 +718,12 @@ DEV void intra_mb_compute(const h264r_batch& b, const Geom& g, int pic, int mbx,
 
 // Loads then reconstruction of one intra MB (the walk, k_intra_pic).
 DEV void intra_mb2(const h264r_batch& b, const Geom& g, int pic, int mbx, int mby, int lane, IntraScratch& S,
-                   uint8_t* recon, unsigned long long* tph = nullptr)
+                   const uint32_t* tap4, uint8_t* recon, unsigned long long* tph = nullptr)
 {
     const IntraHead hd = intra_head(b, g, pic, mbx, mby, lane, recon);
     if (!mb_is_intra(hd.m) || hd.m.mb_type == H264R_I_PCM) return;
     const IntraLoads ld = intra_body_loads(b, pic, hd, lane);
-    intra_mb_compute(b, g, pic, mbx, mby, lane, S, hd, ld, recon, tph);
+    intra_mb_compute(b, g, pic, mbx, mby, lane, S, tap4, hd, ld, recon, tph);
 }
 
 }  // namespace h264r
