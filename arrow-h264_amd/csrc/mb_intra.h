@@ -624,11 +624,13 @@ DEV void intra_mb_compute(const h264r_batch& b, const Geom& g, int pic, int mbx,
         const int slot = (lane >> 4) & 1, x = lane & 3, y = (lane >> 2) & 3;
         const bool half = lane < 32;
         const int soff = y * ITP + x, roff = y * 16 + x, pos = lane & 15;
-#pragma unroll
-        for (int s = 0; s < 10; ++s) {
-            // compile-time block coordinates of the two slots
+        // the two slots of step s: block coordinates (compile time), mode, availability (scalar);
+        // an absent slot has mode 0 (no DC work) and reads around an interior origin
+        struct StepPar { bool ok0, ok1; int m0, a0, b0, t0, m1, a1, b1, t1, base0, base1, rb0, rb1; };
+        auto step_par = [&](int s) -> StepPar {
+            StepPar q;
             const int by0 = (s >> 1) - 1, bx0 = (s & 1) + 2, by1 = s >> 1, bx1 = s & 1;
-            const bool ok0 = by0 >= 0, ok1 = by1 <= 3;
+            q.ok0 = by0 >= 0; q.ok1 = by1 <= 3;
             auto blk_par = [&](int bx, int by, int& mode, int& aA, int& aB, int& tv) {
                 const int xO = bx * 4, yO = by * 4;
                 const int bk = (by >> 1) * 8 + (bx >> 1) * 4 + (by & 1) * 2 + (bx & 1);   // blkIdx
@@ -637,23 +639,36 @@ DEV void intra_mb_compute(const h264r_batch& b, const Geom& g, int pic, int mbx,
                 tv = yO == 0 ? (xO + 4 < 16 ? avB : avC) : ((xO + 4 < 16) && !(xO == 4 && (yO == 4 || yO == 12)));   // :154
                 mode = (int)((ipw >> (4 * bk)) & 15);
             };
-            // an absent slot: mode 0 (no DC work), its lanes read around an interior origin
-            int m0 = 0, a0 = 0, b0 = 0, t0 = 0, m1 = 0, a1 = 0, b1 = 0, t1 = 0;
-            if (ok0) blk_par(bx0, by0, m0, a0, b0, t0);
-            if (ok1) blk_par(bx1, by1, m1, a1, b1, t1);
-            const int base0 = ok0 ? ti(bx0 * 4, by0 * 4) : ti(4, 4), base1 = ok1 ? ti(bx1 * 4, by1 * 4) : ti(4, 4);
-            const int rb0 = ok0 ? by0 * 64 + bx0 * 4 : 0, rb1 = ok1 ? by1 * 64 + bx1 * 4 : 0;
-            const bool on = half && (slot ? ok1 : ok0);
-            const int mode = slot ? m1 : m0, pb = slot ? base1 : base0;
+            q.m0 = q.a0 = q.b0 = q.t0 = q.m1 = q.a1 = q.b1 = q.t1 = 0;
+            if (q.ok0) blk_par(bx0, by0, q.m0, q.a0, q.b0, q.t0);
+            if (q.ok1) blk_par(bx1, by1, q.m1, q.a1, q.b1, q.t1);
+            q.base0 = q.ok0 ? ti(bx0 * 4, by0 * 4) : ti(4, 4);
+            q.base1 = q.ok1 ? ti(bx1 * 4, by1 * 4) : ti(4, 4);
+            q.rb0 = q.ok0 ? by0 * 64 + bx0 * 4 : 0;
+            q.rb1 = q.ok1 ? by1 * 64 + bx1 * 4 : 0;
+            return q;
+        };
+        // what a step reads that no step writes -- its table entry and residual sample -- is
+        // read during the step before, so a step waits on one LDS round trip (the tile reads)
+        auto step_ent = [&](const StepPar& q) -> uint32_t { return tap4[(slot ? q.m1 * 32 + q.t1 * 16 : q.m0 * 32 + q.t0 * 16) + pos]; };
+        auto step_res = [&](const StepPar& q) -> int { return (&S.res[0][0])[(slot ? q.rb1 : q.rb0) + roff]; };
+        uint32_t ent_next = step_ent(step_par(0));
+        int res_next = step_res(step_par(0));
+#pragma unroll
+        for (int s = 0; s < 10; ++s) {
+            const StepPar q = step_par(s);
+            const uint32_t ent = ent_next;
+            const int rv = res_next;
+            const bool on = half && (slot ? q.ok1 : q.ok0);
+            const int mode = slot ? q.m1 : q.m0, pb = slot ? q.base1 : q.base0;
             int tp = 0, dc = 0;
-            if (m0 != 2 || m1 != 2) {
-                const uint32_t ent = tap4[(slot ? m1 * 32 + t1 * 16 : m0 * 32 + t0 * 16) + pos];
+            if (q.m0 != 2 || q.m1 != 2) {
                 const int e0 = S.tile[pb + (int)(int8_t)ent], e1 = S.tile[pb + (int)(int8_t)(ent >> 8)];
                 const int e2 = S.tile[pb + (int)(int8_t)(ent >> 16)];
                 tp = tap_apply((int)(ent >> 24), e0, e1, e2);
             }
-            if (m0 == 2 || m1 == 2) {                                // DC (intra_prediction.cc:214-229)
-                const int aA = slot ? a1 : a0, aB = slot ? b1 : b0;
+            if (q.m0 == 2 || q.m1 == 2) {                            // DC (intra_prediction.cc:214-229)
+                const int aA = slot ? q.a1 : q.a0, aB = slot ? q.b1 : q.b0;
                 const int st = sum4(lds_u32(&S.tile[pb - ITP]));
                 const int sl = S.tile[pb - 1] + S.tile[pb + ITP - 1] + S.tile[pb + 2 * ITP - 1] + S.tile[pb + 3 * ITP - 1];
                 // by masks: the available sums, shifted by 2 or 3, 128 when neither side is
@@ -661,9 +676,13 @@ DEV void intra_mb_compute(const h264r_batch& b, const Geom& g, int pic, int mbx,
                 dc = (((sl & mA) + (st & mB) + (1 << (dsh - 1))) >> dsh) + (128 & ~(mA | mB));
             }
             const int p = mode == 2 ? dc : tp;
-            // residual (0 in uncoded blocks)
-            const int v = clip255(p + (&S.res[0][0])[(slot ? rb1 : rb0) + roff]);
+            const int v = clip255(p + rv);                           // residual: 0 in uncoded blocks
             if (on) S.tile[pb + soff] = (uint8_t)v;
+            if (s < 9) {
+                const StepPar qn = step_par(s + 1);
+                ent_next = step_ent(qn);
+                res_next = step_res(qn);
+            }
             wave_sync();
         }
     }
