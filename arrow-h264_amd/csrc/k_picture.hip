@@ -117,16 +117,24 @@ DEV void walk_ticket(const h264r_batch& b, int* sync, int* err, Scratch* scratch
     // none is left): MB x may start once the row above has progress >= x + 2.
     const h264r_mb* row = mbs + (size_t)r * g.wmb;
     const uint16_t* lrow = lvl ? lvl + (size_t)pic * g.nmb + (size_t)r * g.wmb : nullptr;
+    // (the row's intra bits are loaded once per 64-MB chunk and kept: records are immutable
+    // during a batch, so the walk does not reload them after every MB)
+    int cbase = -64;
+    uint64_t cbits = 0;
     auto next_intra = [&](int from) -> int {
         for (int c = from & ~63; c < g.wmb; c += 64) {
-            const int m = c + lane;
-            bool in = false;
-            if (m >= from && m < g.wmb) {
-                const uint32_t w0 = *reinterpret_cast<const uint32_t*>(&row[m]);
-                in = ((w0 >> 8) & H264R_MBF_INTRA) && (w0 & 255) != H264R_I_PCM;
-                if (lrow && lrow[m] <= lmax) in = false;      // done by k_intra_lvl
+            if (c != cbase) {
+                const int m = c + lane;
+                bool in = false;
+                if (m < g.wmb) {
+                    const uint32_t w0 = *reinterpret_cast<const uint32_t*>(&row[m]);
+                    in = ((w0 >> 8) & H264R_MBF_INTRA) && (w0 & 255) != H264R_I_PCM;
+                    if (lrow && lrow[m] <= lmax) in = false;      // done by k_intra_lvl
+                }
+                cbits = __ballot(in);
+                cbase = c;
             }
-            const uint64_t bits = __ballot(in);
+            const uint64_t bits = from > c ? cbits & (~0ull << (from - c)) : cbits;
             if (bits) return c + __builtin_ctzll(bits);
         }
         return g.wmb;
