@@ -291,14 +291,18 @@ DEV void luma_block_pred(const uint32_t (&w)[9][3], int W, int x, int xf, int yf
 // 2x2 chroma prediction samples at chroma integer position (xi, yi), eighth phase
 // (xf, yf): get_block_chroma inter_prediction.cc:380-404 with clamped coordinates.
 // Both planes; each plane's four samples as bytes (row 0 in bits 0..15, row 1 in 16..31).
+// A row's three clamped samples come out of its two dwords by one byte permute (the
+// selector computed once per lane), and the two samples of an output row are one packed
+// 16-bit sum: (8-xf)(8-yf) + xf(8-yf) + (8-xf)yf + xf yf = 64, so 255 * 64 + 32 fits.
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+DEV u16x2 as_u16x2(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
 DEV void chroma_block_pred2(const uint8_t* __restrict__ cb, const uint8_t* __restrict__ cr, int W, int H, int xi, int yi,
                             int xf, int yf, uint32_t (&out)[2])
 {
     const int a = clip3(0, W - 1, xi) & ~3;
-    // both planes' three rows first (12 dwords in flight), then byte selection without
-    // branches: a lane-divergent interior / edge split made every row's load wait for the
-    // previous row's use, and one plane at a time left the second plane's last row behind a
-    // full vmcnt wait
+    // both planes' three rows first (12 dwords in flight): a lane-divergent interior / edge
+    // split made every row's load wait for the previous row's use, and one plane at a time
+    // left the second plane's last row behind a full vmcnt wait
     uint32_t w[2][3][2];
 #pragma unroll
     for (int pl = 0; pl < 2; ++pl)
@@ -308,30 +312,29 @@ DEV void chroma_block_pred2(const uint8_t* __restrict__ cb, const uint8_t* __res
             w[pl][k][0] = q[0];
             w[pl][k][1] = q[1];
         }
-    int sh[3];
-    bool hi[3];
+    // byte c (c = 0..2) of the selector: the clamped column's byte in {dword 0 (0..3), dword 1
+    // (4..7)}; byte 3 reads zero
+    uint32_t sel = 0x0c000000u;
 #pragma unroll
-    for (int c = 0; c < 3; ++c) {                       // column c, clamped to the picture
-        const int idx = clip3(0, W - 1, xi + c) - a;
-        hi[c] = idx >= 4;
-        sh[c] = 8 * (idx & 3);
-    }
-    const int wa = (8 - xf) * (8 - yf), wb = xf * (8 - yf), wc = (8 - xf) * yf, wd = xf * yf;
+    for (int c = 0; c < 3; ++c) sel |= (uint32_t)(clip3(0, W - 1, xi + c) - a) << (8 * c);
+    const u16x2 wa = (u16x2)(unsigned short)((8 - xf) * (8 - yf)), wb = (u16x2)(unsigned short)(xf * (8 - yf));
+    const u16x2 wc = (u16x2)(unsigned short)((8 - xf) * yf), wd = (u16x2)(unsigned short)(xf * yf);
 #pragma unroll
     for (int pl = 0; pl < 2; ++pl) {
-        int p[3][3];
+        u16x2 A[3], B[3];                       // row k: {p[k][0], p[k][1]} and {p[k][1], p[k][2]}
 #pragma unroll
-        for (int k = 0; k < 3; ++k)
+        for (int k = 0; k < 3; ++k) {
+            const uint32_t r = __builtin_amdgcn_perm(w[pl][k][1], w[pl][k][0], sel);
+            A[k] = as_u16x2(__builtin_amdgcn_perm(r, r, 0x0c010c00u));
+            B[k] = as_u16x2(__builtin_amdgcn_perm(r, r, 0x0c020c01u));
+        }
+        uint32_t o[2];
 #pragma unroll
-            for (int c = 0; c < 3; ++c) p[k][c] = ((hi[c] ? w[pl][k][1] : w[pl][k][0]) >> sh[c]) & 255;
-        uint32_t o = 0;
-#pragma unroll
-        for (int r = 0; r < 2; ++r)
-#pragma unroll
-            for (int c = 0; c < 2; ++c)
-                o |= (uint32_t)((wa * p[r][c] + wb * p[r][c + 1] + wc * p[r + 1][c] + wd * p[r + 1][c + 1] + 32) >> 6)
-                     << (16 * r + 8 * c);
-        out[pl] = o;
+        for (int rr = 0; rr < 2; ++rr) {
+            const u16x2 v = (wa * A[rr] + wb * B[rr] + wc * A[rr + 1] + wd * B[rr + 1] + (u16x2)(unsigned short)32) >> (u16x2)(unsigned short)6;
+            o[rr] = __builtin_bit_cast(uint32_t, v);
+        }
+        out[pl] = __builtin_amdgcn_perm(o[1], o[0], 0x06040200u);
     }
 }
 
