@@ -210,7 +210,7 @@ extern "C" __global__ __launch_bounds__(64 * H264R_WALK_ROWS, H264R_WALK_WAVES) 
                                                               uint8_t* recon)
 {
     __shared__ IntraScratch scratch[WAVES];
-    __shared__ uint32_t tap4[INTRA4_TAPS];
+    __shared__ uint32_t tap4[INTRA_TAPS];
     __shared__ int lprog[WAVES];
     __shared__ int ticket;
     if (threadIdx.x == 0) ticket = atomicAdd(&sync[0], 1);
@@ -419,7 +419,7 @@ extern "C" __global__ __launch_bounds__(256, H264R_LVL_WAVES) void k_intra_level
                                                                                 int lmax, int* lvsync, int* err, uint8_t* recon)
 {
     __shared__ IntraScratch scratch[4];
-    __shared__ uint32_t tap4[INTRA4_TAPS];
+    __shared__ uint32_t tap4[INTRA_TAPS];
     intra4_tap_fill(tap4, threadIdx.x, blockDim.x);
     __syncthreads();
     const Geom g = make_geom(b.width_mbs, b.height_mbs);

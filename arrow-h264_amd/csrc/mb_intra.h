@@ -50,7 +50,7 @@ DEV int ci(int x, int y) { return (y + 1) * ICP + x + 4; }          // chroma ti
 // e[N+2+k] = T[k] (row above, k = 0..2N-1), e[3N+2] = T[2N-1] again -- the
 // repeated ends give the (a + 3b + 2) >> 2 corner cases of modes 3 and 8.
 template <int N>
-DEV void intra_nxn_tap(int mode, int x, int y, int& kind, int& i)
+constexpr __host__ __device__ void intra_nxn_tap(int mode, int x, int y, int& kind, int& i)
 {
     switch (mode) {
     case 0: kind = 0; i = N + 2 + x; return;                                  // vertical
@@ -84,49 +84,51 @@ DEV void intra_nxn_tap(int mode, int x, int y, int& kind, int& i)
     }
 }
 
-// The (kind, i) of intra_nxn_tap for all 9 modes at one sample position, packed one
-// byte per mode (i | kind << 5; DC entries unused), so a step looks its entry up with
-// a shift instead of branching over the modes.
-template <int N>
-DEV void intra_tap_table(int x, int y, uint32_t (&t)[3])
-{
-    t[0] = t[1] = t[2] = 0;
-#pragma unroll
-    for (int md = 0; md < 9; ++md) {
-        if (md == 2) continue;
-        int kind, i;
-        intra_nxn_tap<N>(md, x, y, kind, i);
-        t[md >> 2] |= (uint32_t)(i | (kind << 5)) << (8 * (md & 3));
-    }
-}
-DEV int intra_tap_entry(const uint32_t (&t)[3], int mode)
-{
-    const uint32_t w = mode < 4 ? t[0] : (mode < 8 ? t[1] : t[2]);
-    return (w >> (8 * (mode & 3))) & 255;
-}
-
-// The I_4x4 taps as tile offsets, one table per workgroup in LDS (INTRA4_TAPS uint32):
-// entry mode * 32 + tv * 16 + (y * 4 + x) holds, for sample (x, y) of a 4x4 block in
-// directional mode `mode`, the tile offsets (from the block origin, int8) of e[i - 1],
-// e[i], e[i + 1] in bytes 0..2 and the kind in byte 3 (intra_nxn_tap<4>); tv = 1 when the
-// block's upper-right neighbours are available (the row above reaches x = 7, else it
-// stops at 3).  e[k]: the left column bottom-up for k <= 5 (the corner at 5), then the row
-// above.  DC entries are 0.
+// The I_4x4 taps as tile offsets, one table per workgroup in LDS (copied from the
+// compile-time INTRA_TAP_TABLE): entry mode * 32 + tv * 16 + (y * 4 + x) holds, for sample
+// (x, y) of a 4x4 block in directional mode `mode`, the tile offsets (from the block
+// origin, int8) of e[i - 1], e[i], e[i + 1] in bytes 0..2 and the kind in byte 3
+// (intra_nxn_tap<4>); tv = 1 when the block's upper-right neighbours are available (the row
+// above reaches x = 7, else it stops at 3).  e[k]: the left column bottom-up for k <= 5 (the
+// corner at 5), then the row above.  DC entries are 0.  After them, the I_8x8 table: byte
+// mode * 64 + (y * 8 + x) = i | kind << 5 of intra_nxn_tap<8> (I_8x8 reads e[] from S.fe, in
+// order).  (Computed at run time in the kernels' prologue, the 8x8 part changed the walk's
+// register allocation: 176 bytes of spills.)
 constexpr int INTRA4_TAPS = 9 * 2 * 16;
+constexpr int INTRA_TAPS = INTRA4_TAPS + 9 * 64 / 4;
+struct IntraTapTable {
+    uint32_t w[INTRA_TAPS];
+};
+constexpr IntraTapTable make_intra_taps()
+{
+    IntraTapTable t{};
+    for (int e = 0; e < INTRA4_TAPS; ++e) {
+        const int mode = e >> 5, tmax = (e & 16) ? 7 : 3, x = e & 3, y = (e >> 2) & 3;
+        if (mode == 2) continue;
+        int kind = 0, i = 0;
+        intra_nxn_tap<4>(mode, x, y, kind, i);
+        int o[3] = {0, 0, 0};
+        for (int d = 0; d < 3; ++d) {
+            const int k = d == 0 ? (i - 1 < 0 ? 0 : i - 1) : (d == 1 ? i : (i + 1 > 14 ? 14 : i + 1));
+            const int up = k - 6 < tmax ? k - 6 : tmax;
+            o[d] = k <= 5 ? (3 - (k - 1 > 0 ? k - 1 : 0)) * ITP - 1 : up - ITP;
+        }
+        t.w[e] = (uint32_t)(uint8_t)o[0] | ((uint32_t)(uint8_t)o[1] << 8) | ((uint32_t)(uint8_t)o[2] << 16) |
+                 ((uint32_t)kind << 24);
+    }
+    for (int j = 0; j < 9 * 64; ++j) {
+        const int mode = j >> 6;
+        int kind = 0, i = 0;
+        if (mode != 2) intra_nxn_tap<8>(mode, j & 7, (j >> 3) & 7, kind, i);
+        t.w[INTRA4_TAPS + (j >> 2)] |= (uint32_t)(i | (kind << 5)) << (8 * (j & 3));
+    }
+    return t;
+}
+__device__ constexpr IntraTapTable INTRA_TAP_TABLE = make_intra_taps();
+DEV const uint8_t* intra8_taps(const uint32_t* taps) { return reinterpret_cast<const uint8_t*>(taps + INTRA4_TAPS); }
 DEV void intra4_tap_fill(uint32_t* tap4, int tid, int nthreads)
 {
-    for (int e = tid; e < INTRA4_TAPS; e += nthreads) {
-        const int mode = e >> 5, tmax = (e & 16) ? 7 : 3, x = e & 3, y = (e >> 2) & 3;
-        uint32_t v = 0;
-        if (mode != 2) {
-            int kind, i;
-            intra_nxn_tap<4>(mode, x, y, kind, i);
-            auto eoff = [&](int k) -> int { return k <= 5 ? (3 - max(k - 1, 0)) * ITP - 1 : min(k - 6, tmax) - ITP; };
-            v = (uint32_t)(uint8_t)eoff(max(i - 1, 0)) | ((uint32_t)(uint8_t)eoff(i) << 8) |
-                ((uint32_t)(uint8_t)eoff(min(i + 1, 14)) << 16) | ((uint32_t)kind << 24);
-        }
-        tap4[e] = v;
-    }
+    for (int e = tid; e < INTRA_TAPS; e += nthreads) tap4[e] = INTRA_TAP_TABLE.w[e];
 }
 
 // kind 0 / 1 / 2 of intra_nxn_tap: all three forms, one kept by masks (a ternary chain on the
@@ -566,8 +568,7 @@ DEV void intra_mb_compute(const h264r_batch& b, const Geom& g, int pic, int mbx,
         // instead of lane-divergent branches.  The result goes to S.fe in e[] order (e[k] at
         // fe[k + 1], the repeated ends included; the taps read fe[i .. i + 2]) and to S.fs
         // (the DC sums).
-        uint32_t tab[3];
-        intra_tap_table<8>(lane & 7, lane >> 3, tab);
+        const uint8_t* t8 = intra8_taps(tap4) + lane;                // + mode * 64: my sample's entry
         const int j = min(lane, 24);
         const int at_e = lane < 25 ? j + 2 : 31, at_dup = lane == 0 ? 1 : (lane == 24 ? 27 : 31);
         const int at_fs = lane >= 25 ? 31 : (j < 8 ? 27 - j : (j == 8 ? 3 : j - 5));
@@ -603,7 +604,7 @@ DEV void intra_mb_compute(const h264r_batch& b, const Geom& g, int pic, int mbx,
                     const int sl = sum4(lds_u32(&S.fs[20])) + sum4(lds_u32(&S.fs[24]));
                     p = aA && aB ? (st + sl + 8) >> 4 : aB ? (st + 4) >> 3 : aA ? (sl + 4) >> 3 : 128;
                 } else {
-                    const int ent = intra_tap_entry(tab, mode), kind = ent >> 5, i = ent & 31;
+                    const int ent = t8[mode * 64], kind = ent >> 5, i = ent & 31;
                     const uint8_t* e = &S.fe[i];                       // e[i - 1], e[i], e[i + 1]
                     p = tap_apply(kind, e[0], e[1], e[2]);
                 }
