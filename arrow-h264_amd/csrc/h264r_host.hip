@@ -281,7 +281,8 @@ static const Knobs& knobs()
         // ever waits on work that is already running: 2 s means a lost wave
         v = 2000; n.ok &= env_long("H264R_WAIT_MS", 1, 40000, &v);
         n.wait_ticks = (uint32_t)(v * 100000);                     // s_memrealtime, 100 MHz
-        v = 16; n.ok &= env_long("H264R_LEVELS", 0, LEVEL_LISTS, &v); n.levels = (int)v;
+        // levels beyond 3 hold few MBs each, and a grid barrier apiece: the walk takes them
+        v = 3; n.ok &= env_long("H264R_LEVELS", 0, LEVEL_LISTS, &v); n.levels = (int)v;
         v = 192; n.ok &= env_long("H264R_DEBLOCK2_MIN", 1, 1L << 30, &v); n.deblock2_min = (int)v;
         v = 1; n.ok &= env_long("H264R_LVL_MARGIN", 0, 7, &v); n.lvl_margin = (int)v;
         v = 1; n.ok &= env_long("H264R_COOP", 0, 1, &v); n.coop = v != 0;
