@@ -112,7 +112,7 @@ extern "C" __global__ __launch_bounds__(256, H264R_INTER_WAVES) void k_inter4r(h
 // k_dbinfo: the deblocking records DbInfo of every MB (dbinfo_block, mb_inter4.h) on their
 // own -- they depend on the MB records and motion only, not on any sample; launched before
 // k_inter4r.  Same grid and lane roles as k_inter4r.
-extern "C" __global__ __launch_bounds__(256) void k_dbinfo(h264r_batch b, DbInfo* dbinfo, int2 rows, int* inter_cnt)
+extern "C" __global__ __launch_bounds__(256, 8) void k_dbinfo(h264r_batch b, DbInfo* dbinfo, int2 rows, int* inter_cnt)
 {
     __shared__ Inter4Lds S;
     const int pic = blockIdx.y;
@@ -125,8 +125,11 @@ extern "C" __global__ __launch_bounds__(256) void k_dbinfo(h264r_batch b, DbInfo
     // the first group's record, motion and neighbour loads go out before the LDS tables are
     // filled; every later group's right after the previous group's use
     int a0 = rows.x * g.wmb + (grp * 4 + wave) * 4;
+    __shared__ DbTables T;
+    const uint2 tv = db_tables_load(threadIdx.x);
     Inter4Pre pre = inter4_pre(b, g, pic, a0, aend, lane);
     DbNb nb = dbinfo_pre(b, g, pic, a0, aend, lane);
+    db_tables_store(T, threadIdx.x, tv);
     inter4_lds(b, pic, S);
     __syncthreads();
     bool inter = false;                      // an inter or I_PCM MB met (k_inter4r has work)
@@ -138,7 +141,7 @@ extern "C" __global__ __launch_bounds__(256) void k_dbinfo(h264r_batch b, DbInfo
         inter |= __any(valid && (!mb_is_intra(pre.q) || pre.q.mb_type == H264R_I_PCM)) != 0;
         const uint2 m0 = motion_word(pre.mv[0], pre.ri[0], slices, S, pre.q.slice, 0);
         const uint2 m1 = motion_word(pre.mv[1], pre.ri[1], slices, S, pre.q.slice, 1);
-        dbinfo_block(b, g, pic, aa, valid, lane & 15, S, pre.q, m0, m1, slice_hdr(slices, S, pre.q.slice), nb,
+        dbinfo_block(b, g, pic, aa, valid, lane & 15, S, T, pre.q, m0, m1, slice_hdr(slices, S, pre.q.slice), nb,
                      dbinfo + (size_t)pic * g.nmb);
         if (++grp >= gend) break;
         a0 = rows.x * g.wmb + (grp * 4 + wave) * 4;

@@ -74,13 +74,25 @@ constexpr int DEBLOCK2_UNITS = 16;   // k_deblock2: (picture, MB row) units per 
 // alpha | beta << 8 | tc0(bS 1..3) << 16 / 21 / 26 for one edge: filter_edge
 // deblock.cc:469-480 (qPav of the two MBs' QPs, indexA/B with MbQ's slice offsets),
 // 8-bit tables (Tables 8-16 / 8-17, deblock.cc:294-324).
-DEV uint32_t edge_word(int qpp, int qpq, int offa, int offb)
+// ab / tc0: DB_AB / DB_TC0 or a copy of them (k_dbinfo keeps one in LDS: read from global
+// memory, the lookup was a dependent round trip per 16-MB group)
+DEV uint32_t edge_word(int qpp, int qpq, int offa, int offb, const uint32_t* ab = DB_AB, const uint32_t* tc0 = DB_TC0)
 {
     const int qPav = (qpp + qpq + 1) >> 1;
     const int idxA = clip3(0, 51, qPav + offa), idxB = clip3(0, 51, qPav + offb);
-    const uint32_t t = DB_TC0[idxA];
-    return (DB_AB[idxA] & 255) | (DB_AB[idxB] & 0xFF00) | ((t & 31) << 16) | (((t >> 8) & 31) << 21) |
+    const uint32_t t = tc0[idxA];
+    return (ab[idxA] & 255) | (ab[idxB] & 0xFF00) | ((t & 31) << 16) | (((t >> 8) & 31) << 21) |
            (((t >> 16) & 31) << 26);
+}
+struct DbTables {
+    uint32_t ab[52], tc0[52];
+};
+// thread t < 52 copies entry t (the workgroup has >= 52 threads): load, then store, so a
+// caller can issue its own loads between the two
+DEV uint2 db_tables_load(int t) { const int i = min(t, 51); return make_uint2(DB_AB[i], DB_TC0[i]); }
+DEV void db_tables_store(DbTables& T, int t, uint2 v)
+{
+    if (t < 52) { T.ab[t] = v.x; T.tc0[t] = v.y; }
 }
 
 constexpr int TP = 5;     // tile pitch in dwords: left margin + 16 samples

@@ -471,7 +471,7 @@ DEV int mb_qp(const h264r_mb& m, int pl)
 // edge parameters :469-480): the block's left edge (vertical edge bx, segment by) and top
 // edge (horizontal edge by, segment bx), and for blk < 9 one alpha/beta/tc0 word.  Inside
 // k_inter4 after the reconstruction (DB = true), or its own kernel k_dbinfo.
-DEV void dbinfo_block(const h264r_batch& b, const Geom& g, int pic, int aa, bool valid, int blk, const Inter4Lds& S,
+DEV void dbinfo_block(const h264r_batch& b, const Geom& g, int pic, int aa, bool valid, int blk, const Inter4Lds& S, const DbTables& T,
                       const h264r_mb& q, uint2 m0, uint2 m1, uint2 qsh, const DbNb& nb, DbInfo* __restrict__ dbout)
 {
     const int bx = blk & 3, by = blk >> 2;
@@ -540,7 +540,7 @@ DEV void dbinfo_block(const h264r_batch& b, const Geom& g, int pic, int aa, bool
             // became a select of their addresses: the record went to memory, promoted to LDS)
             const h264r_mb& P = which == 0 ? L : (which == 1 ? U : q);
             const int qp = mb_qp(P, pl), qq = mb_qp(q, pl);
-            out->par[blk] = edge_word(qp, qq, offa, offb);
+            out->par[blk] = edge_word(qp, qq, offa, offb, T.ab, T.tc0);
         }
     }
 }
