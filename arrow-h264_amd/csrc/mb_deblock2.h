@@ -72,11 +72,10 @@ DEV EdgeP edge_params(uint32_t par, s2 bs2)
     e.am1 = sp2((short)(alpha - 1));
     e.bm1 = sp2((short)(beta - 1));
     e.bs = bs2;
-    const s2 t1 = sp2((short)((par >> 16) & 31)), t2 = sp2((short)((par >> 21) & 31)), t3 = sp2((short)((par >> 26) & 31));
-    // -1 where bS == k: |bS - k| - 1 < 0
-    const s2 is1 = neg_mask(absd(bs2, sp2(1)) - sp2(1)), is2 = neg_mask(absd(bs2, sp2(2)) - sp2(1));
-    const s2 is3 = neg_mask(absd(bs2, sp2(3)) - sp2(1));
-    e.tc0 = sel(is1, t1, sel(is2, t2, sel(is3, t3, sp2(0))));
+    // tc0(bS) of each half by one byte permute: bS (0..4, the half's low byte) indexes the
+    // bytes {0, tc0(1), tc0(2), tc0(3)} and, for bS 4, byte 0 of a zero operand
+    const uint32_t T = (((par >> 16) & 31) << 8) | (((par >> 21) & 31) << 16) | (((par >> 26) & 31) << 24);
+    e.tc0 = as_s2(__builtin_amdgcn_perm(0u, T, as_w(bs2) | 0x0c000c00u));
     return e;
 }
 
