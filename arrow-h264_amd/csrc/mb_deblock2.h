@@ -30,6 +30,14 @@ DEV s2 sel(s2 m, s2 a, s2 b)                    // m (-1 / 0 per half) ? a : b
     return as_s2((as_w(m) & as_w(a)) | (~as_w(m) & as_w(b)));
 }
 DEV s2 clamp255(s2 v) { return smin(smax(v, sp2(0)), sp2(255)); }
+// A mask the compiler must not look through: seen as a sign splat, it became per-half lane
+// compares and every sel() on it two selects plus a re-pack instead of one bitfield insert.
+DEV s2 opaque_mask(s2 m)
+{
+    uint32_t w = as_w(m);
+    asm volatile("" : "+v"(w));
+    return as_s2(w);
+}
 
 // {byte b of A, byte b of B} as an s16x2 (A in the low half).
 DEV s2 unpack2(uint32_t A, uint32_t B, int b)
@@ -94,7 +102,7 @@ DEV void filter2(s2& p3, s2& p2, s2& p1, s2& p0, s2& q0, s2& q1, s2& q2, s2& q3,
         d = smin(smax(d, -tc), tc);
         s2 np0 = clamp255(p0 + d), nq0 = clamp255(q0 - d);
         if (STRONG) {                                  // filter_strong, chroma (deblock.cc:350-364)
-            const s2 is4 = neg_mask(e.bs - sp2(4)) ^ sp2(-1);          // -1 where bS >= 4
+            const s2 is4 = opaque_mask(neg_mask(e.bs - sp2(4)) ^ sp2(-1));          // -1 where bS >= 4
             np0 = sel(is4, (p1 * sp2(2) + p0 + q1 + sp2(2)) >> sp2(2), np0);
             nq0 = sel(is4, (q1 * sp2(2) + q0 + p1 + sp2(2)) >> sp2(2), nq0);
         }
@@ -114,7 +122,7 @@ DEV void filter2(s2& p3, s2& p2, s2& p1, s2& p0, s2& q0, s2& q1, s2& q2, s2& q3,
     s2 nq1 = sel(naq, q1, q1 + smin(smax((q2 + avg - q1 * sp2(2)) >> sp2(1), -e.tc0), e.tc0));
     s2 np2 = p2, nq2 = q2;
     if (STRONG) {                                          // filter_strong (deblock.cc:327-370)
-        const s2 is4 = neg_mask(e.bs - sp2(4)) ^ sp2(-1);
+        const s2 is4 = opaque_mask(neg_mask(e.bs - sp2(4)) ^ sp2(-1));
         const s2 nstrong = neg_mask(((e.alpha >> sp2(2)) + sp2(1)) - dpq);   // NOT (|p0-q0| < (alpha >> 2) + 2)
         const s2 nsp = nap | nstrong, nsq = naq | nstrong;
         const s2 s_p0 = sel(nsp, (p1 * sp2(2) + p0 + q1 + sp2(2)) >> sp2(2),
