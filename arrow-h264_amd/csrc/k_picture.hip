@@ -183,7 +183,7 @@ DEV void walk_ticket(const h264r_batch& b, int* sync, int* err, Scratch* scratch
             else ok = wait_for<false>(&lprog[wave - 1], need, err, seen);
         }
         if (!ok) break;
-        hd.nb = intra_head_samples(g, pic, x, r, ln, recon);
+        hd.nb = intra_head_samples(g, pic, x, r, ln, recon, tap4);
 #ifdef H264R_TRACE_INTRA
         {
             const unsigned long long tw = __builtin_amdgcn_s_memrealtime(), c0 = __builtin_amdgcn_s_memtime();

@@ -95,7 +95,9 @@ constexpr __host__ __device__ void intra_nxn_tap(int mode, int x, int y, int& ki
 // order).  (Computed at run time in the kernels' prologue, the 8x8 part changed the walk's
 // register allocation: 176 bytes of spills.)
 constexpr int INTRA4_TAPS = 9 * 2 * 16;
-constexpr int INTRA_TAPS = INTRA4_TAPS + 9 * 64 / 4;
+constexpr int INTRA8_TAPS = 9 * 64 / 4;
+constexpr int INTRA_NBR = INTRA4_TAPS + INTRA8_TAPS;   // + lane: the lane's neighbour-sample dword
+constexpr int INTRA_TAPS = INTRA_NBR + 64;
 struct IntraTapTable {
     uint32_t w[INTRA_TAPS];
 };
@@ -121,6 +123,26 @@ constexpr IntraTapTable make_intra_taps()
         int kind = 0, i = 0;
         if (mode != 2) intra_nxn_tap<8>(mode, j & 7, (j >> 3) & 7, kind, i);
         t.w[INTRA4_TAPS + (j >> 2)] |= (uint32_t)(i | (kind << 5)) << (8 * (j & 3));
+    }
+    // the neighbour-sample dword of lane l (intra_head_samples): byte offset in the MB-tiled
+    // neighbour MB (bits 0..8), its MB offset dx + 1 (bits 9..10) and dy + 1 (bit 11), the
+    // lane loads (bit 12), its sample is the dword's top byte (bit 13: the left columns)
+    for (int l = 0; l < 64; ++l) {
+        int inner = 0, dx = 0, dy = 0, act = 0, top = 0;
+        if (l < 7) {                                   // luma row above, x = -4 .. 23
+            const int xr = 4 * l - 4;
+            dx = xr < 0 ? -1 : (xr >> 4); dy = -1; inner = 15 * 16 + (xr & 15); act = 1;
+        } else if (l < 23) {                           // luma left column
+            dx = -1; inner = (l - 7) * 16 + 12; act = 1; top = 1;
+        } else if (l < 29) {                           // chroma rows above, x = -4 .. 7
+            const int k = l - 23, pl = k / 3, xc = 4 * (k % 3) - 4;
+            dx = xc < 0 ? -1 : 0; dy = -1; inner = RECON_CB + pl * 64 + 7 * 8 + (xc & 7); act = 1;
+        } else if (l < 45) {                           // chroma left columns
+            const int k = l - 29, pl = k >> 3;
+            dx = -1; inner = RECON_CB + pl * 64 + (k & 7) * 8 + 4; act = 1; top = 1;
+        }
+        t.w[INTRA_NBR + l] = (uint32_t)inner | ((uint32_t)(dx + 1) << 9) | ((uint32_t)(dy + 1) << 11) |
+                             ((uint32_t)act << 12) | ((uint32_t)top << 13);
     }
     return t;
 }
@@ -402,35 +424,22 @@ struct IntraHead {
 
 // The neighbour samples of MB (mbx, mby) for this lane: written by other waves (the row
 // above) or by this one (the MB to the left), so loaded only once they are final.
-DEV uint32_t intra_head_samples(const Geom& g, int pic, int mbx, int mby, int lane, uint8_t* recon)
+DEV uint32_t intra_head_samples(const Geom& g, int pic, int mbx, int mby, int lane, uint8_t* recon, const uint32_t* taps)
 {
-    const int X = mbx * 16, Y = mby * 16, Xc = mbx * 8, Yc = mby * 8;
     // ---- neighbour samples (in-picture addresses only; availability decides later which
     // of them are used): one dword load per lane (a left-column sample is the top byte of
     // the aligned dword that ends at x - 1; lanes with nothing to fetch read their own
-    // MB's first row and drop it).  Loads in lane-divergent branches would each merge
-    // through a copy whose vmcnt(0) serialises them.
+    // MB's first row and drop it).  Each lane's neighbour MB and byte offset come from the
+    // table (INTRA_NBR): a branch per lane group had cost the walk its exec-mask work.
     // (MB-tiled reconstruction, device_common.h: a dword never crosses an MB)
-    const uint8_t* src = recon_mb(recon, g, pic, mby * g.wmb + mbx);
-    bool want = false, left = false;
-    if (lane < 7) {                                   // row above, x = -4..23
-        const int x = X - 4 + 4 * lane;
-        want = mby > 0 && x >= 0 && x < g.W;
-        src = want ? recon_y(recon, g, pic, x, Y - 1) : src;
-    } else if (lane < 23) {                           // left column
-        want = left = mbx > 0;
-        src = want ? recon_y(recon, g, pic, X - 4, Y + lane - 7) : src;
-    } else if (lane < 29) {                           // chroma rows above, x = -4..7
-        const int k = lane - 23, pl = k / 3, x = Xc - 4 + 4 * (k % 3);
-        want = mby > 0 && x >= 0;
-        src = want ? recon_c(recon, g, pic, pl, x, Yc - 1) : src;
-    } else if (lane < 45) {                           // chroma left columns
-        const int k = lane - 29, pl = k >> 3;
-        want = left = mbx > 0;
-        src = want ? recon_c(recon, g, pic, pl, Xc - 4, Yc + (k & 7)) : src;
-    }
+    const uint32_t e = taps[INTRA_NBR + lane];
+    const int dx = (int)((e >> 9) & 3) - 1, dy = (int)((e >> 11) & 1) - 1;
+    const int nx = mbx + dx;
+    const bool want = ((e >> 12) & 1) && (dy == 0 || mby > 0) && nx >= 0 && nx < g.wmb;
+    const int a = want ? (mby + dy) * g.wmb + nx : mby * g.wmb + mbx;
+    const uint8_t* src = recon_mb(recon, g, pic, a) + (want ? (int)(e & 511) : 0);
     const uint32_t w = *as_global(src);
-    return (w >> (left ? 24 : 0)) & (0u - (uint32_t)want);   // arithmetic, not a select: no branch
+    return (w >> ((e >> 13) & 1 ? 24 : 0)) & (0u - (uint32_t)want);   // arithmetic, not a select: no branch
 }
 
 // The records of MB (mbx, mby) and its neighbours: immutable during a batch, so the walk
@@ -454,10 +463,11 @@ DEV void intra_head_records(const h264r_batch& b, const Geom& g, int pic, int mb
     h.m = load_mb_const(&mbs[a]);
 }
 
-DEV IntraHead intra_head(const h264r_batch& b, const Geom& g, int pic, int mbx, int mby, int lane, uint8_t* recon)
+DEV IntraHead intra_head(const h264r_batch& b, const Geom& g, int pic, int mbx, int mby, int lane, uint8_t* recon,
+                         const uint32_t* taps)
 {
     IntraHead h;
-    h.nb = intra_head_samples(g, pic, mbx, mby, lane, recon);
+    h.nb = intra_head_samples(g, pic, mbx, mby, lane, recon, taps);
     intra_head_records(b, g, pic, mbx, mby, lane, h);
     return h;
 }
@@ -740,7 +750,7 @@ DEV void intra_mb_compute(const h264r_batch& b, const Geom& g, int pic, int mbx,
 DEV void intra_mb2(const h264r_batch& b, const Geom& g, int pic, int mbx, int mby, int lane, IntraScratch& S,
                    const uint32_t* tap4, uint8_t* recon, unsigned long long* tph = nullptr)
 {
-    const IntraHead hd = intra_head(b, g, pic, mbx, mby, lane, recon);
+    const IntraHead hd = intra_head(b, g, pic, mbx, mby, lane, recon, tap4);
     if (!mb_is_intra(hd.m) || hd.m.mb_type == H264R_I_PCM) return;
     const IntraLoads ld = intra_body_loads(b, pic, hd, lane);
     intra_mb_compute(b, g, pic, mbx, mby, lane, S, tap4, hd, ld, recon, tph);
