@@ -126,23 +126,32 @@ constexpr IntraTapTable make_intra_taps()
     }
     // the neighbour-sample dword of lane l (intra_head_samples): byte offset in the MB-tiled
     // neighbour MB (bits 0..8), its MB offset dx + 1 (bits 9..10) and dy + 1 (bit 11), the
-    // lane loads (bit 12), its sample is the dword's top byte (bit 13: the left columns)
+    // lane loads (bit 12); bits 14..25: where the dword goes in IntraScratch -- the tile row
+    // above (x = -4 .. 23 / chroma -4 .. 7) or, for the left columns, x = -4 .. -1 of the row
+    // (the sample at -1; -4 .. -2 are not read); lanes without a sample write into S.res,
+    // which every MB type rewrites before reading it
     for (int l = 0; l < 64; ++l) {
-        int inner = 0, dx = 0, dy = 0, act = 0, top = 0;
+        int inner = 0, dx = 0, dy = 0, act = 0, at = 0;
         if (l < 7) {                                   // luma row above, x = -4 .. 23
             const int xr = 4 * l - 4;
             dx = xr < 0 ? -1 : (xr >> 4); dy = -1; inner = 15 * 16 + (xr & 15); act = 1;
+            at = (int)offsetof(IntraScratch, tile) + 4 * l;
         } else if (l < 23) {                           // luma left column
-            dx = -1; inner = (l - 7) * 16 + 12; act = 1; top = 1;
+            dx = -1; inner = (l - 7) * 16 + 12; act = 1;
+            at = (int)offsetof(IntraScratch, tile) + (l - 7 + 1) * ITP;
         } else if (l < 29) {                           // chroma rows above, x = -4 .. 7
             const int k = l - 23, pl = k / 3, xc = 4 * (k % 3) - 4;
             dx = xc < 0 ? -1 : 0; dy = -1; inner = RECON_CB + pl * 64 + 7 * 8 + (xc & 7); act = 1;
+            at = (int)offsetof(IntraScratch, ctile) + pl * 9 * ICP + 4 * (k % 3);
         } else if (l < 45) {                           // chroma left columns
             const int k = l - 29, pl = k >> 3;
-            dx = -1; inner = RECON_CB + pl * 64 + (k & 7) * 8 + 4; act = 1; top = 1;
+            dx = -1; inner = RECON_CB + pl * 64 + (k & 7) * 8 + 4; act = 1;
+            at = (int)offsetof(IntraScratch, ctile) + pl * 9 * ICP + ((k & 7) + 1) * ICP;
+        } else {
+            at = (int)offsetof(IntraScratch, res) + 4 * l;
         }
         t.w[INTRA_NBR + l] = (uint32_t)inner | ((uint32_t)(dx + 1) << 9) | ((uint32_t)(dy + 1) << 11) |
-                             ((uint32_t)act << 12) | ((uint32_t)top << 13);
+                             ((uint32_t)act << 12) | ((uint32_t)at << 14);
     }
     return t;
 }
@@ -415,7 +424,7 @@ DEV void intra_bypass_res(const h264r_mb& m, const int16_t* __restrict__ lv, int
 // The records are wave-uniform scalar loads (constant address space: immutable during
 // a batch).
 struct IntraHead {
-    uint32_t nb;                 // this lane's neighbour sample dword (masked)
+    uint32_t nb;                 // this lane's neighbour sample dword (masked; INTRA_NBR)
     uint32_t nw0, nw2;           // lanes 0..3: neighbour record A, B, C, D (lane k): dwords 0 (type, flags) and 2 (cbp_blks, slice)
     bool nin;                    // lanes 0..3: that neighbour lies inside the picture
     h264r_mb m;
@@ -438,8 +447,7 @@ DEV uint32_t intra_head_samples(const Geom& g, int pic, int mbx, int mby, int la
     const bool want = ((e >> 12) & 1) && (dy == 0 || mby > 0) && nx >= 0 && nx < g.wmb;
     const int a = want ? (mby + dy) * g.wmb + nx : mby * g.wmb + mbx;
     const uint8_t* src = recon_mb(recon, g, pic, a) + (want ? (int)(e & 511) : 0);
-    const uint32_t w = *as_global(src);
-    return (w >> ((e >> 13) & 1 ? 24 : 0)) & (0u - (uint32_t)want);   // arithmetic, not a select: no branch
+    return *as_global(src) & (0u - (uint32_t)want);    // arithmetic, not a select: no branch
 }
 
 // The records of MB (mbx, mby) and its neighbours: immutable during a batch, so the walk
@@ -510,17 +518,8 @@ DEV void intra_mb_compute(const h264r_batch& b, const Geom& g, int pic, int mbx,
     INTRA_STAMP(1);
 
     // ---- neighbours into the tiles
-    {
-        // one LDS byte offset per lane (one live register, not four hoisted addresses)
-        const int kc = lane < 29 ? lane - 23 : lane - 29;
-        const int at = lane < 7 ? 4 * lane
-                     : lane < 23 ? ti(-1, lane - 7)
-                     : lane < 29 ? (int)offsetof(IntraScratch, ctile) + (kc / 3) * 9 * ICP + 4 * (kc % 3)
-                                 : (int)offsetof(IntraScratch, ctile) + (kc >> 3) * 9 * ICP + ci(-1, kc & 7);
-        uint8_t* base = reinterpret_cast<uint8_t*>(&S);
-        if (lane < 7 || (lane >= 23 && lane < 29)) *reinterpret_cast<uint32_t*>(base + at) = nb;
-        else if (lane < 45) base[at] = (uint8_t)nb;
-    }
+    // (one dword store per lane at its INTRA_NBR offset: no lane-group branches)
+    *reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(&S) + ((tap4[INTRA_NBR + lane] >> 14) & 4095)) = nb;
     if (byp) intra_bypass_res(m, b.levels + m.coef_off, lane, S, ipw, resL, resC);   // S.res too
     else if (i8) luma_res8_intra(m, ld, lane, S);      // includes wave_syncs
     else if (!i16) {
