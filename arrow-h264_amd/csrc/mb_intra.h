@@ -241,8 +241,11 @@ DEV void chroma_res2(const h264r_mb& m, const IntraLoads& L, int lane, int (&res
     const int c00 = (int16_t)(L.cdc[0] & 0xFFFF), c01 = (int16_t)(L.cdc[0] >> 16);
     const int c10 = (int16_t)(L.cdc[1] & 0xFFFF), c11 = (int16_t)(L.cdc[1] >> 16);
     const int e00 = c00 + c01, e01 = c00 - c01, e10 = c10 + c11, e11 = c10 - c11;
-    const int f = cb == 0 ? e00 + e10 : cb == 1 ? e01 + e11 : cb == 2 ? e00 - e10 : e01 - e11;
-    if (crow == 0 && chalf == 0) k0 = ((f * L.cdc_scale) * (1 << per)) >> 5;
+    // f = (e00 or e01) +/- (e10 or e11) by cb's bits: arithmetic, not a branch tree
+    const int ea = (cb & 1) ? e01 : e00, eb = (cb & 1) ? e11 : e10;
+    const int f = ea + (eb ^ -(cb >> 1)) + (cb >> 1);
+    const int kdc = ((f * L.cdc_scale) * (1 << per)) >> 5;
+    k0 = (crow == 0 && chalf == 0) ? kdc : k0;
     const int o0 = __shfl_xor(k0, 4), o1 = __shfl_xor(k1, 4);
     const int d0 = chalf ? o0 : k0, d1 = chalf ? o1 : k1, d2 = chalf ? k0 : o0, d3 = chalf ? k1 : o1;
     int t[4];
