@@ -167,6 +167,12 @@ struct h264r_ctx {
     // than the previous one first waits for the previous launch (ev_last)
     hipStream_t last_stream = nullptr;
     hipEvent_t ev_last = nullptr;
+    // the overlapped schedule (launch_all): deblocking of picture chunk k on `side` while the
+    // launch stream reconstructs chunk k + 1; ev_chunk[k] = chunk k reconstructed, ev_side =
+    // the side stream's last deblocking launch (the launch stream waits for it at the end)
+    hipStream_t side = nullptr;
+    std::vector<hipEvent_t> ev_chunk;
+    hipEvent_t ev_side = nullptr;
     // timing: every kernel of every launch bracketed by events on its stream
     bool timing = false;
     int debug = 0;
@@ -251,6 +257,7 @@ struct Knobs {
     int lvl_margin = 1;        // H264R_LVL_MARGIN: k_intra_levels' grid, blocks per CU below occupancy
     bool coop = true;          // H264R_COOP: k_intra_levels by hipLaunchCooperativeKernel
     int walk_gstep = 0;        // H264R_WALK_GSTEP: the walk's band hand-off period (0: by batch size)
+    int overlap = 1;           // H264R_OVERLAP: picture chunks of the overlapped schedule (launch_all; 0, 1: off)
     bool verbose = false;      // H264R_VERBOSE
 };
 static bool env_long(const char* name, long lo, long hi, long* out)
@@ -267,7 +274,8 @@ static bool env_long(const char* name, long lo, long hi, long* out)
     *out = v;
     return true;
 }
-constexpr int SCHEDULE_FLAGS = H264R_DBG_INTRA_WALK | H264R_DBG_DEBLOCK_MB | H264R_DBG_DEBLOCK_ROWS | H264R_DBG_DEBLOCK_GLOBAL;
+constexpr int SCHEDULE_FLAGS = H264R_DBG_INTRA_WALK | H264R_DBG_DEBLOCK_MB | H264R_DBG_DEBLOCK_ROWS | H264R_DBG_DEBLOCK_GLOBAL |
+                               H264R_DBG_OVERLAP;
 static const Knobs& knobs()
 {
     static const Knobs k = [] {
@@ -287,6 +295,8 @@ static const Knobs& knobs()
         v = 1; n.ok &= env_long("H264R_LVL_MARGIN", 0, 7, &v); n.lvl_margin = (int)v;
         v = 1; n.ok &= env_long("H264R_COOP", 0, 1, &v); n.coop = v != 0;
         v = 0; n.ok &= env_long("H264R_WALK_GSTEP", 0, 1 << 20, &v); n.walk_gstep = (int)v;
+        // measured slower than one stage (profiles/r05_b_overlap_ab.txt): off by default
+        v = 1; n.ok &= env_long("H264R_OVERLAP", 0, 16, &v); n.overlap = (int)v;
         v = 0; n.ok &= env_long("H264R_VERBOSE", 0, 1, &v); n.verbose = v != 0;
         return n;
     }();
@@ -353,6 +363,10 @@ int h264r_destroy(h264r_ctx* c)
     c->sc.release();
     for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
     if (c->ev_last) (void)hipEventDestroy(c->ev_last);
+    if (c->side) (void)hipStreamSynchronize(c->side);
+    for (hipEvent_t e : c->ev_chunk) (void)hipEventDestroy(e);
+    if (c->ev_side) (void)hipEventDestroy(c->ev_side);
+    if (c->side) (void)hipStreamDestroy(c->side);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return H264R_OK;
@@ -436,82 +450,53 @@ struct Timed {
 // LEVEL_LISTS).
 static int level_launches() { return knobs().levels; }
 
-// rows [row0, row1): the MB rows of every picture this launch reconstructs and
-// deblocks (the whole picture, or a slice-aligned band: h264r_decode_batch_rows).
-// The launches on stream s: k_dbinfo + k_inter4r + k_inter_sp (inter / PCM MBs and the
-// deblocking records), k_level + k_level_scan + k_level_scatter + k_intra_levels + k_intra_pic
-// (intra MBs), k_deblock or k_deblock2 (by batch size).
-static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row0, int row1, Scratch& X)
+// Pictures [p0, p0 + n) of a batch as a batch of their own: every per-picture array advanced
+// (the level pool is shared: coef_off stays an offset into it).
+static h264r_batch sub_batch(const h264r_batch& b, int p0, int n)
+{
+    h264r_batch r = b;
+    const size_t nmb = (size_t)b.width_mbs * b.height_mbs;
+    r.num_pics = n;
+    r.mbs += (size_t)p0 * nmb;
+    r.mv += (size_t)p0 * 32 * nmb;                 // [list][4H][4W] per picture
+    r.ref_idx += (size_t)p0 * 32 * nmb;
+    r.slices += (size_t)p0 * b.slice_stride;
+    r.pics += p0;
+    r.quant += p0;
+    if (b.ref_planes_stride) r.ref_planes += (size_t)p0 * b.ref_planes_stride;
+    r.out_y += (size_t)p0 * 256 * nmb;
+    r.out_u += (size_t)p0 * 64 * nmb;
+    r.out_v += (size_t)p0 * 64 * nmb;
+    return r;
+}
+
+// ints of one launch sequence's sync region: [intra ticket + per-(picture, row) progress]
+// [deblock ticket][level barrier, deepest level][SP inter MBs seen] + the deblocking kernels'
+// per-XCD ticket counters, done count, then per picture the waves of k_dbinfo that met an inter
+// or I_PCM MB (k_inter4r skips the pictures without one)
+static size_t sync_ints(int P, int H) { return 1 + (size_t)P * H + 5 + 9 + P; }
+
+// One launch sequence's share of the scratch (the whole batch, or one chunk of the overlapped
+// schedule): its pictures, their deblocking records and MB-tiled reconstruction, its sync region.
+struct Stage {
+    h264r_batch b;
+    h264r::DbInfo* dbinfo;
+    uint8_t* recon;
+    int* sync;
+};
+
+// The reconstruction of a stage on stream s: k_dbinfo + k_inter4r + k_inter_sp (inter / PCM MBs
+// and the deblocking records), k_level + k_level_scan + k_level_scatter + k_intra_levels +
+// k_intra_pic (intra MBs).  The level lists are one set: stages on one stream reuse them in order.
+static int recon_launches(h264r_ctx* c, const Stage& S, hipStream_t s, int2 rows, Scratch& X, bool levels, bool coop)
 {
     const Knobs& K = knobs();
-    // H264R_DEBUG: the deblocking-schedule flags of h264r_set_debug OR-ed into every launch
-    // (measurement A/B; validated in knobs(): schedule flags only, so the output is unchanged)
-    const int debug_saved = c->debug;
-    c->debug |= K.debug;
-    struct Restore { h264r_ctx* c; int d; ~Restore() { c->debug = d; } } restore{c, debug_saved};
-    const int W = b.width_mbs, H = b.height_mbs, P = b.num_pics, HB = row1 - row0;
-    const int2 rows = make_int2(row0, row1);
-    const int nbands = (HB + H264R_WALK_ROWS - 1) / H264R_WALK_ROWS, npairs = (HB + 1) / 2;
-    // scratch: per-MB deblocking records, tagged hand-off
-    // records, and a sync region [intra ticket + per-(picture,row) progress][deblock
-    // ticket][level barrier, deepest level][SP inter MBs seen]
-    // + the deblocking kernels' per-XCD ticket counters, done count, then per picture the waves
-    // of k_dbinfo that met an inter or I_PCM MB (k_inter4r skips the pictures without one)
-    const size_t sync_n = 1 + (size_t)P * H + 5 + 9 + P;
-    int st;
-    if ((st = dev_resize(&X.d_dbinfo, &X.c_dbinfo, (size_t)P * W * H * DBINFO_BYTES))) return st;
-    // the reconstruction kernels write the MB-tiled samples (device_common.h), the
-    // deblocking kernel (or k_untile) turns them into the output planes
-    if ((st = dev_resize(&X.d_recon, &X.c_recon, (size_t)P * W * H * 384))) return st;
-    uint8_t* recon = X.d_recon;
-    // k_deblock2 needs many (picture group, band) walks in flight: H264R_DEBLOCK2_MIN is the
-    // crossover measured on whole 1080p pictures (68 MB rows), so a launch qualifies by its
-    // picture-rows (a 2160p picture counts twice, a 17-row slice band a quarter)
-    const bool by_rows = (c->debug & H264R_DBG_DEBLOCK_ROWS) ||
-                         (!(c->debug & H264R_DBG_DEBLOCK_MB) && (int64_t)P * HB >= (int64_t)K.deblock2_min * 68);
-    // hand-off records of the chosen deblocking kernel; fresh memory or a wrapping epoch
-    // restarts from zeroed records, so no record may carry a live tag
-    uint8_t** hb = by_rows ? &X.d_hb2 : &X.d_hb;
-    size_t* hcap = by_rows ? &X.c_hb2 : &X.c_hb;
-    uint32_t* ep = by_rows ? &X.epoch2 : &X.epoch;
-    const uint32_t ep_max = by_rows ? (1u << 20) - 2 : 0xFFFFFF00u;
-    {
-        const size_t cap_before = *hcap;
-        const size_t need = by_rows ? (size_t)P * W * HANDOFF2_BYTES : (size_t)P * npairs * W * HANDOFF_BYTES;
-        if ((st = dev_resize(hb, hcap, need))) return st;
-        if (*hcap != cap_before || *ep > ep_max) {
-            HIP_OK(hipMemsetAsync(*hb, 0, *hcap, s));
-            *ep = 0;
-        }
-    }
-    if ((st = dev_resize(&X.d_sync, &X.c_sync, sync_n))) return st;
-    // H264R_DBG_WAIT_TEST: every intra-walk wait asks for progress no row reaches, under a
-    // 10 ms bound -- the launch must drain and h264r_check report H264R_EDEVICE
+    const h264r_batch& b = S.b;
+    const int W = b.width_mbs, H = b.height_mbs, P = b.num_pics, HB = rows.y - rows.x;
+    const int nbands = (HB + H264R_WALK_ROWS - 1) / H264R_WALK_ROWS;
     const bool wait_test = (c->debug & H264R_DBG_WAIT_TEST) != 0;
-    if ((st = set_wait_bound(c, wait_test ? 1000000u : wait_bound_ticks(), s))) return st;
-    const bool levels = (size_t)W * H <= LEVEL_MAX_MBS && H <= 1024 && level_launches() > 0 &&
-                        !(c->debug & (H264R_DBG_INTRA_WALK | H264R_DBG_WAIT_TEST));
-    if (levels && !c->levels_grid) {
-        // every workgroup of the persistent level kernel must be resident at once: one
-        // block per CU below what the occupancy query reports (MI355X_MICROARCH.md,
-        // residency caveat), at least one per CU
-        int per_cu = 0, cus = 0;
-        HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(k_intra_levels), 256, 0));
-        HIP_OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
-        c->levels_grid = std::max(1, per_cu - K.lvl_margin) * std::max(1, cus);
-        if (K.verbose)
-            fprintf(stderr, "h264r: k_intra_levels occupancy %d blocks/CU, %d CUs, grid %d\n", per_cu, cus, c->levels_grid);
-    }
-    if (levels && ((st = dev_resize(&X.d_lvl, &X.c_lvl, (size_t)P * W * H)) ||
-                   (st = dev_resize(&X.d_list, &X.c_list, (size_t)P * W * H)) ||
-                   (st = dev_resize(&X.d_lcnt, &X.c_lcnt, 3 * (size_t)(LEVEL_LISTS + 2)))))
-        return st;
-    if (levels) HIP_OK(hipMemsetAsync(X.d_lcnt, 0, 3 * (size_t)(LEVEL_LISTS + 2) * sizeof(int), s));
-    HIP_OK(hipMemsetAsync(X.d_sync, 0, sync_n * sizeof(int), s));
-    h264r::DbInfo* dbinfo = reinterpret_cast<h264r::DbInfo*>(X.d_dbinfo);
-    int* sync = X.d_sync;
-    Timed whole(c, 3, s);
-    if (c->timing) c->timed_launches++;
+    int* sync = S.sync;
+    uint8_t* recon = S.recon;
     const int groups = (W * HB + 15) / 16;
     // groups per workgroup (launch_cfg.h), 8 XCD bands (k_recon.hip inter4_groups)
     const dim3 igrid(8 * ((groups + 8 * H264R_INTER_GROUPS - 1) / (8 * H264R_INTER_GROUPS)), P);
@@ -522,9 +507,9 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
         // the deblocking records first (k_inter4r then fits 4 waves/SIMD), with per picture
         // a flag that an inter or I_PCM MB was met (profiles/r03_f_dbinfo_ab.txt, r03_h_inter_ab.txt)
         int* inter_cnt = sync + 1 + (size_t)P * H + 14;
-        hipLaunchKernelGGL(k_dbinfo, dgrid, dim3(256), 0, s, b, dbinfo, rows, inter_cnt);
+        hipLaunchKernelGGL(k_dbinfo, dgrid, dim3(256), 0, s, b, S.dbinfo, rows, inter_cnt);
         HIP_OK(hipGetLastError());
-        hipLaunchKernelGGL(k_inter4r, igrid, dim3(256), 0, s, b, dbinfo, rows, sp_flag, recon, (const int*)inter_cnt);
+        hipLaunchKernelGGL(k_inter4r, igrid, dim3(256), 0, s, b, S.dbinfo, rows, sp_flag, recon, (const int*)inter_cnt);
         HIP_OK(hipGetLastError());
         // inter MBs of SP slices (a short launch when the batch has none)
         hipLaunchKernelGGL(k_inter_sp, dim3(1024), dim3(256), 0, s, b, rows, (const int*)sp_flag, recon);
@@ -539,6 +524,7 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
             int* lcount = X.d_lcnt;
             int* lbase = lcount + (LEVEL_LISTS + 2);
             int* lcursor = lbase + (LEVEL_LISTS + 2);
+            HIP_OK(hipMemsetAsync(X.d_lcnt, 0, 3 * (size_t)(LEVEL_LISTS + 2) * sizeof(int), s));
             // pictures deeper than 4 x lmax levels (all-intra) are left to the walk whole
             hipLaunchKernelGGL(k_level, dim3(P), dim3(64 * ((HB + 63) / 64)), 0, s, b, lvl, lvsync, lcount, rows, 4 * lmax);
             HIP_OK(hipGetLastError());
@@ -557,13 +543,14 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
             // barriers, whose cost grows with the number of arrivals (MI355X_MICROARCH.md
             // price list 'barrier-xcd')
             const int lgrid = std::min(c->levels_grid, std::max(8, (int)(((size_t)P * W * HB + 63) / 64)));
-            if (K.coop) {
+            if (coop) {
                 const int* lcount_c = lcount;
                 const int* lbase_c = lbase;
                 const uint32_t* list_c = X.d_list;
                 int lmax_v = lmax;
                 int* err_p = c->d_err;
-                void* args[] = {(void*)&b, (void*)&lcount_c, (void*)&lbase_c, (void*)&list_c, (void*)&lmax_v,
+                h264r_batch bv = b;
+                void* args[] = {(void*)&bv, (void*)&lcount_c, (void*)&lbase_c, (void*)&list_c, (void*)&lmax_v,
                                 (void*)&lvsync, (void*)&err_p, (void*)&recon};
                 HIP_OK(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(k_intra_levels), dim3(lgrid),
                                                   dim3(256), args, 0, s));
@@ -580,36 +567,157 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
                            (const uint16_t*)lvl, lmax, rows, gstep, recon);
         HIP_OK(hipGetLastError());
     }
-    if (!(c->debug & H264R_DBG_NO_DEBLOCK)) {
-        Timed t(c, 2, s);
-        if (!c->nxcc) {                  // XCDs of the device: the deblocking kernels' placement
-            int nx = 1;
-            if (hipDeviceGetAttribute(&nx, hipDeviceAttributeNumberOfXccs, c->device) != hipSuccess) nx = 1;
-            c->nxcc = std::max(1, std::min(nx, 8));
-        }
-        if (by_rows)
-        {
-            // k_deblock2 keeps a picture group on one XCD (g % nx): nx counters
-            int grid = ((P + DEBLOCK2_PICS - 1) / DEBLOCK2_PICS) * ((HB + H264R_DB2_BAND - 1) / H264R_DB2_BAND);
-            const int nx = grid >= 64 * c->nxcc && !(c->debug & H264R_DBG_DEBLOCK_GLOBAL) ? c->nxcc : 1;
-            grid = (grid + nx - 1) / nx * nx;
-            hipLaunchKernelGGL(k_deblock2, dim3(grid), dim3(64), 0, s, b, dbinfo,
-                               reinterpret_cast<uint64_t*>(X.d_hb2), sync + 1 + (size_t)P * H + 5, c->d_err, ++X.epoch2, rows,
-                               nx, (const uint8_t*)recon);
-        }
-        else {
-            // k_deblock keeps a picture's pairs on one XCD (p % nx): nx times the largest
-            // XCD share of waves, so every XCD runs all its pairs at once
-            const int nx = c->nxcc > 1 && !(c->debug & H264R_DBG_DEBLOCK_GLOBAL) ? c->nxcc : 1;
-            const int grid = nx * ((P + nx - 1) / nx) * npairs;
-            hipLaunchKernelGGL(k_deblock, dim3(grid), dim3(64), 0, s, b, dbinfo,
-                               reinterpret_cast<uint64_t*>(X.d_hb), sync + 1 + (size_t)P * H + 5, c->d_err, ++X.epoch, rows,
-                               nx, recon);
-        }
+    return H264R_OK;
+}
+
+// The deblocking of a stage on stream s (k_deblock2 when by_rows, else k_deblock), or the
+// untiled copy of its reconstruction (H264R_DBG_NO_DEBLOCK).
+static int deblock_launch(h264r_ctx* c, const Stage& S, hipStream_t s, int2 rows, uint8_t* hb, uint32_t epoch, bool by_rows)
+{
+    const h264r_batch& b = S.b;
+    const int W = b.width_mbs, H = b.height_mbs, P = b.num_pics, HB = rows.y - rows.x;
+    const int npairs = (HB + 1) / 2;
+    int* dsync = S.sync + 1 + (size_t)P * H + 5;
+    if (c->debug & H264R_DBG_NO_DEBLOCK) {
+        hipLaunchKernelGGL(k_untile, dim3((W * HB * 32 + 255) / 256, P), dim3(256), 0, s, b, rows, (const uint8_t*)S.recon);
         HIP_OK(hipGetLastError());
+        return H264R_OK;
+    }
+    Timed t(c, 2, s);
+    if (!c->nxcc) {                  // XCDs of the device: the deblocking kernels' placement
+        int nx = 1;
+        if (hipDeviceGetAttribute(&nx, hipDeviceAttributeNumberOfXccs, c->device) != hipSuccess) nx = 1;
+        c->nxcc = std::max(1, std::min(nx, 8));
+    }
+    if (by_rows) {
+        // k_deblock2 keeps a picture group on one XCD (g % nx): nx counters
+        int grid = ((P + DEBLOCK2_PICS - 1) / DEBLOCK2_PICS) * ((HB + H264R_DB2_BAND - 1) / H264R_DB2_BAND);
+        const int nx = grid >= 64 * c->nxcc && !(c->debug & H264R_DBG_DEBLOCK_GLOBAL) ? c->nxcc : 1;
+        grid = (grid + nx - 1) / nx * nx;
+        hipLaunchKernelGGL(k_deblock2, dim3(grid), dim3(64), 0, s, b, S.dbinfo, reinterpret_cast<uint64_t*>(hb), dsync,
+                           c->d_err, epoch, rows, nx, (const uint8_t*)S.recon);
     } else {
-        hipLaunchKernelGGL(k_untile, dim3((W * HB * 32 + 255) / 256, P), dim3(256), 0, s, b, rows, (const uint8_t*)recon);
-        HIP_OK(hipGetLastError());
+        // k_deblock keeps a picture's pairs on one XCD (p % nx): nx times the largest
+        // XCD share of waves, so every XCD runs all its pairs at once
+        const int nx = c->nxcc > 1 && !(c->debug & H264R_DBG_DEBLOCK_GLOBAL) ? c->nxcc : 1;
+        const int grid = nx * ((P + nx - 1) / nx) * npairs;
+        hipLaunchKernelGGL(k_deblock, dim3(grid), dim3(64), 0, s, b, S.dbinfo, reinterpret_cast<uint64_t*>(hb), dsync,
+                           c->d_err, epoch, rows, nx, S.recon);
+    }
+    HIP_OK(hipGetLastError());
+    return H264R_OK;
+}
+
+// rows [row0, row1): the MB rows of every picture this launch reconstructs and deblocks (the
+// whole picture, or a slice-aligned band: h264r_decode_batch_rows).
+//
+// Two schedules, both bit-exact:
+// * one stage: the reconstruction kernels, then the deblocking kernel, on stream s;
+// * overlapped (H264R_OVERLAP=<chunks>, each of >= 64 whole 1080p pictures' worth of MB rows;
+//   off by default: measured slower): the batch is cut into picture chunks; the launch stream reconstructs
+//   chunk after chunk and the context's side stream deblocks chunk k (after an event) while
+//   the launch stream reconstructs chunk k + 1, so the latency-bound deblocking walk shares
+//   the CUs with the issue-bound reconstruction (the order the reference keeps per picture,
+//   deblock.cc:537-552 after decoder.cc:65-79 of every MB, is kept: a picture is deblocked
+//   after all its MBs are reconstructed).  The launch stream then waits for the side stream.
+//   k_intra_levels takes a plain launch here: a cooperative launch waits for the device to be
+//   otherwise idle, which would serialise the two streams.
+static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row0, int row1, Scratch& X)
+{
+    const Knobs& K = knobs();
+    // H264R_DEBUG: the deblocking-schedule flags of h264r_set_debug OR-ed into every launch
+    // (measurement A/B; validated in knobs(): schedule flags only, so the output is unchanged)
+    const int debug_saved = c->debug;
+    c->debug |= K.debug;
+    struct Restore { h264r_ctx* c; int d; ~Restore() { c->debug = d; } } restore{c, debug_saved};
+    const int W = b.width_mbs, H = b.height_mbs, P = b.num_pics, HB = row1 - row0;
+    const int2 rows = make_int2(row0, row1);
+    const int npairs = (HB + 1) / 2;
+    const size_t nmb = (size_t)W * H;
+    const bool wait_test = (c->debug & H264R_DBG_WAIT_TEST) != 0;
+    // chunks of the overlapped schedule: each of >= 64 x 68 picture-MB-rows
+    int nch = (c->debug & H264R_DBG_OVERLAP) ? std::max(K.overlap, 4) : K.overlap;
+    nch = std::min(nch, (int)std::min<int64_t>(P, (int64_t)P * HB / (64 * 68)));
+    if (nch < 2 || wait_test || (c->debug & H264R_DBG_NO_DEBLOCK)) nch = 1;
+    const int chunk_min = P / nch;
+    int st;
+    if ((st = dev_resize(&X.d_dbinfo, &X.c_dbinfo, (size_t)P * nmb * DBINFO_BYTES))) return st;
+    // the reconstruction kernels write the MB-tiled samples (device_common.h), the
+    // deblocking kernel (or k_untile) turns them into the output planes
+    if ((st = dev_resize(&X.d_recon, &X.c_recon, (size_t)P * nmb * 384))) return st;
+    // k_deblock2 needs many (picture group, band) walks in flight: H264R_DEBLOCK2_MIN is the
+    // crossover measured on whole 1080p pictures (68 MB rows), so a launch qualifies by its
+    // picture-rows (a 2160p picture counts twice, a 17-row slice band a quarter); the chunks of
+    // the overlapped schedule all take the schedule of the smallest
+    const bool by_rows = (c->debug & H264R_DBG_DEBLOCK_ROWS) ||
+                         (!(c->debug & H264R_DBG_DEBLOCK_MB) && (int64_t)chunk_min * HB >= (int64_t)K.deblock2_min * 68);
+    // hand-off records of the chosen deblocking kernel, a region per picture; fresh memory or a
+    // wrapping epoch restarts from zeroed records, so no record may carry a live tag
+    uint8_t** hb = by_rows ? &X.d_hb2 : &X.d_hb;
+    size_t* hcap = by_rows ? &X.c_hb2 : &X.c_hb;
+    uint32_t* ep = by_rows ? &X.epoch2 : &X.epoch;
+    const uint32_t ep_max = by_rows ? (1u << 20) - 2 - 16 : 0xFFFFFF00u;
+    const size_t hb_pic = by_rows ? (size_t)W * HANDOFF2_BYTES : (size_t)npairs * W * HANDOFF_BYTES;
+    {
+        const size_t cap_before = *hcap;
+        if ((st = dev_resize(hb, hcap, (size_t)P * hb_pic))) return st;
+        if (*hcap != cap_before || *ep > ep_max) {
+            HIP_OK(hipMemsetAsync(*hb, 0, *hcap, s));
+            *ep = 0;
+        }
+    }
+    const size_t sync_n = (size_t)nch * sync_ints(chunk_min + 1, H);
+    if ((st = dev_resize(&X.d_sync, &X.c_sync, sync_n))) return st;
+    // H264R_DBG_WAIT_TEST: every intra-walk wait asks for progress no row reaches, under a
+    // 10 ms bound -- the launch must drain and h264r_check report H264R_EDEVICE
+    if ((st = set_wait_bound(c, wait_test ? 1000000u : wait_bound_ticks(), s))) return st;
+    const bool levels = nmb <= LEVEL_MAX_MBS && H <= 1024 && level_launches() > 0 &&
+                        !(c->debug & (H264R_DBG_INTRA_WALK | H264R_DBG_WAIT_TEST));
+    if (levels && !c->levels_grid) {
+        // every workgroup of the persistent level kernel must be resident at once: one
+        // block per CU below what the occupancy query reports (MI355X_MICROARCH.md,
+        // residency caveat), at least one per CU
+        int per_cu = 0, cus = 0;
+        HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(k_intra_levels), 256, 0));
+        HIP_OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
+        c->levels_grid = std::max(1, per_cu - K.lvl_margin) * std::max(1, cus);
+        if (K.verbose)
+            fprintf(stderr, "h264r: k_intra_levels occupancy %d blocks/CU, %d CUs, grid %d\n", per_cu, cus, c->levels_grid);
+    }
+    if (levels && ((st = dev_resize(&X.d_lvl, &X.c_lvl, (size_t)P * nmb)) ||
+                   (st = dev_resize(&X.d_list, &X.c_list, (size_t)P * nmb)) ||
+                   (st = dev_resize(&X.d_lcnt, &X.c_lcnt, 3 * (size_t)(LEVEL_LISTS + 2)))))
+        return st;
+    HIP_OK(hipMemsetAsync(X.d_sync, 0, sync_n * sizeof(int), s));
+    if (nch > 1) {
+        if (!c->side) HIP_OK(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+        if (!c->ev_side) HIP_OK(hipEventCreateWithFlags(&c->ev_side, hipEventDisableTiming));
+        while ((int)c->ev_chunk.size() < nch) {
+            hipEvent_t e = nullptr;
+            HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            c->ev_chunk.push_back(e);
+        }
+    }
+    Timed whole(c, 3, s);
+    if (c->timing) c->timed_launches++;
+    for (int k = 0, p0 = 0; k < nch; ++k) {
+        const int n = P / nch + (k < P % nch ? 1 : 0);
+        Stage S{nch > 1 ? sub_batch(b, p0, n) : b, reinterpret_cast<h264r::DbInfo*>(X.d_dbinfo + (size_t)p0 * nmb * DBINFO_BYTES),
+                X.d_recon + (size_t)p0 * nmb * 384,
+                X.d_sync + (size_t)k * sync_ints(chunk_min + 1, H)};
+        if ((st = recon_launches(c, S, s, rows, X, levels, K.coop && nch == 1))) return st;
+        hipStream_t ds = s;
+        if (nch > 1) {
+            HIP_OK(hipEventRecord(c->ev_chunk[k], s));
+            HIP_OK(hipStreamWaitEvent(c->side, c->ev_chunk[k], 0));
+            ds = c->side;
+        }
+        if ((st = deblock_launch(c, S, ds, rows, *hb + (size_t)p0 * hb_pic, ++*ep, by_rows))) return st;
+        p0 += n;
+    }
+    if (nch > 1) {
+        HIP_OK(hipEventRecord(c->ev_side, c->side));
+        HIP_OK(hipStreamWaitEvent(s, c->ev_side, 0));
     }
     return H264R_OK;
 }
@@ -699,6 +807,7 @@ int h264r_check(h264r_ctx* c)
     (void)hipSetDevice(c->device);
     HIP_OK(hipStreamSynchronize(c->stream));
     if (c->last_stream) HIP_OK(hipStreamSynchronize(c->last_stream));
+    if (c->side) HIP_OK(hipStreamSynchronize(c->side));
     int e = 0;
     HIP_OK(hipMemcpy(&e, c->d_err, sizeof(int), hipMemcpyDeviceToHost));
     if (e) { (void)hipMemset(c->d_err, 0, sizeof(int)); return H264R_EDEVICE; }

@@ -78,6 +78,23 @@ struct alignas(16) UnitLds {
 };
 static_assert(sizeof(UnitLds) == 848, "UnitLds layout");
 
+// A unit's output staging: the final samples of its MB row, collected per group of 4 MBs (luma)
+// and 8 MBs (chroma), so that the output planes take whole 64-byte pieces of their rows (16- and
+// 8-byte row pieces, each of a line the walk completes only 8 steps later, had left L2 partly
+// written: 2.8x the output bytes written, and the stores took 1.8 of the kernel's 5.0 ms;
+// profiles/r05_l_deblock_store_ab.txt).  Rows 13..15 (chroma 7) of a row are final only after the
+// row below has filtered its top edges: the unit below writes them into this unit's staging
+// (same wave), or, for the band's first row, into its own `yu` / `cu` (the row above is
+// another wave's).
+struct alignas(16) StageLds {
+    uint32_t y[16][4][4];      // luma rows 0..15, MB m & 3 of the 4-MB group: 16 bytes
+    uint32_t c[2][8][8][2];    // chroma plane, rows 0..7, MB m & 7 of the 8-MB group: 8 bytes
+    uint32_t yu[3][4][4];      // band's first row: rows 13..15 of the row above
+    uint32_t cu[2][8][2];      // band's first row: chroma row 7 of the row above
+    uint32_t pad[4];           // unit stride 596 dwords (20 banks apart)
+};
+static_assert(sizeof(StageLds) == 2384, "StageLds layout");
+
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));   // native vectors: registers, not stack
 typedef uint32_t v2u __attribute__((ext_vector_type(2)));
 
@@ -135,11 +152,17 @@ extern "C" void h264r_db2_trace_copy(void* dst) { (void)hipMemcpyFromSymbol(dst,
 #ifndef H264R_DB2_DIAG
 #define H264R_DB2_DIAG 0   // diagnostic builds only (wrong output): bit 0 drops the output stores, bit 1 fetches MB 0
 #endif
-extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_deblock2(
+extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_deblock2(
     h264r_batch b, const DbInfo* __restrict__ dbinfo, uint64_t* hb, int* sync, int* err, uint32_t epoch, int2 rows, int nx,
     const uint8_t* __restrict__ recon)
 {
     __shared__ UnitLds S[UNITS];
+    __shared__ StageLds G[UNITS];
+#ifdef H264R_DB2_LDS_PAD
+    // measurement builds only: LDS padding that lowers the resident waves per CU
+    __shared__ uint32_t lds_pad[H264R_DB2_LDS_PAD / 4];
+    if (threadIdx.x == 0 && epoch == 0xFFFFFFFFu) { lds_pad[0] = 1; __syncthreads(); err[0] = lds_pad[0]; }
+#endif
     const Geom g = make_geom(b.width_mbs, b.height_mbs);
     const int W = g.wmb, R0 = rows.x, R1 = rows.y;
     const int ngroups = (b.num_pics + PICS - 1) / PICS;
@@ -185,6 +208,8 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3
 
     UnitLds& U = S[u];
     const UnitLds& A = S[rb ? u - PICS : u];                  // the unit of the row above (rb > 0)
+    StageLds& T = G[u];
+    StageLds& TA = G[rb ? u - PICS : u];                      // its staging
     const uint32_t Wl = (uint32_t)g.W, Wc = (uint32_t)g.Wc;
     const uint32_t ysz = (uint32_t)g.ysz, csz = (uint32_t)g.csz;
     // the group's output planes through wave-uniform descriptors; per-lane byte offsets of
@@ -235,25 +260,73 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3
             *reinterpret_cast<v2u*>(&U.c[j][2 * q + 1][2 * s]) = wc[j].zw;
         }
     };
-    // Rows the row below still changes (luma 13..15, chroma 7) become a second store of row
-    // 12 / 6 with the same bytes.
-    const int ylast = last_row ? 15 : 12, clast = last_row ? 7 : 6;
-    // final MB m (slot s): luma rows 4i + q; chroma instruction i: plane i / 2, row 4 (i & 1) + q
-    auto store_mb = [&](int m, int s, bool ok) {
-#if H264R_DB2_DIAG & 1
-        ok = false;                      // diagnostic build: output stores dropped
-#endif
-        const uint32_t yb = (ok ? yrow : OOB) + (uint32_t)max(m, 0) * 16u;
-        const uint32_t cb = (ok ? crow : OOB) + (uint32_t)max(m, 0) * 8u;
+    // Rows 0..12 (chroma 0..6) of a row are final once the next MB's left edge is filtered, rows
+    // 13..15 (chroma 7) once the row below has filtered its top edges -- or at once in the
+    // launch's last row, and never in this wave for the band's last row (the next band's first
+    // row stores them).
+    const int ylast = last_row || rb < BAND - 1 ? 15 : 12, clast = last_row || rb < BAND - 1 ? 7 : 6;
+    // final MB m (slot s) into the staging: luma rows 4i + q; chroma instruction i: plane i / 2,
+    // row 4 (i & 1) + q (rows 13..15 / 7 are overwritten by the row below when it has filtered them)
+    auto stage_own = [&](int m, int s) {
+        const int mc = max(m, 0);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const int r = min(4 * i + q, ylast);
-            st16<OUT_AUX>(rY, yb + (uint32_t)r * Wl, *reinterpret_cast<const v4u*>(&U.y[r][4 * s]));
+            const int r = 4 * i + q;
+            *reinterpret_cast<v4u*>(&T.y[r][mc & 3][0]) = *reinterpret_cast<const v4u*>(&U.y[r][4 * s]);
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const int pl = i >> 1, r = min(4 * (i & 1) + q, clast);
-            st8<OUT_AUX>(pl ? rV : rU, cb + (uint32_t)r * Wc, *reinterpret_cast<const v2u*>(&U.c[pl][r][2 * s]));
+            const int pl = i >> 1, r = 4 * (i & 1) + q;
+            *reinterpret_cast<v2u*>(&T.c[pl][r][mc & 7][0]) = *reinterpret_cast<const v2u*>(&U.c[pl][r][2 * s]);
+        }
+    };
+    // The groups that are complete at the end of a step, stored by the whole wave: each unit's
+    // flag (its four lanes agree) as a wave-uniform mask, one unit per luma instruction (16 rows
+    // x 4 MBs = 64 lanes), one unit and plane per chroma instruction (8 rows x 8 MBs); a group
+    // cut by the row end stores its MBs only.  Byte offsets per lane, OOB for lanes without a
+    // sample (dropped by the buffer unit).
+    auto store_groups = [&](int xs) {
+        const int mo = xs - 1;                                   // final since V(xs), rows 13..15 now
+        const bool own = active && mo >= 0 && mo < W;
+        const int r = lane >> 2, pp = lane & 3, rc = lane >> 3, mm = lane & 7;
+        for (uint64_t bm = __ballot(own && q == 0 && ((mo & 3) == 3 || mo == W - 1)); bm; bm &= bm - 1) {
+            const int l0 = __builtin_ctzll(bm), u2 = l0 >> 2;
+            const int m2 = __builtin_amdgcn_readlane(mo, l0), yl2 = __builtin_amdgcn_readlane(ylast, l0);
+            const uint32_t yr2 = (uint32_t)__builtin_amdgcn_readlane((int)yrow, l0);
+            const int g0 = m2 & ~3;
+            const bool ok = r <= yl2 && g0 + pp <= m2;
+            st16<OUT_AUX>(rY, ok ? yr2 + (uint32_t)r * Wl + (uint32_t)(g0 + pp) * 16u : OOB,
+                          *reinterpret_cast<const v4u*>(&G[u2].y[r][pp][0]));
+        }
+        for (uint64_t bm = __ballot(own && q == 0 && ((mo & 7) == 7 || mo == W - 1)); bm; bm &= bm - 1) {
+            const int l0 = __builtin_ctzll(bm), u2 = l0 >> 2;
+            const int m2 = __builtin_amdgcn_readlane(mo, l0), cl2 = __builtin_amdgcn_readlane(clast, l0);
+            const uint32_t cr2 = (uint32_t)__builtin_amdgcn_readlane((int)crow, l0);
+            const int g8 = m2 & ~7;
+            const bool ok = rc <= cl2 && g8 + mm <= m2;
+            const uint32_t off = ok ? cr2 + (uint32_t)rc * Wc + (uint32_t)(g8 + mm) * 8u : OOB;
+            st8<OUT_AUX>(rU, off, *reinterpret_cast<const v2u*>(&G[u2].c[0][rc][mm][0]));
+            st8<OUT_AUX>(rV, off, *reinterpret_cast<const v2u*>(&G[u2].c[1][rc][mm][0]));
+        }
+        // the band's first row: rows 13..15 (chroma 7) of the row above, final since H(xs)
+        const bool up = active && rb == 0 && above && xs >= 0 && xs < W;
+        for (uint64_t bm = __ballot(up && q == 0 && ((xs & 3) == 3 || xs == W - 1)); bm; bm &= bm - 1) {
+            const int l0 = __builtin_ctzll(bm), u2 = l0 >> 2;
+            const int x2 = __builtin_amdgcn_readlane(xs, l0);
+            const uint32_t yr2 = (uint32_t)__builtin_amdgcn_readlane((int)yrow, l0);
+            const int g0 = x2 & ~3;
+            const bool ok = r < 3 && g0 + pp <= x2;
+            st16<OUT_AUX>(rY, ok ? yr2 - (uint32_t)(3 - r) * Wl + (uint32_t)(g0 + pp) * 16u : OOB,
+                          *reinterpret_cast<const v4u*>(&G[u2].yu[min(r, 2)][pp][0]));
+        }
+        for (uint64_t bm = __ballot(up && q == 0 && ((xs & 7) == 7 || xs == W - 1)); bm; bm &= bm - 1) {
+            const int l0 = __builtin_ctzll(bm), u2 = l0 >> 2;
+            const int x2 = __builtin_amdgcn_readlane(xs, l0);
+            const uint32_t cr2 = (uint32_t)__builtin_amdgcn_readlane((int)crow, l0);
+            const int g8 = x2 & ~7;
+            const uint32_t off = rc == 0 && g8 + mm <= x2 ? cr2 - Wc + (uint32_t)(g8 + mm) * 8u : OOB;
+            st8<OUT_AUX>(rU, off, *reinterpret_cast<const v2u*>(&G[u2].cu[0][mm][0]));
+            st8<OUT_AUX>(rV, off, *reinterpret_cast<const v2u*>(&G[u2].cu[1][mm][0]));
         }
     };
     // granule i of consumer lane c of MB m in slot s: luma row 12+i dword c (i < 4), chroma
@@ -426,7 +499,14 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3
         }
         // 5. MB x-1 is final (V(x) done): it leaves the ring, and MB x+1 (fetched during the
         // previous step) takes its slot with its DbInfo
-        store_mb(x - 1, sl, active && x >= 1 && x <= W);
+#if !(H264R_DB2_DIAG & 1)
+        // the groups the previous step completed (issued here, a whole step before the next wait
+        // on this wave's loads, which vmcnt orders behind them), read before MB x-1 takes the
+        // first slot of the next group (a wave's LDS operations execute in issue order)
+        store_groups(x - 1);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+#endif
+        stage_own(x - 1, sl);                    // MB x-1 is final (rows 13..15: below)
         wave_sync();                             // every lane has read slot sl
         fill(sl);
         put_info(active && x + 1 >= 0 && x + 1 < W);
@@ -487,17 +567,13 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3
         // change, four per lane; rows 13..15 (chroma 7) of MB (x, y-1)
 #pragma unroll
         for (int j = 0; j < 2; ++j) publish_pair(xok ? rec_out : OOB, max(x, 0), sc, early_c(q, j), early_k(q, j));
-        {
-#if H264R_DB2_DIAG & 1
-            const uint32_t yb = OOB + (uint32_t)max(x, 0) * 16u + 4u * (uint32_t)q;
-#else
-            const uint32_t yb = (xok && above ? yrow : OOB) + (uint32_t)max(x, 0) * 16u + 4u * (uint32_t)q;
+        // rows 13..15 (chroma 7) of MB (x, y-1), final now: into the staging of the unit above, or
+        // (the band's first row) into this unit's own
+        if (xok && above) {
+            uint32_t* yd = rb ? &TA.y[13][x & 3][q] : &T.yu[0][x & 3][q];
 #pragma unroll
-#endif
-            for (int r = 1; r < 4; ++r) st4<OUT_AUX>(rY, yb - (uint32_t)(4 - r) * Wl, wy[r]);
-            const uint32_t cb = (xok && above ? crow : OOB) + (uint32_t)max(x, 0) * 8u + 4u * (uint32_t)d - Wc;
-            st4<OUT_AUX>(rU, p ? OOB : cb, wcv[1]);
-            st4<OUT_AUX>(rV, p ? cb : OOB, wcv[1]);
+            for (int r = 1; r < 4; ++r) yd[(r - 1) * 16] = wy[r];
+            *(rb ? &TA.c[p][7][x & 7][d] : &T.cu[p][x & 7][d]) = wcv[1];
         }
         // 8. what the next step fills: MB x+2 and its DbInfo
         fetch(x + 2);
@@ -505,6 +581,12 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3
         wave_sync();                             // H(x) of every unit is in LDS
         TRACE({ const unsigned long long t2 = __builtin_amdgcn_s_memtime(); tph[3] += t2 - tm; tm = t2; })
     }
+#if !(H264R_DB2_DIAG & 1)
+    if (ok) {                            // the groups the last step completed
+        wave_sync();
+        store_groups(x - 1);
+    }
+#endif
     if (!ok) {
         // release the band below (the error is flagged)
         for (int m = 0; m < W; ++m)

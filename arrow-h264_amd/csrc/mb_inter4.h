@@ -1013,6 +1013,19 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
             }
         }
         // ---- construction + store, luma
+#if H264R_INTER_DIAG & 1
+        {   // diagnostic build (wrong output): one 16-byte store per lane, an MB's 16 lanes contiguous
+            uint32_t wv4[4];
+    #pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                uint32_t wv = 0;
+    #pragma unroll
+                for (int c = 0; c < 4; ++c) wv |= (uint32_t)clip255((int)((predY[i] >> (8 * c)) & 255) + res[i][c]) << (8 * c);
+                wv4[i] = wv;
+            }
+            *reinterpret_cast<uint4*>(rmb + blk * 16) = make_uint4(wv4[0], wv4[1], wv4[2], wv4[3]);
+        }
+#else
     #pragma unroll
         for (int i = 0; i < 4; ++i) {
             uint32_t wv = 0;
@@ -1020,6 +1033,7 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
             for (int c = 0; c < 4; ++c) wv |= (uint32_t)clip255((int)((predY[i] >> (8 * c)) & 255) + res[i][c]) << (8 * c);
             *reinterpret_cast<uint32_t*>(ydst + i * 16) = wv;
         }
+#endif
 
         // ---- chroma residual (transform.cc:1081-1091, DC :875-889): chroma block cb is
         // spread over lanes {blk, ^1, ^4, ^5}; my quadrant rows cr.., cols cc..

@@ -7,16 +7,18 @@ batch of synthetic pictures already resident in HBM (B independent 
 sharing a reference set).  Workload: SURVEY config 3, 1080p (120x68 MBs) IPPP Main P
 pictures, B = 1024 per GPU (the order-dependent walks need many pictures in flight).
 
-N > 1 GPUs (default): chain mode on config 5 (2160p High B pictures, 8 slices,
-disable_deblocking_filter_idc 2), slice-sharded: K = 32 x N dependent chains advance one
-picture per step, each rank decodes its band of slices of every picture, and the rows of
-the other bands that its next motion compensation can reach come in by point-to-point RCCL
-transfers over xGMI (or --exchange allgather: every band).  Weak scaling; the JSON also
-carries the one-GPU line of the same mode (`same_mode_n1`).  `--gpus N` without a launcher
-starts the N ranks itself (torch.distributed.run as a child process); under
+N > 1 GPUs (default): the headline workload as N replicas (config 3 pictures, B per rank, no
+collective: disable_deblocking_filter_idc 0 chains every MB of a picture through the loop filter,
+deblock.cc:547-551), value = all ranks' MBs / the slowest rank's time -- the same workload as the
+one-GPU line, so the scaling curve compares like with like.  Beside it in the same line,
+`slice_sharded`: chain mode on config 5 (2160p High B pictures, 8 slices,
+disable_deblocking_filter_idc 2), K = 32 x N dependent chains advance one picture per step, each
+rank decodes its band of slices of every picture, and the rows of the other bands that its next
+motion compensation can reach come in by point-to-point RCCL transfers over xGMI (or --exchange
+allgather: every band); weak scaling, with the one-GPU line of the same mode (`same_mode_n1`)
+and its CPU baseline.  `--mode chain` makes the chain line the whole output.  `--gpus N`
+without a launcher starts the N ranks itself (torch.distributed.run as a child process); under
 `torch.distributed.run` one process per GPU reads RANK / LOCAL_RANK / WORLD_SIZE.
-Config 3 (idc 0) chains every MB of a picture through the loop filter
-(deblock.cc:547-551): `--mode throughput --shard replicas` runs N independent replicas.
 
 Prints ONE JSON line on rank 0.
 """
@@ -312,19 +314,21 @@ def chain_run(args, rank: int, world: int, local: int, cs, rehearse: bool, nchai
         step()
         torch.cuda.synchronize()
         dec.check()
-        G = groups[0]
-        want0 = O.decode(G["pics"][0], refs)
-        want1 = O.decode(G["pics"][0], [want0] + list(refs[1:]))
         rows = (16, 8, 8)
         ok = True
-        for t, want, lo, hi in ((0, want0, max(band[0] - halo, 0), min(band[1] + halo, H)), (1, want1, band[0], band[1])):
-            if exchange == "allgather" and t == 0:
-                lo, hi = 0, H
-            if hi <= lo:
-                continue
-            for k3 in range(3):
-                got = G["sets"][t][k3][: psz[k3]].cpu().numpy().reshape(want[k3].shape)
-                ok &= bool(np.array_equal(got[lo * rows[k3]:hi * rows[k3]], want[k3][lo * rows[k3]:hi * rows[k3]]))
+        # chain 0 of the first group and the last chain of the last group (its pictures sit at
+        # the far end of the batch and read their own DPB table: ref_planes_stride)
+        for G, k in ((groups[0], 0), (groups[-1], nk - 1)):
+            want0 = O.decode(G["pics"][k], refs)
+            want1 = O.decode(G["pics"][k], [want0] + list(refs[1:]))
+            for t, want, lo, hi in ((0, want0, max(band[0] - halo, 0), min(band[1] + halo, H)), (1, want1, band[0], band[1])):
+                if exchange == "allgather" and t == 0:
+                    lo, hi = 0, H
+                if hi <= lo:
+                    continue
+                for k3 in range(3):
+                    got = G["sets"][t][k3][k * psz[k3]: (k + 1) * psz[k3]].cpu().numpy().reshape(want[k3].shape)
+                    ok &= bool(np.array_equal(got[lo * rows[k3]:hi * rows[k3]], want[k3][lo * rows[k3]:hi * rows[k3]]))
         verified = bool(ok) if world == 1 else \
             bool(D.min_over_ranks(1.0 if ok else 0.0, device="cpu" if rehearse else "cuda") == 1.0)
     for _ in range(args.warmup):
@@ -360,8 +364,31 @@ def chain_run(args, rank: int, world: int, local: int, cs, rehearse: bool, nchai
     xin = groups[0]["xch"].bytes_in() * ng if world > 1 else 0
     del groups, dec
     torch.cuda.empty_cache()
+    # PMC traffic of this mode (tools/pmc.sh over a chain-mode run -> profiles/traffic_c<N>_chain.json)
+    traffic, traffic_src = None, None
+    tpath = os.path.join(ROOT, "profiles", f"traffic_c{cfg_idx}_chain.json")
+    if os.path.exists(tpath):
+        tj = json.load(open(tpath))
+        if tj.get("survey_config") == cfg_idx:
+            per_mb = sum(v["traffic_bytes_per_mb"] for v in tj["kernels"].values())
+            traffic = int(per_mb * nchains * nmb * frac_rows)   # this rank's band of every chain
+            traffic_src = f"{os.path.basename(tpath)} ({tj.get('source')}): all kernels of the sequence"
+    # the CPU path beside it (rank 0 at one GPU): the oracle port on a bounded sample of the same
+    # pictures, 1 thread and a thread pool (a chain's picture costs the CPU what an independent one does)
+    cpu = cpu_mt = None
+    if world == 1 and not args.no_cpu:
+        done, el, ncpu = cpu_baseline(cfg, refs, args.cpu_seconds)
+        cpu = {"value": done / el, "unit": "macroblocks/s", "cores": 1, "kind": "port",
+               "sample": f"{ncpu} pictures of {CONFIG_NAMES[cfg_idx]} ({ncpu * nmb} MBs, {el:.1f} s) decoded by "
+                         f"oracle/h264r_oracle.c (1 thread) on {cpu_model()}"}
+        thr = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+        done, el, ncpu = cpu_baseline_threads(cfg, refs, args.cpu_seconds / 2, thr)
+        cpu_mt = {"value": done / el, "unit": "macroblocks/s", "cores": thr, "kind": "port",
+                  "sample": f"{ncpu} pictures ({ncpu * nmb} MBs, {el:.1f} s) over {thr} threads, "
+                            f"oracle_decode_pictures, on {cpu_model()}"}
     return {
-        "metric": "macroblocks/s (decode reconstruct, post-entropy) 1080p P-frame; % HBM roofline",
+        "metric": f"macroblocks/s (decode reconstruct, post-entropy) {CONFIG_NAMES[cfg_idx]}, dependent chains"
+                  f"{', slice-sharded' if world > 1 else ''}; % HBM roofline",
         "value": value, "unit": "macroblocks/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "u8", "data": "synthetic (seeded SURVEY 8(d) generator, arrow-h264_amd/csrc/synth.c)",
@@ -372,7 +399,7 @@ def chain_run(args, rank: int, world: int, local: int, cs, rehearse: bool, nchai
                    "parallelism": f"slices{world}" if world > 1 else "single",
                    "rows_this_rank": list(band), "bands": [list(b) for b in bands]},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": "h264r_decode_batch launch sequences of the chain groups (one per group)",
                      "kernel_ms": float(kern[3]), "kernel_algo_bytes": step_bytes,
                      "numerator": "SURVEY 8(d) R+W of this rank's band of the step's pictures"},
@@ -382,7 +409,8 @@ def chain_run(args, rank: int, world: int, local: int, cs, rehearse: bool, nchai
                      "bytes_in_per_rank_per_step": xin,
                      "ops_per_step": (0 if world == 1 else ng * (1 if exchange == "allgather" else
                                                                  len(groups_peers(bands, rank, halo))))},
-        "cpu_baseline": None,
+        "cpu_baseline": cpu,
+        "cpu_baseline_threads": cpu_mt,
         "verified_vs_oracle": verified,
     }
 
@@ -407,104 +435,16 @@ def spawn_ranks(args) -> int:
     return subprocess.run(cmd).returncode
 
 
-def main() -> int:
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1,
-                    help="GPUs = ranks; without WORLD_SIZE in the environment bench.py starts them itself")
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", type=int, default=None, choices=[2, 3, 4, 5],
-                    help="SURVEY 8(d) workload (default: 3 at one GPU, 5 at N > 1)")
-    ap.add_argument("--mode", choices=["throughput", "chain"], default=None,
-                    help="throughput: independent pictures sharing a reference set (default at one GPU); "
-                         "chain: dependent chains, slice-sharded over the ranks (default at N > 1)")
-    ap.add_argument("--batch", type=int, default=0, help="throughput mode: pictures per GPU per step (default 1024 for configs 2/3, 256 for 4, 64 at 2160p)")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=16, help="threads of the multi-threaded CPU baseline")
-    ap.add_argument("--no-verify", action="store_true")
-    ap.add_argument("--latency-pictures", type=int, default=32,
-                    help="length of the dependent-chain latency run (rank 0, N=1; 0 = skip)")
-    ap.add_argument("--traffic-json", default=None, help="PMC traffic summary (default profiles/traffic.json, "
-                    "profiles/traffic_c<config>.json for other configs when present)")
-    ap.add_argument("--chain", type=int, default=0,
-                    help="chain mode with this many chains in all (a multiple of --chain-groups); "
-                         "default chains-per-gpu x N")
-    ap.add_argument("--chain-groups", type=int, default=1,
-                    help="chain mode: launches per step (groups of chains); with 2 or more the exchange of one "
-                         "group overlaps the decode of the next")
-    ap.add_argument("--chains-per-gpu", type=int, default=32,
-                    help="chain mode: chains per GPU (weak scaling: the job holds chains-per-gpu x N chains)")
-    ap.add_argument("--exchange", choices=["halo", "allgather"], default="halo",
-                    help="chain mode at N > 1: rows within the motion vectors' reach from the neighbouring "
-                         "bands (point-to-point), or every band (all-gather)")
-    ap.add_argument("--no-n1", action="store_true", help="chain mode at N > 1: skip the one-GPU line of the same mode")
-    ap.add_argument("--shard", choices=["replicas", "slices"], default=None,
-                    help="throughput mode at N>1: independent pictures per GPU, or slice bands of shared pictures "
-                         "(default: slices for configs 4/5, replicas for 2/3)")
-    args = ap.parse_args()
-
-    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        return spawn_ranks(args)
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
-    mode = "chain" if args.chain else (args.mode or ("throughput" if world == 1 or args.shard else "chain"))
-    if args.config is None:
-        args.config = 5 if (world > 1 and mode == "chain") else 3
-
+def throughput_run(args, rank: int, world: int, local: int, cs, rehearse: bool, ranks: dict):
+    """Throughput mode (the one-GPU headline; at N > 1 replicas, or slice bands with --shard
+    slices): B pictures per rank per step, one h264r_decode_batch each.  Returns the JSON
+    line's dict on rank 0, None on the other ranks."""
     import torch
     import torch.distributed as dist
     import h264r
     from h264r import batch as B
     from h264r import synth
     from h264r import dist as D
-
-    # H264R_BENCH_REHEARSE=1 (testing the N > 1 code path on a one-GPU box): every rank on
-    # device 0, gloo instead of RCCL (RCCL refuses two ranks on one GPU); never a measurement
-    rehearse = os.environ.get("H264R_BENCH_REHEARSE") == "1"
-    if rehearse:
-        local = 0
-    torch.cuda.set_device(local)
-    # every device operation of this process (allocations, uploads, decode, exchange,
-    # checks) goes on ONE explicit stream, which is also the stream the library launches
-    # on: torch's default stream is the legacy NULL stream, which the C ABI would map to
-    # the context's own stream (ADVICE r01: unordered with torch's fills and copies)
-    cs = torch.cuda.Stream(device=local)
-    torch.cuda.set_stream(cs)
-    backend = None
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        if rehearse:
-            dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        backend = dist.get_backend()
-        assert dist.get_world_size() == args.gpus, (dist.get_world_size(), args.gpus)
-        dist.barrier()                                  # communicators up before any P2P
-    ranks = {"backend": backend, "rccl_ranks": dist.get_world_size() if backend == "nccl" else 0,
-             "ranks": world, "rehearsal": rehearse}
-
-    if mode == "chain":
-        nch = args.chain or args.chains_per_gpu * world
-        out = chain_run(args, rank, world, local, cs, rehearse, nch, args.config, args.exchange)
-        out["distributed"] = ranks
-        if world > 1 and not args.no_n1:
-            # the one-GPU line of the same mode and per-GPU load (weak scaling reference), on
-            # rank 0 alone after the N-rank run; the other ranks wait at the barrier
-            if rank == 0:
-                n1 = chain_run(args, 0, 1, local, cs, rehearse, nch // world, args.config, args.exchange)
-                out["same_mode_n1"] = {k: n1[k] for k in ("value", "ms_per_step", "verified_vs_oracle", "kernel_ms")}
-                out["same_mode_n1"]["chains"] = n1["config"]["chains"]
-                out["scaling_vs_same_mode_n1"] = out["value"] / (world * n1["value"])
-            dist.barrier()
-        if rank == 0:
-            print(json.dumps(out))
-        if world > 1:
-            dist.destroy_process_group()
-        return 0
 
     L = h264r.lib()
     W, H = CONFIG_SIZE[args.config]
@@ -801,6 +741,134 @@ def main() -> int:
             # the HBM fraction the path could reach if every kernel issued VALU back to back at
             # today's instruction counts (the ceiling the second roof puts on the first)
             out["roofline"]["frac_ceiling_at_valu_floor"] = step_bytes / (vf * 1e-3) / 1e9 / HBM_PEAK_GBS
+        return out
+    return None
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="GPUs = ranks; without WORLD_SIZE in the environment bench.py starts them itself")
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", type=int, default=None, choices=[2, 3, 4, 5],
+                    help="SURVEY 8(d) workload (default: 3 at one GPU, 5 at N > 1)")
+    ap.add_argument("--mode", choices=["throughput", "chain"], default=None,
+                    help="throughput: independent pictures sharing a reference set (default at one GPU); "
+                         "chain: dependent chains, slice-sharded over the ranks (default at N > 1)")
+    ap.add_argument("--batch", type=int, default=0, help="throughput mode: pictures per GPU per step (default 1024 for configs 2/3, 256 for 4, 64 at 2160p)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16, help="threads of the multi-threaded CPU baseline")
+    ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--latency-pictures", type=int, default=32,
+                    help="length of the dependent-chain latency run (rank 0, N=1; 0 = skip)")
+    ap.add_argument("--traffic-json", default=None, help="PMC traffic summary (default profiles/traffic.json, "
+                    "profiles/traffic_c<config>.json for other configs when present)")
+    ap.add_argument("--chain", type=int, default=0,
+                    help="chain mode with this many chains in all (a multiple of --chain-groups); "
+                         "default chains-per-gpu x N")
+    ap.add_argument("--chain-groups", type=int, default=1,
+                    help="chain mode: launches per step (groups of chains); with 2 or more the exchange of one "
+                         "group overlaps the decode of the next")
+    ap.add_argument("--chains-per-gpu", type=int, default=32,
+                    help="chain mode: chains per GPU (weak scaling: the job holds chains-per-gpu x N chains)")
+    ap.add_argument("--exchange", choices=["halo", "allgather"], default="halo",
+                    help="chain mode at N > 1: rows within the motion vectors' reach from the neighbouring "
+                         "bands (point-to-point), or every band (all-gather)")
+    ap.add_argument("--no-n1", action="store_true", help="chain mode at N > 1: skip the one-GPU line of the same mode")
+    ap.add_argument("--no-sliced", action="store_true",
+                    help="N > 1 default: skip the slice-sharded config-5 chain line reported beside the replicas")
+    ap.add_argument("--shard", choices=["replicas", "slices"], default=None,
+                    help="throughput mode at N>1: independent pictures per GPU, or slice bands of shared pictures "
+                         "(default: slices for configs 4/5, replicas for 2/3)")
+    args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return spawn_ranks(args)
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
+    mode = "chain" if args.chain else (args.mode or "throughput")
+    # N > 1 with no --mode: the headline workload as replicas (the value the scaling curve
+    # compares with the one-GPU line), plus the slice-sharded dependent-chain run of config 5
+    # beside it in the same JSON line (`slice_sharded`)
+    sliced = world > 1 and args.mode is None and not args.chain and not args.no_sliced
+    if args.config is None:
+        args.config = 5 if mode == "chain" else 3
+
+    import torch
+    import torch.distributed as dist
+    import h264r
+    from h264r import batch as B
+    from h264r import synth
+    from h264r import dist as D
+
+    # H264R_BENCH_REHEARSE=1 (testing the N > 1 code path on a one-GPU box): every rank on
+    # device 0, gloo instead of RCCL (RCCL refuses two ranks on one GPU); never a measurement
+    rehearse = os.environ.get("H264R_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local = 0
+    torch.cuda.set_device(local)
+    # every device operation of this process (allocations, uploads, decode, exchange,
+    # checks) goes on ONE explicit stream, which is also the stream the library launches
+    # on: torch's default stream is the legacy NULL stream, which the C ABI would map to
+    # the context's own stream (ADVICE r01: unordered with torch's fills and copies)
+    cs = torch.cuda.Stream(device=local)
+    torch.cuda.set_stream(cs)
+    backend = None
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = dist.get_backend()
+        assert dist.get_world_size() == args.gpus, (dist.get_world_size(), args.gpus)
+        dist.barrier()                                  # communicators up before any P2P
+    ranks = {"backend": backend, "rccl_ranks": dist.get_world_size() if backend == "nccl" else 0,
+             "ranks": world, "rehearsal": rehearse}
+
+    if mode == "chain":
+        nch = args.chain or args.chains_per_gpu * world
+        out = chain_run(args, rank, world, local, cs, rehearse, nch, args.config, args.exchange)
+        out["distributed"] = ranks
+        if world > 1 and not args.no_n1:
+            # the one-GPU line of the same mode and per-GPU load (weak scaling reference), on
+            # rank 0 alone after the N-rank run; the other ranks wait at the barrier
+            if rank == 0:
+                n1 = chain_run(args, 0, 1, local, cs, rehearse, nch // world, args.config, args.exchange)
+                out["same_mode_n1"] = {k: n1[k] for k in ("value", "ms_per_step", "verified_vs_oracle", "kernel_ms")}
+                out["same_mode_n1"]["chains"] = n1["config"]["chains"]
+                out["scaling_vs_same_mode_n1"] = out["value"] / (world * n1["value"])
+            dist.barrier()
+        if rank == 0:
+            print(json.dumps(out))
+        if world > 1:
+            dist.destroy_process_group()
+        return 0
+
+    out = throughput_run(args, rank, world, local, cs, rehearse, ranks)
+    if sliced:
+        # the slice-sharded line: config 5 chains, each rank its band of every picture, the halo
+        # rows over RCCL; then rank 0 alone runs the same mode at one GPU (its weak-scaling
+        # reference).  Reported beside the headline, which stays the replicas of config 3.
+        torch.cuda.empty_cache()
+        dist.barrier()
+        nch = args.chains_per_gpu * world
+        sl = chain_run(args, rank, world, local, cs, rehearse, nch, 5, args.exchange)
+        if rank == 0:
+            n1 = chain_run(args, 0, 1, local, cs, rehearse, nch // world, 5, args.exchange)
+            keep = ("metric", "value", "unit", "ms_per_step", "config", "roofline", "kernel_ms", "exchange",
+                    "verified_vs_oracle")
+            out["slice_sharded"] = {k: sl[k] for k in keep}
+            out["slice_sharded"]["same_mode_n1"] = {k: n1[k] for k in ("value", "ms_per_step", "verified_vs_oracle",
+                                                                      "kernel_ms", "cpu_baseline")}
+            out["slice_sharded"]["same_mode_n1"]["chains"] = n1["config"]["chains"]
+            out["slice_sharded"]["scaling_vs_same_mode_n1"] = sl["value"] / (world * n1["value"])
+        dist.barrier()
+    if rank == 0:
         print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()

@@ -267,10 +267,12 @@ int  h264r_ref_planes(h264r_ctx* ctx, int slot, uint8_t** y, uint8_t** u, uint8_
 
 /* ---- instrumentation ------------------------------------------------------------- */
 /* Average device time (ms) per h264r_decode_batch of the launches made since timing was
- * enabled, measured with HIP events on each launch's stream: out[0] the inter kernel
- * (k_inter4), out[1] the intra kernels (k_level + k_intra_levels + k_intra_pic),
- * out[2] deblocking (k_deblock / k_deblock2), out[3] the whole batch.  Returns
- * H264R_OK or an error. */
+ * enabled, measured with HIP events on each launch's stream: out[0] the deblocking records
+ * and the inter / I_PCM reconstruction (k_dbinfo + k_inter4r + k_inter_sp), out[1] the intra
+ * kernels (k_level + k_level_scan + k_level_scatter + k_intra_levels + k_intra_pic), out[2]
+ * deblocking (k_deblock / k_deblock2), out[3] the whole batch (the wall time of the launch
+ * sequence on the launch stream; under the overlapped schedule out[0..2] are busy times that
+ * overlap).  Returns H264R_OK or an error. */
 int  h264r_last_timing(h264r_ctx* ctx, float out_ms[4]);
 int  h264r_set_timing(h264r_ctx* ctx, int enable);
 /* Debug hook: H264R_DBG_NO_DEBLOCK skips the loop filter (reconstruction only, to
@@ -294,6 +296,10 @@ int  h264r_set_timing(h264r_ctx* ctx, int enable);
  * launch drains and h264r_check returns H264R_EDEVICE (the output is invalid).  The
  * bound of every wait is wall time: 2 s by default (environment H264R_WAIT_MS). */
 #define H264R_DBG_WAIT_TEST 32
+/* The overlapped schedule (off by default: measured slower): large batches
+ * cut into 4 picture chunks (H264R_OVERLAP=<n> sets the count), chunk k deblocked on the
+ * context's side stream while chunk k + 1 is reconstructed on the launch stream. */
+#define H264R_DBG_OVERLAP 64
 int  h264r_set_debug(h264r_ctx* ctx, int flags);
 /* Wait for the context's work and report a device-side failure (a wavefront wait
  * that timed out): H264R_OK or H264R_EDEVICE. */

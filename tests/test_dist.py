@@ -162,3 +162,60 @@ def test_gloo_band_exchange(world):
         p.join(timeout=60)
         assert p.exitcode == 0
     assert [r[1] for r in res] == [True] * world
+
+
+def _band_worker_c5(rank, world, port, q):
+    """Config 5's real geometry: 2160p = 135 MB rows in 8 slices of
+    17 / 16 rows (synth.c slice_of_row), one band per rank, halo 3 MB rows (|mv_y| <= 32.75 px,
+    dist.halo_mb_rows(131)) -- six interior ranks with two peers each -- in both modes."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        W, H, nk, slack = 2, 135, 2, 64
+        starts = [0, 17, 34, 51, 68, 85, 102, 118]
+        bands = D.slice_bands(starts, H, world)
+        ok = [len(bands) == world]
+        for mode, halo in (("halo", D.halo_mb_rows(131)), ("allgather", 0)):
+            psz = [c * W * H for c in D.ROW_BYTES_PER_MB_COL]
+            rb = [c * W for c in D.ROW_BYTES_PER_MB_COL]
+            planes = [torch.full((nk * psz[pl] + slack,), 0xEE, dtype=torch.uint8) for pl in range(3)]
+            b0, b1 = bands[rank]
+            rowval = [[[((torch.arange(rb[pl], dtype=torch.int64) * 5 + k * 71 + pl * 29 + r * 11) % 251).to(torch.uint8)
+                        for r in range(H)] for pl in range(3)] for k in range(nk)]
+            for pl in range(3):
+                v = planes[pl][: nk * psz[pl]].view(nk, psz[pl])
+                for k in range(nk):
+                    for r in range(b0, b1):
+                        v[k, r * rb[pl]:(r + 1) * rb[pl]] = rowval[k][pl][r]
+            X = D.BandExchange(bands, rank, W, H, nk, mode, halo, "cpu")
+            X.run(planes)
+            lo, hi = (0, H) if mode == "allgather" else (max(b0 - halo, 0), min(b1 + halo, H))
+            for pl in range(3):
+                v = planes[pl][: nk * psz[pl]].view(nk, psz[pl])
+                for k in range(nk):
+                    for r in range(H):
+                        seg = v[k, r * rb[pl]:(r + 1) * rb[pl]]
+                        want = rowval[k][pl][r] if lo <= r < hi else torch.full_like(seg, 0xEE)
+                        ok.append(bool(torch.equal(seg, want)))
+                ok.append(bool((planes[pl][nk * psz[pl]:] == 0xEE).all()))
+            if mode == "halo":
+                need, give = D.halo_plan(bands, rank, halo)
+                ok.append(len(set(need) | set(give)) == (1 if rank in (0, world - 1) else 2))
+        q.put((rank, all(ok), bands[rank]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world8_config5_bands():
+    world, port = 8, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_band_worker_c5, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert [r[1] for r in res] == [True] * world
+    assert [tuple(r[2]) for r in res] == [(0, 17), (17, 34), (34, 51), (51, 68), (68, 85), (85, 102), (102, 118), (118, 135)]

@@ -7,7 +7,7 @@ dependency path: run here with one rank, and rehearsed with two ranks on the one
 exchange moves real rows between processes, and chain 0's second picture (which read its first
 through the exchange) must equal the oracle's chain.  The default is one group of chains per step;
 `--chain-groups 2` overlaps one group's exchange with the next one's decode.  `bench.py --gpus 2` with no launcher starts
-its two ranks itself."""
+its two ranks itself; its default line is the headline workload as replicas with the slice-sharded chain line beside it."""
 import json
 import os
 import subprocess
@@ -49,19 +49,36 @@ def test_gpu_bench_chain_two_ranks_rehearsal():
 
 
 def test_gpu_bench_gpus2_spawns_its_ranks():
-    """`bench.py --gpus 2` with no torchrun: the default N > 1 line (config 5 chain mode,
-    slice-sharded), with the one-GPU line of the same mode beside it."""
-    d = _run([sys.executable, "bench.py", "--gpus", "2", "--chains-per-gpu", "2", "--steps", "2", "--warmup", "1"],
+    """`bench.py --gpus 2` with no torchrun: the default N > 1 line -- the headline workload
+    (config 3) as replicas, with the slice-sharded config-5 chain line beside it (`slice_sharded`,
+    its one-GPU line of the same mode and the CPU baseline of that workload)."""
+    d = _run([sys.executable, "bench.py", "--gpus", "2", "--batch", "8", "--chains-per-gpu", "2", "--steps", "2",
+              "--warmup", "1", "--latency-pictures", "0", "--cpu-seconds", "1"],
              env={"H264R_BENCH_REHEARSE": "1"})
-    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "slices2"
-    assert d["config"]["survey_config"] == 5 and d["config"]["mode"] == "chain" and d["config"]["chains"] == 4
-    assert d["config"]["chain_groups"] == 1 and d["exchange"]["ops_per_step"] == 1
-    assert d["verified_vs_oracle"] is True
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "replicas2" and d["config"]["survey_config"] == 3
+    assert d["config"]["pictures_per_step"] == 16 and d["verified_vs_oracle"] is True
     assert d["distributed"]["ranks"] == 2 and d["distributed"]["backend"] == "gloo"
-    assert d["same_mode_n1"]["verified_vs_oracle"] is True and d["same_mode_n1"]["chains"] == 2
+    s = d["slice_sharded"]
+    assert s["config"]["survey_config"] == 5 and s["config"]["mode"] == "chain" and s["config"]["chains"] == 4
+    assert s["config"]["parallelism"] == "slices2" and s["exchange"]["ops_per_step"] == 1
+    assert s["verified_vs_oracle"] is True and "slice-sharded" in s["metric"]
+    assert s["same_mode_n1"]["verified_vs_oracle"] is True and s["same_mode_n1"]["chains"] == 2
+    assert s["same_mode_n1"]["cpu_baseline"]["kind"] == "port" and s["scaling_vs_same_mode_n1"] > 0
+
+
+def test_gpu_bench_chain_four_ranks_rehearsal():
+    """Config 4's slice-sharded shape at 4 ranks (its 4 slices, one band each; the two interior
+    ranks exchange halo rows with two peers), rehearsed on the box's one GPU (gloo for RCCL)."""
+    d = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "4",
+              "--master-addr", "127.0.0.1", "--master-port", "29519", "bench.py", "--gpus", "4", "--config", "4",
+              "--chain", "8", "--steps", "2", "--warmup", "1", "--no-n1"],
+             env={"H264R_BENCH_REHEARSE": "1"})
+    assert d["verified_vs_oracle"] is True
+    assert d["n_gpus"] == 4 and d["config"]["bands"] == [[0, 17], [17, 34], [34, 51], [51, 68]]
+    assert d["exchange"]["mode"] == "halo" and d["exchange"]["halo_mb_rows"] >= 1
 
 
 def test_gpu_bench_chain_allgather_rehearsal():
-    d = _run([sys.executable, "bench.py", "--gpus", "2", "--config", "4", "--chains-per-gpu", "2", "--exchange",
-              "allgather", "--steps", "2", "--warmup", "1", "--no-n1"], env={"H264R_BENCH_REHEARSE": "1"})
+    d = _run([sys.executable, "bench.py", "--gpus", "2", "--mode", "chain", "--config", "4", "--chains-per-gpu", "2",
+              "--exchange", "allgather", "--steps", "2", "--warmup", "1", "--no-n1"], env={"H264R_BENCH_REHEARSE": "1"})
     assert d["verified_vs_oracle"] is True and d["exchange"]["mode"] == "allgather"

@@ -109,10 +109,11 @@ def _batch_vs_oracle(L, dec, cidx, W, H, n, debug=0, deblocks=DEBLOCKS, qm=None,
                 assert d is None, f"deblock flag {db_flag} picture {i} plane {k}: {d}"
 
 
-def _large_batch_vs_oracle(L, dec, cidx, W, H, n, nbase=8):
+def _large_batch_vs_oracle(L, dec, cidx, W, H, n, nbase=8, debug=A.DBG_DEBLOCK_ROWS, rows=None, **over):
     """n pictures = nbase distinct ones repeated: every output is compared with the oracle's
-    decode of its base picture (a large batch at little oracle cost)."""
-    cfg = synth.default_cfg(L, cidx, W, H)
+    decode of its base picture (a large batch at little oracle cost).  rows: only that MB-row
+    band is decoded (h264r_decode_batch_rows) and compared."""
+    cfg = synth.default_cfg(L, cidx, W, H, **over)
     base = [synth.picture(L, cfg, i) for i in range(nbase)]
     refs = synth.refpics(L, cfg)
     for s, (y, u, v) in enumerate(refs):
@@ -120,16 +121,18 @@ def _large_batch_vs_oracle(L, dec, cidx, W, H, n, nbase=8):
     want = [O.decode(p, refs) for p in base]
     host = B.pack([base[i % nbase] for i in range(n)], h264r.quant_flat())
     db = B.to_device(host, n, None)
-    dec.set_debug(A.DBG_DEBLOCK_ROWS)
+    dec.set_debug(debug)
     try:
-        dec.decode_batch(db.batch)
+        dec.decode_batch(db.batch, rows=rows)
         dec.check()
     finally:
         dec.set_debug(0)
+    r0, r1 = rows if rows else (0, H)
     for i in range(n):
         got = db.planes(i)
         for k in range(3):
-            d = first_diff(got[k], want[i % nbase][k], 16 if k == 0 else 8)
+            m = 16 if k == 0 else 8
+            d = first_diff(got[k][r0 * m:r1 * m], want[i % nbase][k][r0 * m:r1 * m], m)
             assert d is None, f"picture {i} plane {k}: {d}"
 
 
@@ -149,6 +152,77 @@ def test_gpu_large_batch_xcd_groups(L, dec, cidx):
     plain-store records) and the walk's coarse
     band hand-off (batches >= 128 pictures); every picture checked."""
     _large_batch_vs_oracle(L, dec, cidx, 22, 18, 464)
+
+
+@pytest.mark.parametrize("cidx,n,debug", [
+    (3, 1003, A.DBG_DEBLOCK_ROWS),
+    (2, 1003, A.DBG_DEBLOCK_MB),
+    (4, 1003, A.DBG_DEBLOCK_ROWS | A.DBG_DEBLOCK_GLOBAL),
+    (3, 500, 0),
+])
+def test_gpu_overlapped_chunks(L, dec, cidx, n, debug):
+    """The overlapped schedule (h264r_host.hip launch_all, H264R_DBG_OVERLAP): 1003 CIF pictures
+    = 4 chunks of 251/251/251/250 (500 = 2 chunks), the side stream deblocking chunk k while the
+    launch stream reconstructs chunk k + 1, under both deblocking schedules; every picture checked."""
+    _large_batch_vs_oracle(L, dec, cidx, 22, 18, n, debug=debug | A.DBG_OVERLAP)
+
+
+def test_gpu_overlapped_chunks_slice_band(L, dec):
+    """The overlapped schedule over a slice band (h264r_decode_batch_rows, rows 5..14 of CIF
+    pictures with 4 slices and idc 2 as bench.py's slice sharding has them)."""
+    cfg = synth.default_cfg(L, 4, 22, 18, num_slices=4)
+    srow = synth.picture(L, cfg, 0).mbs["slice"].reshape(18, 22)[:, 0]
+    first = [r for r in range(1, 18) if srow[r] != srow[r - 1]]
+    band = (first[0], first[2])
+    _large_batch_vs_oracle(L, dec, 4, 22, 18, 1500, debug=A.DBG_DEBLOCK_ROWS | A.DBG_OVERLAP, rows=band, num_slices=4)
+
+
+@pytest.mark.parametrize("n,nbase", [(6, 6), (1003, 8)])
+def test_gpu_per_picture_dpb_tables(L, dec, n, nbase):
+    """ABI 2 per-picture DPB tables (h264r_batch.ref_planes_stride = 3 x 32 pointers): picture i
+    reads slot 0 from reference set i % 3 (three different pictures) and slot 1 from a shared
+    one, so a kernel that ignored the stride, or a sub-batch of the overlapped schedule that
+    did not advance the table pointer, would predict from the wrong planes.  1003
+    pictures = four chunks of the overlapped schedule; every picture checked."""
+    import torch
+    W, H = 22, 18
+    cfg = synth.default_cfg(L, 3, W, H)
+    base = [synth.picture(L, cfg, i) for i in range(nbase)]
+    refs = synth.refpics(L, cfg)
+    rng = np.random.default_rng(7)
+    alts = [refs[0]] + [tuple(rng.integers(0, 256, a.shape, dtype=np.uint8) for a in refs[0]) for _ in range(2)]
+    slack = 64
+
+    def dev(planes):
+        return [torch.from_numpy(np.concatenate([a.reshape(-1), np.zeros(slack, np.uint8)])).to("cuda") for a in planes]
+    alt_t = [dev(a) for a in alts]
+    shared = dev(refs[1])
+    tab = np.zeros((n, 3 * 32), np.int64)
+    for i in range(n):
+        for k in range(3):
+            tab[i, k] = alt_t[i % 3][k].data_ptr()
+            tab[i, 3 + k] = shared[k].data_ptr()
+    tab_t = torch.from_numpy(tab.reshape(-1)).to("cuda")
+    want = {}
+    for i in range(min(n, 3 * nbase)):
+        key = (i % nbase, i % 3)
+        want[key] = O.decode(base[key[0]], [alts[key[1]], refs[1]])
+    host = B.pack([base[i % nbase] for i in range(n)], h264r.quant_flat())
+    for db_flag in (A.DBG_DEBLOCK_MB, A.DBG_DEBLOCK_ROWS | A.DBG_OVERLAP):
+        db = B.to_device(host, n, tab_t.data_ptr())
+        db.batch.ref_planes_stride = 3 * 32
+        dec.set_debug(db_flag)
+        try:
+            dec.decode_batch(db.batch)
+            dec.check()
+        finally:
+            dec.set_debug(0)
+        for i in range(n):
+            got = db.planes(i)
+            w = want[(i % nbase, i % 3)]
+            for k in range(3):
+                d = first_diff(got[k], w[k], 16 if k == 0 else 8)
+                assert d is None, f"deblock flag {db_flag} picture {i} (ref set {i % 3}) plane {k}: {d}"
 
 
 def test_gpu_stray_env_selectors_are_inert(L, dec, monkeypatch):
