@@ -51,7 +51,7 @@ extern "C" __global__ void k_deblock2(h264r_batch b, const h264r::DbInfo* dbinfo
 constexpr size_t DBINFO_BYTES = 80;
 constexpr size_t HANDOFF_BYTES = 256;   // one tagged record (32 x {dword, epoch}) per MB
 constexpr size_t HANDOFF2_BYTES = 384;  // k_deblock2: 2 row slots x 24 x {dword, tag} per MB column
-constexpr int DEBLOCK2_UNITS = 16;      // k_deblock2: (picture, MB row) units per wave (mb_deblock.h)
+constexpr int DEBLOCK2_UNITS = 64 / H264R_DB2_LPU;   // k_deblock2: (picture, MB row) units per wave (mb_deblock.h)
 constexpr int DEBLOCK2_PICS = DEBLOCK2_UNITS / H264R_DB2_BAND;   // pictures per wave
 
 namespace {
@@ -588,6 +588,13 @@ static int deblock_launch(h264r_ctx* c, const Stage& S, hipStream_t s, int2 rows
         int nx = 1;
         if (hipDeviceGetAttribute(&nx, hipDeviceAttributeNumberOfXccs, c->device) != hipSuccess) nx = 1;
         c->nxcc = std::max(1, std::min(nx, 8));
+    }
+    if (by_rows && knobs().verbose) {
+        static bool once = false;
+        int per_cu = 0;
+        if (!once && hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(k_deblock2), 64, 0) == hipSuccess)
+            fprintf(stderr, "h264r: k_deblock2 occupancy %d waves/CU\n", per_cu);
+        once = true;
     }
     if (by_rows) {
         // k_deblock2 keeps a picture group on one XCD (g % nx): nx counters

@@ -58,7 +58,10 @@ using namespace h264r;
 
 namespace {
 
-constexpr int UNITS = DEBLOCK2_UNITS;  // (picture, MB row) units per wave, 4 lanes each
+constexpr int LPU = H264R_DB2_LPU;     // lanes per (picture, MB row) unit: 4 or 8
+static_assert(LPU == 4 || LPU == 8, "H264R_DB2_LPU");
+constexpr int UNITS = DEBLOCK2_UNITS;  // (picture, MB row) units per wave
+constexpr int NH = LPU / 4;            // lanes per quad index q (8 lanes: the pairs of a dword split in two)
 constexpr int BAND = H264R_DB2_BAND;   // MB rows per wave
 constexpr int PICS = UNITS / BAND;     // pictures per wave
 static_assert(UNITS % BAND == 0, "a band divides the wave's units");
@@ -152,7 +155,12 @@ extern "C" void h264r_db2_trace_copy(void* dst) { (void)hipMemcpyFromSymbol(dst,
 #ifndef H264R_DB2_DIAG
 #define H264R_DB2_DIAG 0   // diagnostic builds only (wrong output): bit 0 drops the output stores, bit 1 fetches MB 0
 #endif
-extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_deblock2(
+// Register budget: the waves a CU holds are set by LDS (UnitLds + StageLds per unit: 6 waves per CU
+// at 8 lanes per unit, 3 at 4); asking for 2 waves per SIMD keeps the compiler from parking values
+// in AGPRs (at a 512-register budget it did, and the wave's VGPR + AGPR footprint of 257 left one
+// wave per SIMD: 4 per CU instead of 6)
+#define H264R_DB2_WAVES_PER_EU (H264R_DB2_LPU == 8 ? 2 : 1)
+extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(H264R_DB2_WAVES_PER_EU, H264R_DB2_WAVES_PER_EU))) void k_deblock2(
     h264r_batch b, const DbInfo* __restrict__ dbinfo, uint64_t* hb, int* sync, int* err, uint32_t epoch, int2 rows, int nx,
     const uint8_t* __restrict__ recon)
 {
@@ -193,7 +201,9 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1
     // the ticket loop and kept live across it
     int lane = threadIdx.x;
     asm volatile("" : "+v"(lane));
-    const int u = lane >> 2, q = lane & 3;
+    // unit u; q = the unit's quarter (luma rows / dword column 4q.., chroma plane q/2, dword q&1);
+    // with 8 lanes per unit, h = which half of q's two row / column pairs this lane filters
+    const int u = lane / LPU, q8 = lane % LPU, q = q8 / NH, h = q8 % NH;
     const int rb = u / PICS, pu = u - rb * PICS;              // row in the band, picture in the group
     const int y = R0 + band * BAND + rb;
     const int pic0 = grp * PICS, npg = min(PICS, b.num_pics - pic0);
@@ -238,26 +248,28 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1
     };
 
     // ---- one MB of the MB-tiled reconstruction (device_common.h), 16 bytes per load:
-    // luma rows 4i + q, chroma chunks 4j + q (plane j, rows 2q and 2q + 1)
+    // luma rows q8 + LPU i, chroma chunks q8 + LPU j (chunk k: plane k / 4, rows 2 (k & 3), +1)
     const uint8_t* rrow = recon + ((size_t)pic * g.nmb + (size_t)yc * W) * RECON_MB;
-    v4u wl[4], wc[2];
+    constexpr int NLR = 16 / LPU, NCK = 8 / LPU;
+    v4u wl[NLR], wc[NCK];
     auto fetch = [&](int m) {
 #if H264R_DB2_DIAG & 2
         m = 0;                           // diagnostic build: every fetch reads MB 0 (L2-resident)
 #endif
         const uint8_t* ma = rrow + (size_t)min(max(m, 0), W - 1) * RECON_MB;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) wl[i] = load_global<v4u>(ma + (4 * i + q) * 16);
+        for (int i = 0; i < NLR; ++i) wl[i] = load_global<v4u>(ma + (LPU * i + q8) * 16);
 #pragma unroll
-        for (int j = 0; j < 2; ++j) wc[j] = load_global<v4u>(ma + RECON_CB + (4 * j + q) * 16);
+        for (int j = 0; j < NCK; ++j) wc[j] = load_global<v4u>(ma + RECON_CB + (LPU * j + q8) * 16);
     };
     auto fill = [&](int s) {                                                            // registers -> ring slot s
 #pragma unroll
-        for (int i = 0; i < 4; ++i) *reinterpret_cast<v4u*>(&U.y[4 * i + q][4 * s]) = wl[i];
+        for (int i = 0; i < NLR; ++i) *reinterpret_cast<v4u*>(&U.y[LPU * i + q8][4 * s]) = wl[i];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            *reinterpret_cast<v2u*>(&U.c[j][2 * q][2 * s]) = wc[j].xy;
-            *reinterpret_cast<v2u*>(&U.c[j][2 * q + 1][2 * s]) = wc[j].zw;
+        for (int j = 0; j < NCK; ++j) {
+            const int k = LPU * j + q8, pl = k >> 2, r = 2 * (k & 3);
+            *reinterpret_cast<v2u*>(&U.c[pl][r][2 * s]) = wc[j].xy;
+            *reinterpret_cast<v2u*>(&U.c[pl][r + 1][2 * s]) = wc[j].zw;
         }
     };
     // Rows 0..12 (chroma 0..6) of a row are final once the next MB's left edge is filtered, rows
@@ -270,13 +282,13 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1
     auto stage_own = [&](int m, int s) {
         const int mc = max(m, 0);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int r = 4 * i + q;
+        for (int i = 0; i < NLR; ++i) {
+            const int r = LPU * i + q8;
             *reinterpret_cast<v4u*>(&T.y[r][mc & 3][0]) = *reinterpret_cast<const v4u*>(&U.y[r][4 * s]);
         }
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int pl = i >> 1, r = 4 * (i & 1) + q;
+        for (int i = 0; i < NLR; ++i) {
+            const int k = LPU * i + q8, pl = k >> 3, r = k & 7;
             *reinterpret_cast<v2u*>(&T.c[pl][r][mc & 7][0]) = *reinterpret_cast<const v2u*>(&U.c[pl][r][2 * s]);
         }
     };
@@ -289,8 +301,8 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1
         const int mo = xs - 1;                                   // final since V(xs), rows 13..15 now
         const bool own = active && mo >= 0 && mo < W;
         const int r = lane >> 2, pp = lane & 3, rc = lane >> 3, mm = lane & 7;
-        for (uint64_t bm = __ballot(own && q == 0 && ((mo & 3) == 3 || mo == W - 1)); bm; bm &= bm - 1) {
-            const int l0 = __builtin_ctzll(bm), u2 = l0 >> 2;
+        for (uint64_t bm = __ballot(own && q8 == 0 && ((mo & 3) == 3 || mo == W - 1)); bm; bm &= bm - 1) {
+            const int l0 = __builtin_ctzll(bm), u2 = l0 / LPU;
             const int m2 = __builtin_amdgcn_readlane(mo, l0), yl2 = __builtin_amdgcn_readlane(ylast, l0);
             const uint32_t yr2 = (uint32_t)__builtin_amdgcn_readlane((int)yrow, l0);
             const int g0 = m2 & ~3;
@@ -298,8 +310,8 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1
             st16<OUT_AUX>(rY, ok ? yr2 + (uint32_t)r * Wl + (uint32_t)(g0 + pp) * 16u : OOB,
                           *reinterpret_cast<const v4u*>(&G[u2].y[r][pp][0]));
         }
-        for (uint64_t bm = __ballot(own && q == 0 && ((mo & 7) == 7 || mo == W - 1)); bm; bm &= bm - 1) {
-            const int l0 = __builtin_ctzll(bm), u2 = l0 >> 2;
+        for (uint64_t bm = __ballot(own && q8 == 0 && ((mo & 7) == 7 || mo == W - 1)); bm; bm &= bm - 1) {
+            const int l0 = __builtin_ctzll(bm), u2 = l0 / LPU;
             const int m2 = __builtin_amdgcn_readlane(mo, l0), cl2 = __builtin_amdgcn_readlane(clast, l0);
             const uint32_t cr2 = (uint32_t)__builtin_amdgcn_readlane((int)crow, l0);
             const int g8 = m2 & ~7;
@@ -310,8 +322,8 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1
         }
         // the band's first row: rows 13..15 (chroma 7) of the row above, final since H(xs)
         const bool up = active && rb == 0 && above && xs >= 0 && xs < W;
-        for (uint64_t bm = __ballot(up && q == 0 && ((xs & 3) == 3 || xs == W - 1)); bm; bm &= bm - 1) {
-            const int l0 = __builtin_ctzll(bm), u2 = l0 >> 2;
+        for (uint64_t bm = __ballot(up && q8 == 0 && ((xs & 3) == 3 || xs == W - 1)); bm; bm &= bm - 1) {
+            const int l0 = __builtin_ctzll(bm), u2 = l0 / LPU;
             const int x2 = __builtin_amdgcn_readlane(xs, l0);
             const uint32_t yr2 = (uint32_t)__builtin_amdgcn_readlane((int)yrow, l0);
             const int g0 = x2 & ~3;
@@ -319,8 +331,8 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1
             st16<OUT_AUX>(rY, ok ? yr2 - (uint32_t)(3 - r) * Wl + (uint32_t)(g0 + pp) * 16u : OOB,
                           *reinterpret_cast<const v4u*>(&G[u2].yu[min(r, 2)][pp][0]));
         }
-        for (uint64_t bm = __ballot(up && q == 0 && ((xs & 7) == 7 || xs == W - 1)); bm; bm &= bm - 1) {
-            const int l0 = __builtin_ctzll(bm), u2 = l0 >> 2;
+        for (uint64_t bm = __ballot(up && q8 == 0 && ((xs & 7) == 7 || xs == W - 1)); bm; bm &= bm - 1) {
+            const int l0 = __builtin_ctzll(bm), u2 = l0 / LPU;
             const int x2 = __builtin_amdgcn_readlane(xs, l0);
             const uint32_t cr2 = (uint32_t)__builtin_amdgcn_readlane((int)crow, l0);
             const int g8 = x2 & ~7;
@@ -346,17 +358,23 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1
     auto early_k = [&](int lq, int j) { return lq < 3 ? lq : j; };
     auto late_c = [&](int lq) { return lq == 0 ? 1 : 3; };
     auto late_k = [&](int lq) { return lq == 0 ? 2 : lq - 1; };
-    // DbInfo of MB m: 5 pieces of 16 bytes, piece q and (every lane) piece 4
-    v4u ninf[2];
+    // DbInfo of MB m: 5 pieces of 16 bytes; 4 lanes: piece q and (every lane) piece 4; 8 lanes:
+    // piece min(q8, 4)
+    constexpr int NINF = LPU == 4 ? 2 : 1;
+    v4u ninf[NINF];
     auto load_info = [&](int m) {
         const v4u* src = info_row + (size_t)min(max(m, 0), W - 1) * 5;
-        ninf[0] = src[q];
-        ninf[1] = src[4];
+        ninf[0] = src[min(q8, 4)];
+        if (NINF == 2) ninf[NINF - 1] = src[4];
     };
     auto put_info = [&](bool ok) {      // zeros (bS 0: no edge filtered) when there is no MB
         const v4u z = {0u, 0u, 0u, 0u};
-        *reinterpret_cast<v4u*>(&U.info[4 * q]) = ok ? ninf[0] : z;
-        *reinterpret_cast<v4u*>(&U.info[16]) = ok ? ninf[1] : z;
+        *reinterpret_cast<v4u*>(&U.info[4 * min(q8, 4)]) = ok ? ninf[0] : z;
+        if (NINF == 2) *reinterpret_cast<v4u*>(&U.info[16]) = ok ? ninf[NINF - 1] : z;
+    };
+    // a value of the lane holding the other half of this lane's pairs (8 lanes per unit)
+    auto partner = [&](uint32_t v) -> uint32_t {
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
     };
 
     TRACE(const unsigned long long tr_start = __builtin_amdgcn_s_memrealtime(); unsigned long long tph[4] = {0, 0, 0, 0};
@@ -401,7 +419,8 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1
 #pragma unroll
             for (int e = 0; e < 4; ++e) ev[e] = edge_params(inf[8 + (e == 0 ? 0 : 2)], bs_pair(inf[e], q, q));
 #pragma unroll
-            for (int i = 0; i < 2; ++i) {
+            for (int ii = 0; ii < 2 / NH; ++ii) {
+                const int i = NH == 2 ? h : ii;
                 const int ra = 4 * q + i, rb2 = ra + 2;
                 uint32_t la = U.y[ra][4 * sl + 3], lb = U.y[rb2][4 * sl + 3];
                 const v4u Av = *reinterpret_cast<const v4u*>(&U.y[ra][4 * sc]);
@@ -432,7 +451,8 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1
             // chroma plane p rows (4d + i, +2); chroma edge 0 = luma edge 0, edge 1 (col 4) =
             // luma edge 2; row j takes the bS of luma row 2j: segment j / 2 (deblock.cc:430-433, 460)
 #pragma unroll
-            for (int i = 0; i < 2; ++i) {
+            for (int ii = 0; ii < 2 / NH; ++ii) {
+                const int i = NH == 2 ? h : ii;
                 const int ra = 4 * d + i, rb2 = ra + 2;
                 EdgeP ec[2];
 #pragma unroll
@@ -488,7 +508,7 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1
         TRACE({ const unsigned long long t2 = __builtin_amdgcn_s_memtime(); tph[1] += t2 - tm; tm = t2; })
         // the late pairs of MB x-1 (luma dword 3, chroma dword 1), final after V(x) (at x = W:
         // after H(W-1)): one per lane
-        publish_pair(active && x >= 1 && x <= W ? rec_out : OOB, max(x - 1, 0), sl, late_c(q), late_k(q));
+        publish_pair(active && x >= 1 && x <= W && h == 0 ? rec_out : OOB, max(x - 1, 0), sl, late_c(q), late_k(q));
         // rows -4..-1 (chroma -2..-1) of MB x's top edge for rows 1.. of the band: the upper unit's
         // left slot (the upper row is on MB x+1), read before that slot is refilled below
         if (rb) {
@@ -521,19 +541,27 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1
             EdgeP eh[4];
 #pragma unroll
             for (int e = 0; e < 4; ++e) eh[e] = edge_params(inf[8 + (e == 0 ? 1 : 2)], bs_pair(inf[4 + e], q, q));
-            s2 c[2][20];
+            s2 c[2 / NH][20];
 #pragma unroll
-            for (int j = 0; j < 2; ++j) {
+            for (int jj = 0; jj < 2 / NH; ++jj) {
+                const int j = NH == 2 ? h : jj;
 #pragma unroll
-                for (int r = 0; r < 20; ++r) c[j][r] = unpack_cols(wy[r], j);
-                filter2<true, false>(c[j][0], c[j][1], c[j][2], c[j][3], c[j][4], c[j][5], c[j][6], c[j][7], eh[0]);
+                for (int r = 0; r < 20; ++r) c[jj][r] = unpack_cols(wy[r], j);
+                filter2<true, false>(c[jj][0], c[jj][1], c[jj][2], c[jj][3], c[jj][4], c[jj][5], c[jj][6], c[jj][7], eh[0]);
 #pragma unroll
                 for (int e = 1; e < 4; ++e)
-                    filter2<false, false>(c[j][4 * e], c[j][4 * e + 1], c[j][4 * e + 2], c[j][4 * e + 3], c[j][4 * e + 4],
-                                          c[j][4 * e + 5], c[j][4 * e + 6], c[j][4 * e + 7], eh[e]);
+                    filter2<false, false>(c[jj][4 * e], c[jj][4 * e + 1], c[jj][4 * e + 2], c[jj][4 * e + 3], c[jj][4 * e + 4],
+                                          c[jj][4 * e + 5], c[jj][4 * e + 6], c[jj][4 * e + 7], eh[e]);
             }
 #pragma unroll
-            for (int r = 1; r < 20; ++r) wy[r] = pack_cols(c[0][r], c[1][r]);
+            for (int r = 1; r < 20; ++r) {
+                if constexpr (NH == 1) {
+                    wy[r] = pack_cols(c[0][r], c[2 / NH - 1][r]);
+                } else {                    // the other pair from the partner lane
+                    const s2 o = as_s2(partner(as_w(c[0][r])));
+                    wy[r] = h ? pack_cols(o, c[0][r]) : pack_cols(c[0][r], o);
+                }
+            }
 #pragma unroll
             for (int r = 0; r < 16; ++r) U.y[r][4 * sc + q] = wy[4 + r];
         }
@@ -547,17 +575,25 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1
             EdgeP eh[2];
 #pragma unroll
             for (int e = 0; e < 2; ++e) eh[e] = edge_params(cpar[e == 0 ? 1 : 2], bs_pair(inf[4 + 2 * e], 2 * d, 2 * d + 1));
-            s2 c[2][10];
+            s2 c[2 / NH][10];
 #pragma unroll
-            for (int j = 0; j < 2; ++j) {
+            for (int jj = 0; jj < 2 / NH; ++jj) {
+                const int j = NH == 2 ? h : jj;
 #pragma unroll
-                for (int r = 0; r < 10; ++r) c[j][r] = unpack_cols(wcv[r], j);
-                s2 d0 = c[j][0], d1 = c[j][9];
-                filter2<true, true>(d0, d0, c[j][0], c[j][1], c[j][2], c[j][3], d1, d1, eh[0]);
-                filter2<false, true>(d0, d0, c[j][4], c[j][5], c[j][6], c[j][7], d1, d1, eh[1]);
+                for (int r = 0; r < 10; ++r) c[jj][r] = unpack_cols(wcv[r], j);
+                s2 d0 = c[jj][0], d1 = c[jj][9];
+                filter2<true, true>(d0, d0, c[jj][0], c[jj][1], c[jj][2], c[jj][3], d1, d1, eh[0]);
+                filter2<false, true>(d0, d0, c[jj][4], c[jj][5], c[jj][6], c[jj][7], d1, d1, eh[1]);
             }
 #pragma unroll
-            for (int r = 1; r < 10; ++r) wcv[r] = pack_cols(c[0][r], c[1][r]);
+            for (int r = 1; r < 10; ++r) {
+                if constexpr (NH == 1) {
+                    wcv[r] = pack_cols(c[0][r], c[2 / NH - 1][r]);
+                } else {
+                    const s2 o = as_s2(partner(as_w(c[0][r])));
+                    wcv[r] = h ? pack_cols(o, c[0][r]) : pack_cols(c[0][r], o);
+                }
+            }
 #pragma unroll
             for (int r = 0; r < 8; ++r) U.c[p][r][2 * sc + d] = wcv[2 + r];
         }
@@ -566,7 +602,10 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1
         // 7. publish / store what is final now: the 16 granules of MB x that MB x+1 cannot
         // change, four per lane; rows 13..15 (chroma 7) of MB (x, y-1)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) publish_pair(xok ? rec_out : OOB, max(x, 0), sc, early_c(q, j), early_k(q, j));
+        for (int jj = 0; jj < 2 / NH; ++jj) {
+            const int j = NH == 2 ? h : jj;
+            publish_pair(xok ? rec_out : OOB, max(x, 0), sc, early_c(q, j), early_k(q, j));
+        }
         // rows 13..15 (chroma 7) of MB (x, y-1), final now: into the staging of the unit above, or
         // (the band's first row) into this unit's own
         if (xok && above) {

@@ -17,3 +17,8 @@
 #ifndef H264R_DB2_BAND
 #define H264R_DB2_BAND 4
 #endif
+
+// k_deblock2: lanes per (picture, MB row) unit (4 or 8); a wave holds 64 / H264R_DB2_LPU units
+#ifndef H264R_DB2_LPU
+#define H264R_DB2_LPU 8
+#endif

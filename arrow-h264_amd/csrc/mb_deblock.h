@@ -11,6 +11,7 @@
 // filter_normal (deblock.cc:327-415), and written back.
 #pragma once
 #include "device_common.h"
+#include "launch_cfg.h"
 
 namespace h264r {
 
@@ -69,7 +70,7 @@ struct DbInfo {
 };
 static_assert(sizeof(DbInfo) == 80, "DbInfo layout");
 constexpr int DBINFO_DWORDS = 20;
-constexpr int DEBLOCK2_UNITS = 16;   // k_deblock2: (picture, MB row) units per wave
+constexpr int DEBLOCK2_UNITS = 64 / H264R_DB2_LPU;   // k_deblock2: (picture, MB row) units per wave
 
 // alpha | beta << 8 | tc0(bS 1..3) << 16 / 21 / 26 for one edge: filter_edge
 // deblock.cc:469-480 (qPav of the two MBs' QPs, indexA/B with MbQ's slice offsets),

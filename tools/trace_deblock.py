@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Diagnostic (GPU box): per-wave timing of the deblocking walk from a trace build,
     make -C arrow-h264_amd OBJ=build_trace LIBDIR=lib_trace EXTRA=-DH264R_TRACE
-    H264R_LIB=arrow-h264_amd/lib_trace/libh264r.so python tools/trace_deblock.py [pictures] [flag]
-(flag 8 = k_deblock2, 4 = k_deblock) [band = the build's H264R_DB2_BAND].  k_deblock2 records
+    H264R_LIB=arrow-h264_amd/lib_trace/libh264r.so python tools/trace_deblock.py [pictures] [flag] [band] [lpu]
+(flag 8 = k_deblock2, 4 = k_deblock) [band = the build's H264R_DB2_BAND, lpu = its H264R_DB2_LPU].  k_deblock2 records
 per ticket (a band of MB rows of a picture group) {start, end} in 100 MHz ticks and the core
 cycles of its four phases summed over the walk."""
 import os
@@ -20,6 +20,7 @@ from h264r import batch as B, synth  # noqa: E402
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 256
 flag = int(sys.argv[2]) if len(sys.argv) > 2 else 8
 band = int(sys.argv[3]) if len(sys.argv) > 3 else 4
+lpu = int(sys.argv[4]) if len(sys.argv) > 4 else 8      # the build's H264R_DB2_LPU (lanes per unit)
 L = h264r.lib()
 W, H = 120, 68
 cfg = synth.default_cfg(L, 3, W, H)
@@ -58,7 +59,8 @@ if flag == 4:
               f"{t[sel, 3].mean() / 100.0:8.1f} us, cycles/step {np.round(t[sel, 4:8].mean(0) / steps, 0)}")
     sys.exit(0)
 t = np.fromfile(out + ".2", np.uint64).reshape(-1, 8).astype(np.int64)
-ng = (n + 16 // band - 1) // (16 // band)
+units = 64 // lpu
+ng = (n + units // band - 1) // (units // band)
 nb = (H + band - 1) // band
 k = ng * nb
 steps = W + band + 2
