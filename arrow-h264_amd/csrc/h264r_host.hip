@@ -253,9 +253,9 @@ struct Knobs {
     int debug = 0;             // H264R_DEBUG: schedule flags of h264r_set_debug OR-ed into every launch
     uint32_t wait_ticks = 0;   // H264R_WAIT_MS: bound of every device-side wait (below)
     int levels = 16;           // H264R_LEVELS: dependency levels from lists (level_launches)
-    int deblock2_min = 192;    // H264R_DEBLOCK2_MIN: batches of this many 68-row pictures' worth of MB rows deblock with k_deblock2
+    int deblock2_min = 8;      // H264R_DEBLOCK2_MIN: batches of this many 68-row pictures' worth of MB rows deblock with k_deblock2
     int lvl_margin = 1;        // H264R_LVL_MARGIN: k_intra_levels' grid, blocks per CU below occupancy
-    bool coop = true;          // H264R_COOP: k_intra_levels by hipLaunchCooperativeKernel
+    bool coop = false;         // H264R_COOP: k_intra_levels by hipLaunchCooperativeKernel (1) or a plain launch
     int walk_gstep = 0;        // H264R_WALK_GSTEP: the walk's band hand-off period (0: by batch size)
     int overlap = 1;           // H264R_OVERLAP: picture chunks of the overlapped schedule (launch_all; 0, 1: off)
     bool verbose = false;      // H264R_VERBOSE
@@ -291,9 +291,15 @@ static const Knobs& knobs()
         n.wait_ticks = (uint32_t)(v * 100000);                     // s_memrealtime, 100 MHz
         // levels beyond 3 hold few MBs each, and a grid barrier apiece: the walk takes them
         v = 3; n.ok &= env_long("H264R_LEVELS", 0, LEVEL_LISTS, &v); n.levels = (int)v;
-        v = 192; n.ok &= env_long("H264R_DEBLOCK2_MIN", 1, 1L << 30, &v); n.deblock2_min = (int)v;
+        // round 5 (8 lanes per unit, staged stores): k_deblock2 wins from 64 1080p pictures of a
+        // throughput batch, 32 2160p chain pictures, up (profiles/r05_x_deblock_min.txt); the lone
+        // picture of the latency chain keeps k_deblock
+        v = 8; n.ok &= env_long("H264R_DEBLOCK2_MIN", 1, 1L << 30, &v); n.deblock2_min = (int)v;
         v = 1; n.ok &= env_long("H264R_LVL_MARGIN", 0, 7, &v); n.lvl_margin = (int)v;
-        v = 1; n.ok &= env_long("H264R_COOP", 0, 1, &v); n.coop = v != 0;
+        // a plain launch by default: the same throughput and latency as the cooperative one
+        // (profiles/r05_w_chain_coop.txt), and the launch rocprofv3 can profile (it crashes at exit
+        // after a cooperative launch), so the profiled sequence is the benchmarked one
+        v = 0; n.ok &= env_long("H264R_COOP", 0, 1, &v); n.coop = v != 0;
         v = 0; n.ok &= env_long("H264R_WALK_GSTEP", 0, 1 << 20, &v); n.walk_gstep = (int)v;
         // measured slower than one stage (profiles/r05_b_overlap_ab.txt): off by default
         v = 1; n.ok &= env_long("H264R_OVERLAP", 0, 16, &v); n.overlap = (int)v;
@@ -533,11 +539,9 @@ static int recon_launches(h264r_ctx* c, const Stage& S, hipStream_t s, int2 rows
             hipLaunchKernelGGL(k_level_scatter, dim3(P), dim3(1024), 0, s, b, (const uint16_t*)lvl, (const int*)lbase,
                                lcursor, X.d_list, rows);
             HIP_OK(hipGetLastError());
-            // a cooperative launch (the runtime checks that the whole grid is resident at
-            // once, or refuses it: the grid barrier's contract, include/h264r.h), the grid
-            // one block per CU below the occupancy answer; H264R_COOP=0 takes a plain launch
-            // (rocprofv3 7.2 crashes at process exit after a cooperative launch: profiling
-            // runs set it; throughput is the same, profiles/r02_intra_levels_launch.txt)
+            // the grid one block per CU below the occupancy answer, all resident at once (the grid
+            // barrier's contract, include/h264r.h); a plain launch by default, H264R_COOP=1 a
+            // cooperative one (the runtime then checks the residency, or refuses the launch)
             // small batches (the latency chain: one picture) take a grid sized to their MBs,
             // 64 per workgroup: most workgroups of the full grid would only attend the grid
             // barriers, whose cost grows with the number of arrivals (MI355X_MICROARCH.md

@@ -621,9 +621,9 @@ def throughput_run(args, rank: int, world: int, local: int, cs, rehearse: bool, 
     # per-kernel split of the same 8(d) bytes (kernel_bytes: R to the reconstructing kernel,
     # W to deblocking; the parts add up to the path's bytes), over each kernel's own event time
     kbytes = [int(k * (band[1] - band[0]) / H) for k in kbytes_all]
-    # the library deblocks launches of >= H264R_DEBLOCK2_MIN (default 192) x 68 picture-MB-rows
+    # the library deblocks launches of >= H264R_DEBLOCK2_MIN (default 8) x 68 picture-MB-rows
     # with k_deblock2, smaller ones with k_deblock (include/h264r.h)
-    dbk = ("k_deblock2" if npics * (band[1] - band[0]) >= int(os.environ.get("H264R_DEBLOCK2_MIN", "192")) * 68
+    dbk = ("k_deblock2" if npics * (band[1] - band[0]) >= int(os.environ.get("H264R_DEBLOCK2_MIN", "8")) * 68
            else "k_deblock")
     inter_k = ["k_dbinfo", "k_inter4r"]
     names = [" + ".join(inter_k), "intra (k_level + k_intra_levels + k_intra_pic)", dbk]

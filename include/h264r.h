@@ -282,12 +282,12 @@ int  h264r_set_timing(h264r_ctx* ctx, int enable);
  * the dependency-level schedule (both are bit-exact; this exercises the walk alone). */
 #define H264R_DBG_INTRA_WALK 2
 /* The loop filter has two schedules (both bit-exact): k_deblock spreads one MB over 32
- * lanes (short latency, small batches), k_deblock2 walks bands of 4 MB rows of 4 pictures
- * per wave (launches of >= H264R_DEBLOCK2_MIN x 68 picture-MB-rows, i.e. 192 whole 1080p
- * pictures by default).  These flags force one of them. */
+ * lanes (short latency, small batches), k_deblock2 walks bands of 4 MB rows of 2 pictures
+ * per wave, 8 lanes per (picture, row) (launches of >= H264R_DEBLOCK2_MIN x 68
+ * picture-MB-rows, i.e. 8 whole 1080p pictures by default).  These flags force one of them. */
 #define H264R_DBG_DEBLOCK_MB   4
 #define H264R_DBG_DEBLOCK_ROWS 8
-/* Both schedules keep a picture's (k_deblock) or a 4-picture group's (k_deblock2) rows on
+/* Both schedules keep a picture's (k_deblock) or a 2-picture group's (k_deblock2) rows on
  * one XCD and hand records over in that XCD's L2; H264R_DBG_DEBLOCK_GLOBAL uses one
  * ticket counter and write-through records instead (any wave on any XCD). */
 #define H264R_DBG_DEBLOCK_GLOBAL 16

@@ -266,10 +266,9 @@ def test_gpu_batch_dense_intra_levels(L, dec):
 
 @pytest.mark.parametrize("n", [33, 70])
 def test_gpu_batch_picture_groups(L, dec, n):
-    """Batches spanning several 4-picture groups of k_deblock2 (the last one ragged; 9 MB rows
-    = bands of 4, 4 and 1 row) under
-    both schedules; flag 0 takes the default for these sizes (k_deblock, below
-    H264R_DEBLOCK2_MIN) -- k_deblock2's default selection is covered by the large batches."""
+    """Batches spanning several picture groups of k_deblock2 (the last one ragged; 9 MB rows =
+    bands of 4, 4 and 1 row) under both schedules; flag 0 takes the default for these sizes
+    (33 x 9 rows: k_deblock, below H264R_DEBLOCK2_MIN x 68; 70 x 9: k_deblock2)."""
     _batch_vs_oracle(L, dec, 3, 11, 9, n, deblocks=(0, A.DBG_DEBLOCK_MB, A.DBG_DEBLOCK_ROWS), pcm_permille=20)
 
 

@@ -27,7 +27,7 @@ if has chain4; then run chain4
 for c in 2 4 5; do if has c$c; then run c$c
   timeout -k 10 400 python bench.py --config $c --no-cpu --latency-pictures 0 > $O/bench_c$c.json 2> $O/bench_c$c.err; tail -c 300 $O/bench_c$c.json; echo; fi; done
 if has prof; then run prof
-  cd /tmp && H264R_COOP=0 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$O/prof -o run -- \
+  cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$O/prof -o run -- \
     python3 $GRAFT_REPO_ROOT/bench.py --steps 5 --warmup 2 --no-cpu --latency-pictures 0 > $GRAFT_REPO_ROOT/$O/prof_bench.json 2> $GRAFT_REPO_ROOT/$O/prof.err
   cd $GRAFT_REPO_ROOT; find $O/prof -name "*kernel_stats.csv" -exec cp {} $O/kernel_stats.csv \; ; head -12 $O/kernel_stats.csv | cut -c1-120; fi
 echo "== done $(date +%T)"

@@ -8,8 +8,7 @@ ROOT=$(cd "$(dirname "$0")/.." && pwd)
 ARGS=${*:-"--batch 64 --steps 3 --warmup 1 --no-cpu --no-verify --latency-pictures 0"}
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-# plain launch of k_intra_levels: rocprofv3 7.2 crashes at exit after a cooperative one
-export H264R_COOP=0
+# (k_intra_levels takes a plain launch by default: rocprofv3 7.2 crashes at exit after a cooperative one)
 timeout -s KILL 120 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/stats" -o run -- python3 "$ROOT/bench.py" $ARGS > "$OUT/stats.log" 2>&1
 i=0
 for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY" \
