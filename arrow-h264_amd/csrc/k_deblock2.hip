@@ -81,22 +81,24 @@ struct alignas(16) UnitLds {
 };
 static_assert(sizeof(UnitLds) == 848, "UnitLds layout");
 
-// A unit's output staging: the final samples of its MB row, collected per group of 4 MBs (luma)
-// and 8 MBs (chroma), so that the output planes take whole 64-byte pieces of their rows (16- and
-// 8-byte row pieces, each of a line the walk completes only 8 steps later, had left L2 partly
-// written: 2.8x the output bytes written, and the stores took 1.8 of the kernel's 5.0 ms;
-// profiles/r05_l_deblock_store_ab.txt).  Rows 13..15 (chroma 7) of a row are final only after the
-// row below has filtered its top edges: the unit below writes them into this unit's staging
-// (same wave), or, for the band's first row, into its own `yu` / `cu` (the row above is
-// another wave's).
+// A unit's output staging: the final samples of its MB row, collected per group of 4 MBs, so
+// that the output planes take whole 64-byte pieces of their luma rows and 32-byte pieces of their
+// chroma rows (16- and 8-byte row pieces, each of a line the walk completes only 8 steps later,
+// had left L2 partly written: 2.8x the output bytes written, and the stores took 1.8 of the
+// kernel's 5.0 ms; profiles/r05_l_deblock_store_ab.txt).  Rows 13..15 (chroma 7) of a row are
+// final only after the row below has filtered its top edges: the unit below writes them into
+// this unit's staging (same wave), or, for the band's first row, into the UpLds of its picture
+// (the row above is another wave's).  1.5 KiB per unit: 8 waves per CU at 8 lanes per unit.
 struct alignas(16) StageLds {
     uint32_t y[16][4][4];      // luma rows 0..15, MB m & 3 of the 4-MB group: 16 bytes
-    uint32_t c[2][8][8][2];    // chroma plane, rows 0..7, MB m & 7 of the 8-MB group: 8 bytes
-    uint32_t yu[3][4][4];      // band's first row: rows 13..15 of the row above
-    uint32_t cu[2][8][2];      // band's first row: chroma row 7 of the row above
-    uint32_t pad[4];           // unit stride 596 dwords (20 banks apart)
+    uint32_t c[2][8][4][2];    // chroma plane, rows 0..7, MB m & 3: 8 bytes
+    uint32_t pad[20];          // unit stride 404 dwords (20 banks apart)
 };
-static_assert(sizeof(StageLds) == 2384, "StageLds layout");
+static_assert(sizeof(StageLds) == 1616, "StageLds layout");
+struct alignas(16) UpLds {     // the band's first row: rows 13..15 (chroma 7) of the row above
+    uint32_t yu[3][4][4];
+    uint32_t cu[2][4][2];
+};
 
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));   // native vectors: registers, not stack
 typedef uint32_t v2u __attribute__((ext_vector_type(2)));
@@ -128,8 +130,8 @@ constexpr int OUT_AUX = H264R_DB2_OUT_AUX;
 
 #ifdef H264R_TRACE
 // Timing trace (trace builds only: make EXTRA=-DH264R_TRACE): per ticket {start, end
-// (s_memrealtime, 100 MHz), then s_memtime cycles spent in: V pass + fill, record wait,
-// H pass, publish + stores}.
+// (s_memrealtime, 100 MHz), then s_memtime cycles spent in: V pass, record wait, output
+// stores + staging + fill, H pass + publishes + next fetch}.
 __device__ unsigned long long h264r_db2_trace[1 << 16][8];
 #define TRACE(...) __VA_ARGS__
 extern "C" void h264r_db2_trace_copy(void* dst) { (void)hipMemcpyFromSymbol(dst, HIP_SYMBOL(h264r_db2_trace), sizeof(h264r_db2_trace)); }
@@ -166,6 +168,7 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(H
 {
     __shared__ UnitLds S[UNITS];
     __shared__ StageLds G[UNITS];
+    __shared__ UpLds UP[PICS];
 #ifdef H264R_DB2_LDS_PAD
     // measurement builds only: LDS padding that lowers the resident waves per CU
     __shared__ uint32_t lds_pad[H264R_DB2_LDS_PAD / 4];
@@ -220,6 +223,7 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(H
     const UnitLds& A = S[rb ? u - PICS : u];                  // the unit of the row above (rb > 0)
     StageLds& T = G[u];
     StageLds& TA = G[rb ? u - PICS : u];                      // its staging
+    UpLds& TU = UP[pu];                                       // (rb == 0) the row above's final rows
     const uint32_t Wl = (uint32_t)g.W, Wc = (uint32_t)g.Wc;
     const uint32_t ysz = (uint32_t)g.ysz, csz = (uint32_t)g.csz;
     // the group's output planes through wave-uniform descriptors; per-lane byte offsets of
@@ -289,56 +293,48 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(H
 #pragma unroll
         for (int i = 0; i < NLR; ++i) {
             const int k = LPU * i + q8, pl = k >> 3, r = k & 7;
-            *reinterpret_cast<v2u*>(&T.c[pl][r][mc & 7][0]) = *reinterpret_cast<const v2u*>(&U.c[pl][r][2 * s]);
+            *reinterpret_cast<v2u*>(&T.c[pl][r][mc & 3][0]) = *reinterpret_cast<const v2u*>(&U.c[pl][r][2 * s]);
         }
     };
     // The groups that are complete at the end of a step, stored by the whole wave: each unit's
-    // flag (its four lanes agree) as a wave-uniform mask, one unit per luma instruction (16 rows
-    // x 4 MBs = 64 lanes), one unit and plane per chroma instruction (8 rows x 8 MBs); a group
-    // cut by the row end stores its MBs only.  Byte offsets per lane, OOB for lanes without a
-    // sample (dropped by the buffer unit).
+    // flag (its lanes agree) as a wave-uniform mask, per unit one luma instruction (16 rows x
+    // 4 MBs = 64 lanes) and one chroma instruction per plane (8 rows x 4 MBs); a group cut by the
+    // row end stores its MBs only.  Byte offsets per lane, OOB for lanes without a sample
+    // (dropped by the buffer unit).
     auto store_groups = [&](int xs) {
         const int mo = xs - 1;                                   // final since V(xs), rows 13..15 now
         const bool own = active && mo >= 0 && mo < W;
-        const int r = lane >> 2, pp = lane & 3, rc = lane >> 3, mm = lane & 7;
+        const int r = lane >> 2, pp = lane & 3, cp = r >> 3, cr = r & 7;
         for (uint64_t bm = __ballot(own && q8 == 0 && ((mo & 3) == 3 || mo == W - 1)); bm; bm &= bm - 1) {
             const int l0 = __builtin_ctzll(bm), u2 = l0 / LPU;
             const int m2 = __builtin_amdgcn_readlane(mo, l0), yl2 = __builtin_amdgcn_readlane(ylast, l0);
+            const int cl2 = __builtin_amdgcn_readlane(clast, l0);
             const uint32_t yr2 = (uint32_t)__builtin_amdgcn_readlane((int)yrow, l0);
-            const int g0 = m2 & ~3;
-            const bool ok = r <= yl2 && g0 + pp <= m2;
-            st16<OUT_AUX>(rY, ok ? yr2 + (uint32_t)r * Wl + (uint32_t)(g0 + pp) * 16u : OOB,
-                          *reinterpret_cast<const v4u*>(&G[u2].y[r][pp][0]));
-        }
-        for (uint64_t bm = __ballot(own && q8 == 0 && ((mo & 7) == 7 || mo == W - 1)); bm; bm &= bm - 1) {
-            const int l0 = __builtin_ctzll(bm), u2 = l0 / LPU;
-            const int m2 = __builtin_amdgcn_readlane(mo, l0), cl2 = __builtin_amdgcn_readlane(clast, l0);
             const uint32_t cr2 = (uint32_t)__builtin_amdgcn_readlane((int)crow, l0);
-            const int g8 = m2 & ~7;
-            const bool ok = rc <= cl2 && g8 + mm <= m2;
-            const uint32_t off = ok ? cr2 + (uint32_t)rc * Wc + (uint32_t)(g8 + mm) * 8u : OOB;
-            st8<OUT_AUX>(rU, off, *reinterpret_cast<const v2u*>(&G[u2].c[0][rc][mm][0]));
-            st8<OUT_AUX>(rV, off, *reinterpret_cast<const v2u*>(&G[u2].c[1][rc][mm][0]));
+            const int g0 = m2 & ~3;
+            const bool inrow = g0 + pp <= m2;
+            st16<OUT_AUX>(rY, r <= yl2 && inrow ? yr2 + (uint32_t)r * Wl + (uint32_t)(g0 + pp) * 16u : OOB,
+                          *reinterpret_cast<const v4u*>(&G[u2].y[r][pp][0]));
+            const uint32_t off = cr <= cl2 && inrow ? cr2 + (uint32_t)cr * Wc + (uint32_t)(g0 + pp) * 8u : OOB;
+            const v2u cv = *reinterpret_cast<const v2u*>(&G[u2].c[cp][cr][pp][0]);
+            st8<OUT_AUX>(rU, cp == 0 ? off : OOB, cv);
+            st8<OUT_AUX>(rV, cp == 1 ? off : OOB, cv);
         }
         // the band's first row: rows 13..15 (chroma 7) of the row above, final since H(xs)
         const bool up = active && rb == 0 && above && xs >= 0 && xs < W;
         for (uint64_t bm = __ballot(up && q8 == 0 && ((xs & 3) == 3 || xs == W - 1)); bm; bm &= bm - 1) {
-            const int l0 = __builtin_ctzll(bm), u2 = l0 / LPU;
+            const int l0 = __builtin_ctzll(bm), pu2 = l0 / LPU;     // rb == 0: unit = picture
             const int x2 = __builtin_amdgcn_readlane(xs, l0);
             const uint32_t yr2 = (uint32_t)__builtin_amdgcn_readlane((int)yrow, l0);
-            const int g0 = x2 & ~3;
-            const bool ok = r < 3 && g0 + pp <= x2;
-            st16<OUT_AUX>(rY, ok ? yr2 - (uint32_t)(3 - r) * Wl + (uint32_t)(g0 + pp) * 16u : OOB,
-                          *reinterpret_cast<const v4u*>(&G[u2].yu[min(r, 2)][pp][0]));
-        }
-        for (uint64_t bm = __ballot(up && q8 == 0 && ((xs & 7) == 7 || xs == W - 1)); bm; bm &= bm - 1) {
-            const int l0 = __builtin_ctzll(bm), u2 = l0 / LPU;
-            const int x2 = __builtin_amdgcn_readlane(xs, l0);
             const uint32_t cr2 = (uint32_t)__builtin_amdgcn_readlane((int)crow, l0);
-            const int g8 = x2 & ~7;
-            const uint32_t off = rc == 0 && g8 + mm <= x2 ? cr2 - Wc + (uint32_t)(g8 + mm) * 8u : OOB;
-            st8<OUT_AUX>(rU, off, *reinterpret_cast<const v2u*>(&G[u2].cu[0][mm][0]));
-            st8<OUT_AUX>(rV, off, *reinterpret_cast<const v2u*>(&G[u2].cu[1][mm][0]));
+            const int g0 = x2 & ~3;
+            const bool inrow = g0 + pp <= x2;
+            st16<OUT_AUX>(rY, r < 3 && inrow ? yr2 - (uint32_t)(3 - r) * Wl + (uint32_t)(g0 + pp) * 16u : OOB,
+                          *reinterpret_cast<const v4u*>(&UP[pu2].yu[min(r, 2)][pp][0]));
+            const uint32_t off = r < 2 && inrow ? cr2 - Wc + (uint32_t)(g0 + pp) * 8u : OOB;
+            const v2u cv = *reinterpret_cast<const v2u*>(&UP[pu2].cu[r & 1][pp][0]);
+            st8<OUT_AUX>(rU, r == 0 ? off : OOB, cv);
+            st8<OUT_AUX>(rV, r == 1 ? off : OOB, cv);
         }
     };
     // granule i of consumer lane c of MB m in slot s: luma row 12+i dword c (i < 4), chroma
@@ -530,6 +526,7 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(H
         wave_sync();                             // every lane has read slot sl
         fill(sl);
         put_info(active && x + 1 >= 0 && x + 1 < W);
+        TRACE({ const unsigned long long t2 = __builtin_amdgcn_s_memtime(); tph[2] += t2 - tm; tm = t2; })
 
         // 6. horizontal edges of MB x (deblock.cc:506-535); rows -4..-1 from the record
         uint32_t wy[20], wcv[10];
@@ -597,7 +594,6 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(H
 #pragma unroll
             for (int r = 0; r < 8; ++r) U.c[p][r][2 * sc + d] = wcv[2 + r];
         }
-        TRACE({ const unsigned long long t2 = __builtin_amdgcn_s_memtime(); tph[2] += t2 - tm; tm = t2; })
 
         // 7. publish / store what is final now: the 16 granules of MB x that MB x+1 cannot
         // change, four per lane; rows 13..15 (chroma 7) of MB (x, y-1)
@@ -609,10 +605,10 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(H
         // rows 13..15 (chroma 7) of MB (x, y-1), final now: into the staging of the unit above, or
         // (the band's first row) into this unit's own
         if (xok && above) {
-            uint32_t* yd = rb ? &TA.y[13][x & 3][q] : &T.yu[0][x & 3][q];
+            uint32_t* yd = rb ? &TA.y[13][x & 3][q] : &TU.yu[0][x & 3][q];
 #pragma unroll
             for (int r = 1; r < 4; ++r) yd[(r - 1) * 16] = wy[r];
-            *(rb ? &TA.c[p][7][x & 7][d] : &T.cu[p][x & 7][d]) = wcv[1];
+            *(rb ? &TA.c[p][7][x & 3][d] : &TU.cu[p][x & 3][d]) = wcv[1];
         }
         // 8. what the next step fills: MB x+2 and its DbInfo
         fetch(x + 2);

@@ -72,7 +72,7 @@ print(f"{n} pictures, {k} waves ({nb} bands of {band} rows x {ng} groups): kerne
       f"start spread {start.min():.0f}..{start.max():.0f} us")
 ph = t[:, 2:6].astype(np.float64)
 tot = ph.sum(1, keepdims=True)
-print("phase share (V + fill, record wait, H, publish/stores):", np.round((ph / tot).mean(0), 3))
+print("phase share (V, record wait, stores + staging + fill, H + publish + fetch):", np.round((ph / tot).mean(0), 3))
 print("cycles per step by phase:", np.round(ph.mean(0) / steps, 0))
 bands = np.arange(k) // ng
 for r in sorted(set((0, 1, 2, nb // 2, nb - 1))):
