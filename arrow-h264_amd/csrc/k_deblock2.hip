@@ -1,40 +1,50 @@
 // k_deblock2.hip -- the in-loop deblocking filter for large batches: bands of MB rows
-// walked in lock step, 4 lanes per (picture, MB row), packed 16-bit filters, LDS rings.
+// walked in lock step, 8 lanes per (picture, MB row), packed 16-bit filters, LDS rings,
+// output staged in LDS and stored as whole 64-byte row pieces.
 //
 // The reference filters MB by MB in raster order, vertical edges then horizontal edges
 // (Deblock::deblock_pic, deblock.cc:537-552): along a row MB x needs MB x-1 finished,
 // and MB (x, y) needs the samples MB (x+1, y-1)'s left edge wrote.  k_deblock
 // (k_deblock.hip) spreads one MB over 32 lanes; its steps are short but latency-bound.
 // Here the parallelism comes from the pictures of the batch: a 64-lane wave owns a BAND
-// of H264R_DB2_BAND consecutive MB rows of 16 / BAND pictures, four lanes per (picture,
-// row) "unit", and walks them in lock step, row rb of the band one MB behind row rb-1
-// (the least lag the reference's order allows: within one step every unit runs its
-// vertical edges before any runs its horizontal edges, so MB x of the upper row has had
-// MB x+1's left edge filtered when the lower row filters its top edge).
+// of H264R_DB2_BAND consecutive MB rows of 64 / (LPU * BAND) pictures, LPU =
+// H264R_DB2_LPU lanes per (picture, row) "unit" (8; 4 is kept for A/B), and walks them
+// in lock step, row rb of the band one MB behind row rb-1 (the least lag the reference's
+// order allows: within one step every unit runs its vertical edges before any runs its
+// horizontal edges, so MB x of the upper row has had MB x+1's left edge filtered when
+// the lower row filters its top edge).
 //
+// A unit's lanes are (q, h), q = 0..3 the quarter of the MB, h = 0..LPU/4-1 the half of it:
 //   vertical edges   lane q filters luma rows 4q .. 4q+3 as the pairs (r, r+2) and
-//                    chroma plane q/2, rows 4(q&1) .. +3 -- filter_vertical deblock.cc:488-504
+//                    chroma plane q/2, rows 4(q&1) .. +3 -- filter_vertical deblock.cc:488-504;
+//                    at 8 lanes lane h takes pair h of the two
 //   horizontal edges lane q filters luma columns 4q .. 4q+3 as the pairs (c, c+2) and
-//                    chroma plane q/2, columns 4(q&1) .. +3 -- filter_horizontal :506-535
+//                    chroma plane q/2, columns 4(q&1) .. +3 -- filter_horizontal :506-535;
+//                    at 8 lanes lane h takes pair h and the partner lane's result comes
+//                    back by one DPP move to rebuild the dword
 //
 // Every operand is an s16x2 of two lines (mb_deblock2.h); the transposition between
 // the two passes is free, since both read the MB from LDS.  Each unit's MB row lives
 // in LDS as two MB slots (MB x in slot x & 1: the left neighbour and the current MB).
 // Between a step's vertical and horizontal edges MB x-1 (final once MB x's left edge is
-// filtered) is stored and MB x+1, fetched into registers during the previous step, takes
-// its slot; the step ends by fetching MB x+2.
-// Two slots instead of three keep a unit at 848 B of LDS: three waves per SIMD instead of
-// two, which is what the walk needs -- at two, a 1080p batch of 1024 pictures takes 2.1
-// rounds of resident waves and its last band ran alone for a third of the kernel
-// (profiles/r04_d_trace_db2.txt).
+// filtered) is copied into the unit's output staging and MB x+1, fetched into registers
+// during the previous step, takes its slot; the step ends by fetching MB x+2.
+//
+// Output staging (StageLds): the final samples are collected per group of 4 MBs, and a
+// completed group is stored as one 64-byte piece per luma row and 32-byte pieces per chroma
+// row.  Storing each MB's 16-byte row pieces as they became final had left the 128-byte
+// lines in L2 partly written for 8 steps, so they were written back piecemeal: 2.8x the
+// output bytes, 1.4-1.8 ms of the kernel (profiles/r05_l_deblock_store_ab.txt).  A unit
+// with two slots, its staging and its share of the band-first row's UpLds takes 20.2 KiB
+// per wave: 8 waves per CU (profiles/r05_aa_deblock_staging_ab.txt).
 //
 // Inside the band the row below reads MB x's bottom rows straight from the upper unit's
 // ring slot (the upper row is on MB x+1 then: MB x is its left neighbour).  Only the
 // band's bottom row hands its bottom rows to the next band (a wave of a later ticket):
 // 24 naturally aligned 8-byte granules {data dword, tag} per MB, laid out so that lane q
 // of the consuming row polls exactly the six it filters with (luma dword q of rows
-// 12..15, chroma plane q/2 dword q&1 of rows 6..7) and the producing lane publishes
-// exactly the six it holds after its horizontal pass.  Luma dword 3 and chroma dword 1
+// 12..15, chroma plane q/2 dword q&1 of rows 6..7) and the producing lanes publish
+// exactly the six they hold after the horizontal pass.  Luma dword 3 and chroma dword 1
 // change again with MB x+1's vertical edges and are published after them.  `sc1`
 // polling loads until every granule carries this launch's tag (MI355X_MICROARCH.md R2
 // granule hand-off).  Waves take tickets band-major, so a wave only waits on tickets
@@ -46,10 +56,11 @@
 // Every memory operation is issued by every lane on every path, so the waitcnt pass can
 // count the operations younger than a load it waits for.
 //
-// Sample ownership (each sample stored once, when final): a row stores MB x's rows
+// Sample ownership (each sample stored once, when final): a row stages MB x's rows
 // 0..12 (chroma 0..6) once MB x+1's vertical edges are done, and the rows 13..15
-// (chroma 7) of MB (x, y-1) after filtering its own top edge.  The launch's last row
-// stores its own bottom rows.
+// (chroma 7) of MB (x, y-1) after filtering its own top edge (into the upper unit's
+// staging inside the band, into UpLds for the band's first row).  The launch's last row
+// stages its own bottom rows.
 #include "launch_cfg.h"
 #include "mb_deblock.h"
 #include "mb_deblock2.h"
@@ -70,10 +81,8 @@ constexpr int AUX_SC1 = 16;            // buffer-op cache policy: sc1 (write-thr
 constexpr int RSRC_W3 = 0x00020000;    // buffer descriptor word 3 (gfx9 raw buffer, range-checked)
 constexpr uint32_t OOB = 0x80000000u;  // added to an offset: past every range (loads 0, stores dropped)
 
-// One unit's MB row in LDS: two MB slots and the DbInfo -- 848 B, so 16 units (13.25 KiB)
-// leave room for three waves per SIMD (12 per CU).  The unit stride of 212 dwords puts the
-// 8 units of a half-wave 20 banks apart (mod 32): the column reads of the horizontal pass
-// are conflict-free.
+// One unit's MB row in LDS: two MB slots and the DbInfo -- 848 B.  The unit stride of 212
+// dwords puts consecutive units 20 banks apart (mod 32).
 struct alignas(16) UnitLds {
     uint32_t y[16][8];        // luma rows 0..15; MB x in slot s = x & 1: dwords 4s .. 4s+3
     uint32_t c[2][8][4];      // chroma plane, rows 0..7; slot s = dwords 2s, 2s+1
@@ -157,10 +166,10 @@ extern "C" void h264r_db2_trace_copy(void* dst) { (void)hipMemcpyFromSymbol(dst,
 #ifndef H264R_DB2_DIAG
 #define H264R_DB2_DIAG 0   // diagnostic builds only (wrong output): bit 0 drops the output stores, bit 1 fetches MB 0
 #endif
-// Register budget: the waves a CU holds are set by LDS (UnitLds + StageLds per unit: 6 waves per CU
-// at 8 lanes per unit, 3 at 4); asking for 2 waves per SIMD keeps the compiler from parking values
-// in AGPRs (at a 512-register budget it did, and the wave's VGPR + AGPR footprint of 257 left one
-// wave per SIMD: 4 per CU instead of 6)
+// Register budget: the waves a CU holds are set by LDS (UnitLds + StageLds per unit + UpLds per
+// picture: 20.2 KiB, 8 waves per CU at 8 lanes per unit); asking for 2 waves per SIMD keeps the
+// compiler from parking values in AGPRs (at a 512-register budget it did, and the wave's VGPR +
+// AGPR footprint of 257 left one wave per SIMD)
 #define H264R_DB2_WAVES_PER_EU (H264R_DB2_LPU == 8 ? 2 : 1)
 extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(H264R_DB2_WAVES_PER_EU, H264R_DB2_WAVES_PER_EU))) void k_deblock2(
     h264r_batch b, const DbInfo* __restrict__ dbinfo, uint64_t* hb, int* sync, int* err, uint32_t epoch, int2 rows, int nx,
