@@ -44,6 +44,7 @@ extern "C" __global__ void k_intra_levels(h264r_batch b, const int* lcount, cons
                                           int lmax, int* lvsync, int* err, uint8_t* recon);
 constexpr int LEVEL_MAX_MBS = 65536;      // k_level's LDS bitmap (k_picture.hip)
 constexpr int LEVEL_LISTS = 64;           // levels with MB lists (H264R_LEVEL_LISTS, k_picture.hip)
+constexpr int LEVEL_IDS = 2 * (LEVEL_LISTS + 1);   // two lists per level (k_picture.hip LEVEL_IDS)
 extern "C" __global__ void k_deblock(h264r_batch b, const h264r::DbInfo* dbinfo, uint64_t* hb,
                                      int* sync, int* err, uint32_t epoch, int2 rows, int nx, uint8_t* recon);
 extern "C" __global__ void k_deblock2(h264r_batch b, const h264r::DbInfo* dbinfo, uint64_t* hb,
@@ -111,7 +112,7 @@ struct Scratch {
     uint32_t epoch2 = 0;            // the same for k_deblock2 (< 2^20: its tags carry the row)
     uint16_t* d_lvl = nullptr; size_t c_lvl = 0;   // intra dependency level per MB
     uint32_t* d_list = nullptr; size_t c_list = 0; // intra MBs by level (pic * nmb + addr)
-    int* d_lcnt = nullptr; size_t c_lcnt = 0;      // [count | base | cursor] x (LEVEL_LISTS + 2)
+    int* d_lcnt = nullptr; size_t c_lcnt = 0;      // [count | base | cursor] x LEVEL_IDS
     uint8_t* d_recon = nullptr; size_t c_recon = 0; // MB-tiled reconstruction, 384 B per (picture, MB)
     void release()
     {
@@ -528,9 +529,9 @@ static int recon_launches(h264r_ctx* c, const Stage& S, hipStream_t s, int2 rows
         if (levels) {
             int* lvsync = sync + 1 + (size_t)P * H + 2;
             int* lcount = X.d_lcnt;
-            int* lbase = lcount + (LEVEL_LISTS + 2);
-            int* lcursor = lbase + (LEVEL_LISTS + 2);
-            HIP_OK(hipMemsetAsync(X.d_lcnt, 0, 3 * (size_t)(LEVEL_LISTS + 2) * sizeof(int), s));
+            int* lbase = lcount + LEVEL_IDS;
+            int* lcursor = lbase + LEVEL_IDS;
+            HIP_OK(hipMemsetAsync(X.d_lcnt, 0, 3 * (size_t)LEVEL_IDS * sizeof(int), s));
             // pictures deeper than 4 x lmax levels (all-intra) are left to the walk whole
             hipLaunchKernelGGL(k_level, dim3(P), dim3(64 * ((HB + 63) / 64)), 0, s, b, lvl, lvsync, lcount, rows, 4 * lmax);
             HIP_OK(hipGetLastError());
@@ -697,7 +698,7 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
     }
     if (levels && ((st = dev_resize(&X.d_lvl, &X.c_lvl, (size_t)P * nmb)) ||
                    (st = dev_resize(&X.d_list, &X.c_list, (size_t)P * nmb)) ||
-                   (st = dev_resize(&X.d_lcnt, &X.c_lcnt, 3 * (size_t)(LEVEL_LISTS + 2)))))
+                   (st = dev_resize(&X.d_lcnt, &X.c_lcnt, 3 * (size_t)LEVEL_IDS))))
         return st;
     HIP_OK(hipMemsetAsync(X.d_sync, 0, sync_n * sizeof(int), s));
     if (nch > 1) {

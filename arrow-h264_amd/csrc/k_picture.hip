@@ -21,6 +21,16 @@
 #endif
 #define H264R_LEVEL_MAX_MBS 65536           // k_level keeps a picture's intra bitmap in LDS
 #define H264R_LEVEL_LISTS 64                // levels 1 .. this many get per-level MB lists
+#ifndef H264R_INTRA_PAIRS
+#define H264R_INTRA_PAIRS 1                 // k_intra_levels reconstructs pairable MBs two per wave (intra_pair_i4)
+#endif
+#ifdef H264R_TRACE_INTRA
+#undef H264R_INTRA_PAIRS
+#define H264R_INTRA_PAIRS 0                 // the trace times one MB per item
+#endif
+// Two lists per level: id 2 L = its pairable MBs (intra_pairable: I_4x4, not lossless), id
+// 2 L + 1 the others, laid out in id order; count / base / cursor arrays of LEVEL_IDS ints.
+constexpr int LEVEL_IDS = 2 * (H264R_LEVEL_LISTS + 1);
 
 using namespace h264r;
 
@@ -241,22 +251,27 @@ extern "C" __global__ __launch_bounds__(1024) void k_level(h264r_batch b, uint16
                                                           int deep_cut)
 {
     __shared__ uint64_t bits[H264R_LEVEL_MAX_MBS / 64];   // intra (not PCM) MBs of the picture
+    __shared__ uint64_t pbits[H264R_LEVEL_MAX_MBS / 64];  // the pairable ones among them
     __shared__ uint16_t ring[1024][4];
-    __shared__ int hist[H264R_LEVEL_LISTS + 1];
-    for (int i = threadIdx.x; i <= H264R_LEVEL_LISTS; i += blockDim.x) hist[i] = 0;
+    __shared__ int hist[LEVEL_IDS];
+    for (int i = threadIdx.x; i < LEVEL_IDS; i += blockDim.x) hist[i] = 0;
     const Geom g = make_geom(b.width_mbs, b.height_mbs);
     const int pic = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
     const h264r_mb* mbs = b.mbs + (size_t)pic * g.nmb;
     const int R0 = rows.x, HB = rows.y - rows.x, mend = rows.y * g.wmb;   // rows above R0 count as level 0
     for (int base = R0 * g.wmb; base < mend; base += blockDim.x) {
         const int m = base + tid;
-        bool in = false;
+        bool in = false, pr = false;
         if (m < mend) {
             const uint32_t w0 = *reinterpret_cast<const uint32_t*>(&mbs[m]);
             in = ((w0 >> 8) & H264R_MBF_INTRA) && (w0 & 255) != H264R_I_PCM;
+            pr = in && (w0 & 255) == H264R_I_4x4 && !((w0 >> 8) & H264R_MBF_BYPASS);   // intra_pairable
         }
-        const uint64_t bl = __ballot(in);
-        if (lane == 0 && m < mend) bits[(base + tid - R0 * g.wmb) >> 6] = bl;
+        const uint64_t bl = __ballot(in), pl = __ballot(pr);
+        if (lane == 0 && m < mend) {
+            bits[(base + tid - R0 * g.wmb) >> 6] = bl;
+            pbits[(base + tid - R0 * g.wmb) >> 6] = pl;
+        }
     }
     __syncthreads();
     const int r = tid;                                      // band row; MB row R0 + r
@@ -281,7 +296,7 @@ extern "C" __global__ __launch_bounds__(1024) void k_level(h264r_batch b, uint16
             deepest = max(deepest, L);
             ring[r][x & 3] = (uint16_t)L;
             out[x] = (uint16_t)L;
-            if (L >= 1 && L <= H264R_LEVEL_LISTS) atomicAdd(&hist[L], 1);
+            if (L >= 1 && L <= H264R_LEVEL_LISTS) atomicAdd(&hist[2 * L + !((pbits[m >> 6] >> (m & 63)) & 1)], 1);
         }
         __syncthreads();
     }
@@ -298,7 +313,7 @@ extern "C" __global__ __launch_bounds__(1024) void k_level(h264r_batch b, uint16
         return;
     }
     if (lane == 0 && deepest) atomicMax(&lvsync[1], deepest);
-    for (int i = threadIdx.x + 1; i <= H264R_LEVEL_LISTS; i += blockDim.x)
+    for (int i = threadIdx.x + 2; i < LEVEL_IDS; i += blockDim.x)
         if (hist[i]) atomicAdd(&lcount[i], hist[i]);
 }
 
@@ -306,17 +321,17 @@ extern "C" __global__ __launch_bounds__(1024) void k_level(h264r_batch b, uint16
 // workgroup, k_level_scan), then every intra MB of level 1 .. H264R_LEVEL_LISTS appends
 // pic * nmb + addr to its level's list (k_level_scatter: a workgroup counts its MBs per
 // level in LDS and reserves each level's range with one global atomic).
-// lcount, lbase, lcursor: H264R_LEVEL_LISTS + 2 ints each.
+// lcount, lbase, lcursor: LEVEL_IDS ints each.
 extern "C" __global__ __launch_bounds__(1024) void k_level_scan(const int* lcount, int* lbase)
 {
     __shared__ int part[1024];
-    constexpr int PER = (H264R_LEVEL_LISTS + 2 + 1023) / 1024;
+    constexpr int PER = (LEVEL_IDS + 1023) / 1024;
     const int t = threadIdx.x;
     int v[PER], sum = 0;
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
         const int i = t * PER + k;
-        v[k] = i <= H264R_LEVEL_LISTS ? lcount[i] : 0;
+        v[k] = i < LEVEL_IDS ? lcount[i] : 0;
         sum += v[k];
     }
     part[t] = sum;
@@ -331,7 +346,7 @@ extern "C" __global__ __launch_bounds__(1024) void k_level_scan(const int* lcoun
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
         const int i = t * PER + k;
-        if (i <= H264R_LEVEL_LISTS + 1) lbase[i] = run;
+        if (i < LEVEL_IDS) lbase[i] = run;
         run += v[k];
     }
 }
@@ -345,26 +360,30 @@ extern "C" __global__ __launch_bounds__(1024) void k_level_scatter(h264r_batch b
                                                                    const int* __restrict__ lbase, int* lcursor,
                                                                    uint32_t* __restrict__ list, int2 rows)
 {
-    __shared__ int cnt[H264R_LEVEL_LISTS + 1];
-    __shared__ int res[H264R_LEVEL_LISTS + 1];
+    __shared__ int cnt[LEVEL_IDS];
+    __shared__ int res[LEVEL_IDS];
     const Geom g = make_geom(b.width_mbs, b.height_mbs);
     const int pic = blockIdx.x, tid = threadIdx.x;
     const int m0 = rows.x * g.wmb, m1 = rows.y * g.wmb;
     const uint16_t* lp = lvl + (size_t)pic * g.nmb;
+    const h264r_mb* mbs = b.mbs + (size_t)pic * g.nmb;
     for (int base = m0; base < m1; base += 1024 * SCATTER_PER) {
-        if (tid <= H264R_LEVEL_LISTS) cnt[tid] = 0;
+        if (tid < LEVEL_IDS) cnt[tid] = 0;
         __syncthreads();
         int L[SCATTER_PER], rank[SCATTER_PER];
 #pragma unroll
         for (int k = 0; k < SCATTER_PER; ++k) {
             const int m = base + k * 1024 + tid;
-            L[k] = m < m1 ? lp[m] : 0;
-            if (L[k] < 1 || L[k] > H264R_LEVEL_LISTS) L[k] = 0;
+            const int lv = m < m1 ? lp[m] : 0;
+            // the list id: 2 L for a pairable MB (intra_pairable; k_level counted the same), else 2 L + 1
+            const uint32_t w0 = lv >= 1 && lv <= H264R_LEVEL_LISTS ? *reinterpret_cast<const uint32_t*>(&mbs[m]) : 0u;
+            const bool pr = (w0 & 255) == H264R_I_4x4 && !((w0 >> 8) & H264R_MBF_BYPASS);
+            L[k] = lv >= 1 && lv <= H264R_LEVEL_LISTS ? 2 * lv + !pr : 0;
         }
 #pragma unroll
         for (int k = 0; k < SCATTER_PER; ++k) rank[k] = L[k] ? atomicAdd(&cnt[L[k]], 1) : 0;
         __syncthreads();
-        if (tid >= 1 && tid <= H264R_LEVEL_LISTS && cnt[tid]) res[tid] = atomicAdd(&lcursor[tid], cnt[tid]);
+        if (tid >= 2 && tid < LEVEL_IDS && cnt[tid]) res[tid] = atomicAdd(&lcursor[tid], cnt[tid]);
         __syncthreads();
 #pragma unroll
         for (int k = 0; k < SCATTER_PER; ++k)
@@ -418,7 +437,7 @@ extern "C" __global__ __launch_bounds__(256, H264R_LVL_WAVES) void k_intra_level
                                                                                 const uint32_t* __restrict__ list,
                                                                                 int lmax, int* lvsync, int* err, uint8_t* recon)
 {
-    __shared__ IntraScratch scratch[4];
+    __shared__ IntraScratch scratch[H264R_INTRA_PAIRS ? 8 : 4];
     __shared__ uint32_t tap4[INTRA_TAPS];
     intra4_tap_fill(tap4, threadIdx.x, blockDim.x);
     __syncthreads();
@@ -428,10 +447,23 @@ extern "C" __global__ __launch_bounds__(256, H264R_LVL_WAVES) void k_intra_level
     const int deepest = __hip_atomic_load(&lvsync[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int top = min(lmax, deepest);
     for (int L = 1; L <= top; ++L) {
-        // the MBs of level L, wave-strided over the list (entry = pic * nmb + addr)
-        const int n = lcount[L], base = lbase[L];
-        for (int e = gw; e < n; e += nw) {
-            const uint32_t k = list[base + e];
+        // the MBs of level L, wave-strided over its items (entry = pic * nmb + addr): the pairs of
+        // its pairable list, then one MB at a time the rest of it and the other list (the two
+        // lists are consecutive)
+        const int n0 = lcount[2 * L], n1 = lcount[2 * L + 1], base = lbase[2 * L];
+        const int np = H264R_INTRA_PAIRS ? n0 / 2 : 0, items = n0 + n1 - np;
+        for (int e = gw; e < items; e += nw) {
+            int ln = lane;                                 // opaque per item (see walk_ticket)
+            asm volatile("" : "+v"(ln));
+            if (e < np) {
+                // k_level and k_level_scatter classify as intra_pairable does: a pair that is not
+                // one is a broken list, flagged as a device error (h264r_check)
+                if (!intra_pair_i4(b, g, list[base + 2 * e], list[base + 2 * e + 1], ln, scratch[wave], scratch[4 + wave],
+                                   tap4, recon))
+                    __hip_atomic_store(err, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                continue;
+            }
+            const uint32_t k = list[base + np + e];
             const int pic = (int)(k / (unsigned)g.nmb), a = (int)(k % (unsigned)g.nmb);
 #ifdef H264R_TRACE_INTRA
             const unsigned long long t0 = __builtin_amdgcn_s_memrealtime(), c0 = __builtin_amdgcn_s_memtime();
@@ -454,8 +486,6 @@ extern "C" __global__ __launch_bounds__(256, H264R_LVL_WAVES) void k_intra_level
                 }
             }
 #else
-            int ln = lane;                                 // opaque per MB (see walk_ticket)
-            asm volatile("" : "+v"(ln));
             intra_mb2(b, g, pic, a % g.wmb, a / g.wmb, ln, scratch[wave], tap4, recon);
 #endif
         }

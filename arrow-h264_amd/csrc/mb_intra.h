@@ -193,13 +193,15 @@ struct IntraLoads {
 // Branch-free: every address is a select, every load is issued, and a lane's "no data"
 // case is applied where the value is used -- a load under a branch, or a select on a
 // loaded value right after it, makes the compiler wait for it there.
+// I4: the MB is known to be I_4x4 (intra_pair_i4): no I_8x8 layout, no I_16x16 DC loads.
+template <bool I4 = false>
 DEV IntraLoads intra_loads(const h264r_mb& m, const int16_t* __restrict__ lv, const h264r_quant* __restrict__ q, int lane)
 {
     IntraLoads L;
     const int qp = m.qp_scaled[0], rem = qp % 6;
     const LevelOffs lo = level_offsets(m);
     const int16_t* dummy = &q->scale4x4[0][0][0][0];
-    const bool i8 = m.mb_type == H264R_I_8x8;
+    const bool i8 = !I4 && m.mb_type == H264R_I_8x8;
     // I_8x8 layout: k = lane >> 4, row, half; 4x4 layout: blk = lane >> 2, row
     const int k8 = lane >> 4, row8 = (lane >> 1) & 7, half8 = lane & 1;
     const int blk = lane >> 2, r4 = lane & 3, bx = blk & 3, by = blk >> 2;
@@ -209,11 +211,16 @@ DEV IntraLoads intra_loads(const h264r_mb& m, const int16_t* __restrict__ lv, co
     const uint2 lv2 = ld8(off >= 0 ? lv + off + within : dummy);
     const uint2 sc2 = ld8(i8 ? &q->scale8x8[0][0][rem][row8 * 8 + half8 * 4] : &q->scale4x4[0][0][rem][r4 * 4]);
     L.lev[0] = lv2.x; L.lev[1] = lv2.y; L.sc[0] = sc2.x; L.sc[1] = sc2.y;
-    const uint4* dcp = reinterpret_cast<const uint4*>(lo.ldc >= 0 ? lv + lo.ldc : dummy);
-    const uint4 d0 = dcp[0], d1 = dcp[1];
-    L.dc[0] = d0.x; L.dc[1] = d0.y; L.dc[2] = d0.z; L.dc[3] = d0.w;
-    L.dc[4] = d1.x; L.dc[5] = d1.y; L.dc[6] = d1.z; L.dc[7] = d1.w;
-    L.dc_scale = q->scale4x4[0][0][rem][0];
+    if (I4) {
+        for (int k = 0; k < 8; ++k) L.dc[k] = 0u;
+        L.dc_scale = 0;
+    } else {
+        const uint4* dcp = reinterpret_cast<const uint4*>(lo.ldc >= 0 ? lv + lo.ldc : dummy);
+        const uint4 d0 = dcp[0], d1 = dcp[1];
+        L.dc[0] = d0.x; L.dc[1] = d0.y; L.dc[2] = d0.z; L.dc[3] = d0.w;
+        L.dc[4] = d1.x; L.dc[5] = d1.y; L.dc[6] = d1.z; L.dc[7] = d1.w;
+        L.dc_scale = q->scale4x4[0][0][rem][0];
+    }
     const int cpl = lane >> 5, cb = (lane >> 3) & 3, chalf = (lane >> 2) & 1, crow = lane & 3;
     const int qpc = (cpl ? m.qp_scaled[2] : m.qp_scaled[1]);
     const uint2 cd = ld8(lo.cdc >= 0 ? lv + lo.cdc + cpl * 4 : dummy);
@@ -258,11 +265,12 @@ DEV void chroma_res2(const h264r_mb& m, const IntraLoads& L, int lane, int (&res
 // Luma residual of an I_4x4 / I_16x16 MB in registers: lane = blk * 4 + row (blk
 // raster over the 4x4 block grid), four samples.  I_16x16 DC: 4x4 Hadamard and
 // scaling of transform_luma_dc (transform.cc:825-856), evaluated per lane.
+template <bool I4 = false>
 DEV void luma_res4_intra(const h264r_mb& m, const IntraLoads& L, int lane, int (&res)[4])
 {
     const int blk = lane >> 2, r = lane & 3, bx = blk & 3, by = blk >> 2;
     const int qp = m.qp_scaled[0], per = qp / 6;
-    const bool i16 = m.mb_type == H264R_I_16x16;
+    const bool i16 = !I4 && m.mb_type == H264R_I_16x16;
     const uint32_t lev0 = L.lev_ok ? L.lev[0] : 0u, lev1 = L.lev_ok ? L.lev[1] : 0u;
     int d[4];
 #pragma unroll
@@ -488,6 +496,120 @@ DEV IntraLoads intra_body_loads(const h264r_batch& b, int pic, const IntraHead& 
     return intra_loads(h.m, b.levels + h.m.coef_off, &b.quant[pic], lane);
 }
 
+// What the I_4x4 steps need of an MB: its neighbours' availability and its 16 modes.
+struct I4Mb {
+    int avA, avB, avC;
+    uint64_t ipw;
+};
+
+// The I_4x4 steps of two MBs at once: MB A on lanes 0..31 (tiles SA), MB B on lanes 32..63
+// (SB), in the slot layout of intra_mb_compute's I_4x4 steps.  The two MBs' modes and availability differ, so a lane
+// derives its block's from its own MB's (per-lane) mode word and availability bits and the
+// step's compile-time block coordinates; whether the step needs the DC sums or the directional
+// taps is one ballot each.
+DEV void intra4_steps_pair(int lane, IntraScratch& SA, IntraScratch& SB, const I4Mb& A, const I4Mb& B, const uint32_t* tap4)
+{
+    const int slot = (lane >> 4) & 1, x = lane & 3, y = (lane >> 2) & 3;
+    const bool mbB = lane >= 32;
+    IntraScratch& S = mbB ? SB : SA;
+    const int soff = y * ITP + x, roff = y * 16 + x, pos = lane & 15;
+    const uint64_t ipw = mbB ? B.ipw : A.ipw;
+    const int avA = mbB ? B.avA : A.avA, avB = mbB ? B.avB : A.avB, avC = mbB ? B.avC : A.avC;
+    // this lane's block of step s: slot 0 = (s & 1) + 2, (s >> 1) - 1; slot 1 = s & 1, s >> 1
+    struct Lb { bool on; int mode, aA, aB, tv, pb, rb; };
+    auto lane_blk = [&](int s) -> Lb {
+        const int by0 = (s >> 1) - 1, bx0 = (s & 1) + 2, by1 = s >> 1, bx1 = s & 1;
+        const bool ok0 = by0 >= 0, ok1 = by1 <= 3;
+        auto bk_of = [](int bx, int by) { return (by >> 1) * 8 + (bx >> 1) * 4 + (by & 1) * 2 + (bx & 1); };   // blkIdx
+        auto tvc = [](int bx, int by) { return (bx * 4 + 4 < 16) && !(bx == 1 && (by == 1 || by == 3)); };  // :154
+        Lb l;
+        l.on = slot ? ok1 : ok0;
+        const int bk = slot ? (ok1 ? bk_of(bx1, by1) : 0) : (ok0 ? bk_of(bx0, by0) : 0);
+        l.mode = l.on ? (int)((ipw >> (4 * bk)) & 15) : 0;
+        const int bx = slot ? bx1 : bx0, by = slot ? by1 : by0;
+        l.aA = bx > 0 ? 1 : avA;
+        l.aB = by > 0 ? 1 : avB;
+        // tv: the block's upper-right neighbours available (row 0: from B / C; below: fixed)
+        const int tv0 = by0 == 0 ? (bx0 < 3 ? avB : avC) : (int)tvc(bx0, by0);
+        const int tv1 = by1 == 0 ? (bx1 < 3 ? avB : avC) : (int)tvc(bx1, by1);
+        l.tv = l.on ? (slot ? tv1 : tv0) : 0;
+        l.pb = slot ? (ok1 ? ti(bx1 * 4, by1 * 4) : ti(4, 4)) : (ok0 ? ti(bx0 * 4, by0 * 4) : ti(4, 4));
+        l.rb = slot ? (ok1 ? by1 * 64 + bx1 * 4 : 0) : (ok0 ? by0 * 64 + bx0 * 4 : 0);
+        return l;
+    };
+    Lb cur = lane_blk(0);
+    uint32_t ent_next = tap4[cur.mode * 32 + cur.tv * 16 + pos];
+    int res_next = (&S.res[0][0])[cur.rb + roff];
+#pragma unroll
+    for (int s = 0; s < 10; ++s) {
+        const Lb l = cur;
+        const uint32_t ent = ent_next;
+        const int rv = res_next;
+        int tp = 0, dc = 0;
+        if (__ballot(l.on && l.mode != 2) != 0) {
+            const int e0 = S.tile[l.pb + (int)(int8_t)ent], e1 = S.tile[l.pb + (int)(int8_t)(ent >> 8)];
+            const int e2 = S.tile[l.pb + (int)(int8_t)(ent >> 16)];
+            tp = tap_apply((int)(ent >> 24), e0, e1, e2);
+        }
+        if (__ballot(l.on && l.mode == 2) != 0) {                 // DC (:214-229)
+            const int st = sum4(lds_u32(&S.tile[l.pb - ITP]));
+            const int sl = S.tile[l.pb - 1] + S.tile[l.pb + ITP - 1] + S.tile[l.pb + 2 * ITP - 1] + S.tile[l.pb + 3 * ITP - 1];
+            const int mA = -l.aA, mB = -l.aB, dsh = 1 + l.aA + l.aB;
+            dc = (((sl & mA) + (st & mB) + (1 << (dsh - 1))) >> dsh) + (128 & ~(mA | mB));
+        }
+        const int p = l.mode == 2 ? dc : tp;
+        const int v = clip255(p + rv);                            // residual: 0 in uncoded blocks
+        if (l.on) S.tile[l.pb + soff] = (uint8_t)v;
+        if (s < 9) {
+            cur = lane_blk(s + 1);
+            ent_next = tap4[cur.mode * 32 + cur.tv * 16 + pos];
+            res_next = (&S.res[0][0])[cur.rb + roff];
+        }
+        wave_sync();
+    }
+}
+
+// IntraPrediction::Chroma (intra_prediction.cc:748-894) + construction_chroma of one MB, in the
+// chroma residual layout (lane = plane << 5 | blk << 3 | half << 2 | row, two samples).
+DEV void intra_chroma(const h264r_mb& m, int avA, int avB, int lane, const IntraScratch& S, const int (&resC)[2], uint8_t* rmb)
+{
+    const int pl = lane >> 5, cb = (lane >> 3) & 3, chalf = (lane >> 2) & 1, crow = lane & 3;
+    const int y = (cb >> 1) * 4 + crow, x0 = (cb & 1) * 4 + chalf * 2;
+    const uint8_t* C = S.ctile[pl];
+    const int mode = m.chroma_mode;
+    int p[2];
+    if (mode == 0) {
+        // per 4x4 block: both sums read, the available ones selected (no lane-divergent branch)
+        const int xO = x0 & 4, yO = y & 4;
+        const bool diag = (xO == 0) == (yO == 0);                  // blocks (0,0) and (4,4)
+        const int aA = diag || xO == 0 ? avA : (avB ? 0 : avA);
+        const int aB = diag || xO > 0 ? avB : (avA ? 0 : avB);
+        const int sl = C[ci(-1, yO)] + C[ci(-1, yO + 1)] + C[ci(-1, yO + 2)] + C[ci(-1, yO + 3)];
+        const int st = sum4(lds_u32(&C[ci(xO, -1)]));
+        const int sum = (aA ? sl : 0) + (aB ? st : 0) + (aA ? 2 : 0) + (aB ? 2 : 0);
+        const int v = aA || aB ? sum >> (1 + aA + aB) : 128;
+        p[0] = p[1] = v;
+    } else if (mode == 1) {
+        p[0] = p[1] = C[ci(-1, y)];
+    } else if (mode == 2) {
+        p[0] = C[ci(x0, -1)];
+        p[1] = C[ci(x0 + 1, -1)];
+    } else {
+        int Hs = 0, Vs = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            Hs += (k + 1) * (C[ci(4 + k, -1)] - C[ci(2 - k, -1)]);
+            Vs += (k + 1) * (C[ci(-1, 4 + k)] - C[ci(-1, 2 - k)]);
+        }
+        const int pa = 16 * (C[ci(-1, 7)] + C[ci(7, -1)]);
+        const int pb = (34 * Hs + 32) >> 6, pc = (34 * Vs + 32) >> 6;
+#pragma unroll
+        for (int c = 0; c < 2; ++c) p[c] = clip255((pa + pb * (x0 + c - 3) + pc * (y - 3) + 16) >> 5);
+    }
+    const uint32_t w = (uint32_t)clip255(p[0] + resC[0]) | ((uint32_t)clip255(p[1] + resC[1]) << 8);
+    *reinterpret_cast<uint16_t*>(rmb + RECON_CB + pl * 64 + y * 8 + x0) = (uint16_t)w;
+}
+
 // Intra MB (mbx, mby) of picture `pic` from its loads (no-op for inter / I_PCM MBs); one
 // wave.  tph (trace builds): s_memtime at the phase boundaries [record known, residual,
 // tiles, prediction, end].
@@ -705,47 +827,68 @@ DEV void intra_mb_compute(const h264r_batch& b, const Geom& g, int pic, int mbx,
         *reinterpret_cast<uint32_t*>(rmb + y * 16 + x0) = lds_u32(&S.tile[ti(x0, y)]);
     }
 
-    // ---- chroma: IntraPrediction::Chroma (intra_prediction.cc:748-894) + construction_chroma,
-    // in the chroma residual layout
-    {
-        const int pl = lane >> 5, cb = (lane >> 3) & 3, chalf = (lane >> 2) & 1, crow = lane & 3;
-        const int y = (cb >> 1) * 4 + crow, x0 = (cb & 1) * 4 + chalf * 2;
-        const uint8_t* C = S.ctile[pl];
-        const int mode = m.chroma_mode;
-        int p[2];
-        if (mode == 0) {
-            // per 4x4 block: both sums read, the available ones selected (no lane-divergent branch)
-            const int xO = x0 & 4, yO = y & 4;
-            const bool diag = (xO == 0) == (yO == 0);                  // blocks (0,0) and (4,4)
-            const int aA = diag || xO == 0 ? avA : (avB ? 0 : avA);
-            const int aB = diag || xO > 0 ? avB : (avA ? 0 : avB);
-            const int sl = C[ci(-1, yO)] + C[ci(-1, yO + 1)] + C[ci(-1, yO + 2)] + C[ci(-1, yO + 3)];
-            const int st = sum4(lds_u32(&C[ci(xO, -1)]));
-            const int sum = (aA ? sl : 0) + (aB ? st : 0) + (aA ? 2 : 0) + (aB ? 2 : 0);
-            const int v = aA || aB ? sum >> (1 + aA + aB) : 128;
-            p[0] = p[1] = v;
-        } else if (mode == 1) {
-            p[0] = p[1] = C[ci(-1, y)];
-        } else if (mode == 2) {
-            p[0] = C[ci(x0, -1)];
-            p[1] = C[ci(x0 + 1, -1)];
-        } else {
-            int Hs = 0, Vs = 0;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                Hs += (k + 1) * (C[ci(4 + k, -1)] - C[ci(2 - k, -1)]);
-                Vs += (k + 1) * (C[ci(-1, 4 + k)] - C[ci(-1, 2 - k)]);
-            }
-            const int pa = 16 * (C[ci(-1, 7)] + C[ci(7, -1)]);
-            const int pb = (34 * Hs + 32) >> 6, pc = (34 * Vs + 32) >> 6;
-#pragma unroll
-            for (int c = 0; c < 2; ++c) p[c] = clip255((pa + pb * (x0 + c - 3) + pc * (y - 3) + 16) >> 5);
-        }
-        const uint32_t w = (uint32_t)clip255(p[0] + resC[0]) | ((uint32_t)clip255(p[1] + resC[1]) << 8);
-        *reinterpret_cast<uint16_t*>(rmb + RECON_CB + pl * 64 + y * 8 + x0) = (uint16_t)w;
-    }
+    // ---- chroma: IntraPrediction::Chroma (intra_prediction.cc:748-894) + construction_chroma
+    intra_chroma(m, avA, avB, lane, S, resC, rmb);
     INTRA_STAMP(4);
 #undef INTRA_STAMP
+}
+
+// The class of MB the level lists pair (k_level): I_4x4, not lossless.
+DEV bool intra_pairable(const h264r_mb& m)
+{
+    return mb_is_intra(m) && m.mb_type == H264R_I_4x4 && !(m.flags & H264R_MBF_BYPASS);
+}
+
+// Two I_4x4 MBs (intra_pairable) of one dependency level in one wave -- independent, since an
+// intra neighbour would put one a level below the other.  The loads of both come first; the
+// residual, the neighbour tiles, the luma stores and the chroma run per MB in the single-MB
+// layouts, and the ten I_4x4 steps -- four fifths of an I_4x4 MB's time in one wave
+// (profiles/r05_ad_intra_trace.txt), with half the wave idle -- once for both: MB A on lanes
+// 0..31, MB B on lanes 32..63 (intra4_steps_pair).  k = pic * nmb + MB address.  Returns
+// false, having stored nothing, when either MB is not pairable.
+DEV bool intra_pair_i4(const h264r_batch& b, const Geom& g, uint32_t kA, uint32_t kB, int lane, IntraScratch& SA,
+                       IntraScratch& SB, const uint32_t* tap4, uint8_t* recon)
+{
+    const int picA = (int)(kA / (unsigned)g.nmb), aA = (int)(kA % (unsigned)g.nmb);
+    const int picB = (int)(kB / (unsigned)g.nmb), aB = (int)(kB % (unsigned)g.nmb);
+    const int xA = aA % g.wmb, yA = aA / g.wmb, xB = aB % g.wmb, yB = aB / g.wmb;
+    const IntraHead hA = intra_head(b, g, picA, xA, yA, lane, recon, tap4);
+    const IntraHead hB = intra_head(b, g, picB, xB, yB, lane, recon, tap4);
+    if (!intra_pairable(hA.m) || !intra_pairable(hB.m)) return false;
+    const IntraLoads lA = intra_loads<true>(hA.m, b.levels + hA.m.coef_off, &b.quant[picA], lane);
+    const IntraLoads lB = intra_loads<true>(hB.m, b.levels + hB.m.coef_off, &b.quant[picB], lane);
+    // per MB: availability (one ballot), residual (luma into S.res, chroma in registers),
+    // neighbour samples into the tile
+    auto pre = [&](const IntraHead& hd, const IntraLoads& ld, IntraScratch& S, int (&resC)[2]) -> I4Mb {
+        const h264r_mb& m = hd.m;
+        const bool av = lane < 4 && hd.nin && (int)(hd.nw2 >> 16) == (int)m.slice &&
+                        !(hd.cip && !((hd.nw0 >> 8) & H264R_MBF_INTRA));
+        const uint32_t avm = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)__ballot(av));
+        int resL[4];
+        luma_res4_intra<true>(m, ld, lane, resL);
+        chroma_res2(m, ld, lane, resC);
+        *reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(&S) + ((tap4[INTRA_NBR + lane] >> 14) & 4095)) = hd.nb;
+        const int blk = lane >> 2, r = lane & 3;
+        *reinterpret_cast<int4*>(&S.res[(blk >> 2) * 4 + r][(blk & 3) * 4]) = make_int4(resL[0], resL[1], resL[2], resL[3]);
+        const uint64_t ipw = (uint64_t)reinterpret_cast<const uint32_t*>(&m)[5] |
+                             ((uint64_t)reinterpret_cast<const uint32_t*>(&m)[6] << 32);
+        return I4Mb{(int)(avm & 1), (int)((avm >> 1) & 1), (int)((avm >> 2) & 1), ipw};
+    };
+    int resCA[2], resCB[2];
+    const I4Mb pA = pre(hA, lA, SA, resCA);
+    const I4Mb pB = pre(hB, lB, SB, resCB);
+    wave_sync();
+    intra4_steps_pair(lane, SA, SB, pA, pB, tap4);
+    uint8_t* const rA = recon_mb(recon, g, picA, aA);
+    uint8_t* const rB = recon_mb(recon, g, picB, aB);
+    {
+        const int y = lane >> 2, x0 = (lane & 3) * 4;
+        *reinterpret_cast<uint32_t*>(rA + y * 16 + x0) = lds_u32(&SA.tile[ti(x0, y)]);
+        *reinterpret_cast<uint32_t*>(rB + y * 16 + x0) = lds_u32(&SB.tile[ti(x0, y)]);
+    }
+    intra_chroma(hA.m, pA.avA, pA.avB, lane, SA, resCA, rA);
+    intra_chroma(hB.m, pB.avA, pB.avB, lane, SB, resCB, rB);
+    return true;
 }
 
 // Loads then reconstruction of one intra MB (the walk, k_intra_pic).
