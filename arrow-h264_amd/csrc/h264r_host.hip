@@ -30,8 +30,9 @@
 
 namespace h264r { struct DbInfo; }
 extern "C" __global__ void k_inter4r(h264r_batch b, h264r::DbInfo* dbinfo, int2 rows, int* sp_flag, uint8_t* recon,
-                                     const int* inter_cnt);
-extern "C" __global__ void k_dbinfo(h264r_batch b, h264r::DbInfo* dbinfo, int2 rows, int* inter_cnt);
+                                     const int* inter_cnt, int tag);
+extern "C" __global__ void k_dbinfo(h264r_batch b, h264r::DbInfo* dbinfo, int2 rows, int* inter_cnt, int tag, int* zero,
+                                    int nz, int* zero2, int nz2);
 extern "C" __global__ void k_inter_sp(h264r_batch b, int2 rows, const int* sp_flag, uint8_t* recon);
 extern "C" __global__ void k_untile(h264r_batch b, int2 rows, const uint8_t* recon);
 extern "C" __global__ void k_intra_pic(h264r_batch b, int* sync, int* err, const uint16_t* lvl, int lmax, int2 rows,
@@ -43,6 +44,7 @@ extern "C" __global__ void k_level_scatter(h264r_batch b, const uint16_t* lvl, c
 extern "C" __global__ void k_intra_levels(h264r_batch b, const int* lcount, const int* lbase, const uint32_t* list,
                                           int lmax, int* lvsync, int* err, uint8_t* recon);
 constexpr int LEVEL_MAX_MBS = 65536;      // k_level's LDS bitmap (k_picture.hip)
+constexpr int LEVEL_LDS = 40960;          // k_level's LDS level bytes: (W + 2) x (rows + 1) (k_picture.hip)
 constexpr int LEVEL_LISTS = 64;           // levels with MB lists (H264R_LEVEL_LISTS, k_picture.hip)
 constexpr int LEVEL_IDS = 2 * (LEVEL_LISTS + 1);   // two lists per level (k_picture.hip LEVEL_IDS)
 extern "C" __global__ void k_deblock(h264r_batch b, const h264r::DbInfo* dbinfo, uint64_t* hb,
@@ -106,6 +108,7 @@ int dev_resize(T** p, size_t* cap, size_t n)
 struct Scratch {
     uint8_t* d_dbinfo = nullptr; size_t c_dbinfo = 0;
     int* d_sync = nullptr; size_t c_sync = 0;
+    int tag = 0;                    // launch-sequence tag of k_dbinfo's per-picture inter flags (> 0)
     uint8_t* d_hb = nullptr; size_t c_hb = 0;
     uint32_t epoch = 0;             // tag of the deblocking hand-off records of the last launch
     uint8_t* d_hb2 = nullptr; size_t c_hb2 = 0;
@@ -514,9 +517,12 @@ static int recon_launches(h264r_ctx* c, const Stage& S, hipStream_t s, int2 rows
         // the deblocking records first (k_inter4r then fits 4 waves/SIMD), with per picture
         // a flag that an inter or I_PCM MB was met (profiles/r03_f_dbinfo_ab.txt, r03_h_inter_ab.txt)
         int* inter_cnt = sync + 1 + (size_t)P * H + 14;
-        hipLaunchKernelGGL(k_dbinfo, dgrid, dim3(256), 0, s, b, S.dbinfo, rows, inter_cnt);
+        // k_dbinfo zeroes the stage's sync words before the flags and the level counters
+        if (++X.tag <= 0) X.tag = 1;
+        hipLaunchKernelGGL(k_dbinfo, dgrid, dim3(256), 0, s, b, S.dbinfo, rows, inter_cnt, X.tag, sync, (int)(1 + (size_t)P * H + 14),
+                           levels ? X.d_lcnt : nullptr, levels ? 3 * LEVEL_IDS : 0);
         HIP_OK(hipGetLastError());
-        hipLaunchKernelGGL(k_inter4r, igrid, dim3(256), 0, s, b, S.dbinfo, rows, sp_flag, recon, (const int*)inter_cnt);
+        hipLaunchKernelGGL(k_inter4r, igrid, dim3(256), 0, s, b, S.dbinfo, rows, sp_flag, recon, (const int*)inter_cnt, X.tag);
         HIP_OK(hipGetLastError());
         // inter MBs of SP slices (a short launch when the batch has none)
         hipLaunchKernelGGL(k_inter_sp, dim3(1024), dim3(256), 0, s, b, rows, (const int*)sp_flag, recon);
@@ -531,9 +537,8 @@ static int recon_launches(h264r_ctx* c, const Stage& S, hipStream_t s, int2 rows
             int* lcount = X.d_lcnt;
             int* lbase = lcount + LEVEL_IDS;
             int* lcursor = lbase + LEVEL_IDS;
-            HIP_OK(hipMemsetAsync(X.d_lcnt, 0, 3 * (size_t)LEVEL_IDS * sizeof(int), s));
             // pictures deeper than 4 x lmax levels (all-intra) are left to the walk whole
-            hipLaunchKernelGGL(k_level, dim3(P), dim3(64 * ((HB + 63) / 64)), 0, s, b, lvl, lvsync, lcount, rows, 4 * lmax);
+            hipLaunchKernelGGL(k_level, dim3(P), dim3(1024), 0, s, b, lvl, lvsync, lcount, rows, 4 * lmax);
             HIP_OK(hipGetLastError());
             hipLaunchKernelGGL(k_level_scan, dim3(1), dim3(1024), 0, s, (const int*)lcount, lbase);
             HIP_OK(hipGetLastError());
@@ -679,11 +684,17 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
         }
     }
     const size_t sync_n = (size_t)nch * sync_ints(chunk_min + 1, H);
-    if ((st = dev_resize(&X.d_sync, &X.c_sync, sync_n))) return st;
+    {
+        // each stage's k_dbinfo zeroes its sync words; fresh memory is zeroed once, so no stale
+        // inter flag can carry a live tag
+        const size_t cap_before = X.c_sync;
+        if ((st = dev_resize(&X.d_sync, &X.c_sync, sync_n))) return st;
+        if (X.c_sync != cap_before) HIP_OK(hipMemsetAsync(X.d_sync, 0, X.c_sync * sizeof(int), s));
+    }
     // H264R_DBG_WAIT_TEST: every intra-walk wait asks for progress no row reaches, under a
     // 10 ms bound -- the launch must drain and h264r_check report H264R_EDEVICE
     if ((st = set_wait_bound(c, wait_test ? 1000000u : wait_bound_ticks(), s))) return st;
-    const bool levels = nmb <= LEVEL_MAX_MBS && H <= 1024 && level_launches() > 0 &&
+    const bool levels = nmb <= LEVEL_MAX_MBS && (size_t)(W + 2) * (HB + 1) <= (size_t)LEVEL_LDS && level_launches() > 0 &&
                         !(c->debug & (H264R_DBG_INTRA_WALK | H264R_DBG_WAIT_TEST));
     if (levels && !c->levels_grid) {
         // every workgroup of the persistent level kernel must be resident at once: one
@@ -700,7 +711,6 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
                    (st = dev_resize(&X.d_list, &X.c_list, (size_t)P * nmb)) ||
                    (st = dev_resize(&X.d_lcnt, &X.c_lcnt, 3 * (size_t)LEVEL_IDS))))
         return st;
-    HIP_OK(hipMemsetAsync(X.d_sync, 0, sync_n * sizeof(int), s));
     if (nch > 1) {
         if (!c->side) HIP_OK(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
         if (!c->ev_side) HIP_OK(hipEventCreateWithFlags(&c->ev_side, hipEventDisableTiming));

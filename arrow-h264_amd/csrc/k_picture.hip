@@ -242,78 +242,113 @@ extern "C" __global__ __launch_bounds__(64 * H264R_WALK_ROWS, H264R_WALK_WAVES) 
 // wavefront walk (k_intra_pic).  Slice boundaries are ignored here: that can only
 // raise a level, never break an order.
 //
-// k_level: one workgroup per picture, thread r = MB row r, which walks its row in
-// lock step: at step t thread r does MB x = t - 2r, after (x+1, r-1) was done at
-// step t-1.  Each row keeps its last four levels in an LDS ring.
-// lcount[L] (L = 1 .. H264R_LEVEL_LISTS): intra MBs of level L over the batch (zeroed per
-// batch); k_level_lists turns them into one MB list per level.
+// k_level: one 1024-thread workgroup per picture, the levels relaxed in LDS.  Its threads load
+// the picture's intra and pairable bits, then iterate L(m) = intra(m) ? 1 + max(L(A), L(B),
+// L(C), L(D)) : 0 over all MBs in place (levels as bytes, a zero border around the rows), from
+// L = 1 on every intra MB, until a pass changes nothing.  The values only grow and never pass
+// the true level (a chaotic relaxation of a monotone map on a DAG, so in-place races are
+// harmless): after k passes every MB of level <= k + 1 is exact, so a picture converges in
+// (deepest level) + 1 passes -- about 8 in the P / B pictures of the benchmark -- and a picture
+// still changing after deep_cut + 1 passes is deeper than deep_cut (all-intra) and goes to the
+// walk whole.  It replaced a walk of the rows in lock step (one thread per row, one workgroup
+// barrier per MB step, x + 2y steps): 88 us per 1080p picture in the latency chain, 148 us per
+// 1024-picture batch (profiles/r05_ac_latency_kernels.txt, r04_ak_kernel_stats_b1024.csv).
+// lcount[id] (id 2 L + c, L = 1 .. H264R_LEVEL_LISTS, c = 0 pairable): intra MBs of level L over
+// the batch (zeroed per batch); k_level_scatter turns them into the lists.
+constexpr int LEVEL_LDS = 40960;            // (W + 2) x (rows + 1) level bytes (h264r_host.hip checks)
 extern "C" __global__ __launch_bounds__(1024) void k_level(h264r_batch b, uint16_t* lvl, int* lvsync, int* lcount, int2 rows,
                                                           int deep_cut)
 {
     __shared__ uint64_t bits[H264R_LEVEL_MAX_MBS / 64];   // intra (not PCM) MBs of the picture
     __shared__ uint64_t pbits[H264R_LEVEL_MAX_MBS / 64];  // the pairable ones among them
-    __shared__ uint16_t ring[1024][4];
+    __shared__ uint8_t lv[LEVEL_LDS];                     // level of band row r, MB x at (r + 1) * (W + 2) + x + 1
     __shared__ int hist[LEVEL_IDS];
-    for (int i = threadIdx.x; i < LEVEL_IDS; i += blockDim.x) hist[i] = 0;
+    __shared__ int pdeep;
     const Geom g = make_geom(b.width_mbs, b.height_mbs);
-    const int pic = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+    const int pic = blockIdx.x, tid = threadIdx.x, lane = tid & 63, nt = (int)blockDim.x;
     const h264r_mb* mbs = b.mbs + (size_t)pic * g.nmb;
-    const int R0 = rows.x, HB = rows.y - rows.x, mend = rows.y * g.wmb;   // rows above R0 count as level 0
-    for (int base = R0 * g.wmb; base < mend; base += blockDim.x) {
-        const int m = base + tid;
-        bool in = false, pr = false;
-        if (m < mend) {
-            const uint32_t w0 = *reinterpret_cast<const uint32_t*>(&mbs[m]);
-            in = ((w0 >> 8) & H264R_MBF_INTRA) && (w0 & 255) != H264R_I_PCM;
-            pr = in && (w0 & 255) == H264R_I_4x4 && !((w0 >> 8) & H264R_MBF_BYPASS);   // intra_pairable
+    const int R0 = rows.x, HB = rows.y - rows.x, W = g.wmb, P = W + 2, n = HB * W;   // rows above R0 count as level 0
+    for (int i = tid; i < LEVEL_IDS; i += nt) hist[i] = 0;
+    for (int i = tid; i < P * (HB + 1); i += nt) lv[i] = 0;
+    if (tid == 0) pdeep = 0;
+    constexpr int UNR = 4;                                 // record loads in flight per thread
+    for (int base = 0; base < n; base += UNR * nt) {
+        uint32_t w0[UNR];
+#pragma unroll
+        for (int k = 0; k < UNR; ++k) {
+            const int m = base + k * nt + tid;
+            w0[k] = m < n ? *reinterpret_cast<const uint32_t*>(&mbs[R0 * W + m]) : 0u;
         }
-        const uint64_t bl = __ballot(in), pl = __ballot(pr);
-        if (lane == 0 && m < mend) {
-            bits[(base + tid - R0 * g.wmb) >> 6] = bl;
-            pbits[(base + tid - R0 * g.wmb) >> 6] = pl;
+#pragma unroll
+        for (int k = 0; k < UNR; ++k) {
+            const int m = base + k * nt + tid;
+            const bool in = ((w0[k] >> 8) & H264R_MBF_INTRA) && (w0[k] & 255) != H264R_I_PCM;
+            const bool pr = in && (w0[k] & 255) == H264R_I_4x4 && !((w0[k] >> 8) & H264R_MBF_BYPASS);   // intra_pairable
+            const uint64_t bl = __ballot(in), pl = __ballot(pr);
+            if (lane == 0 && m < n) {
+                bits[m >> 6] = bl;
+                pbits[m >> 6] = pl;
+            }
         }
     }
     __syncthreads();
-    const int r = tid;                                      // band row; MB row R0 + r
-    uint16_t* out = lvl + (size_t)pic * g.nmb + (size_t)(R0 + r) * g.wmb;
-    int left = 0, deepest = 0;
-    const int steps = g.wmb + 2 * (HB - 1);
-    for (int t = 0; t < steps; ++t) {
-        const int x = t - 2 * r;
-        if (r < HB && x >= 0 && x < g.wmb) {
-            const int m = r * g.wmb + x;            // band-relative MB index
-            int L = 0;
-            if ((bits[m >> 6] >> (m & 63)) & 1) {
-                int up = 0;
-                if (r > 0) {
-                    up = ring[r - 1][x & 3];
-                    if (x > 0) up = max(up, (int)ring[r - 1][(x - 1) & 3]);
-                    if (x + 1 < g.wmb) up = max(up, (int)ring[r - 1][(x + 1) & 3]);
-                }
-                L = 1 + max(up, left);
+    // this thread's MBs m = tid + k nt as LDS byte indices, stepped without a division per MB
+    const int dr = nt / W, dx = nt % W, r0 = tid / W, x0 = tid % W;
+    auto lds_index = [&](int& r, int& x) {
+        const int i = (r + 1) * P + x + 1;
+        x += dx; r += dr;
+        if (x >= W) { x -= W; ++r; }
+        return i;
+    };
+    // L = 1 on every intra MB, then passes until nothing changes (or the picture proves deep)
+    {
+        int r = r0, x = x0;
+        for (int m = tid; m < n; m += nt) {
+            const int i = lds_index(r, x);
+            if ((bits[m >> 6] >> (m & 63)) & 1) lv[i] = 1;
+        }
+    }
+    const int cut = min(deep_cut, 250);                    // bytes: levels up to 251 are kept exact
+    bool deep = true;
+    for (int pass = 0; pass <= cut + 1; ++pass) {
+        __syncthreads();
+        int changed = 0;
+        int r = r0, x = x0;
+        for (int m = tid; m < n; m += nt) {
+            const int i = lds_index(r, x);
+            if (!((bits[m >> 6] >> (m & 63)) & 1)) continue;
+            const int v = 1 + max(max((int)lv[i - P - 1], (int)lv[i - P]), max((int)lv[i - P + 1], (int)lv[i - 1]));
+            if (v != lv[i]) {
+                lv[i] = (uint8_t)min(v, 255);
+                changed = 1;
             }
-            left = L;
+        }
+        if (!__syncthreads_or(changed)) { deep = false; break; }
+    }
+    // the levels out (uint16), the per-list counts, the deepest level
+    int deepest = 0;
+    if (!deep) {
+        uint16_t* out = lvl + (size_t)pic * g.nmb + (size_t)R0 * W;
+        int r = r0, x = x0;
+        for (int m = tid; m < n; m += nt) {
+            const int L = lv[lds_index(r, x)];
+            out[m] = (uint16_t)L;
             deepest = max(deepest, L);
-            ring[r][x & 3] = (uint16_t)L;
-            out[x] = (uint16_t)L;
             if (L >= 1 && L <= H264R_LEVEL_LISTS) atomicAdd(&hist[2 * L + !((pbits[m >> 6] >> (m & 63)) & 1)], 1);
         }
-        __syncthreads();
+        for (int d = 32; d >= 1; d >>= 1) deepest = max(deepest, __shfl_xor(deepest, d));
+        if (lane == 0 && deepest) atomicMax(&pdeep, deepest);
     }
-    for (int d = 32; d >= 1; d >>= 1) deepest = max(deepest, __shfl_xor(deepest, d));
+    __syncthreads();
+    deepest = pdeep;
     // a picture deeper than deep_cut (all-intra: level x + 2y + 1) goes to the walk whole:
     // its few MBs per level would only make k_intra_levels wait at its grid barriers
-    __shared__ int pdeep;
-    if (tid == 0) pdeep = 0;
-    __syncthreads();
-    if (lane == 0 && deepest) atomicMax(&pdeep, deepest);
-    __syncthreads();
-    if (pdeep > deep_cut) {
-        for (int m = R0 * g.wmb + tid; m < mend; m += blockDim.x) lvl[(size_t)pic * g.nmb + m] = 0xFFFF;
+    if (deep || deepest > deep_cut) {
+        for (int m = R0 * W + tid; m < rows.y * W; m += nt) lvl[(size_t)pic * g.nmb + m] = 0xFFFF;
         return;
     }
-    if (lane == 0 && deepest) atomicMax(&lvsync[1], deepest);
-    for (int i = threadIdx.x + 2; i < LEVEL_IDS; i += blockDim.x)
+    if (tid == 0 && deepest) atomicMax(&lvsync[1], deepest);
+    for (int i = tid + 2; i < LEVEL_IDS; i += nt)
         if (hist[i]) atomicAdd(&lcount[i], hist[i]);
 }
 

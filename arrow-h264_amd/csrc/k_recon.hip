@@ -68,7 +68,8 @@ DEV bool inter4_groups(const Geom& g, int2 rows, int per, int& grp, int& gend)
 // blockIdx.x % 8 (one eighth of the MB rows) of every picture: an XCD's motion
 // compensation reads only its band of the reference pictures (+ the MV reach), which its
 // 4 MB L2 holds, instead of every XCD streaming whole references through its L2.
-DEV void inter4_kernel(const h264r_batch& b, int2 rows, int* sp_flag, uint8_t* recon, Inter4Lds& S, const int* inter_cnt)
+DEV void inter4_kernel(const h264r_batch& b, int2 rows, int* sp_flag, uint8_t* recon, Inter4Lds& S, const int* inter_cnt,
+                       int tag)
 {
     const int pic = blockIdx.y;
     const Geom g = make_geom(b.width_mbs, b.height_mbs);
@@ -80,7 +81,7 @@ DEV void inter4_kernel(const h264r_batch& b, int2 rows, int* sp_flag, uint8_t* r
     Inter4Pre pre = inter4_pre(b, g, pic, a0, aend, lane);
     // a picture k_dbinfo found no inter or I_PCM MB in (all-intra) has nothing for this kernel;
     // the flag is loaded with the records, so it adds no round trip
-    const int has_inter = inter_cnt ? inter_cnt[pic] : 1;
+    const int has_inter = inter_cnt ? inter_cnt[pic] == tag : 1;
     const LdsRegs lr = inter4_lds_load(b, pic);
     if (__builtin_amdgcn_readfirstlane(has_inter) == 0) return;
     inter4_lds_store(b, lr, S);
@@ -102,18 +103,29 @@ DEV void inter4_kernel(const h264r_batch& b, int2 rows, int* sp_flag, uint8_t* r
 
 extern "C" __global__ __launch_bounds__(256, H264R_INTER_WAVES) void k_inter4r(h264r_batch b, DbInfo* dbinfo, int2 rows,
                                                                               int* sp_flag, uint8_t* recon,
-                                                                              const int* inter_cnt)
+                                                                              const int* inter_cnt, int tag)
 {
     (void)dbinfo;
     __shared__ Inter4Lds S;
-    inter4_kernel(b, rows, sp_flag, recon, S, inter_cnt);
+    inter4_kernel(b, rows, sp_flag, recon, S, inter_cnt, tag);
 }
 
 // k_dbinfo: the deblocking records DbInfo of every MB (dbinfo_block, mb_inter4.h) on their
 // own -- they depend on the MB records and motion only, not on any sample; launched before
 // k_inter4r.  Same grid and lane roles as k_inter4r.
-extern "C" __global__ __launch_bounds__(256, 8) void k_dbinfo(h264r_batch b, DbInfo* dbinfo, int2 rows, int* inter_cnt)
+// k_dbinfo also zeroes the launch sequence's sync words and level counters (zero[0 .. nz),
+// zero2[0 .. nz2)) for the kernels after it -- two memset launches less per batch (the latency
+// chain paid ~20 us for them, profiles/r05_ac_latency_kernels.txt) -- and marks a picture with
+// an inter or I_PCM MB by storing this launch's tag (nonzero), so the flags need no zeroing.
+extern "C" __global__ __launch_bounds__(256, 8) void k_dbinfo(h264r_batch b, DbInfo* dbinfo, int2 rows, int* inter_cnt, int tag,
+                                                             int* zero, int nz, int* zero2, int nz2)
 {
+    {
+        const int nt = (int)(gridDim.x * gridDim.y * blockDim.x);
+        const int t = (int)((blockIdx.y * gridDim.x + blockIdx.x) * blockDim.x + threadIdx.x);
+        for (int i = t; i < nz; i += nt) zero[i] = 0;
+        for (int i = t; i < nz2; i += nt) zero2[i] = 0;
+    }
     __shared__ Inter4Lds S;
     const int pic = blockIdx.y;
     const Geom g = make_geom(b.width_mbs, b.height_mbs);
@@ -148,7 +160,7 @@ extern "C" __global__ __launch_bounds__(256, 8) void k_dbinfo(h264r_batch b, DbI
         pre = inter4_pre(b, g, pic, a0, aend, lane);
         nb = dbinfo_pre(b, g, pic, a0, aend, lane);
     }
-    if (inter_cnt && inter && lane == 0) inter_cnt[pic] = 1;         // every writer stores 1
+    if (inter_cnt && inter && lane == 0) inter_cnt[pic] = tag;       // every writer stores the tag
 }
 
 // k_inter_sp: the inter MBs of SP slices (inverse_transform_sp), after k_inter4.  A
