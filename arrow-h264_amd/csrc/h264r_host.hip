@@ -51,6 +51,8 @@ extern "C" __global__ void k_deblock(h264r_batch b, const h264r::DbInfo* dbinfo,
                                      int* sync, int* err, uint32_t epoch, int2 rows, int nx, uint8_t* recon);
 extern "C" __global__ void k_deblock2(h264r_batch b, const h264r::DbInfo* dbinfo, uint64_t* hb,
                                       int* sync, int* err, uint32_t epoch, int2 rows, int nx, const uint8_t* recon);
+extern "C" __global__ void k_deblock2l(h264r_batch b, const h264r::DbInfo* dbinfo, uint64_t* hb,
+                                      int* sync, int* err, uint32_t epoch, int2 rows, int nx, const uint8_t* recon);
 constexpr size_t DBINFO_BYTES = 80;
 constexpr size_t HANDOFF_BYTES = 256;   // one tagged record (32 x {dword, epoch}) per MB
 constexpr size_t HANDOFF2_BYTES = 384;  // k_deblock2: 2 row slots x 24 x {dword, tag} per MB column
@@ -258,6 +260,7 @@ struct Knobs {
     uint32_t wait_ticks = 0;   // H264R_WAIT_MS: bound of every device-side wait (below)
     int levels = 16;           // H264R_LEVELS: dependency levels from lists (level_launches)
     int deblock2_min = 8;      // H264R_DEBLOCK2_MIN: batches of this many 68-row pictures' worth of MB rows deblock with k_deblock2
+    int deblock2l_max = 0;     // H264R_DB2L_MAX: batches of fewer 68-row pictures' worth of MB rows take k_deblock2l
     int lvl_margin = 1;        // H264R_LVL_MARGIN: k_intra_levels' grid, blocks per CU below occupancy
     bool coop = false;         // H264R_COOP: k_intra_levels by hipLaunchCooperativeKernel (1) or a plain launch
     int walk_gstep = 0;        // H264R_WALK_GSTEP: the walk's band hand-off period (0: by batch size)
@@ -279,7 +282,7 @@ static bool env_long(const char* name, long lo, long hi, long* out)
     return true;
 }
 constexpr int SCHEDULE_FLAGS = H264R_DBG_INTRA_WALK | H264R_DBG_DEBLOCK_MB | H264R_DBG_DEBLOCK_ROWS | H264R_DBG_DEBLOCK_GLOBAL |
-                               H264R_DBG_OVERLAP;
+                               H264R_DBG_OVERLAP | H264R_DBG_DEBLOCK_LANES16;
 static const Knobs& knobs()
 {
     static const Knobs k = [] {
@@ -299,6 +302,7 @@ static const Knobs& knobs()
         // throughput batch, 32 2160p chain pictures, up (profiles/r05_x_deblock_min.txt); the lone
         // picture of the latency chain keeps k_deblock
         v = 8; n.ok &= env_long("H264R_DEBLOCK2_MIN", 1, 1L << 30, &v); n.deblock2_min = (int)v;
+        v = 0; n.ok &= env_long("H264R_DB2L_MAX", 0, 1L << 30, &v); n.deblock2l_max = (int)v;
         v = 1; n.ok &= env_long("H264R_LVL_MARGIN", 0, 7, &v); n.lvl_margin = (int)v;
         // a plain launch by default: the same throughput and latency as the cooperative one
         // (profiles/r05_w_chain_coop.txt), and the launch rocprofv3 can profile (it crashes at exit
@@ -580,9 +584,9 @@ static int recon_launches(h264r_ctx* c, const Stage& S, hipStream_t s, int2 rows
     return H264R_OK;
 }
 
-// The deblocking of a stage on stream s (k_deblock2 when by_rows, else k_deblock), or the
+// The deblocking of a stage on stream s (sched 1 k_deblock2, 2 k_deblock2l, 0 k_deblock), or the
 // untiled copy of its reconstruction (H264R_DBG_NO_DEBLOCK).
-static int deblock_launch(h264r_ctx* c, const Stage& S, hipStream_t s, int2 rows, uint8_t* hb, uint32_t epoch, bool by_rows)
+static int deblock_launch(h264r_ctx* c, const Stage& S, hipStream_t s, int2 rows, uint8_t* hb, uint32_t epoch, int sched)
 {
     const h264r_batch& b = S.b;
     const int W = b.width_mbs, H = b.height_mbs, P = b.num_pics, HB = rows.y - rows.x;
@@ -599,20 +603,22 @@ static int deblock_launch(h264r_ctx* c, const Stage& S, hipStream_t s, int2 rows
         if (hipDeviceGetAttribute(&nx, hipDeviceAttributeNumberOfXccs, c->device) != hipSuccess) nx = 1;
         c->nxcc = std::max(1, std::min(nx, 8));
     }
-    if (by_rows && knobs().verbose) {
+    if (sched == 1 && knobs().verbose) {
         static bool once = false;
         int per_cu = 0;
         if (!once && hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(k_deblock2), 64, 0) == hipSuccess)
             fprintf(stderr, "h264r: k_deblock2 occupancy %d waves/CU\n", per_cu);
         once = true;
     }
-    if (by_rows) {
-        // k_deblock2 keeps a picture group on one XCD (g % nx): nx counters
-        int grid = ((P + DEBLOCK2_PICS - 1) / DEBLOCK2_PICS) * ((HB + H264R_DB2_BAND - 1) / H264R_DB2_BAND);
+    if (sched) {
+        // k_deblock2 keeps a picture group on one XCD (g % nx): nx counters; k_deblock2l (16 lanes
+        // per unit: one picture per wave) the same with one-picture groups
+        const int pics = sched == 2 ? 1 : DEBLOCK2_PICS;
+        int grid = ((P + pics - 1) / pics) * ((HB + H264R_DB2_BAND - 1) / H264R_DB2_BAND);
         const int nx = grid >= 64 * c->nxcc && !(c->debug & H264R_DBG_DEBLOCK_GLOBAL) ? c->nxcc : 1;
         grid = (grid + nx - 1) / nx * nx;
-        hipLaunchKernelGGL(k_deblock2, dim3(grid), dim3(64), 0, s, b, S.dbinfo, reinterpret_cast<uint64_t*>(hb), dsync,
-                           c->d_err, epoch, rows, nx, (const uint8_t*)S.recon);
+        hipLaunchKernelGGL(sched == 2 ? k_deblock2l : k_deblock2, dim3(grid), dim3(64), 0, s, b, S.dbinfo,
+                           reinterpret_cast<uint64_t*>(hb), dsync, c->d_err, epoch, rows, nx, (const uint8_t*)S.recon);
     } else {
         // k_deblock keeps a picture's pairs on one XCD (p % nx): nx times the largest
         // XCD share of waves, so every XCD runs all its pairs at once
@@ -666,8 +672,15 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
     // crossover measured on whole 1080p pictures (68 MB rows), so a launch qualifies by its
     // picture-rows (a 2160p picture counts twice, a 17-row slice band a quarter); the chunks of
     // the overlapped schedule all take the schedule of the smallest
-    const bool by_rows = (c->debug & H264R_DBG_DEBLOCK_ROWS) ||
-                         (!(c->debug & H264R_DBG_DEBLOCK_MB) && (int64_t)chunk_min * HB >= (int64_t)K.deblock2_min * 68);
+    // k_deblock2l (16 lanes per unit, one picture per wave: the shortest steps) below
+    // H264R_DB2L_MAX pictures' worth of rows
+    const int64_t prows = (int64_t)chunk_min * HB;
+    const int sched = (c->debug & H264R_DBG_DEBLOCK_LANES16) ? 2
+                    : (c->debug & H264R_DBG_DEBLOCK_ROWS)    ? 1
+                    : (c->debug & H264R_DBG_DEBLOCK_MB)      ? 0
+                    : prows < (int64_t)K.deblock2l_max * 68  ? 2
+                    : prows >= (int64_t)K.deblock2_min * 68  ? 1 : 0;
+    const bool by_rows = sched != 0;                 // k_deblock2's hand-off records (both widths)
     // hand-off records of the chosen deblocking kernel, a region per picture; fresh memory or a
     // wrapping epoch restarts from zeroed records, so no record may carry a live tag
     uint8_t** hb = by_rows ? &X.d_hb2 : &X.d_hb;
@@ -734,7 +747,7 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
             HIP_OK(hipStreamWaitEvent(c->side, c->ev_chunk[k], 0));
             ds = c->side;
         }
-        if ((st = deblock_launch(c, S, ds, rows, *hb + (size_t)p0 * hb_pic, ++*ep, by_rows))) return st;
+        if ((st = deblock_launch(c, S, ds, rows, *hb + (size_t)p0 * hb_pic, ++*ep, sched))) return st;
         p0 += n;
     }
     if (nch > 1) {
@@ -759,7 +772,8 @@ static int run_batch(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row0
 #ifdef H264R_TRACE
 void h264r_db_trace_copy(void* dst);    // k_deblock.hip / k_deblock2.hip (trace builds)
 void h264r_db2_trace_copy(void* dst);
-// H264R_TRACE_OUT=<path>: k_deblock's trace to <path>, k_deblock2's to <path>.2
+void h264r_db2l_trace_copy(void* dst);
+// H264R_TRACE_OUT=<path>: k_deblock's trace to <path>, k_deblock2's to <path>.2, k_deblock2l's to <path>.2l
 static void dump_trace(hipStream_t s)
 {
     const char* path = getenv("H264R_TRACE_OUT");
@@ -770,6 +784,8 @@ static void dump_trace(hipStream_t s)
     if (FILE* f = fopen(path, "wb")) { fwrite(buf.data(), 8, buf.size(), f); fclose(f); }
     h264r_db2_trace_copy(buf.data());
     if (FILE* f = fopen((std::string(path) + ".2").c_str(), "wb")) { fwrite(buf.data(), 8, buf.size(), f); fclose(f); }
+    h264r_db2l_trace_copy(buf.data());
+    if (FILE* f = fopen((std::string(path) + ".2l").c_str(), "wb")) { fwrite(buf.data(), 8, buf.size(), f); fclose(f); }
 }
 #endif
 

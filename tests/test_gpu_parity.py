@@ -79,8 +79,8 @@ def test_gpu_matches_reference_fixture(L, dec, fx):
         pytest.fail("; ".join(msgs) or "md5 mismatch")
 
 
-# both deblocking schedules (include/h264r.h): one MB per 32 lanes / a lane pair per MB row
-DEBLOCKS = (A.DBG_DEBLOCK_MB, A.DBG_DEBLOCK_ROWS, A.DBG_DEBLOCK_MB | A.DBG_DEBLOCK_GLOBAL)
+# the deblocking schedules (include/h264r.h): one MB per 32 lanes, the band walk at 8 and at 16 lanes per MB row
+DEBLOCKS = (A.DBG_DEBLOCK_MB, A.DBG_DEBLOCK_ROWS, A.DBG_DEBLOCK_MB | A.DBG_DEBLOCK_GLOBAL, A.DBG_DEBLOCK_LANES16)
 
 
 def _batch_vs_oracle(L, dec, cidx, W, H, n, debug=0, deblocks=DEBLOCKS, qm=None, **over):

@@ -2,7 +2,7 @@
 """Diagnostic (GPU box): per-wave timing of the deblocking walk from a trace build,
     make -C arrow-h264_amd OBJ=build_trace LIBDIR=lib_trace EXTRA=-DH264R_TRACE
     H264R_LIB=arrow-h264_amd/lib_trace/libh264r.so python tools/trace_deblock.py [pictures] [flag] [band] [lpu]
-(flag 8 = k_deblock2, 4 = k_deblock) [band = the build's H264R_DB2_BAND, lpu = its H264R_DB2_LPU].  k_deblock2 records
+(flag 8 = k_deblock2, 4 = k_deblock, 128 = k_deblock2l with lpu 16) [band = the build's H264R_DB2_BAND, lpu = its H264R_DB2_LPU].  k_deblock2 records
 per ticket (a band of MB rows of a picture group) {start, end} in 100 MHz ticks and the core
 cycles of its four phases summed over the walk."""
 import os
@@ -58,7 +58,7 @@ if flag == 4:
         print(f"pair {p:3d}: start {start[sel].mean():8.1f} us end {end[sel].mean():8.1f} us, poll "
               f"{t[sel, 3].mean() / 100.0:8.1f} us, cycles/step {np.round(t[sel, 4:8].mean(0) / steps, 0)}")
     sys.exit(0)
-t = np.fromfile(out + ".2", np.uint64).reshape(-1, 8).astype(np.int64)
+t = np.fromfile(out + (".2l" if lpu == 16 else ".2"), np.uint64).reshape(-1, 8).astype(np.int64)   # lpu 16: k_deblock2l
 units = 64 // lpu
 ng = (n + units // band - 1) // (units // band)
 nb = (H + band - 1) // band
