@@ -32,7 +32,7 @@ namespace h264r { struct DbInfo; }
 extern "C" __global__ void k_inter4r(h264r_batch b, h264r::DbInfo* dbinfo, int2 rows, int* sp_flag, uint8_t* recon,
                                      const int* inter_cnt, int tag);
 extern "C" __global__ void k_dbinfo(h264r_batch b, h264r::DbInfo* dbinfo, int2 rows, int* inter_cnt, int tag, int* zero,
-                                    int nz, int* zero2, int nz2);
+                                    int nz, int* zero2, int nz2, int per);
 extern "C" __global__ void k_inter_sp(h264r_batch b, int2 rows, const int* sp_flag, uint8_t* recon);
 extern "C" __global__ void k_untile(h264r_batch b, int2 rows, const uint8_t* recon);
 extern "C" __global__ void k_intra_pic(h264r_batch b, int* sync, int* err, const uint16_t* lvl, int lmax, int2 rows,
@@ -51,7 +51,9 @@ extern "C" __global__ void k_deblock(h264r_batch b, const h264r::DbInfo* dbinfo,
                                      int* sync, int* err, uint32_t epoch, int2 rows, int nx, uint8_t* recon);
 extern "C" __global__ void k_deblock2(h264r_batch b, const h264r::DbInfo* dbinfo, uint64_t* hb,
                                       int* sync, int* err, uint32_t epoch, int2 rows, int nx, const uint8_t* recon);
-extern "C" __global__ void k_deblock2l(h264r_batch b, const h264r::DbInfo* dbinfo, uint64_t* hb,
+extern "C" __global__ void k_deblock2y(h264r_batch b, const h264r::DbInfo* dbinfo, uint64_t* hb,
+                                      int* sync, int* err, uint32_t epoch, int2 rows, int nx, const uint8_t* recon);
+extern "C" __global__ void k_deblock2c(h264r_batch b, const h264r::DbInfo* dbinfo, uint64_t* hb,
                                       int* sync, int* err, uint32_t epoch, int2 rows, int nx, const uint8_t* recon);
 constexpr size_t DBINFO_BYTES = 80;
 constexpr size_t HANDOFF_BYTES = 256;   // one tagged record (32 x {dword, epoch}) per MB
@@ -179,6 +181,7 @@ struct h264r_ctx {
     hipStream_t side = nullptr;
     std::vector<hipEvent_t> ev_chunk;
     hipEvent_t ev_side = nullptr;
+    hipEvent_t ev_fork = nullptr;              // the split deblocking walk: launch stream -> side stream
     // timing: every kernel of every launch bracketed by events on its stream
     bool timing = false;
     int debug = 0;
@@ -260,7 +263,7 @@ struct Knobs {
     uint32_t wait_ticks = 0;   // H264R_WAIT_MS: bound of every device-side wait (below)
     int levels = 16;           // H264R_LEVELS: dependency levels from lists (level_launches)
     int deblock2_min = 8;      // H264R_DEBLOCK2_MIN: batches of this many 68-row pictures' worth of MB rows deblock with k_deblock2
-    int deblock2l_max = 0;     // H264R_DB2L_MAX: batches of fewer 68-row pictures' worth of MB rows take k_deblock2l
+    int deblock2s_max = 128;   // H264R_DB2S_MAX: batches of fewer 68-row pictures' worth of MB rows take the split walk
     int lvl_margin = 1;        // H264R_LVL_MARGIN: k_intra_levels' grid, blocks per CU below occupancy
     bool coop = false;         // H264R_COOP: k_intra_levels by hipLaunchCooperativeKernel (1) or a plain launch
     int walk_gstep = 0;        // H264R_WALK_GSTEP: the walk's band hand-off period (0: by batch size)
@@ -282,7 +285,7 @@ static bool env_long(const char* name, long lo, long hi, long* out)
     return true;
 }
 constexpr int SCHEDULE_FLAGS = H264R_DBG_INTRA_WALK | H264R_DBG_DEBLOCK_MB | H264R_DBG_DEBLOCK_ROWS | H264R_DBG_DEBLOCK_GLOBAL |
-                               H264R_DBG_OVERLAP | H264R_DBG_DEBLOCK_LANES16;
+                               H264R_DBG_OVERLAP | H264R_DBG_DEBLOCK_SPLIT;
 static const Knobs& knobs()
 {
     static const Knobs k = [] {
@@ -302,7 +305,7 @@ static const Knobs& knobs()
         // throughput batch, 32 2160p chain pictures, up (profiles/r05_x_deblock_min.txt); the lone
         // picture of the latency chain keeps k_deblock
         v = 8; n.ok &= env_long("H264R_DEBLOCK2_MIN", 1, 1L << 30, &v); n.deblock2_min = (int)v;
-        v = 0; n.ok &= env_long("H264R_DB2L_MAX", 0, 1L << 30, &v); n.deblock2l_max = (int)v;
+        v = 128; n.ok &= env_long("H264R_DB2S_MAX", 0, 1L << 30, &v); n.deblock2s_max = (int)v;
         v = 1; n.ok &= env_long("H264R_LVL_MARGIN", 0, 7, &v); n.lvl_margin = (int)v;
         // a plain launch by default: the same throughput and latency as the cooperative one
         // (profiles/r05_w_chain_coop.txt), and the launch rocprofv3 can profile (it crashes at exit
@@ -380,6 +383,7 @@ int h264r_destroy(h264r_ctx* c)
     if (c->side) (void)hipStreamSynchronize(c->side);
     for (hipEvent_t e : c->ev_chunk) (void)hipEventDestroy(e);
     if (c->ev_side) (void)hipEventDestroy(c->ev_side);
+    if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
     if (c->side) (void)hipStreamDestroy(c->side);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -488,7 +492,8 @@ static h264r_batch sub_batch(const h264r_batch& b, int p0, int n)
 // [deblock ticket][level barrier, deepest level][SP inter MBs seen] + the deblocking kernels'
 // per-XCD ticket counters, done count, then per picture the waves of k_dbinfo that met an inter
 // or I_PCM MB (k_inter4r skips the pictures without one)
-static size_t sync_ints(int P, int H) { return 1 + (size_t)P * H + 5 + 9 + P; }
+// (two sets of deblocking counters: the split walk's luma and chroma kernels run together)
+static size_t sync_ints(int P, int H) { return 1 + (size_t)P * H + 5 + 18 + P; }
 
 // One launch sequence's share of the scratch (the whole batch, or one chunk of the overlapped
 // schedule): its pictures, their deblocking records and MB-tiled reconstruction, its sync region.
@@ -514,17 +519,21 @@ static int recon_launches(h264r_ctx* c, const Stage& S, hipStream_t s, int2 rows
     const int groups = (W * HB + 15) / 16;
     // groups per workgroup (launch_cfg.h), 8 XCD bands (k_recon.hip inter4_groups)
     const dim3 igrid(8 * ((groups + 8 * H264R_INTER_GROUPS - 1) / (8 * H264R_INTER_GROUPS)), P);
-    const dim3 dgrid(8 * ((groups + 8 * H264R_DBINFO_GROUPS - 1) / (8 * H264R_DBINFO_GROUPS)), P);
+    // k_dbinfo: H264R_DBINFO_GROUPS groups per workgroup (its LDS tables filled once for them) when
+    // that still makes >= 2048 workgroups; one group each below (the latency chain's lone picture:
+    // 64 workgroups walking 8 groups each took 20 us)
+    const int dper = (int64_t)P * groups >= 2048LL * H264R_DBINFO_GROUPS ? H264R_DBINFO_GROUPS : 1;
+    const dim3 dgrid(8 * ((groups + 8 * dper - 1) / (8 * dper)), P);
     {
         Timed t(c, 0, s);
         int* sp_flag = sync + 1 + (size_t)P * H + 4;
         // the deblocking records first (k_inter4r then fits 4 waves/SIMD), with per picture
         // a flag that an inter or I_PCM MB was met (profiles/r03_f_dbinfo_ab.txt, r03_h_inter_ab.txt)
-        int* inter_cnt = sync + 1 + (size_t)P * H + 14;
+        int* inter_cnt = sync + 1 + (size_t)P * H + 23;
         // k_dbinfo zeroes the stage's sync words before the flags and the level counters
         if (++X.tag <= 0) X.tag = 1;
-        hipLaunchKernelGGL(k_dbinfo, dgrid, dim3(256), 0, s, b, S.dbinfo, rows, inter_cnt, X.tag, sync, (int)(1 + (size_t)P * H + 14),
-                           levels ? X.d_lcnt : nullptr, levels ? 3 * LEVEL_IDS : 0);
+        hipLaunchKernelGGL(k_dbinfo, dgrid, dim3(256), 0, s, b, S.dbinfo, rows, inter_cnt, X.tag, sync, (int)(1 + (size_t)P * H + 23),
+                           levels ? X.d_lcnt : nullptr, levels ? 3 * LEVEL_IDS : 0, dper);
         HIP_OK(hipGetLastError());
         hipLaunchKernelGGL(k_inter4r, igrid, dim3(256), 0, s, b, S.dbinfo, rows, sp_flag, recon, (const int*)inter_cnt, X.tag);
         HIP_OK(hipGetLastError());
@@ -584,7 +593,8 @@ static int recon_launches(h264r_ctx* c, const Stage& S, hipStream_t s, int2 rows
     return H264R_OK;
 }
 
-// The deblocking of a stage on stream s (sched 1 k_deblock2, 2 k_deblock2l, 0 k_deblock), or the
+// The deblocking of a stage on stream s (sched 1 k_deblock2, 2 the split walk: k_deblock2y on s
+// beside k_deblock2c on the context's side stream, 0 k_deblock), or the
 // untiled copy of its reconstruction (H264R_DBG_NO_DEBLOCK).
 static int deblock_launch(h264r_ctx* c, const Stage& S, hipStream_t s, int2 rows, uint8_t* hb, uint32_t epoch, int sched)
 {
@@ -611,14 +621,31 @@ static int deblock_launch(h264r_ctx* c, const Stage& S, hipStream_t s, int2 rows
         once = true;
     }
     if (sched) {
-        // k_deblock2 keeps a picture group on one XCD (g % nx): nx counters; k_deblock2l (16 lanes
-        // per unit: one picture per wave) the same with one-picture groups
-        const int pics = sched == 2 ? 1 : DEBLOCK2_PICS;
-        int grid = ((P + pics - 1) / pics) * ((HB + H264R_DB2_BAND - 1) / H264R_DB2_BAND);
+        // k_deblock2 keeps a picture group on one XCD (g % nx): nx counters
+        int grid = ((P + DEBLOCK2_PICS - 1) / DEBLOCK2_PICS) * ((HB + H264R_DB2_BAND - 1) / H264R_DB2_BAND);
         const int nx = grid >= 64 * c->nxcc && !(c->debug & H264R_DBG_DEBLOCK_GLOBAL) ? c->nxcc : 1;
         grid = (grid + nx - 1) / nx * nx;
-        hipLaunchKernelGGL(sched == 2 ? k_deblock2l : k_deblock2, dim3(grid), dim3(64), 0, s, b, S.dbinfo,
-                           reinterpret_cast<uint64_t*>(hb), dsync, c->d_err, epoch, rows, nx, (const uint8_t*)S.recon);
+        if (sched == 2) {
+            // the split walk: the luma and chroma planes filter independently (deblock.cc:418-535
+            // per plane), so each plane's walk is its own wave with the shorter step; the chroma
+            // walk on the side stream, joined back before anything after the deblocking
+            if (!c->side) HIP_OK(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
+            if (!c->ev_fork) HIP_OK(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
+            if (!c->ev_side) HIP_OK(hipEventCreateWithFlags(&c->ev_side, hipEventDisableTiming));
+            HIP_OK(hipEventRecord(c->ev_fork, s));
+            HIP_OK(hipStreamWaitEvent(c->side, c->ev_fork, 0));
+            hipLaunchKernelGGL(k_deblock2c, dim3(grid), dim3(64), 0, c->side, b, S.dbinfo, reinterpret_cast<uint64_t*>(hb),
+                               dsync + 9, c->d_err, epoch, rows, nx, (const uint8_t*)S.recon);
+            HIP_OK(hipGetLastError());
+            hipLaunchKernelGGL(k_deblock2y, dim3(grid), dim3(64), 0, s, b, S.dbinfo, reinterpret_cast<uint64_t*>(hb),
+                               dsync, c->d_err, epoch, rows, nx, (const uint8_t*)S.recon);
+            HIP_OK(hipGetLastError());
+            HIP_OK(hipEventRecord(c->ev_side, c->side));
+            HIP_OK(hipStreamWaitEvent(s, c->ev_side, 0));
+            return H264R_OK;
+        }
+        hipLaunchKernelGGL(k_deblock2, dim3(grid), dim3(64), 0, s, b, S.dbinfo, reinterpret_cast<uint64_t*>(hb), dsync,
+                           c->d_err, epoch, rows, nx, (const uint8_t*)S.recon);
     } else {
         // k_deblock keeps a picture's pairs on one XCD (p % nx): nx times the largest
         // XCD share of waves, so every XCD runs all its pairs at once
@@ -672,13 +699,14 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
     // crossover measured on whole 1080p pictures (68 MB rows), so a launch qualifies by its
     // picture-rows (a 2160p picture counts twice, a 17-row slice band a quarter); the chunks of
     // the overlapped schedule all take the schedule of the smallest
-    // k_deblock2l (16 lanes per unit, one picture per wave: the shortest steps) below
-    // H264R_DB2L_MAX pictures' worth of rows
+    // the split walk (k_deblock2y + k_deblock2c: shorter steps, twice the waves) below
+    // H264R_DB2S_MAX pictures' worth of rows (not under the overlapped schedule, which has the
+    // side stream already)
     const int64_t prows = (int64_t)chunk_min * HB;
-    const int sched = (c->debug & H264R_DBG_DEBLOCK_LANES16) ? 2
+    const int sched = (c->debug & H264R_DBG_DEBLOCK_SPLIT)   ? (nch > 1 ? 1 : 2)
                     : (c->debug & H264R_DBG_DEBLOCK_ROWS)    ? 1
                     : (c->debug & H264R_DBG_DEBLOCK_MB)      ? 0
-                    : prows < (int64_t)K.deblock2l_max * 68  ? 2
+                    : prows < (int64_t)K.deblock2s_max * 68 && nch == 1 ? 2
                     : prows >= (int64_t)K.deblock2_min * 68  ? 1 : 0;
     const bool by_rows = sched != 0;                 // k_deblock2's hand-off records (both widths)
     // hand-off records of the chosen deblocking kernel, a region per picture; fresh memory or a
@@ -772,8 +800,9 @@ static int run_batch(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row0
 #ifdef H264R_TRACE
 void h264r_db_trace_copy(void* dst);    // k_deblock.hip / k_deblock2.hip (trace builds)
 void h264r_db2_trace_copy(void* dst);
-void h264r_db2l_trace_copy(void* dst);
-// H264R_TRACE_OUT=<path>: k_deblock's trace to <path>, k_deblock2's to <path>.2, k_deblock2l's to <path>.2l
+void h264r_db2y_trace_copy(void* dst);
+void h264r_db2c_trace_copy(void* dst);
+// H264R_TRACE_OUT=<path>: k_deblock's trace to <path>, k_deblock2's to <path>.2, the split walk's to .2y / .2c
 static void dump_trace(hipStream_t s)
 {
     const char* path = getenv("H264R_TRACE_OUT");
@@ -784,8 +813,10 @@ static void dump_trace(hipStream_t s)
     if (FILE* f = fopen(path, "wb")) { fwrite(buf.data(), 8, buf.size(), f); fclose(f); }
     h264r_db2_trace_copy(buf.data());
     if (FILE* f = fopen((std::string(path) + ".2").c_str(), "wb")) { fwrite(buf.data(), 8, buf.size(), f); fclose(f); }
-    h264r_db2l_trace_copy(buf.data());
-    if (FILE* f = fopen((std::string(path) + ".2l").c_str(), "wb")) { fwrite(buf.data(), 8, buf.size(), f); fclose(f); }
+    h264r_db2y_trace_copy(buf.data());
+    if (FILE* f = fopen((std::string(path) + ".2y").c_str(), "wb")) { fwrite(buf.data(), 8, buf.size(), f); fclose(f); }
+    h264r_db2c_trace_copy(buf.data());
+    if (FILE* f = fopen((std::string(path) + ".2c").c_str(), "wb")) { fwrite(buf.data(), 8, buf.size(), f); fclose(f); }
 }
 #endif
 

@@ -69,12 +69,17 @@ using namespace h264r;
 
 namespace {
 
-constexpr int LPU = H264R_DB2_LPU;     // lanes per (picture, MB row) unit: 4, 8 or 16
-static_assert(LPU == 4 || LPU == 8 || LPU == 16, "H264R_DB2_LPU");
+constexpr int LPU = H264R_DB2_LPU;     // lanes per (picture, MB row) unit: 4 or 8
+static_assert(LPU == 4 || LPU == 8, "H264R_DB2_LPU");
 constexpr int UNITS = DEBLOCK2_UNITS;  // (picture, MB row) units per wave
-constexpr int NH = LPU == 16 ? 2 : LPU / 4;   // lanes per quad index q (8 lanes: the pairs of a dword split in two;
-                                       // 16: the same for the unit's luma lanes 0..7 and chroma lanes 8..15)
+constexpr int NH = LPU / 4;            // lanes per quad index q (8 lanes: the pairs of a dword split in two)
 constexpr int BAND = H264R_DB2_BAND;   // MB rows per wave
+#ifndef H264R_DB2_PL
+#define H264R_DB2_PL 2                 // planes a wave filters: 2 both; 0 luma, 1 chroma (the split walk, Makefile)
+#endif
+constexpr int PL = H264R_DB2_PL;
+constexpr bool DOY = PL != 1, DOC = PL != 0;
+static_assert(PL == 2 || LPU == 8, "the split walk is built at 8 lanes per unit");
 constexpr int PICS = UNITS / BAND;     // pictures per wave
 static_assert(UNITS % BAND == 0, "a band divides the wave's units");
 constexpr int RECG = 24;               // granules per MB record: [consumer lane c 0..3][i 0..5]
@@ -139,15 +144,18 @@ constexpr int OUT_AUX = H264R_DB2_OUT_AUX;
 }  // namespace
 
 #ifndef H264R_DB2_KERNEL
-#define H264R_DB2_KERNEL k_deblock2        // the 16-lane build is k_deblock2l (Makefile)
+#define H264R_DB2_KERNEL k_deblock2        // the split walk's builds are k_deblock2y / k_deblock2c (Makefile)
 #endif
 #ifdef H264R_TRACE
 // Timing trace (trace builds only: make EXTRA=-DH264R_TRACE): per ticket {start, end
 // (s_memrealtime, 100 MHz), then s_memtime cycles spent in: V pass, record wait, output
 // stores + staging + fill, H pass + publishes + next fetch}.
-#if H264R_DB2_LPU == 16
-#define h264r_db2_trace h264r_db2l_trace
-#define h264r_db2_trace_copy h264r_db2l_trace_copy
+#if H264R_DB2_PL == 0
+#define h264r_db2_trace h264r_db2y_trace
+#define h264r_db2_trace_copy h264r_db2y_trace_copy
+#elif H264R_DB2_PL == 1
+#define h264r_db2_trace h264r_db2c_trace
+#define h264r_db2_trace_copy h264r_db2c_trace_copy
 #endif
 __device__ unsigned long long h264r_db2_trace[1 << 16][8];
 #define TRACE(...) __VA_ARGS__
@@ -178,7 +186,7 @@ extern "C" void h264r_db2_trace_copy(void* dst) { (void)hipMemcpyFromSymbol(dst,
 // picture: 20.2 KiB, 8 waves per CU at 8 lanes per unit); asking for 2 waves per SIMD keeps the
 // compiler from parking values in AGPRs (at a 512-register budget it did, and the wave's VGPR +
 // AGPR footprint of 257 left one wave per SIMD)
-#define H264R_DB2_WAVES_PER_EU (H264R_DB2_LPU >= 8 ? 2 : 1)
+#define H264R_DB2_WAVES_PER_EU (H264R_DB2_LPU == 8 ? 2 : 1)
 extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(H264R_DB2_WAVES_PER_EU, H264R_DB2_WAVES_PER_EU))) void H264R_DB2_KERNEL(
     h264r_batch b, const DbInfo* __restrict__ dbinfo, uint64_t* hb, int* sync, int* err, uint32_t epoch, int2 rows, int nx,
     const uint8_t* __restrict__ recon)
@@ -223,9 +231,7 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(H
     asm volatile("" : "+v"(lane));
     // unit u; q = the unit's quarter (luma rows / dword column 4q.., chroma plane q/2, dword q&1);
     // with 8 lanes per unit, h = which half of q's two row / column pairs this lane filters
-    // (16 lanes: q8 0..7 luma as at 8 lanes, 8..15 chroma -- q = 2 plane + dword, h the pair)
-    const int u = lane / LPU, q8 = lane % LPU, q = (LPU == 16 ? q8 & 7 : q8) / NH, h = q8 % NH;
-    const bool cl = LPU == 16 && q8 >= 8;                     // a chroma lane (16 lanes per unit)
+    const int u = lane / LPU, q8 = lane % LPU, q = q8 / NH, h = q8 % NH;
     const int rb = u / PICS, pu = u - rb * PICS;              // row in the band, picture in the group
     const int y = R0 + band * BAND + rb;
     const int pic0 = grp * PICS, npg = min(PICS, b.num_pics - pic0);
@@ -273,25 +279,31 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(H
     // ---- one MB of the MB-tiled reconstruction (device_common.h), 16 bytes per load:
     // luma rows q8 + LPU i, chroma chunks q8 + LPU j (chunk k: plane k / 4, rows 2 (k & 3), +1)
     const uint8_t* rrow = recon + ((size_t)pic * g.nmb + (size_t)yc * W) * RECON_MB;
-    constexpr int NLR = 16 / LPU, NCK = LPU == 16 ? 1 : 8 / LPU;   // (16 lanes: chunks on lanes 0..7)
+    constexpr int NLR = 16 / LPU, NCK = 8 / LPU;
     v4u wl[NLR], wc[NCK];
     auto fetch = [&](int m) {
 #if H264R_DB2_DIAG & 2
         m = 0;                           // diagnostic build: every fetch reads MB 0 (L2-resident)
 #endif
         const uint8_t* ma = rrow + (size_t)min(max(m, 0), W - 1) * RECON_MB;
+        if constexpr (DOY) {
 #pragma unroll
-        for (int i = 0; i < NLR; ++i) wl[i] = load_global<v4u>(ma + (LPU * i + q8) * 16);
+            for (int i = 0; i < NLR; ++i) wl[i] = load_global<v4u>(ma + (LPU * i + q8) * 16);
+        }
+        if constexpr (DOC) {
 #pragma unroll
-        for (int j = 0; j < NCK; ++j) wc[j] = load_global<v4u>(ma + RECON_CB + min(LPU * j + q8, 7) * 16);
+            for (int j = 0; j < NCK; ++j) wc[j] = load_global<v4u>(ma + RECON_CB + (LPU * j + q8) * 16);
+        }
     };
     auto fill = [&](int s) {                                                            // registers -> ring slot s
+        if constexpr (DOY) {
 #pragma unroll
-        for (int i = 0; i < NLR; ++i) *reinterpret_cast<v4u*>(&U.y[LPU * i + q8][4 * s]) = wl[i];
+            for (int i = 0; i < NLR; ++i) *reinterpret_cast<v4u*>(&U.y[LPU * i + q8][4 * s]) = wl[i];
+        }
 #pragma unroll
         for (int j = 0; j < NCK; ++j) {
-            const int k = LPU * j + q8, pl = (k >> 2) & 1, r = 2 * (k & 3);
-            if (LPU < 16 || k < 8) {
+            const int k = LPU * j + q8, pl = k >> 2, r = 2 * (k & 3);
+            if (DOC) {
                 *reinterpret_cast<v2u*>(&U.c[pl][r][2 * s]) = wc[j].xy;
                 *reinterpret_cast<v2u*>(&U.c[pl][r + 1][2 * s]) = wc[j].zw;
             }
@@ -306,15 +318,19 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(H
     // row 4 (i & 1) + q (rows 13..15 / 7 are overwritten by the row below when it has filtered them)
     auto stage_own = [&](int m, int s) {
         const int mc = max(m, 0);
+        if constexpr (DOY) {
 #pragma unroll
-        for (int i = 0; i < NLR; ++i) {
-            const int r = LPU * i + q8;
-            *reinterpret_cast<v4u*>(&T.y[r][mc & 3][0]) = *reinterpret_cast<const v4u*>(&U.y[r][4 * s]);
+            for (int i = 0; i < NLR; ++i) {
+                const int r = LPU * i + q8;
+                *reinterpret_cast<v4u*>(&T.y[r][mc & 3][0]) = *reinterpret_cast<const v4u*>(&U.y[r][4 * s]);
+            }
         }
+        if constexpr (DOC) {
 #pragma unroll
-        for (int i = 0; i < NLR; ++i) {
-            const int k = LPU * i + q8, pl = k >> 3, r = k & 7;
-            *reinterpret_cast<v2u*>(&T.c[pl][r][mc & 3][0]) = *reinterpret_cast<const v2u*>(&U.c[pl][r][2 * s]);
+            for (int i = 0; i < NLR; ++i) {
+                const int k = LPU * i + q8, pl = k >> 3, r = k & 7;
+                *reinterpret_cast<v2u*>(&T.c[pl][r][mc & 3][0]) = *reinterpret_cast<const v2u*>(&U.c[pl][r][2 * s]);
+            }
         }
     };
     // The groups that are complete at the end of a step, stored by the whole wave: each unit's
@@ -334,12 +350,15 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(H
             const uint32_t cr2 = (uint32_t)__builtin_amdgcn_readlane((int)crow, l0);
             const int g0 = m2 & ~3;
             const bool inrow = g0 + pp <= m2;
-            st16<OUT_AUX>(rY, r <= yl2 && inrow ? yr2 + (uint32_t)r * Wl + (uint32_t)(g0 + pp) * 16u : OOB,
-                          *reinterpret_cast<const v4u*>(&G[u2].y[r][pp][0]));
-            const uint32_t off = cr <= cl2 && inrow ? cr2 + (uint32_t)cr * Wc + (uint32_t)(g0 + pp) * 8u : OOB;
-            const v2u cv = *reinterpret_cast<const v2u*>(&G[u2].c[cp][cr][pp][0]);
-            st8<OUT_AUX>(rU, cp == 0 ? off : OOB, cv);
-            st8<OUT_AUX>(rV, cp == 1 ? off : OOB, cv);
+            if constexpr (DOY)
+                st16<OUT_AUX>(rY, r <= yl2 && inrow ? yr2 + (uint32_t)r * Wl + (uint32_t)(g0 + pp) * 16u : OOB,
+                              *reinterpret_cast<const v4u*>(&G[u2].y[r][pp][0]));
+            if constexpr (DOC) {
+                const uint32_t off = cr <= cl2 && inrow ? cr2 + (uint32_t)cr * Wc + (uint32_t)(g0 + pp) * 8u : OOB;
+                const v2u cv = *reinterpret_cast<const v2u*>(&G[u2].c[cp][cr][pp][0]);
+                st8<OUT_AUX>(rU, cp == 0 ? off : OOB, cv);
+                st8<OUT_AUX>(rV, cp == 1 ? off : OOB, cv);
+            }
         }
         // the band's first row: rows 13..15 (chroma 7) of the row above, final since H(xs)
         const bool up = active && rb == 0 && above && xs >= 0 && xs < W;
@@ -350,12 +369,15 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(H
             const uint32_t cr2 = (uint32_t)__builtin_amdgcn_readlane((int)crow, l0);
             const int g0 = x2 & ~3;
             const bool inrow = g0 + pp <= x2;
-            st16<OUT_AUX>(rY, r < 3 && inrow ? yr2 - (uint32_t)(3 - r) * Wl + (uint32_t)(g0 + pp) * 16u : OOB,
-                          *reinterpret_cast<const v4u*>(&UP[pu2].yu[min(r, 2)][pp][0]));
-            const uint32_t off = r < 2 && inrow ? cr2 - Wc + (uint32_t)(g0 + pp) * 8u : OOB;
-            const v2u cv = *reinterpret_cast<const v2u*>(&UP[pu2].cu[r & 1][pp][0]);
-            st8<OUT_AUX>(rU, r == 0 ? off : OOB, cv);
-            st8<OUT_AUX>(rV, r == 1 ? off : OOB, cv);
+            if constexpr (DOY)
+                st16<OUT_AUX>(rY, r < 3 && inrow ? yr2 - (uint32_t)(3 - r) * Wl + (uint32_t)(g0 + pp) * 16u : OOB,
+                              *reinterpret_cast<const v4u*>(&UP[pu2].yu[min(r, 2)][pp][0]));
+            if constexpr (DOC) {
+                const uint32_t off = r < 2 && inrow ? cr2 - Wc + (uint32_t)(g0 + pp) * 8u : OOB;
+                const v2u cv = *reinterpret_cast<const v2u*>(&UP[pu2].cu[r & 1][pp][0]);
+                st8<OUT_AUX>(rU, r == 0 ? off : OOB, cv);
+                st8<OUT_AUX>(rV, r == 1 ? off : OOB, cv);
+            }
         }
     };
     // granule i of consumer lane c of MB m in slot s: luma row 12+i dword c (i < 4), chroma
@@ -406,7 +428,7 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(H
     auto load_record = [&](int m) {
         const uint32_t base = active && m >= 0 && m < W ? rec_in : OOB;
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
+        for (int k = PL == 1 ? 2 : 0; k < (PL == 0 ? 2 : 3); ++k) {       // luma pairs 0, 1; chroma pair 2
             const v4u v = __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(hrs, pair_off(base, max(m, 0), q, k), 0, AUX_SC1));
             rin[2 * k] = v.x | (uint64_t)v.y << 32; rin[2 * k + 1] = v.z | (uint64_t)v.w << 32;
         }
@@ -430,50 +452,8 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(H
         const uint32_t cpar[3] = {p ? inf[14] : inf[11], p ? inf[15] : inf[12], p ? inf[16] : inf[13]};
 
         // 2. vertical edges of MB x (deblock.cc:488-504)
-        if constexpr (LPU == 16) {
-            // one pair of lines per lane, luma (lanes 0..7: rows 4q + h, +2) or chroma (8..15:
-            // plane p, rows 4d + h, +2), through one instruction stream (filter2u): a chroma line's
-            // columns are its left neighbour's 4..7 and its own 0..7, its edges 0 and 1 take luma
-            // edges 0 and 2's bS (deblock.cc:430-433, 460), edges 2 and 3 run with bS 0
-            const int ra = cl ? 4 * d + h : 4 * q + h, rb2 = ra + 2;
-            uint32_t* rA = cl ? &U.c[p][ra][0] : &U.y[ra][0];
-            uint32_t* rB = cl ? &U.c[p][rb2][0] : &U.y[rb2][0];
-            const int lo = cl ? 2 * sl + 1 : 4 * sl + 3, ow = cl ? 2 * sc : 4 * sc;
-            uint32_t la = rA[lo], lb = rB[lo];
-            const v2u A0 = *reinterpret_cast<const v2u*>(rA + ow), A1 = *reinterpret_cast<const v2u*>(rA + ow + 2);
-            const v2u B0 = *reinterpret_cast<const v2u*>(rB + ow), B1 = *reinterpret_cast<const v2u*>(rB + ow + 2);
-            uint32_t a[4] = {A0.x, A0.y, A1.x, A1.y}, bb[4] = {B0.x, B0.y, B1.x, B1.y};
-            const s2 cm = cl ? sp2(-1) : sp2(0);
-            EdgeP ev[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const uint32_t par = cl ? cpar[e == 0 ? 0 : 2] : inf[8 + (e == 0 ? 0 : 2)];
-                const s2 bsc = e < 2 ? bs_pair(inf[2 * e], ra >> 1, rb2 >> 1) : sp2(0);
-                ev[e] = edge_params(par, cl ? bsc : bs_pair(inf[e], q, q));
-            }
-            s2 c[20];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) c[k] = unpack2(la, lb, k);
-#pragma unroll
-            for (int k = 4; k < 20; ++k) c[k] = unpack2(a[(k >> 2) - 1], bb[(k >> 2) - 1], k & 3);
-            filter2u<true>(c[0], c[1], c[2], c[3], c[4], c[5], c[6], c[7], ev[0], cm);
-#pragma unroll
-            for (int e = 1; e < 4; ++e)
-                filter2u<false>(c[4 * e], c[4 * e + 1], c[4 * e + 2], c[4 * e + 3], c[4 * e + 4], c[4 * e + 5],
-                                c[4 * e + 6], c[4 * e + 7], ev[e], cm);
-            pack4(c[0], c[1], c[2], c[3], la, lb);
-#pragma unroll
-            for (int k = 0; k < 4; ++k) pack4(c[4 + 4 * k], c[5 + 4 * k], c[6 + 4 * k], c[7 + 4 * k], a[k], bb[k]);
-            rA[lo] = la;
-            rB[lo] = lb;
-            *reinterpret_cast<v2u*>(rA + ow) = (v2u){a[0], a[1]};
-            *reinterpret_cast<v2u*>(rB + ow) = (v2u){bb[0], bb[1]};
-            if (!cl) {
-                *reinterpret_cast<v2u*>(rA + ow + 2) = (v2u){a[2], a[3]};
-                *reinterpret_cast<v2u*>(rB + ow + 2) = (v2u){bb[2], bb[3]};
-            }
-            load_record(x);
-        } else {
+        {
+          if constexpr (DOY) {
             // luma rows (4q + i, 4q + i + 2): bS of V edge e, segment q = byte 4e + q
             EdgeP ev[4];
 #pragma unroll
@@ -504,12 +484,14 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(H
                 *reinterpret_cast<v4u*>(&U.y[ra][4 * sc]) = (v4u){a[0], a[1], a[2], a[3]};
                 *reinterpret_cast<v4u*>(&U.y[rb2][4 * sc]) = (v4u){bb[0], bb[1], bb[2], bb[3]};
             }
+          }
             // the record of MB (x, y-1) from the band above, checked after the vertical edges
             // (issued here rather than at the step head: live across the luma pass its registers
             // spilled at three waves per SIMD)
             load_record(x);
             // chroma plane p rows (4d + i, +2); chroma edge 0 = luma edge 0, edge 1 (col 4) =
             // luma edge 2; row j takes the bS of luma row 2j: segment j / 2 (deblock.cc:430-433, 460)
+          if constexpr (DOC) {
 #pragma unroll
             for (int ii = 0; ii < 2 / NH; ++ii) {
                 const int i = NH == 2 ? h : ii;
@@ -537,6 +519,7 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(H
                 *reinterpret_cast<v2u*>(&U.c[p][ra][2 * sc]) = (v2u){a[0], a[1]};
                 *reinterpret_cast<v2u*>(&U.c[p][rb2][2 * sc]) = (v2u){bb[0], bb[1]};
             }
+          }
         }
         TRACE({ const unsigned long long t2 = __builtin_amdgcn_s_memtime(); tph[0] += t2 - tm; tm = t2; })
 
@@ -544,7 +527,7 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(H
         auto ready = [&]() {
             bool r = true;
 #pragma unroll
-            for (int i = 0; i < 6; ++i) r &= (rin[i] & 0xFFFFFFFF00000000ull) == tag_in;
+            for (int i = PL == 1 ? 4 : 0; i < (PL == 0 ? 4 : 6); ++i) r &= (rin[i] & 0xFFFFFFFF00000000ull) == tag_in;
             return __builtin_amdgcn_readfirstlane(__all(r || !(polls && xok))) != 0;   // wave-uniform
         };
         if (!ready()) {
@@ -568,14 +551,23 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(H
         TRACE({ const unsigned long long t2 = __builtin_amdgcn_s_memtime(); tph[1] += t2 - tm; tm = t2; })
         // the late pairs of MB x-1 (luma dword 3, chroma dword 1), final after V(x) (at x = W:
         // after H(W-1)): one per lane
-        publish_pair(active && x >= 1 && x <= W && h == 0 && !cl ? rec_out : OOB, max(x - 1, 0), sl, late_c(q), late_k(q));
+        if constexpr (PL == 2)
+            publish_pair(active && x >= 1 && x <= W && h == 0 ? rec_out : OOB, max(x - 1, 0), sl, late_c(q), late_k(q));
+        else if constexpr (PL == 0)      // luma dword 3: lanes (3, h) publish pair h
+            publish_pair(active && x >= 1 && x <= W && q == 3 ? rec_out : OOB, max(x - 1, 0), sl, 3, h);
+        else                             // chroma dword 1 (consumers 1, 3): lanes (q odd, 0)
+            publish_pair(active && x >= 1 && x <= W && h == 0 && (q & 1) ? rec_out : OOB, max(x - 1, 0), sl, q, 2);
         // rows -4..-1 (chroma -2..-1) of MB x's top edge for rows 1.. of the band: the upper unit's
         // left slot (the upper row is on MB x+1), read before that slot is refilled below
         if (rb) {
+            if constexpr (DOY) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) rin[r] = A.y[12 + r][4 * sc + q];
+                for (int r = 0; r < 4; ++r) rin[r] = A.y[12 + r][4 * sc + q];
+            }
+            if constexpr (DOC) {
 #pragma unroll
-            for (int r = 0; r < 2; ++r) rin[4 + r] = A.c[p][6 + r][2 * sc + d];
+                for (int r = 0; r < 2; ++r) rin[4 + r] = A.c[p][6 + r][2 * sc + d];
+            }
         }
         // 5. MB x-1 is final (V(x) done): it leaves the ring, and MB x+1 (fetched during the
         // previous step) takes its slot with its DbInfo
@@ -594,47 +586,8 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(H
 
         // 6. horizontal edges of MB x (deblock.cc:506-535); rows -4..-1 from the record
         uint32_t wy[20], wcv[10];
-        if constexpr (LPU == 16) {
-            // luma lanes: columns 4q + h, +2 over rows -4..15; chroma lanes: plane p, columns
-            // 4d + h, +2 over rows -2..7 (-2, -1 from the record), the other rows of the 20
-            // repeats whose edges (2 and 3) run with bS 0
-            uint32_t* col = cl ? &U.c[p][0][2 * sc + d] : &U.y[0][4 * sc + q];
-            const int pitch = cl ? 4 : 8;                                    // dwords per row
-            wy[0] = (uint32_t)(cl ? rin[4] : rin[0]);
-            wy[1] = (uint32_t)(cl ? rin[4] : rin[1]);
-            wy[2] = (uint32_t)(cl ? rin[4] : rin[2]);
-            wy[3] = (uint32_t)(cl ? rin[5] : rin[3]);
-#pragma unroll
-            for (int r = 0; r < 16; ++r) wy[4 + r] = col[(cl ? min(r, 7) : r) * pitch];
-            const s2 cm = cl ? sp2(-1) : sp2(0);
-            EdgeP eh[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const uint32_t par = cl ? cpar[e == 0 ? 1 : 2] : inf[8 + (e == 0 ? 1 : 2)];
-                const s2 bsc = e < 2 ? bs_pair(inf[4 + 2 * e], 2 * d, 2 * d + 1) : sp2(0);
-                eh[e] = edge_params(par, cl ? bsc : bs_pair(inf[4 + e], q, q));
-            }
-            s2 c[20];
-#pragma unroll
-            for (int r = 0; r < 20; ++r) c[r] = unpack_cols(wy[r], h);
-            filter2u<true>(c[0], c[1], c[2], c[3], c[4], c[5], c[6], c[7], eh[0], cm);
-#pragma unroll
-            for (int e = 1; e < 4; ++e)
-                filter2u<false>(c[4 * e], c[4 * e + 1], c[4 * e + 2], c[4 * e + 3], c[4 * e + 4], c[4 * e + 5],
-                                c[4 * e + 6], c[4 * e + 7], eh[e], cm);
-#pragma unroll
-            for (int r = 1; r < 20; ++r) {                // the other pair from the partner lane
-                const s2 o = as_s2(partner(as_w(c[r])));
-                wy[r] = h ? pack_cols(o, c[r]) : pack_cols(c[r], o);
-            }
-#pragma unroll
-            for (int r = 0; r < 8; ++r) col[r * pitch] = wy[4 + r];
-            if (!cl) {
-#pragma unroll
-                for (int r = 8; r < 16; ++r) col[r * pitch] = wy[4 + r];
-            }
-        } else {
         {
+        if constexpr (DOY) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) wy[r] = (uint32_t)rin[r];
 #pragma unroll
@@ -666,7 +619,7 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(H
 #pragma unroll
             for (int r = 0; r < 16; ++r) U.y[r][4 * sc + q] = wy[4 + r];
         }
-        {
+        if constexpr (DOC) {
             // chroma plane p, columns 4d .. 4d+3 (dword d), rows -2..7; the halves of a pair sit
             // in segments 2d and 2d+1 of luma H edge 0 / 2
 #pragma unroll
@@ -705,25 +658,22 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(H
 #pragma unroll
         for (int jj = 0; jj < 2 / NH; ++jj) {
             const int j = NH == 2 ? h : jj;
-            publish_pair(xok && !cl ? rec_out : OOB, max(x, 0), sc, early_c(q, j), early_k(q, j));
+            if constexpr (PL == 2)
+                publish_pair(xok ? rec_out : OOB, max(x, 0), sc, early_c(q, j), early_k(q, j));
+            else if constexpr (PL == 0)  // luma dwords 0..2: lanes (q < 3, h) publish pair h
+                publish_pair(xok && q < 3 ? rec_out : OOB, max(x, 0), sc, q, h);
+            else                         // chroma dword 0 (consumers 0, 2): lanes (q even, 0)
+                publish_pair(xok && h == 0 && !(q & 1) ? rec_out : OOB, max(x, 0), sc, q, 2);
         }
         // rows 13..15 (chroma 7) of MB (x, y-1), final now: into the staging of the unit above, or
         // (the band's first row) into this unit's own
         if (xok && above) {
-            if constexpr (LPU == 16) {
-                if (cl) {
-                    *(rb ? &TA.c[p][7][x & 3][d] : &TU.cu[p][x & 3][d]) = wy[3];
-                } else {
-                    uint32_t* yd = rb ? &TA.y[13][x & 3][q] : &TU.yu[0][x & 3][q];
-#pragma unroll
-                    for (int r = 1; r < 4; ++r) yd[(r - 1) * 16] = wy[r];
-                }
-            } else {
+            if constexpr (DOY) {
                 uint32_t* yd = rb ? &TA.y[13][x & 3][q] : &TU.yu[0][x & 3][q];
 #pragma unroll
                 for (int r = 1; r < 4; ++r) yd[(r - 1) * 16] = wy[r];
-                *(rb ? &TA.c[p][7][x & 3][d] : &TU.cu[p][x & 3][d]) = wcv[1];
             }
+            if constexpr (DOC) *(rb ? &TA.c[p][7][x & 3][d] : &TU.cu[p][x & 3][d]) = wcv[1];
         }
         // 8. what the next step fills: MB x+2 and its DbInfo
         fetch(x + 2);

@@ -118,7 +118,7 @@ extern "C" __global__ __launch_bounds__(256, H264R_INTER_WAVES) void k_inter4r(h
 // chain paid ~20 us for them, profiles/r05_ac_latency_kernels.txt) -- and marks a picture with
 // an inter or I_PCM MB by storing this launch's tag (nonzero), so the flags need no zeroing.
 extern "C" __global__ __launch_bounds__(256, 8) void k_dbinfo(h264r_batch b, DbInfo* dbinfo, int2 rows, int* inter_cnt, int tag,
-                                                             int* zero, int nz, int* zero2, int nz2)
+                                                             int* zero, int nz, int* zero2, int nz2, int per)
 {
     {
         const int nt = (int)(gridDim.x * gridDim.y * blockDim.x);
@@ -130,7 +130,7 @@ extern "C" __global__ __launch_bounds__(256, 8) void k_dbinfo(h264r_batch b, DbI
     const int pic = blockIdx.y;
     const Geom g = make_geom(b.width_mbs, b.height_mbs);
     int grp, gend;
-    if (!inter4_groups(g, rows, H264R_DBINFO_GROUPS, grp, gend)) return;
+    if (!inter4_groups(g, rows, per, grp, gend)) return;
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int aend = rows.y * g.wmb;
     const h264r_slice* slices = b.slices + (size_t)pic * b.slice_stride;

@@ -145,46 +145,4 @@ DEV void filter2(s2& p3, s2& p2, s2& p1, s2& p0, s2& q0, s2& q1, s2& q2, s2& q3,
     q1 = sel(nf, q1, nq1);
 }
 
-// filter2 for a lane that may hold luma or chroma lines (k_deblock2 at 16 lanes per unit: one
-// instruction stream for both).  cm = -1 in both halves for chroma lines: ap / aq read as false,
-// so p1 / q1 (and, strong, p2 / q2) stay, tc = tc0 + 1, and the strong filter's "not strong"
-// branch is chroma's (2 p1 + p0 + q1 + 2) >> 2 -- filter_normal / filter_strong with
-// chromaEdgeFlag (deblock.cc:327-415).  An edge a chroma line does not have runs with bS 0.
-template <bool STRONG>
-DEV void filter2u(s2& p3, s2& p2, s2& p1, s2& p0, s2& q0, s2& q1, s2& q2, s2& q3, const EdgeP& e, s2 cm)
-{
-    const s2 dpq = absd(p0, q0);
-    const s2 nf = neg_mask(smin(smin(e.am1 - dpq, e.bm1 - absd(p1, p0)), smin(e.bm1 - absd(q1, q0), e.bs - sp2(1))));
-    const s2 nap = neg_mask(e.bm1 - absd(p2, p0)) | cm;
-    const s2 naq = neg_mask(e.bm1 - absd(q2, q0)) | cm;
-    const s2 tc = e.tc0 + sp2(2) - cm + nap + naq;          // luma tc0 + ap + aq, chroma tc0 + 1
-    s2 d = ((q0 - p0) * sp2(4) + (p1 - q1) + sp2(4)) >> sp2(3);
-    d = smin(smax(d, -tc), tc);
-    s2 np0 = clamp255(p0 + d), nq0 = clamp255(q0 - d);
-    const s2 avg = (p0 + q0 + sp2(1)) >> sp2(1);
-    s2 np1 = sel(nap, p1, p1 + smin(smax((p2 + avg - p1 * sp2(2)) >> sp2(1), -e.tc0), e.tc0));
-    s2 nq1 = sel(naq, q1, q1 + smin(smax((q2 + avg - q1 * sp2(2)) >> sp2(1), -e.tc0), e.tc0));
-    if (STRONG) {
-        const s2 is4 = opaque_mask(neg_mask(e.bs - sp2(4)) ^ sp2(-1));
-        const s2 nstrong = neg_mask(((e.alpha >> sp2(2)) + sp2(1)) - dpq);
-        const s2 nsp = nap | nstrong, nsq = naq | nstrong;
-        const s2 s_p0 = sel(nsp, (p1 * sp2(2) + p0 + q1 + sp2(2)) >> sp2(2),
-                            (p2 + p1 * sp2(2) + p0 * sp2(2) + q0 * sp2(2) + q1 + sp2(4)) >> sp2(3));
-        const s2 s_p1 = sel(nsp, p1, (p2 + p1 + p0 + q0 + sp2(2)) >> sp2(2));
-        const s2 s_p2 = sel(nsp, p2, (p3 * sp2(2) + p2 * sp2(3) + p1 + p0 + q0 + sp2(4)) >> sp2(3));
-        const s2 s_q0 = sel(nsq, (q1 * sp2(2) + q0 + p1 + sp2(2)) >> sp2(2),
-                            (p1 + p0 * sp2(2) + q0 * sp2(2) + q1 * sp2(2) + q2 + sp2(4)) >> sp2(3));
-        const s2 s_q1 = sel(nsq, q1, (p0 + q0 + q1 + q2 + sp2(2)) >> sp2(2));
-        const s2 s_q2 = sel(nsq, q2, (q3 * sp2(2) + q2 * sp2(3) + q1 + q0 + p0 + sp2(4)) >> sp2(3));
-        np0 = sel(is4, s_p0, np0); nq0 = sel(is4, s_q0, nq0);
-        np1 = sel(is4, s_p1, np1); nq1 = sel(is4, s_q1, nq1);
-        p2 = sel(nf, p2, sel(is4, s_p2, p2));
-        q2 = sel(nf, q2, sel(is4, s_q2, q2));
-    }
-    p1 = sel(nf, p1, np1);
-    p0 = sel(nf, p0, np0);
-    q0 = sel(nf, q0, nq0);
-    q1 = sel(nf, q1, nq1);
-}
-
 }  // namespace h264r

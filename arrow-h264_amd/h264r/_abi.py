@@ -14,7 +14,7 @@ OK, EINVAL, ENOMEM, EDEVICE, ESTATE, EUNSUPPORTED, ENODEVICE = 0, -1, -2, -3, -4
 DBG_NO_DEBLOCK, DBG_INTRA_WALK, DBG_DEBLOCK_MB, DBG_DEBLOCK_ROWS, DBG_DEBLOCK_GLOBAL = 1, 2, 4, 8, 16   # h264r_set_debug flags (include/h264r.h)
 DBG_WAIT_TEST = 32
 DBG_OVERLAP = 64
-DBG_DEBLOCK_LANES16 = 128
+DBG_DEBLOCK_SPLIT = 128
 MAX_REFS, MAX_SLOTS, MAX_SLICES = 16, 32, 256
 ABI_VERSION = 2
 

@@ -300,10 +300,10 @@ int  h264r_set_timing(h264r_ctx* ctx, int enable);
  * cut into 4 picture chunks (H264R_OVERLAP=<n> sets the count), chunk k deblocked on the
  * context's side stream while chunk k + 1 is reconstructed on the launch stream. */
 #define H264R_DBG_OVERLAP 64
-/* H264R_DBG_DEBLOCK_LANES16 forces k_deblock2l, the band walk at 16 lanes per (picture, MB row):
-   one picture per wave, luma and chroma lines in one instruction stream -- the shortest step,
-   for launches of few pictures (the latency chain, slice bands of dependent chains). */
-#define H264R_DBG_DEBLOCK_LANES16 128
+/* H264R_DBG_DEBLOCK_SPLIT forces the split band walk: the luma planes' walk (k_deblock2y) and the
+   chroma planes' (k_deblock2c) as separate waves running together -- the planes filter
+   independently, and each walk's step is shorter than the combined one. */
+#define H264R_DBG_DEBLOCK_SPLIT 128
 int  h264r_set_debug(h264r_ctx* ctx, int flags);
 /* Wait for the context's work and report a device-side failure (a wavefront wait
  * that timed out): H264R_OK or H264R_EDEVICE. */

@@ -79,8 +79,9 @@ def test_gpu_matches_reference_fixture(L, dec, fx):
         pytest.fail("; ".join(msgs) or "md5 mismatch")
 
 
-# the deblocking schedules (include/h264r.h): one MB per 32 lanes, the band walk at 8 and at 16 lanes per MB row
-DEBLOCKS = (A.DBG_DEBLOCK_MB, A.DBG_DEBLOCK_ROWS, A.DBG_DEBLOCK_MB | A.DBG_DEBLOCK_GLOBAL, A.DBG_DEBLOCK_LANES16)
+# the deblocking schedules (include/h264r.h): one MB per 32 lanes, the band walk (8 lanes per MB row),
+# the split walk (the luma and the chroma planes' walks as separate waves)
+DEBLOCKS = (A.DBG_DEBLOCK_MB, A.DBG_DEBLOCK_ROWS, A.DBG_DEBLOCK_MB | A.DBG_DEBLOCK_GLOBAL, A.DBG_DEBLOCK_SPLIT)
 
 
 def _batch_vs_oracle(L, dec, cidx, W, H, n, debug=0, deblocks=DEBLOCKS, qm=None, **over):

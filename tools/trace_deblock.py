@@ -2,7 +2,7 @@
 """Diagnostic (GPU box): per-wave timing of the deblocking walk from a trace build,
     make -C arrow-h264_amd OBJ=build_trace LIBDIR=lib_trace EXTRA=-DH264R_TRACE
     H264R_LIB=arrow-h264_amd/lib_trace/libh264r.so python tools/trace_deblock.py [pictures] [flag] [band] [lpu]
-(flag 8 = k_deblock2, 4 = k_deblock, 128 = k_deblock2l with lpu 16) [band = the build's H264R_DB2_BAND, lpu = its H264R_DB2_LPU].  k_deblock2 records
+(flag 8 = k_deblock2, 4 = k_deblock, 128 = the split walk's luma and chroma kernels) [band = the build's H264R_DB2_BAND, lpu = its H264R_DB2_LPU].  k_deblock2 records
 per ticket (a band of MB rows of a picture group) {start, end} in 100 MHz ticks and the core
 cycles of its four phases summed over the walk."""
 import os
@@ -58,26 +58,33 @@ if flag == 4:
         print(f"pair {p:3d}: start {start[sel].mean():8.1f} us end {end[sel].mean():8.1f} us, poll "
               f"{t[sel, 3].mean() / 100.0:8.1f} us, cycles/step {np.round(t[sel, 4:8].mean(0) / steps, 0)}")
     sys.exit(0)
-t = np.fromfile(out + (".2l" if lpu == 16 else ".2"), np.uint64).reshape(-1, 8).astype(np.int64)   # lpu 16: k_deblock2l
-units = 64 // lpu
-ng = (n + units // band - 1) // (units // band)
-nb = (H + band - 1) // band
-k = ng * nb
-steps = W + band + 2
-t = t[:k]
-t0 = t[:, 0].min()
-start, end = (t[:, 0] - t0) / 100.0, (t[:, 1] - t0) / 100.0       # microseconds
-print(f"{n} pictures, {k} waves ({nb} bands of {band} rows x {ng} groups): kernel span {end.max():.0f} us; "
-      f"wave duration mean {np.mean(end - start):.0f} us ({np.mean(end - start) / steps:.2f} us/step), "
-      f"start spread {start.min():.0f}..{start.max():.0f} us")
-ph = t[:, 2:6].astype(np.float64)
-tot = ph.sum(1, keepdims=True)
-print("phase share (V, record wait, stores + staging + fill, H + publish + fetch):", np.round((ph / tot).mean(0), 3))
-print("cycles per step by phase:", np.round(ph.mean(0) / steps, 0))
-bands = np.arange(k) // ng
-for r in sorted(set((0, 1, 2, nb // 2, nb - 1))):
-    sel = bands == r
-    print(f"band {r:3d}: start {start[sel].mean():8.1f} us end {end[sel].mean():8.1f} us, wait share "
-          f"{(ph[sel, 1] / tot[sel, 0]).mean():.3f}, cycles/step by phase {np.round(ph[sel].mean(0) / steps, 0)}")
-hist = np.histogram(start, bins=10)
-print("wave starts (us) histogram:", hist[0].tolist(), np.round(hist[1], 0).tolist())
+suffixes = [".2y", ".2c"] if flag == 128 else [".2"]   # the split walk's luma / chroma kernels
+def report(t):
+
+    units = 64 // lpu
+    ng = (n + units // band - 1) // (units // band)
+    nb = (H + band - 1) // band
+    k = ng * nb
+    steps = W + band + 2
+    t = t[:k]
+    t0 = t[:, 0].min()
+    start, end = (t[:, 0] - t0) / 100.0, (t[:, 1] - t0) / 100.0       # microseconds
+    print(f"{n} pictures, {k} waves ({nb} bands of {band} rows x {ng} groups): kernel span {end.max():.0f} us; "
+          f"wave duration mean {np.mean(end - start):.0f} us ({np.mean(end - start) / steps:.2f} us/step), "
+          f"start spread {start.min():.0f}..{start.max():.0f} us")
+    ph = t[:, 2:6].astype(np.float64)
+    tot = ph.sum(1, keepdims=True)
+    print("phase share (V, record wait, stores + staging + fill, H + publish + fetch):", np.round((ph / tot).mean(0), 3))
+    print("cycles per step by phase:", np.round(ph.mean(0) / steps, 0))
+    bands = np.arange(k) // ng
+    for r in sorted(set((0, 1, 2, nb // 2, nb - 1))):
+        sel = bands == r
+        print(f"band {r:3d}: start {start[sel].mean():8.1f} us end {end[sel].mean():8.1f} us, wait share "
+              f"{(ph[sel, 1] / tot[sel, 0]).mean():.3f}, cycles/step by phase {np.round(ph[sel].mean(0) / steps, 0)}")
+    hist = np.histogram(start, bins=10)
+    print("wave starts (us) histogram:", hist[0].tolist(), np.round(hist[1], 0).tolist())
+
+
+for sfx in suffixes:
+    print(f"== {sfx}")
+    report(np.fromfile(out + sfx, np.uint64).reshape(-1, 8).astype(np.int64))
