@@ -263,7 +263,7 @@ struct Knobs {
     uint32_t wait_ticks = 0;   // H264R_WAIT_MS: bound of every device-side wait (below)
     int levels = 16;           // H264R_LEVELS: dependency levels from lists (level_launches)
     int deblock2_min = 8;      // H264R_DEBLOCK2_MIN: batches of this many 68-row pictures' worth of MB rows deblock with k_deblock2
-    int deblock2s_max = 128;   // H264R_DB2S_MAX: batches of fewer 68-row pictures' worth of MB rows take the split walk
+    int deblock2s_max = 512;   // H264R_DB2S_MAX: batches of fewer 68-row pictures' worth of MB rows take the split walk
     int lvl_margin = 1;        // H264R_LVL_MARGIN: k_intra_levels' grid, blocks per CU below occupancy
     bool coop = false;         // H264R_COOP: k_intra_levels by hipLaunchCooperativeKernel (1) or a plain launch
     int walk_gstep = 0;        // H264R_WALK_GSTEP: the walk's band hand-off period (0: by batch size)
@@ -305,7 +305,11 @@ static const Knobs& knobs()
         // throughput batch, 32 2160p chain pictures, up (profiles/r05_x_deblock_min.txt); the lone
         // picture of the latency chain keeps k_deblock
         v = 8; n.ok &= env_long("H264R_DEBLOCK2_MIN", 1, 1L << 30, &v); n.deblock2_min = (int)v;
-        v = 128; n.ok &= env_long("H264R_DB2S_MAX", 0, 1L << 30, &v); n.deblock2s_max = (int)v;
+        // the split walk (twice the waves, each step shorter) wins below ~512 1080p pictures: config 3
+        // at 128 / 256 / 1024 pictures 1.06 -> 0.83 / 1.26 -> 1.23 / 3.78 -> 4.46 ms, config 4 (256)
+        // 1.28 -> 1.22, config 5 (64 2160p) 2.07 -> 1.66, the latency chain and chain mode
+        // (profiles/r05_ak_split_walk_ab.txt)
+        v = 512; n.ok &= env_long("H264R_DB2S_MAX", 0, 1L << 30, &v); n.deblock2s_max = (int)v;
         v = 1; n.ok &= env_long("H264R_LVL_MARGIN", 0, 7, &v); n.lvl_margin = (int)v;
         // a plain launch by default: the same throughput and latency as the cooperative one
         // (profiles/r05_w_chain_coop.txt), and the launch rocprofv3 can profile (it crashes at exit

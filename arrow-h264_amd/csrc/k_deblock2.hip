@@ -89,12 +89,15 @@ constexpr uint32_t OOB = 0x80000000u;  // added to an offset: past every range (
 
 // One unit's MB row in LDS: two MB slots and the DbInfo -- 848 B.  The unit stride of 212
 // dwords puts consecutive units 20 banks apart (mod 32).
+// (the split walk's builds keep their plane's arrays only: every layout's unit stride stays
+// 20 banks mod 32)
+constexpr int YR = DOY ? 16 : 0, CR = DOC ? 8 : 0;   // luma / chroma rows held
 struct alignas(16) UnitLds {
-    uint32_t y[16][8];        // luma rows 0..15; MB x in slot s = x & 1: dwords 4s .. 4s+3
-    uint32_t c[2][8][4];      // chroma plane, rows 0..7; slot s = dwords 2s, 2s+1
+    uint32_t y[YR][8];        // luma rows 0..15; MB x in slot s = x & 1: dwords 4s .. 4s+3
+    uint32_t c[2][CR][4];     // chroma plane, rows 0..7; slot s = dwords 2s, 2s+1
     uint32_t info[20];        // DbInfo of the MB being filtered (zeros: no MB this step)
 };
-static_assert(sizeof(UnitLds) == 848, "UnitLds layout");
+static_assert(sizeof(UnitLds) == (PL == 2 ? 848 : PL == 0 ? 592 : 336), "UnitLds layout");
 
 // A unit's output staging: the final samples of its MB row, collected per group of 4 MBs, so
 // that the output planes take whole 64-byte pieces of their luma rows and 32-byte pieces of their
@@ -105,14 +108,14 @@ static_assert(sizeof(UnitLds) == 848, "UnitLds layout");
 // this unit's staging (same wave), or, for the band's first row, into the UpLds of its picture
 // (the row above is another wave's).  1.5 KiB per unit: 8 waves per CU at 8 lanes per unit.
 struct alignas(16) StageLds {
-    uint32_t y[16][4][4];      // luma rows 0..15, MB m & 3 of the 4-MB group: 16 bytes
-    uint32_t c[2][8][4][2];    // chroma plane, rows 0..7, MB m & 3: 8 bytes
+    uint32_t y[YR][4][4];      // luma rows 0..15, MB m & 3 of the 4-MB group: 16 bytes
+    uint32_t c[2][CR][4][2];   // chroma plane, rows 0..7, MB m & 3: 8 bytes
     uint32_t pad[20];          // unit stride 404 dwords (20 banks apart)
 };
-static_assert(sizeof(StageLds) == 1616, "StageLds layout");
+static_assert(sizeof(StageLds) == (PL == 2 ? 1616 : PL == 0 ? 1104 : 592), "StageLds layout");
 struct alignas(16) UpLds {     // the band's first row: rows 13..15 (chroma 7) of the row above
-    uint32_t yu[3][4][4];
-    uint32_t cu[2][4][2];
+    uint32_t yu[DOY ? 3 : 0][4][4];
+    uint32_t cu[2][DOC ? 4 : 0][2];
 };
 
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));   // native vectors: registers, not stack
@@ -186,7 +189,7 @@ extern "C" void h264r_db2_trace_copy(void* dst) { (void)hipMemcpyFromSymbol(dst,
 // picture: 20.2 KiB, 8 waves per CU at 8 lanes per unit); asking for 2 waves per SIMD keeps the
 // compiler from parking values in AGPRs (at a 512-register budget it did, and the wave's VGPR +
 // AGPR footprint of 257 left one wave per SIMD)
-#define H264R_DB2_WAVES_PER_EU (H264R_DB2_LPU == 8 ? 2 : 1)
+#define H264R_DB2_WAVES_PER_EU (H264R_DB2_PL == 1 ? 4 : H264R_DB2_PL == 0 ? 3 : H264R_DB2_LPU == 8 ? 2 : 1)   // split builds: 3 / 4
 extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(H264R_DB2_WAVES_PER_EU, H264R_DB2_WAVES_PER_EU))) void H264R_DB2_KERNEL(
     h264r_batch b, const DbInfo* __restrict__ dbinfo, uint64_t* hb, int* sync, int* err, uint32_t epoch, int2 rows, int nx,
     const uint8_t* __restrict__ recon)

@@ -621,14 +621,16 @@ def throughput_run(args, rank: int, world: int, local: int, cs, rehearse: bool, 
     # per-kernel split of the same 8(d) bytes (kernel_bytes: R to the reconstructing kernel,
     # W to deblocking; the parts add up to the path's bytes), over each kernel's own event time
     kbytes = [int(k * (band[1] - band[0]) / H) for k in kbytes_all]
-    # the library deblocks launches of >= H264R_DEBLOCK2_MIN (default 8) x 68 picture-MB-rows
-    # with k_deblock2, smaller ones with k_deblock (include/h264r.h)
-    dbk = ("k_deblock2" if npics * (band[1] - band[0]) >= int(os.environ.get("H264R_DEBLOCK2_MIN", "8")) * 68
-           else "k_deblock")
+    # the library deblocks launches of fewer than H264R_DB2S_MAX (default 512) x 68 picture-MB-rows
+    # with the split walk (k_deblock2y + k_deblock2c), larger ones with k_deblock2 (h264r_host.hip)
+    prow = npics * (band[1] - band[0])
+    dbk_k = (["k_deblock2y", "k_deblock2c"] if prow < int(os.environ.get("H264R_DB2S_MAX", "512")) * 68
+             else ["k_deblock2"] if prow >= int(os.environ.get("H264R_DEBLOCK2_MIN", "8")) * 68 else ["k_deblock"])
+    dbk = " + ".join(dbk_k)
     inter_k = ["k_dbinfo", "k_inter4r"]
     names = [" + ".join(inter_k), "intra (k_level + k_intra_levels + k_intra_pic)", dbk]
     kern_names = [inter_k + ["k_inter_sp"], ["k_level", "k_level_scan", "k_level_scatter", "k_intra_levels", "k_intra_pic"],
-                  [dbk]]
+                  dbk_k]
     # HBM traffic per launch sequence from the PMC counters of the committed profile run
     # (tools/pmc.sh + tools/pmc_summary.py --json): per-MB FETCH_SIZE (doubled, gfx950) +
     # WRITE_SIZE of every kernel of the sequence, times the MBs this rank processed
