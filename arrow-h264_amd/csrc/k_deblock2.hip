@@ -56,6 +56,11 @@
 // Every memory operation is issued by every lane on every path, so the waitcnt pass can
 // count the operations younger than a load it waits for.
 //
+// The split walk (launches of few pictures, h264r_host.hip): the same source built per plane,
+// H264R_DB2_PL = 0 (k_deblock2y, luma) and 1 (k_deblock2c, chroma) -- the planes filter
+// independently, so each plane's walk runs as its own waves beside the other's, each with only
+// its plane's LDS arrays and hand-off pairs (luma pairs 0-1, chroma pair 2) and a shorter step.
+//
 // Sample ownership (each sample stored once, when final): a row stages MB x's rows
 // 0..12 (chroma 0..6) once MB x+1's vertical edges are done, and the rows 13..15
 // (chroma 7) of MB (x, y-1) after filtering its own top edge (into the upper unit's

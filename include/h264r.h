@@ -249,7 +249,10 @@ int  h264r_picture_wait(h264r_ctx* ctx, uint8_t* y, uint8_t* u, uint8_t* v);
  * kernel k_intra_levels is persistent and separates dependency levels with a grid
  * barrier sized from the occupancy query: kernels of OTHER contexts or libraries
  * running concurrently on the same device may delay it (every wait is bounded; an
- * expired wait is reported by h264r_check as H264R_EDEVICE, never silently). */
+ * expired wait is reported by h264r_check as H264R_EDEVICE, never silently).  It is
+ * launched plainly (H264R_COOP=1: a cooperative launch, whose runtime check refuses a grid
+ * that cannot be resident).  Launches deblocked by the split walk also use the context's
+ * side stream (joined back to the launch stream by an event before the call returns). */
 int  h264r_decode_batch(h264r_ctx* ctx, const h264r_batch* batch, void* stream);
 
 /* Slice-sharded form of h264r_decode_batch (multi-GPU): reconstruct and
@@ -270,7 +273,7 @@ int  h264r_ref_planes(h264r_ctx* ctx, int slot, uint8_t** y, uint8_t** u, uint8_
  * enabled, measured with HIP events on each launch's stream: out[0] the deblocking records
  * and the inter / I_PCM reconstruction (k_dbinfo + k_inter4r + k_inter_sp), out[1] the intra
  * kernels (k_level + k_level_scan + k_level_scatter + k_intra_levels + k_intra_pic), out[2]
- * deblocking (k_deblock / k_deblock2), out[3] the whole batch (the wall time of the launch
+ * deblocking (k_deblock2, or the split walk k_deblock2y + k_deblock2c), out[3] the whole batch (the wall time of the launch
  * sequence on the launch stream; under the overlapped schedule out[0..2] are busy times that
  * overlap).  Returns H264R_OK or an error. */
 int  h264r_last_timing(h264r_ctx* ctx, float out_ms[4]);
@@ -281,10 +284,12 @@ int  h264r_set_timing(h264r_ctx* ctx, int enable);
 /* H264R_DBG_INTRA_WALK reconstructs every intra MB with the wavefront walk instead of
  * the dependency-level schedule (both are bit-exact; this exercises the walk alone). */
 #define H264R_DBG_INTRA_WALK 2
-/* The loop filter has two schedules (both bit-exact): k_deblock spreads one MB over 32
- * lanes (short latency, small batches), k_deblock2 walks bands of 4 MB rows of 2 pictures
- * per wave, 8 lanes per (picture, row) (launches of >= H264R_DEBLOCK2_MIN x 68
- * picture-MB-rows, i.e. 8 whole 1080p pictures by default).  These flags force one of them. */
+/* The loop filter has three schedules (all bit-exact): k_deblock2 walks bands of 4 MB rows of
+ * 2 pictures per wave, 8 lanes per (picture, row) (launches of >= H264R_DB2S_MAX x 68
+ * picture-MB-rows, 512 1080p pictures by default); below that the split walk runs the luma
+ * and the chroma planes' band walks as separate waves (H264R_DBG_DEBLOCK_SPLIT); k_deblock
+ * spreads one MB over 32 lanes (with H264R_DB2S_MAX=0, launches below H264R_DEBLOCK2_MIN x 68
+ * picture-MB-rows).  These flags force one of them. */
 #define H264R_DBG_DEBLOCK_MB   4
 #define H264R_DBG_DEBLOCK_ROWS 8
 /* Both schedules keep a picture's (k_deblock) or a 2-picture group's (k_deblock2) rows on
