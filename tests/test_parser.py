@@ -189,9 +189,13 @@ def test_parser_malformed_streams_under_asan(tmp_path):
             for _ in range(int(rng.integers(1, 4))):
                 pos = int(rng.integers(4, min(len(data), 96))) if k % 2 == 0 else int(rng.integers(4, len(data)))
                 data[pos] ^= 1 << int(rng.integers(0, 8))
-            if k % 6 == 5:                    # an oversized ue(v): 31 zero bits in the first slice header
+            if k % 6 == 5:
+                # an oversized ue(v) in a parameter set or the first slice header: 32 (k % 12 == 5) or
+                # 40 zero bits then a one, i.e. RBSP 00 00 00 00 [00] 80 with its emulation-prevention
+                # bytes (an RBSP 00 00 0x with x <= 3 is sent as 00 00 03 0x), so that Bits::ue() sees
+                # 32+ leading zeros (values >= 2^31: ue_max / se_in reject them)
                 pos = int(rng.integers(8, 40))
-                data[pos:pos + 4] = b"\x00\x00\x00\x01"[:3] + b"\x80"
+                data[pos:pos + 4] = (b"\x00\x00\x03\x00\x00\x80" if k % 12 == 5 else b"\x00\x00\x03\x00\x00\x03\x00\x80")
             src = tmp_path / f"{name}_{k}.264"
             src.write_bytes(bytes(data))
             r = subprocess.run([asan, "-i", str(src), "-o", str(tmp_path / "o.yuv")], capture_output=True, text=True,
@@ -199,3 +203,24 @@ def test_parser_malformed_streams_under_asan(tmp_path):
             if "Sanitizer" in r.stderr or "runtime error" in r.stderr or r.returncode < 0:
                 bad.append((name, k, r.returncode, r.stderr[-1500:]))
     assert not bad, bad[0]
+
+
+def test_parser_oversized_ue_rejected_under_asan(tmp_path):
+    """ue(v) codes of 31, 32 and 40 leading zero bits (values from 2^31 - 1 up: past every int
+    field) reach Bits::ue() through emulation-prevention bytes in an SPS (seq_parameter_set_id),
+    and the ASan + UBSan build reports an error for each, with no sanitizer message."""
+    O.build_oracle()
+    subprocess.run(["make", "-s", "-C", os.path.join(S.ROOT, "oracle"), "asan"], check=True)
+    asan = os.path.join(S.ROOT, "oracle", "_cpu", "h264dec_cpu_asan")
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=0", UBSAN_OPTIONS="print_stacktrace=1")
+    head = b"\x00\x00\x00\x01\x67\x42\x00\x1e"          # start code, SPS NAL, Baseline, level 3.0
+    codes = {31: b"\x00\x00\x03\x00\x01\xff\xff\xff\xfe",     # RBSP 00 00 00 01 ff ff ff fe
+             32: b"\x00\x00\x03\x00\x00\x80",                  # RBSP 00 00 00 00 80
+             40: b"\x00\x00\x03\x00\x00\x03\x00\x80"}          # RBSP 00 00 00 00 00 80
+    for zeros, body in codes.items():
+        src = tmp_path / f"ue{zeros}.264"
+        src.write_bytes(head + body)
+        r = subprocess.run([asan, "-i", str(src), "-o", str(tmp_path / "o.yuv")], capture_output=True, text=True,
+                           timeout=60, env=env)
+        assert "Sanitizer" not in r.stderr and "runtime error" not in r.stderr, r.stderr[-1500:]
+        assert r.returncode > 0 and "h264dec:" in r.stderr, (zeros, r.returncode, r.stderr[-500:])
