@@ -215,9 +215,11 @@ DEV void walk_ticket(const h264r_batch& b, int* sync, int* err, Scratch* scratch
 
 // lvl / lmax: intra MBs with lvl <= lmax were reconstructed by the k_intra_lvl
 // launches before this one (lvl == nullptr: the walk does every intra MB).
+// pdepth[pic] (k_level): the picture's deepest level, or INT_MAX for a picture left to the walk
+// whole -- a picture whose levels the lists covered has nothing here, and its tickets return.
 extern "C" __global__ __launch_bounds__(64 * H264R_WALK_ROWS, H264R_WALK_WAVES) void k_intra_pic(h264r_batch b, int* sync, int* err,
                                                               const uint16_t* lvl, int lmax, int2 rows, int gstep,
-                                                              uint8_t* recon)
+                                                              uint8_t* recon, const int* pdepth)
 {
     __shared__ IntraScratch scratch[WAVES];
     __shared__ uint32_t tap4[INTRA_TAPS];
@@ -225,6 +227,8 @@ extern "C" __global__ __launch_bounds__(64 * H264R_WALK_ROWS, H264R_WALK_WAVES) 
     __shared__ int ticket;
     if (threadIdx.x == 0) ticket = atomicAdd(&sync[0], 1);
     if (threadIdx.x < WAVES) lprog[threadIdx.x] = 0;
+    __syncthreads();
+    if (lvl && pdepth[ticket % b.num_pics] <= lmax) return;     // (block-uniform)
     intra4_tap_fill(tap4, threadIdx.x, blockDim.x);
     __syncthreads();
     walk_ticket(b, sync, err, scratch, tap4, lprog, ticket, lvl, lmax, rows, gstep, recon);
@@ -257,7 +261,7 @@ extern "C" __global__ __launch_bounds__(64 * H264R_WALK_ROWS, H264R_WALK_WAVES) 
 // the batch (zeroed per batch); k_level_scatter turns them into the lists.
 constexpr int LEVEL_LDS = 40960;            // (W + 2) x (rows + 1) level bytes (h264r_host.hip checks)
 extern "C" __global__ __launch_bounds__(1024) void k_level(h264r_batch b, uint16_t* lvl, int* lvsync, int* lcount, int2 rows,
-                                                          int deep_cut)
+                                                          int deep_cut, int* pdepth)
 {
     __shared__ uint64_t bits[H264R_LEVEL_MAX_MBS / 64];   // intra (not PCM) MBs of the picture
     __shared__ uint64_t pbits[H264R_LEVEL_MAX_MBS / 64];  // the pairable ones among them
@@ -345,8 +349,10 @@ extern "C" __global__ __launch_bounds__(1024) void k_level(h264r_batch b, uint16
     // its few MBs per level would only make k_intra_levels wait at its grid barriers
     if (deep || deepest > deep_cut) {
         for (int m = R0 * W + tid; m < rows.y * W; m += nt) lvl[(size_t)pic * g.nmb + m] = 0xFFFF;
+        if (tid == 0) pdepth[pic] = 0x7FFFFFFF;
         return;
     }
+    if (tid == 0) pdepth[pic] = deepest;
     if (tid == 0 && deepest) atomicMax(&lvsync[1], deepest);
     for (int i = tid + 2; i < LEVEL_IDS; i += nt)
         if (hist[i]) atomicAdd(&lcount[i], hist[i]);
