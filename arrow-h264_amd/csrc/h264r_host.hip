@@ -36,9 +36,9 @@ extern "C" __global__ void k_dbinfo(h264r_batch b, h264r::DbInfo* dbinfo, int2 r
 extern "C" __global__ void k_inter_sp(h264r_batch b, int2 rows, const int* sp_flag, uint8_t* recon);
 extern "C" __global__ void k_untile(h264r_batch b, int2 rows, const uint8_t* recon);
 extern "C" __global__ void k_intra_pic(h264r_batch b, int* sync, int* err, const uint16_t* lvl, int lmax, int2 rows,
-                                      int gstep, uint8_t* recon, const int* pdepth);
+                                      int gstep, uint8_t* recon, const int* pband);
 extern "C" __global__ void k_level(h264r_batch b, uint16_t* lvl, int* lvsync, int* lcount, int2 rows, int deep_cut,
-                                   int* pdepth);
+                                   int lmax, int* pband);
 extern "C" __global__ void k_level_scan(const int* lcount, int* lbase);
 extern "C" __global__ void k_level_scatter(h264r_batch b, const uint16_t* lvl, const int* lbase, int* lcursor,
                                            uint32_t* list, int2 rows);
@@ -498,7 +498,7 @@ static h264r_batch sub_batch(const h264r_batch& b, int p0, int n)
 // per-XCD ticket counters, done count, then per picture the waves of k_dbinfo that met an inter
 // or I_PCM MB (k_inter4r skips the pictures without one)
 // (two sets of deblocking counters: the split walk's luma and chroma kernels run together)
-// and per picture its deepest intra level (k_level -> k_intra_pic)
+// and per picture the walk's bands holding an MB deeper than the level lists (k_level -> k_intra_pic)
 static size_t sync_ints(int P, int H) { return 1 + (size_t)P * H + 5 + 18 + 2 * (size_t)P; }
 
 // One launch sequence's share of the scratch (the whole batch, or one chunk of the overlapped
@@ -550,7 +550,7 @@ static int recon_launches(h264r_ctx* c, const Stage& S, hipStream_t s, int2 rows
     {
         Timed t(c, 1, s);
         uint16_t* lvl = levels ? X.d_lvl : nullptr;
-        int* pdepth = sync + 1 + (size_t)P * H + 23 + P;       // after the inter flags
+        int* pband = sync + 1 + (size_t)P * H + 23 + P;        // after the inter flags
         const int lmax = levels ? level_launches() : 0;
         if (levels) {
             int* lvsync = sync + 1 + (size_t)P * H + 2;
@@ -558,7 +558,7 @@ static int recon_launches(h264r_ctx* c, const Stage& S, hipStream_t s, int2 rows
             int* lbase = lcount + LEVEL_IDS;
             int* lcursor = lbase + LEVEL_IDS;
             // pictures deeper than 4 x lmax levels (all-intra) are left to the walk whole
-            hipLaunchKernelGGL(k_level, dim3(P), dim3(1024), 0, s, b, lvl, lvsync, lcount, rows, 4 * lmax, pdepth);
+            hipLaunchKernelGGL(k_level, dim3(P), dim3(1024), 0, s, b, lvl, lvsync, lcount, rows, 4 * lmax, lmax, pband);
             HIP_OK(hipGetLastError());
             hipLaunchKernelGGL(k_level_scan, dim3(1), dim3(1024), 0, s, (const int*)lcount, lbase);
             HIP_OK(hipGetLastError());
@@ -594,7 +594,7 @@ static int recon_launches(h264r_ctx* c, const Stage& S, hipStream_t s, int2 rows
         // H264R_WALK_GSTEP overrides
         const int gstep = wait_test ? -1 : K.walk_gstep > 0 ? K.walk_gstep : (P >= 128 ? 64 : 1);
         hipLaunchKernelGGL(k_intra_pic, dim3(P * nbands), dim3(64 * H264R_WALK_ROWS), 0, s, b, sync, c->d_err,
-                           (const uint16_t*)lvl, lmax, rows, gstep, recon, (const int*)pdepth);
+                           (const uint16_t*)lvl, lmax, rows, gstep, recon, (const int*)pband);
         HIP_OK(hipGetLastError());
     }
     return H264R_OK;

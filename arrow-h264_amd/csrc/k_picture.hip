@@ -103,9 +103,11 @@ DEV bool wait_for(int* counter, int need, int* err, int& seen)
 
 // One (band, picture) ticket: wave `wave` walks MB row r0 + wave of the band.
 // sync: [0] ticket counter, [1 ..] per (picture, row) progress; zeroed before every launch.
+// pband[pic] (with lvl): bit b set when band b of the picture has an MB deeper than lmax
+// (k_level); a band without one needs no walk, and the band below it no wait.
 template <typename Scratch>
 DEV void walk_ticket(const h264r_batch& b, int* sync, int* err, Scratch* scratch, const uint32_t* tap4, int* lprog, int ticket,
-                     const uint16_t* __restrict__ lvl, int lmax, int2 rows, int gstep, uint8_t* recon)
+                     const uint16_t* __restrict__ lvl, int lmax, int2 rows, int gstep, uint8_t* recon, const int* pband)
 {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const Geom g = make_geom(b.width_mbs, b.height_mbs);
@@ -116,6 +118,8 @@ DEV void walk_ticket(const h264r_batch& b, int* sync, int* err, Scratch* scratch
     const int r0 = R0 + band * bh, r1 = min(R1, r0 + bh);
     const int r = r0 + wave;
     if (r >= r1) return;
+    // the band above has nothing deeper than the lists: its rows are final already
+    const bool above_done = lvl && band > 0 && !((pband[pic] >> (band - 1)) & 1);
     int* gprog = sync + 1 + (size_t)pic * g.hmb;
     const bool last_row = r == r1 - 1 && r1 < R1;
     Scratch& S = scratch[wave];
@@ -188,7 +192,7 @@ DEV void walk_ticket(const h264r_batch& b, int* sync, int* err, Scratch* scratch
 #ifdef H264R_TRACE_INTRA
         const unsigned long long t_wait0 = __builtin_amdgcn_s_memrealtime();
 #endif
-        if (r > R0 && need > seen) {
+        if (r > R0 && need > seen && !(wave == 0 && above_done)) {
             if (wave == 0) ok = wait_for<true>(&gprog[r - 1], need, err, seen);
             else ok = wait_for<false>(&lprog[wave - 1], need, err, seen);
         }
@@ -215,11 +219,11 @@ DEV void walk_ticket(const h264r_batch& b, int* sync, int* err, Scratch* scratch
 
 // lvl / lmax: intra MBs with lvl <= lmax were reconstructed by the k_intra_lvl
 // launches before this one (lvl == nullptr: the walk does every intra MB).
-// pdepth[pic] (k_level): the picture's deepest level, or INT_MAX for a picture left to the walk
-// whole -- a picture whose levels the lists covered has nothing here, and its tickets return.
+// pband[pic] (k_level): the picture's bands with an MB deeper than lmax (all for a picture left
+// to the walk whole) -- a band without one has nothing here, and its ticket returns.
 extern "C" __global__ __launch_bounds__(64 * H264R_WALK_ROWS, H264R_WALK_WAVES) void k_intra_pic(h264r_batch b, int* sync, int* err,
                                                               const uint16_t* lvl, int lmax, int2 rows, int gstep,
-                                                              uint8_t* recon, const int* pdepth)
+                                                              uint8_t* recon, const int* pband)
 {
     __shared__ IntraScratch scratch[WAVES];
     __shared__ uint32_t tap4[INTRA_TAPS];
@@ -228,10 +232,10 @@ extern "C" __global__ __launch_bounds__(64 * H264R_WALK_ROWS, H264R_WALK_WAVES) 
     if (threadIdx.x == 0) ticket = atomicAdd(&sync[0], 1);
     if (threadIdx.x < WAVES) lprog[threadIdx.x] = 0;
     __syncthreads();
-    if (lvl && pdepth[ticket % b.num_pics] <= lmax) return;     // (block-uniform)
+    if (lvl && !((pband[ticket % b.num_pics] >> (ticket / b.num_pics)) & 1)) return;     // (block-uniform)
     intra4_tap_fill(tap4, threadIdx.x, blockDim.x);
     __syncthreads();
-    walk_ticket(b, sync, err, scratch, tap4, lprog, ticket, lvl, lmax, rows, gstep, recon);
+    walk_ticket(b, sync, err, scratch, tap4, lprog, ticket, lvl, lmax, rows, gstep, recon, pband);
 }
 
 // ------------------------------------------------------------ level schedule
@@ -261,20 +265,22 @@ extern "C" __global__ __launch_bounds__(64 * H264R_WALK_ROWS, H264R_WALK_WAVES) 
 // the batch (zeroed per batch); k_level_scatter turns them into the lists.
 constexpr int LEVEL_LDS = 40960;            // (W + 2) x (rows + 1) level bytes (h264r_host.hip checks)
 extern "C" __global__ __launch_bounds__(1024) void k_level(h264r_batch b, uint16_t* lvl, int* lvsync, int* lcount, int2 rows,
-                                                          int deep_cut, int* pdepth)
+                                                          int deep_cut, int lmax, int* pband)
 {
     __shared__ uint64_t bits[H264R_LEVEL_MAX_MBS / 64];   // intra (not PCM) MBs of the picture
     __shared__ uint64_t pbits[H264R_LEVEL_MAX_MBS / 64];  // the pairable ones among them
     __shared__ uint8_t lv[LEVEL_LDS];                     // level of band row r, MB x at (r + 1) * (W + 2) + x + 1
     __shared__ int hist[LEVEL_IDS];
-    __shared__ int pdeep;
+    __shared__ int pdeep, sband;
     const Geom g = make_geom(b.width_mbs, b.height_mbs);
     const int pic = blockIdx.x, tid = threadIdx.x, lane = tid & 63, nt = (int)blockDim.x;
     const h264r_mb* mbs = b.mbs + (size_t)pic * g.nmb;
     const int R0 = rows.x, HB = rows.y - rows.x, W = g.wmb, P = W + 2, n = HB * W;   // rows above R0 count as level 0
     for (int i = tid; i < LEVEL_IDS; i += nt) hist[i] = 0;
     for (int i = tid; i < P * (HB + 1); i += nt) lv[i] = 0;
-    if (tid == 0) pdeep = 0;
+    if (tid == 0) { pdeep = 0; sband = 0; }
+    // the walk's bands (walk_ticket): bit b of pband for band b, all bits past 31 bands
+    const int wb = (HB + WAVES - 1) / WAVES, wbh = (HB + wb - 1) / wb;
     constexpr int UNR = 4;                                 // record loads in flight per thread
     for (int base = 0; base < n; base += UNR * nt) {
         uint32_t w0[UNR];
@@ -335,9 +341,11 @@ extern "C" __global__ __launch_bounds__(1024) void k_level(h264r_batch b, uint16
         uint16_t* out = lvl + (size_t)pic * g.nmb + (size_t)R0 * W;
         int r = r0, x = x0;
         for (int m = tid; m < n; m += nt) {
+            const int rr = r;                              // (lds_index steps r, x to the next MB)
             const int L = lv[lds_index(r, x)];
             out[m] = (uint16_t)L;
             deepest = max(deepest, L);
+            if (L > lmax) atomicOr(&sband, wb > 31 ? -1 : 1 << (rr / wbh));
             if (L >= 1 && L <= H264R_LEVEL_LISTS) atomicAdd(&hist[2 * L + !((pbits[m >> 6] >> (m & 63)) & 1)], 1);
         }
         for (int d = 32; d >= 1; d >>= 1) deepest = max(deepest, __shfl_xor(deepest, d));
@@ -349,10 +357,10 @@ extern "C" __global__ __launch_bounds__(1024) void k_level(h264r_batch b, uint16
     // its few MBs per level would only make k_intra_levels wait at its grid barriers
     if (deep || deepest > deep_cut) {
         for (int m = R0 * W + tid; m < rows.y * W; m += nt) lvl[(size_t)pic * g.nmb + m] = 0xFFFF;
-        if (tid == 0) pdepth[pic] = 0x7FFFFFFF;
+        if (tid == 0) pband[pic] = -1;
         return;
     }
-    if (tid == 0) pdepth[pic] = deepest;
+    if (tid == 0) pband[pic] = sband;
     if (tid == 0 && deepest) atomicMax(&lvsync[1], deepest);
     for (int i = tid + 2; i < LEVEL_IDS; i += nt)
         if (hist[i]) atomicAdd(&lcount[i], hist[i]);
