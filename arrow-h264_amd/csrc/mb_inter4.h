@@ -192,22 +192,30 @@ DEV void luma_window_global(const uint8_t* __restrict__ img, int W, int H, int x
     }
 }
 
-// The LDS reference-tile variant of round 3 (one 13-row tile per 8x8 quadrant by LDS-DMA,
-// measured slower: profiles/r03_e_ab.txt) is gone, but its never-taken branch stays in
-// inter4_mbs: without that branch the scheduler's regions change and k_inter4r spills 17
-// VGPRs at its 128-VGPR budget (measured with the round-4 compiler; an explicit
-// sched_barrier, a compiler memory barrier or a wave-uniform branch do not reproduce it).
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-struct alignas(16) QuadTile {
-    u32x4 slot[64];
-};
-
+// (The LDS reference-tile variant of round 3 -- one 13-row tile per 8x8 quadrant by LDS-DMA,
+// measured slower, profiles/r03_e_ab.txt -- is gone, and since round 5 so is its never-taken
+// branch, which had steered k_inter4r's register allocation: each output row is finished as
+// soon as its last tap row is in, so its accumulators are free for the rest of the window and
+// the kernel fits 128 VGPRs without it.)
 DEV void luma_block_pred(const uint32_t (&w)[9][3], int W, int x, int xf, int yf, uint32_t (&out)[4])
 {
     const int hs = xf == 3 ? 1 : 0;                  // G / h column c + 2 + hs
     const int brow = yf == 3 ? 1 : 0;                // b / G row i + 2 + brow
     const bool inside = x - 2 >= 0 && x + 6 < W;
     const int sh = (x - 2) & 3;
+    // output = (X + Y + 1) >> 1, X, Y in {0 G, 1 b, 2 h, 3 j}: (xs, ys) of the 16 phases as a
+    // 64-bit table (an if-chain on the lane's phase compiled to lane-divergent branches)
+    // XSYS nibble 4 xf + yf = xs | ys << 2:  xf 0: (0,0) (0,2) (2,2) (0,2); yf 0: (0,1) (1,1)
+    // (0,1); xf 2: (1,3) (3,3) (1,3); yf 2: (2,3); else (1,2)
+    constexpr uint64_t XSYS = 0x9e94dfd59e948a80ull;
+    const int xsys = (int)(XSYS >> (4 * (xf * 4 + yf))) & 15, xs = xsys & 3, ys = xsys >> 2;
+    // one of four by masks (a ternary chain became a branch tree)
+    const uint32_t mx1 = 0u - (uint32_t)(xs & 1), mx2 = 0u - (uint32_t)(xs >> 1);
+    const uint32_t my1 = 0u - (uint32_t)(ys & 1), my2 = 0u - (uint32_t)(ys >> 1);
+    auto pick = [](uint32_t m1, uint32_t m2, uint32_t a, uint32_t b, uint32_t c, uint32_t d) -> uint32_t {
+        const uint32_t lo = a ^ ((a ^ b) & m1), hi = c ^ ((c ^ d) & m1);
+        return lo ^ ((lo ^ hi) & m2);
+    };
     s16x2 hacc[4][2], bsv[4][2], gsv[4][2];
     int jacc[4][4];
 #pragma unroll
@@ -255,36 +263,24 @@ DEV void luma_block_pred(const uint32_t (&w)[9][3], int W, int x, int xf, int yf
                 gsv[i][1] = take ? g23 : gsv[i][1];
             }
         }
-    }
-    // output = (X + Y + 1) >> 1, X, Y in {0 G, 1 b, 2 h, 3 j}: (xs, ys) of the 16 phases as a
-    // 64-bit table (an if-chain on the lane's phase compiled to lane-divergent branches)
-    // XSYS nibble 4 xf + yf = xs | ys << 2:  xf 0: (0,0) (0,2) (2,2) (0,2); yf 0: (0,1) (1,1)
-    // (0,1); xf 2: (1,3) (3,3) (1,3); yf 2: (2,3); else (1,2)
-    constexpr uint64_t XSYS = 0x9e94dfd59e948a80ull;
-    const int xsys = (int)(XSYS >> (4 * (xf * 4 + yf))) & 15, xs = xsys & 3, ys = xsys >> 2;
-    // one of four by masks (a ternary chain became a branch tree)
-    const uint32_t mx1 = 0u - (uint32_t)(xs & 1), mx2 = 0u - (uint32_t)(xs >> 1);
-    const uint32_t my1 = 0u - (uint32_t)(ys & 1), my2 = 0u - (uint32_t)(ys >> 1);
-    auto pick = [](uint32_t m1, uint32_t m2, uint32_t a, uint32_t b, uint32_t c, uint32_t d) -> uint32_t {
-        const uint32_t lo = a ^ ((a ^ b) & m1), hi = c ^ ((c ^ d) & m1);
-        return lo ^ ((lo ^ hi) & m2);
-    };
+        // output row i has all its taps after row i + 5: finished here, its accumulators free
+        if (r >= 5) {
+            const int i = r - 5;
+            uint32_t o2[2];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        uint32_t o2[2];
-#pragma unroll
-        for (int h2 = 0; h2 < 2; ++h2) {
-            const s16x2 G = gsv[i][h2];
-            const s16x2 hh = pk_clip255((hacc[i][h2] + splat16(16)) >> splat16(5));
-            const s16x2 bb = pk_clip255((bsv[i][h2] + splat16(16)) >> splat16(5));
-            const int j0 = clip255((jacc[i][2 * h2] + 512) >> 10), j1 = clip255((jacc[i][2 * h2 + 1] + 512) >> 10);
-            // all four computed, then picked per lane (the phase differs between lanes)
-            const uint32_t g32 = as_u32(G), b32 = as_u32(bb), h32 = as_u32(hh), j32 = (uint32_t)j0 | ((uint32_t)j1 << 16);
-            const s16x2 X = as_s16x2(pick(mx1, mx2, g32, b32, h32, j32));
-            const s16x2 Y = as_s16x2(pick(my1, my2, g32, b32, h32, j32));
-            o2[h2] = as_u32((X + Y + splat16(1)) >> splat16(1));
+            for (int h2 = 0; h2 < 2; ++h2) {
+                const s16x2 G = gsv[i][h2];
+                const s16x2 hh = pk_clip255((hacc[i][h2] + splat16(16)) >> splat16(5));
+                const s16x2 bb = pk_clip255((bsv[i][h2] + splat16(16)) >> splat16(5));
+                const int j0 = clip255((jacc[i][2 * h2] + 512) >> 10), j1 = clip255((jacc[i][2 * h2 + 1] + 512) >> 10);
+                // all four computed, then picked per lane (the phase differs between lanes)
+                const uint32_t g32 = as_u32(G), b32 = as_u32(bb), h32 = as_u32(hh), j32 = (uint32_t)j0 | ((uint32_t)j1 << 16);
+                const s16x2 X = as_s16x2(pick(mx1, mx2, g32, b32, h32, j32));
+                const s16x2 Y = as_s16x2(pick(my1, my2, g32, b32, h32, j32));
+                o2[h2] = as_u32((X + Y + splat16(1)) >> splat16(1));
+            }
+            out[i] = __builtin_amdgcn_perm(o2[1], o2[0], 0x06040200u);
         }
-        out[i] = __builtin_amdgcn_perm(o2[1], o2[0], 0x06040200u);
     }
 }
 
@@ -553,7 +549,6 @@ template <bool SP>
 DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int aend, int lane,
                     const Inter4Lds& S, int* sp_flag, const Inter4Pre& pre, uint8_t* __restrict__ recon)
 {
-    QuadTile* __restrict__ tiles = nullptr;       // the dead tile branch's (luma_block_pred note)
     const int grp = lane >> 4, blk = lane & 15, bx = blk & 3, by = blk >> 2;
     const int a = a0 + grp;
     const bool valid = a < aend;
@@ -672,47 +667,10 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
             const int vx = X4 * 16 + mvx, vy = Y4 * 16 + mvy;           // quarter luma / eighth chroma units
             const int x = vx >> 2, y = vy >> 2;
             {
-                // quadrant tile (QuadTile): the four lanes of my 8x8 quadrant (blk ^ 1, ^ 4, ^ 5)
-                // predict from one slot with one vector, and the tile stays inside the picture
-                const uint32_t key = ok ? mw.x : 0xFFFFFFFFu;
-                const int skey = ok ? slot : -1;
-                const bool uni = ok && key == (uint32_t)__shfl_xor((int)key, 1) && key == (uint32_t)__shfl_xor((int)key, 4) &&
-                                 key == (uint32_t)__shfl_xor((int)key, 5) && skey == __shfl_xor(skey, 1) &&
-                                 skey == __shfl_xor(skey, 4) && skey == __shfl_xor(skey, 5);
-                const int xq = x - 4 * (bx & 1), yq = y - 4 * (by & 1);
-                const bool tile = false && uni && xq >= 0;
-                // tile row t * 4 + ql (row 12: t = 3, ql = 0) of a quadrant lands, by LDS-DMA, in
-                // the 16-byte slot of the quadrant's lane ql of its wave-instruction t
-                const int qbase = grp * 16 + (by & 2) * 4 + (bx & 2);          // lane of ql = 0
-                if (__any(tile)) {
-                    const int ql = (by & 1) * 2 + (bx & 1);
-                    const uint8_t* img = S.planes[(tile ? slot : 0) * 3] + ((xq - 2) & ~3);
-#pragma unroll
-                    for (int t = 0; t < 4; ++t)
-                        if (tile && (t < 3 || ql == 0))
-                            __builtin_amdgcn_global_load_lds(
-                                (const __attribute__((address_space(1))) void*)(img + (size_t)clip3(0, g.H - 1, yq - 2 + ql + 4 * t) * g.W),
-                                (__attribute__((address_space(3))) void*)(tiles + t), 16, 0, 0);
-                    __builtin_amdgcn_s_waitcnt(0x0F70);                       // vmcnt(0): this wave's tiles landed
-                    __builtin_amdgcn_wave_barrier();
-                }
-                // the 9 window rows: tile rows (by & 1) * 4 + r from dword (bx & 1), or the
-                // lane's own rows of the plane -- one generic (flat) load per row either way
+                // the 9 window rows of the lane's own block, straight from the plane
                 uint32_t w[9][3];
-                if (tile) {
-                    const uint32_t* tb = reinterpret_cast<const uint32_t*>(tiles) + (bx & 1);
-#pragma unroll
-                    for (int r = 0; r < 9; ++r) {
-                        const int jr = (by & 1) * 4 + r;                        // tile row
-                        const int src = qbase + ((jr & 2) << 1) + (jr & 1);    // lane that fetched it
-                        const uint32_t* q = tb + (jr >> 2) * 256 + src * 4;
-                        w[r][0] = q[0]; w[r][1] = q[1]; w[r][2] = q[2];
-                    }
-                } else if (ok) {
-                    luma_window_global(S.planes[slot * 3], g.W, g.H, x, y, w);
-                }
+                if (ok) luma_window_global(S.planes[slot * 3], g.W, g.H, x, y, w);
                 if (ok) luma_block_pred(w, g.W, x, vx & 3, vy & 3, tY);
-                if (__any(tile)) wave_sync();                      // read before the next list's tiles
             }
             if (ok) chroma_block_pred2(S.planes[slot * 3 + 1], S.planes[slot * 3 + 2], g.Wc, g.Hc, vx >> 3, vy >> 3, vx & 7, vy & 7, tC);
             const bool l1 = l != 0;
