@@ -39,11 +39,10 @@ extern "C" __global__ void k_intra_pic(h264r_batch b, int* sync, int* err, const
                                       int gstep, uint8_t* recon, const int* pband);
 extern "C" __global__ void k_level(h264r_batch b, uint16_t* lvl, int* lvsync, int* lcount, int2 rows, int deep_cut,
                                    int lmax, int* pband);
-extern "C" __global__ void k_level_scan(const int* lcount, int* lbase);
-extern "C" __global__ void k_level_scatter(h264r_batch b, const uint16_t* lvl, const int* lbase, int* lcursor,
+extern "C" __global__ void k_level_scatter(h264r_batch b, const uint16_t* lvl, const int* lcount, int* lbase, int* lcursor,
                                            uint32_t* list, int2 rows);
 extern "C" __global__ void k_intra_levels(h264r_batch b, const int* lcount, const int* lbase, const uint32_t* list,
-                                          int lmax, int* lvsync, int* err, uint8_t* recon);
+                                          int lmax, int* lvsync, int* err, uint8_t* recon, int* bar);
 constexpr int LEVEL_MAX_MBS = 65536;      // k_level's LDS bitmap (k_picture.hip)
 constexpr int LEVEL_LDS = 40960;          // k_level's LDS level bytes: (W + 2) x (rows + 1) (k_picture.hip)
 constexpr int LEVEL_LISTS = 64;           // levels with MB lists (H264R_LEVEL_LISTS, k_picture.hip)
@@ -463,7 +462,7 @@ struct Timed {
 };
 
 // Intra MBs are scheduled by dependency level: k_level computes every MB's level and
-// counts them, k_level_scan + k_level_scatter build one MB list per level, and
+// counts them, k_level_scatter builds one MB list per level, and
 // k_intra_levels does levels 1..N from those lists in one persistent cooperative launch
 // (a grid barrier between levels); the wavefront walk k_intra_pic takes whatever lies
 // deeper.  N = 16 by default: P / B pictures rarely go deeper, and in all-intra pictures
@@ -499,7 +498,8 @@ static h264r_batch sub_batch(const h264r_batch& b, int p0, int n)
 // or I_PCM MB (k_inter4r skips the pictures without one)
 // (two sets of deblocking counters: the split walk's luma and chroma kernels run together)
 // and per picture the walk's bands holding an MB deeper than the level lists (k_level -> k_intra_pic)
-static size_t sync_ints(int P, int H) { return 1 + (size_t)P * H + 5 + 18 + 2 * (size_t)P; }
+// (and, before the inter flags, k_intra_levels' sharded grid barrier: 8 shard counters + top)
+static size_t sync_ints(int P, int H) { return 1 + (size_t)P * H + 5 + 18 + 9 + 2 * (size_t)P; }
 
 // One launch sequence's share of the scratch (the whole batch, or one chunk of the overlapped
 // schedule): its pictures, their deblocking records and MB-tiled reconstruction, its sync region.
@@ -511,7 +511,7 @@ struct Stage {
 };
 
 // The reconstruction of a stage on stream s: k_dbinfo + k_inter4r + k_inter_sp (inter / PCM MBs
-// and the deblocking records), k_level + k_level_scan + k_level_scatter + k_intra_levels +
+// and the deblocking records), k_level + k_level_scatter + k_intra_levels +
 // k_intra_pic (intra MBs).  The level lists are one set: stages on one stream reuse them in order.
 static int recon_launches(h264r_ctx* c, const Stage& S, hipStream_t s, int2 rows, Scratch& X, bool levels, bool coop)
 {
@@ -535,10 +535,10 @@ static int recon_launches(h264r_ctx* c, const Stage& S, hipStream_t s, int2 rows
         int* sp_flag = sync + 1 + (size_t)P * H + 4;
         // the deblocking records first (k_inter4r then fits 4 waves/SIMD), with per picture
         // a flag that an inter or I_PCM MB was met (profiles/r03_f_dbinfo_ab.txt, r03_h_inter_ab.txt)
-        int* inter_cnt = sync + 1 + (size_t)P * H + 23;
+        int* inter_cnt = sync + 1 + (size_t)P * H + 32;
         // k_dbinfo zeroes the stage's sync words before the flags and the level counters
         if (++X.tag <= 0) X.tag = 1;
-        hipLaunchKernelGGL(k_dbinfo, dgrid, dim3(256), 0, s, b, S.dbinfo, rows, inter_cnt, X.tag, sync, (int)(1 + (size_t)P * H + 23),
+        hipLaunchKernelGGL(k_dbinfo, dgrid, dim3(256), 0, s, b, S.dbinfo, rows, inter_cnt, X.tag, sync, (int)(1 + (size_t)P * H + 32),
                            levels ? X.d_lcnt : nullptr, levels ? 3 * LEVEL_IDS : 0, dper);
         HIP_OK(hipGetLastError());
         hipLaunchKernelGGL(k_inter4r, igrid, dim3(256), 0, s, b, S.dbinfo, rows, sp_flag, recon, (const int*)inter_cnt, X.tag);
@@ -550,7 +550,8 @@ static int recon_launches(h264r_ctx* c, const Stage& S, hipStream_t s, int2 rows
     {
         Timed t(c, 1, s);
         uint16_t* lvl = levels ? X.d_lvl : nullptr;
-        int* pband = sync + 1 + (size_t)P * H + 23 + P;        // after the inter flags
+        int* pband = sync + 1 + (size_t)P * H + 32 + P;        // after the inter flags
+        int* lbar = sync + 1 + (size_t)P * H + 23;               // k_intra_levels' barrier (9 ints)
         const int lmax = levels ? level_launches() : 0;
         if (levels) {
             int* lvsync = sync + 1 + (size_t)P * H + 2;
@@ -560,9 +561,7 @@ static int recon_launches(h264r_ctx* c, const Stage& S, hipStream_t s, int2 rows
             // pictures deeper than 4 x lmax levels (all-intra) are left to the walk whole
             hipLaunchKernelGGL(k_level, dim3(P), dim3(1024), 0, s, b, lvl, lvsync, lcount, rows, 4 * lmax, lmax, pband);
             HIP_OK(hipGetLastError());
-            hipLaunchKernelGGL(k_level_scan, dim3(1), dim3(1024), 0, s, (const int*)lcount, lbase);
-            HIP_OK(hipGetLastError());
-            hipLaunchKernelGGL(k_level_scatter, dim3(P), dim3(1024), 0, s, b, (const uint16_t*)lvl, (const int*)lbase,
+            hipLaunchKernelGGL(k_level_scatter, dim3(P), dim3(1024), 0, s, b, (const uint16_t*)lvl, (const int*)lcount, lbase,
                                lcursor, X.d_list, rows);
             HIP_OK(hipGetLastError());
             // the grid one block per CU below the occupancy answer, all resident at once (the grid
@@ -581,12 +580,12 @@ static int recon_launches(h264r_ctx* c, const Stage& S, hipStream_t s, int2 rows
                 int* err_p = c->d_err;
                 h264r_batch bv = b;
                 void* args[] = {(void*)&bv, (void*)&lcount_c, (void*)&lbase_c, (void*)&list_c, (void*)&lmax_v,
-                                (void*)&lvsync, (void*)&err_p, (void*)&recon};
+                                (void*)&lvsync, (void*)&err_p, (void*)&recon, (void*)&lbar};
                 HIP_OK(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(k_intra_levels), dim3(lgrid),
                                                   dim3(256), args, 0, s));
             } else {
                 hipLaunchKernelGGL(k_intra_levels, dim3(lgrid), dim3(256), 0, s, b, (const int*)lcount,
-                                   (const int*)lbase, (const uint32_t*)X.d_list, lmax, lvsync, c->d_err, recon);
+                                   (const int*)lbase, (const uint32_t*)X.d_list, lmax, lvsync, c->d_err, recon, lbar);
                 HIP_OK(hipGetLastError());
             }
         }

@@ -366,53 +366,50 @@ extern "C" __global__ __launch_bounds__(1024) void k_level(h264r_batch b, uint16
         if (hist[i]) atomicAdd(&lcount[i], hist[i]);
 }
 
-// The per-level MB lists: lbase[L] = exclusive prefix of lcount over levels (one
-// workgroup, k_level_scan), then every intra MB of level 1 .. H264R_LEVEL_LISTS appends
+// The per-level MB lists: lbase[L] = exclusive prefix of lcount over levels (each
+// k_level_scatter workgroup scans them itself), then every intra MB of level 1 .. H264R_LEVEL_LISTS appends
 // pic * nmb + addr to its level's list (k_level_scatter: a workgroup counts its MBs per
 // level in LDS and reserves each level's range with one global atomic).
 // lcount, lbase, lcursor: LEVEL_IDS ints each.
-extern "C" __global__ __launch_bounds__(1024) void k_level_scan(const int* lcount, int* lbase)
-{
-    __shared__ int part[1024];
-    constexpr int PER = (LEVEL_IDS + 1023) / 1024;
-    const int t = threadIdx.x;
-    int v[PER], sum = 0;
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {
-        const int i = t * PER + k;
-        v[k] = i < LEVEL_IDS ? lcount[i] : 0;
-        sum += v[k];
-    }
-    part[t] = sum;
-    __syncthreads();
-    for (int o = 1; o < 1024; o <<= 1) {                  // inclusive scan of the per-thread sums
-        const int add = t >= o ? part[t - o] : 0;
-        __syncthreads();
-        part[t] += add;
-        __syncthreads();
-    }
-    int run = part[t] - sum;
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {
-        const int i = t * PER + k;
-        if (i < LEVEL_IDS) lbase[i] = run;
-        run += v[k];
-    }
-}
-
 // One workgroup per picture: an LDS count per level over the picture's MBs, one global
 // atomic per (picture, level) to reserve its range, then the entries (a workgroup per
 // 256 MBs reserved per (workgroup, level) instead: 130 k atomics on a few counters,
 // 375 us per 1024 1080p pictures).
 constexpr int SCATTER_PER = 16;             // MBs per thread (1024 threads: pictures up to 16 k MBs per pass)
+// Every workgroup first scans the level counts itself (one wave, 3 ids a lane; workgroup 0
+// stores the bases for k_intra_levels): a separate one-workgroup scan launch cost more.
 extern "C" __global__ __launch_bounds__(1024) void k_level_scatter(h264r_batch b, const uint16_t* __restrict__ lvl,
-                                                                   const int* __restrict__ lbase, int* lcursor,
+                                                                   const int* __restrict__ lcount, int* lbase, int* lcursor,
                                                                    uint32_t* __restrict__ list, int2 rows)
 {
+    static_assert(LEVEL_IDS <= 3 * 64, "one wave scans the level counts");
     __shared__ int cnt[LEVEL_IDS];
     __shared__ int res[LEVEL_IDS];
+    __shared__ int sbase[LEVEL_IDS];
     const Geom g = make_geom(b.width_mbs, b.height_mbs);
     const int pic = blockIdx.x, tid = threadIdx.x;
+    if (tid < 64) {
+        int v[3], sum = 0;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            v[k] = 3 * tid + k < LEVEL_IDS ? lcount[3 * tid + k] : 0;
+            sum += v[k];
+        }
+        int inc = sum;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int up = __shfl_up(inc, o, 64);
+            if (tid >= o) inc += up;
+        }
+        int run = inc - sum;
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+            if (3 * tid + k < LEVEL_IDS) {
+                sbase[3 * tid + k] = run;
+                if (pic == 0) lbase[3 * tid + k] = run;
+                run += v[k];
+            }
+    }
     const int m0 = rows.x * g.wmb, m1 = rows.y * g.wmb;
     const uint16_t* lp = lvl + (size_t)pic * g.nmb;
     const h264r_mb* mbs = b.mbs + (size_t)pic * g.nmb;
@@ -436,7 +433,7 @@ extern "C" __global__ __launch_bounds__(1024) void k_level_scatter(h264r_batch b
         __syncthreads();
 #pragma unroll
         for (int k = 0; k < SCATTER_PER; ++k)
-            if (L[k]) list[lbase[L[k]] + res[L[k]] + rank[k]] = (uint32_t)((size_t)pic * g.nmb + base + k * 1024 + tid);
+            if (L[k]) list[sbase[L[k]] + res[L[k]] + rank[k]] = (uint32_t)((size_t)pic * g.nmb + base + k * 1024 + tid);
         __syncthreads();
     }
 }
@@ -445,22 +442,30 @@ extern "C" __global__ __launch_bounds__(1024) void k_level_scatter(h264r_batch b
 // after the other inside one persistent launch (a launch per level would pay a cold
 // instruction cache on every CU each time).  Every workgroup must be resident: the
 // host sizes the grid from the occupancy query.  Levels are separated by a grid
-// barrier (MI355X_MICROARCH.md price list 'barrier-counter': stores drained, agent
-// release, one counter, agent acquire).  Each wave scans 64 MBs at a time,
-// grid-stride, and reconstructs the ones at the current level one after the other.
-// lvsync: [0] barrier counter, [1] deepest level (k_level), both zeroed per batch.
-DEV bool grid_barrier(int* bar, int target, int* err)
+// barrier: stores drained, agent release, then an arrival on one of 8 shard counters
+// (workgroup b on shard b % 8, the XCD it was dispatched to); a shard's last arrival adds
+// to the top counter (after an acquire-release fence: it carries its shard's releases)
+// and every workgroup waits on the top counter, then acquires.  One counter for all the
+// ~1000 arrivals had serialised them (MI355X_MICROARCH.md price list 'barrier-counter' vs
+// 'barrier-xcd', 'fanin').  Each wave takes its level's items grid-stride.
+// bar: [0..7] shard counters, [8] top counter, zeroed per batch (by k_dbinfo); L = 1, 2, ...
+DEV bool grid_barrier(int* bar, int L, int* err)
 {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     __shared__ int ok;
     if (threadIdx.x == 0) {
+        const int G = (int)gridDim.x, sh = (int)blockIdx.x & 7;
+        const int nsh = (G - sh + 7) / 8, nshards = min(G, 8);           // workgroups of my shard; shards
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_fetch_add(bar, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (__hip_atomic_fetch_add(&bar[sh], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == L * nsh - 1) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
+            __hip_atomic_fetch_add(&bar[8], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         WaitClock wc;
         ok = 1;
-        while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        while (__hip_atomic_load(&bar[8], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < L * nshards) {
             __builtin_amdgcn_s_sleep(2);
             if (wait_give_up(err, wc)) { ok = 0; break; }
         }
@@ -484,7 +489,8 @@ extern "C" __global__ void k_intra_trace_dump(unsigned long long* out, unsigned*
 extern "C" __global__ __launch_bounds__(256, H264R_LVL_WAVES) void k_intra_levels(h264r_batch b, const int* __restrict__ lcount,
                                                                                 const int* __restrict__ lbase,
                                                                                 const uint32_t* __restrict__ list,
-                                                                                int lmax, int* lvsync, int* err, uint8_t* recon)
+                                                                                int lmax, int* lvsync, int* err, uint8_t* recon,
+                                                                                int* bar)
 {
     __shared__ IntraScratch scratch[H264R_INTRA_PAIRS ? 8 : 4];
     __shared__ uint32_t tap4[INTRA_TAPS];
@@ -538,6 +544,6 @@ extern "C" __global__ __launch_bounds__(256, H264R_LVL_WAVES) void k_intra_level
             intra_mb2(b, g, pic, a % g.wmb, a / g.wmb, ln, scratch[wave], tap4, recon);
 #endif
         }
-        if (L < top && !grid_barrier(&lvsync[0], L * (int)gridDim.x, err)) return;
+        if (L < top && !grid_barrier(bar, L, err)) return;
     }
 }

@@ -629,7 +629,7 @@ def throughput_run(args, rank: int, world: int, local: int, cs, rehearse: bool, 
     dbk = " + ".join(dbk_k)
     inter_k = ["k_dbinfo", "k_inter4r"]
     names = [" + ".join(inter_k), "intra (k_level + k_intra_levels + k_intra_pic)", dbk]
-    kern_names = [inter_k + ["k_inter_sp"], ["k_level", "k_level_scan", "k_level_scatter", "k_intra_levels", "k_intra_pic"],
+    kern_names = [inter_k + ["k_inter_sp"], ["k_level", "k_level_scatter", "k_intra_levels", "k_intra_pic"],
                   dbk_k]
     # HBM traffic per launch sequence from the PMC counters of the committed profile run
     # (tools/pmc.sh + tools/pmc_summary.py --json): per-MB FETCH_SIZE (doubled, gfx950) +
