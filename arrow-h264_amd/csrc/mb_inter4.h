@@ -155,6 +155,7 @@ DEV int sel16(uint32_t lo, uint32_t hi, int c) { return (int16_t)(((c & 2) ? hi 
 
 // ---------------------------------------------------------------- packed 16-bit helpers
 typedef short s16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 DEV s16x2 as_s16x2(uint32_t v) { return __builtin_bit_cast(s16x2, v); }
 DEV uint32_t as_u32(s16x2 v) { return __builtin_bit_cast(uint32_t, v); }
 DEV s16x2 splat16(short v) { return (s16x2){v, v}; }
@@ -217,13 +218,16 @@ DEV void luma_block_pred(const uint32_t (&w)[9][3], int W, int x, int xf, int yf
         return lo ^ ((lo ^ hi) & m2);
     };
     s16x2 hacc[4][2], bsv[4][2], gsv[4][2];
-    int jacc[4][4];
+    // the centre j's vertical 6-tap over b1 (|sum| < 2^20) in packed fp32, exact below 2^24:
+    // two columns per v_pk_fma_f32 instead of one 32-bit multiply-add each
+    f32x2 jacc[4][2];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
 #pragma unroll
-        for (int h2 = 0; h2 < 2; ++h2) hacc[i][h2] = bsv[i][h2] = gsv[i][h2] = splat16(0);
-#pragma unroll
-        for (int c = 0; c < 4; ++c) jacc[i][c] = 0;
+        for (int h2 = 0; h2 < 2; ++h2) {
+            hacc[i][h2] = bsv[i][h2] = gsv[i][h2] = splat16(0);
+            jacc[i][h2] = (f32x2){0.f, 0.f};
+        }
     }
     constexpr short C6[6] = {1, -5, 20, 20, -5, 1};
 #pragma unroll
@@ -246,7 +250,7 @@ DEV void luma_block_pred(const uint32_t (&w)[9][3], int W, int x, int xf, int yf
         const s16x2 b01 = (q0 + q5) + splat16(20) * (q2 + q3) - splat16(5) * (q1 + q4);   // b1 cols 0,1
         const s16x2 b23 = (q2 + q7) + splat16(20) * (q4 + q5) - splat16(5) * (q3 + q6);   // b1 cols 2,3
         const s16x2 g01 = hs ? q3 : q2, g23 = hs ? q5 : q4;                                // G column pairs
-        const int bc[4] = {(int)b01.x, (int)b01.y, (int)b23.x, (int)b23.y};
+        const f32x2 bf[2] = {(f32x2){(float)b01.x, (float)b01.y}, (f32x2){(float)b23.x, (float)b23.y}};
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int k = r - i;                       // tap index of row r for output row i
@@ -254,7 +258,8 @@ DEV void luma_block_pred(const uint32_t (&w)[9][3], int W, int x, int xf, int yf
             hacc[i][0] += splat16(C6[k]) * g01;
             hacc[i][1] += splat16(C6[k]) * g23;
 #pragma unroll
-            for (int c = 0; c < 4; ++c) jacc[i][c] += C6[k] * bc[c];
+            for (int h2 = 0; h2 < 2; ++h2)
+                jacc[i][h2] = __builtin_elementwise_fma((f32x2){(float)C6[k], (float)C6[k]}, bf[h2], jacc[i][h2]);
             if (k == 2 || k == 3) {                    // b / G of output row i: row i + 2 + brow
                 const bool take = k == 2 + brow;
                 bsv[i][0] = take ? b01 : bsv[i][0];
@@ -272,7 +277,10 @@ DEV void luma_block_pred(const uint32_t (&w)[9][3], int W, int x, int xf, int yf
                 const s16x2 G = gsv[i][h2];
                 const s16x2 hh = pk_clip255((hacc[i][h2] + splat16(16)) >> splat16(5));
                 const s16x2 bb = pk_clip255((bsv[i][h2] + splat16(16)) >> splat16(5));
-                const int j0 = clip255((jacc[i][2 * h2] + 512) >> 10), j1 = clip255((jacc[i][2 * h2 + 1] + 512) >> 10);
+                // (j1 + 512) >> 10 clipped: j1 / 1024 + 0.5 is exact, and truncation equals the
+                // floor wherever the clip does not send the value to 0 anyway
+                const f32x2 jf = __builtin_elementwise_fma(jacc[i][h2], (f32x2){1.f / 1024.f, 1.f / 1024.f}, (f32x2){0.5f, 0.5f});
+                const int j0 = (int)__builtin_amdgcn_fmed3f(jf.x, 0.f, 255.f), j1 = (int)__builtin_amdgcn_fmed3f(jf.y, 0.f, 255.f);
                 // all four computed, then picked per lane (the phase differs between lanes)
                 const uint32_t g32 = as_u32(G), b32 = as_u32(bb), h32 = as_u32(hh), j32 = (uint32_t)j0 | ((uint32_t)j1 << 16);
                 const s16x2 X = as_s16x2(pick(mx1, mx2, g32, b32, h32, j32));
