@@ -16,8 +16,11 @@
 // whatever the dispatch order or residency.  Every wait is bounded.
 #include "mb_intra.h"
 
+// k_intra_levels' register budget: 6 waves/SIMD = 80 VGPRs, no spill (LDS allows 7; at the
+// default budget it took 82 = 5 waves: config 3 intra 1.235 -> 1.21 ms, configs 4 / 5 within
+// noise, profiles/r05_at_level_waves_ab.txt)
 #ifndef H264R_LVL_WAVES
-#define H264R_LVL_WAVES 4
+#define H264R_LVL_WAVES 6
 #endif
 #define H264R_LEVEL_MAX_MBS 65536           // k_level keeps a picture's intra bitmap in LDS
 #define H264R_LEVEL_LISTS 64                // levels 1 .. this many get per-level MB lists
