@@ -246,6 +246,16 @@ DEV int quad_bcast(int v)       // value of lane K of this lane's quad
     return __builtin_amdgcn_update_dpp(0, v, K * 0x55, 0xF, 0xF, false);
 }
 
+// The value of lane ^ 1 / lane ^ 4 (inside the lane's 16-lane row) by DPP moves: a VALU op or
+// two instead of a ds_bpermute round trip through the LDS crossbar.  lane ^ 4: banks 1, 3 take
+// row_shr:4 (lane - 4), banks 0, 2 row_shl:4 (lane + 4).
+DEV int lane_xor1(int v) { return __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false); }   // quad_perm [1,0,3,2]
+DEV int lane_xor4(int v)
+{
+    const int t = __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xA, false);
+    return __builtin_amdgcn_update_dpp(t, v, 0x104, 0xF, 0x5, false);
+}
+
 // Column pass of inverse_4x4 (transform.cc:619-640) for the lane holding row r of
 // the block: t[k] = row k's value in this column.  Returns ((o_r + 32) >> 6).
 DEV int idct4_col_row(int t0, int t1, int t2, int t3, int r)

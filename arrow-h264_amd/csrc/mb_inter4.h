@@ -765,7 +765,7 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
                 int t[2][2];
     #pragma unroll
                 for (int r = 0; r < 2; ++r) {
-                    const int o0 = __shfl_xor(pr[r][0], 1), o1 = __shfl_xor(pr[r][1], 1);
+                    const int o0 = lane_xor1(pr[r][0]), o1 = lane_xor1(pr[r][1]);
                     const int q0 = cc ? o0 : pr[r][0], q1 = cc ? o1 : pr[r][1], q2 = cc ? pr[r][0] : o0, q3 = cc ? pr[r][1] : o1;
                     int y0, y1, y2, y3;
                     fwd4(q0, q1, q2, q3, y0, y1, y2, y3);
@@ -774,7 +774,7 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
                 }
     #pragma unroll
                 for (int c = 0; c < 2; ++c) {
-                    const int o0 = __shfl_xor(t[0][c], 4), o1 = __shfl_xor(t[1][c], 4);
+                    const int o0 = lane_xor4(t[0][c]), o1 = lane_xor4(t[1][c]);
                     const int q0 = cr ? o0 : t[0][c], q1 = cr ? o1 : t[1][c], q2 = cr ? t[0][c] : o0, q3 = cr ? t[1][c] : o1;
                     int y0, y1, y2, y3;
                     fwd4(q0, q1, q2, q3, y0, y1, y2, y3);
@@ -833,7 +833,7 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
                     int tt[2][2];
     #pragma unroll
                     for (int r = 0; r < 2; ++r) {
-                        const int o0 = __shfl_xor(k[r][0], 1), o1 = __shfl_xor(k[r][1], 1);
+                        const int o0 = lane_xor1(k[r][0]), o1 = lane_xor1(k[r][1]);
                         const int d0 = cc ? o0 : k[r][0], d1 = cc ? o1 : k[r][1], d2 = cc ? k[r][0] : o0, d3 = cc ? k[r][1] : o1;
                         int y0, y1, y2, y3;
                         idct4(d0, d1, d2, d3, y0, y1, y2, y3);
@@ -842,7 +842,7 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
                     }
     #pragma unroll
                     for (int c = 0; c < 2; ++c) {
-                        const int o0 = __shfl_xor(tt[0][c], 4), o1 = __shfl_xor(tt[1][c], 4);
+                        const int o0 = lane_xor4(tt[0][c]), o1 = lane_xor4(tt[1][c]);
                         const int d0 = cr ? o0 : tt[0][c], d1 = cr ? o1 : tt[1][c], d2 = cr ? tt[0][c] : o0, d3 = cr ? tt[1][c] : o1;
                         int y0, y1, y2, y3;
                         idct4(d0, d1, d2, d3, y0, y1, y2, y3);
@@ -907,13 +907,13 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
                 // 8x8: the quadrant above (lane ^ 4) / to the left (lane ^ 1) carries in
     #pragma unroll
                 for (int c = 0; c < 4; ++c) {
-                    const int up = __shfl_xor(d[3][c], 4);
+                    const int up = lane_xor4(d[3][c]);
     #pragma unroll
                     for (int i = 0; i < 4; ++i) d[i][c] += (t8 && vert && (by & 1)) ? up : 0;
                 }
     #pragma unroll
                 for (int i = 0; i < 4; ++i) {
-                    const int left = __shfl_xor(d[i][3], 1);
+                    const int left = lane_xor1(d[i][3]);
     #pragma unroll
                     for (int c = 0; c < 4; ++c) d[i][c] += (t8 && horz && (bx & 1)) ? left : 0;
                 }
@@ -941,7 +941,7 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
                     int in[8], outv[8];
     #pragma unroll
                     for (int c = 0; c < 4; ++c) {
-                        const int ov = __shfl_xor(d[i][c], 1);
+                        const int ov = lane_xor1(d[i][c]);
                         in[c] = (bx & 1) ? ov : d[i][c];
                         in[4 + c] = (bx & 1) ? d[i][c] : ov;
                     }
@@ -957,7 +957,7 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
                     int in[8], outv[8];
     #pragma unroll
                     for (int i = 0; i < 4; ++i) {
-                        const int ov = __shfl_xor(e4[i][c], 4);
+                        const int ov = lane_xor4(e4[i][c]);
                         in[i] = (by & 1) ? ov : e4[i][c];
                         in[4 + i] = (by & 1) ? e4[i][c] : ov;
                     }
@@ -1027,7 +1027,7 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
                 int t[2][2];
     #pragma unroll
                 for (int r = 0; r < 2; ++r) {
-                    const int o0 = __shfl_xor(k[r][0], 1), o1 = __shfl_xor(k[r][1], 1);
+                    const int o0 = lane_xor1(k[r][0]), o1 = lane_xor1(k[r][1]);
                     const int d0 = cc ? o0 : k[r][0], d1 = cc ? o1 : k[r][1], d2 = cc ? k[r][0] : o0, d3 = cc ? k[r][1] : o1;
                     int y0, y1, y2, y3;
                     idct4(d0, d1, d2, d3, y0, y1, y2, y3);
@@ -1037,7 +1037,7 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
                 // columns: my 2 rows + the 2 of lane ^ 4
     #pragma unroll
                 for (int c = 0; c < 2; ++c) {
-                    const int o0 = __shfl_xor(t[0][c], 4), o1 = __shfl_xor(t[1][c], 4);
+                    const int o0 = lane_xor4(t[0][c]), o1 = lane_xor4(t[1][c]);
                     const int d0 = cr ? o0 : t[0][c], d1 = cr ? o1 : t[1][c], d2 = cr ? t[0][c] : o0, d3 = cr ? t[1][c] : o1;
                     int y0, y1, y2, y3;
                     idct4(d0, d1, d2, d3, y0, y1, y2, y3);
