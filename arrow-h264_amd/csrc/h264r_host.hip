@@ -300,7 +300,7 @@ static const Knobs& knobs()
         v = 2000; n.ok &= env_long("H264R_WAIT_MS", 1, 40000, &v);
         n.wait_ticks = (uint32_t)(v * 100000);                     // s_memrealtime, 100 MHz
         // levels beyond 3 hold few MBs each, and a grid barrier apiece: the walk takes them
-        v = 3; n.ok &= env_long("H264R_LEVELS", 0, LEVEL_LISTS, &v); n.levels = (int)v;
+        v = 4; n.ok &= env_long("H264R_LEVELS", 0, LEVEL_LISTS, &v); n.levels = (int)v;
         // round 5 (8 lanes per unit, staged stores): k_deblock2 wins from 64 1080p pictures of a
         // throughput batch, 32 2160p chain pictures, up (profiles/r05_x_deblock_min.txt); the lone
         // picture of the latency chain keeps k_deblock
@@ -465,11 +465,12 @@ struct Timed {
 // counts them, k_level_scatter builds one MB list per level, and
 // k_intra_levels does levels 1..N from those lists in one persistent cooperative launch
 // (a grid barrier between levels); the wavefront walk k_intra_pic takes whatever lies
-// deeper.  N = 16 by default: P / B pictures rarely go deeper, and in all-intra pictures
-// (levels x + 2y + 1) a level holds a few MBs per picture, so the walk's row-to-row
+// deeper.  N = 4 by default (knobs()): P / B pictures rarely go deeper, and in all-intra
+// pictures (levels x + 2y + 1) a level holds a few MBs per picture, so the walk's row-to-row
 // hand-off beats one grid barrier per level (config 2: 36.6 ms of intra walking vs 44.9
-// with every level from lists).  H264R_LEVELS=<N> overrides N (0: walk only; at most
-// LEVEL_LISTS).
+// with every level from lists).  N was 3 until the level barrier was sharded (round 5:
+// config 3 intra 1.215 -> 1.148 ms at 4, profiles/r05_aw_levels4_ab.txt).  H264R_LEVELS=<N>
+// overrides N (0: walk only; at most LEVEL_LISTS).
 static int level_launches() { return knobs().levels; }
 
 // Pictures [p0, p0 + n) of a batch as a batch of their own: every per-picture array advanced

@@ -265,6 +265,20 @@ def test_gpu_batch_dense_intra_levels(L, dec):
     _batch_vs_oracle(L, dec, 3, 40, 30, 3, intra_permille=600, pcm_permille=30)
 
 
+@pytest.mark.parametrize("levels", ["8", "16"])
+def test_gpu_batch_many_level_barriers(L, monkeypatch, levels):
+    """Every level from lists (H264R_LEVELS 8 / 16, read at h264r_create): the dense-intra
+    pictures cross k_intra_levels' sharded grid barrier (8 shard counters + a top counter,
+    k_picture.hip) up to 15 times in one launch; the deeper MBs still go to the walk."""
+    monkeypatch.setenv("H264R_LEVELS", levels)
+    d = h264r.Decoder(0, 240, 135)
+    try:
+        _batch_vs_oracle(L, d, 3, 40, 30, 3, deblocks=(0,), intra_permille=600, pcm_permille=30)
+        _batch_vs_oracle(L, d, 3, 120, 68, 4, deblocks=(0,), intra_permille=300)
+    finally:
+        d.close()
+
+
 @pytest.mark.parametrize("n", [33, 70])
 def test_gpu_batch_picture_groups(L, dec, n):
     """Batches spanning several picture groups of k_deblock2 (the last one ragged; 9 MB rows =
