@@ -261,7 +261,7 @@ struct Knobs {
     bool ok = true;
     int debug = 0;             // H264R_DEBUG: schedule flags of h264r_set_debug OR-ed into every launch
     uint32_t wait_ticks = 0;   // H264R_WAIT_MS: bound of every device-side wait (below)
-    int levels = 16;           // H264R_LEVELS: dependency levels from lists (level_launches)
+    int levels = -1;           // H264R_LEVELS: dependency levels from lists (-1: by launch size, level_launches)
     int deblock2_min = 8;      // H264R_DEBLOCK2_MIN: batches of this many 68-row pictures' worth of MB rows deblock with k_deblock2
     int deblock2s_max = 512;   // H264R_DB2S_MAX: batches of fewer 68-row pictures' worth of MB rows take the split walk
     int lvl_margin = 1;        // H264R_LVL_MARGIN: k_intra_levels' grid, blocks per CU below occupancy
@@ -300,7 +300,7 @@ static const Knobs& knobs()
         v = 2000; n.ok &= env_long("H264R_WAIT_MS", 1, 40000, &v);
         n.wait_ticks = (uint32_t)(v * 100000);                     // s_memrealtime, 100 MHz
         // levels beyond 3 hold few MBs each, and a grid barrier apiece: the walk takes them
-        v = 4; n.ok &= env_long("H264R_LEVELS", 0, LEVEL_LISTS, &v); n.levels = (int)v;
+        v = -1; n.ok &= env_long("H264R_LEVELS", 0, LEVEL_LISTS, &v); n.levels = (int)v;
         // round 5 (8 lanes per unit, staged stores): k_deblock2 wins from 64 1080p pictures of a
         // throughput batch, 32 2160p chain pictures, up (profiles/r05_x_deblock_min.txt); the lone
         // picture of the latency chain keeps k_deblock
@@ -465,13 +465,19 @@ struct Timed {
 // counts them, k_level_scatter builds one MB list per level, and
 // k_intra_levels does levels 1..N from those lists in one persistent cooperative launch
 // (a grid barrier between levels); the wavefront walk k_intra_pic takes whatever lies
-// deeper.  N = 4 by default (knobs()): P / B pictures rarely go deeper, and in all-intra
-// pictures (levels x + 2y + 1) a level holds a few MBs per picture, so the walk's row-to-row
-// hand-off beats one grid barrier per level (config 2: 36.6 ms of intra walking vs 44.9
-// with every level from lists).  N was 3 until the level barrier was sharded (round 5:
-// config 3 intra 1.215 -> 1.148 ms at 4, profiles/r05_aw_levels4_ab.txt).  H264R_LEVELS=<N>
-// overrides N (0: walk only; at most LEVEL_LISTS).
-static int level_launches() { return knobs().levels; }
+// deeper.  N by default: 4 for launches of >= LEVELS4_MIN_MBS MBs, else 3.  P / B pictures
+// rarely go deeper, and in all-intra pictures (levels x + 2y + 1) a level holds a few MBs per
+// picture, so the walk's row-to-row hand-off beats one grid barrier per level (config 2: 36.6 ms
+// of intra walking vs 44.9 with every level from lists).  A fourth level paid once the level
+// barrier was sharded, on large launches only (round 5, profiles/r05_aw_levels4_ab.txt: config
+// 3's 1024 pictures intra 1.215 -> 1.148 ms; config 4's 256 pictures 0.383 -> 0.411, chain
+// mode config 4 0.148 -> 0.200).  H264R_LEVELS=<N> sets N (0: walk only; at most LEVEL_LISTS).
+constexpr size_t LEVELS4_MIN_MBS = (size_t)4 << 20;
+static int level_launches(size_t mbs)
+{
+    const int v = knobs().levels;
+    return v >= 0 ? v : mbs >= LEVELS4_MIN_MBS ? 4 : 3;
+}
 
 // Pictures [p0, p0 + n) of a batch as a batch of their own: every per-picture array advanced
 // (the level pool is shared: coef_off stays an offset into it).
@@ -553,7 +559,7 @@ static int recon_launches(h264r_ctx* c, const Stage& S, hipStream_t s, int2 rows
         uint16_t* lvl = levels ? X.d_lvl : nullptr;
         int* pband = sync + 1 + (size_t)P * H + 32 + P;        // after the inter flags
         int* lbar = sync + 1 + (size_t)P * H + 23;               // k_intra_levels' barrier (9 ints)
-        const int lmax = levels ? level_launches() : 0;
+        const int lmax = levels ? level_launches((size_t)P * W * HB) : 0;
         if (levels) {
             int* lvsync = sync + 1 + (size_t)P * H + 2;
             int* lcount = X.d_lcnt;
@@ -742,7 +748,7 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
     // H264R_DBG_WAIT_TEST: every intra-walk wait asks for progress no row reaches, under a
     // 10 ms bound -- the launch must drain and h264r_check report H264R_EDEVICE
     if ((st = set_wait_bound(c, wait_test ? 1000000u : wait_bound_ticks(), s))) return st;
-    const bool levels = nmb <= LEVEL_MAX_MBS && (size_t)(W + 2) * (HB + 1) <= (size_t)LEVEL_LDS && level_launches() > 0 &&
+    const bool levels = nmb <= LEVEL_MAX_MBS && (size_t)(W + 2) * (HB + 1) <= (size_t)LEVEL_LDS && level_launches(0) > 0 &&
                         !(c->debug & (H264R_DBG_INTRA_WALK | H264R_DBG_WAIT_TEST));
     if (levels && !c->levels_grid) {
         // every workgroup of the persistent level kernel must be resident at once: one
