@@ -256,6 +256,14 @@ DEV int lane_xor4(int v)
     return __builtin_amdgcn_update_dpp(t, v, 0x104, 0xF, 0x5, false);
 }
 
+// The value of the lane of this lane's quad pair (lane, lane ^ 4) whose bit 2 is clear (lo) or
+// set (hi): one banked DPP row shift each, keeping the own value in the other banks, where the
+// exchange needed two moves plus a select per output.  (The pair (lane, lane ^ 1) form by
+// quad_perm [0,0,2,2] / [1,1,3,3] is exact in isolation, tools/dpp/dpp_test.hip, but gave wrong
+// residuals inside k_inter4r / the intra kernels; not used.)
+DEV int lane_lo4(int v) { return __builtin_amdgcn_update_dpp(v, v, 0x114, 0xF, 0xA, false); }   // banks 1, 3: lane - 4
+DEV int lane_hi4(int v) { return __builtin_amdgcn_update_dpp(v, v, 0x104, 0xF, 0x5, false); }   // banks 0, 2: lane + 4
+
 // Column pass of inverse_4x4 (transform.cc:619-640) for the lane holding row r of
 // the block: t[k] = row k's value in this column.  Returns ((o_r + 32) >> 6).
 DEV int idct4_col_row(int t0, int t1, int t2, int t3, int r)

@@ -957,9 +957,8 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
                     int in[8], outv[8];
     #pragma unroll
                     for (int i = 0; i < 4; ++i) {
-                        const int ov = lane_xor4(e4[i][c]);
-                        in[i] = (by & 1) ? ov : e4[i][c];
-                        in[4 + i] = (by & 1) ? e4[i][c] : ov;
+                        in[i] = lane_lo4(e4[i][c]);         // rows 0..3: the lane with by even
+                        in[4 + i] = lane_hi4(e4[i][c]);
                     }
                     idct8(in, outv);
                     const int my = -(by & 1);
@@ -1037,8 +1036,8 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
                 // columns: my 2 rows + the 2 of lane ^ 4
     #pragma unroll
                 for (int c = 0; c < 2; ++c) {
-                    const int o0 = lane_xor4(t[0][c]), o1 = lane_xor4(t[1][c]);
-                    const int d0 = cr ? o0 : t[0][c], d1 = cr ? o1 : t[1][c], d2 = cr ? t[0][c] : o0, d3 = cr ? t[1][c] : o1;
+                    // (rows 0..1 from the lane with by even, 2..3 from the other)
+                    const int d0 = lane_lo4(t[0][c]), d1 = lane_lo4(t[1][c]), d2 = lane_hi4(t[0][c]), d3 = lane_hi4(t[1][c]);
                     int y0, y1, y2, y3;
                     idct4(d0, d1, d2, d3, y0, y1, y2, y3);
                     rc[0][c] = ((cr ? y2 : y0) + 32) >> 6;
