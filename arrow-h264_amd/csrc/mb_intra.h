@@ -253,8 +253,7 @@ DEV void chroma_res2(const h264r_mb& m, const IntraLoads& L, int lane, int (&res
     const int f = ea + (eb ^ -(cb >> 1)) + (cb >> 1);
     const int kdc = ((f * L.cdc_scale) * (1 << per)) >> 5;
     k0 = (crow == 0 && chalf == 0) ? kdc : k0;
-    const int o0 = __shfl_xor(k0, 4), o1 = __shfl_xor(k1, 4);
-    const int d0 = chalf ? o0 : k0, d1 = chalf ? o1 : k1, d2 = chalf ? k0 : o0, d3 = chalf ? k1 : o1;
+    const int d0 = lane_lo4(k0), d1 = lane_lo4(k1), d2 = lane_hi4(k0), d3 = lane_hi4(k1);   // chalf = lane bit 2
     int t[4];
     idct4(d0, d1, d2, d3, t[0], t[1], t[2], t[3]);
     const int u0 = chalf ? t[2] : t[0], u1 = chalf ? t[3] : t[1];
