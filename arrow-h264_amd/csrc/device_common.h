@@ -260,7 +260,9 @@ DEV int lane_xor4(int v)
 // set (hi): one banked DPP row shift each, keeping the own value in the other banks, where the
 // exchange needed two moves plus a select per output.  (The pair (lane, lane ^ 1) form by
 // quad_perm [0,0,2,2] / [1,1,3,3] is exact in isolation, tools/dpp/dpp_test.hip, but gave wrong
-// residuals inside k_inter4r / the intra kernels; not used.)
+// residuals inside k_inter4r / the intra kernels once the compiler folded the moves into their
+// consumers -- exact again with the results kept opaque, and no faster; not used.  These two
+// are verified as folded by every GPU parity test: re-run them after touching a caller.)
 DEV int lane_lo4(int v) { return __builtin_amdgcn_update_dpp(v, v, 0x114, 0xF, 0xA, false); }   // banks 1, 3: lane - 4
 DEV int lane_hi4(int v) { return __builtin_amdgcn_update_dpp(v, v, 0x104, 0xF, 0x5, false); }   // banks 0, 2: lane + 4
 
