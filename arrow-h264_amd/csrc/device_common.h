@@ -209,10 +209,12 @@ DEV const gdword* as_global(const void* p) { return (const gdword*)p; }
 template <typename T>
 DEV T load_global(const void* p) { return *(const __attribute__((address_space(1))) T*)p; }
 
-DEV const gdword* row_dwords(const uint8_t* __restrict__ img, int W, int H, int x, int y)
+// pitch: W for a frame, 2 W for a field of a DPB frame (its rows are every second row,
+// include/h264r.h H264R_REF_BOTTOM; the field's pointer starts at its first row)
+DEV const gdword* row_dwords(const uint8_t* __restrict__ img, int W, int pitch, int H, int x, int y)
 {
     const int a = clip3(0, W - 1, x - 2) & ~3;
-    return as_global(img + (size_t)clip3(0, H - 1, y) * W + a);
+    return as_global(img + (size_t)clip3(0, H - 1, y) * pitch + a);
 }
 
 // ---------------------------------------------------------------- deblocking

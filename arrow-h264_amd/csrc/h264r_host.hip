@@ -987,13 +987,18 @@ int h264r_picture_end_async(h264r_ctx* c, int keep_slot)
     (void)hipSetDevice(c->device);
     const size_t n = (size_t)P.pw * P.ph, ys = n * 256, cs = n * 64;
     if (P.h_levels.empty()) P.h_levels.push_back(0);
-    // every referenced slot must be loaded
+    // every referenced slot must be loaded, with a frame of this picture's size (a field
+    // picture: twice its height; its entries may name either field of a slot, include/h264r.h)
+    const int fld = P.h_pic.structure != H264R_FRAME;
+    if (P.h_pic.structure < H264R_FRAME || P.h_pic.structure > H264R_BOTTOM_FIELD) return H264R_EINVAL;
+    const int frame_h = P.ph << fld;
     for (const h264r_slice& sl : P.h_slices)
         for (int l = 0; l < 2; ++l)
             for (int i = 0; i < sl.num_ref[l]; ++i) {
-                int slot = sl.ref_slot[l][i];
-                if (slot < 0 || slot >= H264R_MAX_SLOTS || !c->slot[slot][0] || c->slot_w[slot] != P.pw || c->slot_h[slot] != P.ph)
-                    return H264R_ESTATE;
+                const int ref = sl.ref_slot[l][i];
+                const int slot = fld ? ref & ~H264R_REF_BOTTOM : ref;
+                if (ref < 0 || slot >= H264R_MAX_SLOTS) return H264R_EINVAL;
+                if (!c->slot[slot][0] || c->slot_w[slot] != P.pw || c->slot_h[slot] != frame_h) return H264R_ESTATE;
             }
     int st = 0;
     // the device inputs are one set, reused in stream order (dev_resize drains before it frees)
@@ -1024,8 +1029,21 @@ int h264r_picture_end_async(h264r_ctx* c, int keep_slot)
     b.out_y = c->d_out; b.out_u = c->d_out + ys; b.out_v = c->d_out + ys + cs;
     if ((st = run_batch(c, b, s, 0, b.height_mbs))) return st;
     if (keep_slot >= 0) {
-        if ((st = ensure_slot(c, keep_slot, P.pw, P.ph))) return st;
-        HIP_OK(hipMemcpyAsync(c->slot[keep_slot][0], c->d_out, ys + 2 * cs, hipMemcpyDeviceToDevice, s));
+        if ((st = ensure_slot(c, keep_slot, P.pw, frame_h))) return st;
+        if (!fld) {
+            HIP_OK(hipMemcpyAsync(c->slot[keep_slot][0], c->d_out, ys + 2 * cs, hipMemcpyDeviceToDevice, s));
+        } else {
+            // a field goes into its parity's rows of the slot's frame (the reference combines the
+            // two fields of a frame with dpb_combine_field_yuv, picture.cc:573-590); the other
+            // field's rows are left as they are
+            const int bot = P.h_pic.structure == H264R_BOTTOM_FIELD;
+            const size_t W = (size_t)P.pw * 16, Wc = W / 2;
+            HIP_OK(hipMemcpy2DAsync(c->slot[keep_slot][0] + bot * W, 2 * W, c->d_out, W, W, (size_t)P.ph * 16,
+                                    hipMemcpyDeviceToDevice, s));
+            for (int k = 1; k < 3; ++k)
+                HIP_OK(hipMemcpy2DAsync(c->slot[keep_slot][k] + bot * Wc, 2 * Wc, c->d_out + ys + (k - 1) * cs, Wc, Wc,
+                                        (size_t)P.ph * 8, hipMemcpyDeviceToDevice, s));
+        }
     }
     // planes and the device error word into this picture's pinned staging; the error word is
     // cleared behind it, so each picture reports its own failures

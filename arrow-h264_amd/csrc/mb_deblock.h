@@ -23,7 +23,8 @@ struct MotionRef {
 
 // Per-4x4-block motion as resolved in k_inter4 (block_motion): {mv, ref_idx | slot << 8} per list.
 // ref identity = DPB slot of RefPicList[l][ref_idx] (pic_motion_params::ref_pic,
-// interpret_mb.cc:611-623), -1 when the list is unused.
+// interpret_mb.cc:611-623) with the field parity bit (H264R_REF_BOTTOM: the two fields of a
+// frame are different pictures), -1 when the list is unused.
 DEV MotionRef motion_of(uint2 w0, uint2 w1)
 {
     MotionRef r;
@@ -38,20 +39,21 @@ DEV MotionRef motion_of(uint2 w0, uint2 w1)
     return r;
 }
 
-DEV int cmp_mv(const MotionRef& a, int la, const MotionRef& c, int lc)   // deblock.cc:35-38 (frame: mvlimit 4)
+// mvlimit 4 in frame pictures, 2 in field pictures (deblock.cc:35-38, 86, 164)
+DEV int cmp_mv(const MotionRef& a, int la, const MotionRef& c, int lc, int mvlim)
 {
-    return (int)(iabs(a.mvx[la] - c.mvx[lc]) >= 4) | (int)(iabs(a.mvy[la] - c.mvy[lc]) >= 4);
+    return (int)(iabs(a.mvx[la] - c.mvx[lc]) >= 4) | (int)(iabs(a.mvy[la] - c.mvy[lc]) >= mvlim);
 }
 
-DEV int bs_compare(const MotionRef& p, const MotionRef& q)              // deblock.cc:40-75
+DEV int bs_compare(const MotionRef& p, const MotionRef& q, int mvlim)   // deblock.cc:40-75
 {
     int p0 = p.ref[0], q0 = q.ref[0], p1 = p.ref[1], q1 = q.ref[1];
     if ((p0 == q0 && p1 == q1) || (p0 == q1 && p1 == q0)) {
         if (p0 != p1) {
-            if (p0 == q0) return cmp_mv(p, 0, q, 0) | cmp_mv(p, 1, q, 1);
-            return cmp_mv(p, 0, q, 1) | cmp_mv(p, 1, q, 0);
+            if (p0 == q0) return cmp_mv(p, 0, q, 0, mvlim) | cmp_mv(p, 1, q, 1, mvlim);
+            return cmp_mv(p, 0, q, 1, mvlim) | cmp_mv(p, 1, q, 0, mvlim);
         }
-        return (cmp_mv(p, 0, q, 0) | cmp_mv(p, 1, q, 1)) & (cmp_mv(p, 0, q, 1) | cmp_mv(p, 1, q, 0));
+        return (cmp_mv(p, 0, q, 0, mvlim) | cmp_mv(p, 1, q, 1, mvlim)) & (cmp_mv(p, 0, q, 1, mvlim) | cmp_mv(p, 1, q, 0, mvlim));
     }
     return 1;
 }

@@ -184,11 +184,11 @@ DEV s16x2 pair_at(uint32_t r0, uint32_t r1, uint32_t r2)
 // out[i] packs row i's four samples as bytes.
 // The 9 window rows of one lane straight from the reference plane (three aligned dwords
 // per row from clip(x - 2) & ~3, row index clamped).
-DEV void luma_window_global(const uint8_t* __restrict__ img, int W, int H, int x, int y, uint32_t (&w)[9][3])
+DEV void luma_window_global(const uint8_t* __restrict__ img, int W, int pitch, int H, int x, int y, uint32_t (&w)[9][3])
 {
 #pragma unroll
     for (int r = 0; r < 9; ++r) {
-        const gdword* q = row_dwords(img, W, H, x, y - 2 + r);
+        const gdword* q = row_dwords(img, W, pitch, H, x, y - 2 + r);
         w[r][0] = q[0]; w[r][1] = q[1]; w[r][2] = q[2];
     }
 }
@@ -300,8 +300,8 @@ DEV void luma_block_pred(const uint32_t (&w)[9][3], int W, int x, int xf, int yf
 // 16-bit sum: (8-xf)(8-yf) + xf(8-yf) + (8-xf)yf + xf yf = 64, so 255 * 64 + 32 fits.
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 DEV u16x2 as_u16x2(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
-DEV void chroma_block_pred2(const uint8_t* __restrict__ cb, const uint8_t* __restrict__ cr, int W, int H, int xi, int yi,
-                            int xf, int yf, uint32_t (&out)[2])
+DEV void chroma_block_pred2(const uint8_t* __restrict__ cb, const uint8_t* __restrict__ cr, int W, int pitch, int H, int xi,
+                            int yi, int xf, int yf, uint32_t (&out)[2])
 {
     const int a = clip3(0, W - 1, xi) & ~3;
     // both planes' three rows first (12 dwords in flight): a lane-divergent interior / edge
@@ -312,7 +312,7 @@ DEV void chroma_block_pred2(const uint8_t* __restrict__ cb, const uint8_t* __res
     for (int pl = 0; pl < 2; ++pl)
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
-            const gdword* q = as_global((pl ? cr : cb) + (size_t)clip3(0, H - 1, yi + k) * W + a);
+            const gdword* q = as_global((pl ? cr : cb) + (size_t)clip3(0, H - 1, yi + k) * pitch + a);
             w[pl][k][0] = q[0];
             w[pl][k][1] = q[1];
         }
@@ -491,6 +491,10 @@ DEV void dbinfo_block(const h264r_batch& b, const Geom& g, int pic, int aa, bool
     const uint2 l0 = motion_word(nb.lmv[0], nb.lri[0], slices, S, lsl, 0), l1 = motion_word(nb.lmv[1], nb.lri[1], slices, S, lsl, 1);
     const uint2 u0 = motion_word(nb.umv[0], nb.uri[0], slices, S, usl, 0), u1 = motion_word(nb.umv[1], nb.uri[1], slices, S, usl, 1);
     const int l_type = slice_type_of(slices, S, L.slice), u_type = slice_type_of(slices, S, U.slice);
+    // field pictures: mvlimit 2 (deblock.cc:86,164) and no bS 4 across horizontal MB edges
+    // (cond_bS4 = !field || vertical, deblock.cc:103-107,184-189)
+    const int fld = (int)__builtin_amdgcn_readfirstlane(ld_const(&b.pics[pic].structure)) != H264R_FRAME;
+    const int mvlim = fld ? 2 : 4;
     // ---- deblocking record (Deblock::strength deblock.cc:78-289): this lane's
     // left edge (vertical edge bx, segment by) and top edge (horizontal edge by,
     // segment bx)
@@ -526,14 +530,14 @@ DEV void dbinfo_block(const h264r_batch& b, const Geom& g, int pic, int aa, bool
                     else if (intra) v = 3;
                     else if (coded) v = 2;
                     else if (same_part) v = 0;
-                    else v = bs_compare(mq, motion_of(l0, l1));
+                    else v = bs_compare(mq, motion_of(l0, l1), mvlim);
                 } else {
-                    if (e == 0 && (special || intra)) v = 4;
+                    if (e == 0 && !fld && (special || intra)) v = 4;
                     else if (special || intra) v = 3;
                     else if (e > 0 && pskip) v = 0;
                     else if (coded) v = 2;
                     else if (same_part) v = 0;
-                    else v = bs_compare(mq, motion_of(u0, u1));
+                    else v = bs_compare(mq, motion_of(u0, u1), mvlim);
                 }
             }
             out->bs[hor * 16 + e * 4 + s] = (uint8_t)v;
@@ -661,6 +665,10 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
         // the prediction of each list in named registers: an array indexed by the (not
         // unrolled) list loop was promoted to LDS by the compiler (48 B per lane)
         uint32_t pY[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}}, pC[2][2] = {{0, 0}, {0, 0}};
+        // a field picture (include/h264r.h H264R_TOP_FIELD) reads fields of the DPB frames:
+        // every second row from the field's first row, clamped to the field's own rows
+        const int structure = (int)__builtin_amdgcn_readfirstlane(ld_const(&b.pics[pic].structure));
+        const int fld = structure != H264R_FRAME;
     #pragma unroll 1
         for (int l = 0; l < 2; ++l) {
             const uint2 mw = l ? m1 : m0;
@@ -669,18 +677,24 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
             if (!__any(use)) continue;                                  // P pictures: list 1 never
             uint32_t tY[4] = {0x80808080u, 0x80808080u, 0x80808080u, 0x80808080u};
             uint32_t tC[2] = {0x80808080u, 0x80808080u};                // no_ref: 128 (inter_prediction.cc:164-167,366-369)
-            const int slot = (int8_t)((mw.y >> 8) & 255);
-            const bool ok = use && slot >= 0 && slot < H264R_MAX_SLOTS && rr < H264R_MAX_REFS && S.planes[slot * 3];
+            const int ref = (int8_t)((mw.y >> 8) & 255);                // slot | H264R_REF_BOTTOM
+            const int slot = ref & 31, bot = fld & (ref >> 6);
+            const bool ok = use && ref >= 0 && (ref & ~H264R_REF_BOTTOM) < H264R_MAX_SLOTS && rr < H264R_MAX_REFS &&
+                            S.planes[slot * 3];
             const int mvx = (int16_t)(mw.x & 0xFFFF), mvy = (int16_t)(mw.x >> 16);
             const int vx = X4 * 16 + mvx, vy = Y4 * 16 + mvy;           // quarter luma / eighth chroma units
             const int x = vx >> 2, y = vy >> 2;
             {
                 // the 9 window rows of the lane's own block, straight from the plane
                 uint32_t w[9][3];
-                if (ok) luma_window_global(S.planes[slot * 3], g.W, g.H, x, y, w);
+                if (ok) luma_window_global(S.planes[slot * 3] + bot * g.W, g.W, g.W << fld, g.H, x, y, w);
                 if (ok) luma_block_pred(w, g.W, x, vx & 3, vy & 3, tY);
             }
-            if (ok) chroma_block_pred2(S.planes[slot * 3 + 1], S.planes[slot * 3 + 2], g.Wc, g.Hc, vx >> 3, vy >> 3, vx & 7, vy & 7, tC);
+            // a reference field of the other parity: the chroma sample grid sits a quarter
+            // chroma row off (get_block_chroma inter_prediction.cc:352-355)
+            const int vyc = vy + (fld && bot != (structure == H264R_BOTTOM_FIELD) ? (bot ? -2 : 2) : 0);
+            if (ok) chroma_block_pred2(S.planes[slot * 3 + 1] + bot * g.Wc, S.planes[slot * 3 + 2] + bot * g.Wc, g.Wc,
+                                       g.Wc << fld, g.Hc, vx >> 3, vyc >> 3, vx & 7, vyc & 7, tC);
             const bool l1 = l != 0;
     #pragma unroll
             for (int i = 0; i < 4; ++i) {

@@ -33,12 +33,30 @@ static const uint8_t QP_SCALE_CR[52] = {                  /* interpret_mb.cc:777
 static int clip3i(int lo, int hi, int x) { return x < lo ? lo : (x > hi ? hi : x); }
 
 int h264r_synth_slot_poc(int slot) { return 4 * slot; }
+int h264r_synth_ref_frames(const h264r_synth_cfg* cfg)
+{
+    return cfg->structure != H264R_FRAME ? (cfg->num_refs + 1) / 2 : cfg->num_refs;
+}
 int h264r_synth_cur_poc(const h264r_synth_cfg* cfg)
 {
-    /* P: after every reference; B: between slot (n/2 - 1) and slot n/2. */
-    if (cfg->kind == H264R_SYNTH_B && cfg->num_refs >= 2) return 4 * (cfg->num_refs / 2) - 2;
-    return 4 * cfg->num_refs;
+    /* P: after every reference; B: between slot (n/2 - 1) and slot n/2 (n DPB frames); a
+       bottom field one after its top field */
+    const int n = h264r_synth_ref_frames(cfg), bot = cfg->structure == H264R_BOTTOM_FIELD;
+    if (cfg->kind == H264R_SYNTH_B && n >= 2) return 4 * (n / 2) - 2 + bot;
+    return 4 * n + bot;
 }
+
+/* POC of list candidate k: frame slot k (frames), or field k of the DPB frames (slot k / 2,
+   bottom when k is odd) */
+static int cand_poc(const h264r_synth_cfg* c, int k)
+{
+    return c->structure != H264R_FRAME ? h264r_synth_slot_poc(k >> 1) + (k & 1) : h264r_synth_slot_poc(k);
+}
+static int cand_ref(const h264r_synth_cfg* c, int k)
+{
+    return c->structure != H264R_FRAME ? (k >> 1) | ((k & 1) ? H264R_REF_BOTTOM : 0) : k;
+}
+static int ref_poc(int ref) { return h264r_synth_slot_poc(ref & 31) + ((ref & H264R_REF_BOTTOM) ? 1 : 0); }
 
 int h264r_synth_default(h264r_synth_cfg* c, int config_idx, int width_mbs, int height_mbs)
 {
@@ -88,12 +106,14 @@ static void make_slices(const h264r_synth_cfg* c, rng_t* r, h264r_slice* sl)
             x->sp_switch = (uint8_t)rrange(r, 0, 1);
             x->qs_c[0] = x->qs_c[1] = (int8_t)x->qs_y;     /* chroma_qp_index_offset 0, QsY < 30 */
         }
-        /* L0: descending POC below cur then ascending above; L1: the reverse (8.2.4.2.3 style) */
-        int l0[H264R_MAX_REFS], l1[H264R_MAX_REFS], k0 = 0, k1 = 0;
-        for (int k = n - 1; k >= 0; --k) if (h264r_synth_slot_poc(k) < cur) l0[k0++] = k;
-        for (int k = 0; k < n; ++k) if (h264r_synth_slot_poc(k) > cur) l0[k0++] = k;
-        for (int k = 0; k < n; ++k) if (h264r_synth_slot_poc(k) > cur) l1[k1++] = k;
-        for (int k = n - 1; k >= 0; --k) if (h264r_synth_slot_poc(k) < cur) l1[k1++] = k;
+        /* L0: descending POC below cur then ascending above; L1: the reverse (8.2.4.2.3 style;
+           fields: the candidates are the DPB frames' fields, so the order alternates parity) */
+        int l0[2 * H264R_MAX_REFS], l1[2 * H264R_MAX_REFS], k0 = 0, k1 = 0;
+        const int nc = c->structure != H264R_FRAME ? 2 * h264r_synth_ref_frames(c) : n;
+        for (int k = nc - 1; k >= 0; --k) if (cand_poc(c, k) < cur) l0[k0++] = cand_ref(c, k);
+        for (int k = 0; k < nc; ++k) if (cand_poc(c, k) > cur) l0[k0++] = cand_ref(c, k);
+        for (int k = 0; k < nc; ++k) if (cand_poc(c, k) > cur) l1[k1++] = cand_ref(c, k);
+        for (int k = nc - 1; k >= 0; --k) if (cand_poc(c, k) < cur) l1[k1++] = cand_ref(c, k);
         x->num_ref[0] = (uint8_t)n;
         x->num_ref[1] = (uint8_t)(c->kind == H264R_SYNTH_B ? n : 0);
         for (int i = 0; i < H264R_MAX_REFS; ++i) { x->ref_slot[0][i] = -1; x->ref_slot[1][i] = -1; }
@@ -115,8 +135,8 @@ static void make_slices(const h264r_synth_cfg* c, rng_t* r, h264r_slice* sl)
         } else if (c->wp_mode == 2) { /* implicit: inter_prediction.cc:112-139 */
             for (int i0 = 0; i0 < n; ++i0)
                 for (int i1 = 0; i1 < n; ++i1) {
-                    int p0 = h264r_synth_slot_poc(x->ref_slot[0][i0]);
-                    int p1 = h264r_synth_slot_poc(x->ref_slot[1][i1] >= 0 ? x->ref_slot[1][i1] : 0);
+                    int p0 = ref_poc(x->ref_slot[0][i0]);
+                    int p1 = ref_poc(x->ref_slot[1][i1] >= 0 ? x->ref_slot[1][i1] : 0);
                     int td = clip3i(-128, 127, p1 - p0), w1;
                     if (td == 0) w1 = 32;
                     else {
@@ -225,6 +245,7 @@ int h264r_synth_picture(const h264r_synth_cfg* c, int index, h264r_mb* mbs, int1
     if (!c || !mbs || !levels || !mv || !ref_idx || !slices || !pic) return H264R_EINVAL;
     if (c->width_mbs <= 0 || c->height_mbs <= 0 || c->num_slices <= 0 || c->num_slices > H264R_MAX_SLICES ||
         c->num_slices > c->height_mbs || c->num_refs < 0 || c->num_refs > H264R_MAX_REFS ||
+        c->structure < H264R_FRAME || c->structure > H264R_BOTTOM_FIELD ||
         (c->kind != H264R_SYNTH_INTRA && c->num_refs < 1) || c->qp_min < 0 || c->qp_max > 51 ||
         c->qp_min > c->qp_max)
         return H264R_EINVAL;
@@ -238,7 +259,7 @@ int h264r_synth_picture(const h264r_synth_cfg* c, int index, h264r_mb* mbs, int1
     pic->constrained_intra_pred = c->constrained_intra;
     pic->num_slices = c->num_slices;
     pic->poc = h264r_synth_cur_poc(c);
-    pic->pad = 0;
+    pic->structure = c->structure;
 
     int64_t off = 0;
     int bslice = c->kind == H264R_SYNTH_B;

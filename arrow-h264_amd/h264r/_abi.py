@@ -16,7 +16,9 @@ DBG_WAIT_TEST = 32
 DBG_OVERLAP = 64
 DBG_DEBLOCK_SPLIT = 128
 MAX_REFS, MAX_SLOTS, MAX_SLICES = 16, 32, 256
-ABI_VERSION = 2
+ABI_VERSION = 3
+FRAME, TOP_FIELD, BOTTOM_FIELD = 0, 1, 2        # h264r_pic.structure
+REF_BOTTOM = 0x40                              # ref_slot entry of a field picture: the slot's bottom field
 
 P_SKIP, P_16x16, P_16x8, P_8x16, P_8x8, P_8x4, P_4x8, P_4x4 = range(8)
 I_4x4, I_8x8, I_16x16, SI, I_PCM = 8, 9, 10, 11, 12
@@ -49,7 +51,7 @@ QUANT_DTYPE = np.dtype([("scale4x4", "<i2", (2, 3, 6, 16)), ("scale8x8", "<i2", 
 assert QUANT_DTYPE.itemsize == 5760
 
 PIC_DTYPE = np.dtype([("constrained_intra_pred", "<i4"), ("num_slices", "<i4"),
-                      ("poc", "<i4"), ("pad", "<i4")])
+                      ("poc", "<i4"), ("structure", "<i4")])
 
 
 class SynthCfg(C.Structure):
@@ -62,7 +64,7 @@ class SynthCfg(C.Structure):
         ("qp_min", C.c_int32), ("qp_max", C.c_int32), ("pcm_permille", C.c_int32),
         ("intra_permille", C.c_int32), ("mv_range_x", C.c_int32),
         ("mv_range_y", C.c_int32), ("lossless_permille", C.c_int32), ("sp_slices", C.c_int32),
-        ("seed", C.c_uint64),
+        ("structure", C.c_int32), ("seed", C.c_uint64),
     ]
 
     def as_dict(self) -> dict:
@@ -103,8 +105,9 @@ def bind_synth(lib: C.CDLL) -> None:
     lib.h264r_synth_refpic.argtypes = [C.c_uint64, C.c_int, C.c_int, C.c_int, P, P, P]
     lib.h264r_synth_slot_poc.argtypes = [C.c_int]
     lib.h264r_synth_cur_poc.argtypes = [C.POINTER(SynthCfg)]
+    lib.h264r_synth_ref_frames.argtypes = [C.POINTER(SynthCfg)]
     lib.h264r_synth_algo_bytes.argtypes = [P, P, C.c_int, C.c_int,
                                            C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
     for f in ("h264r_synth_default", "h264r_synth_picture", "h264r_synth_refpic",
-              "h264r_synth_slot_poc", "h264r_synth_cur_poc", "h264r_synth_algo_bytes"):
+              "h264r_synth_slot_poc", "h264r_synth_cur_poc", "h264r_synth_ref_frames", "h264r_synth_algo_bytes"):
         getattr(lib, f).restype = C.c_int

@@ -55,10 +55,11 @@ def picture(lib: C.CDLL, cfg: A.SynthCfg, index: int) -> Picture:
 
 
 def refpics(lib: C.CDLL, cfg: A.SynthCfg, nslots: int | None = None):
-    """[(y, u, v)] for DPB slots 0..num_refs-1."""
-    W, H = cfg.width_mbs, cfg.height_mbs
+    """[(y, u, v)] for DPB slots 0..n-1: the frames the pictures reference (a field cfg's
+    references are fields of frames of twice its height, include/h264r_synth.h)."""
+    W, H = cfg.width_mbs, cfg.height_mbs * (2 if cfg.structure else 1)
     out = []
-    for s in range(cfg.num_refs if nslots is None else nslots):
+    for s in range(lib.h264r_synth_ref_frames(C.byref(cfg)) if nslots is None else nslots):
         y = np.zeros((16 * H, 16 * W), np.uint8)
         u = np.zeros((8 * H, 8 * W), np.uint8)
         v = np.zeros((8 * H, 8 * W), np.uint8)

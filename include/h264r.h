@@ -22,7 +22,8 @@
  * boundary; the reference's void/assert/exit() error convention
  * (decoder.h:301-338, ldecod.cc:33-48) becomes status codes.
  *
- * Data formats (all little-endian, 4:2:0, 8-bit, frame pictures):
+ * Data formats (all little-endian, 4:2:0, 8-bit; frame pictures and field pictures (PAFF,
+ * h264r_pic.structure below); MBAFF frames are H264R_EUNSUPPORTED):
  *   - h264r_mb       32-byte MB record (subset of mb_t, macroblock.h:78-135).
  *   - levels         int16 pool; each MB owns a compacted block at mb.coef_off
  *                    (in int16 units, multiple of 8):
@@ -53,7 +54,7 @@
 extern "C" {
 #endif
 
-#define H264R_ABI_VERSION 2
+#define H264R_ABI_VERSION 3
 
 /* ---- status codes ---------------------------------------------------------- */
 #define H264R_OK               0
@@ -147,18 +148,40 @@ typedef struct h264r_quant {
 } h264r_quant;
 
 /* Per-picture parameters. */
+#define H264R_FRAME         0   /* PictureStructure FRAME (defines.h)                          */
+#define H264R_TOP_FIELD     1   /* a field picture (field_pic_flag, slice_header bottom_field_flag */
+#define H264R_BOTTOM_FIELD  2   /* 0 / 1; interpret_rbsp.cc): height_mbs is the FIELD's height  */
+/* Field pictures (ABI 3).  A field picture is reconstructed and deblocked as a picture of
+ * PicHeightInMbs = FrameHeightInMbs / 2 rows (slice_header: PicHeightInMbs; the reference
+ * decodes it into a field storable_picture, picture.cc:17-83, and deblocks it on its own,
+ * exit_picture picture.cc:253), with three differences the kernels apply:
+ *   - its references are FIELDS of the DPB's frames: RefPicList entry = slot | H264R_REF_BOTTOM
+ *     for the bottom field of DPB slot `slot`, the plain slot for its top field; the plane is
+ *     read as every second row of the slot's frame (dpb_split_field picture.cc:408-470 without
+ *     the copy), clamped to the field's rows;
+ *   - chroma MC of a reference field of the other parity moves by -2 (top field predicting from
+ *     a bottom field) / +2 (bottom from top) quarter luma rows (get_block_chroma
+ *     inter_prediction.cc:352-355);
+ *   - bS: |dmv_y| >= 2 instead of 4 (mvlimit, deblock.cc:86,164), and intra / SP MB edges that
+ *     are horizontal get bS 3, not 4 (cond_bS4, deblock.cc:103-107,184-189).
+ * Reference identity (deblocking) is (slot, parity).  DPB slots always hold frames: the
+ * streaming API stores a field picture kept as a reference into its parity's rows of the slot
+ * (dpb_combine_field_yuv picture.cc:573-590 without the copy), so the two fields of a frame
+ * share one slot and a frame picture may later reference the frame they make up. */
+#define H264R_REF_BOTTOM  0x40
 typedef struct h264r_pic {
     int32_t  constrained_intra_pred;  /* pps.constrained_intra_pred_flag */
     int32_t  num_slices;
     int32_t  poc;                     /* informational (implicit weights are precomputed) */
-    int32_t  pad;
+    int32_t  structure;               /* H264R_FRAME / H264R_TOP_FIELD / H264R_BOTTOM_FIELD */
 } h264r_pic;
 
 /* A batch of same-sized pictures whose arrays are already resident on the device.
  * Per-picture strides: MBs W*H records; motion 2*(4H)*(4W) entries; slices
  * `slice_stride` entries; planes (16W)*(16H) bytes (Y) and (8W)*(8H) (Cb, Cr).
  * `ref_planes` is a device array of 3*H264R_MAX_SLOTS device pointers
- * (Y,Cb,Cr per DPB slot) to full-size planes; MC reads whole dwords, so each
+ * (Y,Cb,Cr per DPB slot) to full-size planes (frames: 2 * height_mbs MB rows when the
+ * batch's pictures are fields, H264R_TOP_FIELD above); MC reads whole dwords, so each
  * plane must be followed by H264R_PLANE_SLACK readable bytes (the slots of
  * h264r_set_ref / h264r_ref_planes are).  `ref_planes_stride` (ABI 2): 0 = that one
  * table serves every picture of the batch; otherwise picture p reads its own table at
@@ -214,6 +237,8 @@ int  h264r_set_ref(h264r_ctx* ctx, int slot, const uint8_t* y, const uint8_t* u,
                    const uint8_t* v, int width_mbs, int height_mbs);
 
 /* ---- per-picture streaming API (the Decoder shim drives this) ---------------------- */
+/* height_mbs: the picture's own height (a field picture: FrameHeightInMbs / 2, pic->structure
+ * naming its parity); DPB slots it reads or keeps into are frames of the context's size. */
 int  h264r_picture_begin(h264r_ctx* ctx, int width_mbs, int height_mbs,
                          const h264r_pic* pic, const h264r_slice* slices,
                          const h264r_quant* quant);

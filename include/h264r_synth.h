@@ -49,6 +49,12 @@ typedef struct h264r_synth_cfg {
     int32_t  sp_slices;          /* P pictures: every slice an SP slice (QsY 0..5 -- the reference's
                                     itrans_sp_cr indexes LevelScale2 by QsC unreduced, transform.cc:1230,
                                     so only QsC < 6 has defined results -- sp_for_switch_flag random)   */
+    int32_t  structure;          /* H264R_FRAME, or a field picture (H264R_TOP_FIELD / H264R_BOTTOM_FIELD):
+                                    height_mbs is then the field's height, num_refs counts reference
+                                    FIELDS (list entries), taken from DPB frames 0 .. (num_refs+1)/2 - 1
+                                    of 2 * height_mbs MB rows: the fields of frame slot s have POC
+                                    4 s (top) and 4 s + 1 (bottom), the lists order them by POC as
+                                    8.2.4.2.4/8.2.4.2.5 would (alternating parity) */
     uint64_t seed;
 } h264r_synth_cfg;
 
@@ -67,9 +73,11 @@ int  h264r_synth_picture(const h264r_synth_cfg* cfg, int index, h264r_mb* mbs, i
 int  h264r_synth_refpic(uint64_t seed, int slot, int width_mbs, int height_mbs,
                         uint8_t* y, uint8_t* u, uint8_t* v);
 
-/* POC assigned to DPB slot `slot` / to the current picture by the generator. */
+/* POC assigned to DPB slot `slot` (its frame; fields: + 0 top, + 1 bottom) / to the current
+ * picture (a field's own POC) by the generator, and the number of DPB frames it references. */
 int  h264r_synth_slot_poc(int slot);
 int  h264r_synth_cur_poc(const h264r_synth_cfg* cfg);
+int  h264r_synth_ref_frames(const h264r_synth_cfg* cfg);
 
 /* Algorithmic bytes of a batch: R and W summed over the MBs. */
 int  h264r_synth_algo_bytes(const h264r_mb* mbs, const int8_t* ref_idx, int width_mbs,

@@ -132,7 +132,7 @@ static int ensure_slot(h264r_ctx* c, int s, int w, int h)
     if (c->slot[s][0] && c->slot_w[s] == w && c->slot_h[s] == h) return H264R_OK;
     free(c->slot[s][0]);
     size_t ys = (size_t)w * h * 256, cs = (size_t)w * h * 64;
-    uint8_t* b = (uint8_t*)malloc(ys + 2 * cs);
+    uint8_t* b = (uint8_t*)calloc(ys + 2 * cs, 1);
     if (!b) return H264R_ENOMEM;
     c->slot[s][0] = b; c->slot[s][1] = b + ys; c->slot[s][2] = b + ys + cs;
     c->slot_w[s] = w; c->slot_h[s] = h;
@@ -247,21 +247,33 @@ static int picture_end(h264r_ctx* c, uint8_t* y, uint8_t* u, uint8_t* v, int kee
     for (int a = 0; a < n; ++a) if (!c->seen[a]) return H264R_ESTATE;
     if (keep >= H264R_MAX_SLOTS || !y || !u || !v) return H264R_EINVAL;
     if (!c->levels) { c->levels = (int16_t*)calloc(8, 2); c->cap_levels = 8; }
+    if (c->pic.structure < H264R_FRAME || c->pic.structure > H264R_BOTTOM_FIELD) return H264R_EINVAL;
+    /* a field picture's slots are frames of twice its height (include/h264r.h) */
+    const int fld = c->pic.structure != H264R_FRAME, frame_h = c->ph << fld;
     oracle_picture p;
     memset(&p, 0, sizeof(p));
     p.width_mbs = c->pw; p.height_mbs = c->ph;
     p.mbs = c->mbs; p.levels = c->levels; p.mv = c->mv; p.ref_idx = c->ref;
     p.slices = c->slices; p.pic = &c->pic; p.quant = &c->quant;
     for (int s = 0; s < H264R_MAX_SLOTS; ++s)
-        if (c->slot[s][0] && c->slot_w[s] == c->pw && c->slot_h[s] == c->ph)
+        if (c->slot[s][0] && c->slot_w[s] == c->pw && c->slot_h[s] == frame_h)
             for (int k = 0; k < 3; ++k) p.ref_planes[s][k] = c->slot[s][k];
     p.out[0] = y; p.out[1] = u; p.out[2] = v;
     int st = oracle_decode_picture(&p);
     if (st) return H264R_EINVAL;
     uint8_t* out[3] = {y, u, v};
     capture(c, keep, out);
-    if (keep >= 0) {
+    if (keep >= 0 && !fld) {
         if ((st = h264r_set_ref(c, keep, y, u, v, c->pw, c->ph))) return st;
+    } else if (keep >= 0) {
+        /* a field into its parity's rows of the slot's frame (dpb_combine_field_yuv
+           picture.cc:573-590), the other field's rows left as they are */
+        if ((st = ensure_slot(c, keep, c->pw, frame_h))) return st;
+        const int bot = c->pic.structure == H264R_BOTTOM_FIELD;
+        for (int k = 0; k < 3; ++k) {
+            const int w = k ? c->pw * 8 : c->pw * 16, h = k ? c->ph * 8 : c->ph * 16;
+            for (int r = 0; r < h; ++r) memcpy(c->slot[keep][k] + (size_t)(2 * r + bot) * w, out[k] + (size_t)r * w, w);
+        }
     }
     return H264R_OK;
 }

@@ -307,6 +307,7 @@ static void load_cof(const h264r_mb* mb, const int16_t* pool, const h264r_quant*
 typedef struct {
     const oracle_picture* p;
     int wmb, hmb, W, H, Wc, Hc, W4, H4;
+    int fld, bot;          /* a field picture (shr.field_pic_flag) and its parity (bottom_field_flag) */
     int16_t* slice_nr;     /* slice_nr per MB, -1 until decoded (reset_mbs slice_data.cc:55, mb.init :465) */
     uint8_t  (*strength_ver)[4][16];   /* mb_t::strength_ver, deblock.cc:80 */
     uint8_t  (*strength_hor)[4][16];   /* mb_t::strength_hor, deblock.cc:159 */
@@ -608,16 +609,18 @@ static void pred_mb(const pstate* s, int addr, int chroma, int mode, const uint8
 }
 
 /* --------------------------------------------------------- inter prediction */
-static inline int px(const uint8_t* img, int W, int H, int x, int y)
+/* pitch: W for a frame; 2 W for a field of a DPB frame (img at the field's first row): the
+   reference's split field (dpb_split_field picture.cc:408-470) holds exactly those rows */
+static inline int px(const uint8_t* img, int W, int pitch, int H, int x, int y)
 {
-    return img[clip3(0, H - 1, y) * W + clip3(0, W - 1, x)];
+    return img[clip3(0, H - 1, y) * pitch + clip3(0, W - 1, x)];
 }
 static inline int tap6(int a, int b, int c, int d, int e, int f) { return a - 5 * b + 20 * c + 20 * d - 5 * e + f; }
 
 /* One luma sample of get_block_luma (inter_prediction.cc:158-340), spec 8.4.2.2.1 form. */
-static int luma_sample(const uint8_t* img, int W, int H, int x, int y, int xf, int yf)
+static int luma_sample(const uint8_t* img, int W, int pitch, int H, int x, int y, int xf, int yf)
 {
-#define S(dx, dy) px(img, W, H, x + (dx), y + (dy))
+#define S(dx, dy) px(img, W, pitch, H, x + (dx), y + (dy))
 #define B1(dy) tap6(S(-2, dy), S(-1, dy), S(0, dy), S(1, dy), S(2, dy), S(3, dy))
 #define H1(dx) tap6(S(dx, -2), S(dx, -1), S(dx, 0), S(dx, 1), S(dx, 2), S(dx, 3))
     if (xf == 0 && yf == 0) return S(0, 0);
@@ -641,10 +644,10 @@ static int luma_sample(const uint8_t* img, int W, int H, int x, int y, int xf, i
 }
 
 /* get_block_chroma sample (inter_prediction.cc:380-404), 4:2:0 frame. */
-static int chroma_sample(const uint8_t* img, int W, int H, int xi, int yi, int xf, int yf)
+static int chroma_sample(const uint8_t* img, int W, int pitch, int H, int xi, int yi, int xf, int yf)
 {
-    int A = px(img, W, H, xi, yi), B = px(img, W, H, xi + 1, yi);
-    int C = px(img, W, H, xi, yi + 1), D = px(img, W, H, xi + 1, yi + 1);
+    int A = px(img, W, pitch, H, xi, yi), B = px(img, W, pitch, H, xi + 1, yi);
+    int C = px(img, W, pitch, H, xi, yi + 1), D = px(img, W, pitch, H, xi + 1, yi + 1);
     return ((8 - xf) * (8 - yf) * A + xf * (8 - yf) * B + (8 - xf) * yf * C + xf * yf * D + 32) >> 6;
 }
 
@@ -662,18 +665,25 @@ static int inter_pred_mb(const pstate* s, int addr, int mbp[3][16][16])
     for (int j = 0; j < 4; ++j)
         for (int i = 0; i < 4; ++i) {
             int idx = (mby * 4 + j) * s->W4 + mbx * 4 + i;
-            int r[2], vx[2], vy[2], slot[2];
+            int r[2], vx[2], vy[2], slot[2], bot[2], vyc[2];
             for (int l = 0; l < 2; ++l) {
                 r[l] = p->ref_idx[l * plane_n + idx];
                 uint32_t m = p->mv[l * plane_n + idx];
                 vx[l] = (mbx * 4 + i) * 16 + (int16_t)(m & 0xFFFF);
                 vy[l] = (mby * 4 + j) * 16 + (int16_t)(m >> 16);
-                slot[l] = r[l] >= 0 ? sl->ref_slot[l][r[l]] : -1;
+                int ref = r[l] >= 0 ? sl->ref_slot[l][r[l]] : -1;
+                /* a field picture's list entries name a field of a DPB frame (include/h264r.h) */
+                slot[l] = ref < 0 ? -1 : s->fld ? (ref & ~H264R_REF_BOTTOM) : ref;
+                bot[l] = s->fld && ref >= 0 && (ref & H264R_REF_BOTTOM);
+                /* get_block_chroma inter_prediction.cc:352-355: a reference field of the other
+                   parity moves the chroma vector by -2 (top field) / +2 (bottom field) */
+                vyc[l] = vy[l] + (s->fld && bot[l] != s->bot ? (s->bot ? 2 : -2) : 0);
             }
             int dir = (r[0] >= 0 && r[1] >= 0) ? 2 : (r[0] >= 0 ? 0 : (r[1] >= 0 ? 1 : -1));
             if (dir < 0) return H264R_EINVAL;
             for (int l = 0; l < 2; ++l)
-                if ((dir == 2 || dir == l) && (slot[l] < 0 || !p->ref_planes[slot[l]][0])) return H264R_EINVAL;
+                if ((dir == 2 || dir == l) && (slot[l] < 0 || slot[l] >= H264R_MAX_SLOTS || !p->ref_planes[slot[l]][0]))
+                    return H264R_EINVAL;
             for (int pl = 0; pl < 3; ++pl) {
                 int n = pl ? 2 : 4, ox = pl ? i * 2 : i * 4, oy = pl ? j * 2 : j * 4;
                 int Wp = pl ? s->Wc : s->W, Hp = pl ? s->Hc : s->H;
@@ -682,9 +692,10 @@ static int inter_pred_mb(const pstate* s, int addr, int mbp[3][16][16])
                         int v[2] = {0, 0};
                         for (int l = 0; l < 2; ++l) {
                             if (!(dir == 2 || dir == l)) continue;
-                            const uint8_t* img = p->ref_planes[slot[l]][pl];
-                            if (!pl) v[l] = luma_sample(img, Wp, Hp, (vx[l] >> 2) + x, (vy[l] >> 2) + y, vx[l] & 3, vy[l] & 3);
-                            else v[l] = chroma_sample(img, Wp, Hp, (vx[l] >> 3) + x, (vy[l] >> 3) + y, vx[l] & 7, vy[l] & 7);
+                            const uint8_t* img = p->ref_planes[slot[l]][pl] + bot[l] * Wp;
+                            const int pitch = Wp << s->fld;
+                            if (!pl) v[l] = luma_sample(img, Wp, pitch, Hp, (vx[l] >> 2) + x, (vy[l] >> 2) + y, vx[l] & 3, vy[l] & 3);
+                            else v[l] = chroma_sample(img, Wp, pitch, Hp, (vx[l] >> 3) + x, (vyc[l] >> 3) + y, vx[l] & 7, vyc[l] & 7);
                         }
                         int out;
                         if (dir != 2) {
@@ -996,21 +1007,24 @@ static mvinfo_t mvinfo(const pstate* s, int bx4, int by4)
     return m;
 }
 
-static inline int compare_mvs(const mvinfo_t* a, int la, const mvinfo_t* b, int lb)   /* deblock.cc:35-38 */
+/* deblock.cc:35-38; mvlimit = 2 in field pictures, 4 in frames (deblock.cc:86,164) */
+static inline int compare_mvs(const mvinfo_t* a, int la, const mvinfo_t* b, int lb, int mvlimit)
 {
-    return (iabs(a->mvx[la] - b->mvx[lb]) >= 4) | (iabs(a->mvy[la] - b->mvy[lb]) >= 4);
+    return (iabs(a->mvx[la] - b->mvx[lb]) >= 4) | (iabs(a->mvy[la] - b->mvy[lb]) >= mvlimit);
 }
 
-static int bs_compare_mvs(const mvinfo_t* p, const mvinfo_t* q)     /* deblock.cc:40-75 */
+/* deblock.cc:40-75; ref identity: the DPB slot with the field parity bit (the two fields of a
+   frame are different storable_pictures in the reference) */
+static int bs_compare_mvs(const mvinfo_t* p, const mvinfo_t* q, int ml)
 {
     int p0 = p->ref[0], q0 = q->ref[0], p1 = p->ref[1], q1 = q->ref[1];
     if ((p0 == q0 && p1 == q1) || (p0 == q1 && p1 == q0)) {
         if (p0 != p1) {
-            if (p0 == q0) return compare_mvs(p, 0, q, 0) | compare_mvs(p, 1, q, 1);
-            return compare_mvs(p, 0, q, 1) | compare_mvs(p, 1, q, 0);
+            if (p0 == q0) return compare_mvs(p, 0, q, 0, ml) | compare_mvs(p, 1, q, 1, ml);
+            return compare_mvs(p, 0, q, 1, ml) | compare_mvs(p, 1, q, 0, ml);
         }
-        return (compare_mvs(p, 0, q, 0) | compare_mvs(p, 1, q, 1)) &
-               (compare_mvs(p, 0, q, 1) | compare_mvs(p, 1, q, 0));
+        return (compare_mvs(p, 0, q, 0, ml) | compare_mvs(p, 1, q, 1, ml)) &
+               (compare_mvs(p, 0, q, 1, ml) | compare_mvs(p, 1, q, 0, ml));
     }
     return 1;
 }
@@ -1021,7 +1035,9 @@ static int is_special(const pstate* s, const h264r_mb* m)
     return t == H264R_SLICE_SP || t == H264R_SLICE_SI;
 }
 
-/* Deblock::strength + strength_vertical/horizontal (deblock.cc:78-289), frame pictures. */
+/* Deblock::strength + strength_vertical/horizontal (deblock.cc:78-289), frame and field
+   pictures (a field picture: mvlimit 2, and cond_bS4 = !field || verticalEdgeFlag,
+   deblock.cc:103-107,184-189, so its horizontal MB edges get bS 3 where a frame's get 4). */
 static void strength(pstate* s, int addr)
 {
     const h264r_mb* q = mb_at(s, addr);
@@ -1066,7 +1082,7 @@ static void strength(pstate* s, int addr)
                     else {
                         mvinfo_t mq = mvinfo(s, mbx * 4 + e, mby * 4 + y / 4);
                         mvinfo_t mp = mvinfo(s, mbx * 4 + e - 1, mby * 4 + y / 4);
-                        v = bs_compare_mvs(&mq, &mp);
+                        v = bs_compare_mvs(&mq, &mp, s->fld ? 2 : 4);
                     }
                     St[y] = (uint8_t)v;
                 }
@@ -1077,7 +1093,7 @@ static void strength(pstate* s, int addr)
             const h264r_mb* pm = e == 0 ? mb_at(s, U) : q;
             int special = is_special(s, pm) || is_special(s, q);
             int intra = qintra || (pm->flags & H264R_MBF_INTRA);
-            if (e == 0 && (special || intra)) memset(St, 4, 16);
+            if (e == 0 && !s->fld && (special || intra)) memset(St, 4, 16);
             else if (special || intra) memset(St, 3, 16);
             else if (e > 0 && pskip) memset(St, 0, 16);
             else {
@@ -1089,7 +1105,7 @@ static void strength(pstate* s, int addr)
                     else {
                         mvinfo_t mq = mvinfo(s, mbx * 4 + x4, mby * 4 + e);
                         mvinfo_t mp = mvinfo(s, mbx * 4 + x4, mby * 4 + e - 1);
-                        v = bs_compare_mvs(&mq, &mp);
+                        v = bs_compare_mvs(&mq, &mp, s->fld ? 2 : 4);
                     }
                     memset(St + 4 * x4, v, 4);
                 }
@@ -1171,6 +1187,7 @@ int oracle_deblock_picture(const oracle_picture* p)
     pstate s;
     s.p = p; s.wmb = p->width_mbs; s.hmb = p->height_mbs;
     s.W = s.wmb * 16; s.H = s.hmb * 16; s.Wc = s.wmb * 8; s.Hc = s.hmb * 8; s.W4 = s.wmb * 4; s.H4 = s.hmb * 4;
+    s.fld = p->pic->structure != H264R_FRAME; s.bot = p->pic->structure == H264R_BOTTOM_FIELD;
     int any = 0;
     for (int i = 0; i < p->pic->num_slices; ++i) any |= p->slices[i].deblock_idc != 1;
     if (!any) return 0;
@@ -1206,6 +1223,7 @@ int oracle_reconstruct_picture(const oracle_picture* p)
     memset(&s, 0, sizeof(s));
     s.p = p; s.wmb = p->width_mbs; s.hmb = p->height_mbs;
     s.W = s.wmb * 16; s.H = s.hmb * 16; s.Wc = s.wmb * 8; s.Hc = s.hmb * 8; s.W4 = s.wmb * 4; s.H4 = s.hmb * 4;
+    s.fld = p->pic->structure != H264R_FRAME; s.bot = p->pic->structure == H264R_BOTTOM_FIELD;
     s.slice_nr = malloc(sizeof(int16_t) * (size_t)n);
     if (!s.slice_nr) return H264R_ENOMEM;
     for (int a = 0; a < n; ++a) s.slice_nr[a] = -1;

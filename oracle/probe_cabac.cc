@@ -31,6 +31,7 @@ namespace vio {
 namespace h264 {
 extern const uint8_t pos2ctx_map8x8[];
 extern const uint8_t pos2ctx_last8x8[];
+extern const uint8_t pos2ctx_map8x8i[];
 extern const uint8_t pos2ctx_map4x4[];
 extern const uint8_t pos2ctx_map2x4c[];
 extern const uint8_t pos2ctx_last4x4[];
@@ -132,6 +133,7 @@ int main()
 
     // ---- residual context maps
     arr8("pos2ctx_map8x8", pos2ctx_map8x8, 64);
+    arr8("pos2ctx_map8x8_field", pos2ctx_map8x8i, 64);   // field-coded blocks (pos2ctx_map[1])
     arr8("pos2ctx_last8x8", pos2ctx_last8x8, 64);
     arr8("pos2ctx_map4x4", pos2ctx_map4x4, 16);
     arr8("pos2ctx_map2x4c", pos2ctx_map2x4c, 16);

@@ -16,9 +16,14 @@
  *
  * usage: ref_driver W H kind nslices idc offA offB t8 wp cip nrefs qpmin qpmax
  *                   pcm_permille intra_permille mvx mvy seed index out.yuv [recon_only
- *                   [lossless_permille [sp_slices]]]
+ *                   [lossless_permille [sp_slices [structure]]]]
  * lossless_permille > 0 sets sps.qpprime_y_zero_transform_bypass_flag (the synthetic
  * pictures then hold TransformBypassModeFlag MBs, interpret_mb.cc:804).
+ * structure 1 / 2 decodes a top / bottom FIELD picture of H MB rows (shr.field_pic_flag,
+ * frame_mbs_only_flag 0): its references are field storable_pictures split from the synthetic
+ * DPB frames of 2H rows (as dpb_split_field picture.cc:408-470 does), the coefficient push
+ * takes the reference's own field scan (Transform::inverse_scan_* read field_pic_flag,
+ * transform.cc:338-386), and deblock_filter runs on the field (exit_picture picture.cc:253).
  * Output: Y plane then Cb then Cr, 8-bit, unpadded.
  *
  * Timing mode (H264R_TIME_REPS=<n>): the reconstruction of the picture -- the
@@ -83,6 +88,10 @@ int main(int argc, char** argv)
     bool recon_only = argc > k && atoi(argv[k]) != 0;
     if (argc > k + 1) cfg.lossless_permille = atoi(argv[k + 1]);
     if (argc > k + 2) cfg.sp_slices = atoi(argv[k + 2]);
+    if (argc > k + 3) cfg.structure = atoi(argv[k + 3]);
+    const bool fld = cfg.structure != H264R_FRAME;
+    const PictureStructure pstruct = cfg.structure == H264R_TOP_FIELD ? TOP_FIELD
+                                   : cfg.structure == H264R_BOTTOM_FIELD ? BOTTOM_FIELD : FRAME;
 
     const int W = cfg.width_mbs, H = cfg.height_mbs, NMB = W * H, W4 = W * 4, PL = W4 * H * 4;
     std::vector<h264r_mb> mbs(NMB);
@@ -105,8 +114,9 @@ int main(int argc, char** argv)
     sps->chroma_format_idc = 1; sps->ChromaArrayType = 1;
     sps->SubWidthC = 2; sps->SubHeightC = 2; sps->MbWidthC = 8; sps->MbHeightC = 8;
     sps->BitDepthY = 8; sps->BitDepthC = 8;
-    sps->frame_mbs_only_flag = 1; sps->direct_8x8_inference_flag = 1;
-    sps->PicWidthInMbs = W; sps->FrameHeightInMbs = H;
+    sps->frame_mbs_only_flag = !fld; sps->direct_8x8_inference_flag = 1;
+    const int FH = fld ? 2 * H : H;                     /* FrameHeightInMbs */
+    sps->PicWidthInMbs = W; sps->FrameHeightInMbs = FH;
     sps->PicWidthInSamplesL = W * 16; sps->PicWidthInSamplesC = W * 8;
     sps->PicHeightInMapUnits = H; sps->PicSizeInMapUnits = W * H;
     sps->qpprime_y_zero_transform_bypass_flag = cfg.lossless_permille > 0;
@@ -134,26 +144,34 @@ int main(int argc, char** argv)
     vid->active_sps = sps; vid->active_pps = pps;
     vid->no_reference_picture = nullptr;
 
-    /* DPB: reference pictures, padded like exit_picture (picture.cc:258-259) */
-    std::vector<storable_picture*> refs(cfg.num_refs);
-    std::vector<uint8_t> ty(W * 16 * H * 16), tu(W * 8 * H * 8), tv(W * 8 * H * 8);
-    for (int s = 0; s < cfg.num_refs; ++s) {
-        storable_picture* r = new storable_picture(vid, FRAME, W * 16, H * 16, W * 8, H * 8, 1);
-        h264r_synth_refpic(cfg.seed, s, W, H, ty.data(), tu.data(), tv.data());
-        for (int y = 0; y < H * 16; ++y) for (int x = 0; x < W * 16; ++x) r->imgY[y][x] = ty[y * W * 16 + x];
-        for (int y = 0; y < H * 8; ++y) for (int x = 0; x < W * 8; ++x) {
-            r->imgUV[0][y][x] = tu[y * W * 8 + x];
-            r->imgUV[1][y][x] = tv[y * W * 8 + x];
+    /* DPB: reference pictures, padded like exit_picture (picture.cc:258-259); a field picture's
+       references are the fields of the DPB frames, refs[2 s + bottom] */
+    const int nfr = h264r_synth_ref_frames(&cfg);
+    std::vector<storable_picture*> refs(fld ? 2 * nfr : nfr);
+    std::vector<uint8_t> ty(W * 16 * FH * 16), tu(W * 8 * FH * 8), tv(W * 8 * FH * 8);
+    for (int s = 0; s < nfr; ++s) {
+        h264r_synth_refpic(cfg.seed, s, W, FH, ty.data(), tu.data(), tv.data());
+        for (int f = 0; f < (fld ? 2 : 1); ++f) {
+            storable_picture* r = new storable_picture(vid, fld ? (f ? BOTTOM_FIELD : TOP_FIELD) : FRAME,
+                                                       W * 16, FH * 16, W * 8, FH * 8, 1);
+            const int step = fld ? 2 : 1;                /* dpb_split_field: every second row */
+            for (int y = 0; y < H * 16; ++y) for (int x = 0; x < W * 16; ++x) r->imgY[y][x] = ty[(y * step + f) * W * 16 + x];
+            for (int y = 0; y < H * 8; ++y) for (int x = 0; x < W * 8; ++x) {
+                r->imgUV[0][y][x] = tu[(y * step + f) * W * 8 + x];
+                r->imgUV[1][y][x] = tv[(y * step + f) * W * 8 + x];
+            }
+            pad_buf(*r->imgY, W * 16, H * 16, r->iLumaStride, MCBUF_LUMA_PAD_X, MCBUF_LUMA_PAD_Y);
+            pad_buf(*r->imgUV[0], W * 8, H * 8, r->iChromaStride, MCBUF_CHROMA_PAD_X, MCBUF_CHROMA_PAD_Y);
+            pad_buf(*r->imgUV[1], W * 8, H * 8, r->iChromaStride, MCBUF_CHROMA_PAD_X, MCBUF_CHROMA_PAD_Y);
+            r->poc = r->frame_poc = r->top_poc = r->bottom_poc = h264r_synth_slot_poc(s) + f;
+            r->is_long_term = 0; r->used_for_reference = 1;
+            refs[fld ? 2 * s + f : s] = r;
         }
-        pad_buf(*r->imgY, W * 16, H * 16, r->iLumaStride, MCBUF_LUMA_PAD_X, MCBUF_LUMA_PAD_Y);
-        pad_buf(*r->imgUV[0], W * 8, H * 8, r->iChromaStride, MCBUF_CHROMA_PAD_X, MCBUF_CHROMA_PAD_Y);
-        pad_buf(*r->imgUV[1], W * 8, H * 8, r->iChromaStride, MCBUF_CHROMA_PAD_X, MCBUF_CHROMA_PAD_Y);
-        r->poc = r->frame_poc = r->top_poc = r->bottom_poc = h264r_synth_slot_poc(s);
-        r->is_long_term = 0; r->used_for_reference = 1;
-        refs[s] = r;
     }
+    /* RefPicList entry -> storable_picture (include/h264r.h: slot | H264R_REF_BOTTOM for fields) */
+    auto ref_of = [&](int v) { return fld ? refs[2 * (v & 31) + ((v & H264R_REF_BOTTOM) ? 1 : 0)] : refs[v]; };
 
-    storable_picture* dec = new storable_picture(vid, FRAME, W * 16, H * 16, W * 8, H * 8, 1);
+    storable_picture* dec = new storable_picture(vid, pstruct, W * 16, FH * 16, W * 8, FH * 8, 1);
     dec->sps = sps; dec->pps = pps;
     dec->used_for_reference = 1;
     dec->poc = dec->frame_poc = pic.poc;
@@ -170,7 +188,8 @@ int main(int argc, char** argv)
         x->p_Vid = vid; x->active_sps = sps; x->active_pps = pps;
         shr_t& h = x->header;
         h.slice_type = c.slice_type;
-        h.structure = FRAME; h.MbaffFrameFlag = 0; h.field_pic_flag = 0;
+        h.structure = pstruct; h.MbaffFrameFlag = 0; h.field_pic_flag = fld;
+        h.bottom_field_flag = pstruct == BOTTOM_FIELD;
         h.PicHeightInMbs = H; h.PicHeightInSamplesL = H * 16; h.PicHeightInSamplesC = H * 8;
         h.PicSizeInMbs = W * H;
         h.disable_deblocking_filter_idc = c.deblock_idc;
@@ -190,7 +209,7 @@ int main(int argc, char** argv)
             }
         for (int l = 0; l < 2; ++l) {
             x->RefPicSize[l] = (char)c.num_ref[l];
-            for (int i = 0; i < c.num_ref[l]; ++i) x->RefPicList[l][i] = refs[c.ref_slot[l][i]];
+            for (int i = 0; i < c.num_ref[l]; ++i) x->RefPicList[l][i] = ref_of(c.ref_slot[l][i]);
         }
         x->current_slice_nr = (short)s;
         x->dec_picture = dec;
@@ -221,6 +240,20 @@ int main(int argc, char** argv)
     int inv4[16], inv8[64];
     zigzag(4, inv4);
     zigzag(8, inv8);
+    if (fld) {
+        /* the field scans (Tables 8-13 / 8-14) as the reference maps them: raster position of
+           each scan index from its own Transform::inverse_scan_luma_ac on a field slice */
+        mb_t probe;
+        memset((void*)&probe, 0, sizeof(probe));
+        probe.p_Slice = sl[0];
+        for (int t8 = 0; t8 < 2; ++t8) {
+            probe.transform_size_8x8_flag = t8;
+            for (int k = 0; k < (t8 ? 64 : 16); ++k) {
+                const pos_t pos = sl[0]->decoder.transform->inverse_scan_luma_ac(&probe, k);
+                (t8 ? inv8 : inv4)[pos.y * (t8 ? 8 : 4) + pos.x] = k;
+            }
+        }
+    }
 
     const char* reps_env = getenv("H264R_TIME_REPS");
     const int reps = reps_env ? atoi(reps_env) : 1;

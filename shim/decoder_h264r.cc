@@ -40,6 +40,16 @@
  *
  * Reconstruction is deferred to picture end: the parser never reads reconstructed
  * samples (only syntax and mv_info), so the result is the same.
+ *
+ * Field pictures (PAFF, field_pic_flag; MBAFF frames stay H264R_EUNSUPPORTED): the reference
+ * decodes a field into a field storable_picture of half the frame's rows and deblocks it on
+ * its own (exit_picture picture.cc:239-269), splits decoded frames into field views
+ * (dpb_split_field picture.cc:408-470) and combines decoded field pairs into frames
+ * (dpb_combine_field_yuv :573-590).  On the device a DPB slot is a frame: a decoded field is
+ * kept in its parity's rows of a slot -- the second field of a pair in its first field's slot
+ * (the pairing test of store_picture dpb.cc:903-912) -- and a reference list entry names a
+ * slot (frame) or a slot's field (slot | H264R_REF_BOTTOM), found from whichever of a frame
+ * store's pictures (frame, top_field, bottom_field) the shim decoded.
  * Errors: a status other than H264R_OK goes through the reference's own error()
  * (ldecod.cc:33-48), its convention for fatal conditions.
  */
@@ -101,7 +111,11 @@ struct Shim {
     // belongs to is initialised (slice_header.cc:185 vs :195): its tables wait here until
     // init(slice) attaches the slice to its picture
     std::map<const slice_t*, h264r_quant> pending_quant;
-    std::map<const storable_picture*, int> slot_of;   // reference pictures resident on the device
+    // decoded reference pictures resident on the device: their slot and the identity they had
+    // when decoded (a picture the reference has freed may share its address with a later
+    // split field or combined frame; the identity check keeps such an entry from matching)
+    struct Resident { int slot; int structure; int poc; unsigned frame_num; };
+    std::map<const storable_picture*, Resident> slot_of;
     int next_slot = 0;
     std::vector<uint8_t> y8, u8, v8;
 };
@@ -131,15 +145,51 @@ int slice_index(Shim& S, slice_t* sl)
     return -1;
 }
 
+// The slot of a picture the shim decoded (NULL, the reference's no_reference_picture and
+// pictures it did not decode: -1).
+int decoded_slot(const Shim& S, const storable_picture* p)
+{
+    if (!p) return -1;
+    auto it = S.slot_of.find(p);
+    if (it == S.slot_of.end()) return -1;
+    const Shim::Resident& r = it->second;
+    if (r.structure != p->slice.structure || r.poc != p->poc || r.frame_num != p->frame_num) return -1;
+    return r.slot;
+}
+
+// The device reference of a RefPicList entry: a frame picture's entry is a frame -- decoded as
+// one, or combined from two decoded fields (its top_field / bottom_field); a field picture's is
+// a field -- decoded as one, or split from a decoded frame (its `frame`) -- named by its slot and
+// parity (include/h264r.h H264R_REF_BOTTOM).  -1 if none is resident.
+int device_ref(const Shim& S, const storable_picture* p, bool field_pic)
+{
+    if (!p) return -1;
+    const int st = p->slice.structure;
+    int slot = -1;
+    if (field_pic) {
+        if (st == FRAME) return -1;
+        slot = decoded_slot(S, p);
+        if (slot < 0 && p->frame != p && p->frame && p->frame->slice.structure == FRAME) slot = decoded_slot(S, p->frame);
+        return slot < 0 ? -1 : slot | (st == BOTTOM_FIELD ? H264R_REF_BOTTOM : 0);
+    }
+    if (st != FRAME) return -1;
+    slot = decoded_slot(S, p);
+    if (slot < 0 && p->top_field != p && p->top_field) slot = decoded_slot(S, p->top_field);
+    if (slot < 0 && p->bottom_field != p && p->bottom_field) slot = decoded_slot(S, p->bottom_field);
+    return slot;
+}
+
 // Start staging picture `pic` when the first of its slices arrives.
 void begin_picture(Shim& S, slice_t& slice)
 {
     storable_picture* pic = slice.dec_picture;
     if (S.pic == pic) return;
     const sps_t& sps = *slice.active_sps;
-    if (sps.chroma_format_idc != 1 || sps.BitDepthY != 8 || sps.BitDepthC != 8 || !sps.frame_mbs_only_flag)
-        check(H264R_EUNSUPPORTED, "picture format (4:2:0, 8-bit, frame pictures only)");
-    const int W = sps.PicWidthInMbs, H = sps.FrameHeightInMbs;
+    if (sps.chroma_format_idc != 1 || sps.BitDepthY != 8 || sps.BitDepthC != 8)
+        check(H264R_EUNSUPPORTED, "picture format (4:2:0, 8-bit)");
+    if (slice.header.MbaffFrameFlag) check(H264R_EUNSUPPORTED, "MBAFF frames");
+    // the context holds frames; a field picture is PicHeightInMbs = FrameHeightInMbs / 2 rows
+    const int W = sps.PicWidthInMbs, H = sps.FrameHeightInMbs, PH = slice.header.PicHeightInMbs;
     if (!S.ctx || W > S.ctx_w || H > S.ctx_h) {
         if (S.ctx) h264r_destroy(S.ctx);
         S.ctx = nullptr;
@@ -151,8 +201,8 @@ void begin_picture(Shim& S, slice_t& slice)
     S.pic = pic;
     S.slices.clear();
     S.slice_tab.clear();
-    S.mbs.assign((size_t)W * H, StagedMb());
-    S.seen.assign((size_t)W * H, 0);
+    S.mbs.assign((size_t)W * PH, StagedMb());
+    S.seen.assign((size_t)W * PH, 0);
     S.have_quant = false;
 }
 
@@ -163,7 +213,7 @@ h264r_slice slice_record(Shim& S, slice_t& slice)
     const pps_t& pps = *slice.active_pps;
     h264r_slice r;
     memset(&r, 0, sizeof(r));
-    if (shr.MbaffFrameFlag || shr.field_pic_flag) check(H264R_EUNSUPPORTED, "MBAFF / field slices");
+    if (shr.MbaffFrameFlag) check(H264R_EUNSUPPORTED, "MBAFF slices");
     // SI MBs go through mb_pred_inter in the reference with an out-of-range BLOCK_STEP row
     // (decoder.cc:141-146, 212-225): nothing defined to reproduce
     if (shr.slice_type == SI_slice) check(H264R_EUNSUPPORTED, "SI slices");
@@ -188,9 +238,9 @@ h264r_slice slice_record(Shim& S, slice_t& slice)
                 // every picture of a reference list must be resident: a missing one would be
                 // predicted as the reference's no_ref grey (inter_prediction.cc:164-167) --
                 // fail loudly instead
-                auto it = S.slot_of.find(slice.RefPicList[l][i]);
-                if (it == S.slot_of.end()) check(H264R_ESTATE, "reference picture not resident in a device DPB slot");
-                r.ref_slot[l][i] = (int8_t)it->second;
+                const int ref = device_ref(S, slice.RefPicList[l][i], shr.field_pic_flag);
+                if (ref < 0) check(H264R_ESTATE, "reference picture not resident in a device DPB slot");
+                r.ref_slot[l][i] = (int8_t)ref;
             }
             for (int pl = 0; pl < 3; ++pl) {
                 const auto& v = shr.pred_weight_l[l][pl];
@@ -474,7 +524,9 @@ void Decoder::deblock_filter(slice_t& slice)
     if (S.pic != pic) check(H264R_ESTATE, "deblock_filter() of a picture that was not staged");
     const sps_t& sps = *slice.active_sps;
     const pps_t& pps = *slice.active_pps;
-    const int W = sps.PicWidthInMbs, H = sps.FrameHeightInMbs;
+    const shr_t& shr = slice.header;
+    const int W = sps.PicWidthInMbs, H = shr.PicHeightInMbs;        // a field: half the frame's rows
+    const bool fld = shr.field_pic_flag;
     if (!S.have_quant) {
         h264r_quant q;
         check(h264r_quant_init_flat(&q), "h264r_quant_init_flat");
@@ -485,6 +537,7 @@ void Decoder::deblock_filter(slice_t& slice)
     p.constrained_intra_pred = pps.constrained_intra_pred_flag;
     p.num_slices = (int)S.slice_tab.size();
     p.poc = pic->poc;
+    p.structure = !fld ? H264R_FRAME : shr.bottom_field_flag ? H264R_BOTTOM_FIELD : H264R_TOP_FIELD;
     check(h264r_picture_begin(S.ctx, W, H, &p, S.slice_tab.data(), &S.quant), "h264r_picture_begin");
     for (int a = 0; a < W * H; ++a) {
         if (!S.seen[a]) check(H264R_ESTATE, "picture with missing macroblocks (concealment is CPU-only)");
@@ -493,19 +546,36 @@ void Decoder::deblock_filter(slice_t& slice)
                               &st.mv[0][0], &st.ref[0][0]), "h264r_mb_submit");
     }
     int keep = -1;
-    if (pic->used_for_reference) {
-        // a device slot no reference of the DPB holds: the frames of fs_ref / fs_ltref
+    const dpb_t* dpb = slice.p_Dpb;
+    // an IDR picture empties the DPB (idr_memory_management, store_picture dpb.cc:888-891):
+    // nothing resident before it can be referenced again
+    if (pic->slice.idr_flag) S.slot_of.clear();
+    if (pic->used_for_reference && fld && dpb && dpb->last_picture) {
+        // the second field of a pair goes into its first field's slot: the pairing test of
+        // store_picture (dpb.cc:903-912) -- the stored field of the opposite parity, the same
+        // frame number, both reference fields
+        const pic_t* fs = dpb->last_picture;
+        const bool opposite = (pic->slice.structure == TOP_FIELD && fs->is_used == 2) ||
+                              (pic->slice.structure == BOTTOM_FIELD && fs->is_used == 1);
+        if ((int)fs->FrameNum == pic->PicNum && opposite && fs->is_orig_reference != 0)
+            keep = decoded_slot(S, fs->is_used == 1 ? fs->top_field : fs->bottom_field);
+    }
+    if (pic->used_for_reference && keep < 0) {
+        // a device slot no reference of the DPB holds: the frame stores of fs_ref / fs_ltref
         // (dpb.h:30-36) as they stand before this picture is stored (exit_picture ->
         // store_picture, picture.cc:253-269; its own marking can only free more), searched
         // round robin from the last slot given out.  The DPB holds <= 16 reference frames,
         // so one of the 32 slots is always free -- a long-term reference keeps its slot for
         // as long as it stays in the DPB.
         bool busy[H264R_MAX_SLOTS] = {};
-        const dpb_t* dpb = slice.p_Dpb;
         auto mark = [&](pic_t* fs) {
-            if (!fs || !fs->frame) return;
-            auto it = S.slot_of.find(fs->frame);
-            if (it != S.slot_of.end()) busy[it->second] = true;
+            if (!fs) return;
+            for (const storable_picture* q : {fs->frame, fs->top_field, fs->bottom_field}) {
+                int s = -1;
+                if (q && q->slice.structure == FRAME) s = device_ref(S, q, false);
+                else if (q) s = device_ref(S, q, true) & ~H264R_REF_BOTTOM;
+                if (s >= 0) busy[s] = true;
+            }
         };
         for (unsigned i = 0; dpb && i < dpb->ref_frames_in_buffer; ++i) mark(dpb->fs_ref[i]);
         for (unsigned i = 0; dpb && i < dpb->ltref_frames_in_buffer; ++i) mark(dpb->fs_ltref[i]);
@@ -514,14 +584,14 @@ void Decoder::deblock_filter(slice_t& slice)
         if (keep < 0) check(H264R_EUNSUPPORTED, "more than 32 reference frames resident");
         S.next_slot = (keep + 1) % H264R_MAX_SLOTS;
         for (auto it = S.slot_of.begin(); it != S.slot_of.end();)
-            it = it->second == keep ? S.slot_of.erase(it) : std::next(it);
+            it = it->second.slot == keep ? S.slot_of.erase(it) : std::next(it);
     }
     S.y8.resize((size_t)W * H * 256);
     S.u8.resize((size_t)W * H * 64);
     S.v8.resize((size_t)W * H * 64);
     check(h264r_picture_end(S.ctx, S.y8.data(), S.u8.data(), S.v8.data(), keep), "h264r_picture_end");
     S.slot_of.erase(pic);
-    if (keep >= 0) S.slot_of[pic] = keep;
+    if (keep >= 0) S.slot_of[pic] = Shim::Resident{keep, pic->slice.structure, pic->poc, pic->frame_num};
     for (int y = 0; y < H * 16; ++y)
         for (int x = 0; x < W * 16; ++x) pic->imgY[y][x] = S.y8[(size_t)y * W * 16 + x];
     for (int y = 0; y < H * 8; ++y)

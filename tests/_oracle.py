@@ -145,7 +145,7 @@ def run_reference(cfg: A.SynthCfg, index: int, recon_only: bool = False, time_re
                 cfg.filter_offset_b, cfg.transform8x8, cfg.wp_mode, cfg.constrained_intra,
                 cfg.num_refs, cfg.qp_min, cfg.qp_max, cfg.pcm_permille, cfg.intra_permille,
                 cfg.mv_range_x, cfg.mv_range_y, hex(cfg.seed), index, out, int(recon_only),
-                cfg.lossless_permille, cfg.sp_slices]
+                cfg.lossless_permille, cfg.sp_slices, cfg.structure]
         env = dict(os.environ)
         if time_reps:
             env["H264R_TIME_REPS"] = str(time_reps)

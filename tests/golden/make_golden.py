@@ -79,6 +79,24 @@ CASES = [
     ("b_qcif_scaling", 4, 11, 9, dict(qm=11), [0]),
     ("b_1080p_4slices_scaling", 4, 120, 68, dict(qm=12), [0]),
     ("b_2160p_strip_scaling", 5, 240, 8, dict(num_slices=2, qm=13), [0]),
+    # field pictures (PAFF; include/h264r.h H264R_TOP_FIELD): H is the field's MB rows, the
+    # references are fields of DPB frames of 2H rows (both parities, chroma offset
+    # inter_prediction.cc:352-355), mvlimit 2 and bS 3 on horizontal MB edges (deblock.cc:86-189)
+    ("ifield_cif_top", 2, 22, 9, dict(structure=1, pcm_permille=20), [0]),
+    ("ifield_cif_bottom_4x4_cip", 2, 22, 9, dict(structure=2, transform8x8=0, constrained_intra=1), [0]),
+    ("pfield_cif_top", 3, 22, 9, dict(structure=1, num_refs=4), [0, 1]),
+    ("pfield_cif_bottom_pcm", 3, 22, 9, dict(structure=2, num_refs=3, pcm_permille=30, intra_permille=200), [0, 1]),
+    ("pfield_qcif_wp_bottom", 3, 11, 4, dict(structure=2, wp_mode=1, num_refs=4), [0]),
+    ("pfield_cif_cip_3slices_idc2", 3, 22, 9, dict(structure=1, constrained_intra=1, intra_permille=400,
+                                                   num_slices=3, deblock_idc=2), [0]),
+    ("pfield_cif_sp", 3, 22, 9, dict(structure=2, sp_slices=1, num_refs=2), [0]),
+    ("bfield_cif_top_implicit", 4, 22, 9, dict(structure=1, num_refs=4, num_slices=2), [0, 1]),
+    ("bfield_cif_bottom_explicit", 4, 22, 9, dict(structure=2, wp_mode=1, num_refs=6), [0]),
+    ("bfield_cif_bottom_bigmv", 4, 22, 9, dict(structure=2, wp_mode=0, mv_range_x=200, mv_range_y=100,
+                                               num_slices=1, deblock_idc=0), [0]),
+    ("bfield_qcif_lossless", 4, 11, 4, dict(structure=1, qp_min=0, qp_max=20, lossless_permille=500), [0]),
+    ("pfield_1080i_top", 3, 120, 34, dict(structure=1), [0]),
+    ("bfield_1080i_bottom_scaling", 4, 120, 34, dict(structure=2, qm=16), [0]),
 ]
 
 

@@ -32,6 +32,12 @@ RANGE_LPS = _T["rangeTabLPS"]
 TRANS_LPS = _T["transIdxLPS"]
 TRANS_MPS = _T["transIdxMPS"]
 POS_MAP = {"4x4": _T["pos2ctx_map4x4"], "8x8": _T["pos2ctx_map8x8"], "2x4c": _T["pos2ctx_map2x4c"]}
+# field pictures (shr.field_pic_flag): the significance maps of the second context sets
+# map_contexts[1] / last_contexts[1] and, for 8x8 blocks, the field position map
+# (interpret_residual.cc:353-358; bitstream_cabac.h:78-79)
+POS_MAP_FIELD = dict(POS_MAP, **{"8x8": _T["pos2ctx_map8x8_field"]})
+_NFIELD = {name: count for name, _first, count in _T["fields"]}
+MAP_SET, LAST_SET = _NFIELD["map_contexts"] // 2, _NFIELD["last_contexts"] // 2
 POS_LAST = {"4x4": _T["pos2ctx_last4x4"], "8x8": _T["pos2ctx_last8x8"], "2x4c": _T["pos2ctx_last2x4c"]}
 T2C_BCBP, T2C_MAP, T2C_ONE = _T["type2ctx_bcbp"], _T["type2ctx_map"], _T["type2ctx_one"]
 
@@ -133,8 +139,9 @@ class CabacSink:
     """The writer's syntax elements as CABAC bins (see the module docstring).  `enc` is the
     h264_writer.Encoder (its MB array holds the state the context selection reads)."""
 
-    def __init__(self, enc, bits: list, ptype: str, qp: int, init_idc: int, s: int):
+    def __init__(self, enc, bits: list, ptype: str, qp: int, init_idc: int, s: int, field: bool = False):
         self.e = enc
+        self.field = field
         self.ptype = ptype
         self.s = s
         self.a = 0
@@ -464,12 +471,13 @@ class CabacSink:
         m_cur.cbp_bits |= (0x33 if typ == LUMA_8x8 else 0x01) << (bit + (j * 4 + i if ac else 0))
         n = len(coeffs)
         last = max(k for k, v in enumerate(coeffs) if v)
-        pm, pl_ = POS_MAP[_POS[typ]], POS_LAST[_POS[typ]]
+        pm, pl_ = (POS_MAP_FIELD if self.field else POS_MAP)[_POS[typ]], POS_LAST[_POS[typ]]
+        fm, fl = (MAP_SET, LAST_SET) if self.field else (0, 0)
         for k in range(n - 1):
             sig = 1 if coeffs[k] else 0
-            self._dec("map_contexts", T2C_MAP[typ] + pm[k], sig)
+            self._dec("map_contexts", fm + T2C_MAP[typ] + pm[k], sig)
             if sig:
-                self._dec("last_contexts", T2C_MAP[typ] + pl_[k], 1 if k == last else 0)
+                self._dec("last_contexts", fl + T2C_MAP[typ] + pl_[k], 1 if k == last else 0)
                 if k == last:
                     break
         eq1 = gt1 = 0

@@ -145,6 +145,11 @@ class StreamCfg:
     l1_refs: int = 2                 # max num_ref_idx_l1_active of B slices
     cabac: int = 0                   # entropy_coding_mode_flag (CABAC, tests/h264_cabac.py; Main / High)
     cabac_init: tuple = (0, 1, 2)    # cabac_init_idc choices per P / B slice
+    field: float = 0.0               # > 0: frame_mbs_only_flag 0 and this share of the frames coded as two
+                                     # field pictures (PAFF: field_pic_flag, the second field in the
+                                     # first's frame; 1.0 = every frame); P fields predict from any
+                                     # reference field (the first field of their own frame too)
+    bottom_first: float = 0.0        # share of field pairs sent bottom field first
     long_term: int = 0               # the IDR is a long-term reference (LongTermFrameIdx 0) kept for the
                                      # whole stream, and P picture `long_term` becomes a second one by
                                      # MMCO 4 + 6 (LongTermFrameIdx 1); P pictures predict from them
@@ -182,6 +187,8 @@ class Encoder:
         self.c = cfg
         self.rng = random.Random(cfg.seed)
         self.W, self.H = cfg.width_mbs, cfg.height_mbs
+        self.FH = cfg.height_mbs                 # frame height; a field picture has FH / 2 MB rows
+        assert not cfg.field or cfg.height_mbs % 2 == 0
         self.log2_max_frame_num = 4
         self.log2_max_poc_lsb = 8
         self.cab = None                  # the CABAC sink of the slice being written (CABAC streams)
@@ -209,8 +216,13 @@ class Encoder:
         w.ue(c.num_refs)                            # max_num_ref_frames
         w.u(1, 0)                                   # gaps_in_frame_num_value_allowed_flag
         w.ue(self.W - 1)
-        w.ue(self.H - 1)
-        w.u(1, 1)                                   # frame_mbs_only_flag
+        if c.field:
+            w.ue(self.FH // 2 - 1)                  # pic_height_in_map_units_minus1 (field MB rows)
+            w.u(1, 0)                               # frame_mbs_only_flag
+            w.u(1, 0)                               # mb_adaptive_frame_field_flag (PAFF only)
+        else:
+            w.ue(self.H - 1)
+            w.u(1, 1)                               # frame_mbs_only_flag
         w.u(1, 1)                                   # direct_8x8_inference_flag
         crop = any(c.crop)
         w.u(1, 1 if crop else 0)
@@ -808,16 +820,20 @@ class Encoder:
                 else:
                     w.u(1, 0)
 
-    def picture(self, idx: int, idr: bool, kind: str | None = None, ref_idc: int = 3, poc: int = 0):
+    def picture(self, idx: int, idr: bool, kind: str | None = None, ref_idc: int = 3, poc: int = 0,
+                structure: int = 0, second: bool = False, nref_field: int = 0):
         """NAL units of picture idx: one per slice.  kind None = I (idr) or P; "B" writes a
-        B picture (nal_ref_idc = ref_idc, POC lsb from poc)."""
+        B picture (nal_ref_idc = ref_idc, POC lsb from poc).  structure 1 / 2: a top / bottom
+        field picture (field_pic_flag, bottom_field_flag; FH / 2 MB rows), `second` the second
+        field of its frame (same frame_num), `nref_field` its num_ref_idx_l0_active."""
         c, r = self.c, self.rng
+        self.H = self.FH // 2 if structure else self.FH
         n = self.W * self.H
         self.mbs = [_Mb() for _ in range(n)]
         ptype = kind or ("I" if idr else "P")
         sp = ptype == "P" and c.sp > 0 and r.random() < c.sp   # (no draw otherwise: fixed streams stay)
         starts = sorted({0} | set(r.sample(range(1, n), min(c.slices - 1, n - 1)))) if c.slices > 1 else [0]
-        frame_num = 0 if idr else (self.frame_num + 1) % (1 << self.log2_max_frame_num)
+        frame_num = 0 if idr else (self.frame_num + (0 if second else 1)) % (1 << self.log2_max_frame_num)
         tracked = bool(c.bframes or c.long_term)           # DPB bookkeeping of the IBBP / long-term streams
         if tracked and not idr:
             frame_num = (self.prev_ref_fn + 1) % (1 << self.log2_max_frame_num)
@@ -843,11 +859,17 @@ class Encoder:
             w.ue(7 if ptype == "I" else (8 if sp else (6 if ptype == "B" else 5)))   # slice_type (all slices alike)
             w.ue(0)                                 # pic_parameter_set_id
             w.u(self.log2_max_frame_num, frame_num)
+            if c.field:
+                w.u(1, 1 if structure else 0)       # field_pic_flag
+                if structure:
+                    w.u(1, 1 if structure == 2 else 0)   # bottom_field_flag
             if idr:
                 w.ue(idx % 2)                       # idr_pic_id
             if c.bframes:
                 w.u(self.log2_max_poc_lsb, poc % (1 << self.log2_max_poc_lsb))   # pic_order_cnt_lsb
             nref = self.refs if not tracked else (self.refs_p if c.bframes else avail)
+            if structure:
+                nref = nref_field
             if ptype == "B":
                 w.u(1, r.choice(c.direct))          # direct_spatial_mv_pred_flag
                 w.u(1, 1)                           # num_ref_idx_active_override_flag
@@ -901,7 +923,7 @@ class Encoder:
             if c.cabac:
                 while not w.aligned():
                     w.u(1, 1)                       # cabac_alignment_one_bit
-                self.cab = CB.CabacSink(self, w.bits, ptype, sqp, init_idc, s)
+                self.cab = CB.CabacSink(self, w.bits, ptype, sqp, init_idc, s, field=structure != 0)
                 for a in range(first, end):
                     self._mb(w, a, ptype, s, nref_b if ptype == "B" else nref)
                     self.cab.end_of_slice(a == end - 1)   # the flush's last bit is rbsp_stop_one_bit
@@ -932,6 +954,8 @@ class Encoder:
         c = self.c
         out = [self.sps(), self.pps()]
         self.frame_num, self.refs, self.prev_ref_fn, self.st, self.lt = 0, 0, 0, 0, 0
+        if c.field:
+            return b"".join(out + self._field_stream())
         if not c.bframes:
             for i in range(c.frames):
                 out += self.picture(i, idr=(i == 0 or c.all_intra))
@@ -951,6 +975,35 @@ class Encoder:
                 ref_idc = 2 if self.rng.random() < c.b_ref else 0
             out += self.picture(i, idr=(i == 0), kind=kind, ref_idc=ref_idc, poc=2 * disp)
         return b"".join(out)
+
+
+    def _field_stream(self) -> list:
+        """PAFF, pic_order_cnt_type 2 (output = decoding order): each frame a frame picture
+        or, with probability c.field, a pair of field pictures; every picture a reference.
+        A field's list holds the reference FIELDS (8.2.4.2.5): two per reference frame in
+        the DPB, and for the second field of a pair also the first field; the sliding window
+        counts frames, and the first field's frame counts from when it is stored."""
+        c, r = self.c, self.rng
+        out, nfr = [], 0                        # reference frames in the DPB
+        for i in range(c.frames):
+            idr = i == 0 or c.all_intra
+            fld = c.field >= 1.0 or r.random() < c.field
+            if not fld:
+                self.refs = max(nfr - 1, 0)         # picture() counts this frame's list as refs + 1
+                out += self.picture(i, idr=idr)
+                nfr = 1 if idr else min(nfr + 1, c.num_refs)
+                continue
+            first = 2 if c.bottom_first and r.random() < c.bottom_first else 1
+            n1 = 0 if idr else min(2 * nfr, H264R_MAX_FIELD_REFS)
+            out += self.picture(i, idr=idr, structure=first, nref_field=n1)
+            nfr = 1 if idr else min(nfr + 1, c.num_refs)
+            n2 = min(2 * (nfr - 1) + 1, H264R_MAX_FIELD_REFS)
+            out += self.picture(i, idr=False, kind="I" if c.all_intra else "P", structure=3 - first,
+                                second=True, nref_field=n2)
+        return out
+
+
+H264R_MAX_FIELD_REFS = 16                  # the reconstruction ABI's list length (include/h264r.h)
 
 
 class _Deferred:

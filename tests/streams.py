@@ -87,6 +87,21 @@ STREAMS = {
     # along: more reference pictures than device DPB slots over the stream's life
     "bp_qcif_longterm_40": dict(width_mbs=11, height_mbs=9, frames=40, seed=204, num_refs=4, long_term=2, skip=0.3,
                                 intra_in_p=0.05),
+    # field pictures (PAFF, frame_mbs_only_flag 0): every frame or a share of them as a top + bottom field
+    # pair (some bottom first), P fields predicting from reference fields of both parities -- the first
+    # field of their own frame too --, frame pictures predicting from frames decoded as field pairs
+    "mp_cif_paff_cavlc": dict(width_mbs=22, height_mbs=18, frames=6, seed=501, profile=77, field=1.0, num_refs=3,
+                              slices=2, deblock=(0, 2), offsets=3, intra_in_p=0.15, pcm=0.03),
+    "hp_cif_paff_mixed_wp_8x8": dict(width_mbs=22, height_mbs=18, frames=8, seed=502, profile=100, transform8x8=1,
+                                     field=0.5, bottom_first=0.4, num_refs=4, weighted=1, deblock=(0, 1, 2),
+                                     offsets=4),
+    "mp_cif_cabac_paff": dict(width_mbs=22, height_mbs=18, frames=6, seed=503, profile=77, cabac=1, field=0.7,
+                              num_refs=3, slices=3, cip=1, pcm=0.04, deblock=(0, 2)),
+    "hp_cif_cabac_paff_8x8_scaling": dict(width_mbs=22, height_mbs=18, frames=5, seed=504, profile=100,
+                                          transform8x8=1, cabac=1, field=1.0, bottom_first=0.5, num_refs=2,
+                                          scaling=1, qp=(12, 40)),
+    "hp_1080i_cabac_paff": dict(width_mbs=120, height_mbs=68, frames=2, seed=505, profile=100, transform8x8=1,
+                                cabac=1, field=1.0, num_refs=2, slices=4, deblock=(0, 2), crop=(0, 0, 0, 2)),
 }
 
 CAP_MAGIC = 0x43523448
@@ -102,8 +117,45 @@ def capture_path(name: str) -> str:
 
 
 def crop_of(cfg: dict) -> OUT.Crop:
+    """The SPS crop of a stream; its vertical unit is two chroma rows when the stream may
+    hold field pictures (frame_mbs_only_flag 0, CropUnitY = SubHeightC * 2)."""
     l, r, t, b = cfg.get("crop", (0, 0, 0, 0))
-    return OUT.Crop(left=l, right=r, top=t, bottom=b)
+    return OUT.Crop(left=l, right=r, top=t, bottom=b, frame_mbs_only=0 if cfg.get("field") else 1)
+
+
+def structure(p: dict) -> int:
+    return int(p["pic"]["structure"][0])
+
+
+def output_frames(pics: list[dict], outs: list) -> list:
+    """The decoded frames in output order.  A field pair (two consecutive field pictures of
+    opposite parity, as the writer sends them) becomes one frame of interleaved rows
+    (dpb_combine_field_yuv, picture.cc:573-590) with the smaller of its POCs; frames are
+    ordered by POC inside each IDR period (a new period at every POC 0 after the first frame)
+    -- the order the reference's DPB writes them (dpb.cc output process)."""
+    frames, i = [], 0
+    while i < len(pics):
+        st = structure(pics[i])
+        if st == A.FRAME:
+            frames.append((int(pics[i]["pic"]["poc"][0]), i, outs[i]))
+            i += 1
+            continue
+        j = i + 1
+        assert j < len(pics) and structure(pics[j]) == 3 - st, "an unpaired field"
+        top, bot = (outs[i], outs[j]) if st == A.TOP_FIELD else (outs[j], outs[i])
+        planes = []
+        for t, b in zip(top, bot):
+            f = np.empty((2 * t.shape[0], t.shape[1]), np.uint8)
+            f[0::2], f[1::2] = t, b
+            planes.append(f)
+        frames.append((min(int(pics[i]["pic"]["poc"][0]), int(pics[j]["pic"]["poc"][0])), i, tuple(planes)))
+        i += 2
+    keys, period = [], 0
+    for k, (poc, i, _) in enumerate(frames):
+        if k and poc == 0:
+            period += 1
+        keys.append((period, poc, k))
+    return [frames[k][2] for _, _, k in sorted(keys)]
 
 
 def output_order(pics: list[dict]) -> list[int]:

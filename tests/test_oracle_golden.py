@@ -52,6 +52,9 @@ def test_fixture_coverage():
     assert any(c.get("sp_slices") for c in cfgs)                              # F13 (SP)
     assert any("qmatrix" in f and f["cfg"]["kind"] == 2 for f in GOLDEN)        # scaling lists, B
     assert any(c["width_mbs"] == 240 for c in cfgs)                            # a 2160p-wide strip
+    # field pictures (PAFF) of both parities, I / P / B, and one of 1080i's size
+    assert {(c.get("structure", 0), c["kind"]) for c in cfgs} >= {(s, k) for s in (1, 2) for k in (0, 1, 2)}
+    assert any(c.get("structure") and c["width_mbs"] == 120 and c["height_mbs"] == 34 for c in cfgs)
 
 
 @pytest.mark.reference

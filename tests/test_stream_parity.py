@@ -33,9 +33,9 @@ REF_BIN = os.path.join(S.ROOT, "oracle", "_ref")
 
 def _replay(pics, decode_picture):
     """Decode captured pictures in decoding order, keeping each reference picture in the
-    DPB slot the shim gave it; returns the output planes in output order (POC)."""
-    outs = [decode_picture(p) for p in pics]
-    return [outs[i] for i in S.output_order(pics)]
+    DPB slot the shim gave it; returns the output frames in output order (POC), field
+    pairs interleaved into their frames."""
+    return S.output_frames(pics, [decode_picture(p) for p in pics])
 
 
 def test_stream_set_matches_writer_and_golden_table():
@@ -96,6 +96,7 @@ def test_oracle_replay_of_captures_matches_reference(name):
     def dec(p):
         W, H = p["W"], p["H"]
         out = O.new_planes(W, H)
+        fld = S.structure(p) != A.FRAME
         o = O.OraclePicture()
         o.width_mbs, o.height_mbs = W, H
         o.mbs, o.levels = A.ptr(p["mbs"]).value, A.ptr(p["levels"]).value
@@ -107,8 +108,17 @@ def test_oracle_replay_of_captures_matches_reference(name):
         for k in range(3):
             o.out[k] = A.ptr(out[k]).value
         assert L.oracle_decode_picture(C.byref(o)) == 0
-        if p["keep"] >= 0:
+        if p["keep"] >= 0 and not fld:
             slots[p["keep"]] = out
+        elif p["keep"] >= 0:
+            # a field into its parity's rows of the slot's frame (include/h264r.h)
+            fr = slots.get(p["keep"])
+            if fr is None or fr[0].shape != (32 * H, 16 * W):
+                fr = O.new_planes(W, 2 * H)
+            par = 1 if S.structure(p) == A.BOTTOM_FIELD else 0
+            for k in range(3):
+                fr[k][par::2] = out[k]
+            slots[p["keep"]] = fr
         return out
     outs = _replay(pics, dec)
     assert S.frame_md5s(outs, cfg) == GOLD[name]["frame_md5"]
@@ -146,7 +156,7 @@ def test_gpu_replay_of_captures_matches_reference(name, flag):
         dec.set_debug(flag)
         def run(p):
             dec.assign_quant_params(p["quant"])
-            dec.init(W, H, p["pic"], p["slices"])
+            dec.init(p["W"], p["H"], p["pic"], p["slices"])           # a field: half the frame's rows
             for a, rec, lv, mv, ri in S.iter_mbs(p):
                 dec.decode(a, rec, lv, mv, ri)
             return dec.deblock_filter(p["keep"])
