@@ -555,15 +555,44 @@ struct Motion {
     size_t at(int x4, int y4) const { return (size_t)y4 * W4 + x4; }
 };
 
+// A frame store (the reference's pic_t, dpb.h): a frame, or the field pair a frame was coded
+// as (PAFF).  Its field views (`view`, created on demand) are the list entries of field
+// pictures (dpb_split_field picture.cc:408-470 without the copy: on the device a field is every
+// second row of the frame store's slot, include/h264r.h H264R_REF_BOTTOM).
 struct Picture {
     int id = 0;
     int poc = 0, frame_num = 0, frame_num_wrap = 0;
     bool idr = false;
-    bool ref = false;              // used for (short- or long-term) reference
+    bool ref = false;              // used for (short- or long-term) reference (a field pair: either field)
     bool long_term = false;
     int lt_idx = 0;
     int slot = -1;                 // device DPB slot (reference pictures)
     std::shared_ptr<Motion> mot;
+    // field coding (PAFF)
+    bool fields = false;           // coded as field pictures
+    bool has[2] = {true, true};    // top / bottom present (is_used bits)
+    bool ref_f[2] = {false, false};   // top / bottom used for reference
+    int poc_f[2] = {0, 0};         // TopFieldOrderCnt / BottomFieldOrderCnt
+    Picture* parent = nullptr;     // a field view: its frame store
+    int parity = 0;                // a field view: 0 top, 1 bottom
+    std::unique_ptr<Picture> view[2];
+    // the field view of parity k (POC, long-term state and identity of that field)
+    Picture* field(int k, int& next_id)
+    {
+        if (!view[k]) {
+            view[k] = std::make_unique<Picture>();
+            view[k]->id = next_id++;
+            view[k]->parent = this;
+            view[k]->parity = k;
+        }
+        Picture* v = view[k].get();
+        v->poc = poc_f[k];
+        v->frame_num = frame_num;
+        v->long_term = long_term;
+        v->lt_idx = lt_idx;
+        v->ref = ref_f[k];
+        return v;
+    }
 };
 
 struct Output {
@@ -582,6 +611,7 @@ struct ListMod {
 struct SliceHeader {
     int nal_ref_idc = 0, nal_type = 0;
     bool idr = false;
+    bool field = false, bottom = false;   // field_pic_flag, bottom_field_flag (PAFF)
     int first_mb = 0, slice_type = 0, pps_id = 0;
     int frame_num = 0, idr_pic_id = 0, poc_lsb = 0, delta_poc_bottom = 0;
     bool direct_spatial = false;
@@ -633,7 +663,9 @@ struct SliceCtx {
     const SliceHeader& sh;
     int slice_nr;
     Bits& b;
-    int W, H;
+    int W, H;                   // the picture's MBs (a field picture: FrameHeightInMbs / 2 rows)
+    const uint8_t* zz4;         // inverse scans: frame zig-zag, or the field scans of a field picture
+    const uint8_t* zz8;
     int qp;                     // slice.parser.QpY
     int skip_run = -1;
     Cabac* cab = nullptr;       // CABAC slices (entropy_coding_mode_flag)
@@ -710,6 +742,9 @@ public:
     int list_n_[2] = {0, 0};
     std::vector<std::unique_ptr<Picture>> dpb_;  // reference pictures (+ the current one while decoding)
     Picture* cur_ = nullptr;
+    int cur_poc_ = 0;                          // the current picture's POC (a field: its own)
+    int pic_h_ = 0;                            // its height in MBs (a field: half the frame's)
+    Picture* last_field_ = nullptr;            // a frame store holding one decoded field (dpb last_picture)
     std::vector<h264r_slice> slice_tab_;
     h264r_quant quant_;
     bool have_quant_ = false;
@@ -741,6 +776,9 @@ private:
     int prev_poc_msb_ = 0, prev_poc_lsb_ = 0, prev_frame_num_ = 0, prev_frame_num_offset_ = 0;
     int max_lt_idx_ = -1;                      // MaxLongTermFrameIdx (-1: no long-term frame indices)
     int period_ = -1;
+    int inflight_par_ = -1;                    // the picture on the GPU is a field of parity 0 / 1 (-1: frame)
+    int out_of_first_ = -1;                    // pending_ entry of the open field pair's frame
+    std::vector<uint8_t> fy_, fu_, fv_;        // a field's planes between the GPU and its frame's output
     std::vector<Output> pending_;
     h264p_output_fn out_ = nullptr;
     void* user_ = nullptr;
@@ -754,6 +792,7 @@ private:
     void begin_picture(const SliceHeader& h);
     void finish_picture();
     void init_lists(const SliceHeader& h);
+    void init_field_lists(const SliceHeader& h);
     void modify_list(const SliceHeader& h, int l);
     h264r_slice slice_record(const SliceHeader& h);
     void mark_picture();
@@ -856,14 +895,18 @@ void Decoder::parse_slice_header(Bits& b, SliceHeader& h)
     const Sps& sps = sps_[pps.sps_id];
     unsupported(sps.chroma_format_idc != 1 || sps.bit_depth_y != 8 || sps.bit_depth_c != 8,
                 "picture format (4:2:0, 8-bit only)");
-    unsupported(!sps.frame_mbs_only, "field / MBAFF coding");
+    unsupported(sps.mbaff, "MBAFF coding (mb_adaptive_frame_field_flag)");
     unsupported(sps.poc_type == 1, "pic_order_cnt_type 1");
     unsupported(h.slice_type == H264R_SLICE_SI, "SI slices");
     h.frame_num = b.u(sps.log2_max_frame_num);
+    if (!sps.frame_mbs_only) {
+        h.field = b.u(1);
+        if (h.field) h.bottom = b.u(1);
+    }
     if (h.idr) h.idr_pic_id = b.ue_max(65535, "slice: idr_pic_id");
     if (sps.poc_type == 0) {
         h.poc_lsb = b.u(sps.log2_max_poc_lsb);
-        if (pps.bottom_field_poc) h.delta_poc_bottom = b.se();
+        if (pps.bottom_field_poc && !h.field) h.delta_poc_bottom = b.se();
     }
     if (pps.redundant_pic_cnt) unsupported(b.ue_max(127, "slice: redundant_pic_cnt") != 0, "redundant pictures");
     const bool P = h.slice_type == H264R_SLICE_P || h.slice_type == H264R_SLICE_SP, B = h.slice_type == H264R_SLICE_B;
@@ -876,14 +919,19 @@ void Decoder::parse_slice_header(Bits& b, SliceHeader& h)
             if (B) h.nref[1] = b.ue_max(31, "slice: num_ref_idx_l1_active_minus1") + 1;
         }
         // frames: at most 16 per list (the reference asserts it, interpret_rbsp.cc:710;
-        // H264R_MAX_REFS): a larger count would be clamped downstream, not decoded
-        require(h.nref[0] <= 16 && (!B || h.nref[1] <= 16), "slice: num_ref_idx_active above 16 (frames)");
+        // H264R_MAX_REFS): a larger count would be clamped downstream, not decoded; fields: 32,
+        // of which the reconstruction ABI takes 16
+        require(h.nref[0] <= (h.field ? 32 : 16) && (!B || h.nref[1] <= (h.field ? 32 : 16)),
+                "slice: num_ref_idx_active above 16 (frames) / 32 (fields)");
+        unsupported(h.nref[0] > 16 || h.nref[1] > 16, "more than 16 reference fields in a list");
     }
+    unsupported(h.field && B, "B field pictures");
     if (!B) h.nref[1] = 0;
     if (!P && !B) h.nref[0] = 0;
     // ref_pic_list_modification (7.3.3.1)
     for (int l = 0; l < (B ? 2 : P ? 1 : 0); ++l) {
         h.mod_flag[l] = b.u(1);
+        unsupported(h.mod_flag[l] && h.field, "reference list modification in field pictures");
         if (h.mod_flag[l])
             for (;;) {
                 const int idc = b.ue_max(3, "slice: modification_of_pic_nums_idc");
@@ -924,6 +972,7 @@ void Decoder::parse_slice_header(Bits& b, SliceHeader& h)
             h.long_term_reference = b.u(1);
         } else {
             h.adaptive = b.u(1);
+            unsupported(h.adaptive && h.field, "adaptive reference marking in field pictures");
             if (h.adaptive)
                 for (;;) {
                     Mmco m{b.ue_max(6, "slice: memory_management_control_operation"), 0, 0};
@@ -968,7 +1017,8 @@ void Decoder::slice(Bits& b, int nal_ref_idc, int nal_type)
     const bool new_pic = !in_picture_ || h.first_mb == 0 || h.frame_num != first_.frame_num ||
                          h.pps_id != first_.pps_id || (h.nal_ref_idc == 0) != (first_.nal_ref_idc == 0) ||
                          h.idr != first_.idr || (h.idr && h.idr_pic_id != first_.idr_pic_id) ||
-                         h.poc_lsb != first_.poc_lsb || h.delta_poc_bottom != first_.delta_poc_bottom;
+                         h.poc_lsb != first_.poc_lsb || h.delta_poc_bottom != first_.delta_poc_bottom ||
+                         h.field != first_.field || h.bottom != first_.bottom;
     if (new_pic) {
         if (in_picture_) finish_picture();
         if (stop_) return;
@@ -1001,7 +1051,7 @@ void Decoder::run_slices()
 {
     const size_t n = pslices_.size();
     if (!n) return;
-    const int W = psps_->W, H = psps_->H;
+    const int W = psps_->W, H = pic_h_;
     static const int env_threads = [] {
         const char* e = getenv("H264P_THREADS");
         return e ? std::max(1, atoi(e)) : 0;
@@ -1091,7 +1141,8 @@ void Decoder::begin_picture(const SliceHeader& h)
         if (h.poc_lsb < prev_poc_lsb_ && prev_poc_lsb_ - h.poc_lsb >= max_lsb / 2) msb = prev_poc_msb_ + max_lsb;
         else if (h.poc_lsb > prev_poc_lsb_ && h.poc_lsb - prev_poc_lsb_ > max_lsb / 2) msb = prev_poc_msb_ - max_lsb;
         else msb = prev_poc_msb_;
-        const int top = msb + h.poc_lsb, bottom = top + h.delta_poc_bottom;
+        // a field picture: its own lsb gives its field's count (8.2.1.1); a frame: both
+        const int top = msb + h.poc_lsb, bottom = h.field ? top : top + h.delta_poc_bottom;
         poc = std::min(top, bottom);
         if (h.nal_ref_idc) { prev_poc_msb_ = msb; prev_poc_lsb_ = h.poc_lsb; }
     } else {
@@ -1103,23 +1154,46 @@ void Decoder::begin_picture(const SliceHeader& h)
         prev_frame_num_offset_ = offset;
     }
     prev_frame_num_ = h.frame_num;
-    if (h.idr) {
-        flush_output();
-        ++period_;
+    cur_poc_ = poc;
+    pic_h_ = h.field ? H / 2 : H;
+    const int par = h.bottom ? 1 : 0;
+    // the second field of a frame store: the stored field of the opposite parity, the same
+    // frame_num, both reference fields or both not (the pairing of store_picture dpb.cc:903-912)
+    if (last_field_) {
+        const bool pair = h.field && !h.idr && last_field_->frame_num == h.frame_num && !last_field_->has[par] &&
+                          last_field_->ref == (h.nal_ref_idc != 0);
+        unsupported(!pair, "an unpaired field");
+        cur_ = last_field_;
+        cur_->poc_f[par] = poc;
+        cur_->poc = std::min(cur_->poc_f[0], cur_->poc_f[1]);
+    } else {
+        if (h.idr) {
+            flush_output();
+            ++period_;
+        }
+        auto pic = std::make_unique<Picture>();
+        pic->id = next_id_++;
+        pic->poc = poc;
+        pic->frame_num = h.frame_num;
+        pic->idr = h.idr;
+        pic->ref = h.nal_ref_idc != 0;
+        pic->fields = h.field;
+        pic->poc_f[0] = pic->poc_f[1] = poc;
+        if (h.field) {
+            pic->has[0] = par == 0;
+            pic->has[1] = par == 1;
+            // non-reference field pairs are not on the path: a non-reference field is output on
+            // its own by the reference (direct_output dpb.cc), not paired in a frame store
+            unsupported(!pic->ref, "non-reference field pictures");
+        }
+        cur_ = pic.get();
+        dpb_.push_back(std::move(pic));
     }
-    auto pic = std::make_unique<Picture>();
-    pic->id = next_id_++;
-    pic->poc = poc;
-    pic->frame_num = h.frame_num;
-    pic->idr = h.idr;
-    pic->ref = h.nal_ref_idc != 0;
-    cur_ = pic.get();
-    dpb_.push_back(std::move(pic));
     mot_ = std::make_shared<Motion>();
-    mot_->init(W, H);
-    cur_->mot = mot_;
-    staged_.assign((size_t)W * H, StagedMb());
-    seen_.assign((size_t)W * H, 0);
+    mot_->init(W, pic_h_);
+    if (!h.field) cur_->mot = mot_;
+    staged_.assign((size_t)W * pic_h_, StagedMb());
+    seen_.assign((size_t)W * pic_h_, 0);
     slice_tab_.clear();
     have_quant_ = false;
 }
@@ -1129,8 +1203,15 @@ void Decoder::init_lists(const SliceHeader& h)
 {
     const int max_frame_num = 1 << psps_->log2_max_frame_num;
     std::vector<Picture*> st, lt;
+    if (h.field) {
+        init_field_lists(h);
+        return;
+    }
     for (auto& p : dpb_) {
         if (p.get() == cur_ || !p->ref) continue;
+        // a frame's list holds frame stores whose two fields are both reference fields
+        // (init_lists_p_slice slice_ref_list.cc:93-99: is_used == 3, frame used for reference)
+        if (!p->has[0] || !p->has[1] || !p->ref_f[0] || !p->ref_f[1]) continue;
         if (p->long_term) lt.push_back(p.get());
         else {
             p->frame_num_wrap = p->frame_num > h.frame_num ? p->frame_num - max_frame_num : p->frame_num;
@@ -1178,6 +1259,50 @@ void Decoder::init_lists(const SliceHeader& h)
         for (int i = 0; i < list_n_[l]; ++i)
             require(list_[l][i] != nullptr, "RefPicList entry is 'no reference picture'");
     }
+}
+
+// RefPicList0 of a P field (8.2.4.2.5; init_lists_p_slice slice_ref_list.cc:128-170,
+// gen_pic_list_from_frame_list :18-76): the frame stores with a short-term reference field --
+// the current frame's first field included -- by FrameNumWrap, descending, then the long-term
+// ones by LongTermFrameIdx; from each ordered set the fields alternate, same parity first, and
+// a parity that runs out leaves the rest to the other
+void Decoder::init_field_lists(const SliceHeader& h)
+{
+    const int max_frame_num = 1 << psps_->log2_max_frame_num;
+    std::vector<Picture*> st, lt;
+    for (auto& p : dpb_) {
+        const bool r = (p->has[0] && p->ref_f[0]) || (p->has[1] && p->ref_f[1]);
+        if (!p->ref || !r) continue;
+        if (p.get() == cur_ && !p->fields) continue;
+        if (p->long_term) lt.push_back(p.get());
+        else {
+            p->frame_num_wrap = p->frame_num > h.frame_num ? p->frame_num - max_frame_num : p->frame_num;
+            st.push_back(p.get());
+        }
+    }
+    std::sort(st.begin(), st.end(), [](Picture* a, Picture* b) { return a->frame_num_wrap > b->frame_num_wrap; });
+    std::sort(lt.begin(), lt.end(), [](Picture* a, Picture* b) { return a->lt_idx < b->lt_idx; });
+    list_n_[0] = list_n_[1] = 0;
+    for (int l = 0; l < 2; ++l)
+        for (int i = 0; i < 33; ++i) list_[l][i] = nullptr;
+    const int same = h.bottom ? 1 : 0;
+    int n = 0;
+    for (const std::vector<Picture*>* set : {&st, &lt}) {
+        const std::vector<Picture*>& fs = *set;
+        size_t idx[2] = {0, 0};
+        auto next = [&](int k) {                    // the next frame store holding a reference field k
+            for (; idx[k] < fs.size(); ++idx[k])
+                if (fs[idx[k]]->has[k] && fs[idx[k]]->ref_f[k]) { list_[0][n++] = fs[idx[k]++]->field(k, next_id_); return; }
+        };
+        while ((idx[0] < fs.size() || idx[1] < fs.size()) && n < 32) {
+            next(same);
+            next(1 - same);
+        }
+    }
+    list_n_[0] = std::min(n, h.nref[0]);
+    for (int i = list_n_[0]; i < 33; ++i) list_[0][i] = nullptr;
+    list_n_[0] = h.nref[0];
+    for (int i = 0; i < list_n_[0]; ++i) require(list_[0][i] != nullptr, "RefPicList entry is 'no reference picture'");
 }
 
 void Decoder::modify_list(const SliceHeader& h, int l)
@@ -1234,8 +1359,10 @@ h264r_slice Decoder::slice_record(const SliceHeader& h)
         for (int i = 0; i < H264R_MAX_REFS; ++i) {
             r.ref_slot[l][i] = -1;
             if (i < n && list_[l][i]) {
-                if (list_[l][i]->slot < 0) fail(H264R_ESTATE, "reference picture not resident in a device DPB slot");
-                r.ref_slot[l][i] = (int8_t)list_[l][i]->slot;
+                // a field view names its frame store's slot and its parity (include/h264r.h)
+                const Picture* q = list_[l][i]->parent ? list_[l][i]->parent : list_[l][i];
+                if (q->slot < 0) fail(H264R_ESTATE, "reference picture not resident in a device DPB slot");
+                r.ref_slot[l][i] = (int8_t)(q->slot | (list_[l][i]->parent && list_[l][i]->parity ? H264R_REF_BOTTOM : 0));
             }
             if (r.wp_mode == 1 && i < h.nref[l])
                 for (int pl = 0; pl < 3; ++pl) {
@@ -1253,7 +1380,7 @@ h264r_slice Decoder::slice_record(const SliceHeader& h)
                 if (p0 && p1) {
                     const int td = clip3(-128, 127, p1->poc - p0->poc);
                     if (td != 0 && !p0->long_term && !p1->long_term) {
-                        const int tb = clip3(-128, 127, cur_->poc - p0->poc);
+                        const int tb = clip3(-128, 127, cur_poc_ - p0->poc);
                         const int tx = (16384 + std::abs(td / 2)) / td;
                         const int dsf = clip3(-1024, 1023, (tx * tb + 32) >> 6);
                         w1 = dsf >> 2;
@@ -1271,13 +1398,16 @@ void Decoder::finish_picture()
 {
     run_slices();
     in_picture_ = false;
-    const int W = psps_->W, H = psps_->H;
+    const int W = psps_->W, H = pic_h_;
+    const bool fld = first_.field, second = fld && cur_ == last_field_;
+    const int par = first_.bottom ? 1 : 0;
     if (!have_quant_) check(h264r_quant_init_flat(&quant_), "h264r_quant_init_flat");
     h264r_pic p;
     memset(&p, 0, sizeof(p));
     p.constrained_intra_pred = ppps_->cip;
     p.num_slices = (int)slice_tab_.size();
-    p.poc = cur_->poc;
+    p.poc = cur_poc_;
+    p.structure = !fld ? H264R_FRAME : par ? H264R_BOTTOM_FIELD : H264R_TOP_FIELD;
     check(h264r_picture_begin(ctx_, W, H, &p, slice_tab_.data(), &quant_), "h264r_picture_begin");
     for (int a = 0; a < W * H; ++a) {
         if (!seen_[a]) fail(H264R_ESTATE, "picture with missing macroblocks");
@@ -1286,7 +1416,8 @@ void Decoder::finish_picture()
                               &st.mv[0][0], &st.ref[0][0]), "h264r_mb_submit");
     }
     int keep = -1;
-    if (cur_->ref) {
+    if (second) keep = cur_->slot;                     // the second field: its first field's slot
+    else if (cur_->ref) {
         // a device slot no reference picture holds, round robin (the shim's policy: the
         // references as they stand before this picture's own marking)
         bool busy[H264R_MAX_SLOTS] = {};
@@ -1299,23 +1430,34 @@ void Decoder::finish_picture()
         for (auto& q : dpb_)
             if (q->slot == keep) q->slot = -1;
     }
-    pending_.push_back(Output{period_, cur_->poc, W, H, {psps_->crop[0], psps_->crop[1], psps_->crop[2], psps_->crop[3]},
-                              {}, {}, {}});
+    // the output frame: a field pair's second field fills the other rows of its first field's
+    // entry (dpb_combine_field_yuv picture.cc:573-590), whose POC is the pair's smaller one
+    const int FH = fld ? 2 * H : H;
+    // (vertical crop offsets count 2 chroma rows when the stream may hold fields, CropUnitY)
+    const int cuy = psps_->frame_mbs_only ? 1 : 2;
+    if (!second)
+        pending_.push_back(Output{period_, cur_->poc, W, FH,
+                                  {psps_->crop[0], psps_->crop[1], cuy * psps_->crop[2], cuy * psps_->crop[3]}, {}, {}, {}});
+    const int out_idx = second ? out_of_first_ : (int)pending_.size() - 1;
+    pending_[out_idx].poc = cur_->poc;
     if (sync_) {
-        Output& o = pending_.back();
-        o.y.resize((size_t)W * H * 256);
-        o.u.resize((size_t)W * H * 64);
-        o.v.resize((size_t)W * H * 64);
-        check(h264r_picture_end(ctx_, o.y.data(), o.u.data(), o.v.data(), keep), "h264r_picture_end");
+        collect();
+        check(h264r_picture_end_async(ctx_, keep), "h264r_picture_end_async");
+        inflight_ = out_idx;
+        inflight_par_ = fld ? par : -1;
+        collect();
     } else {
         // this picture is reconstructed while the next one is parsed; the previous one is
         // collected now (the h264r ABI stages two pictures)
         check(h264r_picture_end_async(ctx_, keep), "h264r_picture_end_async");
         collect();
-        inflight_ = (int)pending_.size() - 1;
+        inflight_ = out_idx;
+        inflight_par_ = fld ? par : -1;
     }
     cur_->slot = keep;
     mark_picture();
+    last_field_ = fld && !second ? cur_ : nullptr;
+    if (fld && !second) out_of_first_ = out_idx;
     // pictures no longer used for reference leave the DPB (their motion with them)
     dpb_.erase(std::remove_if(dpb_.begin(), dpb_.end(), [](const std::unique_ptr<Picture>& q) { return !q->ref; }),
                dpb_.end());
@@ -1328,6 +1470,23 @@ void Decoder::mark_picture()
 {
     if (!cur_->ref) return;
     const SliceHeader& h = first_;
+    struct Norm {                                  // per-field marking follows the frame store's
+        Decoder& d;
+        ~Norm()
+        {
+            for (auto& q : d.dpb_) {
+                if (!q->fields) q->ref_f[0] = q->ref_f[1] = q->ref;
+                else if (!q->ref) q->ref_f[0] = q->ref_f[1] = false;
+            }
+        }
+    } norm{*this};
+    if (h.field) {
+        cur_->ref_f[h.bottom ? 1 : 0] = true;
+        cur_->has[h.bottom ? 1 : 0] = true;
+        // the second field of a pair: no sliding window (store_picture dpb.cc:903-912 stores it
+        // into its first field's frame store before the window runs)
+        if (cur_ == last_field_) return;
+    }
     auto others = [&](auto fn) {
         for (auto& q : dpb_)
             if (q.get() != cur_ && q->ref) fn(*q);
@@ -1397,10 +1556,28 @@ void Decoder::collect()
     Output& o = pending_[inflight_];
     inflight_ = -1;
     const size_t n = (size_t)o.W * o.H;
-    o.y.resize(n * 256);
-    o.u.resize(n * 64);
-    o.v.resize(n * 64);
-    check(h264r_picture_wait(ctx_, o.y.data(), o.u.data(), o.v.data()), "h264r_picture_wait");
+    if (o.y.size() != n * 256) {
+        o.y.assign(n * 256, 0);
+        o.u.assign(n * 64, 0);
+        o.v.assign(n * 64, 0);
+    }
+    if (inflight_par_ < 0) {
+        check(h264r_picture_wait(ctx_, o.y.data(), o.u.data(), o.v.data()), "h264r_picture_wait");
+        return;
+    }
+    // a field: its rows of the frame (every second row from row `par`)
+    const int par = inflight_par_;
+    inflight_par_ = -1;
+    fy_.resize(n * 128);
+    fu_.resize(n * 32);
+    fv_.resize(n * 32);
+    check(h264r_picture_wait(ctx_, fy_.data(), fu_.data(), fv_.data()), "h264r_picture_wait");
+    const int w = o.W * 16, wc = o.W * 8;
+    for (int r = 0; r < o.H * 8; ++r) memcpy(&o.y[(size_t)(2 * r + par) * w], &fy_[(size_t)r * w], w);
+    for (int r = 0; r < o.H * 4; ++r) {
+        memcpy(&o.u[(size_t)(2 * r + par) * wc], &fu_[(size_t)r * wc], wc);
+        memcpy(&o.v[(size_t)(2 * r + par) * wc], &fv_[(size_t)r * wc], wc);
+    }
 }
 
 void Decoder::flush_output()
@@ -1426,7 +1603,8 @@ void Decoder::flush_output()
 // ------------------------------------------------------------------ macroblock layer
 SliceCtx::SliceCtx(Decoder& d, const Sps& s, const Pps& p, const SliceHeader& h, int nr, Bits& bits,
                    Picture* const (*lists)[33], const int* list_n, int end)
-    : D(d), sps(s), pps(p), sh(h), slice_nr(nr), b(bits), W(s.W), H(s.H), qp(h.qp), list_(lists), list_n_(list_n),
+    : D(d), sps(s), pps(p), sh(h), slice_nr(nr), b(bits), W(s.W), H(h.field ? s.H / 2 : s.H),
+      zz4(h.field ? FIELD_SCAN4X4 : ZZ4), zz8(h.field ? FIELD_SCAN8X8 : ZZ8), qp(h.qp), list_(lists), list_n_(list_n),
       end_mb(end)
 {
 }
@@ -1870,6 +2048,7 @@ void SliceCtx::direct_spatial()
     Motion& M = *D.mot_;
     Picture* col = list_[1][0];
     require(col != nullptr, "direct prediction without RefPicList1[0]");
+    unsupported(col->fields || !col->mot, "direct prediction from a frame coded as two fields");
     const int step = sps.direct_8x8_inference ? 4 : 1;
     for (int blk = 0; blk < 16; blk += step) {
         if (m.sub_type[blk / 4] != 0) continue;
@@ -1915,6 +2094,7 @@ void SliceCtx::direct_temporal()
     Motion& M = *D.mot_;
     Picture* col = list_[1][0];
     require(col != nullptr, "direct prediction without RefPicList1[0]");
+    unsupported(col->fields || !col->mot, "direct prediction from a frame coded as two fields");
     const Motion& C = *col->mot;
     for (int blk = 0; blk < 16; ++blk) {
         if (m.sub_type[blk / 4] != 0) continue;
@@ -1943,7 +2123,7 @@ void SliceCtx::direct_temporal()
             const Picture* p1 = list_[1][0];
             int scale = 9999;
             if (!p0->long_term) {
-                const int tb = clip3(-128, 127, D.cur_->poc - p0->poc), td = clip3(-128, 127, p1->poc - p0->poc);
+                const int tb = clip3(-128, 127, D.cur_poc_ - p0->poc), td = clip3(-128, 127, p1->poc - p0->poc);
                 if (td != 0) {
                     const int tx = (16384 + std::abs(td / 2)) / td;
                     scale = clip3(-1024, 1023, (tb * tx + 32) >> 6);
@@ -2135,7 +2315,7 @@ void SliceCtx::residual()
     if (i16) {
         block(LUMA_16DC, 0, false, false, 0, 0, 16, pl_, &n);
         for (int k = 0; k < n; ++k) {
-            const int r = ZZ4[pl_[2 * k]];
+            const int r = zz4[pl_[2 * k]];
             cof[0][(r / 4) * 4][(r % 4) * 4] = pl_[2 * k + 1];
         }
     }
@@ -2147,7 +2327,7 @@ void SliceCtx::residual()
             block(LUMA_8x8, 0, false, true, i8 * 4, 0, 64, pl_, &n);
             for (int k = 0; k < n; ++k) {
                 cbp_blks |= (uint16_t)(0x33u << (j * 4 + i));
-                const int r = ZZ8[pl_[2 * k]];
+                const int r = zz8[pl_[2 * k]];
                 cof[0][j * 4 + r / 8][i * 4 + r % 8] = pl_[2 * k + 1];
             }
             continue;
@@ -2162,13 +2342,13 @@ void SliceCtx::residual()
                 const int c = pl_[2 * k], lev = pl_[2 * k + 1];
                 if (!m.t8) {
                     cbp_blks |= (uint16_t)(1u << (j * 4 + i));
-                    const int r = ZZ4[c];
+                    const int r = zz4[c];
                     cof[0][j * 4 + r / 4][i * 4 + r % 4] = lev;
                 } else {
                     // 8x8 CAVLC: four interleaved 4x4 readings (:161-164)
                     const int x0 = i & ~1, y0 = j & ~1;
                     cbp_blks |= (uint16_t)(0x33u << (y0 * 4 + x0));
-                    const int r = ZZ8[c * 4 + blk % 4];
+                    const int r = zz8[c * 4 + blk % 4];
                     cof[0][y0 * 4 + r / 8][x0 * 4 + r % 8] = lev;
                 }
             }
@@ -2187,7 +2367,7 @@ void SliceCtx::residual()
             if (!(cbpc & 2)) { if (!cab) m.nz[c][blk / 2][blk % 2] = 0; continue; }
             block(CHROMA_AC, c, true, true, blk, 1, 15, pl_, &n);
             for (int k = 0; k < n; ++k) {
-                const int r = ZZ4[pl_[2 * k]];
+                const int r = zz4[pl_[2 * k]];
                 cof[c][(blk / 2) * 4 + r / 4][(blk % 2) * 4 + r % 4] = pl_[2 * k + 1];
             }
         }
@@ -2400,9 +2580,13 @@ int SliceCtx::block_cabac(int cat, int pl, bool chroma, bool ac, int blk, int st
         const int bit = (!chroma ? (ac ? 1 : 0) : !ac ? (pl == 1 ? 17 : 18) : (pl == 1 ? 19 : 35)) + (ac ? j * 4 + i : 0);
         cur->cbp_bits |= (uint64_t)(cur->t8 && !chroma && ac ? 0x33 : 0x01) << bit;
     }
-    const uint8_t* pmap = cat == LUMA_8x8 ? POS2CTX_MAP8X8 : POS2CTX_MAP4X4;
+    // field pictures: the second set of significance contexts and the field 8x8 map
+    // (interpret_residual.cc:353-358)
+    const bool fld = sh.field;
+    const uint8_t* pmap = cat == LUMA_8x8 ? (fld ? POS2CTX_MAP8X8_FIELD : POS2CTX_MAP8X8) : POS2CTX_MAP4X4;
     const uint8_t* plast = cat == LUMA_8x8 ? POS2CTX_LAST8X8 : POS2CTX_LAST4X4;
-    const int map = CTX_MAP_CONTEXTS + TYPE2CTX_MAP[cat], last = CTX_LAST_CONTEXTS + TYPE2CTX_MAP[cat];
+    const int fset = fld ? (CTX_LAST_CONTEXTS - CTX_MAP_CONTEXTS) / 2 : 0;      // 210 contexts per set
+    const int map = CTX_MAP_CONTEXTS + fset + TYPE2CTX_MAP[cat], last = CTX_LAST_CONTEXTS + fset + TYPE2CTX_MAP[cat];
     int sig[64];
     int num = max_coeff;
     int ii = 0;

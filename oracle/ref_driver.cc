@@ -253,6 +253,19 @@ int main(int argc, char** argv)
                 (t8 ? inv8 : inv4)[pos.y * (t8 ? 8 : 4) + pos.x] = k;
             }
         }
+        /* H264R_PRINT_FIELD_SCANS: the field scans as raster index per scan position, for the
+           repo's parser tables (tools/gen_parser_tables.py via tests/golden/make_cabac_tables.py) */
+        if (getenv("H264R_PRINT_FIELD_SCANS")) {
+            int s4[16], s8[64];
+            for (int r = 0; r < 16; ++r) s4[inv4[r]] = r;
+            for (int r = 0; r < 64; ++r) s8[inv8[r]] = r;
+            printf("{\"field_scan4x4\": [");
+            for (int k = 0; k < 16; ++k) printf("%s%d", k ? ", " : "", s4[k]);
+            printf("], \"field_scan8x8\": [");
+            for (int k = 0; k < 64; ++k) printf("%s%d", k ? ", " : "", s8[k]);
+            printf("]}\n");
+            return 0;
+        }
     }
 
     const char* reps_env = getenv("H264R_TIME_REPS");

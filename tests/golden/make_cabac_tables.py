@@ -59,6 +59,13 @@ def main():
             mn.append(list(fit(pre)))
         init[key] = mn
     d["init"] = init
+    # the field scans (Tables 8-13 / 8-14, field) as the reference maps scan positions of a field
+    # picture: Transform::inverse_scan_luma_ac on a field slice (oracle/ref_driver.cc)
+    scans = subprocess.run([os.path.join(ROOT, "oracle", "_ref", "ref_driver"), "11", "4", "0", "1", "0", "0", "0",
+                            "1", "0", "0", "0", "20", "30", "0", "0", "4", "4", "1", "0", "/dev/null", "0", "0",
+                            "0", "1"], check=True, capture_output=True, text=True,
+                           env=dict(os.environ, H264R_PRINT_FIELD_SCANS="1")).stdout
+    d.update(json.loads(scans))
     d["_source"] = ("oracle/probe_cabac.cc: cabac_contexts_t::init (bitstream_cabac.cc:1215-1264) called for every "
                     "slice kind / cabac_init_idc / SliceQpY, fitted to (m, n) per context; engine tables from "
                     "cabac_engine_t::decode_decision (interpret.cc:318-341) as a black box; residual context maps "
