@@ -573,6 +573,7 @@ struct Picture {
     bool has[2] = {true, true};    // top / bottom present (is_used bits)
     bool ref_f[2] = {false, false};   // top / bottom used for reference
     int poc_f[2] = {0, 0};         // TopFieldOrderCnt / BottomFieldOrderCnt
+    std::shared_ptr<Motion> mot_f[2];  // a field pair's top / bottom field motion
     Picture* parent = nullptr;     // a field view: its frame store
     int parity = 0;                // a field view: 0 top, 1 bottom
     std::unique_ptr<Picture> view[2];
@@ -699,6 +700,7 @@ struct SliceCtx {
                     int out[2]);
     void direct_spatial();
     void direct_temporal();
+    const Motion& colocated(int i4, int j4, size_t& e);
     void residual();
     int nnz_pred(int pl, int i, int j);
     int block_cavlc(int pl, bool chroma, bool ac, int blk, int start, int max_coeff, int32_t* coeff_pos_level,
@@ -925,7 +927,6 @@ void Decoder::parse_slice_header(Bits& b, SliceHeader& h)
                 "slice: num_ref_idx_active above 16 (frames) / 32 (fields)");
         unsupported(h.nref[0] > 16 || h.nref[1] > 16, "more than 16 reference fields in a list");
     }
-    unsupported(h.field && B, "B field pictures");
     if (!B) h.nref[1] = 0;
     if (!P && !B) h.nref[0] = 0;
     // ref_pic_list_modification (7.3.3.1)
@@ -1182,9 +1183,6 @@ void Decoder::begin_picture(const SliceHeader& h)
         if (h.field) {
             pic->has[0] = par == 0;
             pic->has[1] = par == 1;
-            // non-reference field pairs are not on the path: a non-reference field is output on
-            // its own by the reference (direct_output dpb.cc), not paired in a frame store
-            unsupported(!pic->ref, "non-reference field pictures");
         }
         cur_ = pic.get();
         dpb_.push_back(std::move(pic));
@@ -1192,6 +1190,7 @@ void Decoder::begin_picture(const SliceHeader& h)
     mot_ = std::make_shared<Motion>();
     mot_->init(W, pic_h_);
     if (!h.field) cur_->mot = mot_;
+    else cur_->mot_f[par] = mot_;
     staged_.assign((size_t)W * pic_h_, StagedMb());
     seen_.assign((size_t)W * pic_h_, 0);
     slice_tab_.clear();
@@ -1280,29 +1279,57 @@ void Decoder::init_field_lists(const SliceHeader& h)
             st.push_back(p.get());
         }
     }
-    std::sort(st.begin(), st.end(), [](Picture* a, Picture* b) { return a->frame_num_wrap > b->frame_num_wrap; });
     std::sort(lt.begin(), lt.end(), [](Picture* a, Picture* b) { return a->lt_idx < b->lt_idx; });
     list_n_[0] = list_n_[1] = 0;
     for (int l = 0; l < 2; ++l)
         for (int i = 0; i < 33; ++i) list_[l][i] = nullptr;
     const int same = h.bottom ? 1 : 0;
-    int n = 0;
-    for (const std::vector<Picture*>* set : {&st, &lt}) {
-        const std::vector<Picture*>& fs = *set;
+    // the fields of the ordered frame stores fs appended to list l, alternating parity
+    auto gen = [&](const std::vector<Picture*>& fs, int l) {
         size_t idx[2] = {0, 0};
         auto next = [&](int k) {                    // the next frame store holding a reference field k
             for (; idx[k] < fs.size(); ++idx[k])
-                if (fs[idx[k]]->has[k] && fs[idx[k]]->ref_f[k]) { list_[0][n++] = fs[idx[k]++]->field(k, next_id_); return; }
+                if (fs[idx[k]]->has[k] && fs[idx[k]]->ref_f[k]) {
+                    if (list_n_[l] < 32) list_[l][list_n_[l]++] = fs[idx[k]]->field(k, next_id_);
+                    ++idx[k];
+                    return;
+                }
         };
-        while ((idx[0] < fs.size() || idx[1] < fs.size()) && n < 32) {
+        while (idx[0] < fs.size() || idx[1] < fs.size()) {
             next(same);
             next(1 - same);
         }
+    };
+    if (h.slice_type != H264R_SLICE_B) {
+        std::sort(st.begin(), st.end(), [](Picture* a, Picture* b) { return a->frame_num_wrap > b->frame_num_wrap; });
+        gen(st, 0);
+        gen(lt, 0);
+    } else {
+        // B fields (init_lists_b_slice slice_ref_list.cc:256-306): the frame stores by their POC
+        // (a single field's, or the pair's smaller) against the current field's -- list 0 those
+        // at or before it (descending) then after (ascending), list 1 the two halves swapped
+        std::vector<Picture*> before, after, l0, l1;
+        for (Picture* p : st) (cur_poc_ >= p->poc ? before : after).push_back(p);
+        std::stable_sort(before.begin(), before.end(), [](Picture* a, Picture* b) { return a->poc > b->poc; });
+        std::stable_sort(after.begin(), after.end(), [](Picture* a, Picture* b) { return a->poc < b->poc; });
+        l0 = before; l0.insert(l0.end(), after.begin(), after.end());
+        l1 = after; l1.insert(l1.end(), before.begin(), before.end());
+        gen(l0, 0);
+        gen(l1, 1);
+        gen(lt, 0);
+        gen(lt, 1);
+        if (list_n_[0] == list_n_[1] && list_n_[0] > 1) {
+            bool identical = true;
+            for (int j = 0; j < list_n_[0]; ++j) identical &= list_[0][j] == list_[1][j];
+            if (identical) std::swap(list_[1][0], list_[1][1]);
+        }
     }
-    list_n_[0] = std::min(n, h.nref[0]);
-    for (int i = list_n_[0]; i < 33; ++i) list_[0][i] = nullptr;
-    list_n_[0] = h.nref[0];
-    for (int i = 0; i < list_n_[0]; ++i) require(list_[0][i] != nullptr, "RefPicList entry is 'no reference picture'");
+    for (int l = 0; l < 2; ++l) {
+        list_n_[l] = std::min(list_n_[l], h.nref[l]);
+        for (int i = list_n_[l]; i < 33; ++i) list_[l][i] = nullptr;
+        list_n_[l] = h.nref[l];
+        for (int i = 0; i < list_n_[l]; ++i) require(list_[l][i] != nullptr, "RefPicList entry is 'no reference picture'");
+    }
 }
 
 void Decoder::modify_list(const SliceHeader& h, int l)
@@ -1459,7 +1486,9 @@ void Decoder::finish_picture()
     last_field_ = fld && !second ? cur_ : nullptr;
     if (fld && !second) out_of_first_ = out_idx;
     // pictures no longer used for reference leave the DPB (their motion with them)
-    dpb_.erase(std::remove_if(dpb_.begin(), dpb_.end(), [](const std::unique_ptr<Picture>& q) { return !q->ref; }),
+    // (a non-reference first field stays for its second field)
+    dpb_.erase(std::remove_if(dpb_.begin(), dpb_.end(),
+                              [&](const std::unique_ptr<Picture>& q) { return !q->ref && q.get() != last_field_; }),
                dpb_.end());
     cur_ = nullptr;
 }
@@ -2026,6 +2055,39 @@ void SliceCtx::skip_p()
 
 static int rsd(int x) { return (x & 2) ? (x | 1) : (x & ~1); }
 
+// get_colocated (interpret_mv.cc:192-240), frames and PAFF fields (direct_8x8_inference is 1
+// whenever frame_mbs_only_flag is 0): the co-located 4x4 block of (i4, j4) in RefPicList1[0]'s
+// motion -- a frame coded as frame: its own; a field of a frame coded as frame: the frame's
+// rows 2 RSD(j4) (dpb_split_field picture.cc:541-569 copies them into both field views, and the
+// reference takes the view of the CURRENT field's parity); a field of a frame coded as fields:
+// that field's own; a frame coded as fields seen from a frame picture: the field nearer in POC,
+// row RSD(j4) / 2
+const Motion& SliceCtx::colocated(int i4, int j4, size_t& e)
+{
+    Picture* ref = list_[1][0];
+    Picture* fs = ref->parent ? ref->parent : ref;
+    const bool d8 = sps.direct_8x8_inference;
+    if (sh.field) {
+        if (!fs->fields) {
+            require(fs->mot != nullptr, "co-located motion");
+            e = fs->mot->at(rsd(i4), 2 * rsd(j4));
+            return *fs->mot;
+        }
+        require(fs->mot_f[ref->parity] != nullptr, "co-located motion");
+        const Motion& M = *fs->mot_f[ref->parity];
+        e = M.at(rsd(i4), rsd(j4));
+        return M;
+    }
+    if (fs->fields) {
+        const int k = std::abs(D.cur_poc_ - fs->poc_f[1]) > std::abs(D.cur_poc_ - fs->poc_f[0]) ? 0 : 1;
+        require(fs->mot_f[k] != nullptr, "co-located motion");
+        e = fs->mot_f[k]->at(rsd(i4), rsd(j4) >> 1);
+        return *fs->mot_f[k];
+    }
+    e = d8 ? fs->mot->at(rsd(i4), rsd(j4)) : fs->mot->at(i4, j4);
+    return *fs->mot;
+}
+
 // get_direct_spatial (interpret_mv.cc:371-434), frames, direct_8x8_inference as signalled
 void SliceCtx::direct_spatial()
 {
@@ -2048,7 +2110,6 @@ void SliceCtx::direct_spatial()
     Motion& M = *D.mot_;
     Picture* col = list_[1][0];
     require(col != nullptr, "direct prediction without RefPicList1[0]");
-    unsupported(col->fields || !col->mot, "direct prediction from a frame coded as two fields");
     const int step = sps.direct_8x8_inference ? 4 : 1;
     for (int blk = 0; blk < 16; blk += step) {
         if (m.sub_type[blk / 4] != 0) continue;
@@ -2056,9 +2117,8 @@ void SliceCtx::direct_spatial()
         const int i = ((blk / 4) % 2) * 2 + ((blk % 4) % 2), j = ((blk / 4) / 2) * 2 + ((blk % 4) / 2);
         bool colzero = false;
         if (!col->long_term) {
-            const Motion& C = *col->mot;
-            const int i4 = mbx * 4 + i, j4 = mby * 4 + j;
-            const size_t e = sps.direct_8x8_inference ? C.at(rsd(i4), rsd(j4)) : C.at(i4, j4);
+            size_t e;
+            const Motion& C = colocated(mbx * 4 + i, mby * 4 + j, e);
             colzero = (C.ref_idx[0][e] == 0 && std::abs(C.mvx[0][e]) >> 1 == 0 && std::abs(C.mvy[0][e]) >> 1 == 0) ||
                       (C.ref_idx[0][e] == -1 && C.ref_idx[1][e] == 0 && std::abs(C.mvx[1][e]) >> 1 == 0 &&
                        std::abs(C.mvy[1][e]) >> 1 == 0);
@@ -2094,7 +2154,7 @@ void SliceCtx::direct_temporal()
     Motion& M = *D.mot_;
     Picture* col = list_[1][0];
     require(col != nullptr, "direct prediction without RefPicList1[0]");
-    unsupported(col->fields || !col->mot, "direct prediction from a frame coded as two fields");
+    unsupported(sh.field || col->fields || !col->mot, "temporal direct prediction with field pictures");
     const Motion& C = *col->mot;
     for (int blk = 0; blk < 16; ++blk) {
         if (m.sub_type[blk / 4] != 0) continue;

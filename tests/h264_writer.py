@@ -821,11 +821,12 @@ class Encoder:
                     w.u(1, 0)
 
     def picture(self, idx: int, idr: bool, kind: str | None = None, ref_idc: int = 3, poc: int = 0,
-                structure: int = 0, second: bool = False, nref_field: int = 0):
+                structure: int = 0, second: bool = False, nref_field=0):
         """NAL units of picture idx: one per slice.  kind None = I (idr) or P; "B" writes a
         B picture (nal_ref_idc = ref_idc, POC lsb from poc).  structure 1 / 2: a top / bottom
         field picture (field_pic_flag, bottom_field_flag; FH / 2 MB rows), `second` the second
-        field of its frame (same frame_num), `nref_field` its num_ref_idx_l0_active."""
+        field of its frame (same frame_num), `nref_field` its num_ref_idx_l0_active (a B field:
+        the (l0, l1) pair)."""
         c, r = self.c, self.rng
         self.H = self.FH // 2 if structure else self.FH
         n = self.W * self.H
@@ -837,13 +838,15 @@ class Encoder:
         tracked = bool(c.bframes or c.long_term)           # DPB bookkeeping of the IBBP / long-term streams
         if tracked and not idr:
             frame_num = (self.prev_ref_fn + 1) % (1 << self.log2_max_frame_num)
+        if second:
+            frame_num = self.frame_num                   # both fields of a frame share frame_num
         self.frame_num = frame_num
         if ref_idc:
             self.prev_ref_fn = frame_num
         avail = self.st + self.lt                            # reference frames in the DPB before this picture
         mmco_lt = c.long_term and ptype == "P" and idx == c.long_term
         if ptype == "B":
-            nref_b = (avail, min(avail, c.l1_refs))
+            nref_b = tuple(nref_field) if structure else (avail, min(avail, c.l1_refs))
         elif c.bframes:
             # a P picture leaves one reference out of its list: the pictures its motion
             # points to stay in the DPB for the B pictures' temporal direct (the co-located
@@ -868,7 +871,7 @@ class Encoder:
             if c.bframes:
                 w.u(self.log2_max_poc_lsb, poc % (1 << self.log2_max_poc_lsb))   # pic_order_cnt_lsb
             nref = self.refs if not tracked else (self.refs_p if c.bframes else avail)
-            if structure:
+            if structure and ptype != "B":
                 nref = nref_field
             if ptype == "B":
                 w.u(1, r.choice(c.direct))          # direct_spatial_mv_pred_flag
@@ -941,8 +944,8 @@ class Encoder:
                     w.ue(skip_run)
                 w.trailing()
             out.append(nal_unit(ref_idc, 5 if idr else 1, w.bytes()))
-        if ref_idc:                                          # marking after the picture (8.2.5)
-            if idr:
+        if ref_idc and not second:                           # marking after the picture (8.2.5); a second
+            if idr:                                          # field joins its first field's frame
                 self.st, self.lt = (0, 1) if c.long_term else (1, 0)
             elif mmco_lt:
                 self.lt += 1
@@ -954,6 +957,8 @@ class Encoder:
         c = self.c
         out = [self.sps(), self.pps()]
         self.frame_num, self.refs, self.prev_ref_fn, self.st, self.lt = 0, 0, 0, 0, 0
+        if c.field and c.bframes:
+            return b"".join(out + self._field_stream_b())
         if c.field:
             return b"".join(out + self._field_stream())
         if not c.bframes:
@@ -1000,6 +1005,44 @@ class Encoder:
             n2 = min(2 * (nfr - 1) + 1, H264R_MAX_FIELD_REFS)
             out += self.picture(i, idr=False, kind="I" if c.all_intra else "P", structure=3 - first,
                                 second=True, nref_field=n2)
+        return out
+
+
+    def _field_stream_b(self) -> list:
+        """IBBP with field pictures (pic_order_cnt_type 0): every frame a frame picture or,
+        with probability c.field, a field pair; frame POC 4 x output index, a pair's fields
+        4 x index (top) and 4 x index + 1 (bottom).  B pictures (non-reference unless
+        c.b_ref) predict from the reference fields of both lists (8.2.4.2.4); keep direct
+        prediction spatial (c.direct = (1,)) -- temporal direct needs the co-located field's
+        reference in list 0."""
+        c, r = self.c, self.rng
+        order, k = [(0, None)], 0
+        while k + 1 < c.frames:
+            anchor = min(k + c.bframes + 1, c.frames - 1)
+            order.append((anchor, None))
+            order += [(b, "B") for b in range(k + 1, anchor)]
+            k = anchor
+        out = []
+        for i, (disp, kind) in enumerate(order):
+            ref_idc = 3 if kind != "B" else (2 if r.random() < c.b_ref else 0)
+            idr = i == 0
+            fld = c.field >= 1.0 or r.random() < c.field
+            if not fld:
+                out += self.picture(i, idr=idr, kind=kind, ref_idc=ref_idc, poc=4 * disp)
+                continue
+            first = 2 if c.bottom_first and r.random() < c.bottom_first else 1
+            ptype = "B" if kind == "B" else ("I" if idr else "P")
+            nfr = self.st + self.lt                          # reference frames before this one
+            f1 = 2 * nfr
+            n1 = (f1, min(f1, 2 * c.l1_refs)) if ptype == "B" else min(f1, H264R_MAX_FIELD_REFS)
+            out += self.picture(i, idr=idr, kind=kind, ref_idc=ref_idc, poc=4 * disp + (first == 2),
+                                structure=first, nref_field=n1)
+            # the second field: the first one is a reference field of the same frame when it is
+            # one (the sliding window has counted its frame)
+            f2 = 2 * (self.st + self.lt - 1) + 1 if ref_idc else 2 * nfr
+            n2 = (f2, min(f2, 2 * c.l1_refs)) if ptype == "B" else min(f2, H264R_MAX_FIELD_REFS)
+            out += self.picture(i, idr=False, kind="B" if ptype == "B" else "P", ref_idc=ref_idc,
+                                poc=4 * disp + (first == 1), structure=3 - first, second=True, nref_field=n2)
         return out
 
 

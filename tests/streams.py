@@ -100,6 +100,16 @@ STREAMS = {
     "hp_cif_cabac_paff_8x8_scaling": dict(width_mbs=22, height_mbs=18, frames=5, seed=504, profile=100,
                                           transform8x8=1, cabac=1, field=1.0, bottom_first=0.5, num_refs=2,
                                           scaling=1, qp=(12, 40)),
+    # B field pictures (IBBP, pic_order_cnt_type 0): list 0 / list 1 of reference fields by POC, spatial
+    # direct from co-located fields of frames coded as frames or as fields, non-reference and
+    # reference B field pairs, default / implicit / explicit bi-prediction
+    "mp_cif_paff_ibbp_spatial": dict(width_mbs=22, height_mbs=18, frames=7, seed=601, profile=77, field=1.0,
+                                     bframes=2, num_refs=3, direct=(1,), slices=2, deblock=(0, 2), offsets=2),
+    "hp_cif_cabac_paff_ibbp_implicit_bref": dict(width_mbs=22, height_mbs=18, frames=8, seed=602, profile=100,
+                                                 transform8x8=1, cabac=1, field=0.6, bottom_first=0.4, bframes=2,
+                                                 num_refs=3, direct=(1,), bipred=2, b_ref=0.5),
+    "hp_cif_paff_ibbp_explicit": dict(width_mbs=22, height_mbs=18, frames=7, seed=603, profile=100, transform8x8=1,
+                                      field=0.7, bframes=1, num_refs=2, direct=(1,), bipred=1),
     "hp_1080i_cabac_paff": dict(width_mbs=120, height_mbs=68, frames=2, seed=505, profile=100, transform8x8=1,
                                 cabac=1, field=1.0, num_refs=2, slices=4, deblock=(0, 2), crop=(0, 0, 0, 2)),
 }
