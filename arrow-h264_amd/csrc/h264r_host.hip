@@ -301,9 +301,10 @@ static const Knobs& knobs()
         n.wait_ticks = (uint32_t)(v * 100000);                     // s_memrealtime, 100 MHz
         // levels beyond 3 hold few MBs each, and a grid barrier apiece: the walk takes them
         v = -1; n.ok &= env_long("H264R_LEVELS", 0, LEVEL_LISTS, &v); n.levels = (int)v;
-        // round 5 (8 lanes per unit, staged stores): k_deblock2 wins from 64 1080p pictures of a
-        // throughput batch, 32 2160p chain pictures, up (profiles/r05_x_deblock_min.txt); the lone
-        // picture of the latency chain keeps k_deblock
+        // round 5 (8 lanes per unit, staged stores): k_deblock2 wins over k_deblock from 64 1080p
+        // pictures of a throughput batch, 32 2160p chain pictures, up (profiles/r05_x_deblock_min.txt).
+        // Below H264R_DB2S_MAX the split walk is the default, so k_deblock is taken by default only
+        // when H264R_DB2S_MAX is lowered (0: launches below this many picture-rows x 68 take it)
         v = 8; n.ok &= env_long("H264R_DEBLOCK2_MIN", 1, 1L << 30, &v); n.deblock2_min = (int)v;
         // the split walk (twice the waves, each step shorter) wins below ~512 1080p pictures: config 3
         // at 128 / 256 / 1024 pictures 1.06 -> 0.83 / 1.26 -> 1.23 / 3.78 -> 4.46 ms, config 4 (256)
@@ -560,6 +561,7 @@ static int recon_launches(h264r_ctx* c, const Stage& S, hipStream_t s, int2 rows
         int* pband = sync + 1 + (size_t)P * H + 32 + P;        // after the inter flags
         int* lbar = sync + 1 + (size_t)P * H + 23;               // k_intra_levels' barrier (9 ints)
         const int lmax = levels ? level_launches((size_t)P * W * HB) : 0;
+        if (knobs().verbose) fprintf(stderr, "h264r: %d intra levels from lists, %d pictures\n", lmax, P);
         if (levels) {
             int* lvsync = sync + 1 + (size_t)P * H + 2;
             int* lcount = X.d_lcnt;

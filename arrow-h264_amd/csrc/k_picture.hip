@@ -106,6 +106,10 @@ DEV bool wait_for(int* counter, int need, int* err, int& seen)
 
 // One (band, picture) ticket: wave `wave` walks MB row r0 + wave of the band.
 // sync: [0] ticket counter, [1 ..] per (picture, row) progress; zeroed before every launch.
+// Bit `band` of a picture's band mask (k_level: bit b for band b; all bits set, or none, when the
+// picture has more than 31 bands -- a shift by 32 or more is not defined in C++)
+DEV bool band_bit(int pb, int band) { return band >= 32 ? pb != 0 : ((pb >> band) & 1) != 0; }
+
 // pband[pic] (with lvl): bit b set when band b of the picture has an MB deeper than lmax
 // (k_level); a band without one needs no walk, and the band below it no wait.
 template <typename Scratch>
@@ -122,7 +126,7 @@ DEV void walk_ticket(const h264r_batch& b, int* sync, int* err, Scratch* scratch
     const int r = r0 + wave;
     if (r >= r1) return;
     // the band above has nothing deeper than the lists: its rows are final already
-    const bool above_done = lvl && band > 0 && !((pband[pic] >> (band - 1)) & 1);
+    const bool above_done = lvl && band > 0 && !band_bit(pband[pic], band - 1);
     int* gprog = sync + 1 + (size_t)pic * g.hmb;
     const bool last_row = r == r1 - 1 && r1 < R1;
     Scratch& S = scratch[wave];
@@ -235,7 +239,7 @@ extern "C" __global__ __launch_bounds__(64 * H264R_WALK_ROWS, H264R_WALK_WAVES) 
     if (threadIdx.x == 0) ticket = atomicAdd(&sync[0], 1);
     if (threadIdx.x < WAVES) lprog[threadIdx.x] = 0;
     __syncthreads();
-    if (lvl && !((pband[ticket % b.num_pics] >> (ticket / b.num_pics)) & 1)) return;     // (block-uniform)
+    if (lvl && !band_bit(pband[ticket % b.num_pics], ticket / b.num_pics)) return;       // (block-uniform)
     intra4_tap_fill(tap4, threadIdx.x, blockDim.x);
     __syncthreads();
     walk_ticket(b, sync, err, scratch, tap4, lprog, ticket, lvl, lmax, rows, gstep, recon, pband);

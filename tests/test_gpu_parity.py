@@ -265,25 +265,44 @@ def test_gpu_batch_dense_intra_levels(L, dec):
     _batch_vs_oracle(L, dec, 3, 40, 30, 3, intra_permille=600, pcm_permille=30)
 
 
+_LEVELS_CODE = """
+import sys
+sys.path[:0] = [{root!r}, {tests!r}]
+import test_gpu_parity as T, h264r
+L = h264r.lib()
+d = h264r.Decoder(0, 240, 135)
+try:
+    T._batch_vs_oracle(L, d, 3, 40, 30, 3, deblocks=(0,), intra_permille=600, pcm_permille=30)
+    T._batch_vs_oracle(L, d, 3, 120, 68, 4, deblocks=(0,), intra_permille=300)
+finally:
+    d.close()
+print("levels ok")
+"""
+
+
 @pytest.mark.parametrize("levels", ["8", "16"])
-def test_gpu_batch_many_level_barriers(L, monkeypatch, levels):
-    """Every level from lists (H264R_LEVELS 8 / 16, read at h264r_create): the dense-intra
-    pictures cross k_intra_levels' sharded grid barrier (8 shard counters + a top counter,
-    k_picture.hip) up to 15 times in one launch; the deeper MBs still go to the walk."""
-    monkeypatch.setenv("H264R_LEVELS", levels)
-    d = h264r.Decoder(0, 240, 135)
-    try:
-        _batch_vs_oracle(L, d, 3, 40, 30, 3, deblocks=(0,), intra_permille=600, pcm_permille=30)
-        _batch_vs_oracle(L, d, 3, 120, 68, 4, deblocks=(0,), intra_permille=300)
-    finally:
-        d.close()
+def test_gpu_batch_many_level_barriers(L, levels):
+    """Every level from lists (H264R_LEVELS 8 / 16): the dense-intra pictures cross
+    k_intra_levels' sharded grid barrier (8 shard counters + a top counter, k_picture.hip) up to
+    15 times in one launch; the deeper MBs still go to the walk.  The library reads its knobs once
+    per process (h264r_host.hip knobs()), so the case runs in a process of its own, and its
+    H264R_VERBOSE report shows the level count each launch took."""
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    code = _LEVELS_CODE.format(root=os.path.join(os.path.dirname(here), "arrow-h264_amd"), tests=here)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=110,
+                       env=dict(os.environ, H264R_LEVELS=levels, H264R_VERBOSE="1"))
+    assert r.returncode == 0 and "levels ok" in r.stdout, r.stdout[-1500:] + r.stderr[-3000:]
+    took = {ln for ln in r.stderr.splitlines() if "intra levels from lists" in ln}
+    assert took and all(ln.startswith(f"h264r: {levels} intra levels") for ln in took), took
 
 
 @pytest.mark.parametrize("n", [33, 70])
 def test_gpu_batch_picture_groups(L, dec, n):
     """Batches spanning several picture groups of k_deblock2 (the last one ragged; 9 MB rows =
-    bands of 4, 4 and 1 row) under both schedules; flag 0 takes the default for these sizes
-    (33 x 9 rows: k_deblock, below H264R_DEBLOCK2_MIN x 68; 70 x 9: k_deblock2)."""
+    bands of 4, 4 and 1 row) under both schedules; flag 0 takes the default for these sizes (the
+    split walk for both: below H264R_DB2S_MAX x 68 picture-rows)."""
     _batch_vs_oracle(L, dec, 3, 11, 9, n, deblocks=(0, A.DBG_DEBLOCK_MB, A.DBG_DEBLOCK_ROWS), pcm_permille=20)
 
 
