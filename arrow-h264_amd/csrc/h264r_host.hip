@@ -1036,7 +1036,7 @@ int h264r_picture_end_async(h264r_ctx* c, int keep_slot)
             HIP_OK(hipMemcpyAsync(c->slot[keep_slot][0], c->d_out, ys + 2 * cs, hipMemcpyDeviceToDevice, s));
         } else {
             // a field goes into its parity's rows of the slot's frame (the reference combines the
-            // two fields of a frame with dpb_combine_field_yuv, picture.cc:573-590); the other
+            // two fields of a frame with dpb_combine_field_yuv, picture.cc:578-622); the other
             // field's rows are left as they are
             const int bot = P.h_pic.structure == H264R_BOTTOM_FIELD;
             const size_t W = (size_t)P.pw * 16, Wc = W / 2;

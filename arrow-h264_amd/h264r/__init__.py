@@ -83,6 +83,8 @@ def lib() -> C.CDLL:
         f = getattr(L, name)
         f.argtypes, f.restype = args, res
     A.bind_synth(L)
+    from .group import bind as bind_group
+    bind_group(L)
     if L.h264r_abi_version() != A.ABI_VERSION:
         raise ImportError("libh264r ABI version mismatch")
     _lib = L

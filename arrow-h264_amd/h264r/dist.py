@@ -161,12 +161,18 @@ class BandExchange:
     * mode "allgather": every other band whole, one all-gather of all nk pictures' bands
       (padded to the widest band).
 
-    With gloo (CPU rehearsal) device tensors are staged through host memory."""
+    impl "abi" (default) runs the exchange in the library (include/h264r_group.h: pack kernel,
+    RCCL ncclSend / ncclRecv on the decode stream, unpack kernel; over gloo the library's callback
+    transport with torch.distributed operations on host buffers).  impl "torch" is the same
+    exchange in torch.distributed calls (round 4), kept for comparison.  With gloo (CPU
+    rehearsal) device tensors are staged through host memory."""
 
     def __init__(self, bands, rank: int, width_mbs: int, height_mbs: int, nk: int, mode: str, halo: int,
-                 device, group=None):
+                 device, group=None, impl: str = "abi"):
         import torch
+        import torch.distributed as dist
         self.bands, self.rank, self.nk, self.mode, self.group = list(bands), rank, nk, mode, group
+        self.impl = impl
         self.W, self.H = width_mbs, height_mbs
         self.rb = [c * width_mbs for c in ROW_BYTES_PER_MB_COL]           # bytes per MB row, per plane
         self.mbrow = sum(self.rb)
@@ -181,6 +187,16 @@ class BandExchange:
             self.give = {r: self.bands[rank] for r in range(self.world) if r != rank}
         self.wide = max(b1 - b0 for b0, b1 in self.bands)
         self.device = device
+        if impl == "abi":
+            from .group import Group
+            dev = torch.device(device)
+            gloo = dist.get_backend(group) == "gloo"
+            self.grp = Group(self.world, rank, dev.index if dev.type == "cuda" else -1,
+                             "torch" if gloo else "rccl", group)
+            self.grp.set_bands(width_mbs, height_mbs, self.bands, mode, halo, nk)
+            return
+        if impl != "torch":
+            raise ValueError(impl)
 
         def buf(rows):
             return torch.empty(nk * rows * self.mbrow, dtype=torch.uint8, device=device)
@@ -193,6 +209,8 @@ class BandExchange:
 
     def bytes_in(self) -> int:
         """Bytes this rank receives per exchange (the padding of the all-gather included)."""
+        if self.impl == "abi":
+            return self.nk * self.mbrow * sum(n1 - n0 for n0, n1 in self.need.values())
         return sum(t.numel() for t in self.rbuf.values()) - (self.sbuf[0].numel() if self.mode == "allgather" else 0)
 
     def _views(self, planes):
@@ -218,6 +236,12 @@ class BandExchange:
     def run(self, planes) -> None:
         import torch.distributed as dist
         if self.world == 1 or not (dist.is_available() and dist.is_initialized()):
+            return
+        if self.impl == "abi":
+            import torch
+            stream = torch.cuda.current_stream(planes[0].device).cuda_stream if planes[0].is_cuda else None
+            self.grp.exchange(self.nk, planes[0].data_ptr(), planes[1].data_ptr(), planes[2].data_ptr(),
+                              self.psz[0], self.psz[1], stream)
             return
         views = self._views(planes)
         gloo = dist.get_backend(self.group) == "gloo" and self.device != "cpu" and str(self.device) != "cpu"

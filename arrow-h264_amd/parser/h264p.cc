@@ -1458,7 +1458,7 @@ void Decoder::finish_picture()
             if (q->slot == keep) q->slot = -1;
     }
     // the output frame: a field pair's second field fills the other rows of its first field's
-    // entry (dpb_combine_field_yuv picture.cc:573-590), whose POC is the pair's smaller one
+    // entry (dpb_combine_field_yuv picture.cc:578-622), whose POC is the pair's smaller one
     const int FH = fld ? 2 * H : H;
     // (vertical crop offsets count 2 chroma rows when the stream may hold fields, CropUnitY)
     const int cuy = psps_->frame_mbs_only ? 1 : 2;

@@ -274,7 +274,8 @@ def chain_run(args, rank: int, world: int, local: int, cs, rehearse: bool, nchai
         db.batch.ref_planes_stride = 3 * 32
         for t_ in ("out_y", "out_u", "out_v"):          # the sets replace the batch's own outputs
             del db.tensors[t_]
-        xch = D.BandExchange(bands, rank, W, H, nk, exchange, halo, "cuda") if world > 1 else None
+        xch = D.BandExchange(bands, rank, W, H, nk, exchange, halo, f"cuda:{local}",
+                             impl=getattr(args, "exchange_impl", "abi")) if world > 1 else None
         groups.append(dict(pics=pics, sets=sets, tabs=tabs, db=db, xch=xch, ev_ex=[]))
     comm = torch.cuda.Stream(device=local) if world > 1 else None
     stream = cs.cuda_stream
@@ -406,13 +407,21 @@ def chain_run(args, rank: int, world: int, local: int, cs, rehearse: bool, nchai
         "kernel_ms": {"inter": float(kern[0]), "intra": float(kern[1]), "deblock": float(kern[2]),
                       "batch_wall": float(kern[3])},
         "exchange": {"mode": exchange if world > 1 else None, "halo_mb_rows": halo, "max_abs_mvy_qpel": mvy,
+                     "impl": (getattr(args, "exchange_impl", "abi") if world > 1 else None),
                      "bytes_in_per_rank_per_step": xin,
-                     "ops_per_step": (0 if world == 1 else ng * (1 if exchange == "allgather" else
-                                                                 len(groups_peers(bands, rank, halo))))},
+                     "ops_per_step": (0 if world == 1 else ng * xch_ops(groups[0]["xch"], bands, rank, halo, exchange))},
         "cpu_baseline": cpu,
         "cpu_baseline_threads": cpu_mt,
         "verified_vs_oracle": verified,
     }
+
+
+def xch_ops(xch, bands, rank, halo, exchange):
+    """Transfers one group's exchange posts: the library's (h264r_group, point-to-point in both
+    modes), or the torch implementation's (one all-gather, or one send / receive per peer)."""
+    if xch.impl == "abi":
+        return len(xch.need) + len(xch.give)
+    return 1 if exchange == "allgather" else len(groups_peers(bands, rank, halo))
 
 
 def groups_peers(bands, rank, halo):
@@ -777,6 +786,9 @@ def main() -> int:
     ap.add_argument("--exchange", choices=["halo", "allgather"], default="halo",
                     help="chain mode at N > 1: rows within the motion vectors' reach from the neighbouring "
                          "bands (point-to-point), or every band (all-gather)")
+    ap.add_argument("--exchange-impl", choices=["abi", "torch"], default="abi",
+                    help="chain mode at N > 1: the exchange in the library (include/h264r_group.h: RCCL "
+                         "send / recv between pack and unpack kernels) or in torch.distributed calls")
     ap.add_argument("--no-n1", action="store_true", help="chain mode at N > 1: skip the one-GPU line of the same mode")
     ap.add_argument("--no-sliced", action="store_true",
                     help="N > 1 default: skip the slice-sharded config-5 chain line reported beside the replicas")

@@ -166,7 +166,7 @@ typedef struct h264r_quant {
  *     are horizontal get bS 3, not 4 (cond_bS4, deblock.cc:103-107,184-189).
  * Reference identity (deblocking) is (slot, parity).  DPB slots always hold frames: the
  * streaming API stores a field picture kept as a reference into its parity's rows of the slot
- * (dpb_combine_field_yuv picture.cc:573-590 without the copy), so the two fields of a frame
+ * (dpb_combine_field_yuv picture.cc:578-622 without the copy), so the two fields of a frame
  * share one slot and a frame picture may later reference the frame they make up. */
 #define H264R_REF_BOTTOM  0x40
 typedef struct h264r_pic {

@@ -140,7 +140,7 @@ def structure(p: dict) -> int:
 def output_frames(pics: list[dict], outs: list) -> list:
     """The decoded frames in output order.  A field pair (two consecutive field pictures of
     opposite parity, as the writer sends them) becomes one frame of interleaved rows
-    (dpb_combine_field_yuv, picture.cc:573-590) with the smaller of its POCs; frames are
+    (dpb_combine_field_yuv, picture.cc:578-622) with the smaller of its POCs; frames are
     ordered by POC inside each IDR period (a new period at every POC 0 after the first frame)
     -- the order the reference's DPB writes them (dpb.cc output process)."""
     frames, i = [], 0

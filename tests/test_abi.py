@@ -29,7 +29,7 @@ def header_symbols(name):
     return sorted(set(re.findall(r"\b(h264r_\w+)\s*\(", txt)))
 
 
-@pytest.mark.parametrize("hdr", ["h264r.h", "h264r_synth.h"])
+@pytest.mark.parametrize("hdr", ["h264r.h", "h264r_synth.h", "h264r_group.h"])
 def test_exports_every_declared_symbol(L, hdr):
     syms = header_symbols(hdr)
     assert len(syms) >= 5
@@ -43,6 +43,7 @@ def test_struct_layouts_match_c():
 #include <stddef.h>
 #include "h264r.h"
 #include "h264r_synth.h"
+#include "h264r_group.h"
 int main(void) {
   printf("%zu %zu %zu %zu %zu %zu\n", sizeof(h264r_mb), sizeof(h264r_slice), sizeof(h264r_quant),
          sizeof(h264r_pic), sizeof(h264r_batch), sizeof(h264r_synth_cfg));
@@ -50,6 +51,7 @@ int main(void) {
          offsetof(h264r_slice, ref_slot), offsetof(h264r_slice, implicit_w1));
   printf("%zu %zu %zu\n", offsetof(h264r_batch, ref_planes), offsetof(h264r_synth_cfg, seed),
          offsetof(h264r_batch, ref_planes_stride));
+  printf("%zu %zu\n", sizeof(h264r_transport), offsetof(h264r_transport, finish));
   return 0; }
 '''
     with tempfile.TemporaryDirectory() as td:
@@ -64,6 +66,8 @@ int main(void) {
     assert v[6:10] == [A.MB_DTYPE.fields["coef_off"][1], A.MB_DTYPE.fields["ipred"][1],
                        A.SLICE_DTYPE.fields["ref_slot"][1], A.SLICE_DTYPE.fields["implicit_w1"][1]]
     assert v[10:13] == [A.Batch.ref_planes.offset, A.SynthCfg.seed.offset, A.Batch.ref_planes_stride.offset]
+    from h264r import group as G
+    assert v[13:15] == [C.sizeof(G.Transport), G.Transport.finish.offset]
 
 
 def test_quant_flat_matches_oracle(L):
@@ -99,6 +103,10 @@ def test_no_gpu_means_no_decoder(L):
     assert L.h264r_create(C.byref(h), 0, 10, 10, 1, 8) == A.ENODEVICE
     with pytest.raises(h264r.H264RError):
         h264r.Decoder()
+    # a group over device planes needs the device too (host planes: device -1, test_dist.py)
+    from h264r import group as G
+    with pytest.raises(h264r.H264RError):
+        G.Group(2, 0, 0, "torch")
 
 
 @pytest.mark.parametrize("env", [{"H264R_DEBLOCK2_MIN": "abc"}, {"H264R_LEVELS": "99"}, {"H264R_COOP": "2"},

@@ -10,6 +10,8 @@ import torch.multiprocessing as mp
 
 from h264r import dist as D
 
+LIB = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "arrow-h264_amd", "lib", "libh264r.so")
+
 
 def _free_port() -> int:
     with socket.socket() as s:
@@ -107,7 +109,7 @@ def test_halo_rows():
     assert D.halo_plan([(0, 9), (9, 9)], 1, 3) == ({}, {})
 
 
-def _band_worker(rank, world, port, q):
+def _band_worker(rank, world, port, q, impl):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -129,7 +131,7 @@ def _band_worker(rank, world, port, q):
                     for k in range(nk):
                         for r in range(b0, b1):
                             v[k, r * rb[pl]:(r + 1) * rb[pl]] = value(k, pl, r).to(torch.uint8)
-                X = D.BandExchange(bands, rank, W, H, nk, mode, halo, "cpu")
+                X = D.BandExchange(bands, rank, W, H, nk, mode, halo, "cpu", impl=impl)
                 X.run(planes)
                 lo, hi = (0, H) if mode == "allgather" else (max(b0 - halo, 0), min(b1 + halo, H))
                 if b1 <= b0 and mode == "halo":
@@ -149,12 +151,18 @@ def _band_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
+IMPLS = ["torch", pytest.param("abi", marks=pytest.mark.skipif(not os.path.exists(LIB), reason="libh264r.so not built"))]
+
+
+@pytest.mark.parametrize("impl", IMPLS)
 @pytest.mark.parametrize("world", [2, 3])
-def test_gloo_band_exchange(world):
+def test_gloo_band_exchange(world, impl):
+    """BandExchange in both implementations: torch.distributed calls, and the library's
+    h264r_group (include/h264r_group.h) over its callback transport, host planes."""
     port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_band_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_band_worker, args=(r, world, port, q, impl)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted(q.get(timeout=120) for _ in procs)
@@ -164,7 +172,7 @@ def test_gloo_band_exchange(world):
     assert [r[1] for r in res] == [True] * world
 
 
-def _band_worker_c5(rank, world, port, q):
+def _band_worker_c5(rank, world, port, q, impl):
     """Config 5's real geometry: 2160p = 135 MB rows in 8 slices of
     17 / 16 rows (synth.c slice_of_row), one band per rank, halo 3 MB rows (|mv_y| <= 32.75 px,
     dist.halo_mb_rows(131)) -- six interior ranks with two peers each -- in both modes."""
@@ -187,7 +195,7 @@ def _band_worker_c5(rank, world, port, q):
                 for k in range(nk):
                     for r in range(b0, b1):
                         v[k, r * rb[pl]:(r + 1) * rb[pl]] = rowval[k][pl][r]
-            X = D.BandExchange(bands, rank, W, H, nk, mode, halo, "cpu")
+            X = D.BandExchange(bands, rank, W, H, nk, mode, halo, "cpu", impl=impl)
             X.run(planes)
             lo, hi = (0, H) if mode == "allgather" else (max(b0 - halo, 0), min(b1 + halo, H))
             for pl in range(3):
@@ -206,11 +214,12 @@ def _band_worker_c5(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_gloo_world8_config5_bands():
+@pytest.mark.parametrize("impl", IMPLS)
+def test_gloo_world8_config5_bands(impl):
     world, port = 8, _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_band_worker_c5, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_band_worker_c5, args=(r, world, port, q, impl)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted(q.get(timeout=300) for _ in procs)
@@ -219,3 +228,58 @@ def test_gloo_world8_config5_bands():
         assert p.exitcode == 0
     assert [r[1] for r in res] == [True] * world
     assert [tuple(r[2]) for r in res] == [(0, 17), (17, 34), (34, 51), (51, 68), (68, 85), (85, 102), (102, 118), (118, 135)]
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="libh264r.so not built")
+def test_group_plan_matches_halo_plan():
+    """h264r_group_plan (the C ABI's plan) == dist.halo_plan in halo mode, and the all-gather plan
+    (every other nonempty band whole), over random slice layouts, world 1..9."""
+    import random
+    from h264r import group as G
+    rnd = random.Random(5)
+    for _ in range(300):
+        world = rnd.randint(1, 9)
+        H = rnd.randint(1, 40)
+        starts = sorted({0} | {rnd.randrange(H) for _ in range(rnd.randint(0, 8))})
+        bands = D.slice_bands(starts, H, world)
+        halo = rnd.randint(0, 4)
+        for rank in range(world):
+            assert G.plan(bands, rank, "halo", halo) == D.halo_plan(bands, rank, halo)
+            need, give = G.plan(bands, rank, "allgather")
+            assert need == {r: b for r, b in enumerate(bands) if r != rank and b[1] > b[0]}
+            b0, b1 = bands[rank]
+            assert give == ({r: (b0, b1) for r in range(world) if r != rank} if b1 > b0 else {})
+            # pairwise consistency: what rank sends to r is what r receives from rank
+            for r in range(world):
+                if r != rank:
+                    assert G.plan(bands, r, "halo", halo)[0].get(rank) == G.plan(bands, rank, "halo", halo)[1].get(r)
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="libh264r.so not built")
+def test_group_argument_errors():
+    import ctypes as C
+    import h264r
+    from h264r import group as G
+    L = h264r.lib()
+    with pytest.raises(h264r.H264RError):
+        G.plan([(0, 4), (4, 8)], 2)                       # rank outside the world
+    with pytest.raises(KeyError):
+        G.plan([(0, 4), (4, 8)], 0, "ring")
+    b = (C.c_int32 * 4)(0, 4, 4, 8)
+    n = (C.c_int32 * 4)()
+    assert L.h264r_group_plan(2, 0, b, 7, 1, n, n) == h264r.A.EINVAL
+    assert L.h264r_group_plan(2, 0, b, 0, -1, n, n) == h264r.A.EINVAL
+    assert L.h264r_group_exchange(None, 1, None, None, None, 0, 0, None) == h264r.A.EINVAL
+    h = C.c_void_p()
+    assert L.h264r_group_create_transport(C.byref(h), -1, 2, 0, None) == h264r.A.EINVAL
+    assert L.h264r_group_create(C.byref(h), -1, 2, 0, bytes(128)) == h264r.A.EINVAL
+    # a transport group before set_bands: the exchange is out of order
+    g = G.Group(1, 0, -1, "torch")
+    buf = (C.c_uint8 * 4096)()
+    with pytest.raises(h264r.H264RError):
+        g.exchange(1, C.addressof(buf), C.addressof(buf), C.addressof(buf), 256, 64)
+    g.set_bands(1, 1, [(0, 1)], "halo", 1, 2)
+    g.exchange(1, C.addressof(buf), C.addressof(buf), C.addressof(buf), 256, 64)   # world 1: nothing to move
+    with pytest.raises(h264r.H264RError):
+        g.set_bands(1, 1, [(0, 2)], "halo", 1, 2)         # a band below the picture
+    g.close()

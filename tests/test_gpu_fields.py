@@ -111,7 +111,7 @@ def test_gpu_field_pair_shares_a_slot(L, dec):
     """The streaming API (the shim's path): an I top field kept as slot 5, the bottom field
     predicting from it (its complementary field, slot 5's top rows) and from slot 0's fields,
     kept into slot 5's bottom rows, then a frame picture predicting from the frame the two
-    fields make up (dpb_combine_field_yuv picture.cc:573-590) -- each against the oracle."""
+    fields make up (dpb_combine_field_yuv picture.cc:578-622) -- each against the oracle."""
     W, FH = 22, 18
     icfg = synth.default_cfg(L, 2, W, FH // 2, structure=1, seed=0x81)
     pcfg = synth.default_cfg(L, 3, W, FH // 2, structure=2, num_refs=3, seed=0x82)
