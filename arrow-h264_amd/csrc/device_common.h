@@ -261,10 +261,11 @@ DEV int lane_xor4(int v)
 // The value of the lane of this lane's quad pair (lane, lane ^ 4) whose bit 2 is clear (lo) or
 // set (hi): one banked DPP row shift each, keeping the own value in the other banks, where the
 // exchange needed two moves plus a select per output.  (The pair (lane, lane ^ 1) form by
-// quad_perm [0,0,2,2] / [1,1,3,3] is exact in isolation, tools/dpp/dpp_test.hip, but gave wrong
-// residuals inside k_inter4r / the intra kernels once the compiler folded the moves into their
-// consumers -- exact again with the results kept opaque, and no faster; not used.  These two
-// are verified as folded by every GPU parity test: re-run them after touching a caller.)
+// quad_perm [0,0,2,2] / [1,1,3,3] gave wrong residuals inside k_inter4r once the compiler folded
+// the moves into v_subrev_u32_dpp, a reversed opcode, to which MI355X applies the lane select on
+// src1 instead of src0 (tools/dpp/dpp_fold_test.hip); not used.  tests/test_isa.py refuses any
+// reversed opcode with DPP in the built library and holds the other forms -- these two's folds
+// included -- to the set the GPU parity suite verified.)
 DEV int lane_lo4(int v) { return __builtin_amdgcn_update_dpp(v, v, 0x114, 0xF, 0xA, false); }   // banks 1, 3: lane - 4
 DEV int lane_hi4(int v) { return __builtin_amdgcn_update_dpp(v, v, 0x104, 0xF, 0x5, false); }   // banks 0, 2: lane + 4
 

@@ -29,11 +29,9 @@
 #endif
 
 namespace h264r { struct DbInfo; }
-extern "C" __global__ void k_inter4r(h264r_batch b, h264r::DbInfo* dbinfo, int2 rows, int* sp_flag, uint8_t* recon,
-                                     const int* inter_cnt, int tag);
-extern "C" __global__ void k_dbinfo(h264r_batch b, h264r::DbInfo* dbinfo, int2 rows, int* inter_cnt, int tag, int* zero,
-                                    int nz, int* zero2, int nz2, int per);
-extern "C" __global__ void k_inter_sp(h264r_batch b, int2 rows, const int* sp_flag, uint8_t* recon);
+extern "C" __global__ void k_inter4r(h264r_batch b, h264r::DbInfo* dbinfo, int2 rows, int* sp_flag, uint8_t* recon, int tag,
+                                     int* zero, int nz, int* zero2, int nz2);
+extern "C" __global__ void k_inter_sp(h264r_batch b, int2 rows, const int* sp_flag, uint8_t* recon, int tag);
 extern "C" __global__ void k_untile(h264r_batch b, int2 rows, const uint8_t* recon);
 extern "C" __global__ void k_intra_pic(h264r_batch b, int* sync, int* err, const uint16_t* lvl, int lmax, int2 rows,
                                       int gstep, uint8_t* recon, const int* pband);
@@ -112,7 +110,7 @@ int dev_resize(T** p, size_t* cap, size_t n)
 struct Scratch {
     uint8_t* d_dbinfo = nullptr; size_t c_dbinfo = 0;
     int* d_sync = nullptr; size_t c_sync = 0;
-    int tag = 0;                    // launch-sequence tag of k_dbinfo's per-picture inter flags (> 0)
+    int tag = 0;                    // launch-sequence tag (> 0): k_inter4r's SP word
     uint8_t* d_hb = nullptr; size_t c_hb = 0;
     uint32_t epoch = 0;             // tag of the deblocking hand-off records of the last launch
     uint8_t* d_hb2 = nullptr; size_t c_hb2 = 0;
@@ -501,13 +499,13 @@ static h264r_batch sub_batch(const h264r_batch& b, int p0, int n)
 }
 
 // ints of one launch sequence's sync region: [intra ticket + per-(picture, row) progress]
-// [deblock ticket][level barrier, deepest level][SP inter MBs seen] + the deblocking kernels'
-// per-XCD ticket counters, done count, then per picture the waves of k_dbinfo that met an inter
-// or I_PCM MB (k_inter4r skips the pictures without one)
-// (two sets of deblocking counters: the split walk's luma and chroma kernels run together)
-// and per picture the walk's bands holding an MB deeper than the level lists (k_level -> k_intra_pic)
-// (and, before the inter flags, k_intra_levels' sharded grid barrier: 8 shard counters + top)
-static size_t sync_ints(int P, int H) { return 1 + (size_t)P * H + 5 + 18 + 9 + 2 * (size_t)P; }
+// [deblock ticket][level barrier, deepest level][2 unused] + the deblocking kernels' per-XCD
+// ticket counters and done count (two sets: the split walk's luma and chroma kernels run
+// together) + k_intra_levels' sharded grid barrier (8 shard counters + top) -- these 1 + P H + 32
+// are zeroed by k_inter4r -- then per picture the walk's bands holding an MB deeper than the
+// level lists (k_level -> k_intra_pic), and last the SP tag word (k_inter4r stores the launch
+// tag when it met an inter MB of an SP slice).
+static size_t sync_ints(int P, int H) { return 1 + (size_t)P * H + 32 + (size_t)P + 1; }
 
 // One launch sequence's share of the scratch (the whole batch, or one chunk of the overlapped
 // schedule): its pictures, their deblocking records and MB-tiled reconstruction, its sync region.
@@ -518,8 +516,8 @@ struct Stage {
     int* sync;
 };
 
-// The reconstruction of a stage on stream s: k_dbinfo + k_inter4r + k_inter_sp (inter / PCM MBs
-// and the deblocking records), k_level + k_level_scatter + k_intra_levels +
+// The reconstruction of a stage on stream s: k_inter4r + k_inter_sp (the deblocking records and
+// the inter / PCM MBs), k_level + k_level_scatter + k_intra_levels +
 // k_intra_pic (intra MBs).  The level lists are one set: stages on one stream reuse them in order.
 static int recon_launches(h264r_ctx* c, const Stage& S, hipStream_t s, int2 rows, Scratch& X, bool levels, bool coop)
 {
@@ -533,32 +531,23 @@ static int recon_launches(h264r_ctx* c, const Stage& S, hipStream_t s, int2 rows
     const int groups = (W * HB + 15) / 16;
     // groups per workgroup (launch_cfg.h), 8 XCD bands (k_recon.hip inter4_groups)
     const dim3 igrid(8 * ((groups + 8 * H264R_INTER_GROUPS - 1) / (8 * H264R_INTER_GROUPS)), P);
-    // k_dbinfo: H264R_DBINFO_GROUPS groups per workgroup (its LDS tables filled once for them) when
-    // that still makes >= 2048 workgroups; one group each below (the latency chain's lone picture:
-    // 64 workgroups walking 8 groups each took 20 us)
-    const int dper = (int64_t)P * groups >= 2048LL * H264R_DBINFO_GROUPS ? H264R_DBINFO_GROUPS : 1;
-    const dim3 dgrid(8 * ((groups + 8 * dper - 1) / (8 * dper)), P);
     {
         Timed t(c, 0, s);
-        int* sp_flag = sync + 1 + (size_t)P * H + 4;
-        // the deblocking records first (k_inter4r then fits 4 waves/SIMD), with per picture
-        // a flag that an inter or I_PCM MB was met (profiles/r03_f_dbinfo_ab.txt, r03_h_inter_ab.txt)
-        int* inter_cnt = sync + 1 + (size_t)P * H + 32;
-        // k_dbinfo zeroes the stage's sync words before the flags and the level counters
+        int* sp_flag = sync + 1 + (size_t)P * H + 32 + P;    // not zeroed: compared with the tag
+        // the deblocking records and the inter / I_PCM reconstruction in one launch, which also
+        // zeroes the stage's sync words and the level counters
         if (++X.tag <= 0) X.tag = 1;
-        hipLaunchKernelGGL(k_dbinfo, dgrid, dim3(256), 0, s, b, S.dbinfo, rows, inter_cnt, X.tag, sync, (int)(1 + (size_t)P * H + 32),
-                           levels ? X.d_lcnt : nullptr, levels ? 3 * LEVEL_IDS : 0, dper);
-        HIP_OK(hipGetLastError());
-        hipLaunchKernelGGL(k_inter4r, igrid, dim3(256), 0, s, b, S.dbinfo, rows, sp_flag, recon, (const int*)inter_cnt, X.tag);
+        hipLaunchKernelGGL(k_inter4r, igrid, dim3(256), 0, s, b, S.dbinfo, rows, sp_flag, recon, X.tag, sync,
+                           (int)(1 + (size_t)P * H + 32), levels ? X.d_lcnt : nullptr, levels ? 3 * LEVEL_IDS : 0);
         HIP_OK(hipGetLastError());
         // inter MBs of SP slices (a short launch when the batch has none)
-        hipLaunchKernelGGL(k_inter_sp, dim3(1024), dim3(256), 0, s, b, rows, (const int*)sp_flag, recon);
+        hipLaunchKernelGGL(k_inter_sp, dim3(1024), dim3(256), 0, s, b, rows, (const int*)sp_flag, recon, X.tag);
         HIP_OK(hipGetLastError());
     }
     {
         Timed t(c, 1, s);
         uint16_t* lvl = levels ? X.d_lvl : nullptr;
-        int* pband = sync + 1 + (size_t)P * H + 32 + P;        // after the inter flags
+        int* pband = sync + 1 + (size_t)P * H + 32;             // after the zeroed words
         int* lbar = sync + 1 + (size_t)P * H + 23;               // k_intra_levels' barrier (9 ints)
         const int lmax = levels ? level_launches((size_t)P * W * HB) : 0;
         if (knobs().verbose) fprintf(stderr, "h264r: %d intra levels from lists, %d pictures\n", lmax, P);
@@ -741,7 +730,7 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
     }
     const size_t sync_n = (size_t)nch * sync_ints(chunk_min + 1, H);
     {
-        // each stage's k_dbinfo zeroes its sync words; fresh memory is zeroed once, so no stale
+        // each stage's k_inter4r zeroes its sync words; fresh memory is zeroed once, so no stale
         // inter flag can carry a live tag
         const size_t cap_before = X.c_sync;
         if ((st = dev_resize(&X.d_sync, &X.c_sync, sync_n))) return st;

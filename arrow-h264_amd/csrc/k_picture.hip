@@ -455,7 +455,7 @@ extern "C" __global__ __launch_bounds__(1024) void k_level_scatter(h264r_batch b
 // and every workgroup waits on the top counter, then acquires.  One counter for all the
 // ~1000 arrivals had serialised them (MI355X_MICROARCH.md price list 'barrier-counter' vs
 // 'barrier-xcd', 'fanin').  Each wave takes its level's items grid-stride.
-// bar: [0..7] shard counters, [8] top counter, zeroed per batch (by k_dbinfo); L = 1, 2, ...
+// bar: [0..7] shard counters, [8] top counter, zeroed per batch (by k_inter4r); L = 1, 2, ...
 DEV bool grid_barrier(int* bar, int L, int* err)
 {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

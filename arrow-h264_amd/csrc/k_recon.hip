@@ -1,7 +1,7 @@
 // k_recon.hip -- the fully parallel part of a batch.
 //
-// k_dbinfo  the per-MB deblocking record DbInfo of every MB (mb_inter4.h dbinfo_block).
-// k_inter4r four MBs per wave, one lane per 4x4 block: inter MBs and I_PCM reconstructed
+// k_inter4r four MBs per wave, one lane per 4x4 block: the per-MB deblocking record DbInfo of
+//           every MB (mb_inter4.h dbinfo_block), then inter MBs and I_PCM reconstructed
 //           (mb_inter4.h); intra MBs are left to the intra kernels (they depend on their
 //           neighbours).  Motion is read as the parser left it ({mv, ref_idx} per list) and
 //           RefPicList[l][ref_idx] resolved to a DPB slot through an LDS copy of the
@@ -49,8 +49,8 @@ DEV void inter4_lds_store(const h264r_batch& b, const LdsRegs& r, Inter4Lds& S)
 }
 DEV void inter4_lds(const h264r_batch& b, int pic, Inter4Lds& S) { inter4_lds_store(b, inter4_lds_load(b, pic), S); }
 
-// The 16-MB groups [grp, gend) of one k_inter4 / k_dbinfo workgroup: XCD-aware (below),
-// `per` (H264R_INTER_GROUPS / H264R_DBINFO_GROUPS, launch_cfg.h) consecutive groups of its
+// The 16-MB groups [grp, gend) of one k_inter4r workgroup: XCD-aware (below),
+// `per` (H264R_INTER_GROUPS, launch_cfg.h) consecutive groups of its
 // XCD's band per workgroup, so that the workgroup's LDS tables are filled once for several
 // groups.
 DEV bool inter4_groups(const Geom& g, int2 rows, int per, int& grp, int& gend)
@@ -62,63 +62,27 @@ DEV bool inter4_groups(const Geom& g, int2 rows, int per, int& grp, int& gend)
     return grp < gend;
 }
 
-// sp_flag: set when an inter MB of an SP slice was met (k_inter_sp then runs).
+// k_inter4r: per 16-MB group of a workgroup, first the deblocking records DbInfo of the group's
+// MBs (dbinfo_block: their neighbour records and motion are loaded with the group's own record and
+// motion), then the reconstruction of its inter and I_PCM MBs (inter4_mbs); the records' registers
+// are dead before the motion compensation starts (126 VGPRs, 4 waves/SIMD).  Round 6 folded the
+// records' own kernel (k_dbinfo, 1.2 ms per 1024 config-3 pictures at 8 waves/SIMD) into it:
+// config 3 11.96 -> 11.78 ms, config 4 4.64 -> 4.53 ms; all-intra config 2 13.87 -> 14.15 ms
+// (its records now run at 4 waves/SIMD; profiles/r06_e_fused_dbinfo_ab.txt).
+// It also zeroes the launch sequence's sync words and level counters (zero[0 .. nz), zero2[0 ..
+// nz2)) for the kernels after it -- no memset launches per batch (the latency chain paid ~20 us
+// for them, profiles/r05_ac_latency_kernels.txt).
+// sp_flag: set to the launch tag when an inter MB of an SP slice was met (k_inter_sp then runs; a
+// tag, not a flag, so nothing has to zero it between launch sequences -- it lies outside the
+// words this kernel zeroes).
 // Grid (8 * ceil(groups / (8 * per)), pictures), XCD-aware: workgroups go round-robin to the 8
 // XCDs in launch order, so blockIdx.x % 8 is the XCD and it takes the 16-MB groups of band
 // blockIdx.x % 8 (one eighth of the MB rows) of every picture: an XCD's motion
 // compensation reads only its band of the reference pictures (+ the MV reach), which its
 // 4 MB L2 holds, instead of every XCD streaming whole references through its L2.
-DEV void inter4_kernel(const h264r_batch& b, int2 rows, int* sp_flag, uint8_t* recon, Inter4Lds& S, const int* inter_cnt,
-                       int tag)
-{
-    const int pic = blockIdx.y;
-    const Geom g = make_geom(b.width_mbs, b.height_mbs);
-    int grp, gend;
-    if (!inter4_groups(g, rows, H264R_INTER_GROUPS, grp, gend)) return;
-    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int aend = rows.y * g.wmb;
-    int a0 = rows.x * g.wmb + (grp * 4 + wave) * 4;
-    Inter4Pre pre = inter4_pre(b, g, pic, a0, aend, lane);
-    // a picture k_dbinfo found no inter or I_PCM MB in (all-intra) has nothing for this kernel;
-    // the flag is loaded with the records, so it adds no round trip
-    const int has_inter = inter_cnt ? inter_cnt[pic] == tag : 1;
-    const LdsRegs lr = inter4_lds_load(b, pic);
-    if (__builtin_amdgcn_readfirstlane(has_inter) == 0) return;
-    inter4_lds_store(b, lr, S);
-    __syncthreads();
-    for (;;) {
-        if (a0 >= aend) return;
-        // the lane, opaque per group: what derives from it is recomputed per group, not
-        // hoisted out of the loop and kept live across it (that spilled 144 B per lane)
-        int ln = lane;
-        asm volatile("" : "+v"(ln));
-        inter4_mbs<false>(b, g, pic, a0, aend, ln, S, sp_flag, pre, recon);
-        if (++grp >= gend) return;
-        a0 = rows.x * g.wmb + (grp * 4 + wave) * 4;
-        int ln2 = lane;
-        asm volatile("" : "+v"(ln2));
-        pre = inter4_pre(b, g, pic, a0, aend, ln2);
-    }
-}
-
 extern "C" __global__ __launch_bounds__(256, H264R_INTER_WAVES) void k_inter4r(h264r_batch b, DbInfo* dbinfo, int2 rows,
-                                                                              int* sp_flag, uint8_t* recon,
-                                                                              const int* inter_cnt, int tag)
-{
-    (void)dbinfo;
-    __shared__ Inter4Lds S;
-    inter4_kernel(b, rows, sp_flag, recon, S, inter_cnt, tag);
-}
-
-// k_dbinfo: the deblocking records DbInfo of every MB (dbinfo_block, mb_inter4.h) on their
-// own -- they depend on the MB records and motion only, not on any sample; launched before
-// k_inter4r.  Same grid and lane roles as k_inter4r.
-// k_dbinfo also zeroes the launch sequence's sync words and level counters (zero[0 .. nz),
-// zero2[0 .. nz2)) for the kernels after it -- two memset launches less per batch (the latency
-// chain paid ~20 us for them, profiles/r05_ac_latency_kernels.txt) -- and marks a picture with
-// an inter or I_PCM MB by storing this launch's tag (nonzero), so the flags need no zeroing.
-extern "C" __global__ __launch_bounds__(256, 8) void k_dbinfo(h264r_batch b, DbInfo* dbinfo, int2 rows, int* inter_cnt, int tag,
-                                                             int* zero, int nz, int* zero2, int nz2, int per)
+                                                                               int* sp_flag, uint8_t* recon, int tag,
+                                                                               int* zero, int nz, int* zero2, int nz2)
 {
     {
         const int nt = (int)(gridDim.x * gridDim.y * blockDim.x);
@@ -127,48 +91,53 @@ extern "C" __global__ __launch_bounds__(256, 8) void k_dbinfo(h264r_batch b, DbI
         for (int i = t; i < nz2; i += nt) zero2[i] = 0;
     }
     __shared__ Inter4Lds S;
+    __shared__ DbTables T;
     const int pic = blockIdx.y;
     const Geom g = make_geom(b.width_mbs, b.height_mbs);
     int grp, gend;
-    if (!inter4_groups(g, rows, per, grp, gend)) return;
+    if (!inter4_groups(g, rows, H264R_INTER_GROUPS, grp, gend)) return;
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int aend = rows.y * g.wmb;
     const h264r_slice* slices = b.slices + (size_t)pic * b.slice_stride;
-    // the first group's record, motion and neighbour loads go out before the LDS tables are
-    // filled; every later group's right after the previous group's use
     int a0 = rows.x * g.wmb + (grp * 4 + wave) * 4;
-    __shared__ DbTables T;
     const uint2 tv = db_tables_load(threadIdx.x);
     Inter4Pre pre = inter4_pre(b, g, pic, a0, aend, lane);
     DbNb nb = dbinfo_pre(b, g, pic, a0, aend, lane);
+    const LdsRegs lr = inter4_lds_load(b, pic);
     db_tables_store(T, threadIdx.x, tv);
-    inter4_lds(b, pic, S);
+    inter4_lds_store(b, lr, S);
     __syncthreads();
-    bool inter = false;                      // an inter or I_PCM MB met (k_inter4r has work)
     for (;;) {
-        if (a0 >= aend) break;
-        const int a = a0 + (lane >> 4);
-        const bool valid = a < aend;
-        const int aa = valid ? a : aend - 1;
-        inter |= __any(valid && (!mb_is_intra(pre.q) || pre.q.mb_type == H264R_I_PCM)) != 0;
-        const uint2 m0 = motion_word(pre.mv[0], pre.ri[0], slices, S, pre.q.slice, 0);
-        const uint2 m1 = motion_word(pre.mv[1], pre.ri[1], slices, S, pre.q.slice, 1);
-        dbinfo_block(b, g, pic, aa, valid, lane & 15, S, T, pre.q, m0, m1, slice_hdr(slices, S, pre.q.slice), nb,
-                     dbinfo + (size_t)pic * g.nmb);
-        if (++grp >= gend) break;
+        if (a0 >= aend) return;
+        {
+            const int a = a0 + (lane >> 4);
+            const bool valid = a < aend;
+            const int aa = valid ? a : aend - 1;
+            const uint2 m0 = motion_word(pre.mv[0], pre.ri[0], slices, S, pre.q.slice, 0);
+            const uint2 m1 = motion_word(pre.mv[1], pre.ri[1], slices, S, pre.q.slice, 1);
+            dbinfo_block(b, g, pic, aa, valid, lane & 15, S, T, pre.q, m0, m1, slice_hdr(slices, S, pre.q.slice), nb,
+                         dbinfo + (size_t)pic * g.nmb);
+        }
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        inter4_mbs<false>(b, g, pic, a0, aend, ln, S, sp_flag, pre, recon, tag);
+        if (++grp >= gend) return;
         a0 = rows.x * g.wmb + (grp * 4 + wave) * 4;
-        pre = inter4_pre(b, g, pic, a0, aend, lane);
-        nb = dbinfo_pre(b, g, pic, a0, aend, lane);
+        int ln2 = lane;
+        asm volatile("" : "+v"(ln2));
+        pre = inter4_pre(b, g, pic, a0, aend, ln2);
+        nb = dbinfo_pre(b, g, pic, a0, aend, ln2);
     }
-    if (inter_cnt && inter && lane == 0) inter_cnt[pic] = tag;       // every writer stores the tag
 }
+
 
 // k_inter_sp: the inter MBs of SP slices (inverse_transform_sp), after k_inter4.  A
 // persistent grid that leaves at once unless k_inter4 set sp_flag (so a batch without SP
 // slices pays one short launch), then strides over (16-MB group, picture).
-extern "C" __global__ __launch_bounds__(256) void k_inter_sp(h264r_batch b, int2 rows, const int* sp_flag, uint8_t* recon)
+extern "C" __global__ __launch_bounds__(256) void k_inter_sp(h264r_batch b, int2 rows, const int* sp_flag, uint8_t* recon,
+                                                             int tag)
 {
-    if (!__hip_atomic_load(sp_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+    if (__hip_atomic_load(sp_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != tag) return;
     __shared__ Inter4Lds S;
     const Geom g = make_geom(b.width_mbs, b.height_mbs);
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -180,7 +149,7 @@ extern "C" __global__ __launch_bounds__(256) void k_inter_sp(h264r_batch b, int2
         inter4_lds(b, pic, S);
         __syncthreads();
         const int a0 = rows.x * g.wmb + (grp * 4 + wave) * 4;
-        if (a0 < aend) inter4_mbs<true>(b, g, pic, a0, aend, lane, S, nullptr, inter4_pre(b, g, pic, a0, aend, lane), recon);
+        if (a0 < aend) inter4_mbs<true>(b, g, pic, a0, aend, lane, S, nullptr, inter4_pre(b, g, pic, a0, aend, lane), recon, 0);
     }
 }
 

@@ -3,13 +3,9 @@
 
 // consecutive 16-MB groups per workgroup (k_recon.hip): k_inter4 / k_inter4r (1: with
 // more, loop-carried state spilled and config 3 lost 2 %, profiles/r03_h_inter_ab.txt; 2
-// still costs config 3 4 % while config 4 gains 2 %, profiles/r03s2_s_ab.txt), k_dbinfo
-// (8: its next group's loads overlap this group, +0.6 % on config 3 over 4, 2 loses)
+// still costs config 3 4 % while config 4 gains 2 %, profiles/r03s2_s_ab.txt)
 #ifndef H264R_INTER_GROUPS
 #define H264R_INTER_GROUPS 1
-#endif
-#ifndef H264R_DBINFO_GROUPS
-#define H264R_DBINFO_GROUPS 8
 #endif
 
 // k_deblock2: MB rows per wave, walked in lock step one MB apart (k_deblock2.hip); the

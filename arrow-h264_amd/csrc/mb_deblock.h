@@ -77,7 +77,7 @@ constexpr int DEBLOCK2_UNITS = 64 / H264R_DB2_LPU;   // k_deblock2: (picture, MB
 // alpha | beta << 8 | tc0(bS 1..3) << 16 / 21 / 26 for one edge: filter_edge
 // deblock.cc:469-480 (qPav of the two MBs' QPs, indexA/B with MbQ's slice offsets),
 // 8-bit tables (Tables 8-16 / 8-17, deblock.cc:294-324).
-// ab / tc0: DB_AB / DB_TC0 or a copy of them (k_dbinfo keeps one in LDS: read from global
+// ab / tc0: DB_AB / DB_TC0 or a copy of them (k_inter4r keeps one in LDS: read from global
 // memory, the lookup was a dependent round trip per 16-MB group)
 DEV uint32_t edge_word(int qpp, int qpq, int offa, int offb, const uint32_t* ab = DB_AB, const uint32_t* tc0 = DB_TC0)
 {

@@ -121,7 +121,7 @@ DEV Inter4Pre inter4_pre(const h264r_batch& b, const Geom& g, int pic, int a0, i
 
 // What the deblocking record of a lane's block reads besides its own MB: the left and upper
 // MB records and the motion of the blocks left of and above it (the MB's own blocks or the
-// neighbours'), loaded unconditionally and with no dependence on the MB record, so k_dbinfo
+// neighbours'), loaded unconditionally and with no dependence on the MB record, so k_inter4r
 // issues them together with inter4_pre's loads (one global round trip per group).
 struct DbNb {
     h264r_mb L, U;
@@ -474,7 +474,7 @@ DEV int mb_qp(const h264r_mb& m, int pl)
 // The deblocking record of one MB's 4x4 block (Deblock::strength deblock.cc:78-289,
 // edge parameters :469-480): the block's left edge (vertical edge bx, segment by) and top
 // edge (horizontal edge by, segment bx), and for blk < 9 one alpha/beta/tc0 word.  Inside
-// k_inter4 after the reconstruction (DB = true), or its own kernel k_dbinfo.
+// k_inter4r, before the group's reconstruction.
 DEV void dbinfo_block(const h264r_batch& b, const Geom& g, int pic, int aa, bool valid, int blk, const Inter4Lds& S, const DbTables& T,
                       const h264r_mb& q, uint2 m0, uint2 m1, uint2 qsh, const DbNb& nb, DbInfo* __restrict__ dbout)
 {
@@ -554,12 +554,12 @@ DEV void dbinfo_block(const h264r_batch& b, const Geom& g, int pic, int aa, bool
 }
 
 // The inter / I_PCM macroblocks a0 .. a0+3 of picture `pic` (their deblocking records come
-// from k_dbinfo).  SP = false (k_inter4r): inter MBs of SP slices are left out and flagged in
-// *sp_flag; SP = true (k_inter_sp): only those are reconstructed, with inverse_transform_sp
+// first, dbinfo_block).  SP = false (k_inter4r): inter MBs of SP slices are left out and flagged in
+// *sp_flag (the launch tag); SP = true (k_inter_sp): only those are reconstructed, with inverse_transform_sp
 // (decoder.cc:256-257, transform.cc:1267-1300).
 template <bool SP>
 DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int aend, int lane,
-                    const Inter4Lds& S, int* sp_flag, const Inter4Pre& pre, uint8_t* __restrict__ recon)
+                    const Inter4Lds& S, int* sp_flag, const Inter4Pre& pre, uint8_t* __restrict__ recon, int tag)
 {
     const int grp = lane >> 4, blk = lane & 15, bx = blk & 3, by = blk >> 2;
     const int a = a0 + grp;
@@ -585,7 +585,7 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
         if (!valid || (mb_is_intra(q) && !pcm)) return;              // intra: k_intra_* (lanes idle here)
         const bool sp_mb = q_type == H264R_SLICE_SP && !mb_is_intra(q);
         if constexpr (!SP) {
-            if (sp_mb) { *sp_flag = 1; return; }                     // k_inter_sp's
+            if (sp_mb) { *sp_flag = tag; return; }                   // k_inter_sp's
         } else {
             if (!sp_mb) return;
         }

@@ -188,7 +188,10 @@ class BandExchange:
         self.wide = max(b1 - b0 for b0, b1 in self.bands)
         self.device = device
         if impl == "abi":
-            from .group import Group
+            from .group import Group, plan
+            # the library's plan (h264r_group_plan): in all-gather mode a rank with an empty band
+            # sends nothing
+            self.need, self.give = plan(self.bands, rank, mode, halo)
             dev = torch.device(device)
             gloo = dist.get_backend(group) == "gloo"
             self.grp = Group(self.world, rank, dev.index if dev.type == "cuda" else -1,

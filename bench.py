@@ -194,6 +194,34 @@ def latency_chain(dec, L, cfg, refs, stream, n: int, verify: int):
     return (time.perf_counter() - t0) / n * 1e3, n, verified
 
 
+class GpuTurn:
+    """Rehearsal only (H264R_BENCH_REHEARSE=1: several ranks on one GPU): one rank's decode on the
+    device at a time.  Two processes' launch sequences side by side on one GPU can starve each
+    other's k_intra_levels, whose grid barrier needs the whole grid resident; the bounded wait
+    then expires and h264r_check reports H264R_EDEVICE.  A file lock held from the launch until
+    the device has drained keeps the decodes apart (the exchange still runs concurrently).  On
+    separate GPUs (the real N > 1 run) this is a no-op."""
+
+    def __init__(self, on: bool):
+        self.fd = None
+        if on:
+            self.fd = open(f"/tmp/h264r_rehearse_{os.environ.get('MASTER_PORT', '0')}.lock", "w")
+
+    def __enter__(self):
+        if self.fd is not None:
+            import fcntl
+            fcntl.flock(self.fd, fcntl.LOCK_EX)
+        return self
+
+    def __exit__(self, *exc):
+        if self.fd is not None:
+            import fcntl
+            import torch
+            torch.cuda.synchronize()
+            fcntl.flock(self.fd, fcntl.LOCK_UN)
+        return False
+
+
 def chain_run(args, rank: int, world: int, local: int, cs, rehearse: bool, nchains: int, cfg_idx: int,
               exchange: str) -> dict:
     """Dependent chains, slice-sharded.  `nchains` chains advance
@@ -280,6 +308,7 @@ def chain_run(args, rank: int, world: int, local: int, cs, rehearse: bool, nchai
     comm = torch.cuda.Stream(device=local) if world > 1 else None
     stream = cs.cuda_stream
     nstep = [0]
+    turn = GpuTurn(rehearse and world > 1)
 
     def step():
         t = nstep[0]
@@ -292,7 +321,8 @@ def chain_run(args, rank: int, world: int, local: int, cs, rehearse: bool, nchai
             b.out_y, b.out_u, b.out_v = (x.data_ptr() for x in wr)
             b.ref_planes = G["tabs"][rd_].data_ptr()
             if band[1] > band[0]:
-                dec.decode_batch(b, stream, rows=None if band == (0, H) else band)
+                with turn:
+                    dec.decode_batch(b, stream, rows=None if band == (0, H) else band)
             if comm is None:
                 continue
             ev = torch.cuda.Event()
@@ -363,6 +393,7 @@ def chain_run(args, rank: int, world: int, local: int, cs, rehearse: bool, nchai
     step_bytes = int((rd + wr) * frac_rows)
     achieved = step_bytes / (kern[3] * 1e-3) / 1e9 if kern[3] > 0 else 0.0
     xin = groups[0]["xch"].bytes_in() * ng if world > 1 else 0
+    xops = 0 if world == 1 else ng * xch_ops(groups[0]["xch"], bands, rank, halo, exchange)
     del groups, dec
     torch.cuda.empty_cache()
     # PMC traffic of this mode (tools/pmc.sh over a chain-mode run -> profiles/traffic_c<N>_chain.json)
@@ -409,7 +440,7 @@ def chain_run(args, rank: int, world: int, local: int, cs, rehearse: bool, nchai
         "exchange": {"mode": exchange if world > 1 else None, "halo_mb_rows": halo, "max_abs_mvy_qpel": mvy,
                      "impl": (getattr(args, "exchange_impl", "abi") if world > 1 else None),
                      "bytes_in_per_rank_per_step": xin,
-                     "ops_per_step": (0 if world == 1 else ng * xch_ops(groups[0]["xch"], bands, rank, halo, exchange))},
+                     "ops_per_step": xops},
         "cpu_baseline": cpu,
         "cpu_baseline_threads": cpu_mt,
         "verified_vs_oracle": verified,
@@ -541,6 +572,7 @@ def throughput_run(args, rank: int, world: int, local: int, cs, rehearse: bool, 
     stage = list(stage)
     ev_dec, ev_ex = [], []
     nstep = [0]
+    turn = GpuTurn(rehearse and world > 1)
 
     def step():
         t = nstep[0]
@@ -549,7 +581,8 @@ def throughput_run(args, rank: int, world: int, local: int, cs, rehearse: bool, 
             cs.wait_event(ev_ex[t - 2])                # E[t % 3] and stage[t % 2] are free again
         db.batch.ref_planes = tabs[t % len(tabs)].data_ptr()
         if band[1] > band[0]:
-            dec.decode_batch(db.batch, stream, rows=None if band == (0, H) else band)
+            with turn:
+                dec.decode_batch(db.batch, stream, rows=None if band == (0, H) else band)
         if shard != "slices":
             return
         # exchange: this rank's band of picture 0 staged (one small D2D copy, so the next
@@ -636,7 +669,7 @@ def throughput_run(args, rank: int, world: int, local: int, cs, rehearse: bool, 
     dbk_k = (["k_deblock2y", "k_deblock2c"] if prow < int(os.environ.get("H264R_DB2S_MAX", "512")) * 68
              else ["k_deblock2"] if prow >= int(os.environ.get("H264R_DEBLOCK2_MIN", "8")) * 68 else ["k_deblock"])
     dbk = " + ".join(dbk_k)
-    inter_k = ["k_dbinfo", "k_inter4r"]
+    inter_k = ["k_inter4r"]
     names = [" + ".join(inter_k), "intra (k_level + k_intra_levels + k_intra_pic)", dbk]
     kern_names = [inter_k + ["k_inter_sp"], ["k_level", "k_level_scatter", "k_intra_levels", "k_intra_pic"],
                   dbk_k]

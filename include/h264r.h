@@ -296,7 +296,7 @@ int  h264r_ref_planes(h264r_ctx* ctx, int slot, uint8_t** y, uint8_t** u, uint8_
 /* ---- instrumentation ------------------------------------------------------------- */
 /* Average device time (ms) per h264r_decode_batch of the launches made since timing was
  * enabled, measured with HIP events on each launch's stream: out[0] the deblocking records
- * and the inter / I_PCM reconstruction (k_dbinfo + k_inter4r + k_inter_sp), out[1] the intra
+ * and the inter / I_PCM reconstruction (k_inter4r + k_inter_sp), out[1] the intra
  * kernels (k_level + k_level_scatter + k_intra_levels + k_intra_pic), out[2]
  * deblocking (k_deblock2, or the split walk k_deblock2y + k_deblock2c), out[3] the whole batch (the wall time of the launch
  * sequence on the launch stream; under the overlapped schedule out[0..2] are busy times that

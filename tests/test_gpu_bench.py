@@ -45,7 +45,8 @@ def test_gpu_bench_chain_two_ranks_rehearsal():
     assert d["n_gpus"] == 2 and d["config"]["bands"] == [[0, 34], [34, 68]]
     assert d["config"]["chain_groups"] == 2          # the exchange of one group beside the next one's decode
     assert d["exchange"]["mode"] == "halo" and d["exchange"]["halo_mb_rows"] >= 1
-    assert d["exchange"]["ops_per_step"] == 2        # one peer, two groups
+    # the library's exchange (include/h264r_group.h): one send and one receive per peer and group
+    assert d["exchange"]["impl"] == "abi" and d["exchange"]["ops_per_step"] == 4
 
 
 def test_gpu_bench_gpus2_spawns_its_ranks():
@@ -60,7 +61,7 @@ def test_gpu_bench_gpus2_spawns_its_ranks():
     assert d["distributed"]["ranks"] == 2 and d["distributed"]["backend"] == "gloo"
     s = d["slice_sharded"]
     assert s["config"]["survey_config"] == 5 and s["config"]["mode"] == "chain" and s["config"]["chains"] == 4
-    assert s["config"]["parallelism"] == "slices2" and s["exchange"]["ops_per_step"] == 1
+    assert s["config"]["parallelism"] == "slices2" and s["exchange"]["ops_per_step"] == 2   # a send and a receive
     assert s["verified_vs_oracle"] is True and "slice-sharded" in s["metric"]
     assert s["same_mode_n1"]["verified_vs_oracle"] is True and s["same_mode_n1"]["chains"] == 2
     assert s["same_mode_n1"]["cpu_baseline"]["kind"] == "port" and s["scaling_vs_same_mode_n1"] > 0

@@ -1,15 +1,18 @@
 """The DPP instruction forms of the built kernels (tools/isa_dpp.py) are the ones the GPU parity
-suite verified.
+suite verified, and none is a form MI355X executes differently from the compiler's model.
 
-DPP moves that exchange values between lanes can be folded by the compiler into the VOP2
-instruction that consumes them.  On MI355X one such fold was wrong in round 5: the lane ^ 1
-low / high moves (quad_perm [0,0,2,2] / [1,1,3,3]) combined into v_add_u32_dpp /
-v_subrev_u32_dpp gave wrong residuals while the same moves kept as v_mov_b32_dpp were exact
-(tools/dpp/dpp_fold_test.hip runs each encoded form on the GPU).  This test
-runs on the CPU against the library built in the tree: a new compiler or a source change that
-emits any DPP form outside the verified set fails here, before a GPU run, instead of silently
-changing results.  Re-verify a new form on MI355X (pytest -m gpu + the fold micro-test), then add
-it below.
+DPP moves that exchange values between lanes can be folded by the compiler (GCNDPPCombine) into
+the VOP2 instruction that consumes them; the DPP lane select then applies to that instruction's
+src0.  On MI355X a REVERSED VOP2 opcode with DPP -- v_subrev_u32_dpp, v_lshlrev_b32_dpp -- applies
+the lane select to src1 instead: tools/dpp/dpp_fold_test.hip runs each encoded form on the GPU
+(encodings checked field by field: the DPP word's src0 is the intended register), and every
+*rev* case returns exactly "the same operation with the lane select on src1"
+(profiles/r06_e_dpp_fold_test.txt); v_add / v_sub / v_and / v_or / v_mov with DPP are exact.
+That is round 5's miscompile: the lane ^ 1 low / high moves (quad_perm [0,0,2,2] / [1,1,3,3])
+folded into v_subrev_u32_dpp gave wrong residuals.  This test runs on the
+CPU against the library built in the tree: a reversed opcode with DPP fails it outright, and any
+other form outside the verified set fails until it is re-verified on MI355X (pytest -m gpu + the
+fold micro-test) and added below.
 """
 import os
 import sys
@@ -73,3 +76,9 @@ def test_lane_lo4_hi4_stay_moves(forms):
     banked = [(k, op) for (k, op, m) in forms if "bank_mask:0x5" in m or "bank_mask:0xa" in m]
     assert banked
     assert all(op == "v_mov_b32_dpp" for _, op in banked), banked
+
+
+def test_no_dpp_on_a_reversed_opcode(forms):
+    """v_*rev*_dpp (subrev, lshlrev, lshrrev, ashrrev, ...): MI355X applies the lane select to src1."""
+    bad = sorted({(k, op, m) for (k, op, m) in forms if "rev_" in op})
+    assert not bad, bad

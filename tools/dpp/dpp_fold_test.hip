@@ -6,7 +6,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 
-#define NCASE 8
+#define NCASE 13
 __global__ void k(const int* in, int* out)
 {
     const int l = threadIdx.x;
@@ -60,6 +60,28 @@ __global__ void k(const int* in, int* out)
     // 7: quad_bcast folded (k_intra_levels' v_add_u32_dpp quad_perm [0,0,0,0])
     asm volatile("s_nop 4\n\tv_add_u32_dpp %0, %1, %2 quad_perm:[0,0,0,0] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\ts_nop 4"
                  : "=v"(r[7]) : "v"(v), "v"(w));
+    // 8: v_subrev_u32_dpp, DPP source != destination
+    asm volatile("s_nop 4\n\tv_subrev_u32_dpp %0, %1, %2 quad_perm:[1,1,3,3] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\ts_nop 4"
+                 : "=v"(r[8]) : "v"(v), "v"(w));
+    // 9: v_sub_u32_dpp (not reversed), DPP source != destination
+    asm volatile("s_nop 4\n\tv_sub_u32_dpp %0, %1, %2 quad_perm:[1,1,3,3] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\ts_nop 4"
+                 : "=v"(r[9]) : "v"(v), "v"(w));
+    // 10: v_subrev_u32_dpp with the lane ^ 1 exchange
+    asm volatile("s_nop 4\n\tv_subrev_u32_dpp %0, %1, %2 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\ts_nop 4"
+                 : "=v"(r[10]) : "v"(v), "v"(w));
+    // 11: another reversed opcode, v_lshlrev_b32_dpp (shift amount = DPP source & 7)
+    {
+        const int sh = v & 7;
+        asm volatile("s_nop 4\n\tv_lshlrev_b32_dpp %0, %1, %2 quad_perm:[1,1,3,3] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\ts_nop 4"
+                     : "=v"(r[11]) : "v"(sh), "v"(w));
+    }
+    // 12: v_sub_u32_dpp in place
+    {
+        int x = v;
+        asm volatile("s_nop 4\n\tv_sub_u32_dpp %0, %0, %1 quad_perm:[1,1,3,3] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\ts_nop 4"
+                     : "+v"(x) : "v"(w));
+        r[12] = x;
+    }
     for (int c = 0; c < NCASE; ++c) out[64 * c + l] = r[c];
 }
 
@@ -74,7 +96,9 @@ int main()
     (void)hipMemcpy(o, dout, sizeof o, hipMemcpyDeviceToHost);
     const char* names[NCASE] = {"add [1,1,3,3] dst!=src", "subrev [1,1,3,3] in place", "add [0,0,2,2] in place",
                                 "and [1,0,3,2] in place", "mov [1,1,3,3] in place", "add [1,1,3,3] no wait states",
-                                "add row_shr:4 banks 1,3 (old = own)", "add [0,0,0,0] dst!=src"};
+                                "add row_shr:4 banks 1,3 (old = own)", "add [0,0,0,0] dst!=src",
+                                "subrev [1,1,3,3] dst!=src", "sub [1,1,3,3] dst!=src", "subrev [1,0,3,2] dst!=src",
+                                "lshlrev [1,1,3,3] dst!=src", "sub [1,1,3,3] in place"};
     int bad_total = 0;
     for (int c = 0; c < NCASE; ++c) {
         int bad = 0, first = -1;
@@ -92,11 +116,32 @@ int main()
             case 5: e = hi + w; break;
             case 6: e = (bank & 1) ? h[l - 4] + w : v; break;     // banks 0, 2 keep the old (own) value
             case 7: e = b0 + w; break;
+            case 8: e = w - hi; break;
+            case 9: e = hi - w; break;
+            case 10: e = w - x1; break;
+            case 11: e = (int)((unsigned)w << (hi & 7)); break;
+            case 12: e = hi - w; break;
             }
             if (o[64 * c + l] != e) { ++bad; if (first < 0) first = l; }
         }
         printf("%-40s %s", names[c], bad ? "WRONG" : "exact");
-        if (bad) printf(" (%d lanes, first lane %d: got %d want ...)", bad, first, o[64 * c + first]);
+        if (bad) {
+            // what the lane got, against the same operation with the lane select applied to the
+            // OTHER operand (src1 read from the permuted lane, src0 from the own lane)
+            const int l = first, v = h[l], w = h[64 + l];
+            const int pl = (c == 10) ? (l ^ 1) : (l | 1);
+            const int wp = h[64 + pl];
+            int swapped = 0;
+            switch (c) {
+            case 1: case 8: case 10: swapped = wp - v; break;
+            case 5: swapped = v + wp; break;
+            case 9: case 12: swapped = v - wp; break;
+            case 11: swapped = (int)((unsigned)wp << (v & 7)); break;
+            default: swapped = 0x7fffffff; break;
+            }
+            printf(" (%d lanes, first lane %d: got %d%s)", bad, first, o[64 * c + first],
+                   o[64 * c + first] == swapped ? " = the lane select applied to src1" : "");
+        }
         printf("\n");
         bad_total += bad;
     }

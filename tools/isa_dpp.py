@@ -3,13 +3,13 @@
 
 The kernels exchange values between lanes with DPP moves (device_common.h lane_xor1 /
 lane_xor4 / lane_lo4 / lane_hi4 / quad_bcast), and the compiler may fold a DPP move into the
-VOP2 instruction that consumes it (GCNDPPCombine: v_add_u32_dpp, v_and_b32_dpp, ...).  Round 5
-found one such fold wrong on MI355X: the lane ^ 1 low / high moves (quad_perm [0,0,2,2] /
-[1,1,3,3]) gave wrong residuals once combined into their consumers, and were exact as separate
-moves.  The parity suite verifies the forms the product has today; this
-tool lists every (mnemonic, DPP modifiers) pair in the built library so that tests/test_isa.py can
-hold it to that verified set -- a toolchain or source change that produces a new form fails at
-build time instead of waiting for a GPU parity run.
+VOP2 instruction that consumes it (GCNDPPCombine: v_add_u32_dpp, v_and_b32_dpp, ...).  On MI355X
+a reversed VOP2 opcode with DPP (v_subrev_u32_dpp, v_lshlrev_b32_dpp) applies the lane select to
+src1 instead of src0 (tools/dpp/dpp_fold_test.hip); round 5's wrong residuals were the lane ^ 1
+low / high moves folded into v_subrev_u32_dpp.  This tool lists every (mnemonic, DPP modifiers)
+pair in the built library so that tests/test_isa.py can refuse reversed opcodes and hold the rest
+to the verified set -- a toolchain or source change that produces a new form fails at build time
+instead of waiting for a GPU parity run.
 
     python tools/isa_dpp.py [path/to/libh264r.so]
 """

@@ -20,10 +20,10 @@ def analyze(path):
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     k = [(r["Kernel_Name"].split("(")[0], int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in rows]
-    # pictures: a new picture starts at each k_dbinfo
+    # pictures: a new picture starts at each k_inter4r
     pics, cur = [], []
     for e in k:
-        if e[0].startswith("k_dbinfo") and cur:
+        if e[0].startswith("k_inter4r") and cur:
             pics.append(cur)
             cur = []
         cur.append(e)
