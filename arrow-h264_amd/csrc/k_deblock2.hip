@@ -86,6 +86,11 @@ constexpr int PL = H264R_DB2_PL;
 constexpr bool DOY = PL != 1, DOC = PL != 0;
 static_assert(PL == 2 || LPU == 8, "the split walk is built at 8 lanes per unit");
 constexpr int PICS = UNITS / BAND;     // pictures per wave
+#ifndef H264R_DB2_SG
+#define H264R_DB2_SG 4                 // MBs per output-staging group (StageLds): 4 or 2
+#endif
+constexpr int SG = H264R_DB2_SG;
+static_assert(SG == 4 || SG == 2, "H264R_DB2_SG");
 static_assert(UNITS % BAND == 0, "a band divides the wave's units");
 constexpr int RECG = 24;               // granules per MB record: [consumer lane c 0..3][i 0..5]
 constexpr int AUX_SC1 = 16;            // buffer-op cache policy: sc1 (write-through store, L2-served load)
@@ -112,15 +117,17 @@ static_assert(sizeof(UnitLds) == (PL == 2 ? 848 : PL == 0 ? 592 : 336), "UnitLds
 // final only after the row below has filtered its top edges: the unit below writes them into
 // this unit's staging (same wave), or, for the band's first row, into the UpLds of its picture
 // (the row above is another wave's).  1.5 KiB per unit: 8 waves per CU at 8 lanes per unit.
+// (SG = 2: 2-MB groups, 32-byte luma / 16-byte chroma row pieces, 784 B per unit with a unit
+// stride 4 banks apart -- 13.0 KiB per wave, 12 waves per CU)
 struct alignas(16) StageLds {
-    uint32_t y[YR][4][4];      // luma rows 0..15, MB m & 3 of the 4-MB group: 16 bytes
-    uint32_t c[2][CR][4][2];   // chroma plane, rows 0..7, MB m & 3: 8 bytes
-    uint32_t pad[20];          // unit stride 404 dwords (20 banks apart)
+    uint32_t y[YR][SG][4];     // luma rows 0..15, MB m % SG of the group: 16 bytes
+    uint32_t c[2][CR][SG][2];  // chroma plane, rows 0..7, MB m % SG: 8 bytes
+    uint32_t pad[SG == 4 ? 20 : 4];   // unit stride 404 (SG 4) / 196 (SG 2) dwords: 20 / 4 banks apart
 };
-static_assert(sizeof(StageLds) == (PL == 2 ? 1616 : PL == 0 ? 1104 : 592), "StageLds layout");
+static_assert(SG != 4 || sizeof(StageLds) == (PL == 2 ? 1616 : PL == 0 ? 1104 : 592), "StageLds layout");
 struct alignas(16) UpLds {     // the band's first row: rows 13..15 (chroma 7) of the row above
-    uint32_t yu[DOY ? 3 : 0][4][4];
-    uint32_t cu[2][DOC ? 4 : 0][2];
+    uint32_t yu[DOY ? 3 : 0][SG][4];
+    uint32_t cu[2][DOC ? SG : 0][2];
 };
 
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));   // native vectors: registers, not stack
@@ -194,7 +201,7 @@ extern "C" void h264r_db2_trace_copy(void* dst) { (void)hipMemcpyFromSymbol(dst,
 // picture: 20.2 KiB, 8 waves per CU at 8 lanes per unit); asking for 2 waves per SIMD keeps the
 // compiler from parking values in AGPRs (at a 512-register budget it did, and the wave's VGPR +
 // AGPR footprint of 257 left one wave per SIMD)
-#define H264R_DB2_WAVES_PER_EU (H264R_DB2_PL == 1 ? 4 : H264R_DB2_PL == 0 ? 3 : H264R_DB2_LPU == 8 ? 2 : 1)   // split builds: 3 / 4
+#define H264R_DB2_WAVES_PER_EU (H264R_DB2_PL == 1 ? 4 : H264R_DB2_PL == 0 ? 3 : H264R_DB2_LPU == 8 ? (H264R_DB2_SG == 2 ? 3 : 2) : 1)   // split builds: 3 / 4
 extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(H264R_DB2_WAVES_PER_EU, H264R_DB2_WAVES_PER_EU))) void H264R_DB2_KERNEL(
     h264r_batch b, const DbInfo* __restrict__ dbinfo, uint64_t* hb, int* sync, int* err, uint32_t epoch, int2 rows, int nx,
     const uint8_t* __restrict__ recon)
@@ -330,14 +337,14 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(H
 #pragma unroll
             for (int i = 0; i < NLR; ++i) {
                 const int r = LPU * i + q8;
-                *reinterpret_cast<v4u*>(&T.y[r][mc & 3][0]) = *reinterpret_cast<const v4u*>(&U.y[r][4 * s]);
+                *reinterpret_cast<v4u*>(&T.y[r][mc % SG][0]) = *reinterpret_cast<const v4u*>(&U.y[r][4 * s]);
             }
         }
         if constexpr (DOC) {
 #pragma unroll
             for (int i = 0; i < NLR; ++i) {
                 const int k = LPU * i + q8, pl = k >> 3, r = k & 7;
-                *reinterpret_cast<v2u*>(&T.c[pl][r][mc & 3][0]) = *reinterpret_cast<const v2u*>(&U.c[pl][r][2 * s]);
+                *reinterpret_cast<v2u*>(&T.c[pl][r][mc % SG][0]) = *reinterpret_cast<const v2u*>(&U.c[pl][r][2 * s]);
             }
         }
     };
@@ -349,18 +356,19 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(H
     auto store_groups = [&](int xs) {
         const int mo = xs - 1;                                   // final since V(xs), rows 13..15 now
         const bool own = active && mo >= 0 && mo < W;
-        const int r = lane >> 2, pp = lane & 3, cp = r >> 3, cr = r & 7;
-        for (uint64_t bm = __ballot(own && q8 == 0 && ((mo & 3) == 3 || mo == W - 1)); bm; bm &= bm - 1) {
+        // lane = (row r, MB pp of the group); with SG = 2 lanes 32..63 have no row (r >= 16)
+        const int r = lane / SG, pp = lane % SG, rr = min(r, 15), cp = rr >> 3, cr = rr & 7;
+        for (uint64_t bm = __ballot(own && q8 == 0 && (mo % SG == SG - 1 || mo == W - 1)); bm; bm &= bm - 1) {
             const int l0 = __builtin_ctzll(bm), u2 = l0 / LPU;
             const int m2 = __builtin_amdgcn_readlane(mo, l0), yl2 = __builtin_amdgcn_readlane(ylast, l0);
             const int cl2 = __builtin_amdgcn_readlane(clast, l0);
             const uint32_t yr2 = (uint32_t)__builtin_amdgcn_readlane((int)yrow, l0);
             const uint32_t cr2 = (uint32_t)__builtin_amdgcn_readlane((int)crow, l0);
-            const int g0 = m2 & ~3;
-            const bool inrow = g0 + pp <= m2;
+            const int g0 = m2 & ~(SG - 1);
+            const bool inrow = g0 + pp <= m2 && r < 16;
             if constexpr (DOY)
                 st16<OUT_AUX>(rY, r <= yl2 && inrow ? yr2 + (uint32_t)r * Wl + (uint32_t)(g0 + pp) * 16u : OOB,
-                              *reinterpret_cast<const v4u*>(&G[u2].y[r][pp][0]));
+                              *reinterpret_cast<const v4u*>(&G[u2].y[rr][pp][0]));
             if constexpr (DOC) {
                 const uint32_t off = cr <= cl2 && inrow ? cr2 + (uint32_t)cr * Wc + (uint32_t)(g0 + pp) * 8u : OOB;
                 const v2u cv = *reinterpret_cast<const v2u*>(&G[u2].c[cp][cr][pp][0]);
@@ -370,13 +378,13 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(H
         }
         // the band's first row: rows 13..15 (chroma 7) of the row above, final since H(xs)
         const bool up = active && rb == 0 && above && xs >= 0 && xs < W;
-        for (uint64_t bm = __ballot(up && q8 == 0 && ((xs & 3) == 3 || xs == W - 1)); bm; bm &= bm - 1) {
+        for (uint64_t bm = __ballot(up && q8 == 0 && (xs % SG == SG - 1 || xs == W - 1)); bm; bm &= bm - 1) {
             const int l0 = __builtin_ctzll(bm), pu2 = l0 / LPU;     // rb == 0: unit = picture
             const int x2 = __builtin_amdgcn_readlane(xs, l0);
             const uint32_t yr2 = (uint32_t)__builtin_amdgcn_readlane((int)yrow, l0);
             const uint32_t cr2 = (uint32_t)__builtin_amdgcn_readlane((int)crow, l0);
-            const int g0 = x2 & ~3;
-            const bool inrow = g0 + pp <= x2;
+            const int g0 = x2 & ~(SG - 1);
+            const bool inrow = g0 + pp <= x2 && r < 16;
             if constexpr (DOY)
                 st16<OUT_AUX>(rY, r < 3 && inrow ? yr2 - (uint32_t)(3 - r) * Wl + (uint32_t)(g0 + pp) * 16u : OOB,
                               *reinterpret_cast<const v4u*>(&UP[pu2].yu[min(r, 2)][pp][0]));
@@ -677,11 +685,11 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(H
         // (the band's first row) into this unit's own
         if (xok && above) {
             if constexpr (DOY) {
-                uint32_t* yd = rb ? &TA.y[13][x & 3][q] : &TU.yu[0][x & 3][q];
+                uint32_t* yd = rb ? &TA.y[13][x % SG][q] : &TU.yu[0][x % SG][q];
 #pragma unroll
-                for (int r = 1; r < 4; ++r) yd[(r - 1) * 16] = wy[r];
+                for (int r = 1; r < 4; ++r) yd[(r - 1) * 4 * SG] = wy[r];
             }
-            if constexpr (DOC) *(rb ? &TA.c[p][7][x & 3][d] : &TU.cu[p][x & 3][d]) = wcv[1];
+            if constexpr (DOC) *(rb ? &TA.c[p][7][x % SG][d] : &TU.cu[p][x % SG][d]) = wcv[1];
         }
         // 8. what the next step fills: MB x+2 and its DbInfo
         fetch(x + 2);

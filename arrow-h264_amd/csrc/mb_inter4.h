@@ -27,6 +27,14 @@
 #pragma once
 #include "mb_deblock.h"
 
+// H264R_INTER_DIAG: diagnostic builds only (wrong output; make EXTRA=-DH264R_INTER_DIAG=<bits>) that
+// take one part of k_inter4r away to time the rest: 1 one 16-byte store per lane, 2 no luma
+// filter (window loads kept), 4 neither, 8 no chroma MC, 16 no residual (nor its loads), 32 no
+// deblocking records
+#ifndef H264R_INTER_DIAG
+#define H264R_INTER_DIAG 0
+#endif
+
 namespace h264r {
 
 constexpr int INTER4_MBS = 16;   // MBs per 256-thread workgroup (4 waves x 4)
@@ -687,14 +695,31 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
             {
                 // the 9 window rows of the lane's own block, straight from the plane
                 uint32_t w[9][3];
+#if H264R_INTER_DIAG & 4
+                // diagnostic build (wrong output): no window loads, no luma filter
+                (void)x; (void)y;
+                tY[0] = tY[1] = tY[2] = tY[3] = (uint32_t)(vx ^ vy);
+#elif H264R_INTER_DIAG & 2
+                // diagnostic build (wrong output): the window loads without the luma filter
+                if (ok) luma_window_global(S.planes[slot * 3] + bot * g.W, g.W, g.W << fld, g.H, x, y, w);
+                if (ok) { uint32_t acc = 0;
+    #pragma unroll
+                    for (int r = 0; r < 9; ++r) acc ^= w[r][0] ^ w[r][1] ^ w[r][2];
+                    tY[0] = tY[1] = tY[2] = tY[3] = acc; }
+#else
                 if (ok) luma_window_global(S.planes[slot * 3] + bot * g.W, g.W, g.W << fld, g.H, x, y, w);
                 if (ok) luma_block_pred(w, g.W, x, vx & 3, vy & 3, tY);
+#endif
             }
             // a reference field of the other parity: the chroma sample grid sits a quarter
             // chroma row off (get_block_chroma inter_prediction.cc:352-355)
             const int vyc = vy + (fld && bot != (structure == H264R_BOTTOM_FIELD) ? (bot ? -2 : 2) : 0);
+#if H264R_INTER_DIAG & 8
+            tC[0] = tC[1] = (uint32_t)vyc;        // diagnostic build (wrong output): no chroma MC
+#else
             if (ok) chroma_block_pred2(S.planes[slot * 3 + 1] + bot * g.Wc, S.planes[slot * 3 + 2] + bot * g.Wc, g.Wc,
                                        g.Wc << fld, g.Hc, vx >> 3, vyc >> 3, vx & 7, vyc & 7, tC);
+#endif
             const bool l1 = l != 0;
     #pragma unroll
             for (int i = 0; i < 4; ++i) {
@@ -718,7 +743,9 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
         for (int i = 0; i < 4; ++i) predY[i] = wp_combine4(wpp[0], wp_mode, dir, pY[0][i], pY[1][i]);
     #pragma unroll
         for (int pl = 0; pl < 2; ++pl) predC[pl] = wp_combine4(wpp[1 + pl], wp_mode, dir, pC[0][pl], pC[1][pl]);
+#if !(H264R_INTER_DIAG & 16)
         load_residual();
+#endif
 
         if constexpr (SP) {
             // ---- itrans_sp of this lane's 4x4 block (:1132-1187): the prediction is
@@ -880,7 +907,7 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
     #pragma unroll
             for (int c = 0; c < 4; ++c) res[i][c] = 0;
         const bool byp = (q.flags & H264R_MBF_BYPASS) != 0;
-        if (__any(cbpl != 0)) {
+        if (!(H264R_INTER_DIAG & 16) && __any(cbpl != 0)) {
             const int per = qpl / 6;
             // dq4 / dq8 (transform.cc:394-419) as one form, rounding and shift per lane: the
             // lanes of a wave mix 4x4 and 8x8 MBs, and a select per value (not a branch) keeps
@@ -1019,7 +1046,7 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
     #pragma unroll
         for (int pl = 0; pl < 2; ++pl) {
             int rc[2][2] = {{0, 0}, {0, 0}};
-            if (__any(cbpc != 0)) {
+            if (!(H264R_INTER_DIAG & 16) && __any(cbpc != 0)) {
                 const int qpc = q.qp_scaled[1 + pl], per = qpc / 6;
                 int k[2][2], raw[2][2];
     #pragma unroll

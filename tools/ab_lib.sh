@@ -1,12 +1,13 @@
 #!/bin/bash
 # tools/ab_lib.sh <outdir> <config> <lib>... -- bench.py A/B over compile-time variants of
 # libh264r.so (H264R_LIB), one JSON line per library, on one MI355X (GPU box); each run
-# verifies its pictures against the oracle before timing.
+# verifies its pictures against the oracle before timing (AB_ARGS adds bench arguments, e.g.
+# --no-verify for the diagnostic builds whose output is wrong by design).
 OUT=$1; CFG=$2; shift 2
 mkdir -p "$OUT"
 i=0
 for L in "$@"; do
-  H264R_LIB=$L timeout -k 10 240 python bench.py --config $CFG --steps 10 --warmup 2 --no-cpu --latency-pictures 0 \
+  H264R_LIB=$L timeout -k 10 240 python bench.py --config $CFG --steps 10 --warmup 2 --no-cpu --latency-pictures 0 $AB_ARGS \
       > "$OUT/v$i.json" 2> "$OUT/v$i.err" || exit 1
   python -c "import json; d=json.loads(open('$OUT/v$i.json').read().strip().splitlines()[-1]); print('$L', 'config $CFG', 'Mmb/s %.1f' % (d['value']/1e6), 'ms %.2f' % d['ms_per_step'], 'kernels', d['kernel_ms'], 'verified', d['verified_vs_oracle'])"
   i=$((i+1))
