@@ -29,20 +29,11 @@ DEV LdsRegs inter4_lds_load(const h264r_batch& b, int pic)
     const int nsl = min(b.slice_stride, INTER4_LDS_SLICES);
     const h264r_slice* sl = b.slices + (size_t)pic * b.slice_stride;
     LdsRegs r;
-#if H264R_LDS_MASKED
-    // only the threads whose entry is stored load it (the waves past the tables issue nothing)
-    r.plane = nullptr;
-    r.refs = r.hdr = make_uint2(0, 0);
-    if (t < 3 * H264R_MAX_SLOTS) r.plane = b.ref_planes[(size_t)pic * b.ref_planes_stride + t];
-    if (t < nsl * 4) r.refs = *reinterpret_cast<const uint2*>(&sl[t >> 2].ref_slot[0][0] + 8 * (t & 3));
-    if (t < nsl) r.hdr = *reinterpret_cast<const uint2*>(&sl[t]);
-#else
     // the batch's one DPB table, or picture pic's own (ref_planes_stride, include/h264r.h)
     r.plane = b.ref_planes[(size_t)pic * b.ref_planes_stride + min(t, 3 * H264R_MAX_SLOTS - 1)];
     const int ri = min(t, nsl * 4 - 1);                      // ref tables: 32 bytes per slice, 8 per thread
     r.refs = *reinterpret_cast<const uint2*>(&sl[ri >> 2].ref_slot[0][0] + 8 * (ri & 3));
     r.hdr = *reinterpret_cast<const uint2*>(&sl[min(t, nsl - 1)]);
-#endif
     return r;
 }
 DEV void inter4_lds_store(const h264r_batch& b, const LdsRegs& r, Inter4Lds& S)

@@ -92,11 +92,7 @@ struct DbTables {
 };
 // thread t < 52 copies entry t (the workgroup has >= 52 threads): load, then store, so a
 // caller can issue its own loads between the two
-#if H264R_LDS_MASKED
-DEV uint2 db_tables_load(int t) { uint2 v = make_uint2(0, 0); if (t < 52) v = make_uint2(DB_AB[t], DB_TC0[t]); return v; }
-#else
 DEV uint2 db_tables_load(int t) { const int i = min(t, 51); return make_uint2(DB_AB[i], DB_TC0[i]); }
-#endif
 DEV void db_tables_store(DbTables& T, int t, uint2 v)
 {
     if (t < 52) { T.ab[t] = v.x; T.tc0[t] = v.y; }
