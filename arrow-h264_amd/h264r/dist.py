@@ -86,6 +86,18 @@ def allgather_into_slot(send, dst, bands: Sequence[tuple[int, int]], rank: int, 
         dst[a0:a1] = recv[k * wide: k * wide + (a1 - a0)]
 
 
+def rccl_group_ok() -> bool:
+    """Whether this process can make the library's RCCL group (librccl loads, ncclGetUniqueId
+    works).  Checked on every rank, and agreed, before the collective group creation, so that a
+    rank without RCCL cannot leave the others waiting in ncclCommInitRank."""
+    try:
+        from .group import unique_id
+        unique_id()
+        return True
+    except Exception:                           # noqa: BLE001 -- any failure means "no"
+        return False
+
+
 def max_over_ranks(seconds: float, device=None) -> float:
     """The job's time: the slowest rank's (bench.py contract)."""
     import torch

@@ -59,6 +59,13 @@ def plan(bands, rank: int, mode: str = "halo", halo: int = 0):
     return pick(need), pick(give)
 
 
+def unique_id() -> np.ndarray:
+    """h264r_group_unique_id: a fresh RCCL unique id (raises when librccl cannot be loaded)."""
+    uid = np.zeros(ID_BYTES, np.uint8)
+    _check("h264r_group_unique_id", lib().h264r_group_unique_id(uid.ctypes.data))
+    return uid
+
+
 class _TorchTransport:
     """The callback transport over torch.distributed (host buffers; gloo)."""
 
@@ -120,9 +127,7 @@ class Group:
         if transport == "rccl":
             import torch
             import torch.distributed as dist
-            uid = np.zeros(ID_BYTES, np.uint8)
-            if rank == 0:
-                _check("h264r_group_unique_id", L.h264r_group_unique_id(uid.ctypes.data))
+            uid = unique_id() if rank == 0 else np.zeros(ID_BYTES, np.uint8)
             if nranks > 1:
                 t = torch.from_numpy(uid).to(f"cuda:{device}")
                 dist.broadcast(t, 0, group=pg)

@@ -276,6 +276,13 @@ def chain_run(args, rank: int, world: int, local: int, cs, rehearse: bool, nchai
     halo = D.halo_mb_rows(mvy)
     slack = 64
     psz = (256 * nmb, 64 * nmb, 64 * nmb)
+    # the exchange: the library's (include/h264r_group.h) unless --exchange-impl torch; over RCCL
+    # every rank first checks that it can load librccl, and the ranks agree, before the
+    # collective group creation (a rank without it would leave the others waiting)
+    impl, impl_note = getattr(args, "exchange_impl", "abi"), None
+    if world > 1 and impl == "abi" and not rehearse:
+        if D.min_over_ranks(1.0 if D.rccl_group_ok() else 0.0, device="cuda") < 1.0:
+            impl, impl_note = "torch", "librccl not loadable on every rank: torch.distributed exchange"
     dec = h264r.Decoder(local, W, H)
     static = [[torch.from_numpy(np.concatenate([a.reshape(-1), np.zeros(slack, np.uint8)])).to("cuda") for a in r]
               for r in refs[1:]]
@@ -302,8 +309,7 @@ def chain_run(args, rank: int, world: int, local: int, cs, rehearse: bool, nchai
         db.batch.ref_planes_stride = 3 * 32
         for t_ in ("out_y", "out_u", "out_v"):          # the sets replace the batch's own outputs
             del db.tensors[t_]
-        xch = D.BandExchange(bands, rank, W, H, nk, exchange, halo, f"cuda:{local}",
-                             impl=getattr(args, "exchange_impl", "abi")) if world > 1 else None
+        xch = D.BandExchange(bands, rank, W, H, nk, exchange, halo, f"cuda:{local}", impl=impl) if world > 1 else None
         groups.append(dict(pics=pics, sets=sets, tabs=tabs, db=db, xch=xch, ev_ex=[]))
     comm = torch.cuda.Stream(device=local) if world > 1 else None
     stream = cs.cuda_stream
@@ -438,7 +444,7 @@ def chain_run(args, rank: int, world: int, local: int, cs, rehearse: bool, nchai
         "kernel_ms": {"inter": float(kern[0]), "intra": float(kern[1]), "deblock": float(kern[2]),
                       "batch_wall": float(kern[3])},
         "exchange": {"mode": exchange if world > 1 else None, "halo_mb_rows": halo, "max_abs_mvy_qpel": mvy,
-                     "impl": (getattr(args, "exchange_impl", "abi") if world > 1 else None),
+                     "impl": (impl if world > 1 else None), "impl_note": impl_note,
                      "bytes_in_per_rank_per_step": xin,
                      "ops_per_step": xops},
         "cpu_baseline": cpu,
