@@ -30,7 +30,7 @@
 // H264R_INTER_DIAG: diagnostic builds only (wrong output; make EXTRA=-DH264R_INTER_DIAG=<bits>) that
 // take one part of k_inter4r away to time the rest: 1 one 16-byte store per lane, 2 no luma
 // filter (window loads kept), 4 neither, 8 no chroma MC, 16 no residual (nor its loads), 32 no
-// deblocking records
+// deblocking records, 64 no luma residual transform (its loads kept), 128 the same for chroma
 #ifndef H264R_INTER_DIAG
 #define H264R_INTER_DIAG 0
 #endif
@@ -907,7 +907,12 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
     #pragma unroll
             for (int c = 0; c < 4; ++c) res[i][c] = 0;
         const bool byp = (q.flags & H264R_MBF_BYPASS) != 0;
-        if (!(H264R_INTER_DIAG & 16) && __any(cbpl != 0)) {
+#if H264R_INTER_DIAG & 64
+        // diagnostic build (wrong output): the luma levels loaded, not transformed
+        res[0][0] = (int)(lev[0].x ^ lev[0].y ^ lev[0].z ^ lev[0].w ^ lev[1].x ^ lev[1].y ^ lev[1].z ^ lev[1].w ^
+                          lsc[0].x ^ lsc[1].y) & 3;
+#endif
+        if (!(H264R_INTER_DIAG & (16 | 64)) && __any(cbpl != 0)) {
             const int per = qpl / 6;
             // dq4 / dq8 (transform.cc:394-419) as one form, rounding and shift per lane: the
             // lanes of a wave mix 4x4 and 8x8 MBs, and a select per value (not a branch) keeps
@@ -1046,7 +1051,11 @@ DEV void inter4_mbs(const h264r_batch& b, const Geom& g, int pic, int a0, int ae
     #pragma unroll
         for (int pl = 0; pl < 2; ++pl) {
             int rc[2][2] = {{0, 0}, {0, 0}};
-            if (!(H264R_INTER_DIAG & 16) && __any(cbpc != 0)) {
+#if H264R_INTER_DIAG & 128
+            // diagnostic build (wrong output): the chroma levels loaded, not transformed
+            rc[0][0] = (int)(clev[pl][0] ^ clev[pl][1] ^ csc[pl][0] ^ csc[pl][1] ^ cdc[pl].x ^ cdc[pl].y ^ (uint32_t)cdcs[pl]) & 3;
+#endif
+            if (!(H264R_INTER_DIAG & (16 | 128)) && __any(cbpc != 0)) {
                 const int qpc = q.qp_scaled[1 + pl], per = qpc / 6;
                 int k[2][2], raw[2][2];
     #pragma unroll
