@@ -79,7 +79,8 @@ int h264r_group_set_bands(h264r_group* g, int width_mbs, int height_mbs, const i
  * of the other bands the plan names, in place.  RCCL: enqueued on `stream` (a hipStream_t,
  * NULL = the legacy stream) and asynchronous, like h264r_decode_batch -- a decode of the next
  * pictures on the same stream reads the received rows.  Callback transport: returns when the
- * rows are in place. */
+ * rows are in place.  A group's staging buffers are reused by every exchange: drive a group from
+ * one stream (or order the streams), as a context. */
 int h264r_group_exchange(h264r_group* g, int num_pics, uint8_t* y, uint8_t* u, uint8_t* v,
                          int64_t stride_y, int64_t stride_c, void* stream);
 
