@@ -32,6 +32,8 @@ namespace h264r { struct DbInfo; }
 extern "C" __global__ void k_inter4r(h264r_batch b, h264r::DbInfo* dbinfo, int2 rows, int* sp_flag, uint8_t* recon, int tag,
                                      int* zero, int nz, int* zero2, int nz2);
 extern "C" __global__ void k_inter_sp(h264r_batch b, int2 rows, const int* sp_flag, uint8_t* recon, int tag);
+extern "C" __global__ void k_derive444(h264r_batch b, int pl, h264r_mb* mbs, h264r_slice* slices, h264r_quant* quant,
+                                       const uint8_t** refs, int ntab, int* err);
 extern "C" __global__ void k_untile(h264r_batch b, int2 rows, const uint8_t* recon);
 extern "C" __global__ void k_intra_pic(h264r_batch b, int* sync, int* err, const uint16_t* lvl, int lmax, int2 rows,
                                       int gstep, uint8_t* recon, const int* pband);
@@ -129,6 +131,14 @@ struct Scratch {
 struct h264r_ctx {
     int device = 0;
     int max_w = 0, max_h = 0;
+    int fmt = 1;                          // chroma_format_idc: 1 (4:2:0) or 3 (4:4:4, run_444)
+    // 4:4:4: one colour plane's derived batch (k_derive444) -- records, slices, quant, DPB tables --
+    // and the scratch its unused 4:2:0 chroma outputs go to
+    h264r_mb* d444_mbs = nullptr; size_t c444_mbs = 0;
+    h264r_slice* d444_slices = nullptr; size_t c444_slices = 0;
+    h264r_quant* d444_quant = nullptr; size_t c444_quant = 0;
+    const uint8_t** d444_refs = nullptr; size_t c444_refs = 0;
+    uint8_t* d444_chroma = nullptr; size_t c444_chroma = 0;
     hipStream_t stream = nullptr;
     // DPB slots
     uint8_t* slot[H264R_MAX_SLOTS][3] = {};
@@ -340,7 +350,7 @@ int h264r_create(h264r_ctx** out, int device, int max_w, int max_h, int chroma_f
     if (!out || max_w <= 0 || max_h <= 0 || max_w > 1024 || max_h > 1024) return H264R_EINVAL;
     *out = nullptr;
     if (!knobs().ok) return H264R_EINVAL;            // an environment knob out of range (stderr)
-    if (chroma_format_idc != 1 || bit_depth != 8) return H264R_EUNSUPPORTED;
+    if ((chroma_format_idc != 1 && chroma_format_idc != 3) || bit_depth != 8) return H264R_EUNSUPPORTED;
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0 || device < 0 || device >= n) return H264R_ENODEVICE;
     hipDeviceProp_t p;
@@ -348,7 +358,7 @@ int h264r_create(h264r_ctx** out, int device, int max_w, int max_h, int chroma_f
         return H264R_ENODEVICE;
     h264r_ctx* c = new (std::nothrow) h264r_ctx();
     if (!c) return H264R_ENOMEM;
-    c->device = device; c->max_w = max_w; c->max_h = max_h;
+    c->device = device; c->max_w = max_w; c->max_h = max_h; c->fmt = chroma_format_idc;
     // the context's own stream is a BLOCKING stream: work on the legacy NULL stream (torch's
     // default stream) and this stream are ordered with each other
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamDefault) != hipSuccess ||
@@ -374,7 +384,8 @@ int h264r_destroy(h264r_ctx* c)
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (int s = 0; s < H264R_MAX_SLOTS; ++s) if (c->slot[s][0]) (void)hipFree(c->slot[s][0]);
-    void* bufs[] = {c->d_ref_planes, c->d_err, c->d_mbs, c->d_levels, c->d_mv, c->d_ref, c->d_slices, c->d_pic, c->d_quant, c->d_out};
+    void* bufs[] = {c->d_ref_planes, c->d_err, c->d_mbs, c->d_levels, c->d_mv, c->d_ref, c->d_slices, c->d_pic, c->d_quant, c->d_out,
+                    c->d444_mbs, c->d444_slices, c->d444_quant, c->d444_refs, c->d444_chroma};
     for (void* b : bufs) if (b) (void)hipFree(b);
     for (auto& p : c->sp) {
         if (p.out) (void)hipHostFree(p.out);
@@ -393,6 +404,9 @@ int h264r_destroy(h264r_ctx* c)
     return H264R_OK;
 }
 
+// Bytes of one chroma plane of a w x h MB picture: 8 x 8 samples per MB (4:2:0) or 16 x 16 (4:4:4).
+static size_t chroma_bytes(const h264r_ctx* c, int w, int h) { return (size_t)w * h * (c->fmt == 3 ? 256 : 64); }
+
 static int ensure_slot(h264r_ctx* c, int slot, int w, int h)
 {
     if (c->slot[slot][0] && c->slot_w[slot] == w && c->slot_h[slot] == h) return H264R_OK;
@@ -401,7 +415,7 @@ static int ensure_slot(h264r_ctx* c, int slot, int w, int h)
         (void)hipFree(c->slot[slot][0]);
         c->slot[slot][0] = nullptr;
     }
-    size_t ys = (size_t)w * 16 * h * 16, cs = (size_t)w * 8 * h * 8;
+    size_t ys = (size_t)w * 16 * h * 16, cs = chroma_bytes(c, w, h);
     uint8_t* base = nullptr;
     if (hipMalloc(reinterpret_cast<void**>(&base), ys + 2 * cs + H264R_PLANE_SLACK) != hipSuccess) return H264R_ENOMEM;
     c->slot[slot][0] = base; c->slot[slot][1] = base + ys; c->slot[slot][2] = base + ys + cs;
@@ -417,7 +431,7 @@ int h264r_set_ref(h264r_ctx* c, int slot, const uint8_t* y, const uint8_t* u, co
     (void)hipSetDevice(c->device);
     int st = ensure_slot(c, slot, w, h);
     if (st) return st;
-    size_t ys = (size_t)w * 16 * h * 16, cs = (size_t)w * 8 * h * 8;
+    size_t ys = (size_t)w * 16 * h * 16, cs = chroma_bytes(c, w, h);
     HIP_OK(hipMemcpyAsync(c->slot[slot][0], y, ys, hipMemcpyHostToDevice, c->stream));
     HIP_OK(hipMemcpyAsync(c->slot[slot][1], u, cs, hipMemcpyHostToDevice, c->stream));
     HIP_OK(hipMemcpyAsync(c->slot[slot][2], v, cs, hipMemcpyHostToDevice, c->stream));
@@ -789,6 +803,44 @@ static int launch_all(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row
     return H264R_OK;
 }
 
+// 4:4:4 (ChromaArrayType 3): every colour plane is decoded as luma -- decode_one_component for
+// PLANE_Y, PLANE_U, PLANE_V (decoder.cc:65-79) runs the luma prediction, residual and (luma-style,
+// deblock.cc:422) filtering on each, with the plane's QP, levels, weights and scaling lists and the
+// luma bS.  The planes never read each other, so a 4:4:4 batch runs as three 4:2:0-shaped launch
+// sequences of the same kernels: pass pl's batch (k_derive444) has plane pl in the luma slots --
+// records with its QP and level offset, slices with its weights, quant with its lists, DPB tables
+// pointing at the references' plane pl -- and its output luma is the caller's plane pl; its own
+// (empty) chroma goes to scratch.  The passes are stream-ordered and reuse one derived set.
+static int run_444(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row0, int row1)
+{
+    const int P = b.num_pics;
+    const size_t nmb = (size_t)b.width_mbs * b.height_mbs;
+    const int ntab = b.ref_planes_stride ? P : 1;
+    int st;
+    if ((st = dev_resize(&c->d444_mbs, &c->c444_mbs, (size_t)P * nmb)) ||
+        (st = dev_resize(&c->d444_slices, &c->c444_slices, (size_t)P * b.slice_stride)) ||
+        (st = dev_resize(&c->d444_quant, &c->c444_quant, (size_t)P)) ||
+        (st = dev_resize(&c->d444_refs, &c->c444_refs, (size_t)ntab * 3 * H264R_MAX_SLOTS)) ||
+        (st = dev_resize(&c->d444_chroma, &c->c444_chroma, (size_t)P * 2 * 64 * nmb + H264R_PLANE_SLACK)))
+        return st;
+    const bool timing = c->timing;
+    for (int pl = 0; pl < 3; ++pl) {
+        hipLaunchKernelGGL(k_derive444, dim3(1024), dim3(256), 0, s, b, pl, c->d444_mbs, c->d444_slices, c->d444_quant,
+                           c->d444_refs, ntab, c->d_err);
+        HIP_OK(hipGetLastError());
+        h264r_batch d = b;
+        d.mbs = c->d444_mbs; d.slices = c->d444_slices; d.quant = c->d444_quant;
+        d.ref_planes = c->d444_refs;
+        d.ref_planes_stride = b.ref_planes_stride ? 3 * H264R_MAX_SLOTS : 0;
+        d.out_y = pl == 0 ? b.out_y : pl == 1 ? b.out_u : b.out_v;
+        d.out_u = c->d444_chroma;
+        d.out_v = c->d444_chroma + (size_t)P * 64 * nmb;
+        if ((st = launch_all(c, d, s, row0, row1, c->sc))) return st;
+    }
+    if (timing) c->timed_launches -= 2;            // h264r_last_timing: per batch, its three passes together
+    return H264R_OK;
+}
+
 static int run_batch(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row0, int row1)
 {
     // the scratch is shared by every launch of this context: a launch on another stream
@@ -798,6 +850,7 @@ static int run_batch(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row0
         HIP_OK(hipStreamWaitEvent(s, c->ev_last, 0));
     }
     c->last_stream = s;
+    if (c->fmt == 3) return run_444(c, b, s, row0, row1);
     return launch_all(c, b, s, row0, row1, c->sc);
 }
 
@@ -976,8 +1029,11 @@ int h264r_picture_end_async(h264r_ctx* c, int keep_slot)
     for (uint8_t s : P.seen) if (!s) return H264R_ESTATE;      // every MB must be submitted
     if (keep_slot >= H264R_MAX_SLOTS) return H264R_EINVAL;
     (void)hipSetDevice(c->device);
-    const size_t n = (size_t)P.pw * P.ph, ys = n * 256, cs = n * 64;
+    const size_t n = (size_t)P.pw * P.ph, ys = n * 256, cs = chroma_bytes(c, P.pw, P.ph);
     if (P.h_levels.empty()) P.h_levels.push_back(0);
+    // 4:4:4: frame pictures only; a PCM MB's Cr view reads 128 entries past its block (run_444)
+    if (c->fmt == 3 && P.h_pic.structure != H264R_FRAME) return H264R_EUNSUPPORTED;
+    if (c->fmt == 3) P.h_levels.insert(P.h_levels.end(), 128, 0);
     // every referenced slot must be loaded, with a frame of this picture's size (a field
     // picture: twice its height; its entries may name either field of a slot, include/h264r.h)
     const int fld = P.h_pic.structure != H264R_FRAME;
@@ -1058,7 +1114,7 @@ int h264r_picture_wait(h264r_ctx* c, uint8_t* y, uint8_t* u, uint8_t* v)
     P.pending = false;
     --c->sp_pending;
     c->sp_wait = 1 - c->sp_wait;
-    const size_t n = (size_t)P.pw * P.ph, ys = n * 256, cs = n * 64;
+    const size_t n = (size_t)P.pw * P.ph, ys = n * 256, cs = chroma_bytes(c, P.pw, P.ph);
     if (y) memcpy(y, P.out, ys);
     if (u) memcpy(u, P.out + ys, cs);
     if (v) memcpy(v, P.out + ys + cs, cs);

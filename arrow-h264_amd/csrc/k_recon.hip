@@ -174,3 +174,69 @@ extern "C" __global__ __launch_bounds__(256) void k_untile(h264r_batch b, int2 r
         *reinterpret_cast<uint2*>(dst) = *reinterpret_cast<const uint2*>(mb + RECON_CB + pl * 64 + r * 8);
     }
 }
+
+// k_derive444: one colour plane `pl` of a 4:4:4 batch as a 4:2:0-shaped batch whose luma is that
+// plane (h264r_host.hip run_444; decode_one_component decoder.cc:65-79 runs the luma path on each
+// plane of a ChromaArrayType 3 MB):
+//   records: qp_y := QpC[pl - 1] (deblocking, deblock.cc:469-470), qp_scaled[0] := qp_scaled[pl]
+//            (dequantisation, transform.cc:400-401), coef_off := the plane's luma-like level block
+//            (include/h264r.h, 4:4:4), CodedBlockPatternChroma 0, chroma mode DC; cbp_blks stays
+//            the luma plane's (the bS reads cbp_blks[0] only, deblock.cc:135,212);
+//   slices:  the plane's weights and offsets in the luma slots, the chroma denominator
+//            (mc_prediction inter_prediction.cc:68-74);
+//   quant:   the plane's 4x4 and 8x8 lists in the luma slots (set_quant transform.cc:259-301);
+//   DPB tables: every plane entry of a slot -> the slot's plane pl (the luma MC reads it; the
+//            derived chroma reads stay inside it).
+// Field pictures are not on the 4:4:4 path: such a batch flags the device error word.
+extern "C" __global__ __launch_bounds__(256) void k_derive444(h264r_batch b, int pl, h264r_mb* __restrict__ mbs,
+                                                              h264r_slice* __restrict__ slices, h264r_quant* __restrict__ quant,
+                                                              const uint8_t** __restrict__ refs, int ntab, int* err)
+{
+    const int64_t nt = (int64_t)gridDim.x * blockDim.x, t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t nmb = (int64_t)b.width_mbs * b.height_mbs, P = b.num_pics;
+    for (int64_t i = t0; i < P * nmb; i += nt) {
+        h264r_mb m = b.mbs[i];
+        const int cbpl = m.cbp & 15;
+        if (m.mb_type == H264R_I_PCM) m.coef_off += 128u * (uint32_t)pl;
+        else m.coef_off += (uint32_t)(pl * (64 * __builtin_popcount(cbpl) + (m.mb_type == H264R_I_16x16 ? 16 : 0)));
+        if (pl) { m.qp_y = m.qp_c[pl - 1]; m.qp_scaled[0] = m.qp_scaled[pl]; }
+        m.cbp = (uint8_t)cbpl;
+        m.chroma_mode = 0;
+        mbs[i] = m;
+    }
+    for (int64_t i = t0; i < P * b.slice_stride; i += nt) {
+        h264r_slice x = b.slices[i];
+        if (pl) {
+            for (int l = 0; l < 2; ++l)
+                for (int r = 0; r < H264R_MAX_REFS; ++r) {
+                    x.wp_weight[l][r][0] = x.wp_weight[l][r][pl];
+                    x.wp_offset[l][r][0] = x.wp_offset[l][r][pl];
+                }
+            x.luma_log2_wd = x.chroma_log2_wd;
+        }
+        slices[i] = x;
+    }
+    constexpr int QW = (int)(sizeof(h264r_quant) / 2);          // int16 entries of a table
+    constexpr int S4 = 3 * 6 * 16, S8 = 3 * 6 * 64;              // one intra/inter half of each array
+    for (int64_t i = t0; i < P * QW; i += nt) {
+        const int64_t q = i / QW;
+        int k = (int)(i % QW);
+        const int16_t* src = reinterpret_cast<const int16_t*>(b.quant + q);
+        // the luma slot [intra/inter][0] takes plane pl's entry; everything else is copied
+        int from = k;
+        if (k < 2 * S4) {
+            const int half = k / S4, r = k % S4;
+            if (r < 6 * 16) from = half * S4 + pl * 6 * 16 + r;
+        } else {
+            const int k8 = k - 2 * S4, half = k8 / S8, r = k8 % S8;
+            if (r < 6 * 64) from = 2 * S4 + half * S8 + pl * 6 * 64 + r;
+        }
+        reinterpret_cast<int16_t*>(quant + q)[k] = src[from];
+    }
+    for (int64_t i = t0; i < (int64_t)ntab * 3 * H264R_MAX_SLOTS; i += nt) {
+        const int64_t tab = i / (3 * H264R_MAX_SLOTS), e = i % (3 * H264R_MAX_SLOTS), slot = e / 3;
+        refs[i] = b.ref_planes[tab * b.ref_planes_stride + 3 * slot + pl];
+    }
+    for (int64_t i = t0; i < P; i += nt)
+        if (b.pics[i].structure != H264R_FRAME) atomicOr(err, 1);
+}

@@ -247,8 +247,9 @@ int h264r_synth_picture(const h264r_synth_cfg* c, int index, h264r_mb* mbs, int1
         c->num_slices > c->height_mbs || c->num_refs < 0 || c->num_refs > H264R_MAX_REFS ||
         c->structure < H264R_FRAME || c->structure > H264R_BOTTOM_FIELD ||
         (c->kind != H264R_SYNTH_INTRA && c->num_refs < 1) || c->qp_min < 0 || c->qp_max > 51 ||
-        c->qp_min > c->qp_max)
+        c->qp_min > c->qp_max || (c->chroma_format == 3 && c->structure != H264R_FRAME))
         return H264R_EINVAL;
+    const int f444 = c->chroma_format == 3;
     rng_t r = {c->seed * 0x100000001B3ull + (uint64_t)index * 0x9E3779B97F4A7C15ull + 1};
     int W = c->width_mbs, H = c->height_mbs, nmb = W * H;
     gen_t g = {c, W * 4, mbs, mv, ref_idx};
@@ -290,8 +291,9 @@ int h264r_synth_picture(const h264r_synth_cfg* c, int index, h264r_mb* mbs, int1
             m->flags = H264R_MBF_INTRA;
             m->cbp_blks = 0xFFFF;
             uint8_t* raw = (uint8_t*)(levels + off);
-            for (int k = 0; k < 384; ++k) raw[k] = (uint8_t)rnd(&r, 256);
-            off += 192;
+            const int npcm = f444 ? 768 : 384;            /* 4:4:4: Y, Cb, Cr 256 samples each */
+            for (int k = 0; k < npcm; ++k) raw[k] = (uint8_t)rnd(&r, 256);
+            off += npcm / 2;
             continue;
         }
         int cbpl = 0, cbpc = 0, t8 = 0;
@@ -335,7 +337,8 @@ int h264r_synth_picture(const h264r_synth_cfg* c, int index, h264r_mb* mbs, int1
                 if (av[0] && av[1] && av[3]) md[k++] = 3;
                 m->chroma_mode = (uint8_t)pick_mode(&r, md, k);
             }
-            cbpc = rnd(&r, 3);
+            cbpc = f444 ? 0 : rnd(&r, 3);
+            if (f444) m->chroma_mode = 0;                 /* no chroma intra mode in 4:4:4 */
         } else {
             int k = rnd(&r, 90);    /* conditional on inter: skip/16x16/16x8/8x16/8x8 = 15/45/10/10/10 */
             int mt = k < 15 ? H264R_P_SKIP : k < 60 ? H264R_P_16x16 : k < 70 ? H264R_P_16x8 : k < 80 ? H264R_P_8x16 : H264R_P_8x8;
@@ -365,7 +368,7 @@ int h264r_synth_picture(const h264r_synth_cfg* c, int index, h264r_mb* mbs, int1
                 break; }
             }
             int skip_res = mt == H264R_P_SKIP && (!bslice || rnd(&r, 2));
-            if (!skip_res) { cbpl = rnd(&r, 16); cbpc = rnd(&r, 3); }
+            if (!skip_res) { cbpl = rnd(&r, 16); cbpc = f444 ? 0 : rnd(&r, 3); }
             if (t8 == -1) t8 = 0;
             else t8 = c->transform8x8 && cbpl && rnd(&r, 2);
             if (mt == H264R_P_SKIP && !bslice) t8 = 0;
@@ -414,6 +417,20 @@ int h264r_synth_picture(const h264r_synth_cfg* c, int index, h264r_mb* mbs, int1
             for (int k = 0; k < 8; ++k) levels[off + k] = gen_level(&r);
             off += 8;
         }
+        /* 4:4:4: the Cb and Cr planes' luma-like blocks (the same coded 8x8 blocks, their own
+           levels; decode_one_component, decoder.cc:65-79); cbp_blks stays the luma plane's
+           (the reference's bS reads cbp_blks[0] only, deblock.cc:135,212) */
+        for (int pl = 1; f444 && pl <= 2; ++pl) {
+            for (int b8 = 0; b8 < 4; ++b8) {
+                if (!(cbpl & (1 << b8))) continue;
+                for (int k = 0; k < 64; ++k) levels[off + k] = (i16 && (k % 16) == 0 && !t8) ? 0 : gen_level(&r);
+                off += 64;
+            }
+            if (i16) {
+                for (int k = 0; k < 16; ++k) levels[off + k] = gen_level(&r);
+                off += 16;
+            }
+        }
         m->cbp_blks = blks;
     }
     *n_levels = off;
@@ -451,6 +468,18 @@ int h264r_synth_refpic(uint64_t seed, int slot, int width_mbs, int height_mbs, u
     texture(s, y, width_mbs * 16, height_mbs * 16, 8);
     texture(s + 1, u, width_mbs * 8, height_mbs * 8, 4);
     texture(s + 2, v, width_mbs * 8, height_mbs * 8, 4);
+    return H264R_OK;
+}
+
+int h264r_synth_refpic_fmt(uint64_t seed, int slot, int width_mbs, int height_mbs, int chroma_format, uint8_t* y,
+                           uint8_t* u, uint8_t* v)
+{
+    if (chroma_format != 3) return h264r_synth_refpic(seed, slot, width_mbs, height_mbs, y, u, v);
+    if (!y || !u || !v || width_mbs <= 0 || height_mbs <= 0) return H264R_EINVAL;
+    uint64_t s = seed * 31 + (uint64_t)slot * 0x2545F4914F6CDD1Dull;
+    texture(s, y, width_mbs * 16, height_mbs * 16, 8);
+    texture(s + 1, u, width_mbs * 16, height_mbs * 16, 8);
+    texture(s + 2, v, width_mbs * 16, height_mbs * 16, 8);
     return H264R_OK;
 }
 

@@ -120,10 +120,11 @@ def quant_lists(m4: np.ndarray, m8: np.ndarray) -> np.ndarray:
 class Decoder:
     """One reconstruction context on one GPU (reference: one Decoder per slice_t)."""
 
-    def __init__(self, device: int = 0, max_width_mbs: int = 240, max_height_mbs: int = 135):
+    def __init__(self, device: int = 0, max_width_mbs: int = 240, max_height_mbs: int = 135, chroma_format: int = 1):
         L = lib()
         h = C.c_void_p()
-        _check("h264r_create", L.h264r_create(C.byref(h), device, max_width_mbs, max_height_mbs, 1, 8))
+        _check("h264r_create", L.h264r_create(C.byref(h), device, max_width_mbs, max_height_mbs, chroma_format, 8))
+        self._fmt = chroma_format
         self._h = h
         self._L = L
         self._quant = quant_flat()
@@ -185,9 +186,10 @@ class Decoder:
         """Decoder::deblock_filter: runs reconstruction + deblocking for the picture on
         the GPU and returns the (Y, Cb, Cr) planes."""
         W, H = self._dims
+        c = 16 if self._fmt == 3 else 8
         y = np.empty((16 * H, 16 * W), np.uint8)
-        u = np.empty((8 * H, 8 * W), np.uint8)
-        v = np.empty((8 * H, 8 * W), np.uint8)
+        u = np.empty((c * H, c * W), np.uint8)
+        v = np.empty((c * H, c * W), np.uint8)
         _check("h264r_picture_end", self._L.h264r_picture_end(self._h, A.ptr(y), A.ptr(u), A.ptr(v), keep_slot))
         return y, u, v
 
@@ -200,9 +202,10 @@ class Decoder:
     def wait(self):
         """h264r_picture_wait: planes of the oldest picture handed to deblock_filter_async."""
         W, H = self._waiting.pop(0)
+        c = 16 if self._fmt == 3 else 8
         y = np.empty((16 * H, 16 * W), np.uint8)
-        u = np.empty((8 * H, 8 * W), np.uint8)
-        v = np.empty((8 * H, 8 * W), np.uint8)
+        u = np.empty((c * H, c * W), np.uint8)
+        v = np.empty((c * H, c * W), np.uint8)
         _check("h264r_picture_wait", self._L.h264r_picture_wait(self._h, A.ptr(y), A.ptr(u), A.ptr(v)))
         return y, u, v
 

@@ -27,6 +27,7 @@ MBF_INTRA, MBF_T8x8, MBF_BYPASS = 1, 2, 4
 
 SYNTH_INTRA, SYNTH_P, SYNTH_B = 0, 1, 2
 SYNTH_MAX_LEVELS_PER_MB = 416
+SYNTH_MAX_LEVELS_PER_MB_444 = 816
 
 # ---- numpy dtypes of the canonical device formats ----------------------------------
 MB_DTYPE = np.dtype([
@@ -64,7 +65,7 @@ class SynthCfg(C.Structure):
         ("qp_min", C.c_int32), ("qp_max", C.c_int32), ("pcm_permille", C.c_int32),
         ("intra_permille", C.c_int32), ("mv_range_x", C.c_int32),
         ("mv_range_y", C.c_int32), ("lossless_permille", C.c_int32), ("sp_slices", C.c_int32),
-        ("structure", C.c_int32), ("seed", C.c_uint64),
+        ("structure", C.c_int32), ("chroma_format", C.c_int32), ("seed", C.c_uint64),
     ]
 
     def as_dict(self) -> dict:
@@ -103,11 +104,12 @@ def bind_synth(lib: C.CDLL) -> None:
     lib.h264r_synth_picture.argtypes = [C.POINTER(SynthCfg), C.c_int, P, P,
                                         C.POINTER(C.c_int64), P, P, P, P]
     lib.h264r_synth_refpic.argtypes = [C.c_uint64, C.c_int, C.c_int, C.c_int, P, P, P]
+    lib.h264r_synth_refpic_fmt.argtypes = [C.c_uint64, C.c_int, C.c_int, C.c_int, C.c_int, P, P, P]
     lib.h264r_synth_slot_poc.argtypes = [C.c_int]
     lib.h264r_synth_cur_poc.argtypes = [C.POINTER(SynthCfg)]
     lib.h264r_synth_ref_frames.argtypes = [C.POINTER(SynthCfg)]
     lib.h264r_synth_algo_bytes.argtypes = [P, P, C.c_int, C.c_int,
                                            C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
-    for f in ("h264r_synth_default", "h264r_synth_picture", "h264r_synth_refpic",
+    for f in ("h264r_synth_default", "h264r_synth_picture", "h264r_synth_refpic", "h264r_synth_refpic_fmt",
               "h264r_synth_slot_poc", "h264r_synth_cur_poc", "h264r_synth_ref_frames", "h264r_synth_algo_bytes"):
         getattr(lib, f).restype = C.c_int

@@ -19,13 +19,15 @@ class DeviceBatch:
     width_mbs: int
     height_mbs: int
     tensors: dict = field(default_factory=dict)   # keeps device memory alive
+    chroma_format: int = 1
 
     def planes(self, i: int):
         """(Y, Cb, Cr) of picture i as numpy arrays (device -> host copy)."""
         W, H = self.width_mbs, self.height_mbs
+        c = 16 if self.chroma_format == 3 else 8
         y = self.tensors["out_y"][i].cpu().numpy().reshape(16 * H, 16 * W)
-        u = self.tensors["out_u"][i].cpu().numpy().reshape(8 * H, 8 * W)
-        v = self.tensors["out_v"][i].cpu().numpy().reshape(8 * H, 8 * W)
+        u = self.tensors["out_u"][i].cpu().numpy().reshape(c * H, c * W)
+        v = self.tensors["out_v"][i].cpu().numpy().reshape(c * H, c * W)
         return y, u, v
 
 
@@ -53,7 +55,8 @@ def pack(pictures, quant: np.ndarray):
         pics.append(p.pic)
     q = np.repeat(np.ascontiguousarray(quant, A.QUANT_DTYPE).reshape(1), len(pictures))
     return dict(mbs=np.concatenate(mbs), levels=np.concatenate(lv), mv=np.stack(mv), ref_idx=np.stack(rr),
-                slices=np.concatenate(sl), pics=np.concatenate(pics), quant=q, stride=stride, W=W, H=H)
+                slices=np.concatenate(sl), pics=np.concatenate(pics), quant=q, stride=stride, W=W, H=H,
+                chroma_format=int(pictures[0].cfg.chroma_format))
 
 
 def to_device(host: dict, n: int, ref_planes_ptr: int | None, device: str = "cuda") -> DeviceBatch:
@@ -65,11 +68,13 @@ def to_device(host: dict, n: int, ref_planes_ptr: int | None, device: str = "cud
     W, H = host["W"], host["H"]
     t = {k: dev(host[k]) for k in ("mbs", "levels", "mv", "ref_idx", "slices", "pics", "quant")}
     t["out_y"] = torch.zeros((n, 256 * W * H), dtype=torch.uint8, device=device)
-    t["out_u"] = torch.zeros((n, 64 * W * H), dtype=torch.uint8, device=device)
-    t["out_v"] = torch.zeros((n, 64 * W * H), dtype=torch.uint8, device=device)
+    fmt = host.get("chroma_format", 1)
+    cs = (256 if fmt == 3 else 64) * W * H              # 4:4:4: chroma planes of the luma size
+    t["out_u"] = torch.zeros((n, cs), dtype=torch.uint8, device=device)
+    t["out_v"] = torch.zeros((n, cs), dtype=torch.uint8, device=device)
     b = A.Batch()
     b.num_pics, b.width_mbs, b.height_mbs, b.slice_stride = n, W, H, host["stride"]
     for k in ("mbs", "levels", "mv", "ref_idx", "slices", "pics", "quant", "out_y", "out_u", "out_v"):
         setattr(b, k, t[k].data_ptr())
     b.ref_planes = ref_planes_ptr
-    return DeviceBatch(b, n, W, H, t)
+    return DeviceBatch(b, n, W, H, t, fmt)

@@ -6,11 +6,14 @@ import numpy as np
 from . import _abi as A
 
 
-def level_count(rec) -> int:
-    """int16 entries of one MB's compacted level block (include/h264r.h)."""
+def level_count(rec, chroma_format: int = 1) -> int:
+    """int16 entries of one MB's compacted level block (include/h264r.h; 4:4:4: three
+    luma-like blocks, a PCM MB 3 x 256 samples)."""
     if int(rec["mb_type"]) == A.I_PCM:
-        return 192
+        return 384 if chroma_format == 3 else 192
     cbpl, cbpc = int(rec["cbp"]) & 15, int(rec["cbp"]) >> 4
+    if chroma_format == 3:
+        return 3 * (64 * bin(cbpl).count("1") + (16 if int(rec["mb_type"]) == A.I_16x16 else 0))
     n = 64 * bin(cbpl).count("1")
     n += 128 if cbpc == 2 else 0
     n += 16 if int(rec["mb_type"]) == A.I_16x16 else 0
@@ -26,5 +29,5 @@ def iter_mbs(p):
     for a in range(W * H):
         rec = p.mbs[a:a + 1].copy()
         off = int(rec["coef_off"][0])
-        lv = p.levels[off:off + level_count(rec[0])]
+        lv = p.levels[off:off + level_count(rec[0], int(p.cfg.chroma_format))]
         yield a, rec, lv, np.ascontiguousarray(mv[a // W, a % W]), np.ascontiguousarray(rr[a // W, a % W])

@@ -41,7 +41,8 @@ def picture(lib: C.CDLL, cfg: A.SynthCfg, index: int) -> Picture:
     W, H = cfg.width_mbs, cfg.height_mbs
     n = W * H
     mbs = np.zeros(n, A.MB_DTYPE)
-    levels = np.zeros(n * A.SYNTH_MAX_LEVELS_PER_MB, np.int16)
+    f444 = cfg.chroma_format == 3
+    levels = np.zeros(n * (A.SYNTH_MAX_LEVELS_PER_MB_444 if f444 else A.SYNTH_MAX_LEVELS_PER_MB), np.int16)
     mv = np.zeros((2, 4 * H, 4 * W), np.uint32)
     ref_idx = np.zeros((2, 4 * H, 4 * W), np.int8)
     slices = np.zeros(cfg.num_slices, A.SLICE_DTYPE)
@@ -51,19 +52,23 @@ def picture(lib: C.CDLL, cfg: A.SynthCfg, index: int) -> Picture:
                                  A.ptr(mv), A.ptr(ref_idx), A.ptr(slices), A.ptr(pic))
     if st != A.OK:
         raise ValueError(f"h264r_synth_picture -> {st}")
-    return Picture(cfg, index, mbs, levels[: max(int(nlev.value), 8)].copy(), mv, ref_idx, slices, pic)
+    # 4:4:4: a PCM MB's Cr view reads 128 entries past its 384 (include/h264r.h): kept readable
+    keep = max(int(nlev.value), 8) + (128 if f444 else 0)
+    return Picture(cfg, index, mbs, levels[:keep].copy(), mv, ref_idx, slices, pic)
 
 
 def refpics(lib: C.CDLL, cfg: A.SynthCfg, nslots: int | None = None):
     """[(y, u, v)] for DPB slots 0..n-1: the frames the pictures reference (a field cfg's
     references are fields of frames of twice its height, include/h264r_synth.h)."""
     W, H = cfg.width_mbs, cfg.height_mbs * (2 if cfg.structure else 1)
+    c = 16 if cfg.chroma_format == 3 else 8          # 4:4:4: chroma planes of the luma size
     out = []
     for s in range(lib.h264r_synth_ref_frames(C.byref(cfg)) if nslots is None else nslots):
         y = np.zeros((16 * H, 16 * W), np.uint8)
-        u = np.zeros((8 * H, 8 * W), np.uint8)
-        v = np.zeros((8 * H, 8 * W), np.uint8)
-        st = lib.h264r_synth_refpic(C.c_uint64(cfg.seed), s, W, H, A.ptr(y), A.ptr(u), A.ptr(v))
+        u = np.zeros((c * H, c * W), np.uint8)
+        v = np.zeros((c * H, c * W), np.uint8)
+        st = lib.h264r_synth_refpic_fmt(C.c_uint64(cfg.seed), s, W, H, int(cfg.chroma_format), A.ptr(y), A.ptr(u),
+                                        A.ptr(v))
         if st != A.OK:
             raise ValueError(f"h264r_synth_refpic -> {st}")
         out.append((y, u, v))

@@ -23,8 +23,11 @@ extern "C" {
 #define H264R_SYNTH_P     1   /* config 3: P pictures (IPPP Main)         */
 #define H264R_SYNTH_B     2   /* config 4/5: B pictures (IBBP High)       */
 
-/* Upper bound of int16 level-pool entries one MB can use (4*64+128+16+8, rounded to 8). */
+/* Upper bound of int16 level-pool entries one MB can use: 4:2:0 4*64+128+16+8 (rounded to 8);
+ * 4:4:4 three luma-like blocks 3*(4*64+16), and a PCM MB's plane-2 view reads 128 entries past
+ * its 384 (include/h264r.h, 4:4:4). */
 #define H264R_SYNTH_MAX_LEVELS_PER_MB 416
+#define H264R_SYNTH_MAX_LEVELS_PER_MB_444 816
 
 typedef struct h264r_synth_cfg {
     int32_t  width_mbs, height_mbs;
@@ -55,6 +58,9 @@ typedef struct h264r_synth_cfg {
                                     of 2 * height_mbs MB rows: the fields of frame slot s have POC
                                     4 s (top) and 4 s + 1 (bottom), the lists order them by POC as
                                     8.2.4.2.4/8.2.4.2.5 would (alternating parity) */
+    int32_t  chroma_format;      /* chroma_format_idc: 3 = 4:4:4 (every plane coded like luma: three
+                                    luma-like level blocks per MB, CodedBlockPatternChroma 0, a PCM MB
+                                    3 x 256 samples; frame pictures); anything else = 4:2:0            */
     uint64_t seed;
 } h264r_synth_cfg;
 
@@ -72,6 +78,10 @@ int  h264r_synth_picture(const h264r_synth_cfg* cfg, int index, h264r_mb* mbs, i
 /* Deterministic reference-picture content for DPB slot `slot` (smooth texture + noise). */
 int  h264r_synth_refpic(uint64_t seed, int slot, int width_mbs, int height_mbs,
                         uint8_t* y, uint8_t* u, uint8_t* v);
+/* The same for a chroma format: 3 = 4:4:4, chroma planes of the luma plane's size (the 4:2:0
+ * content of h264r_synth_refpic otherwise). */
+int  h264r_synth_refpic_fmt(uint64_t seed, int slot, int width_mbs, int height_mbs, int chroma_format,
+                            uint8_t* y, uint8_t* u, uint8_t* v);
 
 /* POC assigned to DPB slot `slot` (its frame; fields: + 0 top, + 1 bottom) / to the current
  * picture (a field's own POC) by the generator, and the number of DPB frames it references. */

@@ -267,7 +267,7 @@ static int picture_end(h264r_ctx* c, uint8_t* y, uint8_t* u, uint8_t* v, int kee
         if ((st = h264r_set_ref(c, keep, y, u, v, c->pw, c->ph))) return st;
     } else if (keep >= 0) {
         /* a field into its parity's rows of the slot's frame (dpb_combine_field_yuv
-           picture.cc:573-590), the other field's rows left as they are */
+           picture.cc:578-622), the other field's rows left as they are */
         if ((st = ensure_slot(c, keep, c->pw, frame_h))) return st;
         const int bot = c->pic.structure == H264R_BOTTOM_FIELD;
         for (int k = 0; k < 3; ++k) {

@@ -1181,8 +1181,82 @@ static void filter_edge(pstate* s, int addr, int chroma, int pl, int vertical, i
 }
 
 /* deblock_pic (deblock.cc:537-552) + the Deblock::deblock gate (:631-640). */
+/* ---------------------------------------------------------------- 4:4:4 (ChromaArrayType 3)
+ * Decoder::decode runs decode_one_component for PLANE_Y, PLANE_U and PLANE_V (decoder.cc:65-79):
+ * each colour plane takes the LUMA prediction (intra_pred_* with the MB's luma modes, get_block_luma
+ * with plane pl, inter_prediction.cc:158-340, its weights pred_weight_l[][pl][] and the chroma
+ * denominator for pl > 0, :53-86), the luma residual path (coeff_luma_* / transform_luma_dc with
+ * qp_scaled[pl] and plane pl's InvLevelScale, transform.cc:394-456, 825-854), and deblocking filters
+ * it luma-style (chromaStyleFilteringFlag = chromaEdgeFlag && ChromaArrayType != 3, deblock.cc:422)
+ * with the luma bS (strength_* read cbp_blks[0], :135,212; Strength index edge*4/MbWidthC) and QpC
+ * of the plane (:469-470).  Planes never read each other, so a 4:4:4 picture is decoded here as
+ * three pictures whose luma is plane pl, each through the 4:2:0 restatement above with plane
+ * pl's QP, levels, weights, scaling lists and reference planes in the luma slots (their chroma
+ * is scratch).  Pinned to the reference by its own 4:4:4 fixtures (tests/golden, ref_driver). */
+static int derive_plane(const oracle_picture* p, int pl, oracle_picture* d, h264r_mb** mbs, h264r_slice** sl,
+                        h264r_quant** q, uint8_t** scratch)
+{
+    const int n = p->width_mbs * p->height_mbs, ns = p->pic->num_slices;
+    const size_t csz = (size_t)p->width_mbs * 8 * p->height_mbs * 8;
+    *mbs = malloc(sizeof(h264r_mb) * (size_t)n);
+    *sl = malloc(sizeof(h264r_slice) * (size_t)ns);
+    *q = malloc(sizeof(h264r_quant));
+    *scratch = malloc(2 * csz);
+    if (!*mbs || !*sl || !*q || !*scratch) return H264R_ENOMEM;
+    for (int a = 0; a < n; ++a) {
+        h264r_mb m = p->mbs[a];
+        const int cbpl = m.cbp & 15;
+        if (m.mb_type == H264R_I_PCM) m.coef_off += 128u * (uint32_t)pl;           /* 256 samples per plane */
+        else m.coef_off += (uint32_t)(pl * (64 * __builtin_popcount((unsigned)cbpl) + (m.mb_type == H264R_I_16x16 ? 16 : 0)));
+        if (pl) { m.qp_y = m.qp_c[pl - 1]; m.qp_scaled[0] = m.qp_scaled[pl]; }
+        m.cbp = (uint8_t)cbpl;
+        m.chroma_mode = 0;
+        (*mbs)[a] = m;
+    }
+    for (int i = 0; i < ns; ++i) {
+        h264r_slice x = p->slices[i];
+        if (pl) {
+            for (int l = 0; l < 2; ++l)
+                for (int r = 0; r < H264R_MAX_REFS; ++r) {
+                    x.wp_weight[l][r][0] = x.wp_weight[l][r][pl];
+                    x.wp_offset[l][r][0] = x.wp_offset[l][r][pl];
+                }
+            x.luma_log2_wd = x.chroma_log2_wd;
+        }
+        (*sl)[i] = x;
+    }
+    **q = *p->quant;
+    for (int k = 0; k < 2; ++k) {
+        memcpy((*q)->scale4x4[k][0], p->quant->scale4x4[k][pl], sizeof((*q)->scale4x4[k][0]));
+        memcpy((*q)->scale8x8[k][0], p->quant->scale8x8[k][pl], sizeof((*q)->scale8x8[k][0]));
+    }
+    *d = *p;
+    d->chroma_format = 1;
+    d->mbs = *mbs; d->slices = *sl; d->quant = *q;
+    for (int s = 0; s < H264R_MAX_SLOTS; ++s)
+        for (int k = 0; k < 3; ++k) d->ref_planes[s][k] = p->ref_planes[s][pl];   /* chroma: scratch reads */
+    d->out[0] = p->out[pl];
+    d->out[1] = *scratch; d->out[2] = *scratch + csz;
+    return 0;
+}
+
+static int decode_444(const oracle_picture* p, int what /* 1 reconstruct, 2 deblock, 3 both */)
+{
+    int st = 0;
+    for (int pl = 0; pl < 3 && !st; ++pl) {
+        oracle_picture d;
+        h264r_mb* mbs = NULL; h264r_slice* sl = NULL; h264r_quant* q = NULL; uint8_t* scratch = NULL;
+        st = derive_plane(p, pl, &d, &mbs, &sl, &q, &scratch);
+        if (!st && (what & 1)) st = oracle_reconstruct_picture(&d);
+        if (!st && (what & 2)) st = oracle_deblock_picture(&d);
+        free(mbs); free(sl); free(q); free(scratch);
+    }
+    return st;
+}
+
 int oracle_deblock_picture(const oracle_picture* p)
 {
+    if (p->chroma_format == 3) return decode_444(p, 2);
     int n = p->width_mbs * p->height_mbs;
     pstate s;
     s.p = p; s.wmb = p->width_mbs; s.hmb = p->height_mbs;
@@ -1218,6 +1292,7 @@ int oracle_deblock_picture(const oracle_picture* p)
 
 int oracle_reconstruct_picture(const oracle_picture* p)
 {
+    if (p->chroma_format == 3) return decode_444(p, 1);
     int n = p->width_mbs * p->height_mbs;
     pstate s;
     memset(&s, 0, sizeof(s));
@@ -1235,6 +1310,7 @@ int oracle_reconstruct_picture(const oracle_picture* p)
 
 int oracle_decode_picture(const oracle_picture* p)
 {
+    if (p->chroma_format == 3) return decode_444(p, 3);
     int st = oracle_reconstruct_picture(p);
     if (st) return st;
     return oracle_deblock_picture(p);

@@ -16,7 +16,7 @@
  *
  * usage: ref_driver W H kind nslices idc offA offB t8 wp cip nrefs qpmin qpmax
  *                   pcm_permille intra_permille mvx mvy seed index out.yuv [recon_only
- *                   [lossless_permille [sp_slices [structure]]]]
+ *                   [lossless_permille [sp_slices [structure [chroma_format]]]]]
  * lossless_permille > 0 sets sps.qpprime_y_zero_transform_bypass_flag (the synthetic
  * pictures then hold TransformBypassModeFlag MBs, interpret_mb.cc:804).
  * structure 1 / 2 decodes a top / bottom FIELD picture of H MB rows (shr.field_pic_flag,
@@ -24,6 +24,10 @@
  * DPB frames of 2H rows (as dpb_split_field picture.cc:408-470 does), the coefficient push
  * takes the reference's own field scan (Transform::inverse_scan_* read field_pic_flag,
  * transform.cc:338-386), and deblock_filter runs on the field (exit_picture picture.cc:253).
+ * chroma_format 3 decodes a 4:4:4 picture (sps.chroma_format_idc 3, High 4:4:4 Predictive): every
+ * plane's coefficients go through coeff_luma_* / transform_luma_dc with its ColorPlane, as the
+ * parser does for ChromaArrayType 3 (interpret_residual.cc), and the references are padded
+ * with the luma pads, as pad_dec_picture does for 4:4:4 (picture.cc:207-232).
  * Output: Y plane then Cb then Cr, 8-bit, unpadded.
  *
  * Timing mode (H264R_TIME_REPS=<n>): the reconstruction of the picture -- the
@@ -89,13 +93,16 @@ int main(int argc, char** argv)
     if (argc > k + 1) cfg.lossless_permille = atoi(argv[k + 1]);
     if (argc > k + 2) cfg.sp_slices = atoi(argv[k + 2]);
     if (argc > k + 3) cfg.structure = atoi(argv[k + 3]);
+    if (argc > k + 4) cfg.chroma_format = atoi(argv[k + 4]);
+    const bool f444 = cfg.chroma_format == 3;
+    const int CW = f444 ? 16 : 8;                       /* chroma samples per MB side */
     const bool fld = cfg.structure != H264R_FRAME;
     const PictureStructure pstruct = cfg.structure == H264R_TOP_FIELD ? TOP_FIELD
                                    : cfg.structure == H264R_BOTTOM_FIELD ? BOTTOM_FIELD : FRAME;
 
     const int W = cfg.width_mbs, H = cfg.height_mbs, NMB = W * H, W4 = W * 4, PL = W4 * H * 4;
     std::vector<h264r_mb> mbs(NMB);
-    std::vector<int16_t> levels((size_t)NMB * H264R_SYNTH_MAX_LEVELS_PER_MB);
+    std::vector<int16_t> levels((size_t)NMB * H264R_SYNTH_MAX_LEVELS_PER_MB_444);
     std::vector<uint32_t> mv(2 * (size_t)PL);
     std::vector<int8_t> ref_idx(2 * (size_t)PL);
     std::vector<h264r_slice> slices(cfg.num_slices);
@@ -110,14 +117,14 @@ int main(int argc, char** argv)
     VideoParameters* vid = new VideoParameters();
     sps_t* sps = new sps_t();
     pps_t* pps = new pps_t();
-    sps->profile_idc = 100; sps->level_idc = 51;
-    sps->chroma_format_idc = 1; sps->ChromaArrayType = 1;
-    sps->SubWidthC = 2; sps->SubHeightC = 2; sps->MbWidthC = 8; sps->MbHeightC = 8;
+    sps->profile_idc = f444 ? 244 : 100; sps->level_idc = 51;
+    sps->chroma_format_idc = f444 ? 3 : 1; sps->ChromaArrayType = sps->chroma_format_idc;
+    sps->SubWidthC = sps->SubHeightC = f444 ? 1 : 2; sps->MbWidthC = sps->MbHeightC = CW;
     sps->BitDepthY = 8; sps->BitDepthC = 8;
     sps->frame_mbs_only_flag = !fld; sps->direct_8x8_inference_flag = 1;
     const int FH = fld ? 2 * H : H;                     /* FrameHeightInMbs */
     sps->PicWidthInMbs = W; sps->FrameHeightInMbs = FH;
-    sps->PicWidthInSamplesL = W * 16; sps->PicWidthInSamplesC = W * 8;
+    sps->PicWidthInSamplesL = W * 16; sps->PicWidthInSamplesC = W * CW;
     sps->PicHeightInMapUnits = H; sps->PicSizeInMapUnits = W * H;
     sps->qpprime_y_zero_transform_bypass_flag = cfg.lossless_permille > 0;
     /* H264R_QMATRIX=<file>: 6x16 + 6x64 int32 raster scaling lists, every one present in
@@ -148,21 +155,21 @@ int main(int argc, char** argv)
        references are the fields of the DPB frames, refs[2 s + bottom] */
     const int nfr = h264r_synth_ref_frames(&cfg);
     std::vector<storable_picture*> refs(fld ? 2 * nfr : nfr);
-    std::vector<uint8_t> ty(W * 16 * FH * 16), tu(W * 8 * FH * 8), tv(W * 8 * FH * 8);
+    std::vector<uint8_t> ty(W * 16 * FH * 16), tu(W * CW * FH * CW), tv(W * CW * FH * CW);
     for (int s = 0; s < nfr; ++s) {
-        h264r_synth_refpic(cfg.seed, s, W, FH, ty.data(), tu.data(), tv.data());
+        h264r_synth_refpic_fmt(cfg.seed, s, W, FH, cfg.chroma_format, ty.data(), tu.data(), tv.data());
         for (int f = 0; f < (fld ? 2 : 1); ++f) {
             storable_picture* r = new storable_picture(vid, fld ? (f ? BOTTOM_FIELD : TOP_FIELD) : FRAME,
-                                                       W * 16, FH * 16, W * 8, FH * 8, 1);
+                                                       W * 16, FH * 16, W * CW, FH * CW, 1);
             const int step = fld ? 2 : 1;                /* dpb_split_field: every second row */
             for (int y = 0; y < H * 16; ++y) for (int x = 0; x < W * 16; ++x) r->imgY[y][x] = ty[(y * step + f) * W * 16 + x];
-            for (int y = 0; y < H * 8; ++y) for (int x = 0; x < W * 8; ++x) {
-                r->imgUV[0][y][x] = tu[(y * step + f) * W * 8 + x];
-                r->imgUV[1][y][x] = tv[(y * step + f) * W * 8 + x];
+            for (int y = 0; y < H * CW; ++y) for (int x = 0; x < W * CW; ++x) {
+                r->imgUV[0][y][x] = tu[(y * step + f) * W * CW + x];
+                r->imgUV[1][y][x] = tv[(y * step + f) * W * CW + x];
             }
             pad_buf(*r->imgY, W * 16, H * 16, r->iLumaStride, MCBUF_LUMA_PAD_X, MCBUF_LUMA_PAD_Y);
-            pad_buf(*r->imgUV[0], W * 8, H * 8, r->iChromaStride, MCBUF_CHROMA_PAD_X, MCBUF_CHROMA_PAD_Y);
-            pad_buf(*r->imgUV[1], W * 8, H * 8, r->iChromaStride, MCBUF_CHROMA_PAD_X, MCBUF_CHROMA_PAD_Y);
+            pad_buf(*r->imgUV[0], W * CW, H * CW, r->iChromaStride, r->iChromaPadX, r->iChromaPadY);
+            pad_buf(*r->imgUV[1], W * CW, H * CW, r->iChromaStride, r->iChromaPadX, r->iChromaPadY);
             r->poc = r->frame_poc = r->top_poc = r->bottom_poc = h264r_synth_slot_poc(s) + f;
             r->is_long_term = 0; r->used_for_reference = 1;
             refs[fld ? 2 * s + f : s] = r;
@@ -171,7 +178,7 @@ int main(int argc, char** argv)
     /* RefPicList entry -> storable_picture (include/h264r.h: slot | H264R_REF_BOTTOM for fields) */
     auto ref_of = [&](int v) { return fld ? refs[2 * (v & 31) + ((v & H264R_REF_BOTTOM) ? 1 : 0)] : refs[v]; };
 
-    storable_picture* dec = new storable_picture(vid, pstruct, W * 16, FH * 16, W * 8, FH * 8, 1);
+    storable_picture* dec = new storable_picture(vid, pstruct, W * 16, FH * 16, W * CW, FH * CW, 1);
     dec->sps = sps; dec->pps = pps;
     dec->used_for_reference = 1;
     dec->poc = dec->frame_poc = pic.poc;
@@ -190,7 +197,7 @@ int main(int argc, char** argv)
         h.slice_type = c.slice_type;
         h.structure = pstruct; h.MbaffFrameFlag = 0; h.field_pic_flag = fld;
         h.bottom_field_flag = pstruct == BOTTOM_FIELD;
-        h.PicHeightInMbs = H; h.PicHeightInSamplesL = H * 16; h.PicHeightInSamplesC = H * 8;
+        h.PicHeightInMbs = H; h.PicHeightInSamplesL = H * 16; h.PicHeightInSamplesC = H * CW;
         h.PicSizeInMbs = W * H;
         h.disable_deblocking_filter_idc = c.deblock_idc;
         h.FilterOffsetA = c.filter_offset_a; h.FilterOffsetB = c.filter_offset_b;
@@ -333,7 +340,8 @@ int main(int argc, char** argv)
             const uint8_t* raw = (const uint8_t*)lv;
             for (int y = 0; y < 16; ++y) for (int x = 0; x < 16; ++x) tr->cof[0][y][x] = raw[y * 16 + x];
             for (int q = 0; q < 2; ++q)
-                for (int y = 0; y < 8; ++y) for (int x = 0; x < 8; ++x) tr->cof[1 + q][y][x] = raw[256 + q * 64 + y * 8 + x];
+                for (int y = 0; y < CW; ++y) for (int x = 0; x < CW; ++x)
+                    tr->cof[1 + q][y][x] = raw[256 + q * CW * CW + y * CW + x];
             mb.cbp_blks[0] = 0xFFFF;
         } else {
             int cbpl = c.cbp & 15, cbpc = c.cbp >> 4;
@@ -343,28 +351,38 @@ int main(int argc, char** argv)
             const int16_t* cac = nullptr; if (cbpc == 2) { cac = p; p += 128; }
             const int16_t* ldc = nullptr; if (c.mb_type == H264R_I_16x16) { ldc = p; p += 16; }
             const int16_t* cdc = nullptr; if (cbpc) { cdc = p; p += 8; }
-            if (ldc) {
-                for (int pos = 0; pos < 16; ++pos)
-                    if (ldc[pos]) s.decoder.coeff_luma_dc(&mb, PLANE_Y, 0, 0, inv4[pos], ldc[pos]);
-                s.decoder.transform_luma_dc(&mb, PLANE_Y);
-            }
-            for (int q = 0; q < 4; ++q) {
-                if (!b8p[q]) continue;
-                if (!mb.transform_size_8x8_flag) {
-                    for (int b4 = 0; b4 < 4; ++b4) {
-                        int x0 = (q & 1) * 2 + (b4 & 1), y0 = (q >> 1) * 2 + (b4 >> 1);
-                        for (int pos = 0; pos < 16; ++pos) {
-                            int v = b8p[q][b4 * 16 + pos];
-                            if (v) s.decoder.coeff_luma_ac(&mb, PLANE_Y, x0, y0, inv4[pos], v);
+            /* a luma-like block (every plane of a 4:4:4 MB: the coded 8x8 blocks, then the I16 DC) */
+            auto push_luma = [&](ColorPlane pl, const int16_t* const* b8, const int16_t* dc) {
+                if (dc) {
+                    for (int pos = 0; pos < 16; ++pos)
+                        if (dc[pos]) s.decoder.coeff_luma_dc(&mb, pl, 0, 0, inv4[pos], dc[pos]);
+                    s.decoder.transform_luma_dc(&mb, pl);
+                }
+                for (int q = 0; q < 4; ++q) {
+                    if (!b8[q]) continue;
+                    if (!mb.transform_size_8x8_flag) {
+                        for (int b4 = 0; b4 < 4; ++b4) {
+                            int x0 = (q & 1) * 2 + (b4 & 1), y0 = (q >> 1) * 2 + (b4 >> 1);
+                            for (int pos = 0; pos < 16; ++pos) {
+                                int v = b8[q][b4 * 16 + pos];
+                                if (v) s.decoder.coeff_luma_ac(&mb, pl, x0, y0, inv4[pos], v);
+                            }
+                        }
+                    } else {
+                        int x0 = (q & 1) * 2, y0 = (q >> 1) * 2;
+                        for (int pos = 0; pos < 64; ++pos) {
+                            int v = b8[q][pos];
+                            if (v) s.decoder.coeff_luma_ac(&mb, pl, x0, y0, inv8[pos], v);
                         }
                     }
-                } else {
-                    int x0 = (q & 1) * 2, y0 = (q >> 1) * 2;
-                    for (int pos = 0; pos < 64; ++pos) {
-                        int v = b8p[q][pos];
-                        if (v) s.decoder.coeff_luma_ac(&mb, PLANE_Y, x0, y0, inv8[pos], v);
-                    }
                 }
+            };
+            push_luma(PLANE_Y, b8p, ldc);
+            for (int pl = 1; f444 && pl <= 2; ++pl) {
+                const int16_t* cb8[4] = {nullptr, nullptr, nullptr, nullptr};
+                for (int q = 0; q < 4; ++q) if (cbpl & (1 << q)) { cb8[q] = p; p += 64; }
+                const int16_t* cdcp = nullptr; if (c.mb_type == H264R_I_16x16) { cdcp = p; p += 16; }
+                push_luma((ColorPlane)pl, cb8, cdcp);
             }
             if (cbpc) {
                 for (int pl = 1; pl <= 2; ++pl) {
@@ -418,12 +436,12 @@ int main(int argc, char** argv)
         fwrite(row.data(), 1, W * 16, f);
     }
     for (int q = 0; q < 2; ++q)
-        for (int y = 0; y < H * 8; ++y) {
-            for (int x = 0; x < W * 8; ++x) {
+        for (int y = 0; y < H * CW; ++y) {
+            for (int x = 0; x < W * CW; ++x) {
                 if (dec->imgUV[q][y][x] > 255) { fprintf(stderr, "sample > 255 at C%d(%d,%d)\n", q, x, y); return 6; }
                 row[x] = (uint8_t)dec->imgUV[q][y][x];
             }
-            fwrite(row.data(), 1, W * 8, f);
+            fwrite(row.data(), 1, W * CW, f);
         }
     fclose(f);
     return 0;

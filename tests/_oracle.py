@@ -53,7 +53,7 @@ class OraclePicture(C.Structure):
         ("mbs", C.c_void_p), ("levels", C.c_void_p), ("mv", C.c_void_p),
         ("ref_idx", C.c_void_p), ("slices", C.c_void_p), ("pic", C.c_void_p),
         ("quant", C.c_void_p), ("ref_planes", (C.c_void_p * 3) * A.MAX_SLOTS),
-        ("out", C.c_void_p * 3),
+        ("out", C.c_void_p * 3), ("chroma_format", C.c_int),
     ]
 
 
@@ -108,12 +108,14 @@ def make_oracle_picture(p: synth.Picture, refs, quant: np.ndarray, out) -> Oracl
             o.ref_planes[s][k] = A.ptr(planes[k]).value
     for k in range(3):
         o.out[k] = A.ptr(out[k]).value
+    o.chroma_format = int(p.cfg.chroma_format)
     return o
 
 
-def new_planes(W: int, H: int):
-    return (np.zeros((16 * H, 16 * W), np.uint8), np.zeros((8 * H, 8 * W), np.uint8),
-            np.zeros((8 * H, 8 * W), np.uint8))
+def new_planes(W: int, H: int, chroma_format: int = 1):
+    c = 16 if chroma_format == 3 else 8
+    return (np.zeros((16 * H, 16 * W), np.uint8), np.zeros((c * H, c * W), np.uint8),
+            np.zeros((c * H, c * W), np.uint8))
 
 
 def decode(p: synth.Picture, refs=None, stage: str = "full", quant=None):
@@ -123,7 +125,7 @@ def decode(p: synth.Picture, refs=None, stage: str = "full", quant=None):
     if refs is None:
         refs = synth.refpics(L, p.cfg)
     q = quant_flat() if quant is None else quant
-    out = new_planes(p.cfg.width_mbs, p.cfg.height_mbs)
+    out = new_planes(p.cfg.width_mbs, p.cfg.height_mbs, p.cfg.chroma_format)
     o = make_oracle_picture(p, refs, q, out)
     fn = {"full": L.oracle_decode_picture, "recon": L.oracle_reconstruct_picture}[stage]
     st = fn(C.byref(o))
@@ -145,7 +147,7 @@ def run_reference(cfg: A.SynthCfg, index: int, recon_only: bool = False, time_re
                 cfg.filter_offset_b, cfg.transform8x8, cfg.wp_mode, cfg.constrained_intra,
                 cfg.num_refs, cfg.qp_min, cfg.qp_max, cfg.pcm_permille, cfg.intra_permille,
                 cfg.mv_range_x, cfg.mv_range_y, hex(cfg.seed), index, out, int(recon_only),
-                cfg.lossless_permille, cfg.sp_slices, cfg.structure]
+                cfg.lossless_permille, cfg.sp_slices, cfg.structure, cfg.chroma_format]
         env = dict(os.environ)
         if time_reps:
             env["H264R_TIME_REPS"] = str(time_reps)
@@ -158,9 +160,10 @@ def run_reference(cfg: A.SynthCfg, index: int, recon_only: bool = False, time_re
         if r.returncode != 0:
             raise RuntimeError(f"ref_driver failed ({r.returncode}): {r.stderr[-2000:]}")
         raw = np.fromfile(out, np.uint8)
-    ny, nc = 256 * W * H, 64 * W * H
-    planes = (raw[:ny].reshape(16 * H, 16 * W), raw[ny:ny + nc].reshape(8 * H, 8 * W),
-              raw[ny + nc:].reshape(8 * H, 8 * W))
+    c = 16 if cfg.chroma_format == 3 else 8
+    ny, nc = 256 * W * H, c * c * W * H
+    planes = (raw[:ny].reshape(16 * H, 16 * W), raw[ny:ny + nc].reshape(c * H, c * W),
+              raw[ny + nc:].reshape(c * H, c * W))
     if not time_reps:
         return planes
     line = [ln for ln in r.stderr.splitlines() if ln.startswith("ref_time ")][-1].split()

@@ -97,6 +97,19 @@ CASES = [
     ("bfield_qcif_lossless", 4, 11, 4, dict(structure=1, qp_min=0, qp_max=20, lossless_permille=500), [0]),
     ("pfield_1080i_top", 3, 120, 34, dict(structure=1), [0]),
     ("bfield_1080i_bottom_scaling", 4, 120, 34, dict(structure=2, qm=16), [0]),
+    # 4:4:4 (chroma_format_idc 3, High 4:4:4 Predictive): every colour plane coded and decoded
+    # like luma (decode_one_component decoder.cc:65-79), luma-style deblocking of Cb / Cr
+    # (deblock.cc:422) with their QpC and the luma bS
+    ("i444_qcif_pcm", 2, 11, 9, dict(chroma_format=3, pcm_permille=20), [0]),
+    ("i444_qcif_4x4_cip", 2, 11, 9, dict(chroma_format=3, transform8x8=0, constrained_intra=1), [0]),
+    ("p444_qcif", 3, 11, 9, dict(chroma_format=3, num_refs=2), [0, 1]),
+    ("p444_cif_wp_pcm", 3, 22, 9, dict(chroma_format=3, wp_mode=1, num_refs=3, pcm_permille=30, intra_permille=200), [0]),
+    ("b444_qcif_t8", 4, 11, 9, dict(chroma_format=3, num_refs=3), [0, 1]),
+    ("b444_cif_explicit_3slices_idc2", 4, 22, 9, dict(chroma_format=3, wp_mode=1, num_refs=4, num_slices=3,
+                                                     deblock_idc=2), [0]),
+    ("p444_qcif_lossless", 3, 11, 9, dict(chroma_format=3, qp_min=0, qp_max=20, lossless_permille=500), [0]),
+    ("b444_qcif_scaling", 4, 11, 9, dict(chroma_format=3, qm=17), [0]),
+    ("p444_1080p_strip_qp", 3, 120, 6, dict(chroma_format=3, qp_min=0, qp_max=51, num_slices=2), [0]),
 ]
 
 
