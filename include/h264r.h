@@ -43,6 +43,21 @@
  *   - planes         uint8 Y [H][W], Cb/Cr [H/2][W/2], pitch == width, no padding
  *                    (the reference pads by edge replication, picture.cc:182-205;
  *                     the GPU clamps coordinates instead -- equivalent).
+ *
+ * 4:4:4 (a context created with chroma_format_idc 3; frame pictures, 8-bit): every colour plane
+ * is coded and reconstructed like luma (decode_one_component decoder.cc:65-79), so
+ *   - planes         Cb / Cr are [H][W] like Y, in the output, the batch planes and the DPB slots;
+ *   - levels         an MB's block is three luma-like blocks, Y then Cb then Cr, each: for b8 with
+ *                    (cbp & 1<<b8) 64 levels as above, then, if I_16x16, its 16 DC levels;
+ *                    cbp_chroma must be 0 (CodedBlockPatternChroma, 7.4.5); I_PCM: 768 raw
+ *                    samples (Y, Cb, Cr 256 each), and 256 readable bytes after the MB's block;
+ *   - h264r_mb       qp_c[] / qp_scaled[1..2] are the Cb / Cr QPs (deblocking / dequantisation),
+ *                    cbp_blks the luma plane's non-zero mask (deblock.cc:135,212 read cbp_blks[0]);
+ *                    chroma_mode is not used;
+ *   - h264r_slice    wp_weight / wp_offset [..][..][1..2] with chroma_log2_wd weight Cb / Cr;
+ *   - h264r_quant    scale4x4 / scale8x8 [..][1..2] are the Cb / Cr lists (8x8 lists 8..11).
+ * The library decodes a 4:4:4 batch as three launch sequences of the 4:2:0 kernels, plane pl in
+ * the luma slots.  4:2:2 and > 8-bit are H264R_EUNSUPPORTED.
  */
 #ifndef H264R_H_
 #define H264R_H_
@@ -226,7 +241,8 @@ int  h264r_quant_init_flat(h264r_quant* q);
 int  h264r_quant_init_lists(h264r_quant* q, const int32_t* const qmatrix[12]);
 
 /* ---- context ------------------------------------------------------------------- */
-/* chroma_format_idc must be 1 and bit_depth 8 (other formats: H264R_EUNSUPPORTED). */
+/* chroma_format_idc 1 (4:2:0) or 3 (4:4:4, above) and bit_depth 8 (other formats:
+ * H264R_EUNSUPPORTED). */
 int  h264r_create(h264r_ctx** out, int device, int max_width_mbs, int max_height_mbs,
                   int chroma_format_idc, int bit_depth);
 int  h264r_destroy(h264r_ctx* ctx);
