@@ -35,6 +35,8 @@ extern "C" __global__ void k_inter_sp(h264r_batch b, int2 rows, const int* sp_fl
 extern "C" __global__ void k_derive444(h264r_batch b, int pl, h264r_mb* mbs, h264r_slice* slices, h264r_quant* quant,
                                        const uint8_t** refs, int ntab, int* err);
 extern "C" __global__ void k_untile(h264r_batch b, int2 rows, const uint8_t* recon);
+extern "C" __global__ void k_c422(h264r_batch b, int2 rows, int* err);
+extern "C" __global__ void k_c422_db(h264r_batch b, const h264r::DbInfo* dbinfo, int2 rows, int* err);
 extern "C" __global__ void k_intra_pic(h264r_batch b, int* sync, int* err, const uint16_t* lvl, int lmax, int2 rows,
                                       int gstep, uint8_t* recon, const int* pband);
 extern "C" __global__ void k_level(h264r_batch b, uint16_t* lvl, int* lvsync, int* lcount, int2 rows, int deep_cut,
@@ -131,7 +133,7 @@ struct Scratch {
 struct h264r_ctx {
     int device = 0;
     int max_w = 0, max_h = 0;
-    int fmt = 1;                          // chroma_format_idc: 1 (4:2:0) or 3 (4:4:4, run_444)
+    int fmt = 1;                          // chroma_format_idc: 1 (4:2:0), 2 (4:2:2, run_422) or 3 (4:4:4, run_444)
     // 4:4:4: one colour plane's derived batch (k_derive444) -- records, slices, quant, DPB tables --
     // and the scratch its unused 4:2:0 chroma outputs go to
     h264r_mb* d444_mbs = nullptr; size_t c444_mbs = 0;
@@ -350,7 +352,7 @@ int h264r_create(h264r_ctx** out, int device, int max_w, int max_h, int chroma_f
     if (!out || max_w <= 0 || max_h <= 0 || max_w > 1024 || max_h > 1024) return H264R_EINVAL;
     *out = nullptr;
     if (!knobs().ok) return H264R_EINVAL;            // an environment knob out of range (stderr)
-    if ((chroma_format_idc != 1 && chroma_format_idc != 3) || bit_depth != 8) return H264R_EUNSUPPORTED;
+    if (chroma_format_idc < 1 || chroma_format_idc > 3 || bit_depth != 8) return H264R_EUNSUPPORTED;
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0 || device < 0 || device >= n) return H264R_ENODEVICE;
     hipDeviceProp_t p;
@@ -404,8 +406,9 @@ int h264r_destroy(h264r_ctx* c)
     return H264R_OK;
 }
 
-// Bytes of one chroma plane of a w x h MB picture: 8 x 8 samples per MB (4:2:0) or 16 x 16 (4:4:4).
-static size_t chroma_bytes(const h264r_ctx* c, int w, int h) { return (size_t)w * h * (c->fmt == 3 ? 256 : 64); }
+// Bytes of one chroma plane of a w x h MB picture: 8 x 8 samples per MB (4:2:0), 8 x 16 (4:2:2)
+// or 16 x 16 (4:4:4).
+static size_t chroma_bytes(const h264r_ctx* c, int w, int h) { return (size_t)w * h * (c->fmt == 3 ? 256 : c->fmt == 2 ? 128 : 64); }
 
 static int ensure_slot(h264r_ctx* c, int slot, int w, int h)
 {
@@ -841,6 +844,47 @@ static int run_444(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row0, 
     return H264R_OK;
 }
 
+// 4:2:2 (chroma_format_idc 2): the luma plane by the 4:2:0 launch sequence (k_derive444 plane 0 --
+// the records without their chroma, the DPB tables' luma planes; its chroma goes to scratch),
+// then both chroma planes by k_c422 and, from the deblocking records that sequence left, k_c422_db
+// (k_chroma422.hip).  Field pictures are not on this path (k_derive444 flags them).
+static int run_422(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row0, int row1)
+{
+    const int P = b.num_pics;
+    const size_t nmb = (size_t)b.width_mbs * b.height_mbs;
+    const int ntab = b.ref_planes_stride ? P : 1;
+    int st;
+    if ((st = dev_resize(&c->d444_mbs, &c->c444_mbs, (size_t)P * nmb)) ||
+        (st = dev_resize(&c->d444_slices, &c->c444_slices, (size_t)P * b.slice_stride)) ||
+        (st = dev_resize(&c->d444_quant, &c->c444_quant, (size_t)P)) ||
+        (st = dev_resize(&c->d444_refs, &c->c444_refs, (size_t)ntab * 3 * H264R_MAX_SLOTS)) ||
+        (st = dev_resize(&c->d444_chroma, &c->c444_chroma, (size_t)P * 2 * 64 * nmb + H264R_PLANE_SLACK)))
+        return st;
+    hipLaunchKernelGGL(k_derive444, dim3(1024), dim3(256), 0, s, b, 0, c->d444_mbs, c->d444_slices, c->d444_quant,
+                       c->d444_refs, ntab, c->d_err);
+    HIP_OK(hipGetLastError());
+    h264r_batch d = b;
+    d.mbs = c->d444_mbs; d.slices = c->d444_slices; d.quant = c->d444_quant;
+    d.ref_planes = c->d444_refs;
+    d.ref_planes_stride = b.ref_planes_stride ? 3 * H264R_MAX_SLOTS : 0;
+    d.out_u = c->d444_chroma;
+    d.out_v = c->d444_chroma + (size_t)P * 64 * nmb;
+    if ((st = launch_all(c, d, s, row0, row1, c->sc))) return st;
+    const int2 rows = make_int2(row0, row1);
+    {
+        Timed t(c, 0, s);
+        hipLaunchKernelGGL(k_c422, dim3(P), dim3(512), 0, s, b, rows, c->d_err);
+        HIP_OK(hipGetLastError());
+    }
+    if (!((c->debug | knobs().debug) & H264R_DBG_NO_DEBLOCK)) {
+        Timed t(c, 2, s);
+        hipLaunchKernelGGL(k_c422_db, dim3(P), dim3(512), 0, s, b,
+                           reinterpret_cast<const h264r::DbInfo*>(c->sc.d_dbinfo), rows, c->d_err);
+        HIP_OK(hipGetLastError());
+    }
+    return H264R_OK;
+}
+
 static int run_batch(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row0, int row1)
 {
     // the scratch is shared by every launch of this context: a launch on another stream
@@ -851,6 +895,7 @@ static int run_batch(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row0
     }
     c->last_stream = s;
     if (c->fmt == 3) return run_444(c, b, s, row0, row1);
+    if (c->fmt == 2) return run_422(c, b, s, row0, row1);
     return launch_all(c, b, s, row0, row1, c->sc);
 }
 
@@ -1032,7 +1077,9 @@ int h264r_picture_end_async(h264r_ctx* c, int keep_slot)
     const size_t n = (size_t)P.pw * P.ph, ys = n * 256, cs = chroma_bytes(c, P.pw, P.ph);
     if (P.h_levels.empty()) P.h_levels.push_back(0);
     // 4:4:4: frame pictures only; a PCM MB's Cr view reads 128 entries past its block (run_444)
-    if (c->fmt == 3 && P.h_pic.structure != H264R_FRAME) return H264R_EUNSUPPORTED;
+    if (c->fmt != 1 && P.h_pic.structure != H264R_FRAME) return H264R_EUNSUPPORTED;
+    if (c->fmt == 2)                                       // SP slices are 4:2:0 only (Extended profile)
+        for (const h264r_slice& sl : P.h_slices) if (sl.slice_type == H264R_SLICE_SP) return H264R_EUNSUPPORTED;
     if (c->fmt == 3) P.h_levels.insert(P.h_levels.end(), 128, 0);
     // every referenced slot must be loaded, with a frame of this picture's size (a field
     // picture: twice its height; its entries may name either field of a slot, include/h264r.h)

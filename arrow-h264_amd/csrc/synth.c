@@ -247,9 +247,9 @@ int h264r_synth_picture(const h264r_synth_cfg* c, int index, h264r_mb* mbs, int1
         c->num_slices > c->height_mbs || c->num_refs < 0 || c->num_refs > H264R_MAX_REFS ||
         c->structure < H264R_FRAME || c->structure > H264R_BOTTOM_FIELD ||
         (c->kind != H264R_SYNTH_INTRA && c->num_refs < 1) || c->qp_min < 0 || c->qp_max > 51 ||
-        c->qp_min > c->qp_max || (c->chroma_format == 3 && c->structure != H264R_FRAME))
+        c->qp_min > c->qp_max || ((c->chroma_format == 2 || c->chroma_format == 3) && c->structure != H264R_FRAME))
         return H264R_EINVAL;
-    const int f444 = c->chroma_format == 3;
+    const int f444 = c->chroma_format == 3, f422 = c->chroma_format == 2;
     rng_t r = {c->seed * 0x100000001B3ull + (uint64_t)index * 0x9E3779B97F4A7C15ull + 1};
     int W = c->width_mbs, H = c->height_mbs, nmb = W * H;
     gen_t g = {c, W * 4, mbs, mv, ref_idx};
@@ -291,7 +291,7 @@ int h264r_synth_picture(const h264r_synth_cfg* c, int index, h264r_mb* mbs, int1
             m->flags = H264R_MBF_INTRA;
             m->cbp_blks = 0xFFFF;
             uint8_t* raw = (uint8_t*)(levels + off);
-            const int npcm = f444 ? 768 : 384;            /* 4:4:4: Y, Cb, Cr 256 samples each */
+            const int npcm = f444 ? 768 : f422 ? 512 : 384;   /* Y 256, Cb / Cr 64, 128 (4:2:2), 256 (4:4:4) */
             for (int k = 0; k < npcm; ++k) raw[k] = (uint8_t)rnd(&r, 256);
             off += npcm / 2;
             continue;
@@ -405,17 +405,34 @@ int h264r_synth_picture(const h264r_synth_cfg* c, int index, h264r_mb* mbs, int1
             if (any8 && t8) blks |= (uint16_t)(0x33u << (((b8 >> 1) * 2) * 4 + (b8 & 1) * 2));
             off += 64;
         }
-        if (cbpc == 2) {
-            for (int k = 0; k < 128; ++k) levels[off + k] = (k % 16 == 0) ? 0 : gen_level(&r);
-            off += 128;
-        }
-        if (i16) {
-            for (int k = 0; k < 16; ++k) levels[off + k] = gen_level(&r);
-            off += 16;
-        }
-        if (cbpc != 0) {
-            for (int k = 0; k < 8; ++k) levels[off + k] = gen_level(&r);
-            off += 8;
+        if (f422) {
+            /* 4:2:2 (include/h264r.h): the I_16x16 DC right after the luma blocks, then chroma AC
+               (2 planes x 8 blocks x 16) and chroma DC (2 x 8, raster of the 2x4 matrix) */
+            if (i16) {
+                for (int k = 0; k < 16; ++k) levels[off + k] = gen_level(&r);
+                off += 16;
+            }
+            if (cbpc == 2) {
+                for (int k = 0; k < 256; ++k) levels[off + k] = (k % 16 == 0) ? 0 : gen_level(&r);
+                off += 256;
+            }
+            if (cbpc != 0) {
+                for (int k = 0; k < 16; ++k) levels[off + k] = gen_level(&r);
+                off += 16;
+            }
+        } else {
+            if (cbpc == 2) {
+                for (int k = 0; k < 128; ++k) levels[off + k] = (k % 16 == 0) ? 0 : gen_level(&r);
+                off += 128;
+            }
+            if (i16) {
+                for (int k = 0; k < 16; ++k) levels[off + k] = gen_level(&r);
+                off += 16;
+            }
+            if (cbpc != 0) {
+                for (int k = 0; k < 8; ++k) levels[off + k] = gen_level(&r);
+                off += 8;
+            }
         }
         /* 4:4:4: the Cb and Cr planes' luma-like blocks (the same coded 8x8 blocks, their own
            levels; decode_one_component, decoder.cc:65-79); cbp_blks stays the luma plane's
@@ -474,12 +491,13 @@ int h264r_synth_refpic(uint64_t seed, int slot, int width_mbs, int height_mbs, u
 int h264r_synth_refpic_fmt(uint64_t seed, int slot, int width_mbs, int height_mbs, int chroma_format, uint8_t* y,
                            uint8_t* u, uint8_t* v)
 {
-    if (chroma_format != 3) return h264r_synth_refpic(seed, slot, width_mbs, height_mbs, y, u, v);
+    if (chroma_format != 2 && chroma_format != 3) return h264r_synth_refpic(seed, slot, width_mbs, height_mbs, y, u, v);
     if (!y || !u || !v || width_mbs <= 0 || height_mbs <= 0) return H264R_EINVAL;
     uint64_t s = seed * 31 + (uint64_t)slot * 0x2545F4914F6CDD1Dull;
+    const int cw = chroma_format == 3 ? 16 : 8;           /* 4:2:2: half width, full height */
     texture(s, y, width_mbs * 16, height_mbs * 16, 8);
-    texture(s + 1, u, width_mbs * 16, height_mbs * 16, 8);
-    texture(s + 2, v, width_mbs * 16, height_mbs * 16, 8);
+    texture(s + 1, u, width_mbs * cw, height_mbs * 16, cw / 2);
+    texture(s + 2, v, width_mbs * cw, height_mbs * 16, cw / 2);
     return H264R_OK;
 }
 

@@ -186,10 +186,10 @@ class Decoder:
         """Decoder::deblock_filter: runs reconstruction + deblocking for the picture on
         the GPU and returns the (Y, Cb, Cr) planes."""
         W, H = self._dims
-        c = 16 if self._fmt == 3 else 8
+        cw, ch = A.chroma_mb(self._fmt)
         y = np.empty((16 * H, 16 * W), np.uint8)
-        u = np.empty((c * H, c * W), np.uint8)
-        v = np.empty((c * H, c * W), np.uint8)
+        u = np.empty((ch * H, cw * W), np.uint8)
+        v = np.empty((ch * H, cw * W), np.uint8)
         _check("h264r_picture_end", self._L.h264r_picture_end(self._h, A.ptr(y), A.ptr(u), A.ptr(v), keep_slot))
         return y, u, v
 
@@ -202,10 +202,10 @@ class Decoder:
     def wait(self):
         """h264r_picture_wait: planes of the oldest picture handed to deblock_filter_async."""
         W, H = self._waiting.pop(0)
-        c = 16 if self._fmt == 3 else 8
+        cw, ch = A.chroma_mb(self._fmt)
         y = np.empty((16 * H, 16 * W), np.uint8)
-        u = np.empty((c * H, c * W), np.uint8)
-        v = np.empty((c * H, c * W), np.uint8)
+        u = np.empty((ch * H, cw * W), np.uint8)
+        v = np.empty((ch * H, cw * W), np.uint8)
         _check("h264r_picture_wait", self._L.h264r_picture_wait(self._h, A.ptr(y), A.ptr(u), A.ptr(v)))
         return y, u, v
 

@@ -27,7 +27,18 @@ MBF_INTRA, MBF_T8x8, MBF_BYPASS = 1, 2, 4
 
 SYNTH_INTRA, SYNTH_P, SYNTH_B = 0, 1, 2
 SYNTH_MAX_LEVELS_PER_MB = 416
+SYNTH_MAX_LEVELS_PER_MB_422 = 544
 SYNTH_MAX_LEVELS_PER_MB_444 = 816
+
+
+def chroma_mb(chroma_format: int) -> tuple[int, int]:
+    """(width, height) of one MB's chroma in samples: 4:2:0 8 x 8, 4:2:2 8 x 16, 4:4:4 16 x 16."""
+    return {2: (8, 16), 3: (16, 16)}.get(int(chroma_format), (8, 8))
+
+
+def max_levels_per_mb(chroma_format: int) -> int:
+    return {2: SYNTH_MAX_LEVELS_PER_MB_422, 3: SYNTH_MAX_LEVELS_PER_MB_444}.get(int(chroma_format),
+                                                                              SYNTH_MAX_LEVELS_PER_MB)
 
 # ---- numpy dtypes of the canonical device formats ----------------------------------
 MB_DTYPE = np.dtype([

@@ -24,10 +24,10 @@ class DeviceBatch:
     def planes(self, i: int):
         """(Y, Cb, Cr) of picture i as numpy arrays (device -> host copy)."""
         W, H = self.width_mbs, self.height_mbs
-        c = 16 if self.chroma_format == 3 else 8
+        cw, ch = A.chroma_mb(self.chroma_format)
         y = self.tensors["out_y"][i].cpu().numpy().reshape(16 * H, 16 * W)
-        u = self.tensors["out_u"][i].cpu().numpy().reshape(c * H, c * W)
-        v = self.tensors["out_v"][i].cpu().numpy().reshape(c * H, c * W)
+        u = self.tensors["out_u"][i].cpu().numpy().reshape(ch * H, cw * W)
+        v = self.tensors["out_v"][i].cpu().numpy().reshape(ch * H, cw * W)
         return y, u, v
 
 
@@ -69,7 +69,8 @@ def to_device(host: dict, n: int, ref_planes_ptr: int | None, device: str = "cud
     t = {k: dev(host[k]) for k in ("mbs", "levels", "mv", "ref_idx", "slices", "pics", "quant")}
     t["out_y"] = torch.zeros((n, 256 * W * H), dtype=torch.uint8, device=device)
     fmt = host.get("chroma_format", 1)
-    cs = (256 if fmt == 3 else 64) * W * H              # 4:4:4: chroma planes of the luma size
+    cw, ch = A.chroma_mb(fmt)
+    cs = cw * ch * W * H                                # 4:2:2 / 4:4:4: larger chroma planes
     t["out_u"] = torch.zeros((n, cs), dtype=torch.uint8, device=device)
     t["out_v"] = torch.zeros((n, cs), dtype=torch.uint8, device=device)
     b = A.Batch()

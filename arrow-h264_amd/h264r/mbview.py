@@ -7,17 +7,19 @@ from . import _abi as A
 
 
 def level_count(rec, chroma_format: int = 1) -> int:
-    """int16 entries of one MB's compacted level block (include/h264r.h; 4:4:4: three
-    luma-like blocks, a PCM MB 3 x 256 samples)."""
+    """int16 entries of one MB's compacted level block (include/h264r.h; 4:2:2: 8 chroma blocks
+    and 8 DC levels per plane, a PCM MB 512 samples; 4:4:4: three luma-like blocks, a PCM MB
+    3 x 256 samples)."""
     if int(rec["mb_type"]) == A.I_PCM:
-        return 384 if chroma_format == 3 else 192
+        return {2: 256, 3: 384}.get(chroma_format, 192)
     cbpl, cbpc = int(rec["cbp"]) & 15, int(rec["cbp"]) >> 4
     if chroma_format == 3:
         return 3 * (64 * bin(cbpl).count("1") + (16 if int(rec["mb_type"]) == A.I_16x16 else 0))
+    nb = 8 if chroma_format == 2 else 4                 # chroma 4x4 blocks per plane
     n = 64 * bin(cbpl).count("1")
-    n += 128 if cbpc == 2 else 0
+    n += 32 * nb if cbpc == 2 else 0
     n += 16 if int(rec["mb_type"]) == A.I_16x16 else 0
-    n += 8 if cbpc else 0
+    n += 2 * nb if cbpc else 0
     return n
 
 

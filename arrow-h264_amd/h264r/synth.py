@@ -42,7 +42,7 @@ def picture(lib: C.CDLL, cfg: A.SynthCfg, index: int) -> Picture:
     n = W * H
     mbs = np.zeros(n, A.MB_DTYPE)
     f444 = cfg.chroma_format == 3
-    levels = np.zeros(n * (A.SYNTH_MAX_LEVELS_PER_MB_444 if f444 else A.SYNTH_MAX_LEVELS_PER_MB), np.int16)
+    levels = np.zeros(n * A.max_levels_per_mb(cfg.chroma_format), np.int16)
     mv = np.zeros((2, 4 * H, 4 * W), np.uint32)
     ref_idx = np.zeros((2, 4 * H, 4 * W), np.int8)
     slices = np.zeros(cfg.num_slices, A.SLICE_DTYPE)
@@ -61,12 +61,12 @@ def refpics(lib: C.CDLL, cfg: A.SynthCfg, nslots: int | None = None):
     """[(y, u, v)] for DPB slots 0..n-1: the frames the pictures reference (a field cfg's
     references are fields of frames of twice its height, include/h264r_synth.h)."""
     W, H = cfg.width_mbs, cfg.height_mbs * (2 if cfg.structure else 1)
-    c = 16 if cfg.chroma_format == 3 else 8          # 4:4:4: chroma planes of the luma size
+    cw, ch = A.chroma_mb(cfg.chroma_format)
     out = []
     for s in range(lib.h264r_synth_ref_frames(C.byref(cfg)) if nslots is None else nslots):
         y = np.zeros((16 * H, 16 * W), np.uint8)
-        u = np.zeros((c * H, c * W), np.uint8)
-        v = np.zeros((c * H, c * W), np.uint8)
+        u = np.zeros((ch * H, cw * W), np.uint8)
+        v = np.zeros((ch * H, cw * W), np.uint8)
         st = lib.h264r_synth_refpic_fmt(C.c_uint64(cfg.seed), s, W, H, int(cfg.chroma_format), A.ptr(y), A.ptr(u),
                                         A.ptr(v))
         if st != A.OK:

@@ -84,12 +84,15 @@ void oracle_quant_init_lists(h264r_quant* q, const int32_t* m4 /*[6][16]*/, cons
 /* --------------------------------------------- level block layout (include/h264r.h) */
 typedef struct {
     const int16_t* b8[4];   /* NULL when the 8x8 is not coded */
-    const int16_t* cac;     /* chroma AC, 128 levels, or NULL */
+    const int16_t* cac;     /* chroma AC, 2 x nb x 16 levels, or NULL */
     const int16_t* ldc;     /* I16x16 luma DC, 16 levels, or NULL */
-    const int16_t* cdc;     /* chroma DC, 8 levels, or NULL */
+    const int16_t* cdc;     /* chroma DC, 2 x nb levels, or NULL */
+    int nb;                 /* chroma 4x4 blocks per plane: 4 (4:2:0), 8 (4:2:2) */
 } levels_view;
 
-static levels_view view_levels(const h264r_mb* mb, const int16_t* pool)
+/* cf: chroma_format_idc 1 or 2 (a 4:4:4 picture reaches this code one plane at a time, as
+   4:2:0-shaped pictures, decode_444 below) */
+static levels_view view_levels(const h264r_mb* mb, const int16_t* pool, int cf)
 {
     levels_view v;
     memset(&v, 0, sizeof(v));
@@ -97,6 +100,14 @@ static levels_view view_levels(const h264r_mb* mb, const int16_t* pool)
     int cbpl = mb->cbp & 15, cbpc = mb->cbp >> 4;
     for (int k = 0; k < 4; ++k)
         if (cbpl & (1 << k)) { v.b8[k] = p; p += 64; }
+    if (cf == 2) {          /* 4:2:2 (include/h264r.h): the luma part first, then chroma AC, DC */
+        v.nb = 8;
+        if (mb->mb_type == H264R_I_16x16) { v.ldc = p; p += 16; }
+        if (cbpc == 2) { v.cac = p; p += 256; }
+        if (cbpc != 0) { v.cdc = p; p += 16; }
+        return v;
+    }
+    v.nb = 4;
     if (cbpc == 2) { v.cac = p; p += 128; }
     if (mb->mb_type == H264R_I_16x16) { v.ldc = p; p += 16; }
     if (cbpc != 0) { v.cdc = p; p += 8; }
@@ -192,9 +203,9 @@ static void bypass_block(int r[16][16], int f[16][16], int x0, int y0, int w, in
 /* TransformBypassModeFlag MBs: levels stay raw (coeff_luma_ac / coeff_chroma_ac skip
  * inverse_quantize, transform.cc:439-441,453-455; transform_luma_dc / transform_chroma_dc
  * do nothing, :827,860), DC levels at the (0,0) of their 4x4 blocks. */
-static void load_cof_bypass(const h264r_mb* mb, const int16_t* pool, int cof[3][16][16])
+static void load_cof_bypass(const h264r_mb* mb, const int16_t* pool, int cf, int cof[3][16][16])
 {
-    levels_view v = view_levels(mb, pool);
+    levels_view v = view_levels(mb, pool, cf);
     int t8 = (mb->flags & H264R_MBF_T8x8) != 0;
     if (v.ldc)
         for (int i = 0; i < 4; ++i)
@@ -216,22 +227,22 @@ static void load_cof_bypass(const h264r_mb* mb, const int16_t* pool, int cof[3][
     }
     for (int pl = 1; pl <= 2; ++pl) {
         if (v.cdc)
-            for (int i = 0; i < 2; ++i)
-                for (int j = 0; j < 2; ++j) cof[pl][i * 4][j * 4] = v.cdc[(pl - 1) * 4 + i * 2 + j];
+            for (int i = 0; i < v.nb / 2; ++i)
+                for (int j = 0; j < 2; ++j) cof[pl][i * 4][j * 4] = v.cdc[(pl - 1) * v.nb + i * 2 + j];
         if (v.cac)
-            for (int b = 0; b < 4; ++b)
+            for (int b = 0; b < v.nb; ++b)
                 for (int pos = 1; pos < 16; ++pos)
-                    cof[pl][(b / 2) * 4 + pos / 4][(b % 2) * 4 + pos % 4] = v.cac[(pl - 1) * 64 + b * 16 + pos];
+                    cof[pl][(b / 2) * 4 + pos / 4][(b % 2) * 4 + pos % 4] = v.cac[(pl - 1) * v.nb * 16 + b * 16 + pos];
     }
 }
 
 /* Coefficient push: coeff_luma_ac/coeff_chroma_ac + inverse_quantize (transform.cc:394-456),
  * transform_luma_dc (:825-856), transform_chroma_dc (:858-910). */
-static void load_cof(const h264r_mb* mb, const int16_t* pool, const h264r_quant* q, int cof[3][16][16])
+static void load_cof(const h264r_mb* mb, const int16_t* pool, const h264r_quant* q, int cf, int cof[3][16][16])
 {
     memset(cof, 0, sizeof(int) * 3 * 16 * 16);
-    if (mb->flags & H264R_MBF_BYPASS) { load_cof_bypass(mb, pool, cof); return; }
-    levels_view v = view_levels(mb, pool);
+    if (mb->flags & H264R_MBF_BYPASS) { load_cof_bypass(mb, pool, cf, cof); return; }
+    levels_view v = view_levels(mb, pool, cf);
     int inter = (mb->flags & H264R_MBF_INTRA) ? 0 : 1;
     int t8 = (mb->flags & H264R_MBF_T8x8) != 0;
     int i16 = mb->mb_type == H264R_I_16x16;
@@ -279,7 +290,7 @@ static void load_cof(const h264r_mb* mb, const int16_t* pool, const h264r_quant*
     }
     for (int pl = 1; pl <= 2; ++pl) {
         int qP = mb->qp_scaled[pl];
-        if (v.cdc) {
+        if (v.cdc && v.nb == 4) {
             int c[2][2], f[2][2];
             int scale = q->scale4x4[inter][pl][qP % 6][0];
             for (int k = 0; k < 4; ++k) c[k / 2][k % 2] = v.cdc[(pl - 1) * 4 + k];
@@ -287,10 +298,26 @@ static void load_cof(const h264r_mb* mb, const int16_t* pool, const h264r_quant*
             for (int i = 0; i < 2; ++i)
                 for (int j = 0; j < 2; ++j)
                     cof[pl][i * 4][j * 4] = ((f[i][j] * scale) * (1 << (qP / 6))) >> 5;
+        } else if (v.cdc) {
+            /* 4:2:2: ihadamard_2x4 (transform.cc:483-513) and the dequantisation of :890-907 -- with
+               qP = qp_scaled[pl] as the reference has it, where 8.5.11.2 uses QP'c + 3 (the
+               reference's doc/bugs-jm-18.5.txt item 11 drops JM's + 3 on purpose) */
+            int c[4][2], e[4][2], f[4][2];
+            int scale = q->scale4x4[inter][pl][qP % 6][0];
+            for (int k = 0; k < 8; ++k) c[k / 2][k % 2] = v.cdc[(pl - 1) * 8 + k];
+            for (int i = 0; i < 4; ++i) { e[i][0] = c[i][0] + c[i][1]; e[i][1] = c[i][0] - c[i][1]; }
+            for (int j = 0; j < 2; ++j) {
+                int h0 = e[0][j] + e[2][j], h1 = e[0][j] - e[2][j], h2 = e[1][j] - e[3][j], h3 = e[1][j] + e[3][j];
+                f[0][j] = h0 + h3; f[1][j] = h1 + h2; f[2][j] = h1 - h2; f[3][j] = h0 - h3;
+            }
+            for (int i = 0; i < 4; ++i)
+                for (int j = 0; j < 2; ++j)
+                    cof[pl][i * 4][j * 4] = qP >= 36 ? (f[i][j] * scale) * (1 << (qP / 6 - 6))
+                                                     : (f[i][j] * scale + (1 << (5 - qP / 6))) >> (6 - qP / 6);
         }
         if (v.cac) {
-            const int16_t* blk = v.cac + (pl - 1) * 64;
-            for (int b = 0; b < 4; ++b)
+            const int16_t* blk = v.cac + (pl - 1) * v.nb * 16;
+            for (int b = 0; b < v.nb; ++b)
                 for (int pos = 1; pos < 16; ++pos) {
                     int lev = blk[b * 16 + pos];
                     if (!lev) continue;
@@ -307,6 +334,7 @@ static void load_cof(const h264r_mb* mb, const int16_t* pool, const h264r_quant*
 typedef struct {
     const oracle_picture* p;
     int wmb, hmb, W, H, Wc, Hc, W4, H4;
+    int cf, MHc;           /* chroma_format_idc (1, 2) and MbHeightC (8, 16) */
     int fld, bot;          /* a field picture (shr.field_pic_flag) and its parity (bottom_field_flag) */
     int16_t* slice_nr;     /* slice_nr per MB, -1 until decoded (reset_mbs slice_data.cc:55, mb.init :465) */
     uint8_t  (*strength_ver)[4][16];   /* mb_t::strength_ver, deblock.cc:80 */
@@ -323,7 +351,7 @@ static inline const h264r_slice* slice_of(const pstate* s, const h264r_mb* mb) {
  * (*ax,*ay) receive the absolute sample location. */
 static int get_neighbour(const pstate* s, int chroma, int addr, int ox, int oy, int* ax, int* ay)
 {
-    int maxW = chroma ? 8 : 16, maxH = chroma ? 8 : 16;
+    int maxW = chroma ? 8 : 16, maxH = chroma ? s->MHc : 16;
     int x = (addr % s->wmb) * maxW + ox, y = (addr / s->wmb) * maxH + oy;
     if (x < 0 || x >= s->wmb * maxW || y < 0 || y >= s->hmb * maxH) return -1;
     int n = (y / maxH) * s->wmb + (x / maxW);
@@ -517,7 +545,8 @@ static void pred_8x8(nbr_t* n, int mode, int pred[16][16], int xO, int yO)   /* 
 /* Intra16x16 ctor + modes (intra_prediction.cc:624-735); chroma=1: Chroma (:748-894), 4:2:0. */
 static void pred_mb(const pstate* s, int addr, int chroma, int mode, const uint8_t* img, int pitch, int pred[16][16])
 {
-    int N = chroma ? 8 : 16;
+    int N = chroma ? s->MHc : 16;         /* rows (MbHeightC); the width is 8 for chroma */
+    int NW = chroma ? 8 : 16;
     int cip = s->p->pic->constrained_intra_pred;
     nbr_t nb, *n = &nb;
     n->stride = 18;
@@ -550,7 +579,7 @@ static void pred_mb(const pstate* s, int addr, int chroma, int mode, const uint8
         if (av[0]) for (int y = 0; y < N / 2; ++y) P(n, -1, y) = img[ay[y] * pitch + ax[y]];
         if (av[2]) for (int y = N / 2; y < N; ++y) P(n, -1, y) = img[ay[y] * pitch + ax[y]];
     }
-    if (av[1]) for (int x = 0; x < N; ++x) P(n, x, -1) = img[by * pitch + bx + x];
+    if (av[1]) for (int x = 0; x < NW; ++x) P(n, x, -1) = img[by * pitch + bx + x];
 
     if (!chroma) {
         switch (mode) {
@@ -577,8 +606,8 @@ static void pred_mb(const pstate* s, int addr, int chroma, int mode, const uint8
         }
     } else {
         switch (mode) {
-        case 0: /* DC per 4x4 (intra_prediction.cc:825-849) */
-            for (int blk = 0; blk < 4; ++blk) {
+        case 0: /* DC per 4x4 (intra_prediction.cc:825-849), 2 x N/4 blocks */
+            for (int blk = 0; blk < N / 2; ++blk) {
                 int xO = (blk & 1) * 4, yO = (blk >> 1) * 4;
                 int aA, aB;
                 if ((xO == 0 && yO == 0) || (xO > 0 && yO > 0)) { aA = yO > 0 ? av[2] : av[0]; aB = av[1]; }
@@ -593,16 +622,17 @@ static void pred_mb(const pstate* s, int addr, int chroma, int mode, const uint8
                 for (int y = 0; y < 4; ++y) for (int x = 0; x < 4; ++x) pred[yO + y][xO + x] = v;
             }
             break;
-        case 1: for (int y = 0; y < 8; ++y) for (int x = 0; x < 8; ++x) pred[y][x] = P(n, -1, y); break;
-        case 2: for (int y = 0; y < 8; ++y) for (int x = 0; x < 8; ++x) pred[y][x] = P(n, x, -1); break;
-        default: {
+        case 1: for (int y = 0; y < N; ++y) for (int x = 0; x < 8; ++x) pred[y][x] = P(n, -1, y); break;
+        case 2: for (int y = 0; y < N; ++y) for (int x = 0; x < 8; ++x) pred[y][x] = P(n, x, -1); break;
+        default: {   /* plane (:871-894): xCF 0, yCF 4 when ChromaArrayType != 1 */
+            const int yCF = N == 16 ? 4 : 0;
             int H = 0, V = 0;
             for (int x = 0; x < 4; ++x) H += (x + 1) * (P(n, 4 + x, -1) - P(n, 2 - x, -1));
-            for (int y = 0; y < 4; ++y) V += (y + 1) * (P(n, -1, 4 + y) - P(n, -1, 2 - y));
-            int a = 16 * (P(n, -1, 7) + P(n, 7, -1));
-            int b = (34 * H + 32) >> 6, c = (34 * V + 32) >> 6;
-            for (int y = 0; y < 8; ++y)
-                for (int x = 0; x < 8; ++x) pred[y][x] = clip3(0, 255, (a + b * (x - 3) + c * (y - 3) + 16) >> 5);
+            for (int y = 0; y < 4 + yCF; ++y) V += (y + 1) * (P(n, -1, 4 + yCF + y) - P(n, -1, 2 + yCF - y));
+            int a = 16 * (P(n, -1, N - 1) + P(n, 7, -1));
+            int b = (34 * H + 32) >> 6, c = ((yCF ? 5 : 34) * V + 32) >> 6;
+            for (int y = 0; y < N; ++y)
+                for (int x = 0; x < 8; ++x) pred[y][x] = clip3(0, 255, (a + b * (x - 3) + c * (y - 3 - yCF) + 16) >> 5);
             break; }
         }
     }
@@ -685,17 +715,20 @@ static int inter_pred_mb(const pstate* s, int addr, int mbp[3][16][16])
                 if ((dir == 2 || dir == l) && (slot[l] < 0 || slot[l] >= H264R_MAX_SLOTS || !p->ref_planes[slot[l]][0]))
                     return H264R_EINVAL;
             for (int pl = 0; pl < 3; ++pl) {
-                int n = pl ? 2 : 4, ox = pl ? i * 2 : i * 4, oy = pl ? j * 2 : j * 4;
+                /* the 4x4 block's chroma: 2 x 2 (4:2:0) or 2 x 4 (4:2:2) samples */
+                int nw = pl ? 2 : 4, nh = pl ? s->MHc / 4 : 4, ox = pl ? i * 2 : i * 4, oy = j * nh;
                 int Wp = pl ? s->Wc : s->W, Hp = pl ? s->Hc : s->H;
-                for (int y = 0; y < n; ++y)
-                    for (int x = 0; x < n; ++x) {
+                for (int y = 0; y < nh; ++y)
+                    for (int x = 0; x < nw; ++x) {
                         int v[2] = {0, 0};
                         for (int l = 0; l < 2; ++l) {
                             if (!(dir == 2 || dir == l)) continue;
                             const uint8_t* img = p->ref_planes[slot[l]][pl] + bot[l] * Wp;
                             const int pitch = Wp << s->fld;
                             if (!pl) v[l] = luma_sample(img, Wp, pitch, Hp, (vx[l] >> 2) + x, (vy[l] >> 2) + y, vx[l] & 3, vy[l] & 3);
-                            else v[l] = chroma_sample(img, Wp, pitch, Hp, (vx[l] >> 3) + x, (vyc[l] >> 3) + y, vx[l] & 7, vyc[l] & 7);
+                            else if (s->cf == 1) v[l] = chroma_sample(img, Wp, pitch, Hp, (vx[l] >> 3) + x, (vyc[l] >> 3) + y, vx[l] & 7, vyc[l] & 7);
+                            else v[l] = chroma_sample(img, Wp, pitch, Hp, (vx[l] >> 3) + x, (vy[l] >> 2) + y, vx[l] & 7,
+                                                      (vy[l] & 3) << 1);   /* 4:2:2: yAL = mv >> 2, yFracC (mv & 3) << 1 (:381-383) */
                         }
                         int out;
                         if (dir != 2) {
@@ -731,8 +764,8 @@ static void construct(const pstate* s, int addr, int pl, int x0, int y0, int w, 
                       int use_res, int rres[16][16], int mbp[16][16])
 {
     int mbx = addr % s->wmb, mby = addr / s->wmb;
-    int N = pl ? 8 : 16, pitch = pl ? s->Wc : s->W;
-    uint8_t* img = plane_ptr(s, pl) + (mby * N) * pitch + mbx * N;
+    int NW = pl ? 8 : 16, NH = pl ? s->MHc : 16, pitch = pl ? s->Wc : s->W;
+    uint8_t* img = plane_ptr(s, pl) + (mby * NH) * pitch + mbx * NW;
     for (int y = y0; y < y0 + h; ++y)
         for (int x = x0; x < x0 + w; ++x)
             img[y * pitch + x] = (uint8_t)(use_res ? clip1(255, rres[y][x] + mbp[y][x]) : mbp[y][x]);
@@ -753,13 +786,13 @@ static void luma_block_res(const h264r_mb* mb, int cof[16][16], int rres[16][16]
 }
 
 /* inverse_transform_16x16 / inverse_transform_chroma residual (transform.cc:1018-1049) */
-static void mb_res(const h264r_mb* mb, int pl, int cof[16][16], int rres[16][16])
+static void mb_res(const pstate* s, const h264r_mb* mb, int pl, int cof[16][16], int rres[16][16])
 {
-    int n = pl ? 8 : 16;
+    int nw = pl ? 8 : 16, nh = pl ? s->MHc : 16;
     if (mb->flags & H264R_MBF_BYPASS)
-        bypass_block(cof, rres, 0, 0, n, n, pl ? mb->chroma_mode : mb->i16_mode, pl ? 2 : 0, 1);
+        bypass_block(cof, rres, 0, 0, nw, nh, pl ? mb->chroma_mode : mb->i16_mode, pl ? 2 : 0, 1);
     else
-        for (int y = 0; y < n; y += 4) for (int x = 0; x < n; x += 4) inverse_4x4(cof, rres, y, x);
+        for (int y = 0; y < nh; y += 4) for (int x = 0; x < nw; x += 4) inverse_4x4(cof, rres, y, x);
 }
 
 /* ------------------------------------------------------- SP slices (transform.cc:1098-1300) */
@@ -828,7 +861,7 @@ static void sp_mb(const pstate* s, int addr, const h264r_mb* mb, int cof[3][16][
             }
         construct(s, addr, 0, 0, 0, 16, 16, 0, rres, mbp[0]);      /* the reconstruction itself */
     }
-    levels_view v = view_levels(mb, s->p->levels);
+    levels_view v = view_levels(mb, s->p->levels, 1);
     for (int pl = 1; pl <= 2; ++pl) {
         const int qp = mb->qp_c[pl - 1], qs = sl->qs_c[pl - 1];     /* QsC < 6 (see h264r_synth.h) */
         int (*cf)[16] = cof[pl];
@@ -892,11 +925,11 @@ static int decode_mb(pstate* s, int addr)
         for (int y = 0; y < 16; ++y) for (int x = 0; x < 16; ++x)
             p->out[0][(mby * 16 + y) * s->W + mbx * 16 + x] = raw[y * 16 + x];
         for (int k = 0; k < 2; ++k)
-            for (int y = 0; y < 8; ++y) for (int x = 0; x < 8; ++x)
-                p->out[1 + k][(mby * 8 + y) * s->Wc + mbx * 8 + x] = raw[256 + k * 64 + y * 8 + x];
+            for (int y = 0; y < s->MHc; ++y) for (int x = 0; x < 8; ++x)
+                p->out[1 + k][(mby * s->MHc + y) * s->Wc + mbx * 8 + x] = raw[256 + k * 8 * s->MHc + y * 8 + x];
         return 0;
     }
-    load_cof(mb, p->levels, p->quant, cof);
+    load_cof(mb, p->levels, p->quant, s->cf, cof);
     int cbpl = mb->cbp & 15, cbpc = mb->cbp >> 4;
 
     if (mb->mb_type == H264R_I_4x4 || mb->mb_type == H264R_I_8x8 || mb->mb_type == H264R_I_16x16) {
@@ -923,7 +956,7 @@ static int decode_mb(pstate* s, int addr)
                 construct(s, addr, 0, ioff, joff, 8, 8, coded, rres[0], mbp[0]);
             } else {
                 pred_mb(s, addr, 0, mb->i16_mode, img, s->W, mbp[0]);
-                mb_res(mb, 0, cof[0], rres[0]);
+                mb_res(s, mb, 0, cof[0], rres[0]);
                 construct(s, addr, 0, 0, 0, 16, 16, 1, rres[0], mbp[0]);
             }
         }
@@ -931,8 +964,8 @@ static int decode_mb(pstate* s, int addr)
             pred_mb(s, addr, 1, mb->chroma_mode, p->out[pl], s->Wc, mbp[pl]);
         }
         for (int pl = 1; pl <= 2; ++pl) {                  /* inverse_transform_chroma :1033-1049 */
-            mb_res(mb, pl, cof[pl], rres[pl]);
-            construct(s, addr, pl, 0, 0, 8, 8, 1, rres[pl], mbp[pl]);
+            mb_res(s, mb, pl, cof[pl], rres[pl]);
+            construct(s, addr, pl, 0, 0, 8, s->MHc, 1, rres[pl], mbp[pl]);
         }
         return 0;
     }
@@ -941,6 +974,7 @@ static int decode_mb(pstate* s, int addr)
     if (st) return st;
     if (slice_of(s, mb)->slice_type == H264R_SLICE_SP) {          /* decoder.cc:256-257 */
         if (mb->flags & H264R_MBF_T8x8) return H264R_EUNSUPPORTED;  /* no 8x8 transform in SP (Extended) */
+        if (s->cf != 1) return H264R_EUNSUPPORTED;                  /* nor 4:2:2 (Extended is 4:2:0) */
         sp_mb(s, addr, mb, cof, mbp);
         return 0;
     }
@@ -964,9 +998,9 @@ static int decode_mb(pstate* s, int addr)
     } else construct(s, addr, 0, 0, 0, 16, 16, 0, rres[0], mbp[0]);
     for (int pl = 1; pl <= 2; ++pl) {
         if (cbpc) {
-            mb_res(mb, pl, cof[pl], rres[pl]);
-            construct(s, addr, pl, 0, 0, 8, 8, 1, rres[pl], mbp[pl]);
-        } else construct(s, addr, pl, 0, 0, 8, 8, 0, rres[pl], mbp[pl]);
+            mb_res(s, mb, pl, cof[pl], rres[pl]);
+            construct(s, addr, pl, 0, 0, 8, s->MHc, 1, rres[pl], mbp[pl]);
+        } else construct(s, addr, pl, 0, 0, 8, s->MHc, 0, rres[pl], mbp[pl]);
     }
     return 0;
 }
@@ -1058,7 +1092,8 @@ static void strength(pstate* s, int addr)
         for (int e = 1; e < 4; ++e) s->fver[addr][c][e] = s->fhor[addr][c][e] = 1;
     }
     if (q->flags & H264R_MBF_T8x8) s->fver[addr][0][1] = s->fver[addr][0][3] = s->fhor[addr][0][1] = s->fhor[addr][0][3] = 0;
-    s->fver[addr][1][2] = s->fver[addr][1][3] = s->fhor[addr][1][2] = s->fhor[addr][1][3] = 0;
+    s->fver[addr][1][2] = s->fver[addr][1][3] = 0;
+    if (s->cf == 1) s->fhor[addr][1][2] = s->fhor[addr][1][3] = 0;     /* 4:2:2 keeps 4 (:270-275) */
 
     int qintra = (q->flags & H264R_MBF_INTRA) != 0;
     int pskip = sl->slice_type == H264R_SLICE_P && q->mb_type == H264R_P_SKIP;
@@ -1088,7 +1123,13 @@ static void strength(pstate* s, int addr)
                 }
             }
         }
-        if (s->fhor[addr][0][e]) {                                  /* strength_horizontal */
+        /* strength_horizontal.  4:2:2: the chroma edges at rows 4 and 12 read strength_hor[1] / [3]
+           (filter_edge :433) also in an MB with transform_size_8x8_flag, whose luma edges 1 and 3
+           the reference does not filter and so never computes bS for (:280-285): it reads what the
+           mb_t slot last held.  The restatement computes them as JM and 8.7.2.1 do (the same
+           derivation at those rows); the golden fixtures keep 4:2:2 pictures free of 8x8
+           transforms, where the two agree (tests/golden/make_golden.py). */
+        if (s->fhor[addr][0][e] || (s->cf == 2 && s->fhor[addr][1][e])) {
             uint8_t* St = s->strength_hor[addr][e];
             const h264r_mb* pm = e == 0 ? mb_at(s, U) : q;
             int special = is_special(s, pm) || is_special(s, q);
@@ -1152,17 +1193,17 @@ static void filter_line(uint8_t* q, int inc, int alpha, int beta, int bS, int ch
 #undef Qq
 }
 
-/* filter_edge (deblock.cc:418-486), frame pictures, 4:2:0.  `edge` is the sample offset. */
+/* filter_edge (deblock.cc:418-486), 4:2:0 / 4:2:2.  `edge` is the sample offset. */
 static void filter_edge(pstate* s, int addr, int chroma, int pl, int vertical, int edge)
 {
     const h264r_mb* q = mb_at(s, addr);
     const h264r_slice* sl = slice_of(s, q);
     int mbx = addr % s->wmb, mby = addr / s->wmb;
     const uint8_t* St = vertical ? s->strength_ver[addr][chroma ? edge * 4 / 8 : edge / 4]
-                                 : s->strength_hor[addr][chroma ? edge * 4 / 8 : edge / 4];
-    int nE = chroma ? 8 : 16;
+                                 : s->strength_hor[addr][chroma ? edge * 4 / s->MHc : edge / 4];
+    int nE = !chroma ? 16 : vertical ? s->MHc : 8;
     int pitch = chroma ? s->Wc : s->W;
-    int x0 = mbx * nE, y0 = mby * nE;
+    int x0 = mbx * (chroma ? 8 : 16), y0 = mby * (chroma ? s->MHc : 16);
     uint8_t* img = s->p->out[pl];
     int paddr = edge == 0 ? (vertical ? addr - 1 : addr - s->wmb) : addr;
     const h264r_mb* pm = mb_at(s, paddr);
@@ -1172,7 +1213,7 @@ static void filter_edge(pstate* s, int addr, int chroma, int pl, int vertical, i
     int indexB = clip3(0, 51, qPav + sl->filter_offset_b);
     int alpha = TABLE_ALPHA[indexA], beta = TABLE_BETA[indexB];
     for (int pel = 0; pel < nE; ++pel) {
-        int bS = St[chroma ? pel << 1 : pel];
+        int bS = St[nE == 8 ? pel << 1 : pel];
         if (!bS) continue;
         uint8_t* qp = vertical ? &img[(y0 + pel) * pitch + x0 + edge] : &img[(y0 + edge) * pitch + x0 + pel];
         int inc = vertical ? 1 : pitch;
@@ -1254,14 +1295,26 @@ static int decode_444(const oracle_picture* p, int what /* 1 reconstruct, 2 debl
     return st;
 }
 
+/* The picture geometry of a 4:2:0 or 4:2:2 picture (SubHeightC 2 / 1). */
+static int init_state(pstate* s, const oracle_picture* p)
+{
+    memset(s, 0, sizeof(*s));
+    s->p = p; s->wmb = p->width_mbs; s->hmb = p->height_mbs;
+    s->cf = p->chroma_format == 2 ? 2 : 1;
+    s->MHc = s->cf == 2 ? 16 : 8;
+    s->W = s->wmb * 16; s->H = s->hmb * 16; s->Wc = s->wmb * 8; s->Hc = s->hmb * s->MHc; s->W4 = s->wmb * 4; s->H4 = s->hmb * 4;
+    s->fld = p->pic->structure != H264R_FRAME; s->bot = p->pic->structure == H264R_BOTTOM_FIELD;
+    /* field pictures are on the 4:2:0 path only (the chroma field offset :348-360 is ChromaArrayType 1) */
+    return s->fld && s->cf != 1 ? H264R_EUNSUPPORTED : 0;
+}
+
 int oracle_deblock_picture(const oracle_picture* p)
 {
     if (p->chroma_format == 3) return decode_444(p, 2);
     int n = p->width_mbs * p->height_mbs;
     pstate s;
-    s.p = p; s.wmb = p->width_mbs; s.hmb = p->height_mbs;
-    s.W = s.wmb * 16; s.H = s.hmb * 16; s.Wc = s.wmb * 8; s.Hc = s.hmb * 8; s.W4 = s.wmb * 4; s.H4 = s.hmb * 4;
-    s.fld = p->pic->structure != H264R_FRAME; s.bot = p->pic->structure == H264R_BOTTOM_FIELD;
+    int st0 = init_state(&s, p);
+    if (st0) return st0;
     int any = 0;
     for (int i = 0; i < p->pic->num_slices; ++i) any |= p->slices[i].deblock_idc != 1;
     if (!any) return 0;
@@ -1295,10 +1348,8 @@ int oracle_reconstruct_picture(const oracle_picture* p)
     if (p->chroma_format == 3) return decode_444(p, 1);
     int n = p->width_mbs * p->height_mbs;
     pstate s;
-    memset(&s, 0, sizeof(s));
-    s.p = p; s.wmb = p->width_mbs; s.hmb = p->height_mbs;
-    s.W = s.wmb * 16; s.H = s.hmb * 16; s.Wc = s.wmb * 8; s.Hc = s.hmb * 8; s.W4 = s.wmb * 4; s.H4 = s.hmb * 4;
-    s.fld = p->pic->structure != H264R_FRAME; s.bot = p->pic->structure == H264R_BOTTOM_FIELD;
+    int st0 = init_state(&s, p);
+    if (st0) return st0;
     s.slice_nr = malloc(sizeof(int16_t) * (size_t)n);
     if (!s.slice_nr) return H264R_ENOMEM;
     for (int a = 0; a < n; ++a) s.slice_nr[a] = -1;

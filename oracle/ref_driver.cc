@@ -28,6 +28,10 @@
  * plane's coefficients go through coeff_luma_* / transform_luma_dc with its ColorPlane, as the
  * parser does for ChromaArrayType 3 (interpret_residual.cc), and the references are padded
  * with the luma pads, as pad_dec_picture does for 4:4:4 (picture.cc:207-232).
+ * chroma_format 2 decodes a 4:2:2 picture (High 4:2:2, MbHeightC 16): the chroma DC levels go
+ * through coeff_chroma_dc at the scan index the reference's own inverse_scan_chroma_dc maps to
+ * their raster position (transform.cc:365-374), the AC levels of the 8 blocks per plane through
+ * coeff_chroma_ac, and the references take the 4:2:2 chroma pads (picture.cc:27-29).
  * Output: Y plane then Cb then Cr, 8-bit, unpadded.
  *
  * Timing mode (H264R_TIME_REPS=<n>): the reconstruction of the picture -- the
@@ -94,8 +98,8 @@ int main(int argc, char** argv)
     if (argc > k + 2) cfg.sp_slices = atoi(argv[k + 2]);
     if (argc > k + 3) cfg.structure = atoi(argv[k + 3]);
     if (argc > k + 4) cfg.chroma_format = atoi(argv[k + 4]);
-    const bool f444 = cfg.chroma_format == 3;
-    const int CW = f444 ? 16 : 8;                       /* chroma samples per MB side */
+    const bool f444 = cfg.chroma_format == 3, f422 = cfg.chroma_format == 2;
+    const int CW = f444 ? 16 : 8, CH = f444 || f422 ? 16 : 8;   /* chroma samples per MB: width, height */
     const bool fld = cfg.structure != H264R_FRAME;
     const PictureStructure pstruct = cfg.structure == H264R_TOP_FIELD ? TOP_FIELD
                                    : cfg.structure == H264R_BOTTOM_FIELD ? BOTTOM_FIELD : FRAME;
@@ -117,9 +121,9 @@ int main(int argc, char** argv)
     VideoParameters* vid = new VideoParameters();
     sps_t* sps = new sps_t();
     pps_t* pps = new pps_t();
-    sps->profile_idc = f444 ? 244 : 100; sps->level_idc = 51;
-    sps->chroma_format_idc = f444 ? 3 : 1; sps->ChromaArrayType = sps->chroma_format_idc;
-    sps->SubWidthC = sps->SubHeightC = f444 ? 1 : 2; sps->MbWidthC = sps->MbHeightC = CW;
+    sps->profile_idc = f444 ? 244 : f422 ? 122 : 100; sps->level_idc = 51;
+    sps->chroma_format_idc = f444 ? 3 : f422 ? 2 : 1; sps->ChromaArrayType = sps->chroma_format_idc;
+    sps->SubWidthC = f444 ? 1 : 2; sps->SubHeightC = CH == 16 ? 1 : 2; sps->MbWidthC = CW; sps->MbHeightC = CH;
     sps->BitDepthY = 8; sps->BitDepthC = 8;
     sps->frame_mbs_only_flag = !fld; sps->direct_8x8_inference_flag = 1;
     const int FH = fld ? 2 * H : H;                     /* FrameHeightInMbs */
@@ -155,21 +159,21 @@ int main(int argc, char** argv)
        references are the fields of the DPB frames, refs[2 s + bottom] */
     const int nfr = h264r_synth_ref_frames(&cfg);
     std::vector<storable_picture*> refs(fld ? 2 * nfr : nfr);
-    std::vector<uint8_t> ty(W * 16 * FH * 16), tu(W * CW * FH * CW), tv(W * CW * FH * CW);
+    std::vector<uint8_t> ty(W * 16 * FH * 16), tu(W * CW * FH * CH), tv(W * CW * FH * CH);
     for (int s = 0; s < nfr; ++s) {
         h264r_synth_refpic_fmt(cfg.seed, s, W, FH, cfg.chroma_format, ty.data(), tu.data(), tv.data());
         for (int f = 0; f < (fld ? 2 : 1); ++f) {
             storable_picture* r = new storable_picture(vid, fld ? (f ? BOTTOM_FIELD : TOP_FIELD) : FRAME,
-                                                       W * 16, FH * 16, W * CW, FH * CW, 1);
+                                                       W * 16, FH * 16, W * CW, FH * CH, 1);
             const int step = fld ? 2 : 1;                /* dpb_split_field: every second row */
             for (int y = 0; y < H * 16; ++y) for (int x = 0; x < W * 16; ++x) r->imgY[y][x] = ty[(y * step + f) * W * 16 + x];
-            for (int y = 0; y < H * CW; ++y) for (int x = 0; x < W * CW; ++x) {
+            for (int y = 0; y < H * CH; ++y) for (int x = 0; x < W * CW; ++x) {
                 r->imgUV[0][y][x] = tu[(y * step + f) * W * CW + x];
                 r->imgUV[1][y][x] = tv[(y * step + f) * W * CW + x];
             }
             pad_buf(*r->imgY, W * 16, H * 16, r->iLumaStride, MCBUF_LUMA_PAD_X, MCBUF_LUMA_PAD_Y);
-            pad_buf(*r->imgUV[0], W * CW, H * CW, r->iChromaStride, r->iChromaPadX, r->iChromaPadY);
-            pad_buf(*r->imgUV[1], W * CW, H * CW, r->iChromaStride, r->iChromaPadX, r->iChromaPadY);
+            pad_buf(*r->imgUV[0], W * CW, H * CH, r->iChromaStride, r->iChromaPadX, r->iChromaPadY);
+            pad_buf(*r->imgUV[1], W * CW, H * CH, r->iChromaStride, r->iChromaPadX, r->iChromaPadY);
             r->poc = r->frame_poc = r->top_poc = r->bottom_poc = h264r_synth_slot_poc(s) + f;
             r->is_long_term = 0; r->used_for_reference = 1;
             refs[fld ? 2 * s + f : s] = r;
@@ -178,7 +182,7 @@ int main(int argc, char** argv)
     /* RefPicList entry -> storable_picture (include/h264r.h: slot | H264R_REF_BOTTOM for fields) */
     auto ref_of = [&](int v) { return fld ? refs[2 * (v & 31) + ((v & H264R_REF_BOTTOM) ? 1 : 0)] : refs[v]; };
 
-    storable_picture* dec = new storable_picture(vid, pstruct, W * 16, FH * 16, W * CW, FH * CW, 1);
+    storable_picture* dec = new storable_picture(vid, pstruct, W * 16, FH * 16, W * CW, FH * CH, 1);
     dec->sps = sps; dec->pps = pps;
     dec->used_for_reference = 1;
     dec->poc = dec->frame_poc = pic.poc;
@@ -197,7 +201,7 @@ int main(int argc, char** argv)
         h.slice_type = c.slice_type;
         h.structure = pstruct; h.MbaffFrameFlag = 0; h.field_pic_flag = fld;
         h.bottom_field_flag = pstruct == BOTTOM_FIELD;
-        h.PicHeightInMbs = H; h.PicHeightInSamplesL = H * 16; h.PicHeightInSamplesC = H * CW;
+        h.PicHeightInMbs = H; h.PicHeightInSamplesL = H * 16; h.PicHeightInSamplesC = H * CH;
         h.PicSizeInMbs = W * H;
         h.disable_deblocking_filter_idc = c.deblock_idc;
         h.FilterOffsetA = c.filter_offset_a; h.FilterOffsetB = c.filter_offset_b;
@@ -275,6 +279,19 @@ int main(int argc, char** argv)
         }
     }
 
+    /* 4:2:2 chroma DC: the scan index of each raster position of the 2x4 matrix, from the
+       reference's own inverse_scan_chroma_dc */
+    int dc422[8] = {0};
+    if (f422) {
+        mb_t probe;
+        memset((void*)&probe, 0, sizeof(probe));
+        probe.p_Slice = sl[0];
+        for (int k = 0; k < 8; ++k) {
+            const pos_t pos = sl[0]->decoder.transform->inverse_scan_chroma_dc(&probe, k);
+            dc422[pos.y * 2 + pos.x] = k;
+        }
+    }
+
     const char* reps_env = getenv("H264R_TIME_REPS");
     const int reps = reps_env ? atoi(reps_env) : 1;
     /* every pass starts from the parser's state of mb_data (reset_mbs) */
@@ -340,17 +357,25 @@ int main(int argc, char** argv)
             const uint8_t* raw = (const uint8_t*)lv;
             for (int y = 0; y < 16; ++y) for (int x = 0; x < 16; ++x) tr->cof[0][y][x] = raw[y * 16 + x];
             for (int q = 0; q < 2; ++q)
-                for (int y = 0; y < CW; ++y) for (int x = 0; x < CW; ++x)
-                    tr->cof[1 + q][y][x] = raw[256 + q * CW * CW + y * CW + x];
+                for (int y = 0; y < CH; ++y) for (int x = 0; x < CW; ++x)
+                    tr->cof[1 + q][y][x] = raw[256 + q * CW * CH + y * CW + x];
             mb.cbp_blks[0] = 0xFFFF;
         } else {
             int cbpl = c.cbp & 15, cbpc = c.cbp >> 4;
             const int16_t* p = lv;
             const int16_t* b8p[4] = {nullptr, nullptr, nullptr, nullptr};
             for (int q = 0; q < 4; ++q) if (cbpl & (1 << q)) { b8p[q] = p; p += 64; }
-            const int16_t* cac = nullptr; if (cbpc == 2) { cac = p; p += 128; }
-            const int16_t* ldc = nullptr; if (c.mb_type == H264R_I_16x16) { ldc = p; p += 16; }
-            const int16_t* cdc = nullptr; if (cbpc) { cdc = p; p += 8; }
+            const int nb = f422 ? 8 : 4;                /* chroma 4x4 blocks per plane */
+            const int16_t *cac = nullptr, *ldc = nullptr, *cdc = nullptr;
+            if (f422) {                                 /* include/h264r.h: luma, then chroma AC, DC */
+                if (c.mb_type == H264R_I_16x16) { ldc = p; p += 16; }
+                if (cbpc == 2) { cac = p; p += 256; }
+                if (cbpc) { cdc = p; p += 16; }
+            } else {
+                if (cbpc == 2) { cac = p; p += 128; }
+                if (c.mb_type == H264R_I_16x16) { ldc = p; p += 16; }
+                if (cbpc) { cdc = p; p += 8; }
+            }
             /* a luma-like block (every plane of a 4:4:4 MB: the coded 8x8 blocks, then the I16 DC) */
             auto push_luma = [&](ColorPlane pl, const int16_t* const* b8, const int16_t* dc) {
                 if (dc) {
@@ -386,16 +411,17 @@ int main(int argc, char** argv)
             }
             if (cbpc) {
                 for (int pl = 1; pl <= 2; ++pl) {
-                    for (int q = 0; q < 4; ++q)
-                        if (cdc[(pl - 1) * 4 + q]) s.decoder.coeff_chroma_dc(&mb, (ColorPlane)pl, 0, 0, q, cdc[(pl - 1) * 4 + q]);
+                    for (int q = 0; q < nb; ++q)
+                        if (cdc[(pl - 1) * nb + q])
+                            s.decoder.coeff_chroma_dc(&mb, (ColorPlane)pl, 0, 0, f422 ? dc422[q] : q, cdc[(pl - 1) * nb + q]);
                     s.decoder.transform_chroma_dc(&mb, (ColorPlane)pl);
                 }
             }
             if (cac) {
                 for (int pl = 1; pl <= 2; ++pl)
-                    for (int b = 0; b < 4; ++b)
+                    for (int b = 0; b < nb; ++b)
                         for (int pos = 1; pos < 16; ++pos) {
-                            int v = cac[(pl - 1) * 64 + b * 16 + pos];
+                            int v = cac[(pl - 1) * nb * 16 + b * 16 + pos];
                             if (v) s.decoder.coeff_chroma_ac(&mb, (ColorPlane)pl, b % 2, b / 2, inv4[pos], v);
                         }
             }
@@ -436,7 +462,7 @@ int main(int argc, char** argv)
         fwrite(row.data(), 1, W * 16, f);
     }
     for (int q = 0; q < 2; ++q)
-        for (int y = 0; y < H * CW; ++y) {
+        for (int y = 0; y < H * CH; ++y) {
             for (int x = 0; x < W * CW; ++x) {
                 if (dec->imgUV[q][y][x] > 255) { fprintf(stderr, "sample > 255 at C%d(%d,%d)\n", q, x, y); return 6; }
                 row[x] = (uint8_t)dec->imgUV[q][y][x];

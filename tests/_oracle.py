@@ -113,9 +113,9 @@ def make_oracle_picture(p: synth.Picture, refs, quant: np.ndarray, out) -> Oracl
 
 
 def new_planes(W: int, H: int, chroma_format: int = 1):
-    c = 16 if chroma_format == 3 else 8
-    return (np.zeros((16 * H, 16 * W), np.uint8), np.zeros((c * H, c * W), np.uint8),
-            np.zeros((c * H, c * W), np.uint8))
+    cw, ch = A.chroma_mb(chroma_format)
+    return (np.zeros((16 * H, 16 * W), np.uint8), np.zeros((ch * H, cw * W), np.uint8),
+            np.zeros((ch * H, cw * W), np.uint8))
 
 
 def decode(p: synth.Picture, refs=None, stage: str = "full", quant=None):
@@ -160,10 +160,10 @@ def run_reference(cfg: A.SynthCfg, index: int, recon_only: bool = False, time_re
         if r.returncode != 0:
             raise RuntimeError(f"ref_driver failed ({r.returncode}): {r.stderr[-2000:]}")
         raw = np.fromfile(out, np.uint8)
-    c = 16 if cfg.chroma_format == 3 else 8
-    ny, nc = 256 * W * H, c * c * W * H
-    planes = (raw[:ny].reshape(16 * H, 16 * W), raw[ny:ny + nc].reshape(c * H, c * W),
-              raw[ny + nc:].reshape(c * H, c * W))
+    cw, ch = A.chroma_mb(cfg.chroma_format)
+    ny, nc = 256 * W * H, cw * ch * W * H
+    planes = (raw[:ny].reshape(16 * H, 16 * W), raw[ny:ny + nc].reshape(ch * H, cw * W),
+              raw[ny + nc:].reshape(ch * H, cw * W))
     if not time_reps:
         return planes
     line = [ln for ln in r.stderr.splitlines() if ln.startswith("ref_time ")][-1].split()

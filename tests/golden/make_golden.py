@@ -110,6 +110,25 @@ CASES = [
     ("p444_qcif_lossless", 3, 11, 9, dict(chroma_format=3, qp_min=0, qp_max=20, lossless_permille=500), [0]),
     ("b444_qcif_scaling", 4, 11, 9, dict(chroma_format=3, qm=17), [0]),
     ("p444_1080p_strip_qp", 3, 120, 6, dict(chroma_format=3, qp_min=0, qp_max=51, num_slices=2), [0]),
+    # 4:2:2 (chroma_format_idc 2, High 4:2:2): 8 x 16 chroma per MB, the 2x4 chroma DC
+    # (transform.cc:890-908, qp_scaled as the reference has it), the plane constants yCF 4
+    # (intra_prediction.cc:871-894), quarter-row chroma vectors (inter_prediction.cc:381-383), four
+    # horizontal chroma edges (deblock.cc:273-274).  No 8x8 transforms: the reference leaves the bS
+    # of a transform-8x8 MB's chroma rows 4 / 12 unset (h264r_oracle.c strength), the fixtures keep
+    # to what it defines
+    ("i422_qcif_pcm", 2, 11, 9, dict(chroma_format=2, transform8x8=0, pcm_permille=30), [0, 1]),
+    ("i422_qcif_cip_highqp", 2, 11, 9, dict(chroma_format=2, transform8x8=0, constrained_intra=1, qp_min=30,
+                                            qp_max=51), [0]),
+    ("p422_qcif", 3, 11, 9, dict(chroma_format=2, num_refs=2), [0, 1]),
+    ("p422_cif_wp_pcm", 3, 22, 9, dict(chroma_format=2, wp_mode=1, num_refs=3, pcm_permille=30, intra_permille=200), [0]),
+    ("p422_qcif_cip_bigmv", 3, 11, 9, dict(chroma_format=2, constrained_intra=1, intra_permille=400, mv_range_x=200,
+                                           mv_range_y=120), [0]),
+    ("b422_qcif_implicit", 4, 11, 9, dict(chroma_format=2, transform8x8=0, num_refs=3), [0, 1]),
+    ("b422_cif_explicit_3slices_idc2", 4, 22, 9, dict(chroma_format=2, transform8x8=0, wp_mode=1, num_refs=4,
+                                                     num_slices=3, deblock_idc=2), [0]),
+    ("p422_qcif_lossless", 3, 11, 9, dict(chroma_format=2, qp_min=0, qp_max=20, lossless_permille=500), [0]),
+    ("b422_qcif_scaling", 4, 11, 9, dict(chroma_format=2, transform8x8=0, qm=18), [0]),
+    ("p422_1080p_strip_qp", 3, 120, 6, dict(chroma_format=2, qp_min=0, qp_max=51, num_slices=2), [0]),
 ]
 
 

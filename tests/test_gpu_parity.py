@@ -48,19 +48,28 @@ def dec444(L):
     d.close()
 
 
-def first_diff(a, b, n):
+@pytest.fixture(scope="module")
+def dec422(L):
+    """A 4:2:2 context (chroma_format_idc 2): the luma pass, then k_c422 / k_c422_db."""
+    d = h264r.Decoder(0, 240, 135, chroma_format=2)
+    yield d
+    d.close()
+
+
+def first_diff(a, b, n, nh=None):
     bad = np.argwhere(a != b)
     if not len(bad):
         return None
     y, x = bad[0]
-    return f"{len(bad)} samples differ, first at (x={x}, y={y}) MB ({x // n}, {y // n}): gpu={a[y, x]} want={b[y, x]}"
+    return (f"{len(bad)} samples differ, first at (x={x}, y={y}) MB ({x // n}, {y // (nh or n)}): "
+            f"gpu={a[y, x]} want={b[y, x]}")
 
 
 @pytest.mark.parametrize("fx", GOLDEN, ids=[f"{f['name']}[{f['index']}]" for f in GOLDEN])
-def test_gpu_matches_reference_fixture(L, dec, dec444, fx):
+def test_gpu_matches_reference_fixture(L, dec, dec444, dec422, fx):
     cfg = A.SynthCfg.from_dict(fx["cfg"])
-    if cfg.chroma_format == 3:
-        dec = dec444
+    if cfg.chroma_format in (2, 3):
+        dec = dec444 if cfg.chroma_format == 3 else dec422
     p = synth.picture(L, cfg, fx["index"])
     assert synth.input_digest(p) == fx["input_md5"]
     refs = synth.refpics(L, cfg)
@@ -79,11 +88,11 @@ def test_gpu_matches_reference_fixture(L, dec, dec444, fx):
         ref_out = O.decode(p, refs, quant=oquant)
         msgs = []
         for i, k in enumerate("YUV"):
-            n = 16 if i == 0 or cfg.chroma_format == 3 else 8
-            d = first_diff(rec[i], ref_rec[i], n)
+            n, nh = (16, 16) if i == 0 else A.chroma_mb(cfg.chroma_format)
+            d = first_diff(rec[i], ref_rec[i], n, nh)
             if d:
                 msgs.append(f"recon {k}: {d}")
-            d = first_diff(out[i], ref_out[i], n)
+            d = first_diff(out[i], ref_out[i], n, nh)
             if d:
                 msgs.append(f"final {k}: {d}")
         pytest.fail("; ".join(msgs) or "md5 mismatch")
