@@ -35,7 +35,8 @@ extern "C" __global__ void k_inter_sp(h264r_batch b, int2 rows, const int* sp_fl
 extern "C" __global__ void k_derive444(h264r_batch b, int pl, h264r_mb* mbs, h264r_slice* slices, h264r_quant* quant,
                                        const uint8_t** refs, int ntab, int* err);
 extern "C" __global__ void k_untile(h264r_batch b, int2 rows, const uint8_t* recon);
-extern "C" __global__ void k_c422(h264r_batch b, int2 rows, int* err);
+extern "C" __global__ void k_c422_inter(h264r_batch b, int2 rows, int* err);
+extern "C" __global__ void k_c422_intra(h264r_batch b, int2 rows, int* err);
 extern "C" __global__ void k_c422_db(h264r_batch b, const h264r::DbInfo* dbinfo, int2 rows, int* err);
 extern "C" __global__ void k_intra_pic(h264r_batch b, int* sync, int* err, const uint16_t* lvl, int lmax, int2 rows,
                                       int gstep, uint8_t* recon, const int* pband);
@@ -846,7 +847,8 @@ static int run_444(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row0, 
 
 // 4:2:2 (chroma_format_idc 2): the luma plane by the 4:2:0 launch sequence (k_derive444 plane 0 --
 // the records without their chroma, the DPB tables' luma planes; its chroma goes to scratch),
-// then both chroma planes by k_c422 and, from the deblocking records that sequence left, k_c422_db
+// then both chroma planes by k_c422_inter + k_c422_intra and, from the deblocking records that
+// sequence left, k_c422_db
 // (k_chroma422.hip).  Field pictures are not on this path (k_derive444 flags them).
 static int run_422(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row0, int row1)
 {
@@ -873,12 +875,18 @@ static int run_422(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row0, 
     const int2 rows = make_int2(row0, row1);
     {
         Timed t(c, 0, s);
-        hipLaunchKernelGGL(k_c422, dim3(P), dim3(512), 0, s, b, rows, c->d_err);
+        const int64_t mbs = (int64_t)P * (row1 - row0) * b.width_mbs;
+        hipLaunchKernelGGL(k_c422_inter, dim3((unsigned)((mbs + 3) / 4)), dim3(256), 0, s, b, rows, c->d_err);
+        HIP_OK(hipGetLastError());
+    }
+    {
+        Timed t(c, 1, s);
+        hipLaunchKernelGGL(k_c422_intra, dim3(P), dim3(1024), 0, s, b, rows, c->d_err);
         HIP_OK(hipGetLastError());
     }
     if (!((c->debug | knobs().debug) & H264R_DBG_NO_DEBLOCK)) {
         Timed t(c, 2, s);
-        hipLaunchKernelGGL(k_c422_db, dim3(P), dim3(512), 0, s, b,
+        hipLaunchKernelGGL(k_c422_db, dim3(P), dim3(1024), 0, s, b,
                            reinterpret_cast<const h264r::DbInfo*>(c->sc.d_dbinfo), rows, c->d_err);
         HIP_OK(hipGetLastError());
     }

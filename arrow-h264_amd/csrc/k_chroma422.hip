@@ -6,7 +6,8 @@
 //   1. the 4:2:0 launch sequence on the luma plane (k_derive444 plane 0: chroma stripped from the
 //      records, the chroma of that pass goes to scratch) -- it also leaves the deblocking records
 //      (DbInfo, mb_deblock.h) of every MB;
-//   2. k_c422: the reconstruction of both chroma planes, raster into the output planes;
+//   2. k_c422_inter, k_c422_intra: the reconstruction of both chroma planes, raster into the output
+//      planes -- every inter and I_PCM MB at once, then the intra MBs in a row walk;
 //   3. k_c422_db: their deblocking, in place, from those records.
 // The reference paths (R/src/codec/h264/decoder/, H/ below):
 //   prediction   IntraPrediction::Chroma intra_prediction.cc:748-894 (the plane constants
@@ -29,18 +30,18 @@
 //     slot last held.  These kernels derive them as 8.7.2.1 and JM do (intra 3; a coded 8x8
 //     block 2; else 0, the two sides sharing one 8x8 partition).
 //
-// Schedule: one workgroup of C422_WAVES waves per picture; wave w takes MB rows w, w + 8, ...
-// of the band, one MB at a time (64 lanes: lane = plane << 5 | 4x4 block << 2 | row), and
-// publishes per-row progress in LDS.  Intra prediction reads the left, upper and upper-left
-// MBs' unfiltered samples: an intra MB waits until the row above has finished its column;
-// inter and PCM MBs never wait.  Deblocking filters MB (x, y) after MB (x + 1, y - 1) (the
-// raster order's result, mb_deblock.h).  Every wait is bounded (WaitClock).
+// Schedule: an MB is one wave (64 lanes: lane = plane << 5 | 4x4 block << 2 | row).  Inter and
+// PCM MBs need nothing of the picture: one launch takes them all.  Intra prediction reads the
+// left, upper and upper-left MBs' unfiltered samples, and deblocking filters MB (x, y) after
+// MB (x + 1, y - 1) (the raster order's result, mb_deblock.h): those two walk the picture with one
+// workgroup of C422_WAVES waves per picture, wave w taking MB rows w, w + C422_WAVES, ..., with
+// per-row progress in LDS.  Every wait is bounded (WaitClock).
 #include "device_common.h"
 #include "mb_deblock.h"
 
 namespace h264r {
 
-constexpr int C422_WAVES = 8;
+constexpr int C422_WAVES = 16;
 constexpr int C422_MAX_ROWS = 1024;         // the context's max_height_mbs bound (h264r_create)
 
 struct C422Wave {
@@ -254,8 +255,29 @@ DEV void c422_mb(const h264r_batch& b, const Geom& g, int pic, int addr, int lan
     *reinterpret_cast<uint32_t*>(dst) = w;
 }
 
-// Grid: one workgroup per picture, C422_WAVES waves.  rows: the band [rows.x, rows.y).
-extern "C" __global__ __launch_bounds__(64 * C422_WAVES) void k_c422(h264r_batch b, int2 rows, int* err)
+// Inter and I_PCM MBs read nothing of the picture being decoded: k_c422_inter reconstructs them
+// all at once, one wave per MB (grid: ceil(pictures x band MBs / 4) workgroups of 4 waves).
+extern "C" __global__ __launch_bounds__(256) void k_c422_inter(h264r_batch b, int2 rows, int* err)
+{
+    __shared__ C422Wave ws[4];
+    const Geom g = make_geom(b.width_mbs, b.height_mbs);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int nband = (rows.y - rows.x) * g.wmb;
+    const int64_t t = (int64_t)blockIdx.x * 4 + wave;
+    if (t >= (int64_t)b.num_pics * nband) return;
+    const int pic = (int)(t / nband), addr = rows.x * g.wmb + (int)(t % nband);
+    const h264r_mb m = load_mb_const(b.mbs + (size_t)pic * g.nmb + addr);
+    if (mb_is_intra(m) && m.mb_type != H264R_I_PCM) return;              // k_c422_intra
+    if ((ld_const(&b.slices[(size_t)pic * b.slice_stride + m.slice]) & 255) == H264R_SLICE_SP && lane == 0)
+        __hip_atomic_store(err, 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // SP is 4:2:0 only
+    c422_mb(b, g, pic, addr, lane, ws[wave], m, 0, err);
+}
+
+// The intra MBs (not I_PCM), after k_c422_inter: one workgroup of C422_WAVES waves per picture,
+// wave w walks MB rows w, w + C422_WAVES, ... of the band [rows.x, rows.y), skipping the other
+// MBs.  Before an intra MB at column x waits for the row above to pass x (its upper and
+// upper-left neighbours), it publishes x for the row below (every MB left of it is done).
+extern "C" __global__ __launch_bounds__(64 * C422_WAVES) void k_c422_intra(h264r_batch b, int2 rows, int* err)
 {
     __shared__ int prog[C422_MAX_ROWS];
     __shared__ C422Wave ws[C422_WAVES];
@@ -264,26 +286,39 @@ extern "C" __global__ __launch_bounds__(64 * C422_WAVES) void k_c422(h264r_batch
     for (int i = threadIdx.x; i < rows.y - rows.x; i += blockDim.x) prog[i] = 0;
     __syncthreads();
     const int cip = (int)__builtin_amdgcn_readfirstlane(ld_const(&b.pics[pic].constrained_intra_pred));
+    auto publish = [&](int ri, int v) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (lane == 0) __hip_atomic_store(&prog[ri], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
     for (int row = rows.x + wave; row < rows.y; row += C422_WAVES) {
         const int ri = row - rows.x;
         WaitClock wc;
-        for (int x = 0; x < g.wmb; ++x) {
+        // the row's intra MBs 64 columns at a time: one record word per lane, a ballot
+        for (int xb = 0; xb < g.wmb; xb += 64) {
+            const int xl = xb + lane;
+            int is = 0;
+            if (xl < g.wmb) {
+                const uint32_t w0 = *reinterpret_cast<const uint32_t*>(b.mbs + (size_t)pic * g.nmb + row * g.wmb + xl);
+                is = ((w0 >> 8) & H264R_MBF_INTRA) && (w0 & 255) != H264R_I_PCM;        // flags, mb_type
+            }
+            uint64_t mask = __ballot(is);
+            while (mask) {
+            const int x = xb + __builtin_ctzll(mask);
+            mask &= mask - 1;
             const int addr = row * g.wmb + x;
             const h264r_mb m = load_mb_const(b.mbs + (size_t)pic * g.nmb + addr);
-            if (mb_is_intra(m) && ri > 0) {
-                // the MBs above and above-left: the row above has finished column x
+            publish(ri, x);
+            if (ri > 0) {
                 while (__hip_atomic_load(&prog[ri - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) <= x) {
                     if (wait_give_up(err, wc)) return;
                     __builtin_amdgcn_s_sleep(1);
                 }
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
             }
-            if ((ld_const(&b.slices[(size_t)pic * b.slice_stride + m.slice]) & 255) == H264R_SLICE_SP && lane == 0)
-                __hip_atomic_store(err, 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // SP is 4:2:0 only
             c422_mb(b, g, pic, addr, lane, ws[wave], m, cip, err);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            if (lane == 0) __hip_atomic_store(&prog[ri], x + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
         }
+        publish(ri, g.wmb);
     }
 }
 
@@ -291,6 +326,7 @@ extern "C" __global__ __launch_bounds__(64 * C422_WAVES) void k_c422(h264r_batch
 struct C422DbWave {
     uint8_t t[2][18][12];    // per plane: rows -2..15, columns -2..7 of the MB (index + 2)
     uint32_t info[DBINFO_DWORDS];
+    uint32_t rec[8];         // the MB's h264r_mb
 };
 
 // the chroma filter of filter_edge (chromaStyleFilteringFlag, deblock.cc:350-364, 380-400):
@@ -311,70 +347,40 @@ DEV void c422_filter(uint8_t* p1, uint8_t* p0, uint8_t* q0, uint8_t* q1, int bs,
     }
 }
 
-DEV void c422_db_mb(const h264r_batch& b, const Geom& g, int pic, int addr, int first_row, int lane, C422DbWave& T,
-                    const h264r_mb& m, const DbInfo* __restrict__ dbinfo)
+// The MB-row walk of the deblocking: MB x's rows 0..15 (columns 0..7), its deblocking record and
+// its MB record are prefetched two MBs ahead (nothing but MB x itself changes those rows before it
+// is filtered: the row below touches MB x only after this row has passed x + 1); its columns
+// -2, -1 are MB x - 1's final columns 6, 7, kept in the tile; rows -2, -1 come from the row above
+// after the wait.  The stores of MB x are waited for one MB later, when MB x + 1 publishes.
+struct C422DbPrefetch {
+    uint2 row;          // lanes 0..31: plane lane >> 4, row lane & 15, columns 0..7
+    uint32_t info;      // lanes 32..51: DbInfo dword lane - 32; lanes 52..59: h264r_mb dword lane - 52
+};
+
+DEV C422DbPrefetch c422_db_prefetch(const h264r_batch& b, const Geom& g, uint8_t* const (&planes)[2],
+                                    const DbInfo* __restrict__ dbinfo, int pic, int addr, int lane)
 {
+    C422DbPrefetch f;
+    f.row = make_uint2(0, 0); f.info = 0;
     const int mbx = addr % g.wmb, mby = addr / g.wmb;
-    const int Wc = g.Wc, Hc = g.hmb * 16, X = mbx * 8, Y = mby * 16;
-    uint8_t* planes[2] = {b.out_u + (size_t)pic * Wc * Hc, b.out_v + (size_t)pic * Wc * Hc};
-    if (lane < DBINFO_DWORDS)
-        T.info[lane] = reinterpret_cast<const uint32_t*>(dbinfo + (size_t)pic * g.nmb + addr)[lane];
-    if (lane < 36) {                                    // rows -2..15 of each plane
-        const int p = lane / 18, yy = lane % 18, Yr = Y + yy - 2;
-        if (Yr >= 0 && Yr < Hc) {
-            const uint8_t* src = planes[p] + (size_t)Yr * Wc + X;
-            const uint2 v = *reinterpret_cast<const uint2*>(src);
+    if (lane < 32)
+        f.row = *reinterpret_cast<const uint2*>(planes[lane >> 4] + (size_t)(mby * 16 + (lane & 15)) * g.Wc + mbx * 8);
+    else if (lane < 32 + DBINFO_DWORDS)
+        f.info = reinterpret_cast<const uint32_t*>(dbinfo + (size_t)pic * g.nmb + addr)[lane - 32];
+    else if (lane < 60)
+        f.info = reinterpret_cast<const uint32_t*>(b.mbs + (size_t)pic * g.nmb + addr)[lane - 52];
+    return f;
+}
+
+DEV void c422_put8(uint8_t* t, uint2 v)
+{
 #pragma unroll
-            for (int k = 0; k < 4; ++k) { T.t[p][yy][2 + k] = (uint8_t)(v.x >> (8 * k)); T.t[p][yy][6 + k] = (uint8_t)(v.y >> (8 * k)); }
-            if (X > 0) { T.t[p][yy][0] = src[-2]; T.t[p][yy][1] = src[-1]; }
-        }
-    }
-    wave_sync();
-    const uint8_t* bsv = reinterpret_cast<const uint8_t*>(T.info);       // DbInfo::bs
-    const uint32_t* par = T.info + 8;                                     // DbInfo::par
-    {   // vertical edges 0 and 1 (chroma columns 0, 4: luma edges 0, 2), rows 0..15
-        const int p = lane >> 5, e = (lane >> 4) & 1, yr = lane & 15;
-        const int bs = bsv[(2 * e) * 4 + (yr >> 2)];
-        if (bs) {
-            uint8_t* row = &T.t[p][yr + 2][2 + 4 * e];
-            c422_filter(row - 2, row - 1, row, row + 1, bs, par[3 + 3 * p + (e ? 2 : 0)]);
-        }
-    }
-    wave_sync();
-    {   // horizontal edges 0..3 (chroma rows 0, 4, 8, 12 -- strength_hor[e], luma column 2 x)
-        const int p = lane >> 5, e = (lane >> 3) & 3, xc = lane & 7;
-        int bs = bsv[16 + e * 4 + (xc >> 1)];
-        if ((e & 1) && (m.flags & H264R_MBF_T8x8)) {
-            // no luma edge here: 8.7.2.1 / JM (the file comment)
-            const int idc = ((const uint8_t*)(b.slices + (size_t)pic * b.slice_stride + m.slice))[1];
-            bs = idc == 1 ? 0 : mb_is_intra(m) ? 3 : ((m.cbp_blks >> (4 * e + (xc >> 1))) & 1) ? 2 : 0;
-        }
-        if (bs) {
-            uint8_t* q = &T.t[p][4 * e + 2][2 + xc];
-            constexpr int S = 12;
-            c422_filter(q - 2 * S, q - S, q, q + S, bs, par[3 + 3 * p + (e ? 2 : 1)]);
-        }
-    }
-    wave_sync();
-    if (lane < 32) {                                    // rows 0..15: columns 0..7, and -1
-        const int p = lane >> 4, yr = lane & 15;
-        uint8_t* dst = planes[p] + (size_t)(Y + yr) * Wc + X;
-        const uint8_t* s = &T.t[p][yr + 2][2];
-        uint2 v;
-        v.x = s[0] | (s[1] << 8) | (s[2] << 16) | ((uint32_t)s[3] << 24);
-        v.y = s[4] | (s[5] << 8) | (s[6] << 16) | ((uint32_t)s[7] << 24);
-        *reinterpret_cast<uint2*>(dst) = v;
-        if (X > 0) dst[-1] = s[-1];
-    } else if (lane < 34 && !first_row && Y > 0) {     // row -1 (the top edge's p0)
-        const int p = lane - 32;
-        uint8_t* dst = planes[p] + (size_t)(Y - 1) * Wc + X;
-        const uint8_t* s = &T.t[p][1][2];
-        uint2 v;
-        v.x = s[0] | (s[1] << 8) | (s[2] << 16) | ((uint32_t)s[3] << 24);
-        v.y = s[4] | (s[5] << 8) | (s[6] << 16) | ((uint32_t)s[7] << 24);
-        *reinterpret_cast<uint2*>(dst) = v;
-    }
-    wave_sync();                                        // T is reloaded by the next MB
+    for (int k = 0; k < 4; ++k) { t[k] = (uint8_t)(v.x >> (8 * k)); t[4 + k] = (uint8_t)(v.y >> (8 * k)); }
+}
+DEV uint2 c422_get8(const uint8_t* s)
+{
+    return make_uint2(s[0] | (s[1] << 8) | (s[2] << 16) | ((uint32_t)s[3] << 24),
+                      s[4] | (s[5] << 8) | (s[6] << 16) | ((uint32_t)s[7] << 24));
 }
 
 // Grid: one workgroup per picture, C422_WAVES waves; dbinfo: the luma pass's records
@@ -386,13 +392,34 @@ extern "C" __global__ __launch_bounds__(64 * C422_WAVES) void k_c422_db(h264r_ba
     __shared__ C422DbWave ws[C422_WAVES];
     const Geom g = make_geom(b.width_mbs, b.height_mbs);
     const int pic = blockIdx.x, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int Wc = g.Wc, Hc = g.hmb * 16;
+    uint8_t* const planes[2] = {b.out_u + (size_t)pic * Wc * Hc, b.out_v + (size_t)pic * Wc * Hc};
+    C422DbWave& T = ws[wave];
     for (int i = threadIdx.x; i < rows.y - rows.x; i += blockDim.x) prog[i] = 0;
     __syncthreads();
+    auto publish = [&](int ri, int v) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (lane == 0) __hip_atomic_store(&prog[ri], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
     for (int row = rows.x + wave; row < rows.y; row += C422_WAVES) {
-        const int ri = row - rows.x;
+        const int ri = row - rows.x, Y = row * 16;
         WaitClock wc;
+        C422DbPrefetch f = c422_db_prefetch(b, g, planes, dbinfo, pic, row * g.wmb, lane);
+        C422DbPrefetch f2 = f;
+        if (g.wmb > 1) f2 = c422_db_prefetch(b, g, planes, dbinfo, pic, row * g.wmb + 1, lane);
         for (int x = 0; x < g.wmb; ++x) {
-            const int addr = row * g.wmb + x;
+            const int addr = row * g.wmb + x, X = x * 8;
+            // the tile: columns -2, -1 = MB x - 1's columns 6, 7 (same lane, read before the write)
+            if (lane < 32) {
+                uint8_t* t = &T.t[lane >> 4][(lane & 15) + 2][0];
+                t[0] = t[8]; t[1] = t[9];
+                c422_put8(t + 2, f.row);
+            } else if (lane < 32 + DBINFO_DWORDS) {
+                T.info[lane - 32] = f.info;
+            } else if (lane < 60) {
+                T.rec[lane - 52] = f.info;
+            }
+            f = f2;
             if (ri > 0) {
                 const int need = min(x + 2, g.wmb);
                 while (__hip_atomic_load(&prog[ri - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < need) {
@@ -401,11 +428,58 @@ extern "C" __global__ __launch_bounds__(64 * C422_WAVES) void k_c422_db(h264r_ba
                 }
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
             }
-            const h264r_mb m = load_mb_const(b.mbs + (size_t)pic * g.nmb + addr);
-            c422_db_mb(b, g, pic, addr, ri == 0, lane, ws[wave], m, dbinfo);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            if (lane == 0) __hip_atomic_store(&prog[ri], x + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (lane >= 60 && Y > 0) {                        // rows -2, -1 of both planes, columns 0..7
+                const int q = lane - 60, p = q >> 1, k = q & 1;
+                c422_put8(&T.t[p][k][2], *reinterpret_cast<const uint2*>(planes[p] + (size_t)(Y - 2 + k) * Wc + X));
+            }
+            wave_sync();
+            h264r_mb m;
+            {
+                uint32_t* w = reinterpret_cast<uint32_t*>(&m);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) w[k] = T.rec[k];
+            }
+            const uint8_t* bsv = reinterpret_cast<const uint8_t*>(T.info);       // DbInfo::bs
+            const uint32_t* par = T.info + 8;                                     // DbInfo::par
+            {   // vertical edges 0 and 1 (chroma columns 0, 4: luma edges 0, 2), rows 0..15
+                const int p = lane >> 5, e = (lane >> 4) & 1, yr = lane & 15;
+                const int bs = bsv[(2 * e) * 4 + (yr >> 2)];
+                if (bs) {
+                    uint8_t* q = &T.t[p][yr + 2][2 + 4 * e];
+                    c422_filter(q - 2, q - 1, q, q + 1, bs, par[3 + 3 * p + (e ? 2 : 0)]);
+                }
+            }
+            wave_sync();
+            {   // horizontal edges 0..3 (chroma rows 0, 4, 8, 12 -- strength_hor[e], luma column 2 x)
+                const int p = lane >> 5, e = (lane >> 3) & 3, xc = lane & 7;
+                int bs = bsv[16 + e * 4 + (xc >> 1)];
+                if ((e & 1) && (m.flags & H264R_MBF_T8x8)) {
+                    // no luma edge here: 8.7.2.1 / JM (the file comment)
+                    const int idc = (int)((ld_const(&b.slices[(size_t)pic * b.slice_stride + m.slice]) >> 8) & 255);
+                    bs = idc == 1 ? 0 : mb_is_intra(m) ? 3 : ((m.cbp_blks >> (4 * e + (xc >> 1))) & 1) ? 2 : 0;
+                }
+                if (bs) {
+                    uint8_t* q = &T.t[p][4 * e + 2][2 + xc];
+                    constexpr int S = 12;
+                    c422_filter(q - 2 * S, q - S, q, q + S, bs, par[3 + 3 * p + (e ? 2 : 1)]);
+                }
+            }
+            wave_sync();
+            publish(ri, x);                                    // MB x - 1's stores are done
+            if (lane < 32) {                                   // rows 0..15: columns 0..7, and -1
+                const int p = lane >> 4, yr = lane & 15;
+                uint8_t* dst = planes[p] + (size_t)(Y + yr) * Wc + X;
+                const uint8_t* s = &T.t[p][yr + 2][2];
+                *reinterpret_cast<uint2*>(dst) = c422_get8(s);
+                if (X > 0) dst[-1] = s[-1];
+            } else if (lane < 34 && ri > 0 && Y > 0) {        // row -1 (the top edge's p0)
+                const int p = lane - 32;
+                *reinterpret_cast<uint2*>(planes[p] + (size_t)(Y - 1) * Wc + X) = c422_get8(&T.t[p][1][2]);
+            }
+            if (x + 2 < g.wmb) f2 = c422_db_prefetch(b, g, planes, dbinfo, pic, addr + 2, lane);
+            wave_sync();                                       // the tile is rewritten by MB x + 1
         }
+        publish(ri, g.wmb);
     }
 }
 

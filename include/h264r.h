@@ -57,7 +57,22 @@
  *   - h264r_slice    wp_weight / wp_offset [..][..][1..2] with chroma_log2_wd weight Cb / Cr;
  *   - h264r_quant    scale4x4 / scale8x8 [..][1..2] are the Cb / Cr lists (8x8 lists 8..11).
  * The library decodes a 4:4:4 batch as three launch sequences of the 4:2:0 kernels, plane pl in
- * the luma slots.  4:2:2 and > 8-bit are H264R_EUNSUPPORTED.
+ * the luma slots.
+ *
+ * 4:2:2 (a context created with chroma_format_idc 2; frame pictures, 8-bit; not SP slices): Cb / Cr
+ * carry 8 x 16 samples per MB, so
+ *   - planes         Cb / Cr are [H][W/2] (half the luma width, the luma height), in the output, the
+ *                    batch planes and the DPB slots;
+ *   - levels         the luma part first, then chroma: for b8 with (cbp & 1<<b8) 64 levels as above;
+ *                    if I_16x16, its 16 DC levels; if cbp_chroma == 2, 256 levels = Cb 8x16 then
+ *                    Cr 8x16 (4x4 blocks in raster order of the 2 x 4 block grid, raster per block,
+ *                    index 0 unused); if cbp_chroma != 0, 16 chroma DC levels (Cb then Cr, each the
+ *                    raster of the 2-wide, 4-high DC matrix); I_PCM: 512 raw samples (Y 256, Cb 128,
+ *                    Cr 128, raster);
+ *   - deblocking     a transform-8x8 MB's chroma rows 4 and 12 take the bS of 8.7.2.1, which the
+ *                    reference leaves unset.
+ * The library decodes the luma by the 4:2:0 kernels and the chroma by its own kernels (DESIGN.md
+ * section 4e).  4:0:0 and > 8-bit are H264R_EUNSUPPORTED.
  */
 #ifndef H264R_H_
 #define H264R_H_
@@ -241,7 +256,7 @@ int  h264r_quant_init_flat(h264r_quant* q);
 int  h264r_quant_init_lists(h264r_quant* q, const int32_t* const qmatrix[12]);
 
 /* ---- context ------------------------------------------------------------------- */
-/* chroma_format_idc 1 (4:2:0) or 3 (4:4:4, above) and bit_depth 8 (other formats:
+/* chroma_format_idc 1 (4:2:0), 2 (4:2:2) or 3 (4:4:4, above) and bit_depth 8 (other formats:
  * H264R_EUNSUPPORTED). */
 int  h264r_create(h264r_ctx** out, int device, int max_width_mbs, int max_height_mbs,
                   int chroma_format_idc, int bit_depth);

@@ -4,7 +4,7 @@ A 4:2:2 MB carries 8 x 16 chroma samples per plane: eight 4x4 blocks and a 2x4 D
 (transform_chroma_dc transform.cc:890-908), chroma intra prediction with the plane constants of
 yCF 4 (intra_prediction.cc:871-894), chroma vectors in quarter rows (get_block_chroma
 inter_prediction.cc:381-383) and four horizontal chroma edges per MB (deblock.cc:273-274).  The
-library decodes the luma by the 4:2:0 launch sequence and the chroma by k_c422 / k_c422_db
+library decodes the luma by the 4:2:0 launch sequence and the chroma by k_c422_inter / k_c422_intra / k_c422_db
 (k_chroma422.hip, h264r_host.hip run_422).  The oracle is pinned to the compiled reference on
 4:2:2 pictures by the golden fixtures (tests/golden/golden.json, the *422* cases, also run by
 test_gpu_parity.py); these tests add batches under every deblocking schedule -- with 8x8
@@ -90,7 +90,7 @@ def test_gpu_422_batches(L, dec, cidx, W, H, n, over):
 
 @pytest.mark.parametrize("cidx,W,H,n,over", [CASES[0], CASES[3], CASES[6], CASES[7]])
 def test_gpu_422_reconstruction(L, dec, cidx, W, H, n, over):
-    """k_c422 alone (H264R_DBG_NO_DEBLOCK) against the oracle's pre-deblocking planes."""
+    """The chroma reconstruction alone (H264R_DBG_NO_DEBLOCK) against the oracle's pre-deblocking planes."""
     cfg = synth.default_cfg(L, cidx, W, H, chroma_format=2, **over)
     _batch(dec, [synth.picture(L, cfg, i) for i in range(n)], synth.refpics(L, cfg), deblocks=(0,), stage="recon")
 
@@ -105,7 +105,7 @@ def test_gpu_422_slice_band(L, dec):
 
 def test_gpu_422_per_picture_tables(L, dec):
     """ref_planes_stride (ABI 2) on 4:2:2: every picture reads its own DPB table -- its luma
-    through k_derive444's plane-0 table, its chroma through the table itself (k_c422)."""
+    through k_derive444's plane-0 table, its chroma through the table itself (k_c422_inter)."""
     import torch
     cfg = synth.default_cfg(L, 3, 11, 9, chroma_format=2, num_refs=1)
     pics = [synth.picture(L, cfg, i) for i in range(3)]

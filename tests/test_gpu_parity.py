@@ -50,7 +50,7 @@ def dec444(L):
 
 @pytest.fixture(scope="module")
 def dec422(L):
-    """A 4:2:2 context (chroma_format_idc 2): the luma pass, then k_c422 / k_c422_db."""
+    """A 4:2:2 context (chroma_format_idc 2): the luma pass, then k_c422_inter / k_c422_intra / k_c422_db."""
     d = h264r.Decoder(0, 240, 135, chroma_format=2)
     yield d
     d.close()
