@@ -600,6 +600,7 @@ struct Output {
     int period, poc;
     int W, H, crop[4];              // its SPS's, at the time it was decoded (a later SPS may differ)
     std::vector<uint8_t> y, u, v;
+    int cf = 1;                     // chroma_format_idc (4:2:2: chroma planes of 8 x 16 per MB)
 };
 
 // ------------------------------------------------------------------ slice header
@@ -665,6 +666,7 @@ struct SliceCtx {
     int slice_nr;
     Bits& b;
     int W, H;                   // the picture's MBs (a field picture: FrameHeightInMbs / 2 rows)
+    int cf, mhc;                // chroma_format_idc (1, 2) and MbHeightC (8, 16)
     const uint8_t* zz4;         // inverse scans: frame zig-zag, or the field scans of a field picture
     const uint8_t* zz8;
     int qp;                     // slice.parser.QpY
@@ -768,7 +770,7 @@ public:
 private:
     int device_;
     h264r_ctx* ctx_ = nullptr;
-    int ctx_w_ = 0, ctx_h_ = 0, mbs_w_ = 0, mbs_h_ = 0;
+    int ctx_w_ = 0, ctx_h_ = 0, ctx_cf_ = 0, mbs_w_ = 0, mbs_h_ = 0;
     int next_id_ = 0, next_slot_ = 0;
     const Sps* psps_ = nullptr;
     const Pps* ppps_ = nullptr;
@@ -895,8 +897,9 @@ void Decoder::parse_slice_header(Bits& b, SliceHeader& h)
     require(pps_[h.pps_id].valid, "slice: pic_parameter_set_id of no PPS");
     const Pps& pps = pps_[h.pps_id];
     const Sps& sps = sps_[pps.sps_id];
-    unsupported(sps.chroma_format_idc != 1 || sps.bit_depth_y != 8 || sps.bit_depth_c != 8,
-                "picture format (4:2:0, 8-bit only)");
+    unsupported((sps.chroma_format_idc != 1 && sps.chroma_format_idc != 2) || sps.bit_depth_y != 8 ||
+                sps.bit_depth_c != 8, "picture format (4:2:0 or 4:2:2, 8-bit only)");
+    unsupported(sps.chroma_format_idc == 2 && pps.cabac, "4:2:2 with CABAC (entropy_coding_mode_flag)");
     unsupported(sps.mbaff, "MBAFF coding (mb_adaptive_frame_field_flag)");
     unsupported(sps.poc_type == 1, "pic_order_cnt_type 1");
     unsupported(h.slice_type == H264R_SLICE_SI, "SI slices");
@@ -904,6 +907,7 @@ void Decoder::parse_slice_header(Bits& b, SliceHeader& h)
     if (!sps.frame_mbs_only) {
         h.field = b.u(1);
         if (h.field) h.bottom = b.u(1);
+        unsupported(h.field && sps.chroma_format_idc == 2, "4:2:2 field pictures");
     }
     if (h.idr) h.idr_pic_id = b.ue_max(65535, "slice: idr_pic_id");
     if (sps.poc_type == 0) {
@@ -1113,19 +1117,20 @@ void Decoder::begin_picture(const SliceHeader& h)
     const int W = sps.W, H = sps.H;
     // the picture still on the GPU leaves the context (at its own size, Output::W/H) before the
     // context is replaced for a larger picture size
-    if (!ctx_ || W > ctx_w_ || H > ctx_h_) collect();
+    if (!ctx_ || W > ctx_w_ || H > ctx_h_ || sps.chroma_format_idc != ctx_cf_) collect();
     psps_ = &sps;
     ppps_ = &pps;
     first_ = h;
     in_picture_ = true;
     pps_used_.reset();
-    if (!ctx_ || W > ctx_w_ || H > ctx_h_) {
+    if (!ctx_ || W > ctx_w_ || H > ctx_h_ || sps.chroma_format_idc != ctx_cf_) {
         if (ctx_) h264r_destroy(ctx_);
         ctx_ = nullptr;
         for (auto& p : dpb_) p->slot = -1;
-        check(h264r_create(&ctx_, device_, W, H, 1, 8), "h264r_create");
+        check(h264r_create(&ctx_, device_, W, H, sps.chroma_format_idc, 8), "h264r_create");
         ctx_w_ = W;
         ctx_h_ = H;
+        ctx_cf_ = sps.chroma_format_idc;
     }
     if (W != mbs_w_ || H != mbs_h_) {            // the reference's mb_data (init_global_buffers)
         mbs_.assign((size_t)W * H, MbState());
@@ -1464,7 +1469,8 @@ void Decoder::finish_picture()
     const int cuy = psps_->frame_mbs_only ? 1 : 2;
     if (!second)
         pending_.push_back(Output{period_, cur_->poc, W, FH,
-                                  {psps_->crop[0], psps_->crop[1], cuy * psps_->crop[2], cuy * psps_->crop[3]}, {}, {}, {}});
+                                  {psps_->crop[0], psps_->crop[1], cuy * psps_->crop[2], cuy * psps_->crop[3]}, {}, {}, {},
+                                  psps_->chroma_format_idc});
     const int out_idx = second ? out_of_first_ : (int)pending_.size() - 1;
     pending_[out_idx].poc = cur_->poc;
     if (sync_) {
@@ -1584,11 +1590,11 @@ void Decoder::collect()
     if (inflight_ < 0) return;
     Output& o = pending_[inflight_];
     inflight_ = -1;
-    const size_t n = (size_t)o.W * o.H;
-    if (o.y.size() != n * 256) {
+    const size_t n = (size_t)o.W * o.H, cs = n * (o.cf == 2 ? 128 : 64);
+    if (o.y.size() != n * 256 || o.u.size() != cs) {
         o.y.assign(n * 256, 0);
-        o.u.assign(n * 64, 0);
-        o.v.assign(n * 64, 0);
+        o.u.assign(cs, 0);
+        o.v.assign(cs, 0);
     }
     if (inflight_par_ < 0) {
         check(h264r_picture_wait(ctx_, o.y.data(), o.u.data(), o.v.data()), "h264r_picture_wait");
@@ -1620,8 +1626,10 @@ void Decoder::flush_output()
         f.y = o.y.data(); f.u = o.u.data(); f.v = o.v.data();
         f.width = o.W * 16;
         f.height = o.H * 16;
+        const int sub_h = o.cf == 2 ? 1 : 2;                          // SubHeightC
         f.crop_left = 2 * o.crop[0]; f.crop_right = 2 * o.crop[1];
-        f.crop_top = 2 * o.crop[2]; f.crop_bottom = 2 * o.crop[3];
+        f.crop_top = sub_h * o.crop[2]; f.crop_bottom = sub_h * o.crop[3];
+        f.chroma_format = o.cf;
         f.poc = o.poc;
         f.period = o.period;
         if (out_) stop_ = out_(user_, &f);
@@ -1633,6 +1641,7 @@ void Decoder::flush_output()
 SliceCtx::SliceCtx(Decoder& d, const Sps& s, const Pps& p, const SliceHeader& h, int nr, Bits& bits,
                    Picture* const (*lists)[33], const int* list_n, int end)
     : D(d), sps(s), pps(p), sh(h), slice_nr(nr), b(bits), W(s.W), H(h.field ? s.H / 2 : s.H),
+      cf(s.chroma_format_idc), mhc(s.chroma_format_idc == 2 ? 16 : 8),
       zz4(h.field ? FIELD_SCAN4X4 : ZZ4), zz8(h.field ? FIELD_SCAN8X8 : ZZ8), qp(h.qp), list_(lists), list_n_(list_n),
       end_mb(end)
 {
@@ -1689,11 +1698,11 @@ void SliceCtx::update_qp(int q)
 // callers' slice_nr checks); ax, ay = absolute sample position
 MbState* SliceCtx::nb_mb(bool chroma, int xN, int yN, int& ax, int& ay)
 {
-    const int mw = chroma ? 8 : 16;
+    const int mw = chroma ? 8 : 16, mh = chroma ? mhc : 16;
     ax = mbx * mw + xN;
-    ay = mby * mw + yN;
-    if (ax < 0 || ax >= W * mw || ay < 0 || ay >= H * mw) return nullptr;
-    MbState* m = &D.mbs_[(size_t)(ay / mw) * W + ax / mw];
+    ay = mby * mh + yN;
+    if (ax < 0 || ax >= W * mw || ay < 0 || ay >= H * mh) return nullptr;
+    MbState* m = &D.mbs_[(size_t)(ay / mh) * W + ax / mw];
     return m->slice_nr == slice_nr ? m : nullptr;
 }
 
@@ -1794,7 +1803,7 @@ void SliceCtx::macroblock()
         for (int y = 0; y < 16; ++y)
             for (int x = 0; x < 16; ++x) cof[0][y][x] = b.u(8);
         for (int c = 1; c <= 2; ++c)
-            for (int y = 0; y < 8; ++y)
+            for (int y = 0; y < mhc; ++y)
                 for (int x = 0; x < 8; ++x) cof[c][y][x] = b.u(8);
         if (cab) cab->init_engine(b);
         stage();
@@ -2281,12 +2290,12 @@ void SliceCtx::inter_pred()
 int SliceCtx::nnz_pred(int pl, int i, int j)
 {
     const bool chroma = pl != 0;
-    const int mw = chroma ? 8 : 16;
+    const int mw = chroma ? 8 : 16, mh = chroma ? mhc : 16;
     int xa, ya, xb, yb;
     MbState* A = nb_mb(chroma, i - 1, j, xa, ya);
     MbState* Bm = nb_mb(chroma, i, j - 1, xb, yb);
-    int nA = A ? A->nz[pl][(ya % mw) / 4][(xa % mw) / 4] : 0;
-    int nB = Bm ? Bm->nz[pl][(yb % mw) / 4][(xb % mw) / 4] : 0;
+    int nA = A ? A->nz[pl][(ya % mh) / 4][(xa % mw) / 4] : 0;
+    int nB = Bm ? Bm->nz[pl][(yb % mh) / 4][(xb % mw) / 4] : 0;
     int nC = nA + nB;
     if (A && Bm) nC = (nC + 1) >> 1;
     return nC;
@@ -2299,14 +2308,14 @@ int SliceCtx::block_cavlc(int pl, bool chroma, bool ac, int blk, int start, int 
     const Tables& T = tables();
     const int i = chroma ? blk % 2 : ((blk / 4) % 2) * 2 + (blk % 4) % 2;
     const int j = chroma ? blk / 2 : ((blk / 4) / 2) * 2 + (blk % 4) / 2;
-    int nC = (chroma && !ac) ? -1 : nnz_pred(pl, i * 4, j * 4);
+    int nC = (chroma && !ac) ? (cf == 2 ? -2 : -1) : nnz_pred(pl, i * 4, j * 4);
     int tc, t1;
     if (nC >= 8) {
         const int c = b.u(6);
         if (c == 3) tc = t1 = 0;
         else { tc = (c >> 2) + 1; t1 = c & 3; }
     } else {
-        const int cls = nC == -1 ? 3 : nC < 2 ? 0 : nC < 4 ? 1 : 2;
+        const int cls = nC == -1 ? 3 : nC == -2 ? 4 : nC < 2 ? 0 : nC < 4 ? 1 : 2;
         const int v = T.coeff_token[cls].read(b, "coeff_token");
         tc = v >> 2;
         t1 = v & 3;
@@ -2414,16 +2423,21 @@ void SliceCtx::residual()
             }
         }
     }
+    // chroma: 4 (4:2:0) or 8 (4:2:2) 4x4 blocks and DC coefficients per plane; the 4:2:2 DC scan
+    // (inverse_scan_chroma_dc transform.cc:365-374, the field 4x4 scan's first 8 positions) as
+    // raster indices of the 2-wide DC matrix
+    static const uint8_t DC422[8] = {0, 2, 1, 4, 6, 3, 5, 7};
+    const int nbc = cf == 2 ? 8 : 4;
     if (cbpc & 3)
         for (int c = 1; c <= 2; ++c) {
-            block(CHROMA_DC, c, true, false, 0, 0, 4, pl_, &n);
+            block(CHROMA_DC, c, true, false, 0, 0, nbc, pl_, &n);
             for (int k = 0; k < n; ++k) {
-                const int q = pl_[2 * k];
+                const int q = cf == 2 ? DC422[pl_[2 * k]] : pl_[2 * k];
                 cof[c][(q / 2) * 4][(q % 2) * 4] = pl_[2 * k + 1];
             }
         }
     for (int c = 1; c <= 2; ++c)
-        for (int blk = 0; blk < 4; ++blk) {
+        for (int blk = 0; blk < nbc; ++blk) {
             if (!(cbpc & 2)) { if (!cab) m.nz[c][blk / 2][blk % 2] = 0; continue; }
             block(CHROMA_AC, c, true, true, blk, 1, 15, pl_, &n);
             for (int k = 0; k < n; ++k) {
@@ -2722,13 +2736,38 @@ void SliceCtx::stage()
     std::vector<int16_t>& lv = st.levels;
     lv.clear();
     if (m.mb_type == H264R_I_PCM) {
-        lv.resize(192);
+        lv.resize(128 + 8 * mhc);
         uint8_t* raw = reinterpret_cast<uint8_t*>(lv.data());
         for (int y = 0; y < 16; ++y)
             for (int x = 0; x < 16; ++x) raw[y * 16 + x] = (uint8_t)cof[0][y][x];
         for (int p = 0; p < 2; ++p)
-            for (int y = 0; y < 8; ++y)
-                for (int x = 0; x < 8; ++x) raw[256 + p * 64 + y * 8 + x] = (uint8_t)cof[1 + p][y][x];
+            for (int y = 0; y < mhc; ++y)
+                for (int x = 0; x < 8; ++x) raw[256 + p * 8 * mhc + y * 8 + x] = (uint8_t)cof[1 + p][y][x];
+    } else if (cf == 2) {
+        // the 4:2:2 level block (include/h264r.h): the luma part, then chroma AC, then DC
+        for (int b8 = 0; b8 < 4; ++b8) {
+            if (!((cbpl >> b8) & 1)) continue;
+            const int x8 = (b8 & 1) * 8, y8 = (b8 >> 1) * 8;
+            if (!m.t8) {
+                for (int k = 0; k < 4; ++k)
+                    for (int i = 0; i < 16; ++i)
+                        lv.push_back((int16_t)cof[0][y8 + (k >> 1) * 4 + i / 4][x8 + (k & 1) * 4 + i % 4]);
+                if (m.mb_type == H264R_I_16x16)
+                    for (int k = 0; k < 4; ++k) lv[lv.size() - 64 + k * 16] = 0;
+            } else {
+                for (int i = 0; i < 64; ++i) lv.push_back((int16_t)cof[0][y8 + i / 8][x8 + i % 8]);
+            }
+        }
+        if (m.mb_type == H264R_I_16x16)
+            for (int i = 0; i < 16; ++i) lv.push_back((int16_t)cof[0][(i / 4) * 4][(i % 4) * 4]);
+        if (cbpc == 2)
+            for (int p = 1; p <= 2; ++p)
+                for (int bb = 0; bb < 8; ++bb)
+                    for (int i = 0; i < 16; ++i)
+                        lv.push_back(i == 0 ? 0 : (int16_t)cof[p][(bb >> 1) * 4 + i / 4][(bb & 1) * 4 + i % 4]);
+        if (cbpc)
+            for (int p = 1; p <= 2; ++p)
+                for (int q = 0; q < 8; ++q) lv.push_back((int16_t)cof[p][(q / 2) * 4][(q % 2) * 4]);
     } else {
         for (int b8 = 0; b8 < 4; ++b8) {
             if (!((cbpl >> b8) & 1)) continue;

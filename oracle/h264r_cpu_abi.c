@@ -21,6 +21,7 @@
 
 struct h264r_ctx {
     int max_w, max_h;
+    int cf, cb;                 /* chroma_format_idc and chroma bytes per MB and plane (64, 128, 256) */
     uint8_t* slot[H264R_MAX_SLOTS][3];
     int slot_w[H264R_MAX_SLOTS], slot_h[H264R_MAX_SLOTS];
     int in_pic, pw, ph;
@@ -101,10 +102,12 @@ int h264r_create(h264r_ctx** out, int device, int max_w, int max_h, int chroma_f
 {
     (void)device;
     if (!out || max_w <= 0 || max_h <= 0) return H264R_EINVAL;
-    if (chroma_format_idc != 1 || bit_depth != 8) return H264R_EUNSUPPORTED;
+    if (chroma_format_idc < 1 || chroma_format_idc > 3 || bit_depth != 8) return H264R_EUNSUPPORTED;
     h264r_ctx* c = (h264r_ctx*)calloc(1, sizeof(h264r_ctx));
     if (!c) return H264R_ENOMEM;
     c->max_w = max_w; c->max_h = max_h;
+    c->cf = chroma_format_idc;
+    c->cb = chroma_format_idc == 3 ? 256 : chroma_format_idc == 2 ? 128 : 64;
     *out = c;
     return H264R_OK;
 }
@@ -131,7 +134,7 @@ static int ensure_slot(h264r_ctx* c, int s, int w, int h)
 {
     if (c->slot[s][0] && c->slot_w[s] == w && c->slot_h[s] == h) return H264R_OK;
     free(c->slot[s][0]);
-    size_t ys = (size_t)w * h * 256, cs = (size_t)w * h * 64;
+    size_t ys = (size_t)w * h * 256, cs = (size_t)w * h * c->cb;
     uint8_t* b = (uint8_t*)calloc(ys + 2 * cs, 1);
     if (!b) return H264R_ENOMEM;
     c->slot[s][0] = b; c->slot[s][1] = b + ys; c->slot[s][2] = b + ys + cs;
@@ -145,8 +148,8 @@ int h264r_set_ref(h264r_ctx* c, int slot, const uint8_t* y, const uint8_t* u, co
     int st = ensure_slot(c, slot, w, h);
     if (st) return st;
     memcpy(c->slot[slot][0], y, (size_t)w * h * 256);
-    memcpy(c->slot[slot][1], u, (size_t)w * h * 64);
-    memcpy(c->slot[slot][2], v, (size_t)w * h * 64);
+    memcpy(c->slot[slot][1], u, (size_t)w * h * c->cb);
+    memcpy(c->slot[slot][2], v, (size_t)w * h * c->cb);
     return H264R_OK;
 }
 
@@ -216,7 +219,7 @@ int h264r_mb_submit(h264r_ctx* c, int addr, const h264r_mb* mb, const int16_t* l
 }
 
 /* Capture record (little-endian): int32 header[8] = {'H4RC', W, H, num_slices, n_levels,
- * keep_slot, 0, 0}, then mbs, levels, mv, ref_idx, slices, pic, quant, Y, Cb, Cr. */
+ * keep_slot, chroma_format_idc, 0}, then mbs, levels, mv, ref_idx, slices, pic, quant, Y, Cb, Cr. */
 static void capture(const h264r_ctx* c, int keep, uint8_t* const out[3])
 {
     const char* path = getenv("H264R_CAPTURE");
@@ -224,7 +227,7 @@ static void capture(const h264r_ctx* c, int keep, uint8_t* const out[3])
     FILE* f = fopen(path, "ab");
     if (!f) return;
     const size_t n = (size_t)c->pw * c->ph;
-    int32_t hdr[8] = {0x43523448, c->pw, c->ph, c->pic.num_slices, (int32_t)c->n_levels, keep, 0, 0};
+    int32_t hdr[8] = {0x43523448, c->pw, c->ph, c->pic.num_slices, (int32_t)c->n_levels, keep, c->cf, 0};
     fwrite(hdr, 4, 8, f);
     fwrite(c->mbs, sizeof(h264r_mb), n, f);
     fwrite(c->levels, 2, c->n_levels, f);
@@ -234,8 +237,8 @@ static void capture(const h264r_ctx* c, int keep, uint8_t* const out[3])
     fwrite(&c->pic, sizeof(h264r_pic), 1, f);
     fwrite(&c->quant, sizeof(h264r_quant), 1, f);
     fwrite(out[0], 1, n * 256, f);
-    fwrite(out[1], 1, n * 64, f);
-    fwrite(out[2], 1, n * 64, f);
+    fwrite(out[1], 1, n * c->cb, f);
+    fwrite(out[2], 1, n * c->cb, f);
     fclose(f);
 }
 
@@ -259,6 +262,8 @@ static int picture_end(h264r_ctx* c, uint8_t* y, uint8_t* u, uint8_t* v, int kee
         if (c->slot[s][0] && c->slot_w[s] == c->pw && c->slot_h[s] == frame_h)
             for (int k = 0; k < 3; ++k) p.ref_planes[s][k] = c->slot[s][k];
     p.out[0] = y; p.out[1] = u; p.out[2] = v;
+    p.chroma_format = c->cf;
+    if (fld && c->cf != 1) return H264R_EUNSUPPORTED;          /* field pictures: 4:2:0 only */
     int st = oracle_decode_picture(&p);
     if (st) return H264R_EINVAL;
     uint8_t* out[3] = {y, u, v};
@@ -286,11 +291,11 @@ int h264r_picture_end_async(h264r_ctx* c, int keep)
     if (c->n_async == 2) return H264R_ESTATE;
     const size_t n = (size_t)c->pw * c->ph;
     const int k = (c->async_head + c->n_async) % 2;
-    uint8_t* buf = (uint8_t*)realloc(c->async_out[k], n * 384);
+    uint8_t* buf = (uint8_t*)realloc(c->async_out[k], n * (256 + 2 * c->cb));
     if (!buf) return H264R_ENOMEM;
     c->async_out[k] = buf;
     c->async_n[k] = n;
-    int st = picture_end(c, buf, buf + n * 256, buf + n * 320, keep);
+    int st = picture_end(c, buf, buf + n * 256, buf + n * (256 + c->cb), keep);
     if (st) return st;
     ++c->n_async;
     return H264R_OK;
@@ -304,8 +309,8 @@ int h264r_picture_wait(h264r_ctx* c, uint8_t* y, uint8_t* u, uint8_t* v)
     const size_t n = c->async_n[k];
     const uint8_t* buf = c->async_out[k];
     if (y) memcpy(y, buf, n * 256);
-    if (u) memcpy(u, buf + n * 256, n * 64);
-    if (v) memcpy(v, buf + n * 320, n * 64);
+    if (u) memcpy(u, buf + n * 256, n * c->cb);
+    if (v) memcpy(v, buf + n * (256 + c->cb), n * c->cb);
     c->async_head = (k + 1) % 2;
     --c->n_async;
     return H264R_OK;

@@ -50,6 +50,9 @@
  * (the pairing test of store_picture dpb.cc:903-912) -- and a reference list entry names a
  * slot (frame) or a slot's field (slot | H264R_REF_BOTTOM), found from whichever of a frame
  * store's pictures (frame, top_field, bottom_field) the shim decoded.
+ * 4:2:2 (chroma_format_idc 2, MbHeightC 16; frame pictures): the level block takes the 4:2:2
+ * layout of include/h264r.h (luma, then chroma AC of 8 blocks per plane, then the 2x4 DC
+ * matrix -- coeff_chroma_dc left each DC level at its raster position, transform.cc:365-374).
  * Errors: a status other than H264R_OK goes through the reference's own error()
  * (ldecod.cc:33-48), its convention for fatal conditions.
  */
@@ -99,7 +102,7 @@ struct StagedMb {
 // picture and one device context are shared by all of them.
 struct Shim {
     h264r_ctx* ctx = nullptr;
-    int ctx_w = 0, ctx_h = 0;
+    int ctx_w = 0, ctx_h = 0, ctx_cf = 0;   // the context's size and chroma_format_idc
     storable_picture* pic = nullptr;          // picture being staged
     std::vector<slice_t*> slices;             // its slices, in decoding order
     std::vector<h264r_slice> slice_tab;
@@ -185,18 +188,20 @@ void begin_picture(Shim& S, slice_t& slice)
     storable_picture* pic = slice.dec_picture;
     if (S.pic == pic) return;
     const sps_t& sps = *slice.active_sps;
-    if (sps.chroma_format_idc != 1 || sps.BitDepthY != 8 || sps.BitDepthC != 8)
-        check(H264R_EUNSUPPORTED, "picture format (4:2:0, 8-bit)");
+    const int cf = sps.chroma_format_idc;
+    if ((cf != 1 && cf != 2) || sps.BitDepthY != 8 || sps.BitDepthC != 8)
+        check(H264R_EUNSUPPORTED, "picture format (4:2:0 or 4:2:2, 8-bit)");
     if (slice.header.MbaffFrameFlag) check(H264R_EUNSUPPORTED, "MBAFF frames");
+    if (cf == 2 && slice.header.field_pic_flag) check(H264R_EUNSUPPORTED, "4:2:2 field pictures");
     // the context holds frames; a field picture is PicHeightInMbs = FrameHeightInMbs / 2 rows
     const int W = sps.PicWidthInMbs, H = sps.FrameHeightInMbs, PH = slice.header.PicHeightInMbs;
-    if (!S.ctx || W > S.ctx_w || H > S.ctx_h) {
+    if (!S.ctx || W > S.ctx_w || H > S.ctx_h || cf != S.ctx_cf) {
         if (S.ctx) h264r_destroy(S.ctx);
         S.ctx = nullptr;
         S.slot_of.clear();
         const char* dev = getenv("H264R_DEVICE");
-        check(h264r_create(&S.ctx, dev ? atoi(dev) : 0, W, H, 1, 8), "h264r_create");
-        S.ctx_w = W; S.ctx_h = H;
+        check(h264r_create(&S.ctx, dev ? atoi(dev) : 0, W, H, cf, 8), "h264r_create");
+        S.ctx_w = W; S.ctx_h = H; S.ctx_cf = cf;
     }
     S.pic = pic;
     S.slices.clear();
@@ -460,12 +465,40 @@ void Decoder::decode(mb_t& mb)
     // the level block (include/h264r.h layout) from the raw levels in cof
     std::vector<int16_t>& lv = st.levels;
     lv.clear();
+    const bool f422 = slice.active_sps->chroma_format_idc == 2;
+    const int MHc = f422 ? 16 : 8, nbc = f422 ? 8 : 4;     // MbHeightC, chroma 4x4 blocks per plane
     if (mb.mb_type == I_PCM) {
-        lv.resize(192);
+        lv.resize(128 + 8 * MHc);
         uint8_t* raw = reinterpret_cast<uint8_t*>(lv.data());
         for (int y = 0; y < 16; ++y) for (int x = 0; x < 16; ++x) raw[y * 16 + x] = (uint8_t)cof[0][y][x];
         for (int p = 0; p < 2; ++p)
-            for (int y = 0; y < 8; ++y) for (int x = 0; x < 8; ++x) raw[256 + p * 64 + y * 8 + x] = (uint8_t)cof[1 + p][y][x];
+            for (int y = 0; y < MHc; ++y)
+                for (int x = 0; x < 8; ++x) raw[256 + p * 8 * MHc + y * 8 + x] = (uint8_t)cof[1 + p][y][x];
+    } else if (f422) {
+        // 4:2:2 (include/h264r.h): the luma part, then chroma AC (8 blocks per plane), then DC
+        for (int b8 = 0; b8 < 4; ++b8) {
+            if (!((cbpl >> b8) & 1)) continue;
+            const int x8 = (b8 & 1) * 8, y8 = (b8 >> 1) * 8;
+            if (!mb.transform_size_8x8_flag) {
+                for (int k = 0; k < 4; ++k)
+                    for (int i = 0; i < 16; ++i)
+                        lv.push_back((int16_t)cof[0][y8 + (k >> 1) * 4 + i / 4][x8 + (k & 1) * 4 + i % 4]);
+                if (mb.mb_type == I_16x16)
+                    for (int k = 0; k < 4; ++k) lv[lv.size() - 64 + k * 16] = 0;
+            } else {
+                for (int i = 0; i < 64; ++i) lv.push_back((int16_t)cof[0][y8 + i / 8][x8 + i % 8]);
+            }
+        }
+        if (mb.mb_type == I_16x16)
+            for (int i = 0; i < 16; ++i) lv.push_back((int16_t)cof[0][(i / 4) * 4][(i % 4) * 4]);
+        if (cbpc == 2)
+            for (int p = 1; p <= 2; ++p)
+                for (int b = 0; b < nbc; ++b)
+                    for (int i = 0; i < 16; ++i)
+                        lv.push_back(i == 0 ? 0 : (int16_t)cof[p][(b >> 1) * 4 + i / 4][(b & 1) * 4 + i % 4]);
+        if (cbpc)
+            for (int p = 1; p <= 2; ++p)
+                for (int q = 0; q < nbc; ++q) lv.push_back((int16_t)cof[p][(q / 2) * 4][(q % 2) * 4]);
     } else {
         for (int b8 = 0; b8 < 4; ++b8) {
             if (!((cbpl >> b8) & 1)) continue;
@@ -586,15 +619,16 @@ void Decoder::deblock_filter(slice_t& slice)
         for (auto it = S.slot_of.begin(); it != S.slot_of.end();)
             it = it->second.slot == keep ? S.slot_of.erase(it) : std::next(it);
     }
+    const int MHc = S.ctx_cf == 2 ? 16 : 8;                   // MbHeightC
     S.y8.resize((size_t)W * H * 256);
-    S.u8.resize((size_t)W * H * 64);
-    S.v8.resize((size_t)W * H * 64);
+    S.u8.resize((size_t)W * H * 8 * MHc);
+    S.v8.resize((size_t)W * H * 8 * MHc);
     check(h264r_picture_end(S.ctx, S.y8.data(), S.u8.data(), S.v8.data(), keep), "h264r_picture_end");
     S.slot_of.erase(pic);
     if (keep >= 0) S.slot_of[pic] = Shim::Resident{keep, pic->slice.structure, pic->poc, pic->frame_num};
     for (int y = 0; y < H * 16; ++y)
         for (int x = 0; x < W * 16; ++x) pic->imgY[y][x] = S.y8[(size_t)y * W * 16 + x];
-    for (int y = 0; y < H * 8; ++y)
+    for (int y = 0; y < H * MHc; ++y)
         for (int x = 0; x < W * 8; ++x) {
             pic->imgUV[0][y][x] = S.u8[(size_t)y * W * 8 + x];
             pic->imgUV[1][y][x] = S.v8[(size_t)y * W * 8 + x];

@@ -10,7 +10,9 @@ For every stream of tests/streams.py STREAMS:
      (oracle/_ref/ldecod_shim) under H264R_CAPTURE, check that its YUV has the same
      per-frame MD5s, and save what crossed the C ABI as <name>.cap.npz.
 
-    make -C oracle ref && python tests/golden/make_streams.py
+    make -C oracle ref && python tests/golden/make_streams.py [name ...]
+
+With names, only those streams are (re)generated; the other entries of streams.json stay.
 """
 import json
 import os
@@ -39,8 +41,14 @@ def decode(binary: str, stream: str, out: str, env=None) -> str:
 
 def main() -> None:
     os.makedirs(S.STREAM_DIR, exist_ok=True)
-    table = {}
+    only = set(sys.argv[1:])
+    unknown = only - set(S.STREAMS)
+    if unknown:
+        raise SystemExit(f"no such streams: {sorted(unknown)}")
+    table = json.load(open(S.STREAMS_JSON))["streams"] if only and os.path.exists(S.STREAMS_JSON) else {}
     for name, cfg in S.STREAMS.items():
+        if only and name not in only:
+            continue
         data = W.write_stream(S.stream_path(name), W.StreamCfg(**cfg))
         with tempfile.TemporaryDirectory() as td:
             ref_yuv, shim_yuv, cap = (os.path.join(td, f) for f in ("ref.yuv", "shim.yuv", "cap.bin"))
@@ -58,6 +66,7 @@ def main() -> None:
         table[name] = {"cfg": cfg, "bytes": len(data), "frame_md5": want,
                        "source": "oracle/_ref/ldecod (unmodified reference) per-frame MD5 of the cropped YUV"}
         print(f"{name}: {len(data)} bytes, {cfg['frames']} frames, shim == reference")
+    table = {n: table[n] for n in S.STREAMS if n in table}          # the order of STREAMS
     with open(S.STREAMS_JSON, "w") as f:
         json.dump({"streams": table}, f, indent=1)
         f.write("\n")

@@ -150,6 +150,8 @@ class StreamCfg:
                                      # first's frame; 1.0 = every frame); P fields predict from any
                                      # reference field (the first field of their own frame too)
     bottom_first: float = 0.0        # share of field pairs sent bottom field first
+    chroma_format: int = 1           # chroma_format_idc (profiles 100 / 122 / 244): 1 4:2:0, 2 4:2:2 (CAVLC:
+                                     # 8 chroma 4x4 blocks and a 2x4 DC per plane, nC -2, interpret_residual.cc:462-494)
     long_term: int = 0               # the IDR is a long-term reference (LongTermFrameIdx 0) kept for the
                                      # whole stream, and P picture `long_term` becomes a second one by
                                      # MMCO 4 + 6 (LongTermFrameIdx 1); P pictures predict from them
@@ -200,8 +202,8 @@ class Encoder:
         w.u(8, 0)                                   # constraint flags
         w.u(8, 51)                                  # level_idc (largest DPB)
         w.ue(0)                                     # seq_parameter_set_id
-        if c.profile in (100, 244):
-            w.ue(1)                                 # chroma_format_idc 4:2:0
+        if c.profile in (100, 122, 244):
+            w.ue(c.chroma_format)                   # chroma_format_idc
             w.ue(0); w.ue(0)                        # bit depths 8
             w.u(1, 1 if c.lossless else 0)          # qpprime_y_zero_transform_bypass_flag
             w.u(1, c.scaling & 1)                   # seq_scaling_matrix_present_flag
@@ -247,7 +249,7 @@ class Encoder:
         w.u(1, 1)                                   # deblocking_filter_control_present_flag
         w.u(1, c.cip)
         w.u(1, 0)                                   # redundant_pic_cnt_present_flag
-        if c.profile in (100, 244):
+        if c.profile in (100, 122, 244):
             w.u(1, c.transform8x8)
             w.u(1, 1 if c.scaling & 2 else 0)       # pic_scaling_matrix_present_flag
             if c.scaling & 2:
@@ -298,16 +300,17 @@ class Encoder:
     def _nc(self, a: int, pl: int, bx: int, by: int, s: int) -> int:
         """nC of the block at (bx, by) (4x4 units, plane pl), neighbour.cc:263-314."""
         mx, my = a % self.W, a // self.W
-        n = 4 if pl == 0 else 2
+        nw = 4 if pl == 0 else 2                        # 4x4 blocks per MB: across, down
+        nh = 4 if pl == 0 or self.c.chroma_format == 2 else 2
         def nz_of(dx, dy):
             x, y = bx + dx, by + dy
-            ox, oy = mx + (x // n if x >= 0 else -1), my + (y // n if y >= 0 else -1)
+            ox, oy = mx + (x // nw if x >= 0 else -1), my + (y // nh if y >= 0 else -1)
             if x >= 0 and y >= 0:
                 return self.mbs[a].nz[pl][y][x]
             m = self._mb_at(ox, oy, s)
             if m is None:
                 return None
-            return m.nz[pl][y % n][x % n]
+            return m.nz[pl][y % nh][x % nw]
         na, nb = nz_of(-1, 0), nz_of(0, -1)
         if na is not None and nb is not None:
             return (na + nb + 1) >> 1
@@ -409,11 +412,12 @@ class Encoder:
                         m.nz[0][by][bx] = self._block(w, self._levels(16), self._nc(a, 0, bx, by, s), 16)
                 else:
                     m.nz[0][by][bx] = 0
+        nbc = 8 if self.c.chroma_format == 2 else 4     # chroma 4x4 blocks (= DC coefficients) per plane
         if cbpc & 3:
             for _pl in (1, 2):
-                self._block(w, self._levels(4), -1, 4)
+                self._block(w, self._levels(nbc), -1 if nbc == 4 else -2, nbc)
         for pl in (1, 2):
-            for b in range(4):
+            for b in range(nbc):
                 bx, by = b % 2, b // 2
                 if cbpc & 2:
                     m.nz[pl][by][bx] = self._block(w, self._levels(15), self._nc(a, pl, bx, by, s), 15)
@@ -424,6 +428,7 @@ class Encoder:
         """The same blocks and level draws as the CAVLC path, as residual_block_cabac calls:
         an 8x8 transform block is one 64-coefficient block (interpret_residual.cc:453-456)."""
         cab = self.cab
+        assert self.c.chroma_format == 1, "CABAC streams: 4:2:0 only"
         if m.kind == I16:
             cab.block(CB.LUMA_16DC, 0, 0, self._levels(16))
         for b8 in range(4):
@@ -536,14 +541,15 @@ class Encoder:
         A, B, D = self._avail_abd(a, 0, 0, 4, s)
         if m.kind == PCM:
             m.mbt_ref = 12
+            npcm = 256 + (256 if c.chroma_format == 2 else 128)     # 2 x MbWidthC x MbHeightC chroma samples
             if cab:
                 cab.mb_type_intra(25)
-                cab.pcm([r.randint(1, 255) for _ in range(384)])
+                cab.pcm([r.randint(1, 255) for _ in range(npcm)])
             else:
                 w.ue(base + 25)
                 while not w.aligned():
                     w.u(1, 0)
-                for _ in range(384):
+                for _ in range(npcm):
                     w.u(8, r.randint(1, 255))
             m.nz = [[[16] * 4 for _ in range(4)] for _ in range(3)]
             return True

@@ -112,6 +112,18 @@ STREAMS = {
                                       field=0.7, bframes=1, num_refs=2, direct=(1,), bipred=1),
     "hp_1080i_cabac_paff": dict(width_mbs=120, height_mbs=68, frames=2, seed=505, profile=100, transform8x8=1,
                                 cabac=1, field=1.0, num_refs=2, slices=4, deblock=(0, 2), crop=(0, 0, 0, 2)),
+    # 4:2:2 (chroma_format_idc 2; High 4:2:2 / High 4:4:4 Predictive, CAVLC): 8 x 16 chroma per MB, the
+    # 2x4 chroma DC (coeff_token nC -2, total_zeros of 8), 8 chroma AC blocks per plane.  No 8x8
+    # transforms: the reference leaves the bS of a transform-8x8 MB's chroma rows 4 / 12 unset
+    # (DESIGN.md section 4e), so its output there is not defined
+    "hi422_qcif_intra_qp0_51": dict(width_mbs=11, height_mbs=9, frames=3, seed=701, profile=122, chroma_format=2,
+                                    all_intra=True, qp=(0, 51), pcm=0.05, cip=1, level_max=3),
+    "hi422_cif_ibbp_slices": dict(width_mbs=22, height_mbs=18, frames=7, seed=702, profile=122, chroma_format=2,
+                                  bframes=2, num_refs=3, bipred=2, weighted=1, slices=3, deblock=(0, 1, 2),
+                                  offsets=3, intra_in_p=0.2, pcm=0.03, chroma_qp_offset=-3,
+                                  second_chroma_qp_offset=4, crop=(1, 2, 3, 2)),
+    "hi422_qcif_lossless": dict(width_mbs=11, height_mbs=9, frames=4, seed=703, profile=244, chroma_format=2,
+                                lossless=0.5, qp=(0, 30), intra_in_p=0.4, deblock=(0, 2), offsets=4, scaling=2),
 }
 
 CAP_MAGIC = 0x43523448
@@ -183,7 +195,7 @@ def output_order(pics: list[dict]) -> list[int]:
 
 def frame_md5s(planes, cfg: dict) -> list[str]:
     """Per-frame MD5 of cropped output frames (write_out_picture + digest_by_frames)."""
-    geom = OUT.geometry(cfg["width_mbs"], cfg["height_mbs"], crop_of(cfg))
+    geom = OUT.geometry(cfg["width_mbs"], cfg["height_mbs"], crop_of(cfg), cfg.get("chroma_format", 1))
     return [hashlib.md5(OUT.frame_bytes(y, u, v, geom)).hexdigest() for (y, u, v) in planes]
 
 
@@ -194,16 +206,17 @@ def read_capture_file(path: str) -> list[dict]:
     while off < len(raw):
         hdr = np.frombuffer(raw, np.int32, 8, off)
         off += 32
-        magic, W, H, ns, nl, keep = (int(v) for v in hdr[:6])
+        magic, W, H, ns, nl, keep, cf = (int(v) for v in hdr[:7])
         assert magic == CAP_MAGIC, "capture: bad record"
         n = W * H
+        cw, ch = A.chroma_mb(cf or 1)
 
         def take(dtype, count):
             nonlocal off
             a = np.frombuffer(raw, dtype, count, off).copy()
             off += a.nbytes
             return a
-        p = dict(W=W, H=H, keep=keep)
+        p = dict(W=W, H=H, keep=keep, chroma_format=cf or 1)
         p["mbs"] = take(A.MB_DTYPE, n)
         p["levels"] = take(np.int16, nl)
         p["mv"] = take(np.uint32, 2 * 16 * n).reshape(2, 4 * H, 4 * W)
@@ -212,8 +225,8 @@ def read_capture_file(path: str) -> list[dict]:
         p["pic"] = take(A.PIC_DTYPE, 1)
         p["quant"] = take(A.QUANT_DTYPE, 1)
         y = take(np.uint8, 256 * n).reshape(16 * H, 16 * W)
-        u = take(np.uint8, 64 * n).reshape(8 * H, 8 * W)
-        v = take(np.uint8, 64 * n).reshape(8 * H, 8 * W)
+        u = take(np.uint8, cw * ch * n).reshape(ch * H, cw * W)
+        v = take(np.uint8, cw * ch * n).reshape(ch * H, cw * W)
         p["plane_md5"] = [hashlib.md5(a.tobytes()).hexdigest() for a in (y, u, v)]
         pics.append(p)
     return pics
@@ -225,7 +238,7 @@ def save_capture(path: str, pics: list[dict]) -> None:
         for k in ("mbs", "levels", "mv", "ref_idx", "slices", "pic", "quant"):
             a = p[k]
             arrs[f"{i}_{k}"] = a.view(np.uint8) if a.dtype.names else a
-        arrs[f"{i}_meta"] = np.array([p["W"], p["H"], p["keep"]], np.int32)
+        arrs[f"{i}_meta"] = np.array([p["W"], p["H"], p["keep"], p.get("chroma_format", 1)], np.int32)
         arrs[f"{i}_plane_md5"] = np.array(p["plane_md5"])
     np.savez_compressed(path, n=np.array([len(pics)]), **arrs)
 
@@ -235,8 +248,9 @@ def load_capture(path: str) -> list[dict]:
     dt = {"mbs": A.MB_DTYPE, "slices": A.SLICE_DTYPE, "pic": A.PIC_DTYPE, "quant": A.QUANT_DTYPE}
     pics = []
     for i in range(int(z["n"][0])):
-        W, H, keep = (int(v) for v in z[f"{i}_meta"])
-        p = dict(W=W, H=H, keep=keep)
+        meta = [int(v) for v in z[f"{i}_meta"]]
+        W, H, keep = meta[:3]
+        p = dict(W=W, H=H, keep=keep, chroma_format=meta[3] if len(meta) > 3 else 1)
         for k in ("mbs", "levels", "mv", "ref_idx", "slices", "pic", "quant"):
             a = z[f"{i}_{k}"]
             p[k] = a.view(dt[k]) if k in dt else a

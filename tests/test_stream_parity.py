@@ -95,10 +95,11 @@ def test_oracle_replay_of_captures_matches_reference(name):
 
     def dec(p):
         W, H = p["W"], p["H"]
-        out = O.new_planes(W, H)
+        out = O.new_planes(W, H, p["chroma_format"])
         fld = S.structure(p) != A.FRAME
         o = O.OraclePicture()
         o.width_mbs, o.height_mbs = W, H
+        o.chroma_format = p["chroma_format"]
         o.mbs, o.levels = A.ptr(p["mbs"]).value, A.ptr(p["levels"]).value
         o.mv, o.ref_idx = A.ptr(p["mv"]).value, A.ptr(p["ref_idx"]).value
         o.slices, o.pic, o.quant = A.ptr(p["slices"]).value, A.ptr(p["pic"]).value, A.ptr(p["quant"]).value
@@ -152,7 +153,7 @@ def test_gpu_replay_of_captures_matches_reference(name, flag):
     cfg = S.STREAMS[name]
     pics = S.load_capture(S.capture_path(name))
     W, H = cfg["width_mbs"], cfg["height_mbs"]
-    with h264r.Decoder(0, W, H) as dec:
+    with h264r.Decoder(0, W, H, chroma_format=cfg.get("chroma_format", 1)) as dec:
         dec.set_debug(flag)
         def run(p):
             dec.assign_quant_params(p["quant"])
