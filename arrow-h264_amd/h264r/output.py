@@ -57,12 +57,12 @@ class OutputGeometry:
 def geometry(width_mbs: int, height_mbs: int, crop: Crop = Crop(), chroma_format: int = 1) -> OutputGeometry:
     """output.cc:135-165: size_x_l = PicWidthInMbs*16, size_x_c = PicWidthInMbs*MbWidthC;
     crop_*_c from the SPS (vertical offsets x (2 - frame_mbs_only_flag)), crop_*_l =
-    SubWidthC/SubHeightC x crop_*_c.  chroma_format 2 (4:2:2): SubHeightC 1, MbHeightC 16."""
-    sub_w, sub_h = 2, (1 if chroma_format == 2 else 2)
+    SubWidthC/SubHeightC x crop_*_c.  chroma_format 2 (4:2:2): SubHeightC 1; 3 (4:4:4): SubWidthC 1 too."""
+    sub_w, sub_h = (1 if chroma_format == 3 else 2), (2 if chroma_format == 1 else 1)
     lc, rc = crop.left, crop.right
     tc, bc = crop.top * (2 - crop.frame_mbs_only), crop.bottom * (2 - crop.frame_mbs_only)
     size_x_l, size_y_l = 16 * width_mbs, 16 * height_mbs
-    size_x_c, size_y_c = 8 * width_mbs, (16 if chroma_format == 2 else 8) * height_mbs
+    size_x_c, size_y_c = 16 // sub_w * width_mbs, 16 // sub_h * height_mbs
     lw, lh = size_x_l - sub_w * (lc + rc), size_y_l - sub_h * (tc + bc)
     cw, ch = size_x_c - (lc + rc), size_y_c - (tc + bc)
     if min(lc, rc, tc, bc) < 0 or lw <= 0 or lh <= 0 or cw <= 0 or ch <= 0:

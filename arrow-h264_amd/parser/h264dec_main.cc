@@ -1,7 +1,7 @@
 // h264dec_main.cc -- command-line decoder over the repo's own parser (h264p) and the h264r
 // reconstruction ABI: `h264dec -i stream.264 -o out.yuv [-d device]`, the reference's
 // `ldecod -i -o` (core/main.cc) for the path this repo covers.  Frames are written in output
-// order, cropped to the SPS window, 8-bit planar 4:2:0 or 4:2:2 (write_out_picture, output.cc:109-227).
+// order, cropped to the SPS window, 8-bit planar 4:2:0, 4:2:2 or 4:4:4 (write_out_picture, output.cc:109-227).
 // Linked against libh264r.so it decodes on MI355X; the test build links the CPU
 // implementation of the same ABI instead (oracle/Makefile h264dec_cpu).
 // `-r N`: decode the stream N more times after the written pass and print the wall time per
@@ -22,10 +22,12 @@ static int write_frame(void* user, const h264p_frame* f)
     const int y0 = f->crop_top, y1 = f->height - f->crop_bottom;
     for (int y = y0; y < y1; ++y)
         if (fwrite(f->y + (size_t)y * f->width + x0, 1, x1 - x0, out) != (size_t)(x1 - x0)) return 1;
-    const int sh = f->chroma_format == 2 ? 0 : 1;                  // log2 SubHeightC: 4:2:2 keeps every row
+    // log2 SubWidthC / SubHeightC: 4:2:2 keeps every row, 4:4:4 every row and column
+    const int sh = f->chroma_format == 1 ? 1 : 0, sw = f->chroma_format == 3 ? 0 : 1;
+    const int cw = f->width >> sw, n = (x1 - x0) >> sw;
     for (const uint8_t* c : {f->u, f->v})
         for (int y = y0 >> sh; y < y1 >> sh; ++y)
-            if (fwrite(c + (size_t)y * (f->width / 2) + x0 / 2, 1, (x1 - x0) / 2, out) != (size_t)((x1 - x0) / 2)) return 1;
+            if (fwrite(c + (size_t)y * cw + (x0 >> sw), 1, n, out) != (size_t)n) return 1;
     return 0;
 }
 

@@ -395,7 +395,7 @@ struct Sps {
     int max_num_ref_frames = 0;
     bool gaps = false;
     int W = 0, H = 0;
-    bool frame_mbs_only = true, mbaff = false, direct_8x8_inference = false;
+    bool frame_mbs_only = true, mbaff = false, direct_8x8_inference = false, separate_planes = false;
     int crop[4] = {0, 0, 0, 0};   // left, right, top, bottom (frame_crop_*_offset)
 };
 
@@ -425,7 +425,7 @@ int parse_sps(Bits& b, Sps& s)
         s.profile == 83 || s.profile == 86 || s.profile == 118 || s.profile == 128 || s.profile == 138 ||
         s.profile == 139 || s.profile == 134 || s.profile == 135) {
         s.chroma_format_idc = b.ue_max(3, "SPS: chroma_format_idc");
-        if (s.chroma_format_idc == 3) b.u(1);                    // separate_colour_plane_flag
+        if (s.chroma_format_idc == 3) s.separate_planes = b.u(1);   // separate_colour_plane_flag
         s.bit_depth_y = 8 + b.ue_max(6, "SPS: bit_depth_luma_minus8");
         s.bit_depth_c = 8 + b.ue_max(6, "SPS: bit_depth_chroma_minus8");
         s.bypass = b.u(1);
@@ -666,7 +666,7 @@ struct SliceCtx {
     int slice_nr;
     Bits& b;
     int W, H;                   // the picture's MBs (a field picture: FrameHeightInMbs / 2 rows)
-    int cf, mhc;                // chroma_format_idc (1, 2) and MbHeightC (8, 16)
+    int cf, mwc, mhc;           // chroma_format_idc (1, 2, 3), MbWidthC (8, 16) and MbHeightC (8, 16)
     const uint8_t* zz4;         // inverse scans: frame zig-zag, or the field scans of a field picture
     const uint8_t* zz8;
     int qp;                     // slice.parser.QpY
@@ -897,9 +897,9 @@ void Decoder::parse_slice_header(Bits& b, SliceHeader& h)
     require(pps_[h.pps_id].valid, "slice: pic_parameter_set_id of no PPS");
     const Pps& pps = pps_[h.pps_id];
     const Sps& sps = sps_[pps.sps_id];
-    unsupported((sps.chroma_format_idc != 1 && sps.chroma_format_idc != 2) || sps.bit_depth_y != 8 ||
-                sps.bit_depth_c != 8, "picture format (4:2:0 or 4:2:2, 8-bit only)");
-    unsupported(sps.chroma_format_idc == 2 && pps.cabac, "4:2:2 with CABAC (entropy_coding_mode_flag)");
+    unsupported(sps.chroma_format_idc < 1 || sps.separate_planes || sps.bit_depth_y != 8 || sps.bit_depth_c != 8,
+                "picture format (4:2:0, 4:2:2 or 4:4:4 without separate colour planes, 8-bit only)");
+    unsupported(sps.chroma_format_idc != 1 && pps.cabac, "4:2:2 / 4:4:4 with CABAC (entropy_coding_mode_flag)");
     unsupported(sps.mbaff, "MBAFF coding (mb_adaptive_frame_field_flag)");
     unsupported(sps.poc_type == 1, "pic_order_cnt_type 1");
     unsupported(h.slice_type == H264R_SLICE_SI, "SI slices");
@@ -907,7 +907,7 @@ void Decoder::parse_slice_header(Bits& b, SliceHeader& h)
     if (!sps.frame_mbs_only) {
         h.field = b.u(1);
         if (h.field) h.bottom = b.u(1);
-        unsupported(h.field && sps.chroma_format_idc == 2, "4:2:2 field pictures");
+        unsupported(h.field && sps.chroma_format_idc != 1, "4:2:2 / 4:4:4 field pictures");
     }
     if (h.idr) h.idr_pic_id = b.ue_max(65535, "slice: idr_pic_id");
     if (sps.poc_type == 0) {
@@ -1590,7 +1590,7 @@ void Decoder::collect()
     if (inflight_ < 0) return;
     Output& o = pending_[inflight_];
     inflight_ = -1;
-    const size_t n = (size_t)o.W * o.H, cs = n * (o.cf == 2 ? 128 : 64);
+    const size_t n = (size_t)o.W * o.H, cs = n * (o.cf == 3 ? 256 : o.cf == 2 ? 128 : 64);
     if (o.y.size() != n * 256 || o.u.size() != cs) {
         o.y.assign(n * 256, 0);
         o.u.assign(cs, 0);
@@ -1626,8 +1626,8 @@ void Decoder::flush_output()
         f.y = o.y.data(); f.u = o.u.data(); f.v = o.v.data();
         f.width = o.W * 16;
         f.height = o.H * 16;
-        const int sub_h = o.cf == 2 ? 1 : 2;                          // SubHeightC
-        f.crop_left = 2 * o.crop[0]; f.crop_right = 2 * o.crop[1];
+        const int sub_h = o.cf == 1 ? 2 : 1, sub_w = o.cf == 3 ? 1 : 2;   // SubHeightC, SubWidthC
+        f.crop_left = sub_w * o.crop[0]; f.crop_right = sub_w * o.crop[1];
         f.crop_top = sub_h * o.crop[2]; f.crop_bottom = sub_h * o.crop[3];
         f.chroma_format = o.cf;
         f.poc = o.poc;
@@ -1641,7 +1641,7 @@ void Decoder::flush_output()
 SliceCtx::SliceCtx(Decoder& d, const Sps& s, const Pps& p, const SliceHeader& h, int nr, Bits& bits,
                    Picture* const (*lists)[33], const int* list_n, int end)
     : D(d), sps(s), pps(p), sh(h), slice_nr(nr), b(bits), W(s.W), H(h.field ? s.H / 2 : s.H),
-      cf(s.chroma_format_idc), mhc(s.chroma_format_idc == 2 ? 16 : 8),
+      cf(s.chroma_format_idc), mwc(s.chroma_format_idc == 3 ? 16 : 8), mhc(s.chroma_format_idc == 1 ? 8 : 16),
       zz4(h.field ? FIELD_SCAN4X4 : ZZ4), zz8(h.field ? FIELD_SCAN8X8 : ZZ8), qp(h.qp), list_(lists), list_n_(list_n),
       end_mb(end)
 {
@@ -1698,7 +1698,7 @@ void SliceCtx::update_qp(int q)
 // callers' slice_nr checks); ax, ay = absolute sample position
 MbState* SliceCtx::nb_mb(bool chroma, int xN, int yN, int& ax, int& ay)
 {
-    const int mw = chroma ? 8 : 16, mh = chroma ? mhc : 16;
+    const int mw = chroma ? mwc : 16, mh = chroma ? mhc : 16;
     ax = mbx * mw + xN;
     ay = mby * mh + yN;
     if (ax < 0 || ax >= W * mw || ay < 0 || ay >= H * mh) return nullptr;
@@ -1804,7 +1804,7 @@ void SliceCtx::macroblock()
             for (int x = 0; x < 16; ++x) cof[0][y][x] = b.u(8);
         for (int c = 1; c <= 2; ++c)
             for (int y = 0; y < mhc; ++y)
-                for (int x = 0; x < 8; ++x) cof[c][y][x] = b.u(8);
+                for (int x = 0; x < mwc; ++x) cof[c][y][x] = b.u(8);
         if (cab) cab->init_engine(b);
         stage();
         return;
@@ -1852,8 +1852,13 @@ void SliceCtx::macroblock()
             cbp = cabac_cbp();
             if (!cbp) last_dquant = 0;
         } else {
-            const int code = b.ue_max(47, "coded_block_pattern");
-            cbp = m.intra ? CBP_ME_INTRA[code] : CBP_ME_INTER[code];
+            if (cf == 3) {                 // Table 9-4, ChromaArrayType 0 / 3: no chroma CBP
+                const int code = b.ue_max(15, "coded_block_pattern");
+                cbp = m.intra ? CBP_ME_INTRA_444[code] : CBP_ME_INTER_444[code];
+            } else {
+                const int code = b.ue_max(47, "coded_block_pattern");
+                cbp = m.intra ? CBP_ME_INTRA[code] : CBP_ME_INTER[code];
+            }
         }
         cbpl = cbp % 16;
         cbpc = cbp / 16;
@@ -1935,7 +1940,9 @@ void SliceCtx::intra_pred_modes()
             m.i8[k] = (uint8_t)(prev ? pred : rem < pred ? rem : rem + 1);
         }
     }
-    if (cab) {
+    if (cf == 3) {
+        // no intra_chroma_pred_mode in 4:4:4 (7.3.5.1: ChromaArrayType 1 or 2)
+    } else if (cab) {
         // TU cMax 3: bin 0 at A / B available with a non-DC chroma mode (not I_PCM), then 3
         int inc0 = 0;
         for (MbState* n : {nb_cur(-1, 0), nb_cur(0, -1)}) inc0 += n && n->cmode != 0 && n->mb_type != H264R_I_PCM;
@@ -2289,7 +2296,7 @@ void SliceCtx::inter_pred()
 // predict_nnz (neighbour.cc:263-314): nC of the 4x4 block at sample (i, j) of plane pl
 int SliceCtx::nnz_pred(int pl, int i, int j)
 {
-    const bool chroma = pl != 0;
+    const bool chroma = pl != 0 && cf != 3;                 // 4:4:4: Cb / Cr blocks in the luma grid
     const int mw = chroma ? 8 : 16, mh = chroma ? mhc : 16;
     int xa, ya, xb, yb;
     MbState* A = nb_mb(chroma, i - 1, j, xa, ya);
@@ -2381,11 +2388,15 @@ void SliceCtx::residual()
     int32_t pl_[128];
     int n;
     const bool i16 = m.mb_type == H264R_I_16x16;
+    // residual_luma for Y, and for Cb and Cr as luma in 4:4:4 (interpret_residual.cc:497-505);
+    // cbp_blks is the luma plane's (the record's, deblock.cc:135,212)
+    for (int p = 0; p < (cf == 3 ? 3 : 1); ++p) {
+    const uint16_t bmask = p == 0 ? 0xFFFF : 0;
     if (i16) {
-        block(LUMA_16DC, 0, false, false, 0, 0, 16, pl_, &n);
+        block(LUMA_16DC, p, false, false, 0, 0, 16, pl_, &n);
         for (int k = 0; k < n; ++k) {
             const int r = zz4[pl_[2 * k]];
-            cof[0][(r / 4) * 4][(r % 4) * 4] = pl_[2 * k + 1];
+            cof[p][(r / 4) * 4][(r % 4) * 4] = pl_[2 * k + 1];
         }
     }
     for (int i8 = 0; i8 < 4; ++i8) {
@@ -2393,36 +2404,38 @@ void SliceCtx::residual()
             // one 64-coefficient block per coded 8x8 (CABAC, :449-450)
             if (!(cbpl & (1 << i8))) continue;
             const int i = (i8 % 2) * 2, j = (i8 / 2) * 2;
-            block(LUMA_8x8, 0, false, true, i8 * 4, 0, 64, pl_, &n);
+            block(LUMA_8x8, p, false, true, i8 * 4, 0, 64, pl_, &n);
             for (int k = 0; k < n; ++k) {
-                cbp_blks |= (uint16_t)(0x33u << (j * 4 + i));
+                cbp_blks |= (uint16_t)(0x33u << (j * 4 + i)) & bmask;
                 const int r = zz8[pl_[2 * k]];
-                cof[0][j * 4 + r / 8][i * 4 + r % 8] = pl_[2 * k + 1];
+                cof[p][j * 4 + r / 8][i * 4 + r % 8] = pl_[2 * k + 1];
             }
             continue;
         }
         for (int i4 = 0; i4 < 4; ++i4) {
             const int blk = i8 * 4 + i4;
             const int i = ((blk / 4) % 2) * 2 + (blk % 4) % 2, j = ((blk / 4) / 2) * 2 + (blk % 4) / 2;
-            if (!(cbpl & (1 << i8))) { if (!cab) m.nz[0][j][i] = 0; continue; }
-            if (i16) block(LUMA_16AC, 0, false, true, blk, 1, 15, pl_, &n);
-            else block(LUMA_4x4, 0, false, true, blk, 0, 16, pl_, &n);
+            if (!(cbpl & (1 << i8))) { if (!cab) m.nz[p][j][i] = 0; continue; }
+            if (i16) block(LUMA_16AC, p, false, true, blk, 1, 15, pl_, &n);
+            else block(LUMA_4x4, p, false, true, blk, 0, 16, pl_, &n);
             for (int k = 0; k < n; ++k) {
                 const int c = pl_[2 * k], lev = pl_[2 * k + 1];
                 if (!m.t8) {
-                    cbp_blks |= (uint16_t)(1u << (j * 4 + i));
+                    cbp_blks |= (uint16_t)(1u << (j * 4 + i)) & bmask;
                     const int r = zz4[c];
-                    cof[0][j * 4 + r / 4][i * 4 + r % 4] = lev;
+                    cof[p][j * 4 + r / 4][i * 4 + r % 4] = lev;
                 } else {
                     // 8x8 CAVLC: four interleaved 4x4 readings (:161-164)
                     const int x0 = i & ~1, y0 = j & ~1;
-                    cbp_blks |= (uint16_t)(0x33u << (y0 * 4 + x0));
+                    cbp_blks |= (uint16_t)(0x33u << (y0 * 4 + x0)) & bmask;
                     const int r = zz8[c * 4 + blk % 4];
-                    cof[0][y0 * 4 + r / 8][x0 * 4 + r % 8] = lev;
+                    cof[p][y0 * 4 + r / 8][x0 * 4 + r % 8] = lev;
                 }
             }
         }
     }
+    }
+    if (cf == 3) return;
     // chroma: 4 (4:2:0) or 8 (4:2:2) 4x4 blocks and DC coefficients per plane; the 4:2:2 DC scan
     // (inverse_scan_chroma_dc transform.cc:365-374, the field 4x4 scan's first 8 positions) as
     // raster indices of the 2-wide DC matrix
@@ -2736,13 +2749,32 @@ void SliceCtx::stage()
     std::vector<int16_t>& lv = st.levels;
     lv.clear();
     if (m.mb_type == H264R_I_PCM) {
-        lv.resize(128 + 8 * mhc);
+        lv.resize(128 + mwc * mhc);
         uint8_t* raw = reinterpret_cast<uint8_t*>(lv.data());
         for (int y = 0; y < 16; ++y)
             for (int x = 0; x < 16; ++x) raw[y * 16 + x] = (uint8_t)cof[0][y][x];
         for (int p = 0; p < 2; ++p)
             for (int y = 0; y < mhc; ++y)
-                for (int x = 0; x < 8; ++x) raw[256 + p * 8 * mhc + y * 8 + x] = (uint8_t)cof[1 + p][y][x];
+                for (int x = 0; x < mwc; ++x) raw[256 + p * mwc * mhc + y * mwc + x] = (uint8_t)cof[1 + p][y][x];
+    } else if (cf == 3) {
+        // three luma-like blocks (include/h264r.h, 4:4:4): Y, Cb, Cr
+        for (int p = 0; p < 3; ++p) {
+            for (int b8 = 0; b8 < 4; ++b8) {
+                if (!((cbpl >> b8) & 1)) continue;
+                const int x8 = (b8 & 1) * 8, y8 = (b8 >> 1) * 8;
+                if (!m.t8) {
+                    for (int k = 0; k < 4; ++k)
+                        for (int i = 0; i < 16; ++i)
+                            lv.push_back((int16_t)cof[p][y8 + (k >> 1) * 4 + i / 4][x8 + (k & 1) * 4 + i % 4]);
+                    if (m.mb_type == H264R_I_16x16)
+                        for (int k = 0; k < 4; ++k) lv[lv.size() - 64 + k * 16] = 0;
+                } else {
+                    for (int i = 0; i < 64; ++i) lv.push_back((int16_t)cof[p][y8 + i / 8][x8 + i % 8]);
+                }
+            }
+            if (m.mb_type == H264R_I_16x16)
+                for (int i = 0; i < 16; ++i) lv.push_back((int16_t)cof[p][(i / 4) * 4][(i % 4) * 4]);
+        }
     } else if (cf == 2) {
         // the 4:2:2 level block (include/h264r.h): the luma part, then chroma AC, then DC
         for (int b8 = 0; b8 < 4; ++b8) {

@@ -123,6 +123,21 @@ int main()
         }
         printf("]");
     }
+    /* the same for ChromaArrayType 0 / 3 (4:4:4: no chroma CBP, codeNum 0..15, the table's other half) */
+    sps->chroma_format_idc = 3;
+    printf("},\n\"cbp_me_444\": {");
+    for (int inter = 0; inter < 2; ++inter) {
+        mb->is_intra_block = !inter;
+        printf("%s\"%s\": [", inter ? ", " : "", inter ? "inter" : "intra");
+        for (unsigned k = 0; k < 16; ++k) {
+            unsigned v = k + 1; int nb = 0;
+            while ((v >> nb) > 1) ++nb;
+            unsigned pat = v << (15 - 2 * nb);
+            feed(pat);
+            printf("%s%d", k ? ", " : "", (int)se.coded_block_pattern());
+        }
+        printf("]");
+    }
     mb->is_intra_block = 1;
     printf("}\n}\n");
     return 0;

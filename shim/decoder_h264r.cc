@@ -53,6 +53,9 @@
  * 4:2:2 (chroma_format_idc 2, MbHeightC 16; frame pictures): the level block takes the 4:2:2
  * layout of include/h264r.h (luma, then chroma AC of 8 blocks per plane, then the 2x4 DC
  * matrix -- coeff_chroma_dc left each DC level at its raster position, transform.cc:365-374).
+ * 4:4:4 (chroma_format_idc 3, separate_colour_plane_flag 0; frame pictures): Cb and Cr are coded
+ * like luma (coeff_luma_* with their ColorPlane), so the level block is three luma-like blocks
+ * (include/h264r.h), and decode() leaves both coefficient-reset flags cleared (decoder.cc:72-76).
  * Errors: a status other than H264R_OK goes through the reference's own error()
  * (ldecod.cc:33-48), its convention for fatal conditions.
  */
@@ -189,10 +192,10 @@ void begin_picture(Shim& S, slice_t& slice)
     if (S.pic == pic) return;
     const sps_t& sps = *slice.active_sps;
     const int cf = sps.chroma_format_idc;
-    if ((cf != 1 && cf != 2) || sps.BitDepthY != 8 || sps.BitDepthC != 8)
-        check(H264R_EUNSUPPORTED, "picture format (4:2:0 or 4:2:2, 8-bit)");
+    if (cf < 1 || cf > 3 || sps.separate_colour_plane_flag || sps.BitDepthY != 8 || sps.BitDepthC != 8)
+        check(H264R_EUNSUPPORTED, "picture format (4:2:0, 4:2:2 or 4:4:4 without separate planes, 8-bit)");
     if (slice.header.MbaffFrameFlag) check(H264R_EUNSUPPORTED, "MBAFF frames");
-    if (cf == 2 && slice.header.field_pic_flag) check(H264R_EUNSUPPORTED, "4:2:2 field pictures");
+    if (cf != 1 && slice.header.field_pic_flag) check(H264R_EUNSUPPORTED, "4:2:2 / 4:4:4 field pictures");
     // the context holds frames; a field picture is PicHeightInMbs = FrameHeightInMbs / 2 rows
     const int W = sps.PicWidthInMbs, H = sps.FrameHeightInMbs, PH = slice.header.PicHeightInMbs;
     if (!S.ctx || W > S.ctx_w || H > S.ctx_h || cf != S.ctx_cf) {
@@ -465,15 +468,35 @@ void Decoder::decode(mb_t& mb)
     // the level block (include/h264r.h layout) from the raw levels in cof
     std::vector<int16_t>& lv = st.levels;
     lv.clear();
-    const bool f422 = slice.active_sps->chroma_format_idc == 2;
-    const int MHc = f422 ? 16 : 8, nbc = f422 ? 8 : 4;     // MbHeightC, chroma 4x4 blocks per plane
+    const int cfi = slice.active_sps->chroma_format_idc;
+    const bool f422 = cfi == 2, f444 = cfi == 3;
+    const int MWc = f444 ? 16 : 8, MHc = cfi == 1 ? 8 : 16, nbc = f422 ? 8 : 4;   // MbWidthC, MbHeightC, 4x4 blocks
     if (mb.mb_type == I_PCM) {
-        lv.resize(128 + 8 * MHc);
+        lv.resize(128 + MWc * MHc);
         uint8_t* raw = reinterpret_cast<uint8_t*>(lv.data());
         for (int y = 0; y < 16; ++y) for (int x = 0; x < 16; ++x) raw[y * 16 + x] = (uint8_t)cof[0][y][x];
         for (int p = 0; p < 2; ++p)
             for (int y = 0; y < MHc; ++y)
-                for (int x = 0; x < 8; ++x) raw[256 + p * 8 * MHc + y * 8 + x] = (uint8_t)cof[1 + p][y][x];
+                for (int x = 0; x < MWc; ++x) raw[256 + p * MWc * MHc + y * MWc + x] = (uint8_t)cof[1 + p][y][x];
+    } else if (f444) {
+        // three luma-like blocks, Y then Cb then Cr: the coded 8x8 blocks, then the I_16x16 DC
+        for (int pl = 0; pl < 3; ++pl) {
+            for (int b8 = 0; b8 < 4; ++b8) {
+                if (!((cbpl >> b8) & 1)) continue;
+                const int x8 = (b8 & 1) * 8, y8 = (b8 >> 1) * 8;
+                if (!mb.transform_size_8x8_flag) {
+                    for (int k = 0; k < 4; ++k)
+                        for (int i = 0; i < 16; ++i)
+                            lv.push_back((int16_t)cof[pl][y8 + (k >> 1) * 4 + i / 4][x8 + (k & 1) * 4 + i % 4]);
+                    if (mb.mb_type == I_16x16)
+                        for (int k = 0; k < 4; ++k) lv[lv.size() - 64 + k * 16] = 0;
+                } else {
+                    for (int i = 0; i < 64; ++i) lv.push_back((int16_t)cof[pl][y8 + i / 8][x8 + i % 8]);
+                }
+            }
+            if (mb.mb_type == I_16x16)
+                for (int i = 0; i < 16; ++i) lv.push_back((int16_t)cof[pl][(i / 4) * 4][(i % 4) * 4]);
+        }
     } else if (f422) {
         // 4:2:2 (include/h264r.h): the luma part, then chroma AC (8 blocks per plane), then DC
         for (int b8 = 0; b8 < 4; ++b8) {
@@ -539,7 +562,10 @@ void Decoder::decode(mb_t& mb)
 
     // coefficient-reset protocol (slice_data.cc:496-503): the same side effects as the
     // reference's reconstruction leaves behind
-    if (mb.mb_type != I_PCM) {
+    if (f444) {                                                                          // decoder.cc:72-76
+        slice.parser.is_reset_coeff = false;
+        slice.parser.is_reset_coeff_cr = false;
+    } else if (mb.mb_type != I_PCM) {
         if (mb.is_intra_block) {
             if (mb.mb_type == I_16x16 || cbpl || cbpc) slice.parser.is_reset_coeff = false;   // decoder.cc:196-197
             if (cbpc) slice.parser.is_reset_coeff_cr = false;                                // decoder.cc:205-206
@@ -619,19 +645,19 @@ void Decoder::deblock_filter(slice_t& slice)
         for (auto it = S.slot_of.begin(); it != S.slot_of.end();)
             it = it->second.slot == keep ? S.slot_of.erase(it) : std::next(it);
     }
-    const int MHc = S.ctx_cf == 2 ? 16 : 8;                   // MbHeightC
+    const int MWc = S.ctx_cf == 3 ? 16 : 8, MHc = S.ctx_cf == 1 ? 8 : 16;   // MbWidthC, MbHeightC
     S.y8.resize((size_t)W * H * 256);
-    S.u8.resize((size_t)W * H * 8 * MHc);
-    S.v8.resize((size_t)W * H * 8 * MHc);
+    S.u8.resize((size_t)W * H * MWc * MHc);
+    S.v8.resize((size_t)W * H * MWc * MHc);
     check(h264r_picture_end(S.ctx, S.y8.data(), S.u8.data(), S.v8.data(), keep), "h264r_picture_end");
     S.slot_of.erase(pic);
     if (keep >= 0) S.slot_of[pic] = Shim::Resident{keep, pic->slice.structure, pic->poc, pic->frame_num};
     for (int y = 0; y < H * 16; ++y)
         for (int x = 0; x < W * 16; ++x) pic->imgY[y][x] = S.y8[(size_t)y * W * 16 + x];
     for (int y = 0; y < H * MHc; ++y)
-        for (int x = 0; x < W * 8; ++x) {
-            pic->imgUV[0][y][x] = S.u8[(size_t)y * W * 8 + x];
-            pic->imgUV[1][y][x] = S.v8[(size_t)y * W * 8 + x];
+        for (int x = 0; x < W * MWc; ++x) {
+            pic->imgUV[0][y][x] = S.u8[(size_t)y * W * MWc + x];
+            pic->imgUV[1][y][x] = S.v8[(size_t)y * W * MWc + x];
         }
     S.pic = nullptr;
 }

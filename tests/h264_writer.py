@@ -43,6 +43,8 @@ TOTAL_ZEROS = {int(y): {int(t): {v: (ln, code) for v, ln, code in ent} for t, en
                for y, d in _T["total_zeros"].items()}
 RUN_BEFORE = {int(z): {v: (ln, code) for v, ln, code in ent} for z, ent in _T["run_before"].items()}
 CBP_CODE = {k: {cbp: code for code, cbp in enumerate(v)} for k, v in _T["cbp_me"].items()}
+# chroma_format_idc 0 / 3: the other half of Table 9-4 (no chroma CBP)
+CBP_CODE_444 = {k: {cbp: code for code, cbp in enumerate(v)} for k, v in _T["cbp_me_444"].items()}
 
 # 4x4 / 8x8 frame zig-zag scans: raster index of scan position k (spec Tables 8-12/8-13)
 def _zigzag(n):
@@ -151,7 +153,9 @@ class StreamCfg:
                                      # reference field (the first field of their own frame too)
     bottom_first: float = 0.0        # share of field pairs sent bottom field first
     chroma_format: int = 1           # chroma_format_idc (profiles 100 / 122 / 244): 1 4:2:0, 2 4:2:2 (CAVLC:
-                                     # 8 chroma 4x4 blocks and a 2x4 DC per plane, nC -2, interpret_residual.cc:462-494)
+                                     # 8 chroma 4x4 blocks and a 2x4 DC per plane, nC -2, interpret_residual.cc:462-494),
+                                     # 3 4:4:4 (244, CAVLC: Cb and Cr coded as luma, residual_luma per plane
+                                     # interpret_residual.cc:497-505; no intra chroma mode, the 4:4:4 CBP table)
     long_term: int = 0               # the IDR is a long-term reference (LongTermFrameIdx 0) kept for the
                                      # whole stream, and P picture `long_term` becomes a second one by
                                      # MMCO 4 + 6 (LongTermFrameIdx 1); P pictures predict from them
@@ -204,11 +208,13 @@ class Encoder:
         w.ue(0)                                     # seq_parameter_set_id
         if c.profile in (100, 122, 244):
             w.ue(c.chroma_format)                   # chroma_format_idc
+            if c.chroma_format == 3:
+                w.u(1, 0)                           # separate_colour_plane_flag
             w.ue(0); w.ue(0)                        # bit depths 8
             w.u(1, 1 if c.lossless else 0)          # qpprime_y_zero_transform_bypass_flag
             w.u(1, c.scaling & 1)                   # seq_scaling_matrix_present_flag
             if c.scaling & 1:
-                self._scaling_matrix(w, 8)
+                self._scaling_matrix(w, 12 if c.chroma_format == 3 else 8)
         w.ue(self.log2_max_frame_num - 4)
         if c.bframes:
             w.ue(0)                                 # pic_order_cnt_type 0: B pictures reorder
@@ -253,7 +259,7 @@ class Encoder:
             w.u(1, c.transform8x8)
             w.u(1, 1 if c.scaling & 2 else 0)       # pic_scaling_matrix_present_flag
             if c.scaling & 2:
-                self._scaling_matrix(w, 6 + 2 * c.transform8x8)
+                self._scaling_matrix(w, 6 + (6 if c.chroma_format == 3 else 2) * c.transform8x8)
             w.se(c.chroma_qp_offset if c.second_chroma_qp_offset is None else c.second_chroma_qp_offset)
         w.trailing()
         return nal_unit(3, 8, w.bytes())
@@ -300,8 +306,9 @@ class Encoder:
     def _nc(self, a: int, pl: int, bx: int, by: int, s: int) -> int:
         """nC of the block at (bx, by) (4x4 units, plane pl), neighbour.cc:263-314."""
         mx, my = a % self.W, a // self.W
-        nw = 4 if pl == 0 else 2                        # 4x4 blocks per MB: across, down
-        nh = 4 if pl == 0 or self.c.chroma_format == 2 else 2
+        luma = pl == 0 or self.c.chroma_format == 3     # 4:4:4: Cb / Cr blocks in the luma grid
+        nw = 4 if luma else 2                           # 4x4 blocks per MB: across, down
+        nh = 4 if luma or self.c.chroma_format == 2 else 2
         def nz_of(dx, dy):
             x, y = bx + dx, by + dy
             ox, oy = mx + (x // nw if x >= 0 else -1), my + (y // nh if y >= 0 else -1)
@@ -394,24 +401,28 @@ class Encoder:
         if self.cab:
             self._residual_cabac(m, cbpl, cbpc)
             return
-        if m.kind == I16:
-            self._block(w, self._levels(16), self._nc(a, 0, 0, 0, s), 16)
-        for b8 in range(4):
-            if m.t8 and (cbpl >> b8) & 1:
-                l8 = self._levels(64)
+        # residual_luma for Y, and for Cb and Cr in 4:4:4 (interpret_residual.cc:497-505)
+        for pl in ((0, 1, 2) if self.c.chroma_format == 3 else (0,)):
+            if m.kind == I16:
+                self._block(w, self._levels(16), self._nc(a, pl, 0, 0, s), 16)
+            for b8 in range(4):
+                if m.t8 and (cbpl >> b8) & 1:
+                    l8 = self._levels(64)
+                    for b4 in range(4):
+                        bx, by = _blk_xy(b8 * 4 + b4)
+                        m.nz[pl][by][bx] = self._block(w, [l8[4 * k + b4] for k in range(16)], self._nc(a, pl, bx, by, s), 16)
+                    continue
                 for b4 in range(4):
                     bx, by = _blk_xy(b8 * 4 + b4)
-                    m.nz[0][by][bx] = self._block(w, [l8[4 * k + b4] for k in range(16)], self._nc(a, 0, bx, by, s), 16)
-                continue
-            for b4 in range(4):
-                bx, by = _blk_xy(b8 * 4 + b4)
-                if (cbpl >> b8) & 1:
-                    if m.kind == I16:
-                        m.nz[0][by][bx] = self._block(w, self._levels(15), self._nc(a, 0, bx, by, s), 15)
+                    if (cbpl >> b8) & 1:
+                        if m.kind == I16:
+                            m.nz[pl][by][bx] = self._block(w, self._levels(15), self._nc(a, pl, bx, by, s), 15)
+                        else:
+                            m.nz[pl][by][bx] = self._block(w, self._levels(16), self._nc(a, pl, bx, by, s), 16)
                     else:
-                        m.nz[0][by][bx] = self._block(w, self._levels(16), self._nc(a, 0, bx, by, s), 16)
-                else:
-                    m.nz[0][by][bx] = 0
+                        m.nz[pl][by][bx] = 0
+        if self.c.chroma_format == 3:
+            return
         nbc = 8 if self.c.chroma_format == 2 else 4     # chroma 4x4 blocks (= DC coefficients) per plane
         if cbpc & 3:
             for _pl in (1, 2):
@@ -428,7 +439,7 @@ class Encoder:
         """The same blocks and level draws as the CAVLC path, as residual_block_cabac calls:
         an 8x8 transform block is one 64-coefficient block (interpret_residual.cc:453-456)."""
         cab = self.cab
-        assert self.c.chroma_format == 1, "CABAC streams: 4:2:0 only"
+        assert self.c.chroma_format == 1, "CABAC streams: 4:2:0 only"   # (4:2:2 / 4:4:4: CAVLC)
         if m.kind == I16:
             cab.block(CB.LUMA_16DC, 0, 0, self._levels(16))
         for b8 in range(4):
@@ -541,7 +552,7 @@ class Encoder:
         A, B, D = self._avail_abd(a, 0, 0, 4, s)
         if m.kind == PCM:
             m.mbt_ref = 12
-            npcm = 256 + (256 if c.chroma_format == 2 else 128)     # 2 x MbWidthC x MbHeightC chroma samples
+            npcm = 256 + {2: 256, 3: 512}.get(c.chroma_format, 128)   # 2 x MbWidthC x MbHeightC chroma samples
             if cab:
                 cab.mb_type_intra(25)
                 cab.pcm([r.randint(1, 255) for _ in range(npcm)])
@@ -557,7 +568,7 @@ class Encoder:
         if m.kind == I16:
             modes = ([0] if B else []) + ([1] if A else []) + [2] + ([3] if A and B and D else [])
             mode = r.choice(modes)
-            cbpc = r.randint(0, 2)
+            cbpc = r.randint(0, 2) if c.chroma_format != 3 else 0
             cbpl = 15 if r.random() < 0.5 else 0
             m.mbt_ref, m.cbpl, m.cbpc = 10, cbpl, cbpc
             cm = r.choice(cmodes)
@@ -567,7 +578,8 @@ class Encoder:
                 cab.chroma_mode(cm)
             else:
                 w.ue(base + 1 + mode + 4 * cbpc + (12 if cbpl else 0))
-                w.ue(cm)
+                if c.chroma_format != 3:                # intra_chroma_pred_mode: ChromaArrayType 1 / 2 only
+                    w.ue(cm)
             cbp = cbpl | cbpc << 4
         elif m.kind in (I4, I8):
             m.t8 = m.kind == I8
@@ -605,12 +617,14 @@ class Encoder:
                     else:
                         w.u(1, 0); w.u(3, mode if mode < pred else mode - 1)
             cm = r.choice(cmodes)
-            cbp = r.randint(0, 47)
+            cbp = r.randint(0, 47) if c.chroma_format != 3 else r.randint(0, 15)
             m.cbpl, m.cbpc = cbp & 15, cbp >> 4
             if cab:
                 m.cmode = cm
                 cab.chroma_mode(cm)
                 cab.cbp(cbp)
+            elif c.chroma_format == 3:
+                w.ue(CBP_CODE_444["intra"][cbp])
             else:
                 w.ue(cm)
                 w.ue(CBP_CODE["intra"][cbp])
@@ -671,12 +685,12 @@ class Encoder:
                     for sp in {0: [(0, 0, 2, 2)], 1: [(0, 0, 2, 1), (0, 1, 2, 1)], 2: [(0, 0, 1, 2), (1, 0, 1, 2)],
                                3: [(0, 0, 1, 1), (1, 0, 1, 1), (0, 1, 1, 1), (1, 1, 1, 1)]}[sb]:
                         mvd(x8 + sp[0], y8 + sp[1], sp[2], sp[3])
-            cbp = r.randint(0, 47)
+            cbp = r.randint(0, 47) if c.chroma_format != 3 else r.randint(0, 15)
             m.cbpl, m.cbpc = cbp & 15, cbp >> 4
             if cab:
                 cab.cbp(cbp)
             else:
-                w.ue(CBP_CODE["inter"][cbp])
+                w.ue((CBP_CODE_444 if c.chroma_format == 3 else CBP_CODE)["inter"][cbp])
             m.t8 = False
             if (cbp & 15) and c.transform8x8 and not small:
                 m.t8 = r.random() < 0.5
@@ -794,12 +808,12 @@ class Encoder:
                             sps = [(0, 0, 1, 2), (1, 0, 1, 2)]
                         for sp in sps:
                             mvd(lst, x8 + sp[0], y8 + sp[1], sp[2], sp[3])
-        cbp = r.randint(0, 47)
+        cbp = r.randint(0, 47) if self.c.chroma_format != 3 else r.randint(0, 15)
         m.cbpl, m.cbpc = cbp & 15, cbp >> 4
         if cab:
             cab.cbp(cbp)
         else:
-            w.ue(CBP_CODE["inter"][cbp])
+            w.ue((CBP_CODE_444 if self.c.chroma_format == 3 else CBP_CODE)["inter"][cbp])
         return cbp, small
 
     # ------------------------------------------------------------------ pictures

@@ -124,6 +124,15 @@ STREAMS = {
                                   second_chroma_qp_offset=4, crop=(1, 2, 3, 2)),
     "hi422_qcif_lossless": dict(width_mbs=11, height_mbs=9, frames=4, seed=703, profile=244, chroma_format=2,
                                 lossless=0.5, qp=(0, 30), intra_in_p=0.4, deblock=(0, 2), offsets=4, scaling=2),
+    # 4:4:4 (chroma_format_idc 3, High 4:4:4 Predictive, CAVLC): Cb and Cr coded as luma (their own
+    # CAVLC nC), no intra chroma mode, the 4:4:4 CBP table; lossless MBs and 8x8 transforms
+    "hi444_cif_ippp_8x8": dict(width_mbs=22, height_mbs=18, frames=4, seed=801, profile=244, chroma_format=3,
+                               transform8x8=1, num_refs=2, weighted=1, slices=2, deblock=(0, 1, 2), offsets=3,
+                               pcm=0.03, intra_in_p=0.2, chroma_qp_offset=2, second_chroma_qp_offset=-4,
+                               crop=(2, 1, 0, 3)),
+    "hi444_qcif_ibbp_lossless_scaling": dict(width_mbs=11, height_mbs=9, frames=7, seed=802, profile=244,
+                                             chroma_format=3, transform8x8=1, bframes=2, num_refs=3, bipred=2,
+                                             lossless=0.4, qp=(0, 36), intra_in_p=0.3, scaling=3, cip=1),
 }
 
 CAP_MAGIC = 0x43523448
