@@ -899,7 +899,7 @@ void Decoder::parse_slice_header(Bits& b, SliceHeader& h)
     const Sps& sps = sps_[pps.sps_id];
     unsupported(sps.chroma_format_idc < 1 || sps.separate_planes || sps.bit_depth_y != 8 || sps.bit_depth_c != 8,
                 "picture format (4:2:0, 4:2:2 or 4:4:4 without separate colour planes, 8-bit only)");
-    unsupported(sps.chroma_format_idc != 1 && pps.cabac, "4:2:2 / 4:4:4 with CABAC (entropy_coding_mode_flag)");
+    unsupported(sps.chroma_format_idc == 3 && pps.cabac, "4:4:4 with CABAC (entropy_coding_mode_flag)");
     unsupported(sps.mbaff, "MBAFF coding (mb_adaptive_frame_field_flag)");
     unsupported(sps.poc_type == 1, "pic_order_cnt_type 1");
     unsupported(h.slice_type == H264R_SLICE_SI, "SI slices");
@@ -2633,7 +2633,7 @@ int SliceCtx::cbf_inc(int pl, bool chroma, bool ac, int blk)
     const int i = chroma ? blk % 2 : ((blk / 4) % 2) * 2 + (blk % 4) % 2;
     const int j = chroma ? blk / 2 : ((blk / 4) / 2) * 2 + (blk % 4) / 2;
     const int bit = !chroma ? (ac ? 1 : 0) : !ac ? (pl == 1 ? 17 : 18) : (pl == 1 ? 19 : 35);
-    const int nw = chroma ? 8 : 16;
+    const int nw = chroma ? mwc : 16, nh = chroma ? mhc : 16;     // MbWidthC / MbHeightC (neighbour.cc:716-722)
     int inc = 0;
     const int off[2][2] = {{i * 4 - 1, j * 4}, {i * 4, j * 4 - 1}};
     for (int k = 0; k < 2; ++k) {
@@ -2643,7 +2643,7 @@ int SliceCtx::cbf_inc(int pl, bool chroma, bool ac, int blk)
         if (n) {
             if (n->mb_type == H264R_I_PCM) cond = 1;
             else {
-                const int pos = ac ? ((ay % nw) & 12) + (ax % nw) / 4 : 0;
+                const int pos = ac ? ((ay % nh) & 12) + (ax % nw) / 4 : 0;
                 cond = (int)((n->cbp_bits >> (bit + pos)) & 1);
             }
         }
@@ -2670,8 +2670,11 @@ int SliceCtx::block_cabac(int cat, int pl, bool chroma, bool ac, int blk, int st
     // field pictures: the second set of significance contexts and the field 8x8 map
     // (interpret_residual.cc:353-358)
     const bool fld = sh.field;
-    const uint8_t* pmap = cat == LUMA_8x8 ? (fld ? POS2CTX_MAP8X8_FIELD : POS2CTX_MAP8X8) : POS2CTX_MAP4X4;
-    const uint8_t* plast = cat == LUMA_8x8 ? POS2CTX_LAST8X8 : POS2CTX_LAST4X4;
+    // 4:2:2 chroma DC: CHROMA_DC_2x4's maps (ctxIdxInc Min(i / NumC8x8, 2); its context offsets are
+    // CHROMA_DC's, interpret_residual.cc:336)
+    const bool dc2x4 = cat == CHROMA_DC && cf == 2;
+    const uint8_t* pmap = cat == LUMA_8x8 ? (fld ? POS2CTX_MAP8X8_FIELD : POS2CTX_MAP8X8) : dc2x4 ? POS2CTX_MAP2X4C : POS2CTX_MAP4X4;
+    const uint8_t* plast = cat == LUMA_8x8 ? POS2CTX_LAST8X8 : dc2x4 ? POS2CTX_LAST2X4C : POS2CTX_LAST4X4;
     const int fset = fld ? (CTX_LAST_CONTEXTS - CTX_MAP_CONTEXTS) / 2 : 0;      // 210 contexts per set
     const int map = CTX_MAP_CONTEXTS + fset + TYPE2CTX_MAP[cat], last = CTX_LAST_CONTEXTS + fset + TYPE2CTX_MAP[cat];
     int sig[64];

@@ -442,8 +442,9 @@ class CabacSink:
                 if m is None:
                     inc += w if m_cur.intra else 0
                     continue
-                n = 2 if chroma else 4
-                pi, pj = ni % n, nj % n
+                nw = 2 if chroma else 4                     # 4x4 blocks per MB: 4:2:2 chroma 2 x 4
+                nh = (4 if self.e.c.chroma_format == 2 else 2) if chroma else 4
+                pi, pj = ni % nw, nj % nh
             if m.mbt_ref == 12:
                 inc += w
                 continue
@@ -471,7 +472,8 @@ class CabacSink:
         m_cur.cbp_bits |= (0x33 if typ == LUMA_8x8 else 0x01) << (bit + (j * 4 + i if ac else 0))
         n = len(coeffs)
         last = max(k for k, v in enumerate(coeffs) if v)
-        pm, pl_ = (POS_MAP_FIELD if self.field else POS_MAP)[_POS[typ]], POS_LAST[_POS[typ]]
+        pos = "2x4c" if typ == CHROMA_DC and self.e.c.chroma_format == 2 else _POS[typ]   # CHROMA_DC_2x4 maps
+        pm, pl_ = (POS_MAP_FIELD if self.field else POS_MAP)[pos], POS_LAST[pos]
         fm, fl = (MAP_SET, LAST_SET) if self.field else (0, 0)
         for k in range(n - 1):
             sig = 1 if coeffs[k] else 0

@@ -439,7 +439,7 @@ class Encoder:
         """The same blocks and level draws as the CAVLC path, as residual_block_cabac calls:
         an 8x8 transform block is one 64-coefficient block (interpret_residual.cc:453-456)."""
         cab = self.cab
-        assert self.c.chroma_format == 1, "CABAC streams: 4:2:0 only"   # (4:2:2 / 4:4:4: CAVLC)
+        assert self.c.chroma_format in (1, 2), "CABAC streams: 4:2:0 / 4:2:2"   # (4:4:4: CAVLC)
         if m.kind == I16:
             cab.block(CB.LUMA_16DC, 0, 0, self._levels(16))
         for b8 in range(4):
@@ -456,12 +456,13 @@ class Encoder:
                     cab.block(CB.LUMA_16AC, 0, b8 * 4 + b4, self._levels(15))
                 else:
                     cab.block(CB.LUMA_4x4, 0, b8 * 4 + b4, self._levels(16))
+        nbc = 8 if self.c.chroma_format == 2 else 4
         if cbpc & 3:
             for pl in (1, 2):
-                cab.block(CB.CHROMA_DC, pl, 0, self._levels(4))
+                cab.block(CB.CHROMA_DC, pl, 0, self._levels(nbc))
         if cbpc & 2:
             for pl in (1, 2):
-                for b in range(4):
+                for b in range(nbc):
                     cab.block(CB.CHROMA_AC, pl, b, self._levels(15))
 
     # ------------------------------------------------------------------ intra modes

@@ -124,6 +124,14 @@ STREAMS = {
                                   second_chroma_qp_offset=4, crop=(1, 2, 3, 2)),
     "hi422_qcif_lossless": dict(width_mbs=11, height_mbs=9, frames=4, seed=703, profile=244, chroma_format=2,
                                 lossless=0.5, qp=(0, 30), intra_in_p=0.4, deblock=(0, 2), offsets=4, scaling=2),
+    # ... and CABAC: the 2x4 DC with CHROMA_DC_2x4's significance maps (interpret_residual.cc:336), the
+    # coded_block_flag of 8 AC blocks per plane (neighbour.cc:690-740 with MbHeightC 16)
+    "hi422_cif_cabac_ibbp": dict(width_mbs=22, height_mbs=18, frames=7, seed=704, profile=122, chroma_format=2,
+                                 cabac=1, bframes=2, num_refs=3, bipred=1, slices=2, deblock=(0, 2), offsets=2,
+                                 intra_in_p=0.2, pcm=0.04, cip=1, chroma_qp_offset=3),
+    "hi422_qcif_cabac_intra_qp0_51": dict(width_mbs=11, height_mbs=9, frames=2, seed=705, profile=122,
+                                          chroma_format=2, cabac=1, all_intra=True, qp=(0, 51), pcm=0.05,
+                                          level_max=3),
     # 4:4:4 (chroma_format_idc 3, High 4:4:4 Predictive, CAVLC): Cb and Cr coded as luma (their own
     # CAVLC nC), no intra chroma mode, the 4:4:4 CBP table; lossless MBs and 8x8 transforms
     "hi444_cif_ippp_8x8": dict(width_mbs=22, height_mbs=18, frames=4, seed=801, profile=244, chroma_format=3,
