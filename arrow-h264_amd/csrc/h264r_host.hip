@@ -134,7 +134,7 @@ struct Scratch {
 struct h264r_ctx {
     int device = 0;
     int max_w = 0, max_h = 0;
-    int fmt = 1;                          // chroma_format_idc: 1 (4:2:0), 2 (4:2:2, run_422) or 3 (4:4:4, run_444)
+    int fmt = 1;                          // chroma_format_idc: 1 (4:2:0), 0 (4:0:0) / 2 (4:2:2) (run_422) or 3 (4:4:4, run_444)
     // 4:4:4: one colour plane's derived batch (k_derive444) -- records, slices, quant, DPB tables --
     // and the scratch its unused 4:2:0 chroma outputs go to
     h264r_mb* d444_mbs = nullptr; size_t c444_mbs = 0;
@@ -353,7 +353,7 @@ int h264r_create(h264r_ctx** out, int device, int max_w, int max_h, int chroma_f
     if (!out || max_w <= 0 || max_h <= 0 || max_w > 1024 || max_h > 1024) return H264R_EINVAL;
     *out = nullptr;
     if (!knobs().ok) return H264R_EINVAL;            // an environment knob out of range (stderr)
-    if (chroma_format_idc < 1 || chroma_format_idc > 3 || bit_depth != 8) return H264R_EUNSUPPORTED;
+    if (chroma_format_idc < 0 || chroma_format_idc > 3 || bit_depth != 8) return H264R_EUNSUPPORTED;
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0 || device < 0 || device >= n) return H264R_ENODEVICE;
     hipDeviceProp_t p;
@@ -409,7 +409,10 @@ int h264r_destroy(h264r_ctx* c)
 
 // Bytes of one chroma plane of a w x h MB picture: 8 x 8 samples per MB (4:2:0), 8 x 16 (4:2:2)
 // or 16 x 16 (4:4:4).
-static size_t chroma_bytes(const h264r_ctx* c, int w, int h) { return (size_t)w * h * (c->fmt == 3 ? 256 : c->fmt == 2 ? 128 : 64); }
+static size_t chroma_bytes(const h264r_ctx* c, int w, int h)
+{
+    return (size_t)w * h * (c->fmt == 3 ? 256 : c->fmt == 2 ? 128 : c->fmt == 1 ? 64 : 0);     // 4:0:0: none
+}
 
 static int ensure_slot(h264r_ctx* c, int slot, int w, int h)
 {
@@ -430,15 +433,18 @@ static int ensure_slot(h264r_ctx* c, int slot, int w, int h)
 
 int h264r_set_ref(h264r_ctx* c, int slot, const uint8_t* y, const uint8_t* u, const uint8_t* v, int w, int h)
 {
-    if (!c || slot < 0 || slot >= H264R_MAX_SLOTS || !y || !u || !v || w <= 0 || h <= 0 || w > c->max_w || h > c->max_h)
+    if (!c || slot < 0 || slot >= H264R_MAX_SLOTS || !y || (c->fmt && (!u || !v)) || w <= 0 || h <= 0 ||
+        w > c->max_w || h > c->max_h)
         return H264R_EINVAL;
     (void)hipSetDevice(c->device);
     int st = ensure_slot(c, slot, w, h);
     if (st) return st;
     size_t ys = (size_t)w * 16 * h * 16, cs = chroma_bytes(c, w, h);
     HIP_OK(hipMemcpyAsync(c->slot[slot][0], y, ys, hipMemcpyHostToDevice, c->stream));
-    HIP_OK(hipMemcpyAsync(c->slot[slot][1], u, cs, hipMemcpyHostToDevice, c->stream));
-    HIP_OK(hipMemcpyAsync(c->slot[slot][2], v, cs, hipMemcpyHostToDevice, c->stream));
+    if (cs) {
+        HIP_OK(hipMemcpyAsync(c->slot[slot][1], u, cs, hipMemcpyHostToDevice, c->stream));
+        HIP_OK(hipMemcpyAsync(c->slot[slot][2], v, cs, hipMemcpyHostToDevice, c->stream));
+    }
     HIP_OK(hipStreamSynchronize(c->stream));
     return H264R_OK;
 }
@@ -845,7 +851,7 @@ static int run_444(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row0, 
     return H264R_OK;
 }
 
-// 4:2:2 (chroma_format_idc 2): the luma plane by the 4:2:0 launch sequence (k_derive444 plane 0 --
+// 4:2:2 (chroma_format_idc 2) and 4:0:0 (0): the luma plane by the 4:2:0 launch sequence (k_derive444 plane 0 --
 // the records without their chroma, the DPB tables' luma planes; its chroma goes to scratch),
 // then both chroma planes by k_c422_inter + k_c422_intra and, from the deblocking records that
 // sequence left, k_c422_db
@@ -872,6 +878,7 @@ static int run_422(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row0, 
     d.out_u = c->d444_chroma;
     d.out_v = c->d444_chroma + (size_t)P * 64 * nmb;
     if ((st = launch_all(c, d, s, row0, row1, c->sc))) return st;
+    if (c->fmt == 0) return H264R_OK;                       // 4:0:0: no chroma
     const int2 rows = make_int2(row0, row1);
     {
         Timed t(c, 0, s);
@@ -903,7 +910,7 @@ static int run_batch(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row0
     }
     c->last_stream = s;
     if (c->fmt == 3) return run_444(c, b, s, row0, row1);
-    if (c->fmt == 2) return run_422(c, b, s, row0, row1);
+    if (c->fmt == 2 || c->fmt == 0) return run_422(c, b, s, row0, row1);
     return launch_all(c, b, s, row0, row1, c->sc);
 }
 
@@ -1086,9 +1093,10 @@ int h264r_picture_end_async(h264r_ctx* c, int keep_slot)
     if (P.h_levels.empty()) P.h_levels.push_back(0);
     // 4:4:4: frame pictures only; a PCM MB's Cr view reads 128 entries past its block (run_444)
     if (c->fmt != 1 && P.h_pic.structure != H264R_FRAME) return H264R_EUNSUPPORTED;
-    if (c->fmt == 2)                                       // SP slices are 4:2:0 only (Extended profile)
+    if (c->fmt != 1)                                       // SP slices are 4:2:0 only (Extended profile)
         for (const h264r_slice& sl : P.h_slices) if (sl.slice_type == H264R_SLICE_SP) return H264R_EUNSUPPORTED;
     if (c->fmt == 3) P.h_levels.insert(P.h_levels.end(), 128, 0);
+    if (c->fmt == 0) P.h_levels.insert(P.h_levels.end(), 64, 0);     // the luma pass's chroma view of a PCM MB
     // every referenced slot must be loaded, with a frame of this picture's size (a field
     // picture: twice its height; its entries may name either field of a slot, include/h264r.h)
     const int fld = P.h_pic.structure != H264R_FRAME;

@@ -187,7 +187,8 @@ extern "C" __global__ __launch_bounds__(256) void k_untile(h264r_batch b, int2 r
 //   quant:   the plane's 4x4 and 8x8 lists in the luma slots (set_quant transform.cc:259-301);
 //   DPB tables: every plane entry of a slot -> the slot's plane pl (the luma MC reads it; the
 //            derived chroma reads stay inside it).
-// Field pictures are not on the 4:4:4 path: such a batch flags the device error word.
+// Field pictures and SP slices are not on the 4:4:4 / 4:2:2 / 4:0:0 paths: such a batch flags the
+// device error word.
 extern "C" __global__ __launch_bounds__(256) void k_derive444(h264r_batch b, int pl, h264r_mb* __restrict__ mbs,
                                                               h264r_slice* __restrict__ slices, h264r_quant* __restrict__ quant,
                                                               const uint8_t** __restrict__ refs, int ntab, int* err)
@@ -206,6 +207,7 @@ extern "C" __global__ __launch_bounds__(256) void k_derive444(h264r_batch b, int
     }
     for (int64_t i = t0; i < P * b.slice_stride; i += nt) {
         h264r_slice x = b.slices[i];
+        if (x.slice_type == H264R_SLICE_SP) atomicOr(err, 4);     // SP slices: 4:2:0 only (Extended profile)
         if (pl) {
             for (int l = 0; l < 2; ++l)
                 for (int r = 0; r < H264R_MAX_REFS; ++r) {

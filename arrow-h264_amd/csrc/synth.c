@@ -247,9 +247,11 @@ int h264r_synth_picture(const h264r_synth_cfg* c, int index, h264r_mb* mbs, int1
         c->num_slices > c->height_mbs || c->num_refs < 0 || c->num_refs > H264R_MAX_REFS ||
         c->structure < H264R_FRAME || c->structure > H264R_BOTTOM_FIELD ||
         (c->kind != H264R_SYNTH_INTRA && c->num_refs < 1) || c->qp_min < 0 || c->qp_max > 51 ||
-        c->qp_min > c->qp_max || ((c->chroma_format == 2 || c->chroma_format == 3) && c->structure != H264R_FRAME))
+        c->qp_min > c->qp_max || (c->chroma_format >= 2 && c->structure != H264R_FRAME) ||
+        c->chroma_format < 0 || c->chroma_format > 4)
         return H264R_EINVAL;
-    const int f444 = c->chroma_format == 3, f422 = c->chroma_format == 2;
+    const int f444 = c->chroma_format == 3, f422 = c->chroma_format == 2,
+              f400 = c->chroma_format == H264R_SYNTH_CHROMA_400;
     rng_t r = {c->seed * 0x100000001B3ull + (uint64_t)index * 0x9E3779B97F4A7C15ull + 1};
     int W = c->width_mbs, H = c->height_mbs, nmb = W * H;
     gen_t g = {c, W * 4, mbs, mv, ref_idx};
@@ -291,7 +293,7 @@ int h264r_synth_picture(const h264r_synth_cfg* c, int index, h264r_mb* mbs, int1
             m->flags = H264R_MBF_INTRA;
             m->cbp_blks = 0xFFFF;
             uint8_t* raw = (uint8_t*)(levels + off);
-            const int npcm = f444 ? 768 : f422 ? 512 : 384;   /* Y 256, Cb / Cr 64, 128 (4:2:2), 256 (4:4:4) */
+            const int npcm = f444 ? 768 : f422 ? 512 : f400 ? 256 : 384;   /* Y 256, Cb / Cr 64, 128 (4:2:2), 256 (4:4:4) */
             for (int k = 0; k < npcm; ++k) raw[k] = (uint8_t)rnd(&r, 256);
             off += npcm / 2;
             continue;
@@ -337,8 +339,8 @@ int h264r_synth_picture(const h264r_synth_cfg* c, int index, h264r_mb* mbs, int1
                 if (av[0] && av[1] && av[3]) md[k++] = 3;
                 m->chroma_mode = (uint8_t)pick_mode(&r, md, k);
             }
-            cbpc = f444 ? 0 : rnd(&r, 3);
-            if (f444) m->chroma_mode = 0;                 /* no chroma intra mode in 4:4:4 */
+            cbpc = f444 || f400 ? 0 : rnd(&r, 3);
+            if (f444 || f400) m->chroma_mode = 0;         /* no chroma intra mode in 4:4:4 / 4:0:0 */
         } else {
             int k = rnd(&r, 90);    /* conditional on inter: skip/16x16/16x8/8x16/8x8 = 15/45/10/10/10 */
             int mt = k < 15 ? H264R_P_SKIP : k < 60 ? H264R_P_16x16 : k < 70 ? H264R_P_16x8 : k < 80 ? H264R_P_8x16 : H264R_P_8x8;
@@ -368,7 +370,7 @@ int h264r_synth_picture(const h264r_synth_cfg* c, int index, h264r_mb* mbs, int1
                 break; }
             }
             int skip_res = mt == H264R_P_SKIP && (!bslice || rnd(&r, 2));
-            if (!skip_res) { cbpl = rnd(&r, 16); cbpc = f444 ? 0 : rnd(&r, 3); }
+            if (!skip_res) { cbpl = rnd(&r, 16); cbpc = f444 || f400 ? 0 : rnd(&r, 3); }
             if (t8 == -1) t8 = 0;
             else t8 = c->transform8x8 && cbpl && rnd(&r, 2);
             if (mt == H264R_P_SKIP && !bslice) t8 = 0;
@@ -405,7 +407,7 @@ int h264r_synth_picture(const h264r_synth_cfg* c, int index, h264r_mb* mbs, int1
             if (any8 && t8) blks |= (uint16_t)(0x33u << (((b8 >> 1) * 2) * 4 + (b8 & 1) * 2));
             off += 64;
         }
-        if (f422) {
+        if (f422 || f400) {
             /* 4:2:2 (include/h264r.h): the I_16x16 DC right after the luma blocks, then chroma AC
                (2 planes x 8 blocks x 16) and chroma DC (2 x 8, raster of the 2x4 matrix) */
             if (i16) {
@@ -491,9 +493,15 @@ int h264r_synth_refpic(uint64_t seed, int slot, int width_mbs, int height_mbs, u
 int h264r_synth_refpic_fmt(uint64_t seed, int slot, int width_mbs, int height_mbs, int chroma_format, uint8_t* y,
                            uint8_t* u, uint8_t* v)
 {
-    if (chroma_format != 2 && chroma_format != 3) return h264r_synth_refpic(seed, slot, width_mbs, height_mbs, y, u, v);
-    if (!y || !u || !v || width_mbs <= 0 || height_mbs <= 0) return H264R_EINVAL;
+    const int f400 = chroma_format == H264R_SYNTH_CHROMA_400;
+    if (!f400 && chroma_format != 2 && chroma_format != 3)
+        return h264r_synth_refpic(seed, slot, width_mbs, height_mbs, y, u, v);
+    if (!y || (!f400 && (!u || !v)) || width_mbs <= 0 || height_mbs <= 0) return H264R_EINVAL;
     uint64_t s = seed * 31 + (uint64_t)slot * 0x2545F4914F6CDD1Dull;
+    if (f400) {                                            /* 4:0:0: the luma plane only */
+        texture(s, y, width_mbs * 16, height_mbs * 16, 8);
+        return H264R_OK;
+    }
     const int cw = chroma_format == 3 ? 16 : 8;           /* 4:2:2: half width, full height */
     texture(s, y, width_mbs * 16, height_mbs * 16, 8);
     texture(s + 1, u, width_mbs * cw, height_mbs * 16, cw / 2);

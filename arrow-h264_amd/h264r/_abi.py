@@ -31,9 +31,18 @@ SYNTH_MAX_LEVELS_PER_MB_422 = 544
 SYNTH_MAX_LEVELS_PER_MB_444 = 816
 
 
+SYNTH_CHROMA_400 = 4            # h264r_synth_cfg.chroma_format of 4:0:0 (0, the default, is 4:2:0)
+
+
+def idc_of(synth_chroma_format: int) -> int:
+    """chroma_format_idc of a synth configuration's chroma_format (include/h264r_synth.h)."""
+    return {2: 2, 3: 3, SYNTH_CHROMA_400: 0}.get(int(synth_chroma_format), 1)
+
+
 def chroma_mb(chroma_format: int) -> tuple[int, int]:
-    """(width, height) of one MB's chroma in samples: 4:2:0 8 x 8, 4:2:2 8 x 16, 4:4:4 16 x 16."""
-    return {2: (8, 16), 3: (16, 16)}.get(int(chroma_format), (8, 8))
+    """(width, height) of one MB's chroma in samples by chroma_format_idc: 4:2:0 8 x 8, 4:2:2 8 x 16,
+    4:4:4 16 x 16, 4:0:0 none."""
+    return {0: (0, 0), 2: (8, 16), 3: (16, 16)}.get(int(chroma_format), (8, 8))
 
 
 def max_levels_per_mb(chroma_format: int) -> int:

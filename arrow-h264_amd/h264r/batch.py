@@ -56,7 +56,7 @@ def pack(pictures, quant: np.ndarray):
     q = np.repeat(np.ascontiguousarray(quant, A.QUANT_DTYPE).reshape(1), len(pictures))
     return dict(mbs=np.concatenate(mbs), levels=np.concatenate(lv), mv=np.stack(mv), ref_idx=np.stack(rr),
                 slices=np.concatenate(sl), pics=np.concatenate(pics), quant=q, stride=stride, W=W, H=H,
-                chroma_format=int(pictures[0].cfg.chroma_format))
+                chroma_format=A.idc_of(pictures[0].cfg.chroma_format))
 
 
 def to_device(host: dict, n: int, ref_planes_ptr: int | None, device: str = "cuda") -> DeviceBatch:

@@ -44,20 +44,29 @@ class Crop:
 
 @dataclass(frozen=True)
 class OutputGeometry:
-    """Cropped output sizes (output.cc:135-165) for 4:2:0 (SubWidthC = SubHeightC = 2)."""
+    """Cropped output sizes (output.cc:135-165)."""
     luma: tuple[int, int, int, int]      # (x0, y0, width, height) inside the coded luma plane
     chroma: tuple[int, int, int, int]
+    fake_uv: int = 0                     # 4:0:0: bytes of value 128 per chroma plane (output.cc:205-224)
 
     @property
     def frame_bytes(self) -> int:
         """iFrameSize (output.cc:164): one byte per sample at 8 bits."""
-        return self.luma[2] * self.luma[3] + 2 * self.chroma[2] * self.chroma[3]
+        return self.luma[2] * self.luma[3] + 2 * self.chroma[2] * self.chroma[3] + 2 * self.fake_uv
 
 
 def geometry(width_mbs: int, height_mbs: int, crop: Crop = Crop(), chroma_format: int = 1) -> OutputGeometry:
     """output.cc:135-165: size_x_l = PicWidthInMbs*16, size_x_c = PicWidthInMbs*MbWidthC;
     crop_*_c from the SPS (vertical offsets x (2 - frame_mbs_only_flag)), crop_*_l =
-    SubWidthC/SubHeightC x crop_*_c.  chroma_format 2 (4:2:2): SubHeightC 1; 3 (4:4:4): SubWidthC 1 too."""
+    SubWidthC/SubHeightC x crop_*_c.  chroma_format 2 (4:2:2): SubHeightC 1; 3 (4:4:4): SubWidthC 1 too;
+    0 (4:0:0): the cropped luma, then two planes of 128 of a quarter of its size (WriteUV,
+    output.cc:205-224: the reference fakes a 4:2:0 file)."""
+    if chroma_format == 0:                   # CropUnitX 1, CropUnitY 2 - frame_mbs_only_flag (7.4.2.1.1)
+        uy = 2 - crop.frame_mbs_only
+        lw, lh = 16 * width_mbs - (crop.left + crop.right), 16 * height_mbs - uy * (crop.top + crop.bottom)
+        if min(crop.left, crop.right, crop.top, crop.bottom) < 0 or lw <= 0 or lh <= 0:
+            raise ValueError(f"frame cropping {crop} leaves no picture of {width_mbs}x{height_mbs} MBs")
+        return OutputGeometry((crop.left, uy * crop.top, lw, lh), (0, 0, 0, 0), (lw * lh) // 4)
     sub_w, sub_h = (1 if chroma_format == 3 else 2), (2 if chroma_format == 1 else 1)
     lc, rc = crop.left, crop.right
     tc, bc = crop.top * (2 - crop.frame_mbs_only), crop.bottom * (2 - crop.frame_mbs_only)
@@ -83,11 +92,14 @@ def frame_bytes(y: np.ndarray, u: np.ndarray, v: np.ndarray, geom: OutputGeometr
     out = bytearray(geom.frame_bytes)
     mv = memoryview(out)
     off = 0
-    for p, rect, name in ((y, geom.luma, "Y"), (u, geom.chroma, "Cb"), (v, geom.chroma, "Cr")):
+    planes = ((y, geom.luma, "Y"),) if geom.fake_uv else ((y, geom.luma, "Y"), (u, geom.chroma, "Cb"), (v, geom.chroma, "Cr"))
+    for p, rect, name in planes:
         view = _plane_view(np.asarray(p), rect, name)
         n = view.size
         mv[off:off + n] = np.ascontiguousarray(view).reshape(-1).data
         off += n
+    if geom.fake_uv:
+        mv[off:] = b"\x80" * (2 * geom.fake_uv)
     return bytes(out)
 
 

@@ -41,8 +41,8 @@ def picture(lib: C.CDLL, cfg: A.SynthCfg, index: int) -> Picture:
     W, H = cfg.width_mbs, cfg.height_mbs
     n = W * H
     mbs = np.zeros(n, A.MB_DTYPE)
-    f444 = cfg.chroma_format == 3
-    levels = np.zeros(n * A.max_levels_per_mb(cfg.chroma_format), np.int16)
+    idc = A.idc_of(cfg.chroma_format)
+    levels = np.zeros(n * A.max_levels_per_mb(idc), np.int16)
     mv = np.zeros((2, 4 * H, 4 * W), np.uint32)
     ref_idx = np.zeros((2, 4 * H, 4 * W), np.int8)
     slices = np.zeros(cfg.num_slices, A.SLICE_DTYPE)
@@ -52,8 +52,9 @@ def picture(lib: C.CDLL, cfg: A.SynthCfg, index: int) -> Picture:
                                  A.ptr(mv), A.ptr(ref_idx), A.ptr(slices), A.ptr(pic))
     if st != A.OK:
         raise ValueError(f"h264r_synth_picture -> {st}")
-    # 4:4:4: a PCM MB's Cr view reads 128 entries past its 384 (include/h264r.h): kept readable
-    keep = max(int(nlev.value), 8) + (128 if f444 else 0)
+    # 4:4:4: a PCM MB's Cr view reads 128 entries past its 384, 4:0:0 its chroma view 64 past its 128
+    # (include/h264r.h): kept readable
+    keep = max(int(nlev.value), 8) + (128 if idc == 3 else 64 if idc == 0 else 0)
     return Picture(cfg, index, mbs, levels[:keep].copy(), mv, ref_idx, slices, pic)
 
 
@@ -61,7 +62,7 @@ def refpics(lib: C.CDLL, cfg: A.SynthCfg, nslots: int | None = None):
     """[(y, u, v)] for DPB slots 0..n-1: the frames the pictures reference (a field cfg's
     references are fields of frames of twice its height, include/h264r_synth.h)."""
     W, H = cfg.width_mbs, cfg.height_mbs * (2 if cfg.structure else 1)
-    cw, ch = A.chroma_mb(cfg.chroma_format)
+    cw, ch = A.chroma_mb(A.idc_of(cfg.chroma_format))
     out = []
     for s in range(lib.h264r_synth_ref_frames(C.byref(cfg)) if nslots is None else nslots):
         y = np.zeros((16 * H, 16 * W), np.uint8)

@@ -1,7 +1,7 @@
 // h264dec_main.cc -- command-line decoder over the repo's own parser (h264p) and the h264r
 // reconstruction ABI: `h264dec -i stream.264 -o out.yuv [-d device]`, the reference's
 // `ldecod -i -o` (core/main.cc) for the path this repo covers.  Frames are written in output
-// order, cropped to the SPS window, 8-bit planar 4:2:0, 4:2:2 or 4:4:4 (write_out_picture, output.cc:109-227).
+// order, cropped to the SPS window, 8-bit planar 4:2:0, 4:2:2 or 4:4:4, or 4:0:0 with 128-valued 4:2:0 chroma (write_out_picture, output.cc:109-227).
 // Linked against libh264r.so it decodes on MI355X; the test build links the CPU
 // implementation of the same ABI instead (oracle/Makefile h264dec_cpu).
 // `-r N`: decode the stream N more times after the written pass and print the wall time per
@@ -22,6 +22,14 @@ static int write_frame(void* user, const h264p_frame* f)
     const int y0 = f->crop_top, y1 = f->height - f->crop_bottom;
     for (int y = y0; y < y1; ++y)
         if (fwrite(f->y + (size_t)y * f->width + x0, 1, x1 - x0, out) != (size_t)(x1 - x0)) return 1;
+    if (f->chroma_format == 0) {
+        // 4:0:0: two planes of 128 a quarter of the cropped luma each, as the reference's WriteUV
+        // default fakes a 4:2:0 file (output.cc:205-224)
+        const std::vector<uint8_t> fake((size_t)(x1 - x0) * (y1 - y0) / 4, 128);
+        for (int k = 0; k < 2; ++k)
+            if (fwrite(fake.data(), 1, fake.size(), out) != fake.size()) return 1;
+        return 0;
+    }
     // log2 SubWidthC / SubHeightC: 4:2:2 keeps every row, 4:4:4 every row and column
     const int sh = f->chroma_format == 1 ? 1 : 0, sw = f->chroma_format == 3 ? 0 : 1;
     const int cw = f->width >> sw, n = (x1 - x0) >> sw;

@@ -897,8 +897,8 @@ void Decoder::parse_slice_header(Bits& b, SliceHeader& h)
     require(pps_[h.pps_id].valid, "slice: pic_parameter_set_id of no PPS");
     const Pps& pps = pps_[h.pps_id];
     const Sps& sps = sps_[pps.sps_id];
-    unsupported(sps.chroma_format_idc < 1 || sps.separate_planes || sps.bit_depth_y != 8 || sps.bit_depth_c != 8,
-                "picture format (4:2:0, 4:2:2 or 4:4:4 without separate colour planes, 8-bit only)");
+    unsupported(sps.separate_planes || sps.bit_depth_y != 8 || (sps.chroma_format_idc && sps.bit_depth_c != 8),
+                "picture format (4:0:0, 4:2:0, 4:2:2 or 4:4:4 without separate colour planes, 8-bit only)");
     unsupported(sps.chroma_format_idc == 3 && pps.cabac, "4:4:4 with CABAC (entropy_coding_mode_flag)");
     unsupported(sps.mbaff, "MBAFF coding (mb_adaptive_frame_field_flag)");
     unsupported(sps.poc_type == 1, "pic_order_cnt_type 1");
@@ -949,8 +949,9 @@ void Decoder::parse_slice_header(Bits& b, SliceHeader& h)
     }
     // pred_weight_table (7.3.3.2; interpret_rbsp.cc:832-905)
     if ((pps.weighted_pred && P) || (pps.weighted_bipred_idc == 1 && B)) {
+        const bool chroma = sps.chroma_format_idc != 0;        // ChromaArrayType 0: luma weights only
         h.luma_log2_wd = b.ue_max(7, "slice: luma_log2_weight_denom");
-        h.chroma_log2_wd = b.ue_max(7, "slice: chroma_log2_weight_denom");
+        h.chroma_log2_wd = chroma ? b.ue_max(7, "slice: chroma_log2_weight_denom") : 0;   // absent: the header field stays 0
         for (int l = 0; l < (B ? 2 : 1); ++l)
             for (int i = 0; i < h.nref[l]; ++i) {
                 h.weight[l][i][0] = 1 << h.luma_log2_wd;
@@ -959,9 +960,9 @@ void Decoder::parse_slice_header(Bits& b, SliceHeader& h)
                     h.weight[l][i][0] = b.se_in(-128, 127, "slice: luma_weight");
                     h.offset[l][i][0] = b.se_in(-128, 127, "slice: luma_offset");
                 }
-                const bool cf = b.u(1);
+                const bool cf = chroma && b.u(1);
                 for (int j = 1; j < 3; ++j) {
-                    h.weight[l][i][j] = 1 << h.chroma_log2_wd;
+                    h.weight[l][i][j] = chroma ? 1 << h.chroma_log2_wd : 0;      // 4:0:0: left 0, as the reference
                     h.offset[l][i][j] = 0;
                     if (cf) {
                         h.weight[l][i][j] = b.se_in(-128, 127, "slice: chroma_weight");
@@ -1590,7 +1591,7 @@ void Decoder::collect()
     if (inflight_ < 0) return;
     Output& o = pending_[inflight_];
     inflight_ = -1;
-    const size_t n = (size_t)o.W * o.H, cs = n * (o.cf == 3 ? 256 : o.cf == 2 ? 128 : 64);
+    const size_t n = (size_t)o.W * o.H, cs = n * (o.cf == 3 ? 256 : o.cf == 2 ? 128 : o.cf == 1 ? 64 : 0);
     if (o.y.size() != n * 256 || o.u.size() != cs) {
         o.y.assign(n * 256, 0);
         o.u.assign(cs, 0);
@@ -1626,7 +1627,7 @@ void Decoder::flush_output()
         f.y = o.y.data(); f.u = o.u.data(); f.v = o.v.data();
         f.width = o.W * 16;
         f.height = o.H * 16;
-        const int sub_h = o.cf == 1 ? 2 : 1, sub_w = o.cf == 3 ? 1 : 2;   // SubHeightC, SubWidthC
+        const int sub_h = o.cf == 1 ? 2 : 1, sub_w = o.cf == 1 || o.cf == 2 ? 2 : 1;   // CropUnitY / X per crop unit
         f.crop_left = sub_w * o.crop[0]; f.crop_right = sub_w * o.crop[1];
         f.crop_top = sub_h * o.crop[2]; f.crop_bottom = sub_h * o.crop[3];
         f.chroma_format = o.cf;
@@ -1641,7 +1642,8 @@ void Decoder::flush_output()
 SliceCtx::SliceCtx(Decoder& d, const Sps& s, const Pps& p, const SliceHeader& h, int nr, Bits& bits,
                    Picture* const (*lists)[33], const int* list_n, int end)
     : D(d), sps(s), pps(p), sh(h), slice_nr(nr), b(bits), W(s.W), H(h.field ? s.H / 2 : s.H),
-      cf(s.chroma_format_idc), mwc(s.chroma_format_idc == 3 ? 16 : 8), mhc(s.chroma_format_idc == 1 ? 8 : 16),
+      cf(s.chroma_format_idc), mwc(s.chroma_format_idc == 3 ? 16 : s.chroma_format_idc ? 8 : 0),
+      mhc(s.chroma_format_idc == 1 ? 8 : s.chroma_format_idc ? 16 : 0),
       zz4(h.field ? FIELD_SCAN4X4 : ZZ4), zz8(h.field ? FIELD_SCAN8X8 : ZZ8), qp(h.qp), list_(lists), list_n_(list_n),
       end_mb(end)
 {
@@ -1852,7 +1854,7 @@ void SliceCtx::macroblock()
             cbp = cabac_cbp();
             if (!cbp) last_dquant = 0;
         } else {
-            if (cf == 3) {                 // Table 9-4, ChromaArrayType 0 / 3: no chroma CBP
+            if (cf == 0 || cf == 3) {      // Table 9-4, ChromaArrayType 0 / 3: no chroma CBP
                 const int code = b.ue_max(15, "coded_block_pattern");
                 cbp = m.intra ? CBP_ME_INTRA_444[code] : CBP_ME_INTER_444[code];
             } else {
@@ -1940,8 +1942,8 @@ void SliceCtx::intra_pred_modes()
             m.i8[k] = (uint8_t)(prev ? pred : rem < pred ? rem : rem + 1);
         }
     }
-    if (cf == 3) {
-        // no intra_chroma_pred_mode in 4:4:4 (7.3.5.1: ChromaArrayType 1 or 2)
+    if (cf == 0 || cf == 3) {
+        // no intra_chroma_pred_mode in 4:0:0 / 4:4:4 (7.3.5.1: ChromaArrayType 1 or 2)
     } else if (cab) {
         // TU cMax 3: bin 0 at A / B available with a non-DC chroma mode (not I_PCM), then 3
         int inc0 = 0;
@@ -2391,7 +2393,7 @@ void SliceCtx::residual()
     // residual_luma for Y, and for Cb and Cr as luma in 4:4:4 (interpret_residual.cc:497-505);
     // cbp_blks is the luma plane's (the record's, deblock.cc:135,212)
     for (int p = 0; p < (cf == 3 ? 3 : 1); ++p) {
-    const uint16_t bmask = p == 0 ? 0xFFFF : 0;
+    const uint16_t bmask = p == 0 ? 0xFFFF : 0;                  // (4:0:0: the luma plane only)
     if (i16) {
         block(LUMA_16DC, p, false, false, 0, 0, 16, pl_, &n);
         for (int k = 0; k < n; ++k) {
@@ -2435,7 +2437,7 @@ void SliceCtx::residual()
         }
     }
     }
-    if (cf == 3) return;
+    if (cf == 3 || cf == 0) return;
     // chroma: 4 (4:2:0) or 8 (4:2:2) 4x4 blocks and DC coefficients per plane; the 4:2:2 DC scan
     // (inverse_scan_chroma_dc transform.cc:365-374, the field 4x4 scan's first 8 positions) as
     // raster indices of the 2-wide DC matrix
@@ -2581,6 +2583,7 @@ int SliceCtx::cabac_cbp()
             const int inc = ((ca & (1 << ia)) == 0 ? 1 : 0) + 2 * ((cb & (1 << ib)) == 0 ? 1 : 0);
             if (c.dec(CTX_CBP_L_CONTEXTS + inc)) cbp += 1 << (y0 + (x0 >> 1));
         }
+    if (cf == 0 || cf == 3) return cbp;                   // no chroma bins (interpret_se.cc:429)
     auto f = [](MbState* n, bool two) { return n && (n->mb_type == H264R_I_PCM || (two ? n->cbpc == 2 : n->cbpc != 0)); };
     const int inc0 = f(A, false) + 2 * f(Bm, false), inc1 = f(A, true) + 2 * f(Bm, true) + 4;
     if (c.dec(CTX_CBP_C_CONTEXTS + inc0)) cbp += c.dec(CTX_CBP_C_CONTEXTS + inc1) ? 32 : 16;
@@ -2759,9 +2762,9 @@ void SliceCtx::stage()
         for (int p = 0; p < 2; ++p)
             for (int y = 0; y < mhc; ++y)
                 for (int x = 0; x < mwc; ++x) raw[256 + p * mwc * mhc + y * mwc + x] = (uint8_t)cof[1 + p][y][x];
-    } else if (cf == 3) {
-        // three luma-like blocks (include/h264r.h, 4:4:4): Y, Cb, Cr
-        for (int p = 0; p < 3; ++p) {
+    } else if (cf == 3 || cf == 0) {
+        // three luma-like blocks (include/h264r.h, 4:4:4): Y, Cb, Cr; 4:0:0 the luma one
+        for (int p = 0; p < (cf == 3 ? 3 : 1); ++p) {
             for (int b8 = 0; b8 < 4; ++b8) {
                 if (!((cbpl >> b8) & 1)) continue;
                 const int x8 = (b8 & 1) * 8, y8 = (b8 >> 1) * 8;

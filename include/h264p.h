@@ -25,8 +25,8 @@
  * The reconstruction calls are resolved at link time: against libh264r.so (MI355X) for the
  * product, against the CPU implementation of the same ABI in tests.  Status codes are the
  * h264r ones (H264R_OK / H264R_E*).  H264R_EUNSUPPORTED: MBAFF, FMO, data partitioning, formats
- * other than 4:2:0, and 4:2:2 / 4:4:4 (CAVLC, frame pictures, no separate colour planes) 8-bit,
- * POC type 1, MMCO 5, SI slices (as in the reconstruction path).
+ * other than 4:2:0, 4:0:0 and 4:2:2 (frame pictures) or 4:4:4 (CAVLC, frame pictures, no separate
+ * colour planes) 8-bit, POC type 1, MMCO 5, SI slices (as in the reconstruction path).
  */
 #ifndef H264P_H_
 #define H264P_H_
@@ -51,7 +51,8 @@ typedef struct h264p_frame {
     int32_t crop_left, crop_right, crop_top, crop_bottom;
     int32_t poc;
     int32_t period;
-    int32_t chroma_format;   /* chroma_format_idc: 1 (u, v: 8 W x 8 H), 2 (8 W x 16 H) or 3 (16 W x 16 H) */
+    int32_t chroma_format;   /* chroma_format_idc: 1 (u, v: 8 W x 8 H), 2 (8 W x 16 H), 3 (16 W x 16 H) or
+                                0 (4:0:0: no u, v) */
 } h264p_frame;
 
 /* Output callback: return 0 to continue, non-zero to stop decoding (h264p_decode then

@@ -26,6 +26,8 @@ extern "C" {
 /* Upper bound of int16 level-pool entries one MB can use: 4:2:0 4*64+128+16+8 (rounded to 8);
  * 4:2:2 4*64+16+256+16; 4:4:4 three luma-like blocks 3*(4*64+16), and a PCM MB's plane-2 view
  * reads 128 entries past its 384 (include/h264r.h, 4:4:4). */
+#define H264R_SYNTH_CHROMA_400 4       /* h264r_synth_cfg.chroma_format for 4:0:0 (0 stays 4:2:0) */
+
 #define H264R_SYNTH_MAX_LEVELS_PER_MB 416
 #define H264R_SYNTH_MAX_LEVELS_PER_MB_422 544
 #define H264R_SYNTH_MAX_LEVELS_PER_MB_444 816
@@ -63,7 +65,9 @@ typedef struct h264r_synth_cfg {
                                     luma-like level blocks per MB, CodedBlockPatternChroma 0, a PCM MB
                                     3 x 256 samples; frame pictures); 2 = 4:2:2 (chroma 8 x 16 per MB:
                                     8 chroma 4x4 blocks and 8 DC levels per plane, the layout of
-                                    include/h264r.h; frame pictures); anything else = 4:2:0            */
+                                    include/h264r.h; frame pictures); H264R_SYNTH_CHROMA_400 = 4:0:0 (luma
+                                    only: cbp_chroma 0, a PCM MB 256 samples; frame pictures); anything
+                                    else (0 -- the default -- or 1) = 4:2:0                              */
     uint64_t seed;
 } h264r_synth_cfg;
 
@@ -81,8 +85,9 @@ int  h264r_synth_picture(const h264r_synth_cfg* cfg, int index, h264r_mb* mbs, i
 /* Deterministic reference-picture content for DPB slot `slot` (smooth texture + noise). */
 int  h264r_synth_refpic(uint64_t seed, int slot, int width_mbs, int height_mbs,
                         uint8_t* y, uint8_t* u, uint8_t* v);
-/* The same for a chroma format: 3 = 4:4:4, chroma planes of the luma plane's size; 2 = 4:2:2,
- * chroma planes of half the luma width and its full height (the 4:2:0 content of
+/* The same for a chroma format (h264r_synth_cfg.chroma_format): 3 = 4:4:4, chroma planes of the
+ * luma plane's size; 2 = 4:2:2, chroma planes of half the luma width and its full height;
+ * H264R_SYNTH_CHROMA_400, the luma plane only (u, v may be NULL) (the 4:2:0 content of
  * h264r_synth_refpic otherwise). */
 int  h264r_synth_refpic_fmt(uint64_t seed, int slot, int width_mbs, int height_mbs, int chroma_format,
                             uint8_t* y, uint8_t* u, uint8_t* v);

@@ -102,12 +102,12 @@ int h264r_create(h264r_ctx** out, int device, int max_w, int max_h, int chroma_f
 {
     (void)device;
     if (!out || max_w <= 0 || max_h <= 0) return H264R_EINVAL;
-    if (chroma_format_idc < 1 || chroma_format_idc > 3 || bit_depth != 8) return H264R_EUNSUPPORTED;
+    if (chroma_format_idc < 0 || chroma_format_idc > 3 || bit_depth != 8) return H264R_EUNSUPPORTED;
     h264r_ctx* c = (h264r_ctx*)calloc(1, sizeof(h264r_ctx));
     if (!c) return H264R_ENOMEM;
     c->max_w = max_w; c->max_h = max_h;
     c->cf = chroma_format_idc;
-    c->cb = chroma_format_idc == 3 ? 256 : chroma_format_idc == 2 ? 128 : 64;
+    c->cb = chroma_format_idc == 3 ? 256 : chroma_format_idc == 2 ? 128 : chroma_format_idc == 1 ? 64 : 0;
     *out = c;
     return H264R_OK;
 }
@@ -144,12 +144,14 @@ static int ensure_slot(h264r_ctx* c, int s, int w, int h)
 
 int h264r_set_ref(h264r_ctx* c, int slot, const uint8_t* y, const uint8_t* u, const uint8_t* v, int w, int h)
 {
-    if (!c || slot < 0 || slot >= H264R_MAX_SLOTS || !y || !u || !v) return H264R_EINVAL;
+    if (!c || slot < 0 || slot >= H264R_MAX_SLOTS || !y || (c->cb && (!u || !v))) return H264R_EINVAL;
     int st = ensure_slot(c, slot, w, h);
     if (st) return st;
     memcpy(c->slot[slot][0], y, (size_t)w * h * 256);
-    memcpy(c->slot[slot][1], u, (size_t)w * h * c->cb);
-    memcpy(c->slot[slot][2], v, (size_t)w * h * c->cb);
+    if (c->cb) {
+        memcpy(c->slot[slot][1], u, (size_t)w * h * c->cb);
+        memcpy(c->slot[slot][2], v, (size_t)w * h * c->cb);
+    }
     return H264R_OK;
 }
 
@@ -219,7 +221,8 @@ int h264r_mb_submit(h264r_ctx* c, int addr, const h264r_mb* mb, const int16_t* l
 }
 
 /* Capture record (little-endian): int32 header[8] = {'H4RC', W, H, num_slices, n_levels,
- * keep_slot, chroma_format_idc, 0}, then mbs, levels, mv, ref_idx, slices, pic, quant, Y, Cb, Cr. */
+ * keep_slot, chroma_format_idc, 1}, then mbs, levels, mv, ref_idx, slices, pic, quant, Y, Cb, Cr
+ * (header[7] 1: header[6] holds the chroma format; 0 in captures older than that: 4:2:0). */
 static void capture(const h264r_ctx* c, int keep, uint8_t* const out[3])
 {
     const char* path = getenv("H264R_CAPTURE");
@@ -227,7 +230,7 @@ static void capture(const h264r_ctx* c, int keep, uint8_t* const out[3])
     FILE* f = fopen(path, "ab");
     if (!f) return;
     const size_t n = (size_t)c->pw * c->ph;
-    int32_t hdr[8] = {0x43523448, c->pw, c->ph, c->pic.num_slices, (int32_t)c->n_levels, keep, c->cf, 0};
+    int32_t hdr[8] = {0x43523448, c->pw, c->ph, c->pic.num_slices, (int32_t)c->n_levels, keep, c->cf, 1};
     fwrite(hdr, 4, 8, f);
     fwrite(c->mbs, sizeof(h264r_mb), n, f);
     fwrite(c->levels, 2, c->n_levels, f);
@@ -248,8 +251,14 @@ static int picture_end(h264r_ctx* c, uint8_t* y, uint8_t* u, uint8_t* v, int kee
     c->in_pic = 0;
     const int n = c->pw * c->ph;
     for (int a = 0; a < n; ++a) if (!c->seen[a]) return H264R_ESTATE;
-    if (keep >= H264R_MAX_SLOTS || !y || !u || !v) return H264R_EINVAL;
+    if (keep >= H264R_MAX_SLOTS || !y || (c->cb && (!u || !v))) return H264R_EINVAL;
     if (!c->levels) { c->levels = (int16_t*)calloc(8, 2); c->cap_levels = 8; }
+    if (c->cf == 0 && c->cap_levels < c->n_levels + 64) {     /* the chroma view of a 4:0:0 PCM MB */
+        int16_t* q = (int16_t*)realloc(c->levels, (c->n_levels + 64) * 2);
+        if (!q) return H264R_ENOMEM;
+        memset(q + c->cap_levels, 0, (c->n_levels + 64 - c->cap_levels) * 2);
+        c->levels = q; c->cap_levels = c->n_levels + 64;
+    }
     if (c->pic.structure < H264R_FRAME || c->pic.structure > H264R_BOTTOM_FIELD) return H264R_EINVAL;
     /* a field picture's slots are frames of twice its height (include/h264r.h) */
     const int fld = c->pic.structure != H264R_FRAME, frame_h = c->ph << fld;

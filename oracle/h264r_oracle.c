@@ -1281,10 +1281,13 @@ static int derive_plane(const oracle_picture* p, int pl, oracle_picture* d, h264
     return 0;
 }
 
+/* 4:0:0 (ChromaArrayType 0): the luma of a 4:2:0 picture, no chroma at all (decoder.cc:199,
+   deblock.cc:498,522 skip the chroma of ChromaArrayType 0) -- the first of decode_444's passes. */
 static int decode_444(const oracle_picture* p, int what /* 1 reconstruct, 2 deblock, 3 both */)
 {
     int st = 0;
-    for (int pl = 0; pl < 3 && !st; ++pl) {
+    const int np = p->chroma_format == 0 ? 1 : 3;
+    for (int pl = 0; pl < np && !st; ++pl) {
         oracle_picture d;
         h264r_mb* mbs = NULL; h264r_slice* sl = NULL; h264r_quant* q = NULL; uint8_t* scratch = NULL;
         st = derive_plane(p, pl, &d, &mbs, &sl, &q, &scratch);
@@ -1310,7 +1313,7 @@ static int init_state(pstate* s, const oracle_picture* p)
 
 int oracle_deblock_picture(const oracle_picture* p)
 {
-    if (p->chroma_format == 3) return decode_444(p, 2);
+    if (p->chroma_format == 3 || p->chroma_format == 0) return decode_444(p, 2);
     int n = p->width_mbs * p->height_mbs;
     pstate s;
     int st0 = init_state(&s, p);
@@ -1345,7 +1348,7 @@ int oracle_deblock_picture(const oracle_picture* p)
 
 int oracle_reconstruct_picture(const oracle_picture* p)
 {
-    if (p->chroma_format == 3) return decode_444(p, 1);
+    if (p->chroma_format == 3 || p->chroma_format == 0) return decode_444(p, 1);
     int n = p->width_mbs * p->height_mbs;
     pstate s;
     int st0 = init_state(&s, p);
@@ -1361,7 +1364,7 @@ int oracle_reconstruct_picture(const oracle_picture* p)
 
 int oracle_decode_picture(const oracle_picture* p)
 {
-    if (p->chroma_format == 3) return decode_444(p, 3);
+    if (p->chroma_format == 3 || p->chroma_format == 0) return decode_444(p, 3);
     int st = oracle_reconstruct_picture(p);
     if (st) return st;
     return oracle_deblock_picture(p);

@@ -32,7 +32,8 @@ typedef struct oracle_picture {
     const h264r_quant*  quant;
     const uint8_t*      ref_planes[H264R_MAX_SLOTS][3];   /* host planes per DPB slot */
     uint8_t*            out[3];       /* Y, Cb, Cr (unpadded, pitch = width)     */
-    int                 chroma_format;/* 2 = 4:2:2 (chroma W/2 x H), 3 = 4:4:4 (planes of the luma size), else 4:2:0 */
+    int                 chroma_format;/* 0 = 4:0:0 (luma only), 2 = 4:2:2 (chroma W/2 x H), 3 = 4:4:4 (planes of the
+                                         luma size), else 4:2:0 */
 } oracle_picture;
 
 /* Transform::init/set_quant with flat matrices (transform.cc:173-180, 259-302). */

@@ -32,6 +32,8 @@
  * through coeff_chroma_dc at the scan index the reference's own inverse_scan_chroma_dc maps to
  * their raster position (transform.cc:365-374), the AC levels of the 8 blocks per plane through
  * coeff_chroma_ac, and the references take the 4:2:2 chroma pads (picture.cc:27-29).
+ * chroma_format 4 (H264R_SYNTH_CHROMA_400) decodes a 4:0:0 picture (High, ChromaArrayType 0): no chroma planes anywhere
+ * (picture.cc:34, decoder.cc:199, deblock.cc:498,522); the output holds the luma plane alone.
  * Output: Y plane then Cb then Cr, 8-bit, unpadded.
  *
  * Timing mode (H264R_TIME_REPS=<n>): the reconstruction of the picture -- the
@@ -98,8 +100,8 @@ int main(int argc, char** argv)
     if (argc > k + 2) cfg.sp_slices = atoi(argv[k + 2]);
     if (argc > k + 3) cfg.structure = atoi(argv[k + 3]);
     if (argc > k + 4) cfg.chroma_format = atoi(argv[k + 4]);
-    const bool f444 = cfg.chroma_format == 3, f422 = cfg.chroma_format == 2;
-    const int CW = f444 ? 16 : 8, CH = f444 || f422 ? 16 : 8;   /* chroma samples per MB: width, height */
+    const bool f444 = cfg.chroma_format == 3, f422 = cfg.chroma_format == 2, f400 = cfg.chroma_format == H264R_SYNTH_CHROMA_400;
+    const int CW = f400 ? 0 : f444 ? 16 : 8, CH = f400 ? 0 : f444 || f422 ? 16 : 8;   /* chroma samples per MB */
     const bool fld = cfg.structure != H264R_FRAME;
     const PictureStructure pstruct = cfg.structure == H264R_TOP_FIELD ? TOP_FIELD
                                    : cfg.structure == H264R_BOTTOM_FIELD ? BOTTOM_FIELD : FRAME;
@@ -122,8 +124,8 @@ int main(int argc, char** argv)
     sps_t* sps = new sps_t();
     pps_t* pps = new pps_t();
     sps->profile_idc = f444 ? 244 : f422 ? 122 : 100; sps->level_idc = 51;
-    sps->chroma_format_idc = f444 ? 3 : f422 ? 2 : 1; sps->ChromaArrayType = sps->chroma_format_idc;
-    sps->SubWidthC = f444 ? 1 : 2; sps->SubHeightC = CH == 16 ? 1 : 2; sps->MbWidthC = CW; sps->MbHeightC = CH;
+    sps->chroma_format_idc = f444 ? 3 : f422 ? 2 : f400 ? 0 : 1; sps->ChromaArrayType = sps->chroma_format_idc;
+    sps->SubWidthC = f444 ? 1 : 2; sps->SubHeightC = CH == 8 ? 2 : 1; sps->MbWidthC = CW; sps->MbHeightC = CH;
     sps->BitDepthY = 8; sps->BitDepthC = 8;
     sps->frame_mbs_only_flag = !fld; sps->direct_8x8_inference_flag = 1;
     const int FH = fld ? 2 * H : H;                     /* FrameHeightInMbs */
@@ -159,7 +161,7 @@ int main(int argc, char** argv)
        references are the fields of the DPB frames, refs[2 s + bottom] */
     const int nfr = h264r_synth_ref_frames(&cfg);
     std::vector<storable_picture*> refs(fld ? 2 * nfr : nfr);
-    std::vector<uint8_t> ty(W * 16 * FH * 16), tu(W * CW * FH * CH), tv(W * CW * FH * CH);
+    std::vector<uint8_t> ty(W * 16 * FH * 16), tu(W * CW * FH * CH + 1), tv(W * CW * FH * CH + 1);
     for (int s = 0; s < nfr; ++s) {
         h264r_synth_refpic_fmt(cfg.seed, s, W, FH, cfg.chroma_format, ty.data(), tu.data(), tv.data());
         for (int f = 0; f < (fld ? 2 : 1); ++f) {
@@ -172,8 +174,10 @@ int main(int argc, char** argv)
                 r->imgUV[1][y][x] = tv[(y * step + f) * W * CW + x];
             }
             pad_buf(*r->imgY, W * 16, H * 16, r->iLumaStride, MCBUF_LUMA_PAD_X, MCBUF_LUMA_PAD_Y);
-            pad_buf(*r->imgUV[0], W * CW, H * CH, r->iChromaStride, r->iChromaPadX, r->iChromaPadY);
-            pad_buf(*r->imgUV[1], W * CW, H * CH, r->iChromaStride, r->iChromaPadX, r->iChromaPadY);
+            if (!f400) {
+                pad_buf(*r->imgUV[0], W * CW, H * CH, r->iChromaStride, r->iChromaPadX, r->iChromaPadY);
+                pad_buf(*r->imgUV[1], W * CW, H * CH, r->iChromaStride, r->iChromaPadX, r->iChromaPadY);
+            }
             r->poc = r->frame_poc = r->top_poc = r->bottom_poc = h264r_synth_slot_poc(s) + f;
             r->is_long_term = 0; r->used_for_reference = 1;
             refs[fld ? 2 * s + f : s] = r;

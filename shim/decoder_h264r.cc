@@ -192,8 +192,8 @@ void begin_picture(Shim& S, slice_t& slice)
     if (S.pic == pic) return;
     const sps_t& sps = *slice.active_sps;
     const int cf = sps.chroma_format_idc;
-    if (cf < 1 || cf > 3 || sps.separate_colour_plane_flag || sps.BitDepthY != 8 || sps.BitDepthC != 8)
-        check(H264R_EUNSUPPORTED, "picture format (4:2:0, 4:2:2 or 4:4:4 without separate planes, 8-bit)");
+    if (cf < 0 || cf > 3 || sps.separate_colour_plane_flag || sps.BitDepthY != 8 || (cf && sps.BitDepthC != 8))
+        check(H264R_EUNSUPPORTED, "picture format (4:0:0, 4:2:0, 4:2:2 or 4:4:4 without separate planes, 8-bit)");
     if (slice.header.MbaffFrameFlag) check(H264R_EUNSUPPORTED, "MBAFF frames");
     if (cf != 1 && slice.header.field_pic_flag) check(H264R_EUNSUPPORTED, "4:2:2 / 4:4:4 field pictures");
     // the context holds frames; a field picture is PicHeightInMbs = FrameHeightInMbs / 2 rows
@@ -469,8 +469,8 @@ void Decoder::decode(mb_t& mb)
     std::vector<int16_t>& lv = st.levels;
     lv.clear();
     const int cfi = slice.active_sps->chroma_format_idc;
-    const bool f422 = cfi == 2, f444 = cfi == 3;
-    const int MWc = f444 ? 16 : 8, MHc = cfi == 1 ? 8 : 16, nbc = f422 ? 8 : 4;   // MbWidthC, MbHeightC, 4x4 blocks
+    const bool f422 = cfi == 2, f444 = cfi == 3, f400 = cfi == 0;
+    const int MWc = f400 ? 0 : f444 ? 16 : 8, MHc = f400 ? 0 : cfi == 1 ? 8 : 16, nbc = f422 ? 8 : 4;   // MbWidthC, MbHeightC
     if (mb.mb_type == I_PCM) {
         lv.resize(128 + MWc * MHc);
         uint8_t* raw = reinterpret_cast<uint8_t*>(lv.data());
@@ -478,9 +478,10 @@ void Decoder::decode(mb_t& mb)
         for (int p = 0; p < 2; ++p)
             for (int y = 0; y < MHc; ++y)
                 for (int x = 0; x < MWc; ++x) raw[256 + p * MWc * MHc + y * MWc + x] = (uint8_t)cof[1 + p][y][x];
-    } else if (f444) {
-        // three luma-like blocks, Y then Cb then Cr: the coded 8x8 blocks, then the I_16x16 DC
-        for (int pl = 0; pl < 3; ++pl) {
+    } else if (f444 || f400) {
+        // three luma-like blocks, Y then Cb then Cr (4:0:0: the luma one): the coded 8x8 blocks,
+        // then the I_16x16 DC
+        for (int pl = 0; pl < (f400 ? 1 : 3); ++pl) {
             for (int b8 = 0; b8 < 4; ++b8) {
                 if (!((cbpl >> b8) & 1)) continue;
                 const int x8 = (b8 & 1) * 8, y8 = (b8 >> 1) * 8;
@@ -645,7 +646,8 @@ void Decoder::deblock_filter(slice_t& slice)
         for (auto it = S.slot_of.begin(); it != S.slot_of.end();)
             it = it->second.slot == keep ? S.slot_of.erase(it) : std::next(it);
     }
-    const int MWc = S.ctx_cf == 3 ? 16 : 8, MHc = S.ctx_cf == 1 ? 8 : 16;   // MbWidthC, MbHeightC
+    const int MWc = S.ctx_cf == 0 ? 0 : S.ctx_cf == 3 ? 16 : 8;           // MbWidthC (4:0:0: no chroma planes)
+    const int MHc = S.ctx_cf == 0 ? 0 : S.ctx_cf == 1 ? 8 : 16;           // MbHeightC
     S.y8.resize((size_t)W * H * 256);
     S.u8.resize((size_t)W * H * MWc * MHc);
     S.v8.resize((size_t)W * H * MWc * MHc);

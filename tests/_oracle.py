@@ -108,7 +108,7 @@ def make_oracle_picture(p: synth.Picture, refs, quant: np.ndarray, out) -> Oracl
             o.ref_planes[s][k] = A.ptr(planes[k]).value
     for k in range(3):
         o.out[k] = A.ptr(out[k]).value
-    o.chroma_format = int(p.cfg.chroma_format)
+    o.chroma_format = A.idc_of(p.cfg.chroma_format)
     return o
 
 
@@ -125,7 +125,7 @@ def decode(p: synth.Picture, refs=None, stage: str = "full", quant=None):
     if refs is None:
         refs = synth.refpics(L, p.cfg)
     q = quant_flat() if quant is None else quant
-    out = new_planes(p.cfg.width_mbs, p.cfg.height_mbs, p.cfg.chroma_format)
+    out = new_planes(p.cfg.width_mbs, p.cfg.height_mbs, A.idc_of(p.cfg.chroma_format))
     o = make_oracle_picture(p, refs, q, out)
     fn = {"full": L.oracle_decode_picture, "recon": L.oracle_reconstruct_picture}[stage]
     st = fn(C.byref(o))
@@ -160,7 +160,7 @@ def run_reference(cfg: A.SynthCfg, index: int, recon_only: bool = False, time_re
         if r.returncode != 0:
             raise RuntimeError(f"ref_driver failed ({r.returncode}): {r.stderr[-2000:]}")
         raw = np.fromfile(out, np.uint8)
-    cw, ch = A.chroma_mb(cfg.chroma_format)
+    cw, ch = A.chroma_mb(A.idc_of(cfg.chroma_format))
     ny, nc = 256 * W * H, cw * ch * W * H
     planes = (raw[:ny].reshape(16 * H, 16 * W), raw[ny:ny + nc].reshape(ch * H, cw * W),
               raw[ny + nc:].reshape(ch * H, cw * W))

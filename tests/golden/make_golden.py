@@ -129,6 +129,13 @@ CASES = [
     ("p422_qcif_lossless", 3, 11, 9, dict(chroma_format=2, qp_min=0, qp_max=20, lossless_permille=500), [0]),
     ("b422_qcif_scaling", 4, 11, 9, dict(chroma_format=2, transform8x8=0, qm=18), [0]),
     ("p422_1080p_strip_qp", 3, 120, 6, dict(chroma_format=2, qp_min=0, qp_max=51, num_slices=2), [0]),
+    # 4:0:0 (chroma_format_idc 0, High): the luma alone -- no chroma prediction, residual or deblocking
+    # (decoder.cc:199, deblock.cc:498,522); a PCM MB carries 256 samples
+    ("i400_qcif_pcm_t8", 2, 11, 9, dict(chroma_format=4, pcm_permille=30), [0]),
+    ("p400_qcif_wp_cip", 3, 11, 9, dict(chroma_format=4, wp_mode=1, num_refs=2, constrained_intra=1,
+                                         intra_permille=300), [0, 1]),
+    ("b400_cif_3slices_idc2", 4, 22, 9, dict(chroma_format=4, num_refs=3, num_slices=3, deblock_idc=2), [0]),
+    ("p400_qcif_lossless", 3, 11, 9, dict(chroma_format=4, qp_min=0, qp_max=20, lossless_permille=500), [0]),
 ]
 
 

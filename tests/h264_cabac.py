@@ -344,6 +344,10 @@ class CabacSink:
         A, B = self._mb(-1, 0), self._mb(0, -1)
         f = lambda m, two: m is not None and (m.mbt_ref == 12 or (m.cbpc == 2 if two else m.cbpc != 0))
         cbpc = cbp >> 4
+        if self.e.c.chroma_format in (0, 3):          # no chroma bins (interpret_se.cc:429)
+            if not cbp:
+                self.last_dquant = 0
+            return
         self._dec("cbp_c_contexts", int(f(A, False)) + 2 * int(f(B, False)), 1 if cbpc else 0)
         if cbpc:
             self._dec("cbp_c_contexts", int(f(A, True)) + 2 * int(f(B, True)) + 4, 1 if cbpc == 2 else 0)

@@ -155,7 +155,9 @@ class StreamCfg:
     chroma_format: int = 1           # chroma_format_idc (profiles 100 / 122 / 244): 1 4:2:0, 2 4:2:2 (CAVLC:
                                      # 8 chroma 4x4 blocks and a 2x4 DC per plane, nC -2, interpret_residual.cc:462-494),
                                      # 3 4:4:4 (244, CAVLC: Cb and Cr coded as luma, residual_luma per plane
-                                     # interpret_residual.cc:497-505; no intra chroma mode, the 4:4:4 CBP table)
+                                     # interpret_residual.cc:497-505; no intra chroma mode, the 4:4:4 CBP table),
+                                     # 0 4:0:0 (100 / 122 / 244: luma only -- no chroma mode, residual, PCM
+                                     # samples or chroma weights; the ChromaArrayType 0 CBP table)
     long_term: int = 0               # the IDR is a long-term reference (LongTermFrameIdx 0) kept for the
                                      # whole stream, and P picture `long_term` becomes a second one by
                                      # MMCO 4 + 6 (LongTermFrameIdx 1); P pictures predict from them
@@ -421,7 +423,7 @@ class Encoder:
                             m.nz[pl][by][bx] = self._block(w, self._levels(16), self._nc(a, pl, bx, by, s), 16)
                     else:
                         m.nz[pl][by][bx] = 0
-        if self.c.chroma_format == 3:
+        if self.c.chroma_format in (0, 3):
             return
         nbc = 8 if self.c.chroma_format == 2 else 4     # chroma 4x4 blocks (= DC coefficients) per plane
         if cbpc & 3:
@@ -439,7 +441,7 @@ class Encoder:
         """The same blocks and level draws as the CAVLC path, as residual_block_cabac calls:
         an 8x8 transform block is one 64-coefficient block (interpret_residual.cc:453-456)."""
         cab = self.cab
-        assert self.c.chroma_format in (1, 2), "CABAC streams: 4:2:0 / 4:2:2"   # (4:4:4: CAVLC)
+        assert self.c.chroma_format in (0, 1, 2), "CABAC streams: 4:0:0 / 4:2:0 / 4:2:2"   # (4:4:4: CAVLC)
         if m.kind == I16:
             cab.block(CB.LUMA_16DC, 0, 0, self._levels(16))
         for b8 in range(4):
@@ -456,6 +458,8 @@ class Encoder:
                     cab.block(CB.LUMA_16AC, 0, b8 * 4 + b4, self._levels(15))
                 else:
                     cab.block(CB.LUMA_4x4, 0, b8 * 4 + b4, self._levels(16))
+        if self.c.chroma_format == 0:
+            return
         nbc = 8 if self.c.chroma_format == 2 else 4
         if cbpc & 3:
             for pl in (1, 2):
@@ -553,7 +557,7 @@ class Encoder:
         A, B, D = self._avail_abd(a, 0, 0, 4, s)
         if m.kind == PCM:
             m.mbt_ref = 12
-            npcm = 256 + {2: 256, 3: 512}.get(c.chroma_format, 128)   # 2 x MbWidthC x MbHeightC chroma samples
+            npcm = 256 + {0: 0, 2: 256, 3: 512}.get(c.chroma_format, 128)   # 2 x MbWidthC x MbHeightC chroma samples
             if cab:
                 cab.mb_type_intra(25)
                 cab.pcm([r.randint(1, 255) for _ in range(npcm)])
@@ -569,17 +573,18 @@ class Encoder:
         if m.kind == I16:
             modes = ([0] if B else []) + ([1] if A else []) + [2] + ([3] if A and B and D else [])
             mode = r.choice(modes)
-            cbpc = r.randint(0, 2) if c.chroma_format != 3 else 0
+            cbpc = r.randint(0, 2) if c.chroma_format in (1, 2) else 0
             cbpl = 15 if r.random() < 0.5 else 0
             m.mbt_ref, m.cbpl, m.cbpc = 10, cbpl, cbpc
             cm = r.choice(cmodes)
             if cab:
                 cab.mb_type_intra(1 + mode + 4 * cbpc + (12 if cbpl else 0))
-                m.cmode = cm
-                cab.chroma_mode(cm)
+                if c.chroma_format in (1, 2):
+                    m.cmode = cm
+                    cab.chroma_mode(cm)
             else:
                 w.ue(base + 1 + mode + 4 * cbpc + (12 if cbpl else 0))
-                if c.chroma_format != 3:                # intra_chroma_pred_mode: ChromaArrayType 1 / 2 only
+                if c.chroma_format in (1, 2):           # intra_chroma_pred_mode: ChromaArrayType 1 / 2 only
                     w.ue(cm)
             cbp = cbpl | cbpc << 4
         elif m.kind in (I4, I8):
@@ -618,13 +623,14 @@ class Encoder:
                     else:
                         w.u(1, 0); w.u(3, mode if mode < pred else mode - 1)
             cm = r.choice(cmodes)
-            cbp = r.randint(0, 47) if c.chroma_format != 3 else r.randint(0, 15)
+            cbp = r.randint(0, 47) if c.chroma_format in (1, 2) else r.randint(0, 15)
             m.cbpl, m.cbpc = cbp & 15, cbp >> 4
             if cab:
-                m.cmode = cm
-                cab.chroma_mode(cm)
+                if c.chroma_format in (1, 2):
+                    m.cmode = cm
+                    cab.chroma_mode(cm)
                 cab.cbp(cbp)
-            elif c.chroma_format == 3:
+            elif c.chroma_format in (0, 3):
                 w.ue(CBP_CODE_444["intra"][cbp])
             else:
                 w.ue(cm)
@@ -686,12 +692,12 @@ class Encoder:
                     for sp in {0: [(0, 0, 2, 2)], 1: [(0, 0, 2, 1), (0, 1, 2, 1)], 2: [(0, 0, 1, 2), (1, 0, 1, 2)],
                                3: [(0, 0, 1, 1), (1, 0, 1, 1), (0, 1, 1, 1), (1, 1, 1, 1)]}[sb]:
                         mvd(x8 + sp[0], y8 + sp[1], sp[2], sp[3])
-            cbp = r.randint(0, 47) if c.chroma_format != 3 else r.randint(0, 15)
+            cbp = r.randint(0, 47) if c.chroma_format in (1, 2) else r.randint(0, 15)
             m.cbpl, m.cbpc = cbp & 15, cbp >> 4
             if cab:
                 cab.cbp(cbp)
             else:
-                w.ue((CBP_CODE_444 if c.chroma_format == 3 else CBP_CODE)["inter"][cbp])
+                w.ue((CBP_CODE_444 if c.chroma_format in (0, 3) else CBP_CODE)["inter"][cbp])
             m.t8 = False
             if (cbp & 15) and c.transform8x8 and not small:
                 m.t8 = r.random() < 0.5
@@ -809,12 +815,12 @@ class Encoder:
                             sps = [(0, 0, 1, 2), (1, 0, 1, 2)]
                         for sp in sps:
                             mvd(lst, x8 + sp[0], y8 + sp[1], sp[2], sp[3])
-        cbp = r.randint(0, 47) if self.c.chroma_format != 3 else r.randint(0, 15)
+        cbp = r.randint(0, 47) if self.c.chroma_format in (1, 2) else r.randint(0, 15)
         m.cbpl, m.cbpc = cbp & 15, cbp >> 4
         if cab:
             cab.cbp(cbp)
         else:
-            w.ue((CBP_CODE_444 if self.c.chroma_format == 3 else CBP_CODE)["inter"][cbp])
+            w.ue((CBP_CODE_444 if self.c.chroma_format in (0, 3) else CBP_CODE)["inter"][cbp])
         return cbp, small
 
     # ------------------------------------------------------------------ pictures
@@ -823,8 +829,11 @@ class Encoder:
         a chroma flag with weights / offsets.  For B slices the weights stay inside the
         bi-prediction constraint -128 <= w0 + w1 <= 128 (8.4.2.3)."""
         r = self.rng
+        chroma = self.c.chroma_format != 0          # no chroma weights in 4:0:0 (7.3.3.2)
         ld, cd = r.randint(0, 7), r.randint(0, 7)
-        w.ue(ld); w.ue(cd)
+        w.ue(ld)
+        if chroma:
+            w.ue(cd)
         for n in nrefs:
             for _ in range(n):
                 if r.random() < 0.7:
@@ -833,6 +842,8 @@ class Encoder:
                     w.se(r.randint(-20, 20))
                 else:
                     w.u(1, 0)
+                if not chroma:
+                    continue
                 if r.random() < 0.7:
                     w.u(1, 1)
                     for _ in range(2):
@@ -907,12 +918,16 @@ class Encoder:
                 w.u(1, 0)                           # ref_pic_list_modification_flag_l0
                 if c.weighted:
                     ld, cd = r.randint(0, 7), r.randint(0, 7)
-                    w.ue(ld); w.ue(cd)
+                    w.ue(ld)
+                    if c.chroma_format != 0:
+                        w.ue(cd)
                     for _ in range(nref):
                         if r.random() < 0.7:
                             w.u(1, 1); w.se(r.randint(-min(64, 1 << ld), min(127, 2 << ld))); w.se(r.randint(-20, 20))
                         else:
                             w.u(1, 0)
+                        if c.chroma_format == 0:
+                            continue
                         if r.random() < 0.7:
                             w.u(1, 1)
                             for _ in range(2):

@@ -141,6 +141,14 @@ STREAMS = {
     "hi444_qcif_ibbp_lossless_scaling": dict(width_mbs=11, height_mbs=9, frames=7, seed=802, profile=244,
                                              chroma_format=3, transform8x8=1, bframes=2, num_refs=3, bipred=2,
                                              lossless=0.4, qp=(0, 36), intra_in_p=0.3, scaling=3, cip=1),
+    # 4:0:0 (chroma_format_idc 0, High): luma only -- no chroma mode, CBP chroma, residual, PCM samples
+    # or chroma weights; the reference writes 128-valued 4:2:0 chroma beside it (WriteUV, output.cc:205)
+    "hp400_cif_ippp_8x8_wp": dict(width_mbs=22, height_mbs=18, frames=4, seed=901, profile=100, chroma_format=0,
+                                  transform8x8=1, num_refs=2, weighted=1, slices=2, deblock=(0, 1, 2), offsets=3,
+                                  pcm=0.03, intra_in_p=0.2, crop=(3, 1, 2, 5)),
+    "hp400_qcif_cabac_ibbp": dict(width_mbs=11, height_mbs=9, frames=7, seed=902, profile=100, chroma_format=0,
+                                  transform8x8=1, cabac=1, bframes=2, num_refs=3, bipred=1, pcm=0.04,
+                                  intra_in_p=0.3, cip=1, scaling=3),
 }
 
 CAP_MAGIC = 0x43523448
@@ -223,17 +231,18 @@ def read_capture_file(path: str) -> list[dict]:
     while off < len(raw):
         hdr = np.frombuffer(raw, np.int32, 8, off)
         off += 32
-        magic, W, H, ns, nl, keep, cf = (int(v) for v in hdr[:7])
+        magic, W, H, ns, nl, keep, cf, ver = (int(v) for v in hdr[:8])
         assert magic == CAP_MAGIC, "capture: bad record"
         n = W * H
-        cw, ch = A.chroma_mb(cf or 1)
+        cf = cf if ver == 1 else 1                 # header[7] 1: header[6] is chroma_format_idc
+        cw, ch = A.chroma_mb(cf)
 
         def take(dtype, count):
             nonlocal off
             a = np.frombuffer(raw, dtype, count, off).copy()
             off += a.nbytes
             return a
-        p = dict(W=W, H=H, keep=keep, chroma_format=cf or 1)
+        p = dict(W=W, H=H, keep=keep, chroma_format=cf)
         p["mbs"] = take(A.MB_DTYPE, n)
         p["levels"] = take(np.int16, nl)
         p["mv"] = take(np.uint32, 2 * 16 * n).reshape(2, 4 * H, 4 * W)

@@ -88,7 +88,7 @@ def test_error_codes(L):
     assert L.h264r_strerror(A.EINVAL) == b"invalid argument"
     h = C.c_void_p()
     assert L.h264r_create(C.byref(h), 0, 0, 0, 1, 8) == A.EINVAL
-    assert L.h264r_create(C.byref(h), 0, 10, 10, 0, 8) == A.EUNSUPPORTED     # 4:0:0
+    assert L.h264r_create(C.byref(h), 0, 10, 10, 4, 8) == A.EUNSUPPORTED     # no chroma_format_idc 4
     assert L.h264r_create(C.byref(h), 0, 10, 10, 1, 10) == A.EUNSUPPORTED
     assert L.h264r_quant_init_flat(None) == A.EINVAL
     assert L.h264r_destroy(None) == A.EINVAL

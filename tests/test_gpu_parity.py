@@ -49,6 +49,14 @@ def dec444(L):
 
 
 @pytest.fixture(scope="module")
+def dec400(L):
+    """A 4:0:0 context (chroma_format_idc 0): the luma pass alone."""
+    d = h264r.Decoder(0, 240, 135, chroma_format=0)
+    yield d
+    d.close()
+
+
+@pytest.fixture(scope="module")
 def dec422(L):
     """A 4:2:2 context (chroma_format_idc 2): the luma pass, then k_c422_inter / k_c422_intra / k_c422_db."""
     d = h264r.Decoder(0, 240, 135, chroma_format=2)
@@ -66,10 +74,9 @@ def first_diff(a, b, n, nh=None):
 
 
 @pytest.mark.parametrize("fx", GOLDEN, ids=[f"{f['name']}[{f['index']}]" for f in GOLDEN])
-def test_gpu_matches_reference_fixture(L, dec, dec444, dec422, fx):
+def test_gpu_matches_reference_fixture(L, dec, dec444, dec422, dec400, fx):
     cfg = A.SynthCfg.from_dict(fx["cfg"])
-    if cfg.chroma_format in (2, 3):
-        dec = dec444 if cfg.chroma_format == 3 else dec422
+    dec = {0: dec400, 2: dec422, 3: dec444}.get(A.idc_of(cfg.chroma_format), dec)
     p = synth.picture(L, cfg, fx["index"])
     assert synth.input_digest(p) == fx["input_md5"]
     refs = synth.refpics(L, cfg)
@@ -88,7 +95,7 @@ def test_gpu_matches_reference_fixture(L, dec, dec444, dec422, fx):
         ref_out = O.decode(p, refs, quant=oquant)
         msgs = []
         for i, k in enumerate("YUV"):
-            n, nh = (16, 16) if i == 0 else A.chroma_mb(cfg.chroma_format)
+            n, nh = (16, 16) if i == 0 else A.chroma_mb(A.idc_of(cfg.chroma_format))
             d = first_diff(rec[i], ref_rec[i], n, nh)
             if d:
                 msgs.append(f"recon {k}: {d}")
