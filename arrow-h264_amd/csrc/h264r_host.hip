@@ -943,11 +943,17 @@ static bool stride_ok(const h264r_batch* b)
     return b->ref_planes_stride == 0 || (b->ref_planes_stride >= 3 * H264R_MAX_SLOTS && b->ref_planes);
 }
 
+// out_u / out_v: required, except on a 4:0:0 context, which writes no chroma (they may be NULL)
+static bool chroma_out_ok(const h264r_ctx* c, const h264r_batch* b)
+{
+    return c->fmt == 0 || (b->out_u && b->out_v);
+}
+
 int h264r_decode_batch(h264r_ctx* c, const h264r_batch* b, void* stream)
 {
     if (!c || !b || b->num_pics <= 0 || b->width_mbs <= 0 || b->height_mbs <= 0 ||
         b->width_mbs > c->max_w || b->height_mbs > c->max_h || b->slice_stride <= 0 || !b->mbs || !b->levels ||
-        !b->mv || !b->ref_idx || !b->slices || !b->pics || !b->quant || !b->out_y || !b->out_u || !b->out_v ||
+        !b->mv || !b->ref_idx || !b->slices || !b->pics || !b->quant || !b->out_y || !chroma_out_ok(c, b) ||
         !stride_ok(b))
         return H264R_EINVAL;
     (void)hipSetDevice(c->device);
@@ -967,7 +973,7 @@ int h264r_decode_batch_rows(h264r_ctx* c, const h264r_batch* b, int row0, int ro
 {
     if (!c || !b || row0 < 0 || row1 <= row0 || row1 > b->height_mbs) return H264R_EINVAL;
     if (!b->mbs || !b->levels || !b->mv || !b->ref_idx || !b->slices || !b->pics || !b->quant || !b->out_y ||
-        !b->out_u || !b->out_v || b->num_pics <= 0 || b->width_mbs <= 0 || b->width_mbs > c->max_w ||
+        !chroma_out_ok(c, b) || b->num_pics <= 0 || b->width_mbs <= 0 || b->width_mbs > c->max_w ||
         b->height_mbs > c->max_h || b->slice_stride <= 0 || !stride_ok(b))
         return H264R_EINVAL;
     (void)hipSetDevice(c->device);

@@ -72,7 +72,19 @@
  *   - deblocking     a transform-8x8 MB's chroma rows 4 and 12 take the bS of 8.7.2.1, which the
  *                    reference leaves unset.
  * The library decodes the luma by the 4:2:0 kernels and the chroma by its own kernels (DESIGN.md
- * section 4e).  4:0:0 and > 8-bit are H264R_EUNSUPPORTED.
+ * section 4e).
+ *
+ * 4:0:0 (a context created with chroma_format_idc 0, monochrome; frame pictures, 8-bit; not SP
+ * slices): there is no chroma (decoder.cc:199, picture.cc:34), so
+ *   - planes         Y only: out_u / out_v of a batch and u / v of h264r_set_ref may be NULL and are
+ *                    never written or read, nor u / v of h264r_picture_end / h264r_picture_wait;
+ *   - levels         the luma part only: for b8 with (cbp & 1<<b8) 64 levels as above, then, if
+ *                    I_16x16, its 16 DC levels; cbp_chroma must be 0; I_PCM: 256 raw samples, and
+ *                    128 readable bytes after the MB's block;
+ *   - h264r_mb       qp_c[] / qp_scaled[1..2] / chroma_mode are not used;
+ *   - h264r_slice    the chroma weights are not used.
+ * The library decodes the luma by the 4:2:0 kernels alone.  > 8-bit is
+ * H264R_EUNSUPPORTED.
  */
 #ifndef H264R_H_
 #define H264R_H_
@@ -233,7 +245,7 @@ typedef struct h264r_batch {
     const h264r_quant*  quant;       /* one table per picture */
     const uint8_t* const* ref_planes;
     uint8_t*            out_y;
-    uint8_t*            out_u;
+    uint8_t*            out_u;       /* NULL allowed on a 4:0:0 context */
     uint8_t*            out_v;
     int64_t             ref_planes_stride;   /* pointers; 0 = one table for the batch (above) */
 } h264r_batch;
@@ -256,8 +268,8 @@ int  h264r_quant_init_flat(h264r_quant* q);
 int  h264r_quant_init_lists(h264r_quant* q, const int32_t* const qmatrix[12]);
 
 /* ---- context ------------------------------------------------------------------- */
-/* chroma_format_idc 1 (4:2:0), 2 (4:2:2) or 3 (4:4:4, above) and bit_depth 8 (other formats:
- * H264R_EUNSUPPORTED). */
+/* chroma_format_idc 0 (4:0:0), 1 (4:2:0), 2 (4:2:2) or 3 (4:4:4, above) and bit_depth 8 (other
+ * formats: H264R_EUNSUPPORTED). */
 int  h264r_create(h264r_ctx** out, int device, int max_width_mbs, int max_height_mbs,
                   int chroma_format_idc, int bit_depth);
 int  h264r_destroy(h264r_ctx* ctx);
