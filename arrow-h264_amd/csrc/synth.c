@@ -33,9 +33,14 @@ static const uint8_t QP_SCALE_CR[52] = {                  /* interpret_mb.cc:777
 static int clip3i(int lo, int hi, int x) { return x < lo ? lo : (x > hi ? hi : x); }
 
 int h264r_synth_slot_poc(int slot) { return 4 * slot; }
+/* a field picture (PAFF); an MBAFF frame is a frame picture for its lists and POCs */
+static int field_pic(const h264r_synth_cfg* c)
+{
+    return c->structure == H264R_TOP_FIELD || c->structure == H264R_BOTTOM_FIELD;
+}
 int h264r_synth_ref_frames(const h264r_synth_cfg* cfg)
 {
-    return cfg->structure != H264R_FRAME ? (cfg->num_refs + 1) / 2 : cfg->num_refs;
+    return field_pic(cfg) ? (cfg->num_refs + 1) / 2 : cfg->num_refs;
 }
 int h264r_synth_cur_poc(const h264r_synth_cfg* cfg)
 {
@@ -50,11 +55,11 @@ int h264r_synth_cur_poc(const h264r_synth_cfg* cfg)
    bottom when k is odd) */
 static int cand_poc(const h264r_synth_cfg* c, int k)
 {
-    return c->structure != H264R_FRAME ? h264r_synth_slot_poc(k >> 1) + (k & 1) : h264r_synth_slot_poc(k);
+    return field_pic(c) ? h264r_synth_slot_poc(k >> 1) + (k & 1) : h264r_synth_slot_poc(k);
 }
 static int cand_ref(const h264r_synth_cfg* c, int k)
 {
-    return c->structure != H264R_FRAME ? (k >> 1) | ((k & 1) ? H264R_REF_BOTTOM : 0) : k;
+    return field_pic(c) ? (k >> 1) | ((k & 1) ? H264R_REF_BOTTOM : 0) : k;
 }
 static int ref_poc(int ref) { return h264r_synth_slot_poc(ref & 31) + ((ref & H264R_REF_BOTTOM) ? 1 : 0); }
 
@@ -109,7 +114,7 @@ static void make_slices(const h264r_synth_cfg* c, rng_t* r, h264r_slice* sl)
         /* L0: descending POC below cur then ascending above; L1: the reverse (8.2.4.2.3 style;
            fields: the candidates are the DPB frames' fields, so the order alternates parity) */
         int l0[2 * H264R_MAX_REFS], l1[2 * H264R_MAX_REFS], k0 = 0, k1 = 0;
-        const int nc = c->structure != H264R_FRAME ? 2 * h264r_synth_ref_frames(c) : n;
+        const int nc = field_pic(c) ? 2 * h264r_synth_ref_frames(c) : n;
         for (int k = nc - 1; k >= 0; --k) if (cand_poc(c, k) < cur) l0[k0++] = cand_ref(c, k);
         for (int k = 0; k < nc; ++k) if (cand_poc(c, k) > cur) l0[k0++] = cand_ref(c, k);
         for (int k = 0; k < nc; ++k) if (cand_poc(c, k) > cur) l1[k1++] = cand_ref(c, k);
@@ -170,6 +175,42 @@ typedef struct {
     int8_t* ref;
 } gen_t;
 
+/* ---- MBAFF frames: availability where Neighbour::get_neighbour finds a sample (neighbour.cc:
+   123-173) -- the geometric frame sample at (xN, yN) of MB a's own sample grid (a field MB's rows
+   are every second frame row of its pair), in the MB that holds it, decoded before a (MBAFF
+   address order) and in a's slice (intra_prediction.cc:145-152).  maxW / maxH: 16 / 16 luma,
+   8 / 8 chroma (4:2:0).  Returns the MB's storage index or -1. */
+static int mbaff_nb(const gen_t* g, int a, int xN, int yN, int maxW, int maxH)
+{
+    const int W = g->c->width_mbs, HP = g->c->height_mbs / 2;
+    const int mbx = a % W, mby = a / W, py = mby >> 1, b = mby & 1;
+    const int fld = (g->mbs[a].flags & H264R_MBF_FIELD) != 0;
+    const int gx = mbx * maxW + xN;
+    const int gy = py * 2 * maxH + (fld ? b + 2 * yN : b * maxH + yN);
+    if (gx < 0 || gx >= W * maxW || gy < 0 || gy >= HP * 2 * maxH) return -1;
+    const int nx = gx / maxW, npy = gy / (2 * maxH);
+    if (npy * W + nx > py * W + mbx) return -1;                 /* a later pair: not decoded */
+    const int top = (2 * npy) * W + nx;
+    const int nfld = (g->mbs[top].flags & H264R_MBF_FIELD) != 0;
+    const int nb = nfld ? (gy & 1) : ((gy % (2 * maxH)) >= maxH);
+    const int n = top + nb * W;
+    if (n == a) return n;                                       /* inside the MB itself */
+    if (npy * W + nx == py * W + mbx && nb >= b) return -1;     /* the pair's later MB */
+    return g->mbs[n].slice == g->mbs[a].slice ? n : -1;
+}
+static int mbaff_intra_ok(const gen_t* g, int n)
+{
+    return n >= 0 && (!g->c->constrained_intra || (g->mbs[n].flags & H264R_MBF_INTRA));
+}
+/* left neighbours of rows y0 .. y0 + n - 1 at column x: available as the reference's ctor decides
+   (non-CIP: the first row's MB; CIP: every row's MB intra, intra_prediction.cc:156-167) */
+static int mbaff_left(const gen_t* g, int a, int x, int y0, int n, int maxW, int maxH)
+{
+    if (!g->c->constrained_intra) return mbaff_nb(g, a, x, y0, maxW, maxH) >= 0;
+    for (int i = 0; i < n; ++i) if (!mbaff_intra_ok(g, mbaff_nb(g, a, x, y0 + i, maxW, maxH))) return 0;
+    return 1;
+}
+
 static int mb_exists_same_slice(const gen_t* g, int addr, int nx, int ny)
 {
     const h264r_synth_cfg* c = g->c;
@@ -228,6 +269,7 @@ static uint32_t rand_mv(rng_t* r, const h264r_synth_cfg* c)
 static void rand_partition_dir(gen_t* g, rng_t* r, int addr, int bx, int by, int bw, int bh, int bslice, int dir)
 {
     int nref = g->c->num_refs;
+    if (g->mbs[addr].flags & H264R_MBF_FIELD) nref *= 2;          /* MBAFF field MB: refIdx counts fields */
     if (dir < 0) dir = bslice ? rnd(r, 3) : 0;
     int r0 = (dir == 0 || dir == 2) ? rnd(r, nref) : -1;
     int r1 = (dir == 1 || dir == 2) ? rnd(r, nref) : -1;
@@ -245,7 +287,10 @@ int h264r_synth_picture(const h264r_synth_cfg* c, int index, h264r_mb* mbs, int1
     if (!c || !mbs || !levels || !mv || !ref_idx || !slices || !pic) return H264R_EINVAL;
     if (c->width_mbs <= 0 || c->height_mbs <= 0 || c->num_slices <= 0 || c->num_slices > H264R_MAX_SLICES ||
         c->num_slices > c->height_mbs || c->num_refs < 0 || c->num_refs > H264R_MAX_REFS ||
-        c->structure < H264R_FRAME || c->structure > H264R_BOTTOM_FIELD ||
+        c->structure < H264R_FRAME || c->structure > H264R_MBAFF_FRAME ||
+        (c->structure == H264R_MBAFF_FRAME && ((c->height_mbs & 1) || c->num_slices > c->height_mbs / 2 ||
+                                               (c->chroma_format != 0 && c->chroma_format != 1) || c->wp_mode == 2 ||
+                                               c->sp_slices || c->lossless_permille)) ||
         (c->kind != H264R_SYNTH_INTRA && c->num_refs < 1) || c->qp_min < 0 || c->qp_max > 51 ||
         c->qp_min > c->qp_max || (c->chroma_format >= 2 && c->structure != H264R_FRAME) ||
         c->chroma_format < 0 || c->chroma_format > 4)
@@ -266,10 +311,19 @@ int h264r_synth_picture(const h264r_synth_cfg* c, int index, h264r_mb* mbs, int1
 
     int64_t off = 0;
     int bslice = c->kind == H264R_SYNTH_B;
-    for (int a = 0; a < nmb; ++a) {
+    const int mbaff = c->structure == H264R_MBAFF_FRAME;
+    for (int k = 0; k < nmb; ++k) {
+        /* MBAFF: MB address order, pair by pair (top, bottom), a = the storage index */
+        const int a = mbaff ? ((k >> 1) / W * 2 + (k & 1)) * W + (k >> 1) % W : k;
         h264r_mb* m = &mbs[a];
         int mby = a / W;
-        m->slice = (uint16_t)slice_of_row(mby, c->num_slices, H);
+        m->slice = (uint16_t)(mbaff ? slice_of_row(mby >> 1, c->num_slices, H / 2) : slice_of_row(mby, c->num_slices, H));
+        if (mbaff) {
+            /* mb_field_decoding_flag, one per pair (drawn with the top MB) */
+            const int fld = (k & 1) ? (mbs[a - W].flags & H264R_MBF_FIELD) != 0 : rnd(&r, 2);
+            m->flags = fld ? H264R_MBF_FIELD : 0;
+        }
+        const uint8_t fflag = m->flags;
         int is_intra;
         if (c->kind == H264R_SYNTH_INTRA) is_intra = 1;
         else is_intra = rnd(&r, 1000) < c->intra_permille;
@@ -290,7 +344,7 @@ int h264r_synth_picture(const h264r_synth_cfg* c, int index, h264r_mb* mbs, int1
 
         if (pcm) {
             m->mb_type = H264R_I_PCM;
-            m->flags = H264R_MBF_INTRA;
+            m->flags = H264R_MBF_INTRA | fflag;
             m->cbp_blks = 0xFFFF;
             uint8_t* raw = (uint8_t*)(levels + off);
             const int npcm = f444 ? 768 : f422 ? 512 : f400 ? 256 : 384;   /* Y 256, Cb / Cr 64, 128 (4:2:2), 256 (4:4:4) */
@@ -300,13 +354,19 @@ int h264r_synth_picture(const h264r_synth_cfg* c, int index, h264r_mb* mbs, int1
         }
         int cbpl = 0, cbpc = 0, t8 = 0;
         if (is_intra) {
-            m->flags = H264R_MBF_INTRA;
+            m->flags = H264R_MBF_INTRA | fflag;
             int kind = rnd(&r, 100);
             if (kind < 40) m->mb_type = H264R_I_4x4;
             else if (kind < 80) m->mb_type = c->transform8x8 ? H264R_I_8x8 : H264R_I_4x4;
             else m->mb_type = H264R_I_16x16;
             int av[4];
-            mb_avail(&g, a, av);
+            if (mbaff) {
+                av[0] = mbaff_left(&g, a, -1, 0, 16, 16, 16);
+                av[1] = mbaff_intra_ok(&g, mbaff_nb(&g, a, 0, -1, 16, 16));
+                av[2] = 0;
+                av[3] = mbaff_intra_ok(&g, mbaff_nb(&g, a, -1, -1, 16, 16));
+            } else
+                mb_avail(&g, a, av);
             if (m->mb_type == H264R_I_16x16) {
                 int md[4], k = 0;
                 md[k++] = 2;
@@ -326,17 +386,29 @@ int h264r_synth_picture(const h264r_synth_cfg* c, int index, h264r_mb* mbs, int1
                     int A = xO > 0 ? 1 : av[0];
                     int B = yO > 0 ? 1 : av[1];
                     int D = (xO > 0 && yO > 0) ? 1 : (xO == 0 && yO == 0) ? av[3] : (xO == 0 ? av[0] : av[1]);
+                    if (mbaff) {         /* the block's own neighbours (intra_prediction.cc:137-187, 359-411) */
+                        A = mbaff_left(&g, a, xO - 1, yO, size, 16, 16);
+                        B = mbaff_intra_ok(&g, mbaff_nb(&g, a, xO, yO - 1, 16, 16));
+                        D = mbaff_intra_ok(&g, mbaff_nb(&g, a, xO - 1, yO - 1, 16, 16));
+                    }
                     int mode = pick_nxn_mode(&r, A, B, D);
                     m->ipred[b >> 1] |= (uint8_t)(mode << ((b & 1) * 4));
                 }
                 cbpl = rnd(&r, 16);
             }
             {
+                int ca[4] = {av[0], av[1], av[0], av[3]};
+                if (mbaff) {     /* chroma neighbours on the 8 x 8 grid (intra_prediction.cc:745-790) */
+                    ca[0] = mbaff_left(&g, a, -1, 0, 4, 8, 8);
+                    ca[2] = mbaff_left(&g, a, -1, 4, 4, 8, 8) && mbaff_nb(&g, a, -1, 0, 8, 8) >= 0;
+                    ca[1] = mbaff_intra_ok(&g, mbaff_nb(&g, a, 0, -1, 8, 8));
+                    ca[3] = mbaff_intra_ok(&g, mbaff_nb(&g, a, -1, -1, 8, 8));
+                }
                 int md[4], k = 0;
                 md[k++] = 0;
-                if (av[0]) md[k++] = 1;
-                if (av[1]) md[k++] = 2;
-                if (av[0] && av[1] && av[3]) md[k++] = 3;
+                if (ca[0] && ca[2]) md[k++] = 1;
+                if (ca[1]) md[k++] = 2;
+                if (ca[0] && ca[2] && ca[1] && ca[3]) md[k++] = 3;
                 m->chroma_mode = (uint8_t)pick_mode(&r, md, k);
             }
             cbpc = f444 || f400 ? 0 : rnd(&r, 3);
@@ -344,6 +416,7 @@ int h264r_synth_picture(const h264r_synth_cfg* c, int index, h264r_mb* mbs, int1
         } else {
             int k = rnd(&r, 90);    /* conditional on inter: skip/16x16/16x8/8x16/8x8 = 15/45/10/10/10 */
             int mt = k < 15 ? H264R_P_SKIP : k < 60 ? H264R_P_16x16 : k < 70 ? H264R_P_16x8 : k < 80 ? H264R_P_8x16 : H264R_P_8x8;
+            m->flags = fflag;
             m->mb_type = (uint8_t)mt;
             switch (mt) {
             case H264R_P_SKIP:

@@ -16,14 +16,14 @@ DBG_WAIT_TEST = 32
 DBG_OVERLAP = 64
 DBG_DEBLOCK_SPLIT = 128
 MAX_REFS, MAX_SLOTS, MAX_SLICES = 16, 32, 256
-ABI_VERSION = 3
-FRAME, TOP_FIELD, BOTTOM_FIELD = 0, 1, 2        # h264r_pic.structure
+ABI_VERSION = 4
+FRAME, TOP_FIELD, BOTTOM_FIELD, MBAFF_FRAME = 0, 1, 2, 3   # h264r_pic.structure
 REF_BOTTOM = 0x40                              # ref_slot entry of a field picture: the slot's bottom field
 
 P_SKIP, P_16x16, P_16x8, P_8x16, P_8x8, P_8x4, P_4x8, P_4x4 = range(8)
 I_4x4, I_8x8, I_16x16, SI, I_PCM = 8, 9, 10, 11, 12
 SLICE_P, SLICE_B, SLICE_I, SLICE_SP, SLICE_SI = range(5)
-MBF_INTRA, MBF_T8x8, MBF_BYPASS = 1, 2, 4
+MBF_INTRA, MBF_T8x8, MBF_BYPASS, MBF_FIELD = 1, 2, 4, 8
 
 SYNTH_INTRA, SYNTH_P, SYNTH_B = 0, 1, 2
 SYNTH_MAX_LEVELS_PER_MB = 416

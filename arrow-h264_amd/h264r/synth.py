@@ -61,7 +61,7 @@ def picture(lib: C.CDLL, cfg: A.SynthCfg, index: int) -> Picture:
 def refpics(lib: C.CDLL, cfg: A.SynthCfg, nslots: int | None = None):
     """[(y, u, v)] for DPB slots 0..n-1: the frames the pictures reference (a field cfg's
     references are fields of frames of twice its height, include/h264r_synth.h)."""
-    W, H = cfg.width_mbs, cfg.height_mbs * (2 if cfg.structure else 1)
+    W, H = cfg.width_mbs, cfg.height_mbs * (2 if cfg.structure in (A.TOP_FIELD, A.BOTTOM_FIELD) else 1)
     cw, ch = A.chroma_mb(A.idc_of(cfg.chroma_format))
     out = []
     for s in range(lib.h264r_synth_ref_frames(C.byref(cfg)) if nslots is None else nslots):

@@ -22,8 +22,8 @@
  * boundary; the reference's void/assert/exit() error convention
  * (decoder.h:301-338, ldecod.cc:33-48) becomes status codes.
  *
- * Data formats (all little-endian, 4:2:0, 8-bit; frame pictures and field pictures (PAFF,
- * h264r_pic.structure below); MBAFF frames are H264R_EUNSUPPORTED):
+ * Data formats (all little-endian, 4:2:0, 8-bit; frame pictures, field pictures (PAFF) and MBAFF
+ * frames, h264r_pic.structure below):
  *   - h264r_mb       32-byte MB record (subset of mb_t, macroblock.h:78-135).
  *   - levels         int16 pool; each MB owns a compacted block at mb.coef_off
  *                    (in int16 units, multiple of 8):
@@ -96,7 +96,7 @@
 extern "C" {
 #endif
 
-#define H264R_ABI_VERSION 3
+#define H264R_ABI_VERSION 4
 
 /* ---- status codes ---------------------------------------------------------- */
 #define H264R_OK               0
@@ -143,6 +143,8 @@ extern "C" {
                                     DPCM by the block's ipred mode -- for inter MBs too, as the
                                     reference reads Intra4x4/8x8PredMode there, transform.cc:993,1008;
                                     an inter MB's chroma_mode must be 0, the parser's value) */
+#define H264R_MBF_FIELD   0x08   /* mb_t::mb_field_decoding_flag (H264R_MBAFF_FRAME pictures only; both
+                                    MBs of a pair carry the same value) */
 
 /* 32-byte macroblock record (fields named after mb_t, macroblock.h:78-135). */
 typedef struct h264r_mb {
@@ -211,11 +213,31 @@ typedef struct h264r_quant {
  * (dpb_combine_field_yuv picture.cc:578-622 without the copy), so the two fields of a frame
  * share one slot and a frame picture may later reference the frame they make up. */
 #define H264R_REF_BOTTOM  0x40
+/* MBAFF frames (ABI 4, mb_adaptive_frame_field_flag: MbaffFrameFlag of slice_header, macroblock
+ * pairs that are each coded as two frame MBs or as two field MBs, H264R_MBF_FIELD).  A frame picture
+ * of the context's size whose MBs are stored as the reference stores them (mb_t::mb, the position
+ * slice_data.cc gives an MB of address a: x = (a / 2) % W, y = 2 ((a / 2) / W) + a % 2):
+ *   - records  the record of MB address a is mbs[y * W + x] (pair row r: its top MB in row 2r, its
+ *              bottom MB in row 2r + 1), and the streaming API's mb_addr is that index, y * W + x;
+ *   - motion   rows 4 y .. 4 y + 3 of the [H4][W4] arrays hold MB (x, y)'s blocks (the reference's
+ *              mv_info rows, inter_prediction.cc:456), in its own frame or field rows;
+ *   - ref_idx  a field MB's refIdx counts fields (0 .. 2 num_ref - 1): field refIdx / 2 of the slice's
+ *              frame list, the same parity as the MB when refIdx is even (get_ref_pic dpb.cc:1046-1055);
+ *              its explicit weights are those of refIdx / 2 (inter_prediction.cc:66,100-101);
+ *   - output   the frame: a field MB's rows are every second row of its pair, from the pair's
+ *              first (top MB) or second row (bottom MB) -- the picture after MbAffPostProc
+ *              (deblock.cc:581-620), which the reference applies before the loop filter.
+ * Intra prediction takes its neighbours where Neighbour::get_neighbour finds them (neighbour.cc:
+ * 123-173: the geometric sample of the frame, the MB holding it), and the loop filter follows
+ * Deblock::strength / filter_edge (deblock.cc:78-289, 418-535): mixed frame / field edges, the
+ * top edge of a frame MB under a field pair filtered as two field edges, mvlimit 2 in field MBs.
+ * 4:2:0 only; not with SP slices, lossless MBs or implicit weights (H264R_EUNSUPPORTED). */
+#define H264R_MBAFF_FRAME   3
 typedef struct h264r_pic {
     int32_t  constrained_intra_pred;  /* pps.constrained_intra_pred_flag */
     int32_t  num_slices;
     int32_t  poc;                     /* informational (implicit weights are precomputed) */
-    int32_t  structure;               /* H264R_FRAME / H264R_TOP_FIELD / H264R_BOTTOM_FIELD */
+    int32_t  structure;               /* H264R_FRAME / H264R_TOP_FIELD / H264R_BOTTOM_FIELD / H264R_MBAFF_FRAME */
 } h264r_pic;
 
 /* A batch of same-sized pictures whose arrays are already resident on the device.

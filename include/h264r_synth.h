@@ -60,7 +60,11 @@ typedef struct h264r_synth_cfg {
                                     FIELDS (list entries), taken from DPB frames 0 .. (num_refs+1)/2 - 1
                                     of 2 * height_mbs MB rows: the fields of frame slot s have POC
                                     4 s (top) and 4 s + 1 (bottom), the lists order them by POC as
-                                    8.2.4.2.4/8.2.4.2.5 would (alternating parity) */
+                                    8.2.4.2.4/8.2.4.2.5 would (alternating parity); or H264R_MBAFF_FRAME:
+                                    a frame of MB pairs (height_mbs even), each pair frame or field
+                                    (H264R_MBF_FIELD) at random, slices of whole pair rows, a field MB's
+                                    refIdx over the 2 num_refs fields (4:2:0; wp_mode 0/1; no SP,
+                                    no lossless) */
     int32_t  chroma_format;      /* chroma_format_idc: 3 = 4:4:4 (every plane coded like luma: three
                                     luma-like level blocks per MB, CodedBlockPatternChroma 0, a PCM MB
                                     3 x 256 samples; frame pictures); 2 = 4:2:2 (chroma 8 x 16 per MB:

@@ -336,11 +336,14 @@ typedef struct {
     int wmb, hmb, W, H, Wc, Hc, W4, H4;
     int cf, MHc;           /* chroma_format_idc (1, 2) and MbHeightC (8, 16) */
     int fld, bot;          /* a field picture (shr.field_pic_flag) and its parity (bottom_field_flag) */
+    int mbaff;             /* an MBAFF frame (shr.MbaffFrameFlag): MB pairs, records in storage rows */
     int16_t* slice_nr;     /* slice_nr per MB, -1 until decoded (reset_mbs slice_data.cc:55, mb.init :465) */
     uint8_t  (*strength_ver)[4][16];   /* mb_t::strength_ver, deblock.cc:80 */
     uint8_t  (*strength_hor)[4][16];   /* mb_t::strength_hor, deblock.cc:159 */
     uint8_t  (*fver)[2][4];            /* filterVerEdgeFlag[chroma][edge], deblock.cc:255-278 */
     uint8_t  (*fhor)[2][4];            /* filterHorEdgeFlag */
+    uint8_t  (*strength_hor4)[16];     /* MBAFF: strength_hor[4], the second field edge (deblock.cc:285-286) */
+    uint8_t  (*fhor4)[2];              /* MBAFF: filterHorEdgeFlag[chroma][4] (:262-263) */
 } pstate;
 
 static inline const h264r_mb* mb_at(const pstate* s, int addr) { return &s->p->mbs[addr]; }
@@ -349,9 +352,42 @@ static inline const h264r_slice* slice_of(const pstate* s, const h264r_mb* mb) {
 /* Neighbour::get_neighbour for non-MBAFF frames (neighbour.cc:123-173) followed by the
  * callers' slice check (e.g. intra_prediction.cc:145-152).  Returns the MB address or -1;
  * (*ax,*ay) receive the absolute sample location. */
+static inline int is_field_mb(const pstate* s, int addr) { return (s->p->mbs[addr].flags & H264R_MBF_FIELD) != 0; }
+
+/* MBAFF frames.  `addr` is the storage index (mb_t::mb: row 2 pair_row + bottom, include/h264r.h);
+ * the planes hold the frame as it is after MbAffPostProc (deblock.cc:581-620), so a field MB's
+ * row y is frame row 2 y (+ 1 for the bottom MB) of its pair.  Neighbour::get_location (neighbour.cc:
+ * 47-77) of sample (ox, oy) of MB addr, in frame coordinates: */
+static void mbaff_loc(const pstate* s, int addr, int maxW, int maxH, int ox, int oy, int* x, int* y)
+{
+    const int mby = addr / s->wmb, b = mby & 1;
+    *x = (addr % s->wmb) * maxW + ox;
+    *y = (mby >> 1) * 2 * maxH + (is_field_mb(s, addr) ? b + 2 * oy : b * maxH + oy);
+}
+/* Neighbour::get_mb / get_neighbour (neighbour.cc:175-227): the MB holding frame sample (x, y) --
+ * the bottom MB of its pair when the pair is a field pair and y is odd, or a frame pair and y is in
+ * its lower half -- or -1 outside the picture; *ly = the sample's row inside that MB */
+static int mbaff_mb_at(const pstate* s, int maxW, int maxH, int x, int y, int* ly)
+{
+    if (x < 0 || x >= s->wmb * maxW || y < 0 || y >= s->hmb * maxH) return -1;
+    const int top = ((y / (2 * maxH)) * 2) * s->wmb + x / maxW, r = y % (2 * maxH);
+    const int f = is_field_mb(s, top);
+    const int b = f ? (y & 1) : r >= maxH;
+    if (ly) *ly = f ? r / 2 : r % maxH;
+    return top + b * s->wmb;
+}
+
 static int get_neighbour(const pstate* s, int chroma, int addr, int ox, int oy, int* ax, int* ay)
 {
     int maxW = chroma ? 8 : 16, maxH = chroma ? s->MHc : 16;
+    if (s->mbaff) {
+        int x, y;
+        mbaff_loc(s, addr, maxW, maxH, ox, oy, &x, &y);
+        int n = mbaff_mb_at(s, maxW, maxH, x, y, NULL);
+        if (n < 0 || s->slice_nr[n] != s->slice_nr[addr]) return -1;
+        *ax = x; *ay = y;
+        return n;
+    }
     int x = (addr % s->wmb) * maxW + ox, y = (addr / s->wmb) * maxH + oy;
     if (x < 0 || x >= s->wmb * maxW || y < 0 || y >= s->hmb * maxH) return -1;
     int n = (y / maxH) * s->wmb + (x / maxW);
@@ -370,19 +406,14 @@ typedef struct { int avail[4]; int smp[18 * 18]; int stride; } nbr_t;   /* sampl
 static void gather_nxn(const pstate* s, int addr, int size, int xO, int yO, const uint8_t* img, int pitch, nbr_t* n)
 {
     int cip = s->p->pic->constrained_intra_pred;
-    int ax, ay, a0x = 0, a0y = 0, bx = 0, by = 0, cx = 0, cy = 0, dx = 0, dy = 0;
-    int nA[8];
-    for (int i = 0; i < size; ++i) {
-        int tx = 0, ty = 0;
-        nA[i] = get_neighbour(s, 0, addr, xO - 1, yO + i, &tx, &ty);
-        if (i == 0) { a0x = tx; a0y = ty; }
-    }
+    int bx = 0, by = 0, cx = 0, cy = 0, dx = 0, dy = 0;
+    int nA[8], ax[8] = {0}, ay[8] = {0};          /* each row's own sample (an MBAFF pair's rows) */
+    for (int i = 0; i < size; ++i) nA[i] = get_neighbour(s, 0, addr, xO - 1, yO + i, &ax[i], &ay[i]);
     int nB = get_neighbour(s, 0, addr, xO, yO - 1, &bx, &by);
     int nC = get_neighbour(s, 0, addr, xO + size, yO - 1, &cx, &cy);
     int nD = get_neighbour(s, 0, addr, xO - 1, yO - 1, &dx, &dy);
     if (size == 4 && xO == 4 && (yO == 4 || yO == 12)) nC = -1;   /* :154 */
     if (size == 8 && xO == 8 && yO == 8) nC = -1;                  /* :376 */
-    (void)ax; (void)ay;
     n->stride = 18;
     if (cip) {
         n->avail[0] = 1;
@@ -396,7 +427,7 @@ static void gather_nxn(const pstate* s, int addr, int size, int xO, int yO, cons
     }
     if (n->avail[3]) P(n, -1, -1) = img[dy * pitch + dx];
     if (n->avail[0])
-        for (int y = 0; y < size; ++y) P(n, -1, y) = img[(a0y + y) * pitch + a0x];
+        for (int y = 0; y < size; ++y) P(n, -1, y) = img[ay[y] * pitch + ax[y]];
     if (n->avail[1]) {
         for (int x = 0; x < size; ++x) P(n, x, -1) = img[by * pitch + bx + x];
         for (int x = size; x < 2 * size; ++x)
@@ -692,22 +723,29 @@ static int inter_pred_mb(const pstate* s, int addr, int mbp[3][16][16])
     const h264r_slice* sl = slice_of(s, mb);
     int mbx = addr % s->wmb, mby = addr / s->wmb;
     int plane_n = s->W4 * s->H4;
+    /* an MBAFF field MB predicts from fields (get_ref_pic dpb.cc:1046-1055): field refIdx r is frame
+       r / 2 of the list, the MB's own parity when r is even; its block rows are field rows
+       (block_y_aff, inter_prediction.cc:470-474) of a field of half the height (:172,181-183) */
+    const int fmb = s->mbaff && is_field_mb(s, addr), mbot = mby & 1;
+    const int fld = s->fld || fmb, cbot = s->fld ? s->bot : mbot;
+    const int row4 = fmb ? (mby >> 1) * 4 : mby * 4;
     for (int j = 0; j < 4; ++j)
         for (int i = 0; i < 4; ++i) {
             int idx = (mby * 4 + j) * s->W4 + mbx * 4 + i;
-            int r[2], vx[2], vy[2], slot[2], bot[2], vyc[2];
+            int r[2], vx[2], vy[2], slot[2], bot[2], vyc[2], rw[2];
             for (int l = 0; l < 2; ++l) {
                 r[l] = p->ref_idx[l * plane_n + idx];
                 uint32_t m = p->mv[l * plane_n + idx];
                 vx[l] = (mbx * 4 + i) * 16 + (int16_t)(m & 0xFFFF);
-                vy[l] = (mby * 4 + j) * 16 + (int16_t)(m >> 16);
-                int ref = r[l] >= 0 ? sl->ref_slot[l][r[l]] : -1;
+                vy[l] = (row4 + j) * 16 + (int16_t)(m >> 16);
+                rw[l] = fmb && r[l] >= 0 ? r[l] >> 1 : r[l];       /* the weights' index (:66,100-101) */
+                int ref = r[l] >= 0 ? sl->ref_slot[l][rw[l]] : -1;
                 /* a field picture's list entries name a field of a DPB frame (include/h264r.h) */
                 slot[l] = ref < 0 ? -1 : s->fld ? (ref & ~H264R_REF_BOTTOM) : ref;
-                bot[l] = s->fld && ref >= 0 && (ref & H264R_REF_BOTTOM);
-                /* get_block_chroma inter_prediction.cc:352-355: a reference field of the other
-                   parity moves the chroma vector by -2 (top field) / +2 (bottom field) */
-                vyc[l] = vy[l] + (s->fld && bot[l] != s->bot ? (s->bot ? 2 : -2) : 0);
+                bot[l] = s->fld ? ref >= 0 && (ref & H264R_REF_BOTTOM) : fmb && r[l] >= 0 && ((r[l] & 1) != mbot);
+                /* get_block_chroma inter_prediction.cc:352-361: a reference field of the other
+                   parity moves the chroma vector by -2 (top field / top MB) / +2 (bottom) */
+                vyc[l] = vy[l] + (fld && r[l] >= 0 && bot[l] != cbot ? (cbot ? 2 : -2) : 0);
             }
             int dir = (r[0] >= 0 && r[1] >= 0) ? 2 : (r[0] >= 0 ? 0 : (r[1] >= 0 ? 1 : -1));
             if (dir < 0) return H264R_EINVAL;
@@ -724,9 +762,9 @@ static int inter_pred_mb(const pstate* s, int addr, int mbp[3][16][16])
                         for (int l = 0; l < 2; ++l) {
                             if (!(dir == 2 || dir == l)) continue;
                             const uint8_t* img = p->ref_planes[slot[l]][pl] + bot[l] * Wp;
-                            const int pitch = Wp << s->fld;
-                            if (!pl) v[l] = luma_sample(img, Wp, pitch, Hp, (vx[l] >> 2) + x, (vy[l] >> 2) + y, vx[l] & 3, vy[l] & 3);
-                            else if (s->cf == 1) v[l] = chroma_sample(img, Wp, pitch, Hp, (vx[l] >> 3) + x, (vyc[l] >> 3) + y, vx[l] & 7, vyc[l] & 7);
+                            const int pitch = Wp << fld, Hv = fmb ? Hp >> 1 : Hp;
+                            if (!pl) v[l] = luma_sample(img, Wp, pitch, Hv, (vx[l] >> 2) + x, (vy[l] >> 2) + y, vx[l] & 3, vy[l] & 3);
+                            else if (s->cf == 1) v[l] = chroma_sample(img, Wp, pitch, Hv, (vx[l] >> 3) + x, (vyc[l] >> 3) + y, vx[l] & 7, vyc[l] & 7);
                             else v[l] = chroma_sample(img, Wp, pitch, Hp, (vx[l] >> 3) + x, (vy[l] >> 2) + y, vx[l] & 7,
                                                       (vy[l] & 3) << 1);   /* 4:2:2: yAL = mv >> 2, yFracC (mv & 3) << 1 (:381-383) */
                         }
@@ -734,16 +772,17 @@ static int inter_pred_mb(const pstate* s, int addr, int mbp[3][16][16])
                         if (dir != 2) {
                             int wpf = sl->wp_mode == 1;      /* mc_prediction :62-85 */
                             if (wpf) {
-                                int w = sl->wp_weight[dir][r[dir]][pl], o = sl->wp_offset[dir][r[dir]][pl];
+                                int w = sl->wp_weight[dir][rw[dir]][pl], o = sl->wp_offset[dir][rw[dir]][pl];
                                 int d = pl ? sl->chroma_log2_wd : sl->luma_log2_wd;
                                 out = clip1(255, rshift_rnd(w * v[dir], d) + o);
                             } else out = v[dir];
                         } else if (sl->wp_mode) {               /* bi_prediction :99-153 */
                             int w0, w1, o0, o1;
                             if (sl->wp_mode == 1) {
-                                w0 = sl->wp_weight[0][r[0]][pl]; w1 = sl->wp_weight[1][r[1]][pl];
-                                o0 = sl->wp_offset[0][r[0]][pl]; o1 = sl->wp_offset[1][r[1]][pl];
+                                w0 = sl->wp_weight[0][rw[0]][pl]; w1 = sl->wp_weight[1][rw[1]][pl];
+                                o0 = sl->wp_offset[0][rw[0]][pl]; o1 = sl->wp_offset[1][rw[1]][pl];
                             } else {
+                                if (fmb) return H264R_EUNSUPPORTED;      /* field-MB implicit weights: not on the path */
                                 w1 = sl->implicit_w1[r[0]][r[1]]; w0 = 64 - w1; o0 = o1 = 0;
                             }
                             int d = (pl ? sl->chroma_log2_wd : sl->luma_log2_wd) + 1;
@@ -766,9 +805,12 @@ static void construct(const pstate* s, int addr, int pl, int x0, int y0, int w, 
     int mbx = addr % s->wmb, mby = addr / s->wmb;
     int NW = pl ? 8 : 16, NH = pl ? s->MHc : 16, pitch = pl ? s->Wc : s->W;
     uint8_t* img = plane_ptr(s, pl) + (mby * NH) * pitch + mbx * NW;
-    for (int y = y0; y < y0 + h; ++y)
+    for (int y = y0; y < y0 + h; ++y) {
+        uint8_t* row = img + y * pitch;
+        if (s->mbaff) { int gx, gy; mbaff_loc(s, addr, NW, NH, 0, y, &gx, &gy); row = plane_ptr(s, pl) + gy * pitch + gx; }
         for (int x = x0; x < x0 + w; ++x)
-            img[y * pitch + x] = (uint8_t)(use_res ? clip1(255, rres[y][x] + mbp[y][x]) : mbp[y][x]);
+            row[x] = (uint8_t)(use_res ? clip1(255, rres[y][x] + mbp[y][x]) : mbp[y][x]);
+    }
 }
 
 static int intra4_mode(const h264r_mb* mb, int blk) { return (mb->ipred[blk >> 1] >> ((blk & 1) * 4)) & 15; }
@@ -919,14 +961,16 @@ static int decode_mb(pstate* s, int addr)
     int mbx = addr % s->wmb, mby = addr / s->wmb;
     static __thread int cof[3][16][16], rres[3][16][16], mbp[3][16][16];
     s->slice_nr[addr] = (int16_t)mb->slice;               /* mb.init, slice_data.cc:465 */
+    if (s->mbaff && ((mb->flags & H264R_MBF_BYPASS) || slice_of(s, mb)->slice_type >= H264R_SLICE_SP))
+        return H264R_EUNSUPPORTED;                        /* lossless / SP MBAFF: not on the path */
 
     if (mb->mb_type == H264R_I_PCM) {                      /* mb_pred_ipcm decoder.cc:149-168 */
         const uint8_t* raw = (const uint8_t*)(p->levels + mb->coef_off);
-        for (int y = 0; y < 16; ++y) for (int x = 0; x < 16; ++x)
-            p->out[0][(mby * 16 + y) * s->W + mbx * 16 + x] = raw[y * 16 + x];
+        for (int y = 0; y < 16; ++y) for (int x = 0; x < 16; ++x) mbp[0][y][x] = raw[y * 16 + x];
         for (int k = 0; k < 2; ++k)
-            for (int y = 0; y < s->MHc; ++y) for (int x = 0; x < 8; ++x)
-                p->out[1 + k][(mby * s->MHc + y) * s->Wc + mbx * 8 + x] = raw[256 + k * 8 * s->MHc + y * 8 + x];
+            for (int y = 0; y < s->MHc; ++y) for (int x = 0; x < 8; ++x) mbp[1 + k][y][x] = raw[256 + k * 8 * s->MHc + y * 8 + x];
+        for (int pl = 0; pl < 3; ++pl) construct(s, addr, pl, 0, 0, pl ? 8 : 16, pl ? s->MHc : 16, 0, rres[pl], mbp[pl]);
+        (void)mbx; (void)mby;
         return 0;
     }
     load_cof(mb, p->levels, p->quant, s->cf, cof);
@@ -1028,13 +1072,18 @@ static mvinfo_t mvinfo(const pstate* s, int bx4, int by4)
 {
     const oracle_picture* p = s->p;
     int plane_n = s->W4 * s->H4, idx = by4 * s->W4 + bx4;
-    const h264r_mb* mb = mb_at(s, (by4 / 4) * s->wmb + bx4 / 4);
+    const int addr = (by4 / 4) * s->wmb + bx4 / 4;
+    const h264r_mb* mb = mb_at(s, addr);
     const h264r_slice* sl = slice_of(s, mb);
+    /* an MBAFF field MB's pictures are fields (get_ref_pic dpb.cc:1046-1055): slot | 0x80, with
+       H264R_REF_BOTTOM for the bottom field, never equal to the frame's identity */
+    const int fmb = s->mbaff && is_field_mb(s, addr), mbot = (addr / s->wmb) & 1;
     mvinfo_t m;
     for (int l = 0; l < 2; ++l) {
         int r = p->ref_idx[l * plane_n + idx];
         uint32_t v = p->mv[l * plane_n + idx];
-        m.ref[l] = r >= 0 ? sl->ref_slot[l][r] : -1;
+        m.ref[l] = r < 0 ? -1 : !fmb ? sl->ref_slot[l][r]
+                 : (sl->ref_slot[l][r >> 1] | 0x80 | (((r & 1) != mbot) ? H264R_REF_BOTTOM : 0));
         m.mvx[l] = (int16_t)(v & 0xFFFF);
         m.mvy[l] = (int16_t)(v >> 16);
     }
@@ -1221,6 +1270,170 @@ static void filter_edge(pstate* s, int addr, int chroma, int pl, int vertical, i
     }
 }
 
+
+/* ---- MBAFF frames: Deblock::strength / strength_vertical / strength_horizontal / filter_edge with
+   MbaffFrameFlag (deblock.cc:78-289, 418-535), on the frame after MbAffPostProc (:596-629).  Sample
+   positions are Neighbour::get_location / get_neighbour's (mbaff_loc / mbaff_mb_at); a block's
+   motion sits at the MB's storage row (mv_info[nb.y / 4], nb.y the MB-local row). */
+static int mbaff_mvinfo_row(const pstate* s, int n, int ly) { return (n / s->wmb) * 4 + ly / 4; }
+
+static void strength_vertical_mbaff(pstate* s, int addr, int e)          /* deblock.cc:78-155 */
+{
+    const h264r_mb* q = mb_at(s, addr);
+    uint8_t* St = s->strength_ver[addr][e];
+    const int fq = is_field_mb(s, addr), mvlimit = fq ? 2 : 4, dy = 1 + fq;
+    int xq, yq, lyp;
+    mbaff_loc(s, addr, 16, 16, e * 4, 0, &xq, &yq);
+    int P = mbaff_mb_at(s, 16, 16, xq - 1, yq, &lyp);
+    const h264r_mb* pm = mb_at(s, P);
+    const int mixed = fq != is_field_mb(s, P);
+    const int special = is_special(s, pm) || is_special(s, q);
+    /* cond_bS4 = !field || (MbaffFrameFlag && verticalEdgeFlag) = 1; cond_bS3 = !mixed */
+    if (e == 0 && special) { memset(St, 4, 16); return; }
+    if (!mixed && special) { memset(St, 3, 16); return; }
+    if (e > 0 && slice_of(s, q)->slice_type == H264R_SLICE_P && q->mb_type == H264R_P_SKIP) { memset(St, 0, 16); return; }
+    for (int y = 0; y < 16; ++y) {
+        int v;
+        const int intra = ((pm->flags | q->flags) & H264R_MBF_INTRA) != 0;
+        const int blkP = (lyp & 12) + ((xq - 1) & 15) / 4, blkQ = (y & 12) + e;
+        if (e == 0 && intra) v = 4;
+        else if (!mixed && intra) v = 3;
+        else if (((q->cbp_blks >> blkQ) & 1) || ((pm->cbp_blks >> blkP) & 1)) v = 2;
+        else if (mixed) v = 1;
+        else if (e > 0 && (q->mb_type == H264R_P_16x16 || q->mb_type == H264R_P_16x8)) v = 0;
+        else {
+            mvinfo_t mq = mvinfo(s, xq / 4, mbaff_mvinfo_row(s, addr, y));
+            mvinfo_t mp = mvinfo(s, (xq - 1) / 4, mbaff_mvinfo_row(s, P, lyp));
+            v = bs_compare_mvs(&mq, &mp, mvlimit);
+        }
+        St[y] = (uint8_t)v;
+        if (y < 15) { P = mbaff_mb_at(s, 16, 16, xq - 1, yq + dy * (y + 1), &lyp); pm = mb_at(s, P); }
+    }
+}
+
+static void strength_horizontal_mbaff(pstate* s, int addr, int e)        /* deblock.cc:157-228 */
+{
+    const h264r_mb* q = mb_at(s, addr);
+    uint8_t* St = e == 4 ? s->strength_hor4[addr] : s->strength_hor[addr][e];
+    const int fq = is_field_mb(s, addr), mvlimit = fq ? 2 : 4;
+    const int dy = 1 + (fq || ((e == 0 || e == 4) && s->fhor4[addr][0]));
+    int xq, yq, lyq, lyp;
+    mbaff_loc(s, addr, 16, 16, 0, 0, &xq, &yq);
+    yq += e == 4 ? 1 : dy * e * 4;
+    const int Q = mbaff_mb_at(s, 16, 16, xq, yq, &lyq);
+    const int P = mbaff_mb_at(s, 16, 16, xq, yq - dy, &lyp);
+    const h264r_mb* pm = mb_at(s, P);
+    const int mixed = fq != is_field_mb(s, P);
+    const int special = is_special(s, pm) || is_special(s, q);
+    const int field = is_field_mb(s, P) || fq;
+    const int intra = ((pm->flags | q->flags) & H264R_MBF_INTRA) != 0;
+    /* cond_bS4 = !field (horizontal), cond_bS3 = 1 */
+    if (e == 0 && !field && (special || intra)) { memset(St, 4, 16); return; }
+    if (special || intra) { memset(St, 3, 16); return; }
+    if (e > 0 && e < 4 && slice_of(s, q)->slice_type == H264R_SLICE_P && q->mb_type == H264R_P_SKIP) { memset(St, 0, 16); return; }
+    for (int x4 = 0; x4 < 4; ++x4) {
+        int v;
+        if (((q->cbp_blks >> ((lyq & 12) + x4)) & 1) || ((pm->cbp_blks >> ((lyp & 12) + x4)) & 1)) v = 2;
+        else if (mixed) v = 1;
+        else if (e > 0 && e < 4 && (q->mb_type == H264R_P_16x16 || q->mb_type == H264R_P_8x16)) v = 0;
+        else {
+            mvinfo_t mq = mvinfo(s, xq / 4 + x4, mbaff_mvinfo_row(s, Q, lyq));
+            mvinfo_t mp = mvinfo(s, xq / 4 + x4, mbaff_mvinfo_row(s, P, lyp));
+            v = bs_compare_mvs(&mq, &mp, mvlimit);
+        }
+        memset(St + 4 * x4, v, 4);
+    }
+}
+
+static void strength_mbaff(pstate* s, int addr)                          /* deblock.cc:230-289 */
+{
+    const h264r_mb* q = mb_at(s, addr);
+    const h264r_slice* sl = slice_of(s, q);
+    memset(s->fver[addr], 0, sizeof(s->fver[addr]));
+    memset(s->fhor[addr], 0, sizeof(s->fhor[addr]));
+    memset(s->fhor4[addr], 0, sizeof(s->fhor4[addr]));
+    if (sl->deblock_idc == 1) return;
+    const int fq = is_field_mb(s, addr), dy = 1 + fq;
+    int xq, yq;
+    mbaff_loc(s, addr, 16, 16, 0, 0, &xq, &yq);
+    const int L = mbaff_mb_at(s, 16, 16, xq - 1, yq, NULL), U = mbaff_mb_at(s, 16, 16, xq, yq - dy, NULL);
+    int fl = 0, ft = 0;
+    if (sl->deblock_idc == 0) { fl = L >= 0; ft = U >= 0; }
+    else if (sl->deblock_idc == 2) {
+        fl = L >= 0 && mb_at(s, L)->slice == q->slice;
+        ft = U >= 0 && mb_at(s, U)->slice == q->slice;
+    }
+    for (int c = 0; c < 2; ++c) {
+        s->fver[addr][c][0] = fl; s->fhor[addr][c][0] = ft;
+        for (int e = 1; e < 4; ++e) s->fver[addr][c][e] = s->fhor[addr][c][e] = 1;
+        s->fhor4[addr][c] = ft && !fq && is_field_mb(s, U);
+    }
+    if (q->flags & H264R_MBF_T8x8) s->fver[addr][0][1] = s->fver[addr][0][3] = s->fhor[addr][0][1] = s->fhor[addr][0][3] = 0;
+    s->fver[addr][1][2] = s->fver[addr][1][3] = s->fhor[addr][1][2] = s->fhor[addr][1][3] = 0;
+    for (int e = 0; e < 4; ++e) {
+        if (s->fver[addr][0][e]) strength_vertical_mbaff(s, addr, e);
+        if (s->fhor[addr][0][e]) strength_horizontal_mbaff(s, addr, e);
+        if (e == 0 && s->fhor4[addr][0]) strength_horizontal_mbaff(s, addr, 4);
+    }
+}
+
+/* filter_edge (deblock.cc:418-486) on an MBAFF frame: `edge` the sample offset, or 1 for the second
+   field edge of a frame MB under a field pair (strength_hor[4], rows 1, 3, 5 against -1, -3, -5) */
+static void filter_edge_mbaff(pstate* s, int addr, int chroma, int pl, int vertical, int fmode, int edge)
+{
+    const h264r_mb* q = mb_at(s, addr);
+    const h264r_slice* sl = slice_of(s, q);
+    const uint8_t* St = vertical ? s->strength_ver[addr][chroma ? edge * 4 / 8 : edge / 4]
+                      : edge == 1 ? s->strength_hor4[addr] : s->strength_hor[addr][chroma ? edge * 4 / 8 : edge / 4];
+    const int nE = chroma ? 8 : 16, pitch = chroma ? s->Wc : s->W, dy = 1 + fmode;
+    int xI, yI;
+    mbaff_loc(s, addr, 16, 16, 0, 0, &xI, &yI);
+    const int xP = chroma ? xI / 2 : xI, yP = chroma ? (yI + 1) / 2 : yI;
+    int xJ = xI, yJ = yI;
+    if (vertical) xJ += (edge - 1) * (chroma ? 2 : 1);
+    else yJ += dy * (edge - 1) * (chroma ? 2 : 1) - (edge % 2);
+    int P = mbaff_mb_at(s, 16, 16, xJ, yJ, NULL);
+    uint8_t* img = s->p->out[pl];
+    const int incQ = vertical ? 1 : dy * pitch, nxtQ = vertical ? dy * pitch : 1;
+    uint8_t* src = vertical ? &img[yP * pitch + xP + edge] : &img[(yP + dy * edge - (edge % 2)) * pitch + xP];
+    const int mixed = vertical && !is_field_mb(s, addr) && is_field_mb(s, P);
+    for (int pel = 0; pel < nE; ++pel, src += nxtQ) {
+        const int bS = St[nE == 8 ? (pel << 1) + (mixed && (pel & 1)) : pel];
+        if (!bS) continue;
+        if (vertical) P = mbaff_mb_at(s, 16, 16, xJ, yI + dy * pel * (chroma ? 2 : 1) + (chroma && mixed && (pel & 1)), NULL);
+        const h264r_mb* pm = mb_at(s, P);
+        const int qPp = chroma ? pm->qp_c[pl - 1] : pm->qp_y, qPq = chroma ? q->qp_c[pl - 1] : q->qp_y;
+        const int qPav = (qPp + qPq + 1) >> 1;
+        const int indexA = clip3(0, 51, qPav + sl->filter_offset_a), indexB = clip3(0, 51, qPav + sl->filter_offset_b);
+        filter_line(src, incQ, TABLE_ALPHA[indexA], TABLE_BETA[indexB], bS, chroma, bS < 4 ? TABLE_TC0[indexA][bS - 1] : 0);
+    }
+}
+
+/* filter_vertical + filter_horizontal (deblock.cc:488-535) of one MB of an MBAFF frame */
+static void filter_mb_mbaff(pstate* s, int a)
+{
+    const int fq = is_field_mb(s, a);
+    for (int e = 0; e < 4; ++e) {
+        if (s->fver[a][0][e]) filter_edge_mbaff(s, a, 0, 0, 1, fq, e * 4);
+        if (s->fver[a][1][e]) { filter_edge_mbaff(s, a, 1, 1, 1, fq, e * 4); filter_edge_mbaff(s, a, 1, 2, 1, fq, e * 4); }
+    }
+    for (int e = 0; e < 4; ++e) {
+        if (s->fhor[a][0][e]) {
+            if (!(e == 0 && s->fhor4[a][0])) filter_edge_mbaff(s, a, 0, 0, 0, fq, e * 4);
+            else { filter_edge_mbaff(s, a, 0, 0, 0, 1, 0); filter_edge_mbaff(s, a, 0, 0, 0, 1, 1); }
+        }
+        if (s->fhor[a][1][e]) {
+            for (int pl = 1; pl <= 2; ++pl) {
+                if (!(e == 0 && s->fhor4[a][1])) filter_edge_mbaff(s, a, 1, pl, 0, fq, e * 4);
+                else { filter_edge_mbaff(s, a, 1, pl, 0, 1, 0); filter_edge_mbaff(s, a, 1, pl, 0, 1, 1); }
+            }
+        }
+    }
+}
+
+/* MB address a of an MBAFF frame (pair a / 2, top or bottom) -> storage index */
+static inline int mbaff_storage(const pstate* s, int a) { return ((a >> 1) / s->wmb * 2 + (a & 1)) * s->wmb + (a >> 1) % s->wmb; }
+
 /* deblock_pic (deblock.cc:537-552) + the Deblock::deblock gate (:631-640). */
 /* ---------------------------------------------------------------- 4:4:4 (ChromaArrayType 3)
  * Decoder::decode runs decode_one_component for PLANE_Y, PLANE_U and PLANE_V (decoder.cc:65-79):
@@ -1306,9 +1519,13 @@ static int init_state(pstate* s, const oracle_picture* p)
     s->cf = p->chroma_format == 2 ? 2 : 1;
     s->MHc = s->cf == 2 ? 16 : 8;
     s->W = s->wmb * 16; s->H = s->hmb * 16; s->Wc = s->wmb * 8; s->Hc = s->hmb * s->MHc; s->W4 = s->wmb * 4; s->H4 = s->hmb * 4;
-    s->fld = p->pic->structure != H264R_FRAME; s->bot = p->pic->structure == H264R_BOTTOM_FIELD;
-    /* field pictures are on the 4:2:0 path only (the chroma field offset :348-360 is ChromaArrayType 1) */
-    return s->fld && s->cf != 1 ? H264R_EUNSUPPORTED : 0;
+    s->fld = p->pic->structure == H264R_TOP_FIELD || p->pic->structure == H264R_BOTTOM_FIELD;
+    s->bot = p->pic->structure == H264R_BOTTOM_FIELD;
+    s->mbaff = p->pic->structure == H264R_MBAFF_FRAME;
+    if (s->mbaff && (s->hmb & 1)) return H264R_EINVAL;
+    /* field pictures and MBAFF frames are on the 4:2:0 path only (the chroma field offset :348-361 is
+       ChromaArrayType 1) */
+    return (s->fld || s->mbaff) && s->cf != 1 ? H264R_EUNSUPPORTED : 0;
 }
 
 int oracle_deblock_picture(const oracle_picture* p)
@@ -1326,9 +1543,17 @@ int oracle_deblock_picture(const oracle_picture* p)
     s.strength_hor = calloc((size_t)n, sizeof(*s.strength_hor));
     s.fver = calloc((size_t)n, sizeof(*s.fver));
     s.fhor = calloc((size_t)n, sizeof(*s.fhor));
-    if (!s.strength_ver || !s.strength_hor || !s.fver || !s.fhor) {
-        free(s.strength_ver); free(s.strength_hor); free(s.fver); free(s.fhor);
+    s.strength_hor4 = calloc((size_t)n, sizeof(*s.strength_hor4));
+    s.fhor4 = calloc((size_t)n, sizeof(*s.fhor4));
+    if (!s.strength_ver || !s.strength_hor || !s.fver || !s.fhor || !s.strength_hor4 || !s.fhor4) {
+        free(s.strength_ver); free(s.strength_hor); free(s.fver); free(s.fhor); free(s.strength_hor4); free(s.fhor4);
         return H264R_ENOMEM;
+    }
+    if (s.mbaff) {                       /* MBAFF address order (deblock.cc:543-551) */
+        for (int a = 0; a < n; ++a) strength_mbaff(&s, mbaff_storage(&s, a));
+        for (int a = 0; a < n; ++a) filter_mb_mbaff(&s, mbaff_storage(&s, a));
+        free(s.strength_ver); free(s.strength_hor); free(s.fver); free(s.fhor); free(s.strength_hor4); free(s.fhor4);
+        return 0;
     }
     for (int a = 0; a < n; ++a) strength(&s, a);
     for (int a = 0; a < n; ++a) {
@@ -1342,7 +1567,7 @@ int oracle_deblock_picture(const oracle_picture* p)
             if (s.fhor[a][1][e]) { filter_edge(&s, a, 1, 1, 0, e * 4); filter_edge(&s, a, 1, 2, 0, e * 4); }
         }
     }
-    free(s.strength_ver); free(s.strength_hor); free(s.fver); free(s.fhor);
+    free(s.strength_ver); free(s.strength_hor); free(s.fver); free(s.fhor); free(s.strength_hor4); free(s.fhor4);
     return 0;
 }
 
@@ -1357,7 +1582,7 @@ int oracle_reconstruct_picture(const oracle_picture* p)
     if (!s.slice_nr) return H264R_ENOMEM;
     for (int a = 0; a < n; ++a) s.slice_nr[a] = -1;
     int st = 0;
-    for (int a = 0; a < n && !st; ++a) st = decode_mb(&s, a);
+    for (int a = 0; a < n && !st; ++a) st = decode_mb(&s, s.mbaff ? mbaff_storage(&s, a) : a);
     free(s.slice_nr);
     return st;
 }

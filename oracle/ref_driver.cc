@@ -102,7 +102,10 @@ int main(int argc, char** argv)
     if (argc > k + 4) cfg.chroma_format = atoi(argv[k + 4]);
     const bool f444 = cfg.chroma_format == 3, f422 = cfg.chroma_format == 2, f400 = cfg.chroma_format == H264R_SYNTH_CHROMA_400;
     const int CW = f400 ? 0 : f444 ? 16 : 8, CH = f400 ? 0 : f444 || f422 ? 16 : 8;   /* chroma samples per MB */
-    const bool fld = cfg.structure != H264R_FRAME;
+    const bool fld = cfg.structure == H264R_TOP_FIELD || cfg.structure == H264R_BOTTOM_FIELD;
+    /* MBAFF frame (argument 25 = 3): mb_data by MB address (pairs), mb.mb the storage position,
+       field MBs predicting from the fields of the list's frames (get_ref_pic dpb.cc:1046-1055) */
+    const bool mbaff = cfg.structure == H264R_MBAFF_FRAME;
     const PictureStructure pstruct = cfg.structure == H264R_TOP_FIELD ? TOP_FIELD
                                    : cfg.structure == H264R_BOTTOM_FIELD ? BOTTOM_FIELD : FRAME;
 
@@ -182,6 +185,24 @@ int main(int argc, char** argv)
             r->is_long_term = 0; r->used_for_reference = 1;
             refs[fld ? 2 * s + f : s] = r;
         }
+        if (mbaff) {                                     /* the frame's two fields (dpb_split_field) */
+            storable_picture* fr = refs[s];
+            for (int f = 0; f < 2; ++f) {
+                storable_picture* r = new storable_picture(vid, f ? BOTTOM_FIELD : TOP_FIELD, W * 16, FH * 16, W * CW, FH * CH, 1);   /* halved by the ctor */
+                for (int y = 0; y < FH * 8; ++y) for (int x = 0; x < W * 16; ++x) r->imgY[y][x] = ty[(2 * y + f) * W * 16 + x];
+                for (int y = 0; y < FH * CH / 2; ++y) for (int x = 0; x < W * CW; ++x) {
+                    r->imgUV[0][y][x] = tu[(2 * y + f) * W * CW + x];
+                    r->imgUV[1][y][x] = tv[(2 * y + f) * W * CW + x];
+                }
+                pad_buf(*r->imgY, W * 16, FH * 8, r->iLumaStride, MCBUF_LUMA_PAD_X, MCBUF_LUMA_PAD_Y);
+                pad_buf(*r->imgUV[0], W * CW, FH * CH / 2, r->iChromaStride, r->iChromaPadX, r->iChromaPadY);
+                pad_buf(*r->imgUV[1], W * CW, FH * CH / 2, r->iChromaStride, r->iChromaPadX, r->iChromaPadY);
+                r->poc = r->frame_poc = r->top_poc = r->bottom_poc = h264r_synth_slot_poc(s) + f;
+                r->is_long_term = 0; r->used_for_reference = 1;
+                r->frame = fr;
+                (f ? fr->bottom_field : fr->top_field) = r;
+            }
+        }
     }
     /* RefPicList entry -> storable_picture (include/h264r.h: slot | H264R_REF_BOTTOM for fields) */
     auto ref_of = [&](int v) { return fld ? refs[2 * (v & 31) + ((v & H264R_REF_BOTTOM) ? 1 : 0)] : refs[v]; };
@@ -203,7 +224,7 @@ int main(int argc, char** argv)
         x->p_Vid = vid; x->active_sps = sps; x->active_pps = pps;
         shr_t& h = x->header;
         h.slice_type = c.slice_type;
-        h.structure = pstruct; h.MbaffFrameFlag = 0; h.field_pic_flag = fld;
+        h.structure = pstruct; h.MbaffFrameFlag = mbaff; h.field_pic_flag = fld;
         h.bottom_field_flag = pstruct == BOTTOM_FIELD;
         h.PicHeightInMbs = H; h.PicHeightInSamplesL = H * 16; h.PicHeightInSamplesC = H * CH;
         h.PicSizeInMbs = W * H;
@@ -242,19 +263,37 @@ int main(int argc, char** argv)
             const h264r_mb& m = mbs[(y4 / 4) * W + x4 / 4];
             pic_motion_params& p = dec->mv_info[y4][x4];
             p.slice_no = (uint8_t)m.slice;
+            const bool fmb = mbaff && (m.flags & H264R_MBF_FIELD);
+            const int mbot = (y4 / 4) & 1;
             for (int l = 0; l < 2; ++l) {
                 int r = ref_idx[(size_t)l * PL + idx];
                 uint32_t v = mv[(size_t)l * PL + idx];
                 p.ref_idx[l] = (char)r;
                 p.mv[l].mv_x = (int16_t)(v & 0xFFFF);
                 p.mv[l].mv_y = (int16_t)(v >> 16);
-                p.ref_pic[l] = r >= 0 ? sl[m.slice]->RefPicList[l][r] : nullptr;
+                /* get_ref_pic (dpb.cc:1046-1055), as the parser stores it (interpret_mb.cc:617-620) */
+                p.ref_pic[l] = r < 0 ? nullptr : !fmb ? sl[m.slice]->RefPicList[l][r]
+                             : (mbot == r % 2 ? sl[m.slice]->RefPicList[l][r / 2]->top_field
+                                              : sl[m.slice]->RefPicList[l][r / 2]->bottom_field);
             }
         }
 
-    int inv4[16], inv8[64];
+    int inv4[16], inv8[64], inv4f[16], inv8f[64];
     zigzag(4, inv4);
     zigzag(8, inv8);
+    if (mbaff) {                     /* a field MB's scans (transform.cc:344-357: mb_field_decoding_flag) */
+        mb_t probe;
+        memset((void*)&probe, 0, sizeof(probe));
+        probe.p_Slice = sl[0];
+        probe.mb_field_decoding_flag = 1;
+        for (int t8 = 0; t8 < 2; ++t8) {
+            probe.transform_size_8x8_flag = t8;
+            for (int k = 0; k < (t8 ? 64 : 16); ++k) {
+                const pos_t pos = sl[0]->decoder.transform->inverse_scan_luma_ac(&probe, k);
+                (t8 ? inv8f : inv4f)[pos.y * (t8 ? 8 : 4) + pos.x] = k;
+            }
+        }
+    }
     if (fld) {
         /* the field scans (Tables 8-13 / 8-14) as the reference maps them: raster position of
            each scan index from its own Transform::inverse_scan_luma_ac on a field slice */
@@ -306,15 +345,20 @@ int main(int argc, char** argv)
     if (rep) memcpy((void*)mb_data, mb_pristine.data(), mb_pristine.size());
     const auto t0 = std::chrono::steady_clock::now();
     for (int a = 0; a < NMB; ++a) {
-        const h264r_mb& c = mbs[a];
+        /* MBAFF: MB address a is pair a / 2's top or bottom MB, stored at row 2 pair_row + a % 2 */
+        const int si = mbaff ? ((a / 2) / W * 2 + a % 2) * W + (a / 2) % W : a;
+        const h264r_mb& c = mbs[si];
         slice_t& s = *sl[c.slice];
         mb_t& mb = mb_data[a];
-        mb.p_Slice = &s; mb.mbAddrX = a; mb.mb.x = a % W; mb.mb.y = a / W;
+        mb.p_Slice = &s; mb.mbAddrX = a; mb.mb.x = si % W; mb.mb.y = si / W;
         mb.slice_nr = (short)c.slice;
         mb.is_intra_block = (c.flags & H264R_MBF_INTRA) != 0;
         mb.mb_type = c.mb_type;
         mb.transform_size_8x8_flag = (c.flags & H264R_MBF_T8x8) != 0;
-        mb.mb_field_decoding_flag = 0;
+        mb.mb_field_decoding_flag = mbaff && (c.flags & H264R_MBF_FIELD);
+        if (mbaff) dec->motion.mb_field_decoding_flag[a] = mb.mb_field_decoding_flag;
+        const int* sc4 = mb.mb_field_decoding_flag ? inv4f : inv4;
+        const int* sc8 = mb.mb_field_decoding_flag ? inv8f : inv8;
         for (int b = 0; b < 16; ++b) mb.Intra4x4PredMode[b] = (c.ipred[b >> 1] >> ((b & 1) * 4)) & 15;
         for (int b = 0; b < 4; ++b) mb.Intra8x8PredMode[b] = (c.ipred[b >> 1] >> ((b & 1) * 4)) & 15;
         mb.Intra16x16PredMode = c.i16_mode;
@@ -328,7 +372,7 @@ int main(int argc, char** argv)
         /* interpret_mb.cc:804 */
         mb.TransformBypassModeFlag = sps->qpprime_y_zero_transform_bypass_flag && mb.qp_scaled[0] == 0;
         if (mb.TransformBypassModeFlag != ((c.flags & H264R_MBF_BYPASS) != 0) && c.mb_type != H264R_I_PCM) {
-            fprintf(stderr, "bypass flag mismatch at MB %d\n", a);
+            fprintf(stderr, "bypass flag mismatch at MB %d\n", si);
             return 4;
         }
         memset(mb.cbp_blks, 0, sizeof(mb.cbp_blks));
@@ -384,7 +428,7 @@ int main(int argc, char** argv)
             auto push_luma = [&](ColorPlane pl, const int16_t* const* b8, const int16_t* dc) {
                 if (dc) {
                     for (int pos = 0; pos < 16; ++pos)
-                        if (dc[pos]) s.decoder.coeff_luma_dc(&mb, pl, 0, 0, inv4[pos], dc[pos]);
+                        if (dc[pos]) s.decoder.coeff_luma_dc(&mb, pl, 0, 0, sc4[pos], dc[pos]);
                     s.decoder.transform_luma_dc(&mb, pl);
                 }
                 for (int q = 0; q < 4; ++q) {
@@ -394,14 +438,14 @@ int main(int argc, char** argv)
                             int x0 = (q & 1) * 2 + (b4 & 1), y0 = (q >> 1) * 2 + (b4 >> 1);
                             for (int pos = 0; pos < 16; ++pos) {
                                 int v = b8[q][b4 * 16 + pos];
-                                if (v) s.decoder.coeff_luma_ac(&mb, pl, x0, y0, inv4[pos], v);
+                                if (v) s.decoder.coeff_luma_ac(&mb, pl, x0, y0, sc4[pos], v);
                             }
                         }
                     } else {
                         int x0 = (q & 1) * 2, y0 = (q >> 1) * 2;
                         for (int pos = 0; pos < 64; ++pos) {
                             int v = b8[q][pos];
-                            if (v) s.decoder.coeff_luma_ac(&mb, pl, x0, y0, inv8[pos], v);
+                            if (v) s.decoder.coeff_luma_ac(&mb, pl, x0, y0, sc8[pos], v);
                         }
                     }
                 }
@@ -426,12 +470,12 @@ int main(int argc, char** argv)
                     for (int b = 0; b < nb; ++b)
                         for (int pos = 1; pos < 16; ++pos) {
                             int v = cac[(pl - 1) * nb * 16 + b * 16 + pos];
-                            if (v) s.decoder.coeff_chroma_ac(&mb, (ColorPlane)pl, b % 2, b / 2, inv4[pos], v);
+                            if (v) s.decoder.coeff_chroma_ac(&mb, (ColorPlane)pl, b % 2, b / 2, sc4[pos], v);
                         }
             }
         }
         if ((uint16_t)mb.cbp_blks[0] != c.cbp_blks) {
-            fprintf(stderr, "cbp_blks mismatch at MB %d: reference %04x synth %04x\n", a, (unsigned)mb.cbp_blks[0], c.cbp_blks);
+            fprintf(stderr, "cbp_blks mismatch at MB %d: reference %04x synth %04x\n", si, (unsigned)mb.cbp_blks[0], c.cbp_blks);
             return 4;
         }
         static const char* dump = getenv("H264R_DUMP_MB");
@@ -448,7 +492,11 @@ int main(int argc, char** argv)
             for (int y = 0; y < 16; ++y) { for (int x = 0; x < 16; ++x) fprintf(stderr, "%4d", s.mb_pred[0][y][x]); fprintf(stderr, "\n"); }
         }
     }
-    if (!recon_only) sl[0]->decoder.deblock_filter(*sl[0]);
+    /* MBAFF: the loop filter's MbAffPostProc (deblock.cc:596-629) interleaves the field MBs; the
+       reconstruction alone is that with every slice's filter off (:631-640) */
+    if (recon_only && mbaff)
+        for (slice_t* x : sl) x->header.disable_deblocking_filter_idc = 1;
+    if (!recon_only || mbaff) sl[0]->decoder.deblock_filter(*sl[0]);
     sec += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     }
     if (reps_env) {

@@ -136,6 +136,23 @@ CASES = [
                                          intra_permille=300), [0, 1]),
     ("b400_cif_3slices_idc2", 4, 22, 9, dict(chroma_format=4, num_refs=3, num_slices=3, deblock_idc=2), [0]),
     ("p400_qcif_lossless", 3, 11, 9, dict(chroma_format=4, qp_min=0, qp_max=20, lossless_permille=500), [0]),
+    # MBAFF frames (MbaffFrameFlag, structure 3): frame and field MB pairs at random; field MBs predict
+    # from fields (get_ref_pic dpb.cc:1046-1055) with field block rows and the chroma parity offset
+    # (inter_prediction.cc:356-361,470-474), intra neighbours where get_neighbour finds them
+    # (neighbour.cc:123-173), MbAffPostProc and the mixed-edge loop filter (deblock.cc:78-289,418-629)
+    ("imbaff_qcif_pcm", 2, 11, 8, dict(structure=3, pcm_permille=30), [0, 1]),
+    ("imbaff_cif_4x4_cip_2slices_idc2", 2, 22, 18, dict(structure=3, transform8x8=0, constrained_intra=1,
+                                                        num_slices=2, deblock_idc=2), [0]),
+    ("pmbaff_qcif", 3, 11, 8, dict(structure=3, num_refs=3), [0, 1]),
+    ("pmbaff_cif_wp_cip_pcm", 3, 22, 18, dict(structure=3, wp_mode=1, num_refs=2, constrained_intra=1,
+                                              intra_permille=300, pcm_permille=30), [0]),
+    ("pmbaff_qcif_bigmv_offsets", 3, 11, 8, dict(structure=3, mv_range_x=200, mv_range_y=120,
+                                                 filter_offset_a=6, filter_offset_b=-6), [0]),
+    ("bmbaff_qcif_default_t8", 4, 11, 8, dict(structure=3, wp_mode=0, num_refs=3), [0, 1]),
+    ("bmbaff_cif_explicit_3slices_idc2", 4, 22, 18, dict(structure=3, wp_mode=1, num_refs=4, num_slices=3,
+                                                         deblock_idc=2), [0]),
+    ("bmbaff_qcif_scaling_idc1", 4, 11, 8, dict(structure=3, wp_mode=0, deblock_idc=1, qm=19), [0]),
+    ("pmbaff_1080p_strip", 3, 120, 8, dict(structure=3, qp_min=10, qp_max=51), [0]),
 ]
 
 
