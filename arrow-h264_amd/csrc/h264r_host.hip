@@ -38,6 +38,9 @@ extern "C" __global__ void k_untile(h264r_batch b, int2 rows, const uint8_t* rec
 extern "C" __global__ void k_c422_inter(h264r_batch b, int2 rows, int* err);
 extern "C" __global__ void k_c422_intra(h264r_batch b, int2 rows, int* err);
 extern "C" __global__ void k_c422_db(h264r_batch b, const h264r::DbInfo* dbinfo, int2 rows, int* err);
+extern "C" __global__ void k_mbaff_inter(h264r_batch b, int* err);
+extern "C" __global__ void k_mbaff_intra(h264r_batch b, int diag, int* err);
+extern "C" __global__ void k_mbaff_deblock(h264r_batch b, int diag, int* err);
 extern "C" __global__ void k_intra_pic(h264r_batch b, int* sync, int* err, const uint16_t* lvl, int lmax, int2 rows,
                                       int gstep, uint8_t* recon, const int* pband);
 extern "C" __global__ void k_level(h264r_batch b, uint16_t* lvl, int* lvsync, int* lcount, int2 rows, int deep_cut,
@@ -900,6 +903,37 @@ static int run_422(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row0, 
     return H264R_OK;
 }
 
+// MBAFF frames (include/h264r.h H264R_MBAFF_FRAME, k_mbaff.hip): I_PCM and inter MBs in one launch,
+// then the intra MBs and the loop filter each as one launch per anti-diagonal d = x + 2 y of the
+// MB-pair grid (a pair's neighbours -- and the pairs its filtering modifies -- lie on earlier
+// diagonals).  Whole pictures only.
+static int run_mbaff(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row0, int row1)
+{
+    if (c->fmt != 1) return H264R_EUNSUPPORTED;
+    if ((b.height_mbs & 1) || row0 != 0 || row1 != b.height_mbs) return H264R_EINVAL;
+    const int P = b.num_pics, W = b.width_mbs, HP = b.height_mbs / 2, ndiag = W + 2 * (HP - 1);
+    Timed whole(c, 3, s);
+    if (c->timing) c->timed_launches++;
+    {
+        Timed t(c, 0, s);
+        hipLaunchKernelGGL(k_mbaff_inter, dim3((unsigned)((size_t)P * W * b.height_mbs)), dim3(256), 0, s, b, c->d_err);
+        HIP_OK(hipGetLastError());
+    }
+    {
+        Timed t(c, 1, s);
+        for (int d = 0; d < ndiag; ++d)
+            hipLaunchKernelGGL(k_mbaff_intra, dim3((unsigned)(P * HP)), dim3(256), 0, s, b, d, c->d_err);
+        HIP_OK(hipGetLastError());
+    }
+    if (!((c->debug | knobs().debug) & H264R_DBG_NO_DEBLOCK)) {
+        Timed t(c, 2, s);
+        for (int d = 0; d < ndiag; ++d)
+            hipLaunchKernelGGL(k_mbaff_deblock, dim3((unsigned)(P * HP)), dim3(64), 0, s, b, d, c->d_err);
+        HIP_OK(hipGetLastError());
+    }
+    return H264R_OK;
+}
+
 static int run_batch(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row0, int row1)
 {
     // the scratch is shared by every launch of this context: a launch on another stream
@@ -909,6 +943,7 @@ static int run_batch(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row0
         HIP_OK(hipStreamWaitEvent(s, c->ev_last, 0));
     }
     c->last_stream = s;
+    if (b.mbaff) return run_mbaff(c, b, s, row0, row1);
     if (c->fmt == 3) return run_444(c, b, s, row0, row1);
     if (c->fmt == 2 || c->fmt == 0) return run_422(c, b, s, row0, row1);
     return launch_all(c, b, s, row0, row1, c->sc);
@@ -1105,8 +1140,33 @@ int h264r_picture_end_async(h264r_ctx* c, int keep_slot)
     if (c->fmt == 0) P.h_levels.insert(P.h_levels.end(), 64, 0);     // the luma pass's chroma view of a PCM MB
     // every referenced slot must be loaded, with a frame of this picture's size (a field
     // picture: twice its height; its entries may name either field of a slot, include/h264r.h)
-    const int fld = P.h_pic.structure != H264R_FRAME;
-    if (P.h_pic.structure < H264R_FRAME || P.h_pic.structure > H264R_BOTTOM_FIELD) return H264R_EINVAL;
+    const int fld = P.h_pic.structure == H264R_TOP_FIELD || P.h_pic.structure == H264R_BOTTOM_FIELD;
+    const int mbaff = P.h_pic.structure == H264R_MBAFF_FRAME;
+    if (P.h_pic.structure < H264R_FRAME || P.h_pic.structure > H264R_MBAFF_FRAME) return H264R_EINVAL;
+    if (mbaff) {
+        // MBAFF (include/h264r.h): 4:2:0, MB pairs, no SP slices, lossless MBs or implicit weights
+        if (P.ph & 1) return H264R_EINVAL;
+        for (const h264r_slice& sl : P.h_slices)
+            if (sl.slice_type == H264R_SLICE_SP || sl.wp_mode == 2) return H264R_EUNSUPPORTED;
+        for (const h264r_mb& m : P.h_mbs) if (m.flags & H264R_MBF_BYPASS) return H264R_EUNSUPPORTED;
+        for (size_t a = 0; a < P.h_mbs.size(); a += 1) {
+            const size_t top = ((a / P.pw) & ~(size_t)1) * P.pw + a % P.pw;
+            if ((P.h_mbs[a].flags ^ P.h_mbs[top].flags) & H264R_MBF_FIELD) return H264R_EINVAL;   // one flag per pair
+        }
+        // a field MB's refIdx names field refIdx / 2 of the list
+        for (size_t a = 0; a < P.h_mbs.size(); ++a) {
+            const h264r_mb& m = P.h_mbs[a];
+            if (m.flags & H264R_MBF_INTRA) continue;
+            const int x = (int)(a % P.pw), y = (int)(a / P.pw), W4 = P.pw * 4, plane = W4 * P.ph * 4;
+            const int nr = (m.flags & H264R_MBF_FIELD) ? 2 : 1;
+            for (int l = 0; l < 2; ++l)
+                for (int k = 0; k < 16; ++k) {
+                    const int r = P.h_ref[(size_t)l * plane + (y * 4 + k / 4) * W4 + x * 4 + k % 4];
+                    if (r >= nr * P.h_slices[m.slice].num_ref[l]) return H264R_EINVAL;
+                }
+        }
+    } else if (c->fmt == 1)
+        for (const h264r_mb& m : P.h_mbs) if (m.flags & H264R_MBF_FIELD) return H264R_EINVAL;
     const int frame_h = P.ph << fld;
     for (const h264r_slice& sl : P.h_slices)
         for (int l = 0; l < 2; ++l)
@@ -1143,6 +1203,7 @@ int h264r_picture_end_async(h264r_ctx* c, int keep_slot)
     b.mbs = c->d_mbs; b.levels = c->d_levels; b.mv = c->d_mv; b.ref_idx = c->d_ref; b.slices = c->d_slices;
     b.pics = c->d_pic; b.quant = c->d_quant; b.ref_planes = c->d_ref_planes;
     b.out_y = c->d_out; b.out_u = c->d_out + ys; b.out_v = c->d_out + ys + cs;
+    b.mbaff = mbaff;
     if ((st = run_batch(c, b, s, 0, b.height_mbs))) return st;
     if (keep_slot >= 0) {
         if ((st = ensure_slot(c, keep_slot, P.pw, frame_h))) return st;

@@ -78,4 +78,6 @@ def to_device(host: dict, n: int, ref_planes_ptr: int | None, device: str = "cud
     for k in ("mbs", "levels", "mv", "ref_idx", "slices", "pics", "quant", "out_y", "out_u", "out_v"):
         setattr(b, k, t[k].data_ptr())
     b.ref_planes = ref_planes_ptr
+    # MBAFF frames take their own launch sequence (include/h264r.h h264r_batch.mbaff)
+    b.mbaff = int(bool((host["pics"]["structure"] == A.MBAFF_FRAME).all()))
     return DeviceBatch(b, n, W, H, t, fmt)

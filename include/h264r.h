@@ -270,6 +270,9 @@ typedef struct h264r_batch {
     uint8_t*            out_u;       /* NULL allowed on a 4:0:0 context */
     uint8_t*            out_v;
     int64_t             ref_planes_stride;   /* pointers; 0 = one table for the batch (above) */
+    int32_t             mbaff;       /* ABI 4: nonzero = every picture is an H264R_MBAFF_FRAME (its own
+                                        launch sequence, whole pictures only); 0 = frames / fields */
+    int32_t             reserved;
 } h264r_batch;
 
 typedef struct h264r_ctx h264r_ctx;

@@ -1,5 +1,6 @@
 """Throughput of the chroma formats on the reconstruction path (off the headline metric): the
-config-3 workload (1080p P pictures) generated in 4:2:0, 4:2:2, 4:4:4 and 4:0:0, one
+config-3 workload (1080p P pictures) generated in 4:2:0, 4:2:2, 4:4:4 and 4:0:0 and as
+4:2:0 MBAFF frames (H264R_FORMATS=mbaff,1,... selects), one
 h264r_decode_batch of B pictures per step, timed with HIP events on the launch stream over K
 steps after W warm-up steps; picture 0 of each format checked against the oracle first.
 
@@ -31,8 +32,14 @@ def main():
     L = h264r.lib()
     from h264r import _abi as A
     W, H = 120, 68
-    for fmt in (1, 2, 3, 0):
-        cfg = synth.default_cfg(L, 3, W, H, chroma_format=fmt if fmt else A.SYNTH_CHROMA_400)
+    only = os.environ.get("H264R_FORMATS")            # e.g. "mbaff" or "1,2"
+    fmts = [f if f == "mbaff" else int(f) for f in only.split(",")] if only else [1, 2, 3, 0, "mbaff"]
+    for fmt in fmts:
+        # "mbaff": the config-3 workload as MBAFF frames (4:2:0, frame / field MB pairs)
+        mb = fmt == "mbaff"
+        cfg = synth.default_cfg(L, 3, W, H, **(dict(structure=A.MBAFF_FRAME) if mb else
+                                              dict(chroma_format=fmt if fmt else A.SYNTH_CHROMA_400)))
+        fmt = 1 if mb else fmt
         pics = [synth.picture(L, cfg, i % 8) for i in range(npics)]
         refs = synth.refpics(L, cfg)
         dec = h264r.Decoder(0, W, H, chroma_format=fmt)
@@ -57,7 +64,8 @@ def main():
         torch.cuda.synchronize()
         dec.check()
         ms = a.elapsed_time(b) / steps
-        print(json.dumps({"chroma_format": fmt, "workload": "1080p P pictures (config 3)", "pictures": npics,
+        print(json.dumps({"chroma_format": fmt, "workload": "1080p P pictures (config 3)" + (", MBAFF frames" if mb else ""),
+                          "pictures": npics,
                           "ms_per_step": ms, "macroblocks_per_s": npics * W * H / (ms / 1e3),
                           "verified_vs_oracle": ok}), flush=True)
         dec.close()
