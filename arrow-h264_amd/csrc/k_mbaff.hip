@@ -467,7 +467,7 @@ DEV int pred_16x16(const MPic& P, IntraLds& L, int r, int mode, int px, int py, 
     }
     int bx, by, dx, dy;
     const int nB = nbr(P, r, 16, 16, 0, -1, px, py, bx, by);
-    const int nD = nbr(P, r, 16, 16, -1, -1, px, py, dx, dy);
+    (void)nbr(P, r, 16, 16, -1, -1, px, py, dx, dy);
     (void)tx; (void)ty;
     const int a0 = P.cip ? allA : nA0 >= 0, a1 = P.cip ? intra_ok(P, nB) : nB >= 0;
     switch (mode) {
