@@ -32,7 +32,7 @@ namespace h264r { struct DbInfo; }
 extern "C" __global__ void k_inter4r(h264r_batch b, h264r::DbInfo* dbinfo, int2 rows, int* sp_flag, uint8_t* recon, int tag,
                                      int* zero, int nz, int* zero2, int nz2);
 extern "C" __global__ void k_inter_sp(h264r_batch b, int2 rows, const int* sp_flag, uint8_t* recon, int tag);
-extern "C" __global__ void k_derive444(h264r_batch b, int pl, h264r_mb* mbs, h264r_slice* slices, h264r_quant* quant,
+extern "C" __global__ void k_derive444(h264r_batch b, int pl, int qpl, h264r_mb* mbs, h264r_slice* slices, h264r_quant* quant,
                                        const uint8_t** refs, int ntab, int* err);
 extern "C" __global__ void k_untile(h264r_batch b, int2 rows, const uint8_t* recon);
 extern "C" __global__ void k_c422_inter(h264r_batch b, int2 rows, int* err);
@@ -838,7 +838,7 @@ static int run_444(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row0, 
         return st;
     const bool timing = c->timing;
     for (int pl = 0; pl < 3; ++pl) {
-        hipLaunchKernelGGL(k_derive444, dim3(1024), dim3(256), 0, s, b, pl, c->d444_mbs, c->d444_slices, c->d444_quant,
+        hipLaunchKernelGGL(k_derive444, dim3(1024), dim3(256), 0, s, b, pl, pl, c->d444_mbs, c->d444_slices, c->d444_quant,
                            c->d444_refs, ntab, c->d_err);
         HIP_OK(hipGetLastError());
         h264r_batch d = b;
@@ -871,17 +871,22 @@ static int run_422(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row0, 
         (st = dev_resize(&c->d444_refs, &c->c444_refs, (size_t)ntab * 3 * H264R_MAX_SLOTS)) ||
         (st = dev_resize(&c->d444_chroma, &c->c444_chroma, (size_t)P * 2 * 64 * nmb + H264R_PLANE_SLACK)))
         return st;
-    hipLaunchKernelGGL(k_derive444, dim3(1024), dim3(256), 0, s, b, 0, c->d444_mbs, c->d444_slices, c->d444_quant,
-                       c->d444_refs, ntab, c->d_err);
+    // a separate-colour-plane (JV) batch on a 4:4:4 context: monochrome records, colour plane
+    // jv - 1's lists, references and output plane (h264r_batch.colour_plane)
+    const int jv = b.colour_plane;
+    hipLaunchKernelGGL(k_derive444, dim3(1024), dim3(256), 0, s, b, 0, jv ? jv - 1 : 0, c->d444_mbs, c->d444_slices,
+                       c->d444_quant, c->d444_refs, ntab, c->d_err);
     HIP_OK(hipGetLastError());
     h264r_batch d = b;
+    d.colour_plane = 0;
+    if (jv) d.out_y = jv == 1 ? b.out_y : jv == 2 ? b.out_u : b.out_v;
     d.mbs = c->d444_mbs; d.slices = c->d444_slices; d.quant = c->d444_quant;
     d.ref_planes = c->d444_refs;
     d.ref_planes_stride = b.ref_planes_stride ? 3 * H264R_MAX_SLOTS : 0;
     d.out_u = c->d444_chroma;
     d.out_v = c->d444_chroma + (size_t)P * 64 * nmb;
     if ((st = launch_all(c, d, s, row0, row1, c->sc))) return st;
-    if (c->fmt == 0) return H264R_OK;                       // 4:0:0: no chroma
+    if (c->fmt == 0 || jv) return H264R_OK;                 // 4:0:0 / one JV plane: no chroma
     const int2 rows = make_int2(row0, row1);
     {
         Timed t(c, 0, s);
@@ -944,6 +949,11 @@ static int run_batch(h264r_ctx* c, const h264r_batch& b, hipStream_t s, int row0
     }
     c->last_stream = s;
     if (b.mbaff) return run_mbaff(c, b, s, row0, row1);
+    if (b.colour_plane) {                                   // JV: one colour plane on a 4:4:4 context
+        if (c->fmt != 3) return H264R_EUNSUPPORTED;
+        if (b.colour_plane < 0 || b.colour_plane > 3) return H264R_EINVAL;
+        return run_422(c, b, s, row0, row1);
+    }
     if (c->fmt == 3) return run_444(c, b, s, row0, row1);
     if (c->fmt == 2 || c->fmt == 0) return run_422(c, b, s, row0, row1);
     return launch_all(c, b, s, row0, row1, c->sc);

@@ -188,8 +188,10 @@ extern "C" __global__ __launch_bounds__(256) void k_untile(h264r_batch b, int2 r
 //   DPB tables: every plane entry of a slot -> the slot's plane pl (the luma MC reads it; the
 //            derived chroma reads stay inside it).
 // Field pictures and SP slices are not on the 4:4:4 / 4:2:2 / 4:0:0 paths: such a batch flags the
-// device error word.
-extern "C" __global__ __launch_bounds__(256) void k_derive444(h264r_batch b, int pl, h264r_mb* __restrict__ mbs,
+// device error word.  qpl: the plane whose lists and DPB planes the pass takes -- pl, except for a
+// separate-colour-plane (JV) batch: its monochrome records are taken as they are (pl 0) and its
+// lists and references are those of colour plane qpl (transform.cc:402, inter_prediction.cc:175-177).
+extern "C" __global__ __launch_bounds__(256) void k_derive444(h264r_batch b, int pl, int qpl, h264r_mb* __restrict__ mbs,
                                                               h264r_slice* __restrict__ slices, h264r_quant* __restrict__ quant,
                                                               const uint8_t** __restrict__ refs, int ntab, int* err)
 {
@@ -228,16 +230,16 @@ extern "C" __global__ __launch_bounds__(256) void k_derive444(h264r_batch b, int
         int from = k;
         if (k < 2 * S4) {
             const int half = k / S4, r = k % S4;
-            if (r < 6 * 16) from = half * S4 + pl * 6 * 16 + r;
+            if (r < 6 * 16) from = half * S4 + qpl * 6 * 16 + r;
         } else {
             const int k8 = k - 2 * S4, half = k8 / S8, r = k8 % S8;
-            if (r < 6 * 64) from = 2 * S4 + half * S8 + pl * 6 * 64 + r;
+            if (r < 6 * 64) from = 2 * S4 + half * S8 + qpl * 6 * 64 + r;
         }
         reinterpret_cast<int16_t*>(quant + q)[k] = src[from];
     }
     for (int64_t i = t0; i < (int64_t)ntab * 3 * H264R_MAX_SLOTS; i += nt) {
         const int64_t tab = i / (3 * H264R_MAX_SLOTS), e = i % (3 * H264R_MAX_SLOTS), slot = e / 3;
-        refs[i] = b.ref_planes[tab * b.ref_planes_stride + 3 * slot + pl];
+        refs[i] = b.ref_planes[tab * b.ref_planes_stride + 3 * slot + qpl];
     }
     for (int64_t i = t0; i < P; i += nt)
         if (b.pics[i].structure != H264R_FRAME) atomicOr(err, 1);

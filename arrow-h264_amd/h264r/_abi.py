@@ -107,7 +107,7 @@ class Batch(C.Structure):
         ("mv", C.c_void_p), ("ref_idx", C.c_void_p), ("slices", C.c_void_p),
         ("pics", C.c_void_p), ("quant", C.c_void_p), ("ref_planes", C.c_void_p),
         ("out_y", C.c_void_p), ("out_u", C.c_void_p), ("out_v", C.c_void_p),
-        ("ref_planes_stride", C.c_int64), ("mbaff", C.c_int32), ("reserved", C.c_int32),
+        ("ref_planes_stride", C.c_int64), ("mbaff", C.c_int32), ("colour_plane", C.c_int32),
     ]
 
 

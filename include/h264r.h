@@ -272,7 +272,17 @@ typedef struct h264r_batch {
     int64_t             ref_planes_stride;   /* pointers; 0 = one table for the batch (above) */
     int32_t             mbaff;       /* ABI 4: nonzero = every picture is an H264R_MBAFF_FRAME (its own
                                         launch sequence, whole pictures only); 0 = frames / fields */
-    int32_t             reserved;
+    int32_t             colour_plane;/* ABI 4, separate_colour_plane_flag (JV) on a 4:4:4 context: 0 = off;
+                                        k + 1 = every picture is colour plane k (colour_plane_id) of its
+                                        frame: 4:0:0 records and levels (a PCM MB's block followed by 128
+                                        readable bytes), reconstructed and deblocked as luma with plane k's
+                                        scaling lists (transform.cc:402) from plane k of the DPB slots
+                                        (inter_prediction.cc:175-177) into out_y / out_u / out_v for
+                                        k = 0 / 1 / 2 (make_frame_picture_JV deblock.cc:555-579); the other
+                                        two output planes are not written.  The reference scales an
+                                        Intra_16x16 DC of plane k by the Y intra list (transform.cc:831-
+                                        836); the library by plane k's -- the same unless the first
+                                        entries of the two intra 4x4 lists differ */
 } h264r_batch;
 
 typedef struct h264r_ctx h264r_ctx;

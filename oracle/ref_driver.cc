@@ -100,9 +100,17 @@ int main(int argc, char** argv)
     if (argc > k + 2) cfg.sp_slices = atoi(argv[k + 2]);
     if (argc > k + 3) cfg.structure = atoi(argv[k + 3]);
     if (argc > k + 4) cfg.chroma_format = atoi(argv[k + 4]);
+    /* argument 27: 1 + colour_plane_id of a separate-colour-plane (JV) frame: the synthetic picture is
+       monochrome (4:0:0 records) and is decoded as that colour plane of a 4:4:4 frame
+       (separate_colour_plane_flag, slice colour_plane_id); the other two planes are blank
+       pictures whose filter changes nothing, and the output is the decoded plane after the
+       reference's Deblock::deblock / make_frame_picture_JV (deblock.cc:555-579, 641-655) */
+    const int jv = argc > k + 5 ? atoi(argv[k + 5]) : 0;
     const bool f444 = cfg.chroma_format == 3, f422 = cfg.chroma_format == 2, f400 = cfg.chroma_format == H264R_SYNTH_CHROMA_400;
     const int CW = f400 ? 0 : f444 ? 16 : 8, CH = f400 ? 0 : f444 || f422 ? 16 : 8;   /* chroma samples per MB */
     const bool fld = cfg.structure == H264R_TOP_FIELD || cfg.structure == H264R_BOTTOM_FIELD;
+    if (jv && (!f400 || cfg.structure != H264R_FRAME || jv > 3)) { fprintf(stderr, "JV: 4:0:0 records of a frame\n"); return 2; }
+    const int RW = jv ? 16 : CW, RH = jv ? 16 : CH;     /* the planes' chroma samples per MB (JV: 4:4:4) */
     /* MBAFF frame (argument 25 = 3): mb_data by MB address (pairs), mb.mb the storage position,
        field MBs predicting from the fields of the list's frames (get_ref_pic dpb.cc:1046-1055) */
     const bool mbaff = cfg.structure == H264R_MBAFF_FRAME;
@@ -128,6 +136,9 @@ int main(int argc, char** argv)
     pps_t* pps = new pps_t();
     sps->profile_idc = f444 ? 244 : f422 ? 122 : 100; sps->level_idc = 51;
     sps->chroma_format_idc = f444 ? 3 : f422 ? 2 : f400 ? 0 : 1; sps->ChromaArrayType = sps->chroma_format_idc;
+    if (jv) {                          /* interpret_rbsp.cc:100,123-127 */
+        sps->profile_idc = 244; sps->chroma_format_idc = 3; sps->separate_colour_plane_flag = 1; sps->ChromaArrayType = 0;
+    }
     sps->SubWidthC = f444 ? 1 : 2; sps->SubHeightC = CH == 8 ? 2 : 1; sps->MbWidthC = CW; sps->MbHeightC = CH;
     sps->BitDepthY = 8; sps->BitDepthC = 8;
     sps->frame_mbs_only_flag = !fld; sps->direct_8x8_inference_flag = 1;
@@ -164,22 +175,22 @@ int main(int argc, char** argv)
        references are the fields of the DPB frames, refs[2 s + bottom] */
     const int nfr = h264r_synth_ref_frames(&cfg);
     std::vector<storable_picture*> refs(fld ? 2 * nfr : nfr);
-    std::vector<uint8_t> ty(W * 16 * FH * 16), tu(W * CW * FH * CH + 1), tv(W * CW * FH * CH + 1);
+    std::vector<uint8_t> ty(W * 16 * FH * 16), tu(W * RW * FH * RH + 1), tv(W * RW * FH * RH + 1);
     for (int s = 0; s < nfr; ++s) {
-        h264r_synth_refpic_fmt(cfg.seed, s, W, FH, cfg.chroma_format, ty.data(), tu.data(), tv.data());
+        h264r_synth_refpic_fmt(cfg.seed, s, W, FH, jv ? 3 : cfg.chroma_format, ty.data(), tu.data(), tv.data());
         for (int f = 0; f < (fld ? 2 : 1); ++f) {
             storable_picture* r = new storable_picture(vid, fld ? (f ? BOTTOM_FIELD : TOP_FIELD) : FRAME,
-                                                       W * 16, FH * 16, W * CW, FH * CH, 1);
+                                                       W * 16, FH * 16, W * RW, FH * RH, 1);
             const int step = fld ? 2 : 1;                /* dpb_split_field: every second row */
             for (int y = 0; y < H * 16; ++y) for (int x = 0; x < W * 16; ++x) r->imgY[y][x] = ty[(y * step + f) * W * 16 + x];
-            for (int y = 0; y < H * CH; ++y) for (int x = 0; x < W * CW; ++x) {
-                r->imgUV[0][y][x] = tu[(y * step + f) * W * CW + x];
-                r->imgUV[1][y][x] = tv[(y * step + f) * W * CW + x];
+            for (int y = 0; y < H * RH; ++y) for (int x = 0; x < W * RW; ++x) {
+                r->imgUV[0][y][x] = tu[(y * step + f) * W * RW + x];
+                r->imgUV[1][y][x] = tv[(y * step + f) * W * RW + x];
             }
             pad_buf(*r->imgY, W * 16, H * 16, r->iLumaStride, MCBUF_LUMA_PAD_X, MCBUF_LUMA_PAD_Y);
-            if (!f400) {
-                pad_buf(*r->imgUV[0], W * CW, H * CH, r->iChromaStride, r->iChromaPadX, r->iChromaPadY);
-                pad_buf(*r->imgUV[1], W * CW, H * CH, r->iChromaStride, r->iChromaPadX, r->iChromaPadY);
+            if (!f400 || jv) {
+                pad_buf(*r->imgUV[0], W * RW, H * RH, r->iChromaStride, r->iChromaPadX, r->iChromaPadY);
+                pad_buf(*r->imgUV[1], W * RW, H * RH, r->iChromaStride, r->iChromaPadX, r->iChromaPadY);
             }
             r->poc = r->frame_poc = r->top_poc = r->bottom_poc = h264r_synth_slot_poc(s) + f;
             r->is_long_term = 0; r->used_for_reference = 1;
@@ -207,7 +218,7 @@ int main(int argc, char** argv)
     /* RefPicList entry -> storable_picture (include/h264r.h: slot | H264R_REF_BOTTOM for fields) */
     auto ref_of = [&](int v) { return fld ? refs[2 * (v & 31) + ((v & H264R_REF_BOTTOM) ? 1 : 0)] : refs[v]; };
 
-    storable_picture* dec = new storable_picture(vid, pstruct, W * 16, FH * 16, W * CW, FH * CH, 1);
+    storable_picture* dec = new storable_picture(vid, pstruct, W * 16, FH * 16, W * RW, FH * RH, 1);
     dec->sps = sps; dec->pps = pps;
     dec->used_for_reference = 1;
     dec->poc = dec->frame_poc = pic.poc;
@@ -225,6 +236,7 @@ int main(int argc, char** argv)
         shr_t& h = x->header;
         h.slice_type = c.slice_type;
         h.structure = pstruct; h.MbaffFrameFlag = mbaff; h.field_pic_flag = fld;
+        h.colour_plane_id = (uint8_t)(jv ? jv - 1 : 0);
         h.bottom_field_flag = pstruct == BOTTOM_FIELD;
         h.PicHeightInMbs = H; h.PicHeightInSamplesL = H * 16; h.PicHeightInSamplesC = H * CH;
         h.PicSizeInMbs = W * H;
@@ -492,11 +504,53 @@ int main(int argc, char** argv)
             for (int y = 0; y < 16; ++y) { for (int x = 0; x < 16; ++x) fprintf(stderr, "%4d", s.mb_pred[0][y][x]); fprintf(stderr, "\n"); }
         }
     }
+    if (jv) {
+        /* the frame's other two colour planes: blank pictures with the decoded plane's slice headers
+           (Deblock::deblock gates every plane on plane 0's slices, :632-640) and intra MBs of QP 0,
+           whose edges the filter leaves alone (alpha 0) */
+        for (int k = 0; k < 3; ++k) {
+            if (k == jv - 1) { vid->dec_picture_JV[k] = dec; vid->mb_data_JV[k] = mb_data; continue; }
+            storable_picture* dp = new storable_picture(vid, FRAME, W * 16, H * 16, W * 16, H * 16, 1);
+            dp->sps = sps; dp->pps = pps; dp->used_for_reference = 1;
+            mb_t* md = new mb_t[NMB];
+            memset((void*)md, 0, sizeof(mb_t) * NMB);
+            for (slice_t* x0 : sl) {
+                slice_t* x = new slice_t();
+                x->p_Vid = vid; x->active_sps = sps; x->active_pps = pps;
+                x->header = x0->header;
+                x->header.colour_plane_id = (uint8_t)k;
+                x->dec_picture = dp;
+                x->neighbour.mb_data = md;
+                dp->slice_headers.push_back(x);
+            }
+            for (int a = 0; a < NMB; ++a) {
+                md[a].p_Slice = dp->slice_headers[mbs[a].slice]; md[a].mbAddrX = a; md[a].mb.x = a % W; md[a].mb.y = a / W;
+                md[a].slice_nr = (short)mbs[a].slice; md[a].is_intra_block = 1; md[a].mb_type = H264R_I_16x16;
+            }
+            vid->dec_picture_JV[k] = dp; vid->mb_data_JV[k] = md;
+        }
+        vid->dec_picture = vid->dec_picture_JV[0];
+    }
     /* MBAFF: the loop filter's MbAffPostProc (deblock.cc:596-629) interleaves the field MBs; the
        reconstruction alone is that with every slice's filter off (:631-640) */
-    if (recon_only && mbaff)
-        for (slice_t* x : sl) x->header.disable_deblocking_filter_idc = 1;
-    if (!recon_only || mbaff) sl[0]->decoder.deblock_filter(*sl[0]);
+    if (recon_only && (mbaff || jv))
+        for (int k = 0; k < (jv ? 3 : 1); ++k)
+            for (slice_t* x : (jv ? vid->dec_picture_JV[k]->slice_headers : dec->slice_headers)) x->header.disable_deblocking_filter_idc = 1;
+    /* JV: make_frame_picture_JV (:555-579) moves planes 1 and 2 into the frame's imgUV */
+    storable_picture* jv_frame = jv ? vid->dec_picture_JV[0] : nullptr;
+    if (!recon_only || mbaff || jv) sl[0]->decoder.deblock_filter(*sl[0]);
+    if (jv) {
+        px_t** plane = jv == 1 ? jv_frame->imgY : jv_frame->imgUV[jv - 2];
+        FILE* f = fopen(out_path, "wb");
+        if (!f) return 5;
+        std::vector<uint8_t> row(W * 16);
+        for (int y = 0; y < H * 16; ++y) {
+            for (int x = 0; x < W * 16; ++x) row[x] = (uint8_t)plane[y][x];
+            fwrite(row.data(), 1, W * 16, f);
+        }
+        fclose(f);
+        return 0;
+    }
     sec += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     }
     if (reps_env) {

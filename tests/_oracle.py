@@ -134,11 +134,29 @@ def decode(p: synth.Picture, refs=None, stage: str = "full", quant=None):
     return out
 
 
-def run_reference(cfg: A.SynthCfg, index: int, recon_only: bool = False, time_reps: int = 0, qm=None):
+def decode_jv_plane(p: synth.Picture, k: int, qm=None):
+    """Colour plane k of a separate-colour-plane (JV) frame by the restatement: the monochrome
+    picture decoded as 4:0:0 with plane k's scaling lists in the Y slots and plane k of the 4:4:4
+    references (transform.cc:402, inter_prediction.cc:175-177); pinned by golden.json's
+    jv_fixtures (ref_driver's JV mode: the reference's own separate-plane decode and filter)."""
+    L = lib()
+    cfg = p.cfg
+    r444 = synth.refpics(L, synth.default_cfg(L, 3, cfg.width_mbs, cfg.height_mbs, chroma_format=3,
+                                              num_refs=cfg.num_refs, seed=cfg.seed))
+    q = quant_lists(*qm) if qm is not None else quant_flat()
+    q2 = q.copy()
+    for t in ("scale4x4", "scale8x8"):
+        q2[t][:, :, 0] = q[t][:, :, k]
+    return decode(p, [(r[k], r[k], r[k]) for r in r444], quant=q2)[0]
+
+
+def run_reference(cfg: A.SynthCfg, index: int, recon_only: bool = False, time_reps: int = 0, qm=None,
+                  jv_plane: int | None = None):
     """Planes produced by the compiled reference decoder (this container only).  With
     time_reps > 0 the driver reconstructs the picture that many times on one thread and
     (planes, macroblocks, seconds) is returned (ref_driver.cc timing mode).  qm = (m4, m8):
-    explicit SPS scaling lists (all present)."""
+    explicit SPS scaling lists (all present).  jv_plane = k: the (4:0:0) picture decoded as colour plane
+    k of a separate-colour-plane frame; the single decoded plane is returned."""
     drv = build_ref()
     W, H = cfg.width_mbs, cfg.height_mbs
     with tempfile.TemporaryDirectory() as td:
@@ -148,6 +166,8 @@ def run_reference(cfg: A.SynthCfg, index: int, recon_only: bool = False, time_re
                 cfg.num_refs, cfg.qp_min, cfg.qp_max, cfg.pcm_permille, cfg.intra_permille,
                 cfg.mv_range_x, cfg.mv_range_y, hex(cfg.seed), index, out, int(recon_only),
                 cfg.lossless_permille, cfg.sp_slices, cfg.structure, cfg.chroma_format]
+        if jv_plane is not None:
+            args.append(jv_plane + 1)
         env = dict(os.environ)
         if time_reps:
             env["H264R_TIME_REPS"] = str(time_reps)
@@ -160,6 +180,8 @@ def run_reference(cfg: A.SynthCfg, index: int, recon_only: bool = False, time_re
         if r.returncode != 0:
             raise RuntimeError(f"ref_driver failed ({r.returncode}): {r.stderr[-2000:]}")
         raw = np.fromfile(out, np.uint8)
+    if jv_plane is not None:
+        return raw.reshape(16 * H, 16 * W)
     cw, ch = A.chroma_mb(A.idc_of(cfg.chroma_format))
     ny, nc = 256 * W * H, cw * ch * W * H
     planes = (raw[:ny].reshape(16 * H, 16 * W), raw[ny:ny + nc].reshape(ch * H, cw * W),

@@ -156,6 +156,29 @@ CASES = [
 ]
 
 
+# separate colour planes (JV, separate_colour_plane_flag, High 4:4:4): each colour plane of the frame is
+# a monochrome picture with its own MBs, decoded with that plane's scaling lists and from that plane of
+# the 4:4:4 references; ref_driver drives the unmodified reference's JV decode + deblock +
+# make_frame_picture_JV (deblock.cc:555-579, 641-655).  Scaling lists: the first entries of the three
+# intra 4x4 lists agree (the reference scales an Intra_16x16 DC of every plane by the Y list,
+# transform.cc:831-836)
+JV_CASES = [
+    ("jv_i_qcif_pcm", 2, 11, 9, dict(pcm_permille=20), [0, 1, 2]),
+    ("jv_p_cif_2slices_idc2", 3, 22, 9, dict(num_refs=2, num_slices=2, deblock_idc=2), [0, 1, 2]),
+    ("jv_p_qcif_wp_cip", 3, 11, 9, dict(wp_mode=1, num_refs=3, constrained_intra=1, intra_permille=300), [0, 1, 2]),
+    ("jv_b_qcif_explicit_t8", 4, 11, 9, dict(wp_mode=1, num_refs=2), [0, 1, 2]),
+    ("jv_b_qcif_scaling", 4, 11, 9, dict(num_refs=3, qm=22), [0, 1, 2]),
+]
+
+
+def jv_quant(qseed):
+    """qmatrix(qseed) with the Cb / Cr intra 4x4 lists' first entry equal to the Y list's"""
+    m4, m8 = O.qmatrix(qseed)
+    m4 = np.array(m4).copy()
+    m4[1][0] = m4[2][0] = m4[0][0]
+    return m4, np.array(m8)
+
+
 def md5(a: np.ndarray) -> str:
     return hashlib.md5(np.ascontiguousarray(a).tobytes()).hexdigest()
 
@@ -191,11 +214,31 @@ def main() -> int:
                 entry[f"{stage}_md5"] = {pl: md5(ref[k]) for k, pl in enumerate("YUV")}
             fixtures.append(entry)
             print(f"{name}[{idx}] {W}x{H} ok ({time.time() - t0:.2f}s)")
+    jv = []
+    for name, cidx, W, H, over, planes in JV_CASES:
+        over = dict(over)
+        qseed = over.pop("qm", None)
+        qm = jv_quant(qseed) if qseed is not None else None
+        cfg = synth.default_cfg(L, cidx, W, H, chroma_format=4, seed=0x5E9C + cidx, **over)
+        for k in planes:
+            p = synth.picture(L, cfg, k)               # plane k: its own MBs (picture index k)
+            ref = O.run_reference(cfg, k, qm=qm, jv_plane=k)
+            ora = O.decode_jv_plane(p, k, qm)
+            if not np.array_equal(ref, ora):
+                bad = np.argwhere(ref != ora)
+                print(f"MISMATCH {name} plane {k}: {len(bad)} samples, first at {tuple(bad[0])}", file=sys.stderr)
+                return 1
+            entry = {"name": name, "config": cidx, "cfg": cfg.as_dict(), "index": k, "colour_plane": k,
+                     "input_md5": synth.input_digest(p), "out_md5": md5(ref)}
+            if qm is not None:
+                entry["qmatrix"] = {"m4": qm[0].tolist(), "m8": qm[1].tolist()}
+            jv.append(entry)
+            print(f"{name} plane {k} {W}x{H} ok")
     with open(os.path.join(HERE, "golden.json"), "w") as f:
         json.dump({"generator": "tests/golden/make_golden.py",
                    "reference": "luuvish/arrow-h264 decoder/*.cc compiled by oracle/Makefile",
-                   "fixtures": fixtures}, f, indent=1)
-    print(f"wrote {len(fixtures)} fixtures")
+                   "fixtures": fixtures, "jv_fixtures": jv}, f, indent=1)
+    print(f"wrote {len(fixtures)} fixtures, {len(jv)} JV plane fixtures")
     return 0
 
 
