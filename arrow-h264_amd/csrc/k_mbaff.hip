@@ -16,7 +16,8 @@
 //                    grid: a pair's intra neighbours lie in the pairs left, above-left, above and
 //                    above-right, all on earlier diagonals.  The pair and its border (34 x 25 luma,
 //                    2 x 18 x 9 chroma samples) are staged in LDS; the top MB, then the bottom MB,
-//                    each 4x4 / 8x8 block in turn (intra_prediction.cc:137-894).
+//                    each 4x4 / 8x8 block in turn (intra_prediction.cc:137-894), from a table of
+//                    the MB's outside neighbours looked up once per MB (nb_table).
 //   k_mbaff_deblock  one wave per MB pair, per anti-diagonal: Deblock::strength for the pair's two
 //                    MBs, then filter_vertical / filter_horizontal of the top MB and of the bottom
 //                    MB (deblock.cc:78-535) on an LDS tile of the pair and the samples its edges
@@ -345,10 +346,19 @@ DEV bool intra_ok(const MPic& P, int n) { return n >= 0 && (!P.cip || (P.mbs[n].
 
 // luma tile: rows -2 .. 31, columns -1 .. 23 of the pair; chroma: rows -2 .. 15, columns -1 .. 7
 constexpr int TYW = 25, TYH = 34, TCW = 9, TCH = 18;
+// The neighbours of the MB being predicted, looked up once per MB (one lane each) instead of per
+// block: tile index and availability (bit 0 get_neighbour found it in the slice, bit 1 also usable
+// under constrained_intra_pred) of the left column, the top row, the top-right and top-left samples
+// (luma), and of the chroma left column, top row and top-left sample.
+struct NbTab {
+    int16_t lpos[16], tpos, trpos, tlpos, clpos[8], ctpos, ctlpos;
+    uint8_t lav[16], tav, trav, tlav, clav[8], ctav, ctlav;
+};
 struct IntraLds {
     uint8_t ty[TYH * TYW];
     uint8_t tc[2][TCH * TCW];
     ResLds R;
+    NbTab nb;
 };
 DEV uint8_t& TY(IntraLds& L, int x, int y) { return L.ty[(y + 2) * TYW + x + 1]; }
 DEV uint8_t& TC(IntraLds& L, int pl, int x, int y) { return L.tc[pl][(y + 2) * TCW + x + 1]; }
@@ -356,33 +366,6 @@ DEV uint8_t& TC(IntraLds& L, int pl, int x, int y) { return L.tc[pl][(y + 2) * T
 // p(x, y) of an N x N block (N 4 or 8; x in -1 .. 2N - 1, y in -1 .. N - 1), p(-1, -1) at [0]
 struct Nbr { int s[26]; int av[4]; };
 #define PX(n, x, y) ((y) < 0 ? (n).s[1 + (x)] : (n).s[17 + (y)])
-
-// Intra4x4 / Intra8x8 ctors (intra_prediction.cc:137-187, 359-411) for the block at (xO, yO)
-DEV void gather_nxn(const MPic& P, IntraLds& L, int r, int N, int xO, int yO, int px, int py, Nbr& n)
-{
-    int tx, ty, nA0 = -1;
-    bool allA = true;
-    int ax[8], ay[8];
-    for (int i = 0; i < N; ++i) {
-        const int a = nbr(P, r, 16, 16, xO - 1, yO + i, px, py, ax[i], ay[i]);
-        if (i == 0) nA0 = a;
-        allA = allA && intra_ok(P, a);
-    }
-    int bx, by, cx, cy, dx, dy;
-    const int nB = nbr(P, r, 16, 16, xO, yO - 1, px, py, bx, by);
-    int nC = nbr(P, r, 16, 16, xO + N, yO - 1, px, py, cx, cy);
-    const int nD = nbr(P, r, 16, 16, xO - 1, yO - 1, px, py, dx, dy);
-    if (N == 4 && xO == 4 && (yO == 4 || yO == 12)) nC = -1;           // :154
-    if (N == 8 && xO == 8 && yO == 8) nC = -1;                         // :376
-    (void)tx; (void)ty;
-    if (P.cip) { n.av[0] = allA; n.av[1] = intra_ok(P, nB); n.av[2] = intra_ok(P, nC); n.av[3] = intra_ok(P, nD); }
-    else { n.av[0] = nA0 >= 0; n.av[1] = nB >= 0; n.av[2] = nC >= 0; n.av[3] = nD >= 0; }
-    n.s[0] = n.av[3] ? TY(L, dx, dy) : 0;
-    for (int y = 0; y < N; ++y) n.s[17 + y] = n.av[0] ? TY(L, ax[y], ay[y]) : 0;
-    for (int x = 0; x < N; ++x) n.s[1 + x] = n.av[1] ? TY(L, bx + x, by) : 0;
-    for (int x = N; x < 2 * N; ++x) n.s[1 + x] = n.av[1] ? (n.av[2] ? TY(L, cx + x - N, cy) : n.s[N]) : 0;
-    n.av[2] = n.av[1];
-}
 
 // Intra8x8::filtering (intra_prediction.cc:413-447)
 DEV void filter_8x8(const Nbr& n, Nbr& f)
@@ -455,66 +438,117 @@ DEV int pred_nxn(const Nbr& n, int N, int mode, int x, int y)
     }
 }
 
-// Intra16x16 (intra_prediction.cc:624-735) at (x, y)
-DEV int pred_16x16(const MPic& P, IntraLds& L, int r, int mode, int px, int py, int x, int y)
+// fill L.nb for MB r of pair (px, py) (lanes 0..28; the caller synchronises)
+DEV void nb_table(const MPic& P, IntraLds& L, int r, int px, int py, int t)
 {
-    int tx, ty, lx[16], ly[16], nA0 = -1;
-    bool allA = true;
-    for (int i = 0; i < 16; ++i) {
-        const int a = nbr(P, r, 16, 16, -1, i, px, py, lx[i], ly[i]);
-        if (i == 0) nA0 = a;
-        allA = allA && intra_ok(P, a);
-    }
-    int bx, by, dx, dy;
-    const int nB = nbr(P, r, 16, 16, 0, -1, px, py, bx, by);
-    (void)nbr(P, r, 16, 16, -1, -1, px, py, dx, dy);
-    (void)tx; (void)ty;
-    const int a0 = P.cip ? allA : nA0 >= 0, a1 = P.cip ? intra_ok(P, nB) : nB >= 0;
+    int tx = 0, ty = 0, n = -1;
+    const bool chroma = t >= 19;
+    if (t < 16) n = nbr(P, r, 16, 16, -1, t, px, py, tx, ty);
+    else if (t == 16) n = nbr(P, r, 16, 16, 0, -1, px, py, tx, ty);
+    else if (t == 17) n = nbr(P, r, 16, 16, 16, -1, px, py, tx, ty);
+    else if (t == 18) n = nbr(P, r, 16, 16, -1, -1, px, py, tx, ty);
+    else if (t < 27) n = nbr(P, r, 8, 8, -1, t - 19, px, py, tx, ty);
+    else if (t == 27) n = nbr(P, r, 8, 8, 0, -1, px, py, tx, ty);
+    else if (t == 28) n = nbr(P, r, 8, 8, -1, -1, px, py, tx, ty);
+    else return;
+    const uint8_t av = (uint8_t)((n >= 0 ? 1 : 0) | (intra_ok(P, n) ? 2 : 0));
+    const int16_t pos = (int16_t)(chroma ? (ty + 2) * TCW + tx + 1 : (ty + 2) * TYW + tx + 1);
+    NbTab& T = L.nb;
+    if (t < 16) { T.lpos[t] = pos; T.lav[t] = av; }
+    else if (t == 16) { T.tpos = pos; T.tav = av; }
+    else if (t == 17) { T.trpos = pos; T.trav = av; }
+    else if (t == 18) { T.tlpos = pos; T.tlav = av; }
+    else if (t < 27) { T.clpos[t - 19] = pos; T.clav[t - 19] = av; }
+    else if (t == 27) { T.ctpos = pos; T.ctav = av; }
+    else { T.ctlpos = pos; T.ctlav = av; }
+}
+
+// gather_nxn from the table: the block's samples inside the MB are the MB's own (always
+// available, get_neighbour returns the MB itself), outside it the table's
+DEV void gather_tab(IntraLds& L, bool fq, int bb, int N, int xO, int yO, int px, int py, bool cip, Nbr& n)
+{
+    const NbTab& T = L.nb;
+    const int sh = cip ? 2 : 1;                                   // the availability bit to test
+    auto own = [&](int x, int y) -> int {                         // tile index of own sample (x, y)
+        return ((fq ? bb + 2 * y : bb * 16 + y) + 2) * TYW + x + 1;
+    };
+    // A: rows yO .. yO + N - 1 at column xO - 1 (CIP: every row's MB; else the first row's)
+    int av0;
+    if (xO > 0) av0 = 1;
+    else if (cip) { av0 = 1; for (int i = 0; i < N; ++i) av0 &= (T.lav[yO + i] >> 1) & 1; }
+    else av0 = T.lav[yO] & 1;
+    // B, C, D
+    int av1, av2, av3, bpos, cpos = 0, dpos;
+    if (yO > 0) { av1 = 1; bpos = own(xO, yO - 1); }
+    else { av1 = (T.tav & sh) != 0; bpos = T.tpos + xO; }
+    if (xO + N < 16) {
+        av2 = yO > 0 ? 1 : (T.tav & sh) != 0;
+        cpos = yO > 0 ? own(xO + N, yO - 1) : T.tpos + xO + N;
+    } else if (yO == 0) { av2 = (T.trav & sh) != 0; cpos = T.trpos + (xO + N - 16); }
+    else av2 = 0;                                                // the MB to the right: later
+    if (N == 4 && xO == 4 && (yO == 4 || yO == 12)) av2 = 0;     // :154
+    if (N == 8 && xO == 8 && yO == 8) av2 = 0;                   // :376
+    if (xO > 0 && yO > 0) { av3 = 1; dpos = own(xO - 1, yO - 1); }
+    else if (xO > 0) { av3 = (T.tav & sh) != 0; dpos = T.tpos + xO - 1; }
+    else if (yO > 0) { av3 = (T.lav[yO - 1] & sh) != 0; dpos = T.lpos[yO - 1]; }
+    else { av3 = (T.tlav & sh) != 0; dpos = T.tlpos; }
+    n.av[0] = av0; n.av[1] = av1; n.av[2] = av2; n.av[3] = av3;
+    n.s[0] = av3 ? L.ty[dpos] : 0;
+    for (int y = 0; y < N; ++y) n.s[17 + y] = av0 ? L.ty[xO > 0 ? own(xO - 1, yO + y) : T.lpos[yO + y]] : 0;
+    for (int x = 0; x < N; ++x) n.s[1 + x] = av1 ? L.ty[bpos + x] : 0;
+    for (int x = N; x < 2 * N; ++x) n.s[1 + x] = av1 ? (av2 ? L.ty[cpos + x - N] : n.s[N]) : 0;
+    n.av[2] = av1;
+}
+
+// Intra16x16 from the table (intra_prediction.cc:624-735)
+DEV int pred_16x16_tab(IntraLds& L, bool cip, int mode, int x, int y)
+{
+    const NbTab& T = L.nb;
+    int a0 = T.lav[0] & 1, a1 = (T.tav >> (cip ? 1 : 0)) & 1;
+    if (cip) { a0 = 1; for (int i = 0; i < 16; ++i) a0 &= (T.lav[i] >> 1) & 1; }
+#define LT(k) L.ty[T.lpos[k]]
+#define TP(k) L.ty[T.tpos + (k)]
     switch (mode) {
-    case 0: return TY(L, bx + x, by);
-    case 1: return TY(L, lx[y], ly[y]);
+    case 0: return TP(x);
+    case 1: return LT(y);
     case 2: {
         if (!a0 && !a1) return 128;
         int sum = 0;
-        if (a0) for (int k = 0; k < 16; ++k) sum += TY(L, lx[k], ly[k]);
-        if (a1) for (int k = 0; k < 16; ++k) sum += TY(L, bx + k, by);
+        if (a0) for (int k = 0; k < 16; ++k) sum += LT(k);
+        if (a1) for (int k = 0; k < 16; ++k) sum += TP(k);
         return (sum + (a0 ? 8 : 0) + (a1 ? 8 : 0)) >> (3 + a0 + a1);
     }
     default: {
-        const int pd = TY(L, dx, dy);
+        const int pd = L.ty[T.tlpos];
         int H = 0, V = 0;
         for (int k = 0; k < 8; ++k) {
-            H += (k + 1) * (TY(L, bx + 8 + k, by) - (6 - k >= 0 ? TY(L, bx + 6 - k, by) : pd));
-            V += (k + 1) * (TY(L, lx[8 + k], ly[8 + k]) - (6 - k >= 0 ? TY(L, lx[6 - k], ly[6 - k]) : pd));
+            H += (k + 1) * (TP(8 + k) - (6 - k >= 0 ? TP(6 - k) : pd));
+            V += (k + 1) * (LT(8 + k) - (6 - k >= 0 ? LT(6 - k) : pd));
         }
-        const int a = 16 * (TY(L, lx[15], ly[15]) + TY(L, bx + 15, by));
+        const int a = 16 * (LT(15) + TP(15));
         const int b = (5 * H + 32) >> 6, c = (5 * V + 32) >> 6;
         return clip255((a + b * (x - 7) + c * (y - 7) + 16) >> 5);
     }
     }
+#undef LT
+#undef TP
 }
 
-// Chroma (intra_prediction.cc:745-894), 4:2:0, at (x, y) of plane pl (0 Cb, 1 Cr)
-DEV int pred_chroma(const MPic& P, IntraLds& L, int r, int mode, int pl, int px, int py, int x, int y)
+// Chroma from the table (intra_prediction.cc:745-894), 4:2:0
+DEV int pred_chroma_tab(IntraLds& L, bool cip, int mode, int pl, int x, int y)
 {
-    int lx[8], ly[8], nA0 = -1;
-    bool all0 = true, all2 = true;
-    for (int i = 0; i < 8; ++i) {
-        const int a = nbr(P, r, 8, 8, -1, i, px, py, lx[i], ly[i]);
-        if (i == 0) nA0 = a;
-        if (i < 4) all0 = all0 && intra_ok(P, a); else all2 = all2 && intra_ok(P, a);
-    }
-    int bx, by, dx, dy;
-    const int nB = nbr(P, r, 8, 8, 0, -1, px, py, bx, by);
-    (void)nbr(P, r, 8, 8, -1, -1, px, py, dx, dy);
+    const NbTab& T = L.nb;
     int av0, av1, av2;
-    if (P.cip) { av0 = all0; av2 = all2; av1 = intra_ok(P, nB); }
-    else { av0 = nA0 >= 0; av2 = av0; av1 = nB >= 0; }
-    (void)dx; (void)dy;
-#define CL(k) TC(L, pl, lx[k], ly[k])
-#define CT(k) TC(L, pl, bx + (k), by)
+    if (cip) {
+        av0 = 1; av2 = 1;
+        for (int i = 0; i < 4; ++i) { av0 &= (T.clav[i] >> 1) & 1; av2 &= (T.clav[4 + i] >> 1) & 1; }
+        av1 = (T.ctav >> 1) & 1;
+    } else { av0 = T.clav[0] & 1; av2 = av0; av1 = T.ctav & 1; }
+    const uint8_t* tc = L.tc[pl];
+#define CL(k) tc[T.clpos[k]]
+#define CT(k) tc[T.ctpos + (k)]
     switch (mode) {
-    case 0: {                                                           // DC per 4x4 (:825-849)
+    case 0: {
         const int xO = x & 4, yO = y & 4;
         int aA, aB;
         if ((xO == 0 && yO == 0) || (xO > 0 && yO > 0)) { aA = yO > 0 ? av2 : av0; aB = av1; }
@@ -528,8 +562,8 @@ DEV int pred_chroma(const MPic& P, IntraLds& L, int r, int mode, int pl, int px,
     }
     case 1: return CL(y);
     case 2: return CT(x);
-    default: {                                                          // plane (:871-894), xCF = yCF = 0
-        const int pd = TC(L, pl, dx, dy);
+    default: {
+        const int pd = tc[T.ctlpos];
         int H = 0, V = 0;
         for (int k = 0; k < 4; ++k) {
             H += (k + 1) * (CT(4 + k) - (2 - k >= 0 ? CT(2 - k) : pd));
@@ -834,11 +868,13 @@ extern "C" __global__ __launch_bounds__(256) void k_mbaff_intra(h264r_batch b, i
         const int r = half ? rb : rt;
         if (!(half ? ib : it)) continue;
         const h264r_mb m = P.mbs[r];
+        nb_table(P, L, r, px, py, t);                                  // ordered by mb_residual's barriers
         mb_residual(m, b.levels + m.coef_off, *P.q, L.R, t);
+        const bool fq = (m.flags & H264R_MBF_FIELD) != 0, cip = P.cip != 0;
         int gx, gy;
         if (m.mb_type == H264R_I_16x16) {
             const int x = t & 15, y = t >> 4;
-            const int v = clip255(L.R.cof[0][t] + pred_16x16(P, L, r, m.i16_mode, px, py, x, y));
+            const int v = clip255(L.R.cof[0][t] + pred_16x16_tab(L, cip, m.i16_mode, x, y));
             __syncthreads();                                           // every prediction reads the old tile
             mloc(P, r, 16, 16, x, y, gx, gy);
             TY(L, gx - px * 16, gy - py * 32) = (uint8_t)v;
@@ -849,7 +885,7 @@ extern "C" __global__ __launch_bounds__(256) void k_mbaff_intra(h264r_batch b, i
                 const int yO = N == 4 ? (bk >> 3) * 8 + ((bk >> 1) & 1) * 4 : (bk >> 1) * 8;
                 if (t < N * N) {
                     Nbr n, f;
-                    gather_nxn(P, L, r, N, xO, yO, px, py, n);
+                    gather_tab(L, fq, half, N, xO, yO, px, py, cip, n);
                     if (N == 8) filter_8x8(n, f); else f = n;
                     const int mode = (m.ipred[bk >> 1] >> ((bk & 1) * 4)) & 15;
                     const int x = t % N, y = t / N;
@@ -863,7 +899,7 @@ extern "C" __global__ __launch_bounds__(256) void k_mbaff_intra(h264r_batch b, i
         int v = 0, cx = 0, cy = 0, pl = 0;
         if (t < 128) {
             pl = t >> 6; cx = t & 7; cy = (t >> 3) & 7;
-            v = clip255(L.R.cof[1 + pl][cy * 8 + cx] + pred_chroma(P, L, r, m.chroma_mode, pl, px, py, cx, cy));
+            v = clip255(L.R.cof[1 + pl][cy * 8 + cx] + pred_chroma_tab(L, cip, m.chroma_mode, pl, cx, cy));
         }
         __syncthreads();
         if (t < 128) {
