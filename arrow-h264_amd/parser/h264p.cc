@@ -643,6 +643,7 @@ struct MbState {
     uint8_t sub_type[4] = {}, sub_pred[4] = {};
     // read by the CABAC context selection (neighbour.cc:415-764)
     bool skip = false;
+    bool fld = false;                     // mb_field_decoding_flag (MBAFF frames)
     uint8_t cbpl = 0, cbpc = 0, cmode = 0;
     uint64_t cbp_bits = 0;                // coded_block_flag bits (update_coded_block_flag)
     int16_t mvd[2][16][2] = {};           // mvd_l0 / mvd_l1 per 4x4 block (raster)
@@ -671,10 +672,15 @@ struct SliceCtx {
     const uint8_t* zz8;
     int qp;                     // slice.parser.QpY
     int skip_run = -1;
+    bool mbaff;                 // MbaffFrameFlag: MB pairs, addr an MB address, the state at its storage index
+    uint8_t nref_m1[2];         // num_ref_idx_lX_active_minus1 as the reference's parser has it at the current
+                                // MB: it doubles the slice header's count in place, in a uint8_t (slice.h:53-54),
+                                // for every field MB of an MBAFF P / B slice and never halves it
+                                // (interpret_mb.cc:271-275); the te() range of ref_idx
     Cabac* cab = nullptr;       // CABAC slices (entropy_coding_mode_flag)
     int last_dquant = 0;
-    // the current MB
-    int addr = 0, mbx = 0, mby = 0;
+    // the current MB (addr its MB address; MBAFF: stored at row mby = 2 pair_row + addr % 2, include/h264r.h)
+    int addr = 0, si = 0, mbx = 0, mby = 0;
     MbState* cur = nullptr;
     int cbpl = 0, cbpc = 0, qpy = 0, qpc[2] = {0, 0}, qsc[2] = {0, 0}, qp_scaled[3] = {0, 0, 0};
     bool bypass = false, skip = false, allrefzero = false, no_sub_lt8 = true;
@@ -900,7 +906,8 @@ void Decoder::parse_slice_header(Bits& b, SliceHeader& h)
     unsupported(sps.separate_planes || sps.bit_depth_y != 8 || (sps.chroma_format_idc && sps.bit_depth_c != 8),
                 "picture format (4:0:0, 4:2:0, 4:2:2 or 4:4:4 without separate colour planes, 8-bit only)");
     unsupported(sps.chroma_format_idc == 3 && pps.cabac, "4:4:4 with CABAC (entropy_coding_mode_flag)");
-    unsupported(sps.mbaff, "MBAFF coding (mb_adaptive_frame_field_flag)");
+    unsupported(sps.mbaff && pps.cabac, "MBAFF coding with CABAC");
+    unsupported(sps.mbaff && h.slice_type == H264R_SLICE_B, "B slices of MBAFF frames");
     unsupported(sps.poc_type == 1, "pic_order_cnt_type 1");
     unsupported(h.slice_type == H264R_SLICE_SI, "SI slices");
     h.frame_num = b.u(sps.log2_max_frame_num);
@@ -1065,6 +1072,7 @@ void Decoder::run_slices()
     const int hw = std::max(1, (int)std::thread::hardware_concurrency());
     // threads pay off on large pictures; H264P_THREADS forces them (the tests use it)
     int threads = env_threads ? env_threads : (W * H >= 1200 ? std::min(8, hw) : 1);
+    if (psps_->mbaff) threads = 1;                          // MBAFF slices: in order (their lookups reach later pairs)
     threads = std::min<int>(threads, (int)n);
     bool ordered = true;
     for (size_t k = 1; k < n; ++k) ordered &= pslices_[k - 1]->h.first_mb < pslices_[k]->h.first_mb;
@@ -1138,6 +1146,11 @@ void Decoder::begin_picture(const SliceHeader& h)
         mbs_w_ = W;
         mbs_h_ = H;
     }
+    // MBAFF: a neighbour lookup may land in a later pair of this picture (the bottom MB of the
+    // current pair, the pair to the right), which must read as not decoded (reset_mbs,
+    // slice_data.cc:53-58)
+    if (sps.mbaff)
+        for (MbState& m : mbs_) { m.slice_nr = -1; m.fld = false; }
     unsupported(sps.gaps, "gaps_in_frame_num_value_allowed_flag");
     int poc = 0;
     const int max_frame_num = 1 << sps.log2_max_frame_num;
@@ -1440,7 +1453,7 @@ void Decoder::finish_picture()
     p.constrained_intra_pred = ppps_->cip;
     p.num_slices = (int)slice_tab_.size();
     p.poc = cur_poc_;
-    p.structure = !fld ? H264R_FRAME : par ? H264R_BOTTOM_FIELD : H264R_TOP_FIELD;
+    p.structure = !fld ? (psps_->mbaff ? H264R_MBAFF_FRAME : H264R_FRAME) : par ? H264R_BOTTOM_FIELD : H264R_TOP_FIELD;
     check(h264r_picture_begin(ctx_, W, H, &p, slice_tab_.data(), &quant_), "h264r_picture_begin");
     for (int a = 0; a < W * H; ++a) {
         if (!seen_[a]) fail(H264R_ESTATE, "picture with missing macroblocks");
@@ -1644,16 +1657,18 @@ SliceCtx::SliceCtx(Decoder& d, const Sps& s, const Pps& p, const SliceHeader& h,
     : D(d), sps(s), pps(p), sh(h), slice_nr(nr), b(bits), W(s.W), H(h.field ? s.H / 2 : s.H),
       cf(s.chroma_format_idc), mwc(s.chroma_format_idc == 3 ? 16 : s.chroma_format_idc ? 8 : 0),
       mhc(s.chroma_format_idc == 1 ? 8 : s.chroma_format_idc ? 16 : 0),
-      zz4(h.field ? FIELD_SCAN4X4 : ZZ4), zz8(h.field ? FIELD_SCAN8X8 : ZZ8), qp(h.qp), list_(lists), list_n_(list_n),
-      end_mb(end)
+      zz4(h.field ? FIELD_SCAN4X4 : ZZ4), zz8(h.field ? FIELD_SCAN8X8 : ZZ8), qp(h.qp),
+      mbaff(s.mbaff && !h.field), list_(lists), list_n_(list_n), end_mb(end)
 {
+    nref_m1[0] = (uint8_t)(h.nref[0] - 1);
+    nref_m1[1] = (uint8_t)(h.nref[1] - 1);
 }
 
 // slice_data (7.3.4; slice_data.cc:636-660, macroblock_t::close :526-565)
 void SliceCtx::run()
 {
     const bool I = sh.slice_type == H264R_SLICE_I;
-    addr = sh.first_mb;
+    addr = sh.first_mb * (mbaff ? 2 : 1);                   // MBAFF: first_mb_in_slice counts MB pairs
     require(addr < W * H, "slice: first_mb_in_slice");
     if (pps.cabac) {
         // Parser::init / slice_t::init (interpret_mb.cc:138-156, slice_data.cc:602-604); the
@@ -1701,6 +1716,23 @@ void SliceCtx::update_qp(int q)
 MbState* SliceCtx::nb_mb(bool chroma, int xN, int yN, int& ax, int& ay)
 {
     const int mw = chroma ? mwc : 16, mh = chroma ? mhc : 16;
+    if (mbaff) {
+        // MBAFF (neighbour.cc:123-173): the geometric frame sample of the current MB's (xN, yN) -- a
+        // field MB's rows are every second row of its pair --, the MB holding it (the bottom MB of a
+        // field pair for odd rows, of a frame pair for its lower half) and the sample's storage
+        // position in that MB's rows (ax, ay)
+        const int lx = mbx * mw + xN;
+        const int ly = (mby >> 1) * 2 * mh + (cur->fld ? (mby & 1) + 2 * yN : (mby & 1) * mh + yN);
+        if (lx < 0 || lx >= W * mw || ly < 0 || ly >= H * mh) return nullptr;
+        const int npy = ly / (2 * mh), r = ly % (2 * mh);
+        const MbState& top = D.mbs_[(size_t)(2 * npy) * W + lx / mw];
+        const bool nf = top.slice_nr == slice_nr && top.fld;
+        const int nb = nf ? (ly & 1) : (r >= mh);
+        ax = lx;
+        ay = npy * 2 * mh + (nf ? r / 2 + (ly & 1) * mh : r);
+        MbState* m = &D.mbs_[(size_t)(2 * npy + nb) * W + lx / mw];
+        return m->slice_nr == slice_nr ? m : nullptr;
+    }
     ax = mbx * mw + xN;
     ay = mby * mh + yN;
     if (ax < 0 || ax >= W * mw || ay < 0 || ay >= H * mh) return nullptr;
@@ -1710,9 +1742,10 @@ MbState* SliceCtx::nb_mb(bool chroma, int xN, int yN, int& ax, int& ay)
 
 void SliceCtx::macroblock()
 {
-    mbx = addr % W;
-    mby = addr / W;
-    MbState& m = D.mbs_[addr];
+    si = mbaff ? ((addr >> 1) / W * 2 + (addr & 1)) * W + (addr >> 1) % W : addr;
+    mbx = si % W;
+    mby = si / W;
+    MbState& m = D.mbs_[si];
     cur = &m;
     // macroblock_t::init (slice_data.cc:455-524)
     m.slice_nr = slice_nr;
@@ -1740,6 +1773,19 @@ void SliceCtx::macroblock()
         }
     }
     m.skip = skip;
+    if (mbaff) {
+        // mb_field_decoding_flag (interpret_mb.cc:250-262): coded in the top MB of a pair; the inferred
+        // flags of skipped pairs (:208-238) are not on this parser's path
+        unsupported(skip || cab, "skipped MBs / CABAC in MBAFF frames");
+        m.fld = (addr & 1) ? D.mbs_[si - W].fld : b.u(1) != 0;
+        zz4 = m.fld ? FIELD_SCAN4X4 : ZZ4;                   // a field MB's scans (transform.cc:344-357)
+        zz8 = m.fld ? FIELD_SCAN8X8 : ZZ8;
+        if (!I) {                                            // interpret_mb.cc:271-275, as the reference does it
+            if (m.fld)
+                for (uint8_t& v : nref_m1) v = (uint8_t)(((v + 1) << 1) - 1);
+        }
+    } else
+        m.fld = false;
     mb_type = skip ? 0 : (cab ? cabac_mb_type(I, B) : b.ue_max(48, "mb_type")) + ((!I && !B) ? 1 : 0);
     // mb_type tables (interpret_mb.cc:318-406)
     int itype = -1;
@@ -2021,6 +2067,13 @@ void SliceCtx::neighbour_mv(int list, int i, int j, int w, int h, bool avail[3],
             ref[k] = M.ref_idx[list][e];
             mv[k][0] = M.mvx[list][e];
             mv[k][1] = M.mvy[list][e];
+            if (mbaff && cur->fld && !N[k]->fld) {         // interpret_mv.cc:60-104: field MB, frame neighbour
+                if (ref[k] >= 0) ref[k] *= 2;
+                mv[k][1] /= 2;
+            } else if (mbaff && !cur->fld && N[k]->fld) {  // frame MB, field neighbour
+                ref[k] >>= 1;
+                mv[k][1] *= 2;
+            }
         }
     }
 }
@@ -2248,10 +2301,10 @@ void SliceCtx::inter_pred()
                 const int part = 2 * (y8 >> 1) + (x8 >> 1);
                 if ((m.sub_pred[part] == l || m.sub_pred[part] == 2) && m.sub_type[part] != 0) {
                     const bool present = B || !allrefzero || m.mb_type != H264R_P_8x8;
-                    const int n = sh.nref[l];
+                    const int n = mbaff ? nref_m1[l] + 1 : sh.nref[l];   // te() range (MBAFF: the reference's count)
                     int r = 0;
-                    if (present && n > 1) r = cab ? cabac_ref_idx(l, x8, y8) : n == 2 ? 1 - (int)b.u(1) : b.ue_max(31, "ref_idx");
-                    require(r >= 0 && r < n, "ref_idx out of range");
+                    if (present && n > 1) r = cab ? cabac_ref_idx(l, x8, y8) : n == 2 ? 1 - (int)b.u(1) : b.ue_max(63, "ref_idx");
+                    require(r >= 0 && r < sh.nref[l] * (m.fld ? 2 : 1), "ref_idx out of range");
                     for (int y4 = 0; y4 < sv0; ++y4)
                         for (int x4 = 0; x4 < sh0; ++x4) M.ref_idx[l][M.at(mbx * 4 + x8 + x4, mby * 4 + y8 + y4)] = (int8_t)r;
                 }
@@ -2289,7 +2342,8 @@ void SliceCtx::inter_pred()
         for (int x = 0; x < 4; ++x) {
             const size_t e = M.at(mbx * 4 + x, mby * 4 + y);
             for (int l = 0; l < nlists; ++l) {
-                const int r = M.ref_idx[l][e];
+                // an MBAFF field MB's refIdx r names a field of frame r / 2 (get_ref_pic dpb.cc:1046-1055)
+                const int r = m.fld && M.ref_idx[l][e] >= 0 ? M.ref_idx[l][e] >> 1 : M.ref_idx[l][e];
                 M.ref_pic[l][e] = (r >= 0 && list_[l][r]) ? list_[l][r]->id : -1;
             }
         }
@@ -2732,11 +2786,12 @@ void SliceCtx::stage()
         D.slice_tab_[slice_nr].qs_c[0] = (int8_t)qsc[0];
         D.slice_tab_[slice_nr].qs_c[1] = (int8_t)qsc[1];
     }
-    StagedMb& st = D.staged_[addr];
+    StagedMb& st = D.staged_[si];
     h264r_mb& r = st.rec;
     memset(&r, 0, sizeof(r));
     r.mb_type = m.mb_type;
-    r.flags = (uint8_t)((m.intra ? H264R_MBF_INTRA : 0) | (m.t8 ? H264R_MBF_T8x8 : 0) | (bypass ? H264R_MBF_BYPASS : 0));
+    r.flags = (uint8_t)((m.intra ? H264R_MBF_INTRA : 0) | (m.t8 ? H264R_MBF_T8x8 : 0) | (bypass ? H264R_MBF_BYPASS : 0) |
+                        (m.fld ? H264R_MBF_FIELD : 0));
     r.cbp = (uint8_t)(cbpl | cbpc << 4);
     r.qp_y = (int8_t)qpy;
     r.qp_c[0] = (int8_t)qpc[0];
@@ -2839,7 +2894,7 @@ void SliceCtx::stage()
             st.ref[l][k] = M.ref_pic[l][e] >= 0 ? M.ref_idx[l][e] : (int8_t)-1;
         }
     }
-    D.seen_[addr] = 1;
+    D.seen_[si] = 1;
 }
 
 }  // namespace

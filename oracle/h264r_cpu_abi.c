@@ -259,9 +259,9 @@ static int picture_end(h264r_ctx* c, uint8_t* y, uint8_t* u, uint8_t* v, int kee
         memset(q + c->cap_levels, 0, (c->n_levels + 64 - c->cap_levels) * 2);
         c->levels = q; c->cap_levels = c->n_levels + 64;
     }
-    if (c->pic.structure < H264R_FRAME || c->pic.structure > H264R_BOTTOM_FIELD) return H264R_EINVAL;
-    /* a field picture's slots are frames of twice its height (include/h264r.h) */
-    const int fld = c->pic.structure != H264R_FRAME, frame_h = c->ph << fld;
+    if (c->pic.structure < H264R_FRAME || c->pic.structure > H264R_MBAFF_FRAME) return H264R_EINVAL;
+    /* a field picture's slots are frames of twice its height (include/h264r.h); an MBAFF frame is a frame */
+    const int fld = c->pic.structure == H264R_TOP_FIELD || c->pic.structure == H264R_BOTTOM_FIELD, frame_h = c->ph << fld;
     oracle_picture p;
     memset(&p, 0, sizeof(p));
     p.width_mbs = c->pw; p.height_mbs = c->ph;
@@ -274,7 +274,10 @@ static int picture_end(h264r_ctx* c, uint8_t* y, uint8_t* u, uint8_t* v, int kee
     p.chroma_format = c->cf;
     if (fld && c->cf != 1) return H264R_EUNSUPPORTED;          /* field pictures: 4:2:0 only */
     int st = oracle_decode_picture(&p);
-    if (st) return H264R_EINVAL;
+    if (st) {
+        if (getenv("H264R_CPU_VERBOSE")) fprintf(stderr, "h264r (cpu): oracle_decode_picture -> %d\n", st);
+        return H264R_EINVAL;
+    }
     uint8_t* out[3] = {y, u, v};
     capture(c, keep, out);
     if (keep >= 0 && !fld) {

@@ -41,7 +41,9 @@
  * Reconstruction is deferred to picture end: the parser never reads reconstructed
  * samples (only syntax and mv_info), so the result is the same.
  *
- * Field pictures (PAFF, field_pic_flag; MBAFF frames stay H264R_EUNSUPPORTED): the reference
+ * MBAFF frames (MbaffFrameFlag): every MB is staged at its storage position mb_t::mb with its
+ * mb_field_decoding_flag (H264R_MBF_FIELD) and the picture goes in as H264R_MBAFF_FRAME.
+ * Field pictures (PAFF, field_pic_flag): the reference
  * decodes a field into a field storable_picture of half the frame's rows and deblocks it on
  * its own (exit_picture picture.cc:239-269), splits decoded frames into field views
  * (dpb_split_field picture.cc:408-470) and combines decoded field pairs into frames
@@ -194,7 +196,7 @@ void begin_picture(Shim& S, slice_t& slice)
     const int cf = sps.chroma_format_idc;
     if (cf < 0 || cf > 3 || sps.separate_colour_plane_flag || sps.BitDepthY != 8 || (cf && sps.BitDepthC != 8))
         check(H264R_EUNSUPPORTED, "picture format (4:0:0, 4:2:0, 4:2:2 or 4:4:4 without separate planes, 8-bit)");
-    if (slice.header.MbaffFrameFlag) check(H264R_EUNSUPPORTED, "MBAFF frames");
+    if (slice.header.MbaffFrameFlag && cf != 1) check(H264R_EUNSUPPORTED, "MBAFF frames off 4:2:0");
     if (cf != 1 && slice.header.field_pic_flag) check(H264R_EUNSUPPORTED, "4:2:2 / 4:4:4 field pictures");
     // the context holds frames; a field picture is PicHeightInMbs = FrameHeightInMbs / 2 rows
     const int W = sps.PicWidthInMbs, H = sps.FrameHeightInMbs, PH = slice.header.PicHeightInMbs;
@@ -221,7 +223,10 @@ h264r_slice slice_record(Shim& S, slice_t& slice)
     const pps_t& pps = *slice.active_pps;
     h264r_slice r;
     memset(&r, 0, sizeof(r));
-    if (shr.MbaffFrameFlag) check(H264R_EUNSUPPORTED, "MBAFF slices");
+    // MBAFF (include/h264r.h H264R_MBAFF_FRAME): a field MB's implicit weights (per-parity POCs) have
+    // no place in h264r_slice; SP slices and lossless MBs are not on the MBAFF kernels
+    if (shr.MbaffFrameFlag && ((shr.slice_type == B_slice && pps.weighted_bipred_idc == 2) || shr.slice_type == SP_slice))
+        check(H264R_EUNSUPPORTED, "MBAFF slices with implicit weights / SP");
     // SI MBs go through mb_pred_inter in the reference with an out-of-range BLOCK_STEP row
     // (decoder.cc:141-146, 212-225): nothing defined to reproduce
     if (shr.slice_type == SI_slice) check(H264R_EUNSUPPORTED, "SI slices");
@@ -436,12 +441,15 @@ void Decoder::decode(mb_t& mb)
         S.slice_tab[si].qs_c[0] = mb.QsC[0];          // interpret_mb.cc:799-801 (one value per slice)
         S.slice_tab[si].qs_c[1] = mb.QsC[1];
     }
-    StagedMb& st = S.mbs[mb.mbAddrX];
+    // the MB's storage position (mb_t::mb; MBAFF: row 2 pair_row + bottom, include/h264r.h)
+    const int sidx = mb.mb.y * slice.active_sps->PicWidthInMbs + mb.mb.x;
+    StagedMb& st = S.mbs[sidx];
     h264r_mb& r = st.rec;
     memset(&r, 0, sizeof(r));
     r.mb_type = mb.mb_type;
     r.flags = (mb.is_intra_block ? H264R_MBF_INTRA : 0) | (mb.transform_size_8x8_flag ? H264R_MBF_T8x8 : 0) |
-              (mb.TransformBypassModeFlag ? H264R_MBF_BYPASS : 0);
+              (mb.TransformBypassModeFlag ? H264R_MBF_BYPASS : 0) |
+              (slice.header.MbaffFrameFlag && mb.mb_field_decoding_flag ? H264R_MBF_FIELD : 0);
     const int cbpl = mb.CodedBlockPatternLuma, cbpc = mb.CodedBlockPatternChroma;
     r.cbp = (uint8_t)(cbpl | cbpc << 4);
     r.qp_y = mb.QpY;
@@ -559,7 +567,7 @@ void Decoder::decode(mb_t& mb)
             st.ref[l][k] = m.ref_pic[l] ? (int8_t)m.ref_idx[l] : (int8_t)-1;
         }
     }
-    S.seen[mb.mbAddrX] = 1;
+    S.seen[sidx] = 1;
 
     // coefficient-reset protocol (slice_data.cc:496-503): the same side effects as the
     // reference's reconstruction leaves behind
@@ -597,7 +605,8 @@ void Decoder::deblock_filter(slice_t& slice)
     p.constrained_intra_pred = pps.constrained_intra_pred_flag;
     p.num_slices = (int)S.slice_tab.size();
     p.poc = pic->poc;
-    p.structure = !fld ? H264R_FRAME : shr.bottom_field_flag ? H264R_BOTTOM_FIELD : H264R_TOP_FIELD;
+    p.structure = !fld ? (shr.MbaffFrameFlag ? H264R_MBAFF_FRAME : H264R_FRAME)
+                       : shr.bottom_field_flag ? H264R_BOTTOM_FIELD : H264R_TOP_FIELD;
     check(h264r_picture_begin(S.ctx, W, H, &p, S.slice_tab.data(), &S.quant), "h264r_picture_begin");
     for (int a = 0; a < W * H; ++a) {
         if (!S.seen[a]) check(H264R_ESTATE, "picture with missing macroblocks (concealment is CPU-only)");

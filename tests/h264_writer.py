@@ -152,6 +152,13 @@ class StreamCfg:
                                      # first's frame; 1.0 = every frame); P fields predict from any
                                      # reference field (the first field of their own frame too)
     bottom_first: float = 0.0        # share of field pairs sent bottom field first
+    mbaff: float = 0.0               # > 0: MBAFF frames (frame_mbs_only_flag 0, mb_adaptive_frame_field_flag 1),
+                                     # this share of the MB pairs field pairs (mb_field_decoding_flag); CAVLC,
+                                     # no skipped MBs (no inferred field flags), no CIP, I and P pictures; the
+                                     # first three pictures are I so that every P slice has >= 3 references
+                                     # (the reference parser doubles num_ref_idx_l0_active_minus1 in place for
+                                     # every field MB, interpret_mb.cc:271-275, so a te() range of 1 would
+                                     # desynchronise it)
     chroma_format: int = 1           # chroma_format_idc (profiles 100 / 122 / 244): 1 4:2:0, 2 4:2:2 (CAVLC:
                                      # 8 chroma 4x4 blocks and a 2x4 DC per plane, nC -2, interpret_residual.cc:462-494),
                                      # 3 4:4:4 (244, CAVLC: Cb and Cr coded as luma, residual_luma per plane
@@ -169,6 +176,7 @@ class _Mb:
     kind: int = SKIP
     slice: int = -1
     intra: bool = False
+    fld: bool = False                # mb_field_decoding_flag (MBAFF frames)
     i4: list = field(default_factory=lambda: [2] * 16)   # Intra4x4PredMode, blkIdx order
     i8: list = field(default_factory=lambda: [2] * 4)
     t8: bool = False
@@ -197,6 +205,8 @@ class Encoder:
         self.W, self.H = cfg.width_mbs, cfg.height_mbs
         self.FH = cfg.height_mbs                 # frame height; a field picture has FH / 2 MB rows
         assert not cfg.field or cfg.height_mbs % 2 == 0
+        assert not cfg.mbaff or (cfg.height_mbs % 2 == 0 and cfg.skip == 0 and not cfg.cabac and not cfg.cip and
+                                 not cfg.bframes and not cfg.field and cfg.num_refs >= 3)
         self.log2_max_frame_num = 4
         self.log2_max_poc_lsb = 8
         self.cab = None                  # the CABAC sink of the slice being written (CABAC streams)
@@ -226,10 +236,10 @@ class Encoder:
         w.ue(c.num_refs)                            # max_num_ref_frames
         w.u(1, 0)                                   # gaps_in_frame_num_value_allowed_flag
         w.ue(self.W - 1)
-        if c.field:
+        if c.field or c.mbaff:
             w.ue(self.FH // 2 - 1)                  # pic_height_in_map_units_minus1 (field MB rows)
             w.u(1, 0)                               # frame_mbs_only_flag
-            w.u(1, 0)                               # mb_adaptive_frame_field_flag (PAFF only)
+            w.u(1, 1 if c.mbaff else 0)             # mb_adaptive_frame_field_flag
         else:
             w.ue(self.H - 1)
             w.u(1, 1)                               # frame_mbs_only_flag
@@ -291,6 +301,26 @@ class Encoder:
                 last = v
 
     # ------------------------------------------------------------------ availability
+    def _nbr(self, a: int, xN: int, yN: int, chroma: bool = False):
+        """MBAFF frames: Neighbour::get_neighbour (neighbour.cc:123-173) of sample (xN, yN) of MB a
+        (storage index: row 2 pair_row + bottom) -- the geometric frame sample, the MB holding it and
+        the sample's place in that MB -- if decoded in the current slice: (mb, lx, ly) or None."""
+        mw = mh = 8 if chroma else 16
+        W = self.W
+        mbx, mby = a % W, a // W
+        m = self.mbs[a]
+        lx = mbx * mw + xN
+        ly = (mby >> 1) * 2 * mh + ((mby & 1) + 2 * yN if m.fld else (mby & 1) * mh + yN)
+        if lx < 0 or lx >= W * mw or ly < 0 or ly >= self.H * mh:
+            return None
+        npy, nx, rr = ly // (2 * mh), lx // mw, ly % (2 * mh)
+        top = self.mbs[2 * npy * W + nx]
+        nb = (ly & 1) if top.fld else int(rr >= mh)
+        nm = self.mbs[(2 * npy + nb) * W + nx]
+        if nm.slice != m.slice:                          # other slice, or not decoded yet (slice -1)
+            return None
+        return nm, lx % mw, (rr // 2) if top.fld else rr % mh
+
     def _mb_at(self, x: int, y: int, cur_slice: int):
         if x < 0 or y < 0 or x >= self.W or y >= self.H:
             return None
@@ -311,6 +341,14 @@ class Encoder:
         luma = pl == 0 or self.c.chroma_format == 3     # 4:4:4: Cb / Cr blocks in the luma grid
         nw = 4 if luma else 2                           # 4x4 blocks per MB: across, down
         nh = 4 if luma or self.c.chroma_format == 2 else 2
+        if self.c.mbaff:                                # predict_nnz through get_neighbour
+            def nz_at(dx, dy):
+                n = self._nbr(a, bx * 4 + dx, by * 4 + dy, not luma)
+                return None if n is None else n[0].nz[pl][n[2] // 4][n[1] // 4]
+            na, nb = nz_at(-1, 0), nz_at(0, -1)
+            if na is not None and nb is not None:
+                return (na + nb + 1) >> 1
+            return (na or 0) + (nb or 0)
         def nz_of(dx, dy):
             x, y = bx + dx, by + dy
             ox, oy = mx + (x // nw if x >= 0 else -1), my + (y // nh if y >= 0 else -1)
@@ -475,7 +513,12 @@ class Encoder:
         mx, my = a % self.W, a // self.W
         def mode_of(dx, dy):
             x, y = bx + dx, by + dy
-            if x >= 0 and y >= 0:
+            if self.c.mbaff:                             # get_neighbour of the sample (neighbour.cc:318-400)
+                n = self._nbr(a, bx * 4 + (-1 if dx else 0), by * 4 + (-1 if dy else 0))
+                if n is None:
+                    return None
+                nb, lx, ly = n[0], n[1] // 4, n[2] // 4
+            elif x >= 0 and y >= 0:
                 nb, lx, ly = m, x, y
             else:
                 nb = self._intra_avail(mx + (-1 if x < 0 else 0), my + (-1 if y < 0 else 0), s)
@@ -498,6 +541,9 @@ class Encoder:
     def _avail_abd(self, a: int, bx: int, by: int, n: int, s: int):
         """Availability of neighbours A, B, D of an n-wide block at (bx, by) (4x4 units)."""
         mx, my = a % self.W, a // self.W
+        if self.c.mbaff:
+            ok = lambda x, y: self._nbr(a, x, y) is not None
+            return ok(bx * 4 - 1, by * 4), ok(bx * 4, by * 4 - 1), ok(bx * 4 - 1, by * 4 - 1)
         av = lambda dx, dy: self._intra_avail(mx + dx, my + dy, s) is not None
         A = bx > 0 or av(-1, 0)
         B = by > 0 or av(0, -1)
@@ -528,6 +574,11 @@ class Encoder:
         m.slice = s
         if cab:
             cab.start_mb(a)
+        if c.mbaff:                                      # mb_field_decoding_flag, with the pair's top MB
+            top = (a // self.W) % 2 == 0
+            m.fld = (r.random() < c.mbaff) if top else self.mbs[a - self.W].fld
+            if top:
+                w.u(1, 1 if m.fld else 0)
         roll = r.random()
         if ptype in ("P", "B") and roll < c.skip:
             m.kind, m.intra, m.skip, m.mbt_ref = SKIP, False, True, 0
@@ -654,14 +705,16 @@ class Encoder:
             else:
                 w.ue(mbt)
             parts = {0: [(0, 0, 4, 4)], 1: [(0, 0, 4, 2), (0, 2, 4, 2)], 2: [(0, 0, 2, 4), (2, 0, 2, 4)]}
+            nr = nref * 2 if m.fld else nref            # a field MB's refIdx counts fields
+            nhdr = self.nref_hdr * (2 if m.fld else 1) if c.mbaff else nr
             def ref_idx(x0, y0, pw, ph):
-                v = r.randrange(nref)
+                v = r.randrange(nr)
                 if cab:
                     cab.ref_idx(v, nref, 0, x0, y0)
                     self._set_ref(m, 0, x0, y0, pw, ph, v)
-                elif nref == 2:
+                elif nhdr == 2:
                     w.u(1, 1 - v)
-                elif nref > 2:
+                elif nhdr > 2:
                     w.ue(v)
             def mvd(x0, y0, pw, ph):
                 dx, dy = r.randint(-c.mv_range, c.mv_range), r.randint(-c.mv_range, c.mv_range)
@@ -865,7 +918,8 @@ class Encoder:
         self.mbs = [_Mb() for _ in range(n)]
         ptype = kind or ("I" if idr else "P")
         sp = ptype == "P" and c.sp > 0 and r.random() < c.sp   # (no draw otherwise: fixed streams stay)
-        starts = sorted({0} | set(r.sample(range(1, n), min(c.slices - 1, n - 1)))) if c.slices > 1 else [0]
+        units = n // 2 if c.mbaff else n                  # MBAFF: first_mb_in_slice counts MB pairs
+        starts = sorted({0} | set(r.sample(range(1, units), min(c.slices - 1, units - 1)))) if c.slices > 1 else [0]
         frame_num = 0 if idr else (self.frame_num + (0 if second else 1)) % (1 << self.log2_max_frame_num)
         tracked = bool(c.bframes or c.long_term)           # DPB bookkeeping of the IBBP / long-term streams
         if tracked and not idr:
@@ -887,14 +941,18 @@ class Encoder:
         if not tracked:
             self.refs = 0 if idr else min(self.refs + 1, c.num_refs)
         out = []
+        W = self.W
+        # the MBs of a slice in decoding order (MBAFF: pair by pair, top then bottom, by storage index)
+        order = (lambda f, e: [((q // 2) // W * 2 + q % 2) * W + (q // 2) % W for q in range(2 * f, 2 * e)]) \
+            if c.mbaff else (lambda f, e: list(range(f, e)))
         for s, first in enumerate(starts):
-            end = starts[s + 1] if s + 1 < len(starts) else n
+            end = starts[s + 1] if s + 1 < len(starts) else units
             w = BitWriter()
             w.ue(first)
             w.ue(7 if ptype == "I" else (8 if sp else (6 if ptype == "B" else 5)))   # slice_type (all slices alike)
             w.ue(0)                                 # pic_parameter_set_id
             w.u(self.log2_max_frame_num, frame_num)
-            if c.field:
+            if c.field or c.mbaff:
                 w.u(1, 1 if structure else 0)       # field_pic_flag
                 if structure:
                     w.u(1, 1 if structure == 2 else 0)   # bottom_field_flag
@@ -914,6 +972,7 @@ class Encoder:
                     self._pred_weight_table(w, nref_b, True)
             if ptype == "P":
                 w.u(1, 1)                           # num_ref_idx_active_override_flag
+                self.nref_hdr = nref
                 w.ue(nref - 1)
                 w.u(1, 0)                           # ref_pic_list_modification_flag_l0
                 if c.weighted:
@@ -971,7 +1030,7 @@ class Encoder:
                     w.u(1, 0)                       # rbsp_alignment_zero_bit
             else:
                 skip_run = 0
-                for a in range(first, end):
+                for a in order(first, end):
                     coded = self._mb(w if ptype == "I" else _Deferred(w, skip_run), a, ptype, s,
                                      nref_b if ptype == "B" else nref)
                     if ptype != "I":
@@ -999,7 +1058,7 @@ class Encoder:
             return b"".join(out + self._field_stream())
         if not c.bframes:
             for i in range(c.frames):
-                out += self.picture(i, idr=(i == 0 or c.all_intra))
+                out += self.picture(i, idr=(i == 0 or c.all_intra), kind="I" if c.mbaff and i < 3 else None)
             return b"".join(out)
         # IBBP: anchors (I / P) every bframes + 1 pictures in output order, each sent before
         # the B pictures that precede it; trailing pictures past the last anchor are P.

@@ -96,7 +96,7 @@ def test_oracle_replay_of_captures_matches_reference(name):
     def dec(p):
         W, H = p["W"], p["H"]
         out = O.new_planes(W, H, p["chroma_format"])
-        fld = S.structure(p) != A.FRAME
+        fld = S.structure(p) in (A.TOP_FIELD, A.BOTTOM_FIELD)
         o = O.OraclePicture()
         o.width_mbs, o.height_mbs = W, H
         o.chroma_format = p["chroma_format"]
