@@ -673,10 +673,7 @@ struct SliceCtx {
     int qp;                     // slice.parser.QpY
     int skip_run = -1;
     bool mbaff;                 // MbaffFrameFlag: MB pairs, addr an MB address, the state at its storage index
-    uint8_t nref_m1[2];         // num_ref_idx_lX_active_minus1 as the reference's parser has it at the current
-                                // MB: it doubles the slice header's count in place, in a uint8_t (slice.h:53-54),
-                                // for every field MB of an MBAFF P / B slice and never halves it
-                                // (interpret_mb.cc:271-275); the te() range of ref_idx
+    int run_now = 0;            // mb_skip_run as read for the current MB (before its decrement)
     Cabac* cab = nullptr;       // CABAC slices (entropy_coding_mode_flag)
     int last_dquant = 0;
     // the current MB (addr its MB address; MBAFF: stored at row mby = 2 pair_row + addr % 2, include/h264r.h)
@@ -1660,8 +1657,6 @@ SliceCtx::SliceCtx(Decoder& d, const Sps& s, const Pps& p, const SliceHeader& h,
       zz4(h.field ? FIELD_SCAN4X4 : ZZ4), zz8(h.field ? FIELD_SCAN8X8 : ZZ8), qp(h.qp),
       mbaff(s.mbaff && !h.field), list_(lists), list_n_(list_n), end_mb(end)
 {
-    nref_m1[0] = (uint8_t)(h.nref[0] - 1);
-    nref_m1[1] = (uint8_t)(h.nref[1] - 1);
 }
 
 // slice_data (7.3.4; slice_data.cc:636-660, macroblock_t::close :526-565)
@@ -1769,21 +1764,33 @@ void SliceCtx::macroblock()
         } else {
             if (skip_run == -1) skip_run = b.ue_max(W * H, "mb_skip_run");
             skip = skip_run > 0;
+            run_now = skip_run;
             --skip_run;
         }
     }
     m.skip = skip;
     if (mbaff) {
-        // mb_field_decoding_flag (interpret_mb.cc:250-262): coded in the top MB of a pair; the inferred
-        // flags of skipped pairs (:208-238) are not on this parser's path
-        unsupported(skip || cab, "skipped MBs / CABAC in MBAFF frames");
-        m.fld = (addr & 1) ? D.mbs_[si - W].fld : b.u(1) != 0;
+        // mb_field_decoding_flag.  Inferred first (macroblock_t::init slice_data.cc:505-523): a pair's top
+        // MB, or a bottom MB whose top MB was skipped, takes the flag of the pair to the left (its top MB),
+        // else of the pair above (its bottom MB), in the slice, else frame; a bottom MB after a coded top
+        // MB takes the top MB's.  A skipped top MB whose skip run ends with it takes the bottom MB's coded
+        // flag (a peek, interpret_mb.cc:233-236); a coded MB reads it when it is a top MB or follows a
+        // skipped top MB (:250-262).
+        unsupported(cab, "CABAC in MBAFF frames");
+        const bool top = (addr & 1) == 0, prev_skipped = !top && D.mbs_[si - W].skip;
+        if (top || prev_skipped) {
+            const int py = mby >> 1;
+            const MbState* A = mbx > 0 ? &D.mbs_[(size_t)(2 * py) * W + mbx - 1] : nullptr;
+            const MbState* Bm = py > 0 ? &D.mbs_[(size_t)(2 * py - 1) * W + mbx] : nullptr;
+            if (A && A->slice_nr == slice_nr) m.fld = A->fld;
+            else if (Bm && Bm->slice_nr == slice_nr) m.fld = Bm->fld;
+            else m.fld = false;
+        } else
+            m.fld = D.mbs_[si - W].fld;
+        if (top && skip && run_now == 1) m.fld = b.peek(1) != 0;
+        if (!skip && (top || prev_skipped)) m.fld = b.u(1) != 0;
         zz4 = m.fld ? FIELD_SCAN4X4 : ZZ4;                   // a field MB's scans (transform.cc:344-357)
         zz8 = m.fld ? FIELD_SCAN8X8 : ZZ8;
-        if (!I) {                                            // interpret_mb.cc:271-275, as the reference does it
-            if (m.fld)
-                for (uint8_t& v : nref_m1) v = (uint8_t)(((v + 1) << 1) - 1);
-        }
     } else
         m.fld = false;
     mb_type = skip ? 0 : (cab ? cabac_mb_type(I, B) : b.ue_max(48, "mb_type")) + ((!I && !B) ? 1 : 0);
@@ -2301,7 +2308,9 @@ void SliceCtx::inter_pred()
                 const int part = 2 * (y8 >> 1) + (x8 >> 1);
                 if ((m.sub_pred[part] == l || m.sub_pred[part] == 2) && m.sub_type[part] != 0) {
                     const bool present = B || !allrefzero || m.mb_type != H264R_P_8x8;
-                    const int n = mbaff ? nref_m1[l] + 1 : sh.nref[l];   // te() range (MBAFF: the reference's count)
+                    // te() range: a field MB's refIdx counts fields (the reference doubles num_ref_idx_active
+                    // for the MB, interpret_mb.cc:271-275, and halves it after, slice_data.cc:648-651)
+                    const int n = sh.nref[l] * (m.fld ? 2 : 1);
                     int r = 0;
                     if (present && n > 1) r = cab ? cabac_ref_idx(l, x8, y8) : n == 2 ? 1 - (int)b.u(1) : b.ue_max(63, "ref_idx");
                     require(r >= 0 && r < sh.nref[l] * (m.fld ? 2 : 1), "ref_idx out of range");

@@ -154,11 +154,9 @@ class StreamCfg:
     bottom_first: float = 0.0        # share of field pairs sent bottom field first
     mbaff: float = 0.0               # > 0: MBAFF frames (frame_mbs_only_flag 0, mb_adaptive_frame_field_flag 1),
                                      # this share of the MB pairs field pairs (mb_field_decoding_flag); CAVLC,
-                                     # no skipped MBs (no inferred field flags), no CIP, I and P pictures; the
-                                     # first three pictures are I so that every P slice has >= 3 references
-                                     # (the reference parser doubles num_ref_idx_l0_active_minus1 in place for
-                                     # every field MB, interpret_mb.cc:271-275, so a te() range of 1 would
-                                     # desynchronise it)
+                                     # no CIP, I and P pictures.  A pair whose two MBs are skipped takes the
+                                     # inferred flag (the left pair's, else the upper pair's, else frame); a
+                                     # pair whose top MB alone is skipped codes the flag in its bottom MB
     chroma_format: int = 1           # chroma_format_idc (profiles 100 / 122 / 244): 1 4:2:0, 2 4:2:2 (CAVLC:
                                      # 8 chroma 4x4 blocks and a 2x4 DC per plane, nC -2, interpret_residual.cc:462-494),
                                      # 3 4:4:4 (244, CAVLC: Cb and Cr coded as luma, residual_luma per plane
@@ -205,8 +203,8 @@ class Encoder:
         self.W, self.H = cfg.width_mbs, cfg.height_mbs
         self.FH = cfg.height_mbs                 # frame height; a field picture has FH / 2 MB rows
         assert not cfg.field or cfg.height_mbs % 2 == 0
-        assert not cfg.mbaff or (cfg.height_mbs % 2 == 0 and cfg.skip == 0 and not cfg.cabac and not cfg.cip and
-                                 not cfg.bframes and not cfg.field and cfg.num_refs >= 3)
+        assert not cfg.mbaff or (cfg.height_mbs % 2 == 0 and not cfg.cabac and not cfg.cip and not cfg.bframes and
+                                 not cfg.field)
         self.log2_max_frame_num = 4
         self.log2_max_poc_lsb = 8
         self.cab = None                  # the CABAC sink of the slice being written (CABAC streams)
@@ -574,12 +572,31 @@ class Encoder:
         m.slice = s
         if cab:
             cab.start_mb(a)
-        if c.mbaff:                                      # mb_field_decoding_flag, with the pair's top MB
-            top = (a // self.W) % 2 == 0
-            m.fld = (r.random() < c.mbaff) if top else self.mbs[a - self.W].fld
+        if c.mbaff:
+            # mb_field_decoding_flag: both MBs' skip draws are made with the top MB (where the pair's
+            # flag goes depends on them, interpret_mb.cc:208-262, slice_data.cc:505-523)
+            W = self.W
+            top = (a // W) % 2 == 0
             if top:
-                w.u(1, 1 if m.fld else 0)
-        roll = r.random()
+                self.pair_roll = (r.random(), r.random())
+                sk = [ptype == "P" and x < c.skip for x in self.pair_roll]
+                if sk[0] and sk[1]:                      # inferred: left pair, else upper pair, else frame
+                    mx, py = a % W, (a // W) // 2
+                    A = self.mbs[(2 * py) * W + mx - 1] if mx > 0 else None
+                    B = self.mbs[(2 * py - 1) * W + mx] if py > 0 else None
+                    m.fld = A.fld if A is not None and A.slice == s else (B.fld if B is not None and B.slice == s else False)
+                else:
+                    m.fld = r.random() < c.mbaff
+                self.pair_skip = sk
+                if not sk[0]:
+                    w.u(1, 1 if m.fld else 0)
+            else:
+                m.fld = self.mbs[a - W].fld
+                if self.pair_skip[0] and not self.pair_skip[1]:
+                    w.u(1, 1 if m.fld else 0)            # coded in the bottom MB after a skipped top MB
+            roll = self.pair_roll[0 if top else 1]
+        else:
+            roll = r.random()
         if ptype in ("P", "B") and roll < c.skip:
             m.kind, m.intra, m.skip, m.mbt_ref = SKIP, False, True, 0
             m.nz = [[[0] * 4 for _ in range(4)] for _ in range(3)]
@@ -706,7 +723,7 @@ class Encoder:
                 w.ue(mbt)
             parts = {0: [(0, 0, 4, 4)], 1: [(0, 0, 4, 2), (0, 2, 4, 2)], 2: [(0, 0, 2, 4), (2, 0, 2, 4)]}
             nr = nref * 2 if m.fld else nref            # a field MB's refIdx counts fields
-            nhdr = self.nref_hdr * (2 if m.fld else 1) if c.mbaff else nr
+            nhdr = nr
             def ref_idx(x0, y0, pw, ph):
                 v = r.randrange(nr)
                 if cab:
@@ -972,7 +989,6 @@ class Encoder:
                     self._pred_weight_table(w, nref_b, True)
             if ptype == "P":
                 w.u(1, 1)                           # num_ref_idx_active_override_flag
-                self.nref_hdr = nref
                 w.ue(nref - 1)
                 w.u(1, 0)                           # ref_pic_list_modification_flag_l0
                 if c.weighted:
@@ -1058,7 +1074,7 @@ class Encoder:
             return b"".join(out + self._field_stream())
         if not c.bframes:
             for i in range(c.frames):
-                out += self.picture(i, idr=(i == 0 or c.all_intra), kind="I" if c.mbaff and i < 3 else None)
+                out += self.picture(i, idr=(i == 0 or c.all_intra))
             return b"".join(out)
         # IBBP: anchors (I / P) every bframes + 1 pictures in output order, each sent before
         # the B pictures that precede it; trailing pictures past the last anchor are P.

@@ -113,20 +113,23 @@ STREAMS = {
     "hp_1080i_cabac_paff": dict(width_mbs=120, height_mbs=68, frames=2, seed=505, profile=100, transform8x8=1,
                                 cabac=1, field=1.0, num_refs=2, slices=4, deblock=(0, 2), crop=(0, 0, 0, 2)),
     # MBAFF frames (mb_adaptive_frame_field_flag, CAVLC, I and P): frame and field MB pairs at random
-    # (mb_field_decoding_flag in each pair's top MB), CAVLC nC / intra-mode prediction / motion vector
-    # prediction over the pairs' geometric neighbours (neighbour.cc:123-173, interpret_mv.cc:60-104), field
-    # MBs predicting from reference fields with refIdx over 2 x num_ref_idx_active; first_mb_in_slice in
-    # pairs.  No skipped MBs (the inferred field flags of skipped pairs are not on the own parser's path).
+    # (mb_field_decoding_flag in a pair's top MB, in its bottom MB after a skipped top MB, inferred from
+    # the left / upper pair for a skipped pair), CAVLC nC / intra-mode prediction / motion vector and
+    # P_Skip prediction over the pairs' geometric neighbours (neighbour.cc:123-173, interpret_mv.cc:
+    # 60-104, 158-190), field MBs predicting from reference fields with refIdx over 2 x
+    # num_ref_idx_active (a te() of one bit with one reference); first_mb_in_slice in pairs
     "hp_cif_mbaff_intra_pcm": dict(width_mbs=22, height_mbs=18, frames=3, seed=901, profile=100, transform8x8=1,
-                                   mbaff=0.5, skip=0.0, num_refs=3, pcm=0.05, slices=2, deblock=(0, 2), offsets=3),
+                                   mbaff=0.5, all_intra=True, pcm=0.05, slices=2, deblock=(0, 2), offsets=3),
     "mp_cif_mbaff_ippp_slices": dict(width_mbs=22, height_mbs=18, frames=6, seed=902, profile=77, mbaff=0.5,
-                                     skip=0.0, num_refs=3, slices=3, deblock=(0, 1, 2), offsets=4, intra_in_p=0.2,
+                                     skip=0.3, num_refs=3, slices=3, deblock=(0, 1, 2), offsets=4, intra_in_p=0.2,
                                      pcm=0.03),
     "hp_cif_mbaff_wp_8x8_scaling": dict(width_mbs=22, height_mbs=18, frames=6, seed=903, profile=100,
-                                        transform8x8=1, mbaff=0.6, skip=0.0, num_refs=4, weighted=1, scaling=3,
+                                        transform8x8=1, mbaff=0.6, skip=0.2, num_refs=4, weighted=1, scaling=3,
                                         chroma_qp_offset=2, qp=(14, 40)),
+    "mp_qcif_mbaff_oneref_skips": dict(width_mbs=11, height_mbs=10, frames=8, seed=905, profile=77, mbaff=0.5,
+                                       skip=0.5, num_refs=1, intra_in_p=0.1),
     "hp_vga_mbaff_ippp": dict(width_mbs=40, height_mbs=34, frames=5, seed=904, profile=100, transform8x8=1,
-                              mbaff=0.5, skip=0.0, num_refs=3, slices=2, deblock=(0, 2), intra_in_p=0.15),
+                              mbaff=0.5, skip=0.25, num_refs=2, slices=2, deblock=(0, 2), intra_in_p=0.15),
     # 4:2:2 (chroma_format_idc 2; High 4:2:2 / High 4:4:4 Predictive, CAVLC): 8 x 16 chroma per MB, the
     # 2x4 chroma DC (coeff_token nC -2, total_zeros of 8), 8 chroma AC blocks per plane.  No 8x8
     # transforms: the reference leaves the bS of a transform-8x8 MB's chroma rows 4 / 12 unset
