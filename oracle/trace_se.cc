@@ -47,3 +47,33 @@ COEFF("coeff_luma_dc", _ZN3vio4h2647Decoder13coeff_luma_dcEPNS0_12macroblock_tE1
 COEFF("coeff_luma_ac", _ZN3vio4h2647Decoder13coeff_luma_acEPNS0_12macroblock_tE10ColorPlaneiiii)
 COEFF("coeff_chroma_dc", _ZN3vio4h2647Decoder15coeff_chroma_dcEPNS0_12macroblock_tE10ColorPlaneiiii)
 COEFF("coeff_chroma_ac", _ZN3vio4h2647Decoder15coeff_chroma_acEPNS0_12macroblock_tE10ColorPlaneiiii)
+
+// context selections (CtxIdxInc, neighbour.cc), printed as "CTX <name> <args> = <ctxIdxInc>"
+extern "C" int __real__ZN3vio4h2649CtxIdxInc5mvd_lEhhhb(void*, uint8_t, uint8_t, uint8_t, bool);
+extern "C" int __wrap__ZN3vio4h2649CtxIdxInc5mvd_lEhhhb(void* s, uint8_t l, uint8_t x, uint8_t y, bool c)
+{
+    int v = __real__ZN3vio4h2649CtxIdxInc5mvd_lEhhhb(s, l, x, y, c);
+    fprintf(stderr, "CTX mvd %d %d %d %d = %d\n", l, x, y, (int)c, v);
+    return v;
+}
+extern "C" int __real__ZN3vio4h2649CtxIdxInc12mb_skip_flagEv(void*);
+extern "C" int __wrap__ZN3vio4h2649CtxIdxInc12mb_skip_flagEv(void* s)
+{
+    int v = __real__ZN3vio4h2649CtxIdxInc12mb_skip_flagEv(s);
+    fprintf(stderr, "CTX mb_skip_flag = %d\n", v);
+    return v;
+}
+extern "C" int __real__ZN3vio4h2649CtxIdxInc22mb_field_decoding_flagEv(void*);
+extern "C" int __wrap__ZN3vio4h2649CtxIdxInc22mb_field_decoding_flagEv(void* s)
+{
+    int v = __real__ZN3vio4h2649CtxIdxInc22mb_field_decoding_flagEv(s);
+    fprintf(stderr, "CTX mb_field_decoding_flag = %d\n", v);
+    return v;
+}
+extern "C" int __real__ZN3vio4h2649CtxIdxInc9ref_idx_lEhhh(void*, uint8_t, uint8_t, uint8_t);
+extern "C" int __wrap__ZN3vio4h2649CtxIdxInc9ref_idx_lEhhh(void* s, uint8_t l, uint8_t x, uint8_t y)
+{
+    int v = __real__ZN3vio4h2649CtxIdxInc9ref_idx_lEhhh(s, l, x, y);
+    fprintf(stderr, "CTX ref_idx %d %d %d = %d\n", l, x, y, v);
+    return v;
+}

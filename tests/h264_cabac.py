@@ -156,13 +156,21 @@ class CabacSink:
 
     # ---------------------------------------------------------------- neighbours
     def _mb(self, dx: int, dy: int):
-        """The MB at (x + dx, y + dy) of the current MB if it is in the current slice."""
+        """The MB at (x + dx, y + dy) of the current MB if it is in the current slice (MBAFF: the
+        MB holding sample (-1, 0) / (0, -1), get_mb neighbour.cc:175-227)."""
+        if self.e.c.mbaff:
+            nb = self.e._nbr(self.a, -1 if dx < 0 else 0, -1 if dy < 0 else 0)
+            return None if nb is None else nb[0]
         W = self.e.W
         x, y = self.a % W + dx, self.a // W + dy
         return self.e._mb_at(x, y, self.s)
 
     def _blk(self, bx: int, by: int):
-        """(MB, bx & 3, by & 3) of luma 4x4 block (bx, by) relative to the current MB, or None."""
+        """(MB, bx & 3, by & 3) of luma 4x4 block (bx, by) relative to the current MB, or None
+        (MBAFF: the block holding that block's top-left sample, get_neighbour)."""
+        if self.e.c.mbaff and (bx < 0 or by < 0):
+            nb = self.e._nbr(self.a, -1 if bx < 0 else bx * 4, -1 if by < 0 else by * 4)   # (x-1, y) / (x, y-1)
+            return None if nb is None else (nb[0], nb[1] // 4, nb[2] // 4)
         m = self._mb(-1 if bx < 0 else 0, -1 if by < 0 else 0) if (bx < 0 or by < 0) else self.e.mbs[self.a]
         return None if m is None else (m, bx & 3, by & 3)
 
@@ -180,6 +188,16 @@ class CabacSink:
         self._dec("skip_contexts", inc, 1 if skip else 0)
         if skip:
             self.last_dquant = 0
+
+    def field_flag(self, fld: bool) -> None:
+        """mb_field_decoding_flag (neighbour.cc:429-445): ctxIdxInc = the pairs to the left and
+        above in the slice that are field pairs."""
+        W = self.e.W
+        mx, py = self.a % W, (self.a // W) // 2
+        A = self.e.mbs[2 * py * W + mx - 1] if mx > 0 else None
+        B = self.e.mbs[(2 * py - 1) * W + mx] if py > 0 else None
+        inc = sum(1 for n in (A, B) if n is not None and n.slice == self.s and n.fld)
+        self._dec("mb_aff_contexts", inc, 1 if fld else 0)
 
     def end_of_slice(self, last: bool) -> None:
         self.cab.terminate(1 if last else 0)
@@ -328,8 +346,9 @@ class CabacSink:
         for b8 in range(4):
             x0, y0 = (b8 & 1) * 2, (b8 >> 1) * 2
             if x0 == 0:
-                m = self._mb(-1, 0)
-                ca, ia = (m.cbpl, (y0 & ~1) + 1) if (m is not None and m.mbt_ref != 12) else (0x3F, 0)
+                nb = self._blk(-1, y0)                     # the left 8x8 block of this row (MBAFF: its row)
+                m = None if nb is None else nb[0]
+                ca, ia = (m.cbpl, (nb[2] & ~1) + 1) if (m is not None and m.mbt_ref != 12) else (0x3F, 0)
             else:
                 ca, ia = cur, y0
             if y0 == 0:
@@ -405,7 +424,9 @@ class CabacSink:
         for w, nb in zip((1, 2), self._part_neighbours(x0, y0)):
             if nb is not None and self._coded_part(nb):
                 m, bx, by = nb
-                if m.ref[lst][by * 4 + bx] > 0:
+                # a frame MB over a field neighbour: refIdx > 1 (neighbour.cc:533-536)
+                lim = 1 if (self.e.c.mbaff and not self.e.mbs[self.a].fld and m.fld) else 0
+                if m.ref[lst][by * 4 + bx] > lim:
                     inc += w
         incs = [inc, 4, 5]
         for k in range(v):
@@ -418,7 +439,11 @@ class CabacSink:
         for nb in self._part_neighbours(x0, y0):
             if nb is not None and self._coded_part(nb):
                 m, bx, by = nb
-                s += abs(m.mvd[lst][by * 4 + bx][comp])
+                av = abs(m.mvd[lst][by * 4 + bx][comp])
+                if self.e.c.mbaff and comp:                # field / frame units (neighbour.cc:599-604)
+                    cf = self.e.mbs[self.a].fld
+                    av = av * 2 if (not cf and m.fld) else (av // 2 if (cf and not m.fld) else av)
+                s += av
         inc = 0 if s < 3 else (1 if s <= 32 else 2)
         self._ueg("mvd_x_contexts" if comp == 0 else "mvd_y_contexts", [inc, 3, 4, 5, 6], 9, 3, v, True)
 
@@ -441,6 +466,12 @@ class CabacSink:
             ni, nj = i + di, j + dj
             if ni >= 0 and nj >= 0:
                 m, pi, pj = m_cur, ni, nj
+            elif self.e.c.mbaff:                            # get_neighbour of the block's sample
+                nb = self.e._nbr(self.a, -1 if ni < 0 else ni * 4, -1 if nj < 0 else nj * 4, chroma)
+                if nb is None:
+                    inc += w if m_cur.intra else 0
+                    continue
+                m, pi, pj = nb[0], nb[1] // 4, nb[2] // 4
             else:
                 m = self._mb(-1 if ni < 0 else 0, -1 if nj < 0 else 0)
                 if m is None:
@@ -477,8 +508,9 @@ class CabacSink:
         n = len(coeffs)
         last = max(k for k, v in enumerate(coeffs) if v)
         pos = "2x4c" if typ == CHROMA_DC and self.e.c.chroma_format == 2 else _POS[typ]   # CHROMA_DC_2x4 maps
-        pm, pl_ = (POS_MAP_FIELD if self.field else POS_MAP)[pos], POS_LAST[pos]
-        fm, fl = (MAP_SET, LAST_SET) if self.field else (0, 0)
+        fld = self.field or m_cur.fld                      # field pictures and field MBs
+        pm, pl_ = (POS_MAP_FIELD if fld else POS_MAP)[pos], POS_LAST[pos]
+        fm, fl = (MAP_SET, LAST_SET) if fld else (0, 0)
         for k in range(n - 1):
             sig = 1 if coeffs[k] else 0
             self._dec("map_contexts", fm + T2C_MAP[typ] + pm[k], sig)

@@ -203,7 +203,7 @@ class Encoder:
         self.W, self.H = cfg.width_mbs, cfg.height_mbs
         self.FH = cfg.height_mbs                 # frame height; a field picture has FH / 2 MB rows
         assert not cfg.field or cfg.height_mbs % 2 == 0
-        assert not cfg.mbaff or (cfg.height_mbs % 2 == 0 and not cfg.cabac and not cfg.cip and not cfg.bframes and
+        assert not cfg.mbaff or (cfg.height_mbs % 2 == 0 and not cfg.cip and not cfg.bframes and
                                  not cfg.field)
         self.log2_max_frame_num = 4
         self.log2_max_poc_lsb = 8
@@ -580,19 +580,39 @@ class Encoder:
             if top:
                 self.pair_roll = (r.random(), r.random())
                 sk = [ptype == "P" and x < c.skip for x in self.pair_roll]
-                if sk[0] and sk[1]:                      # inferred: left pair, else upper pair, else frame
-                    mx, py = a % W, (a // W) // 2
-                    A = self.mbs[(2 * py) * W + mx - 1] if mx > 0 else None
-                    B = self.mbs[(2 * py - 1) * W + mx] if py > 0 else None
-                    m.fld = A.fld if A is not None and A.slice == s else (B.fld if B is not None and B.slice == s else False)
-                else:
-                    m.fld = r.random() < c.mbaff
+                mx, py = a % W, (a // W) // 2            # inferred: left pair, else upper pair, else frame
+                A = self.mbs[(2 * py) * W + mx - 1] if mx > 0 else None
+                B = self.mbs[(2 * py - 1) * W + mx] if py > 0 else None
+                inferred = A.fld if A is not None and A.slice == s else (B.fld if B is not None and B.slice == s else False)
+                fld = inferred if (sk[0] and sk[1]) else r.random() < c.mbaff
                 self.pair_skip = sk
-                if not sk[0]:
-                    w.u(1, 1 if m.fld else 0)
+                if cab:
+                    # CABAC (interpret_mb.cc:186-262): the top MB's skip flag with the inferred flag; a
+                    # skipped top MB reads the bottom MB's skip flag ahead (the bottom MB with the top MB's
+                    # inferred flag) and then, for a coded bottom MB, the pair's flag
+                    m.fld = inferred
+                    if ptype != "I":
+                        cab.skip_flag(sk[0])
+                        if sk[0]:
+                            m.skip = True
+                            bm = self.mbs[a + W]
+                            bm.slice, bm.fld = s, inferred
+                            cab.start_mb(a + W)
+                            cab.skip_flag(sk[1])
+                            if not sk[1]:
+                                cab.field_flag(fld)
+                            cab.start_mb(a)
+                    if not sk[0]:
+                        cab.field_flag(fld)
+                elif not sk[0]:
+                    w.u(1, 1 if fld else 0)
+                m.fld = fld
             else:
                 m.fld = self.mbs[a - W].fld
-                if self.pair_skip[0] and not self.pair_skip[1]:
+                if cab:
+                    if ptype != "I" and not self.pair_skip[0]:
+                        cab.skip_flag(self.pair_skip[1])
+                elif self.pair_skip[0] and not self.pair_skip[1]:
                     w.u(1, 1 if m.fld else 0)            # coded in the bottom MB after a skipped top MB
             roll = self.pair_roll[0 if top else 1]
         else:
@@ -600,10 +620,10 @@ class Encoder:
         if ptype in ("P", "B") and roll < c.skip:
             m.kind, m.intra, m.skip, m.mbt_ref = SKIP, False, True, 0
             m.nz = [[[0] * 4 for _ in range(4)] for _ in range(3)]
-            if cab:
+            if cab and not c.mbaff:
                 cab.skip_flag(True)
             return False
-        if cab and ptype != "I":
+        if cab and ptype != "I" and not c.mbaff:
             cab.skip_flag(False)
         intra = ptype == "I" or r.random() < c.intra_in_p
         base = 5 if ptype == "P" else (23 if ptype == "B" else 0)
@@ -727,7 +747,7 @@ class Encoder:
             def ref_idx(x0, y0, pw, ph):
                 v = r.randrange(nr)
                 if cab:
-                    cab.ref_idx(v, nref, 0, x0, y0)
+                    cab.ref_idx(v, nr, 0, x0, y0)
                     self._set_ref(m, 0, x0, y0, pw, ph, v)
                 elif nhdr == 2:
                     w.u(1, 1 - v)
@@ -1038,9 +1058,11 @@ class Encoder:
                 while not w.aligned():
                     w.u(1, 1)                       # cabac_alignment_one_bit
                 self.cab = CB.CabacSink(self, w.bits, ptype, sqp, init_idc, s, field=structure != 0)
-                for a in range(first, end):
+                mbs = order(first, end)
+                for k, a in enumerate(mbs):
                     self._mb(w, a, ptype, s, nref_b if ptype == "B" else nref)
-                    self.cab.end_of_slice(a == end - 1)   # the flush's last bit is rbsp_stop_one_bit
+                    if not c.mbaff or (a // W) % 2:       # MBAFF: after bottom MBs only (slice_data.cc:531)
+                        self.cab.end_of_slice(k == len(mbs) - 1)   # the flush's last bit is rbsp_stop_one_bit
                 self.cab = None
                 while not w.aligned():
                     w.u(1, 0)                       # rbsp_alignment_zero_bit

@@ -130,6 +130,16 @@ STREAMS = {
                                        skip=0.5, num_refs=1, intra_in_p=0.1),
     "hp_vga_mbaff_ippp": dict(width_mbs=40, height_mbs=34, frames=5, seed=904, profile=100, transform8x8=1,
                               mbaff=0.5, skip=0.25, num_refs=2, slices=2, deblock=(0, 2), intra_in_p=0.15),
+    # MBAFF with CABAC: mb_field_decoding_flag as a bin (ctxIdxInc from the left / upper pairs), the
+    # skip flags' contexts with the pair's inferred flag, a skipped top MB reading its bottom MB's skip
+    # flag (and the pair's flag) ahead (interpret_mb.cc:186-262), end_of_slice_flag after bottom MBs,
+    # refIdx / mvd contexts across field and frame pairs (neighbour.cc:517-633), field MBs' significance
+    # contexts and 8x8 position map
+    "hp_cif_cabac_mbaff_ippp": dict(width_mbs=22, height_mbs=18, frames=6, seed=911, profile=100, transform8x8=1,
+                                    cabac=1, mbaff=0.5, skip=0.3, num_refs=3, slices=2, deblock=(0, 2),
+                                    intra_in_p=0.15, pcm=0.02, qp=(14, 40)),
+    "mp_qcif_cabac_mbaff_skips": dict(width_mbs=11, height_mbs=10, frames=8, seed=912, profile=77, cabac=1,
+                                      mbaff=0.5, skip=0.5, num_refs=1, intra_in_p=0.1, weighted=1),
     # 4:2:2 (chroma_format_idc 2; High 4:2:2 / High 4:4:4 Predictive, CAVLC): 8 x 16 chroma per MB, the
     # 2x4 chroma DC (coeff_token nC -2, total_zeros of 8), 8 chroma AC blocks per plane.  No 8x8
     # transforms: the reference leaves the bS of a transform-8x8 MB's chroma rows 4 / 12 unset
@@ -179,6 +189,10 @@ def stream_path(name: str) -> str:
 
 def capture_path(name: str) -> str:
     return os.path.join(STREAM_DIR, name + ".cap.npz")
+
+
+# streams the repo's own parser (arrow-h264_amd/parser) refuses: reference-parser captures only
+PARSER_REFUSED = {"hp_cif_cabac_mbaff_ippp": "MBAFF coding with CABAC", "mp_qcif_cabac_mbaff_skips": "MBAFF coding with CABAC"}
 
 
 def crop_of(cfg: dict) -> OUT.Crop:
